@@ -1,0 +1,192 @@
+/*
+ * speedy_ml.h -- C ABI of the MI355X-native SPEEDY-ML hybrid hot path.
+ *
+ * Plain C: pointers, sizes and status codes; no torch or HIP C++ types.  Every
+ * device pointer argument (d_*) is a gfx950 device address; every other pointer
+ * is host memory owned by the caller.  Streams are passed as `void*` holding a
+ * hipStream_t (NULL = the legacy default stream).  Functions return SML_OK (0)
+ * or a negative SML_ERR_* code; sml_last_error() gives the message (per thread).
+ *
+ * Array layouts are the reference's Fortran layouts (column-major), so a Fortran
+ * host passes its arrays unchanged:
+ *   spectral field   v(mx2=62, nx=32)            -> 1984 doubles, m fastest
+ *   grid field       g(ix=96, il=48)             -> 4608 doubles, x fastest, row 1 south
+ *   grid4d           (4, 96, 48, 8)  = (var,x,y,z), var = T,u,v,q[g/kg]
+ *   grid2d / precip  (96, 48)
+ *   W_in             win(n, ninp)       (NetCDF file: win[win_y=ninp][win_x=n])
+ *   W_out            wout(nout, ncs+n)  (NetCDF file: wout[wout_y=ncs+n][wout_x=nout])
+ *   A                COO rows/cols (1-based), vals, k entries, duplicates additive
+ * Batched calls take fields back to back (field stride 1984 or 4608 doubles).
+ *
+ * Reference interfaces replaced:
+ *   sml_grid_batched     <- grid   (src/spe_spectral.f90:389-401)
+ *   sml_spec_batched     <- spec   (src/spe_spectral.f90:403-414)
+ *   sml_vdspec_batched   <- vdspec (src/spe_spectral.f90:416-452)
+ *   sml_uvspec_batched   <- uvspec (src/spe_spectral.f90:351-387)
+ *   sml_spectral_create  <- parmtr + inifft (src/spe_spectral.f90:45-192,
+ *                           src/spe_subfft_fftpack.f90:1-11)
+ *   sml_res_create / sml_res_load_region_*
+ *                        <- trained_reservoir_prediction + read_trained_res +
+ *                           allocate_res_new + mklsparse
+ *                           (src/mod_reservoir.f90:1781-1884, :78-178;
+ *                            src/mod_io.f90:2911-2956; src/mod_linalg.f90:10-25)
+ *   sml_res_step         <- predict / predict_ml for every region on the rank
+ *                           (src/mod_reservoir.f90:1416-1533, called per region from
+ *                            src/parallelmain.f90:225-234)
+ *   sml_exchange_assemble <- the root half of sendrecievegrid: outvec tiles into the
+ *                           global grid + clips (src/mpires.f90:300-478,
+ *                            src/res_domain.f90:769-804)
+ *   sml_res_tile_inputs  <- the scatter half of sendrecievegrid: overlap input tiles,
+ *                           SPEEDY local vectors, standardisation
+ *                           (src/mpires.f90:558-751, src/res_domain.f90:1000-1293)
+ *   sml_nc_read_region   <- read_trained_res (src/mod_io.f90:2911-2956), NetCDF-3
+ *                           classic reader for the per-region weight files
+ *   sml_nc_write_region  <- write_trained_res (src/mod_reservoir.f90:1701-1736,
+ *                           src/mod_io.f90:1247-1496)
+ */
+#ifndef SPEEDY_ML_H
+#define SPEEDY_ML_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SML_OK 0
+#define SML_ERR_ARG (-1)
+#define SML_ERR_HIP (-2)
+#define SML_ERR_NOMEM (-3)
+#define SML_ERR_STATE (-4)
+#define SML_ERR_IO (-5)
+#define SML_ERR_FORMAT (-6)
+
+#define SML_F32 1
+#define SML_F64 2
+
+/* T30L8 grid constants (mod_atparam.f90:9-14) */
+#define SML_MX 31
+#define SML_NX 32
+#define SML_MX2 62
+#define SML_IX 96
+#define SML_IL 48
+#define SML_KX 8
+#define SML_SPEC_FIELD 1984 /* 62*32 doubles */
+#define SML_GRID_FIELD 4608 /* 96*48 doubles */
+
+const char *sml_last_error(void);
+int sml_abi_version(void);
+
+/* ----------------------------------------------------------------- spectral */
+typedef struct sml_spectral sml_spectral;
+
+/* parmtr(a) + inifft: builds the Gaussian latitudes, Legendre tables (T30) and the
+ * Fourier matrices on the host, uploads them to the current device. */
+int sml_spectral_create(double radius, sml_spectral **out);
+int sml_spectral_destroy(sml_spectral *s);
+/* host copies of the tables (any pointer may be NULL):
+ * sia[24], wt[24], cpol[24*32*62] (cpol(mx2,nx,iy) column-major), nsh2[32] */
+int sml_spectral_tables(const sml_spectral *s, double *sia, double *wt, double *cpol, int *nsh2);
+
+/* grid: spectral -> grid for nfields fields; kcos = 1 (plain) or 2 (x 1/cos lat) */
+int sml_grid_batched(sml_spectral *s, const double *d_spec, double *d_grid, int nfields, int kcos, void *stream);
+/* spec: grid -> spectral */
+int sml_spec_batched(sml_spectral *s, const double *d_grid, double *d_spec, int nfields, void *stream);
+/* stage-level entry points (gridy / gridx / specx / specy), Fourier buffers are
+ * varm(mx2=62, il=48) per field */
+int sml_gridy_batched(sml_spectral *s, const double *d_spec, double *d_varm, int nfields, void *stream);
+int sml_gridx_batched(sml_spectral *s, const double *d_varm, double *d_grid, int nfields, int kcos, void *stream);
+int sml_specx_batched(sml_spectral *s, const double *d_grid, double *d_varm, int nfields, void *stream);
+int sml_specy_batched(sml_spectral *s, const double *d_varm, double *d_spec, int nfields, void *stream);
+/* vdspec: (u,v) grid -> (vor,div) spectral, kcos 2: u*1/cos, else u*1/cos^2 */
+int sml_vdspec_batched(sml_spectral *s, const double *d_ug, const double *d_vg, double *d_vor, double *d_div,
+                       int nfields, int kcos, void *stream);
+/* uvspec: (vor,div) spectral -> (u cos, v cos) spectral */
+int sml_uvspec_batched(sml_spectral *s, const double *d_vor, const double *d_div, double *d_ucos, double *d_vcos,
+                       int nfields, void *stream);
+/* host convenience (synchronous, one call = H2D + kernels + D2H): used by the
+ * single-field drop-ins and the Fortran binding tests */
+int sml_grid_host(sml_spectral *s, const double *spec, double *grid, int nfields, int kcos);
+int sml_spec_host(sml_spectral *s, const double *grid, double *spec, int nfields);
+
+/* ---------------------------------------------------------------- reservoirs */
+typedef struct sml_reservoirs sml_reservoirs;
+
+/* One context per rank: the regions listed in region_ids (0-based global region
+ * numbers of a numregions decomposition, res_domain.f90:31-62), bottom level with
+ * logp/precip/tisr inputs, sst input where sst_flags[i] != 0.
+ *   n[i], k[i]      reservoir size and nnz of A for local region i
+ *   chunk_speedy    132 (hybrid, predict) or 0 (ML-only, predict_ml)
+ *   nout            136 (chunk_size_prediction)
+ *   weight_dtype    SML_F32: W_in/A/W_out held as fp32 (exact for weights read from
+ *                   the NF90_REAL files); SML_F64: held as fp64.  Arithmetic is fp64.
+ *   leakage         reservoir%leakage (1.0 in the reference, mod_reservoir.f90:97) */
+int sml_res_create(int numregions, int nlocal, const int *region_ids, const unsigned char *sst_flags,
+                   const int *n, const int *k, int chunk_speedy, int nout, int weight_dtype, double leakage,
+                   sml_reservoirs **out);
+int sml_res_destroy(sml_reservoirs *c);
+/* ninp of local region i (from geometry + sst flag) */
+int sml_res_ninp(const sml_reservoirs *c, int i, int *ninp);
+/* packed feedback layout: offsets[nlocal+1] (in doubles) */
+int sml_res_feedback_offsets(const sml_reservoirs *c, int64_t *offsets);
+/* load region i from reference-layout host arrays (see header comment); mean/std[36] */
+int sml_res_load_region_f32(sml_reservoirs *c, int i, const int *rows, const int *cols, const float *vals,
+                            const float *win, const float *wout, const double *mean, const double *std);
+int sml_res_load_region_f64(sml_reservoirs *c, int i, const int *rows, const int *cols, const double *vals,
+                            const double *win, const double *wout, const double *mean, const double *std);
+/* state x (current_state) of region i, host arrays of n doubles */
+int sml_res_set_state(sml_reservoirs *c, int i, const double *x);
+int sml_res_get_state(sml_reservoirs *c, int i, double *x);
+/* One prediction step for every local region (predict, mod_reservoir.f90:1416):
+ *   d_feedback    packed feedback vectors (sml_res_feedback_offsets)
+ *   d_local_model [nlocal][chunk_speedy] standardized SPEEDY vectors (ignored if 0)
+ *   d_outvec      [nlocal][nout] unstandardized outputs */
+int sml_res_step(sml_reservoirs *c, const double *d_feedback, const double *d_local_model, double *d_outvec,
+                 void *stream);
+/* host convenience: H2D, step, D2H (synchronous) */
+int sml_res_step_host(sml_reservoirs *c, const double *feedback, const double *local_model, double *outvec);
+/* bytes of weights + state resident on the device (for roofline bookkeeping) */
+int sml_res_footprint(const sml_reservoirs *c, int64_t *weight_bytes, int64_t *algorithmic_bytes_per_step);
+/* timing hook: with capacity > 0, the next `capacity` sml_res_step calls record HIP
+ * events around their update and readout kernels on the step's stream (0 = off).
+ * sml_res_kernel_times waits for them and returns per-step milliseconds, then
+ * rearms the recorder. */
+int sml_res_enable_timing(sml_reservoirs *c, int capacity);
+int sml_res_kernel_times(sml_reservoirs *c, float *update_ms, float *readout_ms, int max_steps, int *count);
+
+/* ------------------------------------------------------------- exchange/tiling */
+/* Global grids: d_grid4d[4*96*48*8], d_grid2d[96*48], d_precip[96*48].
+ * assemble: scatter all numregions outvecs ([numregions][nout], region-major, as
+ * produced by an all-gather of every rank's d_outvec) into the grids, then clip
+ * q >= 1e-6 and precip < 1e-5 -> 0. */
+int sml_exchange_assemble(sml_reservoirs *c, const double *d_outvec_all, double *d_grid4d, double *d_grid2d,
+                          double *d_precip, void *stream);
+/* tile: build the next step's inputs of every local region from the grids:
+ *   feedback atmo/logp/precip entries from the overlap tile, standardized;
+ *   feedback tisr entries copied from d_tisr (packed [nlocal][in2d], already
+ *   standardized, may be NULL = keep); sst entries kept as they are;
+ *   local_model from the SPEEDY forecast grids d_fc4d/d_fc2d, standardized
+ *   (skipped when chunk_speedy == 0 or d_fc4d == NULL). */
+int sml_res_tile_inputs(sml_reservoirs *c, const double *d_grid4d, const double *d_grid2d, const double *d_precip,
+                        const double *d_fc4d, const double *d_fc2d, const double *d_tisr, double *d_feedback,
+                        double *d_local_model, void *stream);
+
+/* --------------------------------------------------------- NetCDF weight files */
+/* Reads worker_XXXX_level_1_<trial>.nc (NetCDF-3 classic / 64-bit offset) written
+ * by the reference (write_trained_res).  Sizes come from the file's dimensions:
+ * dims[0]=n (win_x), dims[1]=ninp (win_y), dims[2]=nout (wout_x),
+ * dims[3]=ncs+n (wout_y), dims[4]=k (rows_x), dims[5]=36 (mean_x).
+ * Call once with all array pointers NULL to get dims, then again with buffers.
+ * Arrays are returned in the reference layouts (fp32 values as stored). */
+int sml_nc_read_region(const char *path, int64_t *dims, float *win, float *wout, int *rows, int *cols, float *vals,
+                       float *mean, float *std);
+/* Writes the same layout (CDF-1, big-endian) -- for tests and tooling. */
+int sml_nc_write_region(const char *path, int n, int ninp, int nout, int ncs_plus_n, int k, const float *win,
+                        const float *wout, const int *rows, const int *cols, const float *vals, const float *mean,
+                        const float *std);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SPEEDY_ML_H */

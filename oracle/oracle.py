@@ -1,0 +1,319 @@
+"""oracle/oracle.py -- TEST INFRASTRUCTURE ONLY (ctypes wrapper of liboracle.so).
+
+The checker for the SPEEDY-ML hot path.  Only tests/, __graft_entry__.smoke()
+and bench.py's cpu_baseline leg import this module.  It never ships in the
+product path (speedy-ml-1_amd/ never imports it).
+
+Every function mirrors one routine of speedy_oracle.c, which in turn cites the
+reference file:line it restates.  Arrays are numpy float64, laid out exactly as
+the reference's Fortran arrays (column-major), i.e. a spectral field
+v(mx2=62,nx=32) is a C array of shape (32, 62) and a grid field g(96,48) is a C
+array of shape (48, 96).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liboracle.so")
+REF_SPECTRAL_PATH = os.path.join(HERE, "_ref", "libspeedy_ref_spectral.so")
+
+MX, NX, MX2, IX, IY, IL = 31, 32, 62, 96, 24, 48
+EARTH_RADIUS = 6.371e6  # mod_dyncon1.f90: rearth
+
+_lib = None
+_init_radius = None
+
+
+def build() -> None:
+    """Compile liboracle.so (gcc).  Cheap; called by __graft_entry__.build()."""
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        _lib = ctypes.CDLL(LIB_PATH)
+        _declare(_lib)
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def _declare(L):
+    vp, i, d = ctypes.c_void_p, ctypes.c_int, ctypes.c_double
+    L.orc_spectral_init.argtypes = [d]
+    L.orc_get_tables.argtypes = [vp, vp, vp, vp]
+    for name in ("orc_gridy", "orc_specy", "orc_specx", "orc_spec", "orc_lap", "orc_invlap"):
+        getattr(L, name).argtypes = [vp, vp]
+    L.orc_gridx.argtypes = [vp, vp, i]
+    L.orc_grid.argtypes = [vp, vp, i]
+    L.orc_vds.argtypes = [vp, vp, vp, vp]
+    L.orc_uvspec.argtypes = [vp, vp, vp, vp]
+    L.orc_grad.argtypes = [vp, vp, vp]
+    L.orc_vdspec.argtypes = [vp, vp, vp, vp, i]
+    L.orc_trunct.argtypes = [vp]
+    L.orc_region_geometry_ints.argtypes = [i, i, i, vp]
+    L.orc_radius_by_region.argtypes = [i, i]
+    L.orc_radius_by_region.restype = d
+    L.orc_reservoir_sizes.argtypes = [i, i, i, i, vp]
+    L.orc_predict.argtypes = [i, i, i, vp, vp, vp, vp, vp, i, i, d, vp, vp, vp, vp, vp, vp, i]
+    L.orc_predict_f32.argtypes = [i, i, i, vp, vp, vp, vp, vp, vp, i, i, d, vp, vp, vp, vp, vp, vp]
+    L.orc_unstandardize_res.argtypes = [vp, i, i, i, vp, vp, i, i, i, i]
+    L.orc_assemble.argtypes = [i, vp, i, vp, vp, vp]
+    L.orc_tile_feedback.argtypes = [i, i, vp, vp, vp, vp, vp, vp, vp, vp]
+    L.orc_tile_local_model.argtypes = [i, i, vp, vp, vp, vp, vp]
+
+
+def spectral_init(radius: float = EARTH_RADIUS) -> None:
+    global _init_radius
+    if _init_radius != radius:
+        lib().orc_spectral_init(radius)
+        _init_radius = radius
+
+
+def tables():
+    spectral_init()
+    sia = np.zeros(IY)
+    wt = np.zeros(IY)
+    cpol = np.zeros((IY, NX, MX2))
+    nsh2 = np.zeros(NX, dtype=np.int32)
+    lib().orc_get_tables(_p(sia), _p(wt), _p(cpol), _p(nsh2))
+    return {"sia": sia, "wt": wt, "cpol": cpol, "nsh2": nsh2}
+
+
+def _f64(a, shape):
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    assert a.shape == shape, (a.shape, shape)
+    return a
+
+
+def gridy(v):
+    spectral_init()
+    v = _f64(v, (NX, MX2))
+    out = np.zeros((IL, MX2))
+    lib().orc_gridy(_p(v), _p(out))
+    return out
+
+
+def gridx(varm, kcos=1):
+    spectral_init()
+    varm = _f64(varm, (IL, MX2))
+    out = np.zeros((IL, IX))
+    lib().orc_gridx(_p(varm), _p(out), kcos)
+    return out
+
+
+def specx(g):
+    spectral_init()
+    g = _f64(g, (IL, IX))
+    out = np.zeros((IL, MX2))
+    lib().orc_specx(_p(g), _p(out))
+    return out
+
+
+def specy(varm):
+    spectral_init()
+    varm = _f64(varm, (IL, MX2))
+    out = np.zeros((NX, MX2))
+    lib().orc_specy(_p(varm), _p(out))
+    return out
+
+
+def grid(v, kcos=1):
+    spectral_init()
+    v = _f64(v, (NX, MX2))
+    out = np.zeros((IL, IX))
+    lib().orc_grid(_p(v), _p(out), kcos)
+    return out
+
+
+def spec(g):
+    spectral_init()
+    g = _f64(g, (IL, IX))
+    out = np.zeros((NX, MX2))
+    lib().orc_spec(_p(g), _p(out))
+    return out
+
+
+def vdspec(ug, vg, kcos=2):
+    spectral_init()
+    ug = _f64(ug, (IL, IX))
+    vg = _f64(vg, (IL, IX))
+    vor = np.zeros((NX, MX2))
+    div = np.zeros((NX, MX2))
+    lib().orc_vdspec(_p(ug), _p(vg), _p(vor), _p(div), kcos)
+    return vor, div
+
+
+def uvspec(vor, div):
+    spectral_init()
+    vor = _f64(vor, (NX, MX2))
+    div = _f64(div, (NX, MX2))
+    u = np.zeros((NX, MX2))
+    v = np.zeros((NX, MX2))
+    lib().orc_uvspec(_p(vor), _p(div), _p(u), _p(v))
+    return u, v
+
+
+def vds(ucos, vcos):
+    spectral_init()
+    ucos = _f64(ucos, (NX, MX2))
+    vcos = _f64(vcos, (NX, MX2))
+    vor = np.zeros((NX, MX2))
+    div = np.zeros((NX, MX2))
+    lib().orc_vds(_p(ucos), _p(vcos), _p(vor), _p(div))
+    return vor, div
+
+
+def grad(psi):
+    spectral_init()
+    psi = _f64(psi, (NX, MX2))
+    dx = np.zeros((NX, MX2))
+    dy = np.zeros((NX, MX2))
+    lib().orc_grad(_p(psi), _p(dx), _p(dy))
+    return dx, dy
+
+
+def lap(s):
+    spectral_init()
+    s = _f64(s, (NX, MX2))
+    out = np.zeros((NX, MX2))
+    lib().orc_lap(_p(s), _p(out))
+    return out
+
+
+def invlap(s):
+    spectral_init()
+    s = _f64(s, (NX, MX2))
+    out = np.zeros((NX, MX2))
+    lib().orc_invlap(_p(s), _p(out))
+    return out
+
+
+def trunct(s):
+    spectral_init()
+    s = _f64(s, (NX, MX2)).copy()
+    lib().orc_trunct(_p(s))
+    return s
+
+
+# ---------------------------------------------------------------- domain
+GEOM_FIELDS = ("res_xstart", "res_xend", "res_ystart", "res_yend", "resxchunk", "resychunk",
+               "input_xstart", "input_xend", "input_ystart", "input_yend", "inputxchunk", "inputychunk",
+               "pole", "periodic", "tdata_xstart", "tdata_xend", "tdata_ystart", "tdata_yend")
+
+
+def region_geometry(region: int, numregions: int = 1152, overlap: int = 1) -> dict:
+    out = np.zeros(len(GEOM_FIELDS), dtype=np.int32)
+    lib().orc_region_geometry_ints(numregions, region, overlap, _p(out))
+    return dict(zip(GEOM_FIELDS, (int(v) for v in out)))
+
+
+def radius_by_region(region: int, numregions: int = 1152) -> float:
+    return float(lib().orc_radius_by_region(numregions, region))
+
+
+def reservoir_sizes(region: int, sst: bool, numregions: int = 1152, m_nodes: int = 6000) -> dict:
+    out = np.zeros(5, dtype=np.int32)
+    lib().orc_reservoir_sizes(numregions, region, int(bool(sst)), m_nodes, _p(out))
+    return dict(zip(("ninp", "n", "k", "chunk_pred", "chunk_speedy"), (int(v) for v in out)))
+
+
+# ---------------------------------------------------------------- reservoir
+def predict(rows, cols, vals, win_dense, wout, feedback, local_model, x, mean, std,
+            chunk_speedy=132, leakage=1.0, unstandardize=True):
+    """Reference predict (mod_reservoir.f90:1416-1487).  win_dense: (ninp, n) C array
+    == Fortran win(n, ninp); wout: (ncs+n, nout) C array == Fortran wout(nout, ncs+n).
+    Returns (outvec, x_new)."""
+    ninp, n = win_dense.shape
+    k = len(rows)
+    nout = wout.shape[1]
+    rows = np.ascontiguousarray(rows, dtype=np.int32)
+    cols = np.ascontiguousarray(cols, dtype=np.int32)
+    vals = np.ascontiguousarray(vals, dtype=np.float64)
+    win_dense = np.ascontiguousarray(win_dense, dtype=np.float64)
+    wout = np.ascontiguousarray(wout, dtype=np.float64)
+    feedback = np.ascontiguousarray(feedback, dtype=np.float64)
+    lm = np.ascontiguousarray(local_model if local_model is not None else np.zeros(1), dtype=np.float64)
+    xx = np.array(x, dtype=np.float64, copy=True)
+    mean = np.ascontiguousarray(mean, dtype=np.float64)
+    std = np.ascontiguousarray(std, dtype=np.float64)
+    out = np.zeros(nout)
+    lib().orc_predict(n, ninp, k, _p(rows), _p(cols), _p(vals), _p(win_dense), _p(wout), nout,
+                      chunk_speedy, leakage, _p(feedback), _p(lm), _p(xx), _p(out), _p(mean), _p(std),
+                      int(bool(unstandardize)))
+    return out, xx
+
+
+def predict_f32(rows, cols, vals_f32, win_col, win_val_f32, wout_f32, feedback, local_model, x, mean, std,
+                chunk_speedy=132, leakage=1.0):
+    """Same arithmetic with the compressed W_in (one entry per row) and fp32 weights."""
+    n = len(win_col)
+    nout = wout_f32.shape[1]
+    rows = np.ascontiguousarray(rows, dtype=np.int32)
+    cols = np.ascontiguousarray(cols, dtype=np.int32)
+    vals_f32 = np.ascontiguousarray(vals_f32, dtype=np.float32)
+    win_col = np.ascontiguousarray(win_col, dtype=np.int32)
+    win_val_f32 = np.ascontiguousarray(win_val_f32, dtype=np.float32)
+    wout_f32 = np.ascontiguousarray(wout_f32, dtype=np.float32)
+    feedback = np.ascontiguousarray(feedback, dtype=np.float64)
+    lm = np.ascontiguousarray(local_model if local_model is not None else np.zeros(1), dtype=np.float64)
+    xx = np.array(x, dtype=np.float64, copy=True)
+    out = np.zeros(nout)
+    lib().orc_predict_f32(n, len(feedback), len(rows), _p(rows), _p(cols), _p(vals_f32), _p(win_col),
+                          _p(win_val_f32), _p(wout_f32), nout, chunk_speedy, leakage, _p(feedback), _p(lm),
+                          _p(xx), _p(out), _p(np.ascontiguousarray(mean, dtype=np.float64)),
+                          _p(np.ascontiguousarray(std, dtype=np.float64)))
+    return out, xx
+
+
+# ---------------------------------------------------------------- exchange / tiling
+def assemble(outvecs):
+    outvecs = np.ascontiguousarray(outvecs, dtype=np.float64)
+    nreg, outlen = outvecs.shape
+    g4 = np.zeros((8, 48, 96, 4))
+    g2 = np.zeros((48, 96))
+    pr = np.zeros((48, 96))
+    lib().orc_assemble(nreg, _p(outvecs), outlen, _p(g4), _p(g2), _p(pr))
+    return g4, g2, pr
+
+
+def tile_feedback(region, g4, g2, pr, mean, std, tisr_std, sst_std=None, numregions=1152):
+    geo = region_geometry(region, numregions)
+    in2d = geo["inputxchunk"] * geo["inputychunk"]
+    ninp = 4 * in2d * 8 + 3 * in2d + (in2d if sst_std is not None else 0)
+    fb = np.zeros(ninp)
+    sst_ptr = None
+    if sst_std is not None:
+        sst_std = np.ascontiguousarray(sst_std, dtype=np.float64)
+        sst_ptr = _p(sst_std)
+    lib().orc_tile_feedback(numregions, region, _p(np.ascontiguousarray(g4)), _p(np.ascontiguousarray(g2)),
+                            _p(np.ascontiguousarray(pr)), _p(np.ascontiguousarray(mean, dtype=np.float64)),
+                            _p(np.ascontiguousarray(std, dtype=np.float64)),
+                            _p(np.ascontiguousarray(tisr_std, dtype=np.float64)), sst_ptr, _p(fb))
+    return fb
+
+
+def tile_local_model(region, fc4d, fc2d, mean, std, numregions=1152):
+    lm = np.zeros(132)
+    lib().orc_tile_local_model(numregions, region, _p(np.ascontiguousarray(fc4d)), _p(np.ascontiguousarray(fc2d)),
+                               _p(np.ascontiguousarray(mean, dtype=np.float64)),
+                               _p(np.ascontiguousarray(std, dtype=np.float64)), _p(lm))
+    return lm
+
+
+# ---------------------------------------------------------------- reference (pinning only)
+def ref_spectral():
+    """ctypes handle on the reference's own spectral Fortran (oracle/_ref), or None."""
+    if not os.path.exists(REF_SPECTRAL_PATH):
+        return None
+    return ctypes.CDLL(REF_SPECTRAL_PATH)

@@ -1,0 +1,791 @@
+// sml_reservoir.hip -- batched reservoir forward (predict) for every region of a
+// rank, plus the device-side exchange/tiling that replaces sendrecievegrid's
+// gather / scatter loops.
+//
+// Reference: predict (src/mod_reservoir.f90:1416-1487), per region on the host:
+//     y = A x                (MKL_SPARSE_D_MV, COO, :1442)
+//     temp = W_in feedback   (dense n x ninp matmul, :1443)
+//     x = (1-a) x + a tanh(y + temp)
+//     x~ = x with every 2nd node squared (:1448-1449)
+//     outvec = W_out [local_model; x~]  (:1454), then unstandardize (:1469)
+//
+// MI355X design (DESIGN.md "Reservoir"):
+//   * all regions of the rank run in two launches (update + readout), no host loop;
+//   * A is CSR (rows in the file's entry order, so every row sums in the same order
+//     as the reference's COO traversal) with 16-bit column indices;
+//   * W_in is CSR too: the trained matrix has one entry per row (train_reservoir,
+//     :260-278), so the 26.5 MB dense matmul per region becomes n gathers;
+//   * W_out is stored transposed ([nout][ld], rows padded to 16 B) in the file
+//     precision (fp32 by default: NF90_REAL, mod_io.f90:1282, exact widening);
+//     the readout streams it from HBM once per step with fp64 accumulation and
+//     wave-level reductions -- this kernel carries ~90 % of the step's bytes;
+//   * unstandardize is fused into the readout's epilogue.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "sml_internal.hpp"
+
+using namespace sml;
+
+namespace {
+
+constexpr int kRows = 8;        // W_out rows per wave in the readout
+constexpr int kMeanStd = 36;    // mean/std vector length (mod_reservoir.f90:1815-1846)
+constexpr int kTisrStride = 16; // packed tisr input: [nlocal][16]
+constexpr int kSrcKeep = -1;    // feedback entry left untouched (sst)
+
+struct RegionDev {
+    int n, ninp, ld, pad_;
+    int64_t a_rp, a_nz, w_rp, w_nz, wout, x, xaug, fb;
+};
+
+}  // namespace
+
+struct sml_reservoirs {
+    int numregions = 0, nlocal = 0, ncs = 0, nout = 0, nout_pad = 0, wdtype = SML_F32;
+    double leakage = 1.0;
+    std::vector<int> region_ids, n, k, ninp, ld;
+    std::vector<unsigned char> sst, loaded;
+    std::vector<RegionGeom> geom;
+    std::vector<RegionDev> rd;
+    int64_t tot_a_rp = 0, tot_a_nz = 0, tot_w_rp = 0, tot_w_nz = 0, tot_wout = 0, tot_x = 0, tot_xaug = 0,
+            tot_fb = 0;
+    std::vector<int64_t> w_nz_cap;  // reserved W_in nnz per region (n, grows on reload)
+    int maxn = 0;
+    int device = 0;
+    // device buffers
+    RegionDev *d_rd = nullptr;
+    int32_t *d_a_rp = nullptr, *d_w_rp = nullptr;
+    uint16_t *d_a_col = nullptr, *d_w_col = nullptr;
+    void *d_a_val = nullptr, *d_w_val = nullptr, *d_wout = nullptr;
+    double *d_x[2] = {nullptr, nullptr};
+    int cur = 0;
+    double *d_xaug = nullptr, *d_meanstd = nullptr;
+    int8_t *d_outl = nullptr;
+    int32_t *d_asm_dst = nullptr;   // [numregions*nout] -> concatenated grid index
+    int32_t *d_fb_src = nullptr;    // [tot_fb]
+    uint8_t *d_fb_l = nullptr;      // [tot_fb]
+    uint16_t *d_fb_reg = nullptr;   // [tot_fb]
+    int32_t *d_lm_src = nullptr;    // [nlocal*ncs]
+    uint8_t *d_lm_l = nullptr;
+    double *d_io = nullptr;         // staging for sml_res_step_host
+    std::vector<hipEvent_t> ev;     // 3 events per timed step (start, update done, readout done)
+    int ev_cap = 0, ev_used = 0;
+    bool timing = false;
+    std::vector<double> meanstd_h;  // host copy [nlocal][72]
+};
+
+namespace {
+
+// ------------------------------------------------------------------ kernels
+// update: one thread per reservoir node; blockIdx.y = local region.
+template <typename WT>
+__global__ __launch_bounds__(256) void k_res_update(const RegionDev *__restrict__ R, const int32_t *__restrict__ a_rp,
+                                                    const uint16_t *__restrict__ a_col, const WT *__restrict__ a_val,
+                                                    const int32_t *__restrict__ w_rp,
+                                                    const uint16_t *__restrict__ w_col, const WT *__restrict__ w_val,
+                                                    const double *__restrict__ x_old, double *__restrict__ x_new,
+                                                    double *__restrict__ xaug, const double *__restrict__ feedback,
+                                                    const double *__restrict__ local_model, int ncs, double leak) {
+    const int r = blockIdx.y;
+    const RegionDev rg = R[r];
+    if (blockIdx.x == 0 && local_model)
+        for (int c = threadIdx.x; c < ncs; c += blockDim.x)
+            xaug[rg.xaug + c] = local_model[(size_t)r * ncs + c];
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= rg.n) return;
+    const double *xo = x_old + rg.x;
+    // y = A x, entries of row i in the file's order (COO semantics, duplicates add)
+    const int32_t *rp = a_rp + rg.a_rp;
+    const uint16_t *ac = a_col + rg.a_nz;
+    const WT *av = a_val + rg.a_nz;
+    double y = 0.0;
+    for (int e = rp[i], e1 = rp[i + 1]; e < e1; ++e) y = y + (double)av[e] * xo[ac[e]];
+    // temp = W_in feedback
+    const int32_t *wp = w_rp + rg.w_rp;
+    const uint16_t *wc = w_col + rg.w_nz;
+    const WT *wv = w_val + rg.w_nz;
+    const double *fb = feedback + rg.fb;
+    double t = 0.0;
+    for (int e = wp[i], e1 = wp[i + 1]; e < e1; ++e) t = t + (double)wv[e] * fb[wc[e]];
+    const double xn = tanh(y + t);
+    const double xv = (1.0 - leak) * xo[i] + leak * xn;
+    x_new[rg.x + i] = xv;
+    xaug[rg.xaug + ncs + i] = (i & 1) ? xv * xv : xv;  // x_temp(2:n:2)**2 (1-based even)
+}
+
+template <typename WT>
+struct Vec4;
+template <>
+struct Vec4<float> {
+    typedef float4 T;
+};
+template <>
+struct Vec4<double> {
+    typedef double4 T;
+};
+
+// readout: one wave per (region, 8-row group) item, 4 waves per block; blocks are
+// remapped so that the items of one region stay on one XCD's L2 (x_aug reuse).
+template <typename WT>
+__global__ __launch_bounds__(256) void k_res_readout(const RegionDev *__restrict__ R, const WT *__restrict__ wout,
+                                                     const double *__restrict__ xaug,
+                                                     const double *__restrict__ meanstd,
+                                                     const int8_t *__restrict__ outl, double *__restrict__ outvec,
+                                                     int nout, int groups, int nitems) {
+    const int nb = gridDim.x, b = blockIdx.x;
+    const int q8 = nb / 8, rem = nb % 8, xcd = b % 8, idx = b / 8;
+    const int bs = xcd * q8 + min(xcd, rem) + idx;  // bijective XCD-contiguous remap
+    const int lane = threadIdx.x & 63;
+    const int item = bs * 4 + (threadIdx.x >> 6);
+    if (item >= nitems) return;
+    const int r = item / groups, g = item % groups;
+    const RegionDev rg = R[r];
+    const int ld = rg.ld;
+    const WT *W = wout + rg.wout + (size_t)(g * kRows) * ld;
+    const double *xa = xaug + rg.xaug;
+    typedef typename Vec4<WT>::T V;
+    double acc[kRows];
+#pragma unroll
+    for (int q = 0; q < kRows; ++q) acc[q] = 0.0;
+#pragma unroll 2
+    for (int j = lane * 4; j < ld; j += 256) {
+        const double4 xv = *reinterpret_cast<const double4 *>(xa + j);
+        V w[kRows];
+#pragma unroll
+        for (int q = 0; q < kRows; ++q) w[q] = *reinterpret_cast<const V *>(W + (size_t)q * ld + j);
+#pragma unroll
+        for (int q = 0; q < kRows; ++q) {
+            double s = acc[q];
+            s = fma((double)w[q].x, xv.x, s);
+            s = fma((double)w[q].y, xv.y, s);
+            s = fma((double)w[q].z, xv.z, s);
+            s = fma((double)w[q].w, xv.w, s);
+            acc[q] = s;
+        }
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1)
+#pragma unroll
+        for (int q = 0; q < kRows; ++q) acc[q] += __shfl_xor(acc[q], off, 64);
+    if (lane < kRows) {
+        const int o = g * kRows + lane;
+        double v = acc[0];
+#pragma unroll
+        for (int q = 1; q < kRows; ++q)
+            if (lane == q) v = acc[q];
+        if (o < nout) {
+            const int l = outl[o];
+            if (l >= 0) {  // unstandardize_state_vec_res: x*std + mean (two roundings)
+                const double t = v * meanstd[(size_t)r * 2 * kMeanStd + kMeanStd + l];
+                v = t + meanstd[(size_t)r * 2 * kMeanStd + l];
+            }
+            outvec[(size_t)r * nout + o] = v;
+        }
+    }
+}
+
+// assemble: all regions' outvecs -> global grids, with the root's clips
+__global__ void k_assemble(const int32_t *__restrict__ dst, const double *__restrict__ ov, double *__restrict__ g4,
+                           double *__restrict__ g2, double *__restrict__ pr, int total) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= total) return;
+    const int d = dst[e];
+    if (d < 0) return;
+    double v = ov[e];
+    if (d < kGrid4d) {
+        if ((d & 3) == 3 && v < 0.000001) v = 0.000001;  // mpires.f90:448-450
+        g4[d] = v;
+    } else if (d < kGrid4d + kGrid2d) {
+        g2[d - kGrid4d] = v;
+    } else {
+        if (v < 0.00001) v = 0.0;  // mpires.f90:474-478
+        pr[d - kGrid4d - kGrid2d] = v;
+    }
+}
+
+__device__ inline double grid_at(int src, const double *g4, const double *g2, const double *pr) {
+    if (src < kGrid4d) return g4[src];
+    if (src < kGrid4d + kGrid2d) return g2[src - kGrid4d];
+    return pr[src - kGrid4d - kGrid2d];
+}
+
+// tile feedback: overlap tiles of the global grids, standardized (x-mean)/std
+__global__ void k_tile_feedback(const int32_t *__restrict__ src, const uint8_t *__restrict__ lidx,
+                                const uint16_t *__restrict__ reg, const double *__restrict__ meanstd,
+                                const double *__restrict__ g4, const double *__restrict__ g2,
+                                const double *__restrict__ pr, const double *__restrict__ tisr,
+                                double *__restrict__ feedback, int total) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= total) return;
+    const int s = src[e];
+    if (s == kSrcKeep) return;
+    if (s < kSrcKeep) {  // tisr entry: -2 - packed index
+        if (tisr) feedback[e] = tisr[-2 - s];
+        return;
+    }
+    const double *ms = meanstd + (size_t)reg[e] * 2 * kMeanStd;
+    const int l = lidx[e];
+    const double t = grid_at(s, g4, g2, pr) - ms[l];
+    feedback[e] = t / ms[kMeanStd + l];
+}
+
+// tile local_model: SPEEDY forecast at the region's own points, standardized
+__global__ void k_tile_local_model(const int32_t *__restrict__ src, const uint8_t *__restrict__ lidx,
+                                   const double *__restrict__ meanstd, const double *__restrict__ fc4,
+                                   const double *__restrict__ fc2, double *__restrict__ lm, int ncs, int total) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= total) return;
+    const int s = src[e];
+    const double v = s < kGrid4d ? fc4[s] : fc2[s - kGrid4d];
+    const double *ms = meanstd + (size_t)(e / ncs) * 2 * kMeanStd;
+    const int l = lidx[e];
+    const double t = v - ms[l];
+    lm[e] = t / ms[kMeanStd + l];
+}
+
+// --------------------------------------------------------------- host helpers
+template <typename T>
+int dalloc(T **p, size_t count) {
+    *p = nullptr;
+    if (count == 0) count = 1;
+    SML_HIP(hipMalloc((void **)p, count * sizeof(T)));
+    return SML_OK;
+}
+
+int dalloc_bytes(void **p, size_t bytes) {
+    *p = nullptr;
+    SML_HIP(hipMalloc(p, bytes ? bytes : 16));
+    return SML_OK;
+}
+
+size_t wbytes(const sml_reservoirs *c) { return c->wdtype == SML_F32 ? 4 : 8; }
+
+// mean/std index (0-based) of output o of the bottom-level 2x2 reservoir:
+// atmo (var,x,y,z) -> (var-1)*8+z, logp -> 33, precip -> 35 (1-based; :1815-1846)
+int out_std_index(int o, const RegionGeom &g) {
+    const int res2d = g.resx * g.resy, natmo = kVars * res2d * kZGrid;
+    if (o < natmo) {
+        const int v = o % kVars, z = o / (kVars * res2d);
+        return v * kZGrid + z;
+    }
+    if (o < natmo + res2d) return 32;
+    if (o < natmo + 2 * res2d) return 34;
+    return -1;
+}
+
+int build_tables(sml_reservoirs *c) {
+    // assemble: every region of the decomposition (outvec_all is global)
+    std::vector<int32_t> dst((size_t)c->numregions * c->nout, -1);
+    for (int r = 0; r < c->numregions; ++r) {
+        RegionGeom g;
+        region_geom(c->numregions, r, &g);
+        const int rx = g.resx, ry = g.resy, natmo = kVars * rx * ry * kZGrid;
+        for (int o = 0; o < c->nout; ++o) {
+            int d = -1;
+            if (o < natmo) {
+                const int v = o % kVars, x = (o / kVars) % rx, y = (o / (kVars * rx)) % ry, z = o / (kVars * rx * ry);
+                d = g4(v, g.res_xstart - 1 + x, g.res_ystart - 1 + y, z);
+            } else if (o < natmo + rx * ry) {
+                const int p = o - natmo;
+                d = kGrid4d + g2(g.res_xstart - 1 + p % rx, g.res_ystart - 1 + p / rx);
+            } else if (o < natmo + 2 * rx * ry) {
+                const int p = o - natmo - rx * ry;
+                d = kGrid4d + kGrid2d + g2(g.res_xstart - 1 + p % rx, g.res_ystart - 1 + p / rx);
+            }
+            dst[(size_t)r * c->nout + o] = d;
+        }
+    }
+    // feedback tiles of the local regions (tile_4d_and_logp_to_local_state_input +
+    // standardize_state_vec_input + precip standardisation + tisr + sst)
+    std::vector<int32_t> fsrc(c->tot_fb);
+    std::vector<uint8_t> fl(c->tot_fb, 0);
+    std::vector<uint16_t> freg(c->tot_fb);
+    std::vector<int32_t> lsrc((size_t)c->nlocal * std::max(c->ncs, 1), 0);
+    std::vector<uint8_t> ll((size_t)c->nlocal * std::max(c->ncs, 1), 0);
+    for (int i = 0; i < c->nlocal; ++i) {
+        const RegionGeom &g = c->geom[i];
+        const int ix = g.inx, iy = g.iny, in2d = ix * iy, natmo = kVars * in2d * kZGrid;
+        const int64_t base = c->rd[i].fb;
+        auto gx = [&](int lx) { return input_x(g, lx + 1) - 1; };
+        for (int z = 0; z < kZGrid; ++z)
+            for (int ly = 0; ly < iy; ++ly)
+                for (int lx = 0; lx < ix; ++lx)
+                    for (int v = 0; v < kVars; ++v) {
+                        const int64_t e = base + v + kVars * (lx + ix * (ly + iy * z));
+                        fsrc[e] = g4(v, gx(lx), g.in_ystart - 1 + ly, z);
+                        fl[e] = (uint8_t)(v * kZGrid + z);
+                    }
+        for (int ly = 0; ly < iy; ++ly)
+            for (int lx = 0; lx < ix; ++lx) {
+                const int p = lx + ix * ly;
+                fsrc[base + natmo + p] = kGrid4d + g2(gx(lx), g.in_ystart - 1 + ly);
+                fl[base + natmo + p] = 32;  // logp (l = 33)
+                fsrc[base + natmo + in2d + p] = kGrid4d + kGrid2d + g2(gx(lx), g.in_ystart - 1 + ly);
+                fl[base + natmo + in2d + p] = 34;  // precip (l = 35)
+            }
+        int64_t off = base + natmo + 2 * in2d;
+        if (c->sst[i]) {
+            for (int p = 0; p < in2d; ++p) fsrc[off + p] = kSrcKeep;
+            off += in2d;
+        }
+        for (int p = 0; p < in2d; ++p) fsrc[off + p] = -2 - (i * kTisrStride + p);
+        for (int64_t e = base; e < base + c->ninp[i]; ++e) freg[e] = (uint16_t)i;
+        // local_model: the region's own points of the SPEEDY forecast grids
+        const int rx = g.resx, ry = g.resy, na = kVars * rx * ry * kZGrid;
+        for (int cidx = 0; cidx < c->ncs; ++cidx) {
+            int s = 0, l = 0;
+            if (cidx < na) {
+                const int v = cidx % kVars, x = (cidx / kVars) % rx, y = (cidx / (kVars * rx)) % ry,
+                          z = cidx / (kVars * rx * ry);
+                s = g4(v, g.res_xstart - 1 + x, g.res_ystart - 1 + y, z);
+                l = v * kZGrid + z;
+            } else {
+                const int p = cidx - na;
+                s = kGrid4d + g2(g.res_xstart - 1 + p % rx, g.res_ystart - 1 + (p / rx) % ry);
+                l = 32;
+            }
+            lsrc[(size_t)i * c->ncs + cidx] = s;
+            ll[(size_t)i * c->ncs + cidx] = (uint8_t)l;
+        }
+    }
+    std::vector<int8_t> outl(c->nout);
+    for (int o = 0; o < c->nout; ++o) outl[o] = (int8_t)out_std_index(o, c->geom.empty() ? RegionGeom{} : c->geom[0]);
+    int rc;
+    if ((rc = dalloc(&c->d_asm_dst, dst.size())) || (rc = dalloc(&c->d_fb_src, fsrc.size())) ||
+        (rc = dalloc(&c->d_fb_l, fl.size())) || (rc = dalloc(&c->d_fb_reg, freg.size())) ||
+        (rc = dalloc(&c->d_lm_src, lsrc.size())) || (rc = dalloc(&c->d_lm_l, ll.size())) ||
+        (rc = dalloc(&c->d_outl, outl.size())))
+        return rc;
+    SML_HIP(hipMemcpy(c->d_asm_dst, dst.data(), dst.size() * 4, hipMemcpyHostToDevice));
+    if (!fsrc.empty()) {
+        SML_HIP(hipMemcpy(c->d_fb_src, fsrc.data(), fsrc.size() * 4, hipMemcpyHostToDevice));
+        SML_HIP(hipMemcpy(c->d_fb_l, fl.data(), fl.size(), hipMemcpyHostToDevice));
+        SML_HIP(hipMemcpy(c->d_fb_reg, freg.data(), freg.size() * 2, hipMemcpyHostToDevice));
+    }
+    SML_HIP(hipMemcpy(c->d_lm_src, lsrc.data(), lsrc.size() * 4, hipMemcpyHostToDevice));
+    SML_HIP(hipMemcpy(c->d_lm_l, ll.data(), ll.size(), hipMemcpyHostToDevice));
+    SML_HIP(hipMemcpy(c->d_outl, outl.data(), outl.size(), hipMemcpyHostToDevice));
+    return SML_OK;
+}
+
+template <typename T>
+int upload(T *dst, const std::vector<T> &src) {
+    if (!src.empty()) SML_HIP(hipMemcpy(dst, src.data(), src.size() * sizeof(T), hipMemcpyHostToDevice));
+    return SML_OK;
+}
+
+// convert to the storage dtype; fp32 storage demands exact representability
+template <typename S, typename D>
+bool narrow(const S *src, size_t count, std::vector<D> &out) {
+    out.resize(count);
+    for (size_t i = 0; i < count; ++i) {
+        out[i] = (D)src[i];
+        if ((S)out[i] != src[i] && !(src[i] != src[i])) return false;
+    }
+    return true;
+}
+
+template <typename SrcT, typename StoT>
+int load_region_impl(sml_reservoirs *c, int i, const int *rows, const int *cols, const SrcT *vals, const SrcT *win,
+                     const SrcT *wout, const double *mean, const double *std) {
+    const int n = c->n[i], k = c->k[i], ninp = c->ninp[i], ld = c->ld[i], ncs = c->ncs, nout = c->nout;
+    const RegionDev &rg = c->rd[i];
+    // --- A: COO (1-based) -> CSR, stable in file order (mklsparse, mod_linalg.f90:10-25)
+    std::vector<int32_t> rp(n + 1, 0);
+    for (int e = 0; e < k; ++e) {
+        SML_REQUIRE(rows[e] >= 1 && rows[e] <= n && cols[e] >= 1 && cols[e] <= n,
+                    "region %d: A entry %d out of range (row %d col %d, n %d)", i, e, rows[e], cols[e], n);
+        rp[rows[e]]++;
+    }
+    for (int r = 0; r < n; ++r) rp[r + 1] += rp[r];
+    std::vector<int32_t> fill(rp.begin(), rp.end() - 1);
+    std::vector<uint16_t> acol(k);
+    std::vector<StoT> aval(k);
+    for (int e = 0; e < k; ++e) {
+        const int p = fill[rows[e] - 1]++;
+        acol[p] = (uint16_t)(cols[e] - 1);
+        aval[p] = (StoT)vals[e];
+        SML_REQUIRE((SrcT)aval[p] == vals[e], "region %d: A value %d not representable in the storage dtype", i, e);
+    }
+    // --- W_in: dense win(n, ninp) column-major -> CSR by row, columns ascending
+    std::vector<int32_t> wrp(n + 1, 0);
+    for (int col = 0; col < ninp; ++col)
+        for (int r = 0; r < n; ++r)
+            if (win[(size_t)col * n + r] != (SrcT)0) wrp[r + 1]++;
+    for (int r = 0; r < n; ++r) wrp[r + 1] += wrp[r];
+    const int64_t wnz = wrp[n];
+    SML_REQUIRE(wnz <= c->w_nz_cap[i],
+                "region %d: W_in has %lld nonzeros, more than the %lld reserved (one per row as trained; "
+                "dense W_in is supported through sml_res_create of a fresh context)",
+                i, (long long)wnz, (long long)c->w_nz_cap[i]);
+    std::vector<int32_t> wfill(wrp.begin(), wrp.end() - 1);
+    std::vector<uint16_t> wcol(wnz);
+    std::vector<StoT> wval(wnz);
+    for (int col = 0; col < ninp; ++col)
+        for (int r = 0; r < n; ++r) {
+            const SrcT v = win[(size_t)col * n + r];
+            if (v == (SrcT)0) continue;
+            const int p = wfill[r]++;
+            wcol[p] = (uint16_t)col;
+            wval[p] = (StoT)v;
+            SML_REQUIRE((SrcT)wval[p] == v, "region %d: W_in value not representable in the storage dtype", i);
+        }
+    // --- W_out: wout(nout, ncs+n) column-major -> [nout_pad][ld] row-major
+    std::vector<StoT> wt((size_t)c->nout_pad * ld, (StoT)0);
+    for (int j = 0; j < ncs + n; ++j)
+        for (int o = 0; o < nout; ++o) {
+            const SrcT v = wout[(size_t)j * nout + o];
+            StoT s = (StoT)v;
+            SML_REQUIRE((SrcT)s == v || v != v, "region %d: W_out value not representable in the storage dtype", i);
+            wt[(size_t)o * ld + j] = s;
+        }
+    // --- upload
+    const size_t wb = sizeof(StoT);
+    SML_HIP(hipMemcpy(c->d_a_rp + rg.a_rp, rp.data(), rp.size() * 4, hipMemcpyHostToDevice));
+    SML_HIP(hipMemcpy(c->d_a_col + rg.a_nz, acol.data(), acol.size() * 2, hipMemcpyHostToDevice));
+    SML_HIP(hipMemcpy((char *)c->d_a_val + rg.a_nz * wb, aval.data(), aval.size() * wb, hipMemcpyHostToDevice));
+    SML_HIP(hipMemcpy(c->d_w_rp + rg.w_rp, wrp.data(), wrp.size() * 4, hipMemcpyHostToDevice));
+    if (wnz) {
+        SML_HIP(hipMemcpy(c->d_w_col + rg.w_nz, wcol.data(), wcol.size() * 2, hipMemcpyHostToDevice));
+        SML_HIP(hipMemcpy((char *)c->d_w_val + rg.w_nz * wb, wval.data(), wval.size() * wb, hipMemcpyHostToDevice));
+    }
+    SML_HIP(hipMemcpy((char *)c->d_wout + rg.wout * wb, wt.data(), wt.size() * wb, hipMemcpyHostToDevice));
+    double ms[2 * kMeanStd];
+    std::memcpy(ms, mean, sizeof(double) * kMeanStd);
+    std::memcpy(ms + kMeanStd, std, sizeof(double) * kMeanStd);
+    std::memcpy(&c->meanstd_h[(size_t)i * 2 * kMeanStd], ms, sizeof ms);
+    SML_HIP(hipMemcpy(c->d_meanstd + (size_t)i * 2 * kMeanStd, ms, sizeof ms, hipMemcpyHostToDevice));
+    c->loaded[i] = 1;
+    return SML_OK;
+}
+
+int check_region(const sml_reservoirs *c, int i) {
+    SML_REQUIRE(c != nullptr, "null reservoir context");
+    SML_REQUIRE(i >= 0 && i < c->nlocal, "local region index %d out of range [0,%d)", i, c->nlocal);
+    return SML_OK;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------ API
+extern "C" int sml_res_destroy(sml_reservoirs *c) {
+    if (!c) return SML_OK;
+    void *ptrs[] = {c->d_rd,    c->d_a_rp,    c->d_w_rp,   c->d_a_col,  c->d_w_col,  c->d_a_val,  c->d_w_val,
+                    c->d_wout,  c->d_x[0],    c->d_x[1],   c->d_xaug,   c->d_meanstd, c->d_outl,  c->d_asm_dst,
+                    c->d_fb_src, c->d_fb_l,   c->d_fb_reg, c->d_lm_src, c->d_lm_l,   c->d_io};
+    for (void *p : ptrs)
+        if (p) (void)hipFree(p);
+    for (hipEvent_t e : c->ev)
+        if (e) (void)hipEventDestroy(e);
+    delete c;
+    return SML_OK;
+}
+
+extern "C" int sml_res_create(int numregions, int nlocal, const int *region_ids, const unsigned char *sst_flags,
+                              const int *n, const int *k, int chunk_speedy, int nout, int weight_dtype,
+                              double leakage, sml_reservoirs **out) {
+    SML_REQUIRE(out != nullptr, "out is null");
+    *out = nullptr;
+    int fx, fy;
+    SML_REQUIRE(decompose(numregions, &fx, &fy), "numregions %d does not decompose the 96x48 grid", numregions);
+    SML_REQUIRE(nlocal >= 0 && nlocal <= numregions && nlocal < 65536, "bad nlocal %d", nlocal);
+    SML_REQUIRE(nlocal == 0 || (region_ids && sst_flags && n && k), "null per-region arrays");
+    SML_REQUIRE(chunk_speedy >= 0 && nout > 0, "bad chunk sizes (%d, %d)", chunk_speedy, nout);
+    SML_REQUIRE(weight_dtype == SML_F32 || weight_dtype == SML_F64, "weight_dtype must be SML_F32 or SML_F64");
+    sml_reservoirs *c = new (std::nothrow) sml_reservoirs();
+    if (!c) return fail(SML_ERR_NOMEM, "host allocation failed");
+    c->numregions = numregions;
+    c->nlocal = nlocal;
+    c->ncs = chunk_speedy;
+    c->nout = nout;
+    c->nout_pad = (nout + kRows - 1) / kRows * kRows;
+    c->wdtype = weight_dtype;
+    c->leakage = leakage;
+    (void)hipGetDevice(&c->device);
+    c->region_ids.assign(region_ids, region_ids + nlocal);
+    c->sst.assign(sst_flags, sst_flags + nlocal);
+    c->n.assign(n, n + nlocal);
+    c->k.assign(k, k + nlocal);
+    c->loaded.assign(nlocal, 0);
+    c->meanstd_h.assign((size_t)nlocal * 2 * kMeanStd, 0.0);
+    c->geom.resize(nlocal);
+    c->ninp.resize(nlocal);
+    c->ld.resize(nlocal);
+    c->rd.resize(nlocal);
+    c->w_nz_cap.resize(nlocal);
+    for (int i = 0; i < nlocal; ++i) {
+        if (!region_geom(numregions, region_ids[i], &c->geom[i])) {
+            sml_res_destroy(c);
+            return fail(SML_ERR_ARG, "region id %d out of range", region_ids[i]);
+        }
+        if (n[i] <= 0 || n[i] > 65535 || k[i] < 0) {
+            sml_res_destroy(c);
+            return fail(SML_ERR_ARG, "region %d: n=%d (1..65535) k=%d", i, n[i], k[i]);
+        }
+        const RegionGeom &g = c->geom[i];
+        if (kVars * g.resx * g.resy * kZGrid + 2 * g.resx * g.resy != nout ||
+            (chunk_speedy && chunk_speedy != kVars * g.resx * g.resy * kZGrid + g.resx * g.resy)) {
+            sml_res_destroy(c);
+            return fail(SML_ERR_ARG, "nout %d / chunk_speedy %d do not match the %dx%d region tiles", nout,
+                        chunk_speedy, g.resx, g.resy);
+        }
+        c->ninp[i] = region_ninp(g, sst_flags[i] != 0);
+        c->ld[i] = (chunk_speedy + n[i] + 3) / 4 * 4;
+        c->w_nz_cap[i] = n[i];
+        RegionDev &r = c->rd[i];
+        r.n = n[i];
+        r.ninp = c->ninp[i];
+        r.ld = c->ld[i];
+        r.pad_ = 0;
+        r.a_rp = c->tot_a_rp;
+        c->tot_a_rp += n[i] + 1;
+        r.a_nz = c->tot_a_nz;
+        c->tot_a_nz += k[i];
+        r.w_rp = c->tot_w_rp;
+        c->tot_w_rp += n[i] + 1;
+        r.w_nz = c->tot_w_nz;
+        c->tot_w_nz += n[i];
+        r.wout = c->tot_wout;
+        c->tot_wout += (int64_t)c->nout_pad * c->ld[i];
+        r.x = c->tot_x;
+        c->tot_x += n[i];
+        r.xaug = c->tot_xaug;
+        c->tot_xaug += c->ld[i];
+        r.fb = c->tot_fb;
+        c->tot_fb += c->ninp[i];
+        c->maxn = std::max(c->maxn, n[i]);
+    }
+    const size_t wb = wbytes(c);
+    int rc;
+    if ((rc = dalloc(&c->d_rd, nlocal)) || (rc = dalloc(&c->d_a_rp, c->tot_a_rp)) ||
+        (rc = dalloc(&c->d_a_col, c->tot_a_nz)) || (rc = dalloc_bytes(&c->d_a_val, c->tot_a_nz * wb)) ||
+        (rc = dalloc(&c->d_w_rp, c->tot_w_rp)) || (rc = dalloc(&c->d_w_col, c->tot_w_nz)) ||
+        (rc = dalloc_bytes(&c->d_w_val, c->tot_w_nz * wb)) || (rc = dalloc_bytes(&c->d_wout, c->tot_wout * wb)) ||
+        (rc = dalloc(&c->d_x[0], c->tot_x)) || (rc = dalloc(&c->d_x[1], c->tot_x)) ||
+        (rc = dalloc(&c->d_xaug, c->tot_xaug)) || (rc = dalloc(&c->d_meanstd, (size_t)nlocal * 2 * kMeanStd))) {
+        sml_res_destroy(c);
+        return rc;
+    }
+    hipError_t e = hipSuccess;
+    if (e == hipSuccess) e = hipMemset(c->d_a_rp, 0, std::max<int64_t>(c->tot_a_rp, 1) * 4);
+    if (e == hipSuccess) e = hipMemset(c->d_w_rp, 0, std::max<int64_t>(c->tot_w_rp, 1) * 4);
+    if (e == hipSuccess) e = hipMemset(c->d_wout, 0, std::max<int64_t>(c->tot_wout * wb, 16));
+    if (e == hipSuccess) e = hipMemset(c->d_x[0], 0, std::max<int64_t>(c->tot_x, 1) * 8);
+    if (e == hipSuccess) e = hipMemset(c->d_x[1], 0, std::max<int64_t>(c->tot_x, 1) * 8);
+    if (e == hipSuccess) e = hipMemset(c->d_xaug, 0, std::max<int64_t>(c->tot_xaug, 1) * 8);
+    if (e == hipSuccess && nlocal)
+        e = hipMemcpy(c->d_rd, c->rd.data(), sizeof(RegionDev) * nlocal, hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        sml_res_destroy(c);
+        return fail(SML_ERR_HIP, "sml_res_create: %s", hipGetErrorString(e));
+    }
+    // unit std / zero mean until loaded
+    for (int i = 0; i < nlocal; ++i)
+        for (int l = 0; l < kMeanStd; ++l) c->meanstd_h[(size_t)i * 2 * kMeanStd + kMeanStd + l] = 1.0;
+    if (nlocal) {
+        e = hipMemcpy(c->d_meanstd, c->meanstd_h.data(), c->meanstd_h.size() * 8, hipMemcpyHostToDevice);
+        if (e != hipSuccess) {
+            sml_res_destroy(c);
+            return fail(SML_ERR_HIP, "sml_res_create: %s", hipGetErrorString(e));
+        }
+    }
+    if ((rc = build_tables(c))) {
+        sml_res_destroy(c);
+        return rc;
+    }
+    *out = c;
+    return SML_OK;
+}
+
+extern "C" int sml_res_ninp(const sml_reservoirs *c, int i, int *ninp) {
+    if (int rc = check_region(c, i)) return rc;
+    SML_REQUIRE(ninp, "ninp is null");
+    *ninp = c->ninp[i];
+    return SML_OK;
+}
+
+extern "C" int sml_res_feedback_offsets(const sml_reservoirs *c, int64_t *offsets) {
+    SML_REQUIRE(c && offsets, "null argument");
+    for (int i = 0; i < c->nlocal; ++i) offsets[i] = c->rd[i].fb;
+    offsets[c->nlocal] = c->tot_fb;
+    return SML_OK;
+}
+
+extern "C" int sml_res_load_region_f32(sml_reservoirs *c, int i, const int *rows, const int *cols, const float *vals,
+                                       const float *win, const float *wout, const double *mean, const double *std) {
+    if (int rc = check_region(c, i)) return rc;
+    SML_REQUIRE(win && wout && mean && std && (c->k[i] == 0 || (rows && cols && vals)), "null weight array");
+    if (c->wdtype == SML_F32) return load_region_impl<float, float>(c, i, rows, cols, vals, win, wout, mean, std);
+    return load_region_impl<float, double>(c, i, rows, cols, vals, win, wout, mean, std);
+}
+
+extern "C" int sml_res_load_region_f64(sml_reservoirs *c, int i, const int *rows, const int *cols,
+                                       const double *vals, const double *win, const double *wout,
+                                       const double *mean, const double *std) {
+    if (int rc = check_region(c, i)) return rc;
+    SML_REQUIRE(win && wout && mean && std && (c->k[i] == 0 || (rows && cols && vals)), "null weight array");
+    if (c->wdtype == SML_F32) return load_region_impl<double, float>(c, i, rows, cols, vals, win, wout, mean, std);
+    return load_region_impl<double, double>(c, i, rows, cols, vals, win, wout, mean, std);
+}
+
+extern "C" int sml_res_set_state(sml_reservoirs *c, int i, const double *x) {
+    if (int rc = check_region(c, i)) return rc;
+    SML_REQUIRE(x, "x is null");
+    SML_HIP(hipMemcpy(c->d_x[c->cur] + c->rd[i].x, x, (size_t)c->n[i] * 8, hipMemcpyHostToDevice));
+    return SML_OK;
+}
+
+extern "C" int sml_res_get_state(sml_reservoirs *c, int i, double *x) {
+    if (int rc = check_region(c, i)) return rc;
+    SML_REQUIRE(x, "x is null");
+    SML_HIP(hipDeviceSynchronize());
+    SML_HIP(hipMemcpy(x, c->d_x[c->cur] + c->rd[i].x, (size_t)c->n[i] * 8, hipMemcpyDeviceToHost));
+    return SML_OK;
+}
+
+extern "C" int sml_res_enable_timing(sml_reservoirs *c, int capacity) {
+    SML_REQUIRE(c, "null context");
+    SML_REQUIRE(capacity >= 0, "capacity must be >= 0");
+    while (c->ev_cap < capacity) {
+        for (int q = 0; q < 3; ++q) {
+            hipEvent_t e;
+            SML_HIP(hipEventCreate(&e));
+            c->ev.push_back(e);
+        }
+        ++c->ev_cap;
+    }
+    c->timing = capacity > 0;
+    c->ev_used = 0;
+    return SML_OK;
+}
+
+extern "C" int sml_res_kernel_times(sml_reservoirs *c, float *update_ms, float *readout_ms, int max_steps,
+                                    int *count) {
+    SML_REQUIRE(c && count, "null argument");
+    const int n = std::min(c->ev_used, max_steps);
+    for (int s = 0; s < n; ++s) {
+        SML_HIP(hipEventSynchronize(c->ev[3 * s + 2]));
+        float a = 0, b = 0;
+        SML_HIP(hipEventElapsedTime(&a, c->ev[3 * s], c->ev[3 * s + 1]));
+        SML_HIP(hipEventElapsedTime(&b, c->ev[3 * s + 1], c->ev[3 * s + 2]));
+        if (update_ms) update_ms[s] = a;
+        if (readout_ms) readout_ms[s] = b;
+    }
+    *count = n;
+    c->ev_used = 0;
+    return SML_OK;
+}
+
+extern "C" int sml_res_step(sml_reservoirs *c, const double *d_feedback, const double *d_local_model,
+                            double *d_outvec, void *stream) {
+    SML_REQUIRE(c, "null context");
+    if (c->nlocal == 0) return SML_OK;
+    SML_REQUIRE(d_feedback && d_outvec, "null device buffer");
+    SML_REQUIRE(c->ncs == 0 || d_local_model, "hybrid context needs d_local_model");
+    for (int i = 0; i < c->nlocal; ++i)
+        if (!c->loaded[i]) return fail(SML_ERR_STATE, "local region %d has no weights loaded", i);
+    hipStream_t st = (hipStream_t)stream;
+    const double *xo = c->d_x[c->cur];
+    double *xn = c->d_x[1 - c->cur];
+    const bool rec = c->timing && c->ev_used < c->ev_cap;
+    hipEvent_t *ev = rec ? &c->ev[3 * c->ev_used] : nullptr;
+    if (rec) SML_HIP(hipEventRecord(ev[0], st));
+    dim3 ug((c->maxn + 255) / 256, c->nlocal);
+    if (c->wdtype == SML_F32)
+        hipLaunchKernelGGL(k_res_update<float>, ug, dim3(256), 0, st, c->d_rd, c->d_a_rp, c->d_a_col,
+                           (const float *)c->d_a_val, c->d_w_rp, c->d_w_col, (const float *)c->d_w_val, xo, xn,
+                           c->d_xaug, d_feedback, c->ncs ? d_local_model : nullptr, c->ncs, c->leakage);
+    else
+        hipLaunchKernelGGL(k_res_update<double>, ug, dim3(256), 0, st, c->d_rd, c->d_a_rp, c->d_a_col,
+                           (const double *)c->d_a_val, c->d_w_rp, c->d_w_col, (const double *)c->d_w_val, xo, xn,
+                           c->d_xaug, d_feedback, c->ncs ? d_local_model : nullptr, c->ncs, c->leakage);
+    SML_HIP(hipGetLastError());
+    if (rec) SML_HIP(hipEventRecord(ev[1], st));
+    const int groups = c->nout_pad / kRows;
+    const int nitems = c->nlocal * groups;
+    const int nblocks = (nitems + 3) / 4;
+    if (c->wdtype == SML_F32)
+        hipLaunchKernelGGL(k_res_readout<float>, dim3(nblocks), dim3(256), 0, st, c->d_rd, (const float *)c->d_wout,
+                           c->d_xaug, c->d_meanstd, c->d_outl, d_outvec, c->nout, groups, nitems);
+    else
+        hipLaunchKernelGGL(k_res_readout<double>, dim3(nblocks), dim3(256), 0, st, c->d_rd,
+                           (const double *)c->d_wout, c->d_xaug, c->d_meanstd, c->d_outl, d_outvec, c->nout, groups,
+                           nitems);
+    SML_HIP(hipGetLastError());
+    if (rec) {
+        SML_HIP(hipEventRecord(ev[2], st));
+        ++c->ev_used;
+    }
+    c->cur = 1 - c->cur;
+    return SML_OK;
+}
+
+extern "C" int sml_res_step_host(sml_reservoirs *c, const double *feedback, const double *local_model,
+                                 double *outvec) {
+    SML_REQUIRE(c && feedback && outvec, "null argument");
+    SML_REQUIRE(c->ncs == 0 || local_model, "hybrid context needs local_model");
+    const size_t nfb = c->tot_fb, nlm = (size_t)c->nlocal * c->ncs, nov = (size_t)c->nlocal * c->nout;
+    if (!c->d_io)
+        if (int rc = dalloc(&c->d_io, nfb + nlm + nov)) return rc;
+    double *dfb = c->d_io, *dlm = dfb + nfb, *dov = dlm + nlm;
+    SML_HIP(hipMemcpy(dfb, feedback, nfb * 8, hipMemcpyHostToDevice));
+    if (nlm) SML_HIP(hipMemcpy(dlm, local_model, nlm * 8, hipMemcpyHostToDevice));
+    if (int rc = sml_res_step(c, dfb, dlm, dov, nullptr)) return rc;
+    SML_HIP(hipMemcpy(outvec, dov, nov * 8, hipMemcpyDeviceToHost));
+    return SML_OK;
+}
+
+extern "C" int sml_res_footprint(const sml_reservoirs *c, int64_t *weight_bytes, int64_t *algo_bytes) {
+    SML_REQUIRE(c, "null context");
+    const int64_t wb = (int64_t)wbytes(c);
+    int64_t w = 0, a = 0;
+    for (int i = 0; i < c->nlocal; ++i) {
+        const int64_t n = c->n[i], k = c->k[i], ninp = c->ninp[i];
+        const int64_t wout = wb * c->nout * (c->ncs + n);     // unpadded W_out
+        const int64_t amat = 4 * (n + 1) + (2 + wb) * k;      // CSR row ptr + col + val
+        const int64_t winm = 4 * (n + 1) + (2 + wb) * n;      // CSR, one entry per row
+        w += wout + amat + winm;
+        // minimal traffic: weights once, state in + out, feedback, local model, outvec
+        a += wout + amat + winm + 8 * n + 8 * n + 8 * ninp + 8 * c->ncs + 8 * c->nout;
+    }
+    if (weight_bytes) *weight_bytes = w;
+    if (algo_bytes) *algo_bytes = a;
+    return SML_OK;
+}
+
+extern "C" int sml_exchange_assemble(sml_reservoirs *c, const double *d_outvec_all, double *d_grid4d,
+                                     double *d_grid2d, double *d_precip, void *stream) {
+    SML_REQUIRE(c && d_outvec_all && d_grid4d && d_grid2d && d_precip, "null argument");
+    const int total = c->numregions * c->nout;
+    hipLaunchKernelGGL(k_assemble, dim3((total + 255) / 256), dim3(256), 0, (hipStream_t)stream, c->d_asm_dst,
+                       d_outvec_all, d_grid4d, d_grid2d, d_precip, total);
+    SML_HIP(hipGetLastError());
+    return SML_OK;
+}
+
+extern "C" int sml_res_tile_inputs(sml_reservoirs *c, const double *d_grid4d, const double *d_grid2d,
+                                   const double *d_precip, const double *d_fc4d, const double *d_fc2d,
+                                   const double *d_tisr, double *d_feedback, double *d_local_model, void *stream) {
+    SML_REQUIRE(c && d_grid4d && d_grid2d && d_precip && d_feedback, "null argument");
+    hipStream_t st = (hipStream_t)stream;
+    if (c->tot_fb) {
+        const int total = (int)c->tot_fb;
+        hipLaunchKernelGGL(k_tile_feedback, dim3((total + 255) / 256), dim3(256), 0, st, c->d_fb_src, c->d_fb_l,
+                           c->d_fb_reg, c->d_meanstd, d_grid4d, d_grid2d, d_precip, d_tisr, d_feedback, total);
+        SML_HIP(hipGetLastError());
+    }
+    if (c->ncs && d_fc4d && c->nlocal) {
+        SML_REQUIRE(d_fc2d && d_local_model, "forecast grids need d_fc2d and d_local_model");
+        const int total = c->nlocal * c->ncs;
+        hipLaunchKernelGGL(k_tile_local_model, dim3((total + 255) / 256), dim3(256), 0, st, c->d_lm_src, c->d_lm_l,
+                           c->d_meanstd, d_fc4d, d_fc2d, d_local_model, c->ncs, total);
+        SML_HIP(hipGetLastError());
+    }
+    return SML_OK;
+}

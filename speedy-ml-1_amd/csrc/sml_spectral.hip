@@ -1,0 +1,503 @@
+// sml_spectral.hip -- batched T30 spherical-harmonic transforms on gfx950.
+//
+// The reference transforms one field per call (grid / spec, spe_spectral.f90:389-414):
+// a Legendre sum per latitude (gridy/specy, :454-538) and a 96-point FFTPACK real
+// FFT per latitude row (gridx/specx, spe_subfft_fftpack.f90:15-87).  Here every
+// call transforms a batch of fields and both stages are fp64 MFMA GEMMs
+// (v_mfma_f64_16x16x4_f64):
+//
+//   Legendre (per zonal wavenumber m):  C[(field,Re/Im)][lat] = A[(field,Re/Im)][n] * P_m[n][lat]
+//     16 rows = 8 fields x {Re, Im}; K = the 16 n of one parity (odd n build the
+//     hemispherically symmetric part, even n the antisymmetric part, as gridy does);
+//     N = 24 Gaussian latitudes (padded to 32).  P_m tiles come from a masked
+//     table (the triangular T30 mask nsh2 is baked in as exact zeros).
+//   Fourier (per field):  grid[lat][lon] = varm[lat][c] * D[c][lon]
+//     M = 48 latitudes, N = 96 longitudes, K = 62 packed coefficients (padded to 64).
+//     D is the real-DFT matrix of FFTPACK's half-complex convention.
+//
+// MFMA f64 16x16x4 operand map (cdna_hip_programming.md section 3): lane l holds
+// A[l&15][l>>4] and B[l>>4][l&15]; the 4 results per lane are
+// C[(l>>4) + 4q][l&15], q = 0..3.
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "sml_spectral_tables.hpp"
+
+using namespace sml;
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+#define MFMA64(a, b, c) __builtin_amdgcn_mfma_f64_16x16x4f64((a), (b), (c), 0, 0, 0)
+
+constexpr int kSpecField = kMX2 * kNX;  // 1984
+constexpr int kVarmField = kMX2 * kIL;  // 2976
+constexpr int kGridField = kIX * kIL;   // 4608
+constexpr int kJPad = 32;
+
+struct sml_spectral {
+    SpectralTables t;
+    int device;
+    double *d_pinv;   // [m][n][32]: P_mn(lat j) masked (ll <= ntrun1), j padded to 32
+    double *d_pfwd;   // [m][n][24]: masked (ll <= ntrun1 and n <= ntrun1-1)
+    double *d_dinv;   // [64][96]
+    double *d_dfwd;   // [96][64]
+    double *d_wt;     // [24]
+    double *d_cosgr;  // [48]
+    double *d_cosgr2; // [48]
+    double *d_coef;   // gradx[31] | uvdx | uvdym | uvdyp | vddym | vddyp ([32][31] each)
+    double *d_work;   // varm workspace
+    size_t work_fields;
+    double *d_hbuf;   // staging for the host convenience calls
+    size_t hbuf_doubles;
+};
+
+namespace {
+
+// ------------------------------------------------------------------ kernels
+// gridy: spec[f][n][62] -> varm[f][lat][62]  (one wave per (m, 8-field tile))
+__global__ __launch_bounds__(64) void k_gridy(const double *__restrict__ spec, double *__restrict__ varm,
+                                              const double *__restrict__ pinv, int nf) {
+    const int m = blockIdx.x;
+    const int f0 = blockIdx.y * 8;
+    const int l = threadIdx.x, r = l & 15, kk = l >> 4;
+    const int fa = f0 + (r >> 1);
+    const bool ok = fa < nf;
+    const double *sp = spec + (size_t)(ok ? fa : 0) * kSpecField + 2 * m + (r & 1);
+    const double *pm = pinv + (size_t)m * kNX * kJPad;
+    d4 acc00 = {0, 0, 0, 0}, acc01 = acc00, acc10 = acc00, acc11 = acc00;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        const int n_odd = 2 * (4 * s + kk);  // n = 1,3,.. (1-based): symmetric part
+        const int n_even = n_odd + 1;        // n = 2,4,..: antisymmetric part
+        const double a0 = ok ? sp[n_odd * kMX2] : 0.0;
+        const double a1 = ok ? sp[n_even * kMX2] : 0.0;
+        acc00 = MFMA64(a0, pm[n_odd * kJPad + r], acc00);
+        acc01 = MFMA64(a0, pm[n_odd * kJPad + 16 + r], acc01);
+        acc10 = MFMA64(a1, pm[n_even * kJPad + r], acc10);
+        acc11 = MFMA64(a1, pm[n_even * kJPad + 16 + r], acc11);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int row = kk + 4 * q;
+        const int f = f0 + (row >> 1);
+        if (f >= nf) continue;
+        double *vr = varm + (size_t)f * kVarmField + 2 * m + (row & 1);
+        {   // latitudes j = r (southern half), mirror j1 = 47 - j (northern)
+            const int j = r;
+            const double s = acc00[q], d = acc10[q];
+            vr[(kIL - 1 - j) * kMX2] = s + d;
+            vr[j * kMX2] = s - d;
+        }
+        const int j = 16 + r;
+        if (j < kIY) {
+            const double s = acc01[q], d = acc11[q];
+            vr[(kIL - 1 - j) * kMX2] = s + d;
+            vr[j * kMX2] = s - d;
+        }
+    }
+}
+
+// gridx: varm[f][lat][62] -> grid[f][lat][96]  (one block of 6 waves per field;
+// wave w owns longitudes 16w..16w+15 for all 48 latitudes)
+__global__ __launch_bounds__(384) void k_gridx(const double *__restrict__ varm, double *__restrict__ grid,
+                                               const double *__restrict__ dinv, const double *__restrict__ cosgr,
+                                               int kcos) {
+    const int f = blockIdx.x;
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63, r = l & 15, kk = l >> 4;
+    const double *vr = varm + (size_t)f * kVarmField;
+    d4 acc0 = {0, 0, 0, 0}, acc1 = acc0, acc2 = acc0;
+#pragma unroll 4
+    for (int s = 0; s < kCPad / 4; ++s) {
+        const int c = 4 * s + kk;
+        const double b = dinv[c * kIX + 16 * w + r];
+        const bool cv = c < kMX2;
+        const double a0 = cv ? vr[r * kMX2 + c] : 0.0;
+        const double a1 = cv ? vr[(16 + r) * kMX2 + c] : 0.0;
+        const double a2 = cv ? vr[(32 + r) * kMX2 + c] : 0.0;
+        acc0 = MFMA64(a0, b, acc0);
+        acc1 = MFMA64(a1, b, acc1);
+        acc2 = MFMA64(a2, b, acc2);
+    }
+    double *g = grid + (size_t)f * kGridField + 16 * w + r;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int j0 = kk + 4 * q;
+        double v0 = acc0[q], v1 = acc1[q], v2 = acc2[q];
+        if (kcos != 1) {
+            v0 = v0 * cosgr[j0];
+            v1 = v1 * cosgr[16 + j0];
+            v2 = v2 * cosgr[32 + j0];
+        }
+        g[j0 * kIX] = v0;
+        g[(16 + j0) * kIX] = v1;
+        g[(32 + j0) * kIX] = v2;
+    }
+}
+
+// specx: grid[f][lat][96] (optionally x scale[lat]) -> varm[f][lat][62]
+// (one block of 4 waves per field; wave w owns coefficients 16w..16w+15)
+__global__ __launch_bounds__(256) void k_specx(const double *__restrict__ grid, double *__restrict__ varm,
+                                               const double *__restrict__ dfwd, const double *__restrict__ scale) {
+    const int f = blockIdx.x;
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63, r = l & 15, kk = l >> 4;
+    const double *g = grid + (size_t)f * kGridField;
+    const double s0 = scale ? scale[r] : 1.0, s1 = scale ? scale[16 + r] : 1.0, s2 = scale ? scale[32 + r] : 1.0;
+    d4 acc0 = {0, 0, 0, 0}, acc1 = acc0, acc2 = acc0;
+#pragma unroll 4
+    for (int s = 0; s < kIX / 4; ++s) {
+        const int i = 4 * s + kk;
+        const double b = dfwd[i * kCPad + 16 * w + r];
+        double a0 = g[r * kIX + i], a1 = g[(16 + r) * kIX + i], a2 = g[(32 + r) * kIX + i];
+        if (scale) {  // vdspec's ug*cosgr(j) / ug*cosgr2(j) (spe_spectral.f90:430-445)
+            a0 = a0 * s0;
+            a1 = a1 * s1;
+            a2 = a2 * s2;
+        }
+        acc0 = MFMA64(a0, b, acc0);
+        acc1 = MFMA64(a1, b, acc1);
+        acc2 = MFMA64(a2, b, acc2);
+    }
+    const int c = 16 * w + r;
+    if (c >= kMX2) return;
+    double *vr = varm + (size_t)f * kVarmField + c;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int j0 = kk + 4 * q;
+        vr[j0 * kMX2] = acc0[q];
+        vr[(16 + j0) * kMX2] = acc1[q];
+        vr[(32 + j0) * kMX2] = acc2[q];
+    }
+}
+
+// specy: varm[f][lat][62] -> spec[f][n][62]  (one wave per (m, 8-field tile));
+// symmetric combinations x wt feed odd n, antisymmetric feed even n (specy :513-535)
+__global__ __launch_bounds__(64) void k_specy(const double *__restrict__ varm, double *__restrict__ spec,
+                                              const double *__restrict__ pfwd, const double *__restrict__ wt, int nf) {
+    const int m = blockIdx.x;
+    const int f0 = blockIdx.y * 8;
+    const int l = threadIdx.x, r = l & 15, kk = l >> 4;
+    const int fa = f0 + (r >> 1);
+    const bool ok = fa < nf;
+    const double *vr = varm + (size_t)(ok ? fa : 0) * kVarmField + 2 * m + (r & 1);
+    const double *pm = pfwd + (size_t)m * kNX * kIY;
+    d4 accS = {0, 0, 0, 0}, accD = accS;
+#pragma unroll
+    for (int s = 0; s < kIY / 4; ++s) {
+        const int j = 4 * s + kk;
+        double aS = 0.0, aD = 0.0;
+        if (ok) {
+            const double vn = vr[(kIL - 1 - j) * kMX2], vs = vr[j * kMX2];
+            aS = (vn + vs) * wt[j];
+            aD = (vn - vs) * wt[j];
+        }
+        accS = MFMA64(aS, pm[(2 * r) * kIY + j], accS);
+        accD = MFMA64(aD, pm[(2 * r + 1) * kIY + j], accD);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int row = kk + 4 * q;
+        const int f = f0 + (row >> 1);
+        if (f >= nf) continue;
+        double *sp = spec + (size_t)f * kSpecField + 2 * m + (row & 1);
+        sp[(2 * r) * kMX2] = accS[q];
+        sp[(2 * r + 1) * kMX2] = accD[q];
+    }
+}
+
+// spectral-space operators on complex(mx,nx) = real(2,mx,nx); one thread per
+// (field, m, n) complex coefficient.
+struct Coef {
+    const double *gradx, *uvdx, *uvdym, *uvdyp, *vddym, *vddyp;
+};
+
+__device__ inline int c3(int k, int m, int n) { return k + 2 * (m + kMX * n); }
+
+// vds (spe_spectral.f90:307-349): (u cos, v cos) spectral -> (vor, div)
+__global__ void k_vds(const double *__restrict__ ucos, const double *__restrict__ vcos, double *__restrict__ vor,
+                      double *__restrict__ div, Coef cf, int nf) {
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= nf * kMX * kNX) return;
+    const int f = idx / (kMX * kNX), mn = idx % (kMX * kNX), n = mn / kMX, m = mn % kMX;
+    const double *u = ucos + (size_t)f * kSpecField, *v = vcos + (size_t)f * kSpecField;
+    double *vo = vor + (size_t)f * kSpecField, *dv = div + (size_t)f * kSpecField;
+    const double gx = cf.gradx[m];
+    double zp[2], zc[2];
+    zp[1] = gx * u[c3(0, m, n)];
+    zp[0] = -gx * u[c3(1, m, n)];
+    zc[1] = gx * v[c3(0, m, n)];
+    zc[0] = -gx * v[c3(1, m, n)];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        double a, b;
+        if (n == 0) {
+            const double yp = cf.vddyp[m];
+            a = zc[k] - yp * u[c3(k, m, 1)];
+            b = zp[k] + yp * v[c3(k, m, 1)];
+        } else if (n == kNX - 1) {
+            const double ym = cf.vddym[n * kMX + m];
+            a = ym * u[c3(k, m, kNTRUN1 - 1)];
+            b = -ym * v[c3(k, m, kNTRUN1 - 1)];
+        } else {
+            const double ym = cf.vddym[n * kMX + m], yp = cf.vddyp[n * kMX + m];
+            a = ym * u[c3(k, m, n - 1)] - yp * u[c3(k, m, n + 1)] + zc[k];
+            b = -ym * v[c3(k, m, n - 1)] + yp * v[c3(k, m, n + 1)] + zp[k];
+        }
+        vo[c3(k, m, n)] = a;
+        dv[c3(k, m, n)] = b;
+    }
+}
+
+// uvspec (spe_spectral.f90:351-387): (vor, div) -> (u cos, v cos)
+__global__ void k_uvspec(const double *__restrict__ vor, const double *__restrict__ div, double *__restrict__ ucos,
+                         double *__restrict__ vcos, Coef cf, int nf) {
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= nf * kMX * kNX) return;
+    const int f = idx / (kMX * kNX), mn = idx % (kMX * kNX), n = mn / kMX, m = mn % kMX;
+    const double *vo = vor + (size_t)f * kSpecField, *dv = div + (size_t)f * kSpecField;
+    double *u = ucos + (size_t)f * kSpecField, *v = vcos + (size_t)f * kSpecField;
+    const double ux = cf.uvdx[n * kMX + m];
+    double zp[2], zc[2];
+    zp[1] = ux * vo[c3(0, m, n)];
+    zp[0] = -ux * vo[c3(1, m, n)];
+    zc[1] = ux * dv[c3(0, m, n)];
+    zc[0] = -ux * dv[c3(1, m, n)];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        double a, b;
+        if (n == 0) {
+            const double yp = cf.uvdyp[m];
+            a = zc[k] - yp * vo[c3(k, m, 1)];
+            b = zp[k] + yp * dv[c3(k, m, 1)];
+        } else if (n == kNX - 1) {
+            const double ym = cf.uvdym[n * kMX + m];
+            a = ym * vo[c3(k, m, kNTRUN1 - 1)];
+            b = -ym * dv[c3(k, m, kNTRUN1 - 1)];
+        } else {
+            const double ym = cf.uvdym[n * kMX + m], yp = cf.uvdyp[n * kMX + m];
+            b = -ym * dv[c3(k, m, n - 1)] + yp * dv[c3(k, m, n + 1)] + zp[k];
+            a = ym * vo[c3(k, m, n - 1)] - yp * vo[c3(k, m, n + 1)] + zc[k];
+        }
+        u[c3(k, m, n)] = a;
+        v[c3(k, m, n)] = b;
+    }
+}
+
+Coef coef_of(const sml_spectral *s) {
+    Coef c;
+    const size_t tab = (size_t)kNX * kMX;
+    c.gradx = s->d_coef;
+    c.uvdx = s->d_coef + kMX;
+    c.uvdym = c.uvdx + tab;
+    c.uvdyp = c.uvdym + tab;
+    c.vddym = c.uvdyp + tab;
+    c.vddyp = c.vddym + tab;
+    return c;
+}
+
+int ensure_work(sml_spectral *s, size_t fields) {
+    if (fields <= s->work_fields) return SML_OK;
+    if (s->d_work) SML_HIP(hipFree(s->d_work));
+    s->d_work = nullptr;
+    size_t nf = fields < 64 ? 64 : fields;
+    // varm for 2*nf fields plus 2*nf spectral fields (vdspec transforms u and v
+    // together and keeps their spectral coefficients for vds)
+    SML_HIP(hipMalloc(&s->d_work, 2 * nf * (size_t)(kVarmField + kSpecField) * sizeof(double)));
+    s->work_fields = nf;
+    return SML_OK;
+}
+
+int check_ctx(const sml_spectral *s, int nf) {
+    SML_REQUIRE(s != nullptr, "null spectral context");
+    SML_REQUIRE(nf >= 0, "nfields must be >= 0 (got %d)", nf);
+    return SML_OK;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------ API
+extern "C" int sml_spectral_create(double radius, sml_spectral **out) {
+    SML_REQUIRE(out != nullptr, "out is null");
+    SML_REQUIRE(radius > 0.0, "radius must be positive");
+    *out = nullptr;
+    sml_spectral *s = new (std::nothrow) sml_spectral();
+    if (!s) return fail(SML_ERR_NOMEM, "host allocation failed");
+    build_spectral_tables(radius, &s->t);
+    SML_HIP(hipGetDevice(&s->device));
+    const SpectralTables &t = s->t;
+    std::vector<double> pinv((size_t)kMX * kNX * kJPad, 0.0), pfwd((size_t)kMX * kNX * kIY, 0.0);
+    for (int m = 0; m < kMX; ++m)
+        for (int n = 0; n < kNX; ++n)
+            for (int j = 0; j < kIY; ++j) {
+                const bool in_tri = m + n <= kNTRUN1;  // 2m < nsh2(n) (parmtr :82-107)
+                if (in_tri) pinv[((size_t)m * kNX + n) * kJPad + j] = t.poly[j][n][m];
+                if (in_tri && n < kNTRUN1) pfwd[((size_t)m * kNX + n) * kIY + j] = t.poly[j][n][m];
+            }
+    std::vector<double> coef(kMX + 5 * (size_t)kNX * kMX);
+    std::memcpy(coef.data(), t.gradx, sizeof t.gradx);
+    std::memcpy(coef.data() + kMX, t.uvdx, sizeof t.uvdx);
+    std::memcpy(coef.data() + kMX + 1 * kNX * kMX, t.uvdym, sizeof t.uvdym);
+    std::memcpy(coef.data() + kMX + 2 * kNX * kMX, t.uvdyp, sizeof t.uvdyp);
+    std::memcpy(coef.data() + kMX + 3 * kNX * kMX, t.vddym, sizeof t.vddym);
+    std::memcpy(coef.data() + kMX + 4 * kNX * kMX, t.vddyp, sizeof t.vddyp);
+    auto up = [](double **d, const void *h, size_t bytes) -> int {
+        SML_HIP(hipMalloc(d, bytes));
+        SML_HIP(hipMemcpy(*d, h, bytes, hipMemcpyHostToDevice));
+        return SML_OK;
+    };
+    int rc;
+    if ((rc = up(&s->d_pinv, pinv.data(), pinv.size() * 8)) || (rc = up(&s->d_pfwd, pfwd.data(), pfwd.size() * 8)) ||
+        (rc = up(&s->d_dinv, t.dinv, sizeof t.dinv)) || (rc = up(&s->d_dfwd, t.dfwd, sizeof t.dfwd)) ||
+        (rc = up(&s->d_wt, t.wt, sizeof t.wt)) || (rc = up(&s->d_cosgr, t.cosgr, sizeof t.cosgr)) ||
+        (rc = up(&s->d_cosgr2, t.cosgr2, sizeof t.cosgr2)) || (rc = up(&s->d_coef, coef.data(), coef.size() * 8)) ||
+        (rc = ensure_work(s, 64))) {
+        sml_spectral_destroy(s);
+        return rc;
+    }
+    *out = s;
+    return SML_OK;
+}
+
+extern "C" int sml_spectral_destroy(sml_spectral *s) {
+    if (!s) return SML_OK;
+    double *ptrs[] = {s->d_pinv, s->d_pfwd, s->d_dinv, s->d_dfwd, s->d_wt,
+                      s->d_cosgr, s->d_cosgr2, s->d_coef, s->d_work, s->d_hbuf};
+    for (double *p : ptrs)
+        if (p) (void)hipFree(p);
+    delete s;
+    return SML_OK;
+}
+
+extern "C" int sml_spectral_tables(const sml_spectral *s, double *sia, double *wt, double *cpol, int *nsh2) {
+    SML_REQUIRE(s != nullptr, "null spectral context");
+    const SpectralTables &t = s->t;
+    if (sia) std::memcpy(sia, t.sia, sizeof t.sia);
+    if (wt) std::memcpy(wt, t.wt, sizeof t.wt);
+    if (nsh2) std::memcpy(nsh2, t.nsh2, sizeof t.nsh2);
+    if (cpol)  // cpol(mx2, nx, iy) column-major (mod_spectral.f90:29)
+        for (int j = 0; j < kIY; ++j)
+            for (int n = 0; n < kNX; ++n)
+                for (int m = 0; m < kMX; ++m)
+                    cpol[(j * kNX + n) * kMX2 + 2 * m] = cpol[(j * kNX + n) * kMX2 + 2 * m + 1] = t.poly[j][n][m];
+    return SML_OK;
+}
+
+extern "C" int sml_gridy_batched(sml_spectral *s, const double *d_spec, double *d_varm, int nf, void *stream) {
+    if (int rc = check_ctx(s, nf)) return rc;
+    if (nf == 0) return SML_OK;
+    hipLaunchKernelGGL(k_gridy, dim3(kMX, (nf + 7) / 8), dim3(64), 0, (hipStream_t)stream, d_spec, d_varm, s->d_pinv,
+                       nf);
+    SML_HIP(hipGetLastError());
+    return SML_OK;
+}
+
+extern "C" int sml_gridx_batched(sml_spectral *s, const double *d_varm, double *d_grid, int nf, int kcos,
+                                 void *stream) {
+    if (int rc = check_ctx(s, nf)) return rc;
+    if (nf == 0) return SML_OK;
+    hipLaunchKernelGGL(k_gridx, dim3(nf), dim3(384), 0, (hipStream_t)stream, d_varm, d_grid, s->d_dinv, s->d_cosgr,
+                       kcos);
+    SML_HIP(hipGetLastError());
+    return SML_OK;
+}
+
+extern "C" int sml_specx_batched(sml_spectral *s, const double *d_grid, double *d_varm, int nf, void *stream) {
+    if (int rc = check_ctx(s, nf)) return rc;
+    if (nf == 0) return SML_OK;
+    hipLaunchKernelGGL(k_specx, dim3(nf), dim3(256), 0, (hipStream_t)stream, d_grid, d_varm, s->d_dfwd,
+                       (const double *)nullptr);
+    SML_HIP(hipGetLastError());
+    return SML_OK;
+}
+
+extern "C" int sml_specy_batched(sml_spectral *s, const double *d_varm, double *d_spec, int nf, void *stream) {
+    if (int rc = check_ctx(s, nf)) return rc;
+    if (nf == 0) return SML_OK;
+    hipLaunchKernelGGL(k_specy, dim3(kMX, (nf + 7) / 8), dim3(64), 0, (hipStream_t)stream, d_varm, d_spec, s->d_pfwd,
+                       s->d_wt, nf);
+    SML_HIP(hipGetLastError());
+    return SML_OK;
+}
+
+extern "C" int sml_grid_batched(sml_spectral *s, const double *d_spec, double *d_grid, int nf, int kcos,
+                                void *stream) {
+    if (int rc = check_ctx(s, nf)) return rc;
+    if (nf == 0) return SML_OK;
+    if (int rc = ensure_work(s, nf)) return rc;
+    if (int rc = sml_gridy_batched(s, d_spec, s->d_work, nf, stream)) return rc;
+    return sml_gridx_batched(s, s->d_work, d_grid, nf, kcos, stream);
+}
+
+extern "C" int sml_spec_batched(sml_spectral *s, const double *d_grid, double *d_spec, int nf, void *stream) {
+    if (int rc = check_ctx(s, nf)) return rc;
+    if (nf == 0) return SML_OK;
+    if (int rc = ensure_work(s, nf)) return rc;
+    if (int rc = sml_specx_batched(s, d_grid, s->d_work, nf, stream)) return rc;
+    return sml_specy_batched(s, s->d_work, d_spec, nf, stream);
+}
+
+extern "C" int sml_vdspec_batched(sml_spectral *s, const double *d_ug, const double *d_vg, double *d_vor,
+                                  double *d_div, int nf, int kcos, void *stream) {
+    if (int rc = check_ctx(s, nf)) return rc;
+    if (nf == 0) return SML_OK;
+    if (int rc = ensure_work(s, nf)) return rc;
+    hipStream_t st = (hipStream_t)stream;
+    const double *scale = (kcos == 2) ? s->d_cosgr : s->d_cosgr2;
+    double *um = s->d_work, *vm = s->d_work + (size_t)nf * kVarmField;
+    double *uc = s->d_work + 2 * s->work_fields * (size_t)kVarmField, *vc = uc + (size_t)nf * kSpecField;
+    hipLaunchKernelGGL(k_specx, dim3(nf), dim3(256), 0, st, d_ug, um, s->d_dfwd, scale);
+    hipLaunchKernelGGL(k_specx, dim3(nf), dim3(256), 0, st, d_vg, vm, s->d_dfwd, scale);
+    hipLaunchKernelGGL(k_specy, dim3(kMX, (nf + 7) / 8), dim3(64), 0, st, um, uc, s->d_pfwd, s->d_wt, nf);
+    hipLaunchKernelGGL(k_specy, dim3(kMX, (nf + 7) / 8), dim3(64), 0, st, vm, vc, s->d_pfwd, s->d_wt, nf);
+    SML_HIP(hipGetLastError());
+    const int total = nf * kMX * kNX;
+    hipLaunchKernelGGL(k_vds, dim3((total + 255) / 256), dim3(256), 0, st, uc, vc, d_vor, d_div, coef_of(s), nf);
+    SML_HIP(hipGetLastError());
+    return SML_OK;
+}
+
+extern "C" int sml_uvspec_batched(sml_spectral *s, const double *d_vor, const double *d_div, double *d_ucos,
+                                  double *d_vcos, int nf, void *stream) {
+    if (int rc = check_ctx(s, nf)) return rc;
+    if (nf == 0) return SML_OK;
+    const int total = nf * kMX * kNX;
+    hipLaunchKernelGGL(k_uvspec, dim3((total + 255) / 256), dim3(256), 0, (hipStream_t)stream, d_vor, d_div, d_ucos,
+                       d_vcos, coef_of(s), nf);
+    SML_HIP(hipGetLastError());
+    return SML_OK;
+}
+
+static int ensure_hbuf(sml_spectral *s, size_t doubles) {
+    if (doubles <= s->hbuf_doubles) return SML_OK;
+    if (s->d_hbuf) SML_HIP(hipFree(s->d_hbuf));
+    s->d_hbuf = nullptr;
+    SML_HIP(hipMalloc(&s->d_hbuf, doubles * sizeof(double)));
+    s->hbuf_doubles = doubles;
+    return SML_OK;
+}
+
+extern "C" int sml_grid_host(sml_spectral *s, const double *spec, double *grid, int nf, int kcos) {
+    if (int rc = check_ctx(s, nf)) return rc;
+    SML_REQUIRE(spec && grid, "null host buffer");
+    if (nf == 0) return SML_OK;
+    if (int rc = ensure_hbuf(s, (size_t)nf * (kSpecField + kGridField))) return rc;
+    double *ds = s->d_hbuf, *dg = s->d_hbuf + (size_t)nf * kSpecField;
+    SML_HIP(hipMemcpy(ds, spec, (size_t)nf * kSpecField * 8, hipMemcpyHostToDevice));
+    if (int rc = sml_grid_batched(s, ds, dg, nf, kcos, nullptr)) return rc;
+    SML_HIP(hipMemcpy(grid, dg, (size_t)nf * kGridField * 8, hipMemcpyDeviceToHost));
+    return SML_OK;
+}
+
+extern "C" int sml_spec_host(sml_spectral *s, const double *grid, double *spec, int nf) {
+    if (int rc = check_ctx(s, nf)) return rc;
+    SML_REQUIRE(spec && grid, "null host buffer");
+    if (nf == 0) return SML_OK;
+    if (int rc = ensure_hbuf(s, (size_t)nf * (kSpecField + kGridField))) return rc;
+    double *ds = s->d_hbuf, *dg = s->d_hbuf + (size_t)nf * kSpecField;
+    SML_HIP(hipMemcpy(dg, grid, (size_t)nf * kGridField * 8, hipMemcpyHostToDevice));
+    if (int rc = sml_spec_batched(s, dg, ds, nf, nullptr)) return rc;
+    SML_HIP(hipMemcpy(spec, ds, (size_t)nf * kSpecField * 8, hipMemcpyDeviceToHost));
+    return SML_OK;
+}

@@ -1,0 +1,127 @@
+"""ctypes binding of libspeedyml.so (include/speedy_ml.h).
+
+The product path: every compute call goes to the hand-written gfx950 kernels in
+this library.  There is no CPU fallback -- if the library is missing or no GPU is
+visible, the compute entry points raise.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))  # speedy-ml-1_amd/
+LIB_PATH = os.path.join(PKG_ROOT, "lib", "libspeedyml.so")
+CSRC = os.path.join(PKG_ROOT, "csrc")
+
+SML_OK = 0
+SML_F32 = 1
+SML_F64 = 2
+
+# every symbol include/speedy_ml.h declares (checked by tests/test_abi.py)
+EXPORTED = (
+    "sml_last_error", "sml_abi_version",
+    "sml_spectral_create", "sml_spectral_destroy", "sml_spectral_tables",
+    "sml_grid_batched", "sml_spec_batched", "sml_gridy_batched", "sml_gridx_batched",
+    "sml_specx_batched", "sml_specy_batched", "sml_vdspec_batched", "sml_uvspec_batched",
+    "sml_grid_host", "sml_spec_host",
+    "sml_res_create", "sml_res_destroy", "sml_res_ninp", "sml_res_feedback_offsets",
+    "sml_res_load_region_f32", "sml_res_load_region_f64", "sml_res_set_state", "sml_res_get_state",
+    "sml_res_step", "sml_res_step_host", "sml_res_footprint", "sml_res_enable_timing",
+    "sml_res_kernel_times", "sml_exchange_assemble", "sml_res_tile_inputs",
+    "sml_nc_read_region", "sml_nc_write_region",
+)
+
+
+class SmlError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def build(jobs: int = 8) -> str:
+    """Compile libspeedyml.so for gfx950 (hipcc cross-compiles without a GPU)."""
+    subprocess.run(["make", "-s", "-C", CSRC, f"-j{jobs}"], check=True)
+    return LIB_PATH
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise SmlError(f"{LIB_PATH} is missing: build it with `make -C {CSRC}` "
+                           "(or __graft_entry__.build()); there is no CPU fallback")
+        L = ctypes.CDLL(LIB_PATH)
+        _declare(L)
+        _lib = L
+    return _lib
+
+
+def check(rc: int) -> None:
+    if rc != SML_OK:
+        msg = lib().sml_last_error().decode(errors="replace")
+        raise SmlError(f"libspeedyml error {rc}: {msg}")
+
+
+def _declare(L: ctypes.CDLL) -> None:
+    vp, i, d, i64p = ctypes.c_void_p, ctypes.c_int, ctypes.c_double, ctypes.POINTER(ctypes.c_int64)
+    pp = ctypes.POINTER(ctypes.c_void_p)
+    L.sml_last_error.restype = ctypes.c_char_p
+    L.sml_last_error.argtypes = []
+    L.sml_abi_version.restype = i
+    sig = {
+        "sml_spectral_create": [d, pp],
+        "sml_spectral_destroy": [vp],
+        "sml_spectral_tables": [vp, vp, vp, vp, vp],
+        "sml_grid_batched": [vp, vp, vp, i, i, vp],
+        "sml_spec_batched": [vp, vp, vp, i, vp],
+        "sml_gridy_batched": [vp, vp, vp, i, vp],
+        "sml_gridx_batched": [vp, vp, vp, i, i, vp],
+        "sml_specx_batched": [vp, vp, vp, i, vp],
+        "sml_specy_batched": [vp, vp, vp, i, vp],
+        "sml_vdspec_batched": [vp, vp, vp, vp, vp, i, i, vp],
+        "sml_uvspec_batched": [vp, vp, vp, vp, vp, i, vp],
+        "sml_grid_host": [vp, vp, vp, i, i],
+        "sml_spec_host": [vp, vp, vp, i],
+        "sml_res_create": [i, i, vp, vp, vp, vp, i, i, i, d, pp],
+        "sml_res_destroy": [vp],
+        "sml_res_ninp": [vp, i, ctypes.POINTER(ctypes.c_int)],
+        "sml_res_feedback_offsets": [vp, vp],
+        "sml_res_load_region_f32": [vp, i, vp, vp, vp, vp, vp, vp, vp],
+        "sml_res_load_region_f64": [vp, i, vp, vp, vp, vp, vp, vp, vp],
+        "sml_res_set_state": [vp, i, vp],
+        "sml_res_get_state": [vp, i, vp],
+        "sml_res_step": [vp, vp, vp, vp, vp],
+        "sml_res_step_host": [vp, vp, vp, vp],
+        "sml_res_footprint": [vp, i64p, i64p],
+        "sml_res_enable_timing": [vp, i],
+        "sml_res_kernel_times": [vp, vp, vp, i, ctypes.POINTER(ctypes.c_int)],
+        "sml_exchange_assemble": [vp, vp, vp, vp, vp, vp],
+        "sml_res_tile_inputs": [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp],
+        "sml_nc_read_region": [ctypes.c_char_p, vp, vp, vp, vp, vp, vp, vp, vp],
+        "sml_nc_write_region": [ctypes.c_char_p, i, i, i, i, i, vp, vp, vp, vp, vp, vp, vp],
+    }
+    for name, args in sig.items():
+        fn = getattr(L, name)
+        fn.argtypes = args
+        fn.restype = i
+
+
+def ptr(x) -> ctypes.c_void_p:
+    """Address of a numpy array or a torch tensor (device or host); None -> NULL."""
+    if x is None:
+        return ctypes.c_void_p(0)
+    if hasattr(x, "data_ptr"):
+        return ctypes.c_void_p(x.data_ptr())
+    if hasattr(x, "ctypes"):
+        return x.ctypes.data_as(ctypes.c_void_p)
+    return ctypes.c_void_p(int(x))
+
+
+def stream_ptr(stream) -> ctypes.c_void_p:
+    """hipStream_t of a torch stream (None -> torch's current stream)."""
+    import torch
+
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)

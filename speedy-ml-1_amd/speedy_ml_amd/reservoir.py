@@ -1,0 +1,172 @@
+"""Batched reservoir forward + exchange tiling on the GPU (libspeedyml sml_res_*).
+
+Host-side mirror of the reference's reservoir interface for one rank:
+  Reservoirs(...)            <- initialize_model_parameters + processor_decomposition +
+                                per-region trained_reservoir_prediction
+                                (src/parallelmain.f90:30-199, src/mod_reservoir.f90:1781)
+  .load_region(...)          <- read_trained_res + allocate_res_new + mklsparse
+  .predict(fb, lm, out)      <- predict for every region of the rank (mod_reservoir.f90:1416)
+  .assemble / .tile_inputs   <- sendrecievegrid's gather and scatter (mpires.f90:218-780)
+Device buffers are torch CUDA tensors (plumbing only).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+from ._lib import SML_F32, SML_F64, check, lib, ptr, stream_ptr
+from .domain import CHUNK_PRED, CHUNK_SPEEDY, NUM_REGIONS
+
+
+class Reservoirs:
+    def __init__(self, region_ids, sst_flags, n, k, numregions: int = NUM_REGIONS,
+                 chunk_speedy: int = CHUNK_SPEEDY, nout: int = CHUNK_PRED, weight_dtype: str = "f32",
+                 leakage: float = 1.0):
+        self.region_ids = np.ascontiguousarray(region_ids, dtype=np.int32)
+        self.sst = np.ascontiguousarray(sst_flags, dtype=np.uint8)
+        self.n = np.ascontiguousarray(n, dtype=np.int32)
+        self.k = np.ascontiguousarray(k, dtype=np.int32)
+        self.nlocal = len(self.region_ids)
+        self.numregions = numregions
+        self.ncs = chunk_speedy
+        self.nout = nout
+        self.weight_dtype = weight_dtype
+        dt = {"f32": SML_F32, "f64": SML_F64}[weight_dtype]
+        h = ctypes.c_void_p()
+        check(lib().sml_res_create(numregions, self.nlocal, ptr(self.region_ids), ptr(self.sst), ptr(self.n),
+                                   ptr(self.k), chunk_speedy, nout, dt, leakage, ctypes.byref(h)))
+        self._h = h
+        off = np.zeros(self.nlocal + 1, dtype=np.int64)
+        check(lib().sml_res_feedback_offsets(self._h, ptr(off)))
+        self.fb_offsets = off
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().sml_res_destroy(self._h)
+            self._h = None
+
+    __del__ = close
+
+    @property
+    def handle(self):
+        return self._h
+
+    def ninp(self, i: int) -> int:
+        v = ctypes.c_int()
+        check(lib().sml_res_ninp(self._h, i, ctypes.byref(v)))
+        return v.value
+
+    def load_region(self, i: int, rows, cols, vals, win, wout, mean, std):
+        """Reference layouts: rows/cols 1-based (k,), vals (k,), win (ninp, n) C-order,
+        wout (ncs+n, nout) C-order, mean/std (36,)."""
+        rows = np.ascontiguousarray(rows, dtype=np.int32)
+        cols = np.ascontiguousarray(cols, dtype=np.int32)
+        mean = np.ascontiguousarray(mean, dtype=np.float64)
+        std = np.ascontiguousarray(std, dtype=np.float64)
+        if vals.dtype == np.float32 and win.dtype == np.float32 and wout.dtype == np.float32:
+            f = lib().sml_res_load_region_f32
+            vals, win, wout = (np.ascontiguousarray(a, dtype=np.float32) for a in (vals, win, wout))
+        else:
+            f = lib().sml_res_load_region_f64
+            vals, win, wout = (np.ascontiguousarray(a, dtype=np.float64) for a in (vals, win, wout))
+        check(f(self._h, i, ptr(rows), ptr(cols), ptr(vals), ptr(win), ptr(wout), ptr(mean), ptr(std)))
+
+    def load_region_weights(self, i: int, w):
+        self.load_region(i, w.rows, w.cols, w.vals, w.win, w.wout, w.mean, w.std)
+
+    def load_netcdf(self, i: int, path: str):
+        """Load region i from a reference weight file (read_trained_res)."""
+        d = read_region_netcdf(path)
+        self.load_region(i, d["rows"], d["cols"], d["vals"], d["win"], d["wout"],
+                         d["mean"].astype(np.float64), d["std"].astype(np.float64))
+
+    def set_state(self, i: int, x):
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        check(lib().sml_res_set_state(self._h, i, ptr(x)))
+
+    def get_state(self, i: int) -> np.ndarray:
+        x = np.zeros(int(self.n[i]))
+        check(lib().sml_res_get_state(self._h, i, ptr(x)))
+        return x
+
+    # --- device buffers
+    def alloc_io(self, device="cuda"):
+        import torch
+
+        fb = torch.zeros(int(self.fb_offsets[-1]), dtype=torch.float64, device=device)
+        lm = torch.zeros((self.nlocal, max(self.ncs, 1)), dtype=torch.float64, device=device)
+        ov = torch.zeros((self.nlocal, self.nout), dtype=torch.float64, device=device)
+        return fb, lm, ov
+
+    def predict(self, d_feedback, d_local_model, d_outvec, stream=None):
+        check(lib().sml_res_step(self._h, ptr(d_feedback), ptr(d_local_model if self.ncs else None),
+                                 ptr(d_outvec), stream_ptr(stream)))
+
+    def predict_host(self, feedback: np.ndarray, local_model: np.ndarray | None) -> np.ndarray:
+        fb = np.ascontiguousarray(feedback, dtype=np.float64)
+        lm = np.ascontiguousarray(local_model, dtype=np.float64) if local_model is not None else None
+        out = np.zeros((self.nlocal, self.nout))
+        check(lib().sml_res_step_host(self._h, ptr(fb), ptr(lm), ptr(out)))
+        return out
+
+    def assemble(self, d_outvec_all, d_g4, d_g2, d_pr, stream=None):
+        check(lib().sml_exchange_assemble(self._h, ptr(d_outvec_all), ptr(d_g4), ptr(d_g2), ptr(d_pr),
+                                          stream_ptr(stream)))
+
+    def tile_inputs(self, d_g4, d_g2, d_pr, d_fc4, d_fc2, d_tisr, d_feedback, d_local_model, stream=None):
+        check(lib().sml_res_tile_inputs(self._h, ptr(d_g4), ptr(d_g2), ptr(d_pr), ptr(d_fc4), ptr(d_fc2),
+                                        ptr(d_tisr), ptr(d_feedback), ptr(d_local_model), stream_ptr(stream)))
+
+    # --- measurement
+    def footprint(self):
+        w = ctypes.c_int64()
+        a = ctypes.c_int64()
+        check(lib().sml_res_footprint(self._h, ctypes.byref(w), ctypes.byref(a)))
+        return w.value, a.value
+
+    def enable_timing(self, capacity: int):
+        check(lib().sml_res_enable_timing(self._h, capacity))
+
+    def kernel_times(self, max_steps: int = 100000):
+        upd = np.zeros(max_steps, dtype=np.float32)
+        rd = np.zeros(max_steps, dtype=np.float32)
+        cnt = ctypes.c_int()
+        check(lib().sml_res_kernel_times(self._h, ptr(upd), ptr(rd), max_steps, ctypes.byref(cnt)))
+        return upd[:cnt.value].astype(np.float64), rd[:cnt.value].astype(np.float64)
+
+
+def read_region_netcdf(path: str) -> dict:
+    """Read a worker_XXXX_level_1_<trial>.nc weight file (read_trained_res layout)."""
+    dims = np.zeros(6, dtype=np.int64)
+    p = os.fsencode(path)
+    check(lib().sml_nc_read_region(p, ptr(dims), None, None, None, None, None, None, None))
+    n, ninp, nout, ncsn, k, nms = (int(v) for v in dims)
+    out = {
+        "win": np.zeros((ninp, n), dtype=np.float32),
+        "wout": np.zeros((ncsn, nout), dtype=np.float32),
+        "rows": np.zeros(k, dtype=np.int32),
+        "cols": np.zeros(k, dtype=np.int32),
+        "vals": np.zeros(k, dtype=np.float32),
+        "mean": np.zeros(nms, dtype=np.float32),
+        "std": np.zeros(nms, dtype=np.float32),
+    }
+    check(lib().sml_nc_read_region(p, ptr(dims), ptr(out["win"]), ptr(out["wout"]), ptr(out["rows"]),
+                                   ptr(out["cols"]), ptr(out["vals"]), ptr(out["mean"]), ptr(out["std"])))
+    return out
+
+
+def write_region_netcdf(path: str, win, wout, rows, cols, vals, mean, std) -> None:
+    """Write the reference's per-region weight layout (write_trained_res), CDF-1."""
+    win = np.ascontiguousarray(win, dtype=np.float32)
+    wout = np.ascontiguousarray(wout, dtype=np.float32)
+    ninp, n = win.shape
+    ncsn, nout = wout.shape
+    rows = np.ascontiguousarray(rows, dtype=np.int32)
+    cols = np.ascontiguousarray(cols, dtype=np.int32)
+    vals = np.ascontiguousarray(vals, dtype=np.float32)
+    mean = np.ascontiguousarray(mean, dtype=np.float32)
+    std = np.ascontiguousarray(std, dtype=np.float32)
+    check(lib().sml_nc_write_region(os.fsencode(path), n, ninp, nout, ncsn, len(rows), ptr(win), ptr(wout),
+                                    ptr(rows), ptr(cols), ptr(vals), ptr(mean), ptr(std)))

@@ -1,0 +1,115 @@
+"""Synthetic reservoir weights laid out exactly like the trained NetCDF files.
+
+No trained weights are available offline (Zenodo fetch, scripts/get_trained_coupled_data.sh),
+so benches and tests use weights drawn per region from a seeded generator, with the
+structure the reference's training produces:
+
+  A      k = int(0.001 n^2) COO entries; rows and cols are independent per-n-block
+         random permutations as makesparse builds them (mod_linalg.f90:180-218), so
+         duplicate (row, col) pairs occur; vals U(0,1) * radius / 3 (a degree-6 U(0,1)
+         matrix has spectral radius ~3; gen_res rescales to `radius`, :180-205).
+  W_in   block diagonal, q = n/ninp rows per input, sigma * U(-1,1), sigma = 0.5
+         (train_reservoir, mod_reservoir.f90:260-278).
+  W_out  U(-0.01, 0.01), shape (nout, ncs + n).
+  mean   U(0,1); std 0.5 + U(0,1); std(36) = 0 where the region has no sst input
+         (so sst_bool_input <=> std(36) > 0.2, mod_reservoir.f90:1837-1845).
+
+Every array is rounded to float32 (the NF90_REAL file precision, mod_io.f90:1282).
+Arrays use the reference layouts: win (ninp, n) C-order == Fortran win(n, ninp);
+wout (ncs+n, nout) C-order == Fortran wout(nout, ncs+n).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+
+from .domain import CHUNK_PRED, CHUNK_SPEEDY, radius_by_region, reservoir_sizes
+
+
+@dataclass
+class RegionWeights:
+    region: int
+    sst: bool
+    n: int
+    ninp: int
+    k: int
+    rows: np.ndarray   # int32 (k,), 1-based
+    cols: np.ndarray   # int32 (k,), 1-based
+    vals: np.ndarray   # float32 (k,)
+    win: np.ndarray    # float32 (ninp, n)
+    wout: np.ndarray   # float32 (ncs+n, nout)
+    mean: np.ndarray   # float64 (36,) (file values are float32, widened exactly)
+    std: np.ndarray    # float64 (36,)
+
+    def win_compressed(self):
+        """(col, val) of the single nonzero per row of W_in."""
+        nz = self.win != 0
+        col = np.argmax(nz, axis=0).astype(np.int32)
+        val = self.win[col, np.arange(self.n)]
+        return col, val
+
+
+def region_weights(region: int, sst: bool, seed: int = 1234, chunk_speedy: int = CHUNK_SPEEDY,
+                   nout: int = CHUNK_PRED, n_override: int | None = None) -> RegionWeights:
+    sz = reservoir_sizes(region, sst)
+    n, ninp, k, q = sz.n, sz.ninp, sz.k, sz.q
+    if n_override is not None:  # reduced sizes for fast CPU tests (same structure)
+        q = max(1, n_override // ninp)
+        n = q * ninp
+        k = int((6.0 / 6000.0) * n * n) if n_override >= 1000 else 6 * n
+    rng = np.random.default_rng([seed, region])
+    # A: per-block permutations (makesparse)
+    rows = np.empty(k, dtype=np.int32)
+    cols = np.empty(k, dtype=np.int32)
+    full, left = divmod(k, n)
+    for b in range(full):
+        rows[b * n:(b + 1) * n] = rng.permutation(n)[:n] + 1
+        cols[b * n:(b + 1) * n] = rng.permutation(n)[:n] + 1
+    if left:
+        rows[full * n:] = rng.permutation(n)[:left] + 1
+        cols[full * n:] = rng.permutation(n)[:left] + 1
+    radius = radius_by_region(region)
+    vals = (rng.random(k) * (radius / 3.0)).astype(np.float32)
+    # W_in: block diagonal
+    win = np.zeros((ninp, n), dtype=np.float32)
+    blk = (0.5 * (2.0 * rng.random((ninp, q)) - 1.0)).astype(np.float32)
+    idx = np.arange(ninp)
+    for j in range(q):
+        win[idx, idx * q + j] = blk[:, j]
+    wout = ((rng.random((chunk_speedy + n, nout), dtype=np.float32) * 2.0 - 1.0) * 0.01).astype(np.float32)
+    mean = rng.random(36).astype(np.float32).astype(np.float64)
+    std = (0.5 + rng.random(36)).astype(np.float32).astype(np.float64)
+    if not sst:
+        std[35] = 0.0
+    return RegionWeights(region, sst, n, ninp, k, rows, cols, vals, win, wout, mean, std)
+
+
+def initial_state(region: int, n: int, seed: int = 99) -> np.ndarray:
+    rng = np.random.default_rng([seed, region, 1])
+    return 0.1 * (2.0 * rng.random(n) - 1.0)
+
+
+def feedback_vector(region: int, ninp: int, seed: int = 7) -> np.ndarray:
+    rng = np.random.default_rng([seed, region, 2])
+    return rng.standard_normal(ninp)
+
+
+def local_model_vector(region: int, ncs: int = CHUNK_SPEEDY, seed: int = 7) -> np.ndarray:
+    rng = np.random.default_rng([seed, region, 3])
+    return 2.0 * rng.random(ncs) - 1.0
+
+
+def synthetic_grids(seed: int = 5):
+    """A plausible T30L8 state in the sendrecievegrid layout: grid4d (z, y, x, var)
+    C-order == Fortran (4, 96, 48, 8); grid2d / precip (48, 96) == (96, 48).
+    T ~ 220-300 K, u/v ~ +-20 m/s, q ~ 0-15 g/kg, logp ~ 0 +- 0.1, precip >= 0."""
+    rng = np.random.default_rng(seed)
+    g4 = np.empty((8, 48, 96, 4))
+    g4[..., 0] = 250.0 + 30.0 * rng.random((8, 48, 96))
+    g4[..., 1] = 20.0 * rng.standard_normal((8, 48, 96))
+    g4[..., 2] = 20.0 * rng.standard_normal((8, 48, 96))
+    g4[..., 3] = 15.0 * rng.random((8, 48, 96))
+    g2 = 0.1 * rng.standard_normal((48, 96))
+    pr = np.abs(rng.standard_normal((48, 96)))
+    return g4, g2, pr

@@ -1,0 +1,161 @@
+"""GPU parity of the batched reservoir forward (sml_res_step) against the oracle's
+restatement of predict (mod_reservoir.f90:1416-1487).
+
+Tolerances (fp64 arithmetic on both sides): the SpMV rows are summed in the file's
+entry order on both sides; the differences come from tanh (device vs glibc, <= 2
+ulp) and the W_out readout's summation order (wave reductions vs sequential):
+  state x : |err| <= 1e-14 * (1 + |x|)
+  outvec  : |err| <= 1e-11 * (1 + |outvec|)
+"""
+import numpy as np
+import pytest
+
+import oracle
+from speedy_ml_amd import SmlError, domain
+from speedy_ml_amd.synthetic import feedback_vector, initial_state, local_model_vector, region_weights
+
+pytestmark = pytest.mark.gpu
+
+X_TOL = 1e-14
+OUT_TOL = 1e-11
+
+# one region of every shape class, plus the periodic x edges
+CASES = [(0, False), (5, True), (23, True), (24, False), (600, True), (1127, False), (1151, True)]
+
+
+def _check(a, b, tol):
+    err = np.abs(np.asarray(a) - np.asarray(b)) / (1.0 + np.abs(np.asarray(b)))
+    assert err.max() <= tol, f"max scaled err {err.max():.3e} > {tol:.0e}"
+
+
+def _build(cases, n_override=None, weight_dtype="f32", chunk_speedy=132, seed=1234):
+    from speedy_ml_amd.reservoir import Reservoirs
+
+    ws = [region_weights(r, s, seed=seed, n_override=n_override, chunk_speedy=chunk_speedy) for r, s in cases]
+    res = Reservoirs([w.region for w in ws], [w.sst for w in ws], [w.n for w in ws], [w.k for w in ws],
+                     chunk_speedy=chunk_speedy, weight_dtype=weight_dtype)
+    for i, w in enumerate(ws):
+        assert res.ninp(i) == w.ninp
+        res.load_region_weights(i, w)
+        res.set_state(i, initial_state(w.region, w.n))
+    return res, ws
+
+
+def _oracle_step(w, x, fb, lm, chunk_speedy=132):
+    col, val = w.win_compressed()
+    return oracle.predict_f32(w.rows, w.cols, w.vals, col, val, w.wout, fb, lm, x, w.mean, w.std,
+                              chunk_speedy=chunk_speedy)
+
+
+@pytest.mark.parametrize("steps", [1, 4])
+def test_predict_small_reservoirs(cuda, steps):
+    res, ws = _build(CASES, n_override=700)
+    xs = [initial_state(w.region, w.n) for w in ws]
+    for t in range(steps):
+        fb = np.concatenate([feedback_vector(w.region + 17 * t, w.ninp) for w in ws])
+        lm = np.stack([local_model_vector(w.region + 17 * t) for w in ws])
+        out = res.predict_host(fb, lm)
+        for i, w in enumerate(ws):
+            o = res.fb_offsets
+            ref, xs[i] = _oracle_step(w, xs[i], fb[o[i]:o[i + 1]], lm[i])
+            _check(out[i], ref, OUT_TOL)
+            _check(res.get_state(i), xs[i], X_TOL * (t + 1))
+
+
+def test_predict_full_size_reservoirs(cuda):
+    """Full-size regions of all four shape classes (n = 5760, 6160, 6048, 5880)."""
+    cases = [(5, True), (24, False), (0, True), (1127, False)]
+    res, ws = _build(cases)
+    assert sorted(int(v) for v in res.n) == [5760, 5880, 6048, 6160]
+    fb = np.concatenate([feedback_vector(w.region, w.ninp) for w in ws])
+    lm = np.stack([local_model_vector(w.region) for w in ws])
+    out = res.predict_host(fb, lm)
+    for i, w in enumerate(ws):
+        o = res.fb_offsets
+        ref, x1 = _oracle_step(w, initial_state(w.region, w.n), fb[o[i]:o[i + 1]], lm[i])
+        _check(out[i], ref, OUT_TOL)
+        _check(res.get_state(i), x1, X_TOL)
+
+
+def test_predict_f64_storage_and_dense_oracle(cuda):
+    """fp64 weight storage, checked against the dense-W_in reference arithmetic."""
+    res, ws = _build(CASES[:3], n_override=500, weight_dtype="f64")
+    fb = np.concatenate([feedback_vector(w.region, w.ninp) for w in ws])
+    lm = np.stack([local_model_vector(w.region) for w in ws])
+    out = res.predict_host(fb, lm)
+    for i, w in enumerate(ws):
+        o = res.fb_offsets
+        ref, x1 = oracle.predict(w.rows, w.cols, w.vals.astype(np.float64), w.win.astype(np.float64),
+                                 w.wout.astype(np.float64), fb[o[i]:o[i + 1]], lm[i],
+                                 initial_state(w.region, w.n), w.mean, w.std)
+        _check(out[i], ref, OUT_TOL)
+        _check(res.get_state(i), x1, X_TOL)
+
+
+def test_ml_only_mode(cuda):
+    """chunk_speedy = 0: predict_ml (mod_reservoir.f90:1489-1533)."""
+    res, ws = _build(CASES[:4], n_override=600, chunk_speedy=0)
+    fb = np.concatenate([feedback_vector(w.region, w.ninp) for w in ws])
+    out = res.predict_host(fb, None)
+    for i, w in enumerate(ws):
+        o = res.fb_offsets
+        ref, _ = _oracle_step(w, initial_state(w.region, w.n), fb[o[i]:o[i + 1]], None, chunk_speedy=0)
+        _check(out[i], ref, OUT_TOL)
+
+
+def test_device_path_and_kernel_timing(cuda):
+    import torch
+
+    res, ws = _build(CASES, n_override=800)
+    fb, lm, ov = res.alloc_io(cuda)
+    fb_h = np.concatenate([feedback_vector(w.region, w.ninp) for w in ws])
+    lm_h = np.stack([local_model_vector(w.region) for w in ws])
+    fb.copy_(torch.from_numpy(fb_h))
+    lm.copy_(torch.from_numpy(lm_h))
+    res.enable_timing(3)
+    for _ in range(3):
+        res.predict(fb, lm, ov)
+    upd, rd = res.kernel_times()
+    assert len(upd) == 3 and (upd > 0).all() and (rd > 0).all()
+    xs = [initial_state(w.region, w.n) for w in ws]
+    for _ in range(3):
+        refs = []
+        for i, w in enumerate(ws):
+            o = res.fb_offsets
+            r, xs[i] = _oracle_step(w, xs[i], fb_h[o[i]:o[i + 1]], lm_h[i])
+            refs.append(r)
+    _check(ov.cpu().numpy(), np.stack(refs), OUT_TOL)
+
+
+def test_error_paths(cuda):
+    from speedy_ml_amd.reservoir import Reservoirs
+
+    w = region_weights(5, True, n_override=600)
+    res = Reservoirs([5], [1], [w.n], [w.k])
+    with pytest.raises(SmlError, match="no weights loaded"):
+        res.predict_host(np.zeros(w.ninp), np.zeros((1, 132)))
+    bad = w.wout.astype(np.float64)
+    bad[0, 0] = 0.1  # not representable in fp32 storage
+    with pytest.raises(SmlError, match="not representable"):
+        res.load_region(0, w.rows, w.cols, w.vals.astype(np.float64), w.win.astype(np.float64), bad, w.mean, w.std)
+    rows = w.rows.copy()
+    rows[3] = w.n + 1
+    with pytest.raises(SmlError, match="out of range"):
+        res.load_region(0, rows, w.cols, w.vals, w.win, w.wout, w.mean, w.std)
+    with pytest.raises(SmlError, match="out of range"):
+        res.set_state(2, np.zeros(w.n))
+
+
+def test_netcdf_loaded_weights_match(cuda, tmp_path):
+    from speedy_ml_amd.reservoir import Reservoirs, write_region_netcdf
+
+    w = region_weights(600, True, n_override=576)
+    p = str(tmp_path / "worker_0600_level_1_trial.nc")
+    write_region_netcdf(p, w.win, w.wout, w.rows, w.cols, w.vals, w.mean, w.std)
+    a = Reservoirs([600], [1], [w.n], [w.k])
+    b = Reservoirs([600], [1], [w.n], [w.k])
+    a.load_region_weights(0, w)
+    b.load_netcdf(0, p)
+    fb = feedback_vector(600, w.ninp)
+    lm = local_model_vector(600)[None, :]
+    np.testing.assert_array_equal(a.predict_host(fb, lm), b.predict_host(fb, lm))
