@@ -1,0 +1,270 @@
+#!/usr/bin/env python3
+"""bench.py -- SPEEDY-ML hybrid hot path on MI355X (one process per GPU).
+
+One "step" = one hybrid-step pass over the reservoir side of the hot path for all
+1152 subdomains (BASELINE.json configs[1], sharded per configs[3]):
+
+  1. predict for every local region: A x + W_in u -> tanh -> W_out [model; x~],
+     unstandardize                       (mod_reservoir.f90:1416-1487, 2 kernels)
+  2. exchange: all-gather of every rank's outvecs over RCCL (N > 1)
+                                         (replaces mpires.f90:338-716 MPI p2p)
+  3. assemble the global T30L8 grid + clips (mpires.f90:300-478)
+  4. re-tile every local region's next feedback (overlap tiles, standardized) and
+     its standardized SPEEDY local vector (mpires.f90:558-751)
+
+The SPEEDY window itself (26 dyn_steps with physics) is not part of this step yet:
+the SPEEDY forecast grids consumed in (4) are a fixed synthetic T30L8 state.  Data
+are synthetic, weights random with the trained structure, 6000-node-class
+reservoirs (n = 5760/6160/6048/5880), fp64 arithmetic, weights held at their fp32
+file precision (exact).
+
+Usage: python bench.py [--gpus N --steps K --warmup W]
+       python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "speedy-ml-1_amd"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--regions", type=int, default=1152)
+    p.add_argument("--weights", choices=("f32", "f64"), default="f32")
+    p.add_argument("--cpu-sample", type=int, default=96, help="regions in the CPU-baseline sample (0 = skip)")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    return p.parse_args()
+
+
+def log(rank, *a):
+    if rank == 0:
+        print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    from speedy_ml_amd import domain
+    from speedy_ml_amd.reservoir import Reservoirs
+    from speedy_ml_amd.synthetic import initial_state, region_weights, synthetic_grids
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    dev = torch.device("cuda", local_rank)
+    torch.cuda.set_device(dev)
+
+    nreg = args.regions
+    mask = domain.load_sst_mask()
+    regions = domain.processor_decomposition(nreg, world, rank)
+    counts = [len(domain.processor_decomposition(nreg, world, r)) for r in range(world)]
+    maxc = max(counts)
+
+    # ---- setup: synthetic weights with the trained structure, loaded per region
+    t_setup = time.time()
+    sizes = [domain.reservoir_sizes(r, bool(mask[r])) for r in regions]
+    res = Reservoirs(regions, [mask[r] for r in regions], [s.n for s in sizes], [s.k for s in sizes],
+                     weight_dtype=args.weights)
+    for i, r in enumerate(regions):
+        w = region_weights(r, bool(mask[r]))
+        if args.weights == "f64":
+            res.load_region(i, w.rows, w.cols, w.vals.astype(np.float64), w.win.astype(np.float64),
+                            w.wout.astype(np.float64), w.mean, w.std)
+        else:
+            res.load_region_weights(i, w)
+        res.set_state(i, initial_state(r, w.n))
+        if i % 144 == 0:
+            log(rank, f"loaded {i}/{len(regions)} regions ({time.time() - t_setup:.1f}s)")
+    fb, lm, ov = res.alloc_io(dev)
+    ov_all = torch.zeros((maxc * world, 136), dtype=torch.float64, device=dev)
+    ov_send = torch.zeros((maxc, 136), dtype=torch.float64, device=dev)
+    g4h, g2h, prh = synthetic_grids(11)
+    f4h, f2h, _ = synthetic_grids(12)
+    g4 = torch.from_numpy(g4h).to(dev)
+    g2 = torch.from_numpy(g2h).to(dev)
+    pr = torch.from_numpy(prh).to(dev)
+    f4 = torch.from_numpy(f4h).to(dev)
+    f2 = torch.from_numpy(f2h).to(dev)
+    tisr = torch.from_numpy(np.random.default_rng(13).standard_normal((len(regions), 16))).to(dev)
+    # initial inputs from the synthetic analysis state (start_prediction analogue)
+    res.tile_inputs(g4, g2, pr, f4, f2, tisr, fb, lm)
+    # all-gather order -> global region order
+    gather_rows = np.concatenate([np.arange(counts[r]) + r * maxc for r in range(world)])
+    gather_regions = np.concatenate([domain.processor_decomposition(nreg, world, r) for r in range(world)])
+    contiguous = world == 1 or (np.array_equal(gather_regions, np.arange(nreg)) and len(set(counts)) == 1)
+    perm = torch.from_numpy(gather_rows[np.argsort(gather_regions)]).to(dev)
+    ov_glob = torch.zeros((nreg, 136), dtype=torch.float64, device=dev)
+    torch.cuda.synchronize()
+    log(rank, f"setup {time.time() - t_setup:.1f}s, {len(regions)} regions on rank 0")
+
+    def step():
+        res.predict(fb, lm, ov)
+        if world == 1:
+            glob = ov
+        else:
+            ov_send[:len(regions)].copy_(ov)
+            dist.all_gather_into_tensor(ov_all, ov_send)
+            if contiguous:
+                glob = ov_all
+            else:
+                torch.index_select(ov_all, 0, perm, out=ov_glob)
+                glob = ov_glob
+        res.assemble(glob, g4, g2, pr)
+        res.tile_inputs(g4, g2, pr, f4, f2, tisr, fb, lm)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    res.enable_timing(args.steps)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    upd_ms, rd_ms = res.kernel_times()
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+
+    # ---- roofline of the dominant kernel (readout: streams W_out)
+    wb = 4 if args.weights == "f32" else 8
+    rd_bytes = sum(wb * 136 * (132 + s.n) + 8 * (132 + s.n) + 8 * 136 + 2 * 36 * 8 for s in sizes)
+    rd_bytes_f64 = sum(8 * 136 * (132 + s.n) + 8 * (132 + s.n) + 8 * 136 + 2 * 36 * 8 for s in sizes)
+    rd_avg_s = float(np.mean(rd_ms)) * 1e-3
+    upd_avg_s = float(np.mean(upd_ms)) * 1e-3
+    achieved = rd_bytes / rd_avg_s / 1e9
+    _, algo_step = res.footprint()
+    traffic = None
+    pmc_path = os.path.join(REPO, "profiles", "readout_pmc.json")
+    if os.path.exists(pmc_path) and world == 1 and nreg == 1152 and args.weights == "f32":
+        try:
+            traffic = json.load(open(pmc_path)).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.cpu_sample > 0:
+        cpu = cpu_baseline(args.cpu_sample, nreg, mask)
+
+    if rank == 0:
+        steps_per_s = args.steps / dt
+        line = {
+            "metric": "hybrid timesteps/sec, T30L8 + 1152x6k-node reservoirs; 1/2/4/8-GPU scaling",
+            "value": round(steps_per_s, 3),
+            "unit": "hybrid timesteps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(dt / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (seeded T30L8 state, random weights with the trained structure)",
+            "config": {
+                "workload": "configs[1]: batched reservoir forward for all 1152 subdomains + RCCL outvec "
+                            "all-gather + global-grid assembly + feedback/local-model re-tiling; SPEEDY "
+                            "window not included (fixed synthetic forecast grids)",
+                "regions": nreg,
+                "regions_per_gpu": len(regions),
+                "reservoir_nodes": "5760/6160/6048/5880 (NINT(6000/ninp)*ninp)",
+                "weights": f"{args.weights} storage ({'exact file precision' if args.weights == 'f32' else 'fp64'}), "
+                           "fp64 arithmetic",
+                "parallelism": f"res_domain sharded over {world} GPU(s)",
+            },
+            "roofline": {
+                "kernel": "k_res_readout (W_out GEMV, 17 waves x 8 rows per region)",
+                "bound": "hbm",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic,
+                "algorithmic_bytes_per_launch": rd_bytes,
+                "fp64_weight_equivalent_GBps": round(rd_bytes_f64 / rd_avg_s / 1e9, 1),
+                "readout_avg_ms": round(rd_avg_s * 1e3, 4),
+                "update_avg_ms": round(upd_avg_s * 1e3, 4),
+                "step_algorithmic_bytes": algo_step,
+            },
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(sample: int, nreg: int, mask):
+    """The oracle's restatement of predict (dense W_in matmul, COO SpMV, dense W_out
+    GEMV: the reference's arithmetic) timed on one host core over a bounded sample
+    of regions spread over the shape classes, plus the exchange/tiling oracle on
+    every region; extrapolated to one hybrid step of all 1152 regions."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle
+    from speedy_ml_amd import domain
+    from speedy_ml_amd.synthetic import feedback_vector, initial_state, local_model_vector, region_weights
+
+    stride = max(1, nreg // sample)
+    picks = list(range(0, nreg, stride))[:sample]
+    t_pred = 0.0
+    for r in picks:
+        w = region_weights(r, bool(mask[r]))
+        win = w.win.astype(np.float64)
+        wout = w.wout.astype(np.float64)
+        vals = w.vals.astype(np.float64)
+        x = initial_state(r, w.n)
+        fb = feedback_vector(r, w.ninp)
+        lm = local_model_vector(r)
+        t0 = time.perf_counter()
+        oracle.predict(w.rows, w.cols, vals, win, wout, fb, lm, x, w.mean, w.std)
+        t_pred += time.perf_counter() - t0
+    per_region = t_pred / len(picks)
+    # exchange on the host: assemble + tile every region (root-serial in the reference)
+    outvecs = np.random.default_rng(0).standard_normal((nreg, 136))
+    g4, g2, pr = (None, None, None)
+    t0 = time.perf_counter()
+    g4, g2, pr = oracle.assemble(outvecs)
+    ms = np.ones(36)
+    for r in range(nreg):
+        oracle.tile_feedback(r, g4, g2, pr, np.zeros(36), ms, np.zeros(16))
+        oracle.tile_local_model(r, g4, g2, np.zeros(36), ms)
+    t_xchg = time.perf_counter() - t0
+    step_s = per_region * nreg + t_xchg
+    return {
+        "value": round(1.0 / step_s, 4),
+        "unit": "hybrid timesteps/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": f"oracle predict (dense W_in as the reference) timed on {len(picks)} of {nreg} regions "
+                  f"(every {stride}th, all shape classes), {per_region * 1e3:.3f} ms/region, extrapolated to "
+                  f"{nreg}; + host assemble/tile of all regions {t_xchg * 1e3:.1f} ms; "
+                  f"host {platform.processor() or platform.machine()}, {os.cpu_count()} logical CPUs visible",
+    }
+
+
+if __name__ == "__main__":
+    main()

@@ -64,7 +64,7 @@ def test_predict_small_reservoirs(cuda, steps):
 
 def test_predict_full_size_reservoirs(cuda):
     """Full-size regions of all four shape classes (n = 5760, 6160, 6048, 5880)."""
-    cases = [(5, True), (24, False), (0, True), (1127, False)]
+    cases = [(5, True), (30, False), (0, True), (1127, False)]
     res, ws = _build(cases)
     assert sorted(int(v) for v in res.n) == [5760, 5880, 6048, 6160]
     fb = np.concatenate([feedback_vector(w.region, w.ninp) for w in ws])
