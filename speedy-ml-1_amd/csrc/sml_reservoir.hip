@@ -39,9 +39,15 @@ constexpr int kMeanStd = 36;    // mean/std vector length (mod_reservoir.f90:181
 constexpr int kTisrStride = 16; // packed tisr input: [nlocal][16]
 constexpr int kSrcKeep = -1;    // feedback entry left untouched (sst)
 
+constexpr int kEllA = 8;  // ELL slots per row for A, row-major (makesparse rows hold floor(k/n) or +1 <= 8)
+constexpr int kEllW = 1;  // ELL slots per row for W_in (the trained W_in has one entry per row)
+
 struct RegionDev {
-    int n, ninp, ld, pad_;
+    int n, ninp, ld;
+    int a_w, w_w;  // ELL widths of A and W_in (0 = use the CSR copy)
+    int pad_;
     int64_t a_rp, a_nz, w_rp, w_nz, wout, x, xaug, fb;
+    int64_t a_ell, w_ell;  // offsets into the ELL pools (row-major [n][slots])
 };
 
 }  // namespace
@@ -56,13 +62,18 @@ struct sml_reservoirs {
     int64_t tot_a_rp = 0, tot_a_nz = 0, tot_w_rp = 0, tot_w_nz = 0, tot_wout = 0, tot_x = 0, tot_xaug = 0,
             tot_fb = 0;
     std::vector<int64_t> w_nz_cap;  // reserved W_in nnz per region (n, grows on reload)
-    int maxn = 0;
+    int maxn = 0, maxninp = 0;
     int device = 0;
     // device buffers
     RegionDev *d_rd = nullptr;
     int32_t *d_a_rp = nullptr, *d_w_rp = nullptr;
     uint16_t *d_a_col = nullptr, *d_w_col = nullptr;
     void *d_a_val = nullptr, *d_w_val = nullptr, *d_wout = nullptr;
+    // ELL copies (row-major per region), used when rows are short enough
+    std::vector<int> a_ell_cap, w_ell_cap;  // slots per row reserved per region
+    int64_t tot_a_ell = 0, tot_w_ell = 0;
+    uint16_t *d_a_ell_col = nullptr, *d_w_ell_col = nullptr;
+    void *d_a_ell_val = nullptr, *d_w_ell_val = nullptr;
     double *d_x[2] = {nullptr, nullptr};
     int cur = 0;
     double *d_xaug = nullptr, *d_meanstd = nullptr;
@@ -83,40 +94,138 @@ struct sml_reservoirs {
 namespace {
 
 // ------------------------------------------------------------------ kernels
-// update: one thread per reservoir node; blockIdx.y = local region.
+// XCD-contiguous remap of a 1-D grid: consecutive hardware blocks are dealt
+// round-robin to the 8 XCDs (MI355X_MICROARCH.md, workgroup dispatch); this
+// bijection gives each XCD one contiguous range of logical blocks, so all blocks
+// of a region share one L2 (speed only, never correctness).
+__device__ inline int xcd_remap(int b, int nb) {
+    const int q8 = nb / 8, rem = nb % 8, xcd = b % 8, idx = b / 8;
+    return xcd * q8 + min(xcd, rem) + idx;
+}
+
+constexpr int kUpdThreads = 1024;  // threads per update block (one row per thread per pass)
+
+struct Ell {
+    const uint16_t *a_col;
+    const void *a_val;
+    const uint16_t *w_col;
+    const void *w_val;
+};
+
+// Row loads of one pass, issued ahead of their use (software pipelining).  A's ELL
+// is row-major [n][8]: one 16-B load brings a row's 8 column indices, two 16-B
+// (fp32) or four 16-B (fp64) loads its values, coalesced across the wave.
 template <typename WT>
-__global__ __launch_bounds__(256) void k_res_update(const RegionDev *__restrict__ R, const int32_t *__restrict__ a_rp,
-                                                    const uint16_t *__restrict__ a_col, const WT *__restrict__ a_val,
-                                                    const int32_t *__restrict__ w_rp,
-                                                    const uint16_t *__restrict__ w_col, const WT *__restrict__ w_val,
-                                                    const double *__restrict__ x_old, double *__restrict__ x_new,
-                                                    double *__restrict__ xaug, const double *__restrict__ feedback,
-                                                    const double *__restrict__ local_model, int ncs, double leak) {
-    const int r = blockIdx.y;
+struct RowRegs {
+    uint4 c;
+    WT v[kEllA];
+    uint32_t wc;
+    WT wv;
+};
+
+template <typename WT>
+__device__ inline void load_row(RowRegs<WT> &q, const RegionDev &rg, const Ell &ell, int i, bool live) {
+    if (live && rg.a_w > 0) {
+        q.c = *reinterpret_cast<const uint4 *>(ell.a_col + rg.a_ell + (size_t)i * kEllA);
+        const WT *ev = (const WT *)ell.a_val + rg.a_ell + (size_t)i * kEllA;
+        if constexpr (sizeof(WT) == 4) {
+            const float4 a = reinterpret_cast<const float4 *>(ev)[0], b = reinterpret_cast<const float4 *>(ev)[1];
+            q.v[0] = a.x; q.v[1] = a.y; q.v[2] = a.z; q.v[3] = a.w;
+            q.v[4] = b.x; q.v[5] = b.y; q.v[6] = b.z; q.v[7] = b.w;
+        } else {
+#pragma unroll
+            for (int s = 0; s < kEllA / 2; ++s) {
+                const double2 a = reinterpret_cast<const double2 *>(ev)[s];
+                q.v[2 * s] = a.x;
+                q.v[2 * s + 1] = a.y;
+            }
+        }
+    }
+    if (live && rg.w_w > 0) {
+        q.wc = ell.w_col[rg.w_ell + i];
+        q.wv = ((const WT *)ell.w_val)[rg.w_ell + i];
+    }
+}
+
+__device__ inline int ell_col(const uint4 &c, int s) {
+    const uint32_t w = s < 2 ? c.x : s < 4 ? c.y : s < 6 ? c.z : c.w;
+    return (s & 1) ? (int)(w >> 16) : (int)(w & 0xffffu);
+}
+
+// update: logical block = (region, part); a part is a contiguous range of rows
+// walked in passes of 1024 rows.  With kLds the region's state x and feedback u
+// are staged once per block in LDS and the SpMV's random column gathers hit LDS
+// instead of the L2 (one L2 transaction per gathered double otherwise).  A and
+// W_in are read in ELL form when the region's rows are short (row-major [n][8]:
+// a row's slots arrive in 16-B loads, coalesced across the wave;
+// padding slots hold 0 * x[0] after the row's real entries, so the file-order sum
+// is unchanged), otherwise from the CSR copy.  The next pass's ELL loads are issued
+// before the current pass computes.
+template <typename WT, bool kLds>
+__global__ __launch_bounds__(kUpdThreads) void k_res_update(
+    const RegionDev *__restrict__ R, const int32_t *__restrict__ a_rp, const uint16_t *__restrict__ a_col,
+    const WT *__restrict__ a_val, const int32_t *__restrict__ w_rp, const uint16_t *__restrict__ w_col,
+    const WT *__restrict__ w_val, Ell ell, const double *__restrict__ x_old, double *__restrict__ x_new,
+    double *__restrict__ xaug, const double *__restrict__ feedback, const double *__restrict__ local_model, int ncs,
+    double leak, int parts, int lds_x) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    const int lb = xcd_remap(blockIdx.x, gridDim.x);
+    const int r = lb / parts, part = lb % parts;
     const RegionDev rg = R[r];
-    if (blockIdx.x == 0 && local_model)
-        for (int c = threadIdx.x; c < ncs; c += blockDim.x)
-            xaug[rg.xaug + c] = local_model[(size_t)r * ncs + c];
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= rg.n) return;
+    const int n = rg.n, tid = threadIdx.x;
+    const int per = (n + parts - 1) / parts;
+    const int beg = part * per, end = min(n, beg + per);
+    if (beg >= end) return;  // block-uniform
+    RowRegs<WT> cur, nxt;
+    load_row(cur, rg, ell, beg + tid, beg + tid < end);
+    if (part == 0 && local_model)
+        for (int cc = tid; cc < ncs; cc += kUpdThreads) xaug[rg.xaug + cc] = local_model[(size_t)r * ncs + cc];
     const double *xo = x_old + rg.x;
-    // y = A x, entries of row i in the file's order (COO semantics, duplicates add)
+    const double *fb = feedback + rg.fb;
+    const double *xs = xo, *fs = fb;
+    if (kLds) {
+        double *sx = smem, *sf = smem + lds_x;
+        for (int j = tid; j < n; j += kUpdThreads) sx[j] = xo[j];
+        for (int j = tid; j < rg.ninp; j += kUpdThreads) sf[j] = fb[j];
+        __syncthreads();
+        xs = sx;
+        fs = sf;
+    }
     const int32_t *rp = a_rp + rg.a_rp;
     const uint16_t *ac = a_col + rg.a_nz;
     const WT *av = a_val + rg.a_nz;
-    double y = 0.0;
-    for (int e = rp[i], e1 = rp[i + 1]; e < e1; ++e) y = y + (double)av[e] * xo[ac[e]];
-    // temp = W_in feedback
     const int32_t *wp = w_rp + rg.w_rp;
     const uint16_t *wc = w_col + rg.w_nz;
     const WT *wv = w_val + rg.w_nz;
-    const double *fb = feedback + rg.fb;
-    double t = 0.0;
-    for (int e = wp[i], e1 = wp[i + 1]; e < e1; ++e) t = t + (double)wv[e] * fb[wc[e]];
-    const double xn = tanh(y + t);
-    const double xv = (1.0 - leak) * xo[i] + leak * xn;
-    x_new[rg.x + i] = xv;
-    xaug[rg.xaug + ncs + i] = (i & 1) ? xv * xv : xv;  // x_temp(2:n:2)**2 (1-based even)
+    for (int base = beg; base < end; base += kUpdThreads) {
+        const int i = base + tid;
+        const bool live = i < end;
+        const int inext = i + kUpdThreads;
+        if (base + kUpdThreads < end) load_row(nxt, rg, ell, inext, inext < end);
+        if (live) {
+            // y = A x, entries of row i in the file's order (COO semantics, duplicates add)
+            double y = 0.0;
+            if (rg.a_w > 0) {
+#pragma unroll
+                for (int s = 0; s < kEllA; ++s)
+                    if (s < rg.a_w) y = y + (double)cur.v[s] * xs[ell_col(cur.c, s)];
+            } else {
+                for (int e = rp[i], e1 = rp[i + 1]; e < e1; ++e) y = y + (double)av[e] * xs[ac[e]];
+            }
+            // temp = W_in feedback
+            double t = 0.0;
+            if (rg.w_w > 0) {
+                t = t + (double)cur.wv * fs[cur.wc];
+            } else {
+                for (int e = wp[i], e1 = wp[i + 1]; e < e1; ++e) t = t + (double)wv[e] * fs[wc[e]];
+            }
+            const double xn = tanh(y + t);
+            const double xv = (1.0 - leak) * xs[i] + leak * xn;
+            x_new[rg.x + i] = xv;
+            xaug[rg.xaug + ncs + i] = (i & 1) ? xv * xv : xv;  // x_temp(2:n:2)**2 (1-based even)
+        }
+        cur = nxt;
+    }
 }
 
 template <typename WT>
@@ -138,9 +247,7 @@ __global__ __launch_bounds__(256) void k_res_readout(const RegionDev *__restrict
                                                      const double *__restrict__ meanstd,
                                                      const int8_t *__restrict__ outl, double *__restrict__ outvec,
                                                      int nout, int groups, int nitems) {
-    const int nb = gridDim.x, b = blockIdx.x;
-    const int q8 = nb / 8, rem = nb % 8, xcd = b % 8, idx = b / 8;
-    const int bs = xcd * q8 + min(xcd, rem) + idx;  // bijective XCD-contiguous remap
+    const int bs = xcd_remap(blockIdx.x, gridDim.x);
     const int lane = threadIdx.x & 63;
     const int item = bs * 4 + (threadIdx.x >> 6);
     if (item >= nitems) return;
@@ -456,6 +563,31 @@ int load_region_impl(sml_reservoirs *c, int i, const int *rows, const int *cols,
         SML_HIP(hipMemcpy((char *)c->d_w_val + rg.w_nz * wb, wval.data(), wval.size() * wb, hipMemcpyHostToDevice));
     }
     SML_HIP(hipMemcpy((char *)c->d_wout + rg.wout * wb, wt.data(), wt.size() * wb, hipMemcpyHostToDevice));
+    // --- ELL copies when every row fits the reserved slots (row-major [n][cap], file
+    // order within a row, zero-padded after the row's entries)
+    auto ell = [&](const std::vector<int32_t> &p, const std::vector<uint16_t> &col, const std::vector<StoT> &val,
+                   int cap, uint16_t *dcol, void *dval, int64_t off, int *width) -> int {
+        int w = 0;
+        for (int r = 0; r < n; ++r) w = std::max(w, p[r + 1] - p[r]);
+        *width = 0;
+        if (w == 0 || w > cap) return SML_OK;
+        std::vector<uint16_t> ec((size_t)cap * n, 0);
+        std::vector<StoT> ev((size_t)cap * n, (StoT)0);
+        for (int r = 0; r < n; ++r)
+            for (int e = p[r]; e < p[r + 1]; ++e) {
+                ec[(size_t)r * cap + (e - p[r])] = col[e];
+                ev[(size_t)r * cap + (e - p[r])] = val[e];
+            }
+        SML_HIP(hipMemcpy(dcol + off, ec.data(), ec.size() * 2, hipMemcpyHostToDevice));
+        SML_HIP(hipMemcpy((char *)dval + off * wb, ev.data(), ev.size() * wb, hipMemcpyHostToDevice));
+        *width = w;
+        return SML_OK;
+    };
+    RegionDev &rgm = c->rd[i];
+    if (int rc = ell(rp, acol, aval, c->a_ell_cap[i], c->d_a_ell_col, c->d_a_ell_val, rgm.a_ell, &rgm.a_w)) return rc;
+    if (int rc = ell(wrp, wcol, wval, c->w_ell_cap[i], c->d_w_ell_col, c->d_w_ell_val, rgm.w_ell, &rgm.w_w))
+        return rc;
+    SML_HIP(hipMemcpy(c->d_rd + i, &rgm, sizeof(RegionDev), hipMemcpyHostToDevice));
     double ms[2 * kMeanStd];
     std::memcpy(ms, mean, sizeof(double) * kMeanStd);
     std::memcpy(ms + kMeanStd, std, sizeof(double) * kMeanStd);
@@ -476,6 +608,9 @@ int check_region(const sml_reservoirs *c, int i) {
 // ------------------------------------------------------------------ API
 extern "C" int sml_res_destroy(sml_reservoirs *c) {
     if (!c) return SML_OK;
+    void *ells[] = {c->d_a_ell_col, c->d_w_ell_col, c->d_a_ell_val, c->d_w_ell_val};
+    for (void *p : ells)
+        if (p) (void)hipFree(p);
     void *ptrs[] = {c->d_rd,    c->d_a_rp,    c->d_w_rp,   c->d_a_col,  c->d_w_col,  c->d_a_val,  c->d_w_val,
                     c->d_wout,  c->d_x[0],    c->d_x[1],   c->d_xaug,   c->d_meanstd, c->d_outl,  c->d_asm_dst,
                     c->d_fb_src, c->d_fb_l,   c->d_fb_reg, c->d_lm_src, c->d_lm_l,   c->d_io};
@@ -560,9 +695,23 @@ extern "C" int sml_res_create(int numregions, int nlocal, const int *region_ids,
         r.fb = c->tot_fb;
         c->tot_fb += c->ninp[i];
         c->maxn = std::max(c->maxn, n[i]);
+        c->maxninp = std::max(c->maxninp, c->ninp[i]);
+        // makesparse rows hold floor(k/n) or floor(k/n)+1 entries (per-block permutations)
+        c->a_ell_cap.push_back(k[i] / n[i] + 1 <= kEllA ? kEllA : 0);
+        c->w_ell_cap.push_back(kEllW);
+        r.a_w = r.w_w = 0;
+        r.a_ell = c->tot_a_ell;
+        c->tot_a_ell += (int64_t)c->a_ell_cap.back() * n[i];
+        r.w_ell = c->tot_w_ell;
+        c->tot_w_ell += (int64_t)c->w_ell_cap.back() * n[i];
     }
     const size_t wb = wbytes(c);
     int rc;
+    if ((rc = dalloc(&c->d_a_ell_col, c->tot_a_ell)) || (rc = dalloc_bytes(&c->d_a_ell_val, c->tot_a_ell * wb)) ||
+        (rc = dalloc(&c->d_w_ell_col, c->tot_w_ell)) || (rc = dalloc_bytes(&c->d_w_ell_val, c->tot_w_ell * wb))) {
+        sml_res_destroy(c);
+        return rc;
+    }
     if ((rc = dalloc(&c->d_rd, nlocal)) || (rc = dalloc(&c->d_a_rp, c->tot_a_rp)) ||
         (rc = dalloc(&c->d_a_col, c->tot_a_nz)) || (rc = dalloc_bytes(&c->d_a_val, c->tot_a_nz * wb)) ||
         (rc = dalloc(&c->d_w_rp, c->tot_w_rp)) || (rc = dalloc(&c->d_w_col, c->tot_w_nz)) ||
@@ -696,15 +845,33 @@ extern "C" int sml_res_step(sml_reservoirs *c, const double *d_feedback, const d
     const bool rec = c->timing && c->ev_used < c->ev_cap;
     hipEvent_t *ev = rec ? &c->ev[3 * c->ev_used] : nullptr;
     if (rec) SML_HIP(hipEventRecord(ev[0], st));
-    dim3 ug((c->maxn + 255) / 256, c->nlocal);
-    if (c->wdtype == SML_F32)
-        hipLaunchKernelGGL(k_res_update<float>, ug, dim3(256), 0, st, c->d_rd, c->d_a_rp, c->d_a_col,
-                           (const float *)c->d_a_val, c->d_w_rp, c->d_w_col, (const float *)c->d_w_val, xo, xn,
-                           c->d_xaug, d_feedback, c->ncs ? d_local_model : nullptr, c->ncs, c->leakage);
-    else
-        hipLaunchKernelGGL(k_res_update<double>, ug, dim3(256), 0, st, c->d_rd, c->d_a_rp, c->d_a_col,
-                           (const double *)c->d_a_val, c->d_w_rp, c->d_w_col, (const double *)c->d_w_val, xo, xn,
-                           c->d_xaug, d_feedback, c->ncs ? d_local_model : nullptr, c->ncs, c->leakage);
+    // parts per region: enough blocks for ~4 rounds of the 512 resident 1024-thread
+    // blocks (2 per CU with ~54 KB LDS each), each part at least one 1024-row pass
+    const int max_parts = std::max(1, (c->maxn + kUpdThreads - 1) / kUpdThreads);
+    const int parts = std::max(1, std::min(max_parts, (4 * 512 + c->nlocal - 1) / c->nlocal));
+    const int lds_x = (c->maxn + 1) / 2 * 2;
+    const size_t lds = (size_t)(lds_x + c->maxninp) * sizeof(double);
+    const bool use_lds = lds <= 64 * 1024;
+    const int bpr = parts;
+    dim3 ug(bpr * c->nlocal);
+    const double *lmp = c->ncs ? d_local_model : nullptr;
+#define SML_UPD(WT, L)                                                                                            \
+    hipLaunchKernelGGL((k_res_update<WT, L>), ug, dim3(kUpdThreads), L ? lds : 0, st, c->d_rd, c->d_a_rp,          \
+                       c->d_a_col, (const WT *)c->d_a_val, c->d_w_rp, c->d_w_col, (const WT *)c->d_w_val, ell,    \
+                       xo, xn, c->d_xaug, d_feedback, lmp, c->ncs, c->leakage, bpr, lds_x)
+    Ell ell{c->d_a_ell_col, c->d_a_ell_val, c->d_w_ell_col, c->d_w_ell_val};
+    if (c->wdtype == SML_F32) {
+        if (use_lds)
+            SML_UPD(float, true);
+        else
+            SML_UPD(float, false);
+    } else {
+        if (use_lds)
+            SML_UPD(double, true);
+        else
+            SML_UPD(double, false);
+    }
+#undef SML_UPD
     SML_HIP(hipGetLastError());
     if (rec) SML_HIP(hipEventRecord(ev[1], st));
     const int groups = c->nout_pad / kRows;

@@ -92,6 +92,30 @@ def test_predict_f64_storage_and_dense_oracle(cuda):
         _check(res.get_state(i), x1, X_TOL)
 
 
+def test_long_rows_use_csr_fallback(cuda):
+    """A with a 40-entry row and W_in with a 3-entry row exceed the ELL slots: the
+    CSR copies are used; results still follow the file-order sums."""
+    from speedy_ml_amd.reservoir import Reservoirs
+
+    w = region_weights(300, True, n_override=700)
+    rows = w.rows.copy()
+    rows[:40] = 7  # row 7 gets 40 entries (duplicates of (7, col) add)
+    win = w.win.copy()
+    win[:, 20:23] = 0.0  # three empty rows keep nnz(W_in) <= n (the reserved capacity)
+    win[:3, 11] = [0.25, -0.5, 0.125]  # row 12 of W_in reads three inputs
+    res = Reservoirs([300], [1], [w.n], [w.k])
+    res.load_region(0, rows, w.cols, w.vals, win, w.wout, w.mean, w.std)
+    x0 = initial_state(300, w.n)
+    res.set_state(0, x0)
+    fb = feedback_vector(300, w.ninp)
+    lm = local_model_vector(300)
+    out = res.predict_host(fb, lm[None, :])
+    ref, x1 = oracle.predict(rows, w.cols, w.vals.astype(np.float64), win.astype(np.float64),
+                             w.wout.astype(np.float64), fb, lm, x0, w.mean, w.std)
+    _check(out[0], ref, OUT_TOL)
+    _check(res.get_state(0), x1, X_TOL)
+
+
 def test_ml_only_mode(cuda):
     """chunk_speedy = 0: predict_ml (mod_reservoir.f90:1489-1533)."""
     res, ws = _build(CASES[:4], n_override=600, chunk_speedy=0)
