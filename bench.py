@@ -61,6 +61,7 @@ def main():
     import torch.distributed as dist
 
     from speedy_ml_amd import domain
+    from speedy_ml_amd.exchange import OutvecExchange
     from speedy_ml_amd.reservoir import Reservoirs
     from speedy_ml_amd.synthetic import initial_state, region_weights, synthetic_grids
 
@@ -76,8 +77,6 @@ def main():
     nreg = args.regions
     mask = domain.load_sst_mask()
     regions = domain.processor_decomposition(nreg, world, rank)
-    counts = [len(domain.processor_decomposition(nreg, world, r)) for r in range(world)]
-    maxc = max(counts)
 
     # ---- setup: synthetic weights with the trained structure, loaded per region
     t_setup = time.time()
@@ -95,8 +94,7 @@ def main():
         if i % 144 == 0:
             log(rank, f"loaded {i}/{len(regions)} regions ({time.time() - t_setup:.1f}s)")
     fb, lm, ov = res.alloc_io(dev)
-    ov_all = torch.zeros((maxc * world, 136), dtype=torch.float64, device=dev)
-    ov_send = torch.zeros((maxc, 136), dtype=torch.float64, device=dev)
+    exchange = OutvecExchange(nreg, world, rank, device=dev)
     g4h, g2h, prh = synthetic_grids(11)
     f4h, f2h, _ = synthetic_grids(12)
     g4 = torch.from_numpy(g4h).to(dev)
@@ -107,27 +105,12 @@ def main():
     tisr = torch.from_numpy(np.random.default_rng(13).standard_normal((len(regions), 16))).to(dev)
     # initial inputs from the synthetic analysis state (start_prediction analogue)
     res.tile_inputs(g4, g2, pr, f4, f2, tisr, fb, lm)
-    # all-gather order -> global region order
-    gather_rows = np.concatenate([np.arange(counts[r]) + r * maxc for r in range(world)])
-    gather_regions = np.concatenate([domain.processor_decomposition(nreg, world, r) for r in range(world)])
-    contiguous = world == 1 or (np.array_equal(gather_regions, np.arange(nreg)) and len(set(counts)) == 1)
-    perm = torch.from_numpy(gather_rows[np.argsort(gather_regions)]).to(dev)
-    ov_glob = torch.zeros((nreg, 136), dtype=torch.float64, device=dev)
     torch.cuda.synchronize()
     log(rank, f"setup {time.time() - t_setup:.1f}s, {len(regions)} regions on rank 0")
 
     def step():
         res.predict(fb, lm, ov)
-        if world == 1:
-            glob = ov
-        else:
-            ov_send[:len(regions)].copy_(ov)
-            dist.all_gather_into_tensor(ov_all, ov_send)
-            if contiguous:
-                glob = ov_all
-            else:
-                torch.index_select(ov_all, 0, perm, out=ov_glob)
-                glob = ov_glob
+        glob = exchange(ov)  # RCCL all-gather over xGMI when world > 1
         res.assemble(glob, g4, g2, pr)
         res.tile_inputs(g4, g2, pr, f4, f2, tisr, fb, lm)
 

@@ -1,0 +1,215 @@
+!> sml_hip -- ISO_C_BINDING interface of libspeedyml (include/speedy_ml.h) for the
+!> Fortran host of SPEEDY-ML.
+!>
+!> This is the binding a reference maintainer adds: the reference calls predict()
+!> per region (src/parallelmain.f90:225-234 -> src/mod_reservoir.f90:1416) and the
+!> external spectral routines grid/spec/vdspec/uvspec one field at a time
+!> (src/spe_spectral.f90:351-452).  The interfaces below hand the same
+!> column-major Fortran arrays to the batched GPU entry points.  Helper routines
+!> mirror the reference's names:
+!>   sml_read_trained_res  <- read_trained_res (src/mod_io.f90:2911-2956)
+!>   sml_predict_all       <- predict for every region of the rank
+!>   sml_check             <- nc_check-style error stop (src/mod_io.f90:1732-1744)
+module sml_hip
+  use iso_c_binding
+  implicit none
+
+  integer(c_int), parameter :: SML_OK = 0, SML_F32 = 1, SML_F64 = 2
+  integer, parameter :: SML_SPEC_FIELD = 1984, SML_GRID_FIELD = 4608
+
+  interface
+    function sml_last_error() bind(C, name='sml_last_error') result(p)
+      import :: c_ptr
+      type(c_ptr) :: p
+    end function
+    function sml_abi_version() bind(C, name='sml_abi_version') result(v)
+      import :: c_int
+      integer(c_int) :: v
+    end function
+
+    ! ------------------------------------------------------------ spectral
+    function sml_spectral_create(radius, ctx) bind(C, name='sml_spectral_create') result(rc)
+      import :: c_double, c_ptr, c_int
+      real(c_double), value :: radius
+      type(c_ptr) :: ctx
+      integer(c_int) :: rc
+    end function
+    function sml_spectral_destroy(ctx) bind(C, name='sml_spectral_destroy') result(rc)
+      import :: c_ptr, c_int
+      type(c_ptr), value :: ctx
+      integer(c_int) :: rc
+    end function
+    !> grid for nf fields: spec(62,32,nf) -> grid(96,48,nf) (host arrays, synchronous)
+    function sml_grid_host(ctx, spec, grid, nf, kcos) bind(C, name='sml_grid_host') result(rc)
+      import :: c_ptr, c_double, c_int
+      type(c_ptr), value :: ctx
+      real(c_double), intent(in) :: spec(*)
+      real(c_double), intent(out) :: grid(*)
+      integer(c_int), value :: nf, kcos
+      integer(c_int) :: rc
+    end function
+    function sml_spec_host(ctx, grid, spec, nf) bind(C, name='sml_spec_host') result(rc)
+      import :: c_ptr, c_double, c_int
+      type(c_ptr), value :: ctx
+      real(c_double), intent(in) :: grid(*)
+      real(c_double), intent(out) :: spec(*)
+      integer(c_int), value :: nf
+      integer(c_int) :: rc
+    end function
+    !> device-pointer batched forms (arrays already resident on the GPU)
+    function sml_grid_batched(ctx, d_spec, d_grid, nf, kcos, stream) bind(C, name='sml_grid_batched') result(rc)
+      import :: c_ptr, c_int
+      type(c_ptr), value :: ctx, d_spec, d_grid, stream
+      integer(c_int), value :: nf, kcos
+      integer(c_int) :: rc
+    end function
+    function sml_spec_batched(ctx, d_grid, d_spec, nf, stream) bind(C, name='sml_spec_batched') result(rc)
+      import :: c_ptr, c_int
+      type(c_ptr), value :: ctx, d_grid, d_spec, stream
+      integer(c_int), value :: nf
+      integer(c_int) :: rc
+    end function
+
+    ! ------------------------------------------------------------ reservoirs
+    function sml_res_create(numregions, nlocal, region_ids, sst_flags, n, k, chunk_speedy, nout, &
+                            weight_dtype, leakage, ctx) bind(C, name='sml_res_create') result(rc)
+      import :: c_int, c_signed_char, c_double, c_ptr
+      integer(c_int), value :: numregions, nlocal, chunk_speedy, nout, weight_dtype
+      integer(c_int), intent(in) :: region_ids(*), n(*), k(*)
+      integer(c_signed_char), intent(in) :: sst_flags(*)
+      real(c_double), value :: leakage
+      type(c_ptr) :: ctx
+      integer(c_int) :: rc
+    end function
+    function sml_res_destroy(ctx) bind(C, name='sml_res_destroy') result(rc)
+      import :: c_ptr, c_int
+      type(c_ptr), value :: ctx
+      integer(c_int) :: rc
+    end function
+    function sml_res_ninp(ctx, i, ninp) bind(C, name='sml_res_ninp') result(rc)
+      import :: c_ptr, c_int
+      type(c_ptr), value :: ctx
+      integer(c_int), value :: i
+      integer(c_int), intent(out) :: ninp
+      integer(c_int) :: rc
+    end function
+    function sml_res_feedback_offsets(ctx, offsets) bind(C, name='sml_res_feedback_offsets') result(rc)
+      import :: c_ptr, c_int, c_int64_t
+      type(c_ptr), value :: ctx
+      integer(c_int64_t), intent(out) :: offsets(*)
+      integer(c_int) :: rc
+    end function
+    !> i is 0-based; arrays in the reference layouts: win(n,ninp), wout(nout,ncs+n)
+    function sml_res_load_region_f32(ctx, i, rows, cols, vals, win, wout, mean, std) &
+        bind(C, name='sml_res_load_region_f32') result(rc)
+      import :: c_ptr, c_int, c_float, c_double
+      type(c_ptr), value :: ctx
+      integer(c_int), value :: i
+      integer(c_int), intent(in) :: rows(*), cols(*)
+      real(c_float), intent(in) :: vals(*), win(*), wout(*)
+      real(c_double), intent(in) :: mean(*), std(*)
+      integer(c_int) :: rc
+    end function
+    function sml_res_load_region_f64(ctx, i, rows, cols, vals, win, wout, mean, std) &
+        bind(C, name='sml_res_load_region_f64') result(rc)
+      import :: c_ptr, c_int, c_double
+      type(c_ptr), value :: ctx
+      integer(c_int), value :: i
+      integer(c_int), intent(in) :: rows(*), cols(*)
+      real(c_double), intent(in) :: vals(*), win(*), wout(*)
+      real(c_double), intent(in) :: mean(*), std(*)
+      integer(c_int) :: rc
+    end function
+    function sml_res_set_state(ctx, i, x) bind(C, name='sml_res_set_state') result(rc)
+      import :: c_ptr, c_int, c_double
+      type(c_ptr), value :: ctx
+      integer(c_int), value :: i
+      real(c_double), intent(in) :: x(*)
+      integer(c_int) :: rc
+    end function
+    function sml_res_get_state(ctx, i, x) bind(C, name='sml_res_get_state') result(rc)
+      import :: c_ptr, c_int, c_double
+      type(c_ptr), value :: ctx
+      integer(c_int), value :: i
+      real(c_double), intent(out) :: x(*)
+      integer(c_int) :: rc
+    end function
+    !> predict for every local region, host buffers (PCIe-inclusive convenience)
+    function sml_res_step_host(ctx, feedback, local_model, outvec) bind(C, name='sml_res_step_host') result(rc)
+      import :: c_ptr, c_int, c_double
+      type(c_ptr), value :: ctx
+      real(c_double), intent(in) :: feedback(*), local_model(*)
+      real(c_double), intent(out) :: outvec(*)
+      integer(c_int) :: rc
+    end function
+    !> device-resident form
+    function sml_res_step(ctx, d_feedback, d_local_model, d_outvec, stream) bind(C, name='sml_res_step') result(rc)
+      import :: c_ptr, c_int
+      type(c_ptr), value :: ctx, d_feedback, d_local_model, d_outvec, stream
+      integer(c_int) :: rc
+    end function
+
+    ! ------------------------------------------------------------ NetCDF weight files
+    function sml_nc_read_region(path, dims, win, wout, rows, cols, vals, mean, std) &
+        bind(C, name='sml_nc_read_region') result(rc)
+      import :: c_char, c_int64_t, c_ptr, c_int
+      character(kind=c_char), intent(in) :: path(*)
+      integer(c_int64_t), intent(out) :: dims(6)
+      type(c_ptr), value :: win, wout, rows, cols, vals, mean, std
+      integer(c_int) :: rc
+    end function
+  end interface
+
+contains
+
+  !> stop with the library's message, like nc_check (mod_io.f90:1732-1744)
+  subroutine sml_check(rc, what)
+    integer(c_int), intent(in) :: rc
+    character(len=*), intent(in) :: what
+    character(kind=c_char), pointer :: msg(:)
+    integer :: l
+    if (rc == SML_OK) return
+    call c_f_pointer(sml_last_error(), msg, [1024])
+    l = 0
+    do while (l < 1024)
+      if (msg(l + 1) == c_null_char) exit
+      l = l + 1
+    end do
+    print *, 'libspeedyml error in ', what, ' (', rc, '): ', msg(1:l)
+    stop 1
+  end subroutine
+
+  !> read_trained_res (mod_io.f90:2911-2956) + the load into the GPU context for
+  !> local region i (0-based): the file's fp32 arrays go to the device unchanged.
+  subroutine sml_read_trained_res(ctx, i, filename)
+    type(c_ptr), intent(in) :: ctx
+    integer, intent(in) :: i
+    character(len=*), intent(in) :: filename
+    integer(c_int64_t) :: dims(6)
+    real(c_float), allocatable, target :: win(:), wout(:), vals(:), mean32(:), std32(:)
+    integer(c_int), allocatable, target :: rows(:), cols(:)
+    real(c_double), allocatable :: mean(:), std(:)
+    character(kind=c_char, len=len_trim(filename) + 1) :: cpath
+    cpath = trim(filename) // c_null_char
+    call sml_check(sml_nc_read_region(cpath, dims, c_null_ptr, c_null_ptr, c_null_ptr, c_null_ptr, &
+                                      c_null_ptr, c_null_ptr, c_null_ptr), 'sml_nc_read_region(dims)')
+    allocate(win(dims(1) * dims(2)), wout(dims(3) * dims(4)), rows(dims(5)), cols(dims(5)), vals(dims(5)))
+    allocate(mean32(dims(6)), std32(dims(6)), mean(dims(6)), std(dims(6)))
+    call sml_check(sml_nc_read_region(cpath, dims, c_loc(win), c_loc(wout), c_loc(rows), c_loc(cols), &
+                                      c_loc(vals), c_loc(mean32), c_loc(std32)), 'sml_nc_read_region')
+    mean = real(mean32, c_double)   ! exact widening, as read_netcdf_1d_dp_opened does
+    std = real(std32, c_double)
+    call sml_check(sml_res_load_region_f32(ctx, int(i, c_int), rows, cols, vals, win, wout, mean, std), &
+                   'sml_res_load_region_f32')
+  end subroutine
+
+  !> predict (mod_reservoir.f90:1416) for every local region: packed feedback,
+  !> local_model(132, nlocal), outvec(136, nlocal)
+  subroutine sml_predict_all(ctx, feedback, local_model, outvec)
+    type(c_ptr), intent(in) :: ctx
+    real(c_double), intent(in) :: feedback(:), local_model(:, :)
+    real(c_double), intent(out) :: outvec(:, :)
+    call sml_check(sml_res_step_host(ctx, feedback, local_model, outvec), 'sml_res_step_host')
+  end subroutine
+
+end module sml_hip

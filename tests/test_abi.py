@@ -42,6 +42,15 @@ def test_code_object_targets_gfx950():
     assert b"gfx942" not in blob and b"gfx90a" not in blob
 
 
+def test_fortran_binding_compiles_and_matches_header():
+    fdir = os.path.join(_lib.PKG_ROOT, "fortran")
+    subprocess.run(["make", "-s", "-C", fdir], check=True)
+    src = open(os.path.join(fdir, "sml_hip.f90")).read()
+    bound = set(re.findall(r"bind\(C, name='(sml_[a-z0-9_]+)'\)", src))
+    assert len(bound) >= 15
+    assert bound <= set(header_functions())
+
+
 def test_error_reporting_without_gpu():
     L = _lib.lib()
     import ctypes
