@@ -186,6 +186,46 @@ int sml_nc_write_region(const char *path, int n, int ninp, int nout, int ncs_plu
                         const float *wout, const int *rows, const int *cols, const float *vals, const float *mean,
                         const float *std);
 
+/* ---------------------------------------------------------------- dynamics */
+/* SPEEDY's spectral dynamical core on the device.  The context owns the
+ * prognostic state in the reference's mod_dynvar layout (mod_dynvar.f90:15-27):
+ *   vor, div, t, tr   complex(mx, nx, kx, 2) -> 2*8*1984 doubles each (level 1 first)
+ *   ps                complex(mx, nx, 2)     -> 2*1984 doubles
+ * and the forcing phis (mod_dynvar), tcorh, qcorh (mod_hdifcon), complex(mx, nx).
+ * Physics grid tendencies, when given, are phys[4][kx][il][ix] = u, v, t, q
+ * (the arrays phypar adds to, dyn_grtend.f90:225-226). */
+typedef struct sml_dynamics sml_dynamics;
+
+/* indyns (src/ini_indyns.f90:1-128) + parmtr/inifft; state and forcing zeroed */
+int sml_dyn_create(double radius, sml_dynamics **out);
+int sml_dyn_destroy(sml_dynamics *d);
+/* impint(dt, alph) (src/ini_impint.f90:1-153): must precede sml_dyn_step and be
+ * repeated whenever (dt, alph) changes, as stepone does (src/ini_stepone.f90:19-34) */
+int sml_dyn_impint(sml_dynamics *d, double dt, double alph);
+/* phis, tcorh, qcorh (host, any may be NULL = unchanged) */
+int sml_dyn_set_forcing(sml_dynamics *d, const double *phis, const double *tcorh, const double *qcorh);
+/* host copies in/out of the whole prognostic state (both time levels) */
+int sml_dyn_set_state(sml_dynamics *d, const double *vor, const double *div, const double *t, const double *ps,
+                      const double *tr);
+int sml_dyn_get_state(sml_dynamics *d, double *vor, double *div, double *t, double *ps, double *tr);
+/* phi(mx, nx, kx) = geop(j4) of the last step (src/dyn_geop.f90:1-33) */
+int sml_dyn_get_phi(sml_dynamics *d, double *phi);
+/* tendencies of the last step before time integration, 4*kx+1 spectral fields:
+ * vordt | divdt | tdt | trdt | psdt (only meaningful after a dt <= 0 step: a step
+ * with dt > 0 leaves the grid-point half of grtend's tendencies there) */
+int sml_dyn_get_tendencies(sml_dynamics *d, double *tend);
+/* device addresses of the state buffer ([vor|div|t|tr|ps] as above) and of a
+ * scratch buffer sized for phys (4*kx*4608 doubles) */
+int sml_dyn_state_device(sml_dynamics *d, double **d_state, double **d_phys);
+/* step(j1, j2, dt, alph, rob, wil) (src/dyn_step.f90:1-128): grtend with the
+ * physics tendencies d_phys (device, may be NULL = no physics), sptend, implic,
+ * hordif, stratospheric drag, timint.  Asynchronous on `stream`. */
+int sml_dyn_step(sml_dynamics *d, int j1, int j2, double dt, double alph, double rob, double wil,
+                 const double *d_phys, void *stream);
+/* synchronous variant taking host physics tendencies (may be NULL) */
+int sml_dyn_step_host(sml_dynamics *d, int j1, int j2, double dt, double alph, double rob, double wil,
+                      const double *phys);
+
 #ifdef __cplusplus
 }
 #endif

@@ -71,6 +71,9 @@ def _declare(L):
     L.orc_assemble.argtypes = [i, vp, i, vp, vp, vp]
     L.orc_tile_feedback.argtypes = [i, i, vp, vp, vp, vp, vp, vp, vp, vp]
     L.orc_tile_local_model.argtypes = [i, i, vp, vp, vp, vp, vp]
+    L.orc_dyn_init.argtypes = []
+    L.orc_dyn_impint.argtypes = [d, d]
+    L.orc_dyn_step.argtypes = [vp] * 9 + [i, i, d, d, d, d, vp, vp]
 
 
 def spectral_init(radius: float = EARTH_RADIUS) -> None:
@@ -309,6 +312,41 @@ def tile_local_model(region, fc4d, fc2d, mean, std, numregions=1152):
                                _p(np.ascontiguousarray(mean, dtype=np.float64)),
                                _p(np.ascontiguousarray(std, dtype=np.float64)), _p(lm))
     return lm
+
+
+# ---------------------------------------------------------------- dynamics
+KX = 8
+DYN_FIELDS = ("vor", "div", "t", "tr", "ps")
+
+
+def dyn_state_copy(st):
+    """Contiguous complex128 copies: vor/div/t/tr (2, kx, nx, mx), ps (2, nx, mx)."""
+    return {f: np.ascontiguousarray(st[f], dtype=np.complex128).copy() for f in DYN_FIELDS}
+
+
+def dyn_step(state, phis, tcorh, qcorh, phys, j1, j2, dt, alph, rob=0.05, wil=0.53):
+    """One SPEEDY `step` (dyn_step.f90:1-128) on `state` (updated in place).
+
+    impint(dt, alph) is evaluated first, as stepone/stloop do before their steps.
+    phys: physics grid tendencies (4, kx, 48, 96) = u, v, t, q, or None.
+    Returns (phi = geop(j4) (kx, nx, mx) complex, tendencies before timint
+    (4*kx+1, nx, mx) complex: vordt | divdt | tdt | trdt | psdt)."""
+    spectral_init()
+    L = lib()
+    L.orc_dyn_init()
+    L.orc_dyn_impint(dt, alph)
+    for f in DYN_FIELDS:
+        a = state[f]
+        assert a.dtype == np.complex128 and a.flags.c_contiguous
+    cplx = lambda a: np.ascontiguousarray(a, dtype=np.complex128)
+    phis, tcorh, qcorh = cplx(phis), cplx(tcorh), cplx(qcorh)
+    ph = None if phys is None else np.ascontiguousarray(phys, dtype=np.float64)
+    phi = np.zeros((KX, NX, MX), np.complex128)
+    tend = np.zeros((4 * KX + 1, NX, MX), np.complex128)
+    L.orc_dyn_step(_p(state["vor"]), _p(state["div"]), _p(state["t"]), _p(state["ps"]), _p(state["tr"]),
+                   _p(phis), _p(tcorh), _p(qcorh), None if ph is None else _p(ph), j1, j2, dt, alph, rob, wil,
+                   _p(phi), _p(tend))
+    return phi, tend
 
 
 # ---------------------------------------------------------------- reference (pinning only)

@@ -794,3 +794,479 @@ void orc_tile_local_model(int numregions, int region, const double *fc4d, const 
             local_model[natmo + x + rx * y] = t / std[32];
         }
 }
+
+/* ------------------------------------------------------------------------- */
+/* SPEEDY dynamical core: one `step` (SURVEY.md section 8a, row "step").      */
+/*   indyns  src/ini_indyns.f90:1-128      impint  src/ini_impint.f90:1-153   */
+/*   ludcmp/lubksb/inv src/spe_matinv.f90  geop    src/dyn_geop.f90:1-33      */
+/*   step/hordif/timint src/dyn_step.f90:1-190                                */
+/*   grtend  src/dyn_grtend.f90:1-279      sptend  src/dyn_sptend.f90:1-67    */
+/*   implic  src/dyn_implic.f90:1-68                                          */
+/* Physics (phypar, dyn_grtend.f90:225) is an input: its grid-point tendencies */
+/* (u, v, t, q) are added where phypar adds them, or zero when absent.        */
+/* Pinned against the reference step compiled as-is (tests/golden/dyn_ref.npz, */
+/* tests/golden/make_dyn_golden.py).                                          */
+/* Arrays: Fortran order.  vor/div/t(mx,nx,kx,2) complex = double[2][KX][NX][2*MX], */
+/* ps(mx,nx,2), tr(mx,nx,kx,2,1), phys [4][KX][IL][IX].                        */
+/* ------------------------------------------------------------------------- */
+#define KX 8
+#define KXP 9
+#define LMAX 61
+#define SF (2 * MX * NX)
+#define GF (IX * IL)
+static const double d_rearth = 6.371e+6, d_omega = 7.292e-05, d_grav = 9.81, d_akap = 2. / 7.;
+static const double d_gamma = 6.0, d_hscale = 7.5, d_hshum = 2.5, d_thd = 2.4, d_thdd = 2.4, d_thds = 12.0,
+                    d_tdrs = 24.0 * 30.0;
+#define d_rgas (d_akap * 1004.)
+static double hsg[KXP], dhs[KX], fsg[KX], dhsr[KX], fsgr[KX], coriol[IL], xgeop1[KX], xgeop2[KX];
+static double dmp[NX][MX], dmpd[NX][MX], dmps[NX][MX], dmp1[NX][MX], dmp1d[NX][MX], dmp1s[NX][MX];
+static double tcorv[KX], qcorv[KX];
+static double tref[KX], tref1[KX], tref2[KX], tref3[KX], dhsx[KX], elz[NX][MX];
+/* column-major (k, k1) matrices stored m[k1][k] (xc, xd) and xj(k, k1, l) as xj[l][k1][k] */
+static double xc_[KX][KX], xd_[KX][KX], xj_[LMAX][KX][KX];
+
+/* indyns (ini_indyns.f90:21-127); needs orc_spectral_init(rearth) first */
+void orc_dyn_init(void)
+{
+    static const double h8[KXP] = {0.000, 0.050, 0.140, 0.260, 0.420, 0.600, 0.770, 0.900, 1.000};
+    for (int k = 0; k < KXP; ++k) hsg[k] = h8[k];
+    for (int k = 1; k <= KX; ++k) {
+        dhs[k - 1] = hsg[k] - hsg[k - 1];
+        fsg[k - 1] = 0.5 * (hsg[k] + hsg[k - 1]);
+    }
+    for (int k = 0; k < KX; ++k) {
+        dhsr[k] = 0.5 / dhs[k];
+        fsgr[k] = d_akap / (2. * fsg[k]);
+    }
+    double gsin[IL];
+    for (int j = 1; j <= IY; ++j) {
+        int jj = IL + 1 - j;
+        gsin[j - 1] = -sia[j - 1];
+        gsin[jj - 1] = sia[j - 1];
+    }
+    for (int j = 0; j < IL; ++j) coriol[j] = 2. * d_omega * gsin[j];
+    for (int k = 1; k <= KX; ++k) {
+        xgeop1[k - 1] = d_rgas * log(hsg[k] / fsg[k - 1]);
+        if (k != KX) xgeop2[k] = d_rgas * log(fsg[k] / hsg[k]);
+    }
+    double hdiff = 1. / (d_thd * 3600.), hdifd = 1. / (d_thdd * 3600.), hdifs = 1. / (d_thds * 3600.);
+    double rlap = 1. / (double)(NTRUN * (NTRUN + 1));
+    for (int j = 1; j <= NX; ++j)
+        for (int k = 1; k <= MX; ++k) {
+            double twn = (double)(k - 1 + j - 1);
+            double elap = (twn * (twn + 1.) * rlap);
+            double elapn = pow(elap, 4); /* elap**npowhd, integer power */
+            dmp[j - 1][k - 1] = hdiff * elapn;
+            dmpd[j - 1][k - 1] = hdifd * elapn;
+            dmps[j - 1][k - 1] = hdifs * elap;
+        }
+    double rgam = d_rgas * d_gamma / (1000. * d_grav), qexp = d_hscale / d_hshum;
+    tcorv[0] = 0.;
+    qcorv[0] = 0.;
+    qcorv[1] = 0.;
+    for (int k = 2; k <= KX; ++k) {
+        tcorv[k - 1] = pow(fsg[k - 1], rgam);
+        if (k > 2) qcorv[k - 1] = pow(fsg[k - 1], qexp);
+    }
+}
+
+/* ludcmp / lubksb / inv (spe_matinv.f90), a(i, j) -> a[j][i] */
+static void orc_ludcmp(double a[KX][KX], int n, int *indx)
+{
+    double vv[KX];
+    for (int i = 0; i < n; ++i) {
+        double aamax = 0.;
+        for (int j = 0; j < n; ++j)
+            if (fabs(a[j][i]) > aamax) aamax = fabs(a[j][i]);
+        vv[i] = 1. / aamax;
+    }
+    for (int j = 0; j < n; ++j) {
+        for (int i = 1; i < j; ++i) {
+            double sum = a[j][i];
+            for (int k = 0; k < i; ++k) sum = sum - a[k][i] * a[j][k];
+            a[j][i] = sum;
+        }
+        double aamax = 0.;
+        int imax = j;
+        for (int i = j; i < n; ++i) {
+            double sum = a[j][i];
+            if (j > 0) {
+                for (int k = 0; k < j; ++k) sum = sum - a[k][i] * a[j][k];
+                a[j][i] = sum;
+            }
+            double dum = vv[i] * fabs(sum);
+            if (dum >= aamax) {
+                imax = i;
+                aamax = dum;
+            }
+        }
+        if (j != imax) {
+            for (int k = 0; k < n; ++k) {
+                double dum = a[k][imax];
+                a[k][imax] = a[k][j];
+                a[k][j] = dum;
+            }
+            vv[imax] = vv[j];
+        }
+        indx[j] = imax;
+        if (j != n - 1) {
+            double dum = 1. / a[j][j];
+            for (int i = j + 1; i < n; ++i) a[j][i] = a[j][i] * dum;
+        }
+    }
+}
+
+static void orc_lubksb(double a[KX][KX], int n, const int *indx, double *b)
+{
+    int ii = 0; /* 1-based as the reference, 0 = unset */
+    for (int i = 1; i <= n; ++i) {
+        int ll = indx[i - 1] + 1;
+        double sum = b[ll - 1];
+        b[ll - 1] = b[i - 1];
+        if (ii != 0) {
+            for (int j = ii; j <= i - 1; ++j) sum = sum - a[j - 1][i - 1] * b[j - 1];
+        } else if (sum != 0) {
+            ii = i;
+        }
+        b[i - 1] = sum;
+    }
+    for (int i = n; i >= 1; --i) {
+        double sum = b[i - 1];
+        for (int j = i + 1; j <= n; ++j) sum = sum - a[j - 1][i - 1] * b[j - 1];
+        b[i - 1] = sum / a[i - 1][i - 1];
+    }
+}
+
+/* impint(dt, alph) (ini_impint.f90:26-152) */
+void orc_dyn_impint(double dt, double alph)
+{
+    for (int n = 0; n < NX; ++n)
+        for (int m = 0; m < MX; ++m) {
+            dmp1[n][m] = 1. / (1. + dmp[n][m] * dt);
+            dmp1d[n][m] = 1. / (1. + dmpd[n][m] * dt);
+            dmp1s[n][m] = 1. / (1. + dmps[n][m] * dt);
+        }
+    double rgam = d_rgas * d_gamma / (1000. * d_grav);
+    for (int k = 0; k < KX; ++k) {
+        tref[k] = 288. * pow(fmax(0.2, fsg[k]), rgam);
+        tref1[k] = d_rgas * tref[k];
+        tref2[k] = d_akap * tref[k];
+        tref3[k] = fsgr[k] * tref[k];
+    }
+    double xi = dt * alph, xxi = xi / (d_rearth * d_rearth);
+    for (int k = 0; k < KX; ++k) dhsx[k] = xi * dhs[k];
+    for (int n = 1; n <= NX; ++n)
+        for (int m = 1; m <= MX; ++m) {
+            int ll = m + n - 2;
+            elz[n - 1][m - 1] = (double)ll * (double)(ll + 1) * xxi;
+        }
+    double xa[KX][KX], ya[KX][KX], xb[KX][KX], xe[KX][KX], dsum[KX];
+    memset(xa, 0, sizeof xa);
+    memset(xb, 0, sizeof xb);
+    for (int k = 0; k < KX; ++k)
+        for (int k1 = 0; k1 < KX; ++k1) ya[k1][k] = -d_akap * tref[k] * dhs[k1];
+    for (int k = 1; k < KX; ++k) xa[k - 1][k] = 0.5 * (d_akap * tref[k] / fsg[k] - (tref[k] - tref[k - 1]) / dhs[k]);
+    for (int k = 0; k < KX - 1; ++k) xa[k][k] = 0.5 * (d_akap * tref[k] / fsg[k] - (tref[k + 1] - tref[k]) / dhs[k]);
+    dsum[0] = dhs[0];
+    for (int k = 1; k < KX; ++k) dsum[k] = dsum[k - 1] + dhs[k];
+    for (int k = 0; k < KX - 1; ++k)
+        for (int k1 = 0; k1 < KX; ++k1) {
+            xb[k1][k] = dhs[k1] * dsum[k];
+            if (k1 <= k) xb[k1][k] = xb[k1][k] - dhs[k1];
+        }
+    for (int k = 0; k < KX; ++k)
+        for (int k1 = 0; k1 < KX; ++k1) {
+            xc_[k1][k] = ya[k1][k];
+            for (int k2 = 0; k2 < KX - 1; ++k2) xc_[k1][k] = xc_[k1][k] + xa[k2][k] * xb[k1][k2];
+        }
+    memset(xd_, 0, sizeof xd_);
+    for (int k = 0; k < KX; ++k)
+        for (int k1 = k + 1; k1 < KX; ++k1) xd_[k1][k] = d_rgas * log(hsg[k1 + 1] / hsg[k1]);
+    for (int k = 0; k < KX; ++k) xd_[k][k] = d_rgas * log(hsg[k + 1] / fsg[k]);
+    for (int k = 0; k < KX; ++k)
+        for (int k1 = 0; k1 < KX; ++k1) {
+            xe[k1][k] = 0.;
+            for (int k2 = 0; k2 < KX; ++k2) xe[k1][k] = xe[k1][k] + xd_[k2][k] * xc_[k1][k2];
+        }
+    for (int l = 1; l <= LMAX; ++l) {
+        double xxx = ((double)l * (double)(l + 1)) / (d_rearth * d_rearth);
+        double xf[KX][KX];
+        int indx[KX];
+        for (int k = 0; k < KX; ++k)
+            for (int k1 = 0; k1 < KX; ++k1) xf[k1][k] = xi * xi * xxx * (d_rgas * tref[k] * dhs[k1] - xe[k1][k]);
+        for (int k = 0; k < KX; ++k) xf[k][k] = xf[k][k] + 1.;
+        double(*y)[KX] = xj_[l - 1];
+        memset(y, 0, sizeof(double) * KX * KX);
+        for (int i = 0; i < KX; ++i) y[i][i] = 1.;
+        orc_ludcmp(xf, KX, indx);
+        for (int i = 0; i < KX; ++i) orc_lubksb(xf, KX, indx, y[i]);
+    }
+    for (int k = 0; k < KX; ++k)
+        for (int k1 = 0; k1 < KX; ++k1) xc_[k1][k] = xc_[k1][k] * xi;
+}
+
+#define SPX(a, lev, k) ((a) + ((size_t)(lev) * KX + (k)) * SF) /* field (.., k, lev) of a (mx,nx,kx,2) array */
+
+/* geop(jj) (dyn_geop.f90:16-32) */
+static void orc_geop(const double *t, const double *phis, int jj, double *phi)
+{
+    const double *tj = SPX(t, jj - 1, 0);
+    for (int c = 0; c < SF; ++c) phi[(KX - 1) * SF + c] = phis[c] + xgeop1[KX - 1] * tj[(KX - 1) * SF + c];
+    for (int k = KX - 2; k >= 0; --k)
+        for (int c = 0; c < SF; ++c)
+            phi[k * SF + c] = phi[(k + 1) * SF + c] + xgeop2[k + 1] * tj[(k + 1) * SF + c] + xgeop1[k] * tj[k * SF + c];
+    for (int k = 2; k <= KX - 1; ++k) {
+        double corf = xgeop1[k - 1] * 0.5 * log(hsg[k] / fsg[k - 1]) / log(fsg[k] / fsg[k - 2]);
+        for (int n = 0; n < NX; ++n)
+            for (int p = 0; p < 2; ++p)
+                phi[(k - 1) * SF + C3(p, 0, n)] =
+                    phi[(k - 1) * SF + C3(p, 0, n)] + corf * (tj[k * SF + C3(p, 0, n)] - tj[(k - 2) * SF + C3(p, 0, n)]);
+    }
+}
+
+/* grtend(vordt, divdt, tdt, psdt, trdt, 1, j2) (dyn_grtend.f90:61-278) */
+static void orc_grtend(const double *vor, const double *div, const double *t, const double *ps, const double *tr,
+                       const double *phys, int j2, double *vordt, double *divdt, double *tdt, double *psdt,
+                       double *trdt)
+{
+    static double ug[KX][GF], vg[KX][GF], tg[KX][GF], vorg[KX][GF], divg[KX][GF], tgg[KX][GF], puv[KX][GF];
+    static double trg[KX][GF], utend[KX][GF], vtend[KX][GF], ttend[KX][GF], trtend[KX][GF];
+    static double sigdt[KXP][GF], sigm[KXP][GF], temp[KXP][GF];
+    static double px[GF], py[GF], umean[GF], vmean[GF], dmean[GF], dumr[3][GF];
+    static double dumc[3][SF];
+    const int l2 = j2 - 1;
+    for (int k = 0; k < KX; ++k) {
+        orc_grid(SPX(vor, l2, k), vorg[k], 1);
+        orc_grid(SPX(div, l2, k), divg[k], 1);
+        orc_grid(SPX(t, l2, k), tg[k], 1);
+        orc_grid(SPX(tr, l2, k), trg[k], 1);
+        orc_uvspec(SPX(vor, l2, k), SPX(div, l2, k), dumc[0], dumc[1]);
+        orc_grid(dumc[1], vg[k], 2);
+        orc_grid(dumc[0], ug[k], 2);
+        for (int j = 0; j < IL; ++j)
+            for (int i = 0; i < IX; ++i) vorg[k][j * IX + i] = vorg[k][j * IX + i] + coriol[j];
+    }
+    for (int g = 0; g < GF; ++g) umean[g] = vmean[g] = dmean[g] = 0.0;
+    for (int k = 0; k < KX; ++k)
+        for (int g = 0; g < GF; ++g) {
+            umean[g] = umean[g] + ug[k][g] * dhs[k];
+            vmean[g] = vmean[g] + vg[k][g] * dhs[k];
+            dmean[g] = dmean[g] + divg[k][g] * dhs[k];
+        }
+    orc_grad(ps + (size_t)l2 * SF, dumc[1], dumc[2]);
+    orc_grid(dumc[1], px, 2);
+    orc_grid(dumc[2], py, 2);
+    for (int g = 0; g < GF; ++g) dumr[0][g] = -umean[g] * px[g] - vmean[g] * py[g];
+    orc_spec(dumr[0], psdt);
+    psdt[0] = psdt[1] = 0.0;
+    for (int g = 0; g < GF; ++g) sigdt[0][g] = sigdt[KX][g] = sigm[0][g] = sigm[KX][g] = 0.0;
+    for (int k = 0; k < KX; ++k)
+        for (int g = 0; g < GF; ++g) puv[k][g] = (ug[k][g] - umean[g]) * px[g] + (vg[k][g] - vmean[g]) * py[g];
+    for (int k = 0; k < KX; ++k)
+        for (int g = 0; g < GF; ++g) {
+            sigdt[k + 1][g] = sigdt[k][g] - dhs[k] * (puv[k][g] + divg[k][g] - dmean[g]);
+            sigm[k + 1][g] = sigm[k][g] - dhs[k] * puv[k][g];
+        }
+    for (int k = 0; k < KX; ++k)
+        for (int g = 0; g < GF; ++g) tgg[k][g] = tg[k][g] - tref[k];
+    for (int g = 0; g < GF; ++g) {
+        px[g] = d_rgas * px[g];
+        py[g] = d_rgas * py[g];
+    }
+    for (int g = 0; g < GF; ++g) temp[0][g] = temp[KX][g] = 0.0;
+    for (int k = 1; k < KX; ++k)
+        for (int g = 0; g < GF; ++g) temp[k][g] = sigdt[k][g] * (ug[k][g] - ug[k - 1][g]);
+    for (int k = 0; k < KX; ++k)
+        for (int g = 0; g < GF; ++g)
+            utend[k][g] = vg[k][g] * vorg[k][g] - tgg[k][g] * px[g] - (temp[k + 1][g] + temp[k][g]) * dhsr[k];
+    for (int k = 1; k < KX; ++k)
+        for (int g = 0; g < GF; ++g) temp[k][g] = sigdt[k][g] * (vg[k][g] - vg[k - 1][g]);
+    for (int k = 0; k < KX; ++k)
+        for (int g = 0; g < GF; ++g)
+            vtend[k][g] = -ug[k][g] * vorg[k][g] - tgg[k][g] * py[g] - (temp[k + 1][g] + temp[k][g]) * dhsr[k];
+    for (int k = 1; k < KX; ++k)
+        for (int g = 0; g < GF; ++g)
+            temp[k][g] = sigdt[k][g] * (tgg[k][g] - tgg[k - 1][g]) + sigm[k][g] * (tref[k] - tref[k - 1]);
+    for (int k = 0; k < KX; ++k)
+        for (int g = 0; g < GF; ++g)
+            ttend[k][g] = tgg[k][g] * divg[k][g] - (temp[k + 1][g] + temp[k][g]) * dhsr[k] +
+                          fsgr[k] * tgg[k][g] * (sigdt[k + 1][g] + sigdt[k][g]) +
+                          tref3[k] * (sigm[k + 1][g] + sigm[k][g]) + d_akap * (tg[k][g] * puv[k][g] - tgg[k][g] * dmean[g]);
+    for (int k = 1; k < KX; ++k)
+        for (int g = 0; g < GF; ++g) temp[k][g] = sigdt[k][g] * (trg[k][g] - trg[k - 1][g]);
+    for (int g = 0; g < GF; ++g) temp[1][g] = temp[2][g] = 0.;
+    for (int k = 0; k < KX; ++k)
+        for (int g = 0; g < GF; ++g) trtend[k][g] = trg[k][g] * divg[k][g] - (temp[k + 1][g] + temp[k][g]) * dhsr[k];
+    if (phys) /* phypar's additions (dyn_grtend.f90:223-226) */
+        for (int k = 0; k < KX; ++k)
+            for (int g = 0; g < GF; ++g) {
+                utend[k][g] = utend[k][g] + phys[(0 * KX + k) * GF + g];
+                vtend[k][g] = vtend[k][g] + phys[(1 * KX + k) * GF + g];
+                ttend[k][g] = ttend[k][g] + phys[(2 * KX + k) * GF + g];
+                trtend[k][g] = trtend[k][g] + phys[(3 * KX + k) * GF + g];
+            }
+    for (int k = 0; k < KX; ++k) {
+        orc_vdspec(utend[k], vtend[k], vordt + k * SF, divdt + k * SF, 2);
+        for (int g = 0; g < GF; ++g) {
+            dumr[0][g] = 0.5 * (ug[k][g] * ug[k][g] + vg[k][g] * vg[k][g]);
+            dumr[1][g] = -ug[k][g] * tgg[k][g];
+            dumr[2][g] = -vg[k][g] * tgg[k][g];
+        }
+        orc_spec(dumr[0], dumc[0]);
+        orc_lap(dumc[0], dumc[1]);
+        for (int c = 0; c < SF; ++c) divdt[k * SF + c] = divdt[k * SF + c] - dumc[1][c];
+        orc_vdspec(dumr[1], dumr[2], dumc[0], tdt + k * SF, 2);
+        orc_spec(ttend[k], dumc[1]);
+        for (int c = 0; c < SF; ++c) tdt[k * SF + c] = tdt[k * SF + c] + dumc[1][c];
+        for (int g = 0; g < GF; ++g) {
+            dumr[1][g] = -ug[k][g] * trg[k][g];
+            dumr[2][g] = -vg[k][g] * trg[k][g];
+        }
+        orc_spec(trtend[k], dumc[1]);
+        orc_vdspec(dumr[1], dumr[2], dumc[0], trdt + k * SF, 2);
+        for (int c = 0; c < SF; ++c) trdt[k * SF + c] = trdt[k * SF + c] + dumc[1][c];
+    }
+}
+
+/* sptend(divdt, tdt, psdt, j4) (dyn_sptend.f90:29-66); writes phi = geop(j4) */
+static void orc_sptend(const double *div, const double *t, const double *ps, const double *phis, int j4,
+                       double *divdt, double *tdt, double *psdt, double *phi)
+{
+    static double dmeanc[SF], sigdtc[KXP][SF], dumk[KXP][SF], dumc[2][SF];
+    for (int c = 0; c < SF; ++c) dmeanc[c] = 0.0;
+    for (int k = 0; k < KX; ++k)
+        for (int c = 0; c < SF; ++c) dmeanc[c] = dmeanc[c] + SPX(div, j4 - 1, k)[c] * dhs[k];
+    for (int c = 0; c < SF; ++c) psdt[c] = psdt[c] - dmeanc[c];
+    psdt[0] = psdt[1] = 0.0;
+    for (int c = 0; c < SF; ++c) sigdtc[0][c] = sigdtc[KX][c] = 0.0;
+    for (int k = 0; k < KX - 1; ++k)
+        for (int c = 0; c < SF; ++c) sigdtc[k + 1][c] = sigdtc[k][c] - dhs[k] * (SPX(div, j4 - 1, k)[c] - dmeanc[c]);
+    for (int c = 0; c < SF; ++c) dumk[0][c] = dumk[KX][c] = 0.0;
+    for (int k = 1; k < KX; ++k)
+        for (int c = 0; c < SF; ++c) dumk[k][c] = sigdtc[k][c] * (tref[k] - tref[k - 1]);
+    for (int k = 0; k < KX; ++k)
+        for (int c = 0; c < SF; ++c)
+            tdt[k * SF + c] = tdt[k * SF + c] - (dumk[k + 1][c] + dumk[k][c]) * dhsr[k] +
+                              tref3[k] * (sigdtc[k + 1][c] + sigdtc[k][c]) - tref2[k] * dmeanc[c];
+    orc_geop(t, phis, j4, phi);
+    for (int k = 0; k < KX; ++k) {
+        for (int c = 0; c < SF; ++c) dumc[0][c] = phi[k * SF + c] + d_rgas * tref[k] * ps[(size_t)(j4 - 1) * SF + c];
+        orc_lap(dumc[0], dumc[1]);
+        for (int c = 0; c < SF; ++c) divdt[k * SF + c] = divdt[k * SF + c] - dumc[1][c];
+    }
+}
+
+/* implic(divdt, tdt, psdt) (dyn_implic.f90:22-67) */
+static void orc_implic(double *divdt, double *tdt, double *psdt)
+{
+    static double ye[KX][SF], yf[KX][SF];
+    memset(ye, 0, sizeof ye);
+    for (int k1 = 0; k1 < KX; ++k1)
+        for (int k = 0; k < KX; ++k)
+            for (int c = 0; c < SF; ++c) ye[k][c] = ye[k][c] + xd_[k1][k] * tdt[k1 * SF + c];
+    for (int k = 0; k < KX; ++k)
+        for (int c = 0; c < SF; ++c) ye[k][c] = ye[k][c] + tref1[k] * psdt[c];
+    for (int k = 0; k < KX; ++k)
+        for (int n = 0; n < NX; ++n)
+            for (int m = 0; m < MX; ++m)
+                for (int p = 0; p < 2; ++p)
+                    yf[k][C3(p, m, n)] = divdt[k * SF + C3(p, m, n)] + elz[n][m] * ye[k][C3(p, m, n)];
+    memset(divdt, 0, sizeof(double) * KX * SF);
+    for (int n = 0; n < NX; ++n)
+        for (int m = 0; m < MX; ++m) {
+            int ll = m + n;
+            if (ll == 0) continue;
+            for (int k1 = 0; k1 < KX; ++k1)
+                for (int k = 0; k < KX; ++k)
+                    for (int p = 0; p < 2; ++p)
+                        divdt[k * SF + C3(p, m, n)] =
+                            divdt[k * SF + C3(p, m, n)] + xj_[ll - 1][k1][k] * yf[k1][C3(p, m, n)];
+        }
+    for (int k = 0; k < KX; ++k)
+        for (int c = 0; c < SF; ++c) psdt[c] = psdt[c] - divdt[k * SF + c] * dhsx[k];
+    for (int k = 0; k < KX; ++k)
+        for (int k1 = 0; k1 < KX; ++k1)
+            for (int c = 0; c < SF; ++c) tdt[k * SF + c] = tdt[k * SF + c] + xc_[k1][k] * divdt[k1 * SF + c];
+}
+
+/* hordif (dyn_step.f90:130-151) */
+static void orc_hordif(int nlev, const double *field, double *fdt, double dm[NX][MX], double dm1[NX][MX])
+{
+    for (int k = 0; k < nlev; ++k)
+        for (int n = 0; n < NX; ++n)
+            for (int m = 0; m < MX; ++m)
+                for (int p = 0; p < 2; ++p) {
+                    int c = k * SF + C3(p, m, n);
+                    fdt[c] = (fdt[c] - dm[n][m] * field[c]) * dm1[n][m];
+                }
+}
+
+/* timint (dyn_step.f90:153-190) */
+static void orc_timint(int j1, double dt, double eps, double wil, int nlev, double *field, double *fdt)
+{
+    for (int k = 0; k < nlev; ++k) orc_trunct(fdt + k * SF);
+    for (int k = 0; k < nlev; ++k)
+        for (int c = 0; c < SF; ++c) {
+            double *f1 = field + (size_t)k * SF + c, *f2 = field + ((size_t)nlev + k) * SF + c;
+            double *fj1 = (j1 == 1) ? f1 : f2;
+            double fnew = *f1 + dt * fdt[k * SF + c];
+            *f1 = *fj1 + wil * eps * (*f1 - 2 * *fj1 + fnew);
+            *f2 = fnew - (1 - wil) * eps * (*f1 - 2 * *fj1 + fnew);
+        }
+}
+
+/* step(j1, j2, dt, alph, rob, wil) (dyn_step.f90:1-128).  phys may be NULL.
+ * phi (KX spectral fields) receives geop(j4); tend (optional, 4*KX+1 fields:
+ * vordt|divdt|tdt|trdt|psdt) receives the final tendencies before timint. */
+void orc_dyn_step(double *vor, double *div, double *t, double *ps, double *tr, const double *phis, const double *tcorh,
+                  const double *qcorh, const double *phys, int j1, int j2, double dt, double alph, double rob,
+                  double wil, double *phi, double *tend)
+{
+    static double vordt[KX * SF], divdt[KX * SF], tdt[KX * SF], trdt[KX * SF], psdt[SF], ctmp[KX * SF];
+    static double phil[KX * SF];
+    orc_grtend(vor, div, t, ps, tr, phys, j2, vordt, divdt, tdt, psdt, trdt);
+    if (alph == 0.) {
+        orc_sptend(div, t, ps, phis, j2, divdt, tdt, psdt, phil);
+    } else {
+        orc_sptend(div, t, ps, phis, 1, divdt, tdt, psdt, phil);
+        orc_implic(divdt, tdt, psdt);
+    }
+    if (phi) memcpy(phi, phil, sizeof phil);
+    orc_hordif(KX, vor, vordt, dmp, dmp1);
+    orc_hordif(KX, div, divdt, dmpd, dmp1d);
+    for (int k = 0; k < KX; ++k)
+        for (int n = 0; n < NX; ++n)
+            for (int m = 0; m < MX; ++m)
+                for (int p = 0; p < 2; ++p)
+                    ctmp[k * SF + C3(p, m, n)] = t[k * SF + C3(p, m, n)] + tcorh[C3(p, m, n)] * tcorv[k];
+    orc_hordif(KX, ctmp, tdt, dmp, dmp1);
+    double sdrag = 1. / (d_tdrs * 3600.);
+    for (int n = 0; n < NX; ++n)
+        for (int p = 0; p < 2; ++p) {
+            vordt[C3(p, 0, n)] = vordt[C3(p, 0, n)] - sdrag * vor[C3(p, 0, n)];
+            divdt[C3(p, 0, n)] = divdt[C3(p, 0, n)] - sdrag * div[C3(p, 0, n)];
+        }
+    orc_hordif(1, vor, vordt, dmps, dmp1s);
+    orc_hordif(1, div, divdt, dmps, dmp1s);
+    orc_hordif(1, ctmp, tdt, dmps, dmp1s);
+    for (int k = 0; k < KX; ++k)
+        for (int n = 0; n < NX; ++n)
+            for (int m = 0; m < MX; ++m)
+                for (int p = 0; p < 2; ++p)
+                    ctmp[k * SF + C3(p, m, n)] = tr[k * SF + C3(p, m, n)] + qcorh[C3(p, m, n)] * qcorv[k];
+    orc_hordif(KX, ctmp, trdt, dmpd, dmp1d);
+    if (tend) {
+        memcpy(tend, vordt, sizeof vordt);
+        memcpy(tend + KX * SF, divdt, sizeof divdt);
+        memcpy(tend + 2 * KX * SF, tdt, sizeof tdt);
+        memcpy(tend + 3 * KX * SF, trdt, sizeof trdt);
+        memcpy(tend + 4 * KX * SF, psdt, sizeof psdt);
+    }
+    if (dt <= 0.) return;
+    double eps = (j1 == 1) ? 0. : rob;
+    orc_timint(j1, dt, eps, wil, 1, ps, psdt);
+    orc_timint(j1, dt, eps, wil, KX, vor, vordt);
+    orc_timint(j1, dt, eps, wil, KX, div, divdt);
+    orc_timint(j1, dt, eps, wil, KX, t, tdt);
+    orc_timint(j1, dt, eps, wil, KX, tr, trdt);
+}

@@ -1,0 +1,583 @@
+// sml_dynamics.hip -- one SPEEDY dynamics time step on gfx950.
+//
+// Reference: step (src/dyn_step.f90:1-128) =
+//   grtend  (src/dyn_grtend.f90:1-279): 50 inverse transforms of the j2 state,
+//           grid-point dynamics, physics hook (phypar, :225), 73 forward transforms
+//   sptend  (src/dyn_sptend.f90:1-67) + geop (src/dyn_geop.f90:1-33)
+//   implic  (src/dyn_implic.f90:1-68)         (alph != 0)
+//   hordif, stratospheric drag, tracer diffusion (dyn_step.f90:60-112, :130-151)
+//   timint with trunct, Robert-Williams filter  (dyn_step.f90:114-127, :153-190)
+//
+// MI355X design: the reference's ~164 one-field transforms per step become 7
+// batched MFMA transform launches (gridy on 50 fields, gridx kcos=1/2, specx
+// scaled/unscaled, specy on 73 fields); the grid-point dynamics is one kernel
+// with a thread per grid column (vertical recurrences in registers); everything
+// after the forward transforms (vds/lap assembly, sptend, geop, implic, hordif,
+// drag, timint) runs in two kernels with a thread per spectral coefficient (m, n)
+// that owns all levels, variables and both time levels of that coefficient, so no
+// stage needs a grid-wide synchronisation.  Physics (phypar) is out of scope on
+// the GPU: its grid-point tendencies enter through an optional input buffer at
+// the point where phypar adds them (after the dynamical tendencies, before the
+// spectral conversion), or are zero.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstring>
+#include <new>
+
+#include "sml_dynamics_tables.hpp"
+#include "sml_spectral_internal.hpp"
+
+using namespace sml;
+
+namespace {
+
+constexpr int kSF = kMX2 * kNX;       // 1984 doubles per spectral field
+constexpr int kGF = kIX * kIL;        // 4608 doubles per grid field
+constexpr int kVF = kMX2 * kIL;       // 2976 doubles per Fourier field
+constexpr int kNInv = 6 * kKX + 2;    // 50 inverse transforms per step
+constexpr int kNInv1 = 4 * kKX;       // the first 32 are kcos = 1
+constexpr int kNFwdScaled = 6 * kKX;  // 48 vdspec inputs (x 1/cos lat)
+constexpr int kNFwd = 9 * kKX + 1;    // 73 forward transforms per step
+constexpr int kMN = kMX * kNX;        // 992 complex coefficients
+
+// state buffer: vor(mx,nx,kx,2) | div | t | tr(ntr=1) | ps(mx,nx,2) (reference layouts)
+constexpr size_t kOffVor = 0, kOffDiv = 2 * kKX * kSF, kOffT = 4 * kKX * kSF, kOffTr = 6 * kKX * kSF,
+                 kOffPs = 8 * kKX * kSF, kStateSize = 8 * kKX * kSF + 2 * kSF;
+// tendency buffer: vordt | divdt | tdt | trdt (kx fields each) | psdt
+constexpr size_t kTVor = 0, kTDiv = kKX * kSF, kTT = 2 * kKX * kSF, kTTr = 3 * kKX * kSF, kTPs = 4 * kKX * kSF,
+                 kTendSize = 4 * kKX * kSF + kSF;
+
+__device__ inline int ci(int p, int m, int n) { return p + 2 * (m + kMX * n); }
+__device__ inline int mi(int m, int n) { return m + kMX * n; }
+
+}  // namespace
+
+struct sml_dynamics {
+    sml_spectral *sp = nullptr;
+    DynTables tab;
+    DynTables *d_tab = nullptr;
+    double *d_state = nullptr;
+    double *d_phis = nullptr, *d_tcorh = nullptr, *d_qcorh = nullptr, *d_phi = nullptr;
+    double *d_specin = nullptr, *d_varm = nullptr, *d_grid = nullptr, *d_gfwd = nullptr, *d_sfwd = nullptr;
+    double *d_tend = nullptr;
+    double *d_phys = nullptr;  // staging for host-provided physics tendencies
+    bool impint_done = false;
+};
+
+namespace {
+
+// ---------------------------------------------------------------- kernels
+// prep: inputs of the 50 inverse transforms, [vor 8 | div 8 | t 8 | tr 8 | ucos 8 |
+// vcos 8 | psdx | psdy], from time level j2 (grtend :60-99).  One thread per (m, n).
+__global__ void k_dyn_prep(const double *__restrict__ st, double *__restrict__ sin_, const DynTables *__restrict__ T,
+                           int j2) {
+    const int mn = blockIdx.x * blockDim.x + threadIdx.x;
+    if (mn >= kMN) return;
+    const int k = blockIdx.y;
+    const int m = mn % kMX, n = mn / kMX;
+    const size_t lev = (size_t)(j2 - 1) * kKX;
+    if (k < kKX) {
+        const double *vor = st + kOffVor + (lev + k) * kSF, *div = st + kOffDiv + (lev + k) * kSF;
+        const double *t = st + kOffT + (lev + k) * kSF, *tr = st + kOffTr + (lev + k) * kSF;
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            const int c = ci(p, m, n);
+            sin_[(size_t)k * kSF + c] = vor[c];
+            sin_[(size_t)(kKX + k) * kSF + c] = div[c];
+            sin_[(size_t)(2 * kKX + k) * kSF + c] = t[c];
+            sin_[(size_t)(3 * kKX + k) * kSF + c] = tr[c];
+        }
+        // uvspec(vor, div) -> (ucos, vcos)  (spe_spectral.f90:351-387)
+        const double ux = T->uvdx[n][m];
+        double zp[2], zc[2];
+        zp[1] = ux * vor[ci(0, m, n)];
+        zp[0] = -ux * vor[ci(1, m, n)];
+        zc[1] = ux * div[ci(0, m, n)];
+        zc[0] = -ux * div[ci(1, m, n)];
+        double *uc = sin_ + (size_t)(4 * kKX + k) * kSF, *vc = sin_ + (size_t)(5 * kKX + k) * kSF;
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            double a, b;
+            if (n == 0) {
+                a = zc[p] - T->uvdyp[0][m] * vor[ci(p, m, 1)];
+                b = zp[p] + T->uvdyp[0][m] * div[ci(p, m, 1)];
+            } else if (n == kNX - 1) {
+                a = T->uvdym[n][m] * vor[ci(p, m, kNTRUN1 - 1)];
+                b = -T->uvdym[n][m] * div[ci(p, m, kNTRUN1 - 1)];
+            } else {
+                b = -T->uvdym[n][m] * div[ci(p, m, n - 1)] + T->uvdyp[n][m] * div[ci(p, m, n + 1)] + zp[p];
+                a = T->uvdym[n][m] * vor[ci(p, m, n - 1)] - T->uvdyp[n][m] * vor[ci(p, m, n + 1)] + zc[p];
+            }
+            uc[ci(p, m, n)] = a;
+            vc[ci(p, m, n)] = b;
+        }
+    } else {
+        // grad(ps(j2)) -> (psdx, psdy)  (spe_spectral.f90:271-305)
+        const double *ps = st + kOffPs + (size_t)(j2 - 1) * kSF;
+        double *dx = sin_ + (size_t)(6 * kKX) * kSF, *dy = sin_ + (size_t)(6 * kKX + 1) * kSF;
+        dx[ci(1, m, n)] = T->gradx[m] * ps[ci(0, m, n)];
+        dx[ci(0, m, n)] = -T->gradx[m] * ps[ci(1, m, n)];
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            double v;
+            if (n == 0)
+                v = T->gradyp[0][m] * ps[ci(p, m, 1)];
+            else if (n == kNX - 1)
+                v = -T->gradym[n][m] * ps[ci(p, m, kNTRUN1 - 1)];
+            else
+                v = -T->gradym[n][m] * ps[ci(p, m, n - 1)] + T->gradyp[n][m] * ps[ci(p, m, n + 1)];
+            dy[ci(p, m, n)] = v;
+        }
+    }
+}
+
+// grid-point dynamics (grtend :60-217 and the products of :233-275), one thread
+// per grid column; G = the 50 inverse-transformed fields, P = optional physics
+// tendencies [u 8 | v 8 | t 8 | q 8] in grid space (phypar's additions, :225).
+// Output F = the 73 forward-transform inputs:
+//   [utend 8 | -u*tgg 8 | -u*trg 8 | vtend 8 | -v*tgg 8 | -v*trg 8]  (x 1/cos in specx)
+//   [0.5(u^2+v^2) 8 | ttend 8 | trtend 8 | -umean*px - vmean*py]
+__global__ __launch_bounds__(256) void k_dyn_gridpoint(const double *__restrict__ G, const double *__restrict__ P,
+                                                       double *__restrict__ F, const DynTables *__restrict__ T) {
+    const int pt = blockIdx.x * blockDim.x + threadIdx.x;
+    if (pt >= kGF) return;
+    const int j = pt / kIX;
+    auto g = [&](int f) { return G[(size_t)f * kGF + pt]; };
+    double ug[kKX], vg[kKX], vorg[kKX], divg[kKX], tg[kKX], trg[kKX];
+#pragma unroll
+    for (int k = 0; k < kKX; ++k) {
+        vorg[k] = g(k) + T->coriol[j];
+        divg[k] = g(kKX + k);
+        tg[k] = g(2 * kKX + k);
+        trg[k] = g(3 * kKX + k);
+        ug[k] = g(4 * kKX + k);
+        vg[k] = g(5 * kKX + k);
+    }
+    double px = g(6 * kKX), py = g(6 * kKX + 1);
+    double umean = 0.0, vmean = 0.0, dmean = 0.0;
+#pragma unroll
+    for (int k = 0; k < kKX; ++k) {
+        umean = umean + ug[k] * T->dhs[k];
+        vmean = vmean + vg[k] * T->dhs[k];
+        dmean = dmean + divg[k] * T->dhs[k];
+    }
+    F[(size_t)(kNFwd - 1) * kGF + pt] = -umean * px - vmean * py;  // psdt source (:95-97)
+    double puv[kKX], sigdt[kKXP], sigm[kKXP], tgg[kKX], temp[kKXP];
+#pragma unroll
+    for (int k = 0; k < kKX; ++k) puv[k] = (ug[k] - umean) * px + (vg[k] - vmean) * py;
+    sigdt[0] = 0.0;
+    sigm[0] = 0.0;
+#pragma unroll
+    for (int k = 0; k < kKX; ++k) {
+        sigdt[k + 1] = sigdt[k] - T->dhs[k] * (puv[k] + divg[k] - dmean);
+        sigm[k + 1] = sigm[k] - T->dhs[k] * puv[k];
+    }
+#pragma unroll
+    for (int k = 0; k < kKX; ++k) tgg[k] = tg[k] - T->tref[k];
+    px = kRgas * px;
+    py = kRgas * py;
+    const double *Pu = P, *Pv = P ? P + (size_t)kKX * kGF : nullptr, *Pt = P ? P + (size_t)2 * kKX * kGF : nullptr,
+                 *Pq = P ? P + (size_t)3 * kKX * kGF : nullptr;
+    // zonal wind tendency
+    temp[0] = 0.0;
+    temp[kKX] = 0.0;
+#pragma unroll
+    for (int k = 1; k < kKX; ++k) temp[k] = sigdt[k] * (ug[k] - ug[k - 1]);
+#pragma unroll
+    for (int k = 0; k < kKX; ++k) {
+        double u = vg[k] * vorg[k] - tgg[k] * px - (temp[k + 1] + temp[k]) * T->dhsr[k];
+        if (P) u = u + Pu[(size_t)k * kGF + pt];
+        F[(size_t)k * kGF + pt] = u;
+    }
+    // meridional wind tendency
+#pragma unroll
+    for (int k = 1; k < kKX; ++k) temp[k] = sigdt[k] * (vg[k] - vg[k - 1]);
+#pragma unroll
+    for (int k = 0; k < kKX; ++k) {
+        double v = -ug[k] * vorg[k] - tgg[k] * py - (temp[k + 1] + temp[k]) * T->dhsr[k];
+        if (P) v = v + Pv[(size_t)k * kGF + pt];
+        F[(size_t)(3 * kKX + k) * kGF + pt] = v;
+    }
+    // temperature tendency
+#pragma unroll
+    for (int k = 1; k < kKX; ++k)
+        temp[k] = sigdt[k] * (tgg[k] - tgg[k - 1]) + sigm[k] * (T->tref[k] - T->tref[k - 1]);
+#pragma unroll
+    for (int k = 0; k < kKX; ++k) {
+        double tt = tgg[k] * divg[k] - (temp[k + 1] + temp[k]) * T->dhsr[k] +
+                    T->fsgr[k] * tgg[k] * (sigdt[k + 1] + sigdt[k]) + T->tref3[k] * (sigm[k + 1] + sigm[k]) +
+                    kAkap * (tg[k] * puv[k] - tgg[k] * dmean);
+        if (P) tt = tt + Pt[(size_t)k * kGF + pt];
+        F[(size_t)(7 * kKX + k) * kGF + pt] = tt;
+    }
+    // tracer tendency: no vertical advection between the top three layers (:179-188)
+#pragma unroll
+    for (int k = 1; k < kKX; ++k) temp[k] = sigdt[k] * (trg[k] - trg[k - 1]);
+    temp[1] = 0.0;
+    temp[2] = 0.0;
+#pragma unroll
+    for (int k = 0; k < kKX; ++k) {
+        double q = trg[k] * divg[k] - (temp[k + 1] + temp[k]) * T->dhsr[k];
+        if (P) q = q + Pq[(size_t)k * kGF + pt];
+        F[(size_t)(8 * kKX + k) * kGF + pt] = q;
+    }
+    // products for the spectral conversion (:239-271)
+#pragma unroll
+    for (int k = 0; k < kKX; ++k) {
+        F[(size_t)(kKX + k) * kGF + pt] = -ug[k] * tgg[k];
+        F[(size_t)(4 * kKX + k) * kGF + pt] = -vg[k] * tgg[k];
+        F[(size_t)(2 * kKX + k) * kGF + pt] = -ug[k] * trg[k];
+        F[(size_t)(5 * kKX + k) * kGF + pt] = -vg[k] * trg[k];
+        F[(size_t)(6 * kKX + k) * kGF + pt] = 0.5 * (ug[k] * ug[k] + vg[k] * vg[k]);
+    }
+}
+
+// vds (spe_spectral.f90:307-349) divergence / vorticity of one coefficient
+__device__ inline void vds_at(const double *u, const double *v, const DynTables *T, int m, int n, int p, double *vor,
+                              double *div) {
+    const double gx = T->gradx[m];
+    // zp(2)=gradx*u(1), zp(1)=-gradx*u(2); zc likewise from v
+    const double zp = p == 1 ? gx * u[ci(0, m, n)] : -gx * u[ci(1, m, n)];
+    const double zc = p == 1 ? gx * v[ci(0, m, n)] : -gx * v[ci(1, m, n)];
+    if (n == 0) {
+        *vor = zc - T->vddyp[0][m] * u[ci(p, m, 1)];
+        *div = zp + T->vddyp[0][m] * v[ci(p, m, 1)];
+    } else if (n == kNX - 1) {
+        *vor = T->vddym[n][m] * u[ci(p, m, kNTRUN1 - 1)];
+        *div = -T->vddym[n][m] * v[ci(p, m, kNTRUN1 - 1)];
+    } else {
+        *vor = T->vddym[n][m] * u[ci(p, m, n - 1)] - T->vddyp[n][m] * u[ci(p, m, n + 1)] + zc;
+        *div = -T->vddym[n][m] * v[ci(p, m, n - 1)] + T->vddyp[n][m] * v[ci(p, m, n + 1)] + zp;
+    }
+}
+
+// combine: spectral tendencies of grtend (:229-278) from the 73 forward transforms
+__global__ void k_dyn_combine(const double *__restrict__ S, double *__restrict__ Td, const DynTables *__restrict__ T) {
+    const int mn = blockIdx.x * blockDim.x + threadIdx.x;
+    if (mn >= kMN) return;
+    const int k = blockIdx.y;
+    const int m = mn % kMX, n = mn / kMX;
+    auto fld = [&](int f) { return S + (size_t)f * kSF; };
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+        const int c = ci(p, m, n);
+        double vo, dv, d0, dq, dummy;
+        vds_at(fld(k), fld(3 * kKX + k), T, m, n, p, &vo, &dv);              // vdspec(utend, vtend)
+        const double lapv = -(fld(6 * kKX + k)[c] * T->el2[n][m]);          // lap(spec(0.5(u2+v2)))
+        Td[kTVor + (size_t)k * kSF + c] = vo;
+        Td[kTDiv + (size_t)k * kSF + c] = dv - lapv;
+        vds_at(fld(kKX + k), fld(4 * kKX + k), T, m, n, p, &dummy, &d0);     // vdspec(-u tgg, -v tgg)
+        Td[kTT + (size_t)k * kSF + c] = d0 + fld(7 * kKX + k)[c];
+        vds_at(fld(2 * kKX + k), fld(5 * kKX + k), T, m, n, p, &dummy, &dq); // vdspec(-u trg, -v trg)
+        Td[kTTr + (size_t)k * kSF + c] = dq + fld(8 * kKX + k)[c];
+        if (k == 0) Td[kTPs + c] = (m == 0 && n == 0) ? 0.0 : fld(kNFwd - 1)[c];  // psdt(1,1) = 0
+    }
+}
+
+// tail: sptend + geop + implic + hordif + drag + timint, one thread per (m, n, part)
+__global__ void k_dyn_tail(double *__restrict__ st, double *__restrict__ Td, double *__restrict__ phi_out,
+                           const double *__restrict__ phis, const double *__restrict__ tcorh,
+                           const double *__restrict__ qcorh, const DynTables *__restrict__ T, int j1, int j4,
+                           double dt, double alph, double rob, double wil) {
+    const int mnp = blockIdx.x * blockDim.x + threadIdx.x;
+    if (mnp >= 2 * kMN) return;
+    const int p = mnp & 1, mn = mnp >> 1;
+    const int m = mn % kMX, n = mn / kMX;
+    const int c = ci(p, m, n);
+    auto S = [&](size_t off, int lev, int k) -> double & { return st[off + ((size_t)(lev - 1) * kKX + k) * kSF + c]; };
+    double vordt[kKX], divdt[kKX], tdt[kKX], trdt[kKX], psdt;
+#pragma unroll
+    for (int k = 0; k < kKX; ++k) {
+        vordt[k] = Td[kTVor + (size_t)k * kSF + c];
+        divdt[k] = Td[kTDiv + (size_t)k * kSF + c];
+        tdt[k] = Td[kTT + (size_t)k * kSF + c];
+        trdt[k] = Td[kTTr + (size_t)k * kSF + c];
+    }
+    psdt = Td[kTPs + c];
+    // ---- sptend(divdt, tdt, psdt, j4)  (dyn_sptend.f90:24-66)
+    double dmeanc = 0.0;
+#pragma unroll
+    for (int k = 0; k < kKX; ++k) dmeanc = dmeanc + S(kOffDiv, j4, k) * T->dhs[k];
+    psdt = psdt - dmeanc;
+    if (m == 0 && n == 0) psdt = 0.0;
+    double sigdtc[kKXP], dumk[kKXP];
+    sigdtc[0] = 0.0;
+    sigdtc[kKX] = 0.0;
+#pragma unroll
+    for (int k = 0; k < kKX - 1; ++k) sigdtc[k + 1] = sigdtc[k] - T->dhs[k] * (S(kOffDiv, j4, k) - dmeanc);
+    dumk[0] = 0.0;
+    dumk[kKX] = 0.0;
+#pragma unroll
+    for (int k = 1; k < kKX; ++k) dumk[k] = sigdtc[k] * (T->tref[k] - T->tref[k - 1]);
+#pragma unroll
+    for (int k = 0; k < kKX; ++k)
+        tdt[k] = tdt[k] - (dumk[k + 1] + dumk[k]) * T->dhsr[k] + T->tref3[k] * (sigdtc[k + 1] + sigdtc[k]) -
+                 T->tref2[k] * dmeanc;
+    // geop(j4)  (dyn_geop.f90:16-32)
+    double phi[kKX];
+    phi[kKX - 1] = phis[c] + T->xgeop1[kKX - 1] * S(kOffT, j4, kKX - 1);
+#pragma unroll
+    for (int k = kKX - 2; k >= 0; --k)
+        phi[k] = phi[k + 1] + T->xgeop2[k + 1] * S(kOffT, j4, k + 1) + T->xgeop1[k] * S(kOffT, j4, k);
+    if (m == 0) {
+#pragma unroll
+        for (int k = 1; k < kKX - 1; ++k) phi[k] = phi[k] + T->corf[k] * (S(kOffT, j4, k + 1) - S(kOffT, j4, k - 1));
+    }
+    const double psj4 = S(kOffPs, j4, 0);
+#pragma unroll
+    for (int k = 0; k < kKX; ++k) {
+        phi_out[(size_t)k * kSF + c] = phi[k];
+        const double d1 = phi[k] + kRgas * T->tref[k] * psj4;
+        const double lapd = -(d1 * T->el2[n][m]);
+        divdt[k] = divdt[k] - lapd;
+    }
+    // ---- implic(divdt, tdt, psdt)  (dyn_implic.f90:22-67)
+    if (alph != 0.0) {
+        double ye[kKX], yf[kKX];
+#pragma unroll
+        for (int k = 0; k < kKX; ++k) ye[k] = 0.0;
+#pragma unroll
+        for (int k1 = 0; k1 < kKX; ++k1)
+#pragma unroll
+            for (int k = 0; k < kKX; ++k) ye[k] = ye[k] + T->xd[k1][k] * tdt[k1];
+#pragma unroll
+        for (int k = 0; k < kKX; ++k) ye[k] = ye[k] + T->tref1[k] * psdt;
+#pragma unroll
+        for (int k = 0; k < kKX; ++k) yf[k] = divdt[k] + T->elz[n][m] * ye[k];
+#pragma unroll
+        for (int k = 0; k < kKX; ++k) divdt[k] = 0.0;
+        const int ll = m + n;
+        if (ll != 0) {
+            const double(*xj)[kKX] = T->xj[ll - 1];
+#pragma unroll
+            for (int k1 = 0; k1 < kKX; ++k1)
+#pragma unroll
+                for (int k = 0; k < kKX; ++k) divdt[k] = divdt[k] + xj[k1][k] * yf[k1];
+        }
+#pragma unroll
+        for (int k = 0; k < kKX; ++k) psdt = psdt - divdt[k] * T->dhsx[k];
+#pragma unroll
+        for (int k = 0; k < kKX; ++k)
+#pragma unroll
+            for (int k1 = 0; k1 < kKX; ++k1) tdt[k] = tdt[k] + T->xc[k1][k] * divdt[k1];
+    }
+    // ---- horizontal diffusion (dyn_step.f90:60-112, hordif :130-151)
+    const double dmp = T->dmp[n][m], dmp1 = T->dmp1[n][m], dmpd = T->dmpd[n][m], dmp1d = T->dmp1d[n][m];
+    const double dmps = T->dmps[n][m], dmp1s = T->dmp1s[n][m];
+    double ctmp[kKX];
+#pragma unroll
+    for (int k = 0; k < kKX; ++k) {
+        vordt[k] = (vordt[k] - dmp * S(kOffVor, 1, k)) * dmp1;
+        divdt[k] = (divdt[k] - dmpd * S(kOffDiv, 1, k)) * dmp1d;
+        ctmp[k] = S(kOffT, 1, k) + tcorh[c] * T->tcorv[k];
+        tdt[k] = (tdt[k] - dmp * ctmp[k]) * dmp1;
+    }
+    if (m == 0) {  // stratospheric drag on the zonal mean, top level (:84-88)
+        const double sdrag = 1. / (kTdrs * 3600.);
+        vordt[0] = vordt[0] - sdrag * S(kOffVor, 1, 0);
+        divdt[0] = divdt[0] - sdrag * S(kOffDiv, 1, 0);
+    }
+    vordt[0] = (vordt[0] - dmps * S(kOffVor, 1, 0)) * dmp1s;
+    divdt[0] = (divdt[0] - dmps * S(kOffDiv, 1, 0)) * dmp1s;
+    tdt[0] = (tdt[0] - dmps * ctmp[0]) * dmp1s;
+#pragma unroll
+    for (int k = 0; k < kKX; ++k) {
+        const double cq = S(kOffTr, 1, k) + qcorh[c] * T->qcorv[k];
+        trdt[k] = (trdt[k] - dmpd * cq) * dmp1d;
+    }
+    if (dt <= 0.0) {  // tendencies only (dyn_step.f90:114)
+#pragma unroll
+        for (int k = 0; k < kKX; ++k) {
+            Td[kTVor + (size_t)k * kSF + c] = vordt[k];
+            Td[kTDiv + (size_t)k * kSF + c] = divdt[k];
+            Td[kTT + (size_t)k * kSF + c] = tdt[k];
+            Td[kTTr + (size_t)k * kSF + c] = trdt[k];
+        }
+        Td[kTPs + c] = psdt;
+        return;
+    }
+    // ---- timint with the Robert-Williams filter (dyn_step.f90:153-190)
+    const double eps = (j1 == 1) ? 0.0 : rob;
+    const double trf = T->trfilt[n][m];
+    auto timint = [&](size_t off, int k, double fdt) {
+        fdt = fdt * trf;  // trunct
+        double &f1 = S(off, 1, k);
+        double &f2 = S(off, 2, k);
+        const double fj1_old = (j1 == 1) ? f1 : f2;
+        const double fnew = f1 + dt * fdt;
+        const double f1new = fj1_old + wil * eps * (f1 - 2 * fj1_old + fnew);
+        const double fj1_new = (j1 == 1) ? f1new : fj1_old;
+        f2 = fnew - (1 - wil) * eps * (f1new - 2 * fj1_new + fnew);
+        f1 = f1new;
+    };
+    timint(kOffPs, 0, psdt);
+#pragma unroll
+    for (int k = 0; k < kKX; ++k) timint(kOffVor, k, vordt[k]);
+#pragma unroll
+    for (int k = 0; k < kKX; ++k) timint(kOffDiv, k, divdt[k]);
+#pragma unroll
+    for (int k = 0; k < kKX; ++k) timint(kOffT, k, tdt[k]);
+#pragma unroll
+    for (int k = 0; k < kKX; ++k) timint(kOffTr, k, trdt[k]);
+}
+
+template <typename T>
+int dalloc(T **p, size_t count) {
+    *p = nullptr;
+    SML_HIP(hipMalloc((void **)p, count * sizeof(T)));
+    SML_HIP(hipMemset(*p, 0, count * sizeof(T)));
+    return SML_OK;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------ API
+extern "C" int sml_dyn_destroy(sml_dynamics *d) {
+    if (!d) return SML_OK;
+    void *ptrs[] = {d->d_tab, d->d_state, d->d_phis, d->d_tcorh, d->d_qcorh, d->d_phi, d->d_specin,
+                    d->d_varm, d->d_grid, d->d_gfwd, d->d_sfwd, d->d_tend, d->d_phys};
+    for (void *p : ptrs)
+        if (p) (void)hipFree(p);
+    if (d->sp) sml_spectral_destroy(d->sp);
+    delete d;
+    return SML_OK;
+}
+
+extern "C" int sml_dyn_create(double radius, sml_dynamics **out) {
+    SML_REQUIRE(out, "out is null");
+    *out = nullptr;
+    sml_dynamics *d = new (std::nothrow) sml_dynamics();
+    if (!d) return fail(SML_ERR_NOMEM, "host allocation failed");
+    int rc = sml_spectral_create(radius, &d->sp);
+    if (rc) {
+        delete d;
+        return rc;
+    }
+    build_dyn_indyns(spectral_host_tables(d->sp), &d->tab);
+    if ((rc = dalloc(&d->d_tab, 1)) || (rc = dalloc(&d->d_state, kStateSize)) || (rc = dalloc(&d->d_phis, kSF)) ||
+        (rc = dalloc(&d->d_tcorh, kSF)) || (rc = dalloc(&d->d_qcorh, kSF)) || (rc = dalloc(&d->d_phi, kKX * kSF)) ||
+        (rc = dalloc(&d->d_specin, (size_t)kNInv * kSF)) || (rc = dalloc(&d->d_varm, (size_t)kNFwd * kVF)) ||
+        (rc = dalloc(&d->d_grid, (size_t)kNInv * kGF)) || (rc = dalloc(&d->d_gfwd, (size_t)kNFwd * kGF)) ||
+        (rc = dalloc(&d->d_sfwd, (size_t)kNFwd * kSF)) || (rc = dalloc(&d->d_tend, kTendSize)) ||
+        (rc = dalloc(&d->d_phys, (size_t)4 * kKX * kGF))) {
+        sml_dyn_destroy(d);
+        return rc;
+    }
+    hipError_t e = hipMemcpy(d->d_tab, &d->tab, sizeof(DynTables), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        sml_dyn_destroy(d);
+        return fail(SML_ERR_HIP, "sml_dyn_create: %s", hipGetErrorString(e));
+    }
+    *out = d;
+    return SML_OK;
+}
+
+extern "C" int sml_dyn_impint(sml_dynamics *d, double dt, double alph) {
+    SML_REQUIRE(d, "null context");
+    build_dyn_impint(dt, alph, &d->tab);
+    SML_HIP(hipMemcpy(d->d_tab, &d->tab, sizeof(DynTables), hipMemcpyHostToDevice));
+    d->impint_done = true;
+    return SML_OK;
+}
+
+extern "C" int sml_dyn_set_forcing(sml_dynamics *d, const double *phis, const double *tcorh, const double *qcorh) {
+    SML_REQUIRE(d, "null context");
+    if (phis) SML_HIP(hipMemcpy(d->d_phis, phis, kSF * 8, hipMemcpyHostToDevice));
+    if (tcorh) SML_HIP(hipMemcpy(d->d_tcorh, tcorh, kSF * 8, hipMemcpyHostToDevice));
+    if (qcorh) SML_HIP(hipMemcpy(d->d_qcorh, qcorh, kSF * 8, hipMemcpyHostToDevice));
+    return SML_OK;
+}
+
+extern "C" int sml_dyn_set_state(sml_dynamics *d, const double *vor, const double *div, const double *t,
+                                 const double *ps, const double *tr) {
+    SML_REQUIRE(d && vor && div && t && ps && tr, "null argument");
+    const size_t f3 = 2 * kKX * kSF * 8;
+    SML_HIP(hipMemcpy(d->d_state + kOffVor, vor, f3, hipMemcpyHostToDevice));
+    SML_HIP(hipMemcpy(d->d_state + kOffDiv, div, f3, hipMemcpyHostToDevice));
+    SML_HIP(hipMemcpy(d->d_state + kOffT, t, f3, hipMemcpyHostToDevice));
+    SML_HIP(hipMemcpy(d->d_state + kOffTr, tr, f3, hipMemcpyHostToDevice));
+    SML_HIP(hipMemcpy(d->d_state + kOffPs, ps, 2 * kSF * 8, hipMemcpyHostToDevice));
+    return SML_OK;
+}
+
+extern "C" int sml_dyn_get_state(sml_dynamics *d, double *vor, double *div, double *t, double *ps, double *tr) {
+    SML_REQUIRE(d, "null context");
+    SML_HIP(hipDeviceSynchronize());
+    const size_t f3 = 2 * kKX * kSF * 8;
+    if (vor) SML_HIP(hipMemcpy(vor, d->d_state + kOffVor, f3, hipMemcpyDeviceToHost));
+    if (div) SML_HIP(hipMemcpy(div, d->d_state + kOffDiv, f3, hipMemcpyDeviceToHost));
+    if (t) SML_HIP(hipMemcpy(t, d->d_state + kOffT, f3, hipMemcpyDeviceToHost));
+    if (tr) SML_HIP(hipMemcpy(tr, d->d_state + kOffTr, f3, hipMemcpyDeviceToHost));
+    if (ps) SML_HIP(hipMemcpy(ps, d->d_state + kOffPs, 2 * kSF * 8, hipMemcpyDeviceToHost));
+    return SML_OK;
+}
+
+extern "C" int sml_dyn_get_phi(sml_dynamics *d, double *phi) {
+    SML_REQUIRE(d && phi, "null argument");
+    SML_HIP(hipDeviceSynchronize());
+    SML_HIP(hipMemcpy(phi, d->d_phi, kKX * kSF * 8, hipMemcpyDeviceToHost));
+    return SML_OK;
+}
+
+extern "C" int sml_dyn_get_tendencies(sml_dynamics *d, double *tend) {
+    SML_REQUIRE(d && tend, "null argument");
+    SML_HIP(hipDeviceSynchronize());
+    SML_HIP(hipMemcpy(tend, d->d_tend, kTendSize * 8, hipMemcpyDeviceToHost));
+    return SML_OK;
+}
+
+extern "C" int sml_dyn_state_device(sml_dynamics *d, double **d_state, double **d_phys) {
+    SML_REQUIRE(d, "null context");
+    if (d_state) *d_state = d->d_state;
+    if (d_phys) *d_phys = d->d_phys;
+    return SML_OK;
+}
+
+extern "C" int sml_dyn_step(sml_dynamics *d, int j1, int j2, double dt, double alph, double rob, double wil,
+                            const double *d_phys, void *stream) {
+    SML_REQUIRE(d, "null context");
+    SML_REQUIRE((j1 == 1 || j1 == 2) && (j2 == 1 || j2 == 2), "j1/j2 must be 1 or 2");
+    if (!d->impint_done) return fail(SML_ERR_STATE, "sml_dyn_impint must be called before sml_dyn_step");
+    hipStream_t st = (hipStream_t)stream;
+    const DynTables *T = d->d_tab;
+    // 1. grtend: inverse transforms of the j2 state
+    hipLaunchKernelGGL(k_dyn_prep, dim3((kMN + 127) / 128, kKX + 1), dim3(128), 0, st, d->d_state, d->d_specin, T,
+                       j2);
+    SML_HIP(hipGetLastError());
+    if (int rc = spectral_gridy(d->sp, d->d_specin, d->d_varm, kNInv, st)) return rc;
+    if (int rc = spectral_gridx(d->sp, d->d_varm, d->d_grid, kNInv1, 1, st)) return rc;
+    if (int rc = spectral_gridx(d->sp, d->d_varm + (size_t)kNInv1 * kVF, d->d_grid + (size_t)kNInv1 * kGF,
+                                kNInv - kNInv1, 2, st))
+        return rc;
+    // 2. grid-point dynamics (+ physics tendencies)
+    hipLaunchKernelGGL(k_dyn_gridpoint, dim3((kGF + 255) / 256), dim3(256), 0, st, d->d_grid, d_phys, d->d_gfwd, T);
+    SML_HIP(hipGetLastError());
+    // 3. forward transforms: vdspec inputs x 1/cos (kcos = 2), the rest plain
+    if (int rc = spectral_specx(d->sp, d->d_gfwd, d->d_varm, kNFwdScaled, 1, st)) return rc;
+    if (int rc = spectral_specx(d->sp, d->d_gfwd + (size_t)kNFwdScaled * kGF, d->d_varm + (size_t)kNFwdScaled * kVF,
+                                kNFwd - kNFwdScaled, 0, st))
+        return rc;
+    if (int rc = spectral_specy(d->sp, d->d_varm, d->d_sfwd, kNFwd, st)) return rc;
+    hipLaunchKernelGGL(k_dyn_combine, dim3((kMN + 127) / 128, kKX), dim3(128), 0, st, d->d_sfwd, d->d_tend, T);
+    SML_HIP(hipGetLastError());
+    // 4. sptend / implic / diffusion / time integration
+    const int j4 = (alph == 0.0) ? j2 : 1;
+    hipLaunchKernelGGL(k_dyn_tail, dim3((2 * kMN + 127) / 128), dim3(128), 0, st, d->d_state, d->d_tend, d->d_phi,
+                       d->d_phis, d->d_tcorh, d->d_qcorh, T, j1, j4, dt, alph, rob, wil);
+    SML_HIP(hipGetLastError());
+    return SML_OK;
+}
+
+extern "C" int sml_dyn_step_host(sml_dynamics *d, int j1, int j2, double dt, double alph, double rob, double wil,
+                                 const double *phys) {
+    SML_REQUIRE(d, "null context");
+    const double *dp = nullptr;
+    if (phys) {
+        SML_HIP(hipMemcpy(d->d_phys, phys, (size_t)4 * kKX * kGF * 8, hipMemcpyHostToDevice));
+        dp = d->d_phys;
+    }
+    if (int rc = sml_dyn_step(d, j1, j2, dt, alph, rob, wil, dp, nullptr)) return rc;
+    SML_HIP(hipDeviceSynchronize());
+    return SML_OK;
+}

@@ -1,0 +1,216 @@
+// sml_dynamics_tables.cpp -- restatement of SPEEDY's dynamics initialisation:
+//   indyns  (src/ini_indyns.f90:1-128): sigma levels, Coriolis, hydrostatic and
+//           horizontal-diffusion coefficients
+//   impint  (src/ini_impint.f90:1-153): semi-implicit gravity-wave matrices for a
+//           given (dt, alph), using ludcmp/lubksb/inv (src/spe_matinv.f90)
+// Computed on the host once per (dt, alph) and uploaded by sml_dynamics.hip.
+#include "sml_dynamics_tables.hpp"
+
+#include <cmath>
+#include <cstring>
+
+namespace sml {
+
+void build_dyn_indyns(const SpectralTables &sp, DynTables *d) {
+    std::memset(d, 0, sizeof *d);
+    const double hsg[kKXP] = {0.000, 0.050, 0.140, 0.260, 0.420, 0.600, 0.770, 0.900, 1.000};
+    std::memcpy(d->hsg, hsg, sizeof hsg);
+    for (int k = 0; k < kKX; ++k) {
+        d->dhs[k] = d->hsg[k + 1] - d->hsg[k];
+        d->fsg[k] = 0.5 * (d->hsg[k + 1] + d->hsg[k]);
+    }
+    for (int k = 0; k < kKX; ++k) {
+        d->dhsr[k] = 0.5 / d->dhs[k];
+        d->fsgr[k] = kAkap / (2. * d->fsg[k]);
+    }
+    for (int j = 0; j < kIY; ++j) {
+        const int jj = kIL - 1 - j;
+        const double rad1 = std::asin(sp.sia[j]);
+        d->radang[j] = -rad1;
+        d->radang[jj] = rad1;
+        d->gsin[j] = -sp.sia[j];
+        d->gsin[jj] = sp.sia[j];
+    }
+    for (int j = 0; j < kIL; ++j) d->coriol[j] = 2. * kOmega * d->gsin[j];
+    for (int k = 0; k < kKX; ++k) {
+        d->xgeop1[k] = kRgas * std::log(d->hsg[k + 1] / d->fsg[k]);
+        if (k != kKX - 1) d->xgeop2[k + 1] = kRgas * std::log(d->fsg[k + 1] / d->hsg[k + 1]);
+    }
+    const double hdiff = 1. / (kThd * 3600.), hdifd = 1. / (kThdd * 3600.), hdifs = 1. / (kThds * 3600.);
+    const double rlap = 1. / (double)(kNTRUN * (kNTRUN + 1));
+    for (int n = 0; n < kNX; ++n)
+        for (int m = 0; m < kMX; ++m) {
+            const double twn = (double)(m + n);
+            const double elap = (twn * (twn + 1.) * rlap);
+            const double e2 = elap * elap, elapn = e2 * e2;  // elap**npowhd, npowhd = 4
+            d->dmp[n][m] = hdiff * elapn;
+            d->dmpd[n][m] = hdifd * elapn;
+            d->dmps[n][m] = hdifs * elap;
+        }
+    const double rgam = kRgas * kGamma / (1000. * kGrav), qexp = kHscale / kHshum;
+    d->tcorv[0] = d->qcorv[0] = d->qcorv[1] = 0.;
+    for (int k = 1; k < kKX; ++k) {
+        d->tcorv[k] = std::pow(d->fsg[k], rgam);
+        if (k > 1) d->qcorv[k] = std::pow(d->fsg[k], qexp);
+    }
+    for (int k = 1; k < kKX - 1; ++k)
+        d->corf[k] = d->xgeop1[k] * 0.5 * std::log(d->hsg[k + 1] / d->fsg[k]) /
+                     std::log(d->fsg[k + 1] / d->fsg[k - 1]);
+    std::memcpy(d->gradx, sp.gradx, sizeof d->gradx);
+    std::memcpy(d->gradym, sp.gradym, sizeof d->gradym);
+    std::memcpy(d->gradyp, sp.gradyp, sizeof d->gradyp);
+    std::memcpy(d->uvdx, sp.uvdx, sizeof d->uvdx);
+    std::memcpy(d->uvdym, sp.uvdym, sizeof d->uvdym);
+    std::memcpy(d->uvdyp, sp.uvdyp, sizeof d->uvdyp);
+    std::memcpy(d->vddym, sp.vddym, sizeof d->vddym);
+    std::memcpy(d->vddyp, sp.vddyp, sizeof d->vddyp);
+    std::memcpy(d->el2, sp.el2, sizeof d->el2);
+    for (int n = 0; n < kNX; ++n)
+        for (int m = 0; m < kMX; ++m) d->trfilt[n][m] = (m + n <= kNTRUN) ? 1.0 : 0.0;
+}
+
+// ludcmp / lubksb / inv (src/spe_matinv.f90), on a column-major n x n matrix a(i, j)
+// stored [j][i].  `tiny` is declared integer in the reference, so it is 0.
+static void ludcmp(double a[kKX][kKX], int n, int *indx) {
+    double vv[kKX];
+    for (int i = 0; i < n; ++i) {
+        double aamax = 0.;
+        for (int j = 0; j < n; ++j)
+            if (std::fabs(a[j][i]) > aamax) aamax = std::fabs(a[j][i]);
+        vv[i] = 1. / aamax;
+    }
+    for (int j = 0; j < n; ++j) {
+        for (int i = 0; i < j; ++i) {
+            double sum = a[j][i];
+            if (i > 0) {
+                for (int k = 0; k < i; ++k) sum = sum - a[k][i] * a[j][k];
+                a[j][i] = sum;
+            }
+        }
+        double aamax = 0.;
+        int imax = j;
+        for (int i = j; i < n; ++i) {
+            double sum = a[j][i];
+            if (j > 0) {
+                for (int k = 0; k < j; ++k) sum = sum - a[k][i] * a[j][k];
+                a[j][i] = sum;
+            }
+            const double dum = vv[i] * std::fabs(sum);
+            if (dum >= aamax) {
+                imax = i;
+                aamax = dum;
+            }
+        }
+        if (j != imax) {
+            for (int k = 0; k < n; ++k) {
+                const double dum = a[k][imax];
+                a[k][imax] = a[k][j];
+                a[k][j] = dum;
+            }
+            vv[imax] = vv[j];
+        }
+        indx[j] = imax;
+        if (j != n - 1) {
+            if (a[j][j] == 0.) a[j][j] = 0.;
+            const double dum = 1. / a[j][j];
+            for (int i = j + 1; i < n; ++i) a[j][i] = a[j][i] * dum;
+        }
+    }
+}
+
+static void lubksb(double a[kKX][kKX], int n, const int *indx, double *b) {
+    int ii = -1;
+    for (int i = 0; i < n; ++i) {
+        const int ll = indx[i];
+        double sum = b[ll];
+        b[ll] = b[i];
+        if (ii >= 0) {
+            for (int j = ii; j < i; ++j) sum = sum - a[j][i] * b[j];
+        } else if (sum != 0.) {
+            ii = i;
+        }
+        b[i] = sum;
+    }
+    for (int i = n - 1; i >= 0; --i) {
+        double sum = b[i];
+        for (int j = i + 1; j < n; ++j) sum = sum - a[j][i] * b[j];
+        b[i] = sum / a[i][i];
+    }
+}
+
+static void inv(double a[kKX][kKX], double y[kKX][kKX], int n) {
+    int indx[kKX];
+    std::memset(y, 0, sizeof(double) * kKX * kKX);
+    for (int i = 0; i < n; ++i) y[i][i] = 1.;
+    ludcmp(a, n, indx);
+    for (int i = 0; i < n; ++i) lubksb(a, n, indx, y[i]);
+}
+
+void build_dyn_impint(double dt, double alph, DynTables *d) {
+    d->dt = dt;
+    d->alph = alph;
+    for (int n = 0; n < kNX; ++n)
+        for (int m = 0; m < kMX; ++m) {
+            d->dmp1[n][m] = 1. / (1. + d->dmp[n][m] * dt);
+            d->dmp1d[n][m] = 1. / (1. + d->dmpd[n][m] * dt);
+            d->dmp1s[n][m] = 1. / (1. + d->dmps[n][m] * dt);
+        }
+    const double rgam = kRgas * kGamma / (1000. * kGrav);
+    for (int k = 0; k < kKX; ++k) {
+        d->tref[k] = 288. * std::pow(std::fmax(0.2, d->fsg[k]), rgam);
+        d->tref1[k] = kRgas * d->tref[k];
+        d->tref2[k] = kAkap * d->tref[k];
+        d->tref3[k] = d->fsgr[k] * d->tref[k];
+    }
+    const double xi = dt * alph, xxi = xi / (kRearth * kRearth);
+    for (int k = 0; k < kKX; ++k) d->dhsx[k] = xi * d->dhs[k];
+    for (int n = 0; n < kNX; ++n)
+        for (int m = 0; m < kMX; ++m) {
+            const int ll = m + n;
+            d->elz[n][m] = (double)ll * (double)(ll + 1) * xxi;
+        }
+    // [col][row] storage of the reference's column-major (row, col) matrices
+    double xa[kKX][kKX] = {}, ya[kKX][kKX], xb[kKX][kKX] = {}, xe[kKX][kKX], dsum[kKX];
+    for (int k = 0; k < kKX; ++k)
+        for (int k1 = 0; k1 < kKX; ++k1) ya[k1][k] = -kAkap * d->tref[k] * d->dhs[k1];
+    for (int k = 1; k < kKX; ++k)
+        xa[k - 1][k] = 0.5 * (kAkap * d->tref[k] / d->fsg[k] - (d->tref[k] - d->tref[k - 1]) / d->dhs[k]);
+    for (int k = 0; k < kKX - 1; ++k)
+        xa[k][k] = 0.5 * (kAkap * d->tref[k] / d->fsg[k] - (d->tref[k + 1] - d->tref[k]) / d->dhs[k]);
+    dsum[0] = d->dhs[0];
+    for (int k = 1; k < kKX; ++k) dsum[k] = dsum[k - 1] + d->dhs[k];
+    for (int k = 0; k < kKX - 1; ++k)
+        for (int k1 = 0; k1 < kKX; ++k1) {
+            xb[k1][k] = d->dhs[k1] * dsum[k];
+            if (k1 <= k) xb[k1][k] = xb[k1][k] - d->dhs[k1];
+        }
+    for (int k = 0; k < kKX; ++k)
+        for (int k1 = 0; k1 < kKX; ++k1) {
+            double s = ya[k1][k];
+            for (int k2 = 0; k2 < kKX - 1; ++k2) s = s + xa[k2][k] * xb[k1][k2];
+            d->xc[k1][k] = s;
+        }
+    std::memset(d->xd, 0, sizeof d->xd);
+    for (int k = 0; k < kKX; ++k)
+        for (int k1 = k + 1; k1 < kKX; ++k1) d->xd[k1][k] = kRgas * std::log(d->hsg[k1 + 1] / d->hsg[k1]);
+    for (int k = 0; k < kKX; ++k) d->xd[k][k] = kRgas * std::log(d->hsg[k + 1] / d->fsg[k]);
+    for (int k = 0; k < kKX; ++k)
+        for (int k1 = 0; k1 < kKX; ++k1) {
+            double s = 0.;
+            for (int k2 = 0; k2 < kKX; ++k2) s = s + d->xd[k2][k] * d->xc[k1][k2];
+            xe[k1][k] = s;
+        }
+    for (int l = 1; l <= kLMAX; ++l) {
+        const double xxx = ((double)l * (double)(l + 1)) / (kRearth * kRearth);
+        double xf[kKX][kKX];
+        for (int k = 0; k < kKX; ++k)
+            for (int k1 = 0; k1 < kKX; ++k1)
+                xf[k1][k] = xi * xi * xxx * (kRgas * d->tref[k] * d->dhs[k1] - xe[k1][k]);
+        for (int k = 0; k < kKX; ++k) xf[k][k] = xf[k][k] + 1.;
+        inv(xf, d->xj[l - 1], kKX);
+    }
+    for (int k = 0; k < kKX; ++k)
+        for (int k1 = 0; k1 < kKX; ++k1) d->xc[k1][k] = d->xc[k1][k] * xi;
+}
+
+}  // namespace sml

@@ -48,6 +48,7 @@ struct sml_spectral {
     double *d_cosgr;  // [48]
     double *d_cosgr2; // [48]
     double *d_coef;   // gradx[31] | uvdx | uvdym | uvdyp | vddym | vddyp ([32][31] each)
+    double *d_el2;    // el2[32][31] | trfilt[32][31]
     double *d_work;   // varm workspace
     size_t work_fields;
     double *d_hbuf;   // staging for the host convenience calls
@@ -342,6 +343,12 @@ extern "C" int sml_spectral_create(double radius, sml_spectral **out) {
     std::memcpy(coef.data() + kMX + 2 * kNX * kMX, t.uvdyp, sizeof t.uvdyp);
     std::memcpy(coef.data() + kMX + 3 * kNX * kMX, t.vddym, sizeof t.vddym);
     std::memcpy(coef.data() + kMX + 4 * kNX * kMX, t.vddyp, sizeof t.vddyp);
+    std::vector<double> el2trf(2 * (size_t)kNX * kMX);
+    for (int n = 0; n < kNX; ++n)
+        for (int m = 0; m < kMX; ++m) {
+            el2trf[n * kMX + m] = t.el2[n][m];
+            el2trf[kNX * kMX + n * kMX + m] = (m + n <= kNTRUN) ? 1.0 : 0.0;  // trfilt (parmtr :103-107)
+        }
     auto up = [](double **d, const void *h, size_t bytes) -> int {
         SML_HIP(hipMalloc(d, bytes));
         SML_HIP(hipMemcpy(*d, h, bytes, hipMemcpyHostToDevice));
@@ -352,6 +359,7 @@ extern "C" int sml_spectral_create(double radius, sml_spectral **out) {
         (rc = up(&s->d_dinv, t.dinv, sizeof t.dinv)) || (rc = up(&s->d_dfwd, t.dfwd, sizeof t.dfwd)) ||
         (rc = up(&s->d_wt, t.wt, sizeof t.wt)) || (rc = up(&s->d_cosgr, t.cosgr, sizeof t.cosgr)) ||
         (rc = up(&s->d_cosgr2, t.cosgr2, sizeof t.cosgr2)) || (rc = up(&s->d_coef, coef.data(), coef.size() * 8)) ||
+        (rc = up(&s->d_el2, el2trf.data(), el2trf.size() * 8)) ||
         (rc = ensure_work(s, 64))) {
         sml_spectral_destroy(s);
         return rc;
@@ -362,8 +370,8 @@ extern "C" int sml_spectral_create(double radius, sml_spectral **out) {
 
 extern "C" int sml_spectral_destroy(sml_spectral *s) {
     if (!s) return SML_OK;
-    double *ptrs[] = {s->d_pinv, s->d_pfwd, s->d_dinv, s->d_dfwd, s->d_wt,
-                      s->d_cosgr, s->d_cosgr2, s->d_coef, s->d_work, s->d_hbuf};
+    double *ptrs[] = {s->d_pinv,   s->d_pfwd, s->d_dinv, s->d_dfwd, s->d_wt,  s->d_cosgr,
+                      s->d_cosgr2, s->d_coef, s->d_el2,  s->d_work, s->d_hbuf};
     for (double *p : ptrs)
         if (p) (void)hipFree(p);
     delete s;
@@ -501,3 +509,58 @@ extern "C" int sml_spec_host(sml_spectral *s, const double *grid, double *spec, 
     SML_HIP(hipMemcpy(spec, ds, (size_t)nf * kSpecField * 8, hipMemcpyDeviceToHost));
     return SML_OK;
 }
+
+// ------------------------------------------------------------------ internal API
+#include "sml_spectral_internal.hpp"
+
+namespace sml {
+
+const SpectralTables &spectral_host_tables(const sml_spectral *s) { return s->t; }
+
+SpectralDev spectral_dev(const sml_spectral *s) {
+    SpectralDev d;
+    const Coef c = coef_of(s);
+    d.gradx = c.gradx;
+    d.uvdx = c.uvdx;
+    d.uvdym = c.uvdym;
+    d.uvdyp = c.uvdyp;
+    d.vddym = c.vddym;
+    d.vddyp = c.vddyp;
+    d.el2 = s->d_el2;
+    d.trfilt = s->d_el2 + kNX * kMX;
+    d.cosgr = s->d_cosgr;
+    d.cosgr2 = s->d_cosgr2;
+    d.wt = s->d_wt;
+    return d;
+}
+
+int spectral_gridy(sml_spectral *s, const double *spec, double *varm, int nf, hipStream_t st) {
+    if (nf <= 0) return SML_OK;
+    hipLaunchKernelGGL(k_gridy, dim3(kMX, (nf + 7) / 8), dim3(64), 0, st, spec, varm, s->d_pinv, nf);
+    SML_HIP(hipGetLastError());
+    return SML_OK;
+}
+
+int spectral_gridx(sml_spectral *s, const double *varm, double *grid, int nf, int kcos, hipStream_t st) {
+    if (nf <= 0) return SML_OK;
+    hipLaunchKernelGGL(k_gridx, dim3(nf), dim3(384), 0, st, varm, grid, s->d_dinv, s->d_cosgr, kcos);
+    SML_HIP(hipGetLastError());
+    return SML_OK;
+}
+
+int spectral_specx(sml_spectral *s, const double *grid, double *varm, int nf, int scale, hipStream_t st) {
+    if (nf <= 0) return SML_OK;
+    const double *sc = scale == 1 ? s->d_cosgr : scale == 2 ? s->d_cosgr2 : nullptr;
+    hipLaunchKernelGGL(k_specx, dim3(nf), dim3(256), 0, st, grid, varm, s->d_dfwd, sc);
+    SML_HIP(hipGetLastError());
+    return SML_OK;
+}
+
+int spectral_specy(sml_spectral *s, const double *varm, double *spec, int nf, hipStream_t st) {
+    if (nf <= 0) return SML_OK;
+    hipLaunchKernelGGL(k_specy, dim3(kMX, (nf + 7) / 8), dim3(64), 0, st, varm, spec, s->d_pfwd, s->d_wt, nf);
+    SML_HIP(hipGetLastError());
+    return SML_OK;
+}
+
+}  // namespace sml

@@ -1,0 +1,27 @@
+// sml_spectral_internal.hpp -- library-internal access to the spectral context
+// (used by the dynamics step; not part of the C ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "sml_spectral_tables.hpp"
+
+struct sml_spectral;
+
+namespace sml {
+
+struct SpectralDev {
+    const double *gradx, *uvdx, *uvdym, *uvdyp, *vddym, *vddyp;  // [n][m] (gradx [m])
+    const double *el2, *trfilt;                                   // [n][m]
+    const double *cosgr, *cosgr2, *wt;                            // [48], [48], [24]
+};
+
+const SpectralTables &spectral_host_tables(const sml_spectral *s);
+SpectralDev spectral_dev(const sml_spectral *s);
+// launches on `stream`; nf fields back to back
+int spectral_gridy(sml_spectral *s, const double *spec, double *varm, int nf, hipStream_t st);
+int spectral_gridx(sml_spectral *s, const double *varm, double *grid, int nf, int kcos, hipStream_t st);
+// scale: 0 none, 1 x cosgr(lat), 2 x cosgr2(lat) (vdspec's prescaling)
+int spectral_specx(sml_spectral *s, const double *grid, double *varm, int nf, int scale, hipStream_t st);
+int spectral_specy(sml_spectral *s, const double *varm, double *spec, int nf, hipStream_t st);
+
+}  // namespace sml

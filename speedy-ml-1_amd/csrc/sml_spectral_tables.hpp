@@ -15,6 +15,7 @@ struct SpectralTables {
     int nsh2[kNX];
     double el2[kNX][kMX];
     double gradx[kMX];
+    double gradym[kNX][kMX], gradyp[kNX][kMX];
     double uvdx[kNX][kMX], uvdym[kNX][kMX], uvdyp[kNX][kMX];
     double vddym[kNX][kMX], vddyp[kNX][kMX];
     double poly[kIY][kNX][kMX];   // P_mn at sia(j) (lgndre)

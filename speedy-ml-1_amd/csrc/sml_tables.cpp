@@ -102,9 +102,11 @@ void build_spectral_tables(double a, SpectralTables *t) {
                 t->vddym[0][m] = 0.0;
             } else {
                 t->uvdx[n][m] = -a * (double)m / (el1 * (el1 + 1.0));
+                t->gradym[n][m] = (el1 - 1.0) * epsi[n][m] / a;
                 t->uvdym[n][m] = -a * epsi[n][m] / el1;
                 t->vddym[n][m] = (el1 + 1.0) * epsi[n][m] / a;
             }
+            t->gradyp[n][m] = (el1 + 2.0) * epsi[n + 1][m] / a;
             t->uvdyp[n][m] = -a * epsi[n + 1][m] / (el1 + 1.0);
             t->vddyp[n][m] = el1 * epsi[n + 1][m] / a;
         }

@@ -30,6 +30,9 @@ EXPORTED = (
     "sml_res_step", "sml_res_step_host", "sml_res_footprint", "sml_res_enable_timing",
     "sml_res_kernel_times", "sml_exchange_assemble", "sml_res_tile_inputs",
     "sml_nc_read_region", "sml_nc_write_region",
+    "sml_dyn_create", "sml_dyn_destroy", "sml_dyn_impint", "sml_dyn_set_forcing", "sml_dyn_set_state",
+    "sml_dyn_get_state", "sml_dyn_get_phi", "sml_dyn_get_tendencies", "sml_dyn_state_device",
+    "sml_dyn_step", "sml_dyn_step_host",
 )
 
 
@@ -101,6 +104,17 @@ def _declare(L: ctypes.CDLL) -> None:
         "sml_res_tile_inputs": [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp],
         "sml_nc_read_region": [ctypes.c_char_p, vp, vp, vp, vp, vp, vp, vp, vp],
         "sml_nc_write_region": [ctypes.c_char_p, i, i, i, i, i, vp, vp, vp, vp, vp, vp, vp],
+        "sml_dyn_create": [d, pp],
+        "sml_dyn_destroy": [vp],
+        "sml_dyn_impint": [vp, d, d],
+        "sml_dyn_set_forcing": [vp, vp, vp, vp],
+        "sml_dyn_set_state": [vp, vp, vp, vp, vp, vp],
+        "sml_dyn_get_state": [vp, vp, vp, vp, vp, vp],
+        "sml_dyn_get_phi": [vp, vp],
+        "sml_dyn_get_tendencies": [vp, vp],
+        "sml_dyn_state_device": [vp, pp, pp],
+        "sml_dyn_step": [vp, i, i, d, d, d, d, vp, vp],
+        "sml_dyn_step_host": [vp, i, i, d, d, d, d, vp],
     }
     for name, args in sig.items():
         fn = getattr(L, name)

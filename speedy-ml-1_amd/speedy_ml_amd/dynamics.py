@@ -1,0 +1,115 @@
+"""SPEEDY's spectral dynamical core on the GPU (libspeedyml sml_dyn_*).
+
+Mirrors the reference's time-stepping interface: `impint(dt, alph)`
+(src/ini_impint.f90:1-153) and `step(j1, j2, dt, alph, rob, wil)`
+(src/dyn_step.f90:1-128) acting on the prognostic state of mod_dynvar
+(vor, div, t, ps, tr; src/mod_dynvar.f90:15-27), with `stepone`'s start-up
+sequence (src/ini_stepone.f90:19-34) and the leapfrog loop (src/dyn_stloop.f90:43)
+as conveniences.  Physics (phypar) is not computed here: its grid-point
+tendencies (u, v, t, q) can be handed to each step, or are zero.
+
+State arrays (numpy complex128, C order == the reference's Fortran layout):
+vor/div/t/tr (2, kx=8, nx=32, mx=31), ps (2, 32, 31); forcing phis/tcorh/qcorh
+(32, 31).  Physics tendencies: float64 (4, 8, 48, 96).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from ._lib import check, lib, ptr, stream_ptr
+
+EARTH_RADIUS = 6.371e6  # mod_dyncon1.f90 rearth
+KX, NX, MX = 8, 32, 31
+FIELDS = ("vor", "div", "t", "tr", "ps")
+NSTEPS = 96  # mod_tsteps.f90: nsteps per day
+DELT = 86400.0 / NSTEPS
+ROB, WIL, ALPH = 0.05, 0.53, 0.5  # mod_tsteps.f90:90,93; ini_indyns.f90 alph
+
+
+def _c128(a, shape):
+    a = np.ascontiguousarray(a, dtype=np.complex128)
+    if a.shape != shape:
+        raise ValueError(f"expected shape {shape}, got {a.shape}")
+    return a
+
+
+class Dynamics:
+    def __init__(self, radius: float = EARTH_RADIUS):
+        h = ctypes.c_void_p()
+        check(lib().sml_dyn_create(radius, ctypes.byref(h)))
+        self._h = h
+        self._dtal = None
+
+    def close(self):
+        if self._h:
+            lib().sml_dyn_destroy(self._h)
+            self._h = None
+
+    __del__ = close
+
+    def impint(self, dt: float, alph: float = ALPH):
+        check(lib().sml_dyn_impint(self._h, dt, alph))
+        self._dtal = (dt, alph)
+
+    def set_forcing(self, phis=None, tcorh=None, qcorh=None):
+        args = [None if a is None else _c128(a, (NX, MX)) for a in (phis, tcorh, qcorh)]
+        check(lib().sml_dyn_set_forcing(self._h, *[ptr(a) for a in args]))
+
+    def set_state(self, state):
+        a = {f: _c128(state[f], (2, KX, NX, MX) if f != "ps" else (2, NX, MX)) for f in FIELDS}
+        check(lib().sml_dyn_set_state(self._h, ptr(a["vor"]), ptr(a["div"]), ptr(a["t"]), ptr(a["ps"]),
+                                      ptr(a["tr"])))
+
+    def get_state(self):
+        out = {f: np.zeros((2, KX, NX, MX) if f != "ps" else (2, NX, MX), np.complex128) for f in FIELDS}
+        check(lib().sml_dyn_get_state(self._h, ptr(out["vor"]), ptr(out["div"]), ptr(out["t"]), ptr(out["ps"]),
+                                      ptr(out["tr"])))
+        return out
+
+    def get_phi(self):
+        phi = np.zeros((KX, NX, MX), np.complex128)
+        check(lib().sml_dyn_get_phi(self._h, ptr(phi)))
+        return phi
+
+    def get_tendencies(self):
+        tend = np.zeros((4 * KX + 1, NX, MX), np.complex128)
+        check(lib().sml_dyn_get_tendencies(self._h, ptr(tend)))
+        return tend
+
+    def device_buffers(self):
+        """(state, phys) device addresses: [vor|div|t|tr|ps] and a phys scratch buffer."""
+        s, p = ctypes.c_void_p(), ctypes.c_void_p()
+        check(lib().sml_dyn_state_device(self._h, ctypes.byref(s), ctypes.byref(p)))
+        return s.value, p.value
+
+    def step(self, j1, j2, dt, alph=ALPH, rob=ROB, wil=WIL, phys=None, stream=None):
+        """step(j1, j2, dt, alph, rob, wil).  `phys`: host numpy (4, 8, 48, 96), a
+        float64 CUDA tensor of that shape, or None.  impint(dt, alph) is evaluated
+        when (dt, alph) differs from the last call (the reference calls it
+        explicitly, ini_stepone.f90:21-34)."""
+        if self._dtal != (dt, alph):
+            self.impint(dt, alph)
+        if phys is None or isinstance(phys, np.ndarray):
+            ph = None if phys is None else np.ascontiguousarray(phys, dtype=np.float64)
+            if ph is not None and ph.shape != (4, KX, 48, 96):
+                raise ValueError("phys must be (4, 8, 48, 96)")
+            check(lib().sml_dyn_step_host(self._h, j1, j2, dt, alph, rob, wil, ptr(ph)))
+        else:
+            if not (phys.is_cuda and phys.is_contiguous() and phys.numel() == 4 * KX * 4608):
+                raise ValueError("phys must be a contiguous float64 CUDA tensor (4, 8, 48, 96)")
+            check(lib().sml_dyn_step(self._h, j1, j2, dt, alph, rob, wil, ptr(phys), stream_ptr(stream)))
+
+    def stepone(self, delt: float = DELT, alph: float = ALPH, phys=None):
+        """ini_stepone.f90:19-34 for istart = 0: forward half step, first leapfrog."""
+        self.step(1, 1, 0.5 * delt, alph, phys=phys)
+        self.step(1, 2, delt, alph, phys=phys)
+        self.impint(2 * delt, alph)
+
+    def leapfrog(self, nsteps: int, delt: float = DELT, alph: float = ALPH, stream=None):
+        """dyn_stloop.f90:43: nsteps x step(2, 2, 2 delt), no physics, asynchronous."""
+        if self._dtal != (2 * delt, alph):
+            self.impint(2 * delt, alph)
+        for _ in range(nsteps):
+            check(lib().sml_dyn_step(self._h, 2, 2, 2 * delt, alph, ROB, WIL, None, stream_ptr(stream)))

@@ -36,3 +36,14 @@ def golden():
     import numpy as np
 
     return dict(np.load(os.path.join(REPO, "tests", "golden", "spectral_ref.npz")))
+
+
+@pytest.fixture(scope="session")
+def dyn_golden():
+    """Reference `step` outputs (tests/golden/make_dyn_golden.py)."""
+    import numpy as np
+
+    return dict(np.load(os.path.join(REPO, "tests", "golden", "dyn_ref.npz")))
+
+
+DYN_CASES = ("fwd", "lf0", "lf", "expl")
