@@ -285,7 +285,11 @@ __global__ void k_dyn_tail(double *__restrict__ st, double *__restrict__ Td, dou
     const int p = mnp & 1, mn = mnp >> 1;
     const int m = mn % kMX, n = mn / kMX;
     const int c = ci(p, m, n);
-    auto S = [&](size_t off, int lev, int k) -> double & { return st[off + ((size_t)(lev - 1) * kKX + k) * kSF + c]; };
+    // field (k, lev) of a (mx, nx, kx, 2) array; ps is (mx, nx, 2): one level per time level
+    auto S = [&](size_t off, int lev, int k) -> double & {
+        const size_t nlev = (off == kOffPs) ? 1 : kKX;
+        return st[off + ((size_t)(lev - 1) * nlev + k) * kSF + c];
+    };
     double vordt[kKX], divdt[kKX], tdt[kKX], trdt[kKX], psdt;
 #pragma unroll
     for (int k = 0; k < kKX; ++k) {
