@@ -47,6 +47,8 @@ def parse():
     p.add_argument("--weights", choices=("f32", "f64"), default="f32")
     p.add_argument("--cpu-sample", type=int, default=96, help="regions in the CPU-baseline sample (0 = skip)")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--speedy-steps", type=int, default=48,
+                   help="leapfrog steps timed in the supplementary SPEEDY-dynamics leg (0 = skip)")
     return p.parse_args()
 
 
@@ -153,6 +155,7 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.cpu_sample > 0:
         cpu = cpu_baseline(args.cpu_sample, nreg, mask)
+    speedy = speedy_leg(dev, world, rank, args) if args.speedy_steps > 0 else None
 
     if rank == 0:
         steps_per_s = args.steps / dt
@@ -195,10 +198,55 @@ def main():
                 "step_algorithmic_bytes": algo_step,
             },
             "cpu_baseline": cpu,
+            "speedy_dynamics": speedy,
         }
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def speedy_leg(dev, world, rank, args):
+    """Supplementary measurement, outside the headline step: SPEEDY's dynamical core
+    (dyn_step without physics) on the GPU, timed per leapfrog step with HIP events,
+    launched step by step and replayed from a hipGraph, plus the oracle's step on
+    one host core.  A 6-h window is stepone + 24 leapfrog steps (nsteps = 96/day)."""
+    import torch
+
+    from speedy_ml_amd.dynamics import DELT, Dynamics
+    from speedy_ml_amd.synthetic import dyn_state
+
+    st, forcing = dyn_state()
+    dyn = Dynamics()
+    dyn.set_forcing(**forcing)
+    out = {}
+    for mode, graph in (("launch", False), ("graph", True)):
+        dyn.set_state(st)
+        dyn.stepone()
+        dyn.leapfrog(4, DELT, graph=graph)  # warm-up (and graph capture)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        dyn.leapfrog(args.speedy_steps, DELT, graph=graph)
+        e1.record()
+        torch.cuda.synchronize()
+        out[f"step_ms_{mode}"] = round(e0.elapsed_time(e1) / args.speedy_steps, 4)
+    out["window_ms_graph"] = round(26 * out["step_ms_graph"], 3)
+    out["note"] = ("dynamics only (grtend/sptend/implic/hordif/timint, 164 transforms as 7 batched launches); "
+                   "physics not on the GPU, not part of the headline value")
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(REPO, "oracle"))
+        import oracle
+
+        s = oracle.dyn_state_copy(st)
+        oracle.dyn_step(s, forcing["phis"], forcing["tcorh"], forcing["qcorh"], None, 2, 2, 2 * DELT, 0.5)
+        t0 = time.perf_counter()
+        nrep = 5
+        for _ in range(nrep):
+            oracle.dyn_step(s, forcing["phis"], forcing["tcorh"], forcing["qcorh"], None, 2, 2, 2 * DELT, 0.5)
+        out["cpu_oracle_step_ms"] = round((time.perf_counter() - t0) / nrep * 1e3, 3)
+        out["cpu_oracle_note"] = "oracle C restatement (long-double DFT instead of FFTPACK), 1 core"
+    dyn.close()
+    return out
 
 
 def cpu_baseline(sample: int, nreg: int, mask):

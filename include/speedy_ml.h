@@ -222,6 +222,11 @@ int sml_dyn_state_device(sml_dynamics *d, double **d_state, double **d_phys);
  * hordif, stratospheric drag, timint.  Asynchronous on `stream`. */
 int sml_dyn_step(sml_dynamics *d, int j1, int j2, double dt, double alph, double rob, double wil,
                  const double *d_phys, void *stream);
+/* nsteps x step(2, 2, dt, alph, rob, wil) -- the leapfrog loop of stloop
+ * (src/dyn_stloop.f90:43) -- replayed from one captured hipGraph (re-captured
+ * when (dt, alph, rob, wil, d_phys) change).  impint(dt, alph) must be current. */
+int sml_dyn_leapfrog(sml_dynamics *d, int nsteps, double dt, double alph, double rob, double wil,
+                     const double *d_phys, void *stream);
 /* synchronous variant taking host physics tendencies (may be NULL) */
 int sml_dyn_step_host(sml_dynamics *d, int j1, int j2, double dt, double alph, double rob, double wil,
                       const double *phys);

@@ -63,6 +63,11 @@ struct sml_dynamics {
     double *d_tend = nullptr;
     double *d_phys = nullptr;  // staging for host-provided physics tendencies
     bool impint_done = false;
+    // leapfrog replay: one step(2, 2, ...) captured as a hipGraph
+    hipStream_t cap_stream = nullptr;
+    hipGraphExec_t graph = nullptr;
+    double g_key[4] = {0, 0, 0, 0};
+    const double *g_phys = nullptr;
 };
 
 namespace {
@@ -443,6 +448,8 @@ extern "C" int sml_dyn_destroy(sml_dynamics *d) {
                     d->d_varm, d->d_grid, d->d_gfwd, d->d_sfwd, d->d_tend, d->d_phys};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
+    if (d->graph) (void)hipGraphExecDestroy(d->graph);
+    if (d->cap_stream) (void)hipStreamDestroy(d->cap_stream);
     if (d->sp) sml_spectral_destroy(d->sp);
     delete d;
     return SML_OK;
@@ -538,12 +545,11 @@ extern "C" int sml_dyn_state_device(sml_dynamics *d, double **d_state, double **
     return SML_OK;
 }
 
-extern "C" int sml_dyn_step(sml_dynamics *d, int j1, int j2, double dt, double alph, double rob, double wil,
-                            const double *d_phys, void *stream) {
-    SML_REQUIRE(d, "null context");
-    SML_REQUIRE((j1 == 1 || j1 == 2) && (j2 == 1 || j2 == 2), "j1/j2 must be 1 or 2");
-    if (!d->impint_done) return fail(SML_ERR_STATE, "sml_dyn_impint must be called before sml_dyn_step");
-    hipStream_t st = (hipStream_t)stream;
+namespace {
+
+// the 9 launches of one step(j1, j2, dt, alph, rob, wil) on stream st
+int launch_step(sml_dynamics *d, int j1, int j2, double dt, double alph, double rob, double wil,
+                const double *d_phys, hipStream_t st) {
     const DynTables *T = d->d_tab;
     // 1. grtend: inverse transforms of the j2 state
     hipLaunchKernelGGL(k_dyn_prep, dim3((kMN + 127) / 128, kKX + 1), dim3(128), 0, st, d->d_state, d->d_specin, T,
@@ -570,6 +576,50 @@ extern "C" int sml_dyn_step(sml_dynamics *d, int j1, int j2, double dt, double a
     hipLaunchKernelGGL(k_dyn_tail, dim3((2 * kMN + 127) / 128), dim3(128), 0, st, d->d_state, d->d_tend, d->d_phi,
                        d->d_phis, d->d_tcorh, d->d_qcorh, T, j1, j4, dt, alph, rob, wil);
     SML_HIP(hipGetLastError());
+    return SML_OK;
+}
+
+}  // namespace
+
+extern "C" int sml_dyn_step(sml_dynamics *d, int j1, int j2, double dt, double alph, double rob, double wil,
+                            const double *d_phys, void *stream) {
+    SML_REQUIRE(d, "null context");
+    SML_REQUIRE((j1 == 1 || j1 == 2) && (j2 == 1 || j2 == 2), "j1/j2 must be 1 or 2");
+    if (!d->impint_done) return fail(SML_ERR_STATE, "sml_dyn_impint must be called before sml_dyn_step");
+    return launch_step(d, j1, j2, dt, alph, rob, wil, d_phys, (hipStream_t)stream);
+}
+
+extern "C" int sml_dyn_leapfrog(sml_dynamics *d, int nsteps, double dt, double alph, double rob, double wil,
+                                const double *d_phys, void *stream) {
+    SML_REQUIRE(d && nsteps >= 0, "bad argument");
+    if (!d->impint_done) return fail(SML_ERR_STATE, "sml_dyn_impint must be called before sml_dyn_leapfrog");
+    if (nsteps == 0) return SML_OK;
+    const double key[4] = {dt, alph, rob, wil};
+    if (!d->graph || std::memcmp(key, d->g_key, sizeof key) != 0 || d_phys != d->g_phys) {
+        if (d->graph) {
+            SML_HIP(hipGraphExecDestroy(d->graph));
+            d->graph = nullptr;
+        }
+        if (!d->cap_stream) SML_HIP(hipStreamCreateWithFlags(&d->cap_stream, hipStreamNonBlocking));
+        hipGraph_t g = nullptr;
+        SML_HIP(hipStreamBeginCapture(d->cap_stream, hipStreamCaptureModeThreadLocal));
+        int rc = launch_step(d, 2, 2, dt, alph, rob, wil, d_phys, d->cap_stream);
+        hipError_t e = hipStreamEndCapture(d->cap_stream, &g);
+        if (rc) {
+            if (g) (void)hipGraphDestroy(g);
+            return rc;
+        }
+        if (e != hipSuccess) return fail(SML_ERR_HIP, "sml_dyn_leapfrog capture: %s", hipGetErrorString(e));
+        e = hipGraphInstantiate(&d->graph, g, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(g);
+        if (e != hipSuccess) {
+            d->graph = nullptr;
+            return fail(SML_ERR_HIP, "sml_dyn_leapfrog instantiate: %s", hipGetErrorString(e));
+        }
+        std::memcpy(d->g_key, key, sizeof key);
+        d->g_phys = d_phys;
+    }
+    for (int i = 0; i < nsteps; ++i) SML_HIP(hipGraphLaunch(d->graph, (hipStream_t)stream));
     return SML_OK;
 }
 

@@ -32,7 +32,7 @@ EXPORTED = (
     "sml_nc_read_region", "sml_nc_write_region",
     "sml_dyn_create", "sml_dyn_destroy", "sml_dyn_impint", "sml_dyn_set_forcing", "sml_dyn_set_state",
     "sml_dyn_get_state", "sml_dyn_get_phi", "sml_dyn_get_tendencies", "sml_dyn_state_device",
-    "sml_dyn_step", "sml_dyn_step_host",
+    "sml_dyn_step", "sml_dyn_step_host", "sml_dyn_leapfrog",
 )
 
 
@@ -115,6 +115,7 @@ def _declare(L: ctypes.CDLL) -> None:
         "sml_dyn_state_device": [vp, pp, pp],
         "sml_dyn_step": [vp, i, i, d, d, d, d, vp, vp],
         "sml_dyn_step_host": [vp, i, i, d, d, d, d, vp],
+        "sml_dyn_leapfrog": [vp, i, d, d, d, d, vp, vp],
     }
     for name, args in sig.items():
         fn = getattr(L, name)

@@ -107,9 +107,15 @@ class Dynamics:
         self.step(1, 2, delt, alph, phys=phys)
         self.impint(2 * delt, alph)
 
-    def leapfrog(self, nsteps: int, delt: float = DELT, alph: float = ALPH, stream=None):
-        """dyn_stloop.f90:43: nsteps x step(2, 2, 2 delt), no physics, asynchronous."""
+    def leapfrog(self, nsteps: int, delt: float = DELT, alph: float = ALPH, phys=None, stream=None,
+                 graph: bool = True):
+        """dyn_stloop.f90:43: nsteps x step(2, 2, 2 delt), asynchronous on `stream`.
+        graph=True replays one captured hipGraph per step (sml_dyn_leapfrog);
+        phys: None or a device tensor held fixed over the steps."""
         if self._dtal != (2 * delt, alph):
             self.impint(2 * delt, alph)
+        if graph:
+            check(lib().sml_dyn_leapfrog(self._h, nsteps, 2 * delt, alph, ROB, WIL, ptr(phys), stream_ptr(stream)))
+            return
         for _ in range(nsteps):
-            check(lib().sml_dyn_step(self._h, 2, 2, 2 * delt, alph, ROB, WIL, None, stream_ptr(stream)))
+            check(lib().sml_dyn_step(self._h, 2, 2, 2 * delt, alph, ROB, WIL, ptr(phys), stream_ptr(stream)))

@@ -113,3 +113,47 @@ def synthetic_grids(seed: int = 5):
     g2 = 0.1 * rng.standard_normal((48, 96))
     pr = np.abs(rng.standard_normal((48, 96)))
     return g4, g2, pr
+
+
+# ---------------------------------------------------------------- SPEEDY state
+def _spectral_field(rng, amp, power, mean=0.0):
+    """complex (nx=32, mx=31) coefficients on the T30 triangle (m + n <= 30)
+    decaying as (1 + m + n)^-power, m = 0 imaginary parts zero; mean sets the
+    global mean (P_00 = sqrt(1/2))."""
+    m = np.arange(31)[None, :]
+    n = np.arange(32)[:, None]
+    ll = m + n
+    mask = ll <= 30
+    c = np.zeros((32, 31), np.complex128)
+    a = amp * (1.0 + ll) ** (-power)
+    c[mask] = (rng.standard_normal(mask.sum()) + 1j * rng.standard_normal(mask.sum())) * a[mask]
+    c[:, 0] = c[:, 0].real
+    c[0, 0] = mean * np.sqrt(2.0)
+    return c
+
+
+def dyn_state(seed: int = 2025):
+    """Seeded T30L8 spectral state (mod_dynvar layout, both time levels) around the
+    reference temperature profile tref (ini_impint.f90:43-49), plus forcing
+    (phis, tcorh, qcorh).  Same construction as tests/golden/make_dyn_golden.py."""
+    rng = np.random.default_rng(seed)
+    hsg = np.array([0.000, 0.050, 0.140, 0.260, 0.420, 0.600, 0.770, 0.900, 1.000])
+    fsg = 0.5 * (hsg[1:] + hsg[:-1])
+    rgam = (2.0 / 7.0) * 1004.0 * 6.0 / (1000.0 * 9.81)
+    tref = 288.0 * np.maximum(0.2, fsg) ** rgam
+    st = {f: np.zeros((2, 8, 32, 31), np.complex128) for f in ("vor", "div", "t", "tr")}
+    st["ps"] = np.zeros((2, 32, 31), np.complex128)
+    for k in range(8):
+        st["vor"][0, k] = _spectral_field(rng, 2e-5, 1.0)
+        st["div"][0, k] = _spectral_field(rng, 2e-6, 1.0)
+        st["t"][0, k] = _spectral_field(rng, 2.0, 1.0, mean=tref[k])
+        qm = 12.0 * fsg[k] ** 3
+        st["tr"][0, k] = _spectral_field(rng, 0.2 * qm, 1.5, mean=qm)
+    st["ps"][0] = _spectral_field(rng, 0.02, 1.5)
+    for f, amp in (("vor", 2e-8), ("div", 2e-9), ("t", 2e-3), ("tr", 2e-4)):
+        for k in range(8):
+            st[f][1, k] = st[f][0, k] + _spectral_field(rng, amp, 1.0)
+    st["ps"][1] = st["ps"][0] + _spectral_field(rng, 2e-5, 1.5)
+    forcing = {"phis": _spectral_field(rng, 2000.0, 1.5, mean=3000.0),
+               "tcorh": _spectral_field(rng, 1.0, 1.5), "qcorh": _spectral_field(rng, 0.1, 1.5)}
+    return st, forcing

@@ -111,3 +111,20 @@ def test_step_requires_impint(cuda):
         assert lib().sml_dyn_step(h, 3, 2, 1800.0, 0.5, 0.05, 0.53, None, None) == -1  # bad j1
     finally:
         lib().sml_dyn_destroy(h)
+
+
+def test_leapfrog_graph_matches_step_loop(dyn, dyn_golden):
+    """sml_dyn_leapfrog (hipGraph replay) == the same steps launched one by one."""
+    import torch
+
+    g = dyn_golden
+    delt = float(g["delt"])
+    _load(dyn, g)
+    dyn.leapfrog(5, delt, graph=False)
+    a = dyn.get_state()
+    _load(dyn, g)
+    dyn.leapfrog(5, delt, graph=True)
+    torch.cuda.synchronize()
+    b = dyn.get_state()
+    for f in oracle.DYN_FIELDS:
+        np.testing.assert_array_equal(a[f], b[f])
