@@ -280,139 +280,122 @@ __global__ void k_dyn_combine(const double *__restrict__ S, double *__restrict__
     }
 }
 
-// tail: sptend + geop + implic + hordif + drag + timint, one thread per (m, n, part)
-__global__ void k_dyn_tail(double *__restrict__ st, double *__restrict__ Td, double *__restrict__ phi_out,
-                           const double *__restrict__ phis, const double *__restrict__ tcorh,
-                           const double *__restrict__ qcorh, const DynTables *__restrict__ T, int j1, int j4,
-                           double dt, double alph, double rob, double wil) {
-    const int mnp = blockIdx.x * blockDim.x + threadIdx.x;
-    if (mnp >= 2 * kMN) return;
-    const int p = mnp & 1, mn = mnp >> 1;
-    const int m = mn % kMX, n = mn / kMX;
-    const int c = ci(p, m, n);
-    // field (k, lev) of a (mx, nx, kx, 2) array; ps is (mx, nx, 2): one level per time level
-    auto S = [&](size_t off, int lev, int k) -> double & {
+// tail: sptend + geop + implic + hordif + drag + timint.  A block owns 32 real
+// coefficients c (= Re/Im of (m, n)) x all 8 levels, one thread per (c, level k);
+// the vertical couplings (dmeanc, sigdtc, geop, implic's level matrices) go
+// through LDS, and every sum runs over k in the reference's order.
+constexpr int kTailC = 32;
+__global__ __launch_bounds__(256) void k_dyn_tail(double *__restrict__ st, double *__restrict__ Td,
+                                                  double *__restrict__ phi_out, const double *__restrict__ phis,
+                                                  const double *__restrict__ tcorh, const double *__restrict__ qcorh,
+                                                  const DynTables *__restrict__ T, int j1, int j4, double dt,
+                                                  double alph, double rob, double wil) {
+    __shared__ double sh[2][kKX][kTailC];
+    const int cc = threadIdx.x & (kTailC - 1), k = threadIdx.x / kTailC;
+    const int c = blockIdx.x * kTailC + cc;  // 0 .. 1983 = 2 * (m + mx n) + p
+    const int mn = c >> 1, m = mn % kMX, n = mn / kMX;
+    auto S = [&](size_t off, int lev, int kk) -> double & {  // state (c, kk, lev); ps has one level
         const size_t nlev = (off == kOffPs) ? 1 : kKX;
-        return st[off + ((size_t)(lev - 1) * nlev + k) * kSF + c];
+        return st[off + ((size_t)(lev - 1) * nlev + kk) * kSF + c];
     };
-    double vordt[kKX], divdt[kKX], tdt[kKX], trdt[kKX], psdt;
-#pragma unroll
-    for (int k = 0; k < kKX; ++k) {
-        vordt[k] = Td[kTVor + (size_t)k * kSF + c];
-        divdt[k] = Td[kTDiv + (size_t)k * kSF + c];
-        tdt[k] = Td[kTT + (size_t)k * kSF + c];
-        trdt[k] = Td[kTTr + (size_t)k * kSF + c];
-    }
-    psdt = Td[kTPs + c];
-    // ---- sptend(divdt, tdt, psdt, j4)  (dyn_sptend.f90:24-66)
+    double vordt = Td[kTVor + (size_t)k * kSF + c], divdt = Td[kTDiv + (size_t)k * kSF + c];
+    double tdt = Td[kTT + (size_t)k * kSF + c], trdt = Td[kTTr + (size_t)k * kSF + c];
+    double psdt = Td[kTPs + c];
+    // ---- sptend(divdt, tdt, psdt, j4)  (dyn_sptend.f90:29-66)
+    sh[0][k][cc] = S(kOffDiv, j4, k);
+    sh[1][k][cc] = S(kOffT, j4, k);
+    __syncthreads();
     double dmeanc = 0.0;
 #pragma unroll
-    for (int k = 0; k < kKX; ++k) dmeanc = dmeanc + S(kOffDiv, j4, k) * T->dhs[k];
+    for (int kk = 0; kk < kKX; ++kk) dmeanc = dmeanc + sh[0][kk][cc] * T->dhs[kk];
     psdt = psdt - dmeanc;
-    if (m == 0 && n == 0) psdt = 0.0;
-    double sigdtc[kKXP], dumk[kKXP];
-    sigdtc[0] = 0.0;
-    sigdtc[kKX] = 0.0;
+    if (c < 2) psdt = 0.0;  // psdt(1,1) = 0
+    double sig_k = 0.0, sig_k1 = 0.0;  // sigdtc(k), sigdtc(k+1); sigdtc(1) = sigdtc(kxp) = 0
+    {
+        double sg = 0.0;
 #pragma unroll
-    for (int k = 0; k < kKX - 1; ++k) sigdtc[k + 1] = sigdtc[k] - T->dhs[k] * (S(kOffDiv, j4, k) - dmeanc);
-    dumk[0] = 0.0;
-    dumk[kKX] = 0.0;
-#pragma unroll
-    for (int k = 1; k < kKX; ++k) dumk[k] = sigdtc[k] * (T->tref[k] - T->tref[k - 1]);
-#pragma unroll
-    for (int k = 0; k < kKX; ++k)
-        tdt[k] = tdt[k] - (dumk[k + 1] + dumk[k]) * T->dhsr[k] + T->tref3[k] * (sigdtc[k + 1] + sigdtc[k]) -
-                 T->tref2[k] * dmeanc;
-    // geop(j4)  (dyn_geop.f90:16-32)
-    double phi[kKX];
-    phi[kKX - 1] = phis[c] + T->xgeop1[kKX - 1] * S(kOffT, j4, kKX - 1);
-#pragma unroll
-    for (int k = kKX - 2; k >= 0; --k)
-        phi[k] = phi[k + 1] + T->xgeop2[k + 1] * S(kOffT, j4, k + 1) + T->xgeop1[k] * S(kOffT, j4, k);
-    if (m == 0) {
-#pragma unroll
-        for (int k = 1; k < kKX - 1; ++k) phi[k] = phi[k] + T->corf[k] * (S(kOffT, j4, k + 1) - S(kOffT, j4, k - 1));
+        for (int kk = 0; kk < kKX - 1; ++kk) {
+            const double nx_ = sg - T->dhs[kk] * (sh[0][kk][cc] - dmeanc);
+            if (kk == k - 1) sig_k = nx_;
+            if (kk == k) sig_k1 = nx_;
+            sg = nx_;
+        }
     }
-    const double psj4 = S(kOffPs, j4, 0);
+    const double dumk_k = (k == 0) ? 0.0 : sig_k * (T->tref[k] - T->tref[k - 1]);
+    const double dumk_k1 = (k == kKX - 1) ? 0.0 : sig_k1 * (T->tref[k + 1] - T->tref[k]);
+    tdt = tdt - (dumk_k1 + dumk_k) * T->dhsr[k] + T->tref3[k] * (sig_k1 + sig_k) - T->tref2[k] * dmeanc;
+    // geop(j4)  (dyn_geop.f90:16-32)
+    double phi = phis[c] + T->xgeop1[kKX - 1] * sh[1][kKX - 1][cc];
 #pragma unroll
-    for (int k = 0; k < kKX; ++k) {
-        phi_out[(size_t)k * kSF + c] = phi[k];
-        const double d1 = phi[k] + kRgas * T->tref[k] * psj4;
+    for (int kk = kKX - 2; kk >= k; --kk)
+        phi = phi + T->xgeop2[kk + 1] * sh[1][kk + 1][cc] + T->xgeop1[kk] * sh[1][kk][cc];
+    if (m == 0 && k >= 1 && k <= kKX - 2) phi = phi + T->corf[k] * (sh[1][k + 1][cc] - sh[1][k - 1][cc]);
+    phi_out[(size_t)k * kSF + c] = phi;
+    {
+        const double d1 = phi + kRgas * T->tref[k] * S(kOffPs, j4, 0);
         const double lapd = -(d1 * T->el2[n][m]);
-        divdt[k] = divdt[k] - lapd;
+        divdt = divdt - lapd;
     }
     // ---- implic(divdt, tdt, psdt)  (dyn_implic.f90:22-67)
     if (alph != 0.0) {
-        double ye[kKX], yf[kKX];
+        __syncthreads();  // sh reuse
+        sh[0][k][cc] = tdt;
+        __syncthreads();
+        double ye = 0.0;
 #pragma unroll
-        for (int k = 0; k < kKX; ++k) ye[k] = 0.0;
-#pragma unroll
-        for (int k1 = 0; k1 < kKX; ++k1)
-#pragma unroll
-            for (int k = 0; k < kKX; ++k) ye[k] = ye[k] + T->xd[k1][k] * tdt[k1];
-#pragma unroll
-        for (int k = 0; k < kKX; ++k) ye[k] = ye[k] + T->tref1[k] * psdt;
-#pragma unroll
-        for (int k = 0; k < kKX; ++k) yf[k] = divdt[k] + T->elz[n][m] * ye[k];
-#pragma unroll
-        for (int k = 0; k < kKX; ++k) divdt[k] = 0.0;
+        for (int k1 = 0; k1 < kKX; ++k1) ye = ye + T->xd[k1][k] * sh[0][k1][cc];
+        ye = ye + T->tref1[k] * psdt;
+        sh[1][k][cc] = divdt + T->elz[n][m] * ye;  // yf
+        __syncthreads();
+        divdt = 0.0;
         const int ll = m + n;
         if (ll != 0) {
-            const double(*xj)[kKX] = T->xj[ll - 1];
 #pragma unroll
-            for (int k1 = 0; k1 < kKX; ++k1)
-#pragma unroll
-                for (int k = 0; k < kKX; ++k) divdt[k] = divdt[k] + xj[k1][k] * yf[k1];
+            for (int k1 = 0; k1 < kKX; ++k1) divdt = divdt + T->xj[ll - 1][k1][k] * sh[1][k1][cc];
         }
+        sh[0][k][cc] = divdt;
+        __syncthreads();
 #pragma unroll
-        for (int k = 0; k < kKX; ++k) psdt = psdt - divdt[k] * T->dhsx[k];
+        for (int kk = 0; kk < kKX; ++kk) psdt = psdt - sh[0][kk][cc] * T->dhsx[kk];
 #pragma unroll
-        for (int k = 0; k < kKX; ++k)
-#pragma unroll
-            for (int k1 = 0; k1 < kKX; ++k1) tdt[k] = tdt[k] + T->xc[k1][k] * divdt[k1];
+        for (int k1 = 0; k1 < kKX; ++k1) tdt = tdt + T->xc[k1][k] * sh[0][k1][cc];
     }
     // ---- horizontal diffusion (dyn_step.f90:60-112, hordif :130-151)
     const double dmp = T->dmp[n][m], dmp1 = T->dmp1[n][m], dmpd = T->dmpd[n][m], dmp1d = T->dmp1d[n][m];
-    const double dmps = T->dmps[n][m], dmp1s = T->dmp1s[n][m];
-    double ctmp[kKX];
-#pragma unroll
-    for (int k = 0; k < kKX; ++k) {
-        vordt[k] = (vordt[k] - dmp * S(kOffVor, 1, k)) * dmp1;
-        divdt[k] = (divdt[k] - dmpd * S(kOffDiv, 1, k)) * dmp1d;
-        ctmp[k] = S(kOffT, 1, k) + tcorh[c] * T->tcorv[k];
-        tdt[k] = (tdt[k] - dmp * ctmp[k]) * dmp1;
-    }
-    if (m == 0) {  // stratospheric drag on the zonal mean, top level (:84-88)
-        const double sdrag = 1. / (kTdrs * 3600.);
-        vordt[0] = vordt[0] - sdrag * S(kOffVor, 1, 0);
-        divdt[0] = divdt[0] - sdrag * S(kOffDiv, 1, 0);
-    }
-    vordt[0] = (vordt[0] - dmps * S(kOffVor, 1, 0)) * dmp1s;
-    divdt[0] = (divdt[0] - dmps * S(kOffDiv, 1, 0)) * dmp1s;
-    tdt[0] = (tdt[0] - dmps * ctmp[0]) * dmp1s;
-#pragma unroll
-    for (int k = 0; k < kKX; ++k) {
-        const double cq = S(kOffTr, 1, k) + qcorh[c] * T->qcorv[k];
-        trdt[k] = (trdt[k] - dmpd * cq) * dmp1d;
-    }
-    if (dt <= 0.0) {  // tendencies only (dyn_step.f90:114)
-#pragma unroll
-        for (int k = 0; k < kKX; ++k) {
-            Td[kTVor + (size_t)k * kSF + c] = vordt[k];
-            Td[kTDiv + (size_t)k * kSF + c] = divdt[k];
-            Td[kTT + (size_t)k * kSF + c] = tdt[k];
-            Td[kTTr + (size_t)k * kSF + c] = trdt[k];
+    vordt = (vordt - dmp * S(kOffVor, 1, k)) * dmp1;
+    divdt = (divdt - dmpd * S(kOffDiv, 1, k)) * dmp1d;
+    const double ctmp = S(kOffT, 1, k) + tcorh[c] * T->tcorv[k];
+    tdt = (tdt - dmp * ctmp) * dmp1;
+    if (k == 0) {
+        if (m == 0) {  // stratospheric drag on the zonal mean, top level (:78-82)
+            const double sdrag = 1. / (kTdrs * 3600.);
+            vordt = vordt - sdrag * S(kOffVor, 1, 0);
+            divdt = divdt - sdrag * S(kOffDiv, 1, 0);
         }
-        Td[kTPs + c] = psdt;
+        const double dmps = T->dmps[n][m], dmp1s = T->dmp1s[n][m];
+        vordt = (vordt - dmps * S(kOffVor, 1, 0)) * dmp1s;
+        divdt = (divdt - dmps * S(kOffDiv, 1, 0)) * dmp1s;
+        tdt = (tdt - dmps * ctmp) * dmp1s;
+    }
+    {
+        const double cq = S(kOffTr, 1, k) + qcorh[c] * T->qcorv[k];
+        trdt = (trdt - dmpd * cq) * dmp1d;
+    }
+    if (dt <= 0.0) {  // tendencies only (dyn_step.f90:109)
+        Td[kTVor + (size_t)k * kSF + c] = vordt;
+        Td[kTDiv + (size_t)k * kSF + c] = divdt;
+        Td[kTT + (size_t)k * kSF + c] = tdt;
+        Td[kTTr + (size_t)k * kSF + c] = trdt;
+        if (k == 0) Td[kTPs + c] = psdt;
         return;
     }
     // ---- timint with the Robert-Williams filter (dyn_step.f90:153-190)
     const double eps = (j1 == 1) ? 0.0 : rob;
     const double trf = T->trfilt[n][m];
-    auto timint = [&](size_t off, int k, double fdt) {
+    auto timint = [&](size_t off, int kk, double fdt) {
         fdt = fdt * trf;  // trunct
-        double &f1 = S(off, 1, k);
-        double &f2 = S(off, 2, k);
+        double &f1 = S(off, 1, kk);
+        double &f2 = S(off, 2, kk);
         const double fj1_old = (j1 == 1) ? f1 : f2;
         const double fnew = f1 + dt * fdt;
         const double f1new = fj1_old + wil * eps * (f1 - 2 * fj1_old + fnew);
@@ -420,15 +403,11 @@ __global__ void k_dyn_tail(double *__restrict__ st, double *__restrict__ Td, dou
         f2 = fnew - (1 - wil) * eps * (f1new - 2 * fj1_new + fnew);
         f1 = f1new;
     };
-    timint(kOffPs, 0, psdt);
-#pragma unroll
-    for (int k = 0; k < kKX; ++k) timint(kOffVor, k, vordt[k]);
-#pragma unroll
-    for (int k = 0; k < kKX; ++k) timint(kOffDiv, k, divdt[k]);
-#pragma unroll
-    for (int k = 0; k < kKX; ++k) timint(kOffT, k, tdt[k]);
-#pragma unroll
-    for (int k = 0; k < kKX; ++k) timint(kOffTr, k, trdt[k]);
+    if (k == 0) timint(kOffPs, 0, psdt);
+    timint(kOffVor, k, vordt);
+    timint(kOffDiv, k, divdt);
+    timint(kOffT, k, tdt);
+    timint(kOffTr, k, trdt);
 }
 
 template <typename T>
@@ -573,7 +552,7 @@ int launch_step(sml_dynamics *d, int j1, int j2, double dt, double alph, double 
     SML_HIP(hipGetLastError());
     // 4. sptend / implic / diffusion / time integration
     const int j4 = (alph == 0.0) ? j2 : 1;
-    hipLaunchKernelGGL(k_dyn_tail, dim3((2 * kMN + 127) / 128), dim3(128), 0, st, d->d_state, d->d_tend, d->d_phi,
+    hipLaunchKernelGGL(k_dyn_tail, dim3(kSF / kTailC), dim3(kTailC * kKX), 0, st, d->d_state, d->d_tend, d->d_phi,
                        d->d_phis, d->d_tcorh, d->d_qcorh, T, j1, j4, dt, alph, rob, wil);
     SML_HIP(hipGetLastError());
     return SML_OK;

@@ -101,76 +101,57 @@ __global__ __launch_bounds__(64) void k_gridy(const double *__restrict__ spec, d
     }
 }
 
-// gridx: varm[f][lat][62] -> grid[f][lat][96]  (one block of 6 waves per field;
-// wave w owns longitudes 16w..16w+15 for all 48 latitudes)
-__global__ __launch_bounds__(384) void k_gridx(const double *__restrict__ varm, double *__restrict__ grid,
-                                               const double *__restrict__ dinv, const double *__restrict__ cosgr,
-                                               int kcos) {
+// gridx: varm[f][lat][62] -> grid[f][lat][96]  (one wave per (field, 16-latitude
+// group g, 16-longitude tile w): blockIdx.x = field, blockIdx.y = 3 w + g)
+__global__ __launch_bounds__(64) void k_gridx(const double *__restrict__ varm, double *__restrict__ grid,
+                                              const double *__restrict__ dinv, const double *__restrict__ cosgr,
+                                              int kcos) {
     const int f = blockIdx.x;
-    const int w = threadIdx.x >> 6, l = threadIdx.x & 63, r = l & 15, kk = l >> 4;
-    const double *vr = varm + (size_t)f * kVarmField;
-    d4 acc0 = {0, 0, 0, 0}, acc1 = acc0, acc2 = acc0;
-#pragma unroll 4
+    const int w = blockIdx.y / 3, j0 = 16 * (blockIdx.y % 3);
+    const int l = threadIdx.x, r = l & 15, kk = l >> 4;
+    const double *vr = varm + (size_t)f * kVarmField + (j0 + r) * kMX2;
+    d4 acc = {0, 0, 0, 0};
+#pragma unroll 8
     for (int s = 0; s < kCPad / 4; ++s) {
         const int c = 4 * s + kk;
         const double b = dinv[c * kIX + 16 * w + r];
-        const bool cv = c < kMX2;
-        const double a0 = cv ? vr[r * kMX2 + c] : 0.0;
-        const double a1 = cv ? vr[(16 + r) * kMX2 + c] : 0.0;
-        const double a2 = cv ? vr[(32 + r) * kMX2 + c] : 0.0;
-        acc0 = MFMA64(a0, b, acc0);
-        acc1 = MFMA64(a1, b, acc1);
-        acc2 = MFMA64(a2, b, acc2);
+        const double a = c < kMX2 ? vr[c] : 0.0;
+        acc = MFMA64(a, b, acc);
     }
     double *g = grid + (size_t)f * kGridField + 16 * w + r;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-        const int j0 = kk + 4 * q;
-        double v0 = acc0[q], v1 = acc1[q], v2 = acc2[q];
-        if (kcos != 1) {
-            v0 = v0 * cosgr[j0];
-            v1 = v1 * cosgr[16 + j0];
-            v2 = v2 * cosgr[32 + j0];
-        }
-        g[j0 * kIX] = v0;
-        g[(16 + j0) * kIX] = v1;
-        g[(32 + j0) * kIX] = v2;
+        const int j = j0 + kk + 4 * q;
+        double v = acc[q];
+        if (kcos != 1) v = v * cosgr[j];
+        g[j * kIX] = v;
     }
 }
 
 // specx: grid[f][lat][96] (optionally x scale[lat]) -> varm[f][lat][62]
-// (one block of 4 waves per field; wave w owns coefficients 16w..16w+15)
-__global__ __launch_bounds__(256) void k_specx(const double *__restrict__ grid, double *__restrict__ varm,
-                                               const double *__restrict__ dfwd, const double *__restrict__ scale) {
+// (one wave per (field, 16-latitude group g, 16-coefficient tile w):
+// blockIdx.x = field, blockIdx.y = 3 w + g)
+__global__ __launch_bounds__(64) void k_specx(const double *__restrict__ grid, double *__restrict__ varm,
+                                              const double *__restrict__ dfwd, const double *__restrict__ scale) {
     const int f = blockIdx.x;
-    const int w = threadIdx.x >> 6, l = threadIdx.x & 63, r = l & 15, kk = l >> 4;
-    const double *g = grid + (size_t)f * kGridField;
-    const double s0 = scale ? scale[r] : 1.0, s1 = scale ? scale[16 + r] : 1.0, s2 = scale ? scale[32 + r] : 1.0;
-    d4 acc0 = {0, 0, 0, 0}, acc1 = acc0, acc2 = acc0;
-#pragma unroll 4
+    const int w = blockIdx.y / 3, j0 = 16 * (blockIdx.y % 3);
+    const int l = threadIdx.x, r = l & 15, kk = l >> 4;
+    const double *g = grid + (size_t)f * kGridField + (j0 + r) * kIX;
+    const double s0 = scale ? scale[j0 + r] : 1.0;
+    d4 acc = {0, 0, 0, 0};
+#pragma unroll 8
     for (int s = 0; s < kIX / 4; ++s) {
         const int i = 4 * s + kk;
         const double b = dfwd[i * kCPad + 16 * w + r];
-        double a0 = g[r * kIX + i], a1 = g[(16 + r) * kIX + i], a2 = g[(32 + r) * kIX + i];
-        if (scale) {  // vdspec's ug*cosgr(j) / ug*cosgr2(j) (spe_spectral.f90:430-445)
-            a0 = a0 * s0;
-            a1 = a1 * s1;
-            a2 = a2 * s2;
-        }
-        acc0 = MFMA64(a0, b, acc0);
-        acc1 = MFMA64(a1, b, acc1);
-        acc2 = MFMA64(a2, b, acc2);
+        double a = g[i];
+        if (scale) a = a * s0;  // vdspec's ug*cosgr(j) / ug*cosgr2(j) (spe_spectral.f90:430-445)
+        acc = MFMA64(a, b, acc);
     }
     const int c = 16 * w + r;
     if (c >= kMX2) return;
     double *vr = varm + (size_t)f * kVarmField + c;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int j0 = kk + 4 * q;
-        vr[j0 * kMX2] = acc0[q];
-        vr[(16 + j0) * kMX2] = acc1[q];
-        vr[(32 + j0) * kMX2] = acc2[q];
-    }
+    for (int q = 0; q < 4; ++q) vr[(j0 + kk + 4 * q) * kMX2] = acc[q];
 }
 
 // specy: varm[f][lat][62] -> spec[f][n][62]  (one wave per (m, 8-field tile));
@@ -405,7 +386,7 @@ extern "C" int sml_gridx_batched(sml_spectral *s, const double *d_varm, double *
                                  void *stream) {
     if (int rc = check_ctx(s, nf)) return rc;
     if (nf == 0) return SML_OK;
-    hipLaunchKernelGGL(k_gridx, dim3(nf), dim3(384), 0, (hipStream_t)stream, d_varm, d_grid, s->d_dinv, s->d_cosgr,
+    hipLaunchKernelGGL(k_gridx, dim3(nf, 18), dim3(64), 0, (hipStream_t)stream, d_varm, d_grid, s->d_dinv, s->d_cosgr,
                        kcos);
     SML_HIP(hipGetLastError());
     return SML_OK;
@@ -414,7 +395,7 @@ extern "C" int sml_gridx_batched(sml_spectral *s, const double *d_varm, double *
 extern "C" int sml_specx_batched(sml_spectral *s, const double *d_grid, double *d_varm, int nf, void *stream) {
     if (int rc = check_ctx(s, nf)) return rc;
     if (nf == 0) return SML_OK;
-    hipLaunchKernelGGL(k_specx, dim3(nf), dim3(256), 0, (hipStream_t)stream, d_grid, d_varm, s->d_dfwd,
+    hipLaunchKernelGGL(k_specx, dim3(nf, 12), dim3(64), 0, (hipStream_t)stream, d_grid, d_varm, s->d_dfwd,
                        (const double *)nullptr);
     SML_HIP(hipGetLastError());
     return SML_OK;
@@ -455,8 +436,8 @@ extern "C" int sml_vdspec_batched(sml_spectral *s, const double *d_ug, const dou
     const double *scale = (kcos == 2) ? s->d_cosgr : s->d_cosgr2;
     double *um = s->d_work, *vm = s->d_work + (size_t)nf * kVarmField;
     double *uc = s->d_work + 2 * s->work_fields * (size_t)kVarmField, *vc = uc + (size_t)nf * kSpecField;
-    hipLaunchKernelGGL(k_specx, dim3(nf), dim3(256), 0, st, d_ug, um, s->d_dfwd, scale);
-    hipLaunchKernelGGL(k_specx, dim3(nf), dim3(256), 0, st, d_vg, vm, s->d_dfwd, scale);
+    hipLaunchKernelGGL(k_specx, dim3(nf, 12), dim3(64), 0, st, d_ug, um, s->d_dfwd, scale);
+    hipLaunchKernelGGL(k_specx, dim3(nf, 12), dim3(64), 0, st, d_vg, vm, s->d_dfwd, scale);
     hipLaunchKernelGGL(k_specy, dim3(kMX, (nf + 7) / 8), dim3(64), 0, st, um, uc, s->d_pfwd, s->d_wt, nf);
     hipLaunchKernelGGL(k_specy, dim3(kMX, (nf + 7) / 8), dim3(64), 0, st, vm, vc, s->d_pfwd, s->d_wt, nf);
     SML_HIP(hipGetLastError());
@@ -543,7 +524,7 @@ int spectral_gridy(sml_spectral *s, const double *spec, double *varm, int nf, hi
 
 int spectral_gridx(sml_spectral *s, const double *varm, double *grid, int nf, int kcos, hipStream_t st) {
     if (nf <= 0) return SML_OK;
-    hipLaunchKernelGGL(k_gridx, dim3(nf), dim3(384), 0, st, varm, grid, s->d_dinv, s->d_cosgr, kcos);
+    hipLaunchKernelGGL(k_gridx, dim3(nf, 18), dim3(64), 0, st, varm, grid, s->d_dinv, s->d_cosgr, kcos);
     SML_HIP(hipGetLastError());
     return SML_OK;
 }
@@ -551,7 +532,7 @@ int spectral_gridx(sml_spectral *s, const double *varm, double *grid, int nf, in
 int spectral_specx(sml_spectral *s, const double *grid, double *varm, int nf, int scale, hipStream_t st) {
     if (nf <= 0) return SML_OK;
     const double *sc = scale == 1 ? s->d_cosgr : scale == 2 ? s->d_cosgr2 : nullptr;
-    hipLaunchKernelGGL(k_specx, dim3(nf), dim3(256), 0, st, grid, varm, s->d_dfwd, sc);
+    hipLaunchKernelGGL(k_specx, dim3(nf, 12), dim3(64), 0, st, grid, varm, s->d_dfwd, sc);
     SML_HIP(hipGetLastError());
     return SML_OK;
 }
