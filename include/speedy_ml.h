@@ -227,6 +227,20 @@ int sml_dyn_step(sml_dynamics *d, int j1, int j2, double dt, double alph, double
  * when (dt, alph, rob, wil, d_phys) change).  impint(dt, alph) must be current. */
 int sml_dyn_leapfrog(sml_dynamics *d, int nsteps, double dt, double alph, double rob, double wil,
                      const double *d_phys, void *stream);
+/* iogrid(30) (src/ppo_iogrid.f90:497-571), the window entry: variables3d
+ * grid4d(4, ix, il, kx) (T, u, v, q) and logp(ix, il), device, are rounded to
+ * real(4), q < 0 set to 0, transformed (vdspec / spec + trunct) into time level 1;
+ * the level is transformed back and d_minmax[8] (device, may be NULL) receives
+ * min/max of u, v, t, q for the safety thresholds (see sml_dyn_is_safe). */
+int sml_dyn_from_grid(sml_dynamics *d, const double *d_grid4d, const double *d_logp, double *d_minmax,
+                      void *stream);
+/* iogrid(31) (src/ppo_iogrid.f90:573-595), the window exit: level 1 -> grid4d, logp */
+int sml_dyn_to_grid(sml_dynamics *d, double *d_grid4d, double *d_logp, void *stream);
+/* is_safe_to_run_speedy from the 8 min/max values (src/ppo_iogrid.f90:556-571) */
+int sml_dyn_is_safe(const double *minmax);
+/* synchronous host-buffer variants */
+int sml_dyn_from_grid_host(sml_dynamics *d, const double *grid4d, const double *logp, double *minmax, int *safe);
+int sml_dyn_to_grid_host(sml_dynamics *d, double *grid4d, double *logp);
 /* synchronous variant taking host physics tendencies (may be NULL) */
 int sml_dyn_step_host(sml_dynamics *d, int j1, int j2, double dt, double alph, double rob, double wil,
                       const double *phys);

@@ -74,6 +74,8 @@ def _declare(L):
     L.orc_dyn_init.argtypes = []
     L.orc_dyn_impint.argtypes = [d, d]
     L.orc_dyn_step.argtypes = [vp] * 9 + [i, i, d, d, d, d, vp, vp]
+    L.orc_iogrid30.argtypes = [vp] * 8
+    L.orc_iogrid31.argtypes = [vp] * 7
 
 
 def spectral_init(radius: float = EARTH_RADIUS) -> None:
@@ -347,6 +349,29 @@ def dyn_step(state, phis, tcorh, qcorh, phys, j1, j2, dt, alph, rob=0.05, wil=0.
                    _p(phis), _p(tcorh), _p(qcorh), None if ph is None else _p(ph), j1, j2, dt, alph, rob, wil,
                    _p(phi), _p(tend))
     return phi, tend
+
+
+def iogrid30(state, grid4d, logp):
+    """iogrid(30): window entry into level 1 of `state` (in place); returns
+    (minmax[8], is_safe).  grid4d: variables3d (4, 96, 48, 8) Fortran order ==
+    C (8, 48, 96, 4); logp (48, 96)."""
+    spectral_init()
+    g = np.ascontiguousarray(grid4d, dtype=np.float64)
+    lp = np.ascontiguousarray(logp, dtype=np.float64)
+    mm = np.zeros(8)
+    safe = lib().orc_iogrid30(_p(g), _p(lp), _p(state["vor"]), _p(state["div"]), _p(state["t"]), _p(state["ps"]),
+                              _p(state["tr"]), _p(mm))
+    return mm, bool(safe)
+
+
+def iogrid31(state):
+    """iogrid(31): level 1 of `state` -> (grid4d (8, 48, 96, 4), logp (48, 96))."""
+    spectral_init()
+    g = np.zeros((KX, IL, IX, 4))
+    lp = np.zeros((IL, IX))
+    lib().orc_iogrid31(_p(state["vor"]), _p(state["div"]), _p(state["t"]), _p(state["ps"]), _p(state["tr"]),
+                       _p(g), _p(lp))
+    return g, lp
 
 
 # ---------------------------------------------------------------- reference (pinning only)

@@ -1270,3 +1270,94 @@ void orc_dyn_step(double *vor, double *div, double *t, double *ps, double *tr, c
     orc_timint(j1, dt, eps, wil, KX, t, tdt);
     orc_timint(j1, dt, eps, wil, KX, tr, trdt);
 }
+
+/* ------------------------------------------------------------------------- */
+/* SPEEDY window entry / exit: iogrid(30) / iogrid(31) (ppo_iogrid.f90:497-601) */
+/* grid4d = variables3d(4, ix, il, kx) (var = T, u, v, q), logp(ix, il).       */
+/* Pinning: ppo_iogrid.f90 needs mpires/mod_utilities (MPI) and is not built   */
+/* here; these two routines are compositions of vdspec/spec/trunct/uvspec/grid, */
+/* each pinned to the reference by the spectral fixtures.                     */
+/* ------------------------------------------------------------------------- */
+#define G4I(v, i, j, k) ((v) + 4 * ((i) + IX * ((j) + IL * (k))))
+
+/* spectral state level 1 -> gridded T, u, v, q, logp (iogrid(31), :573-595) */
+static void orc_state_to_grid(const double *vor, const double *div, const double *t, const double *ps,
+                              const double *tr, double *ugr, double *vgr, double *tgr, double *qgr, double *psgr)
+{
+    static double ucos[SF], vcos[SF];
+    for (int k = 0; k < KX; ++k) {
+        orc_uvspec(vor + k * SF, div + k * SF, ucos, vcos);
+        orc_grid(ucos, ugr + k * GF, 2);
+        orc_grid(vcos, vgr + k * GF, 2);
+    }
+    for (int k = 0; k < KX; ++k) {
+        orc_grid(t + k * SF, tgr + k * GF, 1);
+        orc_grid(tr + k * SF, qgr + k * GF, 1);
+    }
+    orc_grid(ps, psgr, 1);
+}
+
+/* iogrid(30): writes level 1 of vor/div/t/tr/ps; minmax[8] = min/max of the
+ * re-gridded u, v, t, q; returns is_safe_to_run_speedy (:556-571) */
+int orc_iogrid30(const double *grid4d, const double *logp, double *vor, double *div, double *t, double *ps,
+                 double *tr, double *minmax)
+{
+    static double ugr[KX * GF], vgr[KX * GF], tgr[KX * GF], qgr[KX * GF], psgr[GF];
+    for (int k = 0; k < KX; ++k)
+        for (int j = 0; j < IL; ++j)
+            for (int i = 0; i < IX; ++i) {
+                int g = k * GF + j * IX + i;
+                /* real(4) copies (:503-511), q < 0 -> 0 on the real(4) copy (:516-518) */
+                tgr[g] = (double)(float)grid4d[G4I(0, i, j, k)];
+                ugr[g] = (double)(float)grid4d[G4I(1, i, j, k)];
+                vgr[g] = (double)(float)grid4d[G4I(2, i, j, k)];
+                float q4 = (float)grid4d[G4I(3, i, j, k)];
+                if (q4 < 0.0f) q4 = 0.0f;
+                qgr[g] = (double)q4;
+            }
+    for (int g = 0; g < GF; ++g) psgr[g] = (double)(float)logp[g];
+    for (int k = 0; k < KX; ++k) {
+        orc_vdspec(ugr + k * GF, vgr + k * GF, vor + k * SF, div + k * SF, 2);
+        orc_spec(tgr + k * GF, t + k * SF);
+        orc_spec(qgr + k * GF, tr + k * SF);
+        orc_trunct(vor + k * SF);
+        orc_trunct(div + k * SF);
+        orc_trunct(t + k * SF);
+        orc_trunct(tr + k * SF);
+    }
+    orc_spec(psgr, ps);
+    orc_trunct(ps);
+    orc_state_to_grid(vor, div, t, ps, tr, ugr, vgr, tgr, qgr, psgr);
+    const double *f[4] = {ugr, vgr, tgr, qgr};
+    for (int v = 0; v < 4; ++v) {
+        double mn = f[v][0], mxv = f[v][0];
+        for (int g = 1; g < KX * GF; ++g) {
+            if (f[v][g] < mn) mn = f[v][g];
+            if (f[v][g] > mxv) mxv = f[v][g];
+        }
+        minmax[2 * v] = mn;
+        minmax[2 * v + 1] = mxv;
+    }
+    if (minmax[0] < -150.0 || minmax[1] > 150.0) return 0;
+    if (minmax[2] < -120.0 || minmax[3] > 120.0) return 0;
+    if (minmax[4] < 160.0 || minmax[5] > 330.0) return 0;
+    if (minmax[6] < -6.0 || minmax[7] > 30.0) return 0;
+    return 1;
+}
+
+/* iogrid(31): level 1 of the spectral state -> grid4d / logp (:573-595) */
+void orc_iogrid31(const double *vor, const double *div, const double *t, const double *ps, const double *tr,
+                  double *grid4d, double *logp)
+{
+    static double ugr[KX * GF], vgr[KX * GF], tgr[KX * GF], qgr[KX * GF];
+    orc_state_to_grid(vor, div, t, ps, tr, ugr, vgr, tgr, qgr, logp);
+    for (int k = 0; k < KX; ++k)
+        for (int j = 0; j < IL; ++j)
+            for (int i = 0; i < IX; ++i) {
+                int g = k * GF + j * IX + i;
+                grid4d[G4I(0, i, j, k)] = tgr[g];
+                grid4d[G4I(1, i, j, k)] = ugr[g];
+                grid4d[G4I(2, i, j, k)] = vgr[g];
+                grid4d[G4I(3, i, j, k)] = qgr[g];
+            }
+}

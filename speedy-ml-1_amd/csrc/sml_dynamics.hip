@@ -62,6 +62,8 @@ struct sml_dynamics {
     double *d_specin = nullptr, *d_varm = nullptr, *d_grid = nullptr, *d_gfwd = nullptr, *d_sfwd = nullptr;
     double *d_tend = nullptr;
     double *d_phys = nullptr;  // staging for host-provided physics tendencies
+    double *d_minmax = nullptr;  // iogrid(30) safety check: min/max of u, v, t, q
+    double *d_io = nullptr;      // staging for the host iogrid calls (grid4d + logp)
     bool impint_done = false;
     // leapfrog replay: one step(2, 2, ...) captured as a hipGraph
     hipStream_t cap_stream = nullptr;
@@ -71,6 +73,34 @@ struct sml_dynamics {
 };
 
 namespace {
+
+// uvspec(vor, div) -> (ucos, vcos) at coefficient (m, n), both parts
+// (spe_spectral.f90:351-387)
+__device__ inline void uvspec_at(const double *vor, const double *div, const DynTables *T, int m, int n, double *uc,
+                                 double *vc) {
+    const double ux = T->uvdx[n][m];
+    double zp[2], zc[2];
+    zp[1] = ux * vor[ci(0, m, n)];
+    zp[0] = -ux * vor[ci(1, m, n)];
+    zc[1] = ux * div[ci(0, m, n)];
+    zc[0] = -ux * div[ci(1, m, n)];
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+        double a, b;
+        if (n == 0) {
+            a = zc[p] - T->uvdyp[0][m] * vor[ci(p, m, 1)];
+            b = zp[p] + T->uvdyp[0][m] * div[ci(p, m, 1)];
+        } else if (n == kNX - 1) {
+            a = T->uvdym[n][m] * vor[ci(p, m, kNTRUN1 - 1)];
+            b = -T->uvdym[n][m] * div[ci(p, m, kNTRUN1 - 1)];
+        } else {
+            b = -T->uvdym[n][m] * div[ci(p, m, n - 1)] + T->uvdyp[n][m] * div[ci(p, m, n + 1)] + zp[p];
+            a = T->uvdym[n][m] * vor[ci(p, m, n - 1)] - T->uvdyp[n][m] * vor[ci(p, m, n + 1)] + zc[p];
+        }
+        uc[ci(p, m, n)] = a;
+        vc[ci(p, m, n)] = b;
+    }
+}
 
 // ---------------------------------------------------------------- kernels
 // prep: inputs of the 50 inverse transforms, [vor 8 | div 8 | t 8 | tr 8 | ucos 8 |
@@ -93,30 +123,7 @@ __global__ void k_dyn_prep(const double *__restrict__ st, double *__restrict__ s
             sin_[(size_t)(2 * kKX + k) * kSF + c] = t[c];
             sin_[(size_t)(3 * kKX + k) * kSF + c] = tr[c];
         }
-        // uvspec(vor, div) -> (ucos, vcos)  (spe_spectral.f90:351-387)
-        const double ux = T->uvdx[n][m];
-        double zp[2], zc[2];
-        zp[1] = ux * vor[ci(0, m, n)];
-        zp[0] = -ux * vor[ci(1, m, n)];
-        zc[1] = ux * div[ci(0, m, n)];
-        zc[0] = -ux * div[ci(1, m, n)];
-        double *uc = sin_ + (size_t)(4 * kKX + k) * kSF, *vc = sin_ + (size_t)(5 * kKX + k) * kSF;
-#pragma unroll
-        for (int p = 0; p < 2; ++p) {
-            double a, b;
-            if (n == 0) {
-                a = zc[p] - T->uvdyp[0][m] * vor[ci(p, m, 1)];
-                b = zp[p] + T->uvdyp[0][m] * div[ci(p, m, 1)];
-            } else if (n == kNX - 1) {
-                a = T->uvdym[n][m] * vor[ci(p, m, kNTRUN1 - 1)];
-                b = -T->uvdym[n][m] * div[ci(p, m, kNTRUN1 - 1)];
-            } else {
-                b = -T->uvdym[n][m] * div[ci(p, m, n - 1)] + T->uvdyp[n][m] * div[ci(p, m, n + 1)] + zp[p];
-                a = T->uvdym[n][m] * vor[ci(p, m, n - 1)] - T->uvdyp[n][m] * vor[ci(p, m, n + 1)] + zc[p];
-            }
-            uc[ci(p, m, n)] = a;
-            vc[ci(p, m, n)] = b;
-        }
+        uvspec_at(vor, div, T, m, n, sin_ + (size_t)(4 * kKX + k) * kSF, sin_ + (size_t)(5 * kKX + k) * kSF);
     } else {
         // grad(ps(j2)) -> (psdx, psdy)  (spe_spectral.f90:271-305)
         const double *ps = st + kOffPs + (size_t)(j2 - 1) * kSF;
@@ -410,6 +417,112 @@ __global__ __launch_bounds__(256) void k_dyn_tail(double *__restrict__ st, doubl
     timint(kOffTr, k, trdt);
 }
 
+// ------------------------------------------------------------ iogrid(30/31)
+// ppo_iogrid.f90:497-601.  grid4d = variables3d(4, ix, il, kx) (T, u, v, q), logp(ix, il).
+// Field-major work layout of both directions: [u 8 | v 8 | t 8 | q 8 | ps] (33 fields).
+constexpr int kNIo = 4 * kKX + 1;
+constexpr int kNIoWind = 2 * kKX;
+
+__device__ inline int g4i(int v, int pt, int k) { return v + 4 * (pt + kGF * k); }
+
+// entry: real(4) copies (:503-511), q < 0 -> 0 on the real(4) copy (:516-518)
+__global__ void k_io_gather(const double *__restrict__ g4, const double *__restrict__ logp, double *__restrict__ F) {
+    const int pt = blockIdx.x * blockDim.x + threadIdx.x;
+    if (pt >= kGF) return;
+    const int k = blockIdx.y;
+    const double *src = g4 + g4i(0, pt, k);
+    F[(size_t)(2 * kKX + k) * kGF + pt] = (double)(float)src[0];
+    F[(size_t)k * kGF + pt] = (double)(float)src[1];
+    F[(size_t)(kKX + k) * kGF + pt] = (double)(float)src[2];
+    float q4 = (float)src[3];
+    if (q4 < 0.0f) q4 = 0.0f;
+    F[(size_t)(3 * kKX + k) * kGF + pt] = (double)q4;
+    if (k == 0) F[(size_t)(4 * kKX) * kGF + pt] = (double)(float)logp[pt];
+}
+
+// entry: vdspec's vds + spec, trunct, into time level 1 (:524-538)
+__global__ void k_io_combine(const double *__restrict__ S, double *__restrict__ st, const DynTables *__restrict__ T) {
+    const int mn = blockIdx.x * blockDim.x + threadIdx.x;
+    if (mn >= kMN) return;
+    const int k = blockIdx.y;
+    const int m = mn % kMX, n = mn / kMX;
+    const double trf = T->trfilt[n][m];
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+        const int c = ci(p, m, n);
+        double vo, dv;
+        vds_at(S + (size_t)k * kSF, S + (size_t)(kKX + k) * kSF, T, m, n, p, &vo, &dv);
+        st[kOffVor + (size_t)k * kSF + c] = vo * trf;
+        st[kOffDiv + (size_t)k * kSF + c] = dv * trf;
+        st[kOffT + (size_t)k * kSF + c] = S[(size_t)(2 * kKX + k) * kSF + c] * trf;
+        st[kOffTr + (size_t)k * kSF + c] = S[(size_t)(3 * kKX + k) * kSF + c] * trf;
+        if (k == 0) st[kOffPs + c] = S[(size_t)(4 * kKX) * kSF + c] * trf;
+    }
+}
+
+// both directions: inverse-transform inputs from level 1 (:541-553 / :576-589):
+// [ucos 8 | vcos 8 | t 8 | q 8 | ps]
+__global__ void k_io_prep(const double *__restrict__ st, double *__restrict__ sin_, const DynTables *__restrict__ T) {
+    const int mn = blockIdx.x * blockDim.x + threadIdx.x;
+    if (mn >= kMN) return;
+    const int k = blockIdx.y;
+    const int m = mn % kMX, n = mn / kMX;
+    const double *vor = st + kOffVor + (size_t)k * kSF, *div = st + kOffDiv + (size_t)k * kSF;
+    uvspec_at(vor, div, T, m, n, sin_ + (size_t)k * kSF, sin_ + (size_t)(kKX + k) * kSF);
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+        const int c = ci(p, m, n);
+        sin_[(size_t)(2 * kKX + k) * kSF + c] = st[kOffT + (size_t)k * kSF + c];
+        sin_[(size_t)(3 * kKX + k) * kSF + c] = st[kOffTr + (size_t)k * kSF + c];
+        if (k == 0) sin_[(size_t)(4 * kKX) * kSF + c] = st[kOffPs + c];
+    }
+}
+
+// exit: grid fields -> variables3d / logp (:590-595)
+__global__ void k_io_scatter(const double *__restrict__ G, double *__restrict__ g4, double *__restrict__ logp) {
+    const int pt = blockIdx.x * blockDim.x + threadIdx.x;
+    if (pt >= kGF) return;
+    const int k = blockIdx.y;
+    double *dst = g4 + g4i(0, pt, k);
+    dst[0] = G[(size_t)(2 * kKX + k) * kGF + pt];
+    dst[1] = G[(size_t)k * kGF + pt];
+    dst[2] = G[(size_t)(kKX + k) * kGF + pt];
+    dst[3] = G[(size_t)(3 * kKX + k) * kGF + pt];
+    if (k == 0) logp[pt] = G[(size_t)(4 * kKX) * kGF + pt];
+}
+
+// entry safety check (:556-571): min / max of the re-gridded u, v, t, q.  One
+// block of 1024 threads per variable.
+__global__ __launch_bounds__(1024) void k_io_minmax(const double *__restrict__ G, double *__restrict__ mm) {
+    __shared__ double smin[16], smax[16];
+    const int v = blockIdx.x;
+    const double *f = G + (size_t)v * kKX * kGF;
+    double lo = f[threadIdx.x], hi = lo;
+    for (int i = threadIdx.x; i < kKX * kGF; i += blockDim.x) {
+        lo = fmin(lo, f[i]);
+        hi = fmax(hi, f[i]);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        lo = fmin(lo, __shfl_xor(lo, o));
+        hi = fmax(hi, __shfl_xor(hi, o));
+    }
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        smin[w] = lo;
+        smax[w] = hi;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int i = 1; i < 16; ++i) {
+            lo = fmin(lo, smin[i]);
+            hi = fmax(hi, smax[i]);
+        }
+        mm[2 * v] = lo;
+        mm[2 * v + 1] = hi;
+    }
+}
+
 template <typename T>
 int dalloc(T **p, size_t count) {
     *p = nullptr;
@@ -424,7 +537,7 @@ int dalloc(T **p, size_t count) {
 extern "C" int sml_dyn_destroy(sml_dynamics *d) {
     if (!d) return SML_OK;
     void *ptrs[] = {d->d_tab, d->d_state, d->d_phis, d->d_tcorh, d->d_qcorh, d->d_phi, d->d_specin,
-                    d->d_varm, d->d_grid, d->d_gfwd, d->d_sfwd, d->d_tend, d->d_phys};
+                    d->d_varm, d->d_grid, d->d_gfwd, d->d_sfwd, d->d_tend, d->d_phys, d->d_minmax, d->d_io};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     if (d->graph) (void)hipGraphExecDestroy(d->graph);
@@ -450,7 +563,8 @@ extern "C" int sml_dyn_create(double radius, sml_dynamics **out) {
         (rc = dalloc(&d->d_specin, (size_t)kNInv * kSF)) || (rc = dalloc(&d->d_varm, (size_t)kNFwd * kVF)) ||
         (rc = dalloc(&d->d_grid, (size_t)kNInv * kGF)) || (rc = dalloc(&d->d_gfwd, (size_t)kNFwd * kGF)) ||
         (rc = dalloc(&d->d_sfwd, (size_t)kNFwd * kSF)) || (rc = dalloc(&d->d_tend, kTendSize)) ||
-        (rc = dalloc(&d->d_phys, (size_t)4 * kKX * kGF))) {
+        (rc = dalloc(&d->d_phys, (size_t)4 * kKX * kGF)) || (rc = dalloc(&d->d_minmax, 8)) ||
+        (rc = dalloc(&d->d_io, (size_t)4 * kKX * kGF + kGF))) {
         sml_dyn_destroy(d);
         return rc;
     }
@@ -599,6 +713,82 @@ extern "C" int sml_dyn_leapfrog(sml_dynamics *d, int nsteps, double dt, double a
         d->g_phys = d_phys;
     }
     for (int i = 0; i < nsteps; ++i) SML_HIP(hipGraphLaunch(d->graph, (hipStream_t)stream));
+    return SML_OK;
+}
+
+namespace {
+
+// iogrid inverse half: level 1 -> G = [u 8 | v 8 | t 8 | q 8 | ps] grids
+int io_to_grid_fields(sml_dynamics *d, hipStream_t st) {
+    const DynTables *T = d->d_tab;
+    hipLaunchKernelGGL(k_io_prep, dim3((kMN + 127) / 128, kKX), dim3(128), 0, st, d->d_state, d->d_specin, T);
+    SML_HIP(hipGetLastError());
+    if (int rc = spectral_gridy(d->sp, d->d_specin, d->d_varm, kNIo, st)) return rc;
+    if (int rc = spectral_gridx(d->sp, d->d_varm, d->d_grid, kNIoWind, 2, st)) return rc;
+    return spectral_gridx(d->sp, d->d_varm + (size_t)kNIoWind * kVF, d->d_grid + (size_t)kNIoWind * kGF,
+                          kNIo - kNIoWind, 1, st);
+}
+
+}  // namespace
+
+extern "C" int sml_dyn_from_grid(sml_dynamics *d, const double *d_grid4d, const double *d_logp, double *d_minmax,
+                                 void *stream) {
+    SML_REQUIRE(d && d_grid4d && d_logp, "null argument");
+    hipStream_t st = (hipStream_t)stream;
+    const DynTables *T = d->d_tab;
+    hipLaunchKernelGGL(k_io_gather, dim3((kGF + 255) / 256, kKX), dim3(256), 0, st, d_grid4d, d_logp, d->d_gfwd);
+    SML_HIP(hipGetLastError());
+    if (int rc = spectral_specx(d->sp, d->d_gfwd, d->d_varm, kNIoWind, 1, st)) return rc;  // vdspec kcos = 2
+    if (int rc = spectral_specx(d->sp, d->d_gfwd + (size_t)kNIoWind * kGF, d->d_varm + (size_t)kNIoWind * kVF,
+                                kNIo - kNIoWind, 0, st))
+        return rc;
+    if (int rc = spectral_specy(d->sp, d->d_varm, d->d_sfwd, kNIo, st)) return rc;
+    hipLaunchKernelGGL(k_io_combine, dim3((kMN + 127) / 128, kKX), dim3(128), 0, st, d->d_sfwd, d->d_state, T);
+    SML_HIP(hipGetLastError());
+    if (int rc = io_to_grid_fields(d, st)) return rc;
+    hipLaunchKernelGGL(k_io_minmax, dim3(4), dim3(1024), 0, st, d->d_grid, d_minmax ? d_minmax : d->d_minmax);
+    SML_HIP(hipGetLastError());
+    return SML_OK;
+}
+
+extern "C" int sml_dyn_to_grid(sml_dynamics *d, double *d_grid4d, double *d_logp, void *stream) {
+    SML_REQUIRE(d && d_grid4d && d_logp, "null argument");
+    hipStream_t st = (hipStream_t)stream;
+    if (int rc = io_to_grid_fields(d, st)) return rc;
+    hipLaunchKernelGGL(k_io_scatter, dim3((kGF + 255) / 256, kKX), dim3(256), 0, st, d->d_grid, d_grid4d, d_logp);
+    SML_HIP(hipGetLastError());
+    return SML_OK;
+}
+
+extern "C" int sml_dyn_is_safe(const double *minmax) {
+    if (!minmax) return 0;
+    if (minmax[0] < -150.0 || minmax[1] > 150.0) return 0;  // u
+    if (minmax[2] < -120.0 || minmax[3] > 120.0) return 0;  // v
+    if (minmax[4] < 160.0 || minmax[5] > 330.0) return 0;   // t
+    if (minmax[6] < -6.0 || minmax[7] > 30.0) return 0;     // q
+    return 1;
+}
+
+extern "C" int sml_dyn_from_grid_host(sml_dynamics *d, const double *grid4d, const double *logp, double *minmax,
+                                      int *safe) {
+    SML_REQUIRE(d && grid4d && logp, "null argument");
+    const size_t n4 = (size_t)4 * kKX * kGF;
+    SML_HIP(hipMemcpy(d->d_io, grid4d, n4 * 8, hipMemcpyHostToDevice));
+    SML_HIP(hipMemcpy(d->d_io + n4, logp, kGF * 8, hipMemcpyHostToDevice));
+    if (int rc = sml_dyn_from_grid(d, d->d_io, d->d_io + n4, d->d_minmax, nullptr)) return rc;
+    double mm[8];
+    SML_HIP(hipMemcpy(mm, d->d_minmax, sizeof mm, hipMemcpyDeviceToHost));
+    if (minmax) std::memcpy(minmax, mm, sizeof mm);
+    if (safe) *safe = sml_dyn_is_safe(mm);
+    return SML_OK;
+}
+
+extern "C" int sml_dyn_to_grid_host(sml_dynamics *d, double *grid4d, double *logp) {
+    SML_REQUIRE(d && grid4d && logp, "null argument");
+    const size_t n4 = (size_t)4 * kKX * kGF;
+    if (int rc = sml_dyn_to_grid(d, d->d_io, d->d_io + n4, nullptr)) return rc;
+    SML_HIP(hipMemcpy(grid4d, d->d_io, n4 * 8, hipMemcpyDeviceToHost));
+    SML_HIP(hipMemcpy(logp, d->d_io + n4, kGF * 8, hipMemcpyDeviceToHost));
     return SML_OK;
 }
 

@@ -32,7 +32,8 @@ EXPORTED = (
     "sml_nc_read_region", "sml_nc_write_region",
     "sml_dyn_create", "sml_dyn_destroy", "sml_dyn_impint", "sml_dyn_set_forcing", "sml_dyn_set_state",
     "sml_dyn_get_state", "sml_dyn_get_phi", "sml_dyn_get_tendencies", "sml_dyn_state_device",
-    "sml_dyn_step", "sml_dyn_step_host", "sml_dyn_leapfrog",
+    "sml_dyn_step", "sml_dyn_step_host", "sml_dyn_leapfrog", "sml_dyn_from_grid", "sml_dyn_to_grid",
+    "sml_dyn_is_safe", "sml_dyn_from_grid_host", "sml_dyn_to_grid_host",
 )
 
 
@@ -116,6 +117,11 @@ def _declare(L: ctypes.CDLL) -> None:
         "sml_dyn_step": [vp, i, i, d, d, d, d, vp, vp],
         "sml_dyn_step_host": [vp, i, i, d, d, d, d, vp],
         "sml_dyn_leapfrog": [vp, i, d, d, d, d, vp, vp],
+        "sml_dyn_from_grid": [vp, vp, vp, vp, vp],
+        "sml_dyn_to_grid": [vp, vp, vp, vp],
+        "sml_dyn_is_safe": [vp],
+        "sml_dyn_from_grid_host": [vp, vp, vp, vp, ctypes.POINTER(ctypes.c_int)],
+        "sml_dyn_to_grid_host": [vp, vp, vp],
     }
     for name, args in sig.items():
         fn = getattr(L, name)

@@ -101,6 +101,34 @@ class Dynamics:
                 raise ValueError("phys must be a contiguous float64 CUDA tensor (4, 8, 48, 96)")
             check(lib().sml_dyn_step(self._h, j1, j2, dt, alph, rob, wil, ptr(phys), stream_ptr(stream)))
 
+    def from_grid(self, grid4d, logp):
+        """iogrid(30) (ppo_iogrid.f90:497-571): window entry from variables3d
+        (4, 96, 48, 8) Fortran order == C (8, 48, 96, 4), and logp (48, 96).
+        Host numpy -> synchronous, returns (minmax[8], is_safe); device tensors ->
+        asynchronous, returns None (min/max left on the device)."""
+        if isinstance(grid4d, np.ndarray):
+            g = np.ascontiguousarray(grid4d, dtype=np.float64)
+            lp = np.ascontiguousarray(logp, dtype=np.float64)
+            if g.size != 4 * KX * 4608 or lp.size != 4608:
+                raise ValueError("grid4d must hold 4*96*48*8 values and logp 96*48")
+            mm = np.zeros(8)
+            safe = ctypes.c_int(0)
+            check(lib().sml_dyn_from_grid_host(self._h, ptr(g), ptr(lp), ptr(mm), ctypes.byref(safe)))
+            return mm, bool(safe.value)
+        check(lib().sml_dyn_from_grid(self._h, ptr(grid4d), ptr(logp), None, None))
+        return None
+
+    def to_grid(self, grid4d=None, logp=None):
+        """iogrid(31) (ppo_iogrid.f90:573-595): level 1 -> (grid4d, logp).  With
+        device tensors given, fills them asynchronously; else returns host arrays."""
+        if grid4d is not None:
+            check(lib().sml_dyn_to_grid(self._h, ptr(grid4d), ptr(logp), None))
+            return grid4d, logp
+        g = np.zeros((KX, 48, 96, 4))
+        lp = np.zeros((48, 96))
+        check(lib().sml_dyn_to_grid_host(self._h, ptr(g), ptr(lp)))
+        return g, lp
+
     def stepone(self, delt: float = DELT, alph: float = ALPH, phys=None):
         """ini_stepone.f90:19-34 for istart = 0: forward half step, first leapfrog."""
         self.step(1, 1, 0.5 * delt, alph, phys=phys)

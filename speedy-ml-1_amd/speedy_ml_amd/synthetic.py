@@ -135,7 +135,8 @@ def _spectral_field(rng, amp, power, mean=0.0):
 def dyn_state(seed: int = 2025):
     """Seeded T30L8 spectral state (mod_dynvar layout, both time levels) around the
     reference temperature profile tref (ini_impint.f90:43-49), plus forcing
-    (phis, tcorh, qcorh).  Same construction as tests/golden/make_dyn_golden.py."""
+    (phis, tcorh, qcorh).  Same construction as tests/golden/make_dyn_golden.py with
+    weaker, redder vorticity and divergence (winds within the iogrid(30) limits)."""
     rng = np.random.default_rng(seed)
     hsg = np.array([0.000, 0.050, 0.140, 0.260, 0.420, 0.600, 0.770, 0.900, 1.000])
     fsg = 0.5 * (hsg[1:] + hsg[:-1])
@@ -144,8 +145,8 @@ def dyn_state(seed: int = 2025):
     st = {f: np.zeros((2, 8, 32, 31), np.complex128) for f in ("vor", "div", "t", "tr")}
     st["ps"] = np.zeros((2, 32, 31), np.complex128)
     for k in range(8):
-        st["vor"][0, k] = _spectral_field(rng, 2e-5, 1.0)
-        st["div"][0, k] = _spectral_field(rng, 2e-6, 1.0)
+        st["vor"][0, k] = _spectral_field(rng, 6e-6, 1.5)
+        st["div"][0, k] = _spectral_field(rng, 6e-7, 1.5)
         st["t"][0, k] = _spectral_field(rng, 2.0, 1.0, mean=tref[k])
         qm = 12.0 * fsg[k] ** 3
         st["tr"][0, k] = _spectral_field(rng, 0.2 * qm, 1.5, mean=qm)

@@ -128,3 +128,55 @@ def test_leapfrog_graph_matches_step_loop(dyn, dyn_golden):
     b = dyn.get_state()
     for f in oracle.DYN_FIELDS:
         np.testing.assert_array_equal(a[f], b[f])
+
+
+def test_iogrid_exit_matches_oracle(dyn):
+    from speedy_ml_amd.synthetic import dyn_state
+
+    st, forcing = dyn_state(7)
+    dyn.set_state(st)
+    g4, lp = dyn.to_grid()
+    og4, olp = oracle.iogrid31(oracle.dyn_state_copy(st))
+    for c in range(4):
+        assert _rel(g4[..., c], og4[..., c]) < TOL, c
+    assert _rel(lp, olp) < TOL
+
+
+def test_iogrid_entry_matches_oracle(dyn):
+    from speedy_ml_amd.synthetic import dyn_state
+
+    st, _ = dyn_state(7)
+    og4, olp = oracle.iogrid31(oracle.dyn_state_copy(st))
+    og4 = og4.copy()
+    og4[..., 3] -= 0.3  # exercise the q clip
+    st2, _ = dyn_state(8)  # different level-1/level-2 contents before entry
+    dyn.set_state(st2)
+    mm, safe = dyn.from_grid(og4, olp)
+    got = dyn.get_state()
+    ref = oracle.dyn_state_copy(st2)
+    omm, osafe = oracle.iogrid30(ref, og4, olp)
+    assert safe == osafe
+    np.testing.assert_allclose(mm, omm, rtol=1e-12, atol=1e-12)
+    for f in oracle.DYN_FIELDS:
+        assert _rel(got[f][0], ref[f][0]) < TOL, f
+        np.testing.assert_array_equal(got[f][1], st2[f][1])  # level 2 untouched
+
+
+def test_iogrid_device_entry_flags_unsafe(dyn, cuda):
+    import torch
+    from speedy_ml_amd._lib import lib
+
+    from speedy_ml_amd.synthetic import dyn_state
+
+    st, _ = dyn_state(7)
+    og4, olp = oracle.iogrid31(oracle.dyn_state_copy(st))
+    og4 = og4.copy()
+    og4[3, 20:30, 40:60, 1] = 400.0
+    g = torch.from_numpy(og4).to(cuda)
+    lp = torch.from_numpy(olp).to(cuda)
+    mm = torch.zeros(8, dtype=torch.float64, device=cuda)
+    assert lib().sml_dyn_from_grid(dyn._h, g.data_ptr(), lp.data_ptr(), mm.data_ptr(), None) == 0
+    torch.cuda.synchronize()
+    mmh = mm.cpu().numpy()
+    assert lib().sml_dyn_is_safe(mmh.ctypes.data) == 0
+    assert mmh[1] > 150.0
