@@ -43,6 +43,14 @@
  *                           classic reader for the per-region weight files
  *   sml_nc_write_region  <- write_trained_res (src/mod_reservoir.f90:1701-1736,
  *                           src/mod_io.f90:1247-1496)
+ *   sml_dyn_create       <- indyns (+ parmtr, inifft) (src/ini_indyns.f90:1-128)
+ *   sml_dyn_impint       <- impint (src/ini_impint.f90:1-153, spe_matinv.f90)
+ *   sml_dyn_step         <- step (src/dyn_step.f90:1-128: grtend, sptend, implic,
+ *                           geop, hordif, timint; dyn_grtend.f90, dyn_sptend.f90,
+ *                           dyn_implic.f90, dyn_geop.f90)
+ *   sml_dyn_leapfrog     <- the step(2,2,...) loop of stloop (src/dyn_stloop.f90:43)
+ *   sml_dyn_from_grid    <- iogrid(30) (src/ppo_iogrid.f90:497-571)
+ *   sml_dyn_to_grid      <- iogrid(31) (src/ppo_iogrid.f90:573-595)
  */
 #ifndef SPEEDY_ML_H
 #define SPEEDY_ML_H

@@ -158,6 +158,73 @@ module sml_hip
       type(c_ptr), value :: win, wout, rows, cols, vals, mean, std
       integer(c_int) :: rc
     end function
+
+    ! ------------------------------------------------------------ SPEEDY dynamics
+    !> indyns (+ parmtr/inifft); the state mirrors mod_dynvar (vor, div, t, ps, tr)
+    function sml_dyn_create(radius, ctx) bind(C, name='sml_dyn_create') result(rc)
+      import :: c_double, c_ptr, c_int
+      real(c_double), value :: radius
+      type(c_ptr), intent(out) :: ctx
+      integer(c_int) :: rc
+    end function
+    function sml_dyn_destroy(ctx) bind(C, name='sml_dyn_destroy') result(rc)
+      import :: c_ptr, c_int
+      type(c_ptr), value :: ctx
+      integer(c_int) :: rc
+    end function
+    !> impint(dt, alph) (ini_impint.f90)
+    function sml_dyn_impint(ctx, dt, alph) bind(C, name='sml_dyn_impint') result(rc)
+      import :: c_ptr, c_double, c_int
+      type(c_ptr), value :: ctx
+      real(c_double), value :: dt, alph
+      integer(c_int) :: rc
+    end function
+    !> phis (mod_dynvar), tcorh / qcorh (mod_hdifcon): complex(mx, nx)
+    function sml_dyn_set_forcing(ctx, phis, tcorh, qcorh) bind(C, name='sml_dyn_set_forcing') result(rc)
+      import :: c_ptr, c_double_complex, c_int
+      type(c_ptr), value :: ctx
+      complex(c_double_complex), intent(in) :: phis(*), tcorh(*), qcorh(*)
+      integer(c_int) :: rc
+    end function
+    !> whole mod_dynvar state in / out: vor/div/t(mx,nx,kx,2), ps(mx,nx,2), tr(mx,nx,kx,2,1)
+    function sml_dyn_set_state(ctx, vor, div, t, ps, tr) bind(C, name='sml_dyn_set_state') result(rc)
+      import :: c_ptr, c_double_complex, c_int
+      type(c_ptr), value :: ctx
+      complex(c_double_complex), intent(in) :: vor(*), div(*), t(*), ps(*), tr(*)
+      integer(c_int) :: rc
+    end function
+    function sml_dyn_get_state(ctx, vor, div, t, ps, tr) bind(C, name='sml_dyn_get_state') result(rc)
+      import :: c_ptr, c_double_complex, c_int
+      type(c_ptr), value :: ctx
+      complex(c_double_complex), intent(out) :: vor(*), div(*), t(*), ps(*), tr(*)
+      integer(c_int) :: rc
+    end function
+    !> step(j1, j2, dt, alph, rob, wil) with host physics tendencies
+    !> phys(ix*il, kx, 4) = (utend, vtend, ttend, qtend) of phypar
+    function sml_dyn_step_host(ctx, j1, j2, dt, alph, rob, wil, phys) bind(C, name='sml_dyn_step_host') result(rc)
+      import :: c_ptr, c_int, c_double
+      type(c_ptr), value :: ctx
+      integer(c_int), value :: j1, j2
+      real(c_double), value :: dt, alph, rob, wil
+      real(c_double), intent(in) :: phys(*)
+      integer(c_int) :: rc
+    end function
+    !> iogrid(30) / iogrid(31) on host buffers: grid4d = variables3d(4, ix, il, kx), logp(ix, il)
+    function sml_dyn_from_grid_host(ctx, grid4d, logp, minmax, safe) bind(C, name='sml_dyn_from_grid_host') &
+        result(rc)
+      import :: c_ptr, c_double, c_int
+      type(c_ptr), value :: ctx
+      real(c_double), intent(in) :: grid4d(*), logp(*)
+      real(c_double), intent(out) :: minmax(8)
+      integer(c_int), intent(out) :: safe
+      integer(c_int) :: rc
+    end function
+    function sml_dyn_to_grid_host(ctx, grid4d, logp) bind(C, name='sml_dyn_to_grid_host') result(rc)
+      import :: c_ptr, c_double, c_int
+      type(c_ptr), value :: ctx
+      real(c_double), intent(out) :: grid4d(*), logp(*)
+      integer(c_int) :: rc
+    end function
   end interface
 
 contains

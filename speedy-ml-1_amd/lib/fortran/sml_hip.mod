@@ -1,4 +1,4 @@
-﻿!mod$ v1 sum:92cdc0a217f16dcb
+﻿!mod$ v1 sum:9234fad67527d1cc
 !need$ 0bde2ac47243ead2 i iso_c_binding
 module sml_hip
 use,intrinsic::iso_c_binding,only:c_associated
@@ -273,6 +273,98 @@ type(c_ptr),value::cols
 type(c_ptr),value::vals
 type(c_ptr),value::mean
 type(c_ptr),value::std
+integer(4)::rc
+end
+end interface
+interface
+function sml_dyn_create(radius,ctx) bind(c,name="sml_dyn_create") result(rc)
+import::c_ptr
+real(8),value::radius
+type(c_ptr),intent(out)::ctx
+integer(4)::rc
+end
+end interface
+interface
+function sml_dyn_destroy(ctx) bind(c,name="sml_dyn_destroy") result(rc)
+import::c_ptr
+type(c_ptr),value::ctx
+integer(4)::rc
+end
+end interface
+interface
+function sml_dyn_impint(ctx,dt,alph) bind(c,name="sml_dyn_impint") result(rc)
+import::c_ptr
+type(c_ptr),value::ctx
+real(8),value::dt
+real(8),value::alph
+integer(4)::rc
+end
+end interface
+interface
+function sml_dyn_set_forcing(ctx,phis,tcorh,qcorh) bind(c,name="sml_dyn_set_forcing") result(rc)
+import::c_ptr
+type(c_ptr),value::ctx
+complex(8),intent(in)::phis(1_8:*)
+complex(8),intent(in)::tcorh(1_8:*)
+complex(8),intent(in)::qcorh(1_8:*)
+integer(4)::rc
+end
+end interface
+interface
+function sml_dyn_set_state(ctx,vor,div,t,ps,tr) bind(c,name="sml_dyn_set_state") result(rc)
+import::c_ptr
+type(c_ptr),value::ctx
+complex(8),intent(in)::vor(1_8:*)
+complex(8),intent(in)::div(1_8:*)
+complex(8),intent(in)::t(1_8:*)
+complex(8),intent(in)::ps(1_8:*)
+complex(8),intent(in)::tr(1_8:*)
+integer(4)::rc
+end
+end interface
+interface
+function sml_dyn_get_state(ctx,vor,div,t,ps,tr) bind(c,name="sml_dyn_get_state") result(rc)
+import::c_ptr
+type(c_ptr),value::ctx
+complex(8),intent(out)::vor(1_8:*)
+complex(8),intent(out)::div(1_8:*)
+complex(8),intent(out)::t(1_8:*)
+complex(8),intent(out)::ps(1_8:*)
+complex(8),intent(out)::tr(1_8:*)
+integer(4)::rc
+end
+end interface
+interface
+function sml_dyn_step_host(ctx,j1,j2,dt,alph,rob,wil,phys) bind(c,name="sml_dyn_step_host") result(rc)
+import::c_ptr
+type(c_ptr),value::ctx
+integer(4),value::j1
+integer(4),value::j2
+real(8),value::dt
+real(8),value::alph
+real(8),value::rob
+real(8),value::wil
+real(8),intent(in)::phys(1_8:*)
+integer(4)::rc
+end
+end interface
+interface
+function sml_dyn_from_grid_host(ctx,grid4d,logp,minmax,safe) bind(c,name="sml_dyn_from_grid_host") result(rc)
+import::c_ptr
+type(c_ptr),value::ctx
+real(8),intent(in)::grid4d(1_8:*)
+real(8),intent(in)::logp(1_8:*)
+real(8),intent(out)::minmax(1_8:8_8)
+integer(4),intent(out)::safe
+integer(4)::rc
+end
+end interface
+interface
+function sml_dyn_to_grid_host(ctx,grid4d,logp) bind(c,name="sml_dyn_to_grid_host") result(rc)
+import::c_ptr
+type(c_ptr),value::ctx
+real(8),intent(out)::grid4d(1_8:*)
+real(8),intent(out)::logp(1_8:*)
 integer(4)::rc
 end
 end interface
