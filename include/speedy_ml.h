@@ -253,6 +253,35 @@ int sml_dyn_to_grid_host(sml_dynamics *d, double *grid4d, double *logp);
 int sml_dyn_step_host(sml_dynamics *d, int j1, int j2, double dt, double alph, double rob, double wil,
                       const double *phys);
 
+/* ---------------------------------------------------------------- training */
+/* W_out ridge training for a batch of regions (one vertical level each).
+ *   chunking_matmul  (src/mod_reservoir.f90:1643-1699): G += S S^T, B += T S^T
+ *   fit_chunk_hybrid (src/mod_reservoir.f90:1233-1332) / fit_chunk_ml (:1175-1231):
+ *                    regularisation + mldivide (src/mod_linalg.f90:109-151)
+ * naug[i] = chunk_size_speedy + n (hybrid) or n (ML only); nout = 136.
+ * Device memory: nlocal x npad^2 doubles of Gram (npad = max naug rounded up to
+ * 128), so batch the regions to fit HBM (e.g. 144 regions of 6300 = 47 GB). */
+typedef struct sml_train sml_train;
+int sml_train_create(int nlocal, const int *naug, int nout, sml_train **out);
+int sml_train_destroy(sml_train *t);
+/* zero the accumulators (a new training run; sml_train_solve consumes them) */
+int sml_train_reset(sml_train *t, void *stream);
+/* one chunking_matmul batch of m time steps for every region:
+ *   d_states : per region augmented_states(naug_i, m), column-major, back to back
+ *   d_targets: per region targetdata(nout, m), column-major, back to back */
+int sml_train_accumulate(sml_train *t, const double *d_states, const double *d_targets, int m, void *stream);
+/* regularise (diag += beta_model for i < ncs, beta_res otherwise; squared and with
+ * prior(i,i) = prior_val*beta_model^2 on b_trans when using_prior), solve
+ * G W^T = B^T, write W_out(nout, naug_i) column-major per region back to back into
+ * d_wout.  info (host, nlocal ints, may be NULL): potrf status per region (0 = ok,
+ * filled when the stream completes).  Destroys the accumulators. */
+int sml_train_solve(sml_train *t, int ncs, double beta_res, double beta_model, int using_prior, double prior_val,
+                    double *d_wout, int *info, void *stream);
+int sml_train_npad(const sml_train *t, int *npad);
+/* host copies for tests: G (npad x npad, column-major, lower triangle valid) and
+ * B(j, o) (npad x nout) of local region i */
+int sml_train_get_gram(sml_train *t, int i, double *G, double *B);
+
 #ifdef __cplusplus
 }
 #endif

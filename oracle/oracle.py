@@ -76,6 +76,8 @@ def _declare(L):
     L.orc_dyn_step.argtypes = [vp] * 9 + [i, i, d, d, d, d, vp, vp]
     L.orc_iogrid30.argtypes = [vp] * 8
     L.orc_iogrid31.argtypes = [vp] * 7
+    L.orc_train_accumulate.argtypes = [i, i, i, vp, vp, vp, vp]
+    L.orc_train_solve.argtypes = [i, i, i, d, d, i, d, vp, vp, vp]
 
 
 def spectral_init(radius: float = EARTH_RADIUS) -> None:
@@ -372,6 +374,31 @@ def iogrid31(state):
     lib().orc_iogrid31(_p(state["vor"]), _p(state["div"]), _p(state["t"]), _p(state["ps"]), _p(state["tr"]),
                        _p(g), _p(lp))
     return g, lp
+
+
+# ---------------------------------------------------------------- training
+def train_accumulate(S, T, G, B):
+    """chunking_matmul: G += S S^T, B += T S^T.  S (naug, m) / T (nout, m) Fortran
+    order == C arrays (m, naug) / (m, nout); G (naug, naug) as C (naug, naug)
+    transposed-symmetric; B (nout, naug) Fortran == C (naug, nout)."""
+    S = np.ascontiguousarray(S, dtype=np.float64)
+    T = np.ascontiguousarray(T, dtype=np.float64)
+    m, naug = S.shape
+    nout = T.shape[1]
+    assert T.shape[0] == m and G.shape == (naug, naug) and B.shape == (naug, nout)
+    lib().orc_train_accumulate(naug, nout, m, _p(S), _p(T), _p(G), _p(B))
+
+
+def train_solve(G, B, ncs, beta_res, beta_model, using_prior=True, prior_val=0.0):
+    """fit_chunk_hybrid + mldivide; returns (wout as C (naug, nout) == Fortran
+    wout(nout, naug), info).  G, B are consumed (copies are made)."""
+    G = np.array(G, dtype=np.float64, order="C")
+    B = np.ascontiguousarray(B, dtype=np.float64)
+    naug, nout = B.shape
+    w = np.zeros((naug, nout))
+    info = lib().orc_train_solve(naug, nout, ncs, beta_res, beta_model, int(using_prior), prior_val, _p(G), _p(B),
+                                 _p(w))
+    return w, info
 
 
 # ---------------------------------------------------------------- reference (pinning only)

@@ -1361,3 +1361,115 @@ void orc_iogrid31(const double *vor, const double *div, const double *t, const d
                 grid4d[G4I(3, i, j, k)] = qgr[g];
             }
 }
+
+/* ------------------------------------------------------------------------- */
+/* W_out training (BASELINE configs[4])          */
+/*   chunking_matmul  src/mod_reservoir.f90:1643-1699                         */
+/*   fit_chunk_hybrid src/mod_reservoir.f90:1233-1332                         */
+/*   mldivide -> LAPACK dgesv (src/mod_linalg.f90:109-151).  LAPACK is not    */
+/*   vendored in the reference; dgesv's published algorithm (LU with partial */
+/*   pivoting, dgetrf + dgetrs) is restated unblocked.  Parity is pinned on   */
+/*   the reference's call sites only (no reference test covers training).    */
+/* Layouts (column-major, as the reference): S = augmented_states(naug, m),   */
+/* T = targetdata(nout, m), G = states_x_states_aug(naug, naug),              */
+/* B = states_x_trainingdata_aug(nout, naug), wout(nout, naug).               */
+/* ------------------------------------------------------------------------- */
+void orc_train_accumulate(int naug, int nout, int m, const double *S, const double *T, double *G, double *B)
+{
+    /* temp = matmul(targetdata, transpose(augmented_states)); B += temp */
+    for (int j = 0; j < naug; ++j)
+        for (int o = 0; o < nout; ++o) {
+            double s = 0.0;
+            for (int t = 0; t < m; ++t) s += T[o + (size_t)nout * t] * S[j + (size_t)naug * t];
+            B[o + (size_t)nout * j] += s;
+        }
+    /* DGEMM(augmented_states, transpose(augmented_states)); G += temp */
+    for (int j = 0; j < naug; ++j)
+        for (int i = 0; i < naug; ++i) {
+            double s = 0.0;
+            for (int t = 0; t < m; ++t) s += S[i + (size_t)naug * t] * S[j + (size_t)naug * t];
+            G[i + (size_t)naug * j] += s;
+        }
+}
+
+/* dgesv: A (n x n, column-major) overwritten by its LU factors, B (n x nrhs)
+ * by the solution.  Returns info (0 = ok, k > 0: U(k,k) = 0). */
+static int orc_dgesv(int n, int nrhs, double *A, double *B)
+{
+    int info = 0;
+    int *ipiv = malloc(sizeof(int) * n);
+    for (int j = 0; j < n; ++j) {
+        int p = j;
+        double amax = fabs(A[j + (size_t)n * j]);
+        for (int i = j + 1; i < n; ++i)
+            if (fabs(A[i + (size_t)n * j]) > amax) {
+                amax = fabs(A[i + (size_t)n * j]);
+                p = i;
+            }
+        ipiv[j] = p;
+        if (A[p + (size_t)n * j] != 0.0) {
+            if (p != j)
+                for (int k = 0; k < n; ++k) {
+                    double tmp = A[j + (size_t)n * k];
+                    A[j + (size_t)n * k] = A[p + (size_t)n * k];
+                    A[p + (size_t)n * k] = tmp;
+                }
+            double r = 1.0 / A[j + (size_t)n * j];
+            for (int i = j + 1; i < n; ++i) A[i + (size_t)n * j] *= r;
+        } else if (info == 0) {
+            info = j + 1;
+        }
+        for (int k = j + 1; k < n; ++k) {
+            double a = A[j + (size_t)n * k];
+            if (a != 0.0)
+                for (int i = j + 1; i < n; ++i) A[i + (size_t)n * k] -= A[i + (size_t)n * j] * a;
+        }
+    }
+    if (info == 0)
+        for (int c = 0; c < nrhs; ++c) {
+            double *b = B + (size_t)n * c;
+            for (int j = 0; j < n; ++j)
+                if (ipiv[j] != j) {
+                    double tmp = b[j];
+                    b[j] = b[ipiv[j]];
+                    b[ipiv[j]] = tmp;
+                }
+            for (int j = 0; j < n; ++j) /* L y = P b (unit lower) */
+                for (int i = j + 1; i < n; ++i) b[i] -= b[j] * A[i + (size_t)n * j];
+            for (int j = n - 1; j >= 0; --j) { /* U x = y */
+                b[j] /= A[j + (size_t)n * j];
+                for (int i = 0; i < j; ++i) b[i] -= b[j] * A[i + (size_t)n * j];
+            }
+        }
+    free(ipiv);
+    return info;
+}
+
+/* fit_chunk_hybrid (using_prior = 1) / the unsquared regularisation of the
+ * no-prior branch, then mldivide(a_trans, b_trans), wout = transpose(b_trans).
+ * G and B are consumed. Returns dgesv's info. */
+int orc_train_solve(int naug, int nout, int ncs, double beta_res, double beta_model, int using_prior,
+                    double prior_val, double *G, const double *B, double *wout)
+{
+    for (int i = 0; i < naug; ++i) {
+        double add;
+        if (using_prior)
+            add = (i < ncs) ? pow(beta_model, 2.0) : pow(beta_res, 2.0);
+        else
+            add = (i < ncs) ? beta_model : beta_res;
+        G[i + (size_t)naug * i] += add;
+    }
+    double *a_t = malloc(sizeof(double) * naug * naug), *b_t = malloc(sizeof(double) * naug * nout);
+    for (int j = 0; j < naug; ++j)
+        for (int i = 0; i < naug; ++i) a_t[i + (size_t)naug * j] = G[j + (size_t)naug * i];
+    for (int o = 0; o < nout; ++o)
+        for (int j = 0; j < naug; ++j) b_t[j + (size_t)naug * o] = B[o + (size_t)nout * j];
+    if (using_prior) /* prior(i,i) = prior_val*beta_model**2, i <= chunk_size_speedy */
+        for (int i = 0; i < ncs && i < nout; ++i) b_t[i + (size_t)naug * i] += prior_val * pow(beta_model, 2.0);
+    int info = orc_dgesv(naug, nout, a_t, b_t);
+    for (int o = 0; o < nout; ++o)
+        for (int j = 0; j < naug; ++j) wout[o + (size_t)nout * j] = b_t[j + (size_t)naug * o];
+    free(a_t);
+    free(b_t);
+    return info;
+}

@@ -1,0 +1,337 @@
+// sml_train.hip -- W_out ridge training for a batch of regions on gfx950.
+//
+// Reference (per region, one vertical level):
+//   chunking_matmul  src/mod_reservoir.f90:1643-1699
+//       states_x_trainingdata_aug += targetdata * augmented_states^T   (136 x naug)
+//       states_x_states_aug       += augmented_states * augmented_states^T  (DGEMM)
+//     with augmented_states(naug = chunk_size_speedy + n, m) = [imperfect model ; x]
+//   fit_chunk_hybrid src/mod_reservoir.f90:1233-1332 (fit_chunk_ml :1175-1231)
+//       diag += beta_model (first chunk_size_speedy) / beta_res (rest), squared when
+//       using_prior, prior(i,i) = prior_val * beta_model^2 added to b_trans
+//   mldivide         src/mod_linalg.f90:109-151: dgesv(a_trans, b_trans), wout = b_trans^T
+//
+// MI355X design.  The Gram accumulation is the flop-heavy part (2 naug^2 m per
+// batch, ~16 TFLOP per region over a full training run): one hand-written fp64
+// MFMA kernel (v_mfma_f64_16x16x4_f64) computes, for every region of the batch,
+// the lower-triangular 128x128 tiles of S S^T and the 136-row strip T S^T in one
+// launch; S and T are read once per tile pair from HBM through LDS.  The solve is
+// SPD (regularised Gram): rocSOLVER's batched Cholesky (potrf + potrs) on the
+// padded matrices -- the same solution as dgesv up to rounding x cond(G).
+#include <hip/hip_runtime.h>
+#include <rocblas/rocblas.h>
+#include <rocsolver/rocsolver.h>
+
+#include <cmath>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "sml_internal.hpp"
+
+using namespace sml;
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+#define MFMA64(a, b, c) __builtin_amdgcn_mfma_f64_16x16x4f64((a), (b), (c), 0, 0, 0)
+
+namespace {
+
+constexpr int kTile = 128;  // C tile edge
+constexpr int kKC = 16;     // time steps per LDS stage
+constexpr int kLdsPad = 4;  // row padding (doubles) against bank conflicts
+constexpr int kStrip = 2;   // tile rows of the T S^T strip (nout <= 256)
+
+struct TrainRegion {
+    long long s_off, t_off;  // offsets of S (naug x m) and T (nout x m) in the batch buffers
+    int naug;
+    int pad_;
+};
+
+// tile index -> (bi, bj): lower triangle of the C x C Gram tiles first, then the
+// kStrip x C strip tiles (rows = outputs).
+__device__ inline bool tile_of(int idx, int C, int *bi, int *bj, bool *strip) {
+    const int tri = C * (C + 1) / 2;
+    if (idx < tri) {
+        int i = (int)((sqrt(8.0 * idx + 1.0) - 1.0) * 0.5);
+        while (i * (i + 1) / 2 > idx) --i;
+        while ((i + 1) * (i + 2) / 2 <= idx) ++i;
+        *bi = i;
+        *bj = idx - i * (i + 1) / 2;
+        *strip = false;
+        return true;
+    }
+    idx -= tri;
+    if (idx >= kStrip * C) return false;
+    *bi = idx / C;
+    *bj = idx % C;
+    *strip = true;
+    return true;
+}
+
+// One workgroup (4 waves, 2 x 2) per (region, 128 x 128 tile); wave (wr, wc) owns a
+// 64 x 64 sub-tile = 4 x 4 MFMA 16x16 tiles.  K loop over the batch's time steps in
+// stages of 16, register-prefetched one stage ahead.
+__global__ __launch_bounds__(256) void k_train_gram(const double *__restrict__ S, const double *__restrict__ T,
+                                                    const TrainRegion *__restrict__ regs, int m, int nout, int npad,
+                                                    double *__restrict__ G, double *__restrict__ B) {
+    __shared__ double sA[kKC][kTile + kLdsPad];
+    __shared__ double sB[kKC][kTile + kLdsPad];
+    const int r = blockIdx.y;
+    const TrainRegion R = regs[r];
+    const int C = npad / kTile;
+    int bi, bj;
+    bool strip;
+    if (!tile_of(blockIdx.x, C, &bi, &bj, &strip)) return;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int wr = w >> 1, wc = w & 1, l16 = lane & 15, kk = lane >> 4;
+    const double *Sr = S + R.s_off, *Tr = T + R.t_off;
+    const int naug = R.naug;
+    // loader: thread -> (row = tid & 127, t = (tid >> 7) + 2q), q = 0..7
+    const int lrow = tid & (kTile - 1), lt0 = tid >> 7;
+    const int arow = bi * kTile + lrow;  // A rows: Gram rows (i) or outputs (o)
+    const int brow = bj * kTile + lrow;  // B rows: Gram columns (j)
+    const bool a_ok = strip ? (arow < nout) : (arow < naug);
+    const bool b_ok = brow < naug;
+    const double *pa = strip ? Tr + arow : Sr + arow;
+    const long long lda = strip ? nout : naug;
+    const double *pb = Sr + brow;
+    double ra[kKC / 2], rb[kKC / 2];
+    auto fetch = [&](int t0) {
+#pragma unroll
+        for (int q = 0; q < kKC / 2; ++q) {
+            const int t = t0 + lt0 + 2 * q;
+            ra[q] = (a_ok && t < m) ? pa[(long long)t * lda] : 0.0;
+            rb[q] = (b_ok && t < m) ? pb[(long long)t * naug] : 0.0;
+        }
+    };
+    d4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = d4{0, 0, 0, 0};
+    fetch(0);
+    for (int t0 = 0; t0 < m; t0 += kKC) {
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < kKC / 2; ++q) {
+            sA[lt0 + 2 * q][lrow] = ra[q];
+            sB[lt0 + 2 * q][lrow] = rb[q];
+        }
+        __syncthreads();
+        if (t0 + kKC < m) fetch(t0 + kKC);
+#pragma unroll
+        for (int s = 0; s < kKC / 4; ++s) {
+            double a[4], b[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) a[i] = sA[4 * s + kk][wr * 64 + i * 16 + l16];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) b[j] = sB[4 * s + kk][wc * 64 + j * 16 + l16];
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[i][j] = MFMA64(a[i], b[j], acc[i][j]);
+        }
+    }
+    // accumulate into G (column-major npad x npad) or B (B(j, o) at j + npad*o)
+    double *Gr = G + (size_t)r * npad * npad;
+    double *Br = B + (size_t)r * npad * nout;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int row = bi * kTile + wr * 64 + i * 16 + kk + 4 * q;
+                const int col = bj * kTile + wc * 64 + j * 16 + l16;
+                if (strip) {
+                    if (row < nout) {
+                        double *p = Br + (size_t)row * npad + col;
+                        *p = *p + acc[i][j][q];
+                    }
+                } else {
+                    double *p = Gr + (size_t)col * npad + row;
+                    *p = *p + acc[i][j][q];
+                }
+            }
+}
+
+// fit_chunk_hybrid regularisation on the padded, column-major Gram:
+// diag(i) += beta_model (i < ncs) / beta_res (i < naug); padding diag = 1, prior on B
+__global__ void k_train_regularise(double *__restrict__ G, double *__restrict__ B,
+                                   const TrainRegion *__restrict__ regs, int npad, int nout, int ncs,
+                                   double add_model, double add_res, double prior) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int r = blockIdx.y;
+    if (i >= npad) return;
+    const int naug = regs[r].naug;
+    double *g = G + (size_t)r * npad * npad + (size_t)i * npad + i;
+    if (i < naug)
+        *g = *g + (i < ncs ? add_model : add_res);
+    else
+        *g = 1.0;
+    if (prior != 0.0 && i < ncs && i < nout) {
+        double *b = B + (size_t)r * npad * nout + (size_t)i * npad + i;  // b_trans(i, i)
+        *b = *b + prior;
+    }
+}
+
+// solution X(j, o) (npad x nout per region) -> wout(nout, naug) column-major
+__global__ void k_train_wout(const double *__restrict__ X, const TrainRegion *__restrict__ regs, int npad, int nout,
+                             const long long *__restrict__ wout_off, double *__restrict__ wout) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    const int r = blockIdx.y;
+    const int naug = regs[r].naug;
+    if (j >= naug) return;
+    const double *x = X + (size_t)r * npad * nout + j;
+    double *w = wout + wout_off[r] + (size_t)j * nout;
+    for (int o = 0; o < nout; ++o) w[o] = x[(size_t)o * npad];
+}
+
+}  // namespace
+
+struct sml_train {
+    int nlocal = 0, nout = 0, npad = 0, C = 0;
+    std::vector<int> naug;
+    TrainRegion *d_regs = nullptr;
+    double *d_G = nullptr, *d_B = nullptr;
+    long long *d_wout_off = nullptr;
+    int *d_info = nullptr;
+    rocblas_handle handle = nullptr;
+    long long s_total = 0, t_total = 0;
+    int last_m = -1;
+};
+
+static void set_offsets(sml_train *t, int m, std::vector<TrainRegion> &h) {
+    long long so = 0, to = 0;
+    for (int i = 0; i < t->nlocal; ++i) {
+        h[i].s_off = so;
+        h[i].t_off = to;
+        h[i].naug = t->naug[i];
+        so += (long long)t->naug[i] * m;
+        to += (long long)t->nout * m;
+    }
+}
+
+extern "C" int sml_train_destroy(sml_train *t) {
+    if (!t) return SML_OK;
+    void *ptrs[] = {t->d_regs, t->d_G, t->d_B, t->d_wout_off, t->d_info};
+    for (void *p : ptrs)
+        if (p) (void)hipFree(p);
+    if (t->handle) rocblas_destroy_handle(t->handle);
+    delete t;
+    return SML_OK;
+}
+
+extern "C" int sml_train_create(int nlocal, const int *naug, int nout, sml_train **out) {
+    SML_REQUIRE(out && naug && nlocal > 0, "bad argument");
+    SML_REQUIRE(nout > 0 && nout <= kStrip * kTile, "nout must be in 1..256");
+    *out = nullptr;
+    sml_train *t = new (std::nothrow) sml_train();
+    if (!t) return fail(SML_ERR_NOMEM, "host allocation failed");
+    t->nlocal = nlocal;
+    t->nout = nout;
+    t->naug.assign(naug, naug + nlocal);
+    int mx = 0;
+    for (int i = 0; i < nlocal; ++i) {
+        if (naug[i] <= 0) {
+            delete t;
+            return fail(SML_ERR_ARG, "naug[%d] = %d", i, naug[i]);
+        }
+        mx = naug[i] > mx ? naug[i] : mx;
+    }
+    t->npad = (mx + kTile - 1) / kTile * kTile;  // uniform padded size: one batched solve
+    t->C = t->npad / kTile;
+    const size_t g = (size_t)nlocal * t->npad * t->npad, b = (size_t)nlocal * t->npad * nout;
+    hipError_t e;
+    if ((e = hipMalloc(&t->d_G, g * 8)) != hipSuccess || (e = hipMalloc(&t->d_B, b * 8)) != hipSuccess ||
+        (e = hipMalloc(&t->d_regs, nlocal * sizeof(TrainRegion))) != hipSuccess ||
+        (e = hipMalloc(&t->d_wout_off, nlocal * sizeof(long long))) != hipSuccess ||
+        (e = hipMalloc(&t->d_info, nlocal * sizeof(int))) != hipSuccess) {
+        sml_train_destroy(t);
+        return fail(SML_ERR_NOMEM, "sml_train_create: %s (%.2f GB of Gram matrices)", hipGetErrorString(e),
+                    g * 8e-9);
+    }
+    std::vector<long long> wo(nlocal);
+    long long off = 0;
+    for (int i = 0; i < nlocal; ++i) {
+        wo[i] = off;
+        off += (long long)nout * naug[i];
+    }
+    SML_HIP(hipMemcpy(t->d_wout_off, wo.data(), nlocal * sizeof(long long), hipMemcpyHostToDevice));
+    if (rocblas_create_handle(&t->handle) != rocblas_status_success) {
+        sml_train_destroy(t);
+        return fail(SML_ERR_STATE, "rocblas_create_handle failed");
+    }
+    *out = t;
+    return sml_train_reset(t, nullptr);
+}
+
+extern "C" int sml_train_reset(sml_train *t, void *stream) {
+    SML_REQUIRE(t, "null context");
+    const size_t g = (size_t)t->nlocal * t->npad * t->npad, b = (size_t)t->nlocal * t->npad * t->nout;
+    SML_HIP(hipMemsetAsync(t->d_G, 0, g * 8, (hipStream_t)stream));
+    SML_HIP(hipMemsetAsync(t->d_B, 0, b * 8, (hipStream_t)stream));
+    return SML_OK;
+}
+
+extern "C" int sml_train_accumulate(sml_train *t, const double *d_states, const double *d_targets, int m,
+                                    void *stream) {
+    SML_REQUIRE(t && d_states && d_targets && m > 0, "bad argument");
+    if (m != t->last_m) {
+        std::vector<TrainRegion> h(t->nlocal);
+        set_offsets(t, m, h);
+        SML_HIP(hipMemcpy(t->d_regs, h.data(), h.size() * sizeof(TrainRegion), hipMemcpyHostToDevice));
+        t->last_m = m;
+    }
+    const int tiles = t->C * (t->C + 1) / 2 + kStrip * t->C;
+    hipLaunchKernelGGL(k_train_gram, dim3(tiles, t->nlocal), dim3(256), 0, (hipStream_t)stream, d_states, d_targets,
+                       t->d_regs, m, t->nout, t->npad, t->d_G, t->d_B);
+    SML_HIP(hipGetLastError());
+    return SML_OK;
+}
+
+extern "C" int sml_train_solve(sml_train *t, int ncs, double beta_res, double beta_model, int using_prior,
+                               double prior_val, double *d_wout, int *info, void *stream) {
+    SML_REQUIRE(t && d_wout, "bad argument");
+    SML_REQUIRE(ncs >= 0, "ncs must be >= 0");
+    if (t->last_m < 0) {  // regions table (offsets unused by the solve)
+        std::vector<TrainRegion> h(t->nlocal);
+        set_offsets(t, 1, h);
+        SML_HIP(hipMemcpy(t->d_regs, h.data(), h.size() * sizeof(TrainRegion), hipMemcpyHostToDevice));
+        t->last_m = 1;
+    }
+    hipStream_t st = (hipStream_t)stream;
+    const double add_model = using_prior ? beta_model * beta_model : beta_model;
+    const double add_res = using_prior ? beta_res * beta_res : beta_res;
+    const double prior = using_prior ? prior_val * beta_model * beta_model : 0.0;
+    hipLaunchKernelGGL(k_train_regularise, dim3((t->npad + 255) / 256, t->nlocal), dim3(256), 0, st, t->d_G, t->d_B,
+                       t->d_regs, t->npad, t->nout, ncs, add_model, add_res, prior);
+    SML_HIP(hipGetLastError());
+    if (rocblas_set_stream(t->handle, st) != rocblas_status_success) return fail(SML_ERR_STATE, "rocblas_set_stream");
+    const rocblas_stride sg = (rocblas_stride)t->npad * t->npad, sb = (rocblas_stride)t->npad * t->nout;
+    rocblas_status s = rocsolver_dpotrf_strided_batched(t->handle, rocblas_fill_lower, t->npad, t->d_G, t->npad, sg,
+                                                        t->d_info, t->nlocal);
+    if (s != rocblas_status_success) return fail(SML_ERR_STATE, "rocsolver_dpotrf_strided_batched: status %d", (int)s);
+    s = rocsolver_dpotrs_strided_batched(t->handle, rocblas_fill_lower, t->npad, t->nout, t->d_G, t->npad, sg, t->d_B,
+                                         t->npad, sb, t->nlocal);
+    if (s != rocblas_status_success) return fail(SML_ERR_STATE, "rocsolver_dpotrs_strided_batched: status %d", (int)s);
+    hipLaunchKernelGGL(k_train_wout, dim3((t->npad + 255) / 256, t->nlocal), dim3(256), 0, st, t->d_B, t->d_regs,
+                       t->npad, t->nout, t->d_wout_off, d_wout);
+    SML_HIP(hipGetLastError());
+    if (info) SML_HIP(hipMemcpyAsync(info, t->d_info, t->nlocal * sizeof(int), hipMemcpyDeviceToHost, st));
+    return SML_OK;
+}
+
+extern "C" int sml_train_npad(const sml_train *t, int *npad) {
+    SML_REQUIRE(t && npad, "null argument");
+    *npad = t->npad;
+    return SML_OK;
+}
+
+extern "C" int sml_train_get_gram(sml_train *t, int i, double *G, double *B) {
+    SML_REQUIRE(t && i >= 0 && i < t->nlocal, "bad region index");
+    SML_HIP(hipDeviceSynchronize());
+    const size_t g = (size_t)t->npad * t->npad, b = (size_t)t->npad * t->nout;
+    if (G) SML_HIP(hipMemcpy(G, t->d_G + i * g, g * 8, hipMemcpyDeviceToHost));
+    if (B) SML_HIP(hipMemcpy(B, t->d_B + i * b, b * 8, hipMemcpyDeviceToHost));
+    return SML_OK;
+}

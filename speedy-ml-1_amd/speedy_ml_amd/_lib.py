@@ -34,6 +34,8 @@ EXPORTED = (
     "sml_dyn_get_state", "sml_dyn_get_phi", "sml_dyn_get_tendencies", "sml_dyn_state_device",
     "sml_dyn_step", "sml_dyn_step_host", "sml_dyn_leapfrog", "sml_dyn_from_grid", "sml_dyn_to_grid",
     "sml_dyn_is_safe", "sml_dyn_from_grid_host", "sml_dyn_to_grid_host",
+    "sml_train_create", "sml_train_destroy", "sml_train_reset", "sml_train_accumulate", "sml_train_solve",
+    "sml_train_npad", "sml_train_get_gram",
 )
 
 
@@ -122,6 +124,13 @@ def _declare(L: ctypes.CDLL) -> None:
         "sml_dyn_is_safe": [vp],
         "sml_dyn_from_grid_host": [vp, vp, vp, vp, ctypes.POINTER(ctypes.c_int)],
         "sml_dyn_to_grid_host": [vp, vp, vp],
+        "sml_train_create": [i, vp, i, pp],
+        "sml_train_destroy": [vp],
+        "sml_train_reset": [vp, vp],
+        "sml_train_accumulate": [vp, vp, vp, i, vp],
+        "sml_train_solve": [vp, i, d, d, i, d, vp, vp, vp],
+        "sml_train_npad": [vp, ctypes.POINTER(ctypes.c_int)],
+        "sml_train_get_gram": [vp, i, vp, vp],
     }
     for name, args in sig.items():
         fn = getattr(L, name)
