@@ -58,7 +58,7 @@ def test_gram_matches_oracle(cuda):
         Gl = np.tril(G[:n, :n].T)  # C (npad, npad) = transposed column-major; lower triangle valid
         assert np.abs(Gl - np.tril(Go)).max() <= GRAM_TOL * np.abs(Go).max()
         assert np.abs(B[:, :n].T - Bo).max() <= GRAM_TOL * np.abs(Bo).max()
-        assert not G[n:, :].any() or np.all(G[:n, n:] == 0)  # padding rows/cols stay zero
+        assert not G[n:, :].any() and not G[:, n:].any()  # padding rows/cols stay zero
     tr.close()
 
 
