@@ -47,6 +47,9 @@ def parse():
     p.add_argument("--weights", choices=("f32", "f64"), default="f32")
     p.add_argument("--cpu-sample", type=int, default=96, help="regions in the CPU-baseline sample (0 = skip)")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--train-regions", type=int, default=8,
+                   help="regions in the supplementary W_out-training leg (0 = skip)")
+    p.add_argument("--train-steps", type=int, default=4096, help="training time steps per region in that leg")
     p.add_argument("--speedy-steps", type=int, default=48,
                    help="leapfrog steps timed in the supplementary SPEEDY-dynamics leg (0 = skip)")
     return p.parse_args()
@@ -156,6 +159,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.cpu_sample > 0:
         cpu = cpu_baseline(args.cpu_sample, nreg, mask)
     speedy = speedy_leg(dev, world, rank, args) if args.speedy_steps > 0 else None
+    training = training_leg(dev, mask, args) if args.train_regions > 0 and world == 1 else None
 
     if rank == 0:
         steps_per_s = args.steps / dt
@@ -199,6 +203,7 @@ def main():
             },
             "cpu_baseline": cpu,
             "speedy_dynamics": speedy,
+            "training": training,
         }
         print(json.dumps(line), flush=True)
     if world > 1:
@@ -247,6 +252,71 @@ def speedy_leg(dev, world, rank, args):
         out["cpu_oracle_note"] = "oracle C restatement (long-double DFT instead of FFTPACK), 1 core"
     dyn.close()
     return out
+
+
+def training_leg(dev, mask, args):
+    """Supplementary measurement (BASELINE configs[4] shape on one GPU): W_out ridge
+    training for a batch of 6000-node-class regions -- chunking_matmul Gram and
+    cross products (hand-written fp64 MFMA kernel) over args.train_steps time steps
+    in 4 batches, then regularisation + batched Cholesky solve (rocSOLVER).
+    Roofline: Gram kernel flops / its time vs the measured fp64 MFMA rate."""
+    import ctypes
+
+    import torch
+
+    from speedy_ml_amd import domain
+    from speedy_ml_amd._lib import check, lib
+    from speedy_ml_amd.training import Trainer
+
+    regions = [r * (1152 // args.train_regions) for r in range(args.train_regions)]
+    naug = [132 + domain.reservoir_sizes(r, bool(mask[r])).n for r in regions]
+    nb = 4
+    m = args.train_steps // nb
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(3)
+    S = torch.tanh(torch.randn(sum(naug) * m, dtype=torch.float64, device=dev, generator=gen))
+    T = torch.randn(len(naug) * m * 136, dtype=torch.float64, device=dev, generator=gen)
+    tr = Trainer(naug)
+    tr.accumulate(S, T, m)  # warm-up
+    tr.reset()
+    torch.cuda.synchronize()
+    e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+    e0.record()
+    for _ in range(nb):
+        tr.accumulate(S, T, m)
+    e1.record()
+    _, info = tr.solve()
+    e2.record()
+    torch.cuda.synchronize()
+    gram_ms = e0.elapsed_time(e1)
+    solve_ms = e1.elapsed_time(e2)
+    npad = tr.npad
+    # algorithmic flops: lower-triangle Gram (naug(naug+1)/2 dot products) + T S^T, 2 flops per FMA
+    algo = sum(2.0 * (n * (n + 1) / 2 + 136 * n) * m * nb for n in naug)
+    # executed by the tiles (128 x 128, padded): the MFMA work actually issued
+    C = npad // 128
+    issued = len(naug) * (C * (C + 1) // 2 + 2 * C) * 2.0 * 128 * 128 * m * nb
+    peak = ctypes.c_double()
+    check(lib().sml_probe_mfma_f64(20000, ctypes.byref(peak)))
+    tr.close()
+    achieved = algo / (gram_ms * 1e-3) / 1e12
+    return {
+        "workload": f"{len(naug)} regions (naug {min(naug)}..{max(naug)}), {m * nb} training steps in {nb} "
+                    "chunking_matmul batches, then fit_chunk_hybrid regularisation + solve",
+        "gram_ms": round(gram_ms, 3),
+        "solve_ms": round(solve_ms, 3),
+        "solve_info_ok": bool((info == 0).all()),
+        "roofline": {
+            "kernel": "k_train_gram (fp64 MFMA 16x16x4, 128x128 tiles, lower triangle + T S^T strip)",
+            "bound": "mfma", "unit": "TFLOP/s",
+            "achieved": round(achieved, 2),
+            "issued_tflops": round(issued / (gram_ms * 1e-3) / 1e12, 2),
+            "peak": round(peak.value, 2),
+            "peak_source": "measured: back-to-back v_mfma_f64_16x16x4_f64 on every SIMD (sml_probe_mfma_f64)",
+            "frac": round(achieved / peak.value, 4),
+            "algorithmic_flops": algo,
+        },
+    }
 
 
 def cpu_baseline(sample: int, nreg: int, mask):

@@ -282,6 +282,10 @@ int sml_train_npad(const sml_train *t, int *npad);
  * B(j, o) (npad x nout) of local region i */
 int sml_train_get_gram(sml_train *t, int i, double *G, double *B);
 
+/* measurement: sustained fp64 MFMA rate of the current device (TFLOP/s), from
+ * back-to-back v_mfma_f64_16x16x4_f64 chains on every SIMD */
+int sml_probe_mfma_f64(int iters, double *tflops);
+
 #ifdef __cplusplus
 }
 #endif

@@ -335,3 +335,50 @@ extern "C" int sml_train_get_gram(sml_train *t, int i, double *G, double *B) {
     if (B) SML_HIP(hipMemcpy(B, t->d_B + i * b, b * 8, hipMemcpyDeviceToHost));
     return SML_OK;
 }
+
+// ------------------------------------------------------------------ measurement
+// Back-to-back v_mfma_f64_16x16x4_f64 with 8 independent accumulators per wave on
+// every SIMD: the chip's sustained fp64 MFMA rate, the `peak` of the training
+// roofline (MI355X_MICROARCH.md lists no fp64 MFMA figure).
+namespace {
+__global__ __launch_bounds__(256) void k_probe_mfma_f64(int iters, double *sink) {
+    d4 acc[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[i] = d4{0, 0, 0, 0};
+    double a = 1.0 + threadIdx.x * 1e-9, b = 1.0 - threadIdx.x * 1e-9;
+    for (int it = 0; it < iters; ++it) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc[i] = MFMA64(a, b, acc[i]);
+    }
+    double s = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s += acc[i][0] + acc[i][1] + acc[i][2] + acc[i][3];
+    if (s == 12345.678) sink[0] = s;  // keep the chain live
+}
+}  // namespace
+
+extern "C" int sml_probe_mfma_f64(int iters, double *tflops) {
+    SML_REQUIRE(tflops && iters > 0, "bad argument");
+    int dev = 0, ncu = 0;
+    SML_HIP(hipGetDevice(&dev));
+    SML_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+    double *sink = nullptr;
+    SML_HIP(hipMalloc(&sink, 8));
+    hipEvent_t e0, e1;
+    SML_HIP(hipEventCreate(&e0));
+    SML_HIP(hipEventCreate(&e1));
+    const int blocks = ncu * 2;  // 8 waves per CU = 2 per SIMD
+    hipLaunchKernelGGL(k_probe_mfma_f64, dim3(blocks), dim3(256), 0, nullptr, iters / 10, sink);  // warm-up
+    SML_HIP(hipEventRecord(e0, nullptr));
+    hipLaunchKernelGGL(k_probe_mfma_f64, dim3(blocks), dim3(256), 0, nullptr, iters, sink);
+    SML_HIP(hipEventRecord(e1, nullptr));
+    SML_HIP(hipEventSynchronize(e1));
+    float ms = 0;
+    SML_HIP(hipEventElapsedTime(&ms, e0, e1));
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    (void)hipFree(sink);
+    const double flops = (double)blocks * 4 * iters * 8 * 2.0 * 16 * 16 * 4;
+    *tflops = flops / (ms * 1e-3) / 1e12;
+    return SML_OK;
+}

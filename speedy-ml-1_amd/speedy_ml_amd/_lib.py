@@ -35,7 +35,7 @@ EXPORTED = (
     "sml_dyn_step", "sml_dyn_step_host", "sml_dyn_leapfrog", "sml_dyn_from_grid", "sml_dyn_to_grid",
     "sml_dyn_is_safe", "sml_dyn_from_grid_host", "sml_dyn_to_grid_host",
     "sml_train_create", "sml_train_destroy", "sml_train_reset", "sml_train_accumulate", "sml_train_solve",
-    "sml_train_npad", "sml_train_get_gram",
+    "sml_train_npad", "sml_train_get_gram", "sml_probe_mfma_f64",
 )
 
 
@@ -131,6 +131,7 @@ def _declare(L: ctypes.CDLL) -> None:
         "sml_train_solve": [vp, i, d, d, i, d, vp, vp, vp],
         "sml_train_npad": [vp, ctypes.POINTER(ctypes.c_int)],
         "sml_train_get_gram": [vp, i, vp, vp],
+        "sml_probe_mfma_f64": [i, ctypes.POINTER(ctypes.c_double)],
     }
     for name, args in sig.items():
         fn = getattr(L, name)
