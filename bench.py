@@ -50,6 +50,9 @@ def parse():
     p.add_argument("--train-regions", type=int, default=8,
                    help="regions in the supplementary W_out-training leg (0 = skip)")
     p.add_argument("--train-steps", type=int, default=4096, help="training time steps per region in that leg")
+    p.add_argument("--hybrid-steps", type=int, default=10,
+                   help="hybrid steps timed in the supplementary configs[2] leg (reservoir + SPEEDY dynamics "
+                        "window; 0 = skip)")
     p.add_argument("--speedy-steps", type=int, default=48,
                    help="leapfrog steps timed in the supplementary SPEEDY-dynamics leg (0 = skip)")
     return p.parse_args()
@@ -89,7 +92,7 @@ def main():
     res = Reservoirs(regions, [mask[r] for r in regions], [s.n for s in sizes], [s.k for s in sizes],
                      weight_dtype=args.weights)
     for i, r in enumerate(regions):
-        w = region_weights(r, bool(mask[r]))
+        w = region_weights(r, bool(mask[r]), climatology=True)
         if args.weights == "f64":
             res.load_region(i, w.rows, w.cols, w.vals.astype(np.float64), w.win.astype(np.float64),
                             w.wout.astype(np.float64), w.mean, w.std)
@@ -159,6 +162,9 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.cpu_sample > 0:
         cpu = cpu_baseline(args.cpu_sample, nreg, mask)
     speedy = speedy_leg(dev, world, rank, args) if args.speedy_steps > 0 else None
+    hybrid = None
+    if args.hybrid_steps > 0:
+        hybrid = hybrid_leg(dev, world, res, exchange, (fb, lm, ov), (g4, g2, pr, f4, f2, tisr), args)
     training = training_leg(dev, mask, args) if args.train_regions > 0 and world == 1 else None
 
     if rank == 0:
@@ -203,6 +209,7 @@ def main():
             },
             "cpu_baseline": cpu,
             "speedy_dynamics": speedy,
+            "hybrid_with_dynamics": hybrid,
             "training": training,
         }
         print(json.dumps(line), flush=True)
@@ -252,6 +259,63 @@ def speedy_leg(dev, world, rank, args):
         out["cpu_oracle_note"] = "oracle C restatement (long-double DFT instead of FFTPACK), 1 core"
     dyn.close()
     return out
+
+
+def hybrid_leg(dev, world, res, exchange, io, grids, args):
+    """Supplementary measurement, BASELINE configs[2] shape (dynamics only): one
+    hybrid step = predict for every local region -> RCCL all-gather -> assemble ->
+    iogrid(30) -> stepone + 24 leapfrog steps of the dynamical core -> iogrid(31)
+    -> re-tile feedback and local model.  Every stage on the GPU, no host sync
+    inside the step.  Physics (phypar) is not computed (zero tendencies), so this
+    is not the reference's full window and not the headline value."""
+    import torch
+    import torch.distributed as dist
+
+    from speedy_ml_amd.dynamics import Dynamics
+    from speedy_ml_amd.synthetic import dyn_state
+
+    fb, lm, ov = io
+    g4, g2, pr, f4, f2, tisr = grids
+    _, forcing = dyn_state()
+    dyn = Dynamics()
+    dyn.set_forcing(**forcing)
+
+    def hstep():
+        res.predict(fb, lm, ov)
+        glob = exchange(ov)
+        res.assemble(glob, g4, g2, pr)
+        dyn.from_grid(g4, g2)   # iogrid(30), min/max for the safety check stay on the device
+        dyn.window(24)          # stepone + 24 x step(2,2) (hipGraph replay)
+        dyn.to_grid(f4, f2)     # iogrid(31)
+        res.tile_inputs(g4, g2, pr, f4, f2, tisr, fb, lm)
+
+    for _ in range(2):
+        hstep()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.hybrid_steps):
+        hstep()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    _, safe = dyn.from_grid(g4.cpu().numpy(), g2.cpu().numpy())
+    dyn.close()
+    return {
+        "value": round(args.hybrid_steps / dt, 3),
+        "unit": "hybrid timesteps/s",
+        "ms_per_step": round(dt / args.hybrid_steps * 1e3, 4),
+        "steps": args.hybrid_steps,
+        "last_window_safe": bool(safe),
+        "note": "configs[2] shape without physics: SPEEDY window = iogrid(30) + stepone + 24 leapfrog dynamics "
+                "steps + iogrid(31), replicated on every rank; phypar not on the GPU yet",
+    }
 
 
 def training_leg(dev, mask, args):

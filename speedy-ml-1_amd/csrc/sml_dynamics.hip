@@ -56,7 +56,12 @@ __device__ inline int mi(int m, int n) { return m + kMX * n; }
 struct sml_dynamics {
     sml_spectral *sp = nullptr;
     DynTables tab;
-    DynTables *d_tab = nullptr;
+    DynTables *d_tab = nullptr;   // current impint slot (one of d_tabs)
+    DynTables *d_tabs = nullptr;  // kTabSlots device copies keyed by (dt, alph): stepone's
+                                  // three impint calls per window become pointer switches
+    double slot_key[4][2] = {};
+    bool slot_used[4] = {};
+    int slot_next = 0;
     double *d_state = nullptr;
     double *d_phis = nullptr, *d_tcorh = nullptr, *d_qcorh = nullptr, *d_phi = nullptr;
     double *d_specin = nullptr, *d_varm = nullptr, *d_grid = nullptr, *d_gfwd = nullptr, *d_sfwd = nullptr;
@@ -70,6 +75,7 @@ struct sml_dynamics {
     hipGraphExec_t graph = nullptr;
     double g_key[4] = {0, 0, 0, 0};
     const double *g_phys = nullptr;
+    const DynTables *g_tab = nullptr;
 };
 
 namespace {
@@ -536,7 +542,7 @@ int dalloc(T **p, size_t count) {
 // ------------------------------------------------------------------ API
 extern "C" int sml_dyn_destroy(sml_dynamics *d) {
     if (!d) return SML_OK;
-    void *ptrs[] = {d->d_tab, d->d_state, d->d_phis, d->d_tcorh, d->d_qcorh, d->d_phi, d->d_specin,
+    void *ptrs[] = {d->d_tabs, d->d_state, d->d_phis, d->d_tcorh, d->d_qcorh, d->d_phi, d->d_specin,
                     d->d_varm, d->d_grid, d->d_gfwd, d->d_sfwd, d->d_tend, d->d_phys, d->d_minmax, d->d_io};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
@@ -558,7 +564,7 @@ extern "C" int sml_dyn_create(double radius, sml_dynamics **out) {
         return rc;
     }
     build_dyn_indyns(spectral_host_tables(d->sp), &d->tab);
-    if ((rc = dalloc(&d->d_tab, 1)) || (rc = dalloc(&d->d_state, kStateSize)) || (rc = dalloc(&d->d_phis, kSF)) ||
+    if ((rc = dalloc(&d->d_tabs, 4)) || (rc = dalloc(&d->d_state, kStateSize)) || (rc = dalloc(&d->d_phis, kSF)) ||
         (rc = dalloc(&d->d_tcorh, kSF)) || (rc = dalloc(&d->d_qcorh, kSF)) || (rc = dalloc(&d->d_phi, kKX * kSF)) ||
         (rc = dalloc(&d->d_specin, (size_t)kNInv * kSF)) || (rc = dalloc(&d->d_varm, (size_t)kNFwd * kVF)) ||
         (rc = dalloc(&d->d_grid, (size_t)kNInv * kGF)) || (rc = dalloc(&d->d_gfwd, (size_t)kNFwd * kGF)) ||
@@ -568,6 +574,7 @@ extern "C" int sml_dyn_create(double radius, sml_dynamics **out) {
         sml_dyn_destroy(d);
         return rc;
     }
+    d->d_tab = d->d_tabs;
     hipError_t e = hipMemcpy(d->d_tab, &d->tab, sizeof(DynTables), hipMemcpyHostToDevice);
     if (e != hipSuccess) {
         sml_dyn_destroy(d);
@@ -579,8 +586,23 @@ extern "C" int sml_dyn_create(double radius, sml_dynamics **out) {
 
 extern "C" int sml_dyn_impint(sml_dynamics *d, double dt, double alph) {
     SML_REQUIRE(d, "null context");
+    for (int i = 0; i < 4; ++i)
+        if (d->slot_used[i] && d->slot_key[i][0] == dt && d->slot_key[i][1] == alph) {
+            d->d_tab = d->d_tabs + i;  // cached: no host work, no copy
+            d->impint_done = true;
+            return SML_OK;
+        }
+    const int i = d->slot_next;
+    d->slot_next = (i + 1) % 4;
     build_dyn_impint(dt, alph, &d->tab);
-    SML_HIP(hipMemcpy(d->d_tab, &d->tab, sizeof(DynTables), hipMemcpyHostToDevice));
+    // the copy is ordered before later launches on the legacy stream; kernels still
+    // reading an evicted slot were launched earlier and complete first
+    SML_HIP(hipDeviceSynchronize());
+    SML_HIP(hipMemcpy(d->d_tabs + i, &d->tab, sizeof(DynTables), hipMemcpyHostToDevice));
+    d->slot_key[i][0] = dt;
+    d->slot_key[i][1] = alph;
+    d->slot_used[i] = true;
+    d->d_tab = d->d_tabs + i;
     d->impint_done = true;
     return SML_OK;
 }
@@ -688,7 +710,7 @@ extern "C" int sml_dyn_leapfrog(sml_dynamics *d, int nsteps, double dt, double a
     if (!d->impint_done) return fail(SML_ERR_STATE, "sml_dyn_impint must be called before sml_dyn_leapfrog");
     if (nsteps == 0) return SML_OK;
     const double key[4] = {dt, alph, rob, wil};
-    if (!d->graph || std::memcmp(key, d->g_key, sizeof key) != 0 || d_phys != d->g_phys) {
+    if (!d->graph || std::memcmp(key, d->g_key, sizeof key) != 0 || d_phys != d->g_phys || d->d_tab != d->g_tab) {
         if (d->graph) {
             SML_HIP(hipGraphExecDestroy(d->graph));
             d->graph = nullptr;
@@ -711,6 +733,7 @@ extern "C" int sml_dyn_leapfrog(sml_dynamics *d, int nsteps, double dt, double a
         }
         std::memcpy(d->g_key, key, sizeof key);
         d->g_phys = d_phys;
+        d->g_tab = d->d_tab;
     }
     for (int i = 0; i < nsteps; ++i) SML_HIP(hipGraphLaunch(d->graph, (hipStream_t)stream));
     return SML_OK;

@@ -85,21 +85,22 @@ class Dynamics:
         return s.value, p.value
 
     def step(self, j1, j2, dt, alph=ALPH, rob=ROB, wil=WIL, phys=None, stream=None):
-        """step(j1, j2, dt, alph, rob, wil).  `phys`: host numpy (4, 8, 48, 96), a
-        float64 CUDA tensor of that shape, or None.  impint(dt, alph) is evaluated
-        when (dt, alph) differs from the last call (the reference calls it
-        explicitly, ini_stepone.f90:21-34)."""
+        """step(j1, j2, dt, alph, rob, wil).  `phys`: host numpy (4, 8, 48, 96)
+        (synchronous), a float64 CUDA tensor of that shape or None (asynchronous on
+        `stream`).  impint(dt, alph) is selected when (dt, alph) differs from the
+        last call (the reference calls it explicitly, ini_stepone.f90:21-34); the
+        library caches the tables of up to 4 (dt, alph) pairs on the device."""
         if self._dtal != (dt, alph):
             self.impint(dt, alph)
-        if phys is None or isinstance(phys, np.ndarray):
-            ph = None if phys is None else np.ascontiguousarray(phys, dtype=np.float64)
-            if ph is not None and ph.shape != (4, KX, 48, 96):
+        if isinstance(phys, np.ndarray):  # host tendencies: synchronous H2D + step
+            ph = np.ascontiguousarray(phys, dtype=np.float64)
+            if ph.shape != (4, KX, 48, 96):
                 raise ValueError("phys must be (4, 8, 48, 96)")
             check(lib().sml_dyn_step_host(self._h, j1, j2, dt, alph, rob, wil, ptr(ph)))
-        else:
-            if not (phys.is_cuda and phys.is_contiguous() and phys.numel() == 4 * KX * 4608):
-                raise ValueError("phys must be a contiguous float64 CUDA tensor (4, 8, 48, 96)")
-            check(lib().sml_dyn_step(self._h, j1, j2, dt, alph, rob, wil, ptr(phys), stream_ptr(stream)))
+            return
+        if phys is not None and not (phys.is_cuda and phys.is_contiguous() and phys.numel() == 4 * KX * 4608):
+            raise ValueError("phys must be a contiguous float64 CUDA tensor (4, 8, 48, 96)")
+        check(lib().sml_dyn_step(self._h, j1, j2, dt, alph, rob, wil, ptr(phys), stream_ptr(stream)))
 
     def from_grid(self, grid4d, logp):
         """iogrid(30) (ppo_iogrid.f90:497-571): window entry from variables3d
@@ -129,11 +130,17 @@ class Dynamics:
         check(lib().sml_dyn_to_grid_host(self._h, ptr(g), ptr(lp)))
         return g, lp
 
-    def stepone(self, delt: float = DELT, alph: float = ALPH, phys=None):
-        """ini_stepone.f90:19-34 for istart = 0: forward half step, first leapfrog."""
-        self.step(1, 1, 0.5 * delt, alph, phys=phys)
-        self.step(1, 2, delt, alph, phys=phys)
+    def stepone(self, delt: float = DELT, alph: float = ALPH, phys=None, stream=None):
+        """ini_stepone.f90:19-34 for istart = 0 / 2: forward half step, first leapfrog."""
+        self.step(1, 1, 0.5 * delt, alph, phys=phys, stream=stream)
+        self.step(1, 2, delt, alph, phys=phys, stream=stream)
         self.impint(2 * delt, alph)
+
+    def window(self, nleap: int = 24, delt: float = DELT, alph: float = ALPH, stream=None, graph: bool = True):
+        """One 6-h SPEEDY window after iogrid(30): stepone + nleap x step(2, 2)
+        (dyn_stloop.f90:37-59 with window_size 4), asynchronous, no physics."""
+        self.stepone(delt, alph, stream=stream)
+        self.leapfrog(nleap, delt, alph, stream=stream, graph=graph)
 
     def leapfrog(self, nsteps: int, delt: float = DELT, alph: float = ALPH, phys=None, stream=None,
                  graph: bool = True):

@@ -50,8 +50,28 @@ class RegionWeights:
         return col, val
 
 
+def climatology_mean_std():
+    """Physically scaled standardisation constants (36 = 4 vars x 8 levels, logp,
+    tisr, precip, sst; index map of unstandardize_state_vec_res,
+    res_domain.f90:1424-1434, mod_reservoir.f90:1821-1846), so that unstandardized
+    synthetic outputs look like a T30L8 state (level 1 = top)."""
+    z = np.arange(8) / 7.0
+    mean = np.zeros(36)
+    std = np.ones(36)
+    mean[0:8], std[0:8] = 210.0 + 75.0 * z, 8.0          # T [K]
+    mean[8:16], std[8:16] = 10.0 - 5.0 * z, 10.0         # u [m/s]
+    mean[16:24], std[16:24] = 0.0, 6.0                   # v [m/s]
+    mean[24:32], std[24:32] = 0.01 + 8.0 * z ** 3, 0.5 + 3.0 * z ** 2  # q [g/kg]
+    mean[32], std[32] = -0.02, 0.05                      # logp
+    mean[33], std[33] = 300.0, 150.0                     # tisr
+    mean[34], std[34] = 1e-3, 2e-3                       # precip
+    mean[35], std[35] = 285.0, 10.0                      # sst
+    return mean.astype(np.float32).astype(np.float64), std.astype(np.float32).astype(np.float64)
+
+
 def region_weights(region: int, sst: bool, seed: int = 1234, chunk_speedy: int = CHUNK_SPEEDY,
-                   nout: int = CHUNK_PRED, n_override: int | None = None) -> RegionWeights:
+                   nout: int = CHUNK_PRED, n_override: int | None = None,
+                   climatology: bool = False) -> RegionWeights:
     sz = reservoir_sizes(region, sst)
     n, ninp, k, q = sz.n, sz.ninp, sz.k, sz.q
     if n_override is not None:  # reduced sizes for fast CPU tests (same structure)
@@ -80,6 +100,8 @@ def region_weights(region: int, sst: bool, seed: int = 1234, chunk_speedy: int =
     wout = ((rng.random((chunk_speedy + n, nout), dtype=np.float32) * 2.0 - 1.0) * 0.01).astype(np.float32)
     mean = rng.random(36).astype(np.float32).astype(np.float64)
     std = (0.5 + rng.random(36)).astype(np.float32).astype(np.float64)
+    if climatology:
+        mean, std = climatology_mean_std()
     if not sst:
         std[35] = 0.0
     return RegionWeights(region, sst, n, ninp, k, rows, cols, vals, win, wout, mean, std)
