@@ -152,6 +152,11 @@ int sml_res_get_state(sml_reservoirs *c, int i, double *x);
  *   d_outvec      [nlocal][nout] unstandardized outputs */
 int sml_res_step(sml_reservoirs *c, const double *d_feedback, const double *d_local_model, double *d_outvec,
                  void *stream);
+/* synchronize (src/mod_reservoir.f90:1352-1378), the spin-up of start_prediction
+ * (:938-959): `length` updates x = (1-leak) x + leak tanh(A x + W_in u_t) for every
+ * local region, no readout.  d_inputs holds `length` blocks in the packed feedback
+ * layout, block t at d_inputs + t * stride doubles (stride >= total feedback). */
+int sml_res_synchronize(sml_reservoirs *c, const double *d_inputs, int length, int64_t stride, void *stream);
 /* host convenience: H2D, step, D2H (synchronous) */
 int sml_res_step_host(sml_reservoirs *c, const double *feedback, const double *local_model, double *outvec);
 /* bytes of weights + state resident on the device (for roofline bookkeeping) */

@@ -831,20 +831,10 @@ extern "C" int sml_res_kernel_times(sml_reservoirs *c, float *update_ms, float *
     return SML_OK;
 }
 
-extern "C" int sml_res_step(sml_reservoirs *c, const double *d_feedback, const double *d_local_model,
-                            double *d_outvec, void *stream) {
-    SML_REQUIRE(c, "null context");
-    if (c->nlocal == 0) return SML_OK;
-    SML_REQUIRE(d_feedback && d_outvec, "null device buffer");
-    SML_REQUIRE(c->ncs == 0 || d_local_model, "hybrid context needs d_local_model");
-    for (int i = 0; i < c->nlocal; ++i)
-        if (!c->loaded[i]) return fail(SML_ERR_STATE, "local region %d has no weights loaded", i);
-    hipStream_t st = (hipStream_t)stream;
-    const double *xo = c->d_x[c->cur];
-    double *xn = c->d_x[1 - c->cur];
-    const bool rec = c->timing && c->ev_used < c->ev_cap;
-    hipEvent_t *ev = rec ? &c->ev[3 * c->ev_used] : nullptr;
-    if (rec) SML_HIP(hipEventRecord(ev[0], st));
+namespace {
+// x_new = (1 - leak) x + leak tanh(A x + W_in u) for every local region (+ x~, x_aug)
+int launch_update(sml_reservoirs *c, const double *xo, double *xn, const double *d_feedback, const double *lmp,
+                  hipStream_t st) {
     // parts per region: enough blocks for ~4 rounds of the 512 resident 1024-thread
     // blocks (2 per CU with ~54 KB LDS each), each part at least one 1024-row pass
     const int max_parts = std::max(1, (c->maxn + kUpdThreads - 1) / kUpdThreads);
@@ -854,7 +844,6 @@ extern "C" int sml_res_step(sml_reservoirs *c, const double *d_feedback, const d
     const bool use_lds = lds <= 64 * 1024;
     const int bpr = parts;
     dim3 ug(bpr * c->nlocal);
-    const double *lmp = c->ncs ? d_local_model : nullptr;
 #define SML_UPD(WT, L)                                                                                            \
     hipLaunchKernelGGL((k_res_update<WT, L>), ug, dim3(kUpdThreads), L ? lds : 0, st, c->d_rd, c->d_a_rp,          \
                        c->d_a_col, (const WT *)c->d_a_val, c->d_w_rp, c->d_w_col, (const WT *)c->d_w_val, ell,    \
@@ -873,6 +862,27 @@ extern "C" int sml_res_step(sml_reservoirs *c, const double *d_feedback, const d
     }
 #undef SML_UPD
     SML_HIP(hipGetLastError());
+    SML_HIP(hipGetLastError());
+    return SML_OK;
+}
+}  // namespace
+
+extern "C" int sml_res_step(sml_reservoirs *c, const double *d_feedback, const double *d_local_model,
+                            double *d_outvec, void *stream) {
+    SML_REQUIRE(c, "null context");
+    if (c->nlocal == 0) return SML_OK;
+    SML_REQUIRE(d_feedback && d_outvec, "null device buffer");
+    SML_REQUIRE(c->ncs == 0 || d_local_model, "hybrid context needs d_local_model");
+    for (int i = 0; i < c->nlocal; ++i)
+        if (!c->loaded[i]) return fail(SML_ERR_STATE, "local region %d has no weights loaded", i);
+    hipStream_t st = (hipStream_t)stream;
+    const double *xo = c->d_x[c->cur];
+    double *xn = c->d_x[1 - c->cur];
+    const bool rec = c->timing && c->ev_used < c->ev_cap;
+    hipEvent_t *ev = rec ? &c->ev[3 * c->ev_used] : nullptr;
+    if (rec) SML_HIP(hipEventRecord(ev[0], st));
+    const double *lmp = c->ncs ? d_local_model : nullptr;
+    if (int rc = launch_update(c, xo, xn, d_feedback, lmp, st)) return rc;
     if (rec) SML_HIP(hipEventRecord(ev[1], st));
     const int groups = c->nout_pad / kRows;
     const int nitems = c->nlocal * groups;
@@ -890,6 +900,26 @@ extern "C" int sml_res_step(sml_reservoirs *c, const double *d_feedback, const d
         ++c->ev_used;
     }
     c->cur = 1 - c->cur;
+    return SML_OK;
+}
+
+// synchronize (src/mod_reservoir.f90:1352-1378): `length` reservoir updates driven
+// by a sequence of inputs, no readout -- the spin-up of start_prediction (:938-959).
+// d_inputs: length blocks of the packed feedback layout (sml_res_feedback_offsets),
+// block i at d_inputs + i * stride doubles.
+extern "C" int sml_res_synchronize(sml_reservoirs *c, const double *d_inputs, int length, int64_t stride,
+                                   void *stream) {
+    SML_REQUIRE(c && length >= 0, "bad argument");
+    if (c->nlocal == 0 || length == 0) return SML_OK;
+    SML_REQUIRE(d_inputs && stride >= (int64_t)c->tot_fb, "stride smaller than the packed feedback size");
+    for (int i = 0; i < c->nlocal; ++i)
+        if (!c->loaded[i]) return fail(SML_ERR_STATE, "local region %d has no weights loaded", i);
+    hipStream_t st = (hipStream_t)stream;
+    for (int t = 0; t < length; ++t) {
+        if (int rc = launch_update(c, c->d_x[c->cur], c->d_x[1 - c->cur], d_inputs + (size_t)t * stride, nullptr, st))
+            return rc;
+        c->cur = 1 - c->cur;
+    }
     return SML_OK;
 }
 

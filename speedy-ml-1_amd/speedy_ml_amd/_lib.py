@@ -27,7 +27,7 @@ EXPORTED = (
     "sml_grid_host", "sml_spec_host",
     "sml_res_create", "sml_res_destroy", "sml_res_ninp", "sml_res_feedback_offsets",
     "sml_res_load_region_f32", "sml_res_load_region_f64", "sml_res_set_state", "sml_res_get_state",
-    "sml_res_step", "sml_res_step_host", "sml_res_footprint", "sml_res_enable_timing",
+    "sml_res_step", "sml_res_step_host", "sml_res_synchronize", "sml_res_footprint", "sml_res_enable_timing",
     "sml_res_kernel_times", "sml_exchange_assemble", "sml_res_tile_inputs",
     "sml_nc_read_region", "sml_nc_write_region",
     "sml_dyn_create", "sml_dyn_destroy", "sml_dyn_impint", "sml_dyn_set_forcing", "sml_dyn_set_state",
@@ -100,6 +100,7 @@ def _declare(L: ctypes.CDLL) -> None:
         "sml_res_get_state": [vp, i, vp],
         "sml_res_step": [vp, vp, vp, vp, vp],
         "sml_res_step_host": [vp, vp, vp, vp],
+        "sml_res_synchronize": [vp, vp, i, ctypes.c_int64, vp],
         "sml_res_footprint": [vp, i64p, i64p],
         "sml_res_enable_timing": [vp, i],
         "sml_res_kernel_times": [vp, vp, vp, i, ctypes.POINTER(ctypes.c_int)],

@@ -104,6 +104,15 @@ class Reservoirs:
         check(lib().sml_res_step(self._h, ptr(d_feedback), ptr(d_local_model if self.ncs else None),
                                  ptr(d_outvec), stream_ptr(stream)))
 
+    def synchronize(self, d_inputs, length: int, stride: int | None = None, stream=None):
+        """synchronize (mod_reservoir.f90:1352-1378): `length` state updates, no
+        readout.  d_inputs: device tensor of `length` packed feedback blocks
+        (row t = block t, stride = total feedback doubles unless given)."""
+        stride = int(self.fb_offsets[-1]) if stride is None else int(stride)
+        if d_inputs.numel() < length * stride:
+            raise ValueError("d_inputs holds fewer than length * stride doubles")
+        check(lib().sml_res_synchronize(self._h, ptr(d_inputs), length, stride, stream_ptr(stream)))
+
     def predict_host(self, feedback: np.ndarray, local_model: np.ndarray | None) -> np.ndarray:
         fb = np.ascontiguousarray(feedback, dtype=np.float64)
         lm = np.ascontiguousarray(local_model, dtype=np.float64) if local_model is not None else None

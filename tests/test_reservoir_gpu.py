@@ -183,3 +183,24 @@ def test_netcdf_loaded_weights_match(cuda, tmp_path):
     fb = feedback_vector(600, w.ninp)
     lm = local_model_vector(600)[None, :]
     np.testing.assert_array_equal(a.predict_host(fb, lm), b.predict_host(fb, lm))
+
+
+def test_synchronize_matches_oracle(cuda):
+    """synchronize (mod_reservoir.f90:1352-1378) updates the state exactly as
+    predict does (:1440-1446) without the readout: the oracle's predict restatement
+    gives the reference state sequence."""
+    import torch
+
+    res, ws = _build(CASES[:4], n_override=700)
+    length = 6
+    tot = res.fb_offsets[-1]
+    rng = np.random.default_rng(4)
+    inputs = rng.standard_normal((length, tot))
+    res.synchronize(torch.from_numpy(inputs).to(cuda), length)
+    torch.cuda.synchronize()
+    o = res.fb_offsets
+    for i, w in enumerate(ws):
+        x = initial_state(w.region, w.n)
+        for t in range(length):
+            _, x = _oracle_step(w, x, inputs[t, o[i]:o[i + 1]], np.zeros(132))
+        _check(res.get_state(i), x, 1e-13)
