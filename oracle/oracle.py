@@ -77,6 +77,11 @@ def _declare(L):
     L.orc_iogrid30.argtypes = [vp] * 8
     L.orc_iogrid31.argtypes = [vp] * 7
     L.orc_train_accumulate.argtypes = [i, i, i, vp, vp, vp, vp]
+    L.orc_phys_init.argtypes = [vp, vp]
+    L.orc_phys_tables.argtypes = [vp, vp, vp]
+    L.orc_sol_oz.argtypes = [d, vp, vp, vp, vp, vp]
+    L.orc_sflset.argtypes = [vp, vp]
+    L.orc_phypar_grid.argtypes = [vp] * 11 + [i, vp]
     L.orc_train_solve.argtypes = [i, i, i, d, d, i, d, vp, vp, vp]
 
 
@@ -399,6 +404,61 @@ def train_solve(G, B, ncs, beta_res, beta_model, using_prior=True, prior_val=0.0
     info = lib().orc_train_solve(naug, nout, ncs, beta_res, beta_model, int(using_prior), prior_val, _p(G), _p(B),
                                  _p(w))
     return w, info
+
+
+# ---------------------------------------------------------------- physics
+NGP = IX * IL
+PHYS_BC = ("fmask1", "phis0", "stl_am", "sst_am", "soilw_am", "alb_l", "alb_s", "albsfc", "snowc",
+           "fsol", "ozone", "ozupp", "zenit", "stratz", "forog")
+HSG = np.array([0.000, 0.050, 0.140, 0.260, 0.420, 0.600, 0.770, 0.900, 1.000])
+
+
+def radang():
+    """radang(il) of indyns (ini_indyns.f90:49-56) from the Gaussian latitudes."""
+    sia = tables()["sia"]
+    r = np.zeros(IL)
+    r[:IY] = -np.arcsin(sia)
+    r[IL - 1:IY - 1:-1] = np.arcsin(sia)
+    return r
+
+
+def phys_init():
+    """inphys(hsg, ppl, radang) + radset."""
+    spectral_init()
+    lib().orc_phys_init(_p(np.ascontiguousarray(HSG)), _p(np.ascontiguousarray(radang())))
+
+
+def sol_oz(tyear):
+    phys_init()
+    out = [np.zeros(NGP) for _ in range(5)]
+    lib().orc_sol_oz(tyear, *[_p(o) for o in out])
+    return dict(zip(("fsol", "ozone", "ozupp", "zenit", "stratz"), out))
+
+
+def sflset(phi0):
+    forog = np.zeros(NGP)
+    lib().orc_sflset(_p(np.ascontiguousarray(phi0, dtype=np.float64).ravel()), _p(forog))
+    return forog
+
+
+def phys_state():
+    """Radiation state kept between physics calls: tau2 (4, kx, ngp), stratc
+    (2, ngp), tt_rsw (kx, ngp), ssrd (ngp)."""
+    return {"tau2": np.zeros((4, KX, NGP)), "stratc": np.zeros((2, NGP)), "tt_rsw": np.zeros((KX, NGP)),
+            "ssrd": np.zeros(NGP)}
+
+
+def phypar_grid(ug1, vg1, tg1, qg1, phig1, pslg1, bc, state, lradsw):
+    """phypar's physics tendencies (4, kx, ngp) = u, v, t, q from grid inputs
+    (kx, ngp) / (ngp,); bc: dict of PHYS_BC arrays (ngp,); state updated in place."""
+    phys_init()
+    f = lambda a: np.ascontiguousarray(a, dtype=np.float64)
+    bcs = np.ascontiguousarray(np.stack([np.asarray(bc[k], dtype=np.float64).ravel() for k in PHYS_BC]))
+    tend = np.zeros((4, KX, NGP))
+    ins = [f(x) for x in (ug1, vg1, tg1, qg1, phig1, pslg1)]
+    lib().orc_phypar_grid(*[_p(x) for x in ins], _p(bcs), _p(state["tau2"]), _p(state["stratc"]),
+                          _p(state["tt_rsw"]), _p(state["ssrd"]), int(bool(lradsw)), _p(tend))
+    return tend
 
 
 # ---------------------------------------------------------------- reference (pinning only)
