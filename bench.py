@@ -1,22 +1,27 @@
 #!/usr/bin/env python3
 """bench.py -- SPEEDY-ML hybrid hot path on MI355X (one process per GPU).
 
-One "step" = one hybrid-step pass over the reservoir side of the hot path for all
-1152 subdomains (BASELINE.json configs[1], sharded per configs[3]):
+One "step" = one hybrid timestep (BASELINE.json
+configs[2] on one GPU, configs[3] sharded over N):
 
   1. predict for every local region: A x + W_in u -> tanh -> W_out [model; x~],
      unstandardize                       (mod_reservoir.f90:1416-1487, 2 kernels)
   2. exchange: all-gather of every rank's outvecs over RCCL (N > 1)
                                          (replaces mpires.f90:338-716 MPI p2p)
   3. assemble the global T30L8 grid + clips (mpires.f90:300-478)
-  4. re-tile every local region's next feedback (overlap tiles, standardized) and
+  4. the SPEEDY 6-h window on the assembled grid (run_model -> agcm_main,
+     mpires.f90:1516-1628): iogrid(30) entry transforms + safety check, stepone +
+     24 leapfrog steps of dyn_step WITH phypar's physics (dyn_stloop.f90:26-92),
+     iogrid(31) exit transforms -- every transform, the dynamics and the column
+     physics on the GPU, replicated on every rank
+  5. re-tile every local region's next feedback (overlap tiles, standardized) and
      its standardized SPEEDY local vector (mpires.f90:558-751)
 
-The SPEEDY window itself (26 dyn_steps with physics) is not part of this step yet:
-the SPEEDY forecast grids consumed in (4) are a fixed synthetic T30L8 state.  Data
-are synthetic, weights random with the trained structure, 6000-node-class
-reservoirs (n = 5760/6160/6048/5880), fp64 arithmetic, weights held at their fp32
-file precision (exact).
+Data are synthetic: weights random with the trained structure, 6000-node-class
+reservoirs (n = 5760/6160/6048/5880), a seeded T30L8 analysis state, synthetic
+boundary fields for the physics.  fp64 arithmetic throughout; reservoir weights
+held at their fp32 file precision (exact).  The reservoir side alone (configs[1])
+is reported beside the headline as `reservoir_only`.
 
 Usage: python bench.py [--gpus N --steps K --warmup W]
        python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
@@ -41,7 +46,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level para
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--steps", type=int, default=30)
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--regions", type=int, default=1152)
     p.add_argument("--weights", choices=("f32", "f64"), default="f32")
@@ -50,11 +55,10 @@ def parse():
     p.add_argument("--train-regions", type=int, default=8,
                    help="regions in the supplementary W_out-training leg (0 = skip)")
     p.add_argument("--train-steps", type=int, default=4096, help="training time steps per region in that leg")
-    p.add_argument("--hybrid-steps", type=int, default=10,
-                   help="hybrid steps timed in the supplementary configs[2] leg (reservoir + SPEEDY dynamics "
-                        "window; 0 = skip)")
+    p.add_argument("--reservoir-steps", type=int, default=50,
+                   help="steps timed in the supplementary reservoir-only (configs[1]) leg (0 = skip)")
     p.add_argument("--speedy-steps", type=int, default=48,
-                   help="leapfrog steps timed in the supplementary SPEEDY-dynamics leg (0 = skip)")
+                   help="leapfrog steps timed in the supplementary SPEEDY-step leg (0 = skip)")
     return p.parse_args()
 
 
@@ -69,9 +73,11 @@ def main():
     import torch.distributed as dist
 
     from speedy_ml_amd import domain
+    from speedy_ml_amd.dynamics import Dynamics
     from speedy_ml_amd.exchange import OutvecExchange
     from speedy_ml_amd.reservoir import Reservoirs
-    from speedy_ml_amd.synthetic import initial_state, region_weights, synthetic_grids
+    from speedy_ml_amd.synthetic import (dyn_state, initial_state, phys_boundary, region_weights,
+                                         synthetic_grids)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -111,6 +117,13 @@ def main():
     f4 = torch.from_numpy(f4h).to(dev)
     f2 = torch.from_numpy(f2h).to(dev)
     tisr = torch.from_numpy(np.random.default_rng(13).standard_normal((len(regions), 16))).to(dev)
+    # SPEEDY on the GPU: dynamical core + physics, forcing and boundary fields
+    st0, forcing = dyn_state()
+    dyn = Dynamics()
+    dyn.set_forcing(**forcing)
+    dyn.set_state(st0)
+    phys_bc = phys_boundary(dyn, forcing["phis"])
+    dyn.set_physics(phys_bc)
     # initial inputs from the synthetic analysis state (start_prediction analogue)
     res.tile_inputs(g4, g2, pr, f4, f2, tisr, fb, lm)
     torch.cuda.synchronize()
@@ -120,27 +133,37 @@ def main():
         res.predict(fb, lm, ov)
         glob = exchange(ov)  # RCCL all-gather over xGMI when world > 1
         res.assemble(glob, g4, g2, pr)
+        dyn.from_grid(g4, g2)  # iogrid(30); min/max for the safety check stay on the device
+        dyn.window(24)         # stepone + 24 x step(2,2) with physics (hipGraph replay)
+        dyn.to_grid(f4, f2)    # iogrid(31): the forecast the next local_model is tiled from
         res.tile_inputs(g4, g2, pr, f4, f2, tisr, fb, lm)
+
+    def timed(fn, nsteps, timing=False):
+        if timing:
+            res.enable_timing(nsteps)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(nsteps):
+            fn()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        dt = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([dt], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dt = float(t.item())
+        return dt
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    res.enable_timing(args.steps)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    dt = time.perf_counter() - t0
+    dt = timed(step, args.steps, timing=True)
     upd_ms, rd_ms = res.kernel_times()
-    if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+    _, safe = dyn.from_grid(g4.cpu().numpy(), g2.cpu().numpy())
+    finite = bool(torch.isfinite(f4).all().item()) and bool(torch.isfinite(ov).all().item())
 
     # ---- roofline of the dominant kernel (readout: streams W_out)
     wb = 4 if args.weights == "f32" else 8
@@ -158,13 +181,28 @@ def main():
         except Exception:
             traffic = None
 
+    # supplementary: the reservoir side alone (configs[1]), SPEEDY's step alone
+    reservoir_only = None
+    if args.reservoir_steps > 0:
+        def rstep():
+            res.predict(fb, lm, ov)
+            glob = exchange(ov)
+            res.assemble(glob, g4, g2, pr)
+            res.tile_inputs(g4, g2, pr, f4, f2, tisr, fb, lm)
+
+        for _ in range(3):
+            rstep()
+        rdt = timed(rstep, args.reservoir_steps)
+        reservoir_only = {
+            "workload": "configs[1]: predict for all 1152 subdomains + RCCL outvec all-gather + assemble + "
+                        "re-tile (SPEEDY forecast grids held fixed)",
+            "value": round(args.reservoir_steps / rdt, 3), "unit": "hybrid timesteps/s",
+            "ms_per_step": round(rdt / args.reservoir_steps * 1e3, 4), "steps": args.reservoir_steps}
+    dyn.close()
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.cpu_sample > 0:
-        cpu = cpu_baseline(args.cpu_sample, nreg, mask)
+        cpu = cpu_baseline(args.cpu_sample, nreg, mask, phys_bc)
     speedy = speedy_leg(dev, world, rank, args) if args.speedy_steps > 0 else None
-    hybrid = None
-    if args.hybrid_steps > 0:
-        hybrid = hybrid_leg(dev, world, res, exchange, (fb, lm, ov), (g4, g2, pr, f4, f2, tisr), args)
     training = training_leg(dev, mask, args) if args.train_regions > 0 and world == 1 else None
 
     if rank == 0:
@@ -181,18 +219,22 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic (seeded T30L8 state, random weights with the trained structure)",
+            "data": "synthetic (seeded T30L8 state and boundary fields, random weights with the trained structure)",
             "config": {
-                "workload": "configs[1]: batched reservoir forward for all 1152 subdomains + RCCL outvec "
-                            "all-gather + global-grid assembly + feedback/local-model re-tiling; SPEEDY "
-                            "window not included (fixed synthetic forecast grids)",
+                "workload": f"configs[{2 if world == 1 else 3}]: full hybrid timestep -- reservoir predict for all "
+                            "1152 subdomains, RCCL outvec all-gather, assemble, SPEEDY 6-h window (iogrid(30), "
+                            "stepone + 24 leapfrog dyn_steps with phypar physics, iogrid(31)) on the GPU, re-tile",
                 "regions": nreg,
                 "regions_per_gpu": len(regions),
                 "reservoir_nodes": "5760/6160/6048/5880 (NINT(6000/ninp)*ninp)",
                 "weights": f"{args.weights} storage ({'exact file precision' if args.weights == 'f32' else 'fp64'}), "
                            "fp64 arithmetic",
-                "parallelism": f"res_domain sharded over {world} GPU(s)",
+                "parallelism": f"res_domain sharded over {world} GPU(s); SPEEDY window replicated per GPU",
+                "speedy": "T30L8, 26 dyn_steps per window (nsteps 96/day, delt 900 s), physics on, "
+                          "shortwave every 3rd step",
             },
+            "last_window_safe": bool(safe),
+            "finite": finite,
             "roofline": {
                 "kernel": "k_res_readout (W_out GEMV, 17 waves x 8 rows per region)",
                 "bound": "hbm",
@@ -208,8 +250,8 @@ def main():
                 "step_algorithmic_bytes": algo_step,
             },
             "cpu_baseline": cpu,
-            "speedy_dynamics": speedy,
-            "hybrid_with_dynamics": hybrid,
+            "reservoir_only": reservoir_only,
+            "speedy_step": speedy,
             "training": training,
         }
         print(json.dumps(line), flush=True)
@@ -218,104 +260,54 @@ def main():
 
 
 def speedy_leg(dev, world, rank, args):
-    """Supplementary measurement, outside the headline step: SPEEDY's dynamical core
-    (dyn_step without physics) on the GPU, timed per leapfrog step with HIP events,
-    launched step by step and replayed from a hipGraph, plus the oracle's step on
-    one host core.  A 6-h window is stepone + 24 leapfrog steps (nsteps = 96/day)."""
+    """Supplementary measurement: one SPEEDY dyn_step on the GPU without and with
+    the physics (leapfrog step(2,2), HIP events, launched step by step and replayed
+    from hipGraphs), plus the oracle's step with physics on one host core."""
     import torch
 
     from speedy_ml_amd.dynamics import DELT, Dynamics
-    from speedy_ml_amd.synthetic import dyn_state
+    from speedy_ml_amd.synthetic import dyn_state, phys_boundary
 
     st, forcing = dyn_state()
     dyn = Dynamics()
     dyn.set_forcing(**forcing)
+    bc = phys_boundary(dyn, forcing["phis"])
     out = {}
-    for mode, graph in (("launch", False), ("graph", True)):
-        dyn.set_state(st)
-        dyn.stepone()
-        dyn.leapfrog(4, DELT, graph=graph)  # warm-up (and graph capture)
-        torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        dyn.leapfrog(args.speedy_steps, DELT, graph=graph)
-        e1.record()
-        torch.cuda.synchronize()
-        out[f"step_ms_{mode}"] = round(e0.elapsed_time(e1) / args.speedy_steps, 4)
-    out["window_ms_graph"] = round(26 * out["step_ms_graph"], 3)
-    out["note"] = ("dynamics only (grtend/sptend/implic/hordif/timint, 164 transforms as 7 batched launches); "
-                   "physics not on the GPU, not part of the headline value")
+    for phys in (False, True):
+        dyn.set_physics(bc if phys else None)
+        for mode, graph in (("launch", False), ("graph", True)):
+            dyn.set_state(st)
+            dyn.set_rad_state(None)
+            dyn.set_clock(1, True)
+            dyn.stepone()
+            dyn.leapfrog(6, DELT, graph=graph)  # warm-up (and graph capture for both lradsw values)
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            dyn.leapfrog(args.speedy_steps, DELT, graph=graph)
+            e1.record()
+            torch.cuda.synchronize()
+            out[f"step_ms_{mode}{'_physics' if phys else ''}"] = round(e0.elapsed_time(e1) / args.speedy_steps, 4)
+    out["window_ms_graph_physics"] = round(26 * out["step_ms_graph_physics"], 3)
+    out["note"] = ("dyn_step = grtend/sptend/implic/hordif/timint (164 transforms) without physics; with physics "
+                   "+ phypar on level 1 (41 more transforms, one column-physics kernel)")
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         sys.path.insert(0, os.path.join(REPO, "oracle"))
         import oracle
 
         s = oracle.dyn_state_copy(st)
-        oracle.dyn_step(s, forcing["phis"], forcing["tcorh"], forcing["qcorh"], None, 2, 2, 2 * DELT, 0.5)
+        rad = oracle.phys_state()
+        oracle.dyn_step_physics(s, forcing["phis"], forcing["tcorh"], forcing["qcorh"], bc, rad, True, 2, 2,
+                                2 * DELT, 0.5)
         t0 = time.perf_counter()
         nrep = 5
-        for _ in range(nrep):
-            oracle.dyn_step(s, forcing["phis"], forcing["tcorh"], forcing["qcorh"], None, 2, 2, 2 * DELT, 0.5)
-        out["cpu_oracle_step_ms"] = round((time.perf_counter() - t0) / nrep * 1e3, 3)
-        out["cpu_oracle_note"] = "oracle C restatement (long-double DFT instead of FFTPACK), 1 core"
+        for i in range(nrep):
+            oracle.dyn_step_physics(s, forcing["phis"], forcing["tcorh"], forcing["qcorh"], bc, rad, i % 3 == 0, 2, 2,
+                                    2 * DELT, 0.5)
+        out["cpu_oracle_step_ms_physics"] = round((time.perf_counter() - t0) / nrep * 1e3, 3)
+        out["cpu_oracle_note"] = "oracle C restatement (direct DFT instead of FFTPACK), 1 core"
     dyn.close()
     return out
-
-
-def hybrid_leg(dev, world, res, exchange, io, grids, args):
-    """Supplementary measurement, BASELINE configs[2] shape (dynamics only): one
-    hybrid step = predict for every local region -> RCCL all-gather -> assemble ->
-    iogrid(30) -> stepone + 24 leapfrog steps of the dynamical core -> iogrid(31)
-    -> re-tile feedback and local model.  Every stage on the GPU, no host sync
-    inside the step.  Physics (phypar) is not computed (zero tendencies), so this
-    is not the reference's full window and not the headline value."""
-    import torch
-    import torch.distributed as dist
-
-    from speedy_ml_amd.dynamics import Dynamics
-    from speedy_ml_amd.synthetic import dyn_state
-
-    fb, lm, ov = io
-    g4, g2, pr, f4, f2, tisr = grids
-    _, forcing = dyn_state()
-    dyn = Dynamics()
-    dyn.set_forcing(**forcing)
-
-    def hstep():
-        res.predict(fb, lm, ov)
-        glob = exchange(ov)
-        res.assemble(glob, g4, g2, pr)
-        dyn.from_grid(g4, g2)   # iogrid(30), min/max for the safety check stay on the device
-        dyn.window(24)          # stepone + 24 x step(2,2) (hipGraph replay)
-        dyn.to_grid(f4, f2)     # iogrid(31)
-        res.tile_inputs(g4, g2, pr, f4, f2, tisr, fb, lm)
-
-    for _ in range(2):
-        hstep()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.hybrid_steps):
-        hstep()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-    _, safe = dyn.from_grid(g4.cpu().numpy(), g2.cpu().numpy())
-    dyn.close()
-    return {
-        "value": round(args.hybrid_steps / dt, 3),
-        "unit": "hybrid timesteps/s",
-        "ms_per_step": round(dt / args.hybrid_steps * 1e3, 4),
-        "steps": args.hybrid_steps,
-        "last_window_safe": bool(safe),
-        "note": "configs[2] shape without physics: SPEEDY window = iogrid(30) + stepone + 24 leapfrog dynamics "
-                "steps + iogrid(31), replicated on every rank; phypar not on the GPU yet",
-    }
 
 
 def training_leg(dev, mask, args):
@@ -383,11 +375,12 @@ def training_leg(dev, mask, args):
     }
 
 
-def cpu_baseline(sample: int, nreg: int, mask):
-    """The oracle's restatement of predict (dense W_in matmul, COO SpMV, dense W_out
-    GEMV: the reference's arithmetic) timed on one host core over a bounded sample
-    of regions spread over the shape classes, plus the exchange/tiling oracle on
-    every region; extrapolated to one hybrid step of all 1152 regions."""
+def cpu_baseline(sample: int, nreg: int, mask, bc):
+    """The oracle's restatement of the hybrid step on one host core: predict
+    (dense W_in matmul, COO SpMV, dense W_out GEMV: the reference's arithmetic) over
+    a bounded sample of regions spread over the shape classes, extrapolated to all
+    1152; the exchange/tiling oracle on every region; one whole SPEEDY window
+    (iogrid(30), stepone + 24 leapfrog steps with physics, iogrid(31))."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle
     from speedy_ml_amd import domain
@@ -418,7 +411,24 @@ def cpu_baseline(sample: int, nreg: int, mask):
         oracle.tile_feedback(r, g4, g2, pr, np.zeros(36), ms, np.zeros(16))
         oracle.tile_local_model(r, g4, g2, np.zeros(36), ms)
     t_xchg = time.perf_counter() - t0
-    step_s = per_region * nreg + t_xchg
+    # the SPEEDY window
+    from speedy_ml_amd.dynamics import DELT
+    from speedy_ml_amd.synthetic import dyn_state
+
+    st, forcing = dyn_state()
+    s = oracle.dyn_state_copy(st)
+    og4, olp = oracle.iogrid31(oracle.dyn_state_copy(st))
+    rad = oracle.phys_state()
+    f = (forcing["phis"], forcing["tcorh"], forcing["qcorh"], bc, rad)
+    t0 = time.perf_counter()
+    oracle.iogrid30(s, og4, olp)
+    oracle.dyn_step_physics(s, *f, True, 1, 1, 0.5 * DELT, 0.5)
+    oracle.dyn_step_physics(s, *f, True, 1, 2, DELT, 0.5)
+    for i in range(1, 25):
+        oracle.dyn_step_physics(s, *f, i % 3 == 1, 2, 2, 2 * DELT, 0.5)
+    oracle.iogrid31(s)
+    t_win = time.perf_counter() - t0
+    step_s = per_region * nreg + t_xchg + t_win
     return {
         "value": round(1.0 / step_s, 4),
         "unit": "hybrid timesteps/s",
@@ -426,7 +436,8 @@ def cpu_baseline(sample: int, nreg: int, mask):
         "kind": "port",
         "sample": f"oracle predict (dense W_in as the reference) timed on {len(picks)} of {nreg} regions "
                   f"(every {stride}th, all shape classes), {per_region * 1e3:.3f} ms/region, extrapolated to "
-                  f"{nreg}; + host assemble/tile of all regions {t_xchg * 1e3:.1f} ms; "
+                  f"{nreg}; + host assemble/tile of all regions {t_xchg * 1e3:.1f} ms; + one SPEEDY window "
+                  f"(26 steps with physics + iogrid) {t_win * 1e3:.1f} ms; "
                   f"host {platform.processor() or platform.machine()}, {os.cpu_count()} logical CPUs visible",
     }
 

@@ -258,6 +258,40 @@ int sml_dyn_to_grid_host(sml_dynamics *d, double *grid4d, double *logp);
 int sml_dyn_step_host(sml_dynamics *d, int j1, int j2, double dt, double alph, double rob, double wil,
                       const double *phys);
 
+/* ---------------------------------------------------------------- physics */
+/* phypar on the GPU (src/phy_phypar.f90:1-228 with convmf, lscond, cloud, radsw,
+ * radlw, suflux, vdifsc; icsea = 0, lrandf and sppt off as in the hybrid runs).
+ * bc: host [15][ix*il] boundary fields in this order -- fmask1, phis0 (mod_surfcon),
+ * stl_am, sst_am, soilw_am (mod_var_land/sea), alb_l, alb_s, albsfc, snowc, fsol,
+ * ozone, ozupp, zenit, stratz (mod_radcon), forog (mod_sflcon).  Once set, every
+ * step computes the physics of time level 1 on the GPU (dyn_grtend.f90:223-226)
+ * and d_phys arguments must be NULL; bc = NULL switches it off.  Call again when the
+ * fields change (the coupler / sol_oz run once a day, ini_fordate.f90). */
+int sml_dyn_set_physics(sml_dynamics *d, const double *bc);
+/* stloop's clock (dyn_stloop.f90:37-56): istep and mod_lflags' lradsw.  sml_dyn_step
+ * uses lradsw as it stands; sml_dyn_leapfrog sets lradsw = (mod(istep, 3) == 1)
+ * before each step and advances istep, as stloop does.  Initial: istep 1, lradsw 1. */
+int sml_dyn_set_clock(sml_dynamics *d, int istep, int lradsw);
+int sml_dyn_get_clock(const sml_dynamics *d, int *istep, int *lradsw);
+/* radiation state kept between steps (mod_radcon tau2, stratc; mod_physvar tt_rsw,
+ * ssrd), host [4*kx*ngp tau2 | 2*ngp stratc | kx*ngp tt_rsw | ngp ssrd], layouts
+ * [band][k][ngp], [2][ngp], [k][ngp]; NULL to set = zero */
+int sml_dyn_set_rad_state(sml_dynamics *d, const double *rad);
+int sml_dyn_get_rad_state(sml_dynamics *d, double *rad);
+/* phypar alone on grid inputs (the arrays phypar builds, phy_phypar.f90:54-66):
+ * ug1, vg1, tg1, qg1, phig1 [kx][ngp] (k = 1 top), pslg1 [ngp]; tendencies
+ * d_tend [4][kx][ngp] = u, v, t, q.  Uses and updates the radiation state. */
+int sml_dyn_phypar(sml_dynamics *d, const double *d_ug1, const double *d_vg1, const double *d_tg1,
+                   const double *d_qg1, const double *d_phig1, const double *d_pslg1, int lradsw, double *d_tend,
+                   void *stream);
+int sml_dyn_phypar_host(sml_dynamics *d, const double *ug1, const double *vg1, const double *tg1, const double *qg1,
+                        const double *phig1, const double *pslg1, int lradsw, double *tend);
+/* host forcing helpers: sol_oz(tyear) (src/phy_radiat.f90:1-121) -> fields5
+ * [5][ngp] = fsol, ozone, ozupp, zenit, stratz; sflset (src/phy_suflux.f90:358-382)
+ * phi0 [ngp] -> forog [ngp] */
+int sml_dyn_sol_oz(const sml_dynamics *d, double tyear, double *fields5);
+int sml_phys_sflset(const double *phi0, double *forog);
+
 /* ---------------------------------------------------------------- training */
 /* W_out ridge training for a batch of regions (one vertical level each).
  *   chunking_matmul  (src/mod_reservoir.f90:1643-1699): G += S S^T, B += T S^T

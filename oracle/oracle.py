@@ -82,6 +82,7 @@ def _declare(L):
     L.orc_sol_oz.argtypes = [d, vp, vp, vp, vp, vp]
     L.orc_sflset.argtypes = [vp, vp]
     L.orc_phypar_grid.argtypes = [vp] * 11 + [i, vp]
+    L.orc_phys_inputs.argtypes = [vp] * 12
     L.orc_train_solve.argtypes = [i, i, i, d, d, i, d, vp, vp, vp]
 
 
@@ -439,6 +440,26 @@ def sflset(phi0):
     forog = np.zeros(NGP)
     lib().orc_sflset(_p(np.ascontiguousarray(phi0, dtype=np.float64).ravel()), _p(forog))
     return forog
+
+
+def phys_inputs(state, phis):
+    """phypar's grid inputs of level 1 of `state` (geop(1), uvspec, grid):
+    (ug1, vg1, tg1, qg1, phig1 (kx, ngp), pslg1 (ngp,))."""
+    spectral_init()
+    L = lib()
+    L.orc_dyn_init()
+    outs = [np.zeros((KX, NGP)) for _ in range(5)] + [np.zeros(NGP)]
+    ph = np.ascontiguousarray(phis, dtype=np.complex128)
+    L.orc_phys_inputs(_p(state["vor"]), _p(state["div"]), _p(state["t"]), _p(state["ps"]), _p(state["tr"]), _p(ph),
+                      *[_p(o) for o in outs])
+    return outs
+
+
+def dyn_step_physics(state, phis, tcorh, qcorh, bc, rad, lradsw, j1, j2, dt, alph, rob=0.05, wil=0.53):
+    """step with phypar evaluated on level 1 first (dyn_step.f90:45 -> grtend(.., 1, j2)
+    -> phypar, dyn_grtend.f90:223-226); rad (phys_state()) is updated in place."""
+    tend = phypar_grid(*phys_inputs(state, phis), bc, rad, lradsw)
+    return dyn_step(state, phis, tcorh, qcorh, tend.reshape(4, KX, IL, IX), j1, j2, dt, alph, rob, wil)
 
 
 def phys_state():

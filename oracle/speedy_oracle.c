@@ -1024,6 +1024,28 @@ static void orc_geop(const double *t, const double *phis, int jj, double *phi)
     }
 }
 
+/* phypar's grid inputs of time level 1 (dyn_grtend.f90:223-226, phy_phypar.f90:54-66):
+ * geop(1), then per level uvspec + grid(.,2) -> ug1, vg1; grid(t1), grid(q1),
+ * grid(phi) -> tg1, qg1, phig1 [KX][GF]; grid(ps1) -> pslg1 [GF]. */
+void orc_phys_inputs(const double *vor, const double *div, const double *t, const double *ps, const double *tr,
+                     const double *phis, double *ug1, double *vg1, double *tg1, double *qg1, double *phig1,
+                     double *pslg1)
+{
+    static double phi[KX * SF], uc[SF], vc[SF];
+    orc_geop(t, phis, 1, phi);
+    for (int k = 0; k < KX; ++k) {
+        orc_uvspec(SPX(vor, 0, k), SPX(div, 0, k), uc, vc);
+        orc_grid(uc, ug1 + (size_t)k * GF, 2);
+        orc_grid(vc, vg1 + (size_t)k * GF, 2);
+    }
+    for (int k = 0; k < KX; ++k) {
+        orc_grid(SPX(t, 0, k), tg1 + (size_t)k * GF, 1);
+        orc_grid(SPX(tr, 0, k), qg1 + (size_t)k * GF, 1);
+        orc_grid(phi + (size_t)k * SF, phig1 + (size_t)k * GF, 1);
+    }
+    orc_grid(ps, pslg1, 1);
+}
+
 /* grtend(vordt, divdt, tdt, psdt, trdt, 1, j2) (dyn_grtend.f90:61-278) */
 static void orc_grtend(const double *vor, const double *div, const double *t, const double *ps, const double *tr,
                        const double *phys, int j2, double *vordt, double *divdt, double *tdt, double *psdt,

@@ -15,10 +15,16 @@
 // after the forward transforms (vds/lap assembly, sptend, geop, implic, hordif,
 // drag, timint) runs in two kernels with a thread per spectral coefficient (m, n)
 // that owns all levels, variables and both time levels of that coefficient, so no
-// stage needs a grid-wide synchronisation.  Physics (phypar) is out of scope on
-// the GPU: its grid-point tendencies enter through an optional input buffer at
-// the point where phypar adds them (after the dynamical tendencies, before the
-// spectral conversion), or are zero.
+// stage needs a grid-wide synchronisation.
+//
+// Physics (phypar, dyn_grtend.f90:223-226) runs on the GPU when the context has
+// boundary fields (sml_dyn_set_physics): grtend always evaluates it on time level 1
+// (dyn_step.f90:45), so the step adds 41 inverse transforms of level 1 (ucos,
+// vcos, t, q, geop(1), ps; phy_phypar.f90:54-66) to the same batched launches and
+// one column-physics kernel (sml_physics.hpp) whose tendencies enter where phypar
+// adds them (after the dynamical tendencies, before the spectral conversion).
+// Without boundary fields the tendencies come from an optional input buffer (a
+// host that keeps phypar on the CPU) or are zero.
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -26,6 +32,7 @@
 #include <new>
 
 #include "sml_dynamics_tables.hpp"
+#include "sml_physics.hpp"
 #include "sml_spectral_internal.hpp"
 
 using namespace sml;
@@ -35,11 +42,18 @@ namespace {
 constexpr int kSF = kMX2 * kNX;       // 1984 doubles per spectral field
 constexpr int kGF = kIX * kIL;        // 4608 doubles per grid field
 constexpr int kVF = kMX2 * kIL;       // 2976 doubles per Fourier field
-constexpr int kNInv = 6 * kKX + 2;    // 50 inverse transforms per step
+constexpr int kNInv = 6 * kKX + 2;    // 50 inverse transforms per step (dynamics)
 constexpr int kNInv1 = 4 * kKX;       // the first 32 are kcos = 1
+// with the physics on the GPU: kcos = 1 fields [vor div t tr (j2) | t1 q1 phi1 (8 each) | ps1]
+// then kcos = 2 fields [ucos vcos (j2) | psdx psdy | ucos1 vcos1]
+constexpr int kNInv1P = kNInv1 + 3 * kKX + 1;  // 57
+constexpr int kNInvP = kNInv1P + 4 * kKX + 2;  // 91 (= the reference's 91 grid calls per step)
+constexpr int kPT1 = kNInv1, kPQ1 = kNInv1 + kKX, kPPhi1 = kNInv1 + 2 * kKX, kPPs1 = kNInv1 + 3 * kKX;
+constexpr int kNInvMax = kNInvP;
 constexpr int kNFwdScaled = 6 * kKX;  // 48 vdspec inputs (x 1/cos lat)
 constexpr int kNFwd = 9 * kKX + 1;    // 73 forward transforms per step
 constexpr int kMN = kMX * kNX;        // 992 complex coefficients
+constexpr int kNstrad = 3;            // shortwave radiation every 3rd step (mod_tsteps.f90:65)
 
 // state buffer: vor(mx,nx,kx,2) | div | t | tr(ntr=1) | ps(mx,nx,2) (reference layouts)
 constexpr size_t kOffVor = 0, kOffDiv = 2 * kKX * kSF, kOffT = 4 * kKX * kSF, kOffTr = 6 * kKX * kSF,
@@ -66,16 +80,27 @@ struct sml_dynamics {
     double *d_phis = nullptr, *d_tcorh = nullptr, *d_qcorh = nullptr, *d_phi = nullptr;
     double *d_specin = nullptr, *d_varm = nullptr, *d_grid = nullptr, *d_gfwd = nullptr, *d_sfwd = nullptr;
     double *d_tend = nullptr;
-    double *d_phys = nullptr;  // staging for host-provided physics tendencies
+    double *d_phys = nullptr;  // physics tendencies: staging for a host's, or the GPU phypar's output
     double *d_minmax = nullptr;  // iogrid(30) safety check: min/max of u, v, t, q
     double *d_io = nullptr;      // staging for the host iogrid calls (grid4d + logp)
     bool impint_done = false;
-    // leapfrog replay: one step(2, 2, ...) captured as a hipGraph
+    // GPU physics (phypar): tables, boundary fields [kNBc][ngp], radiation state
+    PhysTables ptab;
+    PhysTables *d_ptab = nullptr;
+    double *d_pbc = nullptr, *d_rad = nullptr, *d_pio = nullptr;
+    bool phys_on = false;
+    // mod_lflags lradsw (module default .true.) and stloop's istep (at_gcm.f90:81)
+    bool lradsw = true;
+    int istep = 1;
+    // leapfrog replay: one step(2, 2, ...) captured as a hipGraph per lradsw value
     hipStream_t cap_stream = nullptr;
-    hipGraphExec_t graph = nullptr;
-    double g_key[4] = {0, 0, 0, 0};
-    const double *g_phys = nullptr;
-    const DynTables *g_tab = nullptr;
+    struct Replay {
+        hipGraphExec_t exec = nullptr;
+        double key[4] = {0, 0, 0, 0};
+        const double *phys = nullptr;
+        const DynTables *tab = nullptr;
+        bool phys_on = false;
+    } replay[2];
 };
 
 namespace {
@@ -108,11 +133,25 @@ __device__ inline void uvspec_at(const double *vor, const double *div, const Dyn
     }
 }
 
+// geop(1) at level k of one real coefficient c = 2 (m + mx n) + p (dyn_geop.f90:16-32):
+// the hydrostatic sum from the bottom, then the free-troposphere lapse-rate
+// correction of the zonal-mean row; t = level-1 temperature, all kx levels
+__device__ inline double geop_at(const double *t, const double *phis, const DynTables *T, int c, int m, int k) {
+    double phi = phis[c] + T->xgeop1[kKX - 1] * t[(size_t)(kKX - 1) * kSF + c];
+    for (int kk = kKX - 2; kk >= k; --kk)
+        phi = phi + T->xgeop2[kk + 1] * t[(size_t)(kk + 1) * kSF + c] + T->xgeop1[kk] * t[(size_t)kk * kSF + c];
+    if (m == 0 && k >= 1 && k <= kKX - 2)
+        phi = phi + T->corf[k] * (t[(size_t)(k + 1) * kSF + c] - t[(size_t)(k - 1) * kSF + c]);
+    return phi;
+}
+
 // ---------------------------------------------------------------- kernels
-// prep: inputs of the 50 inverse transforms, [vor 8 | div 8 | t 8 | tr 8 | ucos 8 |
-// vcos 8 | psdx | psdy], from time level j2 (grtend :60-99).  One thread per (m, n).
+// prep: inputs of the inverse transforms from time level j2 (grtend :60-99),
+// [vor 8 | div 8 | t 8 | tr 8] then at o2 [ucos 8 | vcos 8 | psdx | psdy]; with
+// phys, also the level-1 inputs of phypar (phy_phypar.f90:54-66): t1, q1, geop(1),
+// ps1 at kPT1.. and ucos1, vcos1 at o2 + 18.  One thread per (m, n).
 __global__ void k_dyn_prep(const double *__restrict__ st, double *__restrict__ sin_, const DynTables *__restrict__ T,
-                           int j2) {
+                           const double *__restrict__ phis, int j2, int o2, int phys) {
     const int mn = blockIdx.x * blockDim.x + threadIdx.x;
     if (mn >= kMN) return;
     const int k = blockIdx.y;
@@ -129,11 +168,28 @@ __global__ void k_dyn_prep(const double *__restrict__ st, double *__restrict__ s
             sin_[(size_t)(2 * kKX + k) * kSF + c] = t[c];
             sin_[(size_t)(3 * kKX + k) * kSF + c] = tr[c];
         }
-        uvspec_at(vor, div, T, m, n, sin_ + (size_t)(4 * kKX + k) * kSF, sin_ + (size_t)(5 * kKX + k) * kSF);
+        uvspec_at(vor, div, T, m, n, sin_ + (size_t)(o2 + k) * kSF, sin_ + (size_t)(o2 + kKX + k) * kSF);
+        if (phys) {
+            const double *vor1 = st + kOffVor + (size_t)k * kSF, *div1 = st + kOffDiv + (size_t)k * kSF;
+            const double *t1 = st + kOffT, *tr1 = st + kOffTr + (size_t)k * kSF;
+#pragma unroll
+            for (int p = 0; p < 2; ++p) {
+                const int c = ci(p, m, n);
+                sin_[(size_t)(kPT1 + k) * kSF + c] = t1[(size_t)k * kSF + c];
+                sin_[(size_t)(kPQ1 + k) * kSF + c] = tr1[c];
+                sin_[(size_t)(kPPhi1 + k) * kSF + c] = geop_at(t1, phis, T, c, m, k);
+            }
+            uvspec_at(vor1, div1, T, m, n, sin_ + (size_t)(o2 + 2 * kKX + 2 + k) * kSF,
+                      sin_ + (size_t)(o2 + 3 * kKX + 2 + k) * kSF);
+        }
     } else {
+        if (phys) {
+#pragma unroll
+            for (int p = 0; p < 2; ++p) sin_[(size_t)kPPs1 * kSF + ci(p, m, n)] = st[kOffPs + ci(p, m, n)];
+        }
         // grad(ps(j2)) -> (psdx, psdy)  (spe_spectral.f90:271-305)
         const double *ps = st + kOffPs + (size_t)(j2 - 1) * kSF;
-        double *dx = sin_ + (size_t)(6 * kKX) * kSF, *dy = sin_ + (size_t)(6 * kKX + 1) * kSF;
+        double *dx = sin_ + (size_t)(o2 + 2 * kKX) * kSF, *dy = sin_ + (size_t)(o2 + 2 * kKX + 1) * kSF;
         dx[ci(1, m, n)] = T->gradx[m] * ps[ci(0, m, n)];
         dx[ci(0, m, n)] = -T->gradx[m] * ps[ci(1, m, n)];
 #pragma unroll
@@ -157,7 +213,8 @@ __global__ void k_dyn_prep(const double *__restrict__ st, double *__restrict__ s
 //   [utend 8 | -u*tgg 8 | -u*trg 8 | vtend 8 | -v*tgg 8 | -v*trg 8]  (x 1/cos in specx)
 //   [0.5(u^2+v^2) 8 | ttend 8 | trtend 8 | -umean*px - vmean*py]
 __global__ __launch_bounds__(256) void k_dyn_gridpoint(const double *__restrict__ G, const double *__restrict__ P,
-                                                       double *__restrict__ F, const DynTables *__restrict__ T) {
+                                                       double *__restrict__ F, const DynTables *__restrict__ T,
+                                                       int o2) {
     const int pt = blockIdx.x * blockDim.x + threadIdx.x;
     if (pt >= kGF) return;
     const int j = pt / kIX;
@@ -169,10 +226,10 @@ __global__ __launch_bounds__(256) void k_dyn_gridpoint(const double *__restrict_
         divg[k] = g(kKX + k);
         tg[k] = g(2 * kKX + k);
         trg[k] = g(3 * kKX + k);
-        ug[k] = g(4 * kKX + k);
-        vg[k] = g(5 * kKX + k);
+        ug[k] = g(o2 + k);
+        vg[k] = g(o2 + kKX + k);
     }
-    double px = g(6 * kKX), py = g(6 * kKX + 1);
+    double px = g(o2 + 2 * kKX), py = g(o2 + 2 * kKX + 1);
     double umean = 0.0, vmean = 0.0, dmean = 0.0;
 #pragma unroll
     for (int k = 0; k < kKX; ++k) {
@@ -248,6 +305,34 @@ __global__ __launch_bounds__(256) void k_dyn_gridpoint(const double *__restrict_
         F[(size_t)(2 * kKX + k) * kGF + pt] = -ug[k] * trg[k];
         F[(size_t)(5 * kKX + k) * kGF + pt] = -vg[k] * trg[k];
         F[(size_t)(6 * kKX + k) * kGF + pt] = 0.5 * (ug[k] * ug[k] + vg[k] * vg[k]);
+    }
+}
+
+// phypar's physics, one thread per grid column (sml_physics.hpp): level fields
+// [kx][ngp] in, tendencies P = [u 8 | v 8 | t 8 | q 8] x ngp out
+__global__ __launch_bounds__(64) void k_phys(const double *__restrict__ ug1, const double *__restrict__ vg1,
+                                             const double *__restrict__ tg1, const double *__restrict__ qg1,
+                                             const double *__restrict__ phig1, const double *__restrict__ pslg1,
+                                             const double *__restrict__ bc, double *__restrict__ rad,
+                                             const PhysTables *__restrict__ PT, int lradsw, double *__restrict__ P) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= kNGP) return;
+    double ua[kKX], va[kKX], ta[kKX], qa[kKX], phi[kKX], ut[kKX], vt[kKX], tt[kKX], qt[kKX];
+#pragma unroll
+    for (int k = 0; k < kKX; ++k) {
+        ua[k] = ug1[(size_t)k * kNGP + j];
+        va[k] = vg1[(size_t)k * kNGP + j];
+        ta[k] = tg1[(size_t)k * kNGP + j];
+        qa[k] = qg1[(size_t)k * kNGP + j];
+        phi[k] = phig1[(size_t)k * kNGP + j];
+    }
+    phys_column(j, ua, va, ta, qa, phi, pslg1[j], bc, rad, PT, lradsw != 0, ut, vt, tt, qt);
+#pragma unroll
+    for (int k = 0; k < kKX; ++k) {
+        P[(size_t)k * kNGP + j] = ut[k];
+        P[(size_t)(kKX + k) * kNGP + j] = vt[k];
+        P[(size_t)(2 * kKX + k) * kNGP + j] = tt[k];
+        P[(size_t)(3 * kKX + k) * kNGP + j] = qt[k];
     }
 }
 
@@ -543,10 +628,12 @@ int dalloc(T **p, size_t count) {
 extern "C" int sml_dyn_destroy(sml_dynamics *d) {
     if (!d) return SML_OK;
     void *ptrs[] = {d->d_tabs, d->d_state, d->d_phis, d->d_tcorh, d->d_qcorh, d->d_phi, d->d_specin,
-                    d->d_varm, d->d_grid, d->d_gfwd, d->d_sfwd, d->d_tend, d->d_phys, d->d_minmax, d->d_io};
+                    d->d_varm, d->d_grid, d->d_gfwd, d->d_sfwd, d->d_tend, d->d_phys, d->d_minmax, d->d_io,
+                    d->d_ptab, d->d_pbc, d->d_rad, d->d_pio};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
-    if (d->graph) (void)hipGraphExecDestroy(d->graph);
+    for (auto &r : d->replay)
+        if (r.exec) (void)hipGraphExecDestroy(r.exec);
     if (d->cap_stream) (void)hipStreamDestroy(d->cap_stream);
     if (d->sp) sml_spectral_destroy(d->sp);
     delete d;
@@ -564,18 +651,23 @@ extern "C" int sml_dyn_create(double radius, sml_dynamics **out) {
         return rc;
     }
     build_dyn_indyns(spectral_host_tables(d->sp), &d->tab);
+    build_phys_tables(d->tab, &d->ptab);
     if ((rc = dalloc(&d->d_tabs, 4)) || (rc = dalloc(&d->d_state, kStateSize)) || (rc = dalloc(&d->d_phis, kSF)) ||
         (rc = dalloc(&d->d_tcorh, kSF)) || (rc = dalloc(&d->d_qcorh, kSF)) || (rc = dalloc(&d->d_phi, kKX * kSF)) ||
-        (rc = dalloc(&d->d_specin, (size_t)kNInv * kSF)) || (rc = dalloc(&d->d_varm, (size_t)kNFwd * kVF)) ||
-        (rc = dalloc(&d->d_grid, (size_t)kNInv * kGF)) || (rc = dalloc(&d->d_gfwd, (size_t)kNFwd * kGF)) ||
+        (rc = dalloc(&d->d_specin, (size_t)kNInvMax * kSF)) ||
+        (rc = dalloc(&d->d_varm, (size_t)(kNInvMax > kNFwd ? kNInvMax : kNFwd) * kVF)) ||
+        (rc = dalloc(&d->d_grid, (size_t)kNInvMax * kGF)) || (rc = dalloc(&d->d_gfwd, (size_t)kNFwd * kGF)) ||
         (rc = dalloc(&d->d_sfwd, (size_t)kNFwd * kSF)) || (rc = dalloc(&d->d_tend, kTendSize)) ||
         (rc = dalloc(&d->d_phys, (size_t)4 * kKX * kGF)) || (rc = dalloc(&d->d_minmax, 8)) ||
-        (rc = dalloc(&d->d_io, (size_t)4 * kKX * kGF + kGF))) {
+        (rc = dalloc(&d->d_io, (size_t)4 * kKX * kGF + kGF)) || (rc = dalloc(&d->d_ptab, 1)) ||
+        (rc = dalloc(&d->d_pbc, (size_t)kNBc * kNGP)) || (rc = dalloc(&d->d_rad, kRadSize)) ||
+        (rc = dalloc(&d->d_pio, (size_t)(5 * kKX + 1 + 4 * kKX) * kNGP))) {
         sml_dyn_destroy(d);
         return rc;
     }
     d->d_tab = d->d_tabs;
     hipError_t e = hipMemcpy(d->d_tab, &d->tab, sizeof(DynTables), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(d->d_ptab, &d->ptab, sizeof(PhysTables), hipMemcpyHostToDevice);
     if (e != hipSuccess) {
         sml_dyn_destroy(d);
         return fail(SML_ERR_HIP, "sml_dyn_create: %s", hipGetErrorString(e));
@@ -662,27 +754,34 @@ extern "C" int sml_dyn_state_device(sml_dynamics *d, double **d_state, double **
 
 namespace {
 
-// the 9 launches of one step(j1, j2, dt, alph, rob, wil) on stream st
+// the launches of one step(j1, j2, dt, alph, rob, wil) on stream st: 7 without
+// GPU physics, 8 with it
 int launch_step(sml_dynamics *d, int j1, int j2, double dt, double alph, double rob, double wil,
-                const double *d_phys, hipStream_t st) {
+                const double *d_phys, bool lradsw, hipStream_t st) {
     const DynTables *T = d->d_tab;
-    // 1. grtend: inverse transforms of the j2 state
+    const bool phys = d->phys_on;
+    const int n1 = phys ? kNInv1P : kNInv1, nin = phys ? kNInvP : kNInv;
+    // 1. grtend: inverse transforms of the j2 state (+ phypar's level-1 inputs)
     hipLaunchKernelGGL(k_dyn_prep, dim3((kMN + 127) / 128, kKX + 1), dim3(128), 0, st, d->d_state, d->d_specin, T,
-                       j2);
+                       d->d_phis, j2, n1, phys ? 1 : 0);
     SML_HIP(hipGetLastError());
-    if (int rc = spectral_gridy(d->sp, d->d_specin, d->d_varm, kNInv, st)) return rc;
-    if (int rc = spectral_gridx(d->sp, d->d_varm, d->d_grid, kNInv1, 1, st)) return rc;
-    if (int rc = spectral_gridx(d->sp, d->d_varm + (size_t)kNInv1 * kVF, d->d_grid + (size_t)kNInv1 * kGF,
-                                kNInv - kNInv1, 2, st))
-        return rc;
-    // 2. grid-point dynamics (+ physics tendencies)
-    hipLaunchKernelGGL(k_dyn_gridpoint, dim3((kGF + 255) / 256), dim3(256), 0, st, d->d_grid, d_phys, d->d_gfwd, T);
+    if (int rc = spectral_gridy(d->sp, d->d_specin, d->d_varm, nin, st)) return rc;
+    if (int rc = spectral_gridx_split(d->sp, d->d_varm, d->d_grid, nin, n1, st)) return rc;
+    // 2. physics (phypar on level 1), then grid-point dynamics + physics tendencies
+    if (phys) {
+        const double *G = d->d_grid;
+        hipLaunchKernelGGL(k_phys, dim3(kNGP / 64), dim3(64), 0, st, G + (size_t)(n1 + 2 * kKX + 2) * kGF,
+                           G + (size_t)(n1 + 3 * kKX + 2) * kGF, G + (size_t)kPT1 * kGF, G + (size_t)kPQ1 * kGF,
+                           G + (size_t)kPPhi1 * kGF, G + (size_t)kPPs1 * kGF, d->d_pbc, d->d_rad, d->d_ptab,
+                           lradsw ? 1 : 0, d->d_phys);
+        SML_HIP(hipGetLastError());
+        d_phys = d->d_phys;
+    }
+    hipLaunchKernelGGL(k_dyn_gridpoint, dim3((kGF + 255) / 256), dim3(256), 0, st, d->d_grid, d_phys, d->d_gfwd, T,
+                       n1);
     SML_HIP(hipGetLastError());
     // 3. forward transforms: vdspec inputs x 1/cos (kcos = 2), the rest plain
-    if (int rc = spectral_specx(d->sp, d->d_gfwd, d->d_varm, kNFwdScaled, 1, st)) return rc;
-    if (int rc = spectral_specx(d->sp, d->d_gfwd + (size_t)kNFwdScaled * kGF, d->d_varm + (size_t)kNFwdScaled * kVF,
-                                kNFwd - kNFwdScaled, 0, st))
-        return rc;
+    if (int rc = spectral_specx_split(d->sp, d->d_gfwd, d->d_varm, kNFwd, kNFwdScaled, st)) return rc;
     if (int rc = spectral_specy(d->sp, d->d_varm, d->d_sfwd, kNFwd, st)) return rc;
     hipLaunchKernelGGL(k_dyn_combine, dim3((kMN + 127) / 128, kKX), dim3(128), 0, st, d->d_sfwd, d->d_tend, T);
     SML_HIP(hipGetLastError());
@@ -700,42 +799,148 @@ extern "C" int sml_dyn_step(sml_dynamics *d, int j1, int j2, double dt, double a
                             const double *d_phys, void *stream) {
     SML_REQUIRE(d, "null context");
     SML_REQUIRE((j1 == 1 || j1 == 2) && (j2 == 1 || j2 == 2), "j1/j2 must be 1 or 2");
+    SML_REQUIRE(!(d->phys_on && d_phys), "physics runs on the GPU (sml_dyn_set_physics): d_phys must be NULL");
     if (!d->impint_done) return fail(SML_ERR_STATE, "sml_dyn_impint must be called before sml_dyn_step");
-    return launch_step(d, j1, j2, dt, alph, rob, wil, d_phys, (hipStream_t)stream);
+    return launch_step(d, j1, j2, dt, alph, rob, wil, d_phys, d->lradsw, (hipStream_t)stream);
 }
+
+namespace {
+
+// the step(2, 2, dt, ...) graph for one lradsw value, (re)captured when its inputs change
+int leapfrog_graph(sml_dynamics *d, bool lradsw, const double key[4], const double *d_phys, hipGraphExec_t *out) {
+    sml_dynamics::Replay &r = d->replay[lradsw ? 1 : 0];
+    if (r.exec && std::memcmp(key, r.key, sizeof r.key) == 0 && d_phys == r.phys && d->d_tab == r.tab &&
+        d->phys_on == r.phys_on) {
+        *out = r.exec;
+        return SML_OK;
+    }
+    if (r.exec) {
+        SML_HIP(hipGraphExecDestroy(r.exec));
+        r.exec = nullptr;
+    }
+    if (!d->cap_stream) SML_HIP(hipStreamCreateWithFlags(&d->cap_stream, hipStreamNonBlocking));
+    hipGraph_t g = nullptr;
+    SML_HIP(hipStreamBeginCapture(d->cap_stream, hipStreamCaptureModeThreadLocal));
+    int rc = launch_step(d, 2, 2, key[0], key[1], key[2], key[3], d_phys, lradsw, d->cap_stream);
+    hipError_t e = hipStreamEndCapture(d->cap_stream, &g);
+    if (rc) {
+        if (g) (void)hipGraphDestroy(g);
+        return rc;
+    }
+    if (e != hipSuccess) return fail(SML_ERR_HIP, "sml_dyn_leapfrog capture: %s", hipGetErrorString(e));
+    e = hipGraphInstantiate(&r.exec, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    if (e != hipSuccess) {
+        r.exec = nullptr;
+        return fail(SML_ERR_HIP, "sml_dyn_leapfrog instantiate: %s", hipGetErrorString(e));
+    }
+    std::memcpy(r.key, key, sizeof r.key);
+    r.phys = d_phys;
+    r.tab = d->d_tab;
+    r.phys_on = d->phys_on;
+    *out = r.exec;
+    return SML_OK;
+}
+
+}  // namespace
 
 extern "C" int sml_dyn_leapfrog(sml_dynamics *d, int nsteps, double dt, double alph, double rob, double wil,
                                 const double *d_phys, void *stream) {
     SML_REQUIRE(d && nsteps >= 0, "bad argument");
+    SML_REQUIRE(!(d->phys_on && d_phys), "physics runs on the GPU (sml_dyn_set_physics): d_phys must be NULL");
     if (!d->impint_done) return fail(SML_ERR_STATE, "sml_dyn_impint must be called before sml_dyn_leapfrog");
-    if (nsteps == 0) return SML_OK;
     const double key[4] = {dt, alph, rob, wil};
-    if (!d->graph || std::memcmp(key, d->g_key, sizeof key) != 0 || d_phys != d->g_phys || d->d_tab != d->g_tab) {
-        if (d->graph) {
-            SML_HIP(hipGraphExecDestroy(d->graph));
-            d->graph = nullptr;
-        }
-        if (!d->cap_stream) SML_HIP(hipStreamCreateWithFlags(&d->cap_stream, hipStreamNonBlocking));
-        hipGraph_t g = nullptr;
-        SML_HIP(hipStreamBeginCapture(d->cap_stream, hipStreamCaptureModeThreadLocal));
-        int rc = launch_step(d, 2, 2, dt, alph, rob, wil, d_phys, d->cap_stream);
-        hipError_t e = hipStreamEndCapture(d->cap_stream, &g);
-        if (rc) {
-            if (g) (void)hipGraphDestroy(g);
-            return rc;
-        }
-        if (e != hipSuccess) return fail(SML_ERR_HIP, "sml_dyn_leapfrog capture: %s", hipGetErrorString(e));
-        e = hipGraphInstantiate(&d->graph, g, nullptr, nullptr, 0);
-        (void)hipGraphDestroy(g);
-        if (e != hipSuccess) {
-            d->graph = nullptr;
-            return fail(SML_ERR_HIP, "sml_dyn_leapfrog instantiate: %s", hipGetErrorString(e));
-        }
-        std::memcpy(d->g_key, key, sizeof key);
-        d->g_phys = d_phys;
-        d->g_tab = d->d_tab;
+    // stloop (dyn_stloop.f90:37-56): lradsw = (mod(istep, nstrad) == 1) before each step
+    for (int i = 0; i < nsteps; ++i) {
+        const bool lradsw = (d->istep % kNstrad == 1);
+        hipGraphExec_t exec = nullptr;  // without GPU physics lradsw is irrelevant: one graph
+        if (int rc = leapfrog_graph(d, d->phys_on && lradsw, key, d_phys, &exec)) return rc;
+        SML_HIP(hipGraphLaunch(exec, (hipStream_t)stream));
+        d->lradsw = lradsw;
+        ++d->istep;
     }
-    for (int i = 0; i < nsteps; ++i) SML_HIP(hipGraphLaunch(d->graph, (hipStream_t)stream));
+    return SML_OK;
+}
+
+extern "C" int sml_dyn_set_clock(sml_dynamics *d, int istep, int lradsw) {
+    SML_REQUIRE(d, "null context");
+    d->istep = istep;
+    d->lradsw = lradsw != 0;
+    return SML_OK;
+}
+
+extern "C" int sml_dyn_get_clock(const sml_dynamics *d, int *istep, int *lradsw) {
+    SML_REQUIRE(d, "null context");
+    if (istep) *istep = d->istep;
+    if (lradsw) *lradsw = d->lradsw ? 1 : 0;
+    return SML_OK;
+}
+
+extern "C" int sml_dyn_set_physics(sml_dynamics *d, const double *bc) {
+    SML_REQUIRE(d, "null context");
+    if (!bc) {
+        d->phys_on = false;
+        return SML_OK;
+    }
+    SML_HIP(hipDeviceSynchronize());  // steps in flight may still read the old fields
+    SML_HIP(hipMemcpy(d->d_pbc, bc, (size_t)kNBc * kNGP * 8, hipMemcpyHostToDevice));
+    d->phys_on = true;
+    return SML_OK;
+}
+
+extern "C" int sml_dyn_set_rad_state(sml_dynamics *d, const double *rad) {
+    SML_REQUIRE(d, "null context");
+    SML_HIP(hipDeviceSynchronize());
+    if (rad)
+        SML_HIP(hipMemcpy(d->d_rad, rad, kRadSize * 8, hipMemcpyHostToDevice));
+    else
+        SML_HIP(hipMemset(d->d_rad, 0, kRadSize * 8));
+    return SML_OK;
+}
+
+extern "C" int sml_dyn_get_rad_state(sml_dynamics *d, double *rad) {
+    SML_REQUIRE(d && rad, "null argument");
+    SML_HIP(hipDeviceSynchronize());
+    SML_HIP(hipMemcpy(rad, d->d_rad, kRadSize * 8, hipMemcpyDeviceToHost));
+    return SML_OK;
+}
+
+extern "C" int sml_dyn_phypar(sml_dynamics *d, const double *d_ug1, const double *d_vg1, const double *d_tg1,
+                              const double *d_qg1, const double *d_phig1, const double *d_pslg1, int lradsw,
+                              double *d_tend, void *stream) {
+    SML_REQUIRE(d && d_ug1 && d_vg1 && d_tg1 && d_qg1 && d_phig1 && d_pslg1 && d_tend, "null argument");
+    SML_REQUIRE(d->phys_on, "sml_dyn_set_physics must provide the boundary fields first");
+    hipLaunchKernelGGL(k_phys, dim3(kNGP / 64), dim3(64), 0, (hipStream_t)stream, d_ug1, d_vg1, d_tg1, d_qg1,
+                       d_phig1, d_pslg1, d->d_pbc, d->d_rad, d->d_ptab, lradsw ? 1 : 0, d_tend);
+    SML_HIP(hipGetLastError());
+    return SML_OK;
+}
+
+extern "C" int sml_dyn_phypar_host(sml_dynamics *d, const double *ug1, const double *vg1, const double *tg1,
+                                   const double *qg1, const double *phig1, const double *pslg1, int lradsw,
+                                   double *tend) {
+    SML_REQUIRE(d && ug1 && vg1 && tg1 && qg1 && phig1 && pslg1 && tend, "null argument");
+    const size_t f3 = (size_t)kKX * kNGP;
+    double *b = d->d_pio;
+    const double *src[5] = {ug1, vg1, tg1, qg1, phig1};
+    for (int i = 0; i < 5; ++i) SML_HIP(hipMemcpy(b + i * f3, src[i], f3 * 8, hipMemcpyHostToDevice));
+    SML_HIP(hipMemcpy(b + 5 * f3, pslg1, kNGP * 8, hipMemcpyHostToDevice));
+    double *out = b + 5 * f3 + kNGP;
+    if (int rc = sml_dyn_phypar(d, b, b + f3, b + 2 * f3, b + 3 * f3, b + 4 * f3, b + 5 * f3, lradsw, out, nullptr))
+        return rc;
+    SML_HIP(hipMemcpy(tend, out, 4 * f3 * 8, hipMemcpyDeviceToHost));
+    return SML_OK;
+}
+
+extern "C" int sml_dyn_sol_oz(const sml_dynamics *d, double tyear, double *fields5) {
+    SML_REQUIRE(d && fields5, "null argument");
+    phys_sol_oz(d->ptab, tyear, fields5);
+    return SML_OK;
+}
+
+extern "C" int sml_phys_sflset(const double *phi0, double *forog) {
+    SML_REQUIRE(phi0 && forog, "null argument");
+    phys_sflset(phi0, forog);
     return SML_OK;
 }
 
@@ -820,6 +1025,7 @@ extern "C" int sml_dyn_step_host(sml_dynamics *d, int j1, int j2, double dt, dou
     SML_REQUIRE(d, "null context");
     const double *dp = nullptr;
     if (phys) {
+        SML_REQUIRE(!d->phys_on, "physics runs on the GPU (sml_dyn_set_physics): phys must be NULL");
         SML_HIP(hipMemcpy(d->d_phys, phys, (size_t)4 * kKX * kGF * 8, hipMemcpyHostToDevice));
         dp = d->d_phys;
     }

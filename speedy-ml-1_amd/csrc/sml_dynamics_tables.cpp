@@ -5,6 +5,7 @@
 //           given (dt, alph), using ludcmp/lubksb/inv (src/spe_matinv.f90)
 // Computed on the host once per (dt, alph) and uploaded by sml_dynamics.hip.
 #include "sml_dynamics_tables.hpp"
+#include "sml_physics.hpp"
 
 #include <cmath>
 #include <cstring>
@@ -211,6 +212,99 @@ void build_dyn_impint(double dt, double alph, DynTables *d) {
     }
     for (int k = 0; k < kKX; ++k)
         for (int k1 = 0; k1 < kKX; ++k1) d->xc[k1][k] = d->xc[k1][k] * xi;
+}
+
+// ---------------------------------------------------------------- physics
+// inphys(hsg, ppl, radang) (src/ini_inphys.f90:22-50) and radset's longwave band
+// fractions (src/phy_radiat.f90:659-688).
+void build_phys_tables(const DynTables &dt, PhysTables *p) {
+    std::memset(p, 0, sizeof *p);
+    const double gg = phys::gg, p0 = phys::p0, cp = phys::cp;
+    p->sigh[0] = dt.hsg[0];
+    for (int k = 0; k < kKX; ++k) {
+        p->sig[k] = 0.5 * (dt.hsg[k + 1] + dt.hsg[k]);
+        p->sigl[k] = std::log(p->sig[k]);
+        p->sigh[k + 1] = dt.hsg[k + 1];
+        p->dsig[k] = dt.hsg[k + 1] - dt.hsg[k];
+        p->grdsig[k] = gg / (p->dsig[k] * p0);
+        p->grdscp[k] = p->grdsig[k] / cp;
+    }
+    // half-level interpolation weights; the last row extrapolates to sigma = 0.99
+    for (int k = 0; k < kKX - 1; ++k) {
+        p->wvi[k][0] = 1. / (p->sigl[k + 1] - p->sigl[k]);
+        p->wvi[k][1] = (std::log(p->sigh[k + 1]) - p->sigl[k]) * p->wvi[k][0];
+    }
+    p->wvi[kKX - 1][0] = 0.;
+    p->wvi[kKX - 1][1] = (std::log(0.99) - p->sigl[kKX - 1]) * p->wvi[kKX - 2][0];
+    for (int j = 0; j < kIL; ++j) {
+        p->slat[j] = std::sin(dt.radang[j]);
+        p->clat[j] = std::cos(dt.radang[j]);
+    }
+    // fband(T, band): emission fraction of each of the 4 bands at temperature T
+    const double eps1 = 1. - phys::epslw;
+    for (int it = 200; it <= 320; ++it) {
+        double *f = p->fband[it - 100];
+        const double d1 = (double)((it - 247) * (it - 247)), d2 = (double)((it - 282) * (it - 282)),
+                     d3 = (double)((it - 315) * (it - 315));
+        f[1] = (0.148 - 3.0e-6 * d1) * eps1;
+        f[2] = (0.356 - 5.2e-6 * d2) * eps1;
+        f[3] = (0.314 + 1.0e-5 * d3) * eps1;
+        f[0] = eps1 - (f[1] + f[2] + f[3]);
+    }
+    for (int b = 0; b < 4; ++b) {
+        for (int it = 100; it < 200; ++it) p->fband[it - 100][b] = p->fband[200 - 100][b];
+        for (int it = 321; it <= 400; ++it) p->fband[it - 100][b] = p->fband[320 - 100][b];
+    }
+}
+
+// sol_oz + solar (src/phy_radiat.f90:1-121): zonal daily-mean insolation and
+// ozone absorption, replicated along each latitude row.
+void phys_sol_oz(const PhysTables &p, double tyear, double *out5) {
+    const double pi = 2. * std::asin(1.);
+    // solar(tyear, 4 solc): declination and Earth-Sun distance (Hartmann 1994)
+    const double a = 2. * pi * tyear;
+    const double c1 = std::cos(a), s1 = std::sin(a);
+    const double c2 = c1 * c1 - s1 * s1, s2 = 2. * s1 * c1;
+    const double c3 = c1 * c2 - s1 * s2, s3 = s1 * c2 + s2 * c1;
+    const double decl = 0.006918 - 0.399912 * c1 + 0.070257 * s1 - 0.006758 * c2 + 0.000907 * s2 - 0.002697 * c3 +
+                        0.001480 * s3;
+    const double fdis = 1.000110 + 0.034221 * c1 + 0.001280 * s1 + 0.000719 * c2 + 0.000077 * s2;
+    const double cdecl = std::cos(decl), sdecl = std::sin(decl), tdecl = sdecl / cdecl;
+    const double csolp = (4. * phys::solc) / pi;
+    // sol_oz proper
+    const double alpha = 4. * std::asin(1.) * (tyear + 10. / 365.), dalpha = 0.;
+    const double coz1 = 1.0 * std::fmax(0., std::cos(alpha - dalpha)), coz2 = 1.8, azen = 1.0;
+    const double rzen = -std::cos(alpha) * 23.45 * std::asin(1.) / 90.;
+    const double czen = std::cos(rzen), szen = std::sin(rzen), fs0 = 6.;
+    double *fsol = out5, *ozone = out5 + kNGP, *ozupp = out5 + 2 * kNGP, *zenit = out5 + 3 * kNGP,
+           *stratz = out5 + 4 * kNGP;
+    for (int j = 0; j < kIL; ++j) {
+        const double ch0 = std::fmin(1., std::fmax(-1., -tdecl * p.slat[j] / p.clat[j]));
+        const double h0 = std::acos(ch0), sh0 = std::sin(h0);
+        const double top = csolp * fdis * (h0 * p.slat[j] * sdecl + sh0 * p.clat[j] * cdecl);
+        const double flat2 = 1.5 * p.slat[j] * p.slat[j] - 0.5;
+        double up = 0.5 * phys::epssw;
+        double oz = 0.4 * phys::epssw * (1.0 + coz1 * p.slat[j] + coz2 * flat2);
+        const double b = 1. - (p.clat[j] * czen + p.slat[j] * szen);
+        const double zen = 1. + azen * (b * b);  // (..)**nzen, nzen = 2
+        up = top * up * zen;
+        oz = top * oz * zen;
+        const double st = std::fmax(fs0 - top, 0.);
+        for (int i = 0; i < kIX; ++i) {
+            const int g = j * kIX + i;
+            fsol[g] = top;
+            ozone[g] = oz;
+            ozupp[g] = up;
+            zenit[g] = zen;
+            stratz[g] = st;
+        }
+    }
+}
+
+// sflset (src/phy_suflux.f90:358-382): orographic drag factor
+void phys_sflset(const double *phi0, double *forog) {
+    const double rhdrag = 1. / (phys::gg * phys::hdrag);
+    for (int j = 0; j < kNGP; ++j) forog[j] = 1. + phys::fhdrag * (1. - std::exp(-std::fmax(phi0[j], 0.) * rhdrag));
 }
 
 }  // namespace sml

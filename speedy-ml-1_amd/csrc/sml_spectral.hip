@@ -102,10 +102,12 @@ __global__ __launch_bounds__(64) void k_gridy(const double *__restrict__ spec, d
 }
 
 // gridx: varm[f][lat][62] -> grid[f][lat][96]  (one wave per (field, 16-latitude
-// group g, 16-longitude tile w): blockIdx.x = field, blockIdx.y = 3 w + g)
+// group g, 16-longitude tile w): blockIdx.x = field, blockIdx.y = 3 w + g).  The
+// first ncos1 fields are kcos = 1, the rest kcos = 2 (x cosgr), so one launch can
+// carry a batch holding both kinds.
 __global__ __launch_bounds__(64) void k_gridx(const double *__restrict__ varm, double *__restrict__ grid,
                                               const double *__restrict__ dinv, const double *__restrict__ cosgr,
-                                              int kcos) {
+                                              int ncos1) {
     const int f = blockIdx.x;
     const int w = blockIdx.y / 3, j0 = 16 * (blockIdx.y % 3);
     const int l = threadIdx.x, r = l & 15, kk = l >> 4;
@@ -123,21 +125,23 @@ __global__ __launch_bounds__(64) void k_gridx(const double *__restrict__ varm, d
     for (int q = 0; q < 4; ++q) {
         const int j = j0 + kk + 4 * q;
         double v = acc[q];
-        if (kcos != 1) v = v * cosgr[j];
+        if (f >= ncos1) v = v * cosgr[j];
         g[j * kIX] = v;
     }
 }
 
-// specx: grid[f][lat][96] (optionally x scale[lat]) -> varm[f][lat][62]
+// specx: grid[f][lat][96] (the first nscaled fields x scale[lat]) -> varm[f][lat][62]
 // (one wave per (field, 16-latitude group g, 16-coefficient tile w):
 // blockIdx.x = field, blockIdx.y = 3 w + g)
 __global__ __launch_bounds__(64) void k_specx(const double *__restrict__ grid, double *__restrict__ varm,
-                                              const double *__restrict__ dfwd, const double *__restrict__ scale) {
+                                              const double *__restrict__ dfwd, const double *__restrict__ scale_tab,
+                                              int nscaled) {
     const int f = blockIdx.x;
     const int w = blockIdx.y / 3, j0 = 16 * (blockIdx.y % 3);
     const int l = threadIdx.x, r = l & 15, kk = l >> 4;
     const double *g = grid + (size_t)f * kGridField + (j0 + r) * kIX;
-    const double s0 = scale ? scale[j0 + r] : 1.0;
+    const bool scale = scale_tab && f < nscaled;  // block-uniform
+    const double s0 = scale ? scale_tab[j0 + r] : 1.0;
     d4 acc = {0, 0, 0, 0};
 #pragma unroll 8
     for (int s = 0; s < kIX / 4; ++s) {
@@ -387,7 +391,7 @@ extern "C" int sml_gridx_batched(sml_spectral *s, const double *d_varm, double *
     if (int rc = check_ctx(s, nf)) return rc;
     if (nf == 0) return SML_OK;
     hipLaunchKernelGGL(k_gridx, dim3(nf, 18), dim3(64), 0, (hipStream_t)stream, d_varm, d_grid, s->d_dinv, s->d_cosgr,
-                       kcos);
+                       kcos == 1 ? nf : 0);
     SML_HIP(hipGetLastError());
     return SML_OK;
 }
@@ -396,7 +400,7 @@ extern "C" int sml_specx_batched(sml_spectral *s, const double *d_grid, double *
     if (int rc = check_ctx(s, nf)) return rc;
     if (nf == 0) return SML_OK;
     hipLaunchKernelGGL(k_specx, dim3(nf, 12), dim3(64), 0, (hipStream_t)stream, d_grid, d_varm, s->d_dfwd,
-                       (const double *)nullptr);
+                       (const double *)nullptr, 0);
     SML_HIP(hipGetLastError());
     return SML_OK;
 }
@@ -436,8 +440,8 @@ extern "C" int sml_vdspec_batched(sml_spectral *s, const double *d_ug, const dou
     const double *scale = (kcos == 2) ? s->d_cosgr : s->d_cosgr2;
     double *um = s->d_work, *vm = s->d_work + (size_t)nf * kVarmField;
     double *uc = s->d_work + 2 * s->work_fields * (size_t)kVarmField, *vc = uc + (size_t)nf * kSpecField;
-    hipLaunchKernelGGL(k_specx, dim3(nf, 12), dim3(64), 0, st, d_ug, um, s->d_dfwd, scale);
-    hipLaunchKernelGGL(k_specx, dim3(nf, 12), dim3(64), 0, st, d_vg, vm, s->d_dfwd, scale);
+    hipLaunchKernelGGL(k_specx, dim3(nf, 12), dim3(64), 0, st, d_ug, um, s->d_dfwd, scale, nf);
+    hipLaunchKernelGGL(k_specx, dim3(nf, 12), dim3(64), 0, st, d_vg, vm, s->d_dfwd, scale, nf);
     hipLaunchKernelGGL(k_specy, dim3(kMX, (nf + 7) / 8), dim3(64), 0, st, um, uc, s->d_pfwd, s->d_wt, nf);
     hipLaunchKernelGGL(k_specy, dim3(kMX, (nf + 7) / 8), dim3(64), 0, st, vm, vc, s->d_pfwd, s->d_wt, nf);
     SML_HIP(hipGetLastError());
@@ -523,8 +527,12 @@ int spectral_gridy(sml_spectral *s, const double *spec, double *varm, int nf, hi
 }
 
 int spectral_gridx(sml_spectral *s, const double *varm, double *grid, int nf, int kcos, hipStream_t st) {
+    return spectral_gridx_split(s, varm, grid, nf, kcos == 1 ? nf : 0, st);
+}
+
+int spectral_gridx_split(sml_spectral *s, const double *varm, double *grid, int nf, int ncos1, hipStream_t st) {
     if (nf <= 0) return SML_OK;
-    hipLaunchKernelGGL(k_gridx, dim3(nf, 18), dim3(64), 0, st, varm, grid, s->d_dinv, s->d_cosgr, kcos);
+    hipLaunchKernelGGL(k_gridx, dim3(nf, 18), dim3(64), 0, st, varm, grid, s->d_dinv, s->d_cosgr, ncos1);
     SML_HIP(hipGetLastError());
     return SML_OK;
 }
@@ -532,7 +540,14 @@ int spectral_gridx(sml_spectral *s, const double *varm, double *grid, int nf, in
 int spectral_specx(sml_spectral *s, const double *grid, double *varm, int nf, int scale, hipStream_t st) {
     if (nf <= 0) return SML_OK;
     const double *sc = scale == 1 ? s->d_cosgr : scale == 2 ? s->d_cosgr2 : nullptr;
-    hipLaunchKernelGGL(k_specx, dim3(nf, 12), dim3(64), 0, st, grid, varm, s->d_dfwd, sc);
+    hipLaunchKernelGGL(k_specx, dim3(nf, 12), dim3(64), 0, st, grid, varm, s->d_dfwd, sc, nf);
+    SML_HIP(hipGetLastError());
+    return SML_OK;
+}
+
+int spectral_specx_split(sml_spectral *s, const double *grid, double *varm, int nf, int nscaled, hipStream_t st) {
+    if (nf <= 0) return SML_OK;
+    hipLaunchKernelGGL(k_specx, dim3(nf, 12), dim3(64), 0, st, grid, varm, s->d_dfwd, s->d_cosgr, nscaled);
     SML_HIP(hipGetLastError());
     return SML_OK;
 }

@@ -34,6 +34,8 @@ EXPORTED = (
     "sml_dyn_get_state", "sml_dyn_get_phi", "sml_dyn_get_tendencies", "sml_dyn_state_device",
     "sml_dyn_step", "sml_dyn_step_host", "sml_dyn_leapfrog", "sml_dyn_from_grid", "sml_dyn_to_grid",
     "sml_dyn_is_safe", "sml_dyn_from_grid_host", "sml_dyn_to_grid_host",
+    "sml_dyn_set_physics", "sml_dyn_set_clock", "sml_dyn_get_clock", "sml_dyn_set_rad_state",
+    "sml_dyn_get_rad_state", "sml_dyn_phypar", "sml_dyn_phypar_host", "sml_dyn_sol_oz", "sml_phys_sflset",
     "sml_train_create", "sml_train_destroy", "sml_train_reset", "sml_train_accumulate", "sml_train_solve",
     "sml_train_npad", "sml_train_get_gram", "sml_probe_mfma_f64",
 )
@@ -125,6 +127,15 @@ def _declare(L: ctypes.CDLL) -> None:
         "sml_dyn_is_safe": [vp],
         "sml_dyn_from_grid_host": [vp, vp, vp, vp, ctypes.POINTER(ctypes.c_int)],
         "sml_dyn_to_grid_host": [vp, vp, vp],
+        "sml_dyn_set_physics": [vp, vp],
+        "sml_dyn_set_clock": [vp, i, i],
+        "sml_dyn_get_clock": [vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)],
+        "sml_dyn_set_rad_state": [vp, vp],
+        "sml_dyn_get_rad_state": [vp, vp],
+        "sml_dyn_phypar": [vp, vp, vp, vp, vp, vp, vp, i, vp, vp],
+        "sml_dyn_phypar_host": [vp, vp, vp, vp, vp, vp, vp, i, vp],
+        "sml_dyn_sol_oz": [vp, d, vp],
+        "sml_phys_sflset": [vp, vp],
         "sml_train_create": [i, vp, i, pp],
         "sml_train_destroy": [vp],
         "sml_train_reset": [vp, vp],

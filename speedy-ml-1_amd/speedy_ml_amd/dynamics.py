@@ -5,8 +5,9 @@ Mirrors the reference's time-stepping interface: `impint(dt, alph)`
 (src/dyn_step.f90:1-128) acting on the prognostic state of mod_dynvar
 (vor, div, t, ps, tr; src/mod_dynvar.f90:15-27), with `stepone`'s start-up
 sequence (src/ini_stepone.f90:19-34) and the leapfrog loop (src/dyn_stloop.f90:43)
-as conveniences.  Physics (phypar) is not computed here: its grid-point
-tendencies (u, v, t, q) can be handed to each step, or are zero.
+as conveniences.  Physics (phypar, src/phy_phypar.f90) runs on the GPU once the
+boundary fields are given (`set_physics`); otherwise its grid-point tendencies
+(u, v, t, q) can be handed to each step, or are zero.
 
 State arrays (numpy complex128, C order == the reference's Fortran layout):
 vor/div/t/tr (2, kx=8, nx=32, mx=31), ps (2, 32, 31); forcing phis/tcorh/qcorh
@@ -24,6 +25,11 @@ EARTH_RADIUS = 6.371e6  # mod_dyncon1.f90 rearth
 KX, NX, MX = 8, 32, 31
 FIELDS = ("vor", "div", "t", "tr", "ps")
 NSTEPS = 96  # mod_tsteps.f90: nsteps per day
+NGP = 96 * 48
+# phypar's boundary fields, in the order of sml_dyn_set_physics (include/speedy_ml.h)
+PHYS_BC = ("fmask1", "phis0", "stl_am", "sst_am", "soilw_am", "alb_l", "alb_s", "albsfc", "snowc",
+           "fsol", "ozone", "ozupp", "zenit", "stratz", "forog")
+RAD_SIZE = (4 * KX + 2 + KX + 1) * NGP
 DELT = 86400.0 / NSTEPS
 ROB, WIL, ALPH = 0.05, 0.53, 0.5  # mod_tsteps.f90:90,93; ini_indyns.f90 alph
 
@@ -84,6 +90,71 @@ class Dynamics:
         check(lib().sml_dyn_state_device(self._h, ctypes.byref(s), ctypes.byref(p)))
         return s.value, p.value
 
+    # ------------------------------------------------------------- physics
+    def set_physics(self, bc):
+        """Boundary fields of phypar (dict of PHYS_BC arrays of 96*48 values, or a
+        (15, 4608) array in that order); None switches the GPU physics off."""
+        if bc is None:
+            check(lib().sml_dyn_set_physics(self._h, None))
+            return
+        if isinstance(bc, dict):
+            bc = np.stack([np.asarray(bc[k], dtype=np.float64).ravel() for k in PHYS_BC])
+        a = np.ascontiguousarray(bc, dtype=np.float64)
+        if a.size != len(PHYS_BC) * NGP:
+            raise ValueError("bc must hold 15 x 4608 values")
+        check(lib().sml_dyn_set_physics(self._h, ptr(a)))
+
+    def set_clock(self, istep: int, lradsw: bool):
+        check(lib().sml_dyn_set_clock(self._h, int(istep), int(bool(lradsw))))
+
+    def get_clock(self):
+        i, r = ctypes.c_int(), ctypes.c_int()
+        check(lib().sml_dyn_get_clock(self._h, ctypes.byref(i), ctypes.byref(r)))
+        return i.value, bool(r.value)
+
+    def set_rad_state(self, rad=None):
+        """Radiation state (tau2 (4, kx, ngp), stratc (2, ngp), tt_rsw (kx, ngp), ssrd
+        (ngp,)) as a dict, or None = zero."""
+        if rad is None:
+            check(lib().sml_dyn_set_rad_state(self._h, None))
+            return
+        a = np.concatenate([np.asarray(rad[k], dtype=np.float64).ravel()
+                            for k in ("tau2", "stratc", "tt_rsw", "ssrd")])
+        assert a.size == RAD_SIZE
+        check(lib().sml_dyn_set_rad_state(self._h, ptr(a)))
+
+    def get_rad_state(self):
+        a = np.zeros(RAD_SIZE)
+        check(lib().sml_dyn_get_rad_state(self._h, ptr(a)))
+        o = np.cumsum([0, 4 * KX * NGP, 2 * NGP, KX * NGP, NGP])
+        return {"tau2": a[o[0]:o[1]].reshape(4, KX, NGP), "stratc": a[o[1]:o[2]].reshape(2, NGP),
+                "tt_rsw": a[o[2]:o[3]].reshape(KX, NGP), "ssrd": a[o[3]:o[4]]}
+
+    def phypar(self, ug1, vg1, tg1, qg1, phig1, pslg1, lradsw):
+        """phypar alone on host grid inputs (kx, ngp) / (ngp,): returns the physics
+        tendencies (4, kx, ngp) = u, v, t, q; updates the radiation state."""
+        f = [np.ascontiguousarray(x, dtype=np.float64) for x in (ug1, vg1, tg1, qg1, phig1, pslg1)]
+        for x in f[:5]:
+            assert x.size == KX * NGP
+        assert f[5].size == NGP
+        tend = np.zeros((4, KX, NGP))
+        check(lib().sml_dyn_phypar_host(self._h, *[ptr(x) for x in f], int(bool(lradsw)), ptr(tend)))
+        return tend
+
+    def sol_oz(self, tyear: float):
+        """sol_oz(tyear): dict fsol, ozone, ozupp, zenit, stratz (ngp,)."""
+        out = np.zeros((5, NGP))
+        check(lib().sml_dyn_sol_oz(self._h, float(tyear), ptr(out)))
+        return dict(zip(("fsol", "ozone", "ozupp", "zenit", "stratz"), out))
+
+    @staticmethod
+    def sflset(phi0):
+        phi0 = np.ascontiguousarray(phi0, dtype=np.float64).ravel()
+        assert phi0.size == NGP
+        forog = np.zeros(NGP)
+        check(lib().sml_phys_sflset(ptr(phi0), ptr(forog)))
+        return forog
+
     def step(self, j1, j2, dt, alph=ALPH, rob=ROB, wil=WIL, phys=None, stream=None):
         """step(j1, j2, dt, alph, rob, wil).  `phys`: host numpy (4, 8, 48, 96)
         (synchronous), a float64 CUDA tensor of that shape or None (asynchronous on
@@ -138,8 +209,12 @@ class Dynamics:
 
     def window(self, nleap: int = 24, delt: float = DELT, alph: float = ALPH, stream=None, graph: bool = True):
         """One 6-h SPEEDY window after iogrid(30): stepone + nleap x step(2, 2)
-        (dyn_stloop.f90:37-59 with window_size 4), asynchronous, no physics."""
+        (dyn_stloop.f90:37-59 with window_size 4), asynchronous.  With the GPU
+        physics on, stepone uses the lradsw the previous window left (the module
+        flag persists) and stloop restarts at istep = 1 (at_gcm.f90:81, jday = 1)."""
         self.stepone(delt, alph, stream=stream)
+        _, lradsw = self.get_clock()
+        self.set_clock(1, lradsw)
         self.leapfrog(nleap, delt, alph, stream=stream, graph=graph)
 
     def leapfrog(self, nsteps: int, delt: float = DELT, alph: float = ALPH, phys=None, stream=None,
@@ -152,5 +227,8 @@ class Dynamics:
         if graph:
             check(lib().sml_dyn_leapfrog(self._h, nsteps, 2 * delt, alph, ROB, WIL, ptr(phys), stream_ptr(stream)))
             return
-        for _ in range(nsteps):
+        for _ in range(nsteps):  # stloop's clock, launched step by step
+            istep, _ = self.get_clock()
+            self.set_clock(istep, istep % 3 == 1)
             check(lib().sml_dyn_step(self._h, 2, 2, 2 * delt, alph, ROB, WIL, ptr(phys), stream_ptr(stream)))
+            self.set_clock(istep + 1, istep % 3 == 1)

@@ -180,3 +180,37 @@ def dyn_state(seed: int = 2025):
     forcing = {"phis": _spectral_field(rng, 2000.0, 1.5, mean=3000.0),
                "tcorh": _spectral_field(rng, 1.0, 1.5), "qcorh": _spectral_field(rng, 0.1, 1.5)}
     return st, forcing
+
+
+def phys_boundary(dyn, phis, tyear: float = 0.25, seed: int = 41):
+    """Synthetic boundary fields for phypar (sml_dyn_set_physics order, see
+    dynamics.PHYS_BC) on the T30 grid: a smooth land-sea mask, SST / land
+    temperature falling off with latitude, soil water, albedos, a little snow;
+    phis0 = grid image of the spectral orography `phis` (as inbcon builds it,
+    ini_inbcon.f90:38-44), forog = sflset(phis0), and the radiation forcing of
+    sol_oz(tyear).  Shaped like the reference's boundary files, not read from them."""
+    from .spectral import Spectral
+
+    rng = np.random.default_rng(seed)
+    ngp = 96 * 48
+    sp = Spectral()
+    sia = sp.tables()["sia"]
+    lat_s = -np.arcsin(sia)
+    radang = np.concatenate([lat_s, lat_s[::-1] * -1.0])  # south -> north (indyns)
+    lat = np.repeat(radang, 96)
+    lon = np.tile(np.arange(96) * 2 * np.pi / 96, 48)
+    bc = {
+        "fmask1": np.clip(0.5 + 0.6 * np.sin(2 * lon) * np.cos(3 * lat), 0.0, 1.0),
+        "sst_am": 271.0 + 30.0 * np.cos(lat) ** 2 + 0.5 * rng.standard_normal(ngp),
+        "stl_am": 265.0 + 30.0 * np.cos(lat) ** 2 + 1.0 * rng.standard_normal(ngp),
+        "soilw_am": np.clip(0.4 + 0.3 * rng.standard_normal(ngp), 0.0, 1.0),
+        "alb_l": 0.2 + 0.1 * rng.random(ngp),
+        "alb_s": 0.07 + 0.05 * rng.random(ngp),
+        "snowc": np.clip(rng.random(ngp) - 0.7, 0.0, 1.0),
+    }
+    bc["albsfc"] = bc["alb_s"] + bc["fmask1"] * (bc["alb_l"] - bc["alb_s"])
+    ph = np.ascontiguousarray(np.asarray(phis, dtype=np.complex128)).view(np.float64).reshape(1, 32, 62)
+    bc["phis0"] = np.asarray(sp.grid_host(ph, kcos=1)).ravel()
+    bc["forog"] = dyn.sflset(bc["phis0"])
+    bc.update(dyn.sol_oz(tyear))
+    return bc
