@@ -28,6 +28,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 
@@ -89,6 +90,9 @@ struct sml_dynamics {
     PhysTables *d_ptab = nullptr;
     double *d_pbc = nullptr, *d_rad = nullptr, *d_pio = nullptr;
     bool phys_on = false;
+    // step kernels: the 7/8-launch form (default) or the 3-launch fused form
+    // (SML_DYN_FUSED=1 at creation; same results bit for bit)
+    bool fused = false;
     // mod_lflags lradsw (module default .true.) and stloop's istep (at_gcm.f90:81)
     bool lradsw = true;
     int istep = 1;
@@ -206,19 +210,15 @@ __global__ void k_dyn_prep(const double *__restrict__ st, double *__restrict__ s
     }
 }
 
-// grid-point dynamics (grtend :60-217 and the products of :233-275), one thread
-// per grid column; G = the 50 inverse-transformed fields, P = optional physics
-// tendencies [u 8 | v 8 | t 8 | q 8] in grid space (phypar's additions, :225).
-// Output F = the 73 forward-transform inputs:
+// grid-point dynamics of one column (grtend :60-217 and the products of :233-275).
+// g(f) = inverse-transformed field f at the column (layout of k_dyn_prep, kcos = 2
+// group at o2); hasP: add phypar's tendencies pu/pv/pt/pq [kx] where phypar adds
+// them (:225); put(f, v) receives the 73 forward-transform inputs
 //   [utend 8 | -u*tgg 8 | -u*trg 8 | vtend 8 | -v*tgg 8 | -v*trg 8]  (x 1/cos in specx)
 //   [0.5(u^2+v^2) 8 | ttend 8 | trtend 8 | -umean*px - vmean*py]
-__global__ __launch_bounds__(256) void k_dyn_gridpoint(const double *__restrict__ G, const double *__restrict__ P,
-                                                       double *__restrict__ F, const DynTables *__restrict__ T,
-                                                       int o2) {
-    const int pt = blockIdx.x * blockDim.x + threadIdx.x;
-    if (pt >= kGF) return;
-    const int j = pt / kIX;
-    auto g = [&](int f) { return G[(size_t)f * kGF + pt]; };
+template <class GetF, class PutF>
+__device__ inline void gridpoint_column(int j, int o2, GetF g, bool hasP, const double *pu, const double *pv,
+                                        const double *pt, const double *pq, PutF put, const DynTables *T) {
     double ug[kKX], vg[kKX], vorg[kKX], divg[kKX], tg[kKX], trg[kKX];
 #pragma unroll
     for (int k = 0; k < kKX; ++k) {
@@ -237,7 +237,7 @@ __global__ __launch_bounds__(256) void k_dyn_gridpoint(const double *__restrict_
         vmean = vmean + vg[k] * T->dhs[k];
         dmean = dmean + divg[k] * T->dhs[k];
     }
-    F[(size_t)(kNFwd - 1) * kGF + pt] = -umean * px - vmean * py;  // psdt source (:95-97)
+    put(kNFwd - 1, -umean * px - vmean * py);  // psdt source (:95-97)
     double puv[kKX], sigdt[kKXP], sigm[kKXP], tgg[kKX], temp[kKXP];
 #pragma unroll
     for (int k = 0; k < kKX; ++k) puv[k] = (ug[k] - umean) * px + (vg[k] - vmean) * py;
@@ -252,8 +252,6 @@ __global__ __launch_bounds__(256) void k_dyn_gridpoint(const double *__restrict_
     for (int k = 0; k < kKX; ++k) tgg[k] = tg[k] - T->tref[k];
     px = kRgas * px;
     py = kRgas * py;
-    const double *Pu = P, *Pv = P ? P + (size_t)kKX * kGF : nullptr, *Pt = P ? P + (size_t)2 * kKX * kGF : nullptr,
-                 *Pq = P ? P + (size_t)3 * kKX * kGF : nullptr;
     // zonal wind tendency
     temp[0] = 0.0;
     temp[kKX] = 0.0;
@@ -262,8 +260,8 @@ __global__ __launch_bounds__(256) void k_dyn_gridpoint(const double *__restrict_
 #pragma unroll
     for (int k = 0; k < kKX; ++k) {
         double u = vg[k] * vorg[k] - tgg[k] * px - (temp[k + 1] + temp[k]) * T->dhsr[k];
-        if (P) u = u + Pu[(size_t)k * kGF + pt];
-        F[(size_t)k * kGF + pt] = u;
+        if (hasP) u = u + pu[k];
+        put(k, u);
     }
     // meridional wind tendency
 #pragma unroll
@@ -271,8 +269,8 @@ __global__ __launch_bounds__(256) void k_dyn_gridpoint(const double *__restrict_
 #pragma unroll
     for (int k = 0; k < kKX; ++k) {
         double v = -ug[k] * vorg[k] - tgg[k] * py - (temp[k + 1] + temp[k]) * T->dhsr[k];
-        if (P) v = v + Pv[(size_t)k * kGF + pt];
-        F[(size_t)(3 * kKX + k) * kGF + pt] = v;
+        if (hasP) v = v + pv[k];
+        put(3 * kKX + k, v);
     }
     // temperature tendency
 #pragma unroll
@@ -283,8 +281,8 @@ __global__ __launch_bounds__(256) void k_dyn_gridpoint(const double *__restrict_
         double tt = tgg[k] * divg[k] - (temp[k + 1] + temp[k]) * T->dhsr[k] +
                     T->fsgr[k] * tgg[k] * (sigdt[k + 1] + sigdt[k]) + T->tref3[k] * (sigm[k + 1] + sigm[k]) +
                     kAkap * (tg[k] * puv[k] - tgg[k] * dmean);
-        if (P) tt = tt + Pt[(size_t)k * kGF + pt];
-        F[(size_t)(7 * kKX + k) * kGF + pt] = tt;
+        if (hasP) tt = tt + pt[k];
+        put(7 * kKX + k, tt);
     }
     // tracer tendency: no vertical advection between the top three layers (:179-188)
 #pragma unroll
@@ -294,18 +292,41 @@ __global__ __launch_bounds__(256) void k_dyn_gridpoint(const double *__restrict_
 #pragma unroll
     for (int k = 0; k < kKX; ++k) {
         double q = trg[k] * divg[k] - (temp[k + 1] + temp[k]) * T->dhsr[k];
-        if (P) q = q + Pq[(size_t)k * kGF + pt];
-        F[(size_t)(8 * kKX + k) * kGF + pt] = q;
+        if (hasP) q = q + pq[k];
+        put(8 * kKX + k, q);
     }
     // products for the spectral conversion (:239-271)
 #pragma unroll
     for (int k = 0; k < kKX; ++k) {
-        F[(size_t)(kKX + k) * kGF + pt] = -ug[k] * tgg[k];
-        F[(size_t)(4 * kKX + k) * kGF + pt] = -vg[k] * tgg[k];
-        F[(size_t)(2 * kKX + k) * kGF + pt] = -ug[k] * trg[k];
-        F[(size_t)(5 * kKX + k) * kGF + pt] = -vg[k] * trg[k];
-        F[(size_t)(6 * kKX + k) * kGF + pt] = 0.5 * (ug[k] * ug[k] + vg[k] * vg[k]);
+        put(kKX + k, -ug[k] * tgg[k]);
+        put(4 * kKX + k, -vg[k] * tgg[k]);
+        put(2 * kKX + k, -ug[k] * trg[k]);
+        put(5 * kKX + k, -vg[k] * trg[k]);
+        put(6 * kKX + k, 0.5 * (ug[k] * ug[k] + vg[k] * vg[k]));
     }
+}
+
+// grid-point dynamics, one thread per grid column; G = the inverse-transformed
+// fields, P = optional physics tendencies [u 8 | v 8 | t 8 | q 8] in grid space,
+// F = the 73 forward-transform inputs (gridpoint_column)
+__global__ __launch_bounds__(256) void k_dyn_gridpoint(const double *__restrict__ G, const double *__restrict__ P,
+                                                       double *__restrict__ F, const DynTables *__restrict__ T,
+                                                       int o2) {
+    const int pt = blockIdx.x * blockDim.x + threadIdx.x;
+    if (pt >= kGF) return;
+    double pu[kKX], pv[kKX], ptt[kKX], pq[kKX];
+    if (P) {
+#pragma unroll
+        for (int k = 0; k < kKX; ++k) {
+            pu[k] = P[(size_t)k * kGF + pt];
+            pv[k] = P[(size_t)(kKX + k) * kGF + pt];
+            ptt[k] = P[(size_t)(2 * kKX + k) * kGF + pt];
+            pq[k] = P[(size_t)(3 * kKX + k) * kGF + pt];
+        }
+    }
+    gridpoint_column(
+        pt / kIX, o2, [&](int f) { return G[(size_t)f * kGF + pt]; }, P != nullptr, pu, pv, ptt, pq,
+        [&](int f, double v) { F[(size_t)f * kGF + pt] = v; }, T);
 }
 
 // phypar's physics, one thread per grid column (sml_physics.hpp): level fields
@@ -336,23 +357,30 @@ __global__ __launch_bounds__(64) void k_phys(const double *__restrict__ ug1, con
     }
 }
 
-// vds (spe_spectral.f90:307-349) divergence / vorticity of one coefficient
-__device__ inline void vds_at(const double *u, const double *v, const DynTables *T, int m, int n, int p, double *vor,
-                              double *div) {
+// vds (spe_spectral.f90:307-349) divergence / vorticity of one coefficient;
+// u(pp, nn), v(pp, nn) read part pp of coefficient (m, nn)
+template <class U, class V>
+__device__ inline void vds_gen(U u, V v, const DynTables *T, int m, int n, int p, double *vor, double *div) {
     const double gx = T->gradx[m];
     // zp(2)=gradx*u(1), zp(1)=-gradx*u(2); zc likewise from v
-    const double zp = p == 1 ? gx * u[ci(0, m, n)] : -gx * u[ci(1, m, n)];
-    const double zc = p == 1 ? gx * v[ci(0, m, n)] : -gx * v[ci(1, m, n)];
+    const double zp = p == 1 ? gx * u(0, n) : -gx * u(1, n);
+    const double zc = p == 1 ? gx * v(0, n) : -gx * v(1, n);
     if (n == 0) {
-        *vor = zc - T->vddyp[0][m] * u[ci(p, m, 1)];
-        *div = zp + T->vddyp[0][m] * v[ci(p, m, 1)];
+        *vor = zc - T->vddyp[0][m] * u(p, 1);
+        *div = zp + T->vddyp[0][m] * v(p, 1);
     } else if (n == kNX - 1) {
-        *vor = T->vddym[n][m] * u[ci(p, m, kNTRUN1 - 1)];
-        *div = -T->vddym[n][m] * v[ci(p, m, kNTRUN1 - 1)];
+        *vor = T->vddym[n][m] * u(p, kNTRUN1 - 1);
+        *div = -T->vddym[n][m] * v(p, kNTRUN1 - 1);
     } else {
-        *vor = T->vddym[n][m] * u[ci(p, m, n - 1)] - T->vddyp[n][m] * u[ci(p, m, n + 1)] + zc;
-        *div = -T->vddym[n][m] * v[ci(p, m, n - 1)] + T->vddyp[n][m] * v[ci(p, m, n + 1)] + zp;
+        *vor = T->vddym[n][m] * u(p, n - 1) - T->vddyp[n][m] * u(p, n + 1) + zc;
+        *div = -T->vddym[n][m] * v(p, n - 1) + T->vddyp[n][m] * v(p, n + 1) + zp;
     }
+}
+
+__device__ inline void vds_at(const double *u, const double *v, const DynTables *T, int m, int n, int p, double *vor,
+                              double *div) {
+    vds_gen([&](int pp, int nn) { return u[ci(pp, m, nn)]; }, [&](int pp, int nn) { return v[ci(pp, m, nn)]; }, T, m,
+            n, p, vor, div);
 }
 
 // combine: spectral tendencies of grtend (:229-278) from the 73 forward transforms
@@ -378,27 +406,21 @@ __global__ void k_dyn_combine(const double *__restrict__ S, double *__restrict__
     }
 }
 
-// tail: sptend + geop + implic + hordif + drag + timint.  A block owns 32 real
-// coefficients c (= Re/Im of (m, n)) x all 8 levels, one thread per (c, level k);
-// the vertical couplings (dmeanc, sigdtc, geop, implic's level matrices) go
-// through LDS, and every sum runs over k in the reference's order.
-constexpr int kTailC = 32;
-__global__ __launch_bounds__(256) void k_dyn_tail(double *__restrict__ st, double *__restrict__ Td,
-                                                  double *__restrict__ phi_out, const double *__restrict__ phis,
-                                                  const double *__restrict__ tcorh, const double *__restrict__ qcorh,
-                                                  const DynTables *__restrict__ T, int j1, int j4, double dt,
-                                                  double alph, double rob, double wil) {
-    __shared__ double sh[2][kKX][kTailC];
-    const int cc = threadIdx.x & (kTailC - 1), k = threadIdx.x / kTailC;
-    const int c = blockIdx.x * kTailC + cc;  // 0 .. 1983 = 2 * (m + mx n) + p
-    const int mn = c >> 1, m = mn % kMX, n = mn / kMX;
+// tail: sptend + geop + implic + hordif + drag + timint of one real coefficient c
+// (= Re/Im of (m, n)) at level k, given grtend's spectral tendencies of (c, k).
+// The CW coefficients x 8 levels of a block share sh[2][kx][CW] (LDS) for the
+// vertical couplings (dmeanc, sigdtc, geop, implic's level matrices); every sum
+// runs over k in the reference's order.  The whole block must call it (barriers).
+template <int CW>
+__device__ inline void tail_coef(double *__restrict__ st, double *__restrict__ Td, double *__restrict__ phi_out,
+                                 const double *__restrict__ phis, const double *__restrict__ tcorh,
+                                 const double *__restrict__ qcorh, const DynTables *__restrict__ T, double (*sh)[kKX][CW],
+                                 int cc, int k, int c, int m, int n, double vordt, double divdt, double tdt, double trdt,
+                                 double psdt, int j1, int j4, double dt, double alph, double rob, double wil) {
     auto S = [&](size_t off, int lev, int kk) -> double & {  // state (c, kk, lev); ps has one level
         const size_t nlev = (off == kOffPs) ? 1 : kKX;
         return st[off + ((size_t)(lev - 1) * nlev + kk) * kSF + c];
     };
-    double vordt = Td[kTVor + (size_t)k * kSF + c], divdt = Td[kTDiv + (size_t)k * kSF + c];
-    double tdt = Td[kTT + (size_t)k * kSF + c], trdt = Td[kTTr + (size_t)k * kSF + c];
-    double psdt = Td[kTPs + c];
     // ---- sptend(divdt, tdt, psdt, j4)  (dyn_sptend.f90:29-66)
     sh[0][k][cc] = S(kOffDiv, j4, k);
     sh[1][k][cc] = S(kOffT, j4, k);
@@ -407,7 +429,7 @@ __global__ __launch_bounds__(256) void k_dyn_tail(double *__restrict__ st, doubl
 #pragma unroll
     for (int kk = 0; kk < kKX; ++kk) dmeanc = dmeanc + sh[0][kk][cc] * T->dhs[kk];
     psdt = psdt - dmeanc;
-    if (c < 2) psdt = 0.0;  // psdt(1,1) = 0
+    if (m == 0 && n == 0) psdt = 0.0;  // psdt(1,1) = 0
     double sig_k = 0.0, sig_k1 = 0.0;  // sigdtc(k), sigdtc(k+1); sigdtc(1) = sigdtc(kxp) = 0
     {
         double sg = 0.0;
@@ -506,6 +528,283 @@ __global__ __launch_bounds__(256) void k_dyn_tail(double *__restrict__ st, doubl
     timint(kOffDiv, k, divdt);
     timint(kOffT, k, tdt);
     timint(kOffTr, k, trdt);
+}
+
+// tail kernel of the unfused step: a block owns 32 real coefficients x 8 levels
+constexpr int kTailC = 32;
+__global__ __launch_bounds__(256) void k_dyn_tail(double *__restrict__ st, double *__restrict__ Td,
+                                                  double *__restrict__ phi_out, const double *__restrict__ phis,
+                                                  const double *__restrict__ tcorh, const double *__restrict__ qcorh,
+                                                  const DynTables *__restrict__ T, int j1, int j4, double dt,
+                                                  double alph, double rob, double wil) {
+    __shared__ double sh[2][kKX][kTailC];
+    const int cc = threadIdx.x & (kTailC - 1), k = threadIdx.x / kTailC;
+    const int c = blockIdx.x * kTailC + cc;  // 0 .. 1983 = 2 * (m + mx n) + p
+    const int mn = c >> 1, m = mn % kMX, n = mn / kMX;
+    tail_coef<kTailC>(st, Td, phi_out, phis, tcorh, qcorh, T, sh, cc, k, c, m, n, Td[kTVor + (size_t)k * kSF + c],
+                      Td[kTDiv + (size_t)k * kSF + c], Td[kTT + (size_t)k * kSF + c], Td[kTTr + (size_t)k * kSF + c],
+                      Td[kTPs + c], j1, j4, dt, alph, rob, wil);
+}
+
+// ======================================================= fused step (3 launches)
+// The step's ten stages regrouped at the only all-to-all seams of the spectral
+// transform (spectral <-> Fourier per zonal wavenumber m, Fourier <-> grid per
+// latitude row): every kernel owns either one m or one latitude row, so each
+// regrouped stage works on data its own block produced or that the previous
+// launch left in L2.  Same arithmetic and summation order as the unfused
+// kernels above (bit-identical results).
+//   K1 k_dyn_inv  (m, 8-field tile): prep's inputs computed on the fly + gridy
+//   K2 k_dyn_row  (latitude row j):  gridx -> LDS -> physics + grid-point dynamics
+//                                    -> LDS -> specx (vdspec's 1/cos scaling)
+//   K3 k_dyn_spec (m):               specy -> LDS -> combine (vds, lap) -> tail
+typedef double d4 __attribute__((ext_vector_type(4)));
+#define MFMA64(a, b, c) __builtin_amdgcn_mfma_f64_16x16x4f64((a), (b), (c), 0, 0, 0)
+
+// one value of k_dyn_prep's output: inverse-transform input field f at (m, n), part p
+__device__ inline double inv_input(const double *__restrict__ st, const double *__restrict__ phis,
+                                   const DynTables *__restrict__ T, int f, int m, int n, int p, int j2, int o2,
+                                   bool phys) {
+    const size_t lev2 = (size_t)(j2 - 1) * kKX;
+    const int c = ci(p, m, n);
+    if (f < 4 * kKX) {
+        const int var = f / kKX, k = f % kKX;
+        const size_t off = var == 0 ? kOffVor : var == 1 ? kOffDiv : var == 2 ? kOffT : kOffTr;
+        return st[off + (lev2 + k) * kSF + c];
+    }
+    if (f < o2) {  // phypar's level-1 inputs (phys only)
+        if (f < kPQ1) return st[kOffT + (size_t)(f - kPT1) * kSF + c];
+        if (f < kPPhi1) return st[kOffTr + (size_t)(f - kPQ1) * kSF + c];
+        if (f < kPPs1) return geop_at(st + kOffT, phis, T, c, m, f - kPPhi1);
+        return st[kOffPs + c];
+    }
+    int g = f - o2;
+    if (g == 2 * kKX || g == 2 * kKX + 1) {  // grad(ps(j2))
+        const double *ps = st + kOffPs + (size_t)(j2 - 1) * kSF;
+        if (g == 2 * kKX) return p == 1 ? T->gradx[m] * ps[ci(0, m, n)] : -T->gradx[m] * ps[ci(1, m, n)];
+        if (n == 0) return T->gradyp[0][m] * ps[ci(p, m, 1)];
+        if (n == kNX - 1) return -T->gradym[n][m] * ps[ci(p, m, kNTRUN1 - 1)];
+        return -T->gradym[n][m] * ps[ci(p, m, n - 1)] + T->gradyp[n][m] * ps[ci(p, m, n + 1)];
+    }
+    size_t lev = lev2;
+    if (g > 2 * kKX + 1) {  // ucos1 / vcos1 of level 1
+        g -= 2 * kKX + 2;
+        lev = 0;
+    }
+    const int k = g % kKX;
+    const bool vcos = g >= kKX;
+    (void)phys;
+    const double *vor = st + kOffVor + (lev + k) * kSF, *div = st + kOffDiv + (lev + k) * kSF;
+    // uvspec (spe_spectral.f90:351-387), the part of uvspec_at this value needs
+    const double ux = T->uvdx[n][m];
+    if (!vcos) {
+        const double zc = p == 1 ? ux * div[ci(0, m, n)] : -ux * div[ci(1, m, n)];
+        if (n == 0) return zc - T->uvdyp[0][m] * vor[ci(p, m, 1)];
+        if (n == kNX - 1) return T->uvdym[n][m] * vor[ci(p, m, kNTRUN1 - 1)];
+        return T->uvdym[n][m] * vor[ci(p, m, n - 1)] - T->uvdyp[n][m] * vor[ci(p, m, n + 1)] + zc;
+    }
+    const double zp = p == 1 ? ux * vor[ci(0, m, n)] : -ux * vor[ci(1, m, n)];
+    if (n == 0) return zp + T->uvdyp[0][m] * div[ci(p, m, 1)];
+    if (n == kNX - 1) return -T->uvdym[n][m] * div[ci(p, m, kNTRUN1 - 1)];
+    return -T->uvdym[n][m] * div[ci(p, m, n - 1)] + T->uvdyp[n][m] * div[ci(p, m, n + 1)] + zp;
+}
+
+// K1: gridy of the step's inverse-transform inputs (k_gridy's tiling: one wave per
+// (m, 8 fields x Re/Im); lanes gather their 8 spectral values from the state)
+__global__ __launch_bounds__(64) void k_dyn_inv(const double *__restrict__ st, const double *__restrict__ phis,
+                                                const DynTables *__restrict__ T, const double *__restrict__ pinv,
+                                                double *__restrict__ varm, int nf, int j2, int o2, int phys) {
+    const int m = blockIdx.x;
+    const int f0 = blockIdx.y * 8;
+    const int l = threadIdx.x, r = l & 15, kk = l >> 4;
+    const int fa = f0 + (r >> 1), p = r & 1;
+    const bool ok = fa < nf;
+    const double *pm = pinv + (size_t)m * kNX * 32;
+    d4 acc00 = {0, 0, 0, 0}, acc01 = acc00, acc10 = acc00, acc11 = acc00;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        const int n_odd = 2 * (4 * s + kk);  // n = 1,3,.. (1-based): symmetric part
+        const int n_even = n_odd + 1;        // n = 2,4,..: antisymmetric part
+        const double a0 = ok ? inv_input(st, phis, T, fa, m, n_odd, p, j2, o2, phys) : 0.0;
+        const double a1 = ok ? inv_input(st, phis, T, fa, m, n_even, p, j2, o2, phys) : 0.0;
+        acc00 = MFMA64(a0, pm[n_odd * 32 + r], acc00);
+        acc01 = MFMA64(a0, pm[n_odd * 32 + 16 + r], acc01);
+        acc10 = MFMA64(a1, pm[n_even * 32 + r], acc10);
+        acc11 = MFMA64(a1, pm[n_even * 32 + 16 + r], acc11);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int row = kk + 4 * q;
+        const int f = f0 + (row >> 1);
+        if (f >= nf) continue;
+        double *vr = varm + (size_t)f * kVF + 2 * m + (row & 1);
+        {
+            const int j = r;
+            const double sym = acc00[q], asym = acc10[q];
+            vr[(kIL - 1 - j) * kMX2] = sym + asym;
+            vr[j * kMX2] = sym - asym;
+        }
+        const int j = 16 + r;
+        if (j < kIY) {
+            const double sym = acc01[q], asym = acc11[q];
+            vr[(kIL - 1 - j) * kMX2] = sym + asym;
+            vr[j * kMX2] = sym - asym;
+        }
+    }
+}
+
+// K2: one latitude row j per block.  LDS holds the row's inverse-transformed fields
+// and then its 73 forward-transform inputs (stride kRowLd breaks LDS bank aliasing).
+constexpr int kRowThreads = 256, kRowWaves = kRowThreads / 64, kRowLd = 100;
+__global__ __launch_bounds__(kRowThreads) void k_dyn_row(
+    const double *__restrict__ varm, double *__restrict__ varm_out, const double *__restrict__ dinv,
+    const double *__restrict__ dfwd, const double *__restrict__ cosgr, const DynTables *__restrict__ T, int nin,
+    int n1, const double *__restrict__ Pext, const double *__restrict__ bc, double *__restrict__ rad,
+    const PhysTables *__restrict__ PT, int phys, int lradsw) {
+    __shared__ double G[kNInvMax * kRowLd];
+    __shared__ double F[kNFwd * kRowLd];
+    const int j = blockIdx.x;
+    const int wave = threadIdx.x >> 6, l = threadIdx.x & 63, r = l & 15, kk = l >> 4;
+    // a) gridx (k_gridx with fields in the M role): G[f][lon] = sum_c varm[f][j][c] dinv[c][lon]
+    const int nft = (nin + 15) / 16;
+    for (int t = wave; t < nft * 6; t += kRowWaves) {
+        const int ft = t / 6, lt = t % 6;
+        const int fa = ft * 16 + r;
+        const bool ok = fa < nin;
+        const double *vr = varm + (size_t)(ok ? fa : 0) * kVF + j * kMX2;
+        d4 acc = {0, 0, 0, 0};
+#pragma unroll 8
+        for (int s = 0; s < kCPad / 4; ++s) {
+            const int c = 4 * s + kk;
+            const double b = dinv[c * kIX + 16 * lt + r];
+            const double a = (ok && c < kMX2) ? vr[c] : 0.0;
+            acc = MFMA64(a, b, acc);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int f = ft * 16 + kk + 4 * q;
+            if (f < nin) {
+                double v = acc[q];
+                if (f >= n1) v = v * cosgr[j];  // kcos = 2
+                G[f * kRowLd + 16 * lt + r] = v;
+            }
+        }
+    }
+    __syncthreads();
+    // b) one thread per grid column: phypar on level 1, grid-point dynamics
+    if (threadIdx.x < kIX) {
+        const int i = threadIdx.x, pt = j * kIX + i;
+        auto g = [&](int f) { return G[f * kRowLd + i]; };
+        double pu[kKX], pv[kKX], ptt[kKX], pq[kKX];
+        bool hasP = false;
+        if (phys) {
+            double ua[kKX], va[kKX], ta[kKX], qa[kKX], ph[kKX];
+#pragma unroll
+            for (int k = 0; k < kKX; ++k) {
+                ua[k] = g(n1 + 2 * kKX + 2 + k);
+                va[k] = g(n1 + 3 * kKX + 2 + k);
+                ta[k] = g(kPT1 + k);
+                qa[k] = g(kPQ1 + k);
+                ph[k] = g(kPPhi1 + k);
+            }
+            phys_column(pt, ua, va, ta, qa, ph, g(kPPs1), bc, rad, PT, lradsw != 0, pu, pv, ptt, pq);
+            hasP = true;
+        } else if (Pext) {
+#pragma unroll
+            for (int k = 0; k < kKX; ++k) {
+                pu[k] = Pext[(size_t)k * kGF + pt];
+                pv[k] = Pext[(size_t)(kKX + k) * kGF + pt];
+                ptt[k] = Pext[(size_t)(2 * kKX + k) * kGF + pt];
+                pq[k] = Pext[(size_t)(3 * kKX + k) * kGF + pt];
+            }
+            hasP = true;
+        }
+        gridpoint_column(j, n1, g, hasP, pu, pv, ptt, pq, [&](int f, double v) { F[f * kRowLd + i] = v; }, T);
+    }
+    __syncthreads();
+    // c) specx (k_specx with fields in the M role), vdspec inputs x cosgr (kcos = 2)
+    const double s0 = cosgr[j];
+    for (int t = wave; t < 5 * 4; t += kRowWaves) {
+        const int ft = t / 4, ct = t % 4;
+        const int fa = ft * 16 + r;
+        const bool ok = fa < kNFwd;
+        const bool scale = fa < kNFwdScaled;
+        const double *fr = F + (ok ? fa : 0) * kRowLd;
+        d4 acc = {0, 0, 0, 0};
+#pragma unroll 8
+        for (int s = 0; s < kIX / 4; ++s) {
+            const int i = 4 * s + kk;
+            const double b = dfwd[i * kCPad + 16 * ct + r];
+            double a = ok ? fr[i] : 0.0;
+            if (scale) a = a * s0;
+            acc = MFMA64(a, b, acc);
+        }
+        const int c = 16 * ct + r;
+        if (c < kMX2) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int f = ft * 16 + kk + 4 * q;
+                if (f < kNFwd) varm_out[(size_t)f * kVF + j * kMX2 + c] = acc[q];
+            }
+        }
+    }
+}
+
+// K3: one zonal wavenumber m per block: specy of the 73 fields into LDS, then the
+// combine and tail of the m's 64 real coefficients x 8 levels (one thread each).
+constexpr int kSpecThreads = 512;
+__global__ __launch_bounds__(kSpecThreads) void k_dyn_spec(
+    const double *__restrict__ varm, const double *__restrict__ pfwd, const double *__restrict__ wt,
+    double *__restrict__ st, double *__restrict__ Td, double *__restrict__ phi_out, const double *__restrict__ phis,
+    const double *__restrict__ tcorh, const double *__restrict__ qcorh, const DynTables *__restrict__ T, int j1,
+    int j4, double dt, double alph, double rob, double wil) {
+    __shared__ double S[kNFwd * 2 * kNX];  // [f][2 n + p] of this m
+    __shared__ double sh[2][kKX][2 * kNX];
+    const int m = blockIdx.x;
+    const int wave = threadIdx.x >> 6, l = threadIdx.x & 63, r = l & 15, kk = l >> 4;
+    // a) specy (k_specy's tiling: 8 fields x Re/Im per wave)
+    const double *pm = pfwd + (size_t)m * kNX * kIY;
+    for (int tile = wave; tile < (kNFwd + 7) / 8; tile += kSpecThreads / 64) {
+        const int f0 = tile * 8;
+        const int fa = f0 + (r >> 1);
+        const bool ok = fa < kNFwd;
+        const double *vr = varm + (size_t)(ok ? fa : 0) * kVF + 2 * m + (r & 1);
+        d4 accS = {0, 0, 0, 0}, accD = accS;
+#pragma unroll
+        for (int s = 0; s < kIY / 4; ++s) {
+            const int j = 4 * s + kk;
+            double aS = 0.0, aD = 0.0;
+            if (ok) {
+                const double vn = vr[(kIL - 1 - j) * kMX2], vs = vr[j * kMX2];
+                aS = (vn + vs) * wt[j];
+                aD = (vn - vs) * wt[j];
+            }
+            accS = MFMA64(aS, pm[(2 * r) * kIY + j], accS);
+            accD = MFMA64(aD, pm[(2 * r + 1) * kIY + j], accD);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int row = kk + 4 * q;
+            const int f = f0 + (row >> 1);
+            if (f >= kNFwd) continue;
+            S[f * 2 * kNX + 2 * (2 * r) + (row & 1)] = accS[q];
+            S[f * 2 * kNX + 2 * (2 * r + 1) + (row & 1)] = accD[q];
+        }
+    }
+    __syncthreads();
+    // b) combine (k_dyn_combine) for coefficient (n, p) at level k
+    const int cc = threadIdx.x & (2 * kNX - 1), k = threadIdx.x / (2 * kNX);
+    const int n = cc >> 1, p = cc & 1;
+    const int c = ci(p, m, n);
+    auto fl = [&](int f) { return [=](int pp, int nn) { return S[f * 2 * kNX + 2 * nn + pp]; }; };
+    double vo, dv, d0, dq, dummy;
+    vds_gen(fl(k), fl(3 * kKX + k), T, m, n, p, &vo, &dv);  // vdspec(utend, vtend)
+    const double lapv = -(fl(6 * kKX + k)(p, n) * T->el2[n][m]);
+    vds_gen(fl(kKX + k), fl(4 * kKX + k), T, m, n, p, &dummy, &d0);      // vdspec(-u tgg, -v tgg)
+    vds_gen(fl(2 * kKX + k), fl(5 * kKX + k), T, m, n, p, &dummy, &dq);  // vdspec(-u trg, -v trg)
+    const double psdt = (m == 0 && n == 0) ? 0.0 : fl(kNFwd - 1)(p, n);
+    // c) sptend / implic / diffusion / time integration
+    tail_coef<2 * kNX>(st, Td, phi_out, phis, tcorh, qcorh, T, sh, cc, k, c, m, n, vo, dv - lapv,
+                       d0 + fl(7 * kKX + k)(p, n), dq + fl(8 * kKX + k)(p, n), psdt, j1, j4, dt, alph, rob, wil);
 }
 
 // ------------------------------------------------------------ iogrid(30/31)
@@ -652,6 +951,7 @@ extern "C" int sml_dyn_create(double radius, sml_dynamics **out) {
     }
     build_dyn_indyns(spectral_host_tables(d->sp), &d->tab);
     build_phys_tables(d->tab, &d->ptab);
+    if (const char *e = std::getenv("SML_DYN_FUSED")) d->fused = *e && *e != '0';
     if ((rc = dalloc(&d->d_tabs, 4)) || (rc = dalloc(&d->d_state, kStateSize)) || (rc = dalloc(&d->d_phis, kSF)) ||
         (rc = dalloc(&d->d_tcorh, kSF)) || (rc = dalloc(&d->d_qcorh, kSF)) || (rc = dalloc(&d->d_phi, kKX * kSF)) ||
         (rc = dalloc(&d->d_specin, (size_t)kNInvMax * kSF)) ||
@@ -754,10 +1054,10 @@ extern "C" int sml_dyn_state_device(sml_dynamics *d, double **d_state, double **
 
 namespace {
 
-// the launches of one step(j1, j2, dt, alph, rob, wil) on stream st: 7 without
-// GPU physics, 8 with it
-int launch_step(sml_dynamics *d, int j1, int j2, double dt, double alph, double rob, double wil,
-                const double *d_phys, bool lradsw, hipStream_t st) {
+// the unfused launches of one step(j1, j2, dt, alph, rob, wil) on stream st: 7
+// without GPU physics, 8 with it
+int launch_step_unfused(sml_dynamics *d, int j1, int j2, double dt, double alph, double rob, double wil,
+                        const double *d_phys, bool lradsw, hipStream_t st) {
     const DynTables *T = d->d_tab;
     const bool phys = d->phys_on;
     const int n1 = phys ? kNInv1P : kNInv1, nin = phys ? kNInvP : kNInv;
@@ -791,6 +1091,34 @@ int launch_step(sml_dynamics *d, int j1, int j2, double dt, double alph, double 
                        d->d_phis, d->d_tcorh, d->d_qcorh, T, j1, j4, dt, alph, rob, wil);
     SML_HIP(hipGetLastError());
     return SML_OK;
+}
+
+// the fused step: K1 k_dyn_inv, K2 k_dyn_row, K3 k_dyn_spec
+int launch_step_fused(sml_dynamics *d, int j1, int j2, double dt, double alph, double rob, double wil,
+                      const double *d_phys, bool lradsw, hipStream_t st) {
+    const DynTables *T = d->d_tab;
+    const bool phys = d->phys_on;
+    const int n1 = phys ? kNInv1P : kNInv1, nin = phys ? kNInvP : kNInv;
+    const SpectralDev sd = spectral_dev(d->sp);
+    hipLaunchKernelGGL(k_dyn_inv, dim3(kMX, (nin + 7) / 8), dim3(64), 0, st, d->d_state, d->d_phis, T, sd.pinv,
+                       d->d_varm, nin, j2, n1, phys ? 1 : 0);
+    SML_HIP(hipGetLastError());
+    // the Fourier coefficients of the forward transforms go to d_gfwd ([73][48][62] fits)
+    hipLaunchKernelGGL(k_dyn_row, dim3(kIL), dim3(kRowThreads), 0, st, d->d_varm, d->d_gfwd, sd.dinv, sd.dfwd,
+                       sd.cosgr, T, nin, n1, phys ? nullptr : d_phys, d->d_pbc, d->d_rad, d->d_ptab, phys ? 1 : 0,
+                       lradsw ? 1 : 0);
+    SML_HIP(hipGetLastError());
+    const int j4 = (alph == 0.0) ? j2 : 1;
+    hipLaunchKernelGGL(k_dyn_spec, dim3(kMX), dim3(kSpecThreads), 0, st, d->d_gfwd, sd.pfwd, sd.wt, d->d_state,
+                       d->d_tend, d->d_phi, d->d_phis, d->d_tcorh, d->d_qcorh, T, j1, j4, dt, alph, rob, wil);
+    SML_HIP(hipGetLastError());
+    return SML_OK;
+}
+
+int launch_step(sml_dynamics *d, int j1, int j2, double dt, double alph, double rob, double wil, const double *d_phys,
+                bool lradsw, hipStream_t st) {
+    return d->fused ? launch_step_fused(d, j1, j2, dt, alph, rob, wil, d_phys, lradsw, st)
+                    : launch_step_unfused(d, j1, j2, dt, alph, rob, wil, d_phys, lradsw, st);
 }
 
 }  // namespace

@@ -516,6 +516,10 @@ SpectralDev spectral_dev(const sml_spectral *s) {
     d.cosgr = s->d_cosgr;
     d.cosgr2 = s->d_cosgr2;
     d.wt = s->d_wt;
+    d.pinv = s->d_pinv;
+    d.pfwd = s->d_pfwd;
+    d.dinv = s->d_dinv;
+    d.dfwd = s->d_dfwd;
     return d;
 }
 

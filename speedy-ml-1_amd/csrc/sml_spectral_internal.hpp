@@ -13,6 +13,10 @@ struct SpectralDev {
     const double *gradx, *uvdx, *uvdym, *uvdyp, *vddym, *vddyp;  // [n][m] (gradx [m])
     const double *el2, *trfilt;                                   // [n][m]
     const double *cosgr, *cosgr2, *wt;                            // [48], [48], [24]
+    // the transform matrices (layouts in sml_spectral.hip): Legendre inverse
+    // [m][n][32 lat], forward [m][n][24 lat]; Fourier inverse [64 c][96 lon],
+    // forward [96 lon][64 c]
+    const double *pinv, *pfwd, *dinv, *dfwd;
 };
 
 const SpectralTables &spectral_host_tables(const sml_spectral *s);

@@ -186,3 +186,46 @@ def test_host_tendencies_rejected_while_gpu_physics_on(dyn, dyn_golden):
         dyn.step(2, 2, 1800.0, 0.5, phys=g["phys"])
     dyn.set_physics(None)
     dyn.step(2, 2, 1800.0, 0.5, phys=g["phys"])
+
+
+@pytest.mark.parametrize("physics", [False, True])
+def test_fused_step_is_bitwise_the_unfused_step(pg, cuda, physics):
+    """The 3-launch fused step (k_dyn_inv, k_dyn_row, k_dyn_spec; SML_DYN_FUSED=1) and
+    the 7/8-launch step (the default) evaluate the same operations in the same
+    order: a window of steps must agree bit for bit (state, radiation state)."""
+    import os
+
+    import torch
+
+    from speedy_ml_amd.dynamics import Dynamics
+    from speedy_ml_amd.synthetic import dyn_state
+
+    st, forcing = dyn_state(9)
+    out = []
+    for fused in ("0", "1"):
+        os.environ["SML_DYN_FUSED"] = fused
+        try:
+            d = Dynamics()
+        finally:
+            os.environ.pop("SML_DYN_FUSED", None)
+        d.set_forcing(**forcing)
+        d.set_state(st)
+        if physics:
+            d.set_physics(_window_bc(pg, d))
+            d.set_rad_state(None)
+        d.set_clock(1, True)
+        d.stepone()
+        d.set_clock(1, True)
+        d.leapfrog(4, graph=True)
+        d.leapfrog(2, graph=False)
+        d.step(2, 2, 0.0, 0.5)  # tendencies only
+        torch.cuda.synchronize()
+        out.append((d.get_state(), d.get_rad_state(), d.get_tendencies(), d.get_phi()))
+        d.close()
+    (a, ra, ta, pa), (b, rb, tb, pb) = out
+    for f in oracle.DYN_FIELDS:
+        np.testing.assert_array_equal(a[f], b[f])
+    for k in ra:
+        np.testing.assert_array_equal(ra[k], rb[k])
+    np.testing.assert_array_equal(ta, tb)
+    np.testing.assert_array_equal(pa, pb)
