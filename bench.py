@@ -52,6 +52,9 @@ def parse():
     p.add_argument("--weights", choices=("f32", "f64"), default="f32")
     p.add_argument("--cpu-sample", type=int, default=96, help="regions in the CPU-baseline sample (0 = skip)")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--overlap", action="store_true",
+                   help="issue the reservoir half and SPEEDY's window on two streams (speedy_ml_amd/hybrid.py); "
+                        "measured no faster on MI355X: the readout's HBM stream raises the window's memory latency")
     p.add_argument("--train-regions", type=int, default=8,
                    help="regions in the supplementary W_out-training leg (0 = skip)")
     p.add_argument("--train-steps", type=int, default=4096, help="training time steps per region in that leg")
@@ -75,6 +78,7 @@ def main():
     from speedy_ml_amd import domain
     from speedy_ml_amd.dynamics import Dynamics
     from speedy_ml_amd.exchange import OutvecExchange
+    from speedy_ml_amd.hybrid import HybridLoop
     from speedy_ml_amd.reservoir import Reservoirs
     from speedy_ml_amd.synthetic import (dyn_state, initial_state, phys_boundary, region_weights,
                                          synthetic_grids)
@@ -107,16 +111,11 @@ def main():
         res.set_state(i, initial_state(r, w.n))
         if i % 144 == 0:
             log(rank, f"loaded {i}/{len(regions)} regions ({time.time() - t_setup:.1f}s)")
-    fb, lm, ov = res.alloc_io(dev)
     exchange = OutvecExchange(nreg, world, rank, device=dev)
     g4h, g2h, prh = synthetic_grids(11)
     f4h, f2h, _ = synthetic_grids(12)
-    g4 = torch.from_numpy(g4h).to(dev)
-    g2 = torch.from_numpy(g2h).to(dev)
-    pr = torch.from_numpy(prh).to(dev)
-    f4 = torch.from_numpy(f4h).to(dev)
-    f2 = torch.from_numpy(f2h).to(dev)
-    tisr = torch.from_numpy(np.random.default_rng(13).standard_normal((len(regions), 16))).to(dev)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    tisr = t(np.random.default_rng(13).standard_normal((len(regions), 16)))
     # SPEEDY on the GPU: dynamical core + physics, forcing and boundary fields
     st0, forcing = dyn_state()
     dyn = Dynamics()
@@ -124,19 +123,17 @@ def main():
     dyn.set_state(st0)
     phys_bc = phys_boundary(dyn, forcing["phis"])
     dyn.set_physics(phys_bc)
+    # the hybrid loop (speedy_ml_amd/hybrid.py); --overlap puts SPEEDY's window on a
+    # second stream beside the reservoir update + v_ml readout
+    loop = HybridLoop(res, dyn, exchange, dev, tisr=tisr, overlap=args.overlap)
     # initial inputs from the synthetic analysis state (start_prediction analogue)
-    res.tile_inputs(g4, g2, pr, f4, f2, tisr, fb, lm)
+    loop.start(t(g4h), t(g2h), t(prh), t(f4h), t(f2h))
+    fb, lm, ov, g4, g2, pr, f4, f2 = loop.fb, loop.lm, loop.ov, loop.g4, loop.g2, loop.pr, loop.f4, loop.f2
     torch.cuda.synchronize()
     log(rank, f"setup {time.time() - t_setup:.1f}s, {len(regions)} regions on rank 0")
 
     def step():
-        res.predict(fb, lm, ov)
-        glob = exchange(ov)  # RCCL all-gather over xGMI when world > 1
-        res.assemble(glob, g4, g2, pr)
-        dyn.from_grid(g4, g2)  # iogrid(30); min/max for the safety check stay on the device
-        dyn.window(24)         # stepone + 24 x step(2,2) with physics (hipGraph replay)
-        dyn.to_grid(f4, f2)    # iogrid(31): the forecast the next local_model is tiled from
-        res.tile_inputs(g4, g2, pr, f4, f2, tisr, fb, lm)
+        loop.step()
 
     def timed(fn, nsteps, timing=False):
         if timing:
@@ -147,6 +144,7 @@ def main():
         t0 = time.perf_counter()
         for _ in range(nsteps):
             fn()
+        loop.sync()
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -159,7 +157,7 @@ def main():
 
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize()
+    loop.sync()
     dt = timed(step, args.steps, timing=True)
     upd_ms, rd_ms = res.kernel_times()
     _, safe = dyn.from_grid(g4.cpu().numpy(), g2.cpu().numpy())
@@ -167,8 +165,15 @@ def main():
 
     # ---- roofline of the dominant kernel (readout: streams W_out)
     wb = 4 if args.weights == "f32" else 8
-    rd_bytes = sum(wb * 136 * (132 + s.n) + 8 * (132 + s.n) + 8 * 136 + 2 * 36 * 8 for s in sizes)
-    rd_bytes_f64 = sum(8 * 136 * (132 + s.n) + 8 * (132 + s.n) + 8 * 136 + 2 * 36 * 8 for s in sizes)
+    # the timed readout launch: one pass over W_out [local_model; x~] + unstandardize
+    # (columns 132 + n, x_aug in, outvec + mean/std), or with --overlap the v_ml half
+    # (W_out(:, ncs+1:) x~: n columns, x~ in, 136 partial sums out), per region
+    if args.overlap:
+        rd_cost = lambda s, b: b * 136 * s.n + 8 * s.n + 8 * 136  # noqa: E731
+    else:
+        rd_cost = lambda s, b: b * 136 * (132 + s.n) + 8 * (132 + s.n) + 8 * 136 + 2 * 36 * 8  # noqa: E731
+    rd_bytes = sum(rd_cost(s, wb) for s in sizes)
+    rd_bytes_f64 = sum(rd_cost(s, 8) for s in sizes)
     rd_avg_s = float(np.mean(rd_ms)) * 1e-3
     upd_avg_s = float(np.mean(upd_ms)) * 1e-3
     achieved = rd_bytes / rd_avg_s / 1e9
@@ -236,7 +241,9 @@ def main():
             "last_window_safe": bool(safe),
             "finite": finite,
             "roofline": {
-                "kernel": "k_res_readout (W_out GEMV, 17 waves x 8 rows per region)",
+                "kernel": ("k_res_readout<ml> (v_ml = W_out(:, ncs+1:) x~" if args.overlap else
+                           "k_res_readout<full> (W_out [local_model; x~] + unstandardize") +
+                          ", GEMV, 17 waves x 8 rows per region)",
                 "bound": "hbm",
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS,

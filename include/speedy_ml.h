@@ -49,6 +49,8 @@
  *                           geop, hordif, timint; dyn_grtend.f90, dyn_sptend.f90,
  *                           dyn_implic.f90, dyn_geop.f90)
  *   sml_dyn_leapfrog     <- the step(2,2,...) loop of stloop (src/dyn_stloop.f90:43)
+ *   sml_dyn_window       <- stepone + stloop of one agcm_main window (src/ini_stepone.f90,
+ *                           src/dyn_stloop.f90:37-56; run_model, src/mpires.f90:1605)
  *   sml_dyn_from_grid    <- iogrid(30) (src/ppo_iogrid.f90:497-571)
  *   sml_dyn_to_grid      <- iogrid(31) (src/ppo_iogrid.f90:573-595)
  */
@@ -152,6 +154,17 @@ int sml_res_get_state(sml_reservoirs *c, int i, double *x);
  *   d_outvec      [nlocal][nout] unstandardized outputs */
 int sml_res_step(sml_reservoirs *c, const double *d_feedback, const double *d_local_model, double *d_outvec,
                  void *stream);
+/* The same step in two halves, so the reservoir's share overlaps SPEEDY's window:
+ * outvec = W_out(:,1:ncs) local_model + W_out(:,ncs+1:) x~ is split at column ncs
+ * exactly as the reference's outvec_component_contribs (v_p + v_ml,
+ * src/mod_reservoir.f90:1456-1459).
+ *   begin:  x update from d_feedback, then v_ml into a context-owned buffer
+ *           (~98 % of the step's bytes; needs no SPEEDY output)
+ *   finish: v_p from d_local_model, outvec = v_p + v_ml, unstandardize
+ * sml_res_step == begin + finish on one stream.  Each begin needs one finish
+ * before the next begin (SML_ERR_STATE otherwise). */
+int sml_res_step_begin(sml_reservoirs *c, const double *d_feedback, void *stream);
+int sml_res_step_finish(sml_reservoirs *c, const double *d_local_model, double *d_outvec, void *stream);
 /* synchronize (src/mod_reservoir.f90:1352-1378), the spin-up of start_prediction
  * (:938-959): `length` updates x = (1-leak) x + leak tanh(A x + W_in u_t) for every
  * local region, no readout.  d_inputs holds `length` blocks in the packed feedback
@@ -184,6 +197,12 @@ int sml_exchange_assemble(sml_reservoirs *c, const double *d_outvec_all, double 
 int sml_res_tile_inputs(sml_reservoirs *c, const double *d_grid4d, const double *d_grid2d, const double *d_precip,
                         const double *d_fc4d, const double *d_fc2d, const double *d_tisr, double *d_feedback,
                         double *d_local_model, void *stream);
+/* the two halves of sml_res_tile_inputs: feedback needs only the assembled grids
+ * (ready before SPEEDY runs), local_model needs SPEEDY's forecast */
+int sml_res_tile_feedback(sml_reservoirs *c, const double *d_grid4d, const double *d_grid2d, const double *d_precip,
+                          const double *d_tisr, double *d_feedback, void *stream);
+int sml_res_tile_local_model(sml_reservoirs *c, const double *d_fc4d, const double *d_fc2d, double *d_local_model,
+                             void *stream);
 
 /* --------------------------------------------------------- NetCDF weight files */
 /* Reads worker_XXXX_level_1_<trial>.nc (NetCDF-3 classic / 64-bit offset) written
@@ -240,6 +259,15 @@ int sml_dyn_step(sml_dynamics *d, int j1, int j2, double dt, double alph, double
  * when (dt, alph, rob, wil, d_phys) change).  impint(dt, alph) must be current. */
 int sml_dyn_leapfrog(sml_dynamics *d, int nsteps, double dt, double alph, double rob, double wil,
                      const double *d_phys, void *stream);
+/* One SPEEDY window after iogrid(30), as run_model's agcm_main runs it
+ * (src/mpires.f90:1605 -> at_gcm.f90): stepone (src/ini_stepone.f90:19-34:
+ * step(1,1,delt/2), step(1,2,delt), with the lradsw the previous window left) and
+ * nleap x step(2,2,2 delt) with stloop's clock restarted at istep = 1
+ * (src/dyn_stloop.f90:37-56).  impint tables for delt/2, delt and 2 delt are built
+ * (cached) first; the whole window is one hipGraph launch.  GPU physics as set by
+ * sml_dyn_set_physics (no host tendencies).  Afterwards istep = 1 + nleap and
+ * impint(2 delt, alph) is current. */
+int sml_dyn_window(sml_dynamics *d, int nleap, double delt, double alph, double rob, double wil, void *stream);
 /* iogrid(30) (src/ppo_iogrid.f90:497-571), the window entry: variables3d
  * grid4d(4, ix, il, kx) (T, u, v, q) and logp(ix, il), device, are rounded to
  * real(4), q < 0 set to 0, transformed (vdspec / spec + trunct) into time level 1;

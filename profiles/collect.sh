@@ -10,7 +10,7 @@ OUT=$ROOT/gpurun_out/prof_$R
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd /tmp
-ARGS="$ROOT/bench.py --steps 20 --warmup 3 --no-cpu-baseline"
+ARGS="$ROOT/bench.py --steps 20 --warmup 3 --no-cpu-baseline --train-regions 0 --speedy-steps 8 --reservoir-steps 10"
 timeout -k 10 500 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o trace --output-format csv \
     -- python3 $ARGS > "$OUT/trace_bench.json" 2> "$OUT/trace_bench.err"
 timeout -k 10 500 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch" -o fetch --output-format csv \

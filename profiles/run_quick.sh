@@ -1,0 +1,11 @@
+# GPU tests + default bench (no profiling)
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests -m gpu -v -x --timeout 200 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1
+rc=$?; echo "pytest rc=$rc" >> gpurun_out/gpu_tests.log; tail -3 gpurun_out/gpu_tests.log
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 400 python -u bench.py ${BENCH_ARGS:-} > gpurun_out/bench.json 2> gpurun_out/bench.err || exit $?
+python3 -c "
+import json; d=json.loads(open('gpurun_out/bench.json').read().strip().splitlines()[-1])
+print('value', d['value'], 'ms', d['ms_per_step'], 'readout', d['roofline']['readout_avg_ms'], 'frac', d['roofline']['frac'], 'window', d['speedy_step']['window_ms_graph_physics'], 'res_only', d['reservoir_only']['ms_per_step'])"

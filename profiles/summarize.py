@@ -37,6 +37,11 @@ def _find(root, pattern):
 
 
 def _short(name: str) -> str:
+    if "k_res_readout" in name:  # <WT, mode>: mode 0 = v_ml half (step_begin), 1 = finish
+        wt = "float" if ("<float" in name or "IfL" in name) else "double"
+        mode = ("finish" if (", 1>" in name or "Li1E" in name) else
+                "full" if (", 2>" in name or "Li2E" in name) else "ml")
+        return f"k_res_readout_{mode}<{wt}>"
     for key in ("k_res_readout", "k_res_update", "k_tile_feedback", "k_tile_local_model", "k_assemble",
                 "k_gridy", "k_gridx", "k_specx", "k_specy", "k_vds", "k_uvspec"):
         if key in name:
@@ -86,7 +91,7 @@ def main():
         pass
     lines = [f"# rocprofv3 summary, round {rnd}", "",
              "Command: `rocprofv3 --kernel-trace --stats -- python3 bench.py --steps 20 --warmup 3 "
-             "--no-cpu-baseline` (1 x MI355X), then one `--pmc FETCH_SIZE` and one `--pmc WRITE_SIZE` pass "
+             "--no-cpu-baseline --train-regions 0 --speedy-steps 8 --reservoir-steps 10` (1 x MI355X), then one `--pmc FETCH_SIZE` and one `--pmc WRITE_SIZE` pass "
              f"of the same command.  Source commit: {commit or 'n/a'}.", "",
              "| kernel | calls | avg us | % time | FETCH_SIZE KiB/launch (raw) | WRITE_SIZE KiB/launch |",
              "|---|---|---|---|---|---|"]
@@ -96,7 +101,9 @@ def main():
     if bench:
         lines += ["", "bench line of the traced run (profiled clocks run lower, MI355X_MICROARCH.md "
                       "DVFS item 2):", "", "```", json.dumps(bench), "```"]
-    rd = [r for r in rows if r[0].startswith("k_res_readout")]
+    # the dominant readout launch: one-pass (full) by default, the v_ml half with --overlap
+    rd = sorted([r for r in rows if r[0].startswith(("k_res_readout_full", "k_res_readout_ml"))],
+                key=lambda r: -r[1] * r[2])
     if rd and rd[0][4] is not None and rd[0][5] is not None:
         name, calls, avg, _, fk, wk = rd[0]
         hbm = (2.0 * fk + wk) * 1024.0
@@ -106,7 +113,7 @@ def main():
         if bench:
             out["algorithmic_bytes_per_launch"] = bench.get("roofline", {}).get("algorithmic_bytes_per_launch")
         json.dump(out, open(os.path.join(HERE, "readout_pmc.json"), "w"), indent=1)
-        lines += ["", f"k_res_readout HBM traffic per launch (2 x FETCH + WRITE): {hbm / 1e9:.3f} GB"]
+        lines += ["", f"{name} HBM traffic per launch (2 x FETCH + WRITE): {hbm / 1e9:.3f} GB"]
     open(os.path.join(HERE, f"{rnd}_summary.md"), "w").write("\n".join(lines) + "\n")
     print("\n".join(lines))
 

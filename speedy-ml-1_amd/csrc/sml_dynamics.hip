@@ -105,6 +105,12 @@ struct sml_dynamics {
         const DynTables *tab = nullptr;
         bool phys_on = false;
     } replay[2];
+    // whole-window replay (sml_dyn_window): stepone + nleap leapfrog steps, one graph
+    struct WindowReplay {
+        hipGraphExec_t exec = nullptr;
+        double key[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        DynTables *tab[3] = {nullptr, nullptr, nullptr};
+    } wreplay[2];
 };
 
 namespace {
@@ -933,6 +939,8 @@ extern "C" int sml_dyn_destroy(sml_dynamics *d) {
         if (p) (void)hipFree(p);
     for (auto &r : d->replay)
         if (r.exec) (void)hipGraphExecDestroy(r.exec);
+    for (auto &r : d->wreplay)
+        if (r.exec) (void)hipGraphExecDestroy(r.exec);
     if (d->cap_stream) (void)hipStreamDestroy(d->cap_stream);
     if (d->sp) sml_spectral_destroy(d->sp);
     delete d;
@@ -1187,6 +1195,61 @@ extern "C" int sml_dyn_leapfrog(sml_dynamics *d, int nsteps, double dt, double a
         d->lradsw = lradsw;
         ++d->istep;
     }
+    return SML_OK;
+}
+
+// One SPEEDY window after iogrid(30): stepone (ini_stepone.f90:19-34: step(1, 1,
+// delt/2), step(1, 2, delt) with the lradsw the previous window left) and nleap x
+// step(2, 2, 2 delt) with stloop's radiation clock restarted at istep = 1
+// (dyn_stloop.f90:37-56, at_gcm.f90:81), captured once as ONE hipGraph per
+// (entry lradsw, delt, alph, rob, wil, physics on, impint slots) and replayed with
+// a single launch, so the host thread never waits on the window's ~200 kernels.
+extern "C" int sml_dyn_window(sml_dynamics *d, int nleap, double delt, double alph, double rob, double wil,
+                              void *stream) {
+    SML_REQUIRE(d && nleap >= 0 && delt > 0.0, "bad argument");
+    const double dts[3] = {0.5 * delt, delt, 2.0 * delt};
+    DynTables *tab[3];
+    for (int i = 0; i < 3; ++i) {  // 4 cached slots hold all three tables at once
+        if (int rc = sml_dyn_impint(d, dts[i], alph)) return rc;
+        tab[i] = d->d_tab;
+    }
+    const bool entry = d->lradsw;
+    sml_dynamics::WindowReplay &r = d->wreplay[entry ? 1 : 0];
+    const double key[8] = {(double)nleap, delt, alph, rob, wil, d->phys_on ? 1.0 : 0.0, d->fused ? 1.0 : 0.0, 1.0};
+    if (!(r.exec && std::memcmp(key, r.key, sizeof key) == 0 && std::memcmp(tab, r.tab, sizeof tab) == 0)) {
+        if (r.exec) {
+            SML_HIP(hipGraphExecDestroy(r.exec));
+            r.exec = nullptr;
+        }
+        if (!d->cap_stream) SML_HIP(hipStreamCreateWithFlags(&d->cap_stream, hipStreamNonBlocking));
+        hipGraph_t g = nullptr;
+        SML_HIP(hipStreamBeginCapture(d->cap_stream, hipStreamCaptureModeThreadLocal));
+        d->d_tab = tab[0];
+        int rc = launch_step(d, 1, 1, dts[0], alph, rob, wil, nullptr, entry, d->cap_stream);
+        d->d_tab = tab[1];
+        if (!rc) rc = launch_step(d, 1, 2, dts[1], alph, rob, wil, nullptr, entry, d->cap_stream);
+        d->d_tab = tab[2];
+        for (int i = 0; i < nleap && !rc; ++i)
+            rc = launch_step(d, 2, 2, dts[2], alph, rob, wil, nullptr, (1 + i) % kNstrad == 1, d->cap_stream);
+        hipError_t e = hipStreamEndCapture(d->cap_stream, &g);
+        if (rc) {
+            if (g) (void)hipGraphDestroy(g);
+            return rc;
+        }
+        if (e != hipSuccess) return fail(SML_ERR_HIP, "sml_dyn_window capture: %s", hipGetErrorString(e));
+        e = hipGraphInstantiate(&r.exec, g, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(g);
+        if (e != hipSuccess) {
+            r.exec = nullptr;
+            return fail(SML_ERR_HIP, "sml_dyn_window instantiate: %s", hipGetErrorString(e));
+        }
+        std::memcpy(r.key, key, sizeof key);
+        std::memcpy(r.tab, tab, sizeof tab);
+    }
+    SML_HIP(hipGraphLaunch(r.exec, (hipStream_t)stream));
+    d->d_tab = tab[2];
+    d->istep = 1 + nleap;
+    if (nleap > 0) d->lradsw = (nleap % kNstrad == 1);
     return SML_OK;
 }
 

@@ -77,6 +77,8 @@ struct sml_reservoirs {
     double *d_x[2] = {nullptr, nullptr};
     int cur = 0;
     double *d_xaug = nullptr, *d_meanstd = nullptr;
+    double *d_part = nullptr;       // [nlocal][nout_pad] W_out(:, ncs+1:) x~ of the step in flight
+    bool begun = false;             // sml_res_step_begin issued, finish pending
     int8_t *d_outl = nullptr;
     int32_t *d_asm_dst = nullptr;   // [numregions*nout] -> concatenated grid index
     int32_t *d_fb_src = nullptr;    // [tot_fb]
@@ -166,7 +168,7 @@ __global__ __launch_bounds__(kUpdThreads) void k_res_update(
     const RegionDev *__restrict__ R, const int32_t *__restrict__ a_rp, const uint16_t *__restrict__ a_col,
     const WT *__restrict__ a_val, const int32_t *__restrict__ w_rp, const uint16_t *__restrict__ w_col,
     const WT *__restrict__ w_val, Ell ell, const double *__restrict__ x_old, double *__restrict__ x_new,
-    double *__restrict__ xaug, const double *__restrict__ feedback, const double *__restrict__ local_model, int ncs,
+    double *__restrict__ xaug, const double *__restrict__ feedback, int ncs,
     double leak, int parts, int lds_x) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const int lb = xcd_remap(blockIdx.x, gridDim.x);
@@ -178,8 +180,6 @@ __global__ __launch_bounds__(kUpdThreads) void k_res_update(
     if (beg >= end) return;  // block-uniform
     RowRegs<WT> cur, nxt;
     load_row(cur, rg, ell, beg + tid, beg + tid < end);
-    if (part == 0 && local_model)
-        for (int cc = tid; cc < ncs; cc += kUpdThreads) xaug[rg.xaug + cc] = local_model[(size_t)r * ncs + cc];
     const double *xo = x_old + rg.x;
     const double *fb = feedback + rg.fb;
     const double *xs = xo, *fs = fb;
@@ -241,28 +241,33 @@ struct Vec4<double> {
 
 // readout: one wave per (region, 8-row group) item, 4 waves per block; blocks are
 // remapped so that the items of one region stay on one XCD's L2 (x_aug reuse).
-template <typename WT>
-__global__ __launch_bounds__(256) void k_res_readout(const RegionDev *__restrict__ R, const WT *__restrict__ wout,
-                                                     const double *__restrict__ xaug,
-                                                     const double *__restrict__ meanstd,
-                                                     const int8_t *__restrict__ outl, double *__restrict__ outvec,
-                                                     int nout, int groups, int nitems) {
-    const int bs = xcd_remap(blockIdx.x, gridDim.x);
-    const int lane = threadIdx.x & 63;
-    const int item = bs * 4 + (threadIdx.x >> 6);
-    if (item >= nitems) return;
-    const int r = item / groups, g = item % groups;
-    const RegionDev rg = R[r];
-    const int ld = rg.ld;
-    const WT *W = wout + rg.wout + (size_t)(g * kRows) * ld;
-    const double *xa = xaug + rg.xaug;
+// The product W_out [local_model; x~] is split at column ncs as the reference's
+// outvec_component_contribs does (v_p + v_ml, mod_reservoir.f90:1456-1459):
+//   kReadML:     part = v_ml = W_out(:, ncs+1:) x~     (needs only this step's feedback)
+//   kReadFinish: v = v_p + part, v_p = W_out(:, 1:ncs) local_model, unstandardize
+//   kReadFull:   v = v_p + v_ml in one pass (sml_res_step)
+// Every mode forms v_ml and v_p with the same per-lane partial sums and the same
+// butterfly, so the split step and the one-pass step agree bit for bit; the split
+// lets the ML part -- ~98 % of the bytes -- run before SPEEDY's local_model exists.
+enum ReadMode { kReadML = 0, kReadFinish = 1, kReadFull = 2 };
+
+// dot products of the wave's 8 W_out rows with x over columns [c0, c1) (16-B groups;
+// lanes own columns c0 + 4 lane + 256 t), reduced across the wave; x values outside
+// [x0, x1) are zero (fma(w, 0, s) == s), which matters only when ncs % 4 != 0
+struct Rows {
+    double v[kRows];
+};
+
+template <typename WT, typename XF>
+__device__ __attribute__((always_inline)) inline Rows rows_dot(const WT *W, int ld, int lane, int c0, int c1,
+                                                               XF xload) {
     typedef typename Vec4<WT>::T V;
     double acc[kRows];
 #pragma unroll
     for (int q = 0; q < kRows; ++q) acc[q] = 0.0;
 #pragma unroll 2
-    for (int j = lane * 4; j < ld; j += 256) {
-        const double4 xv = *reinterpret_cast<const double4 *>(xa + j);
+    for (int j = c0 + lane * 4; j < c1; j += 256) {
+        const double4 xv = xload(j);
         V w[kRows];
 #pragma unroll
         for (int q = 0; q < kRows; ++q) w[q] = *reinterpret_cast<const V *>(W + (size_t)q * ld + j);
@@ -280,19 +285,75 @@ __global__ __launch_bounds__(256) void k_res_readout(const RegionDev *__restrict
     for (int off = 32; off >= 1; off >>= 1)
 #pragma unroll
         for (int q = 0; q < kRows; ++q) acc[q] += __shfl_xor(acc[q], off, 64);
-    if (lane < kRows) {
-        const int o = g * kRows + lane;
-        double v = acc[0];
+    Rows out;
 #pragma unroll
-        for (int q = 1; q < kRows; ++q)
-            if (lane == q) v = acc[q];
-        if (o < nout) {
-            const int l = outl[o];
-            if (l >= 0) {  // unstandardize_state_vec_res: x*std + mean (two roundings)
-                const double t = v * meanstd[(size_t)r * 2 * kMeanStd + kMeanStd + l];
-                v = t + meanstd[(size_t)r * 2 * kMeanStd + l];
+    for (int q = 0; q < kRows; ++q) out.v[q] = acc[q];
+    return out;
+}
+
+template <typename WT, int kMode>
+__global__ __launch_bounds__(256) void k_res_readout(const RegionDev *__restrict__ R, const WT *__restrict__ wout,
+                                                     const double *__restrict__ xaug,
+                                                     const double *__restrict__ local_model,
+                                                     const double *__restrict__ meanstd,
+                                                     const int8_t *__restrict__ outl, double *__restrict__ part,
+                                                     double *__restrict__ outvec, int nout, int nout_pad, int ncs,
+                                                     int groups, int nitems) {
+    const int bs = xcd_remap(blockIdx.x, gridDim.x);
+    const int lane = threadIdx.x & 63;
+    const int item = bs * 4 + (threadIdx.x >> 6);
+    if (item >= nitems) return;
+    const int r = item / groups, g = item % groups;
+    const RegionDev rg = R[r];
+    const int ld = rg.ld;
+    const WT *W = wout + rg.wout + (size_t)(g * kRows) * ld;
+    Rows ml{}, lmv{};
+    if (kMode != kReadFinish) {  // v_ml: x~ from x_aug, columns ncs .. ld
+        const double *xa = xaug + rg.xaug;
+        ml = rows_dot<WT>(W, ld, lane, ncs & ~3, ld, [=](int j) {
+            double4 xv = *reinterpret_cast<const double4 *>(xa + j);
+            if (j < ncs) {  // the group that straddles column ncs
+                if (j + 0 < ncs) xv.x = 0.0;
+                if (j + 1 < ncs) xv.y = 0.0;
+                if (j + 2 < ncs) xv.z = 0.0;
+                if (j + 3 < ncs) xv.w = 0.0;
             }
-            outvec[(size_t)r * nout + o] = v;
+            return xv;
+        });
+    }
+    if (kMode != kReadML) {  // v_p: x_augment(1:chunk_size_speedy) = local_model (:1451), read in place
+        const double *lm = local_model + (size_t)r * ncs;
+        lmv = rows_dot<WT>(W, ld, lane, 0, (ncs + 3) & ~3, [=](int j) {
+            double4 xv;
+            xv.x = j + 0 < ncs ? lm[j + 0] : 0.0;
+            xv.y = j + 1 < ncs ? lm[j + 1] : 0.0;
+            xv.z = j + 2 < ncs ? lm[j + 2] : 0.0;
+            xv.w = j + 3 < ncs ? lm[j + 3] : 0.0;
+            return xv;
+        });
+    }
+    // every lane holds all 8 sums after the butterfly; lane 0 writes the group's rows
+    // (static indices only: a lane-indexed pick would put the sums in scratch)
+    if (lane == 0) {
+        const int o0 = g * kRows;
+        if (kMode == kReadML) {
+#pragma unroll
+            for (int q = 0; q < kRows; ++q) part[(size_t)r * nout_pad + o0 + q] = ml.v[q];
+        } else {
+            const double *ms = meanstd + (size_t)r * 2 * kMeanStd;
+#pragma unroll
+            for (int q = 0; q < kRows; ++q) {
+                const int o = o0 + q;
+                if (o >= nout) break;
+                const double vml = kMode == kReadFull ? ml.v[q] : part[(size_t)r * nout_pad + o];
+                double v = lmv.v[q] + vml;
+                const int l = outl[o];
+                if (l >= 0) {  // unstandardize_state_vec_res: x*std + mean (two roundings)
+                    const double t = v * ms[kMeanStd + l];
+                    v = t + ms[l];
+                }
+                outvec[(size_t)r * nout + o] = v;
+            }
         }
     }
 }
@@ -613,7 +674,7 @@ extern "C" int sml_res_destroy(sml_reservoirs *c) {
         if (p) (void)hipFree(p);
     void *ptrs[] = {c->d_rd,    c->d_a_rp,    c->d_w_rp,   c->d_a_col,  c->d_w_col,  c->d_a_val,  c->d_w_val,
                     c->d_wout,  c->d_x[0],    c->d_x[1],   c->d_xaug,   c->d_meanstd, c->d_outl,  c->d_asm_dst,
-                    c->d_fb_src, c->d_fb_l,   c->d_fb_reg, c->d_lm_src, c->d_lm_l,   c->d_io};
+                    c->d_fb_src, c->d_fb_l,   c->d_fb_reg, c->d_lm_src, c->d_lm_l,   c->d_io,     c->d_part};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     for (hipEvent_t e : c->ev)
@@ -717,7 +778,8 @@ extern "C" int sml_res_create(int numregions, int nlocal, const int *region_ids,
         (rc = dalloc(&c->d_w_rp, c->tot_w_rp)) || (rc = dalloc(&c->d_w_col, c->tot_w_nz)) ||
         (rc = dalloc_bytes(&c->d_w_val, c->tot_w_nz * wb)) || (rc = dalloc_bytes(&c->d_wout, c->tot_wout * wb)) ||
         (rc = dalloc(&c->d_x[0], c->tot_x)) || (rc = dalloc(&c->d_x[1], c->tot_x)) ||
-        (rc = dalloc(&c->d_xaug, c->tot_xaug)) || (rc = dalloc(&c->d_meanstd, (size_t)nlocal * 2 * kMeanStd))) {
+        (rc = dalloc(&c->d_xaug, c->tot_xaug)) || (rc = dalloc(&c->d_meanstd, (size_t)nlocal * 2 * kMeanStd)) ||
+        (rc = dalloc(&c->d_part, (size_t)std::max(nlocal, 1) * c->nout_pad))) {
         sml_res_destroy(c);
         return rc;
     }
@@ -833,8 +895,7 @@ extern "C" int sml_res_kernel_times(sml_reservoirs *c, float *update_ms, float *
 
 namespace {
 // x_new = (1 - leak) x + leak tanh(A x + W_in u) for every local region (+ x~, x_aug)
-int launch_update(sml_reservoirs *c, const double *xo, double *xn, const double *d_feedback, const double *lmp,
-                  hipStream_t st) {
+int launch_update(sml_reservoirs *c, const double *xo, double *xn, const double *d_feedback, hipStream_t st) {
     // parts per region: enough blocks for ~4 rounds of the 512 resident 1024-thread
     // blocks (2 per CU with ~54 KB LDS each), each part at least one 1024-row pass
     const int max_parts = std::max(1, (c->maxn + kUpdThreads - 1) / kUpdThreads);
@@ -847,7 +908,7 @@ int launch_update(sml_reservoirs *c, const double *xo, double *xn, const double 
 #define SML_UPD(WT, L)                                                                                            \
     hipLaunchKernelGGL((k_res_update<WT, L>), ug, dim3(kUpdThreads), L ? lds : 0, st, c->d_rd, c->d_a_rp,          \
                        c->d_a_col, (const WT *)c->d_a_val, c->d_w_rp, c->d_w_col, (const WT *)c->d_w_val, ell,    \
-                       xo, xn, c->d_xaug, d_feedback, lmp, c->ncs, c->leakage, bpr, lds_x)
+                       xo, xn, c->d_xaug, d_feedback, c->ncs, c->leakage, bpr, lds_x)
     Ell ell{c->d_a_ell_col, c->d_a_ell_val, c->d_w_ell_col, c->d_w_ell_val};
     if (c->wdtype == SML_F32) {
         if (use_lds)
@@ -862,10 +923,68 @@ int launch_update(sml_reservoirs *c, const double *xo, double *xn, const double 
     }
 #undef SML_UPD
     SML_HIP(hipGetLastError());
-    SML_HIP(hipGetLastError());
     return SML_OK;
 }
+
+int check_loaded(const sml_reservoirs *c) {
+    for (int i = 0; i < c->nlocal; ++i)
+        if (!c->loaded[i]) return fail(SML_ERR_STATE, "local region %d has no weights loaded", i);
+    return SML_OK;
+}
+
+template <int kMode>
+void launch_readout(sml_reservoirs *c, const double *d_local_model, double *d_outvec, hipStream_t st) {
+    const int groups = c->nout_pad / kRows;
+    const int nitems = c->nlocal * groups;
+    const int nblocks = (nitems + 3) / 4;
+    if (c->wdtype == SML_F32)
+        hipLaunchKernelGGL((k_res_readout<float, kMode>), dim3(nblocks), dim3(256), 0, st, c->d_rd,
+                           (const float *)c->d_wout, c->d_xaug, d_local_model, c->d_meanstd, c->d_outl, c->d_part, d_outvec, c->nout,
+                           c->nout_pad, c->ncs, groups, nitems);
+    else
+        hipLaunchKernelGGL((k_res_readout<double, kMode>), dim3(nblocks), dim3(256), 0, st, c->d_rd,
+                           (const double *)c->d_wout, c->d_xaug, d_local_model, c->d_meanstd, c->d_outl, c->d_part, d_outvec, c->nout,
+                           c->nout_pad, c->ncs, groups, nitems);
+}
 }  // namespace
+
+extern "C" int sml_res_step_begin(sml_reservoirs *c, const double *d_feedback, void *stream) {
+    SML_REQUIRE(c, "null context");
+    if (c->nlocal == 0) return SML_OK;
+    SML_REQUIRE(d_feedback, "null device buffer");
+    if (c->begun) return fail(SML_ERR_STATE, "sml_res_step_begin called twice without sml_res_step_finish");
+    if (int rc = check_loaded(c)) return rc;
+    hipStream_t st = (hipStream_t)stream;
+    const double *xo = c->d_x[c->cur];
+    double *xn = c->d_x[1 - c->cur];
+    const bool rec = c->timing && c->ev_used < c->ev_cap;
+    hipEvent_t *ev = rec ? &c->ev[3 * c->ev_used] : nullptr;
+    if (rec) SML_HIP(hipEventRecord(ev[0], st));
+    if (int rc = launch_update(c, xo, xn, d_feedback, st)) return rc;
+    if (rec) SML_HIP(hipEventRecord(ev[1], st));
+    launch_readout<kReadML>(c, nullptr, nullptr, st);
+    SML_HIP(hipGetLastError());
+    if (rec) {
+        SML_HIP(hipEventRecord(ev[2], st));
+        ++c->ev_used;
+    }
+    c->cur = 1 - c->cur;
+    c->begun = true;
+    return SML_OK;
+}
+
+extern "C" int sml_res_step_finish(sml_reservoirs *c, const double *d_local_model, double *d_outvec, void *stream) {
+    SML_REQUIRE(c, "null context");
+    if (c->nlocal == 0) return SML_OK;
+    SML_REQUIRE(d_outvec, "null device buffer");
+    SML_REQUIRE(c->ncs == 0 || d_local_model, "hybrid context needs d_local_model");
+    if (!c->begun) return fail(SML_ERR_STATE, "sml_res_step_finish without sml_res_step_begin");
+    hipStream_t st = (hipStream_t)stream;
+    launch_readout<kReadFinish>(c, d_local_model, d_outvec, st);
+    SML_HIP(hipGetLastError());
+    c->begun = false;
+    return SML_OK;
+}
 
 extern "C" int sml_res_step(sml_reservoirs *c, const double *d_feedback, const double *d_local_model,
                             double *d_outvec, void *stream) {
@@ -873,27 +992,15 @@ extern "C" int sml_res_step(sml_reservoirs *c, const double *d_feedback, const d
     if (c->nlocal == 0) return SML_OK;
     SML_REQUIRE(d_feedback && d_outvec, "null device buffer");
     SML_REQUIRE(c->ncs == 0 || d_local_model, "hybrid context needs d_local_model");
-    for (int i = 0; i < c->nlocal; ++i)
-        if (!c->loaded[i]) return fail(SML_ERR_STATE, "local region %d has no weights loaded", i);
+    if (c->begun) return fail(SML_ERR_STATE, "sml_res_step inside a begun step");
+    if (int rc = check_loaded(c)) return rc;
     hipStream_t st = (hipStream_t)stream;
-    const double *xo = c->d_x[c->cur];
-    double *xn = c->d_x[1 - c->cur];
     const bool rec = c->timing && c->ev_used < c->ev_cap;
     hipEvent_t *ev = rec ? &c->ev[3 * c->ev_used] : nullptr;
     if (rec) SML_HIP(hipEventRecord(ev[0], st));
-    const double *lmp = c->ncs ? d_local_model : nullptr;
-    if (int rc = launch_update(c, xo, xn, d_feedback, lmp, st)) return rc;
+    if (int rc = launch_update(c, c->d_x[c->cur], c->d_x[1 - c->cur], d_feedback, st)) return rc;
     if (rec) SML_HIP(hipEventRecord(ev[1], st));
-    const int groups = c->nout_pad / kRows;
-    const int nitems = c->nlocal * groups;
-    const int nblocks = (nitems + 3) / 4;
-    if (c->wdtype == SML_F32)
-        hipLaunchKernelGGL(k_res_readout<float>, dim3(nblocks), dim3(256), 0, st, c->d_rd, (const float *)c->d_wout,
-                           c->d_xaug, c->d_meanstd, c->d_outl, d_outvec, c->nout, groups, nitems);
-    else
-        hipLaunchKernelGGL(k_res_readout<double>, dim3(nblocks), dim3(256), 0, st, c->d_rd,
-                           (const double *)c->d_wout, c->d_xaug, c->d_meanstd, c->d_outl, d_outvec, c->nout, groups,
-                           nitems);
+    launch_readout<kReadFull>(c, d_local_model, d_outvec, st);
     SML_HIP(hipGetLastError());
     if (rec) {
         SML_HIP(hipEventRecord(ev[2], st));
@@ -912,11 +1019,12 @@ extern "C" int sml_res_synchronize(sml_reservoirs *c, const double *d_inputs, in
     SML_REQUIRE(c && length >= 0, "bad argument");
     if (c->nlocal == 0 || length == 0) return SML_OK;
     SML_REQUIRE(d_inputs && stride >= (int64_t)c->tot_fb, "stride smaller than the packed feedback size");
+    if (c->begun) return fail(SML_ERR_STATE, "sml_res_synchronize inside a begun step");
     for (int i = 0; i < c->nlocal; ++i)
         if (!c->loaded[i]) return fail(SML_ERR_STATE, "local region %d has no weights loaded", i);
     hipStream_t st = (hipStream_t)stream;
     for (int t = 0; t < length; ++t) {
-        if (int rc = launch_update(c, c->d_x[c->cur], c->d_x[1 - c->cur], d_inputs + (size_t)t * stride, nullptr, st))
+        if (int rc = launch_update(c, c->d_x[c->cur], c->d_x[1 - c->cur], d_inputs + (size_t)t * stride, st))
             return rc;
         c->cur = 1 - c->cur;
     }
@@ -966,23 +1074,35 @@ extern "C" int sml_exchange_assemble(sml_reservoirs *c, const double *d_outvec_a
     return SML_OK;
 }
 
+extern "C" int sml_res_tile_feedback(sml_reservoirs *c, const double *d_grid4d, const double *d_grid2d,
+                                     const double *d_precip, const double *d_tisr, double *d_feedback, void *stream) {
+    SML_REQUIRE(c && d_grid4d && d_grid2d && d_precip && d_feedback, "null argument");
+    if (c->tot_fb) {
+        const int total = (int)c->tot_fb;
+        hipLaunchKernelGGL(k_tile_feedback, dim3((total + 255) / 256), dim3(256), 0, (hipStream_t)stream, c->d_fb_src,
+                           c->d_fb_l, c->d_fb_reg, c->d_meanstd, d_grid4d, d_grid2d, d_precip, d_tisr, d_feedback,
+                           total);
+        SML_HIP(hipGetLastError());
+    }
+    return SML_OK;
+}
+
+extern "C" int sml_res_tile_local_model(sml_reservoirs *c, const double *d_fc4d, const double *d_fc2d,
+                                        double *d_local_model, void *stream) {
+    SML_REQUIRE(c && d_fc4d && d_fc2d && d_local_model, "null argument");
+    if (c->ncs && c->nlocal) {
+        const int total = c->nlocal * c->ncs;
+        hipLaunchKernelGGL(k_tile_local_model, dim3((total + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                           c->d_lm_src, c->d_lm_l, c->d_meanstd, d_fc4d, d_fc2d, d_local_model, c->ncs, total);
+        SML_HIP(hipGetLastError());
+    }
+    return SML_OK;
+}
+
 extern "C" int sml_res_tile_inputs(sml_reservoirs *c, const double *d_grid4d, const double *d_grid2d,
                                    const double *d_precip, const double *d_fc4d, const double *d_fc2d,
                                    const double *d_tisr, double *d_feedback, double *d_local_model, void *stream) {
-    SML_REQUIRE(c && d_grid4d && d_grid2d && d_precip && d_feedback, "null argument");
-    hipStream_t st = (hipStream_t)stream;
-    if (c->tot_fb) {
-        const int total = (int)c->tot_fb;
-        hipLaunchKernelGGL(k_tile_feedback, dim3((total + 255) / 256), dim3(256), 0, st, c->d_fb_src, c->d_fb_l,
-                           c->d_fb_reg, c->d_meanstd, d_grid4d, d_grid2d, d_precip, d_tisr, d_feedback, total);
-        SML_HIP(hipGetLastError());
-    }
-    if (c->ncs && d_fc4d && c->nlocal) {
-        SML_REQUIRE(d_fc2d && d_local_model, "forecast grids need d_fc2d and d_local_model");
-        const int total = c->nlocal * c->ncs;
-        hipLaunchKernelGGL(k_tile_local_model, dim3((total + 255) / 256), dim3(256), 0, st, c->d_lm_src, c->d_lm_l,
-                           c->d_meanstd, d_fc4d, d_fc2d, d_local_model, c->ncs, total);
-        SML_HIP(hipGetLastError());
-    }
+    if (int rc = sml_res_tile_feedback(c, d_grid4d, d_grid2d, d_precip, d_tisr, d_feedback, stream)) return rc;
+    if (c->ncs && d_fc4d && c->nlocal) return sml_res_tile_local_model(c, d_fc4d, d_fc2d, d_local_model, stream);
     return SML_OK;
 }

@@ -149,6 +149,19 @@ module sml_hip
       integer(c_int) :: rc
     end function
 
+    ! predict split at column chunk_size_speedy (v_ml + v_p, mod_reservoir.f90:1456-1459)
+    function sml_res_step_begin(ctx, d_feedback, stream) bind(C, name='sml_res_step_begin') result(rc)
+      import :: c_ptr, c_int
+      type(c_ptr), value :: ctx, d_feedback, stream
+      integer(c_int) :: rc
+    end function
+
+    function sml_res_step_finish(ctx, d_local_model, d_outvec, stream) bind(C, name='sml_res_step_finish') result(rc)
+      import :: c_ptr, c_int
+      type(c_ptr), value :: ctx, d_local_model, d_outvec, stream
+      integer(c_int) :: rc
+    end function
+
     ! ------------------------------------------------------------ NetCDF weight files
     function sml_nc_read_region(path, dims, win, wout, rows, cols, vals, mean, std) &
         bind(C, name='sml_nc_read_region') result(rc)
@@ -201,6 +214,15 @@ module sml_hip
     end function
     !> step(j1, j2, dt, alph, rob, wil) with host physics tendencies
     !> phys(ix*il, kx, 4) = (utend, vtend, ttend, qtend) of phypar
+    ! one agcm_main window: stepone + nleap leapfrog steps as one hipGraph launch
+    function sml_dyn_window(ctx, nleap, delt, alph, rob, wil, stream) bind(C, name='sml_dyn_window') result(rc)
+      import :: c_ptr, c_int, c_double
+      type(c_ptr), value :: ctx, stream
+      integer(c_int), value :: nleap
+      real(c_double), value :: delt, alph, rob, wil
+      integer(c_int) :: rc
+    end function
+
     function sml_dyn_step_host(ctx, j1, j2, dt, alph, rob, wil, phys) bind(C, name='sml_dyn_step_host') result(rc)
       import :: c_ptr, c_int, c_double
       type(c_ptr), value :: ctx

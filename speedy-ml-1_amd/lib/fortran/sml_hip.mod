@@ -1,4 +1,4 @@
-﻿!mod$ v1 sum:9234fad67527d1cc
+﻿!mod$ v1 sum:57c4611cc5073336
 !need$ 0bde2ac47243ead2 i iso_c_binding
 module sml_hip
 use,intrinsic::iso_c_binding,only:c_associated
@@ -262,6 +262,25 @@ integer(4)::rc
 end
 end interface
 interface
+function sml_res_step_begin(ctx,d_feedback,stream) bind(c,name="sml_res_step_begin") result(rc)
+import::c_ptr
+type(c_ptr),value::ctx
+type(c_ptr),value::d_feedback
+type(c_ptr),value::stream
+integer(4)::rc
+end
+end interface
+interface
+function sml_res_step_finish(ctx,d_local_model,d_outvec,stream) bind(c,name="sml_res_step_finish") result(rc)
+import::c_ptr
+type(c_ptr),value::ctx
+type(c_ptr),value::d_local_model
+type(c_ptr),value::d_outvec
+type(c_ptr),value::stream
+integer(4)::rc
+end
+end interface
+interface
 function sml_nc_read_region(path,dims,win,wout,rows,cols,vals,mean,std) bind(c,name="sml_nc_read_region") result(rc)
 import::c_ptr
 character(1_8,1),intent(in)::path(1_8:*)
@@ -331,6 +350,19 @@ complex(8),intent(out)::div(1_8:*)
 complex(8),intent(out)::t(1_8:*)
 complex(8),intent(out)::ps(1_8:*)
 complex(8),intent(out)::tr(1_8:*)
+integer(4)::rc
+end
+end interface
+interface
+function sml_dyn_window(ctx,nleap,delt,alph,rob,wil,stream) bind(c,name="sml_dyn_window") result(rc)
+import::c_ptr
+type(c_ptr),value::ctx
+integer(4),value::nleap
+real(8),value::delt
+real(8),value::alph
+real(8),value::rob
+real(8),value::wil
+type(c_ptr),value::stream
 integer(4)::rc
 end
 end interface

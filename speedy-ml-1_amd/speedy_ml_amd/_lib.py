@@ -27,12 +27,13 @@ EXPORTED = (
     "sml_grid_host", "sml_spec_host",
     "sml_res_create", "sml_res_destroy", "sml_res_ninp", "sml_res_feedback_offsets",
     "sml_res_load_region_f32", "sml_res_load_region_f64", "sml_res_set_state", "sml_res_get_state",
-    "sml_res_step", "sml_res_step_host", "sml_res_synchronize", "sml_res_footprint", "sml_res_enable_timing",
-    "sml_res_kernel_times", "sml_exchange_assemble", "sml_res_tile_inputs",
+    "sml_res_step", "sml_res_step_begin", "sml_res_step_finish", "sml_res_step_host", "sml_res_synchronize",
+    "sml_res_footprint", "sml_res_enable_timing", "sml_res_kernel_times", "sml_exchange_assemble",
+    "sml_res_tile_inputs", "sml_res_tile_feedback", "sml_res_tile_local_model",
     "sml_nc_read_region", "sml_nc_write_region",
     "sml_dyn_create", "sml_dyn_destroy", "sml_dyn_impint", "sml_dyn_set_forcing", "sml_dyn_set_state",
     "sml_dyn_get_state", "sml_dyn_get_phi", "sml_dyn_get_tendencies", "sml_dyn_state_device",
-    "sml_dyn_step", "sml_dyn_step_host", "sml_dyn_leapfrog", "sml_dyn_from_grid", "sml_dyn_to_grid",
+    "sml_dyn_step", "sml_dyn_step_host", "sml_dyn_leapfrog", "sml_dyn_window", "sml_dyn_from_grid", "sml_dyn_to_grid",
     "sml_dyn_is_safe", "sml_dyn_from_grid_host", "sml_dyn_to_grid_host",
     "sml_dyn_set_physics", "sml_dyn_set_clock", "sml_dyn_get_clock", "sml_dyn_set_rad_state",
     "sml_dyn_get_rad_state", "sml_dyn_phypar", "sml_dyn_phypar_host", "sml_dyn_sol_oz", "sml_phys_sflset",
@@ -101,6 +102,8 @@ def _declare(L: ctypes.CDLL) -> None:
         "sml_res_set_state": [vp, i, vp],
         "sml_res_get_state": [vp, i, vp],
         "sml_res_step": [vp, vp, vp, vp, vp],
+        "sml_res_step_begin": [vp, vp, vp],
+        "sml_res_step_finish": [vp, vp, vp, vp],
         "sml_res_step_host": [vp, vp, vp, vp],
         "sml_res_synchronize": [vp, vp, i, ctypes.c_int64, vp],
         "sml_res_footprint": [vp, i64p, i64p],
@@ -108,6 +111,8 @@ def _declare(L: ctypes.CDLL) -> None:
         "sml_res_kernel_times": [vp, vp, vp, i, ctypes.POINTER(ctypes.c_int)],
         "sml_exchange_assemble": [vp, vp, vp, vp, vp, vp],
         "sml_res_tile_inputs": [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp],
+        "sml_res_tile_feedback": [vp, vp, vp, vp, vp, vp, vp],
+        "sml_res_tile_local_model": [vp, vp, vp, vp, vp],
         "sml_nc_read_region": [ctypes.c_char_p, vp, vp, vp, vp, vp, vp, vp, vp],
         "sml_nc_write_region": [ctypes.c_char_p, i, i, i, i, i, vp, vp, vp, vp, vp, vp, vp],
         "sml_dyn_create": [d, pp],
@@ -122,6 +127,7 @@ def _declare(L: ctypes.CDLL) -> None:
         "sml_dyn_step": [vp, i, i, d, d, d, d, vp, vp],
         "sml_dyn_step_host": [vp, i, i, d, d, d, d, vp],
         "sml_dyn_leapfrog": [vp, i, d, d, d, d, vp, vp],
+        "sml_dyn_window": [vp, i, d, d, d, d, vp],
         "sml_dyn_from_grid": [vp, vp, vp, vp, vp],
         "sml_dyn_to_grid": [vp, vp, vp, vp],
         "sml_dyn_is_safe": [vp],

@@ -173,7 +173,7 @@ class Dynamics:
             raise ValueError("phys must be a contiguous float64 CUDA tensor (4, 8, 48, 96)")
         check(lib().sml_dyn_step(self._h, j1, j2, dt, alph, rob, wil, ptr(phys), stream_ptr(stream)))
 
-    def from_grid(self, grid4d, logp):
+    def from_grid(self, grid4d, logp, stream=None):
         """iogrid(30) (ppo_iogrid.f90:497-571): window entry from variables3d
         (4, 96, 48, 8) Fortran order == C (8, 48, 96, 4), and logp (48, 96).
         Host numpy -> synchronous, returns (minmax[8], is_safe); device tensors ->
@@ -187,14 +187,14 @@ class Dynamics:
             safe = ctypes.c_int(0)
             check(lib().sml_dyn_from_grid_host(self._h, ptr(g), ptr(lp), ptr(mm), ctypes.byref(safe)))
             return mm, bool(safe.value)
-        check(lib().sml_dyn_from_grid(self._h, ptr(grid4d), ptr(logp), None, None))
+        check(lib().sml_dyn_from_grid(self._h, ptr(grid4d), ptr(logp), None, stream_ptr(stream)))
         return None
 
-    def to_grid(self, grid4d=None, logp=None):
+    def to_grid(self, grid4d=None, logp=None, stream=None):
         """iogrid(31) (ppo_iogrid.f90:573-595): level 1 -> (grid4d, logp).  With
         device tensors given, fills them asynchronously; else returns host arrays."""
         if grid4d is not None:
-            check(lib().sml_dyn_to_grid(self._h, ptr(grid4d), ptr(logp), None))
+            check(lib().sml_dyn_to_grid(self._h, ptr(grid4d), ptr(logp), stream_ptr(stream)))
             return grid4d, logp
         g = np.zeros((KX, 48, 96, 4))
         lp = np.zeros((48, 96))
@@ -212,10 +212,14 @@ class Dynamics:
         (dyn_stloop.f90:37-59 with window_size 4), asynchronous.  With the GPU
         physics on, stepone uses the lradsw the previous window left (the module
         flag persists) and stloop restarts at istep = 1 (at_gcm.f90:81, jday = 1)."""
+        if graph:  # the whole window as one captured hipGraph (sml_dyn_window)
+            check(lib().sml_dyn_window(self._h, nleap, delt, alph, ROB, WIL, stream_ptr(stream)))
+            self._dtal = (2 * delt, alph)
+            return
         self.stepone(delt, alph, stream=stream)
         _, lradsw = self.get_clock()
         self.set_clock(1, lradsw)
-        self.leapfrog(nleap, delt, alph, stream=stream, graph=graph)
+        self.leapfrog(nleap, delt, alph, stream=stream, graph=False)
 
     def leapfrog(self, nsteps: int, delt: float = DELT, alph: float = ALPH, phys=None, stream=None,
                  graph: bool = True):

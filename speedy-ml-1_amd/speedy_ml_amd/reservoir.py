@@ -104,6 +104,16 @@ class Reservoirs:
         check(lib().sml_res_step(self._h, ptr(d_feedback), ptr(d_local_model if self.ncs else None),
                                  ptr(d_outvec), stream_ptr(stream)))
 
+    def predict_begin(self, d_feedback, stream=None):
+        """First half of predict: the state update and W_out(:, ncs+1:) x~ (v_ml of
+        outvec_component_contribs, mod_reservoir.f90:1456-1459) -- no local_model needed."""
+        check(lib().sml_res_step_begin(self._h, ptr(d_feedback), stream_ptr(stream)))
+
+    def predict_finish(self, d_local_model, d_outvec, stream=None):
+        """Second half: outvec = W_out(:, 1:ncs) local_model + v_ml, unstandardized."""
+        check(lib().sml_res_step_finish(self._h, ptr(d_local_model if self.ncs else None), ptr(d_outvec),
+                                        stream_ptr(stream)))
+
     def synchronize(self, d_inputs, length: int, stride: int | None = None, stream=None):
         """synchronize (mod_reservoir.f90:1352-1378): `length` state updates, no
         readout.  d_inputs: device tensor of `length` packed feedback blocks
@@ -127,6 +137,14 @@ class Reservoirs:
     def tile_inputs(self, d_g4, d_g2, d_pr, d_fc4, d_fc2, d_tisr, d_feedback, d_local_model, stream=None):
         check(lib().sml_res_tile_inputs(self._h, ptr(d_g4), ptr(d_g2), ptr(d_pr), ptr(d_fc4), ptr(d_fc2),
                                         ptr(d_tisr), ptr(d_feedback), ptr(d_local_model), stream_ptr(stream)))
+
+    def tile_feedback(self, d_g4, d_g2, d_pr, d_tisr, d_feedback, stream=None):
+        check(lib().sml_res_tile_feedback(self._h, ptr(d_g4), ptr(d_g2), ptr(d_pr), ptr(d_tisr), ptr(d_feedback),
+                                          stream_ptr(stream)))
+
+    def tile_local_model(self, d_fc4, d_fc2, d_local_model, stream=None):
+        check(lib().sml_res_tile_local_model(self._h, ptr(d_fc4), ptr(d_fc2), ptr(d_local_model),
+                                             stream_ptr(stream)))
 
     # --- measurement
     def footprint(self):

@@ -1,0 +1,141 @@
+"""The hybrid step on the GPU (speedy_ml_amd.hybrid.HybridLoop; the loop of
+parallelmain.f90:204-270 with sendrecievegrid / run_model, mpires.f90:218-780,
+1516-1628).
+
+* sml_res_step_begin / _finish: the readout split at column ncs (v_ml + v_p of
+  outvec_component_contribs, mod_reservoir.f90:1456-1459) matches the oracle's
+  predict, and misuse of the pair is reported (SML_ERR_STATE);
+* the two-stream schedule (reservoir update + v_ml overlapping SPEEDY's window)
+  gives bit-identical results to the same launches issued on one stream, and to
+  the sequential predict -> assemble -> window -> tile chain."""
+import numpy as np
+import pytest
+
+import oracle
+from speedy_ml_amd import domain
+from speedy_ml_amd.synthetic import feedback_vector, initial_state, local_model_vector, region_weights
+
+pytestmark = pytest.mark.gpu
+
+
+def test_begin_finish_matches_oracle_and_checks_order(cuda):
+    import torch
+
+    from speedy_ml_amd._lib import SmlError
+    from speedy_ml_amd.reservoir import Reservoirs
+
+    cases = [(5, True), (30, False), (0, True), (1127, False)]
+    ws = [region_weights(r, s, n_override=700, seed=3) for r, s in cases]
+    res = Reservoirs([w.region for w in ws], [w.sst for w in ws], [w.n for w in ws], [w.k for w in ws])
+    for i, w in enumerate(ws):
+        res.load_region_weights(i, w)
+        res.set_state(i, initial_state(w.region, w.n))
+    fb_h = np.concatenate([feedback_vector(w.region, w.ninp) for w in ws])
+    lm_h = np.stack([local_model_vector(w.region) for w in ws])
+    fb = torch.from_numpy(fb_h).to(cuda)
+    lm = torch.from_numpy(lm_h).to(cuda)
+    ov = torch.zeros((len(ws), 136), dtype=torch.float64, device=cuda)
+    with pytest.raises(SmlError):
+        res.predict_finish(lm, ov)  # no begin
+    res.predict_begin(fb)
+    with pytest.raises(SmlError):
+        res.predict_begin(fb)  # begin twice
+    res.predict_finish(lm, ov)
+    torch.cuda.synchronize()
+    out = ov.cpu().numpy()
+    o = res.fb_offsets
+    for i, w in enumerate(ws):
+        col, val = w.win_compressed()
+        ref, x1 = oracle.predict_f32(w.rows, w.cols, w.vals, col, val, w.wout, fb_h[o[i]:o[i + 1]], lm_h[i],
+                                     initial_state(w.region, w.n), w.mean, w.std)
+        err = np.abs(out[i] - ref) / (1 + np.abs(ref))
+        assert err.max() < 1e-11, f"region {w.region}: outvec {err.max():.3e}"  # readout summation order
+        xerr = np.abs(res.get_state(i) - x1) / (1 + np.abs(x1))
+        assert xerr.max() < 1e-14, f"region {w.region}: state {xerr.max():.3e}"  # device vs glibc tanh
+
+
+def _loop(cuda, overlap):
+    import torch
+
+    from speedy_ml_amd.dynamics import Dynamics
+    from speedy_ml_amd.exchange import OutvecExchange
+    from speedy_ml_amd.hybrid import HybridLoop
+    from speedy_ml_amd.reservoir import Reservoirs
+    from speedy_ml_amd.synthetic import dyn_state, phys_boundary, synthetic_grids
+
+    mask = domain.load_sst_mask()
+    ws = [region_weights(r, bool(mask[r]), n_override=96, seed=5, climatology=True) for r in range(1152)]
+    res = Reservoirs(list(range(1152)), mask, [w.n for w in ws], [w.k for w in ws])
+    for i, w in enumerate(ws):
+        res.load_region_weights(i, w)
+        res.set_state(i, initial_state(w.region, w.n))
+    st0, forcing = dyn_state()
+    dyn = Dynamics()
+    dyn.set_forcing(**forcing)
+    dyn.set_state(st0)
+    dyn.set_physics(phys_boundary(dyn, forcing["phis"]))
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(cuda)  # noqa: E731
+    tisr = t(np.random.default_rng(13).standard_normal((1152, 16)))
+    loop = HybridLoop(res, dyn, OutvecExchange(1152, 1, 0, device=cuda), cuda, tisr=tisr, overlap=overlap)
+    g4, g2, pr = synthetic_grids(11)
+    f4, f2, _ = synthetic_grids(12)
+    loop.start(t(g4), t(g2), t(pr), t(f4), t(f2))
+    loop.sync()
+    return loop, ws
+
+
+def _snapshot(loop):
+    import torch
+
+    torch.cuda.synchronize()
+    return {k: getattr(loop, k).cpu().numpy().copy() for k in ("ov", "fb", "lm", "g4", "g2", "pr", "f4", "f2")}
+
+
+def test_overlapped_loop_is_bitwise_the_serial_loop(cuda):
+    import torch
+
+    runs = {}
+    for overlap in (False, True):
+        loop, ws = _loop(cuda, overlap)
+        snaps = []
+        for _ in range(3):
+            loop.step()
+            loop.sync()
+            snaps.append(_snapshot(loop))
+        runs[overlap] = (snaps, [loop.res.get_state(i) for i in (0, 500, 1151)])
+        loop.dyn.close()
+        loop.res.close()
+        torch.cuda.synchronize()
+    (sa, xa), (sb, xb) = runs[False], runs[True]
+    for a, b in zip(sa, sb):
+        for k in a:
+            np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+    for a, b in zip(xa, xb):
+        np.testing.assert_array_equal(a, b)
+    last = sa[-1]
+    assert np.isfinite(last["f4"]).all() and np.isfinite(last["ov"]).all()
+    assert np.abs(last["f4"]).max() > 0
+
+
+def test_loop_matches_the_sequential_chain(cuda):
+    """HybridLoop.step == predict -> assemble -> iogrid(30) -> window -> iogrid(31) ->
+    tile, issued one after the other on the current stream (the bench's former step)."""
+    import torch
+
+    loop, _ = _loop(cuda, True)
+    seq, _ = _loop(cuda, False)
+    for _ in range(2):
+        loop.step()
+        # the sequential chain on `seq`'s buffers
+        seq.res.predict(seq.fb, seq.lm, seq.ov)
+        glob = seq.exchange(seq.ov)
+        seq.res.assemble(glob, seq.g4, seq.g2, seq.pr)
+        seq.dyn.from_grid(seq.g4, seq.g2)
+        seq.dyn.window(24)
+        seq.dyn.to_grid(seq.f4, seq.f2)
+        seq.res.tile_inputs(seq.g4, seq.g2, seq.pr, seq.f4, seq.f2, seq.tisr, seq.fb, seq.lm)
+    loop.sync()
+    torch.cuda.synchronize()
+    a, b = _snapshot(loop), _snapshot(seq)
+    for k in a:
+        np.testing.assert_array_equal(a[k], b[k], err_msg=k)

@@ -229,3 +229,37 @@ def test_fused_step_is_bitwise_the_unfused_step(pg, cuda, physics):
         np.testing.assert_array_equal(ra[k], rb[k])
     np.testing.assert_array_equal(ta, tb)
     np.testing.assert_array_equal(pa, pb)
+
+
+def test_window_graph_is_bitwise_the_launched_window(pg, cuda):
+    """sml_dyn_window (stepone + 24 leapfrog steps as ONE captured hipGraph) against
+    the same window launched step by step (stepone, stloop clock on the host): same
+    state, radiation state and clock, for two consecutive windows (entry lradsw of
+    the second one comes from the first)."""
+    import torch
+
+    from speedy_ml_amd.dynamics import Dynamics
+    from speedy_ml_amd.synthetic import dyn_state
+
+    st, forcing = dyn_state(4)
+    out = []
+    for graph in (False, True):
+        d = Dynamics()
+        d.set_forcing(**forcing)
+        d.set_state(st)
+        d.set_physics(_window_bc(pg, d))
+        d.set_rad_state(None)
+        d.set_clock(1, True)
+        clocks = []
+        for _ in range(2):
+            d.window(24, graph=graph)
+            clocks.append(d.get_clock())
+        torch.cuda.synchronize()
+        out.append((d.get_state(), d.get_rad_state(), clocks))
+        d.close()
+    (a, ra, ca), (b, rb, cb) = out
+    assert ca == cb
+    for f in oracle.DYN_FIELDS:
+        np.testing.assert_array_equal(a[f], b[f])
+    for k in ra:
+        np.testing.assert_array_equal(ra[k], rb[k])
