@@ -1,0 +1,87 @@
+// oracle/fft_check.cpp -- TEST INFRASTRUCTURE ONLY.  Checks that the FFTPACK-order
+// real FFT of speedy-ml-1_amd/csrc/sml_fft.hpp (host build of the same pass code the
+// GPU runs) is bit-identical to the reference's own FFTPACK (rffti / rfftb / rfftf
+// from src/spe_subfft_fftpack2.f90, compiled as-is into oracle/_ref by `make ref`).
+//   g++ -O2 -ffp-contract=off -DSML_FFT_HOST -I../speedy-ml-1_amd/csrc fft_check.cpp -ldl
+//   ./fft_check oracle/_ref/libspeedy_ref_spectral.so
+#include <dlfcn.h>
+
+#include <cstdio>
+#include <cstring>
+#include <random>
+
+#include "sml_fft.hpp"
+
+using namespace sml;
+
+typedef void (*fft_fn)(int *, double *, double *);
+typedef void (*init_fn)(int *, double *);
+
+template <int P>
+static void bwd(double *a) {  // the passes in rfftb96's order, P "threads" run one after the other
+    double b[kFftN];
+    double wa[kFftWa];
+    sml_fft_twiddles(wa);
+    for (int t = 0; t < P; ++t) fft::radb2<48, 1, P>(a, b, 1, wa + 0, t);
+    for (int t = 0; t < P; ++t) fft::radb4<12, 2, P>(b, a, 1, wa + 48, wa + 60, wa + 72, t);
+    for (int t = 0; t < P; ++t) fft::radb4<3, 8, P>(a, b, 1, wa + 84, wa + 87, wa + 90, t);
+    for (int t = 0; t < P; ++t) fft::radb3_ido1<32, P>(b, a, 1, t);
+}
+
+template <int P>
+static void fwd(double *a) {
+    double b[kFftN];
+    double wa[kFftWa];
+    sml_fft_twiddles(wa);
+    for (int t = 0; t < P; ++t) fft::radf3_ido1<32, P>(a, b, 1, t);
+    for (int t = 0; t < P; ++t) fft::radf4<3, 8, P>(b, a, 1, wa + 84, wa + 87, wa + 90, t);
+    for (int t = 0; t < P; ++t) fft::radf4<12, 2, P>(a, b, 1, wa + 48, wa + 60, wa + 72, t);
+    for (int t = 0; t < P; ++t) fft::radf2<48, 1, P>(b, a, 1, wa + 0, t);
+}
+
+int main(int argc, char **argv) {
+    void *h = dlopen(argc > 1 ? argv[1] : "oracle/_ref/libspeedy_ref_spectral.so", RTLD_NOW);
+    if (!h) { std::printf("dlopen: %s\n", dlerror()); return 2; }
+    init_fn rffti = (init_fn)dlsym(h, "rffti_");
+    fft_fn rfftb = (fft_fn)dlsym(h, "rfftb_"), rfftf = (fft_fn)dlsym(h, "rfftf_");
+    if (!rffti || !rfftb || !rfftf) { std::printf("missing FFTPACK symbols\n"); return 2; }
+    int n = kFftN;
+    double wsave[2 * kFftN + 15];
+    std::memset(wsave, 0, sizeof wsave);
+    rffti(&n, wsave);
+    double wa[kFftWa];
+    sml_fft_twiddles(wa);
+    int bad = 0;
+    for (int i = 0; i < 94; ++i)
+        if (std::memcmp(&wa[i], &wsave[n + i], 8)) { ++bad; std::printf("twiddle %d differs: %.17g %.17g\n", i, wa[i], wsave[n + i]); }
+    std::mt19937_64 rng(42);
+    std::normal_distribution<double> nd;
+    int nbwd = 0, nfwd = 0;
+    for (int rep = 0; rep < 200; ++rep) {
+        double x[kFftN], r[kFftN], y1[kFftN], y3[kFftN], y8[kFftN];
+        for (int i = 0; i < n; ++i) x[i] = nd(rng) * (rep % 7 + 1);
+        std::memcpy(r, x, sizeof x);
+        rfftb(&n, r, wsave);
+        std::memcpy(y1, x, sizeof x); bwd<1>(y1);
+        std::memcpy(y3, x, sizeof x); bwd<3>(y3);
+        std::memcpy(y8, x, sizeof x); bwd<8>(y8);
+        double yr[kFftN];
+        std::memcpy(yr, x, sizeof x);
+        fft::rfftb96_reg(yr, wa);
+        if (std::memcmp(r, y1, sizeof r) || std::memcmp(r, y3, sizeof r) || std::memcmp(r, y8, sizeof r) ||
+            std::memcmp(r, yr, sizeof r))
+            ++nbwd;
+        std::memcpy(r, x, sizeof x);
+        rfftf(&n, r, wsave);
+        std::memcpy(y1, x, sizeof x); fwd<1>(y1);
+        std::memcpy(y3, x, sizeof x); fwd<3>(y3);
+        std::memcpy(y8, x, sizeof x); fwd<8>(y8);
+        std::memcpy(yr, x, sizeof x);
+        fft::rfftf96_reg(yr, wa);
+        if (std::memcmp(r, y1, sizeof r) || std::memcmp(r, y3, sizeof r) || std::memcmp(r, y8, sizeof r) ||
+            std::memcmp(r, yr, sizeof r))
+            ++nfwd;
+    }
+    std::printf("twiddles differing: %d / 94; rfftb mismatches: %d / 200; rfftf mismatches: %d / 200\n", bad, nbwd, nfwd);
+    return (bad || nbwd || nfwd) ? 1 : 0;
+}

@@ -1,0 +1,16 @@
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest tests/test_physics_gpu.py -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1
+rc=$?; tail -2 gpurun_out/gpu_tests.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 120 python -u tools/probe_phases.py 1 2>&1 | grep -v amdgpu.ids | tail -2 || exit $?
+timeout -k 10 120 python -u tools/probe_phases.py 0 2>&1 | grep -v amdgpu.ids | tail -2 || exit $?
+SML_DYN_FUSED=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/fprof -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --train-regions 0 --reservoir-steps 0 --speedy-steps 8 > gpurun_out/fprof.log 2>&1 || exit $?
+python3 - <<'PY'
+import csv
+r=list(csv.DictReader(open('gpurun_out/fprof/run_kernel_stats.csv')))
+for x in r[:16]:
+    print(f"{x['Name'][:60]:60s} {int(x['Calls']):6d} {float(x['AverageNs'])/1000:8.2f} {float(x['TotalDurationNs'])/1e6:8.2f}")
+PY
+tail -1 gpurun_out/fprof.log | cut -c1-200

@@ -33,6 +33,7 @@
 #include <new>
 
 #include "sml_dynamics_tables.hpp"
+#include "sml_fft.hpp"
 #include "sml_physics.hpp"
 #include "sml_spectral_internal.hpp"
 
@@ -80,6 +81,9 @@ struct sml_dynamics {
     double *d_state = nullptr;
     double *d_phis = nullptr, *d_tcorh = nullptr, *d_qcorh = nullptr, *d_phi = nullptr;
     double *d_specin = nullptr, *d_varm = nullptr, *d_grid = nullptr, *d_gfwd = nullptr, *d_sfwd = nullptr;
+    double *d_vfm = nullptr;  // fused step: m-major forward Fourier coefficients [m][73][lat][2]
+    double *d_sm = nullptr;   // fused step: m-major state [m][var 5][lev 2][kx][n p]
+    long long *d_dbg = nullptr;  // diagnostic phase stamps (SML_DYN_STAMPS=1)
     double *d_tend = nullptr;
     double *d_phys = nullptr;  // physics tendencies: staging for a host's, or the GPU phypar's output
     double *d_minmax = nullptr;  // iogrid(30) safety check: min/max of u, v, t, q
@@ -90,9 +94,9 @@ struct sml_dynamics {
     PhysTables *d_ptab = nullptr;
     double *d_pbc = nullptr, *d_rad = nullptr, *d_pio = nullptr;
     bool phys_on = false;
-    // step kernels: the 7/8-launch form (default) or the 3-launch fused form
-    // (SML_DYN_FUSED=1 at creation; same results bit for bit)
-    bool fused = false;
+    // step kernels: the fused form (default: 2-3 launches per chained step) or the
+    // 8/9-launch form (SML_DYN_FUSED=0 at creation; same results bit for bit)
+    bool fused = true;
     // mod_lflags lradsw (module default .true.) and stloop's istep (at_gcm.f90:81)
     bool lradsw = true;
     int istep = 1;
@@ -417,19 +421,18 @@ __global__ void k_dyn_combine(const double *__restrict__ S, double *__restrict__
 // The CW coefficients x 8 levels of a block share sh[2][kx][CW] (LDS) for the
 // vertical couplings (dmeanc, sigdtc, geop, implic's level matrices); every sum
 // runs over k in the reference's order.  The whole block must call it (barriers).
-template <int CW>
-__device__ inline void tail_coef(double *__restrict__ st, double *__restrict__ Td, double *__restrict__ phi_out,
+template <int CW, class SA>
+__device__ inline void tail_coef(SA S, double *__restrict__ Td, double *__restrict__ phi_out,
                                  const double *__restrict__ phis, const double *__restrict__ tcorh,
-                                 const double *__restrict__ qcorh, const DynTables *__restrict__ T, double (*sh)[kKX][CW],
-                                 int cc, int k, int c, int m, int n, double vordt, double divdt, double tdt, double trdt,
-                                 double psdt, int j1, int j4, double dt, double alph, double rob, double wil) {
-    auto S = [&](size_t off, int lev, int kk) -> double & {  // state (c, kk, lev); ps has one level
-        const size_t nlev = (off == kOffPs) ? 1 : kKX;
-        return st[off + ((size_t)(lev - 1) * nlev + kk) * kSF + c];
-    };
+                                 const double *__restrict__ qcorh, int fc, const DynTables *__restrict__ T,
+                                 double (*sh)[kKX][CW], int cc, int k, int c, int m, int n, double vordt, double divdt,
+                                 double tdt, double trdt, double psdt, int j1, int j4, double dt, double alph,
+                                 double rob, double wil) {
+    // S(var, lev, kk): the state of coefficient c (var 0..4 = vor, div, t, tr, ps at
+    // kk = 0; lev 1 or 2), updated in place; phis / tcorh / qcorh at index fc
     // ---- sptend(divdt, tdt, psdt, j4)  (dyn_sptend.f90:29-66)
-    sh[0][k][cc] = S(kOffDiv, j4, k);
-    sh[1][k][cc] = S(kOffT, j4, k);
+    sh[0][k][cc] = S(1, j4, k);
+    sh[1][k][cc] = S(2, j4, k);
     __syncthreads();
     double dmeanc = 0.0;
 #pragma unroll
@@ -451,14 +454,14 @@ __device__ inline void tail_coef(double *__restrict__ st, double *__restrict__ T
     const double dumk_k1 = (k == kKX - 1) ? 0.0 : sig_k1 * (T->tref[k + 1] - T->tref[k]);
     tdt = tdt - (dumk_k1 + dumk_k) * T->dhsr[k] + T->tref3[k] * (sig_k1 + sig_k) - T->tref2[k] * dmeanc;
     // geop(j4)  (dyn_geop.f90:16-32)
-    double phi = phis[c] + T->xgeop1[kKX - 1] * sh[1][kKX - 1][cc];
+    double phi = phis[fc] + T->xgeop1[kKX - 1] * sh[1][kKX - 1][cc];
 #pragma unroll
     for (int kk = kKX - 2; kk >= k; --kk)
         phi = phi + T->xgeop2[kk + 1] * sh[1][kk + 1][cc] + T->xgeop1[kk] * sh[1][kk][cc];
     if (m == 0 && k >= 1 && k <= kKX - 2) phi = phi + T->corf[k] * (sh[1][k + 1][cc] - sh[1][k - 1][cc]);
     phi_out[(size_t)k * kSF + c] = phi;
     {
-        const double d1 = phi + kRgas * T->tref[k] * S(kOffPs, j4, 0);
+        const double d1 = phi + kRgas * T->tref[k] * S(4, j4, 0);
         const double lapd = -(d1 * T->el2[n][m]);
         divdt = divdt - lapd;
     }
@@ -488,23 +491,23 @@ __device__ inline void tail_coef(double *__restrict__ st, double *__restrict__ T
     }
     // ---- horizontal diffusion (dyn_step.f90:60-112, hordif :130-151)
     const double dmp = T->dmp[n][m], dmp1 = T->dmp1[n][m], dmpd = T->dmpd[n][m], dmp1d = T->dmp1d[n][m];
-    vordt = (vordt - dmp * S(kOffVor, 1, k)) * dmp1;
-    divdt = (divdt - dmpd * S(kOffDiv, 1, k)) * dmp1d;
-    const double ctmp = S(kOffT, 1, k) + tcorh[c] * T->tcorv[k];
+    vordt = (vordt - dmp * S(0, 1, k)) * dmp1;
+    divdt = (divdt - dmpd * S(1, 1, k)) * dmp1d;
+    const double ctmp = S(2, 1, k) + tcorh[fc] * T->tcorv[k];
     tdt = (tdt - dmp * ctmp) * dmp1;
     if (k == 0) {
         if (m == 0) {  // stratospheric drag on the zonal mean, top level (:78-82)
             const double sdrag = 1. / (kTdrs * 3600.);
-            vordt = vordt - sdrag * S(kOffVor, 1, 0);
-            divdt = divdt - sdrag * S(kOffDiv, 1, 0);
+            vordt = vordt - sdrag * S(0, 1, 0);
+            divdt = divdt - sdrag * S(1, 1, 0);
         }
         const double dmps = T->dmps[n][m], dmp1s = T->dmp1s[n][m];
-        vordt = (vordt - dmps * S(kOffVor, 1, 0)) * dmp1s;
-        divdt = (divdt - dmps * S(kOffDiv, 1, 0)) * dmp1s;
+        vordt = (vordt - dmps * S(0, 1, 0)) * dmp1s;
+        divdt = (divdt - dmps * S(1, 1, 0)) * dmp1s;
         tdt = (tdt - dmps * ctmp) * dmp1s;
     }
     {
-        const double cq = S(kOffTr, 1, k) + qcorh[c] * T->qcorv[k];
+        const double cq = S(3, 1, k) + qcorh[fc] * T->qcorv[k];
         trdt = (trdt - dmpd * cq) * dmp1d;
     }
     if (dt <= 0.0) {  // tendencies only (dyn_step.f90:109)
@@ -518,10 +521,10 @@ __device__ inline void tail_coef(double *__restrict__ st, double *__restrict__ T
     // ---- timint with the Robert-Williams filter (dyn_step.f90:153-190)
     const double eps = (j1 == 1) ? 0.0 : rob;
     const double trf = T->trfilt[n][m];
-    auto timint = [&](size_t off, int kk, double fdt) {
+    auto timint = [&](int var, int kk, double fdt) {
         fdt = fdt * trf;  // trunct
-        double &f1 = S(off, 1, kk);
-        double &f2 = S(off, 2, kk);
+        double &f1 = S(var, 1, kk);
+        double &f2 = S(var, 2, kk);
         const double fj1_old = (j1 == 1) ? f1 : f2;
         const double fnew = f1 + dt * fdt;
         const double f1new = fj1_old + wil * eps * (f1 - 2 * fj1_old + fnew);
@@ -529,11 +532,11 @@ __device__ inline void tail_coef(double *__restrict__ st, double *__restrict__ T
         f2 = fnew - (1 - wil) * eps * (f1new - 2 * fj1_new + fnew);
         f1 = f1new;
     };
-    if (k == 0) timint(kOffPs, 0, psdt);
-    timint(kOffVor, k, vordt);
-    timint(kOffDiv, k, divdt);
-    timint(kOffT, k, tdt);
-    timint(kOffTr, k, trdt);
+    if (k == 0) timint(4, 0, psdt);
+    timint(0, k, vordt);
+    timint(1, k, divdt);
+    timint(2, k, tdt);
+    timint(3, k, trdt);
 }
 
 // tail kernel of the unfused step: a block owns 32 real coefficients x 8 levels
@@ -547,174 +550,299 @@ __global__ __launch_bounds__(256) void k_dyn_tail(double *__restrict__ st, doubl
     const int cc = threadIdx.x & (kTailC - 1), k = threadIdx.x / kTailC;
     const int c = blockIdx.x * kTailC + cc;  // 0 .. 1983 = 2 * (m + mx n) + p
     const int mn = c >> 1, m = mn % kMX, n = mn / kMX;
-    tail_coef<kTailC>(st, Td, phi_out, phis, tcorh, qcorh, T, sh, cc, k, c, m, n, Td[kTVor + (size_t)k * kSF + c],
+    auto S = [&](int var, int lev, int kk) -> double & {  // reference layout; ps has one level
+        if (var == 4) return st[kOffPs + (size_t)(lev - 1) * kSF + c];
+        const size_t off = var == 0 ? kOffVor : var == 1 ? kOffDiv : var == 2 ? kOffT : kOffTr;
+        return st[off + ((size_t)(lev - 1) * kKX + kk) * kSF + c];
+    };
+    tail_coef<kTailC>(S, Td, phi_out, phis, tcorh, qcorh, c, T, sh, cc, k, c, m, n, Td[kTVor + (size_t)k * kSF + c],
                       Td[kTDiv + (size_t)k * kSF + c], Td[kTT + (size_t)k * kSF + c], Td[kTTr + (size_t)k * kSF + c],
                       Td[kTPs + c], j1, j4, dt, alph, rob, wil);
 }
 
-// ======================================================= fused step (3 launches)
-// The step's ten stages regrouped at the only all-to-all seams of the spectral
-// transform (spectral <-> Fourier per zonal wavenumber m, Fourier <-> grid per
-// latitude row): every kernel owns either one m or one latitude row, so each
-// regrouped stage works on data its own block produced or that the previous
-// launch left in L2.  Same arithmetic and summation order as the unfused
-// kernels above (bit-identical results).
-//   K1 k_dyn_inv  (m, 8-field tile): prep's inputs computed on the fly + gridy
-//   K2 k_dyn_row  (latitude row j):  gridx -> LDS -> physics + grid-point dynamics
-//                                    -> LDS -> specx (vdspec's 1/cos scaling)
-//   K3 k_dyn_spec (m):               specy -> LDS -> combine (vds, lap) -> tail
+// ======================================================= fused step
+// The step's stages regrouped at the all-to-all seams of the spectral transform
+// (spectral <-> Fourier per zonal wavenumber m, Fourier <-> grid per latitude row):
+//   k_st_rows   (latitude row j, no GPU physics): gridx (FFT) -> LDS -> grid-point
+//               dynamics -> LDS -> specx (FFT)
+//   k_st_grid   (with GPU physics): blocks 0..47 a row's dynamics (gridx + grid-
+//               point dynamics), blocks 48..95 the same row's physics (gridx of the
+//               level-1 fields + phypar) side by side in one launch
+//   k_st_specx  (with GPU physics): dynamics + physics tendencies, specx (FFT)
+//   k_st_spec   (zonal wavenumber m, 512 threads = 64 coefficients x 8 levels):
+//               specy -> combine (vds, lap) -> sptend / geop / implic / hordif /
+//               timint -> the NEXT step's inverse-transform inputs from the new
+//               state (uvspec, grad, geop) -> gridy
+//   k_st_inv    (m): the inverse-transform inputs + gridy from the state in memory,
+//               for a step that follows no fused step (window start)
+// A leapfrog step is 2 launches (3 with GPU physics) instead of 8 / 9.  Each block
+// first stages everything it reads -- the m's slice of the state, the row's Fourier
+// coefficients -- in LDS with coalesced loads: the fused step keeps its own m-major
+// copies of the state ([m][var][lev][k][n p], k_state_to_m / k_state_from_m around
+// a run of fused steps) and of the forward Fourier coefficients ([m][f][lat][p]),
+// so each block's slice is contiguous.  Every stage keeps the unfused kernels'
+// arithmetic, operand order and MFMA tiling: results are bit-identical to them
+// (tests/test_physics_gpu.py).
 typedef double d4 __attribute__((ext_vector_type(4)));
 #define MFMA64(a, b, c) __builtin_amdgcn_mfma_f64_16x16x4f64((a), (b), (c), 0, 0, 0)
 
-// one value of k_dyn_prep's output: inverse-transform input field f at (m, n), part p
-__device__ inline double inv_input(const double *__restrict__ st, const double *__restrict__ phis,
-                                   const DynTables *__restrict__ T, int f, int m, int n, int p, int j2, int o2,
-                                   bool phys) {
-    const size_t lev2 = (size_t)(j2 - 1) * kKX;
-    const int c = ci(p, m, n);
-    if (f < 4 * kKX) {
-        const int var = f / kKX, k = f % kKX;
-        const size_t off = var == 0 ? kOffVor : var == 1 ? kOffDiv : var == 2 ? kOffT : kOffTr;
-        return st[off + (lev2 + k) * kSF + c];
-    }
-    if (f < o2) {  // phypar's level-1 inputs (phys only)
-        if (f < kPQ1) return st[kOffT + (size_t)(f - kPT1) * kSF + c];
-        if (f < kPPhi1) return st[kOffTr + (size_t)(f - kPQ1) * kSF + c];
-        if (f < kPPs1) return geop_at(st + kOffT, phis, T, c, m, f - kPPhi1);
-        return st[kOffPs + c];
-    }
-    int g = f - o2;
-    if (g == 2 * kKX || g == 2 * kKX + 1) {  // grad(ps(j2))
-        const double *ps = st + kOffPs + (size_t)(j2 - 1) * kSF;
-        if (g == 2 * kKX) return p == 1 ? T->gradx[m] * ps[ci(0, m, n)] : -T->gradx[m] * ps[ci(1, m, n)];
-        if (n == 0) return T->gradyp[0][m] * ps[ci(p, m, 1)];
-        if (n == kNX - 1) return -T->gradym[n][m] * ps[ci(p, m, kNTRUN1 - 1)];
-        return -T->gradym[n][m] * ps[ci(p, m, n - 1)] + T->gradyp[n][m] * ps[ci(p, m, n + 1)];
-    }
-    size_t lev = lev2;
-    if (g > 2 * kKX + 1) {  // ucos1 / vcos1 of level 1
-        g -= 2 * kKX + 2;
-        lev = 0;
-    }
-    const int k = g % kKX;
-    const bool vcos = g >= kKX;
-    (void)phys;
-    const double *vor = st + kOffVor + (lev + k) * kSF, *div = st + kOffDiv + (lev + k) * kSF;
-    // uvspec (spe_spectral.f90:351-387), the part of uvspec_at this value needs
-    const double ux = T->uvdx[n][m];
-    if (!vcos) {
-        const double zc = p == 1 ? ux * div[ci(0, m, n)] : -ux * div[ci(1, m, n)];
-        if (n == 0) return zc - T->uvdyp[0][m] * vor[ci(p, m, 1)];
-        if (n == kNX - 1) return T->uvdym[n][m] * vor[ci(p, m, kNTRUN1 - 1)];
-        return T->uvdym[n][m] * vor[ci(p, m, n - 1)] - T->uvdyp[n][m] * vor[ci(p, m, n + 1)] + zc;
-    }
-    const double zp = p == 1 ? ux * vor[ci(0, m, n)] : -ux * vor[ci(1, m, n)];
-    if (n == 0) return zp + T->uvdyp[0][m] * div[ci(p, m, 1)];
-    if (n == kNX - 1) return -T->uvdym[n][m] * div[ci(p, m, kNTRUN1 - 1)];
-    return -T->uvdym[n][m] * div[ci(p, m, n - 1)] + T->uvdyp[n][m] * div[ci(p, m, n + 1)] + zp;
+constexpr int kCW = 2 * kNX;                  // real coefficients (n, p) of one m
+constexpr int kSM = 5 * 2 * kKX * kCW;        // m-major state slice: [var 5][lev 2][k][cc] (ps at k = 0)
+constexpr int kVFs = kIL * 2 + 2;              // field stride of the m-major forward Fourier slice (LDS banks)
+constexpr int kVFm = kNFwd * kVFs;            // m-major forward Fourier slice: [f][lat][p] (+2 pad)
+__device__ inline int smi(int var, int lev, int k, int cc) { return ((var * 2 + lev - 1) * kKX + k) * kCW + cc; }
+
+// diagnostic phase stamps (SML_DYN_STAMPS=1 at creation): thread 0 of each block
+// writes wall_clock64() (100 MHz) at phase boundaries, [kernel][block][8]
+constexpr int kStampBlocks = 64, kStamps = 8;
+__device__ inline void stamp(long long *dbg, int kern, int i) {
+    if (dbg && threadIdx.x == 0) dbg[((size_t)kern * kStampBlocks + blockIdx.x) * kStamps + i] = wall_clock64();
 }
 
-// K1: gridy of the step's inverse-transform inputs (k_gridy's tiling: one wave per
-// (m, 8 fields x Re/Im); lanes gather their 8 spectral values from the state)
-__global__ __launch_bounds__(64) void k_dyn_inv(const double *__restrict__ st, const double *__restrict__ phis,
-                                                const DynTables *__restrict__ T, const double *__restrict__ pinv,
-                                                double *__restrict__ varm, int nf, int j2, int o2, int phys) {
-    const int m = blockIdx.x;
-    const int f0 = blockIdx.y * 8;
-    const int l = threadIdx.x, r = l & 15, kk = l >> 4;
-    const int fa = f0 + (r >> 1), p = r & 1;
-    const bool ok = fa < nf;
+// reference state layout <-> the fused step's m-major copy
+__global__ void k_state_to_m(const double *__restrict__ st, double *__restrict__ sm) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= kMX * kSM) return;
+    const int m = e / kSM, i = e % kSM;
+    const int cc = i % kCW, k = (i / kCW) % kKX, lev = (i / (kCW * kKX)) % 2, var = i / (2 * kKX * kCW);
+    const int c = ci(cc & 1, m, cc >> 1);
+    double v = 0.0;
+    if (var < 4) {
+        const size_t off = var == 0 ? kOffVor : var == 1 ? kOffDiv : var == 2 ? kOffT : kOffTr;
+        v = st[off + ((size_t)lev * kKX + k) * kSF + c];
+    } else if (k == 0) {
+        v = st[kOffPs + (size_t)lev * kSF + c];
+    }
+    sm[e] = v;
+}
+
+__global__ void k_state_from_m(const double *__restrict__ sm, double *__restrict__ st) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= kMX * kSM) return;
+    const int m = e / kSM, i = e % kSM;
+    const int cc = i % kCW, k = (i / kCW) % kKX, lev = (i / (kCW * kKX)) % 2, var = i / (2 * kKX * kCW);
+    const int c = ci(cc & 1, m, cc >> 1);
+    if (var < 4) {
+        const size_t off = var == 0 ? kOffVor : var == 1 ? kOffDiv : var == 2 ? kOffT : kOffTr;
+        st[off + ((size_t)lev * kKX + k) * kSF + c] = sm[e];
+    } else if (k == 0) {
+        st[kOffPs + (size_t)lev * kSF + c] = sm[e];
+    }
+}
+
+// The inverse-transform inputs of one m (k_dyn_prep's fields, same expressions)
+// from the m's state slice Sst (smi layout); writes In[f][kCW] for f < nin.  The
+// whole block calls it.
+__device__ inline void inv_inputs(const double *Sst, double *In, const double *phis_m, const DynTables *__restrict__ T,
+                                  int m, int j2, int n1, int nin) {
+    auto sv = [&](int var, int lev, int k, int cc) { return Sst[smi(var, lev, k, cc)]; };
+    for (int idx = threadIdx.x; idx < nin * kCW; idx += blockDim.x) {
+        const int f = idx / kCW, cc = idx % kCW, n = cc >> 1, p = cc & 1;
+        double v;
+        if (f < 4 * kKX) {
+            v = sv(f / kKX, j2, f % kKX, cc);
+        } else if (f < n1) {  // phypar's level-1 inputs (phys only)
+            if (f < kPQ1) {
+                v = sv(2, 1, f - kPT1, cc);
+            } else if (f < kPPhi1) {
+                v = sv(3, 1, f - kPQ1, cc);
+            } else if (f < kPPs1) {  // geop(1) (geop_at)
+                const int k = f - kPPhi1;
+                double phi = phis_m[cc] + T->xgeop1[kKX - 1] * sv(2, 1, kKX - 1, cc);
+                for (int kk = kKX - 2; kk >= k; --kk)
+                    phi = phi + T->xgeop2[kk + 1] * sv(2, 1, kk + 1, cc) + T->xgeop1[kk] * sv(2, 1, kk, cc);
+                if (m == 0 && k >= 1 && k <= kKX - 2)
+                    phi = phi + T->corf[k] * (sv(2, 1, k + 1, cc) - sv(2, 1, k - 1, cc));
+                v = phi;
+            } else {
+                v = sv(4, 1, 0, cc);
+            }
+        } else {
+            int g = f - n1;
+            if (g == 2 * kKX || g == 2 * kKX + 1) {  // grad(ps(j2))
+                if (g == 2 * kKX) {
+                    v = p == 1 ? T->gradx[m] * sv(4, j2, 0, 2 * n) : -T->gradx[m] * sv(4, j2, 0, 2 * n + 1);
+                } else if (n == 0) {
+                    v = T->gradyp[0][m] * sv(4, j2, 0, 2 + p);
+                } else if (n == kNX - 1) {
+                    v = -T->gradym[n][m] * sv(4, j2, 0, 2 * (kNTRUN1 - 1) + p);
+                } else {
+                    v = -T->gradym[n][m] * sv(4, j2, 0, 2 * (n - 1) + p) + T->gradyp[n][m] * sv(4, j2, 0, 2 * (n + 1) + p);
+                }
+            } else {  // uvspec of level j2, or of level 1 (ucos1 / vcos1)
+                int lev = j2;
+                if (g > 2 * kKX + 1) {
+                    g -= 2 * kKX + 2;
+                    lev = 1;
+                }
+                const int k = g % kKX;
+                const bool vcos = g >= kKX;
+                auto vor = [&](int pp, int nn) { return sv(0, lev, k, 2 * nn + pp); };
+                auto div = [&](int pp, int nn) { return sv(1, lev, k, 2 * nn + pp); };
+                const double ux = T->uvdx[n][m];
+                if (!vcos) {
+                    const double zc = p == 1 ? ux * div(0, n) : -ux * div(1, n);
+                    if (n == 0) v = zc - T->uvdyp[0][m] * vor(p, 1);
+                    else if (n == kNX - 1) v = T->uvdym[n][m] * vor(p, kNTRUN1 - 1);
+                    else v = T->uvdym[n][m] * vor(p, n - 1) - T->uvdyp[n][m] * vor(p, n + 1) + zc;
+                } else {
+                    const double zp = p == 1 ? ux * vor(0, n) : -ux * vor(1, n);
+                    if (n == 0) v = zp + T->uvdyp[0][m] * div(p, 1);
+                    else if (n == kNX - 1) v = -T->uvdym[n][m] * div(p, kNTRUN1 - 1);
+                    else v = -T->uvdym[n][m] * div(p, n - 1) + T->uvdyp[n][m] * div(p, n + 1) + zp;
+                }
+            }
+        }
+        In[f * kCW + cc] = v;
+    }
+}
+
+// gridy of In[f][kCW] (this m) -> varm[f][lat][62] (k_gridy's tiling: one wave per
+// 8-field x Re/Im tile, waves of the block stride over the tiles)
+__device__ inline void gridy_m(const double *In, const double *__restrict__ pinv, double *__restrict__ varm, int m,
+                               int nf) {
+    const int wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const int l = threadIdx.x & 63, r = l & 15, kk = l >> 4;
     const double *pm = pinv + (size_t)m * kNX * 32;
-    d4 acc00 = {0, 0, 0, 0}, acc01 = acc00, acc10 = acc00, acc11 = acc00;
+    double b00[4], b01[4], b10[4], b11[4];  // the Legendre operands, loaded once per wave
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-        const int n_odd = 2 * (4 * s + kk);  // n = 1,3,.. (1-based): symmetric part
-        const int n_even = n_odd + 1;        // n = 2,4,..: antisymmetric part
-        const double a0 = ok ? inv_input(st, phis, T, fa, m, n_odd, p, j2, o2, phys) : 0.0;
-        const double a1 = ok ? inv_input(st, phis, T, fa, m, n_even, p, j2, o2, phys) : 0.0;
-        acc00 = MFMA64(a0, pm[n_odd * 32 + r], acc00);
-        acc01 = MFMA64(a0, pm[n_odd * 32 + 16 + r], acc01);
-        acc10 = MFMA64(a1, pm[n_even * 32 + r], acc10);
-        acc11 = MFMA64(a1, pm[n_even * 32 + 16 + r], acc11);
+        const int n_odd = 2 * (4 * s + kk), n_even = n_odd + 1;
+        b00[s] = pm[n_odd * 32 + r];
+        b01[s] = pm[n_odd * 32 + 16 + r];
+        b10[s] = pm[n_even * 32 + r];
+        b11[s] = pm[n_even * 32 + 16 + r];
     }
+    for (int tile = wave; tile < (nf + 7) / 8; tile += nw) {
+        const int f0 = tile * 8;
+        const int fa = f0 + (r >> 1), p = r & 1;
+        const bool ok = fa < nf;
+        const double *a = In + (ok ? fa : 0) * kCW + p;
+        d4 acc00 = {0, 0, 0, 0}, acc01 = acc00, acc10 = acc00, acc11 = acc00;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int row = kk + 4 * q;
-        const int f = f0 + (row >> 1);
-        if (f >= nf) continue;
-        double *vr = varm + (size_t)f * kVF + 2 * m + (row & 1);
-        {
-            const int j = r;
-            const double sym = acc00[q], asym = acc10[q];
-            vr[(kIL - 1 - j) * kMX2] = sym + asym;
-            vr[j * kMX2] = sym - asym;
-        }
-        const int j = 16 + r;
-        if (j < kIY) {
-            const double sym = acc01[q], asym = acc11[q];
-            vr[(kIL - 1 - j) * kMX2] = sym + asym;
-            vr[j * kMX2] = sym - asym;
-        }
-    }
-}
-
-// K2: one latitude row j per block.  LDS holds the row's inverse-transformed fields
-// and then its 73 forward-transform inputs (stride kRowLd breaks LDS bank aliasing).
-constexpr int kRowThreads = 256, kRowWaves = kRowThreads / 64, kRowLd = 100;
-__global__ __launch_bounds__(kRowThreads) void k_dyn_row(
-    const double *__restrict__ varm, double *__restrict__ varm_out, const double *__restrict__ dinv,
-    const double *__restrict__ dfwd, const double *__restrict__ cosgr, const DynTables *__restrict__ T, int nin,
-    int n1, const double *__restrict__ Pext, const double *__restrict__ bc, double *__restrict__ rad,
-    const PhysTables *__restrict__ PT, int phys, int lradsw) {
-    __shared__ double G[kNInvMax * kRowLd];
-    __shared__ double F[kNFwd * kRowLd];
-    const int j = blockIdx.x;
-    const int wave = threadIdx.x >> 6, l = threadIdx.x & 63, r = l & 15, kk = l >> 4;
-    // a) gridx (k_gridx with fields in the M role): G[f][lon] = sum_c varm[f][j][c] dinv[c][lon]
-    const int nft = (nin + 15) / 16;
-    for (int t = wave; t < nft * 6; t += kRowWaves) {
-        const int ft = t / 6, lt = t % 6;
-        const int fa = ft * 16 + r;
-        const bool ok = fa < nin;
-        const double *vr = varm + (size_t)(ok ? fa : 0) * kVF + j * kMX2;
-        d4 acc = {0, 0, 0, 0};
-#pragma unroll 8
-        for (int s = 0; s < kCPad / 4; ++s) {
-            const int c = 4 * s + kk;
-            const double b = dinv[c * kIX + 16 * lt + r];
-            const double a = (ok && c < kMX2) ? vr[c] : 0.0;
-            acc = MFMA64(a, b, acc);
+        for (int s = 0; s < 4; ++s) {
+            const int n_odd = 2 * (4 * s + kk);  // n = 1,3,.. (1-based): symmetric part
+            const int n_even = n_odd + 1;        // n = 2,4,..: antisymmetric part
+            const double a0 = ok ? a[2 * n_odd] : 0.0;
+            const double a1 = ok ? a[2 * n_even] : 0.0;
+            acc00 = MFMA64(a0, b00[s], acc00);
+            acc01 = MFMA64(a0, b01[s], acc01);
+            acc10 = MFMA64(a1, b10[s], acc10);
+            acc11 = MFMA64(a1, b11[s], acc11);
         }
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            const int f = ft * 16 + kk + 4 * q;
-            if (f < nin) {
-                double v = acc[q];
-                if (f >= n1) v = v * cosgr[j];  // kcos = 2
-                G[f * kRowLd + 16 * lt + r] = v;
+            const int row = kk + 4 * q;
+            const int f = f0 + (row >> 1);
+            if (f >= nf) continue;
+            double *vr = varm + (size_t)f * kVF + 2 * m + (row & 1);
+            {
+                const int j = r;
+                const double sym = acc00[q], asym = acc10[q];
+                vr[(kIL - 1 - j) * kMX2] = sym + asym;
+                vr[j * kMX2] = sym - asym;
+            }
+            const int j = 16 + r;
+            if (j < kIY) {
+                const double sym = acc01[q], asym = acc11[q];
+                vr[(kIL - 1 - j) * kMX2] = sym + asym;
+                vr[j * kMX2] = sym - asym;
             }
         }
     }
+}
+
+// stage the m's forcing (phis, tcorh, qcorh: reference layout) into Fm[3][kCW]
+__device__ inline void load_forcing_m(double *Fm, const double *__restrict__ phis, const double *__restrict__ tcorh,
+                                      const double *__restrict__ qcorh, int m) {
+    for (int i = threadIdx.x; i < 3 * kCW; i += blockDim.x) {
+        const int which = i / kCW, cc = i % kCW;
+        const double *src = which == 0 ? phis : which == 1 ? tcorh : qcorh;
+        Fm[i] = src[ci(cc & 1, m, cc >> 1)];
+    }
+}
+
+constexpr int kSpecThreads = kCW * kKX;  // 512
+
+// window start: the inverse transforms of step (.., j2) from the m-major state
+__global__ __launch_bounds__(kSpecThreads) void k_st_inv(const double *__restrict__ sm, const double *__restrict__ phis,
+                                                         const DynTables *__restrict__ T,
+                                                         const double *__restrict__ pinv, double *__restrict__ varm,
+                                                         int j2, int n1, int nin) {
+    __shared__ double Sst[kSM];
+    __shared__ double In[kNInvMax * kCW];
+    __shared__ double Fm[kCW];
+    const int m = blockIdx.x;
+    const double *src = sm + (size_t)m * kSM;
+    for (int i = threadIdx.x; i < kSM / 2; i += blockDim.x)
+        reinterpret_cast<double2 *>(Sst)[i] = reinterpret_cast<const double2 *>(src)[i];
+    for (int cc = threadIdx.x; cc < kCW; cc += blockDim.x) Fm[cc] = phis[ci(cc & 1, m, cc >> 1)];
     __syncthreads();
-    // b) one thread per grid column: phypar on level 1, grid-point dynamics
-    if (threadIdx.x < kIX) {
-        const int i = threadIdx.x, pt = j * kIX + i;
-        auto g = [&](int f) { return G[f * kRowLd + i]; };
-        double pu[kKX], pv[kKX], ptt[kKX], pq[kKX];
-        bool hasP = false;
-        if (phys) {
-            double ua[kKX], va[kKX], ta[kKX], qa[kKX], ph[kKX];
+    inv_inputs(Sst, In, Fm, T, m, j2, n1, nin);
+    __syncthreads();
+    gridy_m(In, pinv, varm, m, nin);
+}
+
+// Fourier stage of one latitude row: FFTPACK's real FFT (sml_fft.hpp, the reference's
+// rfftb / rfftf operation order), one transform per thread held in registers; the
+// row's grid values meet the column-wise grid-point stage in LDS, element-major
+// A[lon][f] (row stride kRowLd, odd: the column threads' reads spread over banks).
+constexpr int kRowThreads = 128, kRowLd = 97;
+static_assert(kNInvMax <= kRowThreads && kNFwd <= kRowThreads && kIX <= kRowThreads, "one thread per transform");
+
+// gridx of field f, row j (spe_subfft_fftpack.f90:24-45): packing, rfftb, x cosgr(j)
+// for kcos = 2; the 96 values into A[lon][f]
+__device__ inline void row_gridx(double *A, const double *__restrict__ varm, const double *__restrict__ wa, int f,
+                                 int j, bool kcos2, double cj) {
+    const double *v = varm + (size_t)f * kVF + j * kMX2;
+    double x[kFftN];
+    x[0] = v[0];
 #pragma unroll
-            for (int k = 0; k < kKX; ++k) {
-                ua[k] = g(n1 + 2 * kKX + 2 + k);
-                va[k] = g(n1 + 3 * kKX + 2 + k);
-                ta[k] = g(kPT1 + k);
-                qa[k] = g(kPQ1 + k);
-                ph[k] = g(kPPhi1 + k);
-            }
-            phys_column(pt, ua, va, ta, qa, ph, g(kPPs1), bc, rad, PT, lradsw != 0, pu, pv, ptt, pq);
-            hasP = true;
-        } else if (Pext) {
+    for (int e = 1; e <= kMX2 - 2; ++e) x[e] = v[e + 1];
+#pragma unroll
+    for (int e = kMX2 - 1; e < kFftN; ++e) x[e] = 0.0;
+    fft::rfftb96_reg(x, wa);
+#pragma unroll
+    for (int e = 0; e < kFftN; ++e) A[e * kRowLd + f] = kcos2 ? x[e] * cj : x[e];
+}
+
+// specx of field f, row j from x[96] (already x cosgr(j) where vdspec scales):
+// rfftf, varm(1) = fvar(1)/ix, varm(2) = 0, varm(m) = fvar(m-1)/ix, into the m-major
+// forward coefficients vfm[m][f][j][p]
+__device__ inline void row_specx(double *x, double *__restrict__ vfm, const double *__restrict__ wa, int f, int j) {
+    fft::rfftf96_reg(x, wa);
+    const double scale = 1. / (double)kIX;
+    double *o = vfm + (size_t)f * kVFs + j * 2;
+    o[0] = x[0] * scale;
+    o[1] = 0.0;
+#pragma unroll
+    for (int c = 2; c < kMX2; ++c) o[(size_t)(c >> 1) * kVFm + (c & 1)] = x[c - 1] * scale;
+}
+
+// one latitude row without GPU physics: gridx of the 50 inverse transforms, grid-
+// point dynamics of the row's 96 columns (+ a host's physics tendencies Pext
+// [u|v|t|q][kx][ngp] if given) into LDS, specx straight to the m-major coefficients.
+__global__ __launch_bounds__(kRowThreads) void k_st_rows(const double *__restrict__ varm, double *__restrict__ vfm,
+                                                         const double *__restrict__ wa,
+                                                         const double *__restrict__ cosgr,
+                                                         const DynTables *__restrict__ T,
+                                                         const double *__restrict__ Pext, long long *dbg) {
+    __shared__ double A[kFftN * kRowLd], B[kFftN * kRowLd];
+    constexpr int n1 = kNInv1, nin = kNInv;
+    const int j = blockIdx.x, tid = threadIdx.x;
+    const double cj = cosgr[j];
+    stamp(dbg, 0, 0);
+    stamp(dbg, 0, 1);
+    // gridx: one field per thread
+    if (tid < nin) row_gridx(A, varm, wa, tid, j, tid >= n1, cj);
+    __syncthreads();
+    stamp(dbg, 0, 2);
+    // one thread per grid column: grid-point dynamics, the forward-transform inputs into B
+    if (tid < kIX) {
+        const int i = tid, pt = j * kIX + i;
+        auto g = [&](int f) { return A[i * kRowLd + f]; };
+        double pu[kKX], pv[kKX], ptt[kKX], pq[kKX];
+        if (Pext) {
 #pragma unroll
             for (int k = 0; k < kKX; ++k) {
                 pu[k] = Pext[(size_t)k * kGF + pt];
@@ -722,95 +850,202 @@ __global__ __launch_bounds__(kRowThreads) void k_dyn_row(
                 ptt[k] = Pext[(size_t)(2 * kKX + k) * kGF + pt];
                 pq[k] = Pext[(size_t)(3 * kKX + k) * kGF + pt];
             }
-            hasP = true;
         }
-        gridpoint_column(j, n1, g, hasP, pu, pv, ptt, pq, [&](int f, double v) { F[f * kRowLd + i] = v; }, T);
+        gridpoint_column(j, n1, g, Pext != nullptr, pu, pv, ptt, pq, [&](int f, double v) { B[i * kRowLd + f] = v; },
+                         T);
     }
     __syncthreads();
-    // c) specx (k_specx with fields in the M role), vdspec inputs x cosgr (kcos = 2)
-    const double s0 = cosgr[j];
-    for (int t = wave; t < 5 * 4; t += kRowWaves) {
-        const int ft = t / 4, ct = t % 4;
-        const int fa = ft * 16 + r;
-        const bool ok = fa < kNFwd;
-        const bool scale = fa < kNFwdScaled;
-        const double *fr = F + (ok ? fa : 0) * kRowLd;
-        d4 acc = {0, 0, 0, 0};
-#pragma unroll 8
-        for (int s = 0; s < kIX / 4; ++s) {
-            const int i = 4 * s + kk;
-            const double b = dfwd[i * kCPad + 16 * ct + r];
-            double a = ok ? fr[i] : 0.0;
-            if (scale) a = a * s0;
-            acc = MFMA64(a, b, acc);
-        }
-        const int c = 16 * ct + r;
-        if (c < kMX2) {
+    stamp(dbg, 0, 3);
+    // specx: vdspec's x cosgr(j) on its inputs (spe_spectral.f90:430-445), rfftf
+    if (tid < kNFwd) {
+        double x[kFftN];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int f = ft * 16 + kk + 4 * q;
-                if (f < kNFwd) varm_out[(size_t)f * kVF + j * kMX2 + c] = acc[q];
-            }
+        for (int e = 0; e < kFftN; ++e) x[e] = tid < kNFwdScaled ? B[e * kRowLd + tid] * cj : B[e * kRowLd + tid];
+        row_specx(x, vfm, wa, tid, j);
+    }
+    __syncthreads();
+    stamp(dbg, 0, 4);
+}
+
+// With GPU physics the grid stage splits by role in ONE launch: blocks 0..47 take a
+// latitude row's dynamics (gridx of the 50 level-j2 fields, grid-point dynamics ->
+// F), blocks 48..95 the same row's physics (gridx of phypar's 41 level-1 fields,
+// phypar per column -> P); the two halves of the step's grid work run side by side
+// and meet in k_st_specx, which adds P to F where grtend adds it (dyn_grtend.f90:225).
+__global__ __launch_bounds__(kRowThreads) void k_st_grid(
+    const double *__restrict__ varm, double *__restrict__ F, double *__restrict__ P, const double *__restrict__ wa,
+    const double *__restrict__ cosgr, const DynTables *__restrict__ T, const double *__restrict__ bc,
+    double *__restrict__ rad, const PhysTables *__restrict__ PT, int lradsw, long long *dbg) {
+    __shared__ double A[kFftN * kRowLd];
+    constexpr int n1 = kNInv1P, nin = kNInvP;
+    constexpr int nphys = (n1 - kPT1) + (nin - (n1 + 2 * kKX + 2));  // 25 + 16 = 41
+    const bool is_phys = blockIdx.x >= kIL;
+    const int j = is_phys ? blockIdx.x - kIL : blockIdx.x, tid = threadIdx.x;
+    const double cj = cosgr[j];
+    // gridx of the role's fields (field index f of the step's nin inverse transforms)
+    if (!is_phys) {
+        if (tid < kNInv) {
+            const int f = tid < kNInv1 ? tid : n1 + (tid - kNInv1);  // [vor div t tr] | [ucos vcos psdx psdy]
+            row_gridx(A, varm, wa, f, j, f >= n1, cj);
         }
+    } else if (tid < nphys) {
+        const int f = tid < n1 - kPT1 ? kPT1 + tid : n1 + 2 * kKX + 2 + (tid - (n1 - kPT1));
+        row_gridx(A, varm, wa, f, j, f >= n1, cj);
+    }
+    __syncthreads();
+    if (tid >= kIX) return;
+    const int i = tid, pt = j * kIX + i;
+    auto g = [&](int f) { return A[i * kRowLd + f]; };
+    if (!is_phys) {
+        double dummy[kKX];
+        gridpoint_column(j, n1, g, false, dummy, dummy, dummy, dummy,
+                         [&](int f, double v) { F[(size_t)f * kGF + pt] = v; }, T);
+        return;
+    }
+    double ua[kKX], va[kKX], ta[kKX], qa[kKX], ph[kKX], ut[kKX], vt[kKX], tt[kKX], qt[kKX];
+#pragma unroll
+    for (int k = 0; k < kKX; ++k) {
+        ua[k] = g(n1 + 2 * kKX + 2 + k);
+        va[k] = g(n1 + 3 * kKX + 2 + k);
+        ta[k] = g(kPT1 + k);
+        qa[k] = g(kPQ1 + k);
+        ph[k] = g(kPPhi1 + k);
+    }
+    phys_column(pt, ua, va, ta, qa, ph, g(kPPs1), bc, rad, PT, lradsw != 0, ut, vt, tt, qt);
+#pragma unroll
+    for (int k = 0; k < kKX; ++k) {
+        P[(size_t)k * kGF + pt] = ut[k];
+        P[(size_t)(kKX + k) * kGF + pt] = vt[k];
+        P[(size_t)(2 * kKX + k) * kGF + pt] = tt[k];
+        P[(size_t)(3 * kKX + k) * kGF + pt] = qt[k];
     }
 }
 
-// K3: one zonal wavenumber m per block: specy of the 73 fields into LDS, then the
-// combine and tail of the m's 64 real coefficients x 8 levels (one thread each).
-constexpr int kSpecThreads = 512;
-__global__ __launch_bounds__(kSpecThreads) void k_dyn_spec(
-    const double *__restrict__ varm, const double *__restrict__ pfwd, const double *__restrict__ wt,
-    double *__restrict__ st, double *__restrict__ Td, double *__restrict__ phi_out, const double *__restrict__ phis,
+// specx (with GPU physics): one (field, row) transform per thread; F[f][ngp] + the
+// physics tendencies P of the u, v, t, q fields (the dynamical tendency first, as
+// grtend adds them), x cosgr(j) for vdspec's inputs, rfftf -> m-major coefficients
+__global__ __launch_bounds__(64) void k_st_specx(const double *__restrict__ F, const double *__restrict__ P,
+                                                 double *__restrict__ vfm, const double *__restrict__ wa,
+                                                 const double *__restrict__ cosgr) {
+    const int id = blockIdx.x * 64 + threadIdx.x;
+    if (id >= kNFwd * kIL) return;
+    const int f = id / kIL, j = id % kIL;
+    // F field -> tendency slot of P: u 0..7, v 24..31, t 56..63, q 64..71
+    const int pf = f < kKX ? f : (f >= 3 * kKX && f < 4 * kKX) ? kKX + f - 3 * kKX
+                 : (f >= 7 * kKX && f < 9 * kKX) ? 2 * kKX + f - 7 * kKX : -1;
+    const double *g = F + (size_t)f * kGF + j * kIX;
+    const double *pp = P + (size_t)(pf < 0 ? 0 : pf) * kGF + j * kIX;
+    const double cj = cosgr[j];
+    double x[kFftN];
+#pragma unroll
+    for (int e = 0; e < kFftN; ++e) {
+        double v = g[e];
+        if (pf >= 0) v = v + pp[e];
+        x[e] = f < kNFwdScaled ? v * cj : v;
+    }
+    row_specx(x, vfm, wa, f, j);
+}
+
+// one zonal wavenumber m: specy of the 73 forward transforms, combine and tail of
+// the m's 64 real coefficients x 8 levels (one thread each) on the m's state slice
+// in LDS; with next_j2 > 0 the new state feeds the next step's inverse transforms
+__global__ __launch_bounds__(kSpecThreads) void k_st_spec(
+    const double *__restrict__ vfm, const double *__restrict__ pfwd, const double *__restrict__ wt,
+    double *__restrict__ sm, double *__restrict__ Td, double *__restrict__ phi_out, const double *__restrict__ phis,
     const double *__restrict__ tcorh, const double *__restrict__ qcorh, const DynTables *__restrict__ T, int j1,
-    int j4, double dt, double alph, double rob, double wil) {
-    __shared__ double S[kNFwd * 2 * kNX];  // [f][2 n + p] of this m
-    __shared__ double sh[2][kKX][2 * kNX];
+    int j4, double dt, double alph, double rob, double wil, const double *__restrict__ pinv,
+    double *__restrict__ varm_next, int next_j2, int n1, int nin, long long *dbg) {
+    __shared__ double V[kVFm];            // this m's forward Fourier coefficients [f][lat][p]
+    __shared__ double S[kNInvMax * kCW];  // specy output [f][2 n + p]; then the next step's inputs
+    __shared__ double sh[2][kKX][kCW];
+    __shared__ double Sst[kSM];           // this m's state, updated in place
+    __shared__ double Fm[3 * kCW];        // phis, tcorh, qcorh of this m
     const int m = blockIdx.x;
     const int wave = threadIdx.x >> 6, l = threadIdx.x & 63, r = l & 15, kk = l >> 4;
-    // a) specy (k_specy's tiling: 8 fields x Re/Im per wave)
+    stamp(dbg, 1, 0);
+    {
+        const double2 *src = reinterpret_cast<const double2 *>(vfm + (size_t)m * kVFm);
+        for (int i = threadIdx.x; i < kVFm / 2; i += kSpecThreads) reinterpret_cast<double2 *>(V)[i] = src[i];
+        const double2 *ss = reinterpret_cast<const double2 *>(sm + (size_t)m * kSM);
+        for (int i = threadIdx.x; i < kSM / 2; i += kSpecThreads) reinterpret_cast<double2 *>(Sst)[i] = ss[i];
+        load_forcing_m(Fm, phis, tcorh, qcorh, m);
+    }
+    // specy operands: wave w's tiles all use this m's Legendre columns of its lanes
     const double *pm = pfwd + (size_t)m * kNX * kIY;
+    double wv[kIY / 4], bS[kIY / 4], bD[kIY / 4];
+#pragma unroll
+    for (int s = 0; s < kIY / 4; ++s) {
+        const int j = 4 * s + kk;
+        wv[s] = wt[j];
+        bS[s] = pm[(2 * r) * kIY + j];
+        bD[s] = pm[(2 * r + 1) * kIY + j];
+    }
+    __syncthreads();
+    stamp(dbg, 1, 1);
+    // a) specy (k_specy's tiling: 8 fields x Re/Im per wave)
     for (int tile = wave; tile < (kNFwd + 7) / 8; tile += kSpecThreads / 64) {
         const int f0 = tile * 8;
         const int fa = f0 + (r >> 1);
         const bool ok = fa < kNFwd;
-        const double *vr = varm + (size_t)(ok ? fa : 0) * kVF + 2 * m + (r & 1);
+        const double *vr = V + (ok ? fa : 0) * kVFs + (r & 1);
         d4 accS = {0, 0, 0, 0}, accD = accS;
 #pragma unroll
         for (int s = 0; s < kIY / 4; ++s) {
             const int j = 4 * s + kk;
             double aS = 0.0, aD = 0.0;
             if (ok) {
-                const double vn = vr[(kIL - 1 - j) * kMX2], vs = vr[j * kMX2];
-                aS = (vn + vs) * wt[j];
-                aD = (vn - vs) * wt[j];
+                const double vn = vr[(kIL - 1 - j) * 2], vs = vr[j * 2];
+                aS = (vn + vs) * wv[s];
+                aD = (vn - vs) * wv[s];
             }
-            accS = MFMA64(aS, pm[(2 * r) * kIY + j], accS);
-            accD = MFMA64(aD, pm[(2 * r + 1) * kIY + j], accD);
+            accS = MFMA64(aS, bS[s], accS);
+            accD = MFMA64(aD, bD[s], accD);
         }
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int row = kk + 4 * q;
             const int f = f0 + (row >> 1);
             if (f >= kNFwd) continue;
-            S[f * 2 * kNX + 2 * (2 * r) + (row & 1)] = accS[q];
-            S[f * 2 * kNX + 2 * (2 * r + 1) + (row & 1)] = accD[q];
+            S[f * kCW + 2 * (2 * r) + (row & 1)] = accS[q];
+            S[f * kCW + 2 * (2 * r + 1) + (row & 1)] = accD[q];
         }
     }
     __syncthreads();
+    stamp(dbg, 1, 2);
     // b) combine (k_dyn_combine) for coefficient (n, p) at level k
-    const int cc = threadIdx.x & (2 * kNX - 1), k = threadIdx.x / (2 * kNX);
+    const int cc = threadIdx.x & (kCW - 1), k = threadIdx.x / kCW;
     const int n = cc >> 1, p = cc & 1;
     const int c = ci(p, m, n);
-    auto fl = [&](int f) { return [=](int pp, int nn) { return S[f * 2 * kNX + 2 * nn + pp]; }; };
+    auto fl = [&](int f) { return [=](int pp, int nn) { return S[f * kCW + 2 * nn + pp]; }; };
     double vo, dv, d0, dq, dummy;
     vds_gen(fl(k), fl(3 * kKX + k), T, m, n, p, &vo, &dv);  // vdspec(utend, vtend)
     const double lapv = -(fl(6 * kKX + k)(p, n) * T->el2[n][m]);
     vds_gen(fl(kKX + k), fl(4 * kKX + k), T, m, n, p, &dummy, &d0);      // vdspec(-u tgg, -v tgg)
     vds_gen(fl(2 * kKX + k), fl(5 * kKX + k), T, m, n, p, &dummy, &dq);  // vdspec(-u trg, -v trg)
     const double psdt = (m == 0 && n == 0) ? 0.0 : fl(kNFwd - 1)(p, n);
-    // c) sptend / implic / diffusion / time integration
-    tail_coef<2 * kNX>(st, Td, phi_out, phis, tcorh, qcorh, T, sh, cc, k, c, m, n, vo, dv - lapv,
-                       d0 + fl(7 * kKX + k)(p, n), dq + fl(8 * kKX + k)(p, n), psdt, j1, j4, dt, alph, rob, wil);
+    const double tdt0 = d0 + fl(7 * kKX + k)(p, n), trdt0 = dq + fl(8 * kKX + k)(p, n);
+    if (dbg) {
+        __syncthreads();
+        stamp(dbg, 1, 3);
+    }
+    // c) sptend / implic / diffusion / time integration on the LDS state
+    auto SA = [&](int var, int lev, int kk2) -> double & { return Sst[smi(var, lev, kk2, cc)]; };
+    tail_coef<kCW>(SA, Td, phi_out, Fm, Fm + kCW, Fm + 2 * kCW, cc, T, sh, cc, k, c, m, n, vo, dv - lapv, tdt0, trdt0,
+                   psdt, j1, j4, dt, alph, rob, wil);
+    __syncthreads();  // S is free, Sst complete
+    stamp(dbg, 1, 4);
+    {
+        double2 *dst = reinterpret_cast<double2 *>(sm + (size_t)m * kSM);
+        for (int i = threadIdx.x; i < kSM / 2; i += kSpecThreads) dst[i] = reinterpret_cast<const double2 *>(Sst)[i];
+    }
+    if (next_j2 <= 0) return;  // block-uniform
+    // d) the next step's inverse-transform inputs (k_dyn_prep) and gridy
+    inv_inputs(Sst, S, Fm, T, m, next_j2, n1, nin);
+    __syncthreads();
+    stamp(dbg, 1, 5);
+    gridy_m(S, pinv, varm_next, m, nin);
+    __syncthreads();
+    stamp(dbg, 1, 6);
 }
 
 // ------------------------------------------------------------ iogrid(30/31)
@@ -933,7 +1168,7 @@ int dalloc(T **p, size_t count) {
 extern "C" int sml_dyn_destroy(sml_dynamics *d) {
     if (!d) return SML_OK;
     void *ptrs[] = {d->d_tabs, d->d_state, d->d_phis, d->d_tcorh, d->d_qcorh, d->d_phi, d->d_specin,
-                    d->d_varm, d->d_grid, d->d_gfwd, d->d_sfwd, d->d_tend, d->d_phys, d->d_minmax, d->d_io,
+                    d->d_varm, d->d_grid, d->d_gfwd, d->d_sfwd, d->d_tend, d->d_phys, d->d_minmax, d->d_io, d->d_vfm, d->d_sm, d->d_dbg,
                     d->d_ptab, d->d_pbc, d->d_rad, d->d_pio};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
@@ -960,12 +1195,18 @@ extern "C" int sml_dyn_create(double radius, sml_dynamics **out) {
     build_dyn_indyns(spectral_host_tables(d->sp), &d->tab);
     build_phys_tables(d->tab, &d->ptab);
     if (const char *e = std::getenv("SML_DYN_FUSED")) d->fused = *e && *e != '0';
+    if (const char *e = std::getenv("SML_DYN_STAMPS"))
+        if (*e && *e != '0' && (rc = dalloc(reinterpret_cast<double **>(&d->d_dbg), 2 * kStampBlocks * kStamps))) {
+            sml_dyn_destroy(d);
+            return rc;
+        }
     if ((rc = dalloc(&d->d_tabs, 4)) || (rc = dalloc(&d->d_state, kStateSize)) || (rc = dalloc(&d->d_phis, kSF)) ||
         (rc = dalloc(&d->d_tcorh, kSF)) || (rc = dalloc(&d->d_qcorh, kSF)) || (rc = dalloc(&d->d_phi, kKX * kSF)) ||
         (rc = dalloc(&d->d_specin, (size_t)kNInvMax * kSF)) ||
         (rc = dalloc(&d->d_varm, (size_t)(kNInvMax > kNFwd ? kNInvMax : kNFwd) * kVF)) ||
         (rc = dalloc(&d->d_grid, (size_t)kNInvMax * kGF)) || (rc = dalloc(&d->d_gfwd, (size_t)kNFwd * kGF)) ||
         (rc = dalloc(&d->d_sfwd, (size_t)kNFwd * kSF)) || (rc = dalloc(&d->d_tend, kTendSize)) ||
+        (rc = dalloc(&d->d_vfm, (size_t)kMX * kVFm)) || (rc = dalloc(&d->d_sm, (size_t)kMX * kSM)) ||
         (rc = dalloc(&d->d_phys, (size_t)4 * kKX * kGF)) || (rc = dalloc(&d->d_minmax, 8)) ||
         (rc = dalloc(&d->d_io, (size_t)4 * kKX * kGF + kGF)) || (rc = dalloc(&d->d_ptab, 1)) ||
         (rc = dalloc(&d->d_pbc, (size_t)kNBc * kNGP)) || (rc = dalloc(&d->d_rad, kRadSize)) ||
@@ -1101,31 +1342,53 @@ int launch_step_unfused(sml_dynamics *d, int j1, int j2, double dt, double alph,
     return SML_OK;
 }
 
-// the fused step: K1 k_dyn_inv, K2 k_dyn_row, K3 k_dyn_spec
+// the fused step: [k_state_to_m k_st_inv] (k_st_rows | k_st_grid k_st_specx) k_st_spec
+// [k_state_from_m].  chained: the previous launch_step's k_st_spec left the m-major
+// state and this step's gridy output (its next_j2 was this j2); next_j2 > 0: this
+// step's k_st_spec prepares step (.., next_j2) and the state stays m-major.
+
 int launch_step_fused(sml_dynamics *d, int j1, int j2, double dt, double alph, double rob, double wil,
-                      const double *d_phys, bool lradsw, hipStream_t st) {
+                      const double *d_phys, bool lradsw, hipStream_t st, bool chained, int next_j2) {
     const DynTables *T = d->d_tab;
     const bool phys = d->phys_on;
     const int n1 = phys ? kNInv1P : kNInv1, nin = phys ? kNInvP : kNInv;
     const SpectralDev sd = spectral_dev(d->sp);
-    hipLaunchKernelGGL(k_dyn_inv, dim3(kMX, (nin + 7) / 8), dim3(64), 0, st, d->d_state, d->d_phis, T, sd.pinv,
-                       d->d_varm, nin, j2, n1, phys ? 1 : 0);
-    SML_HIP(hipGetLastError());
-    // the Fourier coefficients of the forward transforms go to d_gfwd ([73][48][62] fits)
-    hipLaunchKernelGGL(k_dyn_row, dim3(kIL), dim3(kRowThreads), 0, st, d->d_varm, d->d_gfwd, sd.dinv, sd.dfwd,
-                       sd.cosgr, T, nin, n1, phys ? nullptr : d_phys, d->d_pbc, d->d_rad, d->d_ptab, phys ? 1 : 0,
-                       lradsw ? 1 : 0);
-    SML_HIP(hipGetLastError());
+    if (dt <= 0.0) next_j2 = 0;  // tendencies only: the state does not advance
+    const int conv_blocks = (kMX * kSM + 255) / 256;
+    if (!chained) {
+        hipLaunchKernelGGL(k_state_to_m, dim3(conv_blocks), dim3(256), 0, st, d->d_state, d->d_sm);
+        SML_HIP(hipGetLastError());
+        hipLaunchKernelGGL(k_st_inv, dim3(kMX), dim3(kSpecThreads), 0, st, d->d_sm, d->d_phis, T, sd.pinv, d->d_varm,
+                           j2, n1, nin);
+        SML_HIP(hipGetLastError());
+    }
+    if (phys) {
+        hipLaunchKernelGGL(k_st_grid, dim3(2 * kIL), dim3(kRowThreads), 0, st, d->d_varm, d->d_gfwd, d->d_phys, sd.wa,
+                           sd.cosgr, T, d->d_pbc, d->d_rad, d->d_ptab, lradsw ? 1 : 0, d->d_dbg);
+        SML_HIP(hipGetLastError());
+        hipLaunchKernelGGL(k_st_specx, dim3((kNFwd * kIL + 63) / 64), dim3(64), 0, st, d->d_gfwd, d->d_phys,
+                           d->d_vfm, sd.wa, sd.cosgr);
+        SML_HIP(hipGetLastError());
+    } else {
+        hipLaunchKernelGGL(k_st_rows, dim3(kIL), dim3(kRowThreads), 0, st, d->d_varm, d->d_vfm, sd.wa, sd.cosgr, T,
+                           d_phys, d->d_dbg);
+        SML_HIP(hipGetLastError());
+    }
     const int j4 = (alph == 0.0) ? j2 : 1;
-    hipLaunchKernelGGL(k_dyn_spec, dim3(kMX), dim3(kSpecThreads), 0, st, d->d_gfwd, sd.pfwd, sd.wt, d->d_state,
-                       d->d_tend, d->d_phi, d->d_phis, d->d_tcorh, d->d_qcorh, T, j1, j4, dt, alph, rob, wil);
+    hipLaunchKernelGGL(k_st_spec, dim3(kMX), dim3(kSpecThreads), 0, st, d->d_vfm, sd.pfwd, sd.wt, d->d_sm, d->d_tend,
+                       d->d_phi, d->d_phis, d->d_tcorh, d->d_qcorh, T, j1, j4, dt, alph, rob, wil, sd.pinv, d->d_varm,
+                       next_j2, n1, nin, d->d_dbg);
     SML_HIP(hipGetLastError());
+    if (next_j2 <= 0) {
+        hipLaunchKernelGGL(k_state_from_m, dim3(conv_blocks), dim3(256), 0, st, d->d_sm, d->d_state);
+        SML_HIP(hipGetLastError());
+    }
     return SML_OK;
 }
 
 int launch_step(sml_dynamics *d, int j1, int j2, double dt, double alph, double rob, double wil, const double *d_phys,
-                bool lradsw, hipStream_t st) {
-    return d->fused ? launch_step_fused(d, j1, j2, dt, alph, rob, wil, d_phys, lradsw, st)
+                bool lradsw, hipStream_t st, bool chained = false, int next_j2 = 0) {
+    return d->fused ? launch_step_fused(d, j1, j2, dt, alph, rob, wil, d_phys, lradsw, st, chained, next_j2)
                     : launch_step_unfused(d, j1, j2, dt, alph, rob, wil, d_phys, lradsw, st);
 }
 
@@ -1224,13 +1487,16 @@ extern "C" int sml_dyn_window(sml_dynamics *d, int nleap, double delt, double al
         if (!d->cap_stream) SML_HIP(hipStreamCreateWithFlags(&d->cap_stream, hipStreamNonBlocking));
         hipGraph_t g = nullptr;
         SML_HIP(hipStreamBeginCapture(d->cap_stream, hipStreamCaptureModeThreadLocal));
+        // consecutive steps chained: each step's last kernel prepares the next one's
+        // inverse transforms (j2 = 1 for step(1, 1), then 2)
         d->d_tab = tab[0];
-        int rc = launch_step(d, 1, 1, dts[0], alph, rob, wil, nullptr, entry, d->cap_stream);
+        int rc = launch_step(d, 1, 1, dts[0], alph, rob, wil, nullptr, entry, d->cap_stream, false, 2);
         d->d_tab = tab[1];
-        if (!rc) rc = launch_step(d, 1, 2, dts[1], alph, rob, wil, nullptr, entry, d->cap_stream);
+        if (!rc) rc = launch_step(d, 1, 2, dts[1], alph, rob, wil, nullptr, entry, d->cap_stream, true, nleap > 0 ? 2 : 0);
         d->d_tab = tab[2];
         for (int i = 0; i < nleap && !rc; ++i)
-            rc = launch_step(d, 2, 2, dts[2], alph, rob, wil, nullptr, (1 + i) % kNstrad == 1, d->cap_stream);
+            rc = launch_step(d, 2, 2, dts[2], alph, rob, wil, nullptr, (1 + i) % kNstrad == 1, d->cap_stream, true,
+                             i + 1 < nleap ? 2 : 0);
         hipError_t e = hipStreamEndCapture(d->cap_stream, &g);
         if (rc) {
             if (g) (void)hipGraphDestroy(g);
@@ -1422,5 +1688,14 @@ extern "C" int sml_dyn_step_host(sml_dynamics *d, int j1, int j2, double dt, dou
     }
     if (int rc = sml_dyn_step(d, j1, j2, dt, alph, rob, wil, dp, nullptr)) return rc;
     SML_HIP(hipDeviceSynchronize());
+    return SML_OK;
+}
+
+// diagnostic: the phase stamps of the last fused launches ([2][64][8] wall_clock64
+// ticks, 100 MHz); not part of the ABI header
+extern "C" int sml_dbg_dyn_stamps(sml_dynamics *d, long long *out) {
+    SML_REQUIRE(d && out && d->d_dbg, "stamps not enabled (SML_DYN_STAMPS=1 at creation)");
+    SML_HIP(hipDeviceSynchronize());
+    SML_HIP(hipMemcpy(out, d->d_dbg, 2 * kStampBlocks * kStamps * sizeof(long long), hipMemcpyDeviceToHost));
     return SML_OK;
 }

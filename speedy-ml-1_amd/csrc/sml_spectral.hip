@@ -11,9 +11,10 @@
 //     hemispherically symmetric part, even n the antisymmetric part, as gridy does);
 //     N = 24 Gaussian latitudes (padded to 32).  P_m tiles come from a masked
 //     table (the triangular T30 mask nsh2 is baked in as exact zeros).
-//   Fourier (per field):  grid[lat][lon] = varm[lat][c] * D[c][lon]
-//     M = 48 latitudes, N = 96 longitudes, K = 62 packed coefficients (padded to 64).
-//     D is the real-DFT matrix of FFTPACK's half-complex convention.
+//   Fourier (per latitude row): FFTPACK's real FFT (rfftb / rfftf for n = 96,
+//     sml_fft.hpp) in the reference's operation order, many rows x fields per block
+//     in LDS -- bit-identical to the reference's gridx / specx, and ~7x fewer flops
+//     than a dense DFT.
 //
 // MFMA f64 16x16x4 operand map (cdna_hip_programming.md section 3): lane l holds
 // A[l&15][l>>4] and B[l>>4][l&15]; the 4 results per lane are
@@ -24,6 +25,7 @@
 #include <new>
 #include <vector>
 
+#include "sml_fft.hpp"
 #include "sml_spectral_tables.hpp"
 
 using namespace sml;
@@ -44,6 +46,7 @@ struct sml_spectral {
     double *d_pfwd;   // [m][n][24]: masked (ll <= ntrun1 and n <= ntrun1-1)
     double *d_dinv;   // [64][96]
     double *d_dfwd;   // [96][64]
+    double *d_wa;     // FFTPACK twiddles for n = 96 (rffti1)
     double *d_wt;     // [24]
     double *d_cosgr;  // [48]
     double *d_cosgr2; // [48]
@@ -101,61 +104,55 @@ __global__ __launch_bounds__(64) void k_gridy(const double *__restrict__ spec, d
     }
 }
 
-// gridx: varm[f][lat][62] -> grid[f][lat][96]  (one wave per (field, 16-latitude
-// group g, 16-longitude tile w): blockIdx.x = field, blockIdx.y = 3 w + g).  The
-// first ncos1 fields are kcos = 1, the rest kcos = 2 (x cosgr), so one launch can
-// carry a batch holding both kinds.
-__global__ __launch_bounds__(64) void k_gridx(const double *__restrict__ varm, double *__restrict__ grid,
-                                              const double *__restrict__ dinv, const double *__restrict__ cosgr,
-                                              int ncos1) {
-    const int f = blockIdx.x;
-    const int w = blockIdx.y / 3, j0 = 16 * (blockIdx.y % 3);
-    const int l = threadIdx.x, r = l & 15, kk = l >> 4;
-    const double *vr = varm + (size_t)f * kVarmField + (j0 + r) * kMX2;
-    d4 acc = {0, 0, 0, 0};
-#pragma unroll 8
-    for (int s = 0; s < kCPad / 4; ++s) {
-        const int c = 4 * s + kk;
-        const double b = dinv[c * kIX + 16 * w + r];
-        const double a = c < kMX2 ? vr[c] : 0.0;
-        acc = MFMA64(a, b, acc);
-    }
-    double *g = grid + (size_t)f * kGridField + 16 * w + r;
+// gridx / specx: FFTPACK's real FFT along each latitude row, one (field, row)
+// transform per thread held in registers (sml_fft.hpp rfftb96_reg / rfftf96_reg).
+constexpr int kFftThreads = 64;
+
+// gridx (spe_subfft_fftpack.f90:15-51): fvar(1) = varm(1) (Im of m = 0 dropped),
+// fvar(m-1) = varm(m) for m = 3..mx2, 0 beyond; rfftb; x cosgr(j) for kcos = 2 (the
+// fields from ncos1 on)
+__global__ __launch_bounds__(kFftThreads) void k_gridx(const double *__restrict__ varm, double *__restrict__ grid,
+                                                       const double *__restrict__ wa, const double *__restrict__ cosgr,
+                                                       int nf, int ncos1) {
+    const int id = blockIdx.x * kFftThreads + threadIdx.x;
+    if (id >= nf * kIL) return;
+    const int f = id / kIL, j = id % kIL;
+    const double *v = varm + (size_t)f * kVarmField + j * kMX2;
+    double x[kFftN];
+    x[0] = v[0];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int j = j0 + kk + 4 * q;
-        double v = acc[q];
-        if (f >= ncos1) v = v * cosgr[j];
-        g[j * kIX] = v;
-    }
+    for (int e = 1; e <= kMX2 - 2; ++e) x[e] = v[e + 1];
+#pragma unroll
+    for (int e = kMX2 - 1; e < kFftN; ++e) x[e] = 0.0;
+    fft::rfftb96_reg(x, wa);
+    const double cj = f >= ncos1 ? cosgr[j] : 1.0;
+    double *g = grid + (size_t)f * kGridField + j * kIX;
+#pragma unroll
+    for (int e = 0; e < kFftN; ++e) g[e] = f >= ncos1 ? x[e] * cj : x[e];
 }
 
-// specx: grid[f][lat][96] (the first nscaled fields x scale[lat]) -> varm[f][lat][62]
-// (one wave per (field, 16-latitude group g, 16-coefficient tile w):
-// blockIdx.x = field, blockIdx.y = 3 w + g)
-__global__ __launch_bounds__(64) void k_specx(const double *__restrict__ grid, double *__restrict__ varm,
-                                              const double *__restrict__ dfwd, const double *__restrict__ scale_tab,
-                                              int nscaled) {
-    const int f = blockIdx.x;
-    const int w = blockIdx.y / 3, j0 = 16 * (blockIdx.y % 3);
-    const int l = threadIdx.x, r = l & 15, kk = l >> 4;
-    const double *g = grid + (size_t)f * kGridField + (j0 + r) * kIX;
-    const bool scale = scale_tab && f < nscaled;  // block-uniform
-    const double s0 = scale ? scale_tab[j0 + r] : 1.0;
-    d4 acc = {0, 0, 0, 0};
-#pragma unroll 8
-    for (int s = 0; s < kIX / 4; ++s) {
-        const int i = 4 * s + kk;
-        const double b = dfwd[i * kCPad + 16 * w + r];
-        double a = g[i];
-        if (scale) a = a * s0;  // vdspec's ug*cosgr(j) / ug*cosgr2(j) (spe_spectral.f90:430-445)
-        acc = MFMA64(a, b, acc);
-    }
-    const int c = 16 * w + r;
-    if (c >= kMX2) return;
-    double *vr = varm + (size_t)f * kVarmField + c;
+// specx (spe_subfft_fftpack.f90:55-87): fvar = vorg(:, j) (the first nscaled fields
+// x scale_tab(j): vdspec's ug*cosgr(j) / ug*cosgr2(j), spe_spectral.f90:430-445);
+// rfftf; varm(1) = fvar(1)/ix, varm(2) = 0, varm(m) = fvar(m-1)/ix
+__global__ __launch_bounds__(kFftThreads) void k_specx(const double *__restrict__ grid, double *__restrict__ varm,
+                                                       const double *__restrict__ wa,
+                                                       const double *__restrict__ scale_tab, int nf, int nscaled) {
+    const int id = blockIdx.x * kFftThreads + threadIdx.x;
+    if (id >= nf * kIL) return;
+    const int f = id / kIL, j = id % kIL;
+    const double *g = grid + (size_t)f * kGridField + j * kIX;
+    const bool sc = scale_tab && f < nscaled;
+    const double s0 = sc ? scale_tab[j] : 1.0;
+    double x[kFftN];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) vr[(j0 + kk + 4 * q) * kMX2] = acc[q];
+    for (int e = 0; e < kFftN; ++e) x[e] = sc ? g[e] * s0 : g[e];
+    fft::rfftf96_reg(x, wa);
+    const double scale = 1. / (double)kIX;
+    double *v = varm + (size_t)f * kVarmField + j * kMX2;
+    v[0] = x[0] * scale;
+    v[1] = 0.0;
+#pragma unroll
+    for (int c = 2; c < kMX2; ++c) v[c] = x[c - 1] * scale;
 }
 
 // specy: varm[f][lat][62] -> spec[f][n][62]  (one wave per (m, 8-field tile));
@@ -334,6 +331,8 @@ extern "C" int sml_spectral_create(double radius, sml_spectral **out) {
             el2trf[n * kMX + m] = t.el2[n][m];
             el2trf[kNX * kMX + n * kMX + m] = (m + n <= kNTRUN) ? 1.0 : 0.0;  // trfilt (parmtr :103-107)
         }
+    double wa[kFftWa];
+    sml_fft_twiddles(wa);
     auto up = [](double **d, const void *h, size_t bytes) -> int {
         SML_HIP(hipMalloc(d, bytes));
         SML_HIP(hipMemcpy(*d, h, bytes, hipMemcpyHostToDevice));
@@ -344,7 +343,7 @@ extern "C" int sml_spectral_create(double radius, sml_spectral **out) {
         (rc = up(&s->d_dinv, t.dinv, sizeof t.dinv)) || (rc = up(&s->d_dfwd, t.dfwd, sizeof t.dfwd)) ||
         (rc = up(&s->d_wt, t.wt, sizeof t.wt)) || (rc = up(&s->d_cosgr, t.cosgr, sizeof t.cosgr)) ||
         (rc = up(&s->d_cosgr2, t.cosgr2, sizeof t.cosgr2)) || (rc = up(&s->d_coef, coef.data(), coef.size() * 8)) ||
-        (rc = up(&s->d_el2, el2trf.data(), el2trf.size() * 8)) ||
+        (rc = up(&s->d_el2, el2trf.data(), el2trf.size() * 8)) || (rc = up(&s->d_wa, wa, sizeof wa)) ||
         (rc = ensure_work(s, 64))) {
         sml_spectral_destroy(s);
         return rc;
@@ -355,8 +354,8 @@ extern "C" int sml_spectral_create(double radius, sml_spectral **out) {
 
 extern "C" int sml_spectral_destroy(sml_spectral *s) {
     if (!s) return SML_OK;
-    double *ptrs[] = {s->d_pinv,   s->d_pfwd, s->d_dinv, s->d_dfwd, s->d_wt,  s->d_cosgr,
-                      s->d_cosgr2, s->d_coef, s->d_el2,  s->d_work, s->d_hbuf};
+    double *ptrs[] = {s->d_pinv,   s->d_pfwd, s->d_dinv, s->d_dfwd, s->d_wt,   s->d_cosgr,
+                      s->d_cosgr2, s->d_coef, s->d_el2,  s->d_work, s->d_hbuf, s->d_wa};
     for (double *p : ptrs)
         if (p) (void)hipFree(p);
     delete s;
@@ -390,8 +389,8 @@ extern "C" int sml_gridx_batched(sml_spectral *s, const double *d_varm, double *
                                  void *stream) {
     if (int rc = check_ctx(s, nf)) return rc;
     if (nf == 0) return SML_OK;
-    hipLaunchKernelGGL(k_gridx, dim3(nf, 18), dim3(64), 0, (hipStream_t)stream, d_varm, d_grid, s->d_dinv, s->d_cosgr,
-                       kcos == 1 ? nf : 0);
+    hipLaunchKernelGGL(k_gridx, dim3((nf * kIL + kFftThreads - 1) / kFftThreads), dim3(kFftThreads), 0, (hipStream_t)stream,
+                       d_varm, d_grid, s->d_wa, s->d_cosgr, nf, kcos == 1 ? nf : 0);
     SML_HIP(hipGetLastError());
     return SML_OK;
 }
@@ -399,8 +398,8 @@ extern "C" int sml_gridx_batched(sml_spectral *s, const double *d_varm, double *
 extern "C" int sml_specx_batched(sml_spectral *s, const double *d_grid, double *d_varm, int nf, void *stream) {
     if (int rc = check_ctx(s, nf)) return rc;
     if (nf == 0) return SML_OK;
-    hipLaunchKernelGGL(k_specx, dim3(nf, 12), dim3(64), 0, (hipStream_t)stream, d_grid, d_varm, s->d_dfwd,
-                       (const double *)nullptr, 0);
+    hipLaunchKernelGGL(k_specx, dim3((nf * kIL + kFftThreads - 1) / kFftThreads), dim3(kFftThreads), 0, (hipStream_t)stream,
+                       d_grid, d_varm, s->d_wa, (const double *)nullptr, nf, 0);
     SML_HIP(hipGetLastError());
     return SML_OK;
 }
@@ -440,8 +439,9 @@ extern "C" int sml_vdspec_batched(sml_spectral *s, const double *d_ug, const dou
     const double *scale = (kcos == 2) ? s->d_cosgr : s->d_cosgr2;
     double *um = s->d_work, *vm = s->d_work + (size_t)nf * kVarmField;
     double *uc = s->d_work + 2 * s->work_fields * (size_t)kVarmField, *vc = uc + (size_t)nf * kSpecField;
-    hipLaunchKernelGGL(k_specx, dim3(nf, 12), dim3(64), 0, st, d_ug, um, s->d_dfwd, scale, nf);
-    hipLaunchKernelGGL(k_specx, dim3(nf, 12), dim3(64), 0, st, d_vg, vm, s->d_dfwd, scale, nf);
+    const dim3 fg((nf * kIL + kFftThreads - 1) / kFftThreads), fb(kFftThreads);
+    hipLaunchKernelGGL(k_specx, fg, fb, 0, st, d_ug, um, s->d_wa, scale, nf, nf);
+    hipLaunchKernelGGL(k_specx, fg, fb, 0, st, d_vg, vm, s->d_wa, scale, nf, nf);
     hipLaunchKernelGGL(k_specy, dim3(kMX, (nf + 7) / 8), dim3(64), 0, st, um, uc, s->d_pfwd, s->d_wt, nf);
     hipLaunchKernelGGL(k_specy, dim3(kMX, (nf + 7) / 8), dim3(64), 0, st, vm, vc, s->d_pfwd, s->d_wt, nf);
     SML_HIP(hipGetLastError());
@@ -520,6 +520,7 @@ SpectralDev spectral_dev(const sml_spectral *s) {
     d.pfwd = s->d_pfwd;
     d.dinv = s->d_dinv;
     d.dfwd = s->d_dfwd;
+    d.wa = s->d_wa;
     return d;
 }
 
@@ -536,7 +537,8 @@ int spectral_gridx(sml_spectral *s, const double *varm, double *grid, int nf, in
 
 int spectral_gridx_split(sml_spectral *s, const double *varm, double *grid, int nf, int ncos1, hipStream_t st) {
     if (nf <= 0) return SML_OK;
-    hipLaunchKernelGGL(k_gridx, dim3(nf, 18), dim3(64), 0, st, varm, grid, s->d_dinv, s->d_cosgr, ncos1);
+    hipLaunchKernelGGL(k_gridx, dim3((nf * kIL + kFftThreads - 1) / kFftThreads), dim3(kFftThreads), 0, st, varm, grid, s->d_wa,
+                       s->d_cosgr, nf, ncos1);
     SML_HIP(hipGetLastError());
     return SML_OK;
 }
@@ -544,14 +546,16 @@ int spectral_gridx_split(sml_spectral *s, const double *varm, double *grid, int 
 int spectral_specx(sml_spectral *s, const double *grid, double *varm, int nf, int scale, hipStream_t st) {
     if (nf <= 0) return SML_OK;
     const double *sc = scale == 1 ? s->d_cosgr : scale == 2 ? s->d_cosgr2 : nullptr;
-    hipLaunchKernelGGL(k_specx, dim3(nf, 12), dim3(64), 0, st, grid, varm, s->d_dfwd, sc, nf);
+    hipLaunchKernelGGL(k_specx, dim3((nf * kIL + kFftThreads - 1) / kFftThreads), dim3(kFftThreads), 0, st, grid, varm, s->d_wa,
+                       sc, nf, nf);
     SML_HIP(hipGetLastError());
     return SML_OK;
 }
 
 int spectral_specx_split(sml_spectral *s, const double *grid, double *varm, int nf, int nscaled, hipStream_t st) {
     if (nf <= 0) return SML_OK;
-    hipLaunchKernelGGL(k_specx, dim3(nf, 12), dim3(64), 0, st, grid, varm, s->d_dfwd, s->d_cosgr, nscaled);
+    hipLaunchKernelGGL(k_specx, dim3((nf * kIL + kFftThreads - 1) / kFftThreads), dim3(kFftThreads), 0, st, grid, varm, s->d_wa,
+                       s->d_cosgr, nf, nscaled);
     SML_HIP(hipGetLastError());
     return SML_OK;
 }

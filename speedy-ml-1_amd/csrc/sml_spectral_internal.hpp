@@ -17,6 +17,7 @@ struct SpectralDev {
     // [m][n][32 lat], forward [m][n][24 lat]; Fourier inverse [64 c][96 lon],
     // forward [96 lon][64 c]
     const double *pinv, *pfwd, *dinv, *dfwd;
+    const double *wa;  // FFTPACK twiddles for n = 96 (sml_fft.hpp)
 };
 
 const SpectralTables &spectral_host_tables(const sml_spectral *s);

@@ -190,9 +190,10 @@ def test_host_tendencies_rejected_while_gpu_physics_on(dyn, dyn_golden):
 
 @pytest.mark.parametrize("physics", [False, True])
 def test_fused_step_is_bitwise_the_unfused_step(pg, cuda, physics):
-    """The 3-launch fused step (k_dyn_inv, k_dyn_row, k_dyn_spec; SML_DYN_FUSED=1) and
-    the 7/8-launch step (the default) evaluate the same operations in the same
-    order: a window of steps must agree bit for bit (state, radiation state)."""
+    """The fused step (k_st_inv, k_st_rows, [k_phys_add, specx], k_st_spec; chained
+    across the steps of a window) and the 8/9-launch step evaluate the same
+    operations in the same order: a run of steps and windows must agree bit for bit
+    (state, radiation state, tendencies, geopotential)."""
     import os
 
     import torch
@@ -220,7 +221,11 @@ def test_fused_step_is_bitwise_the_unfused_step(pg, cuda, physics):
         d.leapfrog(2, graph=False)
         d.step(2, 2, 0.0, 0.5)  # tendencies only
         torch.cuda.synchronize()
-        out.append((d.get_state(), d.get_rad_state(), d.get_tendencies(), d.get_phi()))
+        tend, phi = d.get_tendencies(), d.get_phi()
+        d.window(24)  # one graph; the fused form chains each step's gridy into the previous step's last kernel
+        d.window(24)
+        torch.cuda.synchronize()
+        out.append((d.get_state(), d.get_rad_state(), tend, phi))
         d.close()
     (a, ra, ta, pa), (b, rb, tb, pb) = out
     for f in oracle.DYN_FIELDS:

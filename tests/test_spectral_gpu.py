@@ -1,9 +1,11 @@
-"""GPU parity of the batched spectral transforms (MFMA f64 Legendre + DFT GEMMs)
-against the oracle and the reference's golden vectors.
+"""GPU parity of the batched spectral transforms (MFMA f64 Legendre GEMMs + FFTPACK-
+order real FFTs) against the oracle and the reference's golden vectors.
 
-Tolerance: the GPU sums in a different order than the reference (MFMA K-blocks,
-DFT instead of FFTPACK), so results agree to fp64 rounding: max |err| <= 1e-12 x
-max |value| of the field (TOL below)."""
+Tolerance: the Legendre stage sums in a different order than the reference (MFMA
+K-blocks) and the oracle restates the FFT as a direct DFT, so results agree to fp64
+rounding: max |err| <= 1e-12 x max |value| of the field (TOL below).  The Fourier
+stage alone (gridx, specx) runs FFTPACK's algorithm in its operation order and is
+compared with the reference's own outputs bit for bit."""
 import numpy as np
 import pytest
 
@@ -102,6 +104,18 @@ def test_golden_vectors(sp, cuda, golden):
     vor, div = sp.vdspec(_t(golden["grid_in"], cuda), _t(golden["grid_in2"], cuda), kcos=2)
     assert _rel(vor.cpu().numpy(), golden["vdspec_k2_vor"]) < 1e-11
     assert _rel(div.cpu().numpy(), golden["vdspec_k2_div"]) < 1e-11
+
+
+def test_fourier_stage_bitwise_vs_reference(sp, cuda, golden):
+    """gridx / specx (spe_subfft_fftpack.f90:15-87, FFTPACK rfftb / rfftf) equal the
+    reference's outputs exactly: specx(grid_in) vs the reference's specx, and
+    gridx(the reference's gridy(spec_in)) vs the reference's grid(spec_in)."""
+    sx = sp.specx(_t(golden["grid_in"], cuda)).cpu().numpy()
+    np.testing.assert_array_equal(sx, golden["specx"])
+    gx = sp.gridx(_t(golden["gridy"], cuda), kcos=1).cpu().numpy()
+    np.testing.assert_array_equal(gx, golden["grid_k1"])
+    gx2 = sp.gridx(_t(golden["gridy"], cuda), kcos=2).cpu().numpy()
+    np.testing.assert_array_equal(gx2, golden["grid_k2"])
 
 
 def test_roundtrip_large_batch(sp, cuda):

@@ -1,0 +1,49 @@
+"""Diagnostic: per-phase durations inside the fused SPEEDY step kernels
+(SML_DYN_STAMPS=1).  python tools/probe_phases.py [phys=1]"""
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "speedy-ml-1_amd"))
+os.environ["SML_DYN_FUSED"] = "1"
+os.environ["SML_DYN_STAMPS"] = "1"
+from speedy_ml_amd._lib import lib  # noqa: E402
+from speedy_ml_amd.dynamics import Dynamics  # noqa: E402
+from speedy_ml_amd.synthetic import dyn_state, phys_boundary  # noqa: E402
+
+phys = (sys.argv[1] if len(sys.argv) > 1 else "1") == "1"
+st, forcing = dyn_state()
+d = Dynamics()
+d.set_forcing(**forcing)
+d.set_state(st)
+if phys:
+    d.set_physics(phys_boundary(d, forcing["phis"]))
+d.set_clock(1, True)
+d.stepone()
+d.leapfrog(4, graph=False)
+torch.cuda.synchronize()
+names = {0: ["load", "gridx", "gridpoint", "specx"], 1: ["load", "specy", "combine", "tail", "inv_inputs", "gridy"]}
+L = lib()
+L.sml_dbg_dyn_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+for rep in range(3):
+    d.leapfrog(1, graph=False)
+    torch.cuda.synchronize()
+    buf = np.zeros((2, 64, 8), dtype=np.int64)
+    assert L.sml_dbg_dyn_stamps(d._h, buf.ctypes.data) == 0
+    for kern, nb in ((0, 48), (1, 31)):
+        b = buf[kern, :nb].astype(np.float64)
+        t0 = b[:, 0].min()
+        nph = len(names[kern])
+        line = [f"k{kern} start spread {(b[:, 0].max() - t0) / 100:.2f}us"]
+        for i in range(nph):
+            if b[:, i + 1].max() == 0:
+                continue
+            dt = (b[:, i + 1] - b[:, i]) / 100.0
+            line.append(f"{names[kern][i]} med {np.median(dt):.2f} max {dt.max():.2f}")
+        last = max(i for i in range(8) if b[:, i].max() > 0)
+        line.append(f"total(max end - min start) {(b[:, last].max() - t0) / 100:.2f}us")
+        print(" | ".join(line))
