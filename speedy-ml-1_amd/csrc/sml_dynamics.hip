@@ -28,9 +28,11 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstddef>
 #include <cstdlib>
 #include <cstring>
 #include <new>
+#include <vector>
 
 #include "sml_dynamics_tables.hpp"
 #include "sml_fft.hpp"
@@ -73,6 +75,7 @@ struct sml_dynamics {
     sml_spectral *sp = nullptr;
     DynTables tab;
     DynTables *d_tab = nullptr;   // current impint slot (one of d_tabs)
+    double *d_tabm = nullptr;     // per slot: TabM of every m (the fused spectral stage's per-m tables)
     DynTables *d_tabs = nullptr;  // kTabSlots device copies keyed by (dt, alph): stepone's
                                   // three impint calls per window become pointer switches
     double slot_key[4][2] = {};
@@ -367,30 +370,116 @@ __global__ __launch_bounds__(64) void k_phys(const double *__restrict__ ug1, con
     }
 }
 
+// Table access for the spectral-space stages of one zonal wavenumber m: GTab reads
+// the DynTables in device memory (unfused kernels), LTab a per-m copy staged in LDS
+// (TabM, the fused k_st_spec).  Vectors by level k, per-(n, m) tables by n, and
+// xj(n, k1, k) = xj[m + n - 1][k1][k] (implic's matrix of ll = m + n).
+struct TabM {
+    double dhs[kKX], dhsr[kKX], fsgr[kKX], tref[kKX], tref1[kKX], tref2[kKX], tref3[kKX];
+    double xgeop1[kKX], xgeop2[kKX], corf[kKX], tcorv[kKX], qcorv[kKX], dhsx[kKX];
+    double xc[kKX][kKX], xd[kKX][kKX];
+    double el2[kNX], elz[kNX], dmp[kNX], dmp1[kNX], dmpd[kNX], dmp1d[kNX], dmps[kNX], dmp1s[kNX], trfilt[kNX];
+    double vddym[kNX], vddyp[kNX], gradym[kNX], gradyp[kNX], uvdx[kNX], uvdym[kNX], uvdyp[kNX];
+    double gradx, pad_;
+    double xj[kNX][kKX][kKX];
+};
+constexpr int kTabMDoubles = (int)(sizeof(TabM) / sizeof(double));
+static_assert(kTabMDoubles % 2 == 0, "TabM is copied in 16-B pieces");
+
+#define SML_TAB_VEC(X) \
+    X(dhs) X(dhsr) X(fsgr) X(tref) X(tref1) X(tref2) X(tref3) X(xgeop1) X(xgeop2) X(corf) X(tcorv) X(qcorv) X(dhsx)
+#define SML_TAB_NM(X)                                                                                       \
+    X(el2) X(elz) X(dmp) X(dmp1) X(dmpd) X(dmp1d) X(dmps) X(dmp1s) X(trfilt) X(vddym) X(vddyp) X(gradym) \
+        X(gradyp) X(uvdx) X(uvdym) X(uvdyp)
+
+struct GTab {
+    const DynTables *T;
+    int m;
+#define X(name) \
+    __device__ double name(int k) const { return T->name[k]; }
+    SML_TAB_VEC(X)
+#undef X
+#define X(name) \
+    __device__ double name##_n(int n) const { return T->name[n][m]; }
+    SML_TAB_NM(X)
+#undef X
+    __device__ double gradx_m() const { return T->gradx[m]; }
+    __device__ double xc(int k1, int k) const { return T->xc[k1][k]; }
+    __device__ double xd(int k1, int k) const { return T->xd[k1][k]; }
+    __device__ double xj(int n, int k1, int k) const { return T->xj[m + n - 1][k1][k]; }
+};
+
+struct LTab {
+    const TabM *t;
+#define X(name) \
+    __device__ double name(int k) const { return t->name[k]; }
+    SML_TAB_VEC(X)
+#undef X
+#define X(name) \
+    __device__ double name##_n(int n) const { return t->name[n]; }
+    SML_TAB_NM(X)
+#undef X
+    __device__ double gradx_m() const { return t->gradx; }
+    __device__ double xc(int k1, int k) const { return t->xc[k1][k]; }
+    __device__ double xd(int k1, int k) const { return t->xd[k1][k]; }
+    __device__ double xj(int n, int k1, int k) const { return t->xj[n][k1][k]; }
+};
+
+// the value at flat index i of m's TabM, read from the DynTables (host: the per-slot
+// TabM copies built at impint time)
+__host__ __device__ inline double tabm_value(const DynTables *__restrict__ T, int m, int i) {
+    const TabM *z = nullptr;
+    const size_t off = (size_t)i * sizeof(double);
+#define X(name)                                                                             \
+    {                                                                                       \
+        const size_t a = offsetof(TabM, name), b = a + sizeof(z->name);                      \
+        if (off >= a && off < b) return T->name[(off - a) / sizeof(double)];                 \
+    }
+    SML_TAB_VEC(X)
+#undef X
+#define X(name)                                                                             \
+    {                                                                                       \
+        const size_t a = offsetof(TabM, name), b = a + sizeof(z->name);                      \
+        if (off >= a && off < b) return T->name[(off - a) / sizeof(double)][m];              \
+    }
+    SML_TAB_NM(X)
+#undef X
+    if (off >= offsetof(TabM, xc) && off < offsetof(TabM, xc) + sizeof(z->xc))
+        return (&T->xc[0][0])[(off - offsetof(TabM, xc)) / sizeof(double)];
+    if (off >= offsetof(TabM, xd) && off < offsetof(TabM, xd) + sizeof(z->xd))
+        return (&T->xd[0][0])[(off - offsetof(TabM, xd)) / sizeof(double)];
+    if (off == offsetof(TabM, gradx)) return T->gradx[m];
+    if (off >= offsetof(TabM, xj)) {
+        const int q = (int)((off - offsetof(TabM, xj)) / sizeof(double)), n = q / (kKX * kKX);
+        return m + n >= 1 ? (&T->xj[m + n - 1][0][0])[q % (kKX * kKX)] : 0.0;
+    }
+    return 0.0;
+}
+
 // vds (spe_spectral.f90:307-349) divergence / vorticity of one coefficient;
 // u(pp, nn), v(pp, nn) read part pp of coefficient (m, nn)
-template <class U, class V>
-__device__ inline void vds_gen(U u, V v, const DynTables *T, int m, int n, int p, double *vor, double *div) {
-    const double gx = T->gradx[m];
+template <class U, class V, class TB>
+__device__ inline void vds_gen(U u, V v, const TB &tb, int n, int p, double *vor, double *div) {
+    const double gx = tb.gradx_m();
     // zp(2)=gradx*u(1), zp(1)=-gradx*u(2); zc likewise from v
     const double zp = p == 1 ? gx * u(0, n) : -gx * u(1, n);
     const double zc = p == 1 ? gx * v(0, n) : -gx * v(1, n);
     if (n == 0) {
-        *vor = zc - T->vddyp[0][m] * u(p, 1);
-        *div = zp + T->vddyp[0][m] * v(p, 1);
+        *vor = zc - tb.vddyp_n(0) * u(p, 1);
+        *div = zp + tb.vddyp_n(0) * v(p, 1);
     } else if (n == kNX - 1) {
-        *vor = T->vddym[n][m] * u(p, kNTRUN1 - 1);
-        *div = -T->vddym[n][m] * v(p, kNTRUN1 - 1);
+        *vor = tb.vddym_n(n) * u(p, kNTRUN1 - 1);
+        *div = -tb.vddym_n(n) * v(p, kNTRUN1 - 1);
     } else {
-        *vor = T->vddym[n][m] * u(p, n - 1) - T->vddyp[n][m] * u(p, n + 1) + zc;
-        *div = -T->vddym[n][m] * v(p, n - 1) + T->vddyp[n][m] * v(p, n + 1) + zp;
+        *vor = tb.vddym_n(n) * u(p, n - 1) - tb.vddyp_n(n) * u(p, n + 1) + zc;
+        *div = -tb.vddym_n(n) * v(p, n - 1) + tb.vddyp_n(n) * v(p, n + 1) + zp;
     }
 }
 
 __device__ inline void vds_at(const double *u, const double *v, const DynTables *T, int m, int n, int p, double *vor,
                               double *div) {
-    vds_gen([&](int pp, int nn) { return u[ci(pp, m, nn)]; }, [&](int pp, int nn) { return v[ci(pp, m, nn)]; }, T, m,
-            n, p, vor, div);
+    vds_gen([&](int pp, int nn) { return u[ci(pp, m, nn)]; }, [&](int pp, int nn) { return v[ci(pp, m, nn)]; },
+            GTab{T, m}, n, p, vor, div);
 }
 
 // combine: spectral tendencies of grtend (:229-278) from the 73 forward transforms
@@ -421,10 +510,10 @@ __global__ void k_dyn_combine(const double *__restrict__ S, double *__restrict__
 // The CW coefficients x 8 levels of a block share sh[2][kx][CW] (LDS) for the
 // vertical couplings (dmeanc, sigdtc, geop, implic's level matrices); every sum
 // runs over k in the reference's order.  The whole block must call it (barriers).
-template <int CW, class SA>
+template <int CW, class SA, class TB>
 __device__ inline void tail_coef(SA S, double *__restrict__ Td, double *__restrict__ phi_out,
                                  const double *__restrict__ phis, const double *__restrict__ tcorh,
-                                 const double *__restrict__ qcorh, int fc, const DynTables *__restrict__ T,
+                                 const double *__restrict__ qcorh, int fc, const TB &tb,
                                  double (*sh)[kKX][CW], int cc, int k, int c, int m, int n, double vordt, double divdt,
                                  double tdt, double trdt, double psdt, int j1, int j4, double dt, double alph,
                                  double rob, double wil) {
@@ -436,7 +525,7 @@ __device__ inline void tail_coef(SA S, double *__restrict__ Td, double *__restri
     __syncthreads();
     double dmeanc = 0.0;
 #pragma unroll
-    for (int kk = 0; kk < kKX; ++kk) dmeanc = dmeanc + sh[0][kk][cc] * T->dhs[kk];
+    for (int kk = 0; kk < kKX; ++kk) dmeanc = dmeanc + sh[0][kk][cc] * tb.dhs(kk);
     psdt = psdt - dmeanc;
     if (m == 0 && n == 0) psdt = 0.0;  // psdt(1,1) = 0
     double sig_k = 0.0, sig_k1 = 0.0;  // sigdtc(k), sigdtc(k+1); sigdtc(1) = sigdtc(kxp) = 0
@@ -444,25 +533,25 @@ __device__ inline void tail_coef(SA S, double *__restrict__ Td, double *__restri
         double sg = 0.0;
 #pragma unroll
         for (int kk = 0; kk < kKX - 1; ++kk) {
-            const double nx_ = sg - T->dhs[kk] * (sh[0][kk][cc] - dmeanc);
+            const double nx_ = sg - tb.dhs(kk) * (sh[0][kk][cc] - dmeanc);
             if (kk == k - 1) sig_k = nx_;
             if (kk == k) sig_k1 = nx_;
             sg = nx_;
         }
     }
-    const double dumk_k = (k == 0) ? 0.0 : sig_k * (T->tref[k] - T->tref[k - 1]);
-    const double dumk_k1 = (k == kKX - 1) ? 0.0 : sig_k1 * (T->tref[k + 1] - T->tref[k]);
-    tdt = tdt - (dumk_k1 + dumk_k) * T->dhsr[k] + T->tref3[k] * (sig_k1 + sig_k) - T->tref2[k] * dmeanc;
+    const double dumk_k = (k == 0) ? 0.0 : sig_k * (tb.tref(k) - tb.tref(k - 1));
+    const double dumk_k1 = (k == kKX - 1) ? 0.0 : sig_k1 * (tb.tref(k + 1) - tb.tref(k));
+    tdt = tdt - (dumk_k1 + dumk_k) * tb.dhsr(k) + tb.tref3(k) * (sig_k1 + sig_k) - tb.tref2(k) * dmeanc;
     // geop(j4)  (dyn_geop.f90:16-32)
-    double phi = phis[fc] + T->xgeop1[kKX - 1] * sh[1][kKX - 1][cc];
+    double phi = phis[fc] + tb.xgeop1(kKX - 1) * sh[1][kKX - 1][cc];
 #pragma unroll
     for (int kk = kKX - 2; kk >= k; --kk)
-        phi = phi + T->xgeop2[kk + 1] * sh[1][kk + 1][cc] + T->xgeop1[kk] * sh[1][kk][cc];
-    if (m == 0 && k >= 1 && k <= kKX - 2) phi = phi + T->corf[k] * (sh[1][k + 1][cc] - sh[1][k - 1][cc]);
+        phi = phi + tb.xgeop2(kk + 1) * sh[1][kk + 1][cc] + tb.xgeop1(kk) * sh[1][kk][cc];
+    if (m == 0 && k >= 1 && k <= kKX - 2) phi = phi + tb.corf(k) * (sh[1][k + 1][cc] - sh[1][k - 1][cc]);
     phi_out[(size_t)k * kSF + c] = phi;
     {
-        const double d1 = phi + kRgas * T->tref[k] * S(4, j4, 0);
-        const double lapd = -(d1 * T->el2[n][m]);
+        const double d1 = phi + kRgas * tb.tref(k) * S(4, j4, 0);
+        const double lapd = -(d1 * tb.el2_n(n));
         divdt = divdt - lapd;
     }
     // ---- implic(divdt, tdt, psdt)  (dyn_implic.f90:22-67)
@@ -472,28 +561,28 @@ __device__ inline void tail_coef(SA S, double *__restrict__ Td, double *__restri
         __syncthreads();
         double ye = 0.0;
 #pragma unroll
-        for (int k1 = 0; k1 < kKX; ++k1) ye = ye + T->xd[k1][k] * sh[0][k1][cc];
-        ye = ye + T->tref1[k] * psdt;
-        sh[1][k][cc] = divdt + T->elz[n][m] * ye;  // yf
+        for (int k1 = 0; k1 < kKX; ++k1) ye = ye + tb.xd(k1, k) * sh[0][k1][cc];
+        ye = ye + tb.tref1(k) * psdt;
+        sh[1][k][cc] = divdt + tb.elz_n(n) * ye;  // yf
         __syncthreads();
         divdt = 0.0;
         const int ll = m + n;
         if (ll != 0) {
 #pragma unroll
-            for (int k1 = 0; k1 < kKX; ++k1) divdt = divdt + T->xj[ll - 1][k1][k] * sh[1][k1][cc];
+            for (int k1 = 0; k1 < kKX; ++k1) divdt = divdt + tb.xj(n, k1, k) * sh[1][k1][cc];
         }
         sh[0][k][cc] = divdt;
         __syncthreads();
 #pragma unroll
-        for (int kk = 0; kk < kKX; ++kk) psdt = psdt - sh[0][kk][cc] * T->dhsx[kk];
+        for (int kk = 0; kk < kKX; ++kk) psdt = psdt - sh[0][kk][cc] * tb.dhsx(kk);
 #pragma unroll
-        for (int k1 = 0; k1 < kKX; ++k1) tdt = tdt + T->xc[k1][k] * sh[0][k1][cc];
+        for (int k1 = 0; k1 < kKX; ++k1) tdt = tdt + tb.xc(k1, k) * sh[0][k1][cc];
     }
     // ---- horizontal diffusion (dyn_step.f90:60-112, hordif :130-151)
-    const double dmp = T->dmp[n][m], dmp1 = T->dmp1[n][m], dmpd = T->dmpd[n][m], dmp1d = T->dmp1d[n][m];
+    const double dmp = tb.dmp_n(n), dmp1 = tb.dmp1_n(n), dmpd = tb.dmpd_n(n), dmp1d = tb.dmp1d_n(n);
     vordt = (vordt - dmp * S(0, 1, k)) * dmp1;
     divdt = (divdt - dmpd * S(1, 1, k)) * dmp1d;
-    const double ctmp = S(2, 1, k) + tcorh[fc] * T->tcorv[k];
+    const double ctmp = S(2, 1, k) + tcorh[fc] * tb.tcorv(k);
     tdt = (tdt - dmp * ctmp) * dmp1;
     if (k == 0) {
         if (m == 0) {  // stratospheric drag on the zonal mean, top level (:78-82)
@@ -501,13 +590,13 @@ __device__ inline void tail_coef(SA S, double *__restrict__ Td, double *__restri
             vordt = vordt - sdrag * S(0, 1, 0);
             divdt = divdt - sdrag * S(1, 1, 0);
         }
-        const double dmps = T->dmps[n][m], dmp1s = T->dmp1s[n][m];
+        const double dmps = tb.dmps_n(n), dmp1s = tb.dmp1s_n(n);
         vordt = (vordt - dmps * S(0, 1, 0)) * dmp1s;
         divdt = (divdt - dmps * S(1, 1, 0)) * dmp1s;
         tdt = (tdt - dmps * ctmp) * dmp1s;
     }
     {
-        const double cq = S(3, 1, k) + qcorh[fc] * T->qcorv[k];
+        const double cq = S(3, 1, k) + qcorh[fc] * tb.qcorv(k);
         trdt = (trdt - dmpd * cq) * dmp1d;
     }
     if (dt <= 0.0) {  // tendencies only (dyn_step.f90:109)
@@ -520,7 +609,7 @@ __device__ inline void tail_coef(SA S, double *__restrict__ Td, double *__restri
     }
     // ---- timint with the Robert-Williams filter (dyn_step.f90:153-190)
     const double eps = (j1 == 1) ? 0.0 : rob;
-    const double trf = T->trfilt[n][m];
+    const double trf = tb.trfilt_n(n);
     auto timint = [&](int var, int kk, double fdt) {
         fdt = fdt * trf;  // trunct
         double &f1 = S(var, 1, kk);
@@ -555,7 +644,7 @@ __global__ __launch_bounds__(256) void k_dyn_tail(double *__restrict__ st, doubl
         const size_t off = var == 0 ? kOffVor : var == 1 ? kOffDiv : var == 2 ? kOffT : kOffTr;
         return st[off + ((size_t)(lev - 1) * kKX + kk) * kSF + c];
     };
-    tail_coef<kTailC>(S, Td, phi_out, phis, tcorh, qcorh, c, T, sh, cc, k, c, m, n, Td[kTVor + (size_t)k * kSF + c],
+    tail_coef<kTailC>(S, Td, phi_out, phis, tcorh, qcorh, c, GTab{T, m}, sh, cc, k, c, m, n, Td[kTVor + (size_t)k * kSF + c],
                       Td[kTDiv + (size_t)k * kSF + c], Td[kTT + (size_t)k * kSF + c], Td[kTTr + (size_t)k * kSF + c],
                       Td[kTPs + c], j1, j4, dt, alph, rob, wil);
 }
@@ -594,7 +683,7 @@ __device__ inline int smi(int var, int lev, int k, int cc) { return ((var * 2 + 
 
 // diagnostic phase stamps (SML_DYN_STAMPS=1 at creation): thread 0 of each block
 // writes wall_clock64() (100 MHz) at phase boundaries, [kernel][block][8]
-constexpr int kStampBlocks = 64, kStamps = 8;
+constexpr int kStampKernels = 4, kStampBlocks = 96, kStamps = 8;  // kernels: grid/rows, spec, specx, last spec
 __device__ inline void stamp(long long *dbg, int kern, int i) {
     if (dbg && threadIdx.x == 0) dbg[((size_t)kern * kStampBlocks + blockIdx.x) * kStamps + i] = wall_clock64();
 }
@@ -633,71 +722,57 @@ __global__ void k_state_from_m(const double *__restrict__ sm, double *__restrict
 // The inverse-transform inputs of one m (k_dyn_prep's fields, same expressions)
 // from the m's state slice Sst (smi layout); writes In[f][kCW] for f < nin.  The
 // whole block calls it.
-__device__ inline void inv_inputs(const double *Sst, double *In, const double *phis_m, const DynTables *__restrict__ T,
-                                  int m, int j2, int n1, int nin) {
-    auto sv = [&](int var, int lev, int k, int cc) { return Sst[smi(var, lev, k, cc)]; };
-    for (int idx = threadIdx.x; idx < nin * kCW; idx += blockDim.x) {
-        const int f = idx / kCW, cc = idx % kCW, n = cc >> 1, p = cc & 1;
+template <class TB>
+__device__ inline void inv_inputs(const double *Sst, double *In, const double *phis_m, const TB &tb, int m, int j2,
+                                  int n1, int nin) {
+    // one thread per (coefficient cc = 2 n + p, level k) (512 threads): the fields of
+    // level k, in the same expressions as k_dyn_prep
+    const bool phys = nin > kNInv;
+    const int cc = threadIdx.x & (kCW - 1), k = threadIdx.x / kCW, n = cc >> 1, p = cc & 1;
+    auto sv = [&](int var, int lev, int kk, int c2) { return Sst[smi(var, lev, kk, c2)]; };
+    auto put = [&](int f, double v) { In[f * kCW + cc] = v; };
+#pragma unroll
+    for (int var = 0; var < 4; ++var) put(var * kKX + k, sv(var, j2, k, cc));
+    // uvspec (spe_spectral.f90:351-387) of level lev at k -> ucos (field fu), vcos (fv)
+    auto uvspec = [&](int lev, int fu, int fv) {
+        auto vor = [&](int pp, int nn) { return sv(0, lev, k, 2 * nn + pp); };
+        auto div = [&](int pp, int nn) { return sv(1, lev, k, 2 * nn + pp); };
+        const double ux = tb.uvdx_n(n);
+        double u, v;
+        const double zc = p == 1 ? ux * div(0, n) : -ux * div(1, n);
+        if (n == 0) u = zc - tb.uvdyp_n(0) * vor(p, 1);
+        else if (n == kNX - 1) u = tb.uvdym_n(n) * vor(p, kNTRUN1 - 1);
+        else u = tb.uvdym_n(n) * vor(p, n - 1) - tb.uvdyp_n(n) * vor(p, n + 1) + zc;
+        const double zp = p == 1 ? ux * vor(0, n) : -ux * vor(1, n);
+        if (n == 0) v = zp + tb.uvdyp_n(0) * div(p, 1);
+        else if (n == kNX - 1) v = -tb.uvdym_n(n) * div(p, kNTRUN1 - 1);
+        else v = -tb.uvdym_n(n) * div(p, n - 1) + tb.uvdyp_n(n) * div(p, n + 1) + zp;
+        put(fu, u);
+        put(fv, v);
+    };
+    uvspec(j2, n1 + k, n1 + kKX + k);
+    if (k == 0) {  // grad(ps(j2))
+        put(n1 + 2 * kKX, p == 1 ? tb.gradx_m() * sv(4, j2, 0, 2 * n) : -tb.gradx_m() * sv(4, j2, 0, 2 * n + 1));
         double v;
-        if (f < 4 * kKX) {
-            v = sv(f / kKX, j2, f % kKX, cc);
-        } else if (f < n1) {  // phypar's level-1 inputs (phys only)
-            if (f < kPQ1) {
-                v = sv(2, 1, f - kPT1, cc);
-            } else if (f < kPPhi1) {
-                v = sv(3, 1, f - kPQ1, cc);
-            } else if (f < kPPs1) {  // geop(1) (geop_at)
-                const int k = f - kPPhi1;
-                double phi = phis_m[cc] + T->xgeop1[kKX - 1] * sv(2, 1, kKX - 1, cc);
-                for (int kk = kKX - 2; kk >= k; --kk)
-                    phi = phi + T->xgeop2[kk + 1] * sv(2, 1, kk + 1, cc) + T->xgeop1[kk] * sv(2, 1, kk, cc);
-                if (m == 0 && k >= 1 && k <= kKX - 2)
-                    phi = phi + T->corf[k] * (sv(2, 1, k + 1, cc) - sv(2, 1, k - 1, cc));
-                v = phi;
-            } else {
-                v = sv(4, 1, 0, cc);
-            }
-        } else {
-            int g = f - n1;
-            if (g == 2 * kKX || g == 2 * kKX + 1) {  // grad(ps(j2))
-                if (g == 2 * kKX) {
-                    v = p == 1 ? T->gradx[m] * sv(4, j2, 0, 2 * n) : -T->gradx[m] * sv(4, j2, 0, 2 * n + 1);
-                } else if (n == 0) {
-                    v = T->gradyp[0][m] * sv(4, j2, 0, 2 + p);
-                } else if (n == kNX - 1) {
-                    v = -T->gradym[n][m] * sv(4, j2, 0, 2 * (kNTRUN1 - 1) + p);
-                } else {
-                    v = -T->gradym[n][m] * sv(4, j2, 0, 2 * (n - 1) + p) + T->gradyp[n][m] * sv(4, j2, 0, 2 * (n + 1) + p);
-                }
-            } else {  // uvspec of level j2, or of level 1 (ucos1 / vcos1)
-                int lev = j2;
-                if (g > 2 * kKX + 1) {
-                    g -= 2 * kKX + 2;
-                    lev = 1;
-                }
-                const int k = g % kKX;
-                const bool vcos = g >= kKX;
-                auto vor = [&](int pp, int nn) { return sv(0, lev, k, 2 * nn + pp); };
-                auto div = [&](int pp, int nn) { return sv(1, lev, k, 2 * nn + pp); };
-                const double ux = T->uvdx[n][m];
-                if (!vcos) {
-                    const double zc = p == 1 ? ux * div(0, n) : -ux * div(1, n);
-                    if (n == 0) v = zc - T->uvdyp[0][m] * vor(p, 1);
-                    else if (n == kNX - 1) v = T->uvdym[n][m] * vor(p, kNTRUN1 - 1);
-                    else v = T->uvdym[n][m] * vor(p, n - 1) - T->uvdyp[n][m] * vor(p, n + 1) + zc;
-                } else {
-                    const double zp = p == 1 ? ux * vor(0, n) : -ux * vor(1, n);
-                    if (n == 0) v = zp + T->uvdyp[0][m] * div(p, 1);
-                    else if (n == kNX - 1) v = -T->uvdym[n][m] * div(p, kNTRUN1 - 1);
-                    else v = -T->uvdym[n][m] * div(p, n - 1) + T->uvdyp[n][m] * div(p, n + 1) + zp;
-                }
-            }
-        }
-        In[f * kCW + cc] = v;
+        if (n == 0) v = tb.gradyp_n(0) * sv(4, j2, 0, 2 + p);
+        else if (n == kNX - 1) v = -tb.gradym_n(n) * sv(4, j2, 0, 2 * (kNTRUN1 - 1) + p);
+        else v = -tb.gradym_n(n) * sv(4, j2, 0, 2 * (n - 1) + p) + tb.gradyp_n(n) * sv(4, j2, 0, 2 * (n + 1) + p);
+        put(n1 + 2 * kKX + 1, v);
     }
+    if (!phys) return;
+    // phypar's level-1 inputs: t1, q1, geop(1) (geop_at), ps1, ucos1, vcos1
+    put(kPT1 + k, sv(2, 1, k, cc));
+    put(kPQ1 + k, sv(3, 1, k, cc));
+    double phi = phis_m[cc] + tb.xgeop1(kKX - 1) * sv(2, 1, kKX - 1, cc);
+    for (int kk = kKX - 2; kk >= k; --kk)
+        phi = phi + tb.xgeop2(kk + 1) * sv(2, 1, kk + 1, cc) + tb.xgeop1(kk) * sv(2, 1, kk, cc);
+    if (m == 0 && k >= 1 && k <= kKX - 2) phi = phi + tb.corf(k) * (sv(2, 1, k + 1, cc) - sv(2, 1, k - 1, cc));
+    put(kPPhi1 + k, phi);
+    if (k == 0) put(kPPs1, sv(4, 1, 0, cc));
+    uvspec(1, n1 + 2 * kKX + 2 + k, n1 + 3 * kKX + 2 + k);
 }
 
-// gridy of In[f][kCW] (this m) -> varm[f][lat][62] (k_gridy's tiling: one wave per
+// gridy of In[f][kCW] (this m) -> vim[m][f][lat][p] (k_gridy's tiling: one wave per
 // 8-field x Re/Im tile, waves of the block stride over the tiles)
 __device__ inline void gridy_m(const double *In, const double *__restrict__ pinv, double *__restrict__ varm, int m,
                                int nf) {
@@ -735,18 +810,20 @@ __device__ inline void gridy_m(const double *In, const double *__restrict__ pinv
             const int row = kk + 4 * q;
             const int f = f0 + (row >> 1);
             if (f >= nf) continue;
-            double *vr = varm + (size_t)f * kVF + 2 * m + (row & 1);
+            // m-major inverse Fourier coefficients vim[m][f][lat][p]: lanes (r, kk) of a
+            // q write 16 consecutive latitudes x (Re, Im) = 256 contiguous bytes
+            double *vr = varm + ((size_t)m * kNInvMax + f) * (kIL * 2) + (row & 1);
             {
                 const int j = r;
                 const double sym = acc00[q], asym = acc10[q];
-                vr[(kIL - 1 - j) * kMX2] = sym + asym;
-                vr[j * kMX2] = sym - asym;
+                vr[(kIL - 1 - j) * 2] = sym + asym;
+                vr[j * 2] = sym - asym;
             }
             const int j = 16 + r;
             if (j < kIY) {
                 const double sym = acc01[q], asym = acc11[q];
-                vr[(kIL - 1 - j) * kMX2] = sym + asym;
-                vr[j * kMX2] = sym - asym;
+                vr[(kIL - 1 - j) * 2] = sym + asym;
+                vr[j * 2] = sym - asym;
             }
         }
     }
@@ -778,7 +855,7 @@ __global__ __launch_bounds__(kSpecThreads) void k_st_inv(const double *__restric
         reinterpret_cast<double2 *>(Sst)[i] = reinterpret_cast<const double2 *>(src)[i];
     for (int cc = threadIdx.x; cc < kCW; cc += blockDim.x) Fm[cc] = phis[ci(cc & 1, m, cc >> 1)];
     __syncthreads();
-    inv_inputs(Sst, In, Fm, T, m, j2, n1, nin);
+    inv_inputs(Sst, In, Fm, GTab{T, m}, m, j2, n1, nin);
     __syncthreads();
     gridy_m(In, pinv, varm, m, nin);
 }
@@ -794,11 +871,13 @@ static_assert(kNInvMax <= kRowThreads && kNFwd <= kRowThreads && kIX <= kRowThre
 // for kcos = 2; the 96 values into A[lon][f]
 __device__ inline void row_gridx(double *A, const double *__restrict__ varm, const double *__restrict__ wa, int f,
                                  int j, bool kcos2, double cj) {
-    const double *v = varm + (size_t)f * kVF + j * kMX2;
+    // the m-major coefficients vim[m][f][lat][p] of (f, j): coefficient c = 2 m + p
+    const double *v = varm + (size_t)f * (kIL * 2) + j * 2;
+    auto V = [&](int c) { return v[(size_t)(c >> 1) * kNInvMax * (kIL * 2) + (c & 1)]; };
     double x[kFftN];
-    x[0] = v[0];
+    x[0] = V(0);
 #pragma unroll
-    for (int e = 1; e <= kMX2 - 2; ++e) x[e] = v[e + 1];
+    for (int e = 1; e <= kMX2 - 2; ++e) x[e] = V(e + 1);
 #pragma unroll
     for (int e = kMX2 - 1; e < kFftN; ++e) x[e] = 0.0;
     fft::rfftb96_reg(x, wa);
@@ -827,14 +906,16 @@ __global__ __launch_bounds__(kRowThreads) void k_st_rows(const double *__restric
                                                          const double *__restrict__ cosgr,
                                                          const DynTables *__restrict__ T,
                                                          const double *__restrict__ Pext, long long *dbg) {
-    __shared__ double A[kFftN * kRowLd], B[kFftN * kRowLd];
+    __shared__ double A[kFftN * kRowLd], B[kFftN * kRowLd], was[kFftWa];
     constexpr int n1 = kNInv1, nin = kNInv;
     const int j = blockIdx.x, tid = threadIdx.x;
+    if (tid < kFftWa) was[tid] = wa[tid];
+    __syncthreads();
     const double cj = cosgr[j];
     stamp(dbg, 0, 0);
     stamp(dbg, 0, 1);
     // gridx: one field per thread
-    if (tid < nin) row_gridx(A, varm, wa, tid, j, tid >= n1, cj);
+    if (tid < nin) row_gridx(A, varm, was, tid, j, tid >= n1, cj);
     __syncthreads();
     stamp(dbg, 0, 2);
     // one thread per grid column: grid-point dynamics, the forward-transform inputs into B
@@ -861,7 +942,7 @@ __global__ __launch_bounds__(kRowThreads) void k_st_rows(const double *__restric
         double x[kFftN];
 #pragma unroll
         for (int e = 0; e < kFftN; ++e) x[e] = tid < kNFwdScaled ? B[e * kRowLd + tid] * cj : B[e * kRowLd + tid];
-        row_specx(x, vfm, wa, tid, j);
+        row_specx(x, vfm, was, tid, j);
     }
     __syncthreads();
     stamp(dbg, 0, 4);
@@ -876,23 +957,27 @@ __global__ __launch_bounds__(kRowThreads) void k_st_grid(
     const double *__restrict__ varm, double *__restrict__ F, double *__restrict__ P, const double *__restrict__ wa,
     const double *__restrict__ cosgr, const DynTables *__restrict__ T, const double *__restrict__ bc,
     double *__restrict__ rad, const PhysTables *__restrict__ PT, int lradsw, long long *dbg) {
-    __shared__ double A[kFftN * kRowLd];
+    __shared__ double A[kFftN * kRowLd], was[kFftWa];
     constexpr int n1 = kNInv1P, nin = kNInvP;
+    if (threadIdx.x < kFftWa) was[threadIdx.x] = wa[threadIdx.x];
+    __syncthreads();
     constexpr int nphys = (n1 - kPT1) + (nin - (n1 + 2 * kKX + 2));  // 25 + 16 = 41
     const bool is_phys = blockIdx.x >= kIL;
     const int j = is_phys ? blockIdx.x - kIL : blockIdx.x, tid = threadIdx.x;
     const double cj = cosgr[j];
+    stamp(dbg, 0, 0);
     // gridx of the role's fields (field index f of the step's nin inverse transforms)
     if (!is_phys) {
         if (tid < kNInv) {
             const int f = tid < kNInv1 ? tid : n1 + (tid - kNInv1);  // [vor div t tr] | [ucos vcos psdx psdy]
-            row_gridx(A, varm, wa, f, j, f >= n1, cj);
+            row_gridx(A, varm, was, f, j, f >= n1, cj);
         }
     } else if (tid < nphys) {
         const int f = tid < n1 - kPT1 ? kPT1 + tid : n1 + 2 * kKX + 2 + (tid - (n1 - kPT1));
-        row_gridx(A, varm, wa, f, j, f >= n1, cj);
+        row_gridx(A, varm, was, f, j, f >= n1, cj);
     }
     __syncthreads();
+    stamp(dbg, 0, 1);
     if (tid >= kIX) return;
     const int i = tid, pt = j * kIX + i;
     auto g = [&](int f) { return A[i * kRowLd + f]; };
@@ -900,6 +985,7 @@ __global__ __launch_bounds__(kRowThreads) void k_st_grid(
         double dummy[kKX];
         gridpoint_column(j, n1, g, false, dummy, dummy, dummy, dummy,
                          [&](int f, double v) { F[(size_t)f * kGF + pt] = v; }, T);
+        stamp(dbg, 0, 2);
         return;
     }
     double ua[kKX], va[kKX], ta[kKX], qa[kKX], ph[kKX], ut[kKX], vt[kKX], tt[kKX], qt[kKX];
@@ -919,31 +1005,74 @@ __global__ __launch_bounds__(kRowThreads) void k_st_grid(
         P[(size_t)(2 * kKX + k) * kGF + pt] = tt[k];
         P[(size_t)(3 * kKX + k) * kGF + pt] = qt[k];
     }
+    stamp(dbg, 0, 2);
 }
 
-// specx (with GPU physics): one (field, row) transform per thread; F[f][ngp] + the
-// physics tendencies P of the u, v, t, q fields (the dynamical tendency first, as
-// grtend adds them), x cosgr(j) for vdspec's inputs, rfftf -> m-major coefficients
-__global__ __launch_bounds__(64) void k_st_specx(const double *__restrict__ F, const double *__restrict__ P,
-                                                 double *__restrict__ vfm, const double *__restrict__ wa,
-                                                 const double *__restrict__ cosgr) {
-    const int id = blockIdx.x * 64 + threadIdx.x;
-    if (id >= kNFwd * kIL) return;
-    const int f = id / kIL, j = id % kIL;
-    // F field -> tendency slot of P: u 0..7, v 24..31, t 56..63, q 64..71
-    const int pf = f < kKX ? f : (f >= 3 * kKX && f < 4 * kKX) ? kKX + f - 3 * kKX
-                 : (f >= 7 * kKX && f < 9 * kKX) ? 2 * kKX + f - 7 * kKX : -1;
-    const double *g = F + (size_t)f * kGF + j * kIX;
-    const double *pp = P + (size_t)(pf < 0 ? 0 : pf) * kGF + j * kIX;
-    const double cj = cosgr[j];
-    double x[kFftN];
+// specx (with GPU physics), one latitude row per block: the row's F[f][ngp] and the
+// physics tendencies P[4 kx][ngp] staged in LDS with coalesced loads (all issued
+// before the first LDS store; 8 waves for the memory-level parallelism); then one
+// field per thread: F (+ P for the u, v, t, q fields: the dynamical tendency first,
+// as grtend adds them), x cosgr(j) for vdspec's inputs, rfftf -> m-major coefficients
+constexpr int kSpecxThreads = 512;
+__global__ __launch_bounds__(kSpecxThreads) void k_st_specx(const double *__restrict__ F, const double *__restrict__ P,
+                                                            double *__restrict__ vfm, const double *__restrict__ wa,
+                                                            const double *__restrict__ cosgr, long long *dbg) {
+    constexpr int LB = kNFwd + 2, LP = 4 * kKX + 1;        // element-major: lanes (fields) hit distinct banks
+    __shared__ double B[kIX * LB], PB[kIX * LP];            // [lon][f], [lon][slot]
+    __shared__ double was[kFftWa];                          // twiddles: LDS broadcast reads inside the FFT
+    const int j = blockIdx.x, tid = threadIdx.x;
+    stamp(dbg, 2, 0);
+    if (tid < kFftWa) was[tid] = wa[tid];
+    {
+        constexpr int NF = kNFwd * (kIX / 2), NP = 4 * kKX * (kIX / 2);
+        constexpr int RF = (NF + kSpecxThreads - 1) / kSpecxThreads, RP = (NP + kSpecxThreads - 1) / kSpecxThreads;
+        double2 rf[RF], rp[RP];
 #pragma unroll
-    for (int e = 0; e < kFftN; ++e) {
-        double v = g[e];
-        if (pf >= 0) v = v + pp[e];
-        x[e] = f < kNFwdScaled ? v * cj : v;
+        for (int q = 0; q < RF; ++q) {
+            const int i = tid + q * kSpecxThreads, ii = i < NF ? i : NF - 1;
+            rf[q] = reinterpret_cast<const double2 *>(F + (size_t)(ii / (kIX / 2)) * kGF + j * kIX)[ii % (kIX / 2)];
+        }
+#pragma unroll
+        for (int q = 0; q < RP; ++q) {
+            const int i = tid + q * kSpecxThreads, ii = i < NP ? i : NP - 1;
+            rp[q] = reinterpret_cast<const double2 *>(P + (size_t)(ii / (kIX / 2)) * kGF + j * kIX)[ii % (kIX / 2)];
+        }
+#pragma unroll
+        for (int q = 0; q < RF; ++q) {
+            const int i = tid + q * kSpecxThreads, f = i / (kIX / 2), e = 2 * (i % (kIX / 2));
+            if (i < NF) {
+                B[e * LB + f] = rf[q].x;
+                B[(e + 1) * LB + f] = rf[q].y;
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < RP; ++q) {
+            const int i = tid + q * kSpecxThreads, f = i / (kIX / 2), e = 2 * (i % (kIX / 2));
+            if (i < NP) {
+                PB[e * LP + f] = rp[q].x;
+                PB[(e + 1) * LP + f] = rp[q].y;
+            }
+        }
     }
-    row_specx(x, vfm, wa, f, j);
+    __syncthreads();
+    stamp(dbg, 2, 1);
+    if (tid < kNFwd) {
+        const int f = tid;
+        // F field -> tendency slot of P: u 0..7, v 24..31, t 56..63, q 64..71
+        const int pf = f < kKX ? f : (f >= 3 * kKX && f < 4 * kKX) ? kKX + f - 3 * kKX
+                     : (f >= 7 * kKX && f < 9 * kKX) ? 2 * kKX + f - 7 * kKX : -1;
+        const double cj = cosgr[j];
+        const double *fr = B + f, *pr = PB + (pf < 0 ? 0 : pf);
+        double x[kFftN];
+#pragma unroll
+        for (int e = 0; e < kFftN; ++e) {
+            double v = fr[e * LB];
+            if (pf >= 0) v = v + pr[e * LP];
+            x[e] = f < kNFwdScaled ? v * cj : v;
+        }
+        row_specx(x, vfm, was, f, j);
+    }
+    stamp(dbg, 2, 2);
 }
 
 // one zonal wavenumber m: specy of the 73 forward transforms, combine and tail of
@@ -954,7 +1083,7 @@ __global__ __launch_bounds__(kSpecThreads) void k_st_spec(
     double *__restrict__ sm, double *__restrict__ Td, double *__restrict__ phi_out, const double *__restrict__ phis,
     const double *__restrict__ tcorh, const double *__restrict__ qcorh, const DynTables *__restrict__ T, int j1,
     int j4, double dt, double alph, double rob, double wil, const double *__restrict__ pinv,
-    double *__restrict__ varm_next, int next_j2, int n1, int nin, long long *dbg) {
+    double *__restrict__ varm_next, int next_j2, int n1, int nin, const double *__restrict__ tabm, long long *dbg) {
     __shared__ double V[kVFm];            // this m's forward Fourier coefficients [f][lat][p]
     __shared__ double S[kNInvMax * kCW];  // specy output [f][2 n + p]; then the next step's inputs
     __shared__ double sh[2][kKX][kCW];
@@ -962,13 +1091,43 @@ __global__ __launch_bounds__(kSpecThreads) void k_st_spec(
     __shared__ double Fm[3 * kCW];        // phis, tcorh, qcorh of this m
     const int m = blockIdx.x;
     const int wave = threadIdx.x >> 6, l = threadIdx.x & 63, r = l & 15, kk = l >> 4;
-    stamp(dbg, 1, 0);
-    {
+    const int sk = next_j2 > 0 ? 1 : 3;
+    stamp(dbg, sk, 0);
+    constexpr int RT = (kTabMDoubles / 2 + kSpecThreads - 1) / kSpecThreads;
+    double2 rt[RT];
+    {   // stage the m's slices: every 16-B load issued before the first LDS store
+        constexpr int NV = kVFm / 2, NS = kSM / 2, RV = (NV + kSpecThreads - 1) / kSpecThreads,
+                      RS = (NS + kSpecThreads - 1) / kSpecThreads;
         const double2 *src = reinterpret_cast<const double2 *>(vfm + (size_t)m * kVFm);
-        for (int i = threadIdx.x; i < kVFm / 2; i += kSpecThreads) reinterpret_cast<double2 *>(V)[i] = src[i];
         const double2 *ss = reinterpret_cast<const double2 *>(sm + (size_t)m * kSM);
-        for (int i = threadIdx.x; i < kSM / 2; i += kSpecThreads) reinterpret_cast<double2 *>(Sst)[i] = ss[i];
+        double2 rv[RV], rs[RS];
+#pragma unroll
+        for (int q = 0; q < RV; ++q) {
+            const int i = threadIdx.x + q * kSpecThreads;
+            rv[q] = src[i < NV ? i : NV - 1];
+        }
+#pragma unroll
+        for (int q = 0; q < RS; ++q) {
+            const int i = threadIdx.x + q * kSpecThreads;
+            rs[q] = ss[i < NS ? i : NS - 1];
+        }
         load_forcing_m(Fm, phis, tcorh, qcorh, m);
+        const double2 *tsrc = reinterpret_cast<const double2 *>(tabm + (size_t)m * kTabMDoubles);
+#pragma unroll
+        for (int q = 0; q < RT; ++q) {  // this m's tables (into V's space once specy is done)
+            const int i = threadIdx.x + q * kSpecThreads;
+            rt[q] = tsrc[i < kTabMDoubles / 2 ? i : 0];
+        }
+#pragma unroll
+        for (int q = 0; q < RV; ++q) {
+            const int i = threadIdx.x + q * kSpecThreads;
+            if (i < NV) reinterpret_cast<double2 *>(V)[i] = rv[q];
+        }
+#pragma unroll
+        for (int q = 0; q < RS; ++q) {
+            const int i = threadIdx.x + q * kSpecThreads;
+            if (i < NS) reinterpret_cast<double2 *>(Sst)[i] = rs[q];
+        }
     }
     // specy operands: wave w's tiles all use this m's Legendre columns of its lanes
     const double *pm = pfwd + (size_t)m * kNX * kIY;
@@ -981,7 +1140,7 @@ __global__ __launch_bounds__(kSpecThreads) void k_st_spec(
         bD[s] = pm[(2 * r + 1) * kIY + j];
     }
     __syncthreads();
-    stamp(dbg, 1, 1);
+    stamp(dbg, sk, 1);
     // a) specy (k_specy's tiling: 8 fields x Re/Im per wave)
     for (int tile = wave; tile < (kNFwd + 7) / 8; tile += kSpecThreads / 64) {
         const int f0 = tile * 8;
@@ -1010,42 +1169,50 @@ __global__ __launch_bounds__(kSpecThreads) void k_st_spec(
             S[f * kCW + 2 * (2 * r + 1) + (row & 1)] = accD[q];
         }
     }
+    __syncthreads();  // V is free: this m's tables go there
+    TabM *tm = reinterpret_cast<TabM *>(V);
+#pragma unroll
+    for (int q = 0; q < RT; ++q) {
+        const int i = threadIdx.x + q * kSpecThreads;
+        if (i < kTabMDoubles / 2) reinterpret_cast<double2 *>(V)[i] = rt[q];
+    }
     __syncthreads();
-    stamp(dbg, 1, 2);
+    const LTab tb{tm};
+    stamp(dbg, sk, 2);
     // b) combine (k_dyn_combine) for coefficient (n, p) at level k
     const int cc = threadIdx.x & (kCW - 1), k = threadIdx.x / kCW;
     const int n = cc >> 1, p = cc & 1;
     const int c = ci(p, m, n);
     auto fl = [&](int f) { return [=](int pp, int nn) { return S[f * kCW + 2 * nn + pp]; }; };
     double vo, dv, d0, dq, dummy;
-    vds_gen(fl(k), fl(3 * kKX + k), T, m, n, p, &vo, &dv);  // vdspec(utend, vtend)
-    const double lapv = -(fl(6 * kKX + k)(p, n) * T->el2[n][m]);
-    vds_gen(fl(kKX + k), fl(4 * kKX + k), T, m, n, p, &dummy, &d0);      // vdspec(-u tgg, -v tgg)
-    vds_gen(fl(2 * kKX + k), fl(5 * kKX + k), T, m, n, p, &dummy, &dq);  // vdspec(-u trg, -v trg)
+    vds_gen(fl(k), fl(3 * kKX + k), tb, n, p, &vo, &dv);  // vdspec(utend, vtend)
+    const double lapv = -(fl(6 * kKX + k)(p, n) * tb.el2_n(n));
+    vds_gen(fl(kKX + k), fl(4 * kKX + k), tb, n, p, &dummy, &d0);      // vdspec(-u tgg, -v tgg)
+    vds_gen(fl(2 * kKX + k), fl(5 * kKX + k), tb, n, p, &dummy, &dq);  // vdspec(-u trg, -v trg)
     const double psdt = (m == 0 && n == 0) ? 0.0 : fl(kNFwd - 1)(p, n);
     const double tdt0 = d0 + fl(7 * kKX + k)(p, n), trdt0 = dq + fl(8 * kKX + k)(p, n);
     if (dbg) {
         __syncthreads();
-        stamp(dbg, 1, 3);
+        stamp(dbg, sk, 3);
     }
     // c) sptend / implic / diffusion / time integration on the LDS state
     auto SA = [&](int var, int lev, int kk2) -> double & { return Sst[smi(var, lev, kk2, cc)]; };
-    tail_coef<kCW>(SA, Td, phi_out, Fm, Fm + kCW, Fm + 2 * kCW, cc, T, sh, cc, k, c, m, n, vo, dv - lapv, tdt0, trdt0,
+    tail_coef<kCW>(SA, Td, phi_out, Fm, Fm + kCW, Fm + 2 * kCW, cc, tb, sh, cc, k, c, m, n, vo, dv - lapv, tdt0, trdt0,
                    psdt, j1, j4, dt, alph, rob, wil);
     __syncthreads();  // S is free, Sst complete
-    stamp(dbg, 1, 4);
+    stamp(dbg, sk, 4);
     {
         double2 *dst = reinterpret_cast<double2 *>(sm + (size_t)m * kSM);
         for (int i = threadIdx.x; i < kSM / 2; i += kSpecThreads) dst[i] = reinterpret_cast<const double2 *>(Sst)[i];
     }
     if (next_j2 <= 0) return;  // block-uniform
     // d) the next step's inverse-transform inputs (k_dyn_prep) and gridy
-    inv_inputs(Sst, S, Fm, T, m, next_j2, n1, nin);
+    inv_inputs(Sst, S, Fm, tb, m, next_j2, n1, nin);
     __syncthreads();
-    stamp(dbg, 1, 5);
+    stamp(dbg, sk, 5);
     gridy_m(S, pinv, varm_next, m, nin);
     __syncthreads();
-    stamp(dbg, 1, 6);
+    stamp(dbg, sk, 6);
 }
 
 // ------------------------------------------------------------ iogrid(30/31)
@@ -1167,7 +1334,7 @@ int dalloc(T **p, size_t count) {
 // ------------------------------------------------------------------ API
 extern "C" int sml_dyn_destroy(sml_dynamics *d) {
     if (!d) return SML_OK;
-    void *ptrs[] = {d->d_tabs, d->d_state, d->d_phis, d->d_tcorh, d->d_qcorh, d->d_phi, d->d_specin,
+    void *ptrs[] = {d->d_tabs, d->d_tabm, d->d_state, d->d_phis, d->d_tcorh, d->d_qcorh, d->d_phi, d->d_specin,
                     d->d_varm, d->d_grid, d->d_gfwd, d->d_sfwd, d->d_tend, d->d_phys, d->d_minmax, d->d_io, d->d_vfm, d->d_sm, d->d_dbg,
                     d->d_ptab, d->d_pbc, d->d_rad, d->d_pio};
     for (void *p : ptrs)
@@ -1196,11 +1363,11 @@ extern "C" int sml_dyn_create(double radius, sml_dynamics **out) {
     build_phys_tables(d->tab, &d->ptab);
     if (const char *e = std::getenv("SML_DYN_FUSED")) d->fused = *e && *e != '0';
     if (const char *e = std::getenv("SML_DYN_STAMPS"))
-        if (*e && *e != '0' && (rc = dalloc(reinterpret_cast<double **>(&d->d_dbg), 2 * kStampBlocks * kStamps))) {
+        if (*e && *e != '0' && (rc = dalloc(reinterpret_cast<double **>(&d->d_dbg), kStampKernels * kStampBlocks * kStamps))) {
             sml_dyn_destroy(d);
             return rc;
         }
-    if ((rc = dalloc(&d->d_tabs, 4)) || (rc = dalloc(&d->d_state, kStateSize)) || (rc = dalloc(&d->d_phis, kSF)) ||
+    if ((rc = dalloc(&d->d_tabs, 4)) || (rc = dalloc(&d->d_tabm, (size_t)4 * kMX * kTabMDoubles)) || (rc = dalloc(&d->d_state, kStateSize)) || (rc = dalloc(&d->d_phis, kSF)) ||
         (rc = dalloc(&d->d_tcorh, kSF)) || (rc = dalloc(&d->d_qcorh, kSF)) || (rc = dalloc(&d->d_phi, kKX * kSF)) ||
         (rc = dalloc(&d->d_specin, (size_t)kNInvMax * kSF)) ||
         (rc = dalloc(&d->d_varm, (size_t)(kNInvMax > kNFwd ? kNInvMax : kNFwd) * kVF)) ||
@@ -1240,6 +1407,12 @@ extern "C" int sml_dyn_impint(sml_dynamics *d, double dt, double alph) {
     // reading an evicted slot were launched earlier and complete first
     SML_HIP(hipDeviceSynchronize());
     SML_HIP(hipMemcpy(d->d_tabs + i, &d->tab, sizeof(DynTables), hipMemcpyHostToDevice));
+    {
+        std::vector<double> tm((size_t)kMX * kTabMDoubles);
+        for (int m = 0; m < kMX; ++m)
+            for (int q = 0; q < kTabMDoubles; ++q) tm[(size_t)m * kTabMDoubles + q] = tabm_value(&d->tab, m, q);
+        SML_HIP(hipMemcpy(d->d_tabm + (size_t)i * kMX * kTabMDoubles, tm.data(), tm.size() * 8, hipMemcpyHostToDevice));
+    }
     d->slot_key[i][0] = dt;
     d->slot_key[i][1] = alph;
     d->slot_used[i] = true;
@@ -1366,8 +1539,8 @@ int launch_step_fused(sml_dynamics *d, int j1, int j2, double dt, double alph, d
         hipLaunchKernelGGL(k_st_grid, dim3(2 * kIL), dim3(kRowThreads), 0, st, d->d_varm, d->d_gfwd, d->d_phys, sd.wa,
                            sd.cosgr, T, d->d_pbc, d->d_rad, d->d_ptab, lradsw ? 1 : 0, d->d_dbg);
         SML_HIP(hipGetLastError());
-        hipLaunchKernelGGL(k_st_specx, dim3((kNFwd * kIL + 63) / 64), dim3(64), 0, st, d->d_gfwd, d->d_phys,
-                           d->d_vfm, sd.wa, sd.cosgr);
+        hipLaunchKernelGGL(k_st_specx, dim3(kIL), dim3(kSpecxThreads), 0, st, d->d_gfwd, d->d_phys, d->d_vfm, sd.wa,
+                           sd.cosgr, d->d_dbg);
         SML_HIP(hipGetLastError());
     } else {
         hipLaunchKernelGGL(k_st_rows, dim3(kIL), dim3(kRowThreads), 0, st, d->d_varm, d->d_vfm, sd.wa, sd.cosgr, T,
@@ -1377,7 +1550,7 @@ int launch_step_fused(sml_dynamics *d, int j1, int j2, double dt, double alph, d
     const int j4 = (alph == 0.0) ? j2 : 1;
     hipLaunchKernelGGL(k_st_spec, dim3(kMX), dim3(kSpecThreads), 0, st, d->d_vfm, sd.pfwd, sd.wt, d->d_sm, d->d_tend,
                        d->d_phi, d->d_phis, d->d_tcorh, d->d_qcorh, T, j1, j4, dt, alph, rob, wil, sd.pinv, d->d_varm,
-                       next_j2, n1, nin, d->d_dbg);
+                       next_j2, n1, nin, d->d_tabm + (size_t)(d->d_tab - d->d_tabs) * kMX * kTabMDoubles, d->d_dbg);
     SML_HIP(hipGetLastError());
     if (next_j2 <= 0) {
         hipLaunchKernelGGL(k_state_from_m, dim3(conv_blocks), dim3(256), 0, st, d->d_sm, d->d_state);
@@ -1691,11 +1864,11 @@ extern "C" int sml_dyn_step_host(sml_dynamics *d, int j1, int j2, double dt, dou
     return SML_OK;
 }
 
-// diagnostic: the phase stamps of the last fused launches ([2][64][8] wall_clock64
+// diagnostic: the phase stamps of the last fused launches ([4][96][8] wall_clock64
 // ticks, 100 MHz); not part of the ABI header
 extern "C" int sml_dbg_dyn_stamps(sml_dynamics *d, long long *out) {
     SML_REQUIRE(d && out && d->d_dbg, "stamps not enabled (SML_DYN_STAMPS=1 at creation)");
     SML_HIP(hipDeviceSynchronize());
-    SML_HIP(hipMemcpy(out, d->d_dbg, 2 * kStampBlocks * kStamps * sizeof(long long), hipMemcpyDeviceToHost));
+    SML_HIP(hipMemcpy(out, d->d_dbg, kStampKernels * kStampBlocks * kStamps * sizeof(long long), hipMemcpyDeviceToHost));
     return SML_OK;
 }

@@ -114,6 +114,10 @@ constexpr int kFftThreads = 64;
 __global__ __launch_bounds__(kFftThreads) void k_gridx(const double *__restrict__ varm, double *__restrict__ grid,
                                                        const double *__restrict__ wa, const double *__restrict__ cosgr,
                                                        int nf, int ncos1) {
+    __shared__ double was[kFftWa];  // twiddles: LDS broadcast reads inside the FFT
+    if (threadIdx.x < kFftWa) was[threadIdx.x] = wa[threadIdx.x];
+    if (threadIdx.x + kFftThreads < kFftWa) was[threadIdx.x + kFftThreads] = wa[threadIdx.x + kFftThreads];
+    __syncthreads();
     const int id = blockIdx.x * kFftThreads + threadIdx.x;
     if (id >= nf * kIL) return;
     const int f = id / kIL, j = id % kIL;
@@ -124,7 +128,7 @@ __global__ __launch_bounds__(kFftThreads) void k_gridx(const double *__restrict_
     for (int e = 1; e <= kMX2 - 2; ++e) x[e] = v[e + 1];
 #pragma unroll
     for (int e = kMX2 - 1; e < kFftN; ++e) x[e] = 0.0;
-    fft::rfftb96_reg(x, wa);
+    fft::rfftb96_reg(x, was);
     const double cj = f >= ncos1 ? cosgr[j] : 1.0;
     double *g = grid + (size_t)f * kGridField + j * kIX;
 #pragma unroll
@@ -137,6 +141,10 @@ __global__ __launch_bounds__(kFftThreads) void k_gridx(const double *__restrict_
 __global__ __launch_bounds__(kFftThreads) void k_specx(const double *__restrict__ grid, double *__restrict__ varm,
                                                        const double *__restrict__ wa,
                                                        const double *__restrict__ scale_tab, int nf, int nscaled) {
+    __shared__ double was[kFftWa];
+    if (threadIdx.x < kFftWa) was[threadIdx.x] = wa[threadIdx.x];
+    if (threadIdx.x + kFftThreads < kFftWa) was[threadIdx.x + kFftThreads] = wa[threadIdx.x + kFftThreads];
+    __syncthreads();
     const int id = blockIdx.x * kFftThreads + threadIdx.x;
     if (id >= nf * kIL) return;
     const int f = id / kIL, j = id % kIL;
@@ -146,7 +154,7 @@ __global__ __launch_bounds__(kFftThreads) void k_specx(const double *__restrict_
     double x[kFftN];
 #pragma unroll
     for (int e = 0; e < kFftN; ++e) x[e] = sc ? g[e] * s0 : g[e];
-    fft::rfftf96_reg(x, wa);
+    fft::rfftf96_reg(x, was);
     const double scale = 1. / (double)kIX;
     double *v = varm + (size_t)f * kVarmField + j * kMX2;
     v[0] = x[0] * scale;

@@ -1,5 +1,5 @@
 """Diagnostic: per-phase durations inside the fused SPEEDY step kernels
-(SML_DYN_STAMPS=1).  python tools/probe_phases.py [phys=1]"""
+(SML_DYN_STAMPS=1), from a chained window.  python tools/probe_phases.py [phys=1]"""
 import ctypes
 import os
 import sys
@@ -23,27 +23,32 @@ d.set_state(st)
 if phys:
     d.set_physics(phys_boundary(d, forcing["phis"]))
 d.set_clock(1, True)
-d.stepone()
-d.leapfrog(4, graph=False)
+d.window(24)
 torch.cuda.synchronize()
-names = {0: ["load", "gridx", "gridpoint", "specx"], 1: ["load", "specy", "combine", "tail", "inv_inputs", "gridy"]}
+K = {0: ("grid" if phys else "rows", ["gridx", "gridpoint/physics"] if phys else ["load", "gridx", "gridpoint", "specx"]),
+     1: ("spec (chained)", ["load", "specy", "combine", "tail", "inv_inputs", "gridy"]),
+     2: ("specx", ["load", "fft+store"]),
+     3: ("spec (last)", ["load", "specy", "combine", "tail"])}
 L = lib()
 L.sml_dbg_dyn_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
-for rep in range(3):
-    d.leapfrog(1, graph=False)
+for rep in range(2):
+    d.window(24)
     torch.cuda.synchronize()
-    buf = np.zeros((2, 64, 8), dtype=np.int64)
+    buf = np.zeros((4, 96, 8), dtype=np.int64)
     assert L.sml_dbg_dyn_stamps(d._h, buf.ctypes.data) == 0
-    for kern, nb in ((0, 48), (1, 31)):
+    for kern, (name, phases) in K.items():
+        nb = int((buf[kern, :, 0] > 0).sum())
+        if nb == 0:
+            continue
         b = buf[kern, :nb].astype(np.float64)
         t0 = b[:, 0].min()
-        nph = len(names[kern])
-        line = [f"k{kern} start spread {(b[:, 0].max() - t0) / 100:.2f}us"]
-        for i in range(nph):
+        line = [f"{name} ({nb} blocks)"]
+        for i, ph in enumerate(phases):
             if b[:, i + 1].max() == 0:
                 continue
             dt = (b[:, i + 1] - b[:, i]) / 100.0
-            line.append(f"{names[kern][i]} med {np.median(dt):.2f} max {dt.max():.2f}")
+            line.append(f"{ph} med {np.median(dt):.2f} max {dt.max():.2f}")
         last = max(i for i in range(8) if b[:, i].max() > 0)
-        line.append(f"total(max end - min start) {(b[:, last].max() - t0) / 100:.2f}us")
+        line.append(f"span {(b[:, last].max() - t0) / 100:.2f}us")
         print(" | ".join(line))
+    print()
