@@ -677,8 +677,13 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 
 constexpr int kCW = 2 * kNX;                  // real coefficients (n, p) of one m
 constexpr int kSM = 5 * 2 * kKX * kCW;        // m-major state slice: [var 5][lev 2][k][cc] (ps at k = 0)
-constexpr int kVFs = kIL * 2 + 2;              // field stride of the m-major forward Fourier slice (LDS banks)
-constexpr int kVFm = kNFwd * kVFs;            // m-major forward Fourier slice: [f][lat][p] (+2 pad)
+// m-major Fourier coefficients, [m][lat][f][p]: a latitude row's fields are contiguous
+// per m (the row kernels' 16-B stores / loads coalesce across the fields' lanes) and
+// each m's slice is contiguous (the spectral kernels stage it with coalesced loads)
+constexpr int kVLs = 2 * kNFwd;               // forward: latitude stride
+constexpr int kVFm = kIL * kVLs;              // forward: per-m slice
+constexpr int kVIl = 2 * kNInvMax;            // inverse: latitude stride
+constexpr int kVIm = kIL * kVIl;              // inverse: per-m slice
 __device__ inline int smi(int var, int lev, int k, int cc) { return ((var * 2 + lev - 1) * kKX + k) * kCW + cc; }
 
 // diagnostic phase stamps (SML_DYN_STAMPS=1 at creation): thread 0 of each block
@@ -772,7 +777,7 @@ __device__ inline void inv_inputs(const double *Sst, double *In, const double *p
     uvspec(1, n1 + 2 * kKX + 2 + k, n1 + 3 * kKX + 2 + k);
 }
 
-// gridy of In[f][kCW] (this m) -> vim[m][f][lat][p] (k_gridy's tiling: one wave per
+// gridy of In[f][kCW] (this m) -> vim[m][lat][f][p] (k_gridy's tiling: one wave per
 // 8-field x Re/Im tile, waves of the block stride over the tiles)
 __device__ inline void gridy_m(const double *In, const double *__restrict__ pinv, double *__restrict__ varm, int m,
                                int nf) {
@@ -810,20 +815,19 @@ __device__ inline void gridy_m(const double *In, const double *__restrict__ pinv
             const int row = kk + 4 * q;
             const int f = f0 + (row >> 1);
             if (f >= nf) continue;
-            // m-major inverse Fourier coefficients vim[m][f][lat][p]: lanes (r, kk) of a
-            // q write 16 consecutive latitudes x (Re, Im) = 256 contiguous bytes
-            double *vr = varm + ((size_t)m * kNInvMax + f) * (kIL * 2) + (row & 1);
+            // m-major inverse Fourier coefficients vim[m][lat][f][p]
+            double *vr = varm + (size_t)m * kVIm + f * 2 + (row & 1);
             {
                 const int j = r;
                 const double sym = acc00[q], asym = acc10[q];
-                vr[(kIL - 1 - j) * 2] = sym + asym;
-                vr[j * 2] = sym - asym;
+                vr[(kIL - 1 - j) * kVIl] = sym + asym;
+                vr[j * kVIl] = sym - asym;
             }
             const int j = 16 + r;
             if (j < kIY) {
                 const double sym = acc01[q], asym = acc11[q];
-                vr[(kIL - 1 - j) * 2] = sym + asym;
-                vr[j * 2] = sym - asym;
+                vr[(kIL - 1 - j) * kVIl] = sym + asym;
+                vr[j * kVIl] = sym - asym;
             }
         }
     }
@@ -871,9 +875,9 @@ static_assert(kNInvMax <= kRowThreads && kNFwd <= kRowThreads && kIX <= kRowThre
 // for kcos = 2; the 96 values into A[lon][f]
 __device__ inline void row_gridx(double *A, const double *__restrict__ varm, const double *__restrict__ wa, int f,
                                  int j, bool kcos2, double cj) {
-    // the m-major coefficients vim[m][f][lat][p] of (f, j): coefficient c = 2 m + p
-    const double *v = varm + (size_t)f * (kIL * 2) + j * 2;
-    auto V = [&](int c) { return v[(size_t)(c >> 1) * kNInvMax * (kIL * 2) + (c & 1)]; };
+    // the m-major coefficients vim[m][lat][f][p] of (f, j): coefficient c = 2 m + p
+    const double *v = varm + (size_t)j * kVIl + f * 2;
+    auto V = [&](int c) { return v[(size_t)(c >> 1) * kVIm + (c & 1)]; };
     double x[kFftN];
     x[0] = V(0);
 #pragma unroll
@@ -891,7 +895,7 @@ __device__ inline void row_gridx(double *A, const double *__restrict__ varm, con
 __device__ inline void row_specx(double *x, double *__restrict__ vfm, const double *__restrict__ wa, int f, int j) {
     fft::rfftf96_reg(x, wa);
     const double scale = 1. / (double)kIX;
-    double *o = vfm + (size_t)f * kVFs + j * 2;
+    double *o = vfm + (size_t)j * kVLs + f * 2;
     o[0] = x[0] * scale;
     o[1] = 0.0;
 #pragma unroll
@@ -1084,7 +1088,7 @@ __global__ __launch_bounds__(kSpecThreads) void k_st_spec(
     const double *__restrict__ tcorh, const double *__restrict__ qcorh, const DynTables *__restrict__ T, int j1,
     int j4, double dt, double alph, double rob, double wil, const double *__restrict__ pinv,
     double *__restrict__ varm_next, int next_j2, int n1, int nin, const double *__restrict__ tabm, long long *dbg) {
-    __shared__ double V[kVFm];            // this m's forward Fourier coefficients [f][lat][p]
+    __shared__ double V[kVFm];            // this m's forward Fourier coefficients [lat][f][p]
     __shared__ double S[kNInvMax * kCW];  // specy output [f][2 n + p]; then the next step's inputs
     __shared__ double sh[2][kKX][kCW];
     __shared__ double Sst[kSM];           // this m's state, updated in place
@@ -1146,14 +1150,14 @@ __global__ __launch_bounds__(kSpecThreads) void k_st_spec(
         const int f0 = tile * 8;
         const int fa = f0 + (r >> 1);
         const bool ok = fa < kNFwd;
-        const double *vr = V + (ok ? fa : 0) * kVFs + (r & 1);
+        const double *vr = V + (ok ? fa : 0) * 2 + (r & 1);
         d4 accS = {0, 0, 0, 0}, accD = accS;
 #pragma unroll
         for (int s = 0; s < kIY / 4; ++s) {
             const int j = 4 * s + kk;
             double aS = 0.0, aD = 0.0;
             if (ok) {
-                const double vn = vr[(kIL - 1 - j) * 2], vs = vr[j * 2];
+                const double vn = vr[(kIL - 1 - j) * kVLs], vs = vr[j * kVLs];
                 aS = (vn + vs) * wv[s];
                 aD = (vn - vs) * wv[s];
             }
