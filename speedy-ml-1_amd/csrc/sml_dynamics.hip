@@ -1068,11 +1068,17 @@ __global__ __launch_bounds__(kSpecxThreads) void k_st_specx(const double *__rest
         const double cj = cosgr[j];
         const double *fr = B + f, *pr = PB + (pf < 0 ? 0 : pf);
         double x[kFftN];
+        // F, then + P (u, v, t, q), then x cosgr(j) (vdspec inputs): one branch per
+        // case around straight-line loops, not a branch per element
 #pragma unroll
-        for (int e = 0; e < kFftN; ++e) {
-            double v = fr[e * LB];
-            if (pf >= 0) v = v + pr[e * LP];
-            x[e] = f < kNFwdScaled ? v * cj : v;
+        for (int e = 0; e < kFftN; ++e) x[e] = fr[e * LB];
+        if (pf >= 0) {
+#pragma unroll
+            for (int e = 0; e < kFftN; ++e) x[e] = x[e] + pr[e * LP];
+        }
+        if (f < kNFwdScaled) {
+#pragma unroll
+            for (int e = 0; e < kFftN; ++e) x[e] = x[e] * cj;
         }
         row_specx(x, vfm, was, f, j);
     }
