@@ -628,6 +628,18 @@ __device__ inline void tail_coef(SA S, double *__restrict__ Td, double *__restri
     timint(3, k, trdt);
 }
 
+// the barriers tail_coef executes, for threads of a block that hold no coefficient
+// (keep in step with tail_coef: 1 in sptend, 4 in implic when alph != 0)
+__device__ inline void tail_coef_barriers(double alph) {
+    __syncthreads();
+    if (alph != 0.0) {
+        __syncthreads();
+        __syncthreads();
+        __syncthreads();
+        __syncthreads();
+    }
+}
+
 // tail kernel of the unfused step: a block owns 32 real coefficients x 8 levels
 constexpr int kTailC = 32;
 __global__ __launch_bounds__(256) void k_dyn_tail(double *__restrict__ st, double *__restrict__ Td,
@@ -779,20 +791,30 @@ __device__ inline void inv_inputs(const double *Sst, double *In, const double *p
 
 // gridy of In[f][kCW] (this m) -> vim[m][lat][f][p] (k_gridy's tiling: one wave per
 // 8-field x Re/Im tile, waves of the block stride over the tiles)
-__device__ inline void gridy_m(const double *In, const double *__restrict__ pinv, double *__restrict__ varm, int m,
-                               int nf) {
-    const int wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+// the Legendre operands of gridy_m for this lane (loaded once per wave; callers
+// issue the loads early so their latency hides behind other work)
+struct GridyB {
+    double b00[4], b01[4], b10[4], b11[4];
+};
+__device__ inline GridyB gridy_operands(const double *__restrict__ pinv, int m) {
     const int l = threadIdx.x & 63, r = l & 15, kk = l >> 4;
     const double *pm = pinv + (size_t)m * kNX * 32;
-    double b00[4], b01[4], b10[4], b11[4];  // the Legendre operands, loaded once per wave
+    GridyB g;
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
         const int n_odd = 2 * (4 * s + kk), n_even = n_odd + 1;
-        b00[s] = pm[n_odd * 32 + r];
-        b01[s] = pm[n_odd * 32 + 16 + r];
-        b10[s] = pm[n_even * 32 + r];
-        b11[s] = pm[n_even * 32 + 16 + r];
+        g.b00[s] = pm[n_odd * 32 + r];
+        g.b01[s] = pm[n_odd * 32 + 16 + r];
+        g.b10[s] = pm[n_even * 32 + r];
+        g.b11[s] = pm[n_even * 32 + 16 + r];
     }
+    return g;
+}
+
+__device__ inline void gridy_m(const double *In, const GridyB &gb, double *__restrict__ varm, int m, int nf) {
+    const int wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const int l = threadIdx.x & 63, r = l & 15, kk = l >> 4;
+    const double *b00 = gb.b00, *b01 = gb.b01, *b10 = gb.b10, *b11 = gb.b11;
     for (int tile = wave; tile < (nf + 7) / 8; tile += nw) {
         const int f0 = tile * 8;
         const int fa = f0 + (r >> 1), p = r & 1;
@@ -843,7 +865,8 @@ __device__ inline void load_forcing_m(double *Fm, const double *__restrict__ phi
     }
 }
 
-constexpr int kSpecThreads = kCW * kKX;  // 512
+constexpr int kSpecThreads = kCW * kKX;  // 512: one thread per (coefficient, level) of one m
+constexpr int kSpecBlk = 512;             // k_st_spec's block (threads past kSpecThreads would only stage)
 
 // window start: the inverse transforms of step (.., j2) from the m-major state
 __global__ __launch_bounds__(kSpecThreads) void k_st_inv(const double *__restrict__ sm, const double *__restrict__ phis,
@@ -861,7 +884,7 @@ __global__ __launch_bounds__(kSpecThreads) void k_st_inv(const double *__restric
     __syncthreads();
     inv_inputs(Sst, In, Fm, GTab{T, m}, m, j2, n1, nin);
     __syncthreads();
-    gridy_m(In, pinv, varm, m, nin);
+    gridy_m(In, gridy_operands(pinv, m), varm, m, nin);
 }
 
 // Fourier stage of one latitude row: FFTPACK's real FFT (sml_fft.hpp, the reference's
@@ -1088,7 +1111,7 @@ __global__ __launch_bounds__(kSpecxThreads) void k_st_specx(const double *__rest
 // one zonal wavenumber m: specy of the 73 forward transforms, combine and tail of
 // the m's 64 real coefficients x 8 levels (one thread each) on the m's state slice
 // in LDS; with next_j2 > 0 the new state feeds the next step's inverse transforms
-__global__ __launch_bounds__(kSpecThreads) void k_st_spec(
+__global__ __launch_bounds__(kSpecBlk) void k_st_spec(
     const double *__restrict__ vfm, const double *__restrict__ pfwd, const double *__restrict__ wt,
     double *__restrict__ sm, double *__restrict__ Td, double *__restrict__ phi_out, const double *__restrict__ phis,
     const double *__restrict__ tcorh, const double *__restrict__ qcorh, const DynTables *__restrict__ T, int j1,
@@ -1103,42 +1126,43 @@ __global__ __launch_bounds__(kSpecThreads) void k_st_spec(
     const int wave = threadIdx.x >> 6, l = threadIdx.x & 63, r = l & 15, kk = l >> 4;
     const int sk = next_j2 > 0 ? 1 : 3;
     stamp(dbg, sk, 0);
-    constexpr int RT = (kTabMDoubles / 2 + kSpecThreads - 1) / kSpecThreads;
+    constexpr int RT = (kTabMDoubles / 2 + kSpecBlk - 1) / kSpecBlk;
     double2 rt[RT];
     {   // stage the m's slices: every 16-B load issued before the first LDS store
-        constexpr int NV = kVFm / 2, NS = kSM / 2, RV = (NV + kSpecThreads - 1) / kSpecThreads,
-                      RS = (NS + kSpecThreads - 1) / kSpecThreads;
+        constexpr int NV = kVFm / 2, NS = kSM / 2, RV = (NV + kSpecBlk - 1) / kSpecBlk,
+                      RS = (NS + kSpecBlk - 1) / kSpecBlk;
         const double2 *src = reinterpret_cast<const double2 *>(vfm + (size_t)m * kVFm);
         const double2 *ss = reinterpret_cast<const double2 *>(sm + (size_t)m * kSM);
         double2 rv[RV], rs[RS];
 #pragma unroll
         for (int q = 0; q < RV; ++q) {
-            const int i = threadIdx.x + q * kSpecThreads;
+            const int i = threadIdx.x + q * kSpecBlk;
             rv[q] = src[i < NV ? i : NV - 1];
         }
 #pragma unroll
         for (int q = 0; q < RS; ++q) {
-            const int i = threadIdx.x + q * kSpecThreads;
+            const int i = threadIdx.x + q * kSpecBlk;
             rs[q] = ss[i < NS ? i : NS - 1];
         }
         load_forcing_m(Fm, phis, tcorh, qcorh, m);
         const double2 *tsrc = reinterpret_cast<const double2 *>(tabm + (size_t)m * kTabMDoubles);
 #pragma unroll
         for (int q = 0; q < RT; ++q) {  // this m's tables (into V's space once specy is done)
-            const int i = threadIdx.x + q * kSpecThreads;
+            const int i = threadIdx.x + q * kSpecBlk;
             rt[q] = tsrc[i < kTabMDoubles / 2 ? i : 0];
         }
 #pragma unroll
         for (int q = 0; q < RV; ++q) {
-            const int i = threadIdx.x + q * kSpecThreads;
+            const int i = threadIdx.x + q * kSpecBlk;
             if (i < NV) reinterpret_cast<double2 *>(V)[i] = rv[q];
         }
 #pragma unroll
         for (int q = 0; q < RS; ++q) {
-            const int i = threadIdx.x + q * kSpecThreads;
+            const int i = threadIdx.x + q * kSpecBlk;
             if (i < NS) reinterpret_cast<double2 *>(Sst)[i] = rs[q];
         }
     }
+    const GridyB gb = next_j2 > 0 ? gridy_operands(pinv, m) : GridyB{};  // the next step's gridy operands, early
     // specy operands: wave w's tiles all use this m's Legendre columns of its lanes
     const double *pm = pfwd + (size_t)m * kNX * kIY;
     double wv[kIY / 4], bS[kIY / 4], bD[kIY / 4];
@@ -1152,7 +1176,7 @@ __global__ __launch_bounds__(kSpecThreads) void k_st_spec(
     __syncthreads();
     stamp(dbg, sk, 1);
     // a) specy (k_specy's tiling: 8 fields x Re/Im per wave)
-    for (int tile = wave; tile < (kNFwd + 7) / 8; tile += kSpecThreads / 64) {
+    for (int tile = wave; tile < (kNFwd + 7) / 8; tile += kSpecBlk / 64) {
         const int f0 = tile * 8;
         const int fa = f0 + (r >> 1);
         const bool ok = fa < kNFwd;
@@ -1183,18 +1207,19 @@ __global__ __launch_bounds__(kSpecThreads) void k_st_spec(
     TabM *tm = reinterpret_cast<TabM *>(V);
 #pragma unroll
     for (int q = 0; q < RT; ++q) {
-        const int i = threadIdx.x + q * kSpecThreads;
+        const int i = threadIdx.x + q * kSpecBlk;
         if (i < kTabMDoubles / 2) reinterpret_cast<double2 *>(V)[i] = rt[q];
     }
     __syncthreads();
     const LTab tb{tm};
     stamp(dbg, sk, 2);
-    // b) combine (k_dyn_combine) for coefficient (n, p) at level k
-    const int cc = threadIdx.x & (kCW - 1), k = threadIdx.x / kCW;
+    // b) combine (k_dyn_combine) for coefficient (n, p) at level k: threads 0..511
+    const bool holds = threadIdx.x < kSpecThreads;
+    const int cc = threadIdx.x & (kCW - 1), k = holds ? threadIdx.x / kCW : 0;
     const int n = cc >> 1, p = cc & 1;
     const int c = ci(p, m, n);
     auto fl = [&](int f) { return [=](int pp, int nn) { return S[f * kCW + 2 * nn + pp]; }; };
-    double vo, dv, d0, dq, dummy;
+    double vo = 0.0, dv = 0.0, d0 = 0.0, dq = 0.0, dummy;
     vds_gen(fl(k), fl(3 * kKX + k), tb, n, p, &vo, &dv);  // vdspec(utend, vtend)
     const double lapv = -(fl(6 * kKX + k)(p, n) * tb.el2_n(n));
     vds_gen(fl(kKX + k), fl(4 * kKX + k), tb, n, p, &dummy, &d0);      // vdspec(-u tgg, -v tgg)
@@ -1207,20 +1232,23 @@ __global__ __launch_bounds__(kSpecThreads) void k_st_spec(
     }
     // c) sptend / implic / diffusion / time integration on the LDS state
     auto SA = [&](int var, int lev, int kk2) -> double & { return Sst[smi(var, lev, kk2, cc)]; };
-    tail_coef<kCW>(SA, Td, phi_out, Fm, Fm + kCW, Fm + 2 * kCW, cc, tb, sh, cc, k, c, m, n, vo, dv - lapv, tdt0, trdt0,
-                   psdt, j1, j4, dt, alph, rob, wil);
+    if (holds)
+        tail_coef<kCW>(SA, Td, phi_out, Fm, Fm + kCW, Fm + 2 * kCW, cc, tb, sh, cc, k, c, m, n, vo, dv - lapv, tdt0,
+                       trdt0, psdt, j1, j4, dt, alph, rob, wil);
+    else
+        tail_coef_barriers(alph);
     __syncthreads();  // S is free, Sst complete
     stamp(dbg, sk, 4);
     {
         double2 *dst = reinterpret_cast<double2 *>(sm + (size_t)m * kSM);
-        for (int i = threadIdx.x; i < kSM / 2; i += kSpecThreads) dst[i] = reinterpret_cast<const double2 *>(Sst)[i];
+        for (int i = threadIdx.x; i < kSM / 2; i += kSpecBlk) dst[i] = reinterpret_cast<const double2 *>(Sst)[i];
     }
     if (next_j2 <= 0) return;  // block-uniform
     // d) the next step's inverse-transform inputs (k_dyn_prep) and gridy
-    inv_inputs(Sst, S, Fm, tb, m, next_j2, n1, nin);
+    if (holds) inv_inputs(Sst, S, Fm, tb, m, next_j2, n1, nin);
     __syncthreads();
     stamp(dbg, sk, 5);
-    gridy_m(S, pinv, varm_next, m, nin);
+    gridy_m(S, gb, varm_next, m, nin);
     __syncthreads();
     stamp(dbg, sk, 6);
 }
@@ -1558,7 +1586,7 @@ int launch_step_fused(sml_dynamics *d, int j1, int j2, double dt, double alph, d
         SML_HIP(hipGetLastError());
     }
     const int j4 = (alph == 0.0) ? j2 : 1;
-    hipLaunchKernelGGL(k_st_spec, dim3(kMX), dim3(kSpecThreads), 0, st, d->d_vfm, sd.pfwd, sd.wt, d->d_sm, d->d_tend,
+    hipLaunchKernelGGL(k_st_spec, dim3(kMX), dim3(kSpecBlk), 0, st, d->d_vfm, sd.pfwd, sd.wt, d->d_sm, d->d_tend,
                        d->d_phi, d->d_phis, d->d_tcorh, d->d_qcorh, T, j1, j4, dt, alph, rob, wil, sd.pinv, d->d_varm,
                        next_j2, n1, nin, d->d_tabm + (size_t)(d->d_tab - d->d_tabs) * kMX * kTabMDoubles, d->d_dbg);
     SML_HIP(hipGetLastError());
