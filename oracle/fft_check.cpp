@@ -58,27 +58,33 @@ int main(int argc, char **argv) {
     std::normal_distribution<double> nd;
     int nbwd = 0, nfwd = 0;
     for (int rep = 0; rep < 200; ++rep) {
-        double x[kFftN], r[kFftN], y1[kFftN], y3[kFftN], y8[kFftN];
+        double x[kFftN], r[kFftN], y1[kFftN], y2[kFftN], y3[kFftN], y4[kFftN], y8[kFftN];
         for (int i = 0; i < n; ++i) x[i] = nd(rng) * (rep % 7 + 1);
         std::memcpy(r, x, sizeof x);
         rfftb(&n, r, wsave);
         std::memcpy(y1, x, sizeof x); bwd<1>(y1);
+        std::memcpy(y2, x, sizeof x); bwd<2>(y2);
         std::memcpy(y3, x, sizeof x); bwd<3>(y3);
+        std::memcpy(y4, x, sizeof x); bwd<4>(y4);
         std::memcpy(y8, x, sizeof x); bwd<8>(y8);
         double yr[kFftN];
         std::memcpy(yr, x, sizeof x);
         fft::rfftb96_reg(yr, wa);
-        if (std::memcmp(r, y1, sizeof r) || std::memcmp(r, y3, sizeof r) || std::memcmp(r, y8, sizeof r) ||
+        if (std::memcmp(r, y1, sizeof r) || std::memcmp(r, y2, sizeof r) || std::memcmp(r, y3, sizeof r) ||
+            std::memcmp(r, y4, sizeof r) || std::memcmp(r, y8, sizeof r) ||
             std::memcmp(r, yr, sizeof r))
             ++nbwd;
         std::memcpy(r, x, sizeof x);
         rfftf(&n, r, wsave);
         std::memcpy(y1, x, sizeof x); fwd<1>(y1);
+        std::memcpy(y2, x, sizeof x); fwd<2>(y2);
         std::memcpy(y3, x, sizeof x); fwd<3>(y3);
+        std::memcpy(y4, x, sizeof x); fwd<4>(y4);
         std::memcpy(y8, x, sizeof x); fwd<8>(y8);
         std::memcpy(yr, x, sizeof x);
         fft::rfftf96_reg(yr, wa);
-        if (std::memcmp(r, y1, sizeof r) || std::memcmp(r, y3, sizeof r) || std::memcmp(r, y8, sizeof r) ||
+        if (std::memcmp(r, y1, sizeof r) || std::memcmp(r, y2, sizeof r) || std::memcmp(r, y3, sizeof r) ||
+            std::memcmp(r, y4, sizeof r) || std::memcmp(r, y8, sizeof r) ||
             std::memcmp(r, yr, sizeof r))
             ++nfwd;
     }

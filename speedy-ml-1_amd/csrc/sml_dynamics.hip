@@ -791,8 +791,7 @@ __device__ inline void inv_inputs(const double *Sst, double *In, const double *p
 
 // gridy of In[f][kCW] (this m) -> vim[m][lat][f][p] (k_gridy's tiling: one wave per
 // 8-field x Re/Im tile, waves of the block stride over the tiles)
-// the Legendre operands of gridy_m for this lane (loaded once per wave; callers
-// issue the loads early so their latency hides behind other work)
+// the Legendre operands of gridy_m for this lane (loaded once per wave)
 struct GridyB {
     double b00[4], b01[4], b10[4], b11[4];
 };
@@ -1162,7 +1161,6 @@ __global__ __launch_bounds__(kSpecBlk) void k_st_spec(
             if (i < NS) reinterpret_cast<double2 *>(Sst)[i] = rs[q];
         }
     }
-    const GridyB gb = next_j2 > 0 ? gridy_operands(pinv, m) : GridyB{};  // the next step's gridy operands, early
     // specy operands: wave w's tiles all use this m's Legendre columns of its lanes
     const double *pm = pfwd + (size_t)m * kNX * kIY;
     double wv[kIY / 4], bS[kIY / 4], bD[kIY / 4];
@@ -1248,7 +1246,7 @@ __global__ __launch_bounds__(kSpecBlk) void k_st_spec(
     if (holds) inv_inputs(Sst, S, Fm, tb, m, next_j2, n1, nin);
     __syncthreads();
     stamp(dbg, sk, 5);
-    gridy_m(S, gb, varm_next, m, nin);
+    gridy_m(S, gridy_operands(pinv, m), varm_next, m, nin);
     __syncthreads();
     stamp(dbg, sk, 6);
 }

@@ -51,4 +51,16 @@ for rep in range(2):
         last = max(i for i in range(8) if b[:, i].max() > 0)
         line.append(f"span {(b[:, last].max() - t0) / 100:.2f}us")
         print(" | ".join(line))
+    # launch-to-launch gaps along one step: spec(chained, previous step) -> grid -> specx -> spec(last)
+    se = {}
+    for kern in (1, 0, 2, 3):
+        nb = int((buf[kern, :, 0] > 0).sum())
+        if nb:
+            b = buf[kern, :nb]
+            last = max(i for i in range(8) if b[:, i].max() > 0)
+            se[kern] = (b[:, 0].min(), b[:, 0].max(), b[:, last].max())
+    seq = [k for k in (1, 0, 2, 3) if k in se]
+    print("gaps (last stamp of one kernel -> first / last block start of the next):",
+          ", ".join(f"{K[a][0]}->{K[b][0]} {(se[b][0] - se[a][2]) / 100:.2f}/{(se[b][1] - se[a][2]) / 100:.2f}us"
+                    for a, b in zip(seq, seq[1:])))
     print()
