@@ -100,6 +100,8 @@ struct sml_dynamics {
     // step kernels: the fused form (default: 2-3 launches per chained step) or the
     // 8/9-launch form (SML_DYN_FUSED=0 at creation; same results bit for bit)
     bool fused = true;
+    // with GPU physics: k_st_grid + k_st_specx instead of k_st_gridspec (SML_DYN_SPLIT_GRID=1)
+    bool split_grid = false;
     // mod_lflags lradsw (module default .true.) and stloop's istep (at_gcm.f90:81)
     bool lradsw = true;
     int istep = 1;
@@ -1107,6 +1109,98 @@ __global__ __launch_bounds__(kSpecxThreads) void k_st_specx(const double *__rest
     stamp(dbg, 2, 2);
 }
 
+// With GPU physics, one latitude row per block (4 waves): gridx of the row's 91
+// inverse transforms (wave 0 the 50 dynamics fields, wave 1 phypar's 41 level-1
+// fields, side by side), then the row's grid-point dynamics (waves 0-1, one column
+// per thread, F -> B) beside phypar (waves 2-3, one column per thread: P into A's
+// columns that only phypar reads, after it has read them), then specx of the 73
+// forward transforms (F, + P where grtend adds it, x cosgr(j) for vdspec's inputs;
+// one transform per thread, spread over the 4 waves) straight into the m-major
+// coefficients.  The same arithmetic as k_st_grid -> k_st_specx, one launch.
+constexpr int kGsThreads = 256;
+static_assert(kNInv <= 64 && kNInvP - kNInv <= 64 && kIX <= 128 && kNFwd <= kGsThreads, "k_st_gridspec roles");
+// P slot s (u 0..7, v 8..15, t 16..23, q 24..31) -> a column of A that only phypar reads
+// (t1 q1 phi1 ps1 at kPT1.., then ucos1 ..)
+__device__ inline int phys_slot_col(int s) { return s < 3 * kKX + 1 ? kPT1 + s : kNInv1P + 2 * kKX + 2 + (s - (3 * kKX + 1)); }
+
+__global__ __launch_bounds__(kGsThreads) void k_st_gridspec(
+    const double *__restrict__ varm, double *__restrict__ vfm, const double *__restrict__ wa,
+    const double *__restrict__ cosgr, const DynTables *__restrict__ T, const double *__restrict__ bc,
+    double *__restrict__ rad, const PhysTables *__restrict__ PT, int lradsw, long long *dbg) {
+    __shared__ double A[kFftN * kRowLd], B[kFftN * kRowLd], was[kFftWa];
+    constexpr int n1 = kNInv1P;
+    constexpr int nphys = (n1 - kPT1) + (kNInvP - (n1 + 2 * kKX + 2));  // 25 + 16 = 41
+    const int j = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    stamp(dbg, 0, 0);
+    if (tid < kFftWa) was[tid] = wa[tid];
+    __syncthreads();
+    const double cj = cosgr[j];
+    // gridx: wave 0 the dynamics fields, wave 1 phypar's
+    if (wave == 0 && lane < kNInv) {
+        const int f = lane < kNInv1 ? lane : n1 + (lane - kNInv1);  // [vor div t tr] | [ucos vcos psdx psdy]
+        row_gridx(A, varm, was, f, j, f >= n1, cj);
+    } else if (wave == 1 && lane < nphys) {
+        const int f = lane < n1 - kPT1 ? kPT1 + lane : n1 + 2 * kKX + 2 + (lane - (n1 - kPT1));
+        row_gridx(A, varm, was, f, j, f >= n1, cj);
+    }
+    __syncthreads();
+    stamp(dbg, 0, 1);
+    if (tid < 128) {
+        if (tid < kIX) {  // grid-point dynamics of column i -> F in B[i][f]
+            const int i = tid;
+            double dummy[kKX];
+            gridpoint_column(j, n1, [&](int f) { return A[i * kRowLd + f]; }, false, dummy, dummy, dummy, dummy,
+                             [&](int f, double v) { B[i * kRowLd + f] = v; }, T);
+        }
+    } else if (tid - 128 < kIX) {  // phypar of column i
+        const int i = tid - 128, pt = j * kIX + i;
+        double *Ai = A + i * kRowLd;
+        double ua[kKX], va[kKX], ta[kKX], qa[kKX], ph[kKX], ut[kKX], vt[kKX], tt[kKX], qt[kKX];
+#pragma unroll
+        for (int k = 0; k < kKX; ++k) {
+            ua[k] = Ai[n1 + 2 * kKX + 2 + k];
+            va[k] = Ai[n1 + 3 * kKX + 2 + k];
+            ta[k] = Ai[kPT1 + k];
+            qa[k] = Ai[kPQ1 + k];
+            ph[k] = Ai[kPPhi1 + k];
+        }
+        const double ps1 = Ai[kPPs1];
+        phys_column(pt, ua, va, ta, qa, ph, ps1, bc, rad, PT, lradsw != 0, ut, vt, tt, qt);
+#pragma unroll
+        for (int k = 0; k < kKX; ++k) {
+            Ai[phys_slot_col(k)] = ut[k];
+            Ai[phys_slot_col(kKX + k)] = vt[k];
+            Ai[phys_slot_col(2 * kKX + k)] = tt[k];
+            Ai[phys_slot_col(3 * kKX + k)] = qt[k];
+        }
+    }
+    __syncthreads();
+    stamp(dbg, 0, 2);
+    // specx: transform f = 4 lane + wave (spread over the waves)
+    const int f = 4 * lane + wave;
+    if (f < kNFwd) {
+        // F field -> tendency slot of P: u 0..7, v 24..31, t 56..63, q 64..71
+        const int pf = f < kKX ? f : (f >= 3 * kKX && f < 4 * kKX) ? kKX + f - 3 * kKX
+                     : (f >= 7 * kKX && f < 9 * kKX) ? 2 * kKX + f - 7 * kKX : -1;
+        const double *fr = B + f, *pr = A + phys_slot_col(pf < 0 ? 0 : pf);
+        double x[kFftN];
+        // F, then + P (u, v, t, q), then x cosgr(j) (vdspec inputs): one branch per
+        // case around straight-line loops
+#pragma unroll
+        for (int e = 0; e < kFftN; ++e) x[e] = fr[e * kRowLd];
+        if (pf >= 0) {
+#pragma unroll
+            for (int e = 0; e < kFftN; ++e) x[e] = x[e] + pr[e * kRowLd];
+        }
+        if (f < kNFwdScaled) {
+#pragma unroll
+            for (int e = 0; e < kFftN; ++e) x[e] = x[e] * cj;
+        }
+        row_specx(x, vfm, was, f, j);
+    }
+    stamp(dbg, 0, 3);
+}
+
 // one zonal wavenumber m: specy of the 73 forward transforms, combine and tail of
 // the m's 64 real coefficients x 8 levels (one thread each) on the m's state slice
 // in LDS; with next_j2 > 0 the new state feeds the next step's inverse transforms
@@ -1398,6 +1492,7 @@ extern "C" int sml_dyn_create(double radius, sml_dynamics **out) {
     build_dyn_indyns(spectral_host_tables(d->sp), &d->tab);
     build_phys_tables(d->tab, &d->ptab);
     if (const char *e = std::getenv("SML_DYN_FUSED")) d->fused = *e && *e != '0';
+    if (const char *e = std::getenv("SML_DYN_SPLIT_GRID")) d->split_grid = *e && *e != '0';
     if (const char *e = std::getenv("SML_DYN_STAMPS"))
         if (*e && *e != '0' && (rc = dalloc(reinterpret_cast<double **>(&d->d_dbg), kStampKernels * kStampBlocks * kStamps))) {
             sml_dyn_destroy(d);
@@ -1572,11 +1667,16 @@ int launch_step_fused(sml_dynamics *d, int j1, int j2, double dt, double alph, d
         SML_HIP(hipGetLastError());
     }
     if (phys) {
-        hipLaunchKernelGGL(k_st_grid, dim3(2 * kIL), dim3(kRowThreads), 0, st, d->d_varm, d->d_gfwd, d->d_phys, sd.wa,
-                           sd.cosgr, T, d->d_pbc, d->d_rad, d->d_ptab, lradsw ? 1 : 0, d->d_dbg);
-        SML_HIP(hipGetLastError());
-        hipLaunchKernelGGL(k_st_specx, dim3(kIL), dim3(kSpecxThreads), 0, st, d->d_gfwd, d->d_phys, d->d_vfm, sd.wa,
-                           sd.cosgr, d->d_dbg);
+        if (d->split_grid) {  // the two-launch form (A/B reference)
+            hipLaunchKernelGGL(k_st_grid, dim3(2 * kIL), dim3(kRowThreads), 0, st, d->d_varm, d->d_gfwd, d->d_phys,
+                               sd.wa, sd.cosgr, T, d->d_pbc, d->d_rad, d->d_ptab, lradsw ? 1 : 0, d->d_dbg);
+            SML_HIP(hipGetLastError());
+            hipLaunchKernelGGL(k_st_specx, dim3(kIL), dim3(kSpecxThreads), 0, st, d->d_gfwd, d->d_phys, d->d_vfm,
+                               sd.wa, sd.cosgr, d->d_dbg);
+        } else {
+            hipLaunchKernelGGL(k_st_gridspec, dim3(kIL), dim3(kGsThreads), 0, st, d->d_varm, d->d_vfm, sd.wa, sd.cosgr,
+                               T, d->d_pbc, d->d_rad, d->d_ptab, lradsw ? 1 : 0, d->d_dbg);
+        }
         SML_HIP(hipGetLastError());
     } else {
         hipLaunchKernelGGL(k_st_rows, dim3(kIL), dim3(kRowThreads), 0, st, d->d_varm, d->d_vfm, sd.wa, sd.cosgr, T,

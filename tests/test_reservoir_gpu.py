@@ -204,3 +204,29 @@ def test_synchronize_matches_oracle(cuda):
         for t in range(length):
             _, x = _oracle_step(w, x, inputs[t, o[i]:o[i + 1]], np.zeros(132))
         _check(res.get_state(i), x, 1e-13)
+
+
+def test_synchronize_matches_repeated_updates(cuda):
+    """synchronize (mod_reservoir.f90:1352-1378): `length` updates from a sequence of
+    feedback blocks, no readout -- the state equals `length` oracle predict steps'
+    x; a following predict reads out from it."""
+    import torch
+
+    res, ws = _build(CASES[:4], n_override=500)
+    length = 5
+    o = res.fb_offsets
+    stride = int(o[-1]) + 3  # padded blocks: stride > packed size
+    blocks = np.zeros((length, stride))
+    for t in range(length):
+        blocks[t, :o[-1]] = np.concatenate([feedback_vector(w.region + 31 * t, w.ninp) for w in ws])
+    res.synchronize(torch.from_numpy(blocks).to(cuda), length, stride=stride)
+    torch.cuda.synchronize()
+    lm0 = np.zeros(132)
+    for i, w in enumerate(ws):
+        x = initial_state(w.region, w.n)
+        for t in range(length):
+            _, x = _oracle_step(w, x, blocks[t, o[i]:o[i + 1]], lm0)
+        _check(res.get_state(i), x, X_TOL * length)
+    with pytest.raises(ValueError):
+        res.synchronize(torch.zeros(10, dtype=torch.float64, device=cuda), length)
+    res.synchronize(torch.zeros(1, dtype=torch.float64, device=cuda), 0)  # no-op

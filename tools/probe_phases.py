@@ -25,7 +25,7 @@ if phys:
 d.set_clock(1, True)
 d.window(24)
 torch.cuda.synchronize()
-K = {0: ("grid" if phys else "rows", ["gridx", "gridpoint/physics"] if phys else ["load", "gridx", "gridpoint", "specx"]),
+K = {0: ("grid" if phys else "rows", ["gridx", "gridpoint/physics", "specx"] if phys else ["load", "gridx", "gridpoint", "specx"]),
      1: ("spec (chained)", ["load", "specy", "combine", "tail", "inv_inputs", "gridy"]),
      2: ("specx", ["load", "fft+store"]),
      3: ("spec (last)", ["load", "specy", "combine", "tail"])}
