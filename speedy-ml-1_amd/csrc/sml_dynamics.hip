@@ -91,6 +91,12 @@ struct sml_dynamics {
     double *d_phys = nullptr;  // physics tendencies: staging for a host's, or the GPU phypar's output
     double *d_minmax = nullptr;  // iogrid(30) safety check: min/max of u, v, t, q
     double *d_io = nullptr;      // staging for the host iogrid calls (grid4d + logp)
+    // iogrid(30)'s safety check (re-grid + min/max) runs on its own stream beside the
+    // window: its inputs [kNIo][kSF], Fourier [kNIo][kVF] and grid [kNIo][kGF] buffers
+    double *d_chk = nullptr;
+    hipStream_t chk_stream = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_chk = nullptr;
+    bool chk_pending = false;  // work on chk_stream that the next user of d_chk must wait for
     bool impint_done = false;
     // GPU physics (phypar): tables, boundary fields [kNBc][ngp], radiation state
     PhysTables ptab;
@@ -362,7 +368,7 @@ __global__ __launch_bounds__(64) void k_phys(const double *__restrict__ ug1, con
         qa[k] = qg1[(size_t)k * kNGP + j];
         phi[k] = phig1[(size_t)k * kNGP + j];
     }
-    phys_column(j, ua, va, ta, qa, phi, pslg1[j], bc, rad, PT, lradsw != 0, ut, vt, tt, qt);
+    phys_column(j, ua, va, ta, qa, phi, pslg1[j], bc, rad, PT, &PT->fband[0][0], lradsw != 0, ut, vt, tt, qt);
 #pragma unroll
     for (int k = 0; k < kKX; ++k) {
         P[(size_t)k * kNGP + j] = ut[k];
@@ -1025,7 +1031,7 @@ __global__ __launch_bounds__(kRowThreads) void k_st_grid(
         qa[k] = g(kPQ1 + k);
         ph[k] = g(kPPhi1 + k);
     }
-    phys_column(pt, ua, va, ta, qa, ph, g(kPPs1), bc, rad, PT, lradsw != 0, ut, vt, tt, qt);
+    phys_column(pt, ua, va, ta, qa, ph, g(kPPs1), bc, rad, PT, &PT->fband[0][0], lradsw != 0, ut, vt, tt, qt);
 #pragma unroll
     for (int k = 0; k < kKX; ++k) {
         P[(size_t)k * kGF + pt] = ut[k];
@@ -1165,7 +1171,7 @@ __global__ __launch_bounds__(kGsThreads) void k_st_gridspec(
             ph[k] = Ai[kPPhi1 + k];
         }
         const double ps1 = Ai[kPPs1];
-        phys_column(pt, ua, va, ta, qa, ph, ps1, bc, rad, PT, lradsw != 0, ut, vt, tt, qt);
+        phys_column(pt, ua, va, ta, qa, ph, ps1, bc, rad, PT, &PT->fband[0][0], lradsw != 0, ut, vt, tt, qt);
 #pragma unroll
         for (int k = 0; k < kKX; ++k) {
             Ai[phys_slot_col(k)] = ut[k];
@@ -1474,6 +1480,13 @@ extern "C" int sml_dyn_destroy(sml_dynamics *d) {
     for (auto &r : d->wreplay)
         if (r.exec) (void)hipGraphExecDestroy(r.exec);
     if (d->cap_stream) (void)hipStreamDestroy(d->cap_stream);
+    if (d->chk_stream) {
+        (void)hipStreamSynchronize(d->chk_stream);
+        (void)hipStreamDestroy(d->chk_stream);
+    }
+    if (d->ev_fork) (void)hipEventDestroy(d->ev_fork);
+    if (d->ev_chk) (void)hipEventDestroy(d->ev_chk);
+    if (d->d_chk) (void)hipFree(d->d_chk);
     if (d->sp) sml_spectral_destroy(d->sp);
     delete d;
     return SML_OK;
@@ -1507,6 +1520,7 @@ extern "C" int sml_dyn_create(double radius, sml_dynamics **out) {
         (rc = dalloc(&d->d_vfm, (size_t)kMX * kVFm)) || (rc = dalloc(&d->d_sm, (size_t)kMX * kSM)) ||
         (rc = dalloc(&d->d_phys, (size_t)4 * kKX * kGF)) || (rc = dalloc(&d->d_minmax, 8)) ||
         (rc = dalloc(&d->d_io, (size_t)4 * kKX * kGF + kGF)) || (rc = dalloc(&d->d_ptab, 1)) ||
+        (rc = dalloc(&d->d_chk, (size_t)kNIo * (kSF + kVF + kGF))) ||
         (rc = dalloc(&d->d_pbc, (size_t)kNBc * kNGP)) || (rc = dalloc(&d->d_rad, kRadSize)) ||
         (rc = dalloc(&d->d_pio, (size_t)(5 * kKX + 1 + 4 * kKX) * kNGP))) {
         sml_dyn_destroy(d);
@@ -1913,14 +1927,18 @@ extern "C" int sml_phys_sflset(const double *phi0, double *forog) {
 namespace {
 
 // iogrid inverse half: level 1 -> G = [u 8 | v 8 | t 8 | q 8 | ps] grids
-int io_to_grid_fields(sml_dynamics *d, hipStream_t st) {
+// spectral state -> grid u, v, t, q, ps (iogrid's re-gridding): k_io_prep into
+// specin, gridy into varm, gridx into grid
+int io_to_grid_fields(sml_dynamics *d, hipStream_t st, double *specin, double *varm, double *grid) {
     const DynTables *T = d->d_tab;
-    hipLaunchKernelGGL(k_io_prep, dim3((kMN + 127) / 128, kKX), dim3(128), 0, st, d->d_state, d->d_specin, T);
+    hipLaunchKernelGGL(k_io_prep, dim3((kMN + 127) / 128, kKX), dim3(128), 0, st, d->d_state, specin, T);
     SML_HIP(hipGetLastError());
-    if (int rc = spectral_gridy(d->sp, d->d_specin, d->d_varm, kNIo, st)) return rc;
-    if (int rc = spectral_gridx(d->sp, d->d_varm, d->d_grid, kNIoWind, 2, st)) return rc;
-    return spectral_gridx(d->sp, d->d_varm + (size_t)kNIoWind * kVF, d->d_grid + (size_t)kNIoWind * kGF,
-                          kNIo - kNIoWind, 1, st);
+    if (int rc = spectral_gridy(d->sp, specin, varm, kNIo, st)) return rc;
+    return spectral_gridx_range(d->sp, varm, grid, kNIo, 0, kNIoWind, st);  // winds kcos = 2, the rest 1
+}
+
+int io_to_grid_fields(sml_dynamics *d, hipStream_t st) {
+    return io_to_grid_fields(d, st, d->d_specin, d->d_varm, d->d_grid);
 }
 
 }  // namespace
@@ -1930,18 +1948,49 @@ extern "C" int sml_dyn_from_grid(sml_dynamics *d, const double *d_grid4d, const 
     SML_REQUIRE(d && d_grid4d && d_logp, "null argument");
     hipStream_t st = (hipStream_t)stream;
     const DynTables *T = d->d_tab;
+    if (d->chk_pending) {  // the previous check still reads d_chk
+        SML_HIP(hipStreamWaitEvent(st, d->ev_chk, 0));
+        d->chk_pending = false;
+    }
     hipLaunchKernelGGL(k_io_gather, dim3((kGF + 255) / 256, kKX), dim3(256), 0, st, d_grid4d, d_logp, d->d_gfwd);
     SML_HIP(hipGetLastError());
-    if (int rc = spectral_specx(d->sp, d->d_gfwd, d->d_varm, kNIoWind, 1, st)) return rc;  // vdspec kcos = 2
-    if (int rc = spectral_specx(d->sp, d->d_gfwd + (size_t)kNIoWind * kGF, d->d_varm + (size_t)kNIoWind * kVF,
-                                kNIo - kNIoWind, 0, st))
-        return rc;
+    // vdspec kcos = 2 (x cosgr) on the winds, none on the rest: one launch
+    if (int rc = spectral_specx_split(d->sp, d->d_gfwd, d->d_varm, kNIo, kNIoWind, st)) return rc;
     if (int rc = spectral_specy(d->sp, d->d_varm, d->d_sfwd, kNIo, st)) return rc;
     hipLaunchKernelGGL(k_io_combine, dim3((kMN + 127) / 128, kKX), dim3(128), 0, st, d->d_sfwd, d->d_state, T);
     SML_HIP(hipGetLastError());
-    if (int rc = io_to_grid_fields(d, st)) return rc;
-    hipLaunchKernelGGL(k_io_minmax, dim3(4), dim3(1024), 0, st, d->d_grid, d_minmax ? d_minmax : d->d_minmax);
+    // the safety check (:556-571) reads the new state: its k_io_prep stays on st (the
+    // window overwrites the state), the rest of it runs on chk_stream beside the
+    // window.  A caller's d_minmax is ready in st's order; the internal one (nullptr)
+    // only for the next user of d_chk (which waits for it).
+    double *cs = d->d_chk, *cv = cs + (size_t)kNIo * kSF, *cg = cv + (size_t)kNIo * kVF;
+    hipLaunchKernelGGL(k_io_prep, dim3((kMN + 127) / 128, kKX), dim3(128), 0, st, d->d_state, cs, T);
     SML_HIP(hipGetLastError());
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    SML_HIP(hipStreamIsCapturing(st, &cap));
+    hipStream_t cst = st;
+    if (cap == hipStreamCaptureStatusNone) {
+        if (!d->chk_stream) {
+            SML_HIP(hipStreamCreateWithFlags(&d->chk_stream, hipStreamNonBlocking));
+            SML_HIP(hipEventCreateWithFlags(&d->ev_fork, hipEventDisableTiming));
+            SML_HIP(hipEventCreateWithFlags(&d->ev_chk, hipEventDisableTiming));
+        }
+        SML_HIP(hipEventRecord(d->ev_fork, st));
+        SML_HIP(hipStreamWaitEvent(d->chk_stream, d->ev_fork, 0));
+        cst = d->chk_stream;
+    }
+    if (int rc = spectral_gridy(d->sp, cs, cv, kNIo, cst)) return rc;
+    if (int rc = spectral_gridx_range(d->sp, cv, cg, kNIo, 0, kNIoWind, cst)) return rc;
+    hipLaunchKernelGGL(k_io_minmax, dim3(4), dim3(1024), 0, cst, cg, d_minmax ? d_minmax : d->d_minmax);
+    SML_HIP(hipGetLastError());
+    if (cst != st) {
+        SML_HIP(hipEventRecord(d->ev_chk, cst));
+        d->chk_pending = true;
+        if (d_minmax) {
+            SML_HIP(hipStreamWaitEvent(st, d->ev_chk, 0));
+            d->chk_pending = false;
+        }
+    }
     return SML_OK;
 }
 

@@ -88,12 +88,13 @@ __device__ inline double qsat_at(double ta, double ps, double s) {
     return 622. * q / (s * ps - 0.378 * q);
 }
 
-// fband(nint(t), jb); the index is clamped to the table (the reference reads
-// outside it only for temperatures outside 100..400 K)
-__device__ inline double fband_at(const PhysTables *P, double t, int jb) {
+// row fband(nint(t), 1:4) of the table fb[301][4] (global or an LDS copy); the
+// index is clamped to the table (the reference reads outside it only for
+// temperatures outside 100..400 K)
+__device__ inline const double *fband_row(const double *fb, double t) {
     int it = (int)round(t);
     it = it < 100 ? 100 : (it > 400 ? 400 : it);
-    return P->fband[it - 100][jb];
+    return fb + (it - 100) * 4;
 }
 
 #endif  // __HIPCC__
@@ -103,12 +104,12 @@ __device__ inline double fband_at(const PhysTables *P, double t, int jb) {
 // One column j of phypar's physics.  Inputs (registers): ua, va, ta, qa, phi [kx]
 // (k = 0 top) and psl = the column's ug1, vg1, tg1, qg1, phig1, pslg1
 // (phy_phypar.f90:53-66); bc = kNBc fields [ngp]; rad = radiation state (in/out,
-// column j).  Outputs: the u, v, t, q tendencies of the physics (phypar's additions
-// to the dynamical tendencies).
+// column j); fbt = P->fband or a copy of it in LDS.  Outputs: the u, v, t, q
+// tendencies of the physics (phypar's additions to the dynamical tendencies).
 __device__ inline void phys_column(int j, const double *ua, const double *va, const double *ta, const double *qa_in,
                                    const double *phi, double psl, const double *__restrict__ bc,
-                                   double *__restrict__ rad, const PhysTables *P, bool lradsw, double *ut_o,
-                                   double *vt_o, double *tt_o, double *qt_o) {
+                                   double *__restrict__ rad, const PhysTables *P, const double *fbt, bool lradsw,
+                                   double *ut_o, double *vt_o, double *tt_o, double *qt_o) {
     using namespace phys;
     constexpr int NL = kKX, nl1 = kKX - 1;  // nl1: 1-based index of the level above the bottom
     auto BC = [&](int f) { return bc[(size_t)f * kNGP + j]; };
@@ -407,6 +408,13 @@ __device__ inline void phys_column(int j, const double *ua, const double *va, co
 
     // 3.2 radlw(-1): downward longwave (phy_radiat.f90:330-413)
     double st4a1[NL], st4a2[NL], flux[4], dfabs[NL], fsfcd;
+    double fbk[NL][4];  // fband(nint(ta(k)), 1:4): one table row per level, for both radlw passes
+#pragma unroll
+    for (int k = 0; k < NL; ++k) {
+        const double *row = fband_row(fbt, ta[k]);
+#pragma unroll
+        for (int jb = 0; jb < 4; ++jb) fbk[k][jb] = row[jb];
+    }
     {
 #pragma unroll
         for (int k = 1; k <= nl1; ++k) st4a1[k - 1] = ta[k - 1] + P->wvi[k - 1][1] * (ta[k] - ta[k - 1]);
@@ -435,7 +443,7 @@ __device__ inline void phys_column(int j, const double *ua, const double *va, co
 #pragma unroll
         for (int jb = 0; jb < 2; ++jb) {
             const double emis = 1. - TAU(jb, 0);
-            const double brad = fband_at(P, ta[0], jb) * (st4a1[0] + emis * st4a2[0]);
+            const double brad = fbk[0][jb] * (st4a1[0] + emis * st4a2[0]);
             flux[jb] = emis * brad;
             dfabs[0] = dfabs[0] - flux[jb];
         }
@@ -446,7 +454,7 @@ __device__ inline void phys_column(int j, const double *ua, const double *va, co
             for (int k = 2; k <= NL; ++k) {
                 const double tau = TAU(jb, k - 1);
                 const double emis = 1. - tau;
-                const double brad = fband_at(P, ta[k - 1], jb) * (st4a1[k - 1] + emis * st4a2[k - 1]);
+                const double brad = fbk[k - 1][jb] * (st4a1[k - 1] + emis * st4a2[k - 1]);
                 dfabs[k - 1] = dfabs[k - 1] + flux[jb];
                 flux[jb] = tau * flux[jb] + emis * brad;
                 dfabs[k - 1] = dfabs[k - 1] - flux[jb];
@@ -539,8 +547,9 @@ __device__ inline void phys_column(int j, const double *ua, const double *va, co
     // 3.4 radlw(1): upward longwave (phy_radiat.f90:414-458)
     {
         const double refsfc = 1. - emisfc, fsfcu = slru3;
+        const double *fsr = fband_row(fbt, tsfc);
 #pragma unroll
-        for (int jb = 0; jb < 4; ++jb) flux[jb] = fband_at(P, tsfc, jb) * fsfcu + refsfc * flux[jb];
+        for (int jb = 0; jb < 4; ++jb) flux[jb] = fsr[jb] * fsfcu + refsfc * flux[jb];
         dfabs[NL - 1] = dfabs[NL - 1] + epslw * fsfcu;
 #pragma unroll
         for (int jb = 0; jb < 4; ++jb)
@@ -548,7 +557,7 @@ __device__ inline void phys_column(int j, const double *ua, const double *va, co
             for (int k = NL; k >= 2; --k) {
                 const double tau = TAU(jb, k - 1);
                 const double emis = 1. - tau;
-                const double brad = fband_at(P, ta[k - 1], jb) * (st4a1[k - 1] - emis * st4a2[k - 1]);
+                const double brad = fbk[k - 1][jb] * (st4a1[k - 1] - emis * st4a2[k - 1]);
                 dfabs[k - 1] = dfabs[k - 1] + flux[jb];
                 flux[jb] = tau * flux[jb] + emis * brad;
                 dfabs[k - 1] = dfabs[k - 1] - flux[jb];
@@ -557,7 +566,7 @@ __device__ inline void phys_column(int j, const double *ua, const double *va, co
         for (int jb = 0; jb < 2; ++jb) {
             const double tau = TAU(jb, 0);
             const double emis = 1. - tau;
-            const double brad = fband_at(P, ta[0], jb) * (st4a1[0] - emis * st4a2[0]);
+            const double brad = fbk[0][jb] * (st4a1[0] - emis * st4a2[0]);
             dfabs[0] = dfabs[0] + flux[jb];
             flux[jb] = tau * flux[jb] + emis * brad;
             dfabs[0] = dfabs[0] - flux[jb];

@@ -110,10 +110,10 @@ constexpr int kFftThreads = 64;
 
 // gridx (spe_subfft_fftpack.f90:15-51): fvar(1) = varm(1) (Im of m = 0 dropped),
 // fvar(m-1) = varm(m) for m = 3..mx2, 0 beyond; rfftb; x cosgr(j) for kcos = 2 (the
-// fields from ncos1 on)
+// fields c0 <= f < c1)
 __global__ __launch_bounds__(kFftThreads) void k_gridx(const double *__restrict__ varm, double *__restrict__ grid,
                                                        const double *__restrict__ wa, const double *__restrict__ cosgr,
-                                                       int nf, int ncos1) {
+                                                       int nf, int c0, int c1) {
     __shared__ double was[kFftWa];  // twiddles: LDS broadcast reads inside the FFT
     if (threadIdx.x < kFftWa) was[threadIdx.x] = wa[threadIdx.x];
     if (threadIdx.x + kFftThreads < kFftWa) was[threadIdx.x + kFftThreads] = wa[threadIdx.x + kFftThreads];
@@ -129,10 +129,11 @@ __global__ __launch_bounds__(kFftThreads) void k_gridx(const double *__restrict_
 #pragma unroll
     for (int e = kMX2 - 1; e < kFftN; ++e) x[e] = 0.0;
     fft::rfftb96_reg(x, was);
-    const double cj = f >= ncos1 ? cosgr[j] : 1.0;
+    const bool k2 = f >= c0 && f < c1;
+    const double cj = k2 ? cosgr[j] : 1.0;
     double *g = grid + (size_t)f * kGridField + j * kIX;
 #pragma unroll
-    for (int e = 0; e < kFftN; ++e) g[e] = f >= ncos1 ? x[e] * cj : x[e];
+    for (int e = 0; e < kFftN; ++e) g[e] = k2 ? x[e] * cj : x[e];
 }
 
 // specx (spe_subfft_fftpack.f90:55-87): fvar = vorg(:, j) (the first nscaled fields
@@ -398,7 +399,7 @@ extern "C" int sml_gridx_batched(sml_spectral *s, const double *d_varm, double *
     if (int rc = check_ctx(s, nf)) return rc;
     if (nf == 0) return SML_OK;
     hipLaunchKernelGGL(k_gridx, dim3((nf * kIL + kFftThreads - 1) / kFftThreads), dim3(kFftThreads), 0, (hipStream_t)stream,
-                       d_varm, d_grid, s->d_wa, s->d_cosgr, nf, kcos == 1 ? nf : 0);
+                       d_varm, d_grid, s->d_wa, s->d_cosgr, nf, kcos == 1 ? nf : 0, nf);
     SML_HIP(hipGetLastError());
     return SML_OK;
 }
@@ -540,13 +541,17 @@ int spectral_gridy(sml_spectral *s, const double *spec, double *varm, int nf, hi
 }
 
 int spectral_gridx(sml_spectral *s, const double *varm, double *grid, int nf, int kcos, hipStream_t st) {
-    return spectral_gridx_split(s, varm, grid, nf, kcos == 1 ? nf : 0, st);
+    return spectral_gridx_range(s, varm, grid, nf, kcos == 1 ? nf : 0, nf, st);
 }
 
 int spectral_gridx_split(sml_spectral *s, const double *varm, double *grid, int nf, int ncos1, hipStream_t st) {
+    return spectral_gridx_range(s, varm, grid, nf, ncos1, nf, st);
+}
+
+int spectral_gridx_range(sml_spectral *s, const double *varm, double *grid, int nf, int c0, int c1, hipStream_t st) {
     if (nf <= 0) return SML_OK;
     hipLaunchKernelGGL(k_gridx, dim3((nf * kIL + kFftThreads - 1) / kFftThreads), dim3(kFftThreads), 0, st, varm, grid, s->d_wa,
-                       s->d_cosgr, nf, ncos1);
+                       s->d_cosgr, nf, c0, c1);
     SML_HIP(hipGetLastError());
     return SML_OK;
 }

@@ -85,15 +85,19 @@ class HybridLoop:
         with torch.cuda.stream(m):
             glob = self.exchange(self.ov)  # RCCL all-gather over xGMI when world > 1
         self.res.assemble(glob, self.g4, self.g2, self.pr, stream=m)
-        self.ev_grid.record(m)
+        if self.overlap:  # (one stream: stream order suffices, and an event record costs ~7 us of GPU idle)
+            self.ev_grid.record(m)
         self.res.tile_feedback(self.g4, self.g2, self.pr, self.tisr, self.fb, stream=m)
-        s.wait_event(self.ev_grid)
+        if self.overlap:
+            s.wait_event(self.ev_grid)
         self.dyn.from_grid(self.g4, self.g2, stream=s)   # iogrid(30)
         self.dyn.window(self.nleap, stream=s)            # stepone + 24 x step(2,2), physics on
         self.dyn.to_grid(self.f4, self.f2, stream=s)     # iogrid(31)
         self.res.tile_local_model(self.f4, self.f2, self.lm, stream=s)
-        self.ev_lm.record(s)
+        if self.overlap:
+            self.ev_lm.record(s)
 
     def sync(self):
-        self.main.wait_event(self.ev_lm)
+        if self.overlap:
+            self.main.wait_event(self.ev_lm)
         torch.cuda.synchronize(self.dev)
