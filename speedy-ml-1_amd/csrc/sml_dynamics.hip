@@ -684,11 +684,12 @@ __global__ __launch_bounds__(256) void k_dyn_tail(double *__restrict__ st, doubl
 //               state (uvspec, grad, geop) -> gridy
 //   k_st_inv    (m): the inverse-transform inputs + gridy from the state in memory,
 //               for a step that follows no fused step (window start)
-// A leapfrog step is 2 launches (3 with GPU physics) instead of 8 / 9.  Each block
-// first stages everything it reads -- the m's slice of the state, the row's Fourier
-// coefficients -- in LDS with coalesced loads: the fused step keeps its own m-major
-// copies of the state ([m][var][lev][k][n p], k_state_to_m / k_state_from_m around
-// a run of fused steps) and of the forward Fourier coefficients ([m][f][lat][p]),
+// A leapfrog step is 2 launches (with GPU physics: k_st_gridspec + k_st_spec)
+// instead of 8 / 9.  Each block first stages everything it reads -- the m's slice of
+// the state, the row's Fourier coefficients -- in LDS with coalesced loads: the
+// fused step keeps its own m-major copies of the state ([m][var][lev][k][n p],
+// k_state_to_m before a run of fused steps; the run's last k_st_spec writes the
+// reference layout back) and of the forward Fourier coefficients ([m][lat][f][p]),
 // so each block's slice is contiguous.  Every stage keeps the unfused kernels'
 // arithmetic, operand order and MFMA tiling: results are bit-identical to them
 // (tests/test_physics_gpu.py).
@@ -730,19 +731,18 @@ __global__ void k_state_to_m(const double *__restrict__ st, double *__restrict__
     sm[e] = v;
 }
 
-__global__ void k_state_from_m(const double *__restrict__ sm, double *__restrict__ st) {
-    const int e = blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= kMX * kSM) return;
-    const int m = e / kSM, i = e % kSM;
+// element i of m's slice (smi layout) into the reference-layout state
+__device__ inline void put_state(double *__restrict__ st, int m, int i, double v) {
     const int cc = i % kCW, k = (i / kCW) % kKX, lev = (i / (kCW * kKX)) % 2, var = i / (2 * kKX * kCW);
     const int c = ci(cc & 1, m, cc >> 1);
     if (var < 4) {
         const size_t off = var == 0 ? kOffVor : var == 1 ? kOffDiv : var == 2 ? kOffT : kOffTr;
-        st[off + ((size_t)lev * kKX + k) * kSF + c] = sm[e];
+        st[off + ((size_t)lev * kKX + k) * kSF + c] = v;
     } else if (k == 0) {
-        st[kOffPs + (size_t)lev * kSF + c] = sm[e];
+        st[kOffPs + (size_t)lev * kSF + c] = v;
     }
 }
+
 
 // The inverse-transform inputs of one m (k_dyn_prep's fields, same expressions)
 // from the m's state slice Sst (smi layout); writes In[f][kCW] for f < nin.  The
@@ -1215,7 +1215,8 @@ __global__ __launch_bounds__(kSpecBlk) void k_st_spec(
     double *__restrict__ sm, double *__restrict__ Td, double *__restrict__ phi_out, const double *__restrict__ phis,
     const double *__restrict__ tcorh, const double *__restrict__ qcorh, const DynTables *__restrict__ T, int j1,
     int j4, double dt, double alph, double rob, double wil, const double *__restrict__ pinv,
-    double *__restrict__ varm_next, int next_j2, int n1, int nin, const double *__restrict__ tabm, long long *dbg) {
+    double *__restrict__ varm_next, int next_j2, int n1, int nin, const double *__restrict__ tabm,
+    double *__restrict__ state_out, long long *dbg) {
     __shared__ double V[kVFm];            // this m's forward Fourier coefficients [lat][f][p]
     __shared__ double S[kNInvMax * kCW];  // specy output [f][2 n + p]; then the next step's inputs
     __shared__ double sh[2][kKX][kCW];
@@ -1337,11 +1338,14 @@ __global__ __launch_bounds__(kSpecBlk) void k_st_spec(
         tail_coef_barriers(alph);
     __syncthreads();  // S is free, Sst complete
     stamp(dbg, sk, 4);
+    if (next_j2 <= 0) {  // the run of fused steps ends: the state straight into the reference layout
+        for (int i = threadIdx.x; i < kSM; i += kSpecBlk) put_state(state_out, m, i, Sst[i]);
+        return;  // block-uniform
+    }
     {
         double2 *dst = reinterpret_cast<double2 *>(sm + (size_t)m * kSM);
         for (int i = threadIdx.x; i < kSM / 2; i += kSpecBlk) dst[i] = reinterpret_cast<const double2 *>(Sst)[i];
     }
-    if (next_j2 <= 0) return;  // block-uniform
     // d) the next step's inverse-transform inputs (k_dyn_prep) and gridy
     if (holds) inv_inputs(Sst, S, Fm, tb, m, next_j2, n1, nin);
     __syncthreads();
@@ -1410,19 +1414,6 @@ __global__ void k_io_prep(const double *__restrict__ st, double *__restrict__ si
         sin_[(size_t)(3 * kKX + k) * kSF + c] = st[kOffTr + (size_t)k * kSF + c];
         if (k == 0) sin_[(size_t)(4 * kKX) * kSF + c] = st[kOffPs + c];
     }
-}
-
-// exit: grid fields -> variables3d / logp (:590-595)
-__global__ void k_io_scatter(const double *__restrict__ G, double *__restrict__ g4, double *__restrict__ logp) {
-    const int pt = blockIdx.x * blockDim.x + threadIdx.x;
-    if (pt >= kGF) return;
-    const int k = blockIdx.y;
-    double *dst = g4 + g4i(0, pt, k);
-    dst[0] = G[(size_t)(2 * kKX + k) * kGF + pt];
-    dst[1] = G[(size_t)k * kGF + pt];
-    dst[2] = G[(size_t)(kKX + k) * kGF + pt];
-    dst[3] = G[(size_t)(3 * kKX + k) * kGF + pt];
-    if (k == 0) logp[pt] = G[(size_t)(4 * kKX) * kGF + pt];
 }
 
 // entry safety check (:556-571): min / max of the re-gridded u, v, t, q.  One
@@ -1660,10 +1651,11 @@ int launch_step_unfused(sml_dynamics *d, int j1, int j2, double dt, double alph,
     return SML_OK;
 }
 
-// the fused step: [k_state_to_m k_st_inv] (k_st_rows | k_st_grid k_st_specx) k_st_spec
-// [k_state_from_m].  chained: the previous launch_step's k_st_spec left the m-major
-// state and this step's gridy output (its next_j2 was this j2); next_j2 > 0: this
-// step's k_st_spec prepares step (.., next_j2) and the state stays m-major.
+// the fused step: [k_state_to_m k_st_inv] (k_st_rows | k_st_gridspec) k_st_spec.
+// chained: the previous launch_step's k_st_spec left the m-major state and this
+// step's gridy output (its next_j2 was this j2); next_j2 > 0: this step's k_st_spec
+// prepares step (.., next_j2) and the state stays m-major, else it writes the
+// reference-layout state.
 
 int launch_step_fused(sml_dynamics *d, int j1, int j2, double dt, double alph, double rob, double wil,
                       const double *d_phys, bool lradsw, hipStream_t st, bool chained, int next_j2) {
@@ -1700,12 +1692,9 @@ int launch_step_fused(sml_dynamics *d, int j1, int j2, double dt, double alph, d
     const int j4 = (alph == 0.0) ? j2 : 1;
     hipLaunchKernelGGL(k_st_spec, dim3(kMX), dim3(kSpecBlk), 0, st, d->d_vfm, sd.pfwd, sd.wt, d->d_sm, d->d_tend,
                        d->d_phi, d->d_phis, d->d_tcorh, d->d_qcorh, T, j1, j4, dt, alph, rob, wil, sd.pinv, d->d_varm,
-                       next_j2, n1, nin, d->d_tabm + (size_t)(d->d_tab - d->d_tabs) * kMX * kTabMDoubles, d->d_dbg);
+                       next_j2, n1, nin, d->d_tabm + (size_t)(d->d_tab - d->d_tabs) * kMX * kTabMDoubles, d->d_state,
+                       d->d_dbg);
     SML_HIP(hipGetLastError());
-    if (next_j2 <= 0) {
-        hipLaunchKernelGGL(k_state_from_m, dim3(conv_blocks), dim3(256), 0, st, d->d_sm, d->d_state);
-        SML_HIP(hipGetLastError());
-    }
     return SML_OK;
 }
 
@@ -1927,20 +1916,6 @@ extern "C" int sml_phys_sflset(const double *phi0, double *forog) {
 namespace {
 
 // iogrid inverse half: level 1 -> G = [u 8 | v 8 | t 8 | q 8 | ps] grids
-// spectral state -> grid u, v, t, q, ps (iogrid's re-gridding): k_io_prep into
-// specin, gridy into varm, gridx into grid
-int io_to_grid_fields(sml_dynamics *d, hipStream_t st, double *specin, double *varm, double *grid) {
-    const DynTables *T = d->d_tab;
-    hipLaunchKernelGGL(k_io_prep, dim3((kMN + 127) / 128, kKX), dim3(128), 0, st, d->d_state, specin, T);
-    SML_HIP(hipGetLastError());
-    if (int rc = spectral_gridy(d->sp, specin, varm, kNIo, st)) return rc;
-    return spectral_gridx_range(d->sp, varm, grid, kNIo, 0, kNIoWind, st);  // winds kcos = 2, the rest 1
-}
-
-int io_to_grid_fields(sml_dynamics *d, hipStream_t st) {
-    return io_to_grid_fields(d, st, d->d_specin, d->d_varm, d->d_grid);
-}
-
 }  // namespace
 
 extern "C" int sml_dyn_from_grid(sml_dynamics *d, const double *d_grid4d, const double *d_logp, double *d_minmax,
@@ -1997,10 +1972,12 @@ extern "C" int sml_dyn_from_grid(sml_dynamics *d, const double *d_grid4d, const 
 extern "C" int sml_dyn_to_grid(sml_dynamics *d, double *d_grid4d, double *d_logp, void *stream) {
     SML_REQUIRE(d && d_grid4d && d_logp, "null argument");
     hipStream_t st = (hipStream_t)stream;
-    if (int rc = io_to_grid_fields(d, st)) return rc;
-    hipLaunchKernelGGL(k_io_scatter, dim3((kGF + 255) / 256, kKX), dim3(256), 0, st, d->d_grid, d_grid4d, d_logp);
+    // exit (:590-595): the state re-gridded (k_io_prep, gridy, gridx) with the gridx
+    // writing variables3d / logp directly
+    hipLaunchKernelGGL(k_io_prep, dim3((kMN + 127) / 128, kKX), dim3(128), 0, st, d->d_state, d->d_specin, d->d_tab);
     SML_HIP(hipGetLastError());
-    return SML_OK;
+    if (int rc = spectral_gridy(d->sp, d->d_specin, d->d_varm, kNIo, st)) return rc;
+    return spectral_gridx_io(d->sp, d->d_varm, d_grid4d, d_logp, kNIoWind, st);
 }
 
 extern "C" int sml_dyn_is_safe(const double *minmax) {

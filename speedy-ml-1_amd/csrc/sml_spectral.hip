@@ -26,7 +26,7 @@
 #include <vector>
 
 #include "sml_fft.hpp"
-#include "sml_spectral_tables.hpp"
+#include "sml_dynamics_tables.hpp"  // (+ sml_spectral_tables.hpp): kx for the iogrid exit layout
 
 using namespace sml;
 
@@ -110,10 +110,13 @@ constexpr int kFftThreads = 64;
 
 // gridx (spe_subfft_fftpack.f90:15-51): fvar(1) = varm(1) (Im of m = 0 dropped),
 // fvar(m-1) = varm(m) for m = 3..mx2, 0 beyond; rfftb; x cosgr(j) for kcos = 2 (the
-// fields c0 <= f < c1)
+// fields c0 <= f < c1).  With g4 set, the 33 fields [u v t q (kx each) | ps] go
+// straight into iogrid(31)'s variables3d(4, ix, il, kx) (var = T, u, v, q) and logp
+// instead of grid (ppo_iogrid.f90:590-595)
 __global__ __launch_bounds__(kFftThreads) void k_gridx(const double *__restrict__ varm, double *__restrict__ grid,
                                                        const double *__restrict__ wa, const double *__restrict__ cosgr,
-                                                       int nf, int c0, int c1) {
+                                                       int nf, int c0, int c1, double *__restrict__ g4,
+                                                       double *__restrict__ logp) {
     __shared__ double was[kFftWa];  // twiddles: LDS broadcast reads inside the FFT
     if (threadIdx.x < kFftWa) was[threadIdx.x] = wa[threadIdx.x];
     if (threadIdx.x + kFftThreads < kFftWa) was[threadIdx.x + kFftThreads] = wa[threadIdx.x + kFftThreads];
@@ -132,8 +135,19 @@ __global__ __launch_bounds__(kFftThreads) void k_gridx(const double *__restrict_
     const bool k2 = f >= c0 && f < c1;
     const double cj = k2 ? cosgr[j] : 1.0;
     double *g = grid + (size_t)f * kGridField + j * kIX;
+    int gs = 1;
+    if (g4) {
+        const int grp = f / kKX, k = f % kKX;
+        if (grp < 4) {
+            const int var = grp == 0 ? 1 : grp == 1 ? 2 : grp == 2 ? 0 : 3;
+            g = g4 + var + 4 * ((size_t)kGridField * k + j * kIX);
+            gs = 4;
+        } else {
+            g = logp + j * kIX;
+        }
+    }
 #pragma unroll
-    for (int e = 0; e < kFftN; ++e) g[e] = k2 ? x[e] * cj : x[e];
+    for (int e = 0; e < kFftN; ++e) g[e * gs] = k2 ? x[e] * cj : x[e];
 }
 
 // specx (spe_subfft_fftpack.f90:55-87): fvar = vorg(:, j) (the first nscaled fields
@@ -399,7 +413,7 @@ extern "C" int sml_gridx_batched(sml_spectral *s, const double *d_varm, double *
     if (int rc = check_ctx(s, nf)) return rc;
     if (nf == 0) return SML_OK;
     hipLaunchKernelGGL(k_gridx, dim3((nf * kIL + kFftThreads - 1) / kFftThreads), dim3(kFftThreads), 0, (hipStream_t)stream,
-                       d_varm, d_grid, s->d_wa, s->d_cosgr, nf, kcos == 1 ? nf : 0, nf);
+                       d_varm, d_grid, s->d_wa, s->d_cosgr, nf, kcos == 1 ? nf : 0, nf, nullptr, nullptr);
     SML_HIP(hipGetLastError());
     return SML_OK;
 }
@@ -551,7 +565,15 @@ int spectral_gridx_split(sml_spectral *s, const double *varm, double *grid, int 
 int spectral_gridx_range(sml_spectral *s, const double *varm, double *grid, int nf, int c0, int c1, hipStream_t st) {
     if (nf <= 0) return SML_OK;
     hipLaunchKernelGGL(k_gridx, dim3((nf * kIL + kFftThreads - 1) / kFftThreads), dim3(kFftThreads), 0, st, varm, grid, s->d_wa,
-                       s->d_cosgr, nf, c0, c1);
+                       s->d_cosgr, nf, c0, c1, nullptr, nullptr);
+    SML_HIP(hipGetLastError());
+    return SML_OK;
+}
+
+int spectral_gridx_io(sml_spectral *s, const double *varm, double *g4, double *logp, int nwind, hipStream_t st) {
+    constexpr int nf = 4 * kKX + 1;
+    hipLaunchKernelGGL(k_gridx, dim3((nf * kIL + kFftThreads - 1) / kFftThreads), dim3(kFftThreads), 0, st, varm, nullptr,
+                       s->d_wa, s->d_cosgr, nf, 0, nwind, g4, logp);
     SML_HIP(hipGetLastError());
     return SML_OK;
 }
