@@ -1361,22 +1361,6 @@ __global__ __launch_bounds__(kSpecBlk) void k_st_spec(
 constexpr int kNIo = 4 * kKX + 1;
 constexpr int kNIoWind = 2 * kKX;
 
-__device__ inline int g4i(int v, int pt, int k) { return v + 4 * (pt + kGF * k); }
-
-// entry: real(4) copies (:503-511), q < 0 -> 0 on the real(4) copy (:516-518)
-__global__ void k_io_gather(const double *__restrict__ g4, const double *__restrict__ logp, double *__restrict__ F) {
-    const int pt = blockIdx.x * blockDim.x + threadIdx.x;
-    if (pt >= kGF) return;
-    const int k = blockIdx.y;
-    const double *src = g4 + g4i(0, pt, k);
-    F[(size_t)(2 * kKX + k) * kGF + pt] = (double)(float)src[0];
-    F[(size_t)k * kGF + pt] = (double)(float)src[1];
-    F[(size_t)(kKX + k) * kGF + pt] = (double)(float)src[2];
-    float q4 = (float)src[3];
-    if (q4 < 0.0f) q4 = 0.0f;
-    F[(size_t)(3 * kKX + k) * kGF + pt] = (double)q4;
-    if (k == 0) F[(size_t)(4 * kKX) * kGF + pt] = (double)(float)logp[pt];
-}
 
 // entry: vdspec's vds + spec, trunct, into time level 1 (:524-538)
 __global__ void k_io_combine(const double *__restrict__ S, double *__restrict__ st, const DynTables *__restrict__ T) {
@@ -1927,10 +1911,9 @@ extern "C" int sml_dyn_from_grid(sml_dynamics *d, const double *d_grid4d, const 
         SML_HIP(hipStreamWaitEvent(st, d->ev_chk, 0));
         d->chk_pending = false;
     }
-    hipLaunchKernelGGL(k_io_gather, dim3((kGF + 255) / 256, kKX), dim3(256), 0, st, d_grid4d, d_logp, d->d_gfwd);
-    SML_HIP(hipGetLastError());
-    // vdspec kcos = 2 (x cosgr) on the winds, none on the rest: one launch
-    if (int rc = spectral_specx_split(d->sp, d->d_gfwd, d->d_varm, kNIo, kNIoWind, st)) return rc;
+    // entry (:503-518): real(4) copies, q clip, then vdspec kcos = 2 (x cosgr) on the
+    // winds and none on the rest: one specx launch reading variables3d / logp
+    if (int rc = spectral_specx_io(d->sp, d_grid4d, d_logp, d->d_varm, kNIoWind, st)) return rc;
     if (int rc = spectral_specy(d->sp, d->d_varm, d->d_sfwd, kNIo, st)) return rc;
     hipLaunchKernelGGL(k_io_combine, dim3((kMN + 127) / 128, kKX), dim3(128), 0, st, d->d_sfwd, d->d_state, T);
     SML_HIP(hipGetLastError());

@@ -153,9 +153,14 @@ __global__ __launch_bounds__(kFftThreads) void k_gridx(const double *__restrict_
 // specx (spe_subfft_fftpack.f90:55-87): fvar = vorg(:, j) (the first nscaled fields
 // x scale_tab(j): vdspec's ug*cosgr(j) / ug*cosgr2(j), spe_spectral.f90:430-445);
 // rfftf; varm(1) = fvar(1)/ix, varm(2) = 0, varm(m) = fvar(m-1)/ix
+// With g4 set, the input is iogrid(30)'s variables3d(4, ix, il, kx) / logp: the 33
+// fields [u v t q (kx each) | ps] as their real(4) copies, q < 0 -> 0 on the copy
+// (ppo_iogrid.f90:503-518), instead of grid.
 __global__ __launch_bounds__(kFftThreads) void k_specx(const double *__restrict__ grid, double *__restrict__ varm,
                                                        const double *__restrict__ wa,
-                                                       const double *__restrict__ scale_tab, int nf, int nscaled) {
+                                                       const double *__restrict__ scale_tab, int nf, int nscaled,
+                                                       const double *__restrict__ g4 = nullptr,
+                                                       const double *__restrict__ logp = nullptr) {
     __shared__ double was[kFftWa];
     if (threadIdx.x < kFftWa) was[threadIdx.x] = wa[threadIdx.x];
     if (threadIdx.x + kFftThreads < kFftWa) was[threadIdx.x + kFftThreads] = wa[threadIdx.x + kFftThreads];
@@ -167,8 +172,29 @@ __global__ __launch_bounds__(kFftThreads) void k_specx(const double *__restrict_
     const bool sc = scale_tab && f < nscaled;
     const double s0 = sc ? scale_tab[j] : 1.0;
     double x[kFftN];
+    if (g4) {
+        const int grp = f / kKX, k = f % kKX;
+        if (grp < 4) {
+            const int var = grp == 0 ? 1 : grp == 1 ? 2 : grp == 2 ? 0 : 3;
+            const double *src = g4 + var + 4 * ((size_t)kGridField * k + j * kIX);
 #pragma unroll
-    for (int e = 0; e < kFftN; ++e) x[e] = sc ? g[e] * s0 : g[e];
+            for (int e = 0; e < kFftN; ++e) {
+                float v4 = (float)src[4 * e];
+                if (grp == 3 && v4 < 0.0f) v4 = 0.0f;
+                x[e] = (double)v4;
+            }
+        } else {
+#pragma unroll
+            for (int e = 0; e < kFftN; ++e) x[e] = (double)(float)logp[j * kIX + e];
+        }
+        if (sc) {
+#pragma unroll
+            for (int e = 0; e < kFftN; ++e) x[e] = x[e] * s0;
+        }
+    } else {
+#pragma unroll
+        for (int e = 0; e < kFftN; ++e) x[e] = sc ? g[e] * s0 : g[e];
+    }
     fft::rfftf96_reg(x, was);
     const double scale = 1. / (double)kIX;
     double *v = varm + (size_t)f * kVarmField + j * kMX2;
@@ -591,6 +617,15 @@ int spectral_specx_split(sml_spectral *s, const double *grid, double *varm, int 
     if (nf <= 0) return SML_OK;
     hipLaunchKernelGGL(k_specx, dim3((nf * kIL + kFftThreads - 1) / kFftThreads), dim3(kFftThreads), 0, st, grid, varm, s->d_wa,
                        s->d_cosgr, nf, nscaled);
+    SML_HIP(hipGetLastError());
+    return SML_OK;
+}
+
+int spectral_specx_io(sml_spectral *s, const double *g4, const double *logp, double *varm, int nwind,
+                      hipStream_t st) {
+    constexpr int nf = 4 * kKX + 1;
+    hipLaunchKernelGGL(k_specx, dim3((nf * kIL + kFftThreads - 1) / kFftThreads), dim3(kFftThreads), 0, st, nullptr, varm,
+                       s->d_wa, s->d_cosgr, nf, nwind, g4, logp);
     SML_HIP(hipGetLastError());
     return SML_OK;
 }

@@ -29,8 +29,11 @@ int spectral_gridx(sml_spectral *s, const double *varm, double *grid, int nf, in
 int spectral_gridx_split(sml_spectral *s, const double *varm, double *grid, int nf, int ncos1, hipStream_t st);
 // kcos = 2 (x cosgr) for the fields c0 <= f < c1, kcos = 1 for the others
 int spectral_gridx_range(sml_spectral *s, const double *varm, double *grid, int nf, int c0, int c1, hipStream_t st);
-// iogrid(31)'s exit: the 33 Fourier fields [u v t q | ps] (kcos = 2 for the first
+// iogrid(30)'s entry / iogrid(31)'s exit: specx from / gridx into variables3d and
+// logp directly (real(4) copies and the q clip on entry).  gridx_io: the 33 Fourier fields [u v t q | ps] (kcos = 2 for the first
 // nwind) straight into variables3d(4, ix, il, kx) and logp(ix, il)
+int spectral_specx_io(sml_spectral *s, const double *g4, const double *logp, double *varm, int nwind,
+                      hipStream_t st);
 int spectral_gridx_io(sml_spectral *s, const double *varm, double *g4, double *logp, int nwind, hipStream_t st);
 // scale: 0 none, 1 x cosgr(lat), 2 x cosgr2(lat) (vdspec's prescaling)
 int spectral_specx(sml_spectral *s, const double *grid, double *varm, int nf, int scale, hipStream_t st);
