@@ -24,6 +24,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <vector>
@@ -896,10 +897,13 @@ extern "C" int sml_res_kernel_times(sml_reservoirs *c, float *update_ms, float *
 namespace {
 // x_new = (1 - leak) x + leak tanh(A x + W_in u) for every local region (+ x~, x_aug)
 int launch_update(sml_reservoirs *c, const double *xo, double *xn, const double *d_feedback, hipStream_t st) {
-    // parts per region: enough blocks for ~4 rounds of the 512 resident 1024-thread
-    // blocks (2 per CU with ~54 KB LDS each), each part at least one 1024-row pass
+    // parts per region: enough blocks to fill the 512 resident 1024-thread block slots
+    // (2 per CU with ~54 KB LDS each) once, each part at least one 1024-row pass.  Every
+    // part stages the region's whole x, so more parts cost HBM traffic: measured on
+    // 1152 regions, 1 part 119 us, 2 parts 128 us, 4 parts 165 us (profiles/r01m)
     const int max_parts = std::max(1, (c->maxn + kUpdThreads - 1) / kUpdThreads);
-    const int parts = std::max(1, std::min(max_parts, (4 * 512 + c->nlocal - 1) / c->nlocal));
+    int parts = std::max(1, std::min(max_parts, (512 + c->nlocal - 1) / c->nlocal));
+    if (const char *e = std::getenv("SML_UPD_PARTS")) parts = std::max(1, std::min(max_parts, std::atoi(e)));
     const int lds_x = (c->maxn + 1) / 2 * 2;
     const size_t lds = (size_t)(lds_x + c->maxninp) * sizeof(double);
     const bool use_lds = lds <= 64 * 1024;
