@@ -903,7 +903,7 @@ static_assert(kNInvMax <= kRowThreads && kNFwd <= kRowThreads && kIX <= kRowThre
 
 // gridx of field f, row j (spe_subfft_fftpack.f90:24-45): packing, rfftb, x cosgr(j)
 // for kcos = 2; the 96 values into A[lon][f]
-__device__ inline void row_gridx(double *A, const double *__restrict__ varm, const double *__restrict__ wa, int f,
+__device__ __attribute__((always_inline)) inline void row_gridx(double *A, const double *__restrict__ varm, const double *__restrict__ wa, int f,
                                  int j, bool kcos2, double cj) {
     // the m-major coefficients vim[m][lat][f][p] of (f, j): coefficient c = 2 m + p
     const double *v = varm + (size_t)j * kVIl + f * 2;
@@ -922,7 +922,7 @@ __device__ inline void row_gridx(double *A, const double *__restrict__ varm, con
 // specx of field f, row j from x[96] (already x cosgr(j) where vdspec scales):
 // rfftf, varm(1) = fvar(1)/ix, varm(2) = 0, varm(m) = fvar(m-1)/ix, into the m-major
 // forward coefficients vfm[m][f][j][p]
-__device__ inline void row_specx(double *x, double *__restrict__ vfm, const double *__restrict__ wa, int f, int j) {
+__device__ __attribute__((always_inline)) inline void row_specx(double *x, double *__restrict__ vfm, const double *__restrict__ wa, int f, int j) {
     fft::rfftf96_reg(x, wa);
     const double scale = 1. / (double)kIX;
     double *o = vfm + (size_t)j * kVLs + f * 2;
