@@ -392,6 +392,7 @@ struct TabM {
     double xj[kNX][kKX][kKX];
 };
 constexpr int kTabMDoubles = (int)(sizeof(TabM) / sizeof(double));
+constexpr int kTabMPad = 2048;  // d_tabm tail: k_st_spec stages whole 16-B rows of 512 threads
 static_assert(kTabMDoubles % 2 == 0, "TabM is copied in 16-B pieces");
 
 #define SML_TAB_VEC(X) \
@@ -1227,7 +1228,10 @@ __global__ __launch_bounds__(kSpecBlk) void k_st_spec(
     const int sk = next_j2 > 0 ? 1 : 3;
     stamp(dbg, sk, 0);
     constexpr int RT = (kTabMDoubles / 2 + kSpecBlk - 1) / kSpecBlk;
-    double2 rt[RT];
+    // three named registers, not an array: held across specy, an array was kept in scratch
+    static_assert(RT == 3 && 2 * RT * kSpecBlk <= kVFm && 2 * RT * kSpecBlk - kTabMDoubles <= kTabMPad,
+                  "TabM staging");
+    double2 rt0, rt1, rt2;
     {   // stage the m's slices: every 16-B load issued before the first LDS store
         constexpr int NV = kVFm / 2, NS = kSM / 2, RV = (NV + kSpecBlk - 1) / kSpecBlk,
                       RS = (NS + kSpecBlk - 1) / kSpecBlk;
@@ -1245,11 +1249,12 @@ __global__ __launch_bounds__(kSpecBlk) void k_st_spec(
             rs[q] = ss[i < NS ? i : NS - 1];
         }
         load_forcing_m(Fm, phis, tcorh, qcorh, m);
-        const double2 *tsrc = reinterpret_cast<const double2 *>(tabm + (size_t)m * kTabMDoubles);
-#pragma unroll
-        for (int q = 0; q < RT; ++q) {  // this m's tables (into V's space once specy is done)
-            const int i = threadIdx.x + q * kSpecBlk;
-            rt[q] = tsrc[i < kTabMDoubles / 2 ? i : 0];
+        {   // this m's tables (into V's space once specy is done); past the slice: the
+            // next m's table or d_tabm's tail pad (unused)
+            const double2 *t = reinterpret_cast<const double2 *>(tabm + (size_t)m * kTabMDoubles) + threadIdx.x;
+            rt0 = t[0];
+            rt1 = t[kSpecBlk];
+            rt2 = t[2 * kSpecBlk];
         }
 #pragma unroll
         for (int q = 0; q < RV; ++q) {
@@ -1304,10 +1309,11 @@ __global__ __launch_bounds__(kSpecBlk) void k_st_spec(
     }
     __syncthreads();  // V is free: this m's tables go there
     TabM *tm = reinterpret_cast<TabM *>(V);
-#pragma unroll
-    for (int q = 0; q < RT; ++q) {
-        const int i = threadIdx.x + q * kSpecBlk;
-        if (i < kTabMDoubles / 2) reinterpret_cast<double2 *>(V)[i] = rt[q];
+    {
+        double2 *v2 = reinterpret_cast<double2 *>(V) + threadIdx.x;  // (V holds kVFm >= 2 RT kSpecBlk doubles)
+        v2[0] = rt0;
+        v2[kSpecBlk] = rt1;
+        v2[2 * kSpecBlk] = rt2;
     }
     __syncthreads();
     const LTab tb{tm};
@@ -1486,7 +1492,7 @@ extern "C" int sml_dyn_create(double radius, sml_dynamics **out) {
             sml_dyn_destroy(d);
             return rc;
         }
-    if ((rc = dalloc(&d->d_tabs, 4)) || (rc = dalloc(&d->d_tabm, (size_t)4 * kMX * kTabMDoubles)) || (rc = dalloc(&d->d_state, kStateSize)) || (rc = dalloc(&d->d_phis, kSF)) ||
+    if ((rc = dalloc(&d->d_tabs, 4)) || (rc = dalloc(&d->d_tabm, (size_t)4 * kMX * kTabMDoubles + kTabMPad)) || (rc = dalloc(&d->d_state, kStateSize)) || (rc = dalloc(&d->d_phis, kSF)) ||
         (rc = dalloc(&d->d_tcorh, kSF)) || (rc = dalloc(&d->d_qcorh, kSF)) || (rc = dalloc(&d->d_phi, kKX * kSF)) ||
         (rc = dalloc(&d->d_specin, (size_t)kNInvMax * kSF)) ||
         (rc = dalloc(&d->d_varm, (size_t)(kNInvMax > kNFwd ? kNInvMax : kNFwd) * kVF)) ||
