@@ -1218,7 +1218,7 @@ __global__ __launch_bounds__(kSpecBlk) void k_st_spec(
     int j4, double dt, double alph, double rob, double wil, const double *__restrict__ pinv,
     double *__restrict__ varm_next, int next_j2, int n1, int nin, const double *__restrict__ tabm,
     double *__restrict__ state_out, long long *dbg) {
-    __shared__ double V[kVFm];            // this m's forward Fourier coefficients [lat][f][p]
+    __shared__ double V[kVFm];            // this m's tables (TabM)
     __shared__ double S[kNInvMax * kCW];  // specy output [f][2 n + p]; then the next step's inputs
     __shared__ double sh[2][kKX][kCW];
     __shared__ double Sst[kSM];           // this m's state, updated in place
@@ -1232,41 +1232,27 @@ __global__ __launch_bounds__(kSpecBlk) void k_st_spec(
     static_assert((RT == 2 || RT == 3) && 2 * RT * kSpecBlk <= kVFm && 2 * RT * kSpecBlk - kTabMDoubles <= kTabMPad,
                   "TabM staging");
     double2 rt0, rt1, rt2 = {0.0, 0.0};
-    {   // stage the m's slices: every 16-B load issued before the first LDS store
-        constexpr int NV = kVFm / 2, NS = kSM / 2, RV = (NV + kSpecBlk - 1) / kSpecBlk,
-                      RS = (NS + kSpecBlk - 1) / kSpecBlk;
-        const double2 *src = reinterpret_cast<const double2 *>(vfm + (size_t)m * kVFm);
-        const double2 *ss = reinterpret_cast<const double2 *>(sm + (size_t)m * kSM);
-        double2 rv[RV], rs[RS];
-#pragma unroll
-        for (int q = 0; q < RV; ++q) {
-            const int i = threadIdx.x + q * kSpecBlk;
-            rv[q] = src[i < NV ? i : NV - 1];
-        }
-#pragma unroll
-        for (int q = 0; q < RS; ++q) {
-            const int i = threadIdx.x + q * kSpecBlk;
-            rs[q] = ss[i < NS ? i : NS - 1];
-        }
-        load_forcing_m(Fm, phis, tcorh, qcorh, m);
-        {   // this m's tables (into V's space once specy is done); past the slice: the
-            // next m's table or d_tabm's tail pad (unused)
-            const double2 *t = reinterpret_cast<const double2 *>(tabm + (size_t)m * kTabMDoubles) + threadIdx.x;
-            rt0 = t[0];
-            rt1 = t[kSpecBlk];
-            if constexpr (RT > 2) rt2 = t[2 * kSpecBlk];
-        }
-#pragma unroll
-        for (int q = 0; q < RV; ++q) {
-            const int i = threadIdx.x + q * kSpecBlk;
-            if (i < NV) reinterpret_cast<double2 *>(V)[i] = rv[q];
-        }
-#pragma unroll
-        for (int q = 0; q < RS; ++q) {
-            const int i = threadIdx.x + q * kSpecBlk;
-            if (i < NS) reinterpret_cast<double2 *>(Sst)[i] = rs[q];
-        }
+    // the m's state slice and tables: loads issued first, stored to LDS after specy
+    // (which reads its Fourier coefficients straight from vfm), so their latency
+    // hides behind it
+    constexpr int NS = kSM / 2, RS = (NS + kSpecBlk - 1) / kSpecBlk;
+    static_assert(RS == 5 && NS % kSpecBlk == 0, "state staging: five whole rows of the block");
+    double2 rs0, rs1, rs2, rs3, rs4;  // named registers (an array held across specy went to scratch)
+    {
+        const double2 *ss = reinterpret_cast<const double2 *>(sm + (size_t)m * kSM) + threadIdx.x;
+        rs0 = ss[0];
+        rs1 = ss[kSpecBlk];
+        rs2 = ss[2 * kSpecBlk];
+        rs3 = ss[3 * kSpecBlk];
+        rs4 = ss[4 * kSpecBlk];
+        // this m's tables (into V's space); past the slice: the next m's table or
+        // d_tabm's tail pad (unused)
+        const double2 *t = reinterpret_cast<const double2 *>(tabm + (size_t)m * kTabMDoubles) + threadIdx.x;
+        rt0 = t[0];
+        rt1 = t[kSpecBlk];
+        if constexpr (RT > 2) rt2 = t[2 * kSpecBlk];
     }
+    load_forcing_m(Fm, phis, tcorh, qcorh, m);
     // specy operands: wave w's tiles all use this m's Legendre columns of its lanes
     const double *pm = pfwd + (size_t)m * kNX * kIY;
     double wv[kIY / 4], bS[kIY / 4], bD[kIY / 4];
@@ -1277,23 +1263,30 @@ __global__ __launch_bounds__(kSpecBlk) void k_st_spec(
         bS[s] = pm[(2 * r) * kIY + j];
         bD[s] = pm[(2 * r + 1) * kIY + j];
     }
-    __syncthreads();
+    if (dbg) __syncthreads();
     stamp(dbg, sk, 1);
-    // a) specy (k_specy's tiling: 8 fields x Re/Im per wave)
+    // a) specy (k_specy's tiling: 8 fields x Re/Im per wave), the wave's A operands
+    // read from vfm [lat][f][p] (per instruction 4 latitudes x 128 contiguous bytes)
+    const double *vm = vfm + (size_t)m * kVFm;
     for (int tile = wave; tile < (kNFwd + 7) / 8; tile += kSpecBlk / 64) {
         const int f0 = tile * 8;
         const int fa = f0 + (r >> 1);
         const bool ok = fa < kNFwd;
-        const double *vr = V + (ok ? fa : 0) * 2 + (r & 1);
-        d4 accS = {0, 0, 0, 0}, accD = accS;
+        const double *vr = vm + (ok ? fa : 0) * 2 + (r & 1);
+        double vn[kIY / 4], vs[kIY / 4];
 #pragma unroll
         for (int s = 0; s < kIY / 4; ++s) {
             const int j = 4 * s + kk;
+            vn[s] = vr[(kIL - 1 - j) * kVLs];
+            vs[s] = vr[j * kVLs];
+        }
+        d4 accS = {0, 0, 0, 0}, accD = accS;
+#pragma unroll
+        for (int s = 0; s < kIY / 4; ++s) {
             double aS = 0.0, aD = 0.0;
             if (ok) {
-                const double vn = vr[(kIL - 1 - j) * kVLs], vs = vr[j * kVLs];
-                aS = (vn + vs) * wv[s];
-                aD = (vn - vs) * wv[s];
+                aS = (vn[s] + vs[s]) * wv[s];
+                aD = (vn[s] - vs[s]) * wv[s];
             }
             accS = MFMA64(aS, bS[s], accS);
             accD = MFMA64(aD, bD[s], accD);
@@ -1307,15 +1300,20 @@ __global__ __launch_bounds__(kSpecBlk) void k_st_spec(
             S[f * kCW + 2 * (2 * r + 1) + (row & 1)] = accD[q];
         }
     }
-    __syncthreads();  // V is free: this m's tables go there
     TabM *tm = reinterpret_cast<TabM *>(V);
     {
         double2 *v2 = reinterpret_cast<double2 *>(V) + threadIdx.x;  // (V holds kVFm >= 2 RT kSpecBlk doubles)
         v2[0] = rt0;
         v2[kSpecBlk] = rt1;
         if constexpr (RT > 2) v2[2 * kSpecBlk] = rt2;
+        double2 *s2 = reinterpret_cast<double2 *>(Sst) + threadIdx.x;
+        s2[0] = rs0;
+        s2[kSpecBlk] = rs1;
+        s2[2 * kSpecBlk] = rs2;
+        s2[3 * kSpecBlk] = rs3;
+        s2[4 * kSpecBlk] = rs4;
     }
-    __syncthreads();
+    __syncthreads();  // S, Sst, the tables complete
     const LTab tb{tm};
     stamp(dbg, sk, 2);
     // b) combine (k_dyn_combine) for coefficient (n, p) at level k: threads 0..511
