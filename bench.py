@@ -52,14 +52,18 @@ def parse():
     p.add_argument("--weights", choices=("f32", "f64"), default="f32")
     p.add_argument("--cpu-sample", type=int, default=96, help="regions in the CPU-baseline sample (0 = skip)")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--overlap", action="store_true",
-                   help="issue the reservoir half and SPEEDY's window on two streams (speedy_ml_amd/hybrid.py); "
-                        "measured no faster on MI355X: the readout's HBM stream raises the window's memory latency")
+    p.add_argument("--overlap", action=argparse.BooleanOptionalAction, default=True,
+                   help="issue the reservoir update + v_ml readout beside SPEEDY's window on two streams "
+                        "(speedy_ml_amd/hybrid.py; default, +2.7 %% at 1 GPU, profiles/r01o); --no-overlap: one "
+                        "stream, one-pass readout")
     p.add_argument("--train-regions", type=int, default=8,
                    help="regions in the supplementary W_out-training leg (0 = skip)")
     p.add_argument("--train-steps", type=int, default=4096, help="training time steps per region in that leg")
     p.add_argument("--reservoir-steps", type=int, default=50,
                    help="steps timed in the supplementary reservoir-only (configs[1]) leg (0 = skip)")
+    p.add_argument("--sim-ranks", type=int, default=1,
+                   help="diagnostic: run rank 0's share of an N-rank decomposition on this one GPU, the "
+                        "all-gather replaced by a local copy (other ranks' outvecs stale); never the headline")
     p.add_argument("--speedy-steps", type=int, default=48,
                    help="leapfrog steps timed in the supplementary SPEEDY-step leg (0 = skip)")
     return p.parse_args()
@@ -94,7 +98,8 @@ def main():
 
     nreg = args.regions
     mask = domain.load_sst_mask()
-    regions = domain.processor_decomposition(nreg, world, rank)
+    sim = args.sim_ranks if world == 1 and args.sim_ranks > 1 else 1
+    regions = domain.processor_decomposition(nreg, world * sim, rank)
 
     # ---- setup: synthetic weights with the trained structure, loaded per region
     t_setup = time.time()
@@ -112,6 +117,12 @@ def main():
         if i % 144 == 0:
             log(rank, f"loaded {i}/{len(regions)} regions ({time.time() - t_setup:.1f}s)")
     exchange = OutvecExchange(nreg, world, rank, device=dev)
+    if sim > 1:  # rank 0 of `sim` ranks: its outvecs into a global array, the others stale
+        glob_sim = torch.zeros((nreg, 136), dtype=torch.float64, device=dev)
+
+        def exchange(ov_local):
+            glob_sim[:len(regions)].copy_(ov_local)
+            return glob_sim
     g4h, g2h, prh = synthetic_grids(11)
     f4h, f2h, _ = synthetic_grids(12)
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
@@ -182,7 +193,10 @@ def main():
     pmc_path = os.path.join(REPO, "profiles", "readout_pmc.json")
     if os.path.exists(pmc_path) and world == 1 and nreg == 1152 and args.weights == "f32":
         try:
-            traffic = json.load(open(pmc_path)).get("hbm_bytes_per_launch")
+            pmc = json.load(open(pmc_path))
+            # the PMC pass must have profiled the same readout form as this run
+            if pmc.get("kernel", "").startswith("k_res_readout_ml" if args.overlap else "k_res_readout_full"):
+                traffic = pmc.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
 
@@ -234,7 +248,8 @@ def main():
                 "reservoir_nodes": "5760/6160/6048/5880 (NINT(6000/ninp)*ninp)",
                 "weights": f"{args.weights} storage ({'exact file precision' if args.weights == 'f32' else 'fp64'}), "
                            "fp64 arithmetic",
-                "parallelism": f"res_domain sharded over {world} GPU(s); SPEEDY window replicated per GPU",
+                "parallelism": f"res_domain sharded over {world} GPU(s); SPEEDY window replicated per GPU"
+                               + (f" [DIAGNOSTIC: rank 0 of {sim} simulated ranks, exchange local]" if sim > 1 else ""),
                 "speedy": "T30L8, 26 dyn_steps per window (nsteps 96/day, delt 900 s), physics on, "
                           "shortwave every 3rd step",
             },

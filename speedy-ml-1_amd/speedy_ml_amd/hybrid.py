@@ -22,11 +22,11 @@ The reservoir's update and ~98 % of its readout bytes run while SPEEDY
 integrates the previous step's window.  Results are identical to the one-stream
 schedule (`overlap=False`, which uses the one-pass readout with the same sums).
 
-Measured on MI355X (profiles/r01h_*): the overlap does not pay.  The readout
-streams ~3.8 GB from HBM at ~6 TB/s, and under that load each of SPEEDY's small
-latency-bound kernels waits far longer on memory (5 us kernels took 70 us), even
-with the window confined to its own CUs (hipExtStreamCreateWithCUMask).  The
-default is therefore the one-stream schedule.
+Measured on MI355X: with the window at 3 launches per step the overlap did not
+pay (profiles/r01h_*: under the readout's ~6 TB/s stream SPEEDY's small
+latency-bound kernels waited far longer on memory); with the window at 2 leaner
+launches per step it does: 496 vs 482 steps/s at 1 GPU and +0.6-1 % for the 2/4/8-
+rank shares (profiles/r01o).  bench.py uses it by default.
 """
 from __future__ import annotations
 
@@ -40,7 +40,7 @@ class HybridLoop:
     exchange: OutvecExchange, tisr: [nlocal, 16] standardized tisr inputs (device)
     or None (feedback tisr entries left as they are)."""
 
-    def __init__(self, res, dyn, exchange, device, tisr=None, overlap: bool = False, nleap: int = 24,
+    def __init__(self, res, dyn, exchange, device, tisr=None, overlap: bool = True, nleap: int = 24,
                  side_priority: int = -1):
         self.res, self.dyn, self.exchange, self.tisr = res, dyn, exchange, tisr
         self.overlap, self.nleap = overlap, nleap
