@@ -2,7 +2,7 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
-for n in ${SIMS:-8}; do for ov in "" "--overlap"; do
+for n in ${SIMS:-8}; do for ov in "--no-overlap" "--overlap"; do
 timeout -k 10 300 python -u bench.py --sim-ranks $n --no-cpu-baseline --train-regions 0 --speedy-steps 0 --reservoir-steps 20 $ov > gpurun_out/sim$n$ov.json 2> gpurun_out/sim$n$ov.err || { tail -5 gpurun_out/sim$n$ov.err; exit 1; }
 python3 -c "
 import json; d=json.loads(open('gpurun_out/sim$n$ov.json').read().strip().splitlines()[-1])

@@ -48,6 +48,7 @@ struct RegionDev {
     int a_w, w_w;  // ELL widths of A and W_in (0 = use the CSR copy)
     int pad_;
     int64_t a_rp, a_nz, w_rp, w_nz, wout, x, xaug, fb;
+    int64_t wlm;  // W_out(:, 1:ncs) transposed, [ncs][nout_pad], in the W_out pool after the row-major blocks
     int64_t a_ell, w_ell;  // offsets into the ELL pools (row-major [n][slots])
 };
 
@@ -60,6 +61,8 @@ struct sml_reservoirs {
     std::vector<unsigned char> sst, loaded;
     std::vector<RegionGeom> geom;
     std::vector<RegionDev> rd;
+    int64_t tot_wlm = 0;  // elements of the transposed local-model blocks (pool d_wlm)
+    void *d_wlm = nullptr;
     int64_t tot_a_rp = 0, tot_a_nz = 0, tot_w_rp = 0, tot_w_nz = 0, tot_wout = 0, tot_x = 0, tot_xaug = 0,
             tot_fb = 0;
     std::vector<int64_t> w_nz_cap;  // reserved W_in nnz per region (n, grows on reload)
@@ -245,10 +248,12 @@ struct Vec4<double> {
 // The product W_out [local_model; x~] is split at column ncs as the reference's
 // outvec_component_contribs does (v_p + v_ml, mod_reservoir.f90:1456-1459):
 //   kReadML:     part = v_ml = W_out(:, ncs+1:) x~     (needs only this step's feedback)
-//   kReadFinish: v = v_p + part, v_p = W_out(:, 1:ncs) local_model, unstandardize
+//   kReadFinish: v = v_p + part, unstandardize (k_res_finish: one thread per output)
 //   kReadFull:   v = v_p + v_ml in one pass (sml_res_step)
-// Every mode forms v_ml and v_p with the same per-lane partial sums and the same
-// butterfly, so the split step and the one-pass step agree bit for bit; the split
+// v_ml is the wave's per-lane partial sums + butterfly over W_out's rows; v_p is a
+// per-output sum over the ncs columns in order from the transposed block
+// W_out(:, 1:ncs) = [ncs][nout_pad] (coalesced across outputs), the same code in
+// both modes, so the split step and the one-pass step agree bit for bit; the split
 // lets the ML part -- ~98 % of the bytes -- run before SPEEDY's local_model exists.
 enum ReadMode { kReadML = 0, kReadFinish = 1, kReadFull = 2 };
 
@@ -292,8 +297,29 @@ __device__ __attribute__((always_inline)) inline Rows rows_dot(const WT *W, int 
     return out;
 }
 
+// v_p = W_out(o, 1:ncs) local_model over the columns in order, from the transposed
+// block wl = [ncs][nout_pad] (a wave's lanes read neighbouring outputs of a column)
+template <typename WT>
+__device__ inline double vp_sum(const WT *__restrict__ wl, int nout_pad, const double *__restrict__ lm, int ncs,
+                                int o) {
+    double s = 0.0;
+#pragma unroll 4
+    for (int j = 0; j < ncs; ++j) s = fma((double)wl[(size_t)j * nout_pad + o], lm[j], s);
+    return s;
+}
+
+// unstandardize_state_vec_res: x*std + mean (two roundings) where the output has a slot
+__device__ inline double unstd(double v, const double *ms, int l) {
+    if (l >= 0) {
+        const double t = v * ms[kMeanStd + l];
+        v = t + ms[l];
+    }
+    return v;
+}
+
 template <typename WT, int kMode>
 __global__ __launch_bounds__(256) void k_res_readout(const RegionDev *__restrict__ R, const WT *__restrict__ wout,
+                                                     const WT *__restrict__ wlm,
                                                      const double *__restrict__ xaug,
                                                      const double *__restrict__ local_model,
                                                      const double *__restrict__ meanstd,
@@ -308,8 +334,8 @@ __global__ __launch_bounds__(256) void k_res_readout(const RegionDev *__restrict
     const RegionDev rg = R[r];
     const int ld = rg.ld;
     const WT *W = wout + rg.wout + (size_t)(g * kRows) * ld;
-    Rows ml{}, lmv{};
-    if (kMode != kReadFinish) {  // v_ml: x~ from x_aug, columns ncs .. ld
+    Rows ml{};
+    {   // v_ml: x~ from x_aug, columns ncs .. ld
         const double *xa = xaug + rg.xaug;
         ml = rows_dot<WT>(W, ld, lane, ncs & ~3, ld, [=](int j) {
             double4 xv = *reinterpret_cast<const double4 *>(xa + j);
@@ -322,41 +348,41 @@ __global__ __launch_bounds__(256) void k_res_readout(const RegionDev *__restrict
             return xv;
         });
     }
-    if (kMode != kReadML) {  // v_p: x_augment(1:chunk_size_speedy) = local_model (:1451), read in place
-        const double *lm = local_model + (size_t)r * ncs;
-        lmv = rows_dot<WT>(W, ld, lane, 0, (ncs + 3) & ~3, [=](int j) {
-            double4 xv;
-            xv.x = j + 0 < ncs ? lm[j + 0] : 0.0;
-            xv.y = j + 1 < ncs ? lm[j + 1] : 0.0;
-            xv.z = j + 2 < ncs ? lm[j + 2] : 0.0;
-            xv.w = j + 3 < ncs ? lm[j + 3] : 0.0;
-            return xv;
-        });
-    }
-    // every lane holds all 8 sums after the butterfly; lane 0 writes the group's rows
-    // (static indices only: a lane-indexed pick would put the sums in scratch)
-    if (lane == 0) {
-        const int o0 = g * kRows;
-        if (kMode == kReadML) {
+    const int o0 = g * kRows;
+    if (kMode == kReadML) {  // every lane holds all 8 sums after the butterfly; lane 0 writes them
+        if (lane == 0) {
 #pragma unroll
             for (int q = 0; q < kRows; ++q) part[(size_t)r * nout_pad + o0 + q] = ml.v[q];
-        } else {
-            const double *ms = meanstd + (size_t)r * 2 * kMeanStd;
+        }
+    } else {  // kReadFull: lane q finishes row o0 + q with v_p (k_res_finish's sum) + v_ml
+        const int o = o0 + lane;
+        if (lane < kRows && o < nout) {
+            double vml = ml.v[0];  // static indices only: a lane-indexed pick would put the sums in scratch
 #pragma unroll
-            for (int q = 0; q < kRows; ++q) {
-                const int o = o0 + q;
-                if (o >= nout) break;
-                const double vml = kMode == kReadFull ? ml.v[q] : part[(size_t)r * nout_pad + o];
-                double v = lmv.v[q] + vml;
-                const int l = outl[o];
-                if (l >= 0) {  // unstandardize_state_vec_res: x*std + mean (two roundings)
-                    const double t = v * ms[kMeanStd + l];
-                    v = t + ms[l];
-                }
-                outvec[(size_t)r * nout + o] = v;
-            }
+            for (int q = 1; q < kRows; ++q)
+                if (lane == q) vml = ml.v[q];
+            const double vp = vp_sum(wlm + rg.wlm, nout_pad, local_model + (size_t)r * ncs, ncs, o);
+            outvec[(size_t)r * nout + o] = unstd(vp + vml, meanstd + (size_t)r * 2 * kMeanStd, outl[o]);
         }
     }
+}
+
+// second half of the split readout (sml_res_step_finish): one thread per (region,
+// output): v = v_p + v_ml (v_ml from k_res_readout<kReadML>), unstandardized --
+// the same sums, in the same order, as k_res_readout<kReadFull>
+template <typename WT>
+__global__ __launch_bounds__(256) void k_res_finish(const RegionDev *__restrict__ R, const WT *__restrict__ wlm,
+                                                    const double *__restrict__ local_model,
+                                                    const double *__restrict__ meanstd,
+                                                    const int8_t *__restrict__ outl, const double *__restrict__ part,
+                                                    double *__restrict__ outvec, int nout, int nout_pad, int ncs,
+                                                    int nlocal) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    const int r = t / nout_pad, o = t % nout_pad;
+    if (r >= nlocal || o >= nout) return;
+    const double vp = vp_sum(wlm + R[r].wlm, nout_pad, local_model + (size_t)r * ncs, ncs, o);
+    outvec[(size_t)r * nout + o] =
+        unstd(vp + part[(size_t)r * nout_pad + o], meanstd + (size_t)r * 2 * kMeanStd, outl[o]);
 }
 
 // assemble: all regions' outvecs -> global grids, with the root's clips
@@ -625,6 +651,12 @@ int load_region_impl(sml_reservoirs *c, int i, const int *rows, const int *cols,
         SML_HIP(hipMemcpy((char *)c->d_w_val + rg.w_nz * wb, wval.data(), wval.size() * wb, hipMemcpyHostToDevice));
     }
     SML_HIP(hipMemcpy((char *)c->d_wout + rg.wout * wb, wt.data(), wt.size() * wb, hipMemcpyHostToDevice));
+    if (ncs > 0) {  // W_out(:, 1:ncs) as [ncs][nout_pad]: the file's own order (outputs fastest), padded
+        std::vector<StoT> wl((size_t)ncs * c->nout_pad, (StoT)0);
+        for (int j = 0; j < ncs; ++j)
+            for (int o = 0; o < nout; ++o) wl[(size_t)j * c->nout_pad + o] = (StoT)wout[(size_t)j * nout + o];
+        SML_HIP(hipMemcpy((char *)c->d_wlm + rg.wlm * wb, wl.data(), wl.size() * wb, hipMemcpyHostToDevice));
+    }
     // --- ELL copies when every row fits the reserved slots (row-major [n][cap], file
     // order within a row, zero-padded after the row's entries)
     auto ell = [&](const std::vector<int32_t> &p, const std::vector<uint16_t> &col, const std::vector<StoT> &val,
@@ -675,7 +707,8 @@ extern "C" int sml_res_destroy(sml_reservoirs *c) {
         if (p) (void)hipFree(p);
     void *ptrs[] = {c->d_rd,    c->d_a_rp,    c->d_w_rp,   c->d_a_col,  c->d_w_col,  c->d_a_val,  c->d_w_val,
                     c->d_wout,  c->d_x[0],    c->d_x[1],   c->d_xaug,   c->d_meanstd, c->d_outl,  c->d_asm_dst,
-                    c->d_fb_src, c->d_fb_l,   c->d_fb_reg, c->d_lm_src, c->d_lm_l,   c->d_io,     c->d_part};
+                    c->d_fb_src, c->d_fb_l,   c->d_fb_reg, c->d_lm_src, c->d_lm_l,   c->d_io,     c->d_part,
+                    c->d_wlm};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     for (hipEvent_t e : c->ev)
@@ -750,6 +783,8 @@ extern "C" int sml_res_create(int numregions, int nlocal, const int *region_ids,
         c->tot_w_nz += n[i];
         r.wout = c->tot_wout;
         c->tot_wout += (int64_t)c->nout_pad * c->ld[i];
+        r.wlm = c->tot_wlm;
+        c->tot_wlm += (int64_t)c->ncs * c->nout_pad;
         r.x = c->tot_x;
         c->tot_x += n[i];
         r.xaug = c->tot_xaug;
@@ -778,6 +813,7 @@ extern "C" int sml_res_create(int numregions, int nlocal, const int *region_ids,
         (rc = dalloc(&c->d_a_col, c->tot_a_nz)) || (rc = dalloc_bytes(&c->d_a_val, c->tot_a_nz * wb)) ||
         (rc = dalloc(&c->d_w_rp, c->tot_w_rp)) || (rc = dalloc(&c->d_w_col, c->tot_w_nz)) ||
         (rc = dalloc_bytes(&c->d_w_val, c->tot_w_nz * wb)) || (rc = dalloc_bytes(&c->d_wout, c->tot_wout * wb)) ||
+        (rc = dalloc_bytes(&c->d_wlm, std::max<int64_t>(c->tot_wlm, 1) * wb)) ||
         (rc = dalloc(&c->d_x[0], c->tot_x)) || (rc = dalloc(&c->d_x[1], c->tot_x)) ||
         (rc = dalloc(&c->d_xaug, c->tot_xaug)) || (rc = dalloc(&c->d_meanstd, (size_t)nlocal * 2 * kMeanStd)) ||
         (rc = dalloc(&c->d_part, (size_t)std::max(nlocal, 1) * c->nout_pad))) {
@@ -788,6 +824,7 @@ extern "C" int sml_res_create(int numregions, int nlocal, const int *region_ids,
     if (e == hipSuccess) e = hipMemset(c->d_a_rp, 0, std::max<int64_t>(c->tot_a_rp, 1) * 4);
     if (e == hipSuccess) e = hipMemset(c->d_w_rp, 0, std::max<int64_t>(c->tot_w_rp, 1) * 4);
     if (e == hipSuccess) e = hipMemset(c->d_wout, 0, std::max<int64_t>(c->tot_wout * wb, 16));
+    if (e == hipSuccess) e = hipMemset(c->d_wlm, 0, std::max<int64_t>(c->tot_wlm, 1) * wb);
     if (e == hipSuccess) e = hipMemset(c->d_x[0], 0, std::max<int64_t>(c->tot_x, 1) * 8);
     if (e == hipSuccess) e = hipMemset(c->d_x[1], 0, std::max<int64_t>(c->tot_x, 1) * 8);
     if (e == hipSuccess) e = hipMemset(c->d_xaug, 0, std::max<int64_t>(c->tot_xaug, 1) * 8);
@@ -938,17 +975,30 @@ int check_loaded(const sml_reservoirs *c) {
 
 template <int kMode>
 void launch_readout(sml_reservoirs *c, const double *d_local_model, double *d_outvec, hipStream_t st) {
-    const int groups = c->nout_pad / kRows;
-    const int nitems = c->nlocal * groups;
-    const int nblocks = (nitems + 3) / 4;
-    if (c->wdtype == SML_F32)
-        hipLaunchKernelGGL((k_res_readout<float, kMode>), dim3(nblocks), dim3(256), 0, st, c->d_rd,
-                           (const float *)c->d_wout, c->d_xaug, d_local_model, c->d_meanstd, c->d_outl, c->d_part, d_outvec, c->nout,
-                           c->nout_pad, c->ncs, groups, nitems);
-    else
-        hipLaunchKernelGGL((k_res_readout<double, kMode>), dim3(nblocks), dim3(256), 0, st, c->d_rd,
-                           (const double *)c->d_wout, c->d_xaug, d_local_model, c->d_meanstd, c->d_outl, c->d_part, d_outvec, c->nout,
-                           c->nout_pad, c->ncs, groups, nitems);
+    if constexpr (kMode == kReadFinish) {
+        const int total = c->nlocal * c->nout_pad;
+        if (c->wdtype == SML_F32)
+            hipLaunchKernelGGL(k_res_finish<float>, dim3((total + 255) / 256), dim3(256), 0, st, c->d_rd,
+                               (const float *)c->d_wlm, d_local_model, c->d_meanstd, c->d_outl, c->d_part, d_outvec,
+                               c->nout, c->nout_pad, c->ncs, c->nlocal);
+        else
+            hipLaunchKernelGGL(k_res_finish<double>, dim3((total + 255) / 256), dim3(256), 0, st, c->d_rd,
+                               (const double *)c->d_wlm, d_local_model, c->d_meanstd, c->d_outl, c->d_part,
+                               d_outvec, c->nout, c->nout_pad, c->ncs, c->nlocal);
+    } else {
+        const int groups = c->nout_pad / kRows;
+        const int nitems = c->nlocal * groups;
+        const int nblocks = (nitems + 3) / 4;
+        if (c->wdtype == SML_F32)
+            hipLaunchKernelGGL((k_res_readout<float, kMode>), dim3(nblocks), dim3(256), 0, st, c->d_rd,
+                               (const float *)c->d_wout, (const float *)c->d_wlm, c->d_xaug, d_local_model, c->d_meanstd,
+                               c->d_outl, c->d_part, d_outvec, c->nout, c->nout_pad, c->ncs, groups, nitems);
+        else
+            hipLaunchKernelGGL((k_res_readout<double, kMode>), dim3(nblocks), dim3(256), 0, st, c->d_rd,
+                               (const double *)c->d_wout, (const double *)c->d_wlm, c->d_xaug, d_local_model,
+                               c->d_meanstd, c->d_outl, c->d_part, d_outvec, c->nout, c->nout_pad, c->ncs, groups,
+                               nitems);
+    }
 }
 }  // namespace
 
