@@ -237,10 +237,12 @@ struct Vec4;
 template <>
 struct Vec4<float> {
     typedef float4 T;
+    typedef float N __attribute__((ext_vector_type(4)));  // native vector (non-temporal loads)
 };
 template <>
 struct Vec4<double> {
     typedef double4 T;
+    typedef double N __attribute__((ext_vector_type(4)));
 };
 
 // readout: one wave per (region, 8-row group) item, 4 waves per block; blocks are
@@ -267,7 +269,7 @@ struct Rows {
 template <typename WT, typename XF>
 __device__ __attribute__((always_inline)) inline Rows rows_dot(const WT *W, int ld, int lane, int c0, int c1,
                                                                XF xload) {
-    typedef typename Vec4<WT>::T V;
+    typedef typename Vec4<WT>::N V;
     double acc[kRows];
 #pragma unroll
     for (int q = 0; q < kRows; ++q) acc[q] = 0.0;
@@ -276,7 +278,8 @@ __device__ __attribute__((always_inline)) inline Rows rows_dot(const WT *W, int 
         const double4 xv = xload(j);
         V w[kRows];
 #pragma unroll
-        for (int q = 0; q < kRows; ++q) w[q] = *reinterpret_cast<const V *>(W + (size_t)q * ld + j);
+        for (int q = 0; q < kRows; ++q)  // streamed once per step: non-temporal, so W_out does not evict the
+            w[q] = __builtin_nontemporal_load(reinterpret_cast<const V *>(W + (size_t)q * ld + j));  // window's data
 #pragma unroll
         for (int q = 0; q < kRows; ++q) {
             double s = acc[q];
