@@ -82,6 +82,11 @@ struct sml_reservoirs {
     int cur = 0;
     double *d_xaug = nullptr, *d_meanstd = nullptr;
     double *d_part = nullptr;       // [nlocal][nout_pad] W_out(:, ncs+1:) x~ of the step in flight
+    // cap on the waves of the v_ml readout (the half that runs beside SPEEDY's window;
+    // 0: one wave per item).  Uncapped it takes ~6 TB/s and SPEEDY's latency-bound
+    // kernels stall behind it; paced at 2048 waves (~4.7 TB/s) the overlapped step
+    // is 1.75 ms instead of 1.98 (profiles/r01p).  SML_READ_WAVES overrides.
+    int read_waves = 2048;
     bool begun = false;             // sml_res_step_begin issued, finish pending
     int8_t *d_outl = nullptr;
     int32_t *d_asm_dst = nullptr;   // [numregions*nout] -> concatenated grid index
@@ -328,44 +333,48 @@ __global__ __launch_bounds__(256) void k_res_readout(const RegionDev *__restrict
                                                      const double *__restrict__ meanstd,
                                                      const int8_t *__restrict__ outl, double *__restrict__ part,
                                                      double *__restrict__ outvec, int nout, int nout_pad, int ncs,
-                                                     int groups, int nitems) {
+                                                     int groups, int nitems, int ipw) {
+    // wave gw takes the items [gw ipw, (gw + 1) ipw): ipw = 1 normally; more when the
+    // launch is throttled (fewer waves, each a run of one region's row groups)
     const int bs = xcd_remap(blockIdx.x, gridDim.x);
     const int lane = threadIdx.x & 63;
-    const int item = bs * 4 + (threadIdx.x >> 6);
-    if (item >= nitems) return;
-    const int r = item / groups, g = item % groups;
-    const RegionDev rg = R[r];
-    const int ld = rg.ld;
-    const WT *W = wout + rg.wout + (size_t)(g * kRows) * ld;
-    Rows ml{};
-    {   // v_ml: x~ from x_aug, columns ncs .. ld
-        const double *xa = xaug + rg.xaug;
-        ml = rows_dot<WT>(W, ld, lane, ncs & ~3, ld, [=](int j) {
-            double4 xv = *reinterpret_cast<const double4 *>(xa + j);
-            if (j < ncs) {  // the group that straddles column ncs
-                if (j + 0 < ncs) xv.x = 0.0;
-                if (j + 1 < ncs) xv.y = 0.0;
-                if (j + 2 < ncs) xv.z = 0.0;
-                if (j + 3 < ncs) xv.w = 0.0;
-            }
-            return xv;
-        });
-    }
-    const int o0 = g * kRows;
-    if (kMode == kReadML) {  // every lane holds all 8 sums after the butterfly; lane 0 writes them
-        if (lane == 0) {
-#pragma unroll
-            for (int q = 0; q < kRows; ++q) part[(size_t)r * nout_pad + o0 + q] = ml.v[q];
+    const int gw = bs * 4 + (threadIdx.x >> 6);
+    const int it0 = gw * ipw, it1 = min(nitems, it0 + ipw);
+    for (int item = it0; item < it1; ++item) {
+        const int r = item / groups, g = item % groups;
+        const RegionDev rg = R[r];
+        const int ld = rg.ld;
+        const WT *W = wout + rg.wout + (size_t)(g * kRows) * ld;
+        Rows ml{};
+        {   // v_ml: x~ from x_aug, columns ncs .. ld
+            const double *xa = xaug + rg.xaug;
+            ml = rows_dot<WT>(W, ld, lane, ncs & ~3, ld, [=](int j) {
+                double4 xv = *reinterpret_cast<const double4 *>(xa + j);
+                if (j < ncs) {  // the group that straddles column ncs
+                    if (j + 0 < ncs) xv.x = 0.0;
+                    if (j + 1 < ncs) xv.y = 0.0;
+                    if (j + 2 < ncs) xv.z = 0.0;
+                    if (j + 3 < ncs) xv.w = 0.0;
+                }
+                return xv;
+            });
         }
-    } else {  // kReadFull: lane q finishes row o0 + q with v_p (k_res_finish's sum) + v_ml
-        const int o = o0 + lane;
-        if (lane < kRows && o < nout) {
-            double vml = ml.v[0];  // static indices only: a lane-indexed pick would put the sums in scratch
-#pragma unroll
-            for (int q = 1; q < kRows; ++q)
-                if (lane == q) vml = ml.v[q];
-            const double vp = vp_sum(wlm + rg.wlm, nout_pad, local_model + (size_t)r * ncs, ncs, o);
-            outvec[(size_t)r * nout + o] = unstd(vp + vml, meanstd + (size_t)r * 2 * kMeanStd, outl[o]);
+        const int o0 = g * kRows;
+        if (kMode == kReadML) {  // every lane holds all 8 sums after the butterfly; lane 0 writes them
+            if (lane == 0) {
+    #pragma unroll
+                for (int q = 0; q < kRows; ++q) part[(size_t)r * nout_pad + o0 + q] = ml.v[q];
+            }
+        } else {  // kReadFull: lane q finishes row o0 + q with v_p (k_res_finish's sum) + v_ml
+            const int o = o0 + lane;
+            if (lane < kRows && o < nout) {
+                double vml = ml.v[0];  // static indices only: a lane-indexed pick would put the sums in scratch
+    #pragma unroll
+                for (int q = 1; q < kRows; ++q)
+                    if (lane == q) vml = ml.v[q];
+                const double vp = vp_sum(wlm + rg.wlm, nout_pad, local_model + (size_t)r * ncs, ncs, o);
+                outvec[(size_t)r * nout + o] = unstd(vp + vml, meanstd + (size_t)r * 2 * kMeanStd, outl[o]);
+            }
         }
     }
 }
@@ -740,6 +749,8 @@ extern "C" int sml_res_create(int numregions, int nlocal, const int *region_ids,
     c->nout_pad = (nout + kRows - 1) / kRows * kRows;
     c->wdtype = weight_dtype;
     c->leakage = leakage;
+    if (const char *e = std::getenv("SML_READ_WAVES")) c->read_waves = std::max(0, std::atoi(e));
+    SML_REQUIRE(c->read_waves >= 0, "bad read_waves");
     (void)hipGetDevice(&c->device);
     c->region_ids.assign(region_ids, region_ids + nlocal);
     c->sst.assign(sst_flags, sst_flags + nlocal);
@@ -991,16 +1002,22 @@ void launch_readout(sml_reservoirs *c, const double *d_local_model, double *d_ou
     } else {
         const int groups = c->nout_pad / kRows;
         const int nitems = c->nlocal * groups;
-        const int nblocks = (nitems + 3) / 4;
+        // the v_ml half runs beside SPEEDY's window: c->read_waves > 0 caps its waves
+        // (each takes a run of items) so it leaves HBM headroom for the window
+        int ipw = 1;
+        if (kMode == kReadML && c->read_waves > 0 && c->read_waves < nitems)
+            ipw = (nitems + c->read_waves - 1) / c->read_waves;
+        const int nwaves = (nitems + ipw - 1) / ipw;
+        const int nblocks = (nwaves + 3) / 4;
         if (c->wdtype == SML_F32)
             hipLaunchKernelGGL((k_res_readout<float, kMode>), dim3(nblocks), dim3(256), 0, st, c->d_rd,
                                (const float *)c->d_wout, (const float *)c->d_wlm, c->d_xaug, d_local_model, c->d_meanstd,
-                               c->d_outl, c->d_part, d_outvec, c->nout, c->nout_pad, c->ncs, groups, nitems);
+                               c->d_outl, c->d_part, d_outvec, c->nout, c->nout_pad, c->ncs, groups, nitems, ipw);
         else
             hipLaunchKernelGGL((k_res_readout<double, kMode>), dim3(nblocks), dim3(256), 0, st, c->d_rd,
                                (const double *)c->d_wout, (const double *)c->d_wlm, c->d_xaug, d_local_model,
                                c->d_meanstd, c->d_outl, c->d_part, d_outvec, c->nout, c->nout_pad, c->ncs, groups,
-                               nitems);
+                               nitems, ipw);
     }
 }
 }  // namespace
