@@ -87,6 +87,7 @@ struct sml_reservoirs {
     // kernels stall behind it; paced at 2048 waves (~4.7 TB/s) the overlapped step
     // is 1.75 ms instead of 1.98 (profiles/r01p).  SML_READ_WAVES overrides.
     int read_waves = 2048;
+    int upd_blocks = 0;  // cap on the update's grid in sml_res_step_begin (0: none; SML_UPD_BLOCKS)
     bool begun = false;             // sml_res_step_begin issued, finish pending
     int8_t *d_outl = nullptr;
     int32_t *d_asm_dst = nullptr;   // [numregions*nout] -> concatenated grid index
@@ -173,14 +174,12 @@ __device__ inline int ell_col(const uint4 &c, int s) {
 // is unchanged), otherwise from the CSR copy.  The next pass's ELL loads are issued
 // before the current pass computes.
 template <typename WT, bool kLds>
-__global__ __launch_bounds__(kUpdThreads) void k_res_update(
-    const RegionDev *__restrict__ R, const int32_t *__restrict__ a_rp, const uint16_t *__restrict__ a_col,
-    const WT *__restrict__ a_val, const int32_t *__restrict__ w_rp, const uint16_t *__restrict__ w_col,
-    const WT *__restrict__ w_val, Ell ell, const double *__restrict__ x_old, double *__restrict__ x_new,
-    double *__restrict__ xaug, const double *__restrict__ feedback, int ncs,
-    double leak, int parts, int lds_x) {
-    extern __shared__ __attribute__((aligned(16))) double smem[];
-    const int lb = xcd_remap(blockIdx.x, gridDim.x);
+__device__ __attribute__((always_inline)) inline void update_block(
+    int lb, double *smem, const RegionDev *__restrict__ R, const int32_t *__restrict__ a_rp,
+    const uint16_t *__restrict__ a_col, const WT *__restrict__ a_val, const int32_t *__restrict__ w_rp,
+    const uint16_t *__restrict__ w_col, const WT *__restrict__ w_val, const Ell &ell,
+    const double *__restrict__ x_old, double *__restrict__ x_new, double *__restrict__ xaug,
+    const double *__restrict__ feedback, int ncs, double leak, int parts, int lds_x) {
     const int r = lb / parts, part = lb % parts;
     const RegionDev rg = R[r];
     const int n = rg.n, tid = threadIdx.x;
@@ -234,6 +233,26 @@ __global__ __launch_bounds__(kUpdThreads) void k_res_update(
             xaug[rg.xaug + ncs + i] = (i & 1) ? xv * xv : xv;  // x_temp(2:n:2)**2 (1-based even)
         }
         cur = nxt;
+    }
+}
+
+// logical blocks (region, part) = nlog; with a grid smaller than nlog (the paced
+// update that runs beside SPEEDY's window) each block takes logical blocks in rounds
+template <typename WT, bool kLds>
+__global__ __launch_bounds__(kUpdThreads) void k_res_update(
+    const RegionDev *__restrict__ R, const int32_t *__restrict__ a_rp, const uint16_t *__restrict__ a_col,
+    const WT *__restrict__ a_val, const int32_t *__restrict__ w_rp, const uint16_t *__restrict__ w_col,
+    const WT *__restrict__ w_val, Ell ell, const double *__restrict__ x_old, double *__restrict__ x_new,
+    double *__restrict__ xaug, const double *__restrict__ feedback, int ncs,
+    double leak, int parts, int lds_x, int nlog) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    const int off = xcd_remap(blockIdx.x, gridDim.x);
+    for (int base = 0; base < nlog; base += gridDim.x) {
+        const int lb = base + off;
+        if (lb < nlog)  // block-uniform
+            update_block<WT, kLds>(lb, smem, R, a_rp, a_col, a_val, w_rp, w_col, w_val, ell, x_old, x_new, xaug,
+                                   feedback, ncs, leak, parts, lds_x);
+        if (base + (int)gridDim.x < nlog) __syncthreads();  // the block's LDS, reused next round
     }
 }
 
@@ -750,6 +769,7 @@ extern "C" int sml_res_create(int numregions, int nlocal, const int *region_ids,
     c->wdtype = weight_dtype;
     c->leakage = leakage;
     if (const char *e = std::getenv("SML_READ_WAVES")) c->read_waves = std::max(0, std::atoi(e));
+    if (const char *e = std::getenv("SML_UPD_BLOCKS")) c->upd_blocks = std::max(0, std::atoi(e));
     SML_REQUIRE(c->read_waves >= 0, "bad read_waves");
     (void)hipGetDevice(&c->device);
     c->region_ids.assign(region_ids, region_ids + nlocal);
@@ -947,7 +967,8 @@ extern "C" int sml_res_kernel_times(sml_reservoirs *c, float *update_ms, float *
 
 namespace {
 // x_new = (1 - leak) x + leak tanh(A x + W_in u) for every local region (+ x~, x_aug)
-int launch_update(sml_reservoirs *c, const double *xo, double *xn, const double *d_feedback, hipStream_t st) {
+int launch_update(sml_reservoirs *c, const double *xo, double *xn, const double *d_feedback, hipStream_t st,
+                  bool paced = false) {
     // parts per region: enough blocks to fill the 512 resident 1024-thread block slots
     // (2 per CU with ~54 KB LDS each) once, each part at least one 1024-row pass.  Every
     // part stages the region's whole x, so more parts cost HBM traffic: measured on
@@ -959,11 +980,14 @@ int launch_update(sml_reservoirs *c, const double *xo, double *xn, const double 
     const size_t lds = (size_t)(lds_x + c->maxninp) * sizeof(double);
     const bool use_lds = lds <= 64 * 1024;
     const int bpr = parts;
-    dim3 ug(bpr * c->nlocal);
+    const int nlog = bpr * c->nlocal;
+    // beside SPEEDY's window (sml_res_step_begin) the grid may be capped (upd_blocks):
+    // fewer blocks in flight, each taking logical blocks in rounds
+    dim3 ug(paced && c->upd_blocks > 0 ? std::min(nlog, c->upd_blocks) : nlog);
 #define SML_UPD(WT, L)                                                                                            \
     hipLaunchKernelGGL((k_res_update<WT, L>), ug, dim3(kUpdThreads), L ? lds : 0, st, c->d_rd, c->d_a_rp,          \
                        c->d_a_col, (const WT *)c->d_a_val, c->d_w_rp, c->d_w_col, (const WT *)c->d_w_val, ell,    \
-                       xo, xn, c->d_xaug, d_feedback, c->ncs, c->leakage, bpr, lds_x)
+                       xo, xn, c->d_xaug, d_feedback, c->ncs, c->leakage, bpr, lds_x, nlog)
     Ell ell{c->d_a_ell_col, c->d_a_ell_val, c->d_w_ell_col, c->d_w_ell_val};
     if (c->wdtype == SML_F32) {
         if (use_lds)
@@ -1034,7 +1058,7 @@ extern "C" int sml_res_step_begin(sml_reservoirs *c, const double *d_feedback, v
     const bool rec = c->timing && c->ev_used < c->ev_cap;
     hipEvent_t *ev = rec ? &c->ev[3 * c->ev_used] : nullptr;
     if (rec) SML_HIP(hipEventRecord(ev[0], st));
-    if (int rc = launch_update(c, xo, xn, d_feedback, st)) return rc;
+    if (int rc = launch_update(c, xo, xn, d_feedback, st, true)) return rc;  // beside SPEEDY's window
     if (rec) SML_HIP(hipEventRecord(ev[1], st));
     launch_readout<kReadML>(c, nullptr, nullptr, st);
     SML_HIP(hipGetLastError());
