@@ -353,13 +353,14 @@ __global__ __launch_bounds__(256) void k_res_readout(const RegionDev *__restrict
                                                      const int8_t *__restrict__ outl, double *__restrict__ part,
                                                      double *__restrict__ outvec, int nout, int nout_pad, int ncs,
                                                      int groups, int nitems, int ipw) {
-    // wave gw takes the items [gw ipw, (gw + 1) ipw): ipw = 1 normally; more when the
-    // launch is throttled (fewer waves, each a run of one region's row groups)
+    // wave gw takes the items gw, gw + W, gw + 2W, .. (W waves; one item each unless
+    // the launch is paced): the waves in flight together work on consecutive items,
+    // so a region's row groups still share its x_aug in one XCD's L2
     const int bs = xcd_remap(blockIdx.x, gridDim.x);
     const int lane = threadIdx.x & 63;
-    const int gw = bs * 4 + (threadIdx.x >> 6);
-    const int it0 = gw * ipw, it1 = min(nitems, it0 + ipw);
-    for (int item = it0; item < it1; ++item) {
+    const int gw = bs * 4 + (threadIdx.x >> 6), nw = gridDim.x * 4;
+    (void)ipw;
+    for (int item = gw; item < nitems; item += nw) {
         const int r = item / groups, g = item % groups;
         const RegionDev rg = R[r];
         const int ld = rg.ld;
