@@ -56,6 +56,9 @@ def parse():
                    help="issue the reservoir update + v_ml readout beside SPEEDY's window on two streams "
                         "(speedy_ml_amd/hybrid.py; default, +2.7 %% at 1 GPU, profiles/r01o); --no-overlap: one "
                         "stream, one-pass readout")
+    p.add_argument("--speedy-cus", type=int, default=64,
+                   help="with --overlap: CUs [0, N) for SPEEDY's stream, the rest for the reservoir's "
+                        "(speedy_ml_amd/hybrid.py; 0 = no split)")
     p.add_argument("--train-regions", type=int, default=8,
                    help="regions in the supplementary W_out-training leg (0 = skip)")
     p.add_argument("--train-steps", type=int, default=4096, help="training time steps per region in that leg")
@@ -136,7 +139,7 @@ def main():
     dyn.set_physics(phys_bc)
     # the hybrid loop (speedy_ml_amd/hybrid.py); --overlap puts SPEEDY's window on a
     # second stream beside the reservoir update + v_ml readout
-    loop = HybridLoop(res, dyn, exchange, dev, tisr=tisr, overlap=args.overlap)
+    loop = HybridLoop(res, dyn, exchange, dev, tisr=tisr, overlap=args.overlap, speedy_cus=args.speedy_cus)
     # initial inputs from the synthetic analysis state (start_prediction analogue)
     loop.start(t(g4h), t(g2h), t(prh), t(f4h), t(f2h))
     fb, lm, ov, g4, g2, pr, f4, f2 = loop.fb, loop.lm, loop.ov, loop.g4, loop.g2, loop.pr, loop.f4, loop.f2
@@ -262,6 +265,9 @@ def main():
                                + (f" [DIAGNOSTIC: rank 0 of {sim} simulated ranks, exchange local]" if sim > 1 else ""),
                 "speedy": "T30L8, 26 dyn_steps per window (nsteps 96/day, delt 900 s), physics on, "
                           "shortwave every 3rd step",
+                "streams": (f"overlapped: SPEEDY on CUs [0, {args.speedy_cus}), reservoir on the rest"
+                            if args.overlap and args.speedy_cus > 0 else
+                            "overlapped, no CU split" if args.overlap else "one stream"),
             },
             "last_window_safe": bool(safe),
             "finite": finite,

@@ -353,6 +353,16 @@ int sml_train_get_gram(sml_train *t, int i, double *G, double *B);
  * back-to-back v_mfma_f64_16x16x4_f64 chains on every SIMD */
 int sml_probe_mfma_f64(int iters, double *tflops);
 
+/* ------------------------------------------------------------------ streams */
+/* A HIP stream whose kernels run only on the logical CUs [first_cu, first_cu +
+ * num_cus) of the current device (hipExtStreamCreateWithCUMask).  The hybrid loop
+ * (no reference counterpart: the reference runs SPEEDY after every predict, serially,
+ * parallelmain.f90:225-260) gives SPEEDY's latency-bound window its own CUs beside
+ * the reservoir's HBM-bound update/readout, so the window's blocks neither wait for
+ * LDS behind update blocks nor share a CU's memory pipeline with readout waves. */
+int sml_stream_create_cu_range(int first_cu, int num_cus, void **stream);
+int sml_stream_destroy(void *stream);
+
 #ifdef __cplusplus
 }
 #endif

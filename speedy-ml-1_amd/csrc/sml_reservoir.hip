@@ -20,6 +20,7 @@
 //     the readout streams it from HBM once per step with fp64 accumulation and
 //     wave-level reductions -- this kernel carries ~90 % of the step's bytes;
 //   * unstandardize is fused into the readout's epilogue.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -1203,5 +1204,27 @@ extern "C" int sml_res_tile_inputs(sml_reservoirs *c, const double *d_grid4d, co
                                    const double *d_tisr, double *d_feedback, double *d_local_model, void *stream) {
     if (int rc = sml_res_tile_feedback(c, d_grid4d, d_grid2d, d_precip, d_tisr, d_feedback, stream)) return rc;
     if (c->ncs && d_fc4d && c->nlocal) return sml_res_tile_local_model(c, d_fc4d, d_fc2d, d_local_model, stream);
+    return SML_OK;
+}
+
+// ---------------------------------------------------------------- CU-range streams
+extern "C" int sml_stream_create_cu_range(int first_cu, int num_cus, void **out) {
+    SML_REQUIRE(out && first_cu >= 0 && num_cus > 0, "bad argument");
+    int dev = 0, ncu = 0;
+    SML_HIP(hipGetDevice(&dev));
+    SML_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+    SML_REQUIRE(first_cu + num_cus <= ncu, "CU range [%d, %d) exceeds the device's %d CUs", first_cu,
+                first_cu + num_cus, ncu);
+    std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+    for (int c = first_cu; c < first_cu + num_cus; ++c) mask[c / 32] |= 1u << (c % 32);
+    hipStream_t s = nullptr;
+    SML_HIP(hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()));
+    *out = s;
+    return SML_OK;
+}
+
+extern "C" int sml_stream_destroy(void *stream) {
+    SML_REQUIRE(stream, "bad argument");
+    SML_HIP(hipStreamDestroy((hipStream_t)stream));
     return SML_OK;
 }

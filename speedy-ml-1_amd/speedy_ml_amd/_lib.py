@@ -150,6 +150,8 @@ def _declare(L: ctypes.CDLL) -> None:
         "sml_train_npad": [vp, ctypes.POINTER(ctypes.c_int)],
         "sml_train_get_gram": [vp, i, vp, vp],
         "sml_probe_mfma_f64": [i, ctypes.POINTER(ctypes.c_double)],
+        "sml_stream_create_cu_range": [i, i, pp],
+        "sml_stream_destroy": [vp],
     }
     for name, args in sig.items():
         fn = getattr(L, name)

@@ -27,10 +27,22 @@ pay (profiles/r01h_*: under the readout's ~6 TB/s stream SPEEDY's small
 latency-bound kernels waited far longer on memory); with the window at 2 leaner
 launches per step it does: 496 vs 482 steps/s at 1 GPU and +0.6-1 % for the 2/4/8-
 rank shares (profiles/r01o).  bench.py uses it by default.
+
+The two streams are also given disjoint CUs (`speedy_cus`, default 64: SPEEDY on
+CUs [0, 64), the reservoir on the other 192; sml_stream_create_cu_range).  Without
+the split, SPEEDY's blocks (146-150 KB of LDS each) wait for a CU whose LDS the
+update's blocks have left, and then share that CU's memory pipeline with readout
+waves: the window ran 1.57 ms beside the readout vs 1.16 ms alone.  With it the
+overlapped step went 1.66 -> 1.43 ms (tools/probe_host_calls.py; 48 or fewer CUs
+for SPEEDY are slower: the 48 latitude-row blocks no longer have a CU each).
 """
 from __future__ import annotations
 
+import os
+
 import torch
+
+from ._lib import check, lib
 
 
 class HybridLoop:
@@ -41,7 +53,7 @@ class HybridLoop:
     or None (feedback tisr entries left as they are)."""
 
     def __init__(self, res, dyn, exchange, device, tisr=None, overlap: bool = True, nleap: int = 24,
-                 side_priority: int = -1):
+                 side_priority: int = -1, speedy_cus: int | None = None):
         self.res, self.dyn, self.exchange, self.tisr = res, dyn, exchange, tisr
         self.overlap, self.nleap = overlap, nleap
         self.dev = torch.device(device)
@@ -54,10 +66,41 @@ class HybridLoop:
         # every blocking stream, which would serialise the two chains again.  SPEEDY's
         # chain is latency-bound: its high-priority stream keeps its small launches
         # ahead of the readout's blocks
-        self.main = torch.cuda.Stream(self.dev)
-        self.side = torch.cuda.Stream(self.dev, priority=side_priority) if overlap else self.main
+        self._owned = []
+        if speedy_cus is None:
+            speedy_cus = int(os.environ.get("SML_SPEEDY_CUS", "64"))
+        ncu = torch.cuda.get_device_properties(self.dev).multi_processor_count if overlap else 0
+        if overlap and 0 < speedy_cus < ncu:
+            with torch.cuda.device(self.dev):
+                self.side = self._cu_stream(0, speedy_cus)
+                self.main = self._cu_stream(speedy_cus, ncu - speedy_cus)
+        else:
+            self.main = torch.cuda.Stream(self.dev)
+            self.side = torch.cuda.Stream(self.dev, priority=side_priority) if overlap else self.main
         self.ev_grid = torch.cuda.Event()
         self.ev_lm = torch.cuda.Event()
+
+    def _cu_stream(self, first: int, count: int):
+        import ctypes
+
+        h = ctypes.c_void_p()
+        check(lib().sml_stream_create_cu_range(first, count, ctypes.byref(h)))
+        self._owned.append(h)
+        return torch.cuda.ExternalStream(h.value, device=self.dev)
+
+    def close(self):
+        """Wait for the loop's work and release the CU-range streams it created."""
+        if self._owned:
+            torch.cuda.synchronize(self.dev)
+            for h in self._owned:
+                check(lib().sml_stream_destroy(h))
+            self._owned = []
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
     def start(self, g4, g2, pr, f4, f2):
         """start_prediction analogue: inputs of the first step from an analysis grid

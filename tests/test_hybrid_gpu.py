@@ -103,6 +103,7 @@ def test_overlapped_loop_is_bitwise_the_serial_loop(cuda):
             loop.sync()
             snaps.append(_snapshot(loop))
         runs[overlap] = (snaps, [loop.res.get_state(i) for i in (0, 500, 1151)])
+        loop.close()
         loop.dyn.close()
         loop.res.close()
         torch.cuda.synchronize()
