@@ -107,38 +107,39 @@ for rep in range(2):
         for k, e in sorted(evs.items(), key=lambda kv: base.elapsed_time(kv[1])):
             print(f"{base.elapsed_time(e) * 1e3:9.1f} us  {k}")
 
-# CU split: SPEEDY's stream on its own CUs, the reservoir stream on the rest
-import ctypes  # noqa: E402
-hip = ctypes.CDLL("libamdhip64.so")
+if os.environ.get("PROBE_SPLITS"):  # each variant creates 2 more HW queues: run alone
+    # CU split: SPEEDY's stream on its own CUs, the reservoir stream on the rest
+    import ctypes  # noqa: E402
+    hip = ctypes.CDLL("libamdhip64.so")
 
 
-def cu_stream(cus, prio=0):
-    mask = (ctypes.c_uint32 * 8)()
-    for c in cus:
-        mask[c // 32] |= 1 << (c % 32)
-    h = ctypes.c_void_p()
-    assert hip.hipExtStreamCreateWithCUMask(ctypes.byref(h), 8, mask) == 0
-    return torch.cuda.ExternalStream(h.value)
+    def cu_stream(cus, prio=0):
+        mask = (ctypes.c_uint32 * 8)()
+        for c in cus:
+            mask[c // 32] |= 1 << (c % 32)
+        h = ctypes.c_void_p()
+        assert hip.hipExtStreamCreateWithCUMask(ctypes.byref(h), 8, mask) == 0
+        return torch.cuda.ExternalStream(h.value)
 
 
-def timed_steps(n=30):
-    for _ in range(5):
-        loop.step()
-    loop.sync()
-    t0 = time.perf_counter()
-    for _ in range(n):
-        loop.step()
-    loop.sync()
-    return (time.perf_counter() - t0) / n * 1e3
+    def timed_steps(n=30):
+        for _ in range(5):
+            loop.step()
+        loop.sync()
+        t0 = time.perf_counter()
+        for _ in range(n):
+            loop.step()
+        loop.sync()
+        return (time.perf_counter() - t0) / n * 1e3
 
 
-m0, s0 = loop.main, loop.side
-print(f"split none: {timed_steps():.3f} ms/step")
-for kind, n in [(k, n) for n in (32, 48, 64, 80, 96, 128) for k in ("lo", "hi")] + [("lo", 64), ("hi", 64)]:
-    side_cus = list(range(n)) if kind == "lo" else list(range(256 - n, 256))
-    main_cus = [c for c in range(256) if c not in side_cus]
-    loop.main, loop.side = cu_stream(main_cus), cu_stream(side_cus)
-    a = timed_steps()
-    loop.main, loop.side = m0, s0
-    c = timed_steps()
-    print(f"split {kind}:{n}: both masked {a:.3f}, none {c:.3f} ms/step")
+    m0, s0 = loop.main, loop.side
+    print(f"split none: {timed_steps():.3f} ms/step")
+    for kind, n in [(k, n) for n in (32, 48, 64, 80, 96, 128) for k in ("lo", "hi")] + [("lo", 64), ("hi", 64)]:
+        side_cus = list(range(n)) if kind == "lo" else list(range(256 - n, 256))
+        main_cus = [c for c in range(256) if c not in side_cus]
+        loop.main, loop.side = cu_stream(main_cus), cu_stream(side_cus)
+        a = timed_steps()
+        loop.main, loop.side = m0, s0
+        c = timed_steps()
+        print(f"split {kind}:{n}: both masked {a:.3f}, none {c:.3f} ms/step")
