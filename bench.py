@@ -139,6 +139,7 @@ def main():
     dyn.set_physics(phys_bc)
     # the hybrid loop (speedy_ml_amd/hybrid.py); --overlap puts SPEEDY's window on a
     # second stream beside the reservoir update + v_ml readout
+    ncu = torch.cuda.get_device_properties(dev).multi_processor_count
     loop = HybridLoop(res, dyn, exchange, dev, tisr=tisr, overlap=args.overlap, speedy_cus=args.speedy_cus)
     # initial inputs from the synthetic analysis state (start_prediction analogue)
     loop.start(t(g4h), t(g2h), t(prh), t(f4h), t(f2h))
@@ -272,8 +273,10 @@ def main():
             "last_window_safe": bool(safe),
             "finite": finite,
             "roofline": {
-                "kernel": ("k_res_readout<ml> (v_ml = W_out(:, ncs+1:) x~, GEMV, 8 rows per item; paced beside "
-                           "SPEEDY's window: at most 2048 waves, see reservoir_only.roofline_unpaced)"
+                "kernel": (("k_res_readout<ml> (v_ml = W_out(:, ncs+1:) x~, GEMV, 8 rows per item; beside "
+                            + (f"SPEEDY's window on the other {ncu - args.speedy_cus} CUs, unpaced"
+                               if args.speedy_cus > 0 else "SPEEDY's window on shared CUs, paced at 2048 waves")
+                            + "; the one-pass form on all CUs: reservoir_only.roofline_unpaced)")
                            if args.overlap else
                            "k_res_readout<full> (W_out [local_model; x~] + unstandardize, GEMV, 17 waves x 8 rows "
                            "per region)"),

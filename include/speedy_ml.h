@@ -165,6 +165,11 @@ int sml_res_step(sml_reservoirs *c, const double *d_feedback, const double *d_lo
  * before the next begin (SML_ERR_STATE otherwise). */
 int sml_res_step_begin(sml_reservoirs *c, const double *d_feedback, void *stream);
 int sml_res_step_finish(sml_reservoirs *c, const double *d_local_model, double *d_outvec, void *stream);
+/* cap on the waves of the v_ml readout issued by sml_res_step_begin (0 = one wave per
+ * 8-row item, the default cap is 2048).  The cap leaves HBM headroom for SPEEDY when
+ * both share CUs; on CUs of their own (sml_stream_create_cu_range) it is not needed.
+ * The environment variable SML_READ_WAVES, when set, takes precedence. */
+int sml_res_set_read_waves(sml_reservoirs *c, int waves);
 /* synchronize (src/mod_reservoir.f90:1352-1378), the spin-up of start_prediction
  * (:938-959): `length` updates x = (1-leak) x + leak tanh(A x + W_in u_t) for every
  * local region, no readout.  d_inputs holds `length` blocks in the packed feedback

@@ -84,9 +84,11 @@ struct sml_reservoirs {
     double *d_xaug = nullptr, *d_meanstd = nullptr;
     double *d_part = nullptr;       // [nlocal][nout_pad] W_out(:, ncs+1:) x~ of the step in flight
     // cap on the waves of the v_ml readout (the half that runs beside SPEEDY's window;
-    // 0: one wave per item).  Uncapped it takes ~6 TB/s and SPEEDY's latency-bound
-    // kernels stall behind it; paced at 2048 waves (~4.7 TB/s) the overlapped step
-    // is 1.75 ms instead of 1.98 (profiles/r01p).  SML_READ_WAVES overrides.
+    // 0: one wave per item).  Sharing CUs with SPEEDY, uncapped it takes ~6 TB/s and
+    // SPEEDY's latency-bound kernels stall behind it; paced at 2048 waves (~4.7 TB/s)
+    // the overlapped step is 1.75 ms instead of 1.98 (profiles/r01p).  On CUs of its
+    // own the pacing does not matter: sml_res_set_read_waves(0).
+    // SML_READ_WAVES overrides both.
     int read_waves = 2048;
     int upd_blocks = 0;  // cap on the update's grid in sml_res_step_begin (0: none; SML_UPD_BLOCKS)
     bool begun = false;             // sml_res_step_begin issued, finish pending
@@ -931,6 +933,12 @@ extern "C" int sml_res_get_state(sml_reservoirs *c, int i, double *x) {
     SML_REQUIRE(x, "x is null");
     SML_HIP(hipDeviceSynchronize());
     SML_HIP(hipMemcpy(x, c->d_x[c->cur] + c->rd[i].x, (size_t)c->n[i] * 8, hipMemcpyDeviceToHost));
+    return SML_OK;
+}
+
+extern "C" int sml_res_set_read_waves(sml_reservoirs *c, int waves) {
+    SML_REQUIRE(c && waves >= 0, "bad argument");
+    if (!std::getenv("SML_READ_WAVES")) c->read_waves = waves;
     return SML_OK;
 }
 

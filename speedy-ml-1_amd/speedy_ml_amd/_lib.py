@@ -108,6 +108,7 @@ def _declare(L: ctypes.CDLL) -> None:
         "sml_res_synchronize": [vp, vp, i, ctypes.c_int64, vp],
         "sml_res_footprint": [vp, i64p, i64p],
         "sml_res_enable_timing": [vp, i],
+        "sml_res_set_read_waves": [vp, i],
         "sml_res_kernel_times": [vp, vp, vp, i, ctypes.POINTER(ctypes.c_int)],
         "sml_exchange_assemble": [vp, vp, vp, vp, vp, vp],
         "sml_res_tile_inputs": [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp],

@@ -74,6 +74,7 @@ class HybridLoop:
             with torch.cuda.device(self.dev):
                 self.side = self._cu_stream(0, speedy_cus)
                 self.main = self._cu_stream(speedy_cus, ncu - speedy_cus)
+            res.set_read_waves(0)  # pacing the readout only pays when it shares CUs with SPEEDY
         else:
             self.main = torch.cuda.Stream(self.dev)
             self.side = torch.cuda.Stream(self.dev, priority=side_priority) if overlap else self.main

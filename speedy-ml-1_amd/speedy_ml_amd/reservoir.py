@@ -109,6 +109,10 @@ class Reservoirs:
         outvec_component_contribs, mod_reservoir.f90:1456-1459) -- no local_model needed."""
         check(lib().sml_res_step_begin(self._h, ptr(d_feedback), stream_ptr(stream)))
 
+    def set_read_waves(self, waves: int):
+        """Cap on the v_ml readout's waves in predict_begin (0 = uncapped)."""
+        check(lib().sml_res_set_read_waves(self._h, int(waves)))
+
     def predict_finish(self, d_local_model, d_outvec, stream=None):
         """Second half: outvec = W_out(:, 1:ncs) local_model + v_ml, unstandardized."""
         check(lib().sml_res_step_finish(self._h, ptr(d_local_model if self.ncs else None), ptr(d_outvec),
