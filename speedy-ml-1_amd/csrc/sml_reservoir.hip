@@ -32,6 +32,13 @@
 
 #include "sml_internal.hpp"
 
+#ifndef SML_READ_NT
+#define SML_READ_NT 1
+#endif
+#ifndef SML_UPD_NT
+#define SML_UPD_NT 1
+#endif
+
 using namespace sml;
 
 namespace {
@@ -138,27 +145,43 @@ struct RowRegs {
     WT wv;
 };
 
+// A and W_in are streamed once per step: non-temporal loads (SML_UPD_NT), like the
+// readout's W_out, so they do not evict the data of the SPEEDY window running beside
+typedef uint32_t nt_u4 __attribute__((ext_vector_type(4)));
+typedef float nt_f4 __attribute__((ext_vector_type(4)));
+typedef double nt_d2 __attribute__((ext_vector_type(2)));
+template <typename T>
+__device__ inline T stream_load(const T *p) {
+#if SML_UPD_NT
+    return __builtin_nontemporal_load(p);
+#else
+    return *p;
+#endif
+}
+
 template <typename WT>
 __device__ inline void load_row(RowRegs<WT> &q, const RegionDev &rg, const Ell &ell, int i, bool live) {
     if (live && rg.a_w > 0) {
-        q.c = *reinterpret_cast<const uint4 *>(ell.a_col + rg.a_ell + (size_t)i * kEllA);
+        const nt_u4 c = stream_load(reinterpret_cast<const nt_u4 *>(ell.a_col + rg.a_ell + (size_t)i * kEllA));
+        q.c = make_uint4(c.x, c.y, c.z, c.w);
         const WT *ev = (const WT *)ell.a_val + rg.a_ell + (size_t)i * kEllA;
         if constexpr (sizeof(WT) == 4) {
-            const float4 a = reinterpret_cast<const float4 *>(ev)[0], b = reinterpret_cast<const float4 *>(ev)[1];
+            const nt_f4 a = stream_load(reinterpret_cast<const nt_f4 *>(ev)),
+                        b = stream_load(reinterpret_cast<const nt_f4 *>(ev) + 1);
             q.v[0] = a.x; q.v[1] = a.y; q.v[2] = a.z; q.v[3] = a.w;
             q.v[4] = b.x; q.v[5] = b.y; q.v[6] = b.z; q.v[7] = b.w;
         } else {
 #pragma unroll
             for (int s = 0; s < kEllA / 2; ++s) {
-                const double2 a = reinterpret_cast<const double2 *>(ev)[s];
+                const nt_d2 a = stream_load(reinterpret_cast<const nt_d2 *>(ev) + s);
                 q.v[2 * s] = a.x;
                 q.v[2 * s + 1] = a.y;
             }
         }
     }
     if (live && rg.w_w > 0) {
-        q.wc = ell.w_col[rg.w_ell + i];
-        q.wv = ((const WT *)ell.w_val)[rg.w_ell + i];
+        q.wc = stream_load(ell.w_col + rg.w_ell + i);
+        q.wv = stream_load((const WT *)ell.w_val + rg.w_ell + i);
     }
 }
 
@@ -306,7 +329,11 @@ __device__ __attribute__((always_inline)) inline Rows rows_dot(const WT *W, int 
         V w[kRows];
 #pragma unroll
         for (int q = 0; q < kRows; ++q)  // streamed once per step: non-temporal, so W_out does not evict the
-            w[q] = __builtin_nontemporal_load(reinterpret_cast<const V *>(W + (size_t)q * ld + j));  // window's data
+#if SML_READ_NT                          // window's data
+            w[q] = __builtin_nontemporal_load(reinterpret_cast<const V *>(W + (size_t)q * ld + j));
+#else
+            w[q] = *reinterpret_cast<const V *>(W + (size_t)q * ld + j);
+#endif
 #pragma unroll
         for (int q = 0; q < kRows; ++q) {
             double s = acc[q];

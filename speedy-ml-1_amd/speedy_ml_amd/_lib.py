@@ -11,7 +11,8 @@ import os
 import subprocess
 
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))  # speedy-ml-1_amd/
-LIB_PATH = os.path.join(PKG_ROOT, "lib", "libspeedyml.so")
+# SML_LIB: an alternative build of the same library (A/B measurements only)
+LIB_PATH = os.environ.get("SML_LIB") or os.path.join(PKG_ROOT, "lib", "libspeedyml.so")
 CSRC = os.path.join(PKG_ROOT, "csrc")
 
 SML_OK = 0

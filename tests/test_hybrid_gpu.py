@@ -54,7 +54,7 @@ def test_begin_finish_matches_oracle_and_checks_order(cuda):
         assert xerr.max() < 1e-14, f"region {w.region}: state {xerr.max():.3e}"  # device vs glibc tanh
 
 
-def _loop(cuda, overlap):
+def _loop(cuda, overlap, speedy_cus=None):
     import torch
 
     from speedy_ml_amd.dynamics import Dynamics
@@ -76,7 +76,8 @@ def _loop(cuda, overlap):
     dyn.set_physics(phys_boundary(dyn, forcing["phis"]))
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(cuda)  # noqa: E731
     tisr = t(np.random.default_rng(13).standard_normal((1152, 16)))
-    loop = HybridLoop(res, dyn, OutvecExchange(1152, 1, 0, device=cuda), cuda, tisr=tisr, overlap=overlap)
+    loop = HybridLoop(res, dyn, OutvecExchange(1152, 1, 0, device=cuda), cuda, tisr=tisr, overlap=overlap,
+                      speedy_cus=speedy_cus)
     g4, g2, pr = synthetic_grids(11)
     f4, f2, _ = synthetic_grids(12)
     loop.start(t(g4), t(g2), t(pr), t(f4), t(f2))
@@ -91,12 +92,14 @@ def _snapshot(loop):
     return {k: getattr(loop, k).cpu().numpy().copy() for k in ("ov", "fb", "lm", "g4", "g2", "pr", "f4", "f2")}
 
 
-def test_overlapped_loop_is_bitwise_the_serial_loop(cuda):
+@pytest.mark.parametrize("speedy_cus", [64, 0])
+def test_overlapped_loop_is_bitwise_the_serial_loop(cuda, speedy_cus):
+    """speedy_cus 64: the streams on disjoint CUs (bench default); 0: shared CUs, paced readout."""
     import torch
 
     runs = {}
     for overlap in (False, True):
-        loop, ws = _loop(cuda, overlap)
+        loop, ws = _loop(cuda, overlap, speedy_cus)
         snaps = []
         for _ in range(3):
             loop.step()
@@ -140,3 +143,27 @@ def test_loop_matches_the_sequential_chain(cuda):
     a, b = _snapshot(loop), _snapshot(seq)
     for k in a:
         np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+
+
+def test_cu_range_streams(cuda):
+    """sml_stream_create_cu_range: a CU-masked stream runs kernels; bad ranges fail loudly."""
+    import ctypes
+
+    import torch
+
+    from speedy_ml_amd._lib import SmlError, check, lib
+
+    ncu = torch.cuda.get_device_properties(cuda).multi_processor_count
+    h = ctypes.c_void_p()
+    with pytest.raises(SmlError):
+        check(lib().sml_stream_create_cu_range(ncu - 8, 16, ctypes.byref(h)))
+    with pytest.raises(SmlError):
+        check(lib().sml_stream_create_cu_range(0, 0, ctypes.byref(h)))
+    check(lib().sml_stream_create_cu_range(0, 8, ctypes.byref(h)))
+    s = torch.cuda.ExternalStream(h.value, device=cuda)
+    x = torch.arange(1 << 20, dtype=torch.float64, device=cuda)
+    with torch.cuda.stream(s):
+        y = (x * 2.0).sum()
+    s.synchronize()
+    assert float(y) == float(np.arange(1 << 20, dtype=np.float64).sum() * 2.0)
+    check(lib().sml_stream_destroy(h))
