@@ -29,7 +29,8 @@ EXPORTED = (
     "sml_res_create", "sml_res_destroy", "sml_res_ninp", "sml_res_feedback_offsets",
     "sml_res_load_region_f32", "sml_res_load_region_f64", "sml_res_set_state", "sml_res_get_state",
     "sml_res_step", "sml_res_step_begin", "sml_res_step_finish", "sml_res_step_host", "sml_res_synchronize",
-    "sml_res_footprint", "sml_res_enable_timing", "sml_res_kernel_times", "sml_exchange_assemble",
+    "sml_res_footprint", "sml_res_enable_timing", "sml_res_kernel_times", "sml_res_set_read_waves",
+    "sml_exchange_assemble",
     "sml_res_tile_inputs", "sml_res_tile_feedback", "sml_res_tile_local_model",
     "sml_nc_read_region", "sml_nc_write_region",
     "sml_dyn_create", "sml_dyn_destroy", "sml_dyn_impint", "sml_dyn_set_forcing", "sml_dyn_set_state",
@@ -40,6 +41,7 @@ EXPORTED = (
     "sml_dyn_get_rad_state", "sml_dyn_phypar", "sml_dyn_phypar_host", "sml_dyn_sol_oz", "sml_phys_sflset",
     "sml_train_create", "sml_train_destroy", "sml_train_reset", "sml_train_accumulate", "sml_train_solve",
     "sml_train_npad", "sml_train_get_gram", "sml_probe_mfma_f64",
+    "sml_stream_create_cu_range", "sml_stream_destroy",
 )
 
 
