@@ -156,6 +156,27 @@ module sml_hip
       integer(c_int) :: rc
     end function
 
+    function sml_res_set_read_waves(ctx, waves) bind(C, name='sml_res_set_read_waves') result(rc)
+      import :: c_ptr, c_int
+      type(c_ptr), value :: ctx
+      integer(c_int), value :: waves
+      integer(c_int) :: rc
+    end function
+
+    ! a stream on the logical CUs [first_cu, first_cu + num_cus) (hipExtStreamCreateWithCUMask)
+    function sml_stream_create_cu_range(first_cu, num_cus, stream) bind(C, name='sml_stream_create_cu_range') result(rc)
+      import :: c_ptr, c_int
+      integer(c_int), value :: first_cu, num_cus
+      type(c_ptr) :: stream
+      integer(c_int) :: rc
+    end function
+
+    function sml_stream_destroy(stream) bind(C, name='sml_stream_destroy') result(rc)
+      import :: c_ptr, c_int
+      type(c_ptr), value :: stream
+      integer(c_int) :: rc
+    end function
+
     function sml_res_step_finish(ctx, d_local_model, d_outvec, stream) bind(C, name='sml_res_step_finish') result(rc)
       import :: c_ptr, c_int
       type(c_ptr), value :: ctx, d_local_model, d_outvec, stream
