@@ -1,4 +1,4 @@
-﻿!mod$ v1 sum:57c4611cc5073336
+﻿!mod$ v1 sum:ef5c8810213d244f
 !need$ 0bde2ac47243ead2 i iso_c_binding
 module sml_hip
 use,intrinsic::iso_c_binding,only:c_associated
@@ -266,6 +266,30 @@ function sml_res_step_begin(ctx,d_feedback,stream) bind(c,name="sml_res_step_beg
 import::c_ptr
 type(c_ptr),value::ctx
 type(c_ptr),value::d_feedback
+type(c_ptr),value::stream
+integer(4)::rc
+end
+end interface
+interface
+function sml_res_set_read_waves(ctx,waves) bind(c,name="sml_res_set_read_waves") result(rc)
+import::c_ptr
+type(c_ptr),value::ctx
+integer(4),value::waves
+integer(4)::rc
+end
+end interface
+interface
+function sml_stream_create_cu_range(first_cu,num_cus,stream) bind(c,name="sml_stream_create_cu_range") result(rc)
+import::c_ptr
+integer(4),value::first_cu
+integer(4),value::num_cus
+type(c_ptr)::stream
+integer(4)::rc
+end
+end interface
+interface
+function sml_stream_destroy(stream) bind(c,name="sml_stream_destroy") result(rc)
+import::c_ptr
 type(c_ptr),value::stream
 integer(4)::rc
 end
