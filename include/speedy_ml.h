@@ -165,6 +165,12 @@ int sml_res_step(sml_reservoirs *c, const double *d_feedback, const double *d_lo
  * before the next begin (SML_ERR_STATE otherwise). */
 int sml_res_step_begin(sml_reservoirs *c, const double *d_feedback, void *stream);
 int sml_res_step_finish(sml_reservoirs *c, const double *d_local_model, double *d_outvec, void *stream);
+/* finish straight from SPEEDY's forecast grids: the local-model tiling of
+ * sml_res_tile_local_model (res_domain.f90:1000-1031, standardize_state_vec_res
+ * :1189-1293) fused into sml_res_step_finish, one launch; identical results.
+ * d_local_model (may be NULL) also receives the tiled vectors. */
+int sml_res_step_finish_grid(sml_reservoirs *c, const double *d_fc4d, const double *d_fc2d, double *d_local_model,
+                             double *d_outvec, void *stream);
 /* cap on the waves of the v_ml readout issued by sml_res_step_begin (0 = one wave per
  * 8-row item, the default cap is 2048).  The cap leaves HBM headroom for SPEEDY when
  * both share CUs; on CUs of their own (sml_stream_create_cu_range) it is not needed.

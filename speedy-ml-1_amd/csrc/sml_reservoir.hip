@@ -44,6 +44,7 @@ using namespace sml;
 namespace {
 
 constexpr int kRows = 8;        // W_out rows per wave in the readout
+constexpr int kMaxNcs = 256;     // local-model length bound of the fused finish (132 in T30L8)
 constexpr int kMeanStd = 36;    // mean/std vector length (mod_reservoir.f90:1815-1846)
 constexpr int kTisrStride = 16; // packed tisr input: [nlocal][16]
 constexpr int kSrcKeep = -1;    // feedback entry left untouched (sst)
@@ -445,6 +446,38 @@ __global__ __launch_bounds__(256) void k_res_finish(const RegionDev *__restrict_
     const double vp = vp_sum(wlm + R[r].wlm, nout_pad, local_model + (size_t)r * ncs, ncs, o);
     outvec[(size_t)r * nout + o] =
         unstd(vp + part[(size_t)r * nout_pad + o], meanstd + (size_t)r * 2 * kMeanStd, outl[o]);
+}
+
+// sml_res_step_finish_grid: k_tile_local_model + k_res_finish in one launch, one
+// block per region.  The region's local-model vector is tiled and standardized
+// into LDS (and to d_lm when given) exactly as k_tile_local_model does, then each
+// thread finishes one output with vp_sum over the LDS copy: the same values, sums
+// and order as the two-launch form, one kernel boundary fewer on the hybrid step's
+// critical path
+template <typename WT>
+__global__ __launch_bounds__(256) void k_res_finish_grid(
+    const RegionDev *__restrict__ R, const WT *__restrict__ wlm, const int32_t *__restrict__ src,
+    const uint8_t *__restrict__ lidx, const double *__restrict__ fc4, const double *__restrict__ fc2,
+    double *__restrict__ lm_out, const double *__restrict__ meanstd, const int8_t *__restrict__ outl,
+    const double *__restrict__ part, double *__restrict__ outvec, int nout, int nout_pad, int ncs) {
+    __shared__ double slm[kMaxNcs];
+    const int r = blockIdx.x, t = threadIdx.x;
+    const double *ms = meanstd + (size_t)r * 2 * kMeanStd;
+    for (int j = t; j < ncs; j += blockDim.x) {
+        const int e = r * ncs + j;
+        const int s = src[e];
+        const double v = s < kGrid4d ? fc4[s] : fc2[s - kGrid4d];
+        const int l = lidx[e];
+        const double d = v - ms[l];
+        const double x = d / ms[kMeanStd + l];
+        slm[j] = x;
+        if (lm_out) lm_out[e] = x;
+    }
+    __syncthreads();
+    for (int o = t; o < nout; o += blockDim.x) {
+        const double vp = vp_sum(wlm + R[r].wlm, nout_pad, slm, ncs, o);
+        outvec[(size_t)r * nout + o] = unstd(vp + part[(size_t)r * nout_pad + o], ms, outl[o]);
+    }
 }
 
 // assemble: all regions' outvecs -> global grids, with the root's clips
@@ -1116,6 +1149,27 @@ extern "C" int sml_res_step_finish(sml_reservoirs *c, const double *d_local_mode
     if (!c->begun) return fail(SML_ERR_STATE, "sml_res_step_finish without sml_res_step_begin");
     hipStream_t st = (hipStream_t)stream;
     launch_readout<kReadFinish>(c, d_local_model, d_outvec, st);
+    SML_HIP(hipGetLastError());
+    c->begun = false;
+    return SML_OK;
+}
+
+extern "C" int sml_res_step_finish_grid(sml_reservoirs *c, const double *d_fc4d, const double *d_fc2d,
+                                        double *d_local_model, double *d_outvec, void *stream) {
+    SML_REQUIRE(c, "null context");
+    if (c->nlocal == 0) return SML_OK;
+    SML_REQUIRE(d_outvec && d_fc4d && d_fc2d, "null device buffer");
+    SML_REQUIRE(c->ncs <= kMaxNcs, "ncs %d exceeds %d", c->ncs, kMaxNcs);
+    if (!c->begun) return fail(SML_ERR_STATE, "sml_res_step_finish_grid without sml_res_step_begin");
+    hipStream_t st = (hipStream_t)stream;
+    if (c->wdtype == SML_F32)
+        hipLaunchKernelGGL(k_res_finish_grid<float>, dim3(c->nlocal), dim3(256), 0, st, c->d_rd,
+                           (const float *)c->d_wlm, c->d_lm_src, c->d_lm_l, d_fc4d, d_fc2d, d_local_model,
+                           c->d_meanstd, c->d_outl, c->d_part, d_outvec, c->nout, c->nout_pad, c->ncs);
+    else
+        hipLaunchKernelGGL(k_res_finish_grid<double>, dim3(c->nlocal), dim3(256), 0, st, c->d_rd,
+                           (const double *)c->d_wlm, c->d_lm_src, c->d_lm_l, d_fc4d, d_fc2d, d_local_model,
+                           c->d_meanstd, c->d_outl, c->d_part, d_outvec, c->nout, c->nout_pad, c->ncs);
     SML_HIP(hipGetLastError());
     c->begun = false;
     return SML_OK;

@@ -109,6 +109,12 @@ class Reservoirs:
         outvec_component_contribs, mod_reservoir.f90:1456-1459) -- no local_model needed."""
         check(lib().sml_res_step_begin(self._h, ptr(d_feedback), stream_ptr(stream)))
 
+    def predict_finish_grid(self, d_fc4d, d_fc2d, d_local_model, d_outvec, stream=None):
+        """tile_local_model + predict_finish in one launch (same results); d_local_model
+        (or None) also receives the tiled local-model vectors."""
+        check(lib().sml_res_step_finish_grid(self._h, ptr(d_fc4d), ptr(d_fc2d), ptr(d_local_model), ptr(d_outvec),
+                                             stream_ptr(stream)))
+
     def set_read_waves(self, waves: int):
         """Cap on the v_ml readout's waves in predict_begin (0 = uncapped)."""
         check(lib().sml_res_set_read_waves(self._h, int(waves)))
