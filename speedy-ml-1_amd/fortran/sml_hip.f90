@@ -156,6 +156,14 @@ module sml_hip
       integer(c_int) :: rc
     end function
 
+    ! finish from SPEEDY's forecast grids: tile_local_model fused into the v_p finish
+    function sml_res_step_finish_grid(ctx, d_fc4d, d_fc2d, d_local_model, d_outvec, stream) &
+        bind(C, name='sml_res_step_finish_grid') result(rc)
+      import :: c_ptr, c_int
+      type(c_ptr), value :: ctx, d_fc4d, d_fc2d, d_local_model, d_outvec, stream
+      integer(c_int) :: rc
+    end function
+
     function sml_res_set_read_waves(ctx, waves) bind(C, name='sml_res_set_read_waves') result(rc)
       import :: c_ptr, c_int
       type(c_ptr), value :: ctx

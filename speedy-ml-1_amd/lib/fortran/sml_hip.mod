@@ -1,4 +1,4 @@
-﻿!mod$ v1 sum:ef5c8810213d244f
+﻿!mod$ v1 sum:09b20f0812bc218b
 !need$ 0bde2ac47243ead2 i iso_c_binding
 module sml_hip
 use,intrinsic::iso_c_binding,only:c_associated
@@ -266,6 +266,18 @@ function sml_res_step_begin(ctx,d_feedback,stream) bind(c,name="sml_res_step_beg
 import::c_ptr
 type(c_ptr),value::ctx
 type(c_ptr),value::d_feedback
+type(c_ptr),value::stream
+integer(4)::rc
+end
+end interface
+interface
+function sml_res_step_finish_grid(ctx,d_fc4d,d_fc2d,d_local_model,d_outvec,stream) bind(c,name="sml_res_step_finish_grid") result(rc)
+import::c_ptr
+type(c_ptr),value::ctx
+type(c_ptr),value::d_fc4d
+type(c_ptr),value::d_fc2d
+type(c_ptr),value::d_local_model
+type(c_ptr),value::d_outvec
 type(c_ptr),value::stream
 integer(4)::rc
 end
