@@ -288,8 +288,23 @@ int sml_dyn_from_grid(sml_dynamics *d, const double *d_grid4d, const double *d_l
                       void *stream);
 /* iogrid(31) (src/ppo_iogrid.f90:573-595), the window exit: level 1 -> grid4d, logp */
 int sml_dyn_to_grid(sml_dynamics *d, double *d_grid4d, double *d_logp, void *stream);
-/* is_safe_to_run_speedy from the 8 min/max values (src/ppo_iogrid.f90:556-571) */
+/* is_safe_to_run_speedy from the 8 min/max values (src/ppo_iogrid.f90:563-577); a NaN
+ * makes the state unsafe */
 int sml_dyn_is_safe(const double *minmax);
+/* run_model (src/mpires.f90:1516-1628) minus its file I/O: iogrid(30) of d_grid4d /
+ * d_logp with the safety check, the window (as sml_dyn_window), iogrid(31) into
+ * d_fc4d / d_fc2d, then q floored at 1e-6 (:1614-1616).  When the check fails,
+ * agcm_main skips the integration (at_gcm.f90:37): the forecast is then the input
+ * grid with q floored (run_model's copy, :1550-1553).  The check runs beside the
+ * window; sml_dyn_last_safe reads its outcome.  The forecast buffers must not alias
+ * the inputs. */
+int sml_dyn_run_model(sml_dynamics *d, const double *d_grid4d, const double *d_logp, int nleap, double delt,
+                      double alph, double rob, double wil, double *d_fc4d, double *d_fc2d, void *stream);
+/* is_safe_to_run_speedy of the last sml_dyn_from_grid / sml_dyn_run_model, i.e. the
+ * run_speedy flag the reference broadcasts (src/mpires.f90:721, :1623) and stops the
+ * prediction loop on (src/parallelmain.f90:268-270).  Waits only for that check;
+ * minmax (may be NULL) receives its 8 values. */
+int sml_dyn_last_safe(sml_dynamics *d, int *safe, double *minmax);
 /* synchronous host-buffer variants */
 int sml_dyn_from_grid_host(sml_dynamics *d, const double *grid4d, const double *logp, double *minmax, int *safe);
 int sml_dyn_to_grid_host(sml_dynamics *d, double *grid4d, double *logp);
@@ -373,6 +388,80 @@ int sml_probe_mfma_f64(int iters, double *tflops);
  * LDS behind update blocks nor share a CU's memory pipeline with readout waves. */
 int sml_stream_create_cu_range(int first_cu, int num_cus, void **stream);
 int sml_stream_destroy(void *stream);
+
+/* ------------------------------------------------------------ communicator */
+/* RCCL communicator of the ranks of one node (one process per GPU, xGMI): replaces
+ * the MPI world of startmpi (src/mpires.f90:21-37) for the one collective of the hot
+ * path.  The 128-byte unique id comes from rank 0 (sml_comm_unique_id) over the
+ * host's own channel, or through a file (sml_comm_create_file: rank 0 publishes it,
+ * the others wait up to timeout_s seconds). */
+typedef struct sml_comm sml_comm;
+int sml_comm_unique_id(unsigned char *id128);
+int sml_comm_create(int world, int rank, const unsigned char *id128, sml_comm **out);
+int sml_comm_create_file(int world, int rank, const char *path, int timeout_s, sml_comm **out);
+int sml_comm_destroy(sml_comm *c);
+int sml_comm_rank(const sml_comm *c, int *world, int *rank);
+/* all-gather of equal slabs of `count` doubles: d_recv[world][count] (ncclAllGather) --
+ * the outvec exchange that replaces sendrecievegrid's point-to-point gather/scatter
+ * (src/mpires.f90:338-716) */
+int sml_comm_allgather(sml_comm *c, const double *d_send, double *d_recv, int64_t count, void *stream);
+
+/* ------------------------------------------------------------ hybrid loop */
+/* The prediction loop of one rank (src/parallelmain.f90:204-270): predict for the
+ * rank's regions -> outvec exchange -> assemble -> run_model (SPEEDY's window on the
+ * GPU) -> re-tile.  res must hold this rank's processor_decomposition
+ * (res_domain.f90:31-62) of comm's world (comm NULL = one rank); dyn must have its
+ * state, forcing and physics set.  overlap != 0: the reservoir's update and v_ml
+ * readout run beside SPEEDY's window on a second stream (identical results), with
+ * SPEEDY on CUs [0, speedy_cus) when 0 < speedy_cus < CUs. */
+typedef struct sml_hybrid sml_hybrid;
+int sml_hybrid_create(sml_reservoirs *res, sml_dynamics *dyn, sml_comm *comm, int nleap, double delt, double alph,
+                      double rob, double wil, int overlap, int speedy_cus, sml_hybrid **out);
+int sml_hybrid_destroy(sml_hybrid *h);
+/* caller-owned device buffers: packed feedback, local model [nlocal][ncs], local
+ * outvecs [nlocal][nout], the assembled grids grid4d(4,96,48,8) / grid2d / precip,
+ * SPEEDY's forecast grids fc4d / fc2d, tisr [nlocal][16] (standardized, may be NULL =
+ * feedback tisr entries left as they are) */
+int sml_hybrid_set_buffers(sml_hybrid *h, double *d_feedback, double *d_local_model, double *d_outvec,
+                           double *d_grid4d, double *d_grid2d, double *d_precip, double *d_fc4d, double *d_fc2d,
+                           const double *d_tisr);
+/* tisr inputs of the next steps (get_tisr_by_date, src/mpires.f90:1644-1676) */
+int sml_hybrid_set_tisr(sml_hybrid *h, const double *d_tisr);
+/* the loop's main (reservoir + exchange) and side (SPEEDY) streams */
+int sml_hybrid_streams(const sml_hybrid *h, void **main, void **side);
+/* start_prediction's hand-over: inputs of the first step from an analysis grid and
+ * a SPEEDY forecast of it (src/mod_reservoir.f90:938-959) */
+int sml_hybrid_start(sml_hybrid *h, const double *d_grid4d, const double *d_grid2d, const double *d_precip,
+                     const double *d_fc4d, const double *d_fc2d);
+/* a step in two halves around a host-provided exchange: predict leaves the local
+ * outvecs in d_outvec on the main stream; advance takes every region's outvecs in
+ * global region order ([numregions][nout]) */
+int sml_hybrid_predict(sml_hybrid *h);
+int sml_hybrid_advance(sml_hybrid *h, const double *d_outvec_all);
+/* predict + the loop's own exchange (identity on one rank, sml_comm_allgather
+ * otherwise) + advance; asynchronous */
+int sml_hybrid_step(sml_hybrid *h);
+/* run_speedy of the last step (0: the reference ends the prediction,
+ * parallelmain.f90:268-270); waits only for that step's safety check */
+int sml_hybrid_run_speedy(sml_hybrid *h, int *run);
+/* wait for the issued steps; d_local_model then holds the last window's local model */
+int sml_hybrid_sync(sml_hybrid *h);
+/* ------------------------------------------------------------ host plumbing */
+/* zeroed device allocation / free, synchronous copies (for hosts without a GPU
+ * runtime binding of their own, e.g. the Fortran host) */
+int sml_device_alloc(int64_t bytes, void **d_ptr);
+int sml_device_free(void *d_ptr);
+int sml_copy_to_device(void *d_dst, const void *src, int64_t bytes);
+int sml_copy_to_host(void *dst, const void *d_src, int64_t bytes);
+/* res_domain geometry of one region (getxyresextent / getoverlapindices,
+ * src/res_domain.f90:123-204), 1-based: g[12] = res_xstart, res_xend, res_ystart,
+ * res_yend, resx, resy, in_xstart, in_xend, in_ystart, in_yend, inx, iny */
+int sml_region_geometry(int numregions, int region, int *g);
+/* processor_decomposition (src/res_domain.f90:31-62): 0-based regions of rank irank */
+int sml_processor_decomposition(int numregions, int numprocs, int irank, int *regions, int *count);
+/* numregions, nlocal, chunk_speedy, nout and the local region ids (any may be NULL) */
+int sml_res_info(const sml_reservoirs *c, int *numregions, int *nlocal, int *chunk_speedy, int *nout,
+                 int *region_ids);
 
 #ifdef __cplusplus
 }

@@ -97,6 +97,12 @@ struct sml_dynamics {
     hipStream_t chk_stream = nullptr;
     hipEvent_t ev_fork = nullptr, ev_chk = nullptr;
     bool chk_pending = false;  // work on chk_stream that the next user of d_chk must wait for
+    // host copy of the last check's min/max (pinned; written behind the check on its
+    // stream, ev_mm marks it): run_speedy for a host loop without a device sync
+    double *h_mm = nullptr;
+    hipEvent_t ev_mm = nullptr;
+    bool mm_issued = false;
+    const double *mm_last = nullptr;  // device min/max of the last from_grid
     bool impint_done = false;
     // GPU physics (phypar): tables, boundary fields [kNBc][ngp], radiation state
     PhysTables ptab;
@@ -1408,19 +1414,24 @@ __global__ void k_io_prep(const double *__restrict__ st, double *__restrict__ si
 
 // entry safety check (:556-571): min / max of the re-gridded u, v, t, q.  One
 // block of 1024 threads per variable.
+// NaN-sticky min / max (fmin / fmax would drop a NaN; a blown-up state must not
+// pass the check, io_state_safe)
+__device__ inline double nmin(double a, double b) { return (a != a || b != b) ? __builtin_nan("") : (b < a ? b : a); }
+__device__ inline double nmax(double a, double b) { return (a != a || b != b) ? __builtin_nan("") : (b > a ? b : a); }
+
 __global__ __launch_bounds__(1024) void k_io_minmax(const double *__restrict__ G, double *__restrict__ mm) {
     __shared__ double smin[16], smax[16];
     const int v = blockIdx.x;
     const double *f = G + (size_t)v * kKX * kGF;
     double lo = f[threadIdx.x], hi = lo;
     for (int i = threadIdx.x; i < kKX * kGF; i += blockDim.x) {
-        lo = fmin(lo, f[i]);
-        hi = fmax(hi, f[i]);
+        lo = nmin(lo, f[i]);
+        hi = nmax(hi, f[i]);
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
-        lo = fmin(lo, __shfl_xor(lo, o));
-        hi = fmax(hi, __shfl_xor(hi, o));
+        lo = nmin(lo, __shfl_xor(lo, o));
+        hi = nmax(hi, __shfl_xor(hi, o));
     }
     const int w = threadIdx.x >> 6;
     if ((threadIdx.x & 63) == 0) {
@@ -1430,8 +1441,8 @@ __global__ __launch_bounds__(1024) void k_io_minmax(const double *__restrict__ G
     __syncthreads();
     if (threadIdx.x == 0) {
         for (int i = 1; i < 16; ++i) {
-            lo = fmin(lo, smin[i]);
-            hi = fmax(hi, smax[i]);
+            lo = nmin(lo, smin[i]);
+            hi = nmax(hi, smax[i]);
         }
         mm[2 * v] = lo;
         mm[2 * v + 1] = hi;
@@ -1467,6 +1478,8 @@ extern "C" int sml_dyn_destroy(sml_dynamics *d) {
     }
     if (d->ev_fork) (void)hipEventDestroy(d->ev_fork);
     if (d->ev_chk) (void)hipEventDestroy(d->ev_chk);
+    if (d->ev_mm) (void)hipEventDestroy(d->ev_mm);
+    if (d->h_mm) (void)hipHostFree(d->h_mm);
     if (d->d_chk) (void)hipFree(d->d_chk);
     if (d->sp) sml_spectral_destroy(d->sp);
     delete d;
@@ -1945,8 +1958,20 @@ extern "C" int sml_dyn_from_grid(sml_dynamics *d, const double *d_grid4d, const 
     }
     if (int rc = spectral_gridy(d->sp, cs, cv, kNIo, cst)) return rc;
     if (int rc = spectral_gridx_range(d->sp, cv, cg, kNIo, 0, kNIoWind, cst)) return rc;
-    hipLaunchKernelGGL(k_io_minmax, dim3(4), dim3(1024), 0, cst, cg, d_minmax ? d_minmax : d->d_minmax);
+    double *mm = d_minmax ? d_minmax : d->d_minmax;
+    hipLaunchKernelGGL(k_io_minmax, dim3(4), dim3(1024), 0, cst, cg, mm);
     SML_HIP(hipGetLastError());
+    d->mm_last = mm;
+    d->mm_issued = false;
+    if (cst != st) {  // a host copy for sml_dyn_last_safe, behind the check on its stream
+        if (!d->h_mm) {
+            SML_HIP(hipHostMalloc((void **)&d->h_mm, 8 * sizeof(double), hipHostMallocDefault));
+            SML_HIP(hipEventCreateWithFlags(&d->ev_mm, hipEventDisableTiming));
+        }
+        SML_HIP(hipMemcpyAsync(d->h_mm, mm, 8 * sizeof(double), hipMemcpyDeviceToHost, cst));
+        SML_HIP(hipEventRecord(d->ev_mm, cst));
+        d->mm_issued = true;
+    }
     if (cst != st) {
         SML_HIP(hipEventRecord(d->ev_chk, cst));
         d->chk_pending = true;
@@ -1971,11 +1996,51 @@ extern "C" int sml_dyn_to_grid(sml_dynamics *d, double *d_grid4d, double *d_logp
 
 extern "C" int sml_dyn_is_safe(const double *minmax) {
     if (!minmax) return 0;
-    if (minmax[0] < -150.0 || minmax[1] > 150.0) return 0;  // u
-    if (minmax[2] < -120.0 || minmax[3] > 120.0) return 0;  // v
-    if (minmax[4] < 160.0 || minmax[5] > 330.0) return 0;   // t
-    if (minmax[6] < -6.0 || minmax[7] > 30.0) return 0;     // q
-    return 1;
+    return io_state_safe(minmax) ? 1 : 0;  // u, v, t, q thresholds (ppo_iogrid.f90:563-577)
+}
+
+// run_model (src/mpires.f90:1516-1628) on the device: agcm_main's window entry
+// iogrid(30) with its safety check, the window (integrated whatever the check says:
+// the outcome is selected at the exit), iogrid(31), then run_model's q floor; when
+// the entry state was unsafe agcm_main skipped the integration (at_gcm.f90:37) and
+// the forecast is the input grid (q floored).  The check runs beside the window on
+// the context's check stream; the exit waits for it.
+extern "C" int sml_dyn_run_model(sml_dynamics *d, const double *d_grid4d, const double *d_logp, int nleap,
+                                 double delt, double alph, double rob, double wil, double *d_fc4d, double *d_fc2d,
+                                 void *stream) {
+    SML_REQUIRE(d && d_grid4d && d_logp && d_fc4d && d_fc2d, "null argument");
+    SML_REQUIRE(d_fc4d != d_grid4d && d_fc2d != d_logp, "the forecast must not overwrite the window's input");
+    hipStream_t st = (hipStream_t)stream;
+    if (int rc = sml_dyn_from_grid(d, d_grid4d, d_logp, nullptr, stream)) return rc;
+    if (int rc = sml_dyn_window(d, nleap, delt, alph, rob, wil, stream)) return rc;
+    if (d->chk_pending) {  // the exit reads the check's min/max
+        SML_HIP(hipStreamWaitEvent(st, d->ev_chk, 0));
+        d->chk_pending = false;
+    }
+    hipLaunchKernelGGL(k_io_prep, dim3((kMN + 127) / 128, kKX), dim3(128), 0, st, d->d_state, d->d_specin, d->d_tab);
+    SML_HIP(hipGetLastError());
+    if (int rc = spectral_gridy(d->sp, d->d_specin, d->d_varm, kNIo, st)) return rc;
+    return spectral_gridx_run_model_exit(d->sp, d->d_varm, d_fc4d, d_fc2d, kNIoWind,
+                                         IoExit{0.000001, d->mm_last, d_grid4d, d_logp}, st);
+}
+
+// run_speedy of the last sml_dyn_from_grid / sml_dyn_run_model (is_safe_to_run_speedy,
+// broadcast as run_speedy, src/mpires.f90:721, 1623): waits only for that check
+extern "C" int sml_dyn_last_safe(sml_dynamics *d, int *safe, double *minmax) {
+    SML_REQUIRE(d && safe, "null argument");
+    double mm[8];
+    if (d->mm_issued) {
+        SML_HIP(hipEventSynchronize(d->ev_mm));
+        std::memcpy(mm, d->h_mm, sizeof mm);
+    } else if (d->mm_last) {  // issued on the caller's stream (capture): synchronous copy
+        SML_HIP(hipDeviceSynchronize());
+        SML_HIP(hipMemcpy(mm, d->mm_last, sizeof mm, hipMemcpyDeviceToHost));
+    } else {
+        return fail(SML_ERR_STATE, "sml_dyn_last_safe before any sml_dyn_from_grid");
+    }
+    *safe = sml_dyn_is_safe(mm);
+    if (minmax) std::memcpy(minmax, mm, sizeof mm);
+    return SML_OK;
 }
 
 extern "C" int sml_dyn_from_grid_host(sml_dynamics *d, const double *grid4d, const double *logp, double *minmax,

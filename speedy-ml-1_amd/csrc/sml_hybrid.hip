@@ -1,0 +1,475 @@
+// sml_hybrid.hip -- the hybrid prediction loop of one rank, native: reservoir predict
+// for the rank's regions, the outvec exchange (RCCL all-gather over xGMI), the
+// global grid assembly, SPEEDY's run_model on the GPU, and the re-tiling of the
+// next step's inputs.
+//
+// Reference: the time loop of src/parallelmain.f90:204-270 -- `predict` per region
+// (:225-234), `sendrecievegrid` (src/mpires.f90:218-780: outvecs gathered at the root
+// :338-430, assembled :300-478, `run_model` :549 -> :1516-1628, tiles scattered
+// :558-751, `run_speedy` broadcast :721), and the loop exit on run_speedy
+// (:268-270).  The startup communicator (startmpi, mpires.f90:21-37) becomes an RCCL
+// communicator (sml_comm).
+//
+// Schedule ("Overlap"): predict needs the feedback tiles for
+// the state update and for W_out(:, ncs+1:) x~, and SPEEDY's local vector only for
+// W_out(:, 1:ncs) local_model -- the split the reference computes under
+// outvec_component_contribs (mod_reservoir.f90:1456-1459).  With overlap on, the
+// update + v_ml readout (main stream) run while SPEEDY integrates the previous
+// step's window (side stream), on disjoint CUs; results are bit-identical to the
+// one-stream schedule.
+//
+//   main : begin(fb_t) .. wait(lm_t) finish_grid -> [all-gather] -> assemble -> tile fb_t+1
+//   side :   [run_model of step t-1 -> forecast grids]            wait(grid_t) run_model ..
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <algorithm>
+#include <new>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "sml_internal.hpp"
+
+using namespace sml;
+
+struct sml_comm {
+    ncclComm_t comm = nullptr;
+    int world = 1, rank = 0;
+};
+
+struct sml_hybrid {
+    sml_reservoirs *res = nullptr;
+    sml_dynamics *dyn = nullptr;
+    sml_comm *comm = nullptr;
+    int numregions = 0, nlocal = 0, ncs = 0, nout = 0;
+    int nleap = 24;
+    double delt = 900.0, alph = 0.5, rob = 0.05, wil = 0.53;
+    bool overlap = true;
+    hipStream_t main = nullptr, side = nullptr;
+    bool own_streams = false;
+    hipEvent_t ev_grid = nullptr, ev_lm = nullptr;
+    // caller-owned device buffers
+    double *fb = nullptr, *lm = nullptr, *ov = nullptr, *g4 = nullptr, *g2 = nullptr, *pr = nullptr, *f4 = nullptr,
+           *f2 = nullptr;
+    const double *tisr = nullptr;
+    // exchange staging (world > 1): send [maxc][nout], recv [world][maxc][nout],
+    // and the region-order permutation when the shares are uneven
+    int maxc = 0;
+    bool contiguous = true;
+    double *d_send = nullptr, *d_recv = nullptr, *d_glob = nullptr;
+    int32_t *d_perm = nullptr;
+    bool started = false, predicted = false, advanced = false;
+};
+
+namespace {
+
+const char *nccl_msg(ncclResult_t r) { return ncclGetErrorString(r); }
+
+#define SML_NCCL(expr)                                                                                       \
+    do {                                                                                                     \
+        ncclResult_t r_ = (expr);                                                                            \
+        if (r_ != ncclSuccess) return ::sml::fail(SML_ERR_HIP, "%s:%d %s: %s", __FILE__, __LINE__, #expr, nccl_msg(r_)); \
+    } while (0)
+
+// global region order from the all-gather's [rank][maxc] slabs
+__global__ void k_gather_rows(const double *__restrict__ recv, const int32_t *__restrict__ perm,
+                              double *__restrict__ glob, int nout, int total) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= total) return;
+    const int r = e / nout, o = e % nout;
+    glob[e] = recv[(size_t)perm[r] * nout + o];
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------- communicator
+extern "C" int sml_comm_unique_id(unsigned char *id) {
+    SML_REQUIRE(id, "null argument");
+    ncclUniqueId u;
+    SML_NCCL(ncclGetUniqueId(&u));
+    std::memcpy(id, u.internal, NCCL_UNIQUE_ID_BYTES);
+    return SML_OK;
+}
+
+extern "C" int sml_comm_create(int world, int rank, const unsigned char *id, sml_comm **out) {
+    SML_REQUIRE(out && world >= 1 && rank >= 0 && rank < world && id, "bad argument");
+    *out = nullptr;
+    sml_comm *c = new (std::nothrow) sml_comm();
+    if (!c) return fail(SML_ERR_NOMEM, "host allocation failed");
+    ncclUniqueId u;
+    std::memcpy(u.internal, id, NCCL_UNIQUE_ID_BYTES);
+    ncclResult_t r = ncclCommInitRank(&c->comm, world, u, rank);
+    if (r != ncclSuccess) {
+        delete c;
+        return fail(SML_ERR_HIP, "ncclCommInitRank(%d of %d): %s", rank, world, nccl_msg(r));
+    }
+    c->world = world;
+    c->rank = rank;
+    *out = c;
+    return SML_OK;
+}
+
+// rank 0 writes the unique id to `path` (atomically: temp file + rename), the other
+// ranks wait for it -- the rendezvous a host without MPI needs
+extern "C" int sml_comm_create_file(int world, int rank, const char *path, int timeout_s, sml_comm **out) {
+    SML_REQUIRE(out && path && world >= 1 && rank >= 0 && rank < world, "bad argument");
+    unsigned char id[NCCL_UNIQUE_ID_BYTES];
+    if (rank == 0) {
+        if (int rc = sml_comm_unique_id(id)) return rc;
+        std::string tmp = std::string(path) + ".tmp";
+        FILE *f = std::fopen(tmp.c_str(), "wb");
+        if (!f) return fail(SML_ERR_IO, "cannot write %s", tmp.c_str());
+        const size_t w = std::fwrite(id, 1, sizeof id, f);
+        std::fclose(f);
+        if (w != sizeof id || std::rename(tmp.c_str(), path) != 0) return fail(SML_ERR_IO, "cannot publish %s", path);
+    } else {
+        const auto t0 = std::chrono::steady_clock::now();
+        for (;;) {
+            FILE *f = std::fopen(path, "rb");
+            if (f) {
+                const size_t r = std::fread(id, 1, sizeof id, f);
+                std::fclose(f);
+                if (r == sizeof id) break;
+            }
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(timeout_s > 0 ? timeout_s : 60))
+                return fail(SML_ERR_IO, "timed out waiting for %s", path);
+            std::this_thread::sleep_for(std::chrono::milliseconds(20));
+        }
+    }
+    return sml_comm_create(world, rank, id, out);
+}
+
+extern "C" int sml_comm_destroy(sml_comm *c) {
+    if (!c) return SML_OK;
+    if (c->comm) (void)ncclCommDestroy(c->comm);
+    delete c;
+    return SML_OK;
+}
+
+extern "C" int sml_comm_rank(const sml_comm *c, int *world, int *rank) {
+    SML_REQUIRE(c, "null communicator");
+    if (world) *world = c->world;
+    if (rank) *rank = c->rank;
+    return SML_OK;
+}
+
+extern "C" int sml_comm_allgather(sml_comm *c, const double *d_send, double *d_recv, int64_t count, void *stream) {
+    SML_REQUIRE(c && d_send && d_recv && count >= 0, "bad argument");
+    SML_NCCL(ncclAllGather(d_send, d_recv, (size_t)count, ncclDouble, c->comm, (hipStream_t)stream));
+    return SML_OK;
+}
+
+// ------------------------------------------------------------------ hybrid loop
+extern "C" int sml_hybrid_destroy(sml_hybrid *h) {
+    if (!h) return SML_OK;
+    if (h->main) (void)hipStreamSynchronize(h->main);
+    if (h->side) (void)hipStreamSynchronize(h->side);
+    if (h->own_streams) {
+        if (h->side && h->side != h->main) (void)hipStreamDestroy(h->side);
+        if (h->main) (void)hipStreamDestroy(h->main);
+    }
+    if (h->ev_grid) (void)hipEventDestroy(h->ev_grid);
+    if (h->ev_lm) (void)hipEventDestroy(h->ev_lm);
+    void *ptrs[] = {h->d_send, h->d_recv, h->d_glob, h->d_perm};
+    for (void *p : ptrs)
+        if (p) (void)hipFree(p);
+    delete h;
+    return SML_OK;
+}
+
+extern "C" int sml_hybrid_create(sml_reservoirs *res, sml_dynamics *dyn, sml_comm *comm, int nleap, double delt,
+                                 double alph, double rob, double wil, int overlap, int speedy_cus, sml_hybrid **out) {
+    SML_REQUIRE(out && res && dyn && nleap >= 0 && delt > 0.0, "bad argument");
+    *out = nullptr;
+    sml_hybrid *h = new (std::nothrow) sml_hybrid();
+    if (!h) return fail(SML_ERR_NOMEM, "host allocation failed");
+    auto bail = [&](int rc) {
+        sml_hybrid_destroy(h);
+        return rc;
+    };
+    h->res = res;
+    h->dyn = dyn;
+    h->comm = comm;
+    h->nleap = nleap;
+    h->delt = delt;
+    h->alph = alph;
+    h->rob = rob;
+    h->wil = wil;
+    h->overlap = overlap != 0;
+    if (int rc = sml_res_info(res, &h->numregions, &h->nlocal, &h->ncs, &h->nout, nullptr)) return bail(rc);
+    const int world = comm ? comm->world : 1, rank = comm ? comm->rank : 0;
+    // the communicator's decomposition must be the one the reservoir context holds
+    std::vector<int> mine(h->numregions), ids(h->nlocal);
+    const int cnt = processor_regions(h->numregions, world, rank, mine.data());
+    if (int rc = sml_res_info(res, nullptr, nullptr, nullptr, nullptr, ids.data())) return bail(rc);
+    // (without a communicator any subset is accepted for predict / advance around a
+    // host exchange; sml_hybrid_step then needs every region local)
+    if (comm && (cnt != h->nlocal || !std::equal(ids.begin(), ids.end(), mine.begin())))
+        return bail(fail(SML_ERR_ARG, "the reservoir context does not hold rank %d of %d's processor_decomposition",
+                         rank, world));
+    int dev = 0, ncu = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        return bail(fail(SML_ERR_HIP, "no device"));
+    // streams: non-default (the legacy NULL stream would serialise the two chains);
+    // with overlap and 0 < speedy_cus < CUs, SPEEDY's chain gets CUs [0, speedy_cus)
+    // and the reservoir the rest (sml_stream_create_cu_range)
+    h->own_streams = true;
+    if (h->overlap && speedy_cus > 0 && speedy_cus < ncu) {
+        void *s = nullptr, *m = nullptr;
+        if (int rc = sml_stream_create_cu_range(0, speedy_cus, &s)) return bail(rc);
+        h->side = (hipStream_t)s;
+        if (int rc = sml_stream_create_cu_range(speedy_cus, ncu - speedy_cus, &m)) return bail(rc);
+        h->main = (hipStream_t)m;
+        if (int rc = sml_res_set_read_waves(res, 0)) return bail(rc);  // pacing pays only on shared CUs
+    } else {
+        if (hipStreamCreateWithFlags(&h->main, hipStreamNonBlocking) != hipSuccess)
+            return bail(fail(SML_ERR_HIP, "stream"));
+        if (h->overlap) {
+            int lo = 0, hi = 0;
+            (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
+            if (hipStreamCreateWithPriority(&h->side, hipStreamNonBlocking, hi) != hipSuccess)
+                return bail(fail(SML_ERR_HIP, "stream"));
+        } else {
+            h->side = h->main;
+        }
+    }
+    if (hipEventCreateWithFlags(&h->ev_grid, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&h->ev_lm, hipEventDisableTiming) != hipSuccess)
+        return bail(fail(SML_ERR_HIP, "event"));
+    if (world > 1) {
+        std::vector<int> all(h->numregions);
+        std::vector<int32_t> perm(h->numregions, -1);
+        h->maxc = 0;
+        std::vector<int> counts(world);
+        for (int r = 0; r < world; ++r) {
+            counts[r] = processor_regions(h->numregions, world, r, all.data());
+            h->maxc = std::max(h->maxc, counts[r]);
+        }
+        h->contiguous = true;
+        for (int r = 0; r < world; ++r) {
+            const int c = processor_regions(h->numregions, world, r, all.data());
+            if (c != counts[0]) h->contiguous = false;
+            for (int i = 0; i < c; ++i) {
+                perm[all[i]] = r * h->maxc + i;
+                if (all[i] != r * counts[0] + i) h->contiguous = false;
+            }
+        }
+        const size_t nout = h->nout;
+        if (hipMalloc(&h->d_send, (size_t)h->maxc * nout * 8) != hipSuccess ||
+            hipMalloc(&h->d_recv, (size_t)world * h->maxc * nout * 8) != hipSuccess ||
+            hipMemset(h->d_send, 0, (size_t)h->maxc * nout * 8) != hipSuccess)
+            return bail(fail(SML_ERR_NOMEM, "exchange buffers"));
+        if (!h->contiguous) {
+            if (hipMalloc(&h->d_glob, (size_t)h->numregions * nout * 8) != hipSuccess ||
+                hipMalloc(&h->d_perm, (size_t)h->numregions * 4) != hipSuccess ||
+                hipMemcpy(h->d_perm, perm.data(), perm.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
+                return bail(fail(SML_ERR_NOMEM, "exchange buffers"));
+        }
+    }
+    *out = h;
+    return SML_OK;
+}
+
+extern "C" int sml_hybrid_set_buffers(sml_hybrid *h, double *d_feedback, double *d_local_model, double *d_outvec,
+                                      double *d_grid4d, double *d_grid2d, double *d_precip, double *d_fc4d,
+                                      double *d_fc2d, const double *d_tisr) {
+    SML_REQUIRE(h && d_feedback && d_outvec && d_grid4d && d_grid2d && d_precip && d_fc4d && d_fc2d,
+                "null buffer");
+    SML_REQUIRE(h->ncs == 0 || d_local_model, "a hybrid context needs d_local_model");
+    h->fb = d_feedback;
+    h->lm = d_local_model;
+    h->ov = d_outvec;
+    h->g4 = d_grid4d;
+    h->g2 = d_grid2d;
+    h->pr = d_precip;
+    h->f4 = d_fc4d;
+    h->f2 = d_fc2d;
+    h->tisr = d_tisr;
+    return SML_OK;
+}
+
+extern "C" int sml_hybrid_set_tisr(sml_hybrid *h, const double *d_tisr) {
+    SML_REQUIRE(h, "null context");
+    h->tisr = d_tisr;
+    return SML_OK;
+}
+
+extern "C" int sml_hybrid_streams(const sml_hybrid *h, void **main, void **side) {
+    SML_REQUIRE(h, "null context");
+    if (main) *main = h->main;
+    if (side) *side = h->side;
+    return SML_OK;
+}
+
+// start_prediction's hand-over (src/mod_reservoir.f90:938-959, parallelmain.f90:207-216):
+// the first step's feedback tiles from an analysis grid and the local model from a
+// SPEEDY forecast of it, both copied into the loop's buffers (on the main stream,
+// ordered after the caller's legacy-stream work)
+extern "C" int sml_hybrid_start(sml_hybrid *h, const double *d_g4, const double *d_g2, const double *d_pr,
+                                const double *d_f4, const double *d_f2) {
+    SML_REQUIRE(h && h->fb, "sml_hybrid_set_buffers first");
+    SML_REQUIRE(d_g4 && d_g2 && d_pr && d_f4 && d_f2, "null argument");
+    SML_HIP(hipDeviceSynchronize());
+    const size_t n4 = (size_t)kGrid4d * 8, n2 = (size_t)kGrid2d * 8;
+    if (d_g4 != h->g4) SML_HIP(hipMemcpyAsync(h->g4, d_g4, n4, hipMemcpyDeviceToDevice, h->main));
+    if (d_g2 != h->g2) SML_HIP(hipMemcpyAsync(h->g2, d_g2, n2, hipMemcpyDeviceToDevice, h->main));
+    if (d_pr != h->pr) SML_HIP(hipMemcpyAsync(h->pr, d_pr, n2, hipMemcpyDeviceToDevice, h->main));
+    if (d_f4 != h->f4) SML_HIP(hipMemcpyAsync(h->f4, d_f4, n4, hipMemcpyDeviceToDevice, h->main));
+    if (d_f2 != h->f2) SML_HIP(hipMemcpyAsync(h->f2, d_f2, n2, hipMemcpyDeviceToDevice, h->main));
+    if (int rc = sml_res_tile_inputs(h->res, h->g4, h->g2, h->pr, h->f4, h->f2, h->tisr, h->fb, h->lm, h->main))
+        return rc;
+    SML_HIP(hipEventRecord(h->ev_lm, h->main));
+    h->started = true;
+    h->predicted = h->advanced = false;
+    return SML_OK;
+}
+
+// predict for every local region (parallelmain.f90:225-234): the local outvecs in
+// d_outvec on the main stream
+extern "C" int sml_hybrid_predict(sml_hybrid *h) {
+    SML_REQUIRE(h, "null context");
+    if (!h->started) return fail(SML_ERR_STATE, "sml_hybrid_start first");
+    if (h->predicted) return fail(SML_ERR_STATE, "sml_hybrid_predict twice without sml_hybrid_advance");
+    if (h->overlap) {
+        if (int rc = sml_res_step_begin(h->res, h->fb, h->main)) return rc;
+        SML_HIP(hipStreamWaitEvent(h->main, h->ev_lm, 0));  // SPEEDY's forecast of the previous window
+        // the local-model tiling fused into the v_p finish: one launch fewer on the critical path
+        if (int rc = sml_res_step_finish_grid(h->res, h->f4, h->f2, h->lm, h->ov, h->main)) return rc;
+    } else {  // one pass over W_out: the same sums as begin + finish
+        if (int rc = sml_res_step(h->res, h->fb, h->lm, h->ov, h->main)) return rc;
+    }
+    h->predicted = true;
+    return SML_OK;
+}
+
+// sendrecievegrid's assembly + run_model + re-tiling (mpires.f90:300-751) from the
+// outvecs of every region in global region order ([numregions][nout], device)
+extern "C" int sml_hybrid_advance(sml_hybrid *h, const double *d_outvec_all) {
+    SML_REQUIRE(h && d_outvec_all, "null argument");
+    if (!h->predicted) return fail(SML_ERR_STATE, "sml_hybrid_advance without sml_hybrid_predict");
+    hipStream_t m = h->main, s = h->side;
+    if (int rc = sml_exchange_assemble(h->res, d_outvec_all, h->g4, h->g2, h->pr, m)) return rc;
+    if (h->overlap) SML_HIP(hipEventRecord(h->ev_grid, m));
+    if (int rc = sml_res_tile_feedback(h->res, h->g4, h->g2, h->pr, h->tisr, h->fb, m)) return rc;
+    if (h->overlap) SML_HIP(hipStreamWaitEvent(s, h->ev_grid, 0));
+    if (int rc = sml_dyn_run_model(h->dyn, h->g4, h->g2, h->nleap, h->delt, h->alph, h->rob, h->wil, h->f4, h->f2, s))
+        return rc;
+    if (h->overlap) {
+        SML_HIP(hipEventRecord(h->ev_lm, s));
+    } else if (h->ncs) {
+        if (int rc = sml_res_tile_local_model(h->res, h->f4, h->f2, h->lm, s)) return rc;
+    }
+    h->predicted = false;
+    h->advanced = true;
+    return SML_OK;
+}
+
+// one hybrid step with the loop's own exchange: identity on one rank, else the
+// all-gather of every rank's outvec slab (RCCL over xGMI) on the main stream
+extern "C" int sml_hybrid_step(sml_hybrid *h) {
+    SML_REQUIRE(h, "null context");
+    if (int rc = sml_hybrid_predict(h)) return rc;
+    const int world = h->comm ? h->comm->world : 1;
+    if (world == 1) {
+        if (h->nlocal != h->numregions)
+            return fail(SML_ERR_STATE, "one rank holds %d of %d regions: exchange through sml_hybrid_advance",
+                        h->nlocal, h->numregions);
+        return sml_hybrid_advance(h, h->ov);
+    }
+    const size_t slab = (size_t)h->maxc * h->nout;
+    SML_HIP(hipMemcpyAsync(h->d_send, h->ov, (size_t)h->nlocal * h->nout * 8, hipMemcpyDeviceToDevice, h->main));
+    if (int rc = sml_comm_allgather(h->comm, h->d_send, h->d_recv, (int64_t)slab, h->main)) return rc;
+    const double *glob = h->d_recv;
+    if (!h->contiguous) {
+        const int total = h->numregions * h->nout;
+        hipLaunchKernelGGL(k_gather_rows, dim3((total + 255) / 256), dim3(256), 0, h->main, h->d_recv, h->d_perm,
+                           h->d_glob, h->nout, total);
+        SML_HIP(hipGetLastError());
+        glob = h->d_glob;
+    }
+    return sml_hybrid_advance(h, glob);
+}
+
+// run_speedy after the last advance (mpires.f90:721, :1623): 0 ends the prediction
+// (parallelmain.f90:268-270).  Waits for that step's safety check only.
+extern "C" int sml_hybrid_run_speedy(sml_hybrid *h, int *run) {
+    SML_REQUIRE(h && run, "null argument");
+    if (!h->advanced) {
+        *run = 1;
+        return SML_OK;
+    }
+    return sml_dyn_last_safe(h->dyn, run, nullptr);
+}
+
+// wait for every issued step; the local model of the last window is tiled as the
+// one-stream loop leaves it (the overlapped loop tiles it inside the next finish)
+extern "C" int sml_hybrid_sync(sml_hybrid *h) {
+    SML_REQUIRE(h, "null context");
+    if (h->overlap && h->advanced && h->ncs) {
+        SML_HIP(hipStreamWaitEvent(h->main, h->ev_lm, 0));
+        if (int rc = sml_res_tile_local_model(h->res, h->f4, h->f2, h->lm, h->main)) return rc;
+    }
+    SML_HIP(hipStreamSynchronize(h->main));
+    SML_HIP(hipStreamSynchronize(h->side));
+    return SML_OK;
+}
+
+// ------------------------------------------------------------- device memory
+// plumbing for hosts without a GPU runtime binding of their own (the Fortran host):
+// zeroed device allocations and synchronous copies
+extern "C" int sml_device_alloc(int64_t bytes, void **d_ptr) {
+    SML_REQUIRE(d_ptr && bytes >= 0, "bad argument");
+    *d_ptr = nullptr;
+    SML_HIP(hipMalloc(d_ptr, bytes > 0 ? (size_t)bytes : 16));
+    SML_HIP(hipMemset(*d_ptr, 0, bytes > 0 ? (size_t)bytes : 16));
+    return SML_OK;
+}
+
+extern "C" int sml_device_free(void *d_ptr) {
+    if (d_ptr) SML_HIP(hipFree(d_ptr));
+    return SML_OK;
+}
+
+extern "C" int sml_copy_to_device(void *d_dst, const void *src, int64_t bytes) {
+    SML_REQUIRE(d_dst && src && bytes >= 0, "bad argument");
+    SML_HIP(hipDeviceSynchronize());
+    SML_HIP(hipMemcpy(d_dst, src, (size_t)bytes, hipMemcpyHostToDevice));
+    return SML_OK;
+}
+
+extern "C" int sml_copy_to_host(void *dst, const void *d_src, int64_t bytes) {
+    SML_REQUIRE(dst && d_src && bytes >= 0, "bad argument");
+    SML_HIP(hipDeviceSynchronize());
+    SML_HIP(hipMemcpy(dst, d_src, (size_t)bytes, hipMemcpyDeviceToHost));
+    return SML_OK;
+}
+
+// region geometry of the res_domain decomposition (getxyresextent, getoverlapindices;
+// res_domain.f90:123-204), 1-based like the reference:
+// g[12] = res_xstart, res_xend, res_ystart, res_yend, resx, resy, in_xstart, in_xend,
+//         in_ystart, in_yend, inx, iny
+extern "C" int sml_region_geometry(int numregions, int region, int *g) {
+    SML_REQUIRE(g, "null argument");
+    RegionGeom r;
+    SML_REQUIRE(region_geom(numregions, region, &r), "region %d of %d does not decompose the grid", region,
+                numregions);
+    const int v[12] = {r.res_xstart, r.res_xend, r.res_ystart, r.res_yend, r.resx, r.resy,
+                       r.in_xstart,  r.in_xend,  r.in_ystart,  r.in_yend,  r.inx,  r.iny};
+    std::memcpy(g, v, sizeof v);
+    return SML_OK;
+}
+
+// processor_decomposition (res_domain.f90:31-62): the regions (0-based) rank irank of
+// numprocs owns; returns their count in *count (regions may be NULL to ask only)
+extern "C" int sml_processor_decomposition(int numregions, int numprocs, int irank, int *regions, int *count) {
+    SML_REQUIRE(count && numregions > 0 && numprocs > 0 && irank >= 0 && irank < numprocs, "bad argument");
+    std::vector<int> r(numregions);
+    *count = processor_regions(numregions, numprocs, irank, r.data());
+    if (regions) std::memcpy(regions, r.data(), sizeof(int) * *count);
+    return SML_OK;
+}

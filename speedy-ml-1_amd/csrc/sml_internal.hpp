@@ -107,6 +107,17 @@ inline int region_ninp(const RegionGeom &g, bool sst) {
     return kVars * in2d * kZGrid + in2d + in2d + (sst ? in2d : 0) + in2d;
 }
 
+// processor_decomposition (res_domain.f90:31-62): the regions rank irank of numprocs
+// owns -- a contiguous block of numregions/numprocs, and for ranks 1..left one of the
+// `left` leftover regions at the end (0-based region numbers)
+inline int processor_regions(int numregions, int numprocs, int irank, int *out) {
+    const int per = numregions / numprocs, left = numregions % numprocs;
+    int c = 0;
+    for (int i = 0; i < per; ++i) out[c++] = per * irank + i;
+    if (irank > 0 && irank <= left) out[c++] = numregions - left + irank - 1;
+    return c;
+}
+
 // grid4d(4,96,48,8) column-major index, 0-based arguments
 inline int g4(int v, int x, int y, int z) { return v + kVars * (x + kXGrid * (y + kYGrid * z)); }
 inline int g2(int x, int y) { return x + kXGrid * y; }

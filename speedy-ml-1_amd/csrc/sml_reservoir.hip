@@ -74,7 +74,8 @@ struct sml_reservoirs {
     void *d_wlm = nullptr;
     int64_t tot_a_rp = 0, tot_a_nz = 0, tot_w_rp = 0, tot_w_nz = 0, tot_wout = 0, tot_x = 0, tot_xaug = 0,
             tot_fb = 0;
-    std::vector<int64_t> w_nz_cap;  // reserved W_in nnz per region (n, grows on reload)
+    std::vector<int64_t> w_nz_cap;  // reserved W_in CSR nnz per region (n at create: one entry per row as
+                                    // trained; grow_win_pool re-lays the pool for a denser W_in)
     int maxn = 0, maxninp = 0;
     int device = 0;
     // device buffers
@@ -681,6 +682,45 @@ bool narrow(const S *src, size_t count, std::vector<D> &out) {
     return true;
 }
 
+// W_in's CSR pool holds n entries per region at create (the trained W_in has one
+// entry per row, mod_reservoir.f90:260-278).  A denser W_in -- up to the dense
+// win(n, ninp) of the reference's matmul (:1443) -- re-lays the pool: region i gets
+// room for wnz entries, the other regions' entries move device to device, every
+// region's offset is re-uploaded.  The ELL copy stays one slot per row: such a region
+// is read from the CSR form.
+int grow_win_pool(sml_reservoirs *c, int i, int64_t wnz) {
+    const size_t wb = wbytes(c);
+    std::vector<int64_t> off(c->nlocal);
+    int64_t tot = 0;
+    for (int j = 0; j < c->nlocal; ++j) {
+        off[j] = tot;
+        tot += (j == i) ? wnz : c->w_nz_cap[j];
+    }
+    uint16_t *col = nullptr;
+    void *val = nullptr;
+    if (int rc = dalloc(&col, tot)) return rc;
+    if (int rc = dalloc_bytes(&val, tot * wb)) {
+        (void)hipFree(col);
+        return rc;
+    }
+    SML_HIP(hipDeviceSynchronize());  // steps in flight read the old pool
+    for (int j = 0; j < c->nlocal; ++j) {
+        if (j == i || !c->loaded[j] || c->w_nz_cap[j] == 0) continue;
+        SML_HIP(hipMemcpy(col + off[j], c->d_w_col + c->rd[j].w_nz, c->w_nz_cap[j] * 2, hipMemcpyDeviceToDevice));
+        SML_HIP(hipMemcpy((char *)val + off[j] * wb, (char *)c->d_w_val + c->rd[j].w_nz * wb, c->w_nz_cap[j] * wb,
+                          hipMemcpyDeviceToDevice));
+    }
+    SML_HIP(hipFree(c->d_w_col));
+    SML_HIP(hipFree(c->d_w_val));
+    c->d_w_col = col;
+    c->d_w_val = val;
+    c->w_nz_cap[i] = wnz;
+    c->tot_w_nz = tot;
+    for (int j = 0; j < c->nlocal; ++j) c->rd[j].w_nz = off[j];
+    SML_HIP(hipMemcpy(c->d_rd, c->rd.data(), sizeof(RegionDev) * c->nlocal, hipMemcpyHostToDevice));
+    return SML_OK;
+}
+
 template <typename SrcT, typename StoT>
 int load_region_impl(sml_reservoirs *c, int i, const int *rows, const int *cols, const SrcT *vals, const SrcT *win,
                      const SrcT *wout, const double *mean, const double *std) {
@@ -710,10 +750,8 @@ int load_region_impl(sml_reservoirs *c, int i, const int *rows, const int *cols,
             if (win[(size_t)col * n + r] != (SrcT)0) wrp[r + 1]++;
     for (int r = 0; r < n; ++r) wrp[r + 1] += wrp[r];
     const int64_t wnz = wrp[n];
-    SML_REQUIRE(wnz <= c->w_nz_cap[i],
-                "region %d: W_in has %lld nonzeros, more than the %lld reserved (one per row as trained; "
-                "dense W_in is supported through sml_res_create of a fresh context)",
-                i, (long long)wnz, (long long)c->w_nz_cap[i]);
+    if (wnz > c->w_nz_cap[i])  // a W_in denser than trained (up to the dense n x ninp matmul, :1443)
+        if (int rc = grow_win_pool(c, i, wnz)) return rc;
     std::vector<int32_t> wfill(wrp.begin(), wrp.end() - 1);
     std::vector<uint16_t> wcol(wnz);
     std::vector<StoT> wval(wnz);
@@ -950,6 +988,17 @@ extern "C" int sml_res_create(int numregions, int nlocal, const int *region_ids,
     return SML_OK;
 }
 
+extern "C" int sml_res_info(const sml_reservoirs *c, int *numregions, int *nlocal, int *chunk_speedy, int *nout,
+                            int *region_ids) {
+    SML_REQUIRE(c, "null context");
+    if (numregions) *numregions = c->numregions;
+    if (nlocal) *nlocal = c->nlocal;
+    if (chunk_speedy) *chunk_speedy = c->ncs;
+    if (nout) *nout = c->nout;
+    if (region_ids) std::memcpy(region_ids, c->region_ids.data(), sizeof(int) * c->nlocal);
+    return SML_OK;
+}
+
 extern "C" int sml_res_ninp(const sml_reservoirs *c, int i, int *ninp) {
     if (int rc = check_region(c, i)) return rc;
     SML_REQUIRE(ninp, "ninp is null");
@@ -1158,7 +1207,7 @@ extern "C" int sml_res_step_finish_grid(sml_reservoirs *c, const double *d_fc4d,
                                         double *d_local_model, double *d_outvec, void *stream) {
     SML_REQUIRE(c, "null context");
     if (c->nlocal == 0) return SML_OK;
-    SML_REQUIRE(d_outvec && d_fc4d && d_fc2d, "null device buffer");
+    SML_REQUIRE(d_outvec && (c->ncs == 0 || (d_fc4d && d_fc2d)), "null device buffer");
     SML_REQUIRE(c->ncs <= kMaxNcs, "ncs %d exceeds %d", c->ncs, kMaxNcs);
     if (!c->begun) return fail(SML_ERR_STATE, "sml_res_step_finish_grid without sml_res_step_begin");
     hipStream_t st = (hipStream_t)stream;

@@ -27,6 +27,7 @@
 
 #include "sml_fft.hpp"
 #include "sml_dynamics_tables.hpp"  // (+ sml_spectral_tables.hpp): kx for the iogrid exit layout
+#include "sml_spectral_internal.hpp"  // IoExit, io_state_safe
 
 using namespace sml;
 
@@ -112,11 +113,12 @@ constexpr int kFftThreads = 64;
 // fvar(m-1) = varm(m) for m = 3..mx2, 0 beyond; rfftb; x cosgr(j) for kcos = 2 (the
 // fields c0 <= f < c1).  With g4 set, the 33 fields [u v t q (kx each) | ps] go
 // straight into iogrid(31)'s variables3d(4, ix, il, kx) (var = T, u, v, q) and logp
-// instead of grid (ppo_iogrid.f90:590-595)
+// instead of grid (ppo_iogrid.f90:590-595); ex.mm set: run_model's exit on top
+// (sml_spectral_internal.hpp IoExit: q floor, the unsafe window's pass-through)
 __global__ __launch_bounds__(kFftThreads) void k_gridx(const double *__restrict__ varm, double *__restrict__ grid,
                                                        const double *__restrict__ wa, const double *__restrict__ cosgr,
                                                        int nf, int c0, int c1, double *__restrict__ g4,
-                                                       double *__restrict__ logp) {
+                                                       double *__restrict__ logp, IoExit ex) {
     __shared__ double was[kFftWa];  // twiddles: LDS broadcast reads inside the FFT
     if (threadIdx.x < kFftWa) was[threadIdx.x] = wa[threadIdx.x];
     if (threadIdx.x + kFftThreads < kFftWa) was[threadIdx.x + kFftThreads] = wa[threadIdx.x + kFftThreads];
@@ -138,12 +140,33 @@ __global__ __launch_bounds__(kFftThreads) void k_gridx(const double *__restrict_
     int gs = 1;
     if (g4) {
         const int grp = f / kKX, k = f % kKX;
+        size_t o;
         if (grp < 4) {
             const int var = grp == 0 ? 1 : grp == 1 ? 2 : grp == 2 ? 0 : 3;
-            g = g4 + var + 4 * ((size_t)kGridField * k + j * kIX);
+            o = var + 4 * ((size_t)kGridField * k + j * kIX);
+            g = g4 + o;
             gs = 4;
         } else {
-            g = logp + j * kIX;
+            o = (size_t)j * kIX;
+            g = logp + o;
+        }
+        if (ex.mm) {  // run_model's exit (uniform across the launch: every thread reads the same flag)
+            const bool q = grp == 3;
+            if (!io_state_safe(ex.mm)) {  // integration skipped: the input grid comes back
+                const double *src = grp < 4 ? ex.in4 + o : ex.inlp + o;
+#pragma unroll
+                for (int e = 0; e < kFftN; ++e) {
+                    const double v = src[e * gs];
+                    g[e * gs] = (q && v < ex.qfloor) ? ex.qfloor : v;
+                }
+                return;
+            }
+#pragma unroll
+            for (int e = 0; e < kFftN; ++e) {
+                const double v = k2 ? x[e] * cj : x[e];
+                g[e * gs] = (q && v < ex.qfloor) ? ex.qfloor : v;
+            }
+            return;
         }
     }
 #pragma unroll
@@ -439,7 +462,7 @@ extern "C" int sml_gridx_batched(sml_spectral *s, const double *d_varm, double *
     if (int rc = check_ctx(s, nf)) return rc;
     if (nf == 0) return SML_OK;
     hipLaunchKernelGGL(k_gridx, dim3((nf * kIL + kFftThreads - 1) / kFftThreads), dim3(kFftThreads), 0, (hipStream_t)stream,
-                       d_varm, d_grid, s->d_wa, s->d_cosgr, nf, kcos == 1 ? nf : 0, nf, nullptr, nullptr);
+                       d_varm, d_grid, s->d_wa, s->d_cosgr, nf, kcos == 1 ? nf : 0, nf, nullptr, nullptr, IoExit{});
     SML_HIP(hipGetLastError());
     return SML_OK;
 }
@@ -591,15 +614,20 @@ int spectral_gridx_split(sml_spectral *s, const double *varm, double *grid, int 
 int spectral_gridx_range(sml_spectral *s, const double *varm, double *grid, int nf, int c0, int c1, hipStream_t st) {
     if (nf <= 0) return SML_OK;
     hipLaunchKernelGGL(k_gridx, dim3((nf * kIL + kFftThreads - 1) / kFftThreads), dim3(kFftThreads), 0, st, varm, grid, s->d_wa,
-                       s->d_cosgr, nf, c0, c1, nullptr, nullptr);
+                       s->d_cosgr, nf, c0, c1, nullptr, nullptr, IoExit{});
     SML_HIP(hipGetLastError());
     return SML_OK;
 }
 
 int spectral_gridx_io(sml_spectral *s, const double *varm, double *g4, double *logp, int nwind, hipStream_t st) {
+    return spectral_gridx_run_model_exit(s, varm, g4, logp, nwind, IoExit{}, st);
+}
+
+int spectral_gridx_run_model_exit(sml_spectral *s, const double *varm, double *g4, double *logp, int nwind,
+                                  IoExit ex, hipStream_t st) {
     constexpr int nf = 4 * kKX + 1;
     hipLaunchKernelGGL(k_gridx, dim3((nf * kIL + kFftThreads - 1) / kFftThreads), dim3(kFftThreads), 0, st, varm, nullptr,
-                       s->d_wa, s->d_cosgr, nf, 0, nwind, g4, logp);
+                       s->d_wa, s->d_cosgr, nf, 0, nwind, g4, logp, ex);
     SML_HIP(hipGetLastError());
     return SML_OK;
 }

@@ -35,6 +35,29 @@ int spectral_gridx_range(sml_spectral *s, const double *varm, double *grid, int 
 int spectral_specx_io(sml_spectral *s, const double *g4, const double *logp, double *varm, int nwind,
                       hipStream_t st);
 int spectral_gridx_io(sml_spectral *s, const double *varm, double *g4, double *logp, int nwind, hipStream_t st);
+
+// run_model's exit (src/mpires.f90:1605-1628) around iogrid(31): the forecast's q is
+// floored at 1e-6 (:1614-1616), and when iogrid(30)'s safety check failed agcm_main
+// skipped the integration (at_gcm.f90:37), so the forecast is run_model's copy of
+// its input grid, q floored the same way (:1550-1553, :1586).  mm: the 8 min/max
+// values of the check (device); in4 / inlp: the window's input grids.
+struct IoExit {
+    double qfloor;
+    const double *mm, *in4, *inlp;
+};
+int spectral_gridx_run_model_exit(sml_spectral *s, const double *varm, double *g4, double *logp, int nwind,
+                                  IoExit ex, hipStream_t st);
+
+// is_safe_to_run_speedy from the re-gridded entry state's min/max (ppo_iogrid.f90:
+// 563-577; thresholds u +-150, v +-120, t 160..330, q -6..30).  A NaN anywhere makes
+// the state unsafe (the reference's minval/maxval with NaN are processor-dependent
+// under -ffast-math; stopping is the conservative reading).
+__host__ __device__ inline bool io_state_safe(const double *mm) {
+    const double lo[4] = {-150.0, -120.0, 160.0, -6.0}, hi[4] = {150.0, 120.0, 330.0, 30.0};
+    for (int v = 0; v < 4; ++v)
+        if (!(mm[2 * v] >= lo[v]) || !(mm[2 * v + 1] <= hi[v])) return false;
+    return true;
+}
 // scale: 0 none, 1 x cosgr(lat), 2 x cosgr2(lat) (vdspec's prescaling)
 int spectral_specx(sml_spectral *s, const double *grid, double *varm, int nf, int scale, hipStream_t st);
 // one launch: the first nscaled fields x cosgr(lat) (vdspec kcos = 2), the rest plain

@@ -42,6 +42,14 @@ EXPORTED = (
     "sml_train_create", "sml_train_destroy", "sml_train_reset", "sml_train_accumulate", "sml_train_solve",
     "sml_train_npad", "sml_train_get_gram", "sml_probe_mfma_f64",
     "sml_stream_create_cu_range", "sml_stream_destroy",
+    "sml_dyn_run_model", "sml_dyn_last_safe", "sml_res_info",
+    "sml_comm_unique_id", "sml_comm_create", "sml_comm_create_file", "sml_comm_destroy", "sml_comm_rank",
+    "sml_comm_allgather",
+    "sml_hybrid_create", "sml_hybrid_destroy", "sml_hybrid_set_buffers", "sml_hybrid_set_tisr",
+    "sml_hybrid_streams", "sml_hybrid_start", "sml_hybrid_predict", "sml_hybrid_advance", "sml_hybrid_step",
+    "sml_hybrid_run_speedy", "sml_hybrid_sync",
+    "sml_device_alloc", "sml_device_free", "sml_copy_to_device", "sml_copy_to_host", "sml_region_geometry",
+    "sml_processor_decomposition",
 )
 
 
@@ -79,6 +87,7 @@ def check(rc: int) -> None:
 def _declare(L: ctypes.CDLL) -> None:
     vp, i, d, i64p = ctypes.c_void_p, ctypes.c_int, ctypes.c_double, ctypes.POINTER(ctypes.c_int64)
     pp = ctypes.POINTER(ctypes.c_void_p)
+    ip = ctypes.POINTER(ctypes.c_int)
     L.sml_last_error.restype = ctypes.c_char_p
     L.sml_last_error.argtypes = []
     L.sml_abi_version.restype = i
@@ -157,6 +166,32 @@ def _declare(L: ctypes.CDLL) -> None:
         "sml_probe_mfma_f64": [i, ctypes.POINTER(ctypes.c_double)],
         "sml_stream_create_cu_range": [i, i, pp],
         "sml_stream_destroy": [vp],
+        "sml_dyn_run_model": [vp, vp, vp, i, d, d, d, d, vp, vp, vp],
+        "sml_dyn_last_safe": [vp, ip, vp],
+        "sml_res_info": [vp, ip, ip, ip, ip, vp],
+        "sml_comm_unique_id": [vp],
+        "sml_comm_create": [i, i, vp, pp],
+        "sml_comm_create_file": [i, i, ctypes.c_char_p, i, pp],
+        "sml_comm_destroy": [vp],
+        "sml_comm_rank": [vp, ip, ip],
+        "sml_comm_allgather": [vp, vp, vp, ctypes.c_int64, vp],
+        "sml_hybrid_create": [vp, vp, vp, i, d, d, d, d, i, i, pp],
+        "sml_hybrid_destroy": [vp],
+        "sml_hybrid_set_buffers": [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp],
+        "sml_hybrid_set_tisr": [vp, vp],
+        "sml_hybrid_streams": [vp, pp, pp],
+        "sml_hybrid_start": [vp, vp, vp, vp, vp, vp],
+        "sml_hybrid_predict": [vp],
+        "sml_hybrid_advance": [vp, vp],
+        "sml_hybrid_step": [vp],
+        "sml_hybrid_run_speedy": [vp, ip],
+        "sml_hybrid_sync": [vp],
+        "sml_device_alloc": [ctypes.c_int64, pp],
+        "sml_device_free": [vp],
+        "sml_copy_to_device": [vp, vp, ctypes.c_int64],
+        "sml_copy_to_host": [vp, vp, ctypes.c_int64],
+        "sml_region_geometry": [i, i, ip],
+        "sml_processor_decomposition": [i, i, i, ip, ip],
     }
     for name, args in sig.items():
         fn = getattr(L, name)

@@ -201,6 +201,23 @@ class Dynamics:
         check(lib().sml_dyn_to_grid_host(self._h, ptr(g), ptr(lp)))
         return g, lp
 
+    def run_model(self, grid4d, logp, fc4d, fc2d, nleap: int = 24, delt: float = DELT, alph: float = ALPH,
+                  stream=None):
+        """run_model (mpires.f90:1516-1628) on device tensors, asynchronous: iogrid(30)
+        + safety check, the window, iogrid(31) into (fc4d, fc2d), q floored at 1e-6;
+        an unsafe entry state returns the input grid (q floored) as agcm_main skips
+        the integration.  `last_safe()` gives the check's outcome."""
+        check(lib().sml_dyn_run_model(self._h, ptr(grid4d), ptr(logp), nleap, delt, alph, ROB, WIL, ptr(fc4d),
+                                      ptr(fc2d), stream_ptr(stream)))
+        self._dtal = (2 * delt, alph)
+
+    def last_safe(self):
+        """(is_safe_to_run_speedy, minmax[8]) of the last from_grid / run_model."""
+        safe = ctypes.c_int()
+        mm = np.zeros(8)
+        check(lib().sml_dyn_last_safe(self._h, ctypes.byref(safe), ptr(mm)))
+        return bool(safe.value), mm
+
     def stepone(self, delt: float = DELT, alph: float = ALPH, phys=None, stream=None):
         """ini_stepone.f90:19-34 for istart = 0 / 2: forward half step, first leapfrog."""
         self.step(1, 1, 0.5 * delt, alph, phys=phys, stream=stream)

@@ -123,7 +123,7 @@ def test_overlapped_loop_is_bitwise_the_serial_loop(cuda, speedy_cus):
 
 def test_loop_matches_the_sequential_chain(cuda):
     """HybridLoop.step == predict -> assemble -> iogrid(30) -> window -> iogrid(31) ->
-    tile, issued one after the other on the current stream (the bench's former step)."""
+    run_model's q floor -> tile, issued one after the other on the current stream."""
     import torch
 
     loop, _ = _loop(cuda, True)
@@ -137,6 +137,8 @@ def test_loop_matches_the_sequential_chain(cuda):
         seq.dyn.from_grid(seq.g4, seq.g2)
         seq.dyn.window(24)
         seq.dyn.to_grid(seq.f4, seq.f2)
+        q = seq.f4[..., 3]
+        q.clamp_(min=0.000001)  # run_model's floor on the forecast (mpires.f90:1614-1616)
         seq.res.tile_inputs(seq.g4, seq.g2, seq.pr, seq.f4, seq.f2, seq.tisr, seq.fb, seq.lm)
     loop.sync()
     torch.cuda.synchronize()

@@ -230,3 +230,95 @@ def test_synchronize_matches_repeated_updates(cuda):
     with pytest.raises(ValueError):
         res.synchronize(torch.zeros(10, dtype=torch.float64, device=cuda), length)
     res.synchronize(torch.zeros(1, dtype=torch.float64, device=cuda), 0)  # no-op
+
+
+def test_dense_win_grows_the_pool(cuda):
+    """A dense W_in (every entry nonzero, the reference's n x ninp matmul, :1443) on one
+    region of a context sized for the trained one-entry-per-row W_in: the W_in pool is
+    re-laid (grow_win_pool) and the other regions keep their weights."""
+    from speedy_ml_amd.reservoir import Reservoirs
+
+    ws = [region_weights(r, s, n_override=400, seed=9) for r, s in CASES[:3]]
+    res = Reservoirs([w.region for w in ws], [w.sst for w in ws], [w.n for w in ws], [w.k for w in ws])
+    rng = np.random.default_rng(4)
+    dense = (0.02 * (2.0 * rng.random(ws[1].win.shape) - 1.0)).astype(np.float32)
+    ws[1].win[:] = dense
+    for i, w in enumerate(ws):
+        res.load_region_weights(i, w)
+        res.set_state(i, initial_state(w.region, w.n))
+    fb = np.concatenate([feedback_vector(w.region, w.ninp) for w in ws])
+    lm = np.stack([local_model_vector(w.region) for w in ws])
+    out = res.predict_host(fb, lm)
+    o = res.fb_offsets
+    for i, w in enumerate(ws):
+        ref, x1 = oracle.predict(w.rows, w.cols, w.vals.astype(np.float64), w.win.astype(np.float64),
+                                 w.wout.astype(np.float64), fb[o[i]:o[i + 1]], lm[i],
+                                 initial_state(w.region, w.n), w.mean, w.std)
+        _check(out[i], ref, OUT_TOL)
+        _check(res.get_state(i), x1, 1e-13)  # dense sum order: matmul's column order, skipped zeros
+
+
+@pytest.mark.parametrize("weight_dtype", ["f32", "f64"])
+def test_finish_grid_equals_tile_then_finish(cuda, weight_dtype):
+    """sml_res_step_finish_grid (local-model tiling fused into the v_p finish) vs
+    begin -> tile_local_model -> finish: outvecs and the tiled local model bitwise,
+    with and without the local-model output."""
+    import torch
+
+    from speedy_ml_amd.reservoir import Reservoirs
+    from speedy_ml_amd.synthetic import synthetic_grids
+
+    ws = [region_weights(r, s, n_override=300, seed=11) for r, s in CASES]
+    g4, g2, pr = synthetic_grids(7)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(cuda)  # noqa: E731
+    outs = {}
+    for mode in ("fused", "fused_nolm", "two"):
+        res = Reservoirs([w.region for w in ws], [w.sst for w in ws], [w.n for w in ws], [w.k for w in ws],
+                         weight_dtype=weight_dtype)
+        for i, w in enumerate(ws):
+            if weight_dtype == "f64":
+                res.load_region(i, w.rows, w.cols, w.vals.astype(np.float64), w.win.astype(np.float64),
+                                w.wout.astype(np.float64), w.mean, w.std)
+            else:
+                res.load_region_weights(i, w)
+            res.set_state(i, initial_state(w.region, w.n))
+        fb = t(np.concatenate([feedback_vector(w.region, w.ninp) for w in ws]))
+        lm = torch.full((len(ws), 132), -7.0, dtype=torch.float64, device=cuda)
+        ov = torch.zeros((len(ws), 136), dtype=torch.float64, device=cuda)
+        res.predict_begin(fb)
+        if mode == "two":
+            res.tile_local_model(t(g4), t(g2), lm)
+            res.predict_finish(lm, ov)
+        else:
+            res.predict_finish_grid(t(g4), t(g2), lm if mode == "fused" else None, ov)
+        torch.cuda.synchronize()
+        outs[mode] = (ov.cpu().numpy(), lm.cpu().numpy())
+        res.close()
+    np.testing.assert_array_equal(outs["fused"][0], outs["two"][0])
+    np.testing.assert_array_equal(outs["fused_nolm"][0], outs["two"][0])
+    np.testing.assert_array_equal(outs["fused"][1], outs["two"][1])
+    assert (outs["fused_nolm"][1] == -7.0).all()  # no local-model output requested
+
+
+def test_finish_grid_ml_only_needs_no_forecast(cuda):
+    """An ML-only context (chunk_speedy 0, predict_ml) finishes without forecast grids."""
+    import torch
+
+    from speedy_ml_amd.reservoir import Reservoirs
+
+    ws = [region_weights(r, s, n_override=200, chunk_speedy=0) for r, s in CASES[:2]]
+    res = Reservoirs([w.region for w in ws], [w.sst for w in ws], [w.n for w in ws], [w.k for w in ws],
+                     chunk_speedy=0)
+    for i, w in enumerate(ws):
+        res.load_region_weights(i, w)
+        res.set_state(i, initial_state(w.region, w.n))
+    fbh = np.concatenate([feedback_vector(w.region, w.ninp) for w in ws])
+    fb = torch.from_numpy(fbh).to(cuda)
+    ov = torch.zeros((len(ws), 136), dtype=torch.float64, device=cuda)
+    res.predict_begin(fb)
+    res.predict_finish_grid(None, None, None, ov)
+    torch.cuda.synchronize()
+    o = res.fb_offsets
+    for i, w in enumerate(ws):
+        ref, _ = _oracle_step(w, initial_state(w.region, w.n), fbh[o[i]:o[i + 1]], None, chunk_speedy=0)
+        _check(ov[i].cpu().numpy(), ref, OUT_TOL)

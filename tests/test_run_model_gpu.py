@@ -1,0 +1,122 @@
+"""run_model on the GPU (sml_dyn_run_model; src/mpires.f90:1516-1628): the window entry
+iogrid(30) with its safety check (ppo_iogrid.f90:563-577), the window, the exit
+iogrid(31), then run_model's q floor (mpires.f90:1614-1616).  An unsafe entry state
+makes agcm_main skip the integration (at_gcm.f90:37): the forecast is run_model's
+copy of the input grid (q floored, :1550-1553) and run_speedy is false (:1623).
+
+Comparisons are bitwise: run_model issues the same kernels as from_grid + window +
+to_grid, and the floor / pass-through are selections, not arithmetic."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture()
+def dyn(cuda):
+    from speedy_ml_amd.dynamics import Dynamics
+    from speedy_ml_amd.synthetic import dyn_state, phys_boundary
+
+    st0, forcing = dyn_state()
+    d = Dynamics()
+    d.set_forcing(**forcing)
+    d.set_state(st0)
+    d.set_physics(phys_boundary(d, forcing["phis"]))
+    d.set_rad_state(None)
+    d.set_clock(1, True)
+    yield d
+    d.close()
+
+
+def _grids(seed=11, dry_top=True):
+    from speedy_ml_amd.synthetic import synthetic_grids
+
+    g4, g2, _ = synthetic_grids(seed)
+    if dry_top:  # a dry stratosphere: the transforms' ringing puts q below 1e-6 there
+        g4[:2, ..., 3] = 0.0
+    return g4, g2
+
+
+def _t(a, cuda):
+    import torch
+
+    return torch.from_numpy(np.ascontiguousarray(a)).to(cuda)
+
+
+def test_run_model_is_window_plus_q_floor(cuda, dyn):
+    import torch
+
+    from speedy_ml_amd.dynamics import Dynamics
+    from speedy_ml_amd.synthetic import dyn_state, phys_boundary
+
+    g4, g2 = _grids()
+    dg4, dg2 = _t(g4, cuda), _t(g2, cuda)
+    f4 = torch.zeros_like(dg4)
+    f2 = torch.zeros_like(dg2)
+    dyn.run_model(dg4, dg2, f4, f2, nleap=6)
+    safe, mm = dyn.last_safe()
+    assert safe, mm
+    # the same chain on a second context, unfloored
+    st0, forcing = dyn_state()
+    ref = Dynamics()
+    ref.set_forcing(**forcing)
+    ref.set_state(st0)
+    ref.set_physics(phys_boundary(ref, forcing["phis"]))
+    ref.set_rad_state(None)
+    ref.set_clock(1, True)
+    r4 = torch.zeros_like(dg4)
+    r2 = torch.zeros_like(dg2)
+    ref.from_grid(dg4, dg2)
+    ref.window(6)
+    ref.to_grid(r4, r2)
+    torch.cuda.synchronize()
+    raw = r4.cpu().numpy()
+    assert (raw[..., 3] < 1e-6).any(), "test setup: the forecast should have q below the floor somewhere"
+    want = raw.copy()
+    want[..., 3] = np.where(raw[..., 3] < 0.000001, 0.000001, raw[..., 3])
+    np.testing.assert_array_equal(f4.cpu().numpy(), want)
+    np.testing.assert_array_equal(f2.cpu().numpy(), r2.cpu().numpy())
+    ref.close()
+
+
+@pytest.mark.parametrize("bad", ["t_hot", "u_fast", "q_wet", "nan"])
+def test_unsafe_state_returns_the_input_grid(cuda, dyn, bad):
+    import torch
+
+    g4, g2 = _grids(seed=5)
+    # (the check reads the state re-gridded after spectral truncation: a single hot
+    # point is smoothed away, so whole levels / bands are perturbed)
+    if bad == "t_hot":
+        g4[3, :, :, 0] = 400.0        # temperature > 330 K
+    elif bad == "u_fast":
+        g4[1, 10:20, :, 1] = 300.0    # |u| > 150 m/s
+    elif bad == "q_wet":
+        g4[7, :, :, 3] = 50.0         # q > 30 g/kg
+    else:
+        g4[0, 0, 0, 2] = np.nan
+    dg4, dg2 = _t(g4, cuda), _t(g2, cuda)
+    f4 = torch.zeros_like(dg4)
+    f2 = torch.zeros_like(dg2)
+    dyn.run_model(dg4, dg2, f4, f2, nleap=3)
+    safe, mm = dyn.last_safe()
+    assert not safe, mm
+    want = g4.copy()
+    want[..., 3] = np.where(g4[..., 3] < 0.000001, 0.000001, g4[..., 3])
+    np.testing.assert_array_equal(f4.cpu().numpy(), want)
+    np.testing.assert_array_equal(f2.cpu().numpy(), g2)
+
+
+def test_safety_thresholds_match_iogrid(cuda, dyn):
+    """sml_dyn_is_safe on min/max vectors at and across each threshold."""
+    from speedy_ml_amd._lib import lib, ptr
+
+    base = np.array([-10.0, 10.0, -10.0, 10.0, 200.0, 300.0, 0.0, 20.0])
+    assert lib().sml_dyn_is_safe(ptr(base)) == 1
+    edges = [(0, -150.0, True), (0, -150.0001, False), (1, 150.0, True), (1, 150.0001, False),
+             (2, -120.0, True), (2, -120.0001, False), (3, 120.0, True), (3, 120.0001, False),
+             (4, 160.0, True), (4, 159.999, False), (5, 330.0, True), (5, 330.001, False),
+             (6, -6.0, True), (6, -6.0001, False), (7, 30.0, True), (7, 30.0001, False), (5, np.nan, False)]
+    for i, v, ok in edges:
+        mm = base.copy()
+        mm[i] = v
+        assert lib().sml_dyn_is_safe(ptr(mm)) == int(ok), (i, v)
