@@ -276,6 +276,153 @@ module sml_hip
       real(c_double), intent(out) :: grid4d(*), logp(*)
       integer(c_int) :: rc
     end function
+
+    ! ------------------------------------------------------------ SPEEDY physics / clock
+    !> phypar's boundary fields bc(ix*il, 15) (include/speedy_ml.h order); switches the GPU physics on
+    function sml_dyn_set_physics(ctx, bc) bind(C, name='sml_dyn_set_physics') result(rc)
+      import :: c_ptr, c_double, c_int
+      type(c_ptr), value :: ctx
+      real(c_double), intent(in) :: bc(*)
+      integer(c_int) :: rc
+    end function
+    function sml_dyn_set_rad_state(ctx, rad) bind(C, name='sml_dyn_set_rad_state') result(rc)
+      import :: c_ptr, c_int
+      type(c_ptr), value :: ctx, rad
+      integer(c_int) :: rc
+    end function
+    function sml_dyn_set_clock(ctx, istep, lradsw) bind(C, name='sml_dyn_set_clock') result(rc)
+      import :: c_ptr, c_int
+      type(c_ptr), value :: ctx
+      integer(c_int), value :: istep, lradsw
+      integer(c_int) :: rc
+    end function
+    function sml_dyn_get_clock(ctx, istep, lradsw) bind(C, name='sml_dyn_get_clock') result(rc)
+      import :: c_ptr, c_int
+      type(c_ptr), value :: ctx
+      integer(c_int), intent(out) :: istep, lradsw
+      integer(c_int) :: rc
+    end function
+    !> run_model (mpires.f90:1516-1628) on device grids: iogrid(30) + check, window,
+    !> iogrid(31), q floor; an unsafe entry state returns the input grid
+    function sml_dyn_run_model(ctx, d_grid4d, d_logp, nleap, delt, alph, rob, wil, d_fc4d, d_fc2d, stream) &
+        bind(C, name='sml_dyn_run_model') result(rc)
+      import :: c_ptr, c_int, c_double
+      type(c_ptr), value :: ctx, d_grid4d, d_logp, d_fc4d, d_fc2d, stream
+      integer(c_int), value :: nleap
+      real(c_double), value :: delt, alph, rob, wil
+      integer(c_int) :: rc
+    end function
+    !> is_safe_to_run_speedy of the last window entry (waits for its check only)
+    function sml_dyn_last_safe(ctx, safe, minmax) bind(C, name='sml_dyn_last_safe') result(rc)
+      import :: c_ptr, c_int, c_double
+      type(c_ptr), value :: ctx
+      integer(c_int), intent(out) :: safe
+      real(c_double), intent(out) :: minmax(8)
+      integer(c_int) :: rc
+    end function
+
+    ! ------------------------------------------------------------ communicator (RCCL)
+    !> startmpi's world (mpires.f90:21-37) for the one collective of the hot path;
+    !> the unique id travels through a file rank 0 writes
+    function sml_comm_create_file(world, rank, path, timeout_s, comm) bind(C, name='sml_comm_create_file') &
+        result(rc)
+      import :: c_int, c_char, c_ptr
+      integer(c_int), value :: world, rank, timeout_s
+      character(kind=c_char), intent(in) :: path(*)
+      type(c_ptr), intent(out) :: comm
+      integer(c_int) :: rc
+    end function
+    function sml_comm_destroy(comm) bind(C, name='sml_comm_destroy') result(rc)
+      import :: c_ptr, c_int
+      type(c_ptr), value :: comm
+      integer(c_int) :: rc
+    end function
+
+    ! ------------------------------------------------------------ the hybrid loop
+    function sml_hybrid_create(res, dyn, comm, nleap, delt, alph, rob, wil, overlap, speedy_cus, h) &
+        bind(C, name='sml_hybrid_create') result(rc)
+      import :: c_ptr, c_int, c_double
+      type(c_ptr), value :: res, dyn, comm
+      integer(c_int), value :: nleap, overlap, speedy_cus
+      real(c_double), value :: delt, alph, rob, wil
+      type(c_ptr), intent(out) :: h
+      integer(c_int) :: rc
+    end function
+    function sml_hybrid_destroy(h) bind(C, name='sml_hybrid_destroy') result(rc)
+      import :: c_ptr, c_int
+      type(c_ptr), value :: h
+      integer(c_int) :: rc
+    end function
+    function sml_hybrid_set_buffers(h, d_feedback, d_local_model, d_outvec, d_grid4d, d_grid2d, d_precip, &
+                                    d_fc4d, d_fc2d, d_tisr) bind(C, name='sml_hybrid_set_buffers') result(rc)
+      import :: c_ptr, c_int
+      type(c_ptr), value :: h, d_feedback, d_local_model, d_outvec, d_grid4d, d_grid2d, d_precip, d_fc4d, d_fc2d, &
+                            d_tisr
+      integer(c_int) :: rc
+    end function
+    function sml_hybrid_start(h, d_grid4d, d_grid2d, d_precip, d_fc4d, d_fc2d) bind(C, name='sml_hybrid_start') &
+        result(rc)
+      import :: c_ptr, c_int
+      type(c_ptr), value :: h, d_grid4d, d_grid2d, d_precip, d_fc4d, d_fc2d
+      integer(c_int) :: rc
+    end function
+    !> predict -> exchange -> assemble -> run_model -> re-tile (asynchronous)
+    function sml_hybrid_step(h) bind(C, name='sml_hybrid_step') result(rc)
+      import :: c_ptr, c_int
+      type(c_ptr), value :: h
+      integer(c_int) :: rc
+    end function
+    function sml_hybrid_run_speedy(h, run) bind(C, name='sml_hybrid_run_speedy') result(rc)
+      import :: c_ptr, c_int
+      type(c_ptr), value :: h
+      integer(c_int), intent(out) :: run
+      integer(c_int) :: rc
+    end function
+    function sml_hybrid_sync(h) bind(C, name='sml_hybrid_sync') result(rc)
+      import :: c_ptr, c_int
+      type(c_ptr), value :: h
+      integer(c_int) :: rc
+    end function
+
+    ! ------------------------------------------------------------ host plumbing
+    function sml_device_alloc(bytes, d_ptr) bind(C, name='sml_device_alloc') result(rc)
+      import :: c_int64_t, c_ptr, c_int
+      integer(c_int64_t), value :: bytes
+      type(c_ptr), intent(out) :: d_ptr
+      integer(c_int) :: rc
+    end function
+    function sml_device_free(d_ptr) bind(C, name='sml_device_free') result(rc)
+      import :: c_ptr, c_int
+      type(c_ptr), value :: d_ptr
+      integer(c_int) :: rc
+    end function
+    function sml_copy_to_device(d_dst, src, bytes) bind(C, name='sml_copy_to_device') result(rc)
+      import :: c_ptr, c_int64_t, c_int
+      type(c_ptr), value :: d_dst, src
+      integer(c_int64_t), value :: bytes
+      integer(c_int) :: rc
+    end function
+    function sml_copy_to_host(dst, d_src, bytes) bind(C, name='sml_copy_to_host') result(rc)
+      import :: c_ptr, c_int64_t, c_int
+      type(c_ptr), value :: dst, d_src
+      integer(c_int64_t), value :: bytes
+      integer(c_int) :: rc
+    end function
+    !> getxyresextent / getoverlapindices (res_domain.f90:123-204), 1-based
+    function sml_region_geometry(numregions, region, g) bind(C, name='sml_region_geometry') result(rc)
+      import :: c_int
+      integer(c_int), value :: numregions, region
+      integer(c_int), intent(out) :: g(12)
+      integer(c_int) :: rc
+    end function
+    !> processor_decomposition (res_domain.f90:31-62), 0-based regions
+    function sml_processor_decomposition(numregions, numprocs, irank, regions, count) &
+        bind(C, name='sml_processor_decomposition') result(rc)
+      import :: c_int
+      integer(c_int), value :: numregions, numprocs, irank
+      integer(c_int), intent(out) :: regions(*), count
+      integer(c_int) :: rc
+    end function
   end interface
 
 contains
@@ -295,6 +442,27 @@ contains
     end do
     print *, 'libspeedyml error in ', what, ' (', rc, '): ', msg(1:l)
     stop 1
+  end subroutine
+
+  !> the dims of a weight file (win_x=n, win_y=ninp, wout_x=nout, wout_y=ncs+n,
+  !> rows_x=k, mean_x=36) and its std vector: trained_reservoir_prediction sizes the
+  !> reservoir from the file and sets sst_bool_input <=> std(36) > 0.2
+  !> (mod_reservoir.f90:1781-1846)
+  subroutine sml_weight_file_header(filename, dims, std)
+    character(len=*), intent(in) :: filename
+    integer(c_int64_t), intent(out) :: dims(6)
+    real(c_double), intent(out) :: std(36)
+    real(c_float), allocatable, target :: win(:), wout(:), vals(:), mean32(:), std32(:)
+    integer(c_int), allocatable, target :: rows(:), cols(:)
+    character(kind=c_char, len=len_trim(filename) + 1) :: cpath
+    cpath = trim(filename) // c_null_char
+    call sml_check(sml_nc_read_region(cpath, dims, c_null_ptr, c_null_ptr, c_null_ptr, c_null_ptr, &
+                                      c_null_ptr, c_null_ptr, c_null_ptr), 'sml_nc_read_region(dims)')
+    allocate(win(dims(1) * dims(2)), wout(dims(3) * dims(4)), rows(dims(5)), cols(dims(5)), vals(dims(5)))
+    allocate(mean32(dims(6)), std32(dims(6)))
+    call sml_check(sml_nc_read_region(cpath, dims, c_loc(win), c_loc(wout), c_loc(rows), c_loc(cols), &
+                                      c_loc(vals), c_loc(mean32), c_loc(std32)), 'sml_nc_read_region')
+    std = real(std32, c_double)
   end subroutine
 
   !> read_trained_res (mod_io.f90:2911-2956) + the load into the GPU context for

@@ -169,3 +169,29 @@ def test_cu_range_streams(cuda):
     s.synchronize()
     assert float(y) == float(np.arange(1 << 20, dtype=np.float64).sum() * 2.0)
     check(lib().sml_stream_destroy(h))
+
+
+def test_loop_reports_unsafe_state_and_passes_the_grid_through(cuda):
+    """One region predicting a 1e5 K temperature makes the assembled grid fail
+    iogrid(30)'s check: run_speedy is false after that step (mpires.f90:721, the
+    reference's loop exits, parallelmain.f90:268-270) and the forecast is the
+    assembled grid with q floored (agcm_main skipped, at_gcm.f90:37)."""
+    import torch
+
+    loop, ws = _loop(cuda, True)
+    loop.step()
+    assert loop.run_speedy()
+    w = ws[500]
+    mean = w.mean.copy()
+    mean[0:8] = 1.0e5  # T of every level (mean/std index l = (var-1)*8 + level)
+    loop.sync()
+    loop.res.load_region(500, w.rows, w.cols, w.vals, w.win, w.wout, mean, w.std)
+    loop.step()
+    assert not loop.run_speedy()
+    loop.sync()
+    torch.cuda.synchronize()
+    g4 = loop.g4.cpu().numpy()
+    want = g4.copy()
+    want[..., 3] = np.where(g4[..., 3] < 0.000001, 0.000001, g4[..., 3])
+    np.testing.assert_array_equal(loop.f4.cpu().numpy(), want)
+    np.testing.assert_array_equal(loop.f2.cpu().numpy(), loop.g2.cpu().numpy())
