@@ -136,6 +136,22 @@ int sml_res_create(int numregions, int nlocal, const int *region_ids, const unsi
                    const int *n, const int *k, int chunk_speedy, int nout, int weight_dtype, double leakage,
                    sml_reservoirs **out);
 int sml_res_destroy(sml_reservoirs *c);
+/* A reservoir context for a different reservoir of the same shape: ninp[i] given per
+ * region (no geometry-derived inputs, no exchange/tiling tables), nout outputs each
+ * unstandardized with mean/std slot out_index[o] (0-based, -1 = none), a local-model
+ * block of chunk_speedy columns.  Used for the slab-ocean reservoir
+ * (src/mod_slab_ocean_reservoir.f90: inputs averaged atmosphere + sst, outputs the
+ * region's sst points, all unstandardized with the sst slot 36 -> out_index 35). */
+int sml_res_create_generic(int numregions, int nlocal, const int *region_ids, const int *ninp, const int *n,
+                           const int *k, int chunk_speedy, int nout, const signed char *out_index, int weight_dtype,
+                           double leakage, sml_reservoirs **out);
+/* predict_slab (src/mod_slab_ocean_reservoir.f90:1201-1249) for every local region:
+ * x = tanh(A x + W_in feedback), outvec = W_out [local_model; x~] unstandardized, and
+ * the raw outvec (before unstandardize) into d_local_model_next -- the reference's
+ * local_model = outvec (:1235).  chunk_speedy must equal nout; the two local-model
+ * buffers must not alias (swap them between steps). */
+int sml_res_step_slab(sml_reservoirs *c, const double *d_feedback, const double *d_local_model,
+                      double *d_local_model_next, double *d_outvec, void *stream);
 /* ninp of local region i (from geometry + sst flag) */
 int sml_res_ninp(const sml_reservoirs *c, int i, int *ninp);
 /* packed feedback layout: offsets[nlocal+1] (in doubles) */
@@ -181,6 +197,13 @@ int sml_res_set_read_waves(sml_reservoirs *c, int waves);
  * local region, no readout.  d_inputs holds `length` blocks in the packed feedback
  * layout, block t at d_inputs + t * stride doubles (stride >= total feedback). */
 int sml_res_synchronize(sml_reservoirs *c, const double *d_inputs, int length, int64_t stride, void *stream);
+/* start_prediction (src/mod_reservoir.f90:938-959): synchronize_print (:1381-1414) over
+ * the first `length` blocks of d_inputs (layout as sml_res_synchronize; the reference
+ * uses synclength/timestep - 1 blocks of its prediction data), then block `length`
+ * copied into d_feedback.  The local model of the first step comes from SPEEDY's
+ * forecast (sml_res_tile_local_model or the hybrid loop's start). */
+int sml_res_start_prediction(sml_reservoirs *c, const double *d_inputs, int length, int64_t stride,
+                             double *d_feedback, void *stream);
 /* host convenience: H2D, step, D2H (synchronous) */
 int sml_res_step_host(sml_reservoirs *c, const double *feedback, const double *local_model, double *outvec);
 /* bytes of weights + state resident on the device (for roofline bookkeeping) */
@@ -425,8 +448,24 @@ int sml_hybrid_destroy(sml_hybrid *h);
 int sml_hybrid_set_buffers(sml_hybrid *h, double *d_feedback, double *d_local_model, double *d_outvec,
                            double *d_grid4d, double *d_grid2d, double *d_precip, double *d_fc4d, double *d_fc2d,
                            const double *d_tisr);
-/* tisr inputs of the next steps (get_tisr_by_date, src/mpires.f90:1644-1676) */
+/* fixed tisr inputs of the next steps ([nlocal][16] standardized) */
 int sml_hybrid_set_tisr(sml_hybrid *h, const double *d_tisr);
+/* get_tisr_by_date (src/mpires.f90:1644-1676): hourly global tisr fields
+ * d_table[nhours][48][96] (nhours >= 8760, unstandardized; the reference's
+ * full_tisr is the same year read per region and standardized, get_full_tisr,
+ * src/mod_reservoir.f90:888-906); after step t the next feedback's tisr entries
+ * come from hour sml_tisr_date_index(startyear, hours_base + (t-1) step_hours) of
+ * the table, tiled and standardized per region.  NULL switches back to set_tisr. */
+int sml_hybrid_set_tisr_table(sml_hybrid *h, const double *d_table, int nhours, int startyear, int64_t hours_base,
+                              int step_hours);
+/* the reference calendar's hour-of-year index (1-based) after hours_elapsed hours from
+ * Jan 1 00 of startyear (get_current_time_delta_hour + numof_hours_into_year,
+ * src/mod_calendar.f90:24-175, wrapped past 8760 as get_tisr_by_date does); *feb29
+ * carries the SAVEd February of the reference's month table (0 at the start) */
+int sml_tisr_date_index(int startyear, int64_t hours_elapsed, int *feb29, int *index);
+/* the tisr entries of every local region's feedback from one hour's global tisr
+ * field d_tisr_grid(96, 48): overlap tile, (x - mean(34)) / std(34) */
+int sml_res_tile_tisr_field(sml_reservoirs *c, const double *d_tisr_grid, double *d_feedback, void *stream);
 /* the loop's main (reservoir + exchange) and side (SPEEDY) streams */
 int sml_hybrid_streams(const sml_hybrid *h, void **main, void **side);
 /* start_prediction's hand-over: inputs of the first step from an analysis grid and

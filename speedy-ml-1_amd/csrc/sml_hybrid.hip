@@ -63,6 +63,12 @@ struct sml_hybrid {
     double *d_send = nullptr, *d_recv = nullptr, *d_glob = nullptr;
     int32_t *d_perm = nullptr;
     bool started = false, predicted = false, advanced = false;
+    // get_tisr_by_date (mpires.f90:1644-1676): a table of hourly global tisr fields
+    // [nhours][48][96] on the device, the calendar's start year, the hours before the
+    // first prediction step and the hours per step; t = steps advanced so far
+    const double *tisr_table = nullptr;
+    int tisr_nhours = 0, tisr_startyear = 0, tisr_feb29 = 0;
+    int64_t tisr_base = 0, tisr_step_hours = 6, t = 0;
 };
 
 namespace {
@@ -160,6 +166,57 @@ extern "C" int sml_comm_rank(const sml_comm *c, int *world, int *rank) {
 extern "C" int sml_comm_allgather(sml_comm *c, const double *d_send, double *d_recv, int64_t count, void *stream) {
     SML_REQUIRE(c && d_send && d_recv && count >= 0, "bad argument");
     SML_NCCL(ncclAllGather(d_send, d_recv, (size_t)count, ncclDouble, c->comm, (hipStream_t)stream));
+    return SML_OK;
+}
+
+// ------------------------------------------------------------------ calendar
+// The reference's calendar arithmetic (src/mod_calendar.f90), restated with its
+// quirks: get_current_time_delta_hour (:24-92) counts years of 8760 h from the
+// start year (start month / day / hour unused), subtracts the leap days of the
+// elapsed years, walks a 365-day month table whose February it sets to 29 in a leap
+// year -- the table is a SAVEd local, so once a leap year is met February keeps 29
+// days for the rest of the run (*feb29 carries that state) -- and an exact month
+// boundary falls to December 31 of the year before; numof_hours_into_year
+// (:133-175) counts whole months, days, the hour, and 0 -> 1.  get_tisr_by_date
+// (mpires.f90:1665-1671) then wraps indices past 8760 by 8760.
+namespace {
+bool leap_year(int y) { return (y % 4 == 0 && y % 100 != 0) || y % 400 == 0; }  // leap_year_check :94-106
+}  // namespace
+
+extern "C" int sml_tisr_date_index(int startyear, int64_t hours_elapsed, int *feb29, int *index) {
+    SML_REQUIRE(feb29 && index && hours_elapsed >= 0, "bad argument");
+    const int64_t hours_in_year = 8760, hours_in_a_day = 24;
+    const int64_t years = hours_elapsed / hours_in_year;
+    int year = (int)(years + startyear);
+    int leap_days = 0;
+    for (int64_t i = 0; i < years; ++i)
+        if (leap_year(startyear + (int)i)) ++leap_days;
+    if (leap_year(year)) *feb29 = 1;
+    const int ncal[12] = {31, *feb29 ? 29 : 28, 31, 30, 31, 30, 31, 31, 30, 31, 30, 31};
+    const int64_t day_of_year = (hours_elapsed % hours_in_year) / hours_in_a_day - leap_days;
+    int64_t counter = day_of_year;
+    int month = 1;
+    while (counter > 0) {
+        counter -= ncal[month - 1];
+        ++month;
+    }
+    month -= 1;
+    if (month <= 0) {
+        month = 12;
+        year -= 1;
+    }
+    const int day = (int)(ncal[month - 1] + counter);
+    const int hour = (int)(hours_elapsed % hours_in_a_day);
+    // numof_hours_into_year(year, month, day, hour) with the year's own leap table
+    const bool ly = leap_year(year);
+    const int nmon[12] = {31, ly ? 29 : 28, 31, 30, 31, 30, 31, 31, 30, 31, 30, 31};
+    int64_t n = 0;
+    for (int i = 1; i < month; ++i) n += 24 * nmon[i - 1];
+    for (int i = 1; i < day; ++i) n += 24;
+    n += hour;
+    if (n == 0) n = 1;
+    if (n > 24 * 365) n -= 24 * 365;
+    *index = (int)n;
     return SML_OK;
 }
 
@@ -299,6 +356,19 @@ extern "C" int sml_hybrid_set_tisr(sml_hybrid *h, const double *d_tisr) {
     return SML_OK;
 }
 
+extern "C" int sml_hybrid_set_tisr_table(sml_hybrid *h, const double *d_table, int nhours, int startyear,
+                                         int64_t hours_base, int step_hours) {
+    SML_REQUIRE(h && (d_table == nullptr || (nhours >= 8760 && step_hours > 0 && hours_base >= 0)), "bad argument");
+    h->tisr_table = d_table;
+    h->tisr_nhours = nhours;
+    h->tisr_startyear = startyear;
+    h->tisr_base = hours_base;
+    h->tisr_step_hours = step_hours;
+    h->tisr_feb29 = 0;
+    h->t = 0;
+    return SML_OK;
+}
+
 extern "C" int sml_hybrid_streams(const sml_hybrid *h, void **main, void **side) {
     SML_REQUIRE(h, "null context");
     if (main) *main = h->main;
@@ -355,7 +425,19 @@ extern "C" int sml_hybrid_advance(sml_hybrid *h, const double *d_outvec_all) {
     hipStream_t m = h->main, s = h->side;
     if (int rc = sml_exchange_assemble(h->res, d_outvec_all, h->g4, h->g2, h->pr, m)) return rc;
     if (h->overlap) SML_HIP(hipEventRecord(h->ev_grid, m));
-    if (int rc = sml_res_tile_feedback(h->res, h->g4, h->g2, h->pr, h->tisr, h->fb, m)) return rc;
+    ++h->t;
+    if (int rc = sml_res_tile_feedback(h->res, h->g4, h->g2, h->pr, h->tisr_table ? nullptr : h->tisr, h->fb, m))
+        return rc;
+    if (h->tisr_table) {  // get_tisr_by_date(..., timestep - 1, ...) for the next feedback (mpires.f90:726-728)
+        int idx = 0;
+        if (int rc = sml_tisr_date_index(h->tisr_startyear, h->tisr_base + (h->t - 1) * h->tisr_step_hours,
+                                         &h->tisr_feb29, &idx))
+            return rc;
+        if (idx < 1 || idx > h->tisr_nhours)
+            return fail(SML_ERR_ARG, "tisr hour %d outside the table's %d hours", idx, h->tisr_nhours);
+        if (int rc = sml_res_tile_tisr_field(h->res, h->tisr_table + (size_t)(idx - 1) * kGrid2d, h->fb, m))
+            return rc;
+    }
     if (h->overlap) SML_HIP(hipStreamWaitEvent(s, h->ev_grid, 0));
     if (int rc = sml_dyn_run_model(h->dyn, h->g4, h->g2, h->nleap, h->delt, h->alph, h->rob, h->wil, h->f4, h->f2, s))
         return rc;

@@ -106,6 +106,11 @@ struct sml_reservoirs {
     int32_t *d_fb_src = nullptr;    // [tot_fb]
     uint8_t *d_fb_l = nullptr;      // [tot_fb]
     uint16_t *d_fb_reg = nullptr;   // [tot_fb]
+    // tisr entries of the feedback (get_tisr_by_date, mpires.f90:1644-1676): feedback
+    // index, grid2d index of the overlap-tile point, local region
+    int tot_tisr = 0;
+    int32_t *d_tisr_fb = nullptr, *d_tisr_grid = nullptr;
+    uint16_t *d_tisr_reg = nullptr;
     int32_t *d_lm_src = nullptr;    // [nlocal*ncs]
     uint8_t *d_lm_l = nullptr;
     double *d_io = nullptr;         // staging for sml_res_step_host
@@ -113,6 +118,10 @@ struct sml_reservoirs {
     int ev_cap = 0, ev_used = 0;
     bool timing = false;
     std::vector<double> meanstd_h;  // host copy [nlocal][72]
+    // generic context (sml_res_create_generic: the slab-ocean reservoir): ninp given,
+    // no exchange tables, every output unstandardized with the mean / std slot out_l[o]
+    bool generic = false;
+    std::vector<int8_t> out_l;
 };
 
 namespace {
@@ -434,19 +443,22 @@ __global__ __launch_bounds__(256) void k_res_readout(const RegionDev *__restrict
 // second half of the split readout (sml_res_step_finish): one thread per (region,
 // output): v = v_p + v_ml (v_ml from k_res_readout<kReadML>), unstandardized --
 // the same sums, in the same order, as k_res_readout<kReadFull>
+// raw (may be NULL): the outputs before unstandardize as well -- predict_slab keeps
+// them as its next local model (mod_slab_ocean_reservoir.f90:1235)
 template <typename WT>
 __global__ __launch_bounds__(256) void k_res_finish(const RegionDev *__restrict__ R, const WT *__restrict__ wlm,
                                                     const double *__restrict__ local_model,
                                                     const double *__restrict__ meanstd,
                                                     const int8_t *__restrict__ outl, const double *__restrict__ part,
                                                     double *__restrict__ outvec, int nout, int nout_pad, int ncs,
-                                                    int nlocal) {
+                                                    int nlocal, double *__restrict__ raw = nullptr) {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     const int r = t / nout_pad, o = t % nout_pad;
     if (r >= nlocal || o >= nout) return;
     const double vp = vp_sum(wlm + R[r].wlm, nout_pad, local_model + (size_t)r * ncs, ncs, o);
-    outvec[(size_t)r * nout + o] =
-        unstd(vp + part[(size_t)r * nout_pad + o], meanstd + (size_t)r * 2 * kMeanStd, outl[o]);
+    const double v = vp + part[(size_t)r * nout_pad + o];
+    if (raw) raw[(size_t)r * nout + o] = v;
+    outvec[(size_t)r * nout + o] = unstd(v, meanstd + (size_t)r * 2 * kMeanStd, outl[o]);
 }
 
 // sml_res_step_finish_grid: k_tile_local_model + k_res_finish in one launch, one
@@ -526,6 +538,20 @@ __global__ void k_tile_feedback(const int32_t *__restrict__ src, const uint8_t *
     feedback[e] = t / ms[kMeanStd + l];
 }
 
+// tisr entries from one hour's global tisr field (96, 48): get_tisr_by_date's
+// full_tisr(:, :, hour) of the region's overlap tile (read_3d_file_parallel over the
+// input extent), standardized with the region's tisr mean / std (l = 34,
+// get_full_tisr, mod_reservoir.f90:888-906)
+__global__ void k_tile_tisr(const int32_t *__restrict__ fbi, const int32_t *__restrict__ gi,
+                            const uint16_t *__restrict__ reg, const double *__restrict__ meanstd,
+                            const double *__restrict__ G, double *__restrict__ feedback, int total) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= total) return;
+    const double *ms = meanstd + (size_t)reg[e] * 2 * kMeanStd;
+    const double t = G[gi[e]] - ms[33];
+    feedback[fbi[e]] = t / ms[kMeanStd + 33];
+}
+
 // tile local_model: SPEEDY forecast at the region's own points, standardized
 __global__ void k_tile_local_model(const int32_t *__restrict__ src, const uint8_t *__restrict__ lidx,
                                    const double *__restrict__ meanstd, const double *__restrict__ fc4,
@@ -570,7 +596,18 @@ int out_std_index(int o, const RegionGeom &g) {
     return -1;
 }
 
+template <typename T>
+int upload(T *dst, const std::vector<T> &src) {
+    if (!src.empty()) SML_HIP(hipMemcpy(dst, src.data(), src.size() * sizeof(T), hipMemcpyHostToDevice));
+    return SML_OK;
+}
+
 int build_tables(sml_reservoirs *c) {
+    if (c->generic) {  // no exchange / tiling tables: only the unstandardize slots
+        if (int rc = dalloc(&c->d_outl, c->nout)) return rc;
+        SML_HIP(hipMemcpy(c->d_outl, c->out_l.data(), c->nout, hipMemcpyHostToDevice));
+        return SML_OK;
+    }
     // assemble: every region of the decomposition (outvec_all is global)
     std::vector<int32_t> dst((size_t)c->numregions * c->nout, -1);
     for (int r = 0; r < c->numregions; ++r) {
@@ -599,6 +636,8 @@ int build_tables(sml_reservoirs *c) {
     std::vector<uint16_t> freg(c->tot_fb);
     std::vector<int32_t> lsrc((size_t)c->nlocal * std::max(c->ncs, 1), 0);
     std::vector<uint8_t> ll((size_t)c->nlocal * std::max(c->ncs, 1), 0);
+    std::vector<int32_t> tfb, tgi;
+    std::vector<uint16_t> treg;
     for (int i = 0; i < c->nlocal; ++i) {
         const RegionGeom &g = c->geom[i];
         const int ix = g.inx, iy = g.iny, in2d = ix * iy, natmo = kVars * in2d * kZGrid;
@@ -625,7 +664,12 @@ int build_tables(sml_reservoirs *c) {
             for (int p = 0; p < in2d; ++p) fsrc[off + p] = kSrcKeep;
             off += in2d;
         }
-        for (int p = 0; p < in2d; ++p) fsrc[off + p] = -2 - (i * kTisrStride + p);
+        for (int p = 0; p < in2d; ++p) {
+            fsrc[off + p] = -2 - (i * kTisrStride + p);
+            tfb.push_back((int32_t)(off + p));
+            tgi.push_back(g2(gx(p % ix), g.in_ystart - 1 + p / ix));
+            treg.push_back((uint16_t)i);
+        }
         for (int64_t e = base; e < base + c->ninp[i]; ++e) freg[e] = (uint16_t)i;
         // local_model: the region's own points of the SPEEDY forecast grids
         const int rx = g.resx, ry = g.resy, na = kVars * rx * ry * kZGrid;
@@ -651,7 +695,11 @@ int build_tables(sml_reservoirs *c) {
     if ((rc = dalloc(&c->d_asm_dst, dst.size())) || (rc = dalloc(&c->d_fb_src, fsrc.size())) ||
         (rc = dalloc(&c->d_fb_l, fl.size())) || (rc = dalloc(&c->d_fb_reg, freg.size())) ||
         (rc = dalloc(&c->d_lm_src, lsrc.size())) || (rc = dalloc(&c->d_lm_l, ll.size())) ||
-        (rc = dalloc(&c->d_outl, outl.size())))
+        (rc = dalloc(&c->d_outl, outl.size())) || (rc = dalloc(&c->d_tisr_fb, tfb.size())) ||
+        (rc = dalloc(&c->d_tisr_grid, tgi.size())) || (rc = dalloc(&c->d_tisr_reg, treg.size())))
+        return rc;
+    c->tot_tisr = (int)tfb.size();
+    if ((rc = upload(c->d_tisr_fb, tfb)) || (rc = upload(c->d_tisr_grid, tgi)) || (rc = upload(c->d_tisr_reg, treg)))
         return rc;
     SML_HIP(hipMemcpy(c->d_asm_dst, dst.data(), dst.size() * 4, hipMemcpyHostToDevice));
     if (!fsrc.empty()) {
@@ -662,12 +710,6 @@ int build_tables(sml_reservoirs *c) {
     SML_HIP(hipMemcpy(c->d_lm_src, lsrc.data(), lsrc.size() * 4, hipMemcpyHostToDevice));
     SML_HIP(hipMemcpy(c->d_lm_l, ll.data(), ll.size(), hipMemcpyHostToDevice));
     SML_HIP(hipMemcpy(c->d_outl, outl.data(), outl.size(), hipMemcpyHostToDevice));
-    return SML_OK;
-}
-
-template <typename T>
-int upload(T *dst, const std::vector<T> &src) {
-    if (!src.empty()) SML_HIP(hipMemcpy(dst, src.data(), src.size() * sizeof(T), hipMemcpyHostToDevice));
     return SML_OK;
 }
 
@@ -841,7 +883,7 @@ extern "C" int sml_res_destroy(sml_reservoirs *c) {
     void *ptrs[] = {c->d_rd,    c->d_a_rp,    c->d_w_rp,   c->d_a_col,  c->d_w_col,  c->d_a_val,  c->d_w_val,
                     c->d_wout,  c->d_x[0],    c->d_x[1],   c->d_xaug,   c->d_meanstd, c->d_outl,  c->d_asm_dst,
                     c->d_fb_src, c->d_fb_l,   c->d_fb_reg, c->d_lm_src, c->d_lm_l,   c->d_io,     c->d_part,
-                    c->d_wlm};
+                    c->d_wlm,   c->d_tisr_fb, c->d_tisr_grid, c->d_tisr_reg};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     for (hipEvent_t e : c->ev)
@@ -850,9 +892,36 @@ extern "C" int sml_res_destroy(sml_reservoirs *c) {
     return SML_OK;
 }
 
+namespace {
+int res_create_impl(int numregions, int nlocal, const int *region_ids, const unsigned char *sst_flags,
+                    const int *n, const int *k, int chunk_speedy, int nout, int weight_dtype, double leakage,
+                    const int *ninp_generic, const signed char *out_index, sml_reservoirs **out);
+}
+
 extern "C" int sml_res_create(int numregions, int nlocal, const int *region_ids, const unsigned char *sst_flags,
                               const int *n, const int *k, int chunk_speedy, int nout, int weight_dtype,
                               double leakage, sml_reservoirs **out) {
+    return res_create_impl(numregions, nlocal, region_ids, sst_flags, n, k, chunk_speedy, nout, weight_dtype, leakage,
+                           nullptr, nullptr, out);
+}
+
+extern "C" int sml_res_create_generic(int numregions, int nlocal, const int *region_ids, const int *ninp,
+                                      const int *n, const int *k, int chunk_speedy, int nout,
+                                      const signed char *out_index, int weight_dtype, double leakage,
+                                      sml_reservoirs **out) {
+    SML_REQUIRE(nlocal == 0 || (ninp && out_index), "null ninp / out_index");
+    for (int o = 0; o < nout && out_index; ++o)
+        SML_REQUIRE(out_index[o] >= -1 && out_index[o] < kMeanStd, "out_index[%d] = %d outside [-1, 36)", o,
+                    out_index[o]);
+    std::vector<unsigned char> sst(std::max(nlocal, 1), 0);
+    return res_create_impl(numregions, nlocal, region_ids, sst.data(), n, k, chunk_speedy, nout, weight_dtype,
+                           leakage, ninp, out_index, out);
+}
+
+namespace {
+int res_create_impl(int numregions, int nlocal, const int *region_ids, const unsigned char *sst_flags,
+                    const int *n, const int *k, int chunk_speedy, int nout, int weight_dtype, double leakage,
+                    const int *ninp_generic, const signed char *out_index, sml_reservoirs **out) {
     SML_REQUIRE(out != nullptr, "out is null");
     *out = nullptr;
     int fx, fy;
@@ -870,6 +939,8 @@ extern "C" int sml_res_create(int numregions, int nlocal, const int *region_ids,
     c->nout_pad = (nout + kRows - 1) / kRows * kRows;
     c->wdtype = weight_dtype;
     c->leakage = leakage;
+    c->generic = ninp_generic != nullptr;
+    if (c->generic) c->out_l.assign(out_index, out_index + nout);
     if (const char *e = std::getenv("SML_READ_WAVES")) c->read_waves = std::max(0, std::atoi(e));
     if (const char *e = std::getenv("SML_UPD_BLOCKS")) c->upd_blocks = std::max(0, std::atoi(e));
     SML_REQUIRE(c->read_waves >= 0, "bad read_waves");
@@ -895,13 +966,17 @@ extern "C" int sml_res_create(int numregions, int nlocal, const int *region_ids,
             return fail(SML_ERR_ARG, "region %d: n=%d (1..65535) k=%d", i, n[i], k[i]);
         }
         const RegionGeom &g = c->geom[i];
-        if (kVars * g.resx * g.resy * kZGrid + 2 * g.resx * g.resy != nout ||
-            (chunk_speedy && chunk_speedy != kVars * g.resx * g.resy * kZGrid + g.resx * g.resy)) {
+        if (!c->generic && (kVars * g.resx * g.resy * kZGrid + 2 * g.resx * g.resy != nout ||
+                            (chunk_speedy && chunk_speedy != kVars * g.resx * g.resy * kZGrid + g.resx * g.resy))) {
             sml_res_destroy(c);
             return fail(SML_ERR_ARG, "nout %d / chunk_speedy %d do not match the %dx%d region tiles", nout,
                         chunk_speedy, g.resx, g.resy);
         }
-        c->ninp[i] = region_ninp(g, sst_flags[i] != 0);
+        c->ninp[i] = c->generic ? ninp_generic[i] : region_ninp(g, sst_flags[i] != 0);
+        if (c->ninp[i] <= 0 || c->ninp[i] > 65535) {
+            sml_res_destroy(c);
+            return fail(SML_ERR_ARG, "region %d: ninp %d (1..65535)", i, c->ninp[i]);
+        }
         c->ld[i] = (chunk_speedy + n[i] + 3) / 4 * 4;
         c->w_nz_cap[i] = n[i];
         RegionDev &r = c->rd[i];
@@ -987,6 +1062,7 @@ extern "C" int sml_res_create(int numregions, int nlocal, const int *region_ids,
     *out = c;
     return SML_OK;
 }
+}  // namespace
 
 extern "C" int sml_res_info(const sml_reservoirs *c, int *numregions, int *nlocal, int *chunk_speedy, int *nout,
                             int *region_ids) {
@@ -1131,17 +1207,18 @@ int check_loaded(const sml_reservoirs *c) {
 }
 
 template <int kMode>
-void launch_readout(sml_reservoirs *c, const double *d_local_model, double *d_outvec, hipStream_t st) {
+void launch_readout(sml_reservoirs *c, const double *d_local_model, double *d_outvec, hipStream_t st,
+                    double *d_raw = nullptr) {
     if constexpr (kMode == kReadFinish) {
         const int total = c->nlocal * c->nout_pad;
         if (c->wdtype == SML_F32)
             hipLaunchKernelGGL(k_res_finish<float>, dim3((total + 255) / 256), dim3(256), 0, st, c->d_rd,
                                (const float *)c->d_wlm, d_local_model, c->d_meanstd, c->d_outl, c->d_part, d_outvec,
-                               c->nout, c->nout_pad, c->ncs, c->nlocal);
+                               c->nout, c->nout_pad, c->ncs, c->nlocal, d_raw);
         else
             hipLaunchKernelGGL(k_res_finish<double>, dim3((total + 255) / 256), dim3(256), 0, st, c->d_rd,
                                (const double *)c->d_wlm, d_local_model, c->d_meanstd, c->d_outl, c->d_part,
-                               d_outvec, c->nout, c->nout_pad, c->ncs, c->nlocal);
+                               d_outvec, c->nout, c->nout_pad, c->ncs, c->nlocal, d_raw);
     } else {
         const int groups = c->nout_pad / kRows;
         const int nitems = c->nlocal * groups;
@@ -1203,11 +1280,32 @@ extern "C" int sml_res_step_finish(sml_reservoirs *c, const double *d_local_mode
     return SML_OK;
 }
 
+// predict_slab (src/mod_slab_ocean_reservoir.f90:1201-1249) for every local region
+// of a generic context: x = tanh(A x + W_in feedback) (leakage as created; the
+// reference's slab update has none, i.e. 1), outvec = W_out [local_model; x~], the
+// raw outvec as the next local model (:1235), then x*std + mean per output slot.
+// d_local_model_next must not alias d_local_model (the host ping-pongs them).
+extern "C" int sml_res_step_slab(sml_reservoirs *c, const double *d_feedback, const double *d_local_model,
+                                 double *d_local_model_next, double *d_outvec, void *stream) {
+    SML_REQUIRE(c, "null context");
+    if (c->nlocal == 0) return SML_OK;
+    SML_REQUIRE(d_feedback && d_outvec && d_local_model_next && (c->ncs == 0 || d_local_model), "null device buffer");
+    SML_REQUIRE(d_local_model_next != d_local_model, "d_local_model_next must not alias d_local_model");
+    SML_REQUIRE(c->ncs == c->nout, "predict_slab feeds its outvec back: chunk_speedy (%d) must equal nout (%d)",
+                c->ncs, c->nout);
+    if (int rc = sml_res_step_begin(c, d_feedback, stream)) return rc;
+    launch_readout<kReadFinish>(c, d_local_model, d_outvec, (hipStream_t)stream, d_local_model_next);
+    SML_HIP(hipGetLastError());
+    c->begun = false;
+    return SML_OK;
+}
+
 extern "C" int sml_res_step_finish_grid(sml_reservoirs *c, const double *d_fc4d, const double *d_fc2d,
                                         double *d_local_model, double *d_outvec, void *stream) {
     SML_REQUIRE(c, "null context");
     if (c->nlocal == 0) return SML_OK;
     SML_REQUIRE(d_outvec && (c->ncs == 0 || (d_fc4d && d_fc2d)), "null device buffer");
+    SML_REQUIRE(!c->generic || c->ncs == 0, "a generic (slab) context has no local-model tiling");
     SML_REQUIRE(c->ncs <= kMaxNcs, "ncs %d exceeds %d", c->ncs, kMaxNcs);
     if (!c->begun) return fail(SML_ERR_STATE, "sml_res_step_finish_grid without sml_res_step_begin");
     hipStream_t st = (hipStream_t)stream;
@@ -1269,6 +1367,19 @@ extern "C" int sml_res_synchronize(sml_reservoirs *c, const double *d_inputs, in
     return SML_OK;
 }
 
+// start_prediction (src/mod_reservoir.f90:938-959): synchronize_print (:1381-1414,
+// the same update loop as synchronize) over the first `length` input blocks, then
+// the next block becomes the feedback (reservoir%feedback = predictiondata(:, L+1))
+extern "C" int sml_res_start_prediction(sml_reservoirs *c, const double *d_inputs, int length, int64_t stride,
+                                        double *d_feedback, void *stream) {
+    SML_REQUIRE(c && d_inputs && d_feedback && length >= 0, "bad argument");
+    if (int rc = sml_res_synchronize(c, d_inputs, length, stride, stream)) return rc;
+    if (c->tot_fb)
+        SML_HIP(hipMemcpyAsync(d_feedback, d_inputs + (size_t)length * stride, (size_t)c->tot_fb * 8,
+                               hipMemcpyDeviceToDevice, (hipStream_t)stream));
+    return SML_OK;
+}
+
 extern "C" int sml_res_step_host(sml_reservoirs *c, const double *feedback, const double *local_model,
                                  double *outvec) {
     SML_REQUIRE(c && feedback && outvec, "null argument");
@@ -1305,6 +1416,7 @@ extern "C" int sml_res_footprint(const sml_reservoirs *c, int64_t *weight_bytes,
 extern "C" int sml_exchange_assemble(sml_reservoirs *c, const double *d_outvec_all, double *d_grid4d,
                                      double *d_grid2d, double *d_precip, void *stream) {
     SML_REQUIRE(c && d_outvec_all && d_grid4d && d_grid2d && d_precip, "null argument");
+    SML_REQUIRE(!c->generic, "a generic (slab) context has no exchange tables");
     const int total = c->numregions * c->nout;
     hipLaunchKernelGGL(k_assemble, dim3((total + 255) / 256), dim3(256), 0, (hipStream_t)stream, c->d_asm_dst,
                        d_outvec_all, d_grid4d, d_grid2d, d_precip, total);
@@ -1315,6 +1427,7 @@ extern "C" int sml_exchange_assemble(sml_reservoirs *c, const double *d_outvec_a
 extern "C" int sml_res_tile_feedback(sml_reservoirs *c, const double *d_grid4d, const double *d_grid2d,
                                      const double *d_precip, const double *d_tisr, double *d_feedback, void *stream) {
     SML_REQUIRE(c && d_grid4d && d_grid2d && d_precip && d_feedback, "null argument");
+    SML_REQUIRE(!c->generic, "a generic (slab) context has no exchange tables");
     if (c->tot_fb) {
         const int total = (int)c->tot_fb;
         hipLaunchKernelGGL(k_tile_feedback, dim3((total + 255) / 256), dim3(256), 0, (hipStream_t)stream, c->d_fb_src,
@@ -1325,9 +1438,23 @@ extern "C" int sml_res_tile_feedback(sml_reservoirs *c, const double *d_grid4d, 
     return SML_OK;
 }
 
+extern "C" int sml_res_tile_tisr_field(sml_reservoirs *c, const double *d_tisr_grid, double *d_feedback,
+                                       void *stream) {
+    SML_REQUIRE(c && d_tisr_grid && d_feedback, "null argument");
+    SML_REQUIRE(!c->generic, "a generic (slab) context has no exchange tables");
+    if (c->tot_tisr) {
+        hipLaunchKernelGGL(k_tile_tisr, dim3((c->tot_tisr + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                           c->d_tisr_fb, c->d_tisr_grid, c->d_tisr_reg, c->d_meanstd, d_tisr_grid, d_feedback,
+                           c->tot_tisr);
+        SML_HIP(hipGetLastError());
+    }
+    return SML_OK;
+}
+
 extern "C" int sml_res_tile_local_model(sml_reservoirs *c, const double *d_fc4d, const double *d_fc2d,
                                         double *d_local_model, void *stream) {
     SML_REQUIRE(c && d_fc4d && d_fc2d && d_local_model, "null argument");
+    SML_REQUIRE(!c->generic, "a generic (slab) context has no exchange tables");
     if (c->ncs && c->nlocal) {
         const int total = c->nlocal * c->ncs;
         hipLaunchKernelGGL(k_tile_local_model, dim3((total + 255) / 256), dim3(256), 0, (hipStream_t)stream,

@@ -49,7 +49,8 @@ EXPORTED = (
     "sml_hybrid_streams", "sml_hybrid_start", "sml_hybrid_predict", "sml_hybrid_advance", "sml_hybrid_step",
     "sml_hybrid_run_speedy", "sml_hybrid_sync",
     "sml_device_alloc", "sml_device_free", "sml_copy_to_device", "sml_copy_to_host", "sml_region_geometry",
-    "sml_processor_decomposition",
+    "sml_processor_decomposition", "sml_hybrid_set_tisr_table", "sml_tisr_date_index", "sml_res_tile_tisr_field",
+    "sml_res_create_generic", "sml_res_step_slab", "sml_res_start_prediction",
 )
 
 
@@ -192,6 +193,12 @@ def _declare(L: ctypes.CDLL) -> None:
         "sml_copy_to_host": [vp, vp, ctypes.c_int64],
         "sml_region_geometry": [i, i, ip],
         "sml_processor_decomposition": [i, i, i, ip, ip],
+        "sml_hybrid_set_tisr_table": [vp, vp, i, i, ctypes.c_int64, i],
+        "sml_tisr_date_index": [i, ctypes.c_int64, ip, ip],
+        "sml_res_tile_tisr_field": [vp, vp, vp, vp],
+        "sml_res_create_generic": [i, i, vp, vp, vp, vp, i, i, vp, i, d, pp],
+        "sml_res_step_slab": [vp, vp, vp, vp, vp, vp],
+        "sml_res_start_prediction": [vp, vp, i, ctypes.c_int64, vp, vp],
     }
     for name, args in sig.items():
         fn = getattr(L, name)

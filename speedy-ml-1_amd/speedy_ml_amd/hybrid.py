@@ -83,6 +83,16 @@ class HybridLoop:
         self.tisr = tisr
         check(lib().sml_hybrid_set_tisr(self._h, ptr(tisr)))
 
+    def set_tisr_table(self, table, startyear: int, hours_base: int, step_hours: int = 6):
+        """get_tisr_by_date (mpires.f90:1644-1676): hourly global tisr fields
+        `table` [nhours, 48, 96] (device), the calendar's start year and the hours
+        before the first prediction step (traininglength + prediction marker +
+        synclength in the reference); None switches back to the fixed tisr."""
+        self._tisr_table = table
+        n = 0 if table is None else int(table.shape[0])
+        check(lib().sml_hybrid_set_tisr_table(self._h, ptr(table), n, int(startyear), int(hours_base),
+                                              int(step_hours)))
+
     def start(self, g4, g2, pr, f4, f2):
         """start_prediction analogue: inputs of the first step from an analysis grid
         (g4, g2, pr) and a SPEEDY forecast from it (f4, f2)."""

@@ -21,9 +21,13 @@ from .domain import CHUNK_PRED, CHUNK_SPEEDY, NUM_REGIONS
 
 
 class Reservoirs:
+    """One rank's reservoirs on the GPU (sml_res_*).  With `ninp` and `out_index` given,
+    a generic context (sml_res_create_generic: the slab-ocean reservoir's shape,
+    ninp per region, outputs unstandardized with mean/std slot out_index[o])."""
+
     def __init__(self, region_ids, sst_flags, n, k, numregions: int = NUM_REGIONS,
                  chunk_speedy: int = CHUNK_SPEEDY, nout: int = CHUNK_PRED, weight_dtype: str = "f32",
-                 leakage: float = 1.0):
+                 leakage: float = 1.0, ninp=None, out_index=None):
         self.region_ids = np.ascontiguousarray(region_ids, dtype=np.int32)
         self.sst = np.ascontiguousarray(sst_flags, dtype=np.uint8)
         self.n = np.ascontiguousarray(n, dtype=np.int32)
@@ -35,8 +39,15 @@ class Reservoirs:
         self.weight_dtype = weight_dtype
         dt = {"f32": SML_F32, "f64": SML_F64}[weight_dtype]
         h = ctypes.c_void_p()
-        check(lib().sml_res_create(numregions, self.nlocal, ptr(self.region_ids), ptr(self.sst), ptr(self.n),
-                                   ptr(self.k), chunk_speedy, nout, dt, leakage, ctypes.byref(h)))
+        if ninp is None:
+            check(lib().sml_res_create(numregions, self.nlocal, ptr(self.region_ids), ptr(self.sst), ptr(self.n),
+                                       ptr(self.k), chunk_speedy, nout, dt, leakage, ctypes.byref(h)))
+        else:
+            self._ninp = np.ascontiguousarray(ninp, dtype=np.int32)
+            self._oidx = np.ascontiguousarray(out_index, dtype=np.int8)
+            check(lib().sml_res_create_generic(numregions, self.nlocal, ptr(self.region_ids), ptr(self._ninp),
+                                               ptr(self.n), ptr(self.k), chunk_speedy, nout, ptr(self._oidx), dt,
+                                               leakage, ctypes.byref(h)))
         self._h = h
         off = np.zeros(self.nlocal + 1, dtype=np.int64)
         check(lib().sml_res_feedback_offsets(self._h, ptr(off)))
@@ -132,6 +143,19 @@ class Reservoirs:
         if d_inputs.numel() < length * stride:
             raise ValueError("d_inputs holds fewer than length * stride doubles")
         check(lib().sml_res_synchronize(self._h, ptr(d_inputs), length, stride, stream_ptr(stream)))
+
+    def start_prediction(self, d_inputs, length: int, d_feedback, stride: int | None = None, stream=None):
+        """start_prediction (mod_reservoir.f90:938-959): synchronize_print over the first
+        `length` input blocks, block `length` into d_feedback."""
+        stride = int(self.fb_offsets[-1]) if stride is None else stride
+        check(lib().sml_res_start_prediction(self._h, ptr(d_inputs), length, stride, ptr(d_feedback),
+                                             stream_ptr(stream)))
+
+    def predict_slab(self, d_feedback, d_local_model, d_local_model_next, d_outvec, stream=None):
+        """predict_slab (mod_slab_ocean_reservoir.f90:1201-1249) on a generic context:
+        outvec unstandardized, the raw outvec into d_local_model_next."""
+        check(lib().sml_res_step_slab(self._h, ptr(d_feedback), ptr(d_local_model), ptr(d_local_model_next),
+                                      ptr(d_outvec), stream_ptr(stream)))
 
     def predict_host(self, feedback: np.ndarray, local_model: np.ndarray | None) -> np.ndarray:
         fb = np.ascontiguousarray(feedback, dtype=np.float64)

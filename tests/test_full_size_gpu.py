@@ -29,8 +29,8 @@ pytestmark = pytest.mark.gpu
 
 X_TOL = 1e-14
 OUT_TOL = 1e-11
-FC_TOL = 1e-10
-OUT2_TOL = 1e-10
+FC_TOL = 1e-12
+OUT2_TOL = 1e-12
 SAMPLE = list(range(0, 1152, 12))
 
 

@@ -195,3 +195,39 @@ def test_loop_reports_unsafe_state_and_passes_the_grid_through(cuda):
     want[..., 3] = np.where(g4[..., 3] < 0.000001, 0.000001, g4[..., 3])
     np.testing.assert_array_equal(loop.f4.cpu().numpy(), want)
     np.testing.assert_array_equal(loop.f2.cpu().numpy(), loop.g2.cpu().numpy())
+
+
+def test_tisr_by_date_from_a_table(cuda):
+    """get_tisr_by_date (mpires.f90:1644-1676) in the loop: after step t the next
+    feedback's tisr entries are the overlap tile of hour sml_tisr_date_index(start,
+    base + (t-1) 6) of the table, (x - mean(34)) / std(34) per region -- bitwise."""
+    import ctypes
+
+    import torch
+
+    from speedy_ml_amd._lib import lib
+
+    loop, ws = _loop(cuda, True)
+    rng = np.random.default_rng(21)
+    table = 300.0 + 100.0 * rng.random((8760, 48, 96))
+    dt = torch.from_numpy(table).to(cuda)
+    start, base = 1981, 227520 + 24 * 40
+    loop.set_tisr_table(dt, start, base)
+    o = loop.res.fb_offsets
+    feb = ctypes.c_int(0)
+    for t in (1, 2):
+        loop.step()
+        loop.sync()
+        idx = ctypes.c_int()
+        assert lib().sml_tisr_date_index(start, base + (t - 1) * 6, ctypes.byref(feb), ctypes.byref(idx)) == 0
+        g = table[idx.value - 1]
+        fb = loop.fb.cpu().numpy()
+        for r in (0, 23, 24, 500, 1151):
+            geo = domain.region_geometry(r)
+            pts = [g[geo.in_ystart - 1 + p // geo.inx, geo.input_x(p % geo.inx + 1) - 1]
+                   for p in range(geo.inx * geo.iny)]
+            w = ws[r]
+            want = (np.array(pts) - w.mean[33]) / w.std[33]
+            got = fb[o[r + 1] - len(pts):o[r + 1]]
+            np.testing.assert_array_equal(got, want, err_msg=f"region {r} step {t}")
+    loop.close()

@@ -322,3 +322,88 @@ def test_finish_grid_ml_only_needs_no_forecast(cuda):
     for i, w in enumerate(ws):
         ref, _ = _oracle_step(w, initial_state(w.region, w.n), fbh[o[i]:o[i + 1]], None, chunk_speedy=0)
         _check(ov[i].cpu().numpy(), ref, OUT_TOL)
+
+
+def test_start_prediction(cuda):
+    """start_prediction (mod_reservoir.f90:938-959): synchronize_print over the first
+    `length` blocks (the oracle's update sequence), then block `length` becomes the
+    feedback."""
+    import torch
+
+    res, ws = _build(CASES[:3], n_override=500)
+    length = 5
+    tot = res.fb_offsets[-1]
+    rng = np.random.default_rng(8)
+    inputs = rng.standard_normal((length + 1, tot))
+    fb = torch.zeros(tot, dtype=torch.float64, device=cuda)
+    res.start_prediction(torch.from_numpy(inputs).to(cuda), length, fb)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(fb.cpu().numpy(), inputs[length])
+    o = res.fb_offsets
+    for i, w in enumerate(ws):
+        x = initial_state(w.region, w.n)
+        for t in range(length):
+            _, x = _oracle_step(w, x, inputs[t, o[i]:o[i + 1]], np.zeros(132))
+        _check(res.get_state(i), x, 1e-13)
+
+
+def _slab_weights(region, ninp, n, seed):
+    """A slab-ocean reservoir's arrays (mod_slab_ocean_reservoir.f90: m = 4000 nodes,
+    one W_in entry per row, sst outputs of the 2x2 region)."""
+    rng = np.random.default_rng([seed, region])
+    k = int(0.001 * n * n)
+    rows = np.concatenate([rng.permutation(n)[:min(n, k - b)] + 1 for b in range(0, k, n)]).astype(np.int32)
+    cols = np.concatenate([rng.permutation(n)[:min(n, k - b)] + 1 for b in range(0, k, n)]).astype(np.int32)
+    vals = (rng.random(k) * 0.3).astype(np.float32)
+    win = np.zeros((ninp, n), dtype=np.float32)
+    q = n // ninp
+    for j in range(q):
+        win[np.arange(ninp), np.arange(ninp) * q + j] = (0.5 * (2 * rng.random(ninp) - 1)).astype(np.float32)
+    wout = ((rng.random((4 + n, 4)) * 2 - 1) * 0.01).astype(np.float32)
+    mean = rng.random(36).astype(np.float32).astype(np.float64)
+    std = (0.5 + rng.random(36)).astype(np.float32).astype(np.float64)
+    return rows, cols, vals, win, wout, mean, std
+
+
+def test_predict_slab_matches_oracle(cuda):
+    """predict_slab (mod_slab_ocean_reservoir.f90:1201-1249) on a generic context over
+    3 steps: x = tanh(A x + W_in u), outvec = W_out [local_model; x~], local_model =
+    the raw outvec (:1235), outvec * std(sst) + mean(sst) -- against the oracle's
+    predict with chunk_speedy = 4 and no unstandardize."""
+    import torch
+
+    from speedy_ml_amd.reservoir import Reservoirs
+
+    regions, ninp = [10, 500, 1100], [48, 40, 64]
+    n = [4000 // p * p for p in ninp]
+    ws = [_slab_weights(r, p, m, 6) for r, p, m in zip(regions, ninp, n)]
+    res = Reservoirs(regions, [0, 0, 0], n, [len(w[0]) for w in ws], chunk_speedy=4, nout=4, ninp=ninp,
+                     out_index=[35] * 4)
+    xs = []
+    for i, w in enumerate(ws):
+        res.load_region(i, *w)
+        xs.append(0.1 * np.random.default_rng(i).random(n[i]))
+        res.set_state(i, xs[i])
+    rng = np.random.default_rng(2)
+    lm = rng.standard_normal((3, 4))
+    d_lm = torch.from_numpy(lm.copy()).to(cuda)
+    d_next = torch.zeros_like(d_lm)
+    d_ov = torch.zeros((3, 4), dtype=torch.float64, device=cuda)
+    o = res.fb_offsets
+    for step in range(3):
+        fb = rng.standard_normal(int(o[-1]))
+        res.predict_slab(torch.from_numpy(fb).to(cuda), d_lm, d_next, d_ov)
+        torch.cuda.synchronize()
+        got_ov, got_raw = d_ov.cpu().numpy(), d_next.cpu().numpy()
+        for i, w in enumerate(ws):
+            rows, cols, vals, win, wout, mean, std = w
+            raw, xs[i] = oracle.predict(rows, cols, vals.astype(np.float64), win.astype(np.float64),
+                                        wout.astype(np.float64), fb[o[i]:o[i + 1]], lm[i], xs[i], mean, std,
+                                        chunk_speedy=4, unstandardize=False)
+            _check(got_raw[i], raw, OUT_TOL)
+            _check(got_ov[i], raw * std[35] + mean[35], OUT_TOL)
+            _check(res.get_state(i), xs[i], 1e-13)
+            lm[i] = raw
+        d_lm, d_next = d_next, d_lm  # the raw outvec is the next local model
+    with pytest.raises(SmlError):
+        res.predict_slab(torch.from_numpy(fb).to(cuda), d_lm, d_lm, d_ov)  # aliasing refused
