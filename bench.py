@@ -50,7 +50,10 @@ def parse():
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--regions", type=int, default=1152)
     p.add_argument("--weights", choices=("f32", "f64"), default="f32")
-    p.add_argument("--cpu-sample", type=int, default=96, help="regions in the CPU-baseline sample (0 = skip)")
+    p.add_argument("--cpu-threads", type=int,
+                   default=min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else 8),
+                   help="OpenMP threads of the CPU baseline's predict leg (0 = skip the CPU baseline; default: "
+                        "the box's CPU share, at most 16)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--overlap", action=argparse.BooleanOptionalAction, default=True,
                    help="issue the reservoir update + v_ml readout beside SPEEDY's window on two streams "
@@ -233,8 +236,8 @@ def main():
             "roofline_unpaced": unpaced}
     dyn.close()
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.cpu_sample > 0:
-        cpu = cpu_baseline(args.cpu_sample, nreg, mask, phys_bc)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.cpu_threads > 0:
+        cpu = cpu_baseline(nreg, mask, args.cpu_threads)
     speedy = speedy_leg(dev, world, rank, args) if args.speedy_steps > 0 else None
     training = training_leg(dev, mask, args) if args.train_regions > 0 and world == 1 else None
 
@@ -434,35 +437,58 @@ def training_leg(dev, mask, args):
     }
 
 
-def cpu_baseline(sample: int, nreg: int, mask, bc):
-    """The oracle's restatement of the hybrid step on one host core: predict
-    (dense W_in matmul, COO SpMV, dense W_out GEMV: the reference's arithmetic) over
-    a bounded sample of regions spread over the shape classes, extrapolated to all
-    1152; the exchange/tiling oracle on every region; one whole SPEEDY window
-    (iogrid(30), stepone + 24 leapfrog steps with physics, iogrid(31))."""
+def _cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or platform.machine()
+
+
+def cpu_baseline(nreg: int, mask, threads: int):
+    """The reference's CPU path of one hybrid step, timed on this host (rank 0, N=1):
+
+      predict      all nreg regions with the reference's arithmetic -- COO SpMV,
+                   the DENSE W_in matmul (mod_reservoir.f90:1443, 26.5 MB per region),
+                   W_out GEMV, unstandardize -- fp64 weights as read_trained_res holds
+                   them: the oracle's C restatement (oracle/speedy_oracle.c
+                   orc_predict, pinned statement by statement), OpenMP over regions;
+      exchange     assemble + tile of every region (the root's serial loops,
+                   mpires.f90:300-751), oracle C, one thread;
+      window       the REFERENCE's own SPEEDY code (oracle/_ref/libspeedy_ref_dyn.so,
+                   dyn_* / phy_* / spe_* compiled as-is) through iogrid(30), stepone,
+                   24 leapfrog steps and iogrid(31), one thread, as the reference runs
+                   it on its root rank (oracle/ref_window_timing.py, a subprocess).
+
+    One full step each with `threads` OpenMP threads (the value) and with one thread
+    (reported beside it); no sample is extrapolated."""
+    import subprocess
+
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle
-    from speedy_ml_amd import domain
     from speedy_ml_amd.synthetic import feedback_vector, initial_state, local_model_vector, region_weights
 
-    stride = max(1, nreg // sample)
-    picks = list(range(0, nreg, stride))[:sample]
-    t_pred = 0.0
-    for r in picks:
+    t_gen = time.perf_counter()
+    regs, fbs, lms, xs = [], [], [], []
+    for r in range(nreg):
         w = region_weights(r, bool(mask[r]))
-        win = w.win.astype(np.float64)
-        wout = w.wout.astype(np.float64)
-        vals = w.vals.astype(np.float64)
-        x = initial_state(r, w.n)
-        fb = feedback_vector(r, w.ninp)
-        lm = local_model_vector(r)
+        regs.append({"rows": w.rows, "cols": w.cols, "vals": w.vals.astype(np.float64),
+                     "win": w.win.astype(np.float64), "wout": w.wout.astype(np.float64), "mean": w.mean,
+                     "std": w.std})
+        fbs.append(feedback_vector(r, w.ninp))
+        lms.append(local_model_vector(r))
+        xs.append(initial_state(r, w.n))
+    t_gen = time.perf_counter() - t_gen
+    wbytes = sum(r["win"].nbytes + r["wout"].nbytes for r in regs)
+    pred = {}
+    for th in sorted({1, threads}):
         t0 = time.perf_counter()
-        oracle.predict(w.rows, w.cols, vals, win, wout, fb, lm, x, w.mean, w.std)
-        t_pred += time.perf_counter() - t0
-    per_region = t_pred / len(picks)
-    # exchange on the host: assemble + tile every region (root-serial in the reference)
-    outvecs = np.random.default_rng(0).standard_normal((nreg, 136))
-    g4, g2, pr = (None, None, None)
+        outvecs = oracle.predict_regions(regs, fbs, lms, xs, nthreads=th)
+        pred[th] = time.perf_counter() - t0
+    del regs
+    # exchange on the host: assemble + tile every region
     t0 = time.perf_counter()
     g4, g2, pr = oracle.assemble(outvecs)
     ms = np.ones(36)
@@ -470,34 +496,28 @@ def cpu_baseline(sample: int, nreg: int, mask, bc):
         oracle.tile_feedback(r, g4, g2, pr, np.zeros(36), ms, np.zeros(16))
         oracle.tile_local_model(r, g4, g2, np.zeros(36), ms)
     t_xchg = time.perf_counter() - t0
-    # the SPEEDY window
-    from speedy_ml_amd.dynamics import DELT
-    from speedy_ml_amd.synthetic import dyn_state
-
-    st, forcing = dyn_state()
-    s = oracle.dyn_state_copy(st)
-    og4, olp = oracle.iogrid31(oracle.dyn_state_copy(st))
-    rad = oracle.phys_state()
-    f = (forcing["phis"], forcing["tcorh"], forcing["qcorh"], bc, rad)
-    t0 = time.perf_counter()
-    oracle.iogrid30(s, og4, olp)
-    oracle.dyn_step_physics(s, *f, True, 1, 1, 0.5 * DELT, 0.5)
-    oracle.dyn_step_physics(s, *f, True, 1, 2, DELT, 0.5)
-    for i in range(1, 25):
-        oracle.dyn_step_physics(s, *f, i % 3 == 1, 2, 2, 2 * DELT, 0.5)
-    oracle.iogrid31(s)
-    t_win = time.perf_counter() - t0
-    step_s = per_region * nreg + t_xchg + t_win
+    # the reference's window, in a subprocess (its stack, its prints)
+    out = subprocess.run([sys.executable, os.path.join(REPO, "oracle", "ref_window_timing.py"), "2"],
+                         capture_output=True, text=True, timeout=300)
+    win = json.loads(out.stdout.strip().splitlines()[-1])
+    t_win = win["window_s"]
+    step = {th: pred[th] + t_xchg + t_win for th in pred}
     return {
-        "value": round(1.0 / step_s, 4),
+        "value": round(1.0 / step[threads], 4),
         "unit": "hybrid timesteps/s",
-        "cores": 1,
+        "cores": threads,
         "kind": "port",
-        "sample": f"oracle predict (dense W_in as the reference) timed on {len(picks)} of {nreg} regions "
-                  f"(every {stride}th, all shape classes), {per_region * 1e3:.3f} ms/region, extrapolated to "
-                  f"{nreg}; + host assemble/tile of all regions {t_xchg * 1e3:.1f} ms; + one SPEEDY window "
-                  f"(26 steps with physics + iogrid) {t_win * 1e3:.1f} ms; "
-                  f"host {platform.processor() or platform.machine()}, {os.cpu_count()} logical CPUs visible",
+        "sample": f"one full hybrid step, no extrapolation: predict of all {nreg} regions with the reference's "
+                  f"arithmetic (dense fp64 W_in, {wbytes / 1e9:.1f} GB of weights) on {threads} OpenMP threads "
+                  f"{pred[threads] * 1e3:.0f} ms (1 thread: {pred[1] * 1e3:.0f} ms, i.e. "
+                  f"{1.0 / step[1]:.3f} steps/s single-core); host assemble + tile of every region "
+                  f"{t_xchg * 1e3:.1f} ms; the reference's own SPEEDY window (compiled reference Fortran, "
+                  f"oracle/_ref, 1 thread) {t_win * 1e3:.0f} ms; host: {_cpu_model()}, {os.cpu_count()} logical "
+                  f"CPUs visible, {threads} used; weight generation {t_gen:.0f} s untimed",
+        "single_thread_value": round(1.0 / step[1], 4),
+        "predict_ms": {str(k): round(v * 1e3, 1) for k, v in pred.items()},
+        "exchange_ms": round(t_xchg * 1e3, 2),
+        "window_ms": round(t_win * 1e3, 1),
     }
 
 

@@ -67,6 +67,7 @@ def _declare(L):
     L.orc_reservoir_sizes.argtypes = [i, i, i, i, vp]
     L.orc_predict.argtypes = [i, i, i, vp, vp, vp, vp, vp, i, i, d, vp, vp, vp, vp, vp, vp, i]
     L.orc_predict_f32.argtypes = [i, i, i, vp, vp, vp, vp, vp, vp, i, i, d, vp, vp, vp, vp, vp, vp]
+    L.orc_predict_regions.argtypes = [i, i, vp, vp, vp, vp, vp, vp, vp, vp, i, i, d, vp, vp, vp, vp, vp, vp]
     L.orc_unstandardize_res.argtypes = [vp, i, i, i, vp, vp, i, i, i, i]
     L.orc_assemble.argtypes = [i, vp, i, vp, vp, vp]
     L.orc_tile_feedback.argtypes = [i, i, vp, vp, vp, vp, vp, vp, vp, vp]
@@ -265,6 +266,29 @@ def predict(rows, cols, vals, win_dense, wout, feedback, local_model, x, mean, s
                       chunk_speedy, leakage, _p(feedback), _p(lm), _p(xx), _p(out), _p(mean), _p(std),
                       int(bool(unstandardize)))
     return out, xx
+
+
+def predict_regions(regions, feedbacks, local_models, xs, nthreads=1, chunk_speedy=132, leakage=1.0):
+    """orc_predict over many regions with OpenMP (the CPU baseline's reservoir leg).
+    regions: list of dicts with rows, cols, vals, win (ninp, n), wout (ncs+n, nout),
+    mean, std as contiguous float64 / int32 arrays; xs updated in place.  Returns
+    outvecs [nreg, nout]."""
+    nreg = len(regions)
+    nout = regions[0]["wout"].shape[1]
+
+    def table(arrs):
+        return (ctypes.c_void_p * nreg)(*[a.ctypes.data for a in arrs])
+
+    n = np.array([r["win"].shape[1] for r in regions], dtype=np.int32)
+    ninp = np.array([r["win"].shape[0] for r in regions], dtype=np.int32)
+    k = np.array([len(r["rows"]) for r in regions], dtype=np.int32)
+    out = np.zeros((nreg, nout))
+    keys = ("rows", "cols", "vals", "win", "wout")
+    tabs = [table([r[key] for r in regions]) for key in keys]
+    lib().orc_predict_regions(nreg, int(nthreads), _p(n), _p(ninp), _p(k), *tabs, nout, chunk_speedy, leakage,
+                              table(feedbacks), table(local_models), table(xs), _p(out),
+                              table([r["mean"] for r in regions]), table([r["std"] for r in regions]))
+    return out
 
 
 def predict_f32(rows, cols, vals_f32, win_col, win_val_f32, wout_f32, feedback, local_model, x, mean, std,

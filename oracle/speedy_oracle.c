@@ -658,6 +658,24 @@ void orc_predict(int n, int ninp, int k, const int *rows, const int *cols, const
     free(xa);
 }
 
+/* The CPU baseline's reservoir leg (bench.py cpu_baseline): orc_predict -- the
+ * reference's arithmetic, dense W_in matmul included -- for every region, OpenMP
+ * over regions (each region as the reference's per-region predict call,
+ * parallelmain.f90:225-234; the reference itself runs one region after another on
+ * each MPI rank).  Per-region arrays are passed as pointer tables; outvecs
+ * [nreg][nout]. */
+void orc_predict_regions(int nreg, int nthreads, const int *n, const int *ninp, const int *k,
+                         const int *const *rows, const int *const *cols, const double *const *vals,
+                         const double *const *win, const double *const *wout, int nout, int chunk_speedy,
+                         double leakage, const double *const *feedback, const double *const *local_model,
+                         double *const *x, double *outvecs, const double *const *mean, const double *const *std)
+{
+#pragma omp parallel for num_threads(nthreads) schedule(dynamic, 1)
+    for (int r = 0; r < nreg; ++r)
+        orc_predict(n[r], ninp[r], k[r], rows[r], cols[r], vals[r], win[r], wout[r], nout, chunk_speedy, leakage,
+                    feedback[r], local_model[r], x[r], outvecs + (size_t)r * nout, mean[r], std[r], 1);
+}
+
 /* Same as orc_predict but W_in given in compressed form (one column index and
  * value per row, the structure train_reservoir writes, mod_reservoir.f90:260-278)
  * and float32 weights (the NetCDF file precision, mod_io.f90:1282); products

@@ -78,3 +78,25 @@ def test_assemble_then_tile_reproduces_region_values():
         atmo = fb[:4 * ix * iy * 8].reshape(8, iy, ix, 4)
         np.testing.assert_array_equal(atmo[:, oy:oy + 2, 1:3, :].ravel(),
                                       ov[:128].reshape(8, 2, 2, 4).ravel())
+
+
+def test_predict_regions_openmp_equals_predict():
+    # the cpu_baseline's reservoir leg (orc_predict_regions) is orc_predict per region
+    regs, fbs, lms, xs, expect = [], [], [], [], []
+    for region, sst in ((3, True), (40, False), (700, True)):
+        w = region_weights(region, sst, n_override=500)
+        d = dict(rows=np.ascontiguousarray(w.rows, np.int32), cols=np.ascontiguousarray(w.cols, np.int32),
+                 vals=w.vals.astype(np.float64), win=np.ascontiguousarray(w.win, np.float64),
+                 wout=np.ascontiguousarray(w.wout, np.float64), mean=np.ascontiguousarray(w.mean, np.float64),
+                 std=np.ascontiguousarray(w.std, np.float64))
+        regs.append(d)
+        fbs.append(feedback_vector(region, w.ninp))
+        lms.append(local_model_vector(region))
+        x0 = initial_state(region, w.n)
+        xs.append(x0.copy())
+        expect.append(oracle.predict(d["rows"], d["cols"], d["vals"], d["win"], d["wout"], fbs[-1], lms[-1], x0,
+                                     d["mean"], d["std"]))
+    out = oracle.predict_regions(regs, fbs, lms, xs, nthreads=3)
+    for i, (o, x) in enumerate(expect):
+        np.testing.assert_array_equal(out[i], o)
+        np.testing.assert_array_equal(xs[i], x)
