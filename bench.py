@@ -376,8 +376,11 @@ def training_leg(dev, mask, args):
     """Supplementary measurement (BASELINE configs[4] shape on one GPU): W_out ridge
     training for a batch of 6000-node-class regions -- chunking_matmul Gram and
     cross products (hand-written fp64 MFMA kernel) over args.train_steps time steps
-    in 4 batches, then regularisation + batched Cholesky solve (rocSOLVER).
-    Roofline: Gram kernel flops / its time vs the measured fp64 MFMA rate."""
+    in 4 batches, then regularisation + the hand-written batched Cholesky solve
+    (k_chol_* / k_solve_*, replacing mldivide's dgesv, mod_linalg.f90:109-151).
+    Roofline: Gram kernel flops / its time, and the solve's algorithmic flops
+    (naug^3/3 potrf + 2 naug^2 nout for the two triangular solves) / its time, both
+    vs the measured fp64 MFMA rate."""
     import ctypes
 
     import torch
@@ -418,12 +421,24 @@ def training_leg(dev, mask, args):
     check(lib().sml_probe_mfma_f64(20000, ctypes.byref(peak)))
     tr.close()
     achieved = algo / (gram_ms * 1e-3) / 1e12
+    solve_algo = sum(n ** 3 / 3.0 + 2.0 * n * n * 136 for n in naug)
+    solve_tf = solve_algo / (solve_ms * 1e-3) / 1e12
     return {
         "workload": f"{len(naug)} regions (naug {min(naug)}..{max(naug)}), {m * nb} training steps in {nb} "
                     "chunking_matmul batches, then fit_chunk_hybrid regularisation + solve",
         "gram_ms": round(gram_ms, 3),
         "solve_ms": round(solve_ms, 3),
         "solve_info_ok": bool((info == 0).all()),
+        "solve_roofline": {
+            "kernels": "k_chol_diag / k_chol_panel / k_chol_update (right-looking, 128-blocked, fp64 MFMA) + "
+                       "k_solve_diag / k_solve_update (block forward / backward substitution)",
+            "bound": "mfma", "unit": "TFLOP/s",
+            "achieved": round(solve_tf, 2),
+            "peak": round(peak.value, 2),
+            "frac": round(solve_tf / peak.value, 4),
+            "algorithmic_flops": solve_algo,
+            "previous": "rocSOLVER dpotrf + dpotrs strided-batched: 333.9 ms for this workload (r02 bench)",
+        },
         "roofline": {
             "kernel": "k_train_gram (fp64 MFMA 16x16x4, 128x128 tiles, lower triangle + T S^T strip)",
             "bound": "mfma", "unit": "TFLOP/s",

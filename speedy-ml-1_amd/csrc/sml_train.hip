@@ -15,11 +15,15 @@
 // MFMA kernel (v_mfma_f64_16x16x4_f64) computes, for every region of the batch,
 // the lower-triangular 128x128 tiles of S S^T and the 136-row strip T S^T in one
 // launch; S and T are read once per tile pair from HBM through LDS.  The solve is
-// SPD (regularised Gram): rocSOLVER's batched Cholesky (potrf + potrs) on the
-// padded matrices -- the same solution as dgesv up to rounding x cond(G).
+// SPD (regularised Gram), so it is a Cholesky factorisation instead of dgesv's LU --
+// the same solution up to rounding x cond(G) -- written here for the batch
+// (right-looking, 128 x 128 blocks, in place on the padded column-major G):
+//   per block column k: k_chol_diag factors the diagonal block in LDS and inverts
+//   its triangle (one workgroup per region); k_chol_panel forms L_ik = A_ik L_kk^-T
+//   as a GEMM against that inverse; k_chol_update subtracts L_ik L_jk^T from every
+//   trailing tile (the n^3/3 flops, fp64 MFMA) -- then the two triangular solves
+//   against the 136 right-hand sides, block by block with the same GEMM tile.
 #include <hip/hip_runtime.h>
-#include <rocblas/rocblas.h>
-#include <rocsolver/rocsolver.h>
 
 #include <cmath>
 #include <cstring>
@@ -186,6 +190,189 @@ __global__ void k_train_wout(const double *__restrict__ X, const TrainRegion *__
     for (int o = 0; o < nout; ++o) w[o] = x[(size_t)o * npad];
 }
 
+// ------------------------------------------------------------ batched Cholesky
+// One 128 x 128 output tile (4 waves, wave (wr, wc) owns 64 x 64 = 4 x 4 MFMA tiles):
+//   O(r, c) = (accumulate ? O(r, c) : 0) + alpha * sum_{l < 128} A(r, l) B(c, l)
+// Operand layouts: AT / BT false: X(row, l) at p[l * ld + row] (rows contiguous, a
+// column-major block); true: X(row, l) at p[row * ld + l] (l contiguous, the block's
+// transpose).  Rows >= arows / brows read as zero and are not stored.  O is
+// column-major: O(r, c) at po[c * ldo + r].
+template <bool AT, bool BT>
+__device__ __forceinline__ void gemm128(const double *__restrict__ pa, long long lda, int arows,
+                                        const double *__restrict__ pb, long long ldb, int brows, double *po,
+                                        long long ldo, double alpha, bool accumulate) {
+    __shared__ double sA[kKC][kTile + kLdsPad];
+    __shared__ double sB[kKC][kTile + kLdsPad];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int wr = w >> 1, wc = w & 1, l16 = lane & 15, kk = lane >> 4;
+    // loader: column-major operands -> (row = tid & 127, l = (tid >> 7) + 2q);
+    // transposed ones -> (row = tid >> 1, l = 8 (tid & 1) + q): 64 contiguous bytes
+    const int nrow = tid & (kTile - 1), nl0 = tid >> 7;
+    const int trow = tid >> 1, tl0 = (tid & 1) * 8;
+    const int arow = AT ? trow : nrow, brow = BT ? trow : nrow;
+    const bool a_ok = arow < arows, b_ok = brow < brows;
+    double ra[kKC / 2], rb[kKC / 2];
+    auto fetch = [&](int t0) {
+#pragma unroll
+        for (int q = 0; q < kKC / 2; ++q) {
+            if (AT)
+                ra[q] = a_ok ? pa[(long long)arow * lda + t0 + tl0 + q] : 0.0;
+            else
+                ra[q] = a_ok ? pa[(long long)(t0 + nl0 + 2 * q) * lda + arow] : 0.0;
+            if (BT)
+                rb[q] = b_ok ? pb[(long long)brow * ldb + t0 + tl0 + q] : 0.0;
+            else
+                rb[q] = b_ok ? pb[(long long)(t0 + nl0 + 2 * q) * ldb + brow] : 0.0;
+        }
+    };
+    d4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = d4{0, 0, 0, 0};
+    fetch(0);
+    for (int t0 = 0; t0 < kTile; t0 += kKC) {
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < kKC / 2; ++q) {
+            sA[AT ? tl0 + q : nl0 + 2 * q][arow] = ra[q];
+            sB[BT ? tl0 + q : nl0 + 2 * q][brow] = rb[q];
+        }
+        __syncthreads();
+        if (t0 + kKC < kTile) fetch(t0 + kKC);
+#pragma unroll
+        for (int s = 0; s < kKC / 4; ++s) {
+            double a[4], b[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) a[i] = sA[4 * s + kk][wr * 64 + i * 16 + l16];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) b[j] = sB[4 * s + kk][wc * 64 + j * 16 + l16];
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[i][j] = MFMA64(a[i], b[j], acc[i][j]);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int row = wr * 64 + i * 16 + kk + 4 * q;
+                const int col = wc * 64 + j * 16 + l16;
+                if (row < arows && col < brows) {
+                    double *p = po + (long long)col * ldo + row;
+                    *p = (accumulate ? *p : 0.0) + alpha * acc[i][j][q];
+                }
+            }
+}
+
+constexpr int kDiagLd = kTile + 1;  // LDS row stride of the diagonal block (doubles)
+constexpr size_t kDiagLds = (size_t)(kTile * kDiagLd + kTile) * sizeof(double);
+
+// Diagonal block k of every region: A_kk = L_kk L_kk^T (potrf's unblocked step,
+// column by column) and X = L_kk^-1, both in one LDS array -- L in the lower
+// triangle, X^T in the strict upper triangle, diag(X) apart.  Step j scales L's
+// column j and finishes X's row j, then updates L's trailing triangle and X's rows
+// below j.  Thread (i = row, h = parity) walks row i's entries 2 at a time.
+// L_kk goes back to G (lower triangle), L_kk^-1 (column-major, zeros above the
+// diagonal) to linv for the panel GEMM and the triangular solves.  info: potrf's
+// (first non-positive pivot, 1-based global index).
+__global__ __launch_bounds__(256) void k_chol_diag(double *__restrict__ G, double *__restrict__ linv, int npad, int k,
+                                                   int *__restrict__ info) {
+    extern __shared__ double S[];  // S[i * kDiagLd + c]
+    double *xd = S + kTile * kDiagLd;
+    const int r = blockIdx.x, C = npad / kTile;
+    const int tid = threadIdx.x, i = tid & (kTile - 1), h = tid >> 7;
+    double *A = G + (size_t)r * npad * npad + (size_t)k * kTile * npad + (size_t)k * kTile;
+    for (int c = h; c < kTile; c += 2) S[i * kDiagLd + c] = c <= i ? A[(size_t)c * npad + i] : 0.0;
+    for (int j = 0; j < kTile; ++j) {
+        __syncthreads();
+        const double d = S[j * kDiagLd + j];
+        const double piv = sqrt(d), inv = 1.0 / piv;
+        if (tid == 0 && !(d > 0.0) && info[r] == 0) info[r] = k * kTile + j + 1;
+        __syncthreads();
+        if (h == 0) {
+            if (i > j) S[i * kDiagLd + j] *= inv;  // L(i, j)
+            else if (i == j) S[j * kDiagLd + j] = piv;
+        } else {
+            if (i < j) S[i * kDiagLd + j] *= inv;  // X(j, c = i), stored at S[c][j]
+            else if (i == j) xd[j] = inv;
+        }
+        __syncthreads();
+        if (i > j) {
+            const double lij = S[i * kDiagLd + j];
+            for (int l = j + 1 + h; l <= i; l += 2) S[i * kDiagLd + l] -= lij * S[l * kDiagLd + j];
+            for (int c = h; c < j; c += 2) S[c * kDiagLd + i] -= lij * S[c * kDiagLd + j];  // X(i, c)
+            if (h == 0) S[j * kDiagLd + i] -= lij * xd[j];                                  // X(i, j)
+        }
+    }
+    __syncthreads();
+    double *Li = linv + ((size_t)r * C + k) * kTile * kTile;
+    for (int c = h; c < kTile; c += 2) {
+        if (c <= i) A[(size_t)c * npad + i] = S[i * kDiagLd + c];
+        Li[(size_t)c * kTile + i] = c < i ? S[c * kDiagLd + i] : (c == i ? xd[i] : 0.0);
+    }
+}
+
+// L_ik = A_ik L_kk^-T for the blocks i > k below the diagonal (in place)
+__global__ __launch_bounds__(256) void k_chol_panel(double *__restrict__ G, const double *__restrict__ linv, int npad,
+                                                    int k) {
+    const int r = blockIdx.y, C = npad / kTile, i = k + 1 + blockIdx.x;
+    double *Gr = G + (size_t)r * npad * npad;
+    double *A = Gr + (size_t)k * kTile * npad + (size_t)i * kTile;
+    const double *Li = linv + ((size_t)r * C + k) * kTile * kTile;
+    gemm128<false, false>(A, npad, kTile, Li, kTile, kTile, A, npad, 1.0, false);
+}
+
+// trailing update A_ij -= L_ik L_jk^T for k < j <= i (the lower-triangle tiles)
+__global__ __launch_bounds__(256) void k_chol_update(double *__restrict__ G, int npad, int k) {
+    const int r = blockIdx.y;
+    const int idx = blockIdx.x;
+    int a = (int)((sqrt(8.0 * idx + 1.0) - 1.0) * 0.5);
+    while (a * (a + 1) / 2 > idx) --a;
+    while ((a + 1) * (a + 2) / 2 <= idx) ++a;
+    const int i = k + 1 + a, j = k + 1 + (idx - a * (a + 1) / 2);
+    double *Gr = G + (size_t)r * npad * npad;
+    const double *Lik = Gr + (size_t)k * kTile * npad + (size_t)i * kTile;
+    const double *Ljk = Gr + (size_t)k * kTile * npad + (size_t)j * kTile;
+    double *Aij = Gr + (size_t)j * kTile * npad + (size_t)i * kTile;
+    gemm128<false, false>(Lik, npad, kTile, Ljk, npad, kTile, Aij, npad, -1.0, true);
+}
+
+// Block k of the triangular solves on B (npad x nout per region, column-major),
+// output columns [128 blockIdx.x, +128):
+//   forward  (upper = 0): B_k = L_kk^-1 B_k        backward (upper = 1): B_k = L_kk^-T B_k
+__global__ __launch_bounds__(256) void k_solve_diag(const double *__restrict__ linv, double *__restrict__ B, int npad,
+                                                    int nout, int k, int upper) {
+    const int r = blockIdx.y, C = npad / kTile, o0 = blockIdx.x * kTile;
+    const double *Li = linv + ((size_t)r * C + k) * kTile * kTile;
+    double *Bk = B + (size_t)r * npad * nout + (size_t)o0 * npad + (size_t)k * kTile;
+    const int nb = min(kTile, nout - o0);
+    if (upper)
+        gemm128<true, true>(Li, kTile, kTile, Bk, npad, nb, Bk, npad, 1.0, false);
+    else
+        gemm128<false, true>(Li, kTile, kTile, Bk, npad, nb, Bk, npad, 1.0, false);
+}
+
+// forward: B_i -= L_ik B_k for i > k;  backward: B_i -= L_ki^T B_k for i < k
+__global__ __launch_bounds__(256) void k_solve_update(const double *__restrict__ G, double *__restrict__ B, int npad,
+                                                      int nout, int k, int upper) {
+    const int r = blockIdx.y, ot = (nout + kTile - 1) / kTile;
+    const int o0 = (blockIdx.x % ot) * kTile, t = blockIdx.x / ot;
+    const int i = upper ? t : k + 1 + t;
+    const double *Gr = G + (size_t)r * npad * npad;
+    double *Br = B + (size_t)r * npad * nout + (size_t)o0 * npad;
+    const int nb = min(kTile, nout - o0);
+    if (upper)  // A(r, l) = L(k kTile + l, i kTile + r): the transposed block (k, i)
+        gemm128<true, true>(Gr + (size_t)i * kTile * npad + (size_t)k * kTile, npad, kTile, Br + (size_t)k * kTile, npad,
+                            nb, Br + (size_t)i * kTile, npad, -1.0, true);
+    else
+        gemm128<false, true>(Gr + (size_t)k * kTile * npad + (size_t)i * kTile, npad, kTile, Br + (size_t)k * kTile,
+                             npad, nb, Br + (size_t)i * kTile, npad, -1.0, true);
+}
+
 }  // namespace
 
 struct sml_train {
@@ -194,8 +381,8 @@ struct sml_train {
     TrainRegion *d_regs = nullptr;
     double *d_G = nullptr, *d_B = nullptr;
     long long *d_wout_off = nullptr;
+    double *d_linv = nullptr;  // L_kk^-1 per region and block column (C x 128 x 128)
     int *d_info = nullptr;
-    rocblas_handle handle = nullptr;
     long long s_total = 0, t_total = 0;
     int last_m = -1;
 };
@@ -213,10 +400,9 @@ static void set_offsets(sml_train *t, int m, std::vector<TrainRegion> &h) {
 
 extern "C" int sml_train_destroy(sml_train *t) {
     if (!t) return SML_OK;
-    void *ptrs[] = {t->d_regs, t->d_G, t->d_B, t->d_wout_off, t->d_info};
+    void *ptrs[] = {t->d_regs, t->d_G, t->d_B, t->d_wout_off, t->d_info, t->d_linv};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
-    if (t->handle) rocblas_destroy_handle(t->handle);
     delete t;
     return SML_OK;
 }
@@ -245,7 +431,8 @@ extern "C" int sml_train_create(int nlocal, const int *naug, int nout, sml_train
     if ((e = hipMalloc(&t->d_G, g * 8)) != hipSuccess || (e = hipMalloc(&t->d_B, b * 8)) != hipSuccess ||
         (e = hipMalloc(&t->d_regs, nlocal * sizeof(TrainRegion))) != hipSuccess ||
         (e = hipMalloc(&t->d_wout_off, nlocal * sizeof(long long))) != hipSuccess ||
-        (e = hipMalloc(&t->d_info, nlocal * sizeof(int))) != hipSuccess) {
+        (e = hipMalloc(&t->d_info, nlocal * sizeof(int))) != hipSuccess ||
+        (e = hipMalloc(&t->d_linv, (size_t)nlocal * t->C * kTile * kTile * 8)) != hipSuccess) {
         sml_train_destroy(t);
         return fail(SML_ERR_NOMEM, "sml_train_create: %s (%.2f GB of Gram matrices)", hipGetErrorString(e),
                     g * 8e-9);
@@ -257,9 +444,11 @@ extern "C" int sml_train_create(int nlocal, const int *naug, int nout, sml_train
         off += (long long)nout * naug[i];
     }
     SML_HIP(hipMemcpy(t->d_wout_off, wo.data(), nlocal * sizeof(long long), hipMemcpyHostToDevice));
-    if (rocblas_create_handle(&t->handle) != rocblas_status_success) {
-        sml_train_destroy(t);
-        return fail(SML_ERR_STATE, "rocblas_create_handle failed");
+    static bool lds_set = false;
+    if (!lds_set) {
+        SML_HIP(hipFuncSetAttribute((const void *)k_chol_diag, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)kDiagLds));
+        lds_set = true;
     }
     *out = t;
     return sml_train_reset(t, nullptr);
@@ -306,14 +495,28 @@ extern "C" int sml_train_solve(sml_train *t, int ncs, double beta_res, double be
     hipLaunchKernelGGL(k_train_regularise, dim3((t->npad + 255) / 256, t->nlocal), dim3(256), 0, st, t->d_G, t->d_B,
                        t->d_regs, t->npad, t->nout, ncs, add_model, add_res, prior);
     SML_HIP(hipGetLastError());
-    if (rocblas_set_stream(t->handle, st) != rocblas_status_success) return fail(SML_ERR_STATE, "rocblas_set_stream");
-    const rocblas_stride sg = (rocblas_stride)t->npad * t->npad, sb = (rocblas_stride)t->npad * t->nout;
-    rocblas_status s = rocsolver_dpotrf_strided_batched(t->handle, rocblas_fill_lower, t->npad, t->d_G, t->npad, sg,
-                                                        t->d_info, t->nlocal);
-    if (s != rocblas_status_success) return fail(SML_ERR_STATE, "rocsolver_dpotrf_strided_batched: status %d", (int)s);
-    s = rocsolver_dpotrs_strided_batched(t->handle, rocblas_fill_lower, t->npad, t->nout, t->d_G, t->npad, sg, t->d_B,
-                                         t->npad, sb, t->nlocal);
-    if (s != rocblas_status_success) return fail(SML_ERR_STATE, "rocsolver_dpotrs_strided_batched: status %d", (int)s);
+    SML_HIP(hipMemsetAsync(t->d_info, 0, t->nlocal * sizeof(int), st));
+    const int C = t->C, nl = t->nlocal, npad = t->npad, nout = t->nout, ot = (nout + kTile - 1) / kTile;
+    for (int k = 0; k < C; ++k) {  // potrf: G = L L^T, right-looking by 128-column blocks
+        hipLaunchKernelGGL(k_chol_diag, dim3(nl), dim3(256), kDiagLds, st, t->d_G, t->d_linv, npad, k, t->d_info);
+        const int w = C - 1 - k;
+        if (w > 0) {
+            hipLaunchKernelGGL(k_chol_panel, dim3(w, nl), dim3(256), 0, st, t->d_G, t->d_linv, npad, k);
+            hipLaunchKernelGGL(k_chol_update, dim3(w * (w + 1) / 2, nl), dim3(256), 0, st, t->d_G, npad, k);
+        }
+    }
+    for (int k = 0; k < C; ++k) {  // potrs: L Y = B
+        hipLaunchKernelGGL(k_solve_diag, dim3(ot, nl), dim3(256), 0, st, t->d_linv, t->d_B, npad, nout, k, 0);
+        if (k < C - 1)
+            hipLaunchKernelGGL(k_solve_update, dim3((C - 1 - k) * ot, nl), dim3(256), 0, st, t->d_G, t->d_B, npad,
+                               nout, k, 0);
+    }
+    for (int k = C - 1; k >= 0; --k) {  // L^T X = Y
+        hipLaunchKernelGGL(k_solve_diag, dim3(ot, nl), dim3(256), 0, st, t->d_linv, t->d_B, npad, nout, k, 1);
+        if (k > 0)
+            hipLaunchKernelGGL(k_solve_update, dim3(k * ot, nl), dim3(256), 0, st, t->d_G, t->d_B, npad, nout, k, 1);
+    }
+    SML_HIP(hipGetLastError());
     hipLaunchKernelGGL(k_train_wout, dim3((t->npad + 255) / 256, t->nlocal), dim3(256), 0, st, t->d_B, t->d_regs,
                        t->npad, t->nout, t->d_wout_off, d_wout);
     SML_HIP(hipGetLastError());

@@ -1,8 +1,8 @@
 """GPU W_out training (sml_train_*) against the oracle.
 
 Gram / cross products: fp64 MFMA sums in a different order than the oracle's
-loops: max |err| <= 1e-12 x max |G| (GRAM_TOL).  Solve: rocSOLVER Cholesky vs the
-oracle's dgesv restatement; both solve the same SPD system, so they agree to
+loops: max |err| <= 1e-12 x max |G| (GRAM_TOL).  Solve: the hand-written batched
+Cholesky (k_chol_* / k_solve_*, 128-blocked) vs the oracle's dgesv restatement; both solve the same SPD system, so they agree to
 rounding x cond: on well-conditioned systems max |err| <= 1e-9 x max |W|
 (W_TOL); with the reference's default (ill-conditioned) betas the test checks the
 relative residual of the regularised system (RES_TOL)."""
@@ -128,3 +128,45 @@ def test_full_size_region(cuda):
     assert res <= RES_TOL, res
     tr.close()
     torch.cuda.synchronize()
+
+
+def test_solve_multi_block_matches_oracle(cuda):
+    """npad = 896: seven block columns -- panel, trailing update and both block
+    triangular solves run at every position; three regions of different naug
+    share the padded batch."""
+    from speedy_ml_amd.training import Trainer
+
+    naugs, nout, m = [777, 401, 640], 136, 1000
+    S, T = _data(naugs, nout, m, seed=11)
+    tr = Trainer(naugs, nout)
+    assert tr.npad == 896
+    _accumulate(tr, S, T, 2, cuda)
+    w, info = tr.solve(132, 0.3, 1.0, True, 0.5)
+    assert (info == 0).all()
+    views = tr.wout_views(w)
+    for i, n in enumerate(naugs):
+        Go = np.zeros((n, n))
+        Bo = np.zeros((n, nout))
+        oracle.train_accumulate(S[i], T[i], Go, Bo)
+        wo, oinfo = oracle.train_solve(Go, Bo, 132, 0.3, 1.0, True, 0.5)
+        assert oinfo == 0
+        got = views[i].cpu().numpy()
+        assert np.abs(got - wo).max() <= W_TOL * np.abs(wo).max(), (i, np.abs(got - wo).max())
+    tr.close()
+
+
+def test_solve_reports_the_first_non_positive_pivot(cuda):
+    """potrf's info: 1-based index of the first leading minor that is not positive
+    definite (a negative beta_res makes the regularised Gram indefinite)."""
+    from speedy_ml_amd.training import Trainer
+
+    naugs, nout, m = [300, 260], 136, 200
+    S, T = _data(naugs, nout, m, seed=21)
+    tr = Trainer(naugs, nout)
+    _accumulate(tr, S, T, 1, cuda)
+    _, info = tr.solve(132, -30.0, 1.0, False, 0.0)
+    for i, n in enumerate(naugs):
+        G = S[i].T @ S[i] + np.diag(np.where(np.arange(n) < 132, 1.0, -30.0))
+        first = next(j for j in range(1, n + 1) if np.linalg.eigvalsh(G[:j, :j]).min() <= 0.0)
+        assert info[i] == first, (i, info[i], first)
+    tr.close()
