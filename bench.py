@@ -62,8 +62,9 @@ def parse():
     p.add_argument("--speedy-cus", type=int, default=64,
                    help="with --overlap: CUs [0, N) for SPEEDY's stream, the rest for the reservoir's "
                         "(speedy_ml_amd/hybrid.py; 0 = no split)")
-    p.add_argument("--train-regions", type=int, default=8,
-                   help="regions in the supplementary W_out-training leg (0 = skip)")
+    p.add_argument("--train-regions", type=int, default=144,
+                   help="regions per rank in the supplementary W_out-training leg, one batch resident in HBM "
+                        "(144 x 8 ranks = all 1152; 0 = skip)")
     p.add_argument("--train-steps", type=int, default=4096, help="training time steps per region in that leg")
     p.add_argument("--reservoir-steps", type=int, default=50,
                    help="steps timed in the supplementary reservoir-only (configs[1]) leg (0 = skip)")
@@ -239,7 +240,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.cpu_threads > 0:
         cpu = cpu_baseline(nreg, mask, args.cpu_threads)
     speedy = speedy_leg(dev, world, rank, args) if args.speedy_steps > 0 else None
-    training = training_leg(dev, mask, args) if args.train_regions > 0 and world == 1 else None
+    training = training_leg(dev, mask, args, world, rank) if args.train_regions > 0 else None
 
     if rank == 0:
         steps_per_s = args.steps / dt
@@ -372,35 +373,42 @@ def speedy_leg(dev, world, rank, args):
     return out
 
 
-def training_leg(dev, mask, args):
-    """Supplementary measurement (BASELINE configs[4] shape on one GPU): W_out ridge
-    training for a batch of 6000-node-class regions -- chunking_matmul Gram and
-    cross products (hand-written fp64 MFMA kernel) over args.train_steps time steps
-    in 4 batches, then regularisation + the hand-written batched Cholesky solve
-    (k_chol_* / k_solve_*, replacing mldivide's dgesv, mod_linalg.f90:109-151).
-    Roofline: Gram kernel flops / its time, and the solve's algorithmic flops
-    (naug^3/3 potrf + 2 naug^2 nout for the two triangular solves) / its time, both
-    vs the measured fp64 MFMA rate."""
+def training_leg(dev, mask, args, world, rank):
+    """Supplementary measurement (BASELINE configs[4]: W_out training of all 1152
+    regions on 8 GPUs): every rank trains its own batch of args.train_regions
+    6000-node-class regions, resident in HBM at once (144 per rank = all 1152 on 8
+    ranks; no collective -- regions are independent, scaling weak).  Per batch:
+    chunking_matmul Gram and cross products (hand-written fp64 MFMA kernel) over
+    args.train_steps time steps in 4 batches, then regularisation + the hand-written
+    batched Cholesky solve (k_chol_* / k_solve_*, replacing mldivide's dgesv,
+    mod_linalg.f90:109-151).  Times are the max over ranks.  Roofline: Gram kernel
+    flops / its time, and the solve's algorithmic flops (naug^3/3 potrf + 2 naug^2
+    nout for the two triangular solves) / its time, both vs the measured fp64 MFMA
+    rate."""
     import ctypes
 
     import torch
+    import torch.distributed as dist
 
     from speedy_ml_amd import domain
     from speedy_ml_amd._lib import check, lib
     from speedy_ml_amd.training import Trainer
 
-    regions = [r * (1152 // args.train_regions) for r in range(args.train_regions)]
+    per = args.train_regions
+    regions = [(rank * per + i) % 1152 for i in range(per)]
     naug = [132 + domain.reservoir_sizes(r, bool(mask[r])).n for r in regions]
     nb = 4
     m = args.train_steps // nb
     gen = torch.Generator(device=dev)
-    gen.manual_seed(3)
+    gen.manual_seed(3 + rank)
     S = torch.tanh(torch.randn(sum(naug) * m, dtype=torch.float64, device=dev, generator=gen))
     T = torch.randn(len(naug) * m * 136, dtype=torch.float64, device=dev, generator=gen)
     tr = Trainer(naug)
     tr.accumulate(S, T, m)  # warm-up
     tr.reset()
     torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
     e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
     e0.record()
     for _ in range(nb):
@@ -409,8 +417,12 @@ def training_leg(dev, mask, args):
     _, info = tr.solve()
     e2.record()
     torch.cuda.synchronize()
-    gram_ms = e0.elapsed_time(e1)
-    solve_ms = e1.elapsed_time(e2)
+    times = torch.tensor([e0.elapsed_time(e1), e1.elapsed_time(e2)], dtype=torch.float64, device=dev)
+    ok = torch.tensor([float((info == 0).all())], device=dev)
+    if world > 1:
+        dist.all_reduce(times, op=dist.ReduceOp.MAX)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    gram_ms, solve_ms = (float(v) for v in times.cpu())
     npad = tr.npad
     # algorithmic flops: lower-triangle Gram (naug(naug+1)/2 dot products) + T S^T, 2 flops per FMA
     algo = sum(2.0 * (n * (n + 1) / 2 + 136 * n) * m * nb for n in naug)
@@ -420,15 +432,22 @@ def training_leg(dev, mask, args):
     peak = ctypes.c_double()
     check(lib().sml_probe_mfma_f64(20000, ctypes.byref(peak)))
     tr.close()
+    del S, T
+    torch.cuda.empty_cache()
     achieved = algo / (gram_ms * 1e-3) / 1e12
     solve_algo = sum(n ** 3 / 3.0 + 2.0 * n * n * 136 for n in naug)
     solve_tf = solve_algo / (solve_ms * 1e-3) / 1e12
     return {
-        "workload": f"{len(naug)} regions (naug {min(naug)}..{max(naug)}), {m * nb} training steps in {nb} "
-                    "chunking_matmul batches, then fit_chunk_hybrid regularisation + solve",
+        "workload": f"{len(naug)} regions per rank x {world} rank(s) (naug {min(naug)}..{max(naug)}, one batch "
+                    f"resident: {len(naug) * npad * npad * 8 / 1e9:.1f} GB of Gram matrices per GPU), "
+                    f"{m * nb} training steps in {nb} chunking_matmul batches, then fit_chunk_hybrid "
+                    "regularisation + solve",
+        "regions_per_s": round(world * len(naug) / ((gram_ms + solve_ms) * 1e-3), 2),
+        "scaling": "weak",
         "gram_ms": round(gram_ms, 3),
         "solve_ms": round(solve_ms, 3),
-        "solve_info_ok": bool((info == 0).all()),
+        "solve_ms_per_region": round(solve_ms / len(naug), 3),
+        "solve_info_ok": bool(ok.item() == 1.0),
         "solve_roofline": {
             "kernels": "k_chol_diag / k_chol_panel / k_chol_update (right-looking, 128-blocked, fp64 MFMA) + "
                        "k_solve_diag / k_solve_update (block forward / backward substitution)",
@@ -437,7 +456,8 @@ def training_leg(dev, mask, args):
             "peak": round(peak.value, 2),
             "frac": round(solve_tf / peak.value, 4),
             "algorithmic_flops": solve_algo,
-            "previous": "rocSOLVER dpotrf + dpotrs strided-batched: 333.9 ms for this workload (r02 bench)",
+            "previous": "rocSOLVER dpotrf + dpotrs strided-batched: 333.9 ms for 8 regions (41.7 ms per region), "
+                        "r02 bench",
         },
         "roofline": {
             "kernel": "k_train_gram (fp64 MFMA 16x16x4, 128x128 tiles, lower triangle + T S^T strip)",

@@ -25,7 +25,9 @@
 //   against the 136 right-hand sides, block by block with the same GEMM tile.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <vector>
@@ -43,6 +45,7 @@ constexpr int kTile = 128;  // C tile edge
 constexpr int kKC = 16;     // time steps per LDS stage
 constexpr int kLdsPad = 4;  // row padding (doubles) against bank conflicts
 constexpr int kStrip = 2;   // tile rows of the T S^T strip (nout <= 256)
+constexpr int kPanel = 8;   // block columns per Cholesky panel (default): trailing-update depth 1024
 
 struct TrainRegion {
     long long s_off, t_off;  // offsets of S (naug x m) and T (nout x m) in the batch buffers
@@ -191,76 +194,87 @@ __global__ void k_train_wout(const double *__restrict__ X, const TrainRegion *__
 }
 
 // ------------------------------------------------------------ batched Cholesky
-// One 128 x 128 output tile (4 waves, wave (wr, wc) owns 64 x 64 = 4 x 4 MFMA tiles):
-//   O(r, c) = (accumulate ? O(r, c) : 0) + alpha * sum_{l < 128} A(r, l) B(c, l)
-// Operand layouts: AT / BT false: X(row, l) at p[l * ld + row] (rows contiguous, a
-// column-major block); true: X(row, l) at p[row * ld + l] (l contiguous, the block's
-// transpose).  Rows >= arows / brows read as zero and are not stored.  O is
-// column-major: O(r, c) at po[c * ldo + r].
-template <bool AT, bool BT>
-__device__ __forceinline__ void gemm128(const double *__restrict__ pa, long long lda, int arows,
-                                        const double *__restrict__ pb, long long ldb, int brows, double *po,
-                                        long long ldo, double alpha, bool accumulate) {
-    __shared__ double sA[kKC][kTile + kLdsPad];
-    __shared__ double sB[kKC][kTile + kLdsPad];
+// Operand loader of the tile GEMM: a TM-row operand, kKC values of l per stage.
+// Column-major operands (T = false, X(row, l) at p[l * ld + row]): row = tid % TM,
+// l = tid / TM + (256 / TM) q -- rows contiguous across lanes; transposed ones
+// (T = true, X(row, l) at p[row * ld + l]): row = tid / (kKC / PER), l = PER
+// (tid % (kKC / PER)) + q -- PER contiguous values per lane.
+template <int TM, bool T>
+struct TileLoader {
+    static constexpr int PER = kKC * TM / 256;
+    __device__ static int row(int tid) { return T ? tid / (kKC / PER) : tid % TM; }
+    __device__ static int l(int tid, int q) { return T ? (tid % (kKC / PER)) * PER + q : tid / TM + (256 / TM) * q; }
+};
+
+// One TR x TC output tile (4 waves, wave (wr, wc) owns (TR/2) x (TC/2) = (TR/32) x
+// (TC/32) MFMA 16x16 tiles):
+//   O(r, c) = (accumulate ? O(r, c) : 0) + alpha * sum_{l < K} A(r, l) B(c, l)
+// A is TR x K, B is TC x K (K a multiple of 16) (layout flags AT / BT as TileLoader); rows >= arows /
+// brows read as zero and are not stored.  O is column-major: O(r, c) at
+// po[c * ldo + r].  128 x 128 tiles for the wide trailing update, 64-wide ones for
+// the narrow launches (panel, triangular solves), where one tile's MFMA chain is the
+// launch's latency.
+template <int TR, int TC, bool AT, bool BT>
+__device__ __forceinline__ void gemm_tile(const double *__restrict__ pa, long long lda, int arows,
+                                          const double *__restrict__ pb, long long ldb, int brows, double *po,
+                                          long long ldo, double alpha, bool accumulate, int K = kTile) {
+    using LA = TileLoader<TR, AT>;
+    using LB = TileLoader<TC, BT>;
+    constexpr int NI = TR / 32, NJ = TC / 32;
+    __shared__ double sA[kKC][TR + kLdsPad];
+    __shared__ double sB[kKC][TC + kLdsPad];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int wr = w >> 1, wc = w & 1, l16 = lane & 15, kk = lane >> 4;
-    // loader: column-major operands -> (row = tid & 127, l = (tid >> 7) + 2q);
-    // transposed ones -> (row = tid >> 1, l = 8 (tid & 1) + q): 64 contiguous bytes
-    const int nrow = tid & (kTile - 1), nl0 = tid >> 7;
-    const int trow = tid >> 1, tl0 = (tid & 1) * 8;
-    const int arow = AT ? trow : nrow, brow = BT ? trow : nrow;
+    const int arow = LA::row(tid), brow = LB::row(tid);
     const bool a_ok = arow < arows, b_ok = brow < brows;
-    double ra[kKC / 2], rb[kKC / 2];
+    double ra[LA::PER], rb[LB::PER];
     auto fetch = [&](int t0) {
 #pragma unroll
-        for (int q = 0; q < kKC / 2; ++q) {
-            if (AT)
-                ra[q] = a_ok ? pa[(long long)arow * lda + t0 + tl0 + q] : 0.0;
-            else
-                ra[q] = a_ok ? pa[(long long)(t0 + nl0 + 2 * q) * lda + arow] : 0.0;
-            if (BT)
-                rb[q] = b_ok ? pb[(long long)brow * ldb + t0 + tl0 + q] : 0.0;
-            else
-                rb[q] = b_ok ? pb[(long long)(t0 + nl0 + 2 * q) * ldb + brow] : 0.0;
+        for (int q = 0; q < LA::PER; ++q) {
+            const int l = t0 + LA::l(tid, q);
+            ra[q] = a_ok ? (AT ? pa[(long long)arow * lda + l] : pa[(long long)l * lda + arow]) : 0.0;
+        }
+#pragma unroll
+        for (int q = 0; q < LB::PER; ++q) {
+            const int l = t0 + LB::l(tid, q);
+            rb[q] = b_ok ? (BT ? pb[(long long)brow * ldb + l] : pb[(long long)l * ldb + brow]) : 0.0;
         }
     };
-    d4 acc[4][4];
+    d4 acc[NI][NJ];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < NI; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = d4{0, 0, 0, 0};
+        for (int j = 0; j < NJ; ++j) acc[i][j] = d4{0, 0, 0, 0};
     fetch(0);
-    for (int t0 = 0; t0 < kTile; t0 += kKC) {
+    for (int t0 = 0; t0 < K; t0 += kKC) {
         __syncthreads();
 #pragma unroll
-        for (int q = 0; q < kKC / 2; ++q) {
-            sA[AT ? tl0 + q : nl0 + 2 * q][arow] = ra[q];
-            sB[BT ? tl0 + q : nl0 + 2 * q][brow] = rb[q];
-        }
+        for (int q = 0; q < LA::PER; ++q) sA[LA::l(tid, q)][arow] = ra[q];
+#pragma unroll
+        for (int q = 0; q < LB::PER; ++q) sB[LB::l(tid, q)][brow] = rb[q];
         __syncthreads();
-        if (t0 + kKC < kTile) fetch(t0 + kKC);
+        if (t0 + kKC < K) fetch(t0 + kKC);
 #pragma unroll
         for (int s = 0; s < kKC / 4; ++s) {
-            double a[4], b[4];
+            double a[NI], b[NJ];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) a[i] = sA[4 * s + kk][wr * 64 + i * 16 + l16];
+            for (int i = 0; i < NI; ++i) a[i] = sA[4 * s + kk][wr * (TR / 2) + i * 16 + l16];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) b[j] = sB[4 * s + kk][wc * 64 + j * 16 + l16];
+            for (int j = 0; j < NJ; ++j) b[j] = sB[4 * s + kk][wc * (TC / 2) + j * 16 + l16];
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
+            for (int i = 0; i < NI; ++i)
 #pragma unroll
-                for (int j = 0; j < 4; ++j) acc[i][j] = MFMA64(a[i], b[j], acc[i][j]);
+                for (int j = 0; j < NJ; ++j) acc[i][j] = MFMA64(a[i], b[j], acc[i][j]);
         }
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < NI; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < NJ; ++j)
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                const int row = wr * 64 + i * 16 + kk + 4 * q;
-                const int col = wc * 64 + j * 16 + l16;
+                const int row = wr * (TR / 2) + i * 16 + kk + 4 * q;
+                const int col = wc * (TC / 2) + j * 16 + l16;
                 if (row < arows && col < brows) {
                     double *p = po + (long long)col * ldo + row;
                     *p = (accumulate ? *p : 0.0) + alpha * acc[i][j][q];
@@ -268,115 +282,221 @@ __device__ __forceinline__ void gemm128(const double *__restrict__ pa, long long
             }
 }
 
-constexpr int kDiagLd = kTile + 1;  // LDS row stride of the diagonal block (doubles)
-constexpr size_t kDiagLds = (size_t)(kTile * kDiagLd + kTile) * sizeof(double);
+constexpr int kDiagThreads = 1024;            // 8 threads per row of the diagonal block
+constexpr int kDiagLd = kTile + 1;            // LDS row stride (doubles)
+constexpr int kDiagH = kDiagThreads / kTile;  // entries of a row per thread stride
+constexpr size_t kDiagLds = (size_t)(kTile * kDiagLd + 2 * kTile) * sizeof(double);
 
 // Diagonal block k of every region: A_kk = L_kk L_kk^T (potrf's unblocked step,
 // column by column) and X = L_kk^-1, both in one LDS array -- L in the lower
-// triangle, X^T in the strict upper triangle, diag(X) apart.  Step j scales L's
-// column j and finishes X's row j, then updates L's trailing triangle and X's rows
-// below j.  Thread (i = row, h = parity) walks row i's entries 2 at a time.
+// triangle, X^T in the strict upper triangle, diag(L) and diag(X) apart.  Step j
+// scales L's column j and finishes X's row j, then updates L's trailing triangle
+// and X's rows below j.  Thread (i = row, h) walks row i's entries with stride 8,
+// four independent LDS reads in flight per chunk (the loop is LDS-latency bound).
 // L_kk goes back to G (lower triangle), L_kk^-1 (column-major, zeros above the
 // diagonal) to linv for the panel GEMM and the triangular solves.  info: potrf's
 // (first non-positive pivot, 1-based global index).
-__global__ __launch_bounds__(256) void k_chol_diag(double *__restrict__ G, double *__restrict__ linv, int npad, int k,
-                                                   int *__restrict__ info) {
+__global__ __launch_bounds__(kDiagThreads) void k_chol_diag(double *__restrict__ G, double *__restrict__ linv,
+                                                            int npad, int k, int *__restrict__ info) {
     extern __shared__ double S[];  // S[i * kDiagLd + c]
-    double *xd = S + kTile * kDiagLd;
+    double *ldg = S + kTile * kDiagLd, *xd = ldg + kTile;
     const int r = blockIdx.x, C = npad / kTile;
     const int tid = threadIdx.x, i = tid & (kTile - 1), h = tid >> 7;
     double *A = G + (size_t)r * npad * npad + (size_t)k * kTile * npad + (size_t)k * kTile;
-    for (int c = h; c < kTile; c += 2) S[i * kDiagLd + c] = c <= i ? A[(size_t)c * npad + i] : 0.0;
+    for (int c = h; c < kTile; c += kDiagH) S[i * kDiagLd + c] = c <= i ? A[(size_t)c * npad + i] : 0.0;
+    double *Si = S + i * kDiagLd;
     for (int j = 0; j < kTile; ++j) {
         __syncthreads();
         const double d = S[j * kDiagLd + j];
-        const double piv = sqrt(d), inv = 1.0 / piv;
-        if (tid == 0 && !(d > 0.0) && info[r] == 0) info[r] = k * kTile + j + 1;
-        __syncthreads();
-        if (h == 0) {
-            if (i > j) S[i * kDiagLd + j] *= inv;  // L(i, j)
-            else if (i == j) S[j * kDiagLd + j] = piv;
-        } else {
-            if (i < j) S[i * kDiagLd + j] *= inv;  // X(j, c = i), stored at S[c][j]
-            else if (i == j) xd[j] = inv;
+        const double inv = 1.0 / sqrt(d);
+        if (tid == 0) {
+            ldg[j] = sqrt(d);
+            xd[j] = inv;
+            if (!(d > 0.0) && info[r] == 0) info[r] = k * kTile + j + 1;
         }
+        if (h == 0 && i > j) Si[j] *= inv;  // L(i, j)
+        if (h == 1 && i < j) Si[j] *= inv;  // X(j, c = i), stored at S[c][j]
         __syncthreads();
-        if (i > j) {
-            const double lij = S[i * kDiagLd + j];
-            for (int l = j + 1 + h; l <= i; l += 2) S[i * kDiagLd + l] -= lij * S[l * kDiagLd + j];
-            for (int c = h; c < j; c += 2) S[c * kDiagLd + i] -= lij * S[c * kDiagLd + j];  // X(i, c)
-            if (h == 0) S[j * kDiagLd + i] -= lij * xd[j];                                  // X(i, j)
+        if (i <= j) continue;
+        const double lij = Si[j];
+        for (int l0 = j + 1 + h; l0 <= i; l0 += 4 * kDiagH) {  // L(i, l) -= L(i, j) L(l, j), j < l <= i
+            double a[4], b[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int l = l0 + u * kDiagH;
+                if (l <= i) {
+                    a[u] = Si[l];
+                    b[u] = S[l * kDiagLd + j];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (l0 + u * kDiagH <= i) Si[l0 + u * kDiagH] = a[u] - lij * b[u];
         }
+        for (int c0 = h; c0 < j; c0 += 4 * kDiagH) {  // X(i, c) -= L(i, j) X(j, c), c < j
+            double a[4], b[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int c = c0 + u * kDiagH;
+                if (c < j) {
+                    a[u] = S[c * kDiagLd + i];
+                    b[u] = S[c * kDiagLd + j];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (c0 + u * kDiagH < j) S[(c0 + u * kDiagH) * kDiagLd + i] = a[u] - lij * b[u];
+        }
+        if (h == kDiagH - 1) S[j * kDiagLd + i] -= lij * xd[j];  // X(i, j)
     }
     __syncthreads();
     double *Li = linv + ((size_t)r * C + k) * kTile * kTile;
-    for (int c = h; c < kTile; c += 2) {
-        if (c <= i) A[(size_t)c * npad + i] = S[i * kDiagLd + c];
+    for (int c = h; c < kTile; c += kDiagH) {
+        if (c <= i) A[(size_t)c * npad + i] = c < i ? S[i * kDiagLd + c] : ldg[i];
         Li[(size_t)c * kTile + i] = c < i ? S[c * kDiagLd + i] : (c == i ? xd[i] : 0.0);
     }
 }
 
-// L_ik = A_ik L_kk^-T for the blocks i > k below the diagonal (in place)
+// L_ik = A_ik L_kk^-T for the blocks i > k below the diagonal, in place: a block
+// owns 64 rows x all 128 columns (it reads the whole rows it overwrites)
 __global__ __launch_bounds__(256) void k_chol_panel(double *__restrict__ G, const double *__restrict__ linv, int npad,
                                                     int k) {
-    const int r = blockIdx.y, C = npad / kTile, i = k + 1 + blockIdx.x;
+    const int r = blockIdx.y, C = npad / kTile, i = k + 1 + (blockIdx.x >> 1), r0 = (blockIdx.x & 1) * 64;
     double *Gr = G + (size_t)r * npad * npad;
-    double *A = Gr + (size_t)k * kTile * npad + (size_t)i * kTile;
+    double *A = Gr + (size_t)k * kTile * npad + (size_t)i * kTile + r0;
     const double *Li = linv + ((size_t)r * C + k) * kTile * kTile;
-    gemm128<false, false>(A, npad, kTile, Li, kTile, kTile, A, npad, 1.0, false);
+    gemm_tile<64, 128, false, false>(A, npad, 64, Li, kTile, kTile, A, npad, 1.0, false);
 }
 
-// trailing update A_ij -= L_ik L_jk^T for k < j <= i (the lower-triangle tiles)
-__global__ __launch_bounds__(256) void k_chol_update(double *__restrict__ G, int npad, int k) {
-    const int r = blockIdx.y;
-    const int idx = blockIdx.x;
-    int a = (int)((sqrt(8.0 * idx + 1.0) - 1.0) * 0.5);
-    while (a * (a + 1) / 2 > idx) --a;
-    while ((a + 1) * (a + 2) / 2 <= idx) ++a;
-    const int i = k + 1 + a, j = k + 1 + (idx - a * (a + 1) / 2);
+// A_ij -= sum_{k0 <= k < k0 + kw} L_ik L_jk^T for the lower-triangle tiles j <= i
+// of block columns jlo <= j < jhi: one GEMM of depth 128 kw per tile (the block
+// columns of L are contiguous in the column-major G).
+__global__ __launch_bounds__(256) void k_chol_update(double *__restrict__ G, int npad, int k0, int kw, int jlo,
+                                                     int jhi) {
+    const int r = blockIdx.y, C = npad / kTile;
+    int idx = blockIdx.x, j = jlo;
+    while (j < jhi && idx >= C - j) idx -= C - j++;
+    if (j >= jhi) return;
+    const int i = j + idx;
     double *Gr = G + (size_t)r * npad * npad;
-    const double *Lik = Gr + (size_t)k * kTile * npad + (size_t)i * kTile;
-    const double *Ljk = Gr + (size_t)k * kTile * npad + (size_t)j * kTile;
+    const double *Lik = Gr + (size_t)k0 * kTile * npad + (size_t)i * kTile;
+    const double *Ljk = Gr + (size_t)k0 * kTile * npad + (size_t)j * kTile;
     double *Aij = Gr + (size_t)j * kTile * npad + (size_t)i * kTile;
-    gemm128<false, false>(Lik, npad, kTile, Ljk, npad, kTile, Aij, npad, -1.0, true);
+    gemm_tile<128, 128, false, false>(Lik, npad, kTile, Ljk, npad, kTile, Aij, npad, -1.0, true, kw * kTile);
 }
 
-// Block k of the triangular solves on B (npad x nout per region, column-major),
-// output columns [128 blockIdx.x, +128):
+static int update_tiles(int C, int jlo, int jhi) {
+    int n = 0;
+    for (int j = jlo; j < jhi; ++j) n += C - j;
+    return n;
+}
+
+// One 128 x kRhs tile of the triangular solves (all right-hand sides at once, so a
+// block of L is read once per pass): 4 waves stacked by rows, each 32 rows x kRhs
+// columns = 2 x 9 MFMA tiles;
+//   O(r, c) = (accumulate ? O(r, c) : 0) + alpha * sum_{l < K} A(r, l) B(c, l)
+// A as TileLoader<128, AT>; B(c, l) at pb[c * ldb + l] (a row range of the
+// right-hand sides), columns c >= nb read as zero and are not stored.
+constexpr int kRhs = 144;  // nout = 136 rounded up to the 16-wide MFMA tile
+template <bool AT>
+__device__ __forceinline__ void gemm_rhs(const double *__restrict__ pa, long long lda, const double *__restrict__ pb,
+                                         long long ldb, int nb, double *po, long long ldo, double alpha,
+                                         bool accumulate, int K = kTile) {
+    using LA = TileLoader<kTile, AT>;
+    constexpr int NJ = kRhs / 16, PB = kRhs * kKC / 256;
+    __shared__ double sA[kKC][kTile + kLdsPad];
+    __shared__ double sB[kKC][kRhs + kLdsPad];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, l16 = lane & 15, kk = lane >> 4;
+    const int arow = LA::row(tid);
+    double ra[LA::PER], rb[PB];
+    auto fetch = [&](int t0) {
+#pragma unroll
+        for (int q = 0; q < LA::PER; ++q) {
+            const int l = t0 + LA::l(tid, q);
+            ra[q] = AT ? pa[(long long)arow * lda + l] : pa[(long long)l * lda + arow];
+        }
+#pragma unroll
+        for (int q = 0; q < PB; ++q) {  // 16 lanes read one column's 16 contiguous values
+            const int idx = tid + 256 * q, c = idx >> 4;
+            rb[q] = c < nb ? pb[(long long)c * ldb + t0 + (idx & 15)] : 0.0;
+        }
+    };
+    d4 acc[2][NJ];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[i][j] = d4{0, 0, 0, 0};
+    fetch(0);
+    for (int t0 = 0; t0 < K; t0 += kKC) {
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < LA::PER; ++q) sA[LA::l(tid, q)][arow] = ra[q];
+#pragma unroll
+        for (int q = 0; q < PB; ++q) sB[(tid + 256 * q) & 15][(tid + 256 * q) >> 4] = rb[q];
+        __syncthreads();
+        if (t0 + kKC < K) fetch(t0 + kKC);
+#pragma unroll
+        for (int s = 0; s < kKC / 4; ++s) {
+            double a[2], b[NJ];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) a[i] = sA[4 * s + kk][w * 32 + i * 16 + l16];
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) b[j] = sB[4 * s + kk][j * 16 + l16];
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < NJ; ++j) acc[i][j] = MFMA64(a[i], b[j], acc[i][j]);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int row = w * 32 + i * 16 + kk + 4 * q, col = j * 16 + l16;
+                if (col < nb) {
+                    double *p = po + (long long)col * ldo + row;
+                    *p = (accumulate ? *p : 0.0) + alpha * acc[i][j][q];
+                }
+            }
+}
+
+// Block k of the triangular solves on B (npad x nout per region, column-major), in
+// place (one block reads the whole block row it overwrites):
 //   forward  (upper = 0): B_k = L_kk^-1 B_k        backward (upper = 1): B_k = L_kk^-T B_k
 __global__ __launch_bounds__(256) void k_solve_diag(const double *__restrict__ linv, double *__restrict__ B, int npad,
                                                     int nout, int k, int upper) {
-    const int r = blockIdx.y, C = npad / kTile, o0 = blockIdx.x * kTile;
+    const int r = blockIdx.y, C = npad / kTile;
     const double *Li = linv + ((size_t)r * C + k) * kTile * kTile;
-    double *Bk = B + (size_t)r * npad * nout + (size_t)o0 * npad + (size_t)k * kTile;
-    const int nb = min(kTile, nout - o0);
+    double *Bk = B + (size_t)r * npad * nout + (size_t)k * kTile;
     if (upper)
-        gemm128<true, true>(Li, kTile, kTile, Bk, npad, nb, Bk, npad, 1.0, false);
+        gemm_rhs<true>(Li, kTile, Bk, npad, nout, Bk, npad, 1.0, false);
     else
-        gemm128<false, true>(Li, kTile, kTile, Bk, npad, nb, Bk, npad, 1.0, false);
+        gemm_rhs<false>(Li, kTile, Bk, npad, nout, Bk, npad, 1.0, false);
 }
 
-// forward: B_i -= L_ik B_k for i > k;  backward: B_i -= L_ki^T B_k for i < k
+// Update of block rows ilo <= i < ihi by the solved block rows [k0, k0 + kw), one
+// GEMM of depth 128 kw per block row:
+//   forward:  B_i -= sum_k L_ik Y_k        backward: B_i -= sum_k L_ki^T X_k
 __global__ __launch_bounds__(256) void k_solve_update(const double *__restrict__ G, double *__restrict__ B, int npad,
-                                                      int nout, int k, int upper) {
-    const int r = blockIdx.y, ot = (nout + kTile - 1) / kTile;
-    const int o0 = (blockIdx.x % ot) * kTile, t = blockIdx.x / ot;
-    const int i = upper ? t : k + 1 + t;
+                                                      int nout, int k0, int kw, int ilo, int upper) {
+    const int r = blockIdx.y, i = ilo + (int)blockIdx.x;
     const double *Gr = G + (size_t)r * npad * npad;
-    double *Br = B + (size_t)r * npad * nout + (size_t)o0 * npad;
-    const int nb = min(kTile, nout - o0);
-    if (upper)  // A(r, l) = L(k kTile + l, i kTile + r): the transposed block (k, i)
-        gemm128<true, true>(Gr + (size_t)i * kTile * npad + (size_t)k * kTile, npad, kTile, Br + (size_t)k * kTile, npad,
-                            nb, Br + (size_t)i * kTile, npad, -1.0, true);
+    double *Br = B + (size_t)r * npad * nout;
+    if (upper)  // A(rr, l) = L(k0 kTile + l, i kTile + rr): the transposed blocks (k, i)
+        gemm_rhs<true>(Gr + (size_t)i * kTile * npad + (size_t)k0 * kTile, npad, Br + (size_t)k0 * kTile, npad, nout,
+                       Br + (size_t)i * kTile, npad, -1.0, true, kw * kTile);
     else
-        gemm128<false, true>(Gr + (size_t)k * kTile * npad + (size_t)i * kTile, npad, kTile, Br + (size_t)k * kTile,
-                             npad, nb, Br + (size_t)i * kTile, npad, -1.0, true);
+        gemm_rhs<false>(Gr + (size_t)k0 * kTile * npad + (size_t)i * kTile, npad, Br + (size_t)k0 * kTile, npad, nout,
+                        Br + (size_t)i * kTile, npad, -1.0, true, kw * kTile);
 }
 
 }  // namespace
 
 struct sml_train {
     int nlocal = 0, nout = 0, npad = 0, C = 0;
+    int panel = kPanel;
     std::vector<int> naug;
     TrainRegion *d_regs = nullptr;
     double *d_G = nullptr, *d_B = nullptr;
@@ -409,12 +529,13 @@ extern "C" int sml_train_destroy(sml_train *t) {
 
 extern "C" int sml_train_create(int nlocal, const int *naug, int nout, sml_train **out) {
     SML_REQUIRE(out && naug && nlocal > 0, "bad argument");
-    SML_REQUIRE(nout > 0 && nout <= kStrip * kTile, "nout must be in 1..256");
+    SML_REQUIRE(nout > 0 && nout <= kRhs, "nout must be in 1..144");
     *out = nullptr;
     sml_train *t = new (std::nothrow) sml_train();
     if (!t) return fail(SML_ERR_NOMEM, "host allocation failed");
     t->nlocal = nlocal;
     t->nout = nout;
+    if (const char *e = getenv("SML_CHOL_PANEL")) t->panel = std::max(1, atoi(e));  // tuning knob
     t->naug.assign(naug, naug + nlocal);
     int mx = 0;
     for (int i = 0; i < nlocal; ++i) {
@@ -496,25 +617,57 @@ extern "C" int sml_train_solve(sml_train *t, int ncs, double beta_res, double be
                        t->d_regs, t->npad, t->nout, ncs, add_model, add_res, prior);
     SML_HIP(hipGetLastError());
     SML_HIP(hipMemsetAsync(t->d_info, 0, t->nlocal * sizeof(int), st));
-    const int C = t->C, nl = t->nlocal, npad = t->npad, nout = t->nout, ot = (nout + kTile - 1) / kTile;
-    for (int k = 0; k < C; ++k) {  // potrf: G = L L^T, right-looking by 128-column blocks
-        hipLaunchKernelGGL(k_chol_diag, dim3(nl), dim3(256), kDiagLds, st, t->d_G, t->d_linv, npad, k, t->d_info);
-        const int w = C - 1 - k;
-        if (w > 0) {
-            hipLaunchKernelGGL(k_chol_panel, dim3(w, nl), dim3(256), 0, st, t->d_G, t->d_linv, npad, k);
-            hipLaunchKernelGGL(k_chol_update, dim3(w * (w + 1) / 2, nl), dim3(256), 0, st, t->d_G, npad, k);
+    const int C = t->C, nl = t->nlocal, npad = t->npad, nout = t->nout;
+    // potrf: G = L L^T over panels of t->panel block columns.  Inside a panel,
+    // left-looking: block column k first takes the update from the panel's earlier
+    // columns (depth 128 (k - p0)), then its diagonal factor and L_ik below it;
+    // after the panel, one right-looking update of the whole trailing matrix at
+    // depth 128 x panel.
+    const int P = t->panel;
+    for (int p0 = 0; p0 < C; p0 += P) {
+        const int p1 = std::min(C, p0 + P);
+        for (int k = p0; k < p1; ++k) {
+            if (k > p0)
+                hipLaunchKernelGGL(k_chol_update, dim3(C - k, nl), dim3(256), 0, st, t->d_G, npad, p0, k - p0, k,
+                                   k + 1);
+            hipLaunchKernelGGL(k_chol_diag, dim3(nl), dim3(kDiagThreads), kDiagLds, st, t->d_G, t->d_linv, npad, k,
+                               t->d_info);
+            if (k < C - 1)
+                hipLaunchKernelGGL(k_chol_panel, dim3(2 * (C - 1 - k), nl), dim3(256), 0, st, t->d_G, t->d_linv,
+                                   npad, k);
         }
+        if (p1 < C)
+            hipLaunchKernelGGL(k_chol_update, dim3(update_tiles(C, p1, C), nl), dim3(256), 0, st, t->d_G, npad, p0,
+                               p1 - p0, p1, C);
     }
-    for (int k = 0; k < C; ++k) {  // potrs: L Y = B
-        hipLaunchKernelGGL(k_solve_diag, dim3(ot, nl), dim3(256), 0, st, t->d_linv, t->d_B, npad, nout, k, 0);
-        if (k < C - 1)
-            hipLaunchKernelGGL(k_solve_update, dim3((C - 1 - k) * ot, nl), dim3(256), 0, st, t->d_G, t->d_B, npad,
-                               nout, k, 0);
+    // potrs, blocked by panels of P block rows: inside a panel, right-looking (block
+    // row k's diagonal inverse, then its update of the panel's remaining rows at
+    // depth 128 -- a handful of tiles per region, latency-bound, so the shortest
+    // chain); then the rows beyond the panel take the whole panel's update at depth
+    // 128 P (MFMA-bound).
+    for (int p0 = 0; p0 < C; p0 += P) {  // L Y = B
+        const int p1 = std::min(C, p0 + P);
+        for (int k = p0; k < p1; ++k) {
+            hipLaunchKernelGGL(k_solve_diag, dim3(1, nl), dim3(256), 0, st, t->d_linv, t->d_B, npad, nout, k, 0);
+            if (k + 1 < p1)
+                hipLaunchKernelGGL(k_solve_update, dim3(p1 - 1 - k, nl), dim3(256), 0, st, t->d_G, t->d_B, npad,
+                                   nout, k, 1, k + 1, 0);
+        }
+        if (p1 < C)
+            hipLaunchKernelGGL(k_solve_update, dim3(C - p1, nl), dim3(256), 0, st, t->d_G, t->d_B, npad, nout, p0,
+                               p1 - p0, p1, 0);
     }
-    for (int k = C - 1; k >= 0; --k) {  // L^T X = Y
-        hipLaunchKernelGGL(k_solve_diag, dim3(ot, nl), dim3(256), 0, st, t->d_linv, t->d_B, npad, nout, k, 1);
-        if (k > 0)
-            hipLaunchKernelGGL(k_solve_update, dim3(k * ot, nl), dim3(256), 0, st, t->d_G, t->d_B, npad, nout, k, 1);
+    for (int p1 = C; p1 > 0; p1 -= P) {  // L^T X = Y, panels from the bottom
+        const int p0 = std::max(0, p1 - P);
+        for (int k = p1 - 1; k >= p0; --k) {
+            hipLaunchKernelGGL(k_solve_diag, dim3(1, nl), dim3(256), 0, st, t->d_linv, t->d_B, npad, nout, k, 1);
+            if (k > p0)
+                hipLaunchKernelGGL(k_solve_update, dim3(k - p0, nl), dim3(256), 0, st, t->d_G, t->d_B, npad, nout, k,
+                                   1, p0, 1);
+        }
+        if (p0 > 0)
+            hipLaunchKernelGGL(k_solve_update, dim3(p0, nl), dim3(256), 0, st, t->d_G, t->d_B, npad, nout, p0,
+                               p1 - p0, 0, 1);
     }
     SML_HIP(hipGetLastError());
     hipLaunchKernelGGL(k_train_wout, dim3((t->npad + 255) / 256, t->nlocal), dim3(256), 0, st, t->d_B, t->d_regs,
