@@ -306,6 +306,94 @@ def main():
         dist.destroy_process_group()
 
 
+F64_VALU_PEAK_TF = 78.6  # MI355X fp64 vector (256 CUs x 4 SIMDs x 64 lanes x 2 flop / 4 clk x 2.4 GHz)
+F64_MFMA_PEAK_TF = 78.6  # v_mfma_f64_16x16x4: 2048 flop in 64 clk per SIMD (SQ_VALU_MFMA_BUSY_CYCLES / MFMAs = 64)
+
+
+def speedy_roofline(st, forcing, bc):
+    """The fused SPEEDY step's two kernels, measured live: per-phase durations from
+    the kernels' own wall_clock64 stamps (SML_DYN_STAMPS, a chained 26-step window,
+    median over blocks) and the work per dispatch from the committed counter pass
+    (profiles/speedy_pmc.json, tools/speedy_pmc.py: SQ_INSTS_VALU_*_F64 and
+    SQ_INSTS_VALU_MFMA_MOPS_F64; deterministic per dispatch).  Both kernels are
+    latency-bound (dependent f64 chains of one lane, one wave per SIMD; barriers
+    between phases), so `frac` is far below 1 by construction: the numbers say how
+    much of the occupied CUs' f64 issue / MFMA the step keeps busy."""
+    import ctypes
+
+    import numpy as np
+    import torch
+
+    from speedy_ml_amd._lib import lib
+    from speedy_ml_amd.dynamics import Dynamics
+
+    pmc_path = os.path.join(REPO, "profiles", "speedy_pmc.json")
+    pmc = json.load(open(pmc_path))["kernels"] if os.path.exists(pmc_path) else {}
+    os.environ["SML_DYN_STAMPS"] = "1"
+    try:
+        d = Dynamics()
+    finally:
+        del os.environ["SML_DYN_STAMPS"]
+    d.set_forcing(**forcing)
+    d.set_state(st)
+    d.set_physics(bc)
+    d.set_rad_state(None)
+    d.set_clock(1, True)
+    d.window(24)
+    d.window(24)
+    torch.cuda.synchronize()
+    buf = np.zeros((4, 96, 8), dtype=np.int64)
+    L = lib()
+    L.sml_dbg_dyn_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    rc = L.sml_dbg_dyn_stamps(d._h, buf.ctypes.data)
+    d.close()
+    if rc != 0:
+        return None
+
+    def phases(kern, names):
+        nb = int((buf[kern, :, 0] > 0).sum())
+        b = buf[kern, :nb].astype(np.float64) / 100.0  # wall_clock64 ticks at 100 MHz -> us
+        ph = {n: round(float(np.median(b[:, i + 1] - b[:, i])), 2) for i, n in enumerate(names)}
+        span = float(b[:, len(names)].max() - b[:, 0].min())
+        return nb, ph, round(span, 2)
+
+    nb_g, ph_g, span_g = phases(0, ["gridx", "gridpoint_and_phypar", "specx"])
+    nb_s, ph_s, span_s = phases(1, ["load", "specy", "combine", "tail", "inv_inputs", "gridy"])
+    g = pmc.get("k_st_gridspec", {})
+    spec_last, inv = pmc.get("k_st_spec", {}), pmc.get("k_st_inv", {})
+    valu_g = g.get("valu_f64_flops_per_dispatch")
+    specy_fl = spec_last.get("mfma_f64_flops_per_dispatch")  # specy (the launched-mode k_st_spec has no gridy)
+    gridy_fl = inv.get("mfma_f64_flops_per_dispatch")        # gridy (k_st_inv)
+    out = {"source": "phase stamps (live, chained window) + profiles/speedy_pmc.json (work per dispatch)",
+           "peak_f64_valu_tflops": F64_VALU_PEAK_TF, "peak_f64_mfma_tflops": F64_MFMA_PEAK_TF}
+    e = {"blocks": nb_g, "span_us": span_g, "phases_us": ph_g, "bound": "latency (per-lane f64 chains: FFTPACK "
+         "passes, phypar; one wave per SIMD)"}
+    if valu_g:
+        tf = valu_g / (span_g * 1e-6) / 1e12
+        occ = F64_VALU_PEAK_TF * nb_g / 256
+        e.update({"valu_f64_flops": valu_g, "achieved_tflops": round(tf, 3),
+                  "frac_of_occupied_cus": round(tf / occ, 4), "frac_of_chip": round(tf / F64_VALU_PEAK_TF, 5)})
+    out["k_st_gridspec"] = e
+    e = {"blocks": nb_s, "span_us": span_s, "phases_us": ph_s, "bound": "latency (phase chain with barriers)"}
+    if specy_fl and gridy_fl:
+        leg = specy_fl + gridy_fl
+        sy = specy_fl / (ph_s["specy"] * 1e-6) / 1e12
+        gy = gridy_fl / (ph_s["gridy"] * 1e-6) / 1e12
+        occ = F64_MFMA_PEAK_TF * nb_s / 256
+        e.update({
+            "legendre_mfma_flops": leg,
+            "achieved_tflops_kernel": round(leg / (span_s * 1e-6) / 1e12, 3),
+            "legendre_mfma_utilisation": {
+                "specy_tflops": round(sy, 3), "gridy_tflops": round(gy, 3),
+                "specy_frac_of_occupied_cus": round(sy / occ, 4), "gridy_frac_of_occupied_cus": round(gy / occ, 4),
+                "specy_frac_of_chip": round(sy / F64_MFMA_PEAK_TF, 5),
+                "gridy_frac_of_chip": round(gy / F64_MFMA_PEAK_TF, 5),
+                "step_frac_of_chip": round(leg / (span_s * 1e-6) / 1e12 / F64_MFMA_PEAK_TF, 5),
+            }})
+    out["k_st_spec"] = e
+    return out
+
+
 def speedy_leg(dev, world, rank, args):
     """Supplementary measurement: one SPEEDY dyn_step on the GPU without and with
     the physics (leapfrog step(2,2), HIP events, launched step by step and replayed
@@ -351,6 +439,7 @@ def speedy_leg(dev, world, rank, args):
     e1.record()
     torch.cuda.synchronize()
     out["window_ms_graph_physics"] = round(e0.elapsed_time(e1) / nwin, 4)
+    out["roofline"] = speedy_roofline(st, forcing, bc)
     out["note"] = ("step_ms_*: one dyn_step (grtend/sptend/implic/hordif/timint, 164 transforms; with physics + "
                    "phypar on level 1, 41 more transforms) launched alone; window_ms_graph_physics: the chained "
                    "26-step window (sml_dyn_window, one hipGraph) as the hybrid step runs it")
@@ -455,6 +544,7 @@ def training_leg(dev, mask, args, world, rank):
             "achieved": round(solve_tf, 2),
             "peak": round(peak.value, 2),
             "frac": round(solve_tf / peak.value, 4),
+            "frac_of_nominal_peak": round(solve_tf / F64_MFMA_PEAK_TF, 4),
             "algorithmic_flops": solve_algo,
             "previous": "rocSOLVER dpotrf + dpotrs strided-batched: 333.9 ms for 8 regions (41.7 ms per region), "
                         "r02 bench",
@@ -465,8 +555,10 @@ def training_leg(dev, mask, args, world, rank):
             "achieved": round(achieved, 2),
             "issued_tflops": round(issued / (gram_ms * 1e-3) / 1e12, 2),
             "peak": round(peak.value, 2),
-            "peak_source": "measured: back-to-back v_mfma_f64_16x16x4_f64 on every SIMD (sml_probe_mfma_f64)",
+            "peak_source": "measured: back-to-back v_mfma_f64_16x16x4_f64 on every SIMD (sml_probe_mfma_f64), the "
+                           "sustained rate under a full-chip MFMA load; nominal 78.6 TF/s (64 clk per MFMA at 2.4 GHz)",
             "frac": round(achieved / peak.value, 4),
+            "frac_of_nominal_peak": round(achieved / F64_MFMA_PEAK_TF, 4),
             "algorithmic_flops": algo,
         },
     }

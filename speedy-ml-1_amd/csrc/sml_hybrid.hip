@@ -30,6 +30,7 @@
 #include <new>
 #include <string>
 #include <thread>
+#include <cstdlib>
 #include <vector>
 
 #include "sml_internal.hpp"
@@ -277,11 +278,24 @@ extern "C" int sml_hybrid_create(sml_reservoirs *res, sml_dynamics *dyn, sml_com
     // and the reservoir the rest (sml_stream_create_cu_range)
     h->own_streams = true;
     if (h->overlap && speedy_cus > 0 && speedy_cus < ncu) {
-        void *s = nullptr, *m = nullptr;
-        if (int rc = sml_stream_create_cu_range(0, speedy_cus, &s)) return bail(rc);
-        h->side = (hipStream_t)s;
-        if (int rc = sml_stream_create_cu_range(speedy_cus, ncu - speedy_cus, &m)) return bail(rc);
-        h->main = (hipStream_t)m;
+        // SML_SPEEDY_CU_STRIDE=s (experiment): SPEEDY on the CUs c with c % s <
+        // speedy_cus s / ncu instead of the first speedy_cus
+        const char *ev = getenv("SML_SPEEDY_CU_STRIDE");
+        const int stride = ev ? atoi(ev) : 0;
+        if (stride > 1 && ncu % stride == 0 && (speedy_cus * stride) % ncu == 0) {
+            std::vector<uint32_t> ms((ncu + 31) / 32, 0u), mm((ncu + 31) / 32, 0u);
+            const int per = speedy_cus * stride / ncu;
+            for (int c = 0; c < ncu; ++c) (c % stride < per ? ms : mm)[c / 32] |= 1u << (c % 32);
+            if (hipExtStreamCreateWithCUMask(&h->side, (uint32_t)ms.size(), ms.data()) != hipSuccess ||
+                hipExtStreamCreateWithCUMask(&h->main, (uint32_t)mm.size(), mm.data()) != hipSuccess)
+                return bail(fail(SML_ERR_HIP, "CU-mask stream"));
+        } else {
+            void *s = nullptr, *m = nullptr;
+            if (int rc = sml_stream_create_cu_range(0, speedy_cus, &s)) return bail(rc);
+            h->side = (hipStream_t)s;
+            if (int rc = sml_stream_create_cu_range(speedy_cus, ncu - speedy_cus, &m)) return bail(rc);
+            h->main = (hipStream_t)m;
+        }
         if (int rc = sml_res_set_read_waves(res, 0)) return bail(rc);  // pacing pays only on shared CUs
     } else {
         if (hipStreamCreateWithFlags(&h->main, hipStreamNonBlocking) != hipSuccess)
