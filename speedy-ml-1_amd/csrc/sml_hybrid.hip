@@ -293,7 +293,10 @@ extern "C" int sml_hybrid_create(sml_reservoirs *res, sml_dynamics *dyn, sml_com
             void *s = nullptr, *m = nullptr;
             if (int rc = sml_stream_create_cu_range(0, speedy_cus, &s)) return bail(rc);
             h->side = (hipStream_t)s;
-            if (int rc = sml_stream_create_cu_range(speedy_cus, ncu - speedy_cus, &m)) return bail(rc);
+            // SML_RES_CUS=n (experiment): the reservoir on CUs [speedy_cus, speedy_cus + n) only
+            const char *er = getenv("SML_RES_CUS");
+            const int res_cus = er ? std::min(std::max(atoi(er), 1), ncu - speedy_cus) : ncu - speedy_cus;
+            if (int rc = sml_stream_create_cu_range(speedy_cus, res_cus, &m)) return bail(rc);
             h->main = (hipStream_t)m;
         }
         if (int rc = sml_res_set_read_waves(res, 0)) return bail(rc);  // pacing pays only on shared CUs

@@ -19,6 +19,7 @@ pytestmark = pytest.mark.gpu
 
 TOL = 1e-12
 CHAIN_TOL = 1e-9
+FUSED_TOL = 1e-11
 
 
 def _rel(a, b):
@@ -192,8 +193,12 @@ def test_host_tendencies_rejected_while_gpu_physics_on(dyn, dyn_golden):
 def test_fused_step_is_bitwise_the_unfused_step(pg, cuda, physics):
     """The fused step (k_st_inv, k_st_rows, [k_phys_add, specx], k_st_spec; chained
     across the steps of a window) and the 8/9-launch step evaluate the same
-    operations in the same order: a run of steps and windows must agree bit for bit
-    (state, radiation state, tendencies, geopotential)."""
+    operations in the same order.  The unfused step's Fourier transforms are the
+    iogrid / drop-in kernels (sml_spectral.hip: FFTPACK's separate multiplies and
+    adds, bit-exact with the reference's FFT) while the fused step's kernels contract
+    a*b + c within an expression into one FMA (sml_dynamics.hip, -ffp-contract=on),
+    so the two agree to rounding (FUSED_TOL per field and level after a run of steps
+    and two windows: state, radiation state, tendencies, geopotential)."""
     import os
 
     import torch
@@ -228,12 +233,19 @@ def test_fused_step_is_bitwise_the_unfused_step(pg, cuda, physics):
         out.append((d.get_state(), d.get_rad_state(), tend, phi))
         d.close()
     (a, ra, ta, pa), (b, rb, tb, pb) = out
+
+    def close(x, y):
+        x, y = np.asarray(x), np.asarray(y)
+        assert np.abs(x - y).max() <= FUSED_TOL * max(np.abs(y).max(), 1e-300), np.abs(x - y).max()
+
     for f in oracle.DYN_FIELDS:
-        np.testing.assert_array_equal(a[f], b[f])
+        for j in range(a[f].shape[0]):
+            close(a[f][j], b[f][j])
     for k in ra:
-        np.testing.assert_array_equal(ra[k], rb[k])
-    np.testing.assert_array_equal(ta, tb)
-    np.testing.assert_array_equal(pa, pb)
+        close(ra[k], rb[k])
+    for i in range(len(ta)):
+        close(ta[i], tb[i])
+    close(pa, pb)
 
 
 def test_window_graph_is_bitwise_the_launched_window(pg, cuda):
