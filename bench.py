@@ -277,7 +277,7 @@ def main():
             "last_window_safe": bool(safe),
             "finite": finite,
             "roofline": {
-                "kernel": (("k_res_readout<ml> (v_ml = W_out(:, ncs+1:) x~, GEMV, 8 rows per item; beside "
+                "kernel": (("k_res_readout<ml> (v_ml = W_out(:, ncs+1:) x~, GEMV, 17 rows per wave, 128-B-aligned rows; beside "
                             + (f"SPEEDY's window on the other {ncu - args.speedy_cus} CUs, unpaced"
                                if args.speedy_cus > 0 else "SPEEDY's window on shared CUs, paced at 2048 waves")
                             + "; the one-pass form on all CUs: reservoir_only.roofline_unpaced)")

@@ -28,6 +28,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <new>
+#include <type_traits>
 #include <vector>
 
 #include "sml_internal.hpp"
@@ -43,7 +44,11 @@ using namespace sml;
 
 namespace {
 
-constexpr int kRows = 8;        // W_out rows per wave in the readout
+constexpr int kLdAlign = 32;    // W_out / x_aug row stride multiple (columns)
+constexpr int kRows = 8;        // W_out rows per wave in the readout (nout_pad's multiple)
+constexpr int kRowsWide = 17;   // rows per wave when nout_pad = 17 w (w <= 8 waves)
+constexpr int kWideWaves = 2;   // waves per readout block with kRowsWide rows (a region = w / 2 blocks;
+                                // 2 / 4 / 8 waves measured: one-pass 0.638 / 0.644 / 0.696 ms)
 constexpr int kMaxNcs = 256;     // local-model length bound of the fused finish (132 in T30L8)
 constexpr int kMeanStd = 36;    // mean/std vector length (mod_reservoir.f90:1815-1846)
 constexpr int kTisrStride = 16; // packed tisr input: [nlocal][16]
@@ -323,30 +328,31 @@ enum ReadMode { kReadML = 0, kReadFinish = 1, kReadFull = 2 };
 // dot products of the wave's 8 W_out rows with x over columns [c0, c1) (16-B groups;
 // lanes own columns c0 + 4 lane + 256 t), reduced across the wave; x values outside
 // [x0, x1) are zero (fma(w, 0, s) == s), which matters only when ncs % 4 != 0
+template <int R>
 struct Rows {
-    double v[kRows];
+    double v[R];
 };
 
-template <typename WT, typename XF>
-__device__ __attribute__((always_inline)) inline Rows rows_dot(const WT *W, int ld, int lane, int c0, int c1,
+template <typename WT, int R, typename XF>
+__device__ __attribute__((always_inline)) inline Rows<R> rows_dot(const WT *W, int ld, int lane, int c0, int c1,
                                                                XF xload) {
     typedef typename Vec4<WT>::N V;
-    double acc[kRows];
+    double acc[R];
 #pragma unroll
-    for (int q = 0; q < kRows; ++q) acc[q] = 0.0;
+    for (int q = 0; q < R; ++q) acc[q] = 0.0;
 #pragma unroll 2
     for (int j = c0 + lane * 4; j < c1; j += 256) {
         const double4 xv = xload(j);
-        V w[kRows];
+        V w[R];
 #pragma unroll
-        for (int q = 0; q < kRows; ++q)  // streamed once per step: non-temporal, so W_out does not evict the
+        for (int q = 0; q < R; ++q)  // streamed once per step: non-temporal, so W_out does not evict the
 #if SML_READ_NT                          // window's data
             w[q] = __builtin_nontemporal_load(reinterpret_cast<const V *>(W + (size_t)q * ld + j));
 #else
             w[q] = *reinterpret_cast<const V *>(W + (size_t)q * ld + j);
 #endif
 #pragma unroll
-        for (int q = 0; q < kRows; ++q) {
+        for (int q = 0; q < R; ++q) {
             double s = acc[q];
             s = fma((double)w[q].x, xv.x, s);
             s = fma((double)w[q].y, xv.y, s);
@@ -358,10 +364,10 @@ __device__ __attribute__((always_inline)) inline Rows rows_dot(const WT *W, int 
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1)
 #pragma unroll
-        for (int q = 0; q < kRows; ++q) acc[q] += __shfl_xor(acc[q], off, 64);
-    Rows out;
+        for (int q = 0; q < R; ++q) acc[q] += __shfl_xor(acc[q], off, 64);
+    Rows<R> out;
 #pragma unroll
-    for (int q = 0; q < kRows; ++q) out.v[q] = acc[q];
+    for (int q = 0; q < R; ++q) out.v[q] = acc[q];
     return out;
 }
 
@@ -385,8 +391,8 @@ __device__ inline double unstd(double v, const double *ms, int l) {
     return v;
 }
 
-template <typename WT, int kMode>
-__global__ __launch_bounds__(256) void k_res_readout(const RegionDev *__restrict__ R, const WT *__restrict__ wout,
+template <typename WT, int kMode, int NR>
+__global__ __launch_bounds__(512) void k_res_readout(const RegionDev *__restrict__ R, const WT *__restrict__ wout,
                                                      const WT *__restrict__ wlm,
                                                      const double *__restrict__ xaug,
                                                      const double *__restrict__ local_model,
@@ -395,23 +401,27 @@ __global__ __launch_bounds__(256) void k_res_readout(const RegionDev *__restrict
                                                      double *__restrict__ outvec, int nout, int nout_pad, int ncs,
                                                      int groups, int nitems, int ipw) {
     // wave gw takes the items gw, gw + W, gw + 2W, .. (W waves; one item each unless
-    // the launch is paced): the waves in flight together work on consecutive items,
-    // so a region's row groups still share its x_aug in one XCD's L2
+    // the launch is paced): the waves in flight together work on consecutive items.
+    // NR = kRowsWide (17 rows a wave, 8 waves a region of 136 outputs): x_aug is read
+    // 8 times per region instead of 17, the waves of a block together; NR = kRows:
+    // 17 waves per region.  Either way a region's blocks are neighbours, kept on one
+    // XCD's L2 by the remap
     const int bs = xcd_remap(blockIdx.x, gridDim.x);
     const int lane = threadIdx.x & 63;
-    const int gw = bs * 4 + (threadIdx.x >> 6), nw = gridDim.x * 4;
+    const int wpb = blockDim.x >> 6;
+    const int gw = bs * wpb + (threadIdx.x >> 6), nw = gridDim.x * wpb;
     (void)ipw;
     for (int item = gw; item < nitems; item += nw) {
         const int r = item / groups, g = item % groups;
         const RegionDev rg = R[r];
         const int ld = rg.ld;
-        const WT *W = wout + rg.wout + (size_t)(g * kRows) * ld;
-        Rows ml{};
+        const WT *W = wout + rg.wout + (size_t)(g * NR) * ld;
+        Rows<NR> ml{};
         {   // v_ml: x~ from x_aug, columns ncs .. ld
             const double *xa = xaug + rg.xaug;
-            ml = rows_dot<WT>(W, ld, lane, ncs & ~3, ld, [=](int j) {
+            ml = rows_dot<WT, NR>(W, ld, lane, ncs & ~(kLdAlign - 1), ld, [=](int j) {
                 double4 xv = *reinterpret_cast<const double4 *>(xa + j);
-                if (j < ncs) {  // the group that straddles column ncs
+                if (j < ncs) {  // the groups below column ncs (from the aligned start)
                     if (j + 0 < ncs) xv.x = 0.0;
                     if (j + 1 < ncs) xv.y = 0.0;
                     if (j + 2 < ncs) xv.z = 0.0;
@@ -420,18 +430,18 @@ __global__ __launch_bounds__(256) void k_res_readout(const RegionDev *__restrict
                 return xv;
             });
         }
-        const int o0 = g * kRows;
+        const int o0 = g * NR;
         if (kMode == kReadML) {  // every lane holds all 8 sums after the butterfly; lane 0 writes them
             if (lane == 0) {
     #pragma unroll
-                for (int q = 0; q < kRows; ++q) part[(size_t)r * nout_pad + o0 + q] = ml.v[q];
+                for (int q = 0; q < NR; ++q) part[(size_t)r * nout_pad + o0 + q] = ml.v[q];
             }
         } else {  // kReadFull: lane q finishes row o0 + q with v_p (k_res_finish's sum) + v_ml
             const int o = o0 + lane;
-            if (lane < kRows && o < nout) {
+            if (lane < NR && o < nout) {
                 double vml = ml.v[0];  // static indices only: a lane-indexed pick would put the sums in scratch
     #pragma unroll
-                for (int q = 1; q < kRows; ++q)
+                for (int q = 1; q < NR; ++q)
                     if (lane == q) vml = ml.v[q];
                 const double vp = vp_sum(wlm + rg.wlm, nout_pad, local_model + (size_t)r * ncs, ncs, o);
                 outvec[(size_t)r * nout + o] = unstd(vp + vml, meanstd + (size_t)r * 2 * kMeanStd, outl[o]);
@@ -977,7 +987,10 @@ int res_create_impl(int numregions, int nlocal, const int *region_ids, const uns
             sml_res_destroy(c);
             return fail(SML_ERR_ARG, "region %d: ninp %d (1..65535)", i, c->ninp[i]);
         }
-        c->ld[i] = (chunk_speedy + n[i] + 3) / 4 * 4;
+        // W_out rows (and x_aug) padded to 32 columns: with the streamed columns starting
+        // at ncs & ~31, every 1 KB load of a wave is whole 128-B lines (no line fetched
+        // by two neighbouring loads)
+        c->ld[i] = (chunk_speedy + n[i] + kLdAlign - 1) / kLdAlign * kLdAlign;
         c->w_nz_cap[i] = n[i];
         RegionDev &r = c->rd[i];
         r.n = n[i];
@@ -1220,24 +1233,34 @@ void launch_readout(sml_reservoirs *c, const double *d_local_model, double *d_ou
                                (const double *)c->d_wlm, d_local_model, c->d_meanstd, c->d_outl, c->d_part,
                                d_outvec, c->nout, c->nout_pad, c->ncs, c->nlocal, d_raw);
     } else {
-        const int groups = c->nout_pad / kRows;
+        const bool wide = c->nout_pad % kRowsWide == 0 && c->nout_pad / kRowsWide <= 8;
+        const int rows = wide ? kRowsWide : kRows;
+        const int groups = c->nout_pad / rows;
         const int nitems = c->nlocal * groups;
+        const int wpb = wide ? kWideWaves : 4;  // waves per block
         // the v_ml half runs beside SPEEDY's window: c->read_waves > 0 caps its waves
         // (each takes a run of items) so it leaves HBM headroom for the window
         int ipw = 1;
         if (kMode == kReadML && c->read_waves > 0 && c->read_waves < nitems)
             ipw = (nitems + c->read_waves - 1) / c->read_waves;
         const int nwaves = (nitems + ipw - 1) / ipw;
-        const int nblocks = (nwaves + 3) / 4;
-        if (c->wdtype == SML_F32)
-            hipLaunchKernelGGL((k_res_readout<float, kMode>), dim3(nblocks), dim3(256), 0, st, c->d_rd,
-                               (const float *)c->d_wout, (const float *)c->d_wlm, c->d_xaug, d_local_model, c->d_meanstd,
+        const int nblocks = (nwaves + wpb - 1) / wpb;
+        auto go = [&](auto wt_tag, auto r_tag) {
+            using WT = decltype(wt_tag);
+            constexpr int R = decltype(r_tag)::value;
+            hipLaunchKernelGGL((k_res_readout<WT, kMode, R>), dim3(nblocks), dim3(64 * wpb), 0, st, c->d_rd,
+                               (const WT *)c->d_wout, (const WT *)c->d_wlm, c->d_xaug, d_local_model, c->d_meanstd,
                                c->d_outl, c->d_part, d_outvec, c->nout, c->nout_pad, c->ncs, groups, nitems, ipw);
-        else
-            hipLaunchKernelGGL((k_res_readout<double, kMode>), dim3(nblocks), dim3(256), 0, st, c->d_rd,
-                               (const double *)c->d_wout, (const double *)c->d_wlm, c->d_xaug, d_local_model,
-                               c->d_meanstd, c->d_outl, c->d_part, d_outvec, c->nout, c->nout_pad, c->ncs, groups,
-                               nitems, ipw);
+        };
+        using RW = std::integral_constant<int, kRowsWide>;
+        using RN = std::integral_constant<int, kRows>;
+        if (c->wdtype == SML_F32) {
+            if (wide) go(float{}, RW{});
+            else go(float{}, RN{});
+        } else {
+            if (wide) go(double{}, RW{});
+            else go(double{}, RN{});
+        }
     }
 }
 }  // namespace
