@@ -131,7 +131,10 @@ struct sml_dynamics {
         hipGraphExec_t exec = nullptr;
         double key[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         DynTables *tab[3] = {nullptr, nullptr, nullptr};
-    } wreplay[2];
+    } wreplay[4];  // [prepared entry (sml_dyn_run_model)][entry lradsw]
+    // while a run_model window is captured: the Fourier buffer its last k_st_spec fills
+    // with iogrid(31)'s gridy (spectral layout), else null
+    double *io_exit = nullptr;
 };
 
 namespace {
@@ -704,6 +707,9 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 #define MFMA64(a, b, c) __builtin_amdgcn_mfma_f64_16x16x4f64((a), (b), (c), 0, 0, 0)
 
 constexpr int kCW = 2 * kNX;                  // real coefficients (n, p) of one m
+// iogrid's field-major work layout, both directions: [u 8 | v 8 | t 8 | q 8 | ps]
+constexpr int kNIo = 4 * kKX + 1;
+constexpr int kNIoWind = 2 * kKX;
 constexpr int kSM = 5 * 2 * kKX * kCW;        // m-major state slice: [var 5][lev 2][k][cc] (ps at k = 0)
 // m-major Fourier coefficients, [m][lat][f][p]: a latitude row's fields are contiguous
 // per m (the row kernels' 16-B stores / loads coalesce across the fields' lanes) and
@@ -867,6 +873,80 @@ __device__ inline void gridy_m(const double *In, const GridyB &gb, double *__res
             }
         }
     }
+}
+
+// gridy_m with the spectral module's Fourier layout [f][lat][2 m + p] (k_gridy's
+// stores): iogrid(31)'s inverse Legendre of the io fields, fused into the window's
+// last per-m kernel (run_model)
+__device__ inline void gridy_io(const double *In, const GridyB &gb, double *__restrict__ varm, int m, int nf) {
+    const int wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const int l = threadIdx.x & 63, r = l & 15, kk = l >> 4;
+    for (int tile = wave; tile < (nf + 7) / 8; tile += nw) {
+        const int f0 = tile * 8;
+        const int fa = f0 + (r >> 1), p = r & 1;
+        const bool ok = fa < nf;
+        const double *a = In + (ok ? fa : 0) * kCW + p;
+        d4 acc00 = {0, 0, 0, 0}, acc01 = acc00, acc10 = acc00, acc11 = acc00;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const int n_odd = 2 * (4 * s + kk);
+            const int n_even = n_odd + 1;
+            const double a0 = ok ? a[2 * n_odd] : 0.0;
+            const double a1 = ok ? a[2 * n_even] : 0.0;
+            acc00 = MFMA64(a0, gb.b00[s], acc00);
+            acc01 = MFMA64(a0, gb.b01[s], acc01);
+            acc10 = MFMA64(a1, gb.b10[s], acc10);
+            acc11 = MFMA64(a1, gb.b11[s], acc11);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int row = kk + 4 * q;
+            const int f = f0 + (row >> 1);
+            if (f >= nf) continue;
+            double *vr = varm + (size_t)f * kVarmField + 2 * m + (row & 1);
+            {
+                const int j = r;
+                const double sym = acc00[q], asym = acc10[q];
+                vr[(kIL - 1 - j) * kMX2] = sym + asym;
+                vr[j * kMX2] = sym - asym;
+            }
+            const int j = 16 + r;
+            if (j < kIY) {
+                const double sym = acc01[q], asym = acc11[q];
+                vr[(kIL - 1 - j) * kMX2] = sym + asym;
+                vr[j * kMX2] = sym - asym;
+            }
+        }
+    }
+}
+
+// iogrid(31)'s k_io_prep at (coefficient cc, level k) from time level 1 of an m-major
+// state slice: uvspec of (vor, div), copies of t, tr, ps -> put(field, value) in the
+// io layout [u 8 | v 8 | t 8 | q 8 | ps] (the same expressions as uvspec_at)
+template <class TB, class Put>
+__device__ inline void io_prep_m(const double *Sst, const TB &tb, int k, int cc, Put put) {
+    const int n = cc >> 1, p = cc & 1;
+    auto vor = [&](int pp, int nn) { return Sst[smi(0, 1, k, 2 * nn + pp)]; };
+    auto div = [&](int pp, int nn) { return Sst[smi(1, 1, k, 2 * nn + pp)]; };
+    const double ux = tb.uvdx_n(n);
+    const double zp = p == 1 ? ux * vor(0, n) : -ux * vor(1, n);
+    const double zc = p == 1 ? ux * div(0, n) : -ux * div(1, n);
+    double a, b;
+    if (n == 0) {
+        a = zc - tb.uvdyp_n(0) * vor(p, 1);
+        b = zp + tb.uvdyp_n(0) * div(p, 1);
+    } else if (n == kNX - 1) {
+        a = tb.uvdym_n(n) * vor(p, kNTRUN1 - 1);
+        b = -tb.uvdym_n(n) * div(p, kNTRUN1 - 1);
+    } else {
+        b = -tb.uvdym_n(n) * div(p, n - 1) + tb.uvdyp_n(n) * div(p, n + 1) + zp;
+        a = tb.uvdym_n(n) * vor(p, n - 1) - tb.uvdyp_n(n) * vor(p, n + 1) + zc;
+    }
+    put(k, a);
+    put(kKX + k, b);
+    put(2 * kKX + k, Sst[smi(2, 1, k, cc)]);
+    put(3 * kKX + k, Sst[smi(3, 1, k, cc)]);
+    if (k == 0) put(4 * kKX, Sst[smi(4, 1, 0, cc)]);
 }
 
 // stage the m's forcing (phis, tcorh, qcorh: reference layout) into Fm[3][kCW]
@@ -1223,7 +1303,7 @@ __global__ __launch_bounds__(kSpecBlk) void k_st_spec(
     const double *__restrict__ tcorh, const double *__restrict__ qcorh, const DynTables *__restrict__ T, int j1,
     int j4, double dt, double alph, double rob, double wil, const double *__restrict__ pinv,
     double *__restrict__ varm_next, int next_j2, int n1, int nin, const double *__restrict__ tabm,
-    double *__restrict__ state_out, long long *dbg) {
+    double *__restrict__ state_out, double *__restrict__ io_varm, long long *dbg) {
     __shared__ double V[kVFm];            // this m's tables (TabM)
     __shared__ double S[kNInvMax * kCW];  // specy output [f][2 n + p]; then the next step's inputs
     __shared__ double sh[2][kKX][kCW];
@@ -1350,6 +1430,11 @@ __global__ __launch_bounds__(kSpecBlk) void k_st_spec(
     stamp(dbg, sk, 4);
     if (next_j2 <= 0) {  // the run of fused steps ends: the state straight into the reference layout
         for (int i = threadIdx.x; i < kSM; i += kSpecBlk) put_state(state_out, m, i, Sst[i]);
+        if (io_varm) {  // run_model: iogrid(31)'s k_io_prep + gridy of this m (block-uniform)
+            if (holds) io_prep_m(Sst, tb, k, cc, [&](int f, double v) { S[f * kCW + cc] = v; });
+            __syncthreads();
+            gridy_io(S, gridy_operands(pinv, m), io_varm, m, kNIo);
+        }
         return;  // block-uniform
     }
     {
@@ -1370,8 +1455,6 @@ __global__ __launch_bounds__(kSpecBlk) void k_st_spec(
 // ------------------------------------------------------------ iogrid(30/31)
 // ppo_iogrid.f90:497-601.  grid4d = variables3d(4, ix, il, kx) (T, u, v, q), logp(ix, il).
 // Field-major work layout of both directions: [u 8 | v 8 | t 8 | q 8 | ps] (33 fields).
-constexpr int kNIo = 4 * kKX + 1;
-constexpr int kNIoWind = 2 * kKX;
 
 
 // entry: vdspec's vds + spec, trunct, into time level 1 (:524-538)
@@ -1410,6 +1493,135 @@ __global__ void k_io_prep(const double *__restrict__ st, double *__restrict__ si
         sin_[(size_t)(3 * kKX + k) * kSF + c] = st[kOffTr + (size_t)k * kSF + c];
         if (k == 0) sin_[(size_t)(4 * kKX) * kSF + c] = st[kOffPs + c];
     }
+}
+
+// run_model's window entry in one launch per zonal wavenumber m (512 threads = 64
+// coefficients x 8 levels), after iogrid(30)'s specx: the same operations as
+//   specy (k_specy's tiling)  -> k_io_combine (vds / spec + trunct into level 1)
+//   -> k_io_prep (the safety check's inputs) -> k_state_to_m -> k_st_inv (the first
+//   step's inverse inputs + gridy)
+// which all stay inside one m.  vio: the io Fourier coefficients, kNIo fields in the
+// spectral module's layout; state: reference layout, level 1 written, level 2 read
+// into the m-major slice sm; chk: k_io_prep's output; varm: gridy for step(1, 1).
+__global__ __launch_bounds__(kSpecThreads) void k_io_entry(const double *__restrict__ vio,
+                                                           const double *__restrict__ pfwd,
+                                                           const double *__restrict__ wt, double *__restrict__ state,
+                                                           double *__restrict__ sm, double *__restrict__ chk,
+                                                           const double *__restrict__ phis,
+                                                           const DynTables *__restrict__ T,
+                                                           const double *__restrict__ pinv, double *__restrict__ varm,
+                                                           int n1, int nin) {
+    __shared__ double S[kNIo * kCW];  // specy output [f][2 n + p]
+    __shared__ double Sst[kSM];       // this m's state slice
+    __shared__ double In[kNInvMax * kCW];
+    __shared__ double Fm[kCW];
+    const int m = blockIdx.x, tid = threadIdx.x;
+    const int wave = tid >> 6, l = tid & 63, r = l & 15, kk = l >> 4;
+    // level 2 of the slice (k_state_to_m) and phis(m) first: plain loads
+    for (int i = tid; i < kSM; i += blockDim.x) {
+        const int cc = i % kCW, k = (i / kCW) % kKX, lev = (i / (kCW * kKX)) % 2, var = i / (2 * kKX * kCW);
+        if (lev != 1) continue;  // level 2 (lev index 1); level 1 comes from the combine
+        const int c = ci(cc & 1, m, cc >> 1);
+        double v = 0.0;
+        if (var < 4) {
+            const size_t off = var == 0 ? kOffVor : var == 1 ? kOffDiv : var == 2 ? kOffT : kOffTr;
+            v = state[off + ((size_t)kKX + k) * kSF + c];
+        } else if (k == 0) {
+            v = state[kOffPs + (size_t)kSF + c];
+        }
+        Sst[i] = v;
+    }
+    for (int cc = tid; cc < kCW; cc += blockDim.x) Fm[cc] = phis[ci(cc & 1, m, cc >> 1)];
+    // a) specy of the io fields (k_specy: a wave per 8 fields x Re/Im)
+    if (wave < (kNIo + 7) / 8) {
+        const int f0 = wave * 8;
+        const int fa = f0 + (r >> 1);
+        const bool ok = fa < kNIo;
+        const double *vr = vio + (size_t)(ok ? fa : 0) * kVarmField + 2 * m + (r & 1);
+        const double *pm = pfwd + (size_t)m * kNX * kIY;
+        d4 accS = {0, 0, 0, 0}, accD = accS;
+#pragma unroll
+        for (int s = 0; s < kIY / 4; ++s) {
+            const int j = 4 * s + kk;
+            double aS = 0.0, aD = 0.0;
+            if (ok) {
+                const double vn = vr[(kIL - 1 - j) * kMX2], vs = vr[j * kMX2];
+                aS = (vn + vs) * wt[j];
+                aD = (vn - vs) * wt[j];
+            }
+            accS = MFMA64(aS, pm[(2 * r) * kIY + j], accS);
+            accD = MFMA64(aD, pm[(2 * r + 1) * kIY + j], accD);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int row = kk + 4 * q;
+            const int f = f0 + (row >> 1);
+            if (f >= kNIo) continue;
+            S[f * kCW + 2 * (2 * r) + (row & 1)] = accS[q];
+            S[f * kCW + 2 * (2 * r + 1) + (row & 1)] = accD[q];
+        }
+    }
+    __syncthreads();
+    // b) k_io_combine: vdspec's vds + spec, trunct, into level 1 (ppo_iogrid.f90:524-538)
+    const GTab tb{T, m};
+    const int cc = tid & (kCW - 1), k = tid / kCW, n = cc >> 1, p = cc & 1, c = ci(p, m, n);
+    {
+        auto fl = [&](int f) { return [=](int pp, int nn) { return S[f * kCW + 2 * nn + pp]; }; };
+        const double trf = T->trfilt[n][m];
+        double vo, dv;
+        vds_gen(fl(k), fl(kKX + k), tb, n, p, &vo, &dv);
+        const double v0 = vo * trf, v1 = dv * trf, v2 = S[(2 * kKX + k) * kCW + cc] * trf,
+                     v3 = S[(3 * kKX + k) * kCW + cc] * trf;
+        Sst[smi(0, 1, k, cc)] = v0;
+        Sst[smi(1, 1, k, cc)] = v1;
+        Sst[smi(2, 1, k, cc)] = v2;
+        Sst[smi(3, 1, k, cc)] = v3;
+        state[kOffVor + (size_t)k * kSF + c] = v0;
+        state[kOffDiv + (size_t)k * kSF + c] = v1;
+        state[kOffT + (size_t)k * kSF + c] = v2;
+        state[kOffTr + (size_t)k * kSF + c] = v3;
+        if (k == 0) {
+            const double v4 = S[(4 * kKX) * kCW + cc] * trf;
+            Sst[smi(4, 1, 0, cc)] = v4;
+            state[kOffPs + c] = v4;
+        } else {
+            Sst[smi(4, 1, k, cc)] = 0.0;  // ps lives at k = 0 only (k_state_to_m)
+        }
+    }
+    __syncthreads();
+    // c) k_io_prep: uvspec of level 1 and copies -> the safety check's inputs
+    {
+        auto vor = [&](int pp, int nn) { return Sst[smi(0, 1, k, 2 * nn + pp)]; };
+        auto div = [&](int pp, int nn) { return Sst[smi(1, 1, k, 2 * nn + pp)]; };
+        const double ux = T->uvdx[n][m];
+        const double zp = p == 1 ? ux * vor(0, n) : -ux * vor(1, n);
+        const double zc = p == 1 ? ux * div(0, n) : -ux * div(1, n);
+        double a, b;
+        if (n == 0) {
+            a = zc - T->uvdyp[0][m] * vor(p, 1);
+            b = zp + T->uvdyp[0][m] * div(p, 1);
+        } else if (n == kNX - 1) {
+            a = T->uvdym[n][m] * vor(p, kNTRUN1 - 1);
+            b = -T->uvdym[n][m] * div(p, kNTRUN1 - 1);
+        } else {
+            b = -T->uvdym[n][m] * div(p, n - 1) + T->uvdyp[n][m] * div(p, n + 1) + zp;
+            a = T->uvdym[n][m] * vor(p, n - 1) - T->uvdyp[n][m] * vor(p, n + 1) + zc;
+        }
+        chk[(size_t)k * kSF + c] = a;
+        chk[(size_t)(kKX + k) * kSF + c] = b;
+        chk[(size_t)(2 * kKX + k) * kSF + c] = Sst[smi(2, 1, k, cc)];
+        chk[(size_t)(3 * kKX + k) * kSF + c] = Sst[smi(3, 1, k, cc)];
+        if (k == 0) chk[(size_t)(4 * kKX) * kSF + c] = Sst[smi(4, 1, 0, cc)];
+    }
+    // d) the m-major slice for the window's first k_st_spec (k_state_to_m)
+    {
+        double2 *dst = reinterpret_cast<double2 *>(sm + (size_t)m * kSM);
+        for (int i = tid; i < kSM / 2; i += blockDim.x) dst[i] = reinterpret_cast<const double2 *>(Sst)[i];
+    }
+    // e) k_st_inv: step(1, 1)'s inverse inputs (j2 = 1) and gridy
+    inv_inputs(Sst, In, Fm, tb, m, 1, n1, nin);
+    __syncthreads();
+    gridy_m(In, gridy_operands(pinv, m), varm, m, nin);
 }
 
 // entry safety check (:556-571): min / max of the re-gridded u, v, t, q.  One
@@ -1696,7 +1908,7 @@ int launch_step_fused(sml_dynamics *d, int j1, int j2, double dt, double alph, d
     hipLaunchKernelGGL(k_st_spec, dim3(kMX), dim3(kSpecBlk), 0, st, d->d_vfm, sd.pfwd, sd.wt, d->d_sm, d->d_tend,
                        d->d_phi, d->d_phis, d->d_tcorh, d->d_qcorh, T, j1, j4, dt, alph, rob, wil, sd.pinv, d->d_varm,
                        next_j2, n1, nin, d->d_tabm + (size_t)(d->d_tab - d->d_tabs) * kMX * kTabMDoubles, d->d_state,
-                       d->d_dbg);
+                       next_j2 > 0 ? nullptr : d->io_exit, d->d_dbg);
     SML_HIP(hipGetLastError());
     return SML_OK;
 }
@@ -1782,9 +1994,23 @@ extern "C" int sml_dyn_leapfrog(sml_dynamics *d, int nsteps, double dt, double a
 // (dyn_stloop.f90:37-56, at_gcm.f90:81), captured once as ONE hipGraph per
 // (entry lradsw, delt, alph, rob, wil, physics on, impint slots) and replayed with
 // a single launch, so the host thread never waits on the window's ~200 kernels.
+namespace {
+int window_impl(sml_dynamics *d, int nleap, double delt, double alph, double rob, double wil, void *stream,
+                bool prepared);
+}  // namespace
+
 extern "C" int sml_dyn_window(sml_dynamics *d, int nleap, double delt, double alph, double rob, double wil,
                               void *stream) {
     SML_REQUIRE(d && nleap >= 0 && delt > 0.0, "bad argument");
+    return window_impl(d, nleap, delt, alph, rob, wil, stream, false);
+}
+
+namespace {
+// prepared: the m-major state and step(1, 1)'s gridy output are already in place
+// (k_io_entry, fused path of sml_dyn_run_model), so the graph starts at the row
+// kernel of the first step
+int window_impl(sml_dynamics *d, int nleap, double delt, double alph, double rob, double wil, void *stream,
+                bool prepared) {
     const double dts[3] = {0.5 * delt, delt, 2.0 * delt};
     DynTables *tab[3];
     for (int i = 0; i < 3; ++i) {  // 4 cached slots hold all three tables at once
@@ -1792,8 +2018,9 @@ extern "C" int sml_dyn_window(sml_dynamics *d, int nleap, double delt, double al
         tab[i] = d->d_tab;
     }
     const bool entry = d->lradsw;
-    sml_dynamics::WindowReplay &r = d->wreplay[entry ? 1 : 0];
-    const double key[8] = {(double)nleap, delt, alph, rob, wil, d->phys_on ? 1.0 : 0.0, d->fused ? 1.0 : 0.0, 1.0};
+    sml_dynamics::WindowReplay &r = d->wreplay[(entry ? 1 : 0) + (prepared ? 2 : 0)];
+    const double key[8] = {(double)nleap, delt,  alph, rob, wil, d->phys_on ? 1.0 : 0.0, d->fused ? 1.0 : 0.0,
+                           prepared ? 2.0 : 1.0};
     if (!(r.exec && std::memcmp(key, r.key, sizeof key) == 0 && std::memcmp(tab, r.tab, sizeof tab) == 0)) {
         if (r.exec) {
             SML_HIP(hipGraphExecDestroy(r.exec));
@@ -1805,7 +2032,8 @@ extern "C" int sml_dyn_window(sml_dynamics *d, int nleap, double delt, double al
         // consecutive steps chained: each step's last kernel prepares the next one's
         // inverse transforms (j2 = 1 for step(1, 1), then 2)
         d->d_tab = tab[0];
-        int rc = launch_step(d, 1, 1, dts[0], alph, rob, wil, nullptr, entry, d->cap_stream, false, 2);
+        d->io_exit = prepared ? d->d_varm : nullptr;  // run_model: the exit's gridy in the last kernel
+        int rc = launch_step(d, 1, 1, dts[0], alph, rob, wil, nullptr, entry, d->cap_stream, prepared, 2);
         d->d_tab = tab[1];
         if (!rc) rc = launch_step(d, 1, 2, dts[1], alph, rob, wil, nullptr, entry, d->cap_stream, true, nleap > 0 ? 2 : 0);
         d->d_tab = tab[2];
@@ -1813,6 +2041,7 @@ extern "C" int sml_dyn_window(sml_dynamics *d, int nleap, double delt, double al
             rc = launch_step(d, 2, 2, dts[2], alph, rob, wil, nullptr, (1 + i) % kNstrad == 1, d->cap_stream, true,
                              i + 1 < nleap ? 2 : 0);
         hipError_t e = hipStreamEndCapture(d->cap_stream, &g);
+        d->io_exit = nullptr;
         if (rc) {
             if (g) (void)hipGraphDestroy(g);
             return rc;
@@ -1833,6 +2062,7 @@ extern "C" int sml_dyn_window(sml_dynamics *d, int nleap, double delt, double al
     if (nleap > 0) d->lradsw = (nleap % kNstrad == 1);
     return SML_OK;
 }
+}  // namespace
 
 extern "C" int sml_dyn_set_clock(sml_dynamics *d, int istep, int lradsw) {
     SML_REQUIRE(d, "null context");
@@ -1921,28 +2151,13 @@ namespace {
 // iogrid inverse half: level 1 -> G = [u 8 | v 8 | t 8 | q 8 | ps] grids
 }  // namespace
 
-extern "C" int sml_dyn_from_grid(sml_dynamics *d, const double *d_grid4d, const double *d_logp, double *d_minmax,
-                                 void *stream) {
-    SML_REQUIRE(d && d_grid4d && d_logp, "null argument");
-    hipStream_t st = (hipStream_t)stream;
-    const DynTables *T = d->d_tab;
-    if (d->chk_pending) {  // the previous check still reads d_chk
-        SML_HIP(hipStreamWaitEvent(st, d->ev_chk, 0));
-        d->chk_pending = false;
-    }
-    // entry (:503-518): real(4) copies, q clip, then vdspec kcos = 2 (x cosgr) on the
-    // winds and none on the rest: one specx launch reading variables3d / logp
-    if (int rc = spectral_specx_io(d->sp, d_grid4d, d_logp, d->d_varm, kNIoWind, st)) return rc;
-    if (int rc = spectral_specy(d->sp, d->d_varm, d->d_sfwd, kNIo, st)) return rc;
-    hipLaunchKernelGGL(k_io_combine, dim3((kMN + 127) / 128, kKX), dim3(128), 0, st, d->d_sfwd, d->d_state, T);
-    SML_HIP(hipGetLastError());
-    // the safety check (:556-571) reads the new state: its k_io_prep stays on st (the
-    // window overwrites the state), the rest of it runs on chk_stream beside the
-    // window.  A caller's d_minmax is ready in st's order; the internal one (nullptr)
-    // only for the next user of d_chk (which waits for it).
+namespace {
+// the safety check of iogrid(30) (ppo_iogrid.f90:556-571) from its spectral inputs in
+// d_chk (k_io_prep / k_io_entry, already on st): the re-grid and its min / max run on
+// chk_stream beside the window.  A caller's d_minmax is ready in st's order; the
+// internal one (nullptr) only for the next user of d_chk (which waits for it).
+int launch_io_check(sml_dynamics *d, hipStream_t st, double *d_minmax) {
     double *cs = d->d_chk, *cv = cs + (size_t)kNIo * kSF, *cg = cv + (size_t)kNIo * kVF;
-    hipLaunchKernelGGL(k_io_prep, dim3((kMN + 127) / 128, kKX), dim3(128), 0, st, d->d_state, cs, T);
-    SML_HIP(hipGetLastError());
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
     SML_HIP(hipStreamIsCapturing(st, &cap));
     hipStream_t cst = st;
@@ -1971,8 +2186,6 @@ extern "C" int sml_dyn_from_grid(sml_dynamics *d, const double *d_grid4d, const 
         SML_HIP(hipMemcpyAsync(d->h_mm, mm, 8 * sizeof(double), hipMemcpyDeviceToHost, cst));
         SML_HIP(hipEventRecord(d->ev_mm, cst));
         d->mm_issued = true;
-    }
-    if (cst != st) {
         SML_HIP(hipEventRecord(d->ev_chk, cst));
         d->chk_pending = true;
         if (d_minmax) {
@@ -1981,6 +2194,29 @@ extern "C" int sml_dyn_from_grid(sml_dynamics *d, const double *d_grid4d, const 
         }
     }
     return SML_OK;
+}
+}  // namespace
+
+extern "C" int sml_dyn_from_grid(sml_dynamics *d, const double *d_grid4d, const double *d_logp, double *d_minmax,
+                                 void *stream) {
+    SML_REQUIRE(d && d_grid4d && d_logp, "null argument");
+    hipStream_t st = (hipStream_t)stream;
+    const DynTables *T = d->d_tab;
+    if (d->chk_pending) {  // the previous check still reads d_chk
+        SML_HIP(hipStreamWaitEvent(st, d->ev_chk, 0));
+        d->chk_pending = false;
+    }
+    // entry (:503-518): real(4) copies, q clip, then vdspec kcos = 2 (x cosgr) on the
+    // winds and none on the rest: one specx launch reading variables3d / logp
+    if (int rc = spectral_specx_io(d->sp, d_grid4d, d_logp, d->d_varm, kNIoWind, st)) return rc;
+    if (int rc = spectral_specy(d->sp, d->d_varm, d->d_sfwd, kNIo, st)) return rc;
+    hipLaunchKernelGGL(k_io_combine, dim3((kMN + 127) / 128, kKX), dim3(128), 0, st, d->d_sfwd, d->d_state, T);
+    SML_HIP(hipGetLastError());
+    // the safety check (:556-571) reads the new state: its k_io_prep stays on st (the
+    // window overwrites the state), the rest of it beside the window
+    hipLaunchKernelGGL(k_io_prep, dim3((kMN + 127) / 128, kKX), dim3(128), 0, st, d->d_state, d->d_chk, T);
+    SML_HIP(hipGetLastError());
+    return launch_io_check(d, st, d_minmax);
 }
 
 extern "C" int sml_dyn_to_grid(sml_dynamics *d, double *d_grid4d, double *d_logp, void *stream) {
@@ -2010,16 +2246,39 @@ extern "C" int sml_dyn_run_model(sml_dynamics *d, const double *d_grid4d, const 
                                  void *stream) {
     SML_REQUIRE(d && d_grid4d && d_logp && d_fc4d && d_fc2d, "null argument");
     SML_REQUIRE(d_fc4d != d_grid4d && d_fc2d != d_logp, "the forecast must not overwrite the window's input");
+    SML_REQUIRE(nleap >= 0 && delt > 0.0, "bad argument");
     hipStream_t st = (hipStream_t)stream;
-    if (int rc = sml_dyn_from_grid(d, d_grid4d, d_logp, nullptr, stream)) return rc;
-    if (int rc = sml_dyn_window(d, nleap, delt, alph, rob, wil, stream)) return rc;
+    if (d->fused) {
+        // iogrid(30)'s specx, then ONE per-m launch for specy, the combine into level 1,
+        // the check's inputs, the m-major state and step(1, 1)'s gridy (k_io_entry);
+        // the window graph then starts at the first row kernel
+        if (d->chk_pending) {
+            SML_HIP(hipStreamWaitEvent(st, d->ev_chk, 0));
+            d->chk_pending = false;
+        }
+        if (int rc = spectral_specx_io(d->sp, d_grid4d, d_logp, d->d_vfm, kNIoWind, st)) return rc;
+        const SpectralDev sd = spectral_dev(d->sp);
+        const bool phys = d->phys_on;
+        hipLaunchKernelGGL(k_io_entry, dim3(kMX), dim3(kSpecThreads), 0, st, d->d_vfm, sd.pfwd, sd.wt, d->d_state,
+                           d->d_sm, d->d_chk, d->d_phis, d->d_tab, sd.pinv, d->d_varm, phys ? kNInv1P : kNInv1,
+                           phys ? kNInvP : kNInv);
+        SML_HIP(hipGetLastError());
+        if (int rc = launch_io_check(d, st, nullptr)) return rc;
+        if (int rc = window_impl(d, nleap, delt, alph, rob, wil, stream, true)) return rc;
+    } else {
+        if (int rc = sml_dyn_from_grid(d, d_grid4d, d_logp, nullptr, stream)) return rc;
+        if (int rc = sml_dyn_window(d, nleap, delt, alph, rob, wil, stream)) return rc;
+    }
     if (d->chk_pending) {  // the exit reads the check's min/max
         SML_HIP(hipStreamWaitEvent(st, d->ev_chk, 0));
         d->chk_pending = false;
     }
-    hipLaunchKernelGGL(k_io_prep, dim3((kMN + 127) / 128, kKX), dim3(128), 0, st, d->d_state, d->d_specin, d->d_tab);
-    SML_HIP(hipGetLastError());
-    if (int rc = spectral_gridy(d->sp, d->d_specin, d->d_varm, kNIo, st)) return rc;
+    if (!d->fused) {  // the fused window's last kernel did iogrid(31)'s prep + gridy already
+        hipLaunchKernelGGL(k_io_prep, dim3((kMN + 127) / 128, kKX), dim3(128), 0, st, d->d_state, d->d_specin,
+                           d->d_tab);
+        SML_HIP(hipGetLastError());
+        if (int rc = spectral_gridy(d->sp, d->d_specin, d->d_varm, kNIo, st)) return rc;
+    }
     return spectral_gridx_run_model_exit(d->sp, d->d_varm, d_fc4d, d_fc2d, kNIoWind,
                                          IoExit{0.000001, d->mm_last, d_grid4d, d_logp}, st);
 }

@@ -35,8 +35,6 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 
 #define MFMA64(a, b, c) __builtin_amdgcn_mfma_f64_16x16x4f64((a), (b), (c), 0, 0, 0)
 
-constexpr int kSpecField = kMX2 * kNX;  // 1984
-constexpr int kVarmField = kMX2 * kIL;  // 2976
 constexpr int kGridField = kIX * kIL;   // 4608
 constexpr int kJPad = 32;
 

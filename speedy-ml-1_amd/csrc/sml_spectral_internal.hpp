@@ -9,6 +9,10 @@ struct sml_spectral;
 
 namespace sml {
 
+// per-field sizes of the batched spectral buffers: spectral [nx][mx2], Fourier [il][mx2]
+constexpr int kSpecField = kMX2 * kNX;  // 1984
+constexpr int kVarmField = kMX2 * kIL;  // 2976
+
 struct SpectralDev {
     const double *gradx, *uvdx, *uvdym, *uvdyp, *vddym, *vddyp;  // [n][m] (gradx [m])
     const double *el2, *trfilt;                                   // [n][m]
