@@ -376,8 +376,10 @@ __device__ __attribute__((always_inline)) inline Rows<R> rows_dot(const WT *W, i
 template <typename WT>
 __device__ inline double vp_sum(const WT *__restrict__ wl, int nout_pad, const double *__restrict__ lm, int ncs,
                                 int o) {
+    // 12 column loads in flight per thread (one thread per output, ~2 waves per
+    // region): the sum stays sequential in j
     double s = 0.0;
-#pragma unroll 4
+#pragma unroll 12
     for (int j = 0; j < ncs; ++j) s = fma((double)wl[(size_t)j * nout_pad + o], lm[j], s);
     return s;
 }
