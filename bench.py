@@ -230,8 +230,8 @@ def main():
                    "algorithmic_bytes_per_launch": full_bytes, "readout_avg_ms": round(u_rd_s * 1e3, 4),
                    "update_avg_ms": round(float(np.mean(u_upd)), 4)}
         reservoir_only = {
-            "workload": "configs[1]: predict for all 1152 subdomains + RCCL outvec all-gather + assemble + "
-                        "re-tile (SPEEDY forecast grids held fixed)",
+            "workload": "configs[1]: predict for all 1152 subdomains + outvec exchange + assemble + re-tile "
+                        "(SPEEDY forecast grids held fixed)",
             "value": round(args.reservoir_steps / rdt, 3), "unit": "hybrid timesteps/s",
             "ms_per_step": round(rdt / args.reservoir_steps * 1e3, 4), "steps": args.reservoir_steps,
             "roofline_unpaced": unpaced}
@@ -259,8 +259,11 @@ def main():
             "data": "synthetic (seeded T30L8 state and boundary fields, random weights with the trained structure)",
             "config": {
                 "workload": f"configs[{2 if world == 1 else 3}]: full hybrid timestep -- reservoir predict for all "
-                            "1152 subdomains, RCCL outvec all-gather, assemble, SPEEDY 6-h window (iogrid(30), "
-                            "stepone + 24 leapfrog dyn_steps with phypar physics, iogrid(31)) on the GPU, re-tile",
+                            "1152 subdomains, "
+                            + ("outvec exchange (identity on one GPU)" if world == 1 else
+                               f"outvec all-gather over RCCL ({world} ranks)")
+                            + ", assemble, SPEEDY 6-h window (iogrid(30), stepone + 24 leapfrog dyn_steps with "
+                              "phypar physics, iogrid(31)) on the GPU, re-tile",
                 "regions": nreg,
                 "regions_per_gpu": len(regions),
                 "reservoir_nodes": "5760/6160/6048/5880 (NINT(6000/ninp)*ninp)",
