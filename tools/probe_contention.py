@@ -68,6 +68,7 @@ def window_ms(partner, reps=8):
 
 def begin():
     res.predict_begin(fb, stream=main)
+    res.predict_finish(lm, ov, stream=main)  # (small) closes the split step
 
 
 def copy():
