@@ -120,3 +120,49 @@ def test_safety_thresholds_match_iogrid(cuda, dyn):
         mm = base.copy()
         mm[i] = v
         assert lib().sml_dyn_is_safe(ptr(mm)) == int(ok), (i, v)
+
+
+def test_fused_and_unfused_run_model_agree(cuda):
+    """sml_dyn_run_model's fused form (k_io_entry + the prepared window graph with
+    iogrid(31)'s prep / gridy in its last kernel) against the unfused chain
+    (SML_DYN_FUSED=0: from_grid, the 8/9-launch steps, k_io_prep + gridy + gridx):
+    the unfused steps' Fourier transforms are FFTPACK's separate multiplies and
+    adds, the fused ones contract a*b + c, so the forecasts agree to rounding
+    (UNFUSED_TOL x max |field| per variable and level after 6 leapfrog steps)."""
+    import os
+
+    import torch
+
+    from speedy_ml_amd.dynamics import Dynamics
+    from speedy_ml_amd.synthetic import dyn_state, phys_boundary
+
+    UNFUSED_TOL = 1e-11
+    g4, g2 = _grids(seed=17)
+    dg4, dg2 = _t(g4, cuda), _t(g2, cuda)
+    outs = []
+    for fused in ("1", "0"):
+        os.environ["SML_DYN_FUSED"] = fused
+        try:
+            d = Dynamics()
+        finally:
+            os.environ.pop("SML_DYN_FUSED", None)
+        st0, forcing = dyn_state()
+        d.set_forcing(**forcing)
+        d.set_state(st0)
+        d.set_physics(phys_boundary(d, forcing["phis"]))
+        d.set_rad_state(None)
+        d.set_clock(1, True)
+        f4 = torch.zeros_like(dg4)
+        f2 = torch.zeros_like(dg2)
+        d.run_model(dg4, dg2, f4, f2, nleap=6)
+        safe, _ = d.last_safe()
+        torch.cuda.synchronize()
+        outs.append((f4.cpu().numpy(), f2.cpu().numpy(), safe))
+        d.close()
+    (a4, a2, sa), (b4, b2, sb) = outs
+    assert sa and sb
+    for v in range(4):
+        for k in range(8):
+            ref = np.abs(b4[k, :, :, v]).max()
+            assert np.abs(a4[k, :, :, v] - b4[k, :, :, v]).max() <= UNFUSED_TOL * ref, (v, k)
+    assert np.abs(a2 - b2).max() <= UNFUSED_TOL * np.abs(b2).max()
