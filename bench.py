@@ -273,7 +273,8 @@ def main():
                                + (f" [DIAGNOSTIC: rank 0 of {sim} simulated ranks, exchange local]" if sim > 1 else ""),
                 "speedy": "T30L8, 26 dyn_steps per window (nsteps 96/day, delt 900 s), physics on, "
                           "shortwave every 3rd step",
-                "streams": (f"overlapped: SPEEDY on CUs [0, {args.speedy_cus}), reservoir on the rest"
+                "streams": (f"overlapped: SPEEDY on CUs [0, {args.speedy_cus}), reservoir on CUs [{args.speedy_cus}, "
+                            f"{args.speedy_cus + min(ncu - args.speedy_cus, ncu * 5 // 8)})"
                             if args.overlap and args.speedy_cus > 0 else
                             "overlapped, no CU split" if args.overlap else "one stream"),
             },
@@ -281,7 +282,8 @@ def main():
             "finite": finite,
             "roofline": {
                 "kernel": (("k_res_readout<ml> (v_ml = W_out(:, ncs+1:) x~, GEMV, 17 rows per wave, 128-B-aligned rows; beside "
-                            + (f"SPEEDY's window on the other {ncu - args.speedy_cus} CUs, unpaced"
+                            + (f"SPEEDY's window on {min(ncu - args.speedy_cus, ncu * 5 // 8)} CUs of their own (less HBM pressure "
+                               "on the window than all of the rest), unpaced"
                                if args.speedy_cus > 0 else "SPEEDY's window on shared CUs, paced at 2048 waves")
                             + "; the one-pass form on all CUs: reservoir_only.roofline_unpaced)")
                            if args.overlap else

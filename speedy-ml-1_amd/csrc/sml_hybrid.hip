@@ -275,30 +275,21 @@ extern "C" int sml_hybrid_create(sml_reservoirs *res, sml_dynamics *dyn, sml_com
         return bail(fail(SML_ERR_HIP, "no device"));
     // streams: non-default (the legacy NULL stream would serialise the two chains);
     // with overlap and 0 < speedy_cus < CUs, SPEEDY's chain gets CUs [0, speedy_cus)
-    // and the reservoir the rest (sml_stream_create_cu_range)
+    // and the reservoir a disjoint range after it (sml_stream_create_cu_range)
     h->own_streams = true;
     if (h->overlap && speedy_cus > 0 && speedy_cus < ncu) {
-        // SML_SPEEDY_CU_STRIDE=s (experiment): SPEEDY on the CUs c with c % s <
-        // speedy_cus s / ncu instead of the first speedy_cus
-        const char *ev = getenv("SML_SPEEDY_CU_STRIDE");
-        const int stride = ev ? atoi(ev) : 0;
-        if (stride > 1 && ncu % stride == 0 && (speedy_cus * stride) % ncu == 0) {
-            std::vector<uint32_t> ms((ncu + 31) / 32, 0u), mm((ncu + 31) / 32, 0u);
-            const int per = speedy_cus * stride / ncu;
-            for (int c = 0; c < ncu; ++c) (c % stride < per ? ms : mm)[c / 32] |= 1u << (c % 32);
-            if (hipExtStreamCreateWithCUMask(&h->side, (uint32_t)ms.size(), ms.data()) != hipSuccess ||
-                hipExtStreamCreateWithCUMask(&h->main, (uint32_t)mm.size(), mm.data()) != hipSuccess)
-                return bail(fail(SML_ERR_HIP, "CU-mask stream"));
-        } else {
-            void *s = nullptr, *m = nullptr;
-            if (int rc = sml_stream_create_cu_range(0, speedy_cus, &s)) return bail(rc);
-            h->side = (hipStream_t)s;
-            // SML_RES_CUS=n (experiment): the reservoir on CUs [speedy_cus, speedy_cus + n) only
-            const char *er = getenv("SML_RES_CUS");
-            const int res_cus = er ? std::min(std::max(atoi(er), 1), ncu - speedy_cus) : ncu - speedy_cus;
-            if (int rc = sml_stream_create_cu_range(speedy_cus, res_cus, &m)) return bail(rc);
-            h->main = (hipStream_t)m;
-        }
+        void *s = nullptr, *m = nullptr;
+        if (int rc = sml_stream_create_cu_range(0, speedy_cus, &s)) return bail(rc);
+        h->side = (hipStream_t)s;
+        // the reservoir on CUs [speedy_cus, speedy_cus + res_cus): 5/8 of the chip by
+        // default (160 of 256).  Its begin (update + v_ml readout) still ends well
+        // inside the window, and the lower HBM pressure slows the window less
+        // (783 -> 789 steps/s vs all remaining 192 CUs).
+        // SML_RES_CUS overrides the count.
+        int res_cus = std::min(ncu - speedy_cus, ncu * 5 / 8);
+        if (const char *er = getenv("SML_RES_CUS")) res_cus = std::min(std::max(atoi(er), 1), ncu - speedy_cus);
+        if (int rc = sml_stream_create_cu_range(speedy_cus, res_cus, &m)) return bail(rc);
+        h->main = (hipStream_t)m;
         if (int rc = sml_res_set_read_waves(res, 0)) return bail(rc);  // pacing pays only on shared CUs
     } else {
         if (hipStreamCreateWithFlags(&h->main, hipStreamNonBlocking) != hipSuccess)
