@@ -1019,6 +1019,96 @@ __device__ __attribute__((always_inline)) inline void row_specx(double *x, doubl
     for (int c = 2; c < kMX2; ++c) o[(size_t)(c >> 1) * kVFm + (c & 1)] = x[c - 1] * scale;
 }
 
+// The n = 96 transforms on lane pairs: FFTPACK's rfftb96 starts with radb2(48, 1),
+// whose two output halves -- the even and the odd grid points -- go through the
+// remaining passes independently, as two n = 48 transforms; rfftf96 ends with
+// radf2(48, 1) over the n = 48 transforms of the even and the odd samples.  Lane h
+// of a pair takes half h, so each lane's dependent chain is about half of a full
+// transform's; the results are FFTPACK's, operation for operation.
+// gridx half h of field f, row j: radb2's half h from the coefficients, rfftb48,
+// grid points 2 q + h into A (x cosgr where kcos2)
+__device__ __attribute__((always_inline)) inline void row_gridx_half(double *A, const double *__restrict__ varm,
+                                                                     const double *__restrict__ wa, int f, int j,
+                                                                     bool kcos2, double cj, int h) {
+    const double *v = varm + (size_t)j * kVIl + f * 2;
+    // FFTPACK's half-complex input x[0] = a0, x[2m-1] = Re, x[2m] = Im (m <= 30), 0
+    // beyond: every load issued before any arithmetic, and both halves' values
+    // computed and selected (no branch on h inside the wave)
+    double xi[kMX2 - 1];
+    xi[0] = v[0];  // a0 (coefficient c = 0); x[e] = coefficient c = e + 1 for e >= 1
+#pragma unroll
+    for (int e = 1; e < kMX2 - 1; ++e) xi[e] = v[(size_t)((e + 1) >> 1) * kVIm + ((e + 1) & 1)];
+    auto X = [&](int e) { return e <= kMX2 - 2 ? xi[e] : 0.0; };
+    double y[48];
+    // radb2 (spe_subfft_fftpack2.f90:233-281) with ido = 48, l1 = 1: cc(i, 1) = x[i-1],
+    // cc(i, 2) = x[47+i]; half h = ch(., 1, h+1)
+    const bool odd = h != 0;
+    const double x95 = 0.0;  // x[95] = Re of m = 48: zero at T30
+    y[0] = odd ? xi[0] - x95 : xi[0] + x95;
+#pragma unroll
+    for (int s2 = 1; s2 <= 23; ++s2) {
+        const double c1 = X(2 * s2 - 1), c2 = X(2 * s2), d1 = X(95 - 2 * s2), d2 = X(96 - 2 * s2);
+        const double e1 = c1 + d1, e2 = c2 - d2;
+        const double tr2 = c1 - d1, ti2 = c2 + d2;
+        const double o1 = wa[2 * s2 - 2] * tr2 - wa[2 * s2 - 1] * ti2;
+        const double o2 = wa[2 * s2 - 2] * ti2 + wa[2 * s2 - 1] * tr2;
+        y[2 * s2 - 1] = odd ? o1 : e1;
+        y[2 * s2] = odd ? o2 : e2;
+    }
+    y[47] = odd ? -(X(48) + X(48)) : X(47) + X(47);
+    fft::rfftb48_reg(y, wa);
+#pragma unroll
+    for (int q = 0; q < 48; ++q) A[(2 * q + h) * kRowLd + f] = kcos2 ? y[q] * cj : y[q];
+}
+
+// specx of transform f, row j, on a lane pair: lane h holds its rfftf48 result of the
+// samples 2 i + h in x48; the pair meets in LDS (E = half 0, O = half 1, rows
+// [48 h, 48 h + 48) of S, column f) for radf2(48, 1) (spe_subfft_fftpack2.f90:741-789)
+// of the outputs m <= 30 (lane 0: m <= 15, lane 1: 16..30), scale 1/ix, into the
+// m-major forward coefficients vfm[m][f][j][p].  The whole block calls it (barrier).
+__device__ __attribute__((always_inline)) inline void row_specx_pair(const double *x48, double *S, bool act,
+                                                                     double *__restrict__ vfm,
+                                                                     const double *__restrict__ wa, int f, int j,
+                                                                     int h) {
+    if (act) {
+#pragma unroll
+        for (int i = 0; i < 48; ++i) S[(48 * h + i) * kRowLd + f] = x48[i];
+    }
+    __syncthreads();
+    if (!act) return;
+    auto E = [&](int i) { return S[i * kRowLd + f]; };
+    auto O = [&](int i) { return S[(48 + i) * kRowLd + f]; };
+    const double scale = 1. / (double)kIX;
+    double *o = vfm + (size_t)j * kVLs + f * 2;
+    auto put = [&](int m, double re, double im) {
+        o[(size_t)m * kVFm] = re * scale;
+        o[(size_t)m * kVFm + 1] = im * scale;
+    };
+    auto out = [&](int m) {  // radf2's outputs for coefficient m (1 <= m <= 30)
+        if (m == 24) {       // ido even: ch(ido, 1) = cc(ido, 1), ch(1, 2) = -cc(ido, 2)
+            put(m, E(47), -O(47));
+            return;
+        }
+        const int s2 = m < 24 ? m : 48 - m;
+        const double c = wa[2 * s2 - 2], sn = wa[2 * s2 - 1];
+        const double tr2 = c * O(2 * s2 - 1) + sn * O(2 * s2);
+        const double ti2 = c * O(2 * s2) - sn * O(2 * s2 - 1);
+        if (m < 24)
+            put(m, E(2 * s2 - 1) + tr2, E(2 * s2) + ti2);
+        else
+            put(m, E(2 * s2 - 1) - tr2, ti2 - E(2 * s2));
+    };
+    if (h == 0) {
+        o[0] = (E(0) + O(0)) * scale;
+        o[1] = 0.0;
+#pragma unroll
+        for (int m = 1; m <= 15; ++m) out(m);
+    } else {
+#pragma unroll
+        for (int m = 16; m <= kMX - 1; ++m) out(m);
+    }
+}
+
 // one latitude row without GPU physics: gridx of the 50 inverse transforms, grid-
 // point dynamics of the row's 96 columns (+ a host's physics tendencies Pext
 // [u|v|t|q][kx][ngp] if given) into LDS, specx straight to the m-major coefficients.
@@ -1223,18 +1313,20 @@ __global__ __launch_bounds__(kGsThreads) void k_st_gridspec(
     __shared__ double A[kFftN * kRowLd], B[kFftN * kRowLd], was[kFftWa];
     constexpr int n1 = kNInv1P;
     constexpr int nphys = (n1 - kPT1) + (kNInvP - (n1 + 2 * kKX + 2));  // 25 + 16 = 41
-    const int j = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int j = blockIdx.x, tid = threadIdx.x;
     stamp(dbg, 0, 0);
     if (tid < kFftWa) was[tid] = wa[tid];
     __syncthreads();
     const double cj = cosgr[j];
-    // gridx: wave 0 the dynamics fields, wave 1 phypar's
-    if (wave == 0 && lane < kNInv) {
-        const int f = lane < kNInv1 ? lane : n1 + (lane - kNInv1);  // [vor div t tr] | [ucos vcos psdx psdy]
-        row_gridx(A, varm, was, f, j, f >= n1, cj);
-    } else if (wave == 1 && lane < nphys) {
-        const int f = lane < n1 - kPT1 ? kPT1 + lane : n1 + 2 * kKX + 2 + (lane - (n1 - kPT1));
-        row_gridx(A, varm, was, f, j, f >= n1, cj);
+    // gridx: transform t (the dynamics fields, then phypar's) on lanes 2 t, 2 t + 1
+    {
+        const int t = tid >> 1, h = tid & 1;
+        if (t < kNInv + nphys) {
+            const int f = t < kNInv ? (t < kNInv1 ? t : n1 + (t - kNInv1))  // [vor div t tr] | [ucos vcos psdx psdy]
+                                    : (t - kNInv < n1 - kPT1 ? kPT1 + (t - kNInv)
+                                                             : n1 + 2 * kKX + 2 + (t - kNInv - (n1 - kPT1)));
+            row_gridx_half(A, varm, was, f, j, f >= n1, cj, h);
+        }
     }
     __syncthreads();
     stamp(dbg, 0, 1);
@@ -1269,27 +1361,32 @@ __global__ __launch_bounds__(kGsThreads) void k_st_gridspec(
     }
     __syncthreads();
     stamp(dbg, 0, 2);
-    // specx: transform f = 4 lane + wave (spread over the waves)
-    const int f = 4 * lane + wave;
-    if (f < kNFwd) {
-        // F field -> tendency slot of P: u 0..7, v 24..31, t 56..63, q 64..71
-        const int pf = f < kKX ? f : (f >= 3 * kKX && f < 4 * kKX) ? kKX + f - 3 * kKX
-                     : (f >= 7 * kKX && f < 9 * kKX) ? 2 * kKX + f - 7 * kKX : -1;
-        const double *fr = B + f, *pr = A + phys_slot_col(pf < 0 ? 0 : pf);
-        double x[kFftN];
-        // F, then + P (u, v, t, q), then x cosgr(j) (vdspec inputs): one branch per
-        // case around straight-line loops
+    // specx: transform f on lanes 2 f, 2 f + 1, lane h on the samples 2 i + h
+    {
+        const int f = tid >> 1, h = tid & 1;
+        const bool act = f < kNFwd;
+        double x[48];
+        if (act) {
+            // F field -> tendency slot of P: u 0..7, v 24..31, t 56..63, q 64..71
+            const int pf = f < kKX ? f : (f >= 3 * kKX && f < 4 * kKX) ? kKX + f - 3 * kKX
+                         : (f >= 7 * kKX && f < 9 * kKX) ? 2 * kKX + f - 7 * kKX : -1;
+            const double *fr = B + f + h * kRowLd, *pr = A + phys_slot_col(pf < 0 ? 0 : pf) + h * kRowLd;
+            // F, then + P (u, v, t, q), then x cosgr(j) (vdspec inputs): one branch per
+            // case around straight-line loops
 #pragma unroll
-        for (int e = 0; e < kFftN; ++e) x[e] = fr[e * kRowLd];
-        if (pf >= 0) {
+            for (int i = 0; i < 48; ++i) x[i] = fr[2 * i * kRowLd];
+            if (pf >= 0) {
 #pragma unroll
-            for (int e = 0; e < kFftN; ++e) x[e] = x[e] + pr[e * kRowLd];
+                for (int i = 0; i < 48; ++i) x[i] = x[i] + pr[2 * i * kRowLd];
+            }
+            if (f < kNFwdScaled) {
+#pragma unroll
+                for (int i = 0; i < 48; ++i) x[i] = x[i] * cj;
+            }
+            fft::rfftf48_reg(x, was);
         }
-        if (f < kNFwdScaled) {
-#pragma unroll
-            for (int e = 0; e < kFftN; ++e) x[e] = x[e] * cj;
-        }
-        row_specx(x, vfm, was, f, j);
+        __syncthreads();  // A's P columns are read: A becomes the pairs' meeting place
+        row_specx_pair(x, A, act, vfm, was, f, j, h);
     }
     stamp(dbg, 0, 3);
 }

@@ -324,6 +324,32 @@ __host__ __device__ __attribute__((always_inline)) inline void rfftf96_reg(doubl
     radf2<48, 1, 1>(y, x, 1, wa + 0, 0);
 }
 
+// n = 48 (rffti1's factors 4, 4, 3), one transform per thread in registers, for
+// the decimated form of the n = 96 transform (two independent halves per lane
+// pair).  Its twiddles are a sub-table of n = 96's: 2 pi ld / 48 = 2 pi (2 ld) / 96,
+// so the n = 48 passes radb4(12, 1) / radb4(3, 4) use wa96 + 48 / 60 / 72 and
+// wa96 + 84 / 87 / 90, exactly the n = 96 passes radb4(12, 2) / radb4(3, 8)'s.
+// rfftb48: x[q] = Y_0 + 2 sum_k (Re Y_k cos - Im Y_k sin)(2 pi k q / 48) + Y_24 (-1)^q
+// from the half-complex x = [Y_0, Re Y_1, Im Y_1, .., Re Y_23, Im Y_23, Y_24].
+__host__ __device__ __attribute__((always_inline)) inline void rfftb48_reg(double *x, const double *__restrict__ wa96) {
+    double y[48];
+    radb4<12, 1, 1>(x, y, 1, wa96 + 48, wa96 + 60, wa96 + 72, 0);
+    radb4<3, 4, 1>(y, x, 1, wa96 + 84, wa96 + 87, wa96 + 90, 0);
+    radb3_ido1<16, 1>(x, y, 1, 0);
+#pragma unroll
+    for (int e = 0; e < 48; ++e) x[e] = y[e];
+}
+
+// rfftf48: the half-complex X_k = sum_q x_q e^{-2 pi i k q / 48} (unnormalised)
+__host__ __device__ __attribute__((always_inline)) inline void rfftf48_reg(double *x, const double *__restrict__ wa96) {
+    double y[48];
+    radf3_ido1<16, 1>(x, y, 1, 0);
+    radf4<3, 4, 1>(y, x, 1, wa96 + 84, wa96 + 87, wa96 + 90, 0);
+    radf4<12, 1, 1>(x, y, 1, wa96 + 48, wa96 + 60, wa96 + 72, 0);
+#pragma unroll
+    for (int e = 0; e < 48; ++e) x[e] = y[e];
+}
+
 }  // namespace fft
 #endif
 
