@@ -56,7 +56,7 @@ int main(int argc, char **argv) {
         if (std::memcmp(&wa[i], &wsave[n + i], 8)) { ++bad; std::printf("twiddle %d differs: %.17g %.17g\n", i, wa[i], wsave[n + i]); }
     std::mt19937_64 rng(42);
     std::normal_distribution<double> nd;
-    int nbwd = 0, nfwd = 0;
+    int nbwd = 0, nfwd = 0, npair = 0;
     for (int rep = 0; rep < 200; ++rep) {
         double x[kFftN], r[kFftN], y1[kFftN], y2[kFftN], y3[kFftN], y4[kFftN], y8[kFftN];
         for (int i = 0; i < n; ++i) x[i] = nd(rng) * (rep % 7 + 1);
@@ -87,7 +87,30 @@ int main(int argc, char **argv) {
             std::memcmp(r, y4, sizeof r) || std::memcmp(r, y8, sizeof r) ||
             std::memcmp(r, yr, sizeof r))
             ++nfwd;
+        // the lane-pair forms: rfftb96_half for both halves, rfftf48 of the even / odd
+        // samples + rfftf96_combine, against the reference's rfftb / rfftf
+        std::memcpy(r, x, sizeof x);
+        rfftb(&n, r, wsave);
+        for (int hh = 0; hh < 2; ++hh) {
+            double yh[48];
+            fft::rfftb96_half([&](int e) { return x[e]; }, hh, yh, wa);
+            for (int q = 0; q < 48; ++q)
+                if (std::memcmp(&yh[q], &r[2 * q + hh], 8)) { ++npair; break; }
+        }
+        std::memcpy(r, x, sizeof x);
+        rfftf(&n, r, wsave);
+        double ev[48], od[48];
+        for (int i = 0; i < 48; ++i) { ev[i] = x[2 * i]; od[i] = x[2 * i + 1]; }
+        fft::rfftf48_reg(ev, wa);
+        fft::rfftf48_reg(od, wa);
+        for (int m = 0; m <= 48; ++m) {
+            double re, im;
+            fft::rfftf96_combine([&](int i) { return ev[i]; }, [&](int i) { return od[i]; }, m, wa, &re, &im);
+            const double want_re = m == 0 ? r[0] : r[2 * m - 1], want_im = (m == 0 || m == 48) ? 0.0 : r[2 * m];
+            if (std::memcmp(&re, &want_re, 8) || std::memcmp(&im, &want_im, 8)) { ++npair; break; }
+        }
     }
-    std::printf("twiddles differing: %d / 94; rfftb mismatches: %d / 200; rfftf mismatches: %d / 200\n", bad, nbwd, nfwd);
-    return (bad || nbwd || nfwd) ? 1 : 0;
+    std::printf("twiddles differing: %d / 94; rfftb mismatches: %d / 200; rfftf mismatches: %d / 200; "
+                "lane-pair mismatches: %d\n", bad, nbwd, nfwd, npair);
+    return (bad || nbwd || nfwd || npair) ? 1 : 0;
 }

@@ -1019,44 +1019,22 @@ __device__ __attribute__((always_inline)) inline void row_specx(double *x, doubl
     for (int c = 2; c < kMX2; ++c) o[(size_t)(c >> 1) * kVFm + (c & 1)] = x[c - 1] * scale;
 }
 
-// The n = 96 transforms on lane pairs: FFTPACK's rfftb96 starts with radb2(48, 1),
-// whose two output halves -- the even and the odd grid points -- go through the
-// remaining passes independently, as two n = 48 transforms; rfftf96 ends with
-// radf2(48, 1) over the n = 48 transforms of the even and the odd samples.  Lane h
-// of a pair takes half h, so each lane's dependent chain is about half of a full
-// transform's; the results are FFTPACK's, operation for operation.
-// gridx half h of field f, row j: radb2's half h from the coefficients, rfftb48,
-// grid points 2 q + h into A (x cosgr where kcos2)
+// The row kernel's transforms on lane pairs (sml_fft.hpp rfftb96_half /
+// rfftf96_combine): lane h of a pair does half h of FFTPACK's n = 96 transform, so a
+// lane's dependent chain is about half of a whole transform's.
+// gridx half h of field f, row j: grid points 2 q + h into A (x cosgr where kcos2)
 __device__ __attribute__((always_inline)) inline void row_gridx_half(double *A, const double *__restrict__ varm,
                                                                      const double *__restrict__ wa, int f, int j,
                                                                      bool kcos2, double cj, int h) {
     const double *v = varm + (size_t)j * kVIl + f * 2;
     // FFTPACK's half-complex input x[0] = a0, x[2m-1] = Re, x[2m] = Im (m <= 30), 0
-    // beyond: every load issued before any arithmetic, and both halves' values
-    // computed and selected (no branch on h inside the wave)
+    // beyond (x(e) is a compile-time zero there): every load issued first
     double xi[kMX2 - 1];
     xi[0] = v[0];  // a0 (coefficient c = 0); x[e] = coefficient c = e + 1 for e >= 1
 #pragma unroll
     for (int e = 1; e < kMX2 - 1; ++e) xi[e] = v[(size_t)((e + 1) >> 1) * kVIm + ((e + 1) & 1)];
-    auto X = [&](int e) { return e <= kMX2 - 2 ? xi[e] : 0.0; };
     double y[48];
-    // radb2 (spe_subfft_fftpack2.f90:233-281) with ido = 48, l1 = 1: cc(i, 1) = x[i-1],
-    // cc(i, 2) = x[47+i]; half h = ch(., 1, h+1)
-    const bool odd = h != 0;
-    const double x95 = 0.0;  // x[95] = Re of m = 48: zero at T30
-    y[0] = odd ? xi[0] - x95 : xi[0] + x95;
-#pragma unroll
-    for (int s2 = 1; s2 <= 23; ++s2) {
-        const double c1 = X(2 * s2 - 1), c2 = X(2 * s2), d1 = X(95 - 2 * s2), d2 = X(96 - 2 * s2);
-        const double e1 = c1 + d1, e2 = c2 - d2;
-        const double tr2 = c1 - d1, ti2 = c2 + d2;
-        const double o1 = wa[2 * s2 - 2] * tr2 - wa[2 * s2 - 1] * ti2;
-        const double o2 = wa[2 * s2 - 2] * ti2 + wa[2 * s2 - 1] * tr2;
-        y[2 * s2 - 1] = odd ? o1 : e1;
-        y[2 * s2] = odd ? o2 : e2;
-    }
-    y[47] = odd ? -(X(48) + X(48)) : X(47) + X(47);
-    fft::rfftb48_reg(y, wa);
+    fft::rfftb96_half([&](int e) { return e <= kMX2 - 2 ? xi[e] : 0.0; }, h, y, wa);
 #pragma unroll
     for (int q = 0; q < 48; ++q) A[(2 * q + h) * kRowLd + f] = kcos2 ? y[q] * cj : y[q];
 }
@@ -1080,26 +1058,14 @@ __device__ __attribute__((always_inline)) inline void row_specx_pair(const doubl
     auto O = [&](int i) { return S[(48 + i) * kRowLd + f]; };
     const double scale = 1. / (double)kIX;
     double *o = vfm + (size_t)j * kVLs + f * 2;
-    auto put = [&](int m, double re, double im) {
+    auto out = [&](int m) {
+        double re, im;
+        fft::rfftf96_combine(E, O, m, wa, &re, &im);
         o[(size_t)m * kVFm] = re * scale;
         o[(size_t)m * kVFm + 1] = im * scale;
     };
-    auto out = [&](int m) {  // radf2's outputs for coefficient m (1 <= m <= 30)
-        if (m == 24) {       // ido even: ch(ido, 1) = cc(ido, 1), ch(1, 2) = -cc(ido, 2)
-            put(m, E(47), -O(47));
-            return;
-        }
-        const int s2 = m < 24 ? m : 48 - m;
-        const double c = wa[2 * s2 - 2], sn = wa[2 * s2 - 1];
-        const double tr2 = c * O(2 * s2 - 1) + sn * O(2 * s2);
-        const double ti2 = c * O(2 * s2) - sn * O(2 * s2 - 1);
-        if (m < 24)
-            put(m, E(2 * s2 - 1) + tr2, E(2 * s2) + ti2);
-        else
-            put(m, E(2 * s2 - 1) - tr2, ti2 - E(2 * s2));
-    };
     if (h == 0) {
-        o[0] = (E(0) + O(0)) * scale;
+        o[0] = (E(0) + O(0)) * scale;  // varm(1) = fvar(1) / ix, varm(2) = 0
         o[1] = 0.0;
 #pragma unroll
         for (int m = 1; m <= 15; ++m) out(m);

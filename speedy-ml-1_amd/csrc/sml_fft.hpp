@@ -350,6 +350,65 @@ __host__ __device__ __attribute__((always_inline)) inline void rfftf48_reg(doubl
     for (int e = 0; e < 48; ++e) x[e] = y[e];
 }
 
+// The n = 96 transforms split over a lane pair.  rfftb96 starts with radb2(48, 1)
+// (:233-281): its two output halves ch(., 1, 1) / ch(., 1, 2) -- which the later
+// passes keep apart and which become the even / odd points -- are two independent
+// n = 48 transforms; rfftf96 ends with radf2(48, 1) (:741-789) over the n = 48
+// transforms of the even and the odd samples.  Half h of a pair does one of them,
+// operation for operation as FFTPACK (fft_check.cpp checks it against the
+// reference's compiled rfftb / rfftf, bit for bit).
+// rfftb96_half: x(e) = the half-complex input (e < 96); y[q] = point 2 q + h.  Both
+// halves' radb2 values are formed and one selected (no branch on h in a wave).
+template <class XF>
+__host__ __device__ __attribute__((always_inline)) inline void rfftb96_half(XF x, int h, double *y,
+                                                                             const double *__restrict__ wa96) {
+    const bool odd = h != 0;
+    y[0] = odd ? x(0) - x(95) : x(0) + x(95);
+#pragma unroll
+    for (int s = 1; s <= 23; ++s) {
+        const double c1 = x(2 * s - 1), c2 = x(2 * s), d1 = x(95 - 2 * s), d2 = x(96 - 2 * s);
+        const double e1 = c1 + d1, e2 = c2 - d2;
+        const double tr2 = c1 - d1, ti2 = c2 + d2;
+        const double o1 = wa96[2 * s - 2] * tr2 - wa96[2 * s - 1] * ti2;
+        const double o2 = wa96[2 * s - 2] * ti2 + wa96[2 * s - 1] * tr2;
+        y[2 * s - 1] = odd ? o1 : e1;
+        y[2 * s] = odd ? o2 : e2;
+    }
+    y[47] = odd ? -(x(48) + x(48)) : x(47) + x(47);
+    rfftb48_reg(y, wa96);
+}
+
+// rfftf96's last pass for output m (0 <= m <= 48) from E = rfftf48 of the even
+// samples and O = rfftf48 of the odd ones (accessors E(i), O(i), i < 48): the
+// unnormalised half-complex coefficient (Re X_m, Im X_m) as rfftf96 leaves it
+// (Im = 0 at m = 0 and 48)
+template <class EF, class OF>
+__host__ __device__ __attribute__((always_inline)) inline void rfftf96_combine(EF E, OF O, int m,
+                                                                                const double *__restrict__ wa96,
+                                                                                double *re, double *im) {
+    if (m == 0 || m == 48) {  // ch(1, 1) = cc(1, 1) + cc(1, 2), ch(ido, 2) = cc(1, 1) - cc(1, 2)
+        *re = m == 0 ? E(0) + O(0) : E(0) - O(0);
+        *im = 0.0;
+        return;
+    }
+    if (m == 24) {  // ido even: ch(ido, 1) = cc(ido, 1), ch(1, 2) = -cc(ido, 2)
+        *re = E(47);
+        *im = -O(47);
+        return;
+    }
+    const int s = m < 24 ? m : 48 - m;
+    const double c = wa96[2 * s - 2], sn = wa96[2 * s - 1];
+    const double tr2 = c * O(2 * s - 1) + sn * O(2 * s);
+    const double ti2 = c * O(2 * s) - sn * O(2 * s - 1);
+    if (m < 24) {
+        *re = E(2 * s - 1) + tr2;
+        *im = E(2 * s) + ti2;
+    } else {
+        *re = E(2 * s - 1) - tr2;
+        *im = ti2 - E(2 * s);
+    }
+}
+
 }  // namespace fft
 #endif
 
