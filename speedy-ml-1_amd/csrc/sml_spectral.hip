@@ -104,7 +104,8 @@ __global__ __launch_bounds__(64) void k_gridy(const double *__restrict__ spec, d
 }
 
 // gridx / specx: FFTPACK's real FFT along each latitude row, one (field, row)
-// transform per thread held in registers (sml_fft.hpp rfftb96_reg / rfftf96_reg).
+// transform per thread pair, each thread one n = 48 half held in registers
+// (sml_fft.hpp rfftb96_half / rfftf48_reg + rfftf96_combine: FFTPACK's operations).
 constexpr int kFftThreads = 64;
 
 // gridx (spe_subfft_fftpack.f90:15-51): fvar(1) = varm(1) (Im of m = 0 dropped),
@@ -121,17 +122,19 @@ __global__ __launch_bounds__(kFftThreads) void k_gridx(const double *__restrict_
     if (threadIdx.x < kFftWa) was[threadIdx.x] = wa[threadIdx.x];
     if (threadIdx.x + kFftThreads < kFftWa) was[threadIdx.x + kFftThreads] = wa[threadIdx.x + kFftThreads];
     __syncthreads();
+    // transform (f, j) on the thread pair 2 t, 2 t + 1: thread h does half h of
+    // FFTPACK's rfftb (sml_fft.hpp rfftb96_half), the grid points 2 q + h
     const int id = blockIdx.x * kFftThreads + threadIdx.x;
-    if (id >= nf * kIL) return;
-    const int f = id / kIL, j = id % kIL;
+    if (id >= 2 * nf * kIL) return;
+    const int t = id >> 1, h = id & 1;
+    const int f = t / kIL, j = t % kIL;
     const double *v = varm + (size_t)f * kVarmField + j * kMX2;
-    double x[kFftN];
-    x[0] = v[0];
+    double xi[kMX2 - 1];
+    xi[0] = v[0];
 #pragma unroll
-    for (int e = 1; e <= kMX2 - 2; ++e) x[e] = v[e + 1];
-#pragma unroll
-    for (int e = kMX2 - 1; e < kFftN; ++e) x[e] = 0.0;
-    fft::rfftb96_reg(x, was);
+    for (int e = 1; e <= kMX2 - 2; ++e) xi[e] = v[e + 1];
+    double y[kFftN / 2];
+    fft::rfftb96_half([&](int e) { return e <= kMX2 - 2 ? xi[e] : 0.0; }, h, y, was);
     const bool k2 = f >= c0 && f < c1;
     const double cj = k2 ? cosgr[j] : 1.0;
     double *g = grid + (size_t)f * kGridField + j * kIX;
@@ -153,22 +156,23 @@ __global__ __launch_bounds__(kFftThreads) void k_gridx(const double *__restrict_
             if (!io_state_safe(ex.mm)) {  // integration skipped: the input grid comes back
                 const double *src = grp < 4 ? ex.in4 + o : ex.inlp + o;
 #pragma unroll
-                for (int e = 0; e < kFftN; ++e) {
-                    const double v = src[e * gs];
-                    g[e * gs] = (q && v < ex.qfloor) ? ex.qfloor : v;
+                for (int qq = 0; qq < kFftN / 2; ++qq) {
+                    const int e = 2 * qq + h;
+                    const double vv = src[e * gs];
+                    g[e * gs] = (q && vv < ex.qfloor) ? ex.qfloor : vv;
                 }
                 return;
             }
 #pragma unroll
-            for (int e = 0; e < kFftN; ++e) {
-                const double v = k2 ? x[e] * cj : x[e];
-                g[e * gs] = (q && v < ex.qfloor) ? ex.qfloor : v;
+            for (int qq = 0; qq < kFftN / 2; ++qq) {
+                const double vv = k2 ? y[qq] * cj : y[qq];
+                g[(2 * qq + h) * gs] = (q && vv < ex.qfloor) ? ex.qfloor : vv;
             }
             return;
         }
     }
 #pragma unroll
-    for (int e = 0; e < kFftN; ++e) g[e * gs] = k2 ? x[e] * cj : x[e];
+    for (int qq = 0; qq < kFftN / 2; ++qq) g[(2 * qq + h) * gs] = k2 ? y[qq] * cj : y[qq];
 }
 
 // specx (spe_subfft_fftpack.f90:55-87): fvar = vorg(:, j) (the first nscaled fields
@@ -183,46 +187,69 @@ __global__ __launch_bounds__(kFftThreads) void k_specx(const double *__restrict_
                                                        const double *__restrict__ g4 = nullptr,
                                                        const double *__restrict__ logp = nullptr) {
     __shared__ double was[kFftWa];
+    __shared__ double S[kFftN * (kFftThreads / 2)];  // a pair's two n = 48 halves (E, O)
     if (threadIdx.x < kFftWa) was[threadIdx.x] = wa[threadIdx.x];
     if (threadIdx.x + kFftThreads < kFftWa) was[threadIdx.x + kFftThreads] = wa[threadIdx.x + kFftThreads];
     __syncthreads();
+    // transform (f, j) on the thread pair 2 t, 2 t + 1: thread h transforms the samples
+    // 2 i + h (rfftf48), the pair meets in LDS for rfftf's last pass (rfftf96_combine)
     const int id = blockIdx.x * kFftThreads + threadIdx.x;
-    if (id >= nf * kIL) return;
-    const int f = id / kIL, j = id % kIL;
-    const double *g = grid + (size_t)f * kGridField + j * kIX;
-    const bool sc = scale_tab && f < nscaled;
-    const double s0 = sc ? scale_tab[j] : 1.0;
-    double x[kFftN];
-    if (g4) {
-        const int grp = f / kKX, k = f % kKX;
-        if (grp < 4) {
-            const int var = grp == 0 ? 1 : grp == 1 ? 2 : grp == 2 ? 0 : 3;
-            const double *src = g4 + var + 4 * ((size_t)kGridField * k + j * kIX);
+    const bool act = id < 2 * nf * kIL;
+    const int t = id >> 1, h = id & 1, pr = threadIdx.x >> 1;
+    const int f = act ? t / kIL : 0, j = act ? t % kIL : 0;
+    double x[kFftN / 2];
+    if (act) {
+        const double *g = grid + (size_t)f * kGridField + j * kIX + h;
+        const bool sc = scale_tab && f < nscaled;
+        const double s0 = sc ? scale_tab[j] : 1.0;
+        if (g4) {
+            const int grp = f / kKX, k = f % kKX;
+            if (grp < 4) {
+                const int var = grp == 0 ? 1 : grp == 1 ? 2 : grp == 2 ? 0 : 3;
+                const double *src = g4 + var + 4 * ((size_t)kGridField * k + j * kIX + h);
 #pragma unroll
-            for (int e = 0; e < kFftN; ++e) {
-                float v4 = (float)src[4 * e];
-                if (grp == 3 && v4 < 0.0f) v4 = 0.0f;
-                x[e] = (double)v4;
+                for (int i = 0; i < kFftN / 2; ++i) {
+                    float v4 = (float)src[8 * i];
+                    if (grp == 3 && v4 < 0.0f) v4 = 0.0f;
+                    x[i] = (double)v4;
+                }
+            } else {
+#pragma unroll
+                for (int i = 0; i < kFftN / 2; ++i) x[i] = (double)(float)logp[j * kIX + 2 * i + h];
+            }
+            if (sc) {
+#pragma unroll
+                for (int i = 0; i < kFftN / 2; ++i) x[i] = x[i] * s0;
             }
         } else {
 #pragma unroll
-            for (int e = 0; e < kFftN; ++e) x[e] = (double)(float)logp[j * kIX + e];
+            for (int i = 0; i < kFftN / 2; ++i) x[i] = sc ? g[2 * i] * s0 : g[2 * i];
         }
-        if (sc) {
+        fft::rfftf48_reg(x, was);
 #pragma unroll
-            for (int e = 0; e < kFftN; ++e) x[e] = x[e] * s0;
-        }
-    } else {
-#pragma unroll
-        for (int e = 0; e < kFftN; ++e) x[e] = sc ? g[e] * s0 : g[e];
+        for (int i = 0; i < kFftN / 2; ++i) S[(48 * h + i) * (kFftThreads / 2) + pr] = x[i];
     }
-    fft::rfftf96_reg(x, was);
+    __syncthreads();
+    if (!act) return;
+    auto E = [&](int i) { return S[i * (kFftThreads / 2) + pr]; };
+    auto O = [&](int i) { return S[(48 + i) * (kFftThreads / 2) + pr]; };
     const double scale = 1. / (double)kIX;
     double *v = varm + (size_t)f * kVarmField + j * kMX2;
-    v[0] = x[0] * scale;
-    v[1] = 0.0;
+    auto out = [&](int m) {  // varm(2m+1..2m+2) = fvar(2m..2m+1) / ix
+        double re, im;
+        fft::rfftf96_combine(E, O, m, was, &re, &im);
+        v[2 * m] = re * scale;
+        v[2 * m + 1] = im * scale;
+    };
+    if (h == 0) {
+        v[0] = (E(0) + O(0)) * scale;  // varm(1) = fvar(1) / ix, varm(2) = 0
+        v[1] = 0.0;
 #pragma unroll
-    for (int c = 2; c < kMX2; ++c) v[c] = x[c - 1] * scale;
+        for (int m = 1; m <= 15; ++m) out(m);
+    } else {
+#pragma unroll
+        for (int m = 16; m <= kMX - 1; ++m) out(m);
+    }
 }
 
 // specy: varm[f][lat][62] -> spec[f][n][62]  (one wave per (m, 8-field tile));
@@ -459,7 +486,7 @@ extern "C" int sml_gridx_batched(sml_spectral *s, const double *d_varm, double *
                                  void *stream) {
     if (int rc = check_ctx(s, nf)) return rc;
     if (nf == 0) return SML_OK;
-    hipLaunchKernelGGL(k_gridx, dim3((nf * kIL + kFftThreads - 1) / kFftThreads), dim3(kFftThreads), 0, (hipStream_t)stream,
+    hipLaunchKernelGGL(k_gridx, dim3((2 * nf * kIL + kFftThreads - 1) / kFftThreads), dim3(kFftThreads), 0, (hipStream_t)stream,
                        d_varm, d_grid, s->d_wa, s->d_cosgr, nf, kcos == 1 ? nf : 0, nf, nullptr, nullptr, IoExit{});
     SML_HIP(hipGetLastError());
     return SML_OK;
@@ -468,7 +495,7 @@ extern "C" int sml_gridx_batched(sml_spectral *s, const double *d_varm, double *
 extern "C" int sml_specx_batched(sml_spectral *s, const double *d_grid, double *d_varm, int nf, void *stream) {
     if (int rc = check_ctx(s, nf)) return rc;
     if (nf == 0) return SML_OK;
-    hipLaunchKernelGGL(k_specx, dim3((nf * kIL + kFftThreads - 1) / kFftThreads), dim3(kFftThreads), 0, (hipStream_t)stream,
+    hipLaunchKernelGGL(k_specx, dim3((2 * nf * kIL + kFftThreads - 1) / kFftThreads), dim3(kFftThreads), 0, (hipStream_t)stream,
                        d_grid, d_varm, s->d_wa, (const double *)nullptr, nf, 0);
     SML_HIP(hipGetLastError());
     return SML_OK;
@@ -509,7 +536,7 @@ extern "C" int sml_vdspec_batched(sml_spectral *s, const double *d_ug, const dou
     const double *scale = (kcos == 2) ? s->d_cosgr : s->d_cosgr2;
     double *um = s->d_work, *vm = s->d_work + (size_t)nf * kVarmField;
     double *uc = s->d_work + 2 * s->work_fields * (size_t)kVarmField, *vc = uc + (size_t)nf * kSpecField;
-    const dim3 fg((nf * kIL + kFftThreads - 1) / kFftThreads), fb(kFftThreads);
+    const dim3 fg((2 * nf * kIL + kFftThreads - 1) / kFftThreads), fb(kFftThreads);
     hipLaunchKernelGGL(k_specx, fg, fb, 0, st, d_ug, um, s->d_wa, scale, nf, nf);
     hipLaunchKernelGGL(k_specx, fg, fb, 0, st, d_vg, vm, s->d_wa, scale, nf, nf);
     hipLaunchKernelGGL(k_specy, dim3(kMX, (nf + 7) / 8), dim3(64), 0, st, um, uc, s->d_pfwd, s->d_wt, nf);
@@ -611,7 +638,7 @@ int spectral_gridx_split(sml_spectral *s, const double *varm, double *grid, int 
 
 int spectral_gridx_range(sml_spectral *s, const double *varm, double *grid, int nf, int c0, int c1, hipStream_t st) {
     if (nf <= 0) return SML_OK;
-    hipLaunchKernelGGL(k_gridx, dim3((nf * kIL + kFftThreads - 1) / kFftThreads), dim3(kFftThreads), 0, st, varm, grid, s->d_wa,
+    hipLaunchKernelGGL(k_gridx, dim3((2 * nf * kIL + kFftThreads - 1) / kFftThreads), dim3(kFftThreads), 0, st, varm, grid, s->d_wa,
                        s->d_cosgr, nf, c0, c1, nullptr, nullptr, IoExit{});
     SML_HIP(hipGetLastError());
     return SML_OK;
@@ -624,7 +651,7 @@ int spectral_gridx_io(sml_spectral *s, const double *varm, double *g4, double *l
 int spectral_gridx_run_model_exit(sml_spectral *s, const double *varm, double *g4, double *logp, int nwind,
                                   IoExit ex, hipStream_t st) {
     constexpr int nf = 4 * kKX + 1;
-    hipLaunchKernelGGL(k_gridx, dim3((nf * kIL + kFftThreads - 1) / kFftThreads), dim3(kFftThreads), 0, st, varm, nullptr,
+    hipLaunchKernelGGL(k_gridx, dim3((2 * nf * kIL + kFftThreads - 1) / kFftThreads), dim3(kFftThreads), 0, st, varm, nullptr,
                        s->d_wa, s->d_cosgr, nf, 0, nwind, g4, logp, ex);
     SML_HIP(hipGetLastError());
     return SML_OK;
@@ -633,7 +660,7 @@ int spectral_gridx_run_model_exit(sml_spectral *s, const double *varm, double *g
 int spectral_specx(sml_spectral *s, const double *grid, double *varm, int nf, int scale, hipStream_t st) {
     if (nf <= 0) return SML_OK;
     const double *sc = scale == 1 ? s->d_cosgr : scale == 2 ? s->d_cosgr2 : nullptr;
-    hipLaunchKernelGGL(k_specx, dim3((nf * kIL + kFftThreads - 1) / kFftThreads), dim3(kFftThreads), 0, st, grid, varm, s->d_wa,
+    hipLaunchKernelGGL(k_specx, dim3((2 * nf * kIL + kFftThreads - 1) / kFftThreads), dim3(kFftThreads), 0, st, grid, varm, s->d_wa,
                        sc, nf, nf);
     SML_HIP(hipGetLastError());
     return SML_OK;
@@ -641,7 +668,7 @@ int spectral_specx(sml_spectral *s, const double *grid, double *varm, int nf, in
 
 int spectral_specx_split(sml_spectral *s, const double *grid, double *varm, int nf, int nscaled, hipStream_t st) {
     if (nf <= 0) return SML_OK;
-    hipLaunchKernelGGL(k_specx, dim3((nf * kIL + kFftThreads - 1) / kFftThreads), dim3(kFftThreads), 0, st, grid, varm, s->d_wa,
+    hipLaunchKernelGGL(k_specx, dim3((2 * nf * kIL + kFftThreads - 1) / kFftThreads), dim3(kFftThreads), 0, st, grid, varm, s->d_wa,
                        s->d_cosgr, nf, nscaled);
     SML_HIP(hipGetLastError());
     return SML_OK;
@@ -650,7 +677,7 @@ int spectral_specx_split(sml_spectral *s, const double *grid, double *varm, int 
 int spectral_specx_io(sml_spectral *s, const double *g4, const double *logp, double *varm, int nwind,
                       hipStream_t st) {
     constexpr int nf = 4 * kKX + 1;
-    hipLaunchKernelGGL(k_specx, dim3((nf * kIL + kFftThreads - 1) / kFftThreads), dim3(kFftThreads), 0, st, nullptr, varm,
+    hipLaunchKernelGGL(k_specx, dim3((2 * nf * kIL + kFftThreads - 1) / kFftThreads), dim3(kFftThreads), 0, st, nullptr, varm,
                        s->d_wa, s->d_cosgr, nf, nwind, g4, logp);
     SML_HIP(hipGetLastError());
     return SML_OK;
