@@ -52,7 +52,16 @@ struct sml_hybrid {
     bool overlap = true;
     hipStream_t main = nullptr, side = nullptr;
     bool own_streams = false;
-    hipEvent_t ev_grid = nullptr, ev_lm = nullptr;
+    // the two cross-stream dependencies of the overlapped schedule (grid_t: main ->
+    // side, lm_t: side -> main): a sequence number in device memory that the
+    // producer's stream writes and the consumer's waits for (CP stream memory
+    // operations: 3.9 us from the producer's end to the consumer's start on gfx950,
+    // 10 us for an event record + wait; tools/probe_hop.hip).  SML_HYBRID_EVENTS=1
+    // keeps events.
+    enum { kHopGrid = 0, kHopLm = 1 };
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    uint64_t *d_seq = nullptr, seq[2] = {0, 0};
+    bool use_events = false;
     // caller-owned device buffers
     double *fb = nullptr, *lm = nullptr, *ov = nullptr, *g4 = nullptr, *g2 = nullptr, *pr = nullptr, *f4 = nullptr,
            *f2 = nullptr;
@@ -222,6 +231,30 @@ extern "C" int sml_tisr_date_index(int startyear, int64_t hours_elapsed, int *fe
 }
 
 // ------------------------------------------------------------------ hybrid loop
+namespace {
+
+// producer side of hop `k`: ordered after everything issued on `s` so far
+int hop_signal(sml_hybrid *h, int k, hipStream_t s) {
+    if (h->use_events) {
+        SML_HIP(hipEventRecord(h->ev[k], s));
+    } else {
+        SML_HIP(hipStreamWriteValue64(s, h->d_seq + k, ++h->seq[k], 0));
+    }
+    return SML_OK;
+}
+
+// consumer side: `s` waits for the latest signal of hop `k`
+int hop_wait(sml_hybrid *h, int k, hipStream_t s) {
+    if (h->use_events) {
+        SML_HIP(hipStreamWaitEvent(s, h->ev[k], 0));
+    } else {
+        SML_HIP(hipStreamWaitValue64(s, h->d_seq + k, h->seq[k], hipStreamWaitValueGte, ~0ull));
+    }
+    return SML_OK;
+}
+
+}  // namespace
+
 extern "C" int sml_hybrid_destroy(sml_hybrid *h) {
     if (!h) return SML_OK;
     if (h->main) (void)hipStreamSynchronize(h->main);
@@ -230,9 +263,9 @@ extern "C" int sml_hybrid_destroy(sml_hybrid *h) {
         if (h->side && h->side != h->main) (void)hipStreamDestroy(h->side);
         if (h->main) (void)hipStreamDestroy(h->main);
     }
-    if (h->ev_grid) (void)hipEventDestroy(h->ev_grid);
-    if (h->ev_lm) (void)hipEventDestroy(h->ev_lm);
-    void *ptrs[] = {h->d_send, h->d_recv, h->d_glob, h->d_perm};
+    for (hipEvent_t e : h->ev)
+        if (e) (void)hipEventDestroy(e);
+    void *ptrs[] = {h->d_send, h->d_recv, h->d_glob, h->d_perm, h->d_seq};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     delete h;
@@ -303,9 +336,13 @@ extern "C" int sml_hybrid_create(sml_reservoirs *res, sml_dynamics *dyn, sml_com
             h->side = h->main;
         }
     }
-    if (hipEventCreateWithFlags(&h->ev_grid, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&h->ev_lm, hipEventDisableTiming) != hipSuccess)
+    if (hipEventCreateWithFlags(&h->ev[0], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&h->ev[1], hipEventDisableTiming) != hipSuccess)
         return bail(fail(SML_ERR_HIP, "event"));
+    if (const char *e = getenv("SML_HYBRID_EVENTS")) h->use_events = atoi(e) != 0;
+    if (hipMalloc(&h->d_seq, 2 * sizeof(uint64_t)) != hipSuccess ||
+        hipMemset(h->d_seq, 0, 2 * sizeof(uint64_t)) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
+        return bail(fail(SML_ERR_HIP, "sequence counters"));
     if (world > 1) {
         std::vector<int> all(h->numregions);
         std::vector<int32_t> perm(h->numregions, -1);
@@ -401,7 +438,7 @@ extern "C" int sml_hybrid_start(sml_hybrid *h, const double *d_g4, const double 
     if (d_f2 != h->f2) SML_HIP(hipMemcpyAsync(h->f2, d_f2, n2, hipMemcpyDeviceToDevice, h->main));
     if (int rc = sml_res_tile_inputs(h->res, h->g4, h->g2, h->pr, h->f4, h->f2, h->tisr, h->fb, h->lm, h->main))
         return rc;
-    SML_HIP(hipEventRecord(h->ev_lm, h->main));
+    if (int rc = hop_signal(h, sml_hybrid::kHopLm, h->main)) return rc;
     h->started = true;
     h->predicted = h->advanced = false;
     return SML_OK;
@@ -415,7 +452,8 @@ extern "C" int sml_hybrid_predict(sml_hybrid *h) {
     if (h->predicted) return fail(SML_ERR_STATE, "sml_hybrid_predict twice without sml_hybrid_advance");
     if (h->overlap) {
         if (int rc = sml_res_step_begin(h->res, h->fb, h->main)) return rc;
-        SML_HIP(hipStreamWaitEvent(h->main, h->ev_lm, 0));  // SPEEDY's forecast of the previous window
+        // SPEEDY's forecast of the previous window
+        if (int rc = hop_wait(h, sml_hybrid::kHopLm, h->main)) return rc;
         // the local-model tiling fused into the v_p finish: one launch fewer on the critical path
         if (int rc = sml_res_step_finish_grid(h->res, h->f4, h->f2, h->lm, h->ov, h->main)) return rc;
     } else {  // one pass over W_out: the same sums as begin + finish
@@ -432,7 +470,8 @@ extern "C" int sml_hybrid_advance(sml_hybrid *h, const double *d_outvec_all) {
     if (!h->predicted) return fail(SML_ERR_STATE, "sml_hybrid_advance without sml_hybrid_predict");
     hipStream_t m = h->main, s = h->side;
     if (int rc = sml_exchange_assemble(h->res, d_outvec_all, h->g4, h->g2, h->pr, m)) return rc;
-    if (h->overlap) SML_HIP(hipEventRecord(h->ev_grid, m));
+    if (h->overlap)
+        if (int rc = hop_signal(h, sml_hybrid::kHopGrid, m)) return rc;
     ++h->t;
     if (int rc = sml_res_tile_feedback(h->res, h->g4, h->g2, h->pr, h->tisr_table ? nullptr : h->tisr, h->fb, m))
         return rc;
@@ -446,11 +485,12 @@ extern "C" int sml_hybrid_advance(sml_hybrid *h, const double *d_outvec_all) {
         if (int rc = sml_res_tile_tisr_field(h->res, h->tisr_table + (size_t)(idx - 1) * kGrid2d, h->fb, m))
             return rc;
     }
-    if (h->overlap) SML_HIP(hipStreamWaitEvent(s, h->ev_grid, 0));
+    if (h->overlap)
+        if (int rc = hop_wait(h, sml_hybrid::kHopGrid, s)) return rc;
     if (int rc = sml_dyn_run_model(h->dyn, h->g4, h->g2, h->nleap, h->delt, h->alph, h->rob, h->wil, h->f4, h->f2, s))
         return rc;
     if (h->overlap) {
-        SML_HIP(hipEventRecord(h->ev_lm, s));
+        if (int rc = hop_signal(h, sml_hybrid::kHopLm, s)) return rc;
     } else if (h->ncs) {
         if (int rc = sml_res_tile_local_model(h->res, h->f4, h->f2, h->lm, s)) return rc;
     }
@@ -501,7 +541,7 @@ extern "C" int sml_hybrid_run_speedy(sml_hybrid *h, int *run) {
 extern "C" int sml_hybrid_sync(sml_hybrid *h) {
     SML_REQUIRE(h, "null context");
     if (h->overlap && h->advanced && h->ncs) {
-        SML_HIP(hipStreamWaitEvent(h->main, h->ev_lm, 0));
+        if (int rc = hop_wait(h, sml_hybrid::kHopLm, h->main)) return rc;
         if (int rc = sml_res_tile_local_model(h->res, h->f4, h->f2, h->lm, h->main)) return rc;
     }
     SML_HIP(hipStreamSynchronize(h->main));
