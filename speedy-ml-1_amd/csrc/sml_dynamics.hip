@@ -1023,16 +1023,23 @@ __device__ __attribute__((always_inline)) inline void row_specx(double *x, doubl
 // rfftf96_combine): lane h of a pair does half h of FFTPACK's n = 96 transform, so a
 // lane's dependent chain is about half of a whole transform's.
 // gridx half h of field f, row j: grid points 2 q + h into A (x cosgr where kcos2)
-__device__ __attribute__((always_inline)) inline void row_gridx_half(double *A, const double *__restrict__ varm,
-                                                                     const double *__restrict__ wa, int f, int j,
-                                                                     bool kcos2, double cj, int h) {
+// FFTPACK's half-complex input of field f, row j: x[0] = a0, x[2m-1] = Re, x[2m] = Im
+// (m <= 30), 0 beyond (x(e) is a compile-time zero there)
+__device__ __attribute__((always_inline)) inline void row_gridx_load(const double *__restrict__ varm, int f, int j,
+                                                                     double (&xi)[kMX2 - 1]) {
     const double *v = varm + (size_t)j * kVIl + f * 2;
-    // FFTPACK's half-complex input x[0] = a0, x[2m-1] = Re, x[2m] = Im (m <= 30), 0
-    // beyond (x(e) is a compile-time zero there): every load issued first
-    double xi[kMX2 - 1];
     xi[0] = v[0];  // a0 (coefficient c = 0); x[e] = coefficient c = e + 1 for e >= 1
 #pragma unroll
     for (int e = 1; e < kMX2 - 1; ++e) xi[e] = v[(size_t)((e + 1) >> 1) * kVIm + ((e + 1) & 1)];
+    // every load in flight before the first use: left alone, the scheduler hoisted
+    // radb2's first add (x(0) + a zero) between the loads, and its wait cost a
+    // whole memory round trip before the remaining loads issued
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+__device__ __attribute__((always_inline)) inline void row_gridx_half(double *A, const double (&xi)[kMX2 - 1],
+                                                                     const double *__restrict__ wa, int f,
+                                                                     bool kcos2, double cj, int h) {
     double y[48];
     fft::rfftb96_half([&](int e) { return e <= kMX2 - 2 ? xi[e] : 0.0; }, h, y, wa);
 #pragma unroll
@@ -1281,21 +1288,24 @@ __global__ __launch_bounds__(kGsThreads) void k_st_gridspec(
     constexpr int nphys = (n1 - kPT1) + (kNInvP - (n1 + 2 * kKX + 2));  // 25 + 16 = 41
     const int j = blockIdx.x, tid = threadIdx.x;
     stamp(dbg, 0, 0);
-    if (tid < kFftWa) was[tid] = wa[tid];
-    __syncthreads();
-    const double cj = cosgr[j];
-    // gridx: transform t (the dynamics fields, then phypar's) on lanes 2 t, 2 t + 1
+    // gridx: transform t (the dynamics fields, then phypar's) on lanes 2 t, 2 t + 1;
+    // its coefficients are loaded before the twiddles are staged, so the two loads
+    // share one memory round trip
     {
         const int t = tid >> 1, h = tid & 1;
-        if (t < kNInv + nphys) {
-            const int f = t < kNInv ? (t < kNInv1 ? t : n1 + (t - kNInv1))  // [vor div t tr] | [ucos vcos psdx psdy]
-                                    : (t - kNInv < n1 - kPT1 ? kPT1 + (t - kNInv)
-                                                             : n1 + 2 * kKX + 2 + (t - kNInv - (n1 - kPT1)));
-            row_gridx_half(A, varm, was, f, j, f >= n1, cj, h);
-        }
+        const bool act = t < kNInv + nphys;
+        const int f = t < kNInv ? (t < kNInv1 ? t : n1 + (t - kNInv1))  // [vor div t tr] | [ucos vcos psdx psdy]
+                                : (t - kNInv < n1 - kPT1 ? kPT1 + (t - kNInv)
+                                                         : n1 + 2 * kKX + 2 + (t - kNInv - (n1 - kPT1)));
+        double xi[kMX2 - 1];
+        if (act) row_gridx_load(varm, f, j, xi);
+        if (tid < kFftWa) was[tid] = wa[tid];
+        __syncthreads();
+        if (act) row_gridx_half(A, xi, was, f, f >= n1, cosgr[j], h);
     }
     __syncthreads();
     stamp(dbg, 0, 1);
+    const double cj = cosgr[j];
     if (tid < 128) {
         if (tid < kIX) {  // grid-point dynamics of column i -> F in B[i][f]
             const int i = tid;
@@ -1401,7 +1411,15 @@ __global__ __launch_bounds__(kSpecBlk) void k_st_spec(
         rt1 = t[kSpecBlk];
         if constexpr (RT > 2) rt2 = t[2 * kSpecBlk];
     }
-    load_forcing_m(Fm, phis, tcorh, qcorh, m);
+    // the m's forcing (load_forcing_m's elements, one per thread) stays in a register
+    // until specy is done: stored to LDS here, its wait would have cost a memory
+    // round trip before specy's loads issued
+    double rf = 0.0;
+    if (threadIdx.x < 3 * kCW) {
+        const int which = threadIdx.x / kCW, cf = threadIdx.x % kCW;
+        const double *src = which == 0 ? phis : which == 1 ? tcorh : qcorh;
+        rf = src[ci(cf & 1, m, cf >> 1)];
+    }
     // specy operands: wave w's tiles all use this m's Legendre columns of its lanes
     const double *pm = pfwd + (size_t)m * kNX * kIY;
     double wv[kIY / 4], bS[kIY / 4], bD[kIY / 4];
@@ -1417,18 +1435,23 @@ __global__ __launch_bounds__(kSpecBlk) void k_st_spec(
     // a) specy (k_specy's tiling: 8 fields x Re/Im per wave), the wave's A operands
     // read from vfm [lat][f][p] (per instruction 4 latitudes x 128 contiguous bytes)
     const double *vm = vfm + (size_t)m * kVFm;
-    for (int tile = wave; tile < (kNFwd + 7) / 8; tile += kSpecBlk / 64) {
-        const int f0 = tile * 8;
-        const int fa = f0 + (r >> 1);
-        const bool ok = fa < kNFwd;
-        const double *vr = vm + (ok ? fa : 0) * 2 + (r & 1);
-        double vn[kIY / 4], vs[kIY / 4];
+    // at most two tiles per wave (10 tiles, 8 waves): both tiles' loads are issued
+    // before the first MFMA, so the second tile costs no memory round trip of its own
+    constexpr int kTiles = (kNFwd + 7) / 8, kWaves = kSpecBlk / 64;
+    static_assert(kTiles <= 2 * kWaves, "specy: two tiles per wave at most");
+    auto tile_load = [&](int tile, double (&vn)[kIY / 4], double (&vs)[kIY / 4]) {
+        const int fa = tile * 8 + (r >> 1);
+        const double *vr = vm + (fa < kNFwd ? fa : 0) * 2 + (r & 1);
 #pragma unroll
         for (int s = 0; s < kIY / 4; ++s) {
             const int j = 4 * s + kk;
             vn[s] = vr[(kIL - 1 - j) * kVLs];
             vs[s] = vr[j * kVLs];
         }
+    };
+    auto tile_mma = [&](int tile, const double (&vn)[kIY / 4], const double (&vs)[kIY / 4]) {
+        const int f0 = tile * 8;
+        const bool ok = f0 + (r >> 1) < kNFwd;
         d4 accS = {0, 0, 0, 0}, accD = accS;
 #pragma unroll
         for (int s = 0; s < kIY / 4; ++s) {
@@ -1448,6 +1471,14 @@ __global__ __launch_bounds__(kSpecBlk) void k_st_spec(
             S[f * kCW + 2 * (2 * r) + (row & 1)] = accS[q];
             S[f * kCW + 2 * (2 * r + 1) + (row & 1)] = accD[q];
         }
+    };
+    {
+        double vn0[kIY / 4], vs0[kIY / 4], vn1[kIY / 4], vs1[kIY / 4];
+        const bool two = wave + kWaves < kTiles;  // wave-uniform
+        tile_load(wave, vn0, vs0);
+        if (two) tile_load(wave + kWaves, vn1, vs1);
+        tile_mma(wave, vn0, vs0);
+        if (two) tile_mma(wave + kWaves, vn1, vs1);
     }
     TabM *tm = reinterpret_cast<TabM *>(V);
     {
@@ -1461,8 +1492,9 @@ __global__ __launch_bounds__(kSpecBlk) void k_st_spec(
         s2[2 * kSpecBlk] = rs2;
         s2[3 * kSpecBlk] = rs3;
         s2[4 * kSpecBlk] = rs4;
+        if (threadIdx.x < 3 * kCW) Fm[threadIdx.x] = rf;
     }
-    __syncthreads();  // S, Sst, the tables complete
+    __syncthreads();  // S, Sst, Fm, the tables complete
     const LTab tb{tm};
     stamp(dbg, sk, 2);
     // b) combine (k_dyn_combine) for coefficient (n, p) at level k: threads 0..511
