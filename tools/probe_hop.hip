@@ -37,6 +37,21 @@ __global__ void k_work(u64 ticks, u64 *stamp, u64 *flag, u64 val) {
     }
 }
 
+// producer that also leaves `n` doubles written (how = 0: plain stores, 1: non-temporal,
+// 2: agent-scope relaxed atomic stores, which write through L2)
+__global__ void k_write(u64 ticks, u64 *stamp, double *buf, int n, int how) {
+    const u64 t0 = wall_clock64();
+    while (wall_clock64() - t0 < ticks) {
+    }
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        if (how == 0) buf[i] = (double)i;
+        else if (how == 1) __builtin_nontemporal_store((double)i, buf + i);
+        else __hip_atomic_store(buf + i, (double)i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) stamp[blockIdx.x] = wall_clock64();
+}
+
 __global__ void k_stamp(u64 *stamp) {
     if (threadIdx.x == 0) stamp[blockIdx.x] = wall_clock64();
 }
@@ -113,6 +128,30 @@ int main() {
         std::sort(gaps.begin(), gaps.end());
         std::printf("%-50s median %7.2f us  min %7.2f  max %7.2f\n", names[mode], gaps[gaps.size() / 2], gaps[0],
                     gaps.back());
+    }
+    // kernel boundary on one stream after the producer wrote `mb` MB
+    double *d_buf;
+    CK(hipMalloc(&d_buf, 64ull << 20));
+    const char *hows[] = {"plain stores", "non-temporal stores", "agent-scope atomic stores"};
+    for (int mb : {0, 1, 2, 8}) {
+        for (int how = 0; how < 3; ++how) {
+            std::vector<double> gaps;
+            for (int r = 0; r < kReps; ++r) {
+                CK(hipDeviceSynchronize());
+                hipLaunchKernelGGL(k_write, dim3(kPB), dim3(256), 0, sa, busy, d_st, d_buf, mb << 17, how);
+                hipLaunchKernelGGL(k_stamp, dim3(kCB), dim3(64), 0, sa, d_st + 64);
+                CK(hipGetLastError());
+                CK(hipDeviceSynchronize());
+                CK(hipMemcpy(h.data(), d_st, sizeof(u64) * 128, hipMemcpyDeviceToHost));
+                u64 pend = 0, cstart = ~0ull;
+                for (int b = 0; b < kPB; ++b) pend = std::max(pend, h[b]);
+                for (int b = 0; b < kCB; ++b) cstart = std::min(cstart, h[64 + b]);
+                if (r >= 4) gaps.push_back(((double)cstart - (double)pend) * 0.01);
+            }
+            std::sort(gaps.begin(), gaps.end());
+            std::printf("same stream after %d MB of %-26s median %7.2f us  min %7.2f  max %7.2f\n", mb, hows[how],
+                        gaps[gaps.size() / 2], gaps[0], gaps.back());
+        }
     }
     return 0;
 }

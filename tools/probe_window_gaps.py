@@ -46,11 +46,16 @@ for k in range(4):
     ns = int((b[0] > 0).sum())  # stamps per block
     s = (b[:, 0] - t0) / 100.0
     e = (b[:, ns - 1] - t0) / 100.0
-    rows.append((s.min(), k, nb, ns, s.min(), s.max(), e.min(), e.max(), np.median(np.diff(b[:, :ns], axis=1), 0) / 100))
+    rows.append((s.min(), k, nb, ns, s.min(), s.max(), e.min(), e.max(), np.median(np.diff(b[:, :ns], axis=1), 0) / 100, e))
 rows.sort()
 prev_end = None
-for _, k, nb, ns, s0, s1, e0, e1, ph in rows:
+for _, k, nb, ns, s0, s1, e0, e1, ph, e in rows:
     gap = "" if prev_end is None else f"  boundary from previous last block: {s0 - prev_end:6.2f} us"
     print(f"{NAMES.get(k, k):30s} blocks {nb:3d}  start {s0:8.2f}..{s1:8.2f}  end {e0:8.2f}..{e1:8.2f}{gap}")
     print(f"{'':30s} median phases (us): {np.round(ph, 2).tolist()}")
+    b = buf[k, :nb]
+    late = np.argsort(e)[::-1][:8]
+    print(f"{'':30s} latest blocks: " + ", ".join(
+        f"{i}: end {e[i]:.2f} phases {np.round(np.diff(b[i, :ns]) / 100, 2).tolist()}" for i in late[:4]))
+    print(f"{'':30s} end by block: {np.round(e - e.min(), 2).tolist()}")
     prev_end = e1
