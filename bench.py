@@ -46,8 +46,10 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level para
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=30)
-    p.add_argument("--warmup", type=int, default=5)
+    # a hybrid step is ~1.2 ms: 300 timed steps (0.35 s) after 20 warmup steps give
+    # the steady state (30 steps after 5 read ~2 % low: clocks and queues still ramping)
+    p.add_argument("--steps", type=int, default=300)
+    p.add_argument("--warmup", type=int, default=20)
     p.add_argument("--regions", type=int, default=1152)
     p.add_argument("--weights", choices=("f32", "f64"), default="f32")
     p.add_argument("--cpu-threads", type=int,
