@@ -328,6 +328,11 @@ int sml_dyn_run_model(sml_dynamics *d, const double *d_grid4d, const double *d_l
  * prediction loop on (src/parallelmain.f90:268-270).  Waits only for that check;
  * minmax (may be NULL) receives its 8 values. */
 int sml_dyn_last_safe(sml_dynamics *d, int *safe, double *minmax);
+/* CUs [first_cu, first_cu + num_cus) for the safety check that runs beside the
+ * window (iogrid(30)'s re-grid + min/max on the context's check stream); num_cus = 0
+ * lets it use any CU.  The hybrid loop puts it on CUs neither SPEEDY's nor the
+ * reservoir's stream uses, so its kernels never share a CU with the window's. */
+int sml_dyn_set_check_cus(sml_dynamics *d, int first_cu, int num_cus);
 /* synchronous host-buffer variants */
 int sml_dyn_from_grid_host(sml_dynamics *d, const double *grid4d, const double *logp, double *minmax, int *safe);
 int sml_dyn_to_grid_host(sml_dynamics *d, double *grid4d, double *logp);

@@ -1603,19 +1603,27 @@ __global__ __launch_bounds__(kSpecThreads) void k_io_entry(const double *__restr
                                                            const double *__restrict__ wt, double *__restrict__ state,
                                                            double *__restrict__ sm, double *__restrict__ chk,
                                                            const double *__restrict__ phis,
-                                                           const DynTables *__restrict__ T,
+                                                           const double *__restrict__ tabm,
                                                            const double *__restrict__ pinv, double *__restrict__ varm,
                                                            int n1, int nin) {
     __shared__ double S[kNIo * kCW];  // specy output [f][2 n + p]
     __shared__ double Sst[kSM];       // this m's state slice
     __shared__ double In[kNInvMax * kCW];
     __shared__ double Fm[kCW];
+    constexpr int RT = (kTabMDoubles / 2 + kSpecThreads - 1) / kSpecThreads;
+    __shared__ double V[2 * RT * kSpecThreads];  // this m's tables (TabM), staged as k_st_spec does
     const int m = blockIdx.x, tid = threadIdx.x;
     const int wave = tid >> 6, l = tid & 63, r = l & 15, kk = l >> 4;
-    // level 2 of the slice (k_state_to_m) and phis(m) first: plain loads
-    for (int i = tid; i < kSM; i += blockDim.x) {
-        const int cc = i % kCW, k = (i / kCW) % kKX, lev = (i / (kCW * kKX)) % 2, var = i / (2 * kKX * kCW);
-        if (lev != 1) continue;  // level 2 (lev index 1); level 1 comes from the combine
+    // every global load of the entry is issued before the first wait (one memory round
+    // trip): level 2 of the slice (k_state_to_m), phis(m), specy's operands and
+    // gridy's Legendre columns.  Element i = tid + 512 q of the slice has lev = q % 2,
+    // var = q / 2, k = tid / 64, cc = tid % 64.
+    constexpr int kSI = kSM / kSpecThreads;
+    static_assert(kSM % kSpecThreads == 0 && kSI == 10, "slice staging: ten rows of the block");
+    double s2[kSI / 2];
+#pragma unroll
+    for (int q = 1; q < kSI; q += 2) {  // level 2 (lev index 1); level 1 comes from the combine
+        const int cc = tid % kCW, k = tid / kCW, var = q / 2;
         const int c = ci(cc & 1, m, cc >> 1);
         double v = 0.0;
         if (var < 4) {
@@ -1624,28 +1632,54 @@ __global__ __launch_bounds__(kSpecThreads) void k_io_entry(const double *__restr
         } else if (k == 0) {
             v = state[kOffPs + (size_t)kSF + c];
         }
-        Sst[i] = v;
+        s2[q / 2] = v;
     }
-    for (int cc = tid; cc < kCW; cc += blockDim.x) Fm[cc] = phis[ci(cc & 1, m, cc >> 1)];
+    const double phis_m = tid < kCW ? phis[ci(tid & 1, m, tid >> 1)] : 0.0;
+    static_assert(2 * RT * kSpecThreads - kTabMDoubles <= kTabMPad, "TabM staging");
+    double2 rt[RT];
+    {
+        const double2 *t = reinterpret_cast<const double2 *>(tabm + (size_t)m * kTabMDoubles) + tid;
+#pragma unroll
+        for (int q = 0; q < RT; ++q) rt[q] = t[q * kSpecThreads];
+    }
     // a) specy of the io fields (k_specy: a wave per 8 fields x Re/Im)
-    if (wave < (kNIo + 7) / 8) {
-        const int f0 = wave * 8;
-        const int fa = f0 + (r >> 1);
-        const bool ok = fa < kNIo;
+    const bool spw = wave < (kNIo + 7) / 8;  // wave-uniform
+    const int f0 = wave * 8, fa = f0 + (r >> 1);
+    const bool ok = spw && fa < kNIo;
+    double vn[kIY / 4], vs[kIY / 4], wv[kIY / 4], bS[kIY / 4], bD[kIY / 4];
+    if (spw) {
         const double *vr = vio + (size_t)(ok ? fa : 0) * kVarmField + 2 * m + (r & 1);
         const double *pm = pfwd + (size_t)m * kNX * kIY;
-        d4 accS = {0, 0, 0, 0}, accD = accS;
 #pragma unroll
         for (int s = 0; s < kIY / 4; ++s) {
             const int j = 4 * s + kk;
+            vn[s] = vr[(kIL - 1 - j) * kMX2];
+            vs[s] = vr[j * kMX2];
+            wv[s] = wt[j];
+            bS[s] = pm[(2 * r) * kIY + j];
+            bD[s] = pm[(2 * r + 1) * kIY + j];
+        }
+    }
+    const GridyB gb = gridy_operands(pinv, m);
+    __builtin_amdgcn_sched_barrier(0);
+    // (the table stores first, in the loads' own block: behind a branch the loads
+    // were sunk next to them, after the first wait)
+#pragma unroll
+    for (int q = 0; q < RT; ++q) reinterpret_cast<double2 *>(V)[tid + q * kSpecThreads] = rt[q];
+#pragma unroll
+    for (int q = 1; q < kSI; q += 2) Sst[tid + kSpecThreads * q] = s2[q / 2];
+    if (tid < kCW) Fm[tid] = phis_m;
+    if (spw) {
+        d4 accS = {0, 0, 0, 0}, accD = accS;
+#pragma unroll
+        for (int s = 0; s < kIY / 4; ++s) {
             double aS = 0.0, aD = 0.0;
             if (ok) {
-                const double vn = vr[(kIL - 1 - j) * kMX2], vs = vr[j * kMX2];
-                aS = (vn + vs) * wt[j];
-                aD = (vn - vs) * wt[j];
+                aS = (vn[s] + vs[s]) * wv[s];
+                aD = (vn[s] - vs[s]) * wv[s];
             }
-            accS = MFMA64(aS, pm[(2 * r) * kIY + j], accS);
-            accD = MFMA64(aD, pm[(2 * r + 1) * kIY + j], accD);
+            accS = MFMA64(aS, bS[s], accS);
+            accD = MFMA64(aD, bD[s], accD);
         }
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -1658,11 +1692,11 @@ __global__ __launch_bounds__(kSpecThreads) void k_io_entry(const double *__restr
     }
     __syncthreads();
     // b) k_io_combine: vdspec's vds + spec, trunct, into level 1 (ppo_iogrid.f90:524-538)
-    const GTab tb{T, m};
+    const LTab tb{reinterpret_cast<const TabM *>(V)};
     const int cc = tid & (kCW - 1), k = tid / kCW, n = cc >> 1, p = cc & 1, c = ci(p, m, n);
     {
         auto fl = [&](int f) { return [=](int pp, int nn) { return S[f * kCW + 2 * nn + pp]; }; };
-        const double trf = T->trfilt[n][m];
+        const double trf = tb.trfilt_n(n);
         double vo, dv;
         vds_gen(fl(k), fl(kKX + k), tb, n, p, &vo, &dv);
         const double v0 = vo * trf, v1 = dv * trf, v2 = S[(2 * kKX + k) * kCW + cc] * trf,
@@ -1688,19 +1722,19 @@ __global__ __launch_bounds__(kSpecThreads) void k_io_entry(const double *__restr
     {
         auto vor = [&](int pp, int nn) { return Sst[smi(0, 1, k, 2 * nn + pp)]; };
         auto div = [&](int pp, int nn) { return Sst[smi(1, 1, k, 2 * nn + pp)]; };
-        const double ux = T->uvdx[n][m];
+        const double ux = tb.uvdx_n(n);
         const double zp = p == 1 ? ux * vor(0, n) : -ux * vor(1, n);
         const double zc = p == 1 ? ux * div(0, n) : -ux * div(1, n);
         double a, b;
         if (n == 0) {
-            a = zc - T->uvdyp[0][m] * vor(p, 1);
-            b = zp + T->uvdyp[0][m] * div(p, 1);
+            a = zc - tb.uvdyp_n(0) * vor(p, 1);
+            b = zp + tb.uvdyp_n(0) * div(p, 1);
         } else if (n == kNX - 1) {
-            a = T->uvdym[n][m] * vor(p, kNTRUN1 - 1);
-            b = -T->uvdym[n][m] * div(p, kNTRUN1 - 1);
+            a = tb.uvdym_n(n) * vor(p, kNTRUN1 - 1);
+            b = -tb.uvdym_n(n) * div(p, kNTRUN1 - 1);
         } else {
-            b = -T->uvdym[n][m] * div(p, n - 1) + T->uvdyp[n][m] * div(p, n + 1) + zp;
-            a = T->uvdym[n][m] * vor(p, n - 1) - T->uvdyp[n][m] * vor(p, n + 1) + zc;
+            b = -tb.uvdym_n(n) * div(p, n - 1) + tb.uvdyp_n(n) * div(p, n + 1) + zp;
+            a = tb.uvdym_n(n) * vor(p, n - 1) - tb.uvdyp_n(n) * vor(p, n + 1) + zc;
         }
         chk[(size_t)k * kSF + c] = a;
         chk[(size_t)(kKX + k) * kSF + c] = b;
@@ -1716,7 +1750,7 @@ __global__ __launch_bounds__(kSpecThreads) void k_io_entry(const double *__restr
     // e) k_st_inv: step(1, 1)'s inverse inputs (j2 = 1) and gridy
     inv_inputs(Sst, In, Fm, tb, m, 1, n1, nin);
     __syncthreads();
-    gridy_m(In, gridy_operands(pinv, m), varm, m, nin);
+    gridy_m(In, gb, varm, m, nin);
 }
 
 // entry safety check (:556-571): min / max of the re-gridded u, v, t, q.  One
@@ -1793,6 +1827,8 @@ extern "C" int sml_dyn_destroy(sml_dynamics *d) {
     return SML_OK;
 }
 
+static int upload_tabm(sml_dynamics *d, int i);
+
 extern "C" int sml_dyn_create(double radius, sml_dynamics **out) {
     SML_REQUIRE(out, "out is null");
     *out = nullptr;
@@ -1834,7 +1870,22 @@ extern "C" int sml_dyn_create(double radius, sml_dynamics **out) {
         sml_dyn_destroy(d);
         return fail(SML_ERR_HIP, "sml_dyn_create: %s", hipGetErrorString(e));
     }
+    // slot 0's per-m copy too: run_model's entry (k_io_entry) reads the current slot's
+    // TabM, before any impint when it is the first call
+    if (int rc = upload_tabm(d, 0)) {
+        sml_dyn_destroy(d);
+        return rc;
+    }
     *out = d;
+    return SML_OK;
+}
+
+// the per-m TabM copies of d->tab into slot i of d_tabm
+static int upload_tabm(sml_dynamics *d, int i) {
+    std::vector<double> tm((size_t)kMX * kTabMDoubles);
+    for (int m = 0; m < kMX; ++m)
+        for (int q = 0; q < kTabMDoubles; ++q) tm[(size_t)m * kTabMDoubles + q] = tabm_value(&d->tab, m, q);
+    SML_HIP(hipMemcpy(d->d_tabm + (size_t)i * kMX * kTabMDoubles, tm.data(), tm.size() * 8, hipMemcpyHostToDevice));
     return SML_OK;
 }
 
@@ -1853,12 +1904,7 @@ extern "C" int sml_dyn_impint(sml_dynamics *d, double dt, double alph) {
     // reading an evicted slot were launched earlier and complete first
     SML_HIP(hipDeviceSynchronize());
     SML_HIP(hipMemcpy(d->d_tabs + i, &d->tab, sizeof(DynTables), hipMemcpyHostToDevice));
-    {
-        std::vector<double> tm((size_t)kMX * kTabMDoubles);
-        for (int m = 0; m < kMX; ++m)
-            for (int q = 0; q < kTabMDoubles; ++q) tm[(size_t)m * kTabMDoubles + q] = tabm_value(&d->tab, m, q);
-        SML_HIP(hipMemcpy(d->d_tabm + (size_t)i * kMX * kTabMDoubles, tm.data(), tm.size() * 8, hipMemcpyHostToDevice));
-    }
+    if (int rc = upload_tabm(d, i)) return rc;
     d->slot_key[i][0] = dt;
     d->slot_key[i][1] = alph;
     d->slot_used[i] = true;
@@ -2355,8 +2401,9 @@ extern "C" int sml_dyn_run_model(sml_dynamics *d, const double *d_grid4d, const 
         const SpectralDev sd = spectral_dev(d->sp);
         const bool phys = d->phys_on;
         hipLaunchKernelGGL(k_io_entry, dim3(kMX), dim3(kSpecThreads), 0, st, d->d_vfm, sd.pfwd, sd.wt, d->d_state,
-                           d->d_sm, d->d_chk, d->d_phis, d->d_tab, sd.pinv, d->d_varm, phys ? kNInv1P : kNInv1,
-                           phys ? kNInvP : kNInv);
+                           d->d_sm, d->d_chk, d->d_phis,
+                           d->d_tabm + (size_t)(d->d_tab - d->d_tabs) * kMX * kTabMDoubles, sd.pinv, d->d_varm,
+                           phys ? kNInv1P : kNInv1, phys ? kNInvP : kNInv);
         SML_HIP(hipGetLastError());
         if (int rc = launch_io_check(d, st, nullptr)) return rc;
         if (int rc = window_impl(d, nleap, delt, alph, rob, wil, stream, true)) return rc;
@@ -2376,6 +2423,26 @@ extern "C" int sml_dyn_run_model(sml_dynamics *d, const double *d_grid4d, const 
     }
     return spectral_gridx_run_model_exit(d->sp, d->d_varm, d_fc4d, d_fc2d, kNIoWind,
                                          IoExit{0.000001, d->mm_last, d_grid4d, d_logp}, st);
+}
+
+extern "C" int sml_dyn_set_check_cus(sml_dynamics *d, int first_cu, int num_cus) {
+    SML_REQUIRE(d && first_cu >= 0 && num_cus >= 0, "bad argument");
+    if (d->chk_stream) {  // the old stream's check completes first
+        SML_HIP(hipStreamSynchronize(d->chk_stream));
+        SML_HIP(hipStreamDestroy(d->chk_stream));
+        d->chk_stream = nullptr;
+        d->chk_pending = false;
+    }
+    if (num_cus > 0) {
+        void *s = nullptr;
+        if (int rc = sml_stream_create_cu_range(first_cu, num_cus, &s)) return rc;
+        d->chk_stream = (hipStream_t)s;
+    } else {
+        SML_HIP(hipStreamCreateWithFlags(&d->chk_stream, hipStreamNonBlocking));
+    }
+    if (!d->ev_fork) SML_HIP(hipEventCreateWithFlags(&d->ev_fork, hipEventDisableTiming));
+    if (!d->ev_chk) SML_HIP(hipEventCreateWithFlags(&d->ev_chk, hipEventDisableTiming));
+    return SML_OK;
 }
 
 // run_speedy of the last sml_dyn_from_grid / sml_dyn_run_model (is_safe_to_run_speedy,

@@ -323,6 +323,13 @@ extern "C" int sml_hybrid_create(sml_reservoirs *res, sml_dynamics *dyn, sml_com
         if (const char *er = getenv("SML_RES_CUS")) res_cus = std::min(std::max(atoi(er), 1), ncu - speedy_cus);
         if (int rc = sml_stream_create_cu_range(speedy_cus, res_cus, &m)) return bail(rc);
         h->main = (hipStream_t)m;
+        // run_model's safety check (re-grid + min/max beside the window) on the CUs
+        // left over, else on the reservoir's: never on SPEEDY's, where its blocks
+        // slowed the window's first kernels (k_st_gridspec 21 vs 17.6 us, rocprof r02u)
+        const int spare = ncu - speedy_cus - res_cus;
+        if (int rc = spare > 0 ? sml_dyn_set_check_cus(dyn, speedy_cus + res_cus, spare)
+                               : sml_dyn_set_check_cus(dyn, speedy_cus, res_cus))
+            return bail(rc);
         if (int rc = sml_res_set_read_waves(res, 0)) return bail(rc);  // pacing pays only on shared CUs
     } else {
         if (hipStreamCreateWithFlags(&h->main, hipStreamNonBlocking) != hipSuccess)

@@ -42,7 +42,7 @@ EXPORTED = (
     "sml_train_create", "sml_train_destroy", "sml_train_reset", "sml_train_accumulate", "sml_train_solve",
     "sml_train_npad", "sml_train_get_gram", "sml_probe_mfma_f64",
     "sml_stream_create_cu_range", "sml_stream_destroy",
-    "sml_dyn_run_model", "sml_dyn_last_safe", "sml_res_info",
+    "sml_dyn_run_model", "sml_dyn_last_safe", "sml_dyn_set_check_cus", "sml_res_info",
     "sml_comm_unique_id", "sml_comm_create", "sml_comm_create_file", "sml_comm_destroy", "sml_comm_rank",
     "sml_comm_allgather",
     "sml_hybrid_create", "sml_hybrid_destroy", "sml_hybrid_set_buffers", "sml_hybrid_set_tisr",
@@ -169,6 +169,7 @@ def _declare(L: ctypes.CDLL) -> None:
         "sml_stream_destroy": [vp],
         "sml_dyn_run_model": [vp, vp, vp, i, d, d, d, d, vp, vp, vp],
         "sml_dyn_last_safe": [vp, ip, vp],
+        "sml_dyn_set_check_cus": [vp, i, i],
         "sml_res_info": [vp, ip, ip, ip, ip, vp],
         "sml_comm_unique_id": [vp],
         "sml_comm_create": [i, i, vp, pp],
