@@ -119,20 +119,30 @@ __global__ __launch_bounds__(kFftThreads) void k_gridx(const double *__restrict_
                                                        int nf, int c0, int c1, double *__restrict__ g4,
                                                        double *__restrict__ logp, IoExit ex) {
     __shared__ double was[kFftWa];  // twiddles: LDS broadcast reads inside the FFT
+    // transform (f, j) on the thread pair 2 t, 2 t + 1: thread h does half h of
+    // FFTPACK's rfftb (sml_fft.hpp rfftb96_half), the grid points 2 q + h.  The
+    // coefficients (and the exit's min/max) are loaded before the twiddles are staged:
+    // one memory round trip for both
+    const int id = blockIdx.x * kFftThreads + threadIdx.x;
+    const bool act = id < 2 * nf * kIL;
+    const int t = id >> 1, h = id & 1;
+    const int f = act ? t / kIL : 0, j = act ? t % kIL : 0;
+    double xi[kMX2 - 1];
+    if (act) {
+        const double *v = varm + (size_t)f * kVarmField + j * kMX2;
+        xi[0] = v[0];
+#pragma unroll
+        for (int e = 1; e <= kMX2 - 2; ++e) xi[e] = v[e + 1];
+    }
+    double mmv[8];
+    if (ex.mm) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) mmv[q] = ex.mm[q];
+    }
     if (threadIdx.x < kFftWa) was[threadIdx.x] = wa[threadIdx.x];
     if (threadIdx.x + kFftThreads < kFftWa) was[threadIdx.x + kFftThreads] = wa[threadIdx.x + kFftThreads];
     __syncthreads();
-    // transform (f, j) on the thread pair 2 t, 2 t + 1: thread h does half h of
-    // FFTPACK's rfftb (sml_fft.hpp rfftb96_half), the grid points 2 q + h
-    const int id = blockIdx.x * kFftThreads + threadIdx.x;
-    if (id >= 2 * nf * kIL) return;
-    const int t = id >> 1, h = id & 1;
-    const int f = t / kIL, j = t % kIL;
-    const double *v = varm + (size_t)f * kVarmField + j * kMX2;
-    double xi[kMX2 - 1];
-    xi[0] = v[0];
-#pragma unroll
-    for (int e = 1; e <= kMX2 - 2; ++e) xi[e] = v[e + 1];
+    if (!act) return;
     double y[kFftN / 2];
     fft::rfftb96_half([&](int e) { return e <= kMX2 - 2 ? xi[e] : 0.0; }, h, y, was);
     const bool k2 = f >= c0 && f < c1;
@@ -153,7 +163,7 @@ __global__ __launch_bounds__(kFftThreads) void k_gridx(const double *__restrict_
         }
         if (ex.mm) {  // run_model's exit (uniform across the launch: every thread reads the same flag)
             const bool q = grp == 3;
-            if (!io_state_safe(ex.mm)) {  // integration skipped: the input grid comes back
+            if (!io_state_safe(mmv)) {  // integration skipped: the input grid comes back
                 const double *src = grp < 4 ? ex.in4 + o : ex.inlp + o;
 #pragma unroll
                 for (int qq = 0; qq < kFftN / 2; ++qq) {
@@ -188,42 +198,54 @@ __global__ __launch_bounds__(kFftThreads) void k_specx(const double *__restrict_
                                                        const double *__restrict__ logp = nullptr) {
     __shared__ double was[kFftWa];
     __shared__ double S[kFftN * (kFftThreads / 2)];  // a pair's two n = 48 halves (E, O)
-    if (threadIdx.x < kFftWa) was[threadIdx.x] = wa[threadIdx.x];
-    if (threadIdx.x + kFftThreads < kFftWa) was[threadIdx.x + kFftThreads] = wa[threadIdx.x + kFftThreads];
-    __syncthreads();
     // transform (f, j) on the thread pair 2 t, 2 t + 1: thread h transforms the samples
-    // 2 i + h (rfftf48), the pair meets in LDS for rfftf's last pass (rfftf96_combine)
+    // 2 i + h (rfftf48), the pair meets in LDS for rfftf's last pass (rfftf96_combine).
+    // The samples are loaded before the twiddles are staged (one memory round trip).
     const int id = blockIdx.x * kFftThreads + threadIdx.x;
     const bool act = id < 2 * nf * kIL;
     const int t = id >> 1, h = id & 1, pr = threadIdx.x >> 1;
     const int f = act ? t / kIL : 0, j = act ? t % kIL : 0;
     double x[kFftN / 2];
+    const bool sc = act && scale_tab && f < nscaled;
+    double s0 = 1.0;
     if (act) {
         const double *g = grid + (size_t)f * kGridField + j * kIX + h;
-        const bool sc = scale_tab && f < nscaled;
-        const double s0 = sc ? scale_tab[j] : 1.0;
+        if (sc) s0 = scale_tab[j];
         if (g4) {
             const int grp = f / kKX, k = f % kKX;
             if (grp < 4) {
                 const int var = grp == 0 ? 1 : grp == 1 ? 2 : grp == 2 ? 0 : 3;
                 const double *src = g4 + var + 4 * ((size_t)kGridField * k + j * kIX + h);
 #pragma unroll
-                for (int i = 0; i < kFftN / 2; ++i) {
-                    float v4 = (float)src[8 * i];
-                    if (grp == 3 && v4 < 0.0f) v4 = 0.0f;
-                    x[i] = (double)v4;
-                }
+                for (int i = 0; i < kFftN / 2; ++i) x[i] = src[8 * i];
             } else {
 #pragma unroll
-                for (int i = 0; i < kFftN / 2; ++i) x[i] = (double)(float)logp[j * kIX + 2 * i + h];
+                for (int i = 0; i < kFftN / 2; ++i) x[i] = logp[j * kIX + 2 * i + h];
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < kFftN / 2; ++i) x[i] = g[2 * i];
+        }
+    }
+    if (threadIdx.x < kFftWa) was[threadIdx.x] = wa[threadIdx.x];
+    if (threadIdx.x + kFftThreads < kFftWa) was[threadIdx.x + kFftThreads] = wa[threadIdx.x + kFftThreads];
+    __syncthreads();
+    if (act) {
+        if (g4) {  // iogrid(30)'s real(4) copies, q < 0 -> 0 on the copy
+            const bool qf = f / kKX == 3;
+#pragma unroll
+            for (int i = 0; i < kFftN / 2; ++i) {
+                float v4 = (float)x[i];
+                if (qf && v4 < 0.0f) v4 = 0.0f;
+                x[i] = (double)v4;
             }
             if (sc) {
 #pragma unroll
                 for (int i = 0; i < kFftN / 2; ++i) x[i] = x[i] * s0;
             }
-        } else {
+        } else if (sc) {
 #pragma unroll
-            for (int i = 0; i < kFftN / 2; ++i) x[i] = sc ? g[2 * i] * s0 : g[2 * i];
+            for (int i = 0; i < kFftN / 2; ++i) x[i] = x[i] * s0;
         }
         fft::rfftf48_reg(x, was);
 #pragma unroll
