@@ -566,7 +566,7 @@ __device__ inline void tail_coef(SA S, double *__restrict__ Td, double *__restri
     for (int kk = kKX - 2; kk >= k; --kk)
         phi = phi + tb.xgeop2(kk + 1) * sh[1][kk + 1][cc] + tb.xgeop1(kk) * sh[1][kk][cc];
     if (m == 0 && k >= 1 && k <= kKX - 2) phi = phi + tb.corf(k) * (sh[1][k + 1][cc] - sh[1][k - 1][cc]);
-    phi_out[(size_t)k * kSF + c] = phi;
+    if (phi_out) phi_out[(size_t)k * kSF + c] = phi;
     {
         const double d1 = phi + kRgas * tb.tref(k) * S(4, j4, 0);
         const double lapd = -(d1 * tb.el2_n(n));
@@ -618,6 +618,7 @@ __device__ inline void tail_coef(SA S, double *__restrict__ Td, double *__restri
         trdt = (trdt - dmpd * cq) * dmp1d;
     }
     if (dt <= 0.0) {  // tendencies only (dyn_step.f90:109)
+        if (!Td) return;
         Td[kTVor + (size_t)k * kSF + c] = vordt;
         Td[kTDiv + (size_t)k * kSF + c] = divdt;
         Td[kTT + (size_t)k * kSF + c] = tdt;
@@ -831,11 +832,13 @@ __device__ inline GridyB gridy_operands(const double *__restrict__ pinv, int m) 
     return g;
 }
 
-__device__ inline void gridy_m(const double *In, const GridyB &gb, double *__restrict__ varm, int m, int nf) {
+__device__ inline void gridy_m(const double *In, const GridyB &gb, double *__restrict__ varm, int m, int nf,
+                               int tile0 = 0, int tile1 = -1) {
     const int wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
     const int l = threadIdx.x & 63, r = l & 15, kk = l >> 4;
     const double *b00 = gb.b00, *b01 = gb.b01, *b10 = gb.b10, *b11 = gb.b11;
-    for (int tile = wave; tile < (nf + 7) / 8; tile += nw) {
+    const int tend = tile1 < 0 ? (nf + 7) / 8 : tile1;
+    for (int tile = tile0 + wave; tile < tend; tile += nw) {
         const int f0 = tile * 8;
         const int fa = f0 + (r >> 1), p = r & 1;
         const bool ok = fa < nf;
@@ -961,6 +964,7 @@ __device__ inline void load_forcing_m(double *Fm, const double *__restrict__ phi
 
 constexpr int kSpecThreads = kCW * kKX;  // 512: one thread per (coefficient, level) of one m
 constexpr int kSpecBlk = 512;             // k_st_spec's block (768: specy -0.6 us, staging +1.2 us, gridy unchanged)
+constexpr int kSpecSplit = 2;             // k_st_spec blocks per m (the next step's gridy tiles split between them)
 
 // window start: the inverse transforms of step (.., j2) from the m-major state
 __global__ __launch_bounds__(kSpecThreads) void k_st_inv(const double *__restrict__ sm, const double *__restrict__ phis,
@@ -1382,7 +1386,12 @@ __global__ __launch_bounds__(kSpecBlk) void k_st_spec(
     __shared__ double sh[2][kKX][kCW];
     __shared__ double Sst[kSM];           // this m's state, updated in place
     __shared__ double Fm[3 * kCW];        // phis, tcorh, qcorh of this m
-    const int m = blockIdx.x;
+    // kSpecSplit blocks per m: each repeats the m's specy, combine and tail (on CUs that
+    // would idle), and takes its share of the next step's gridy tiles; the lead block
+    // (half 0) alone writes the state, phi and the stamps
+    const int m = blockIdx.x % kMX, half = blockIdx.x / kMX;
+    const bool lead = half == 0;
+    if (!lead) dbg = nullptr;
     const int wave = threadIdx.x >> 6, l = threadIdx.x & 63, r = l & 15, kk = l >> 4;
     const int sk = next_j2 > 0 ? 1 : 3;
     stamp(dbg, sk, 0);
@@ -1517,13 +1526,14 @@ __global__ __launch_bounds__(kSpecBlk) void k_st_spec(
     // c) sptend / implic / diffusion / time integration on the LDS state
     auto SA = [&](int var, int lev, int kk2) -> double & { return Sst[smi(var, lev, kk2, cc)]; };
     if (holds)
-        tail_coef<kCW>(SA, Td, phi_out, Fm, Fm + kCW, Fm + 2 * kCW, cc, tb, sh, cc, k, c, m, n, vo, dv - lapv, tdt0,
+        tail_coef<kCW>(SA, lead ? Td : nullptr, lead ? phi_out : nullptr, Fm, Fm + kCW, Fm + 2 * kCW, cc, tb, sh, cc, k, c, m, n, vo, dv - lapv, tdt0,
                        trdt0, psdt, j1, j4, dt, alph, rob, wil);
     else
         tail_coef_barriers(alph);
     __syncthreads();  // S is free, Sst complete
     stamp(dbg, sk, 4);
     if (next_j2 <= 0) {  // the run of fused steps ends: the state straight into the reference layout
+        if (!lead) return;  // block-uniform
         for (int i = threadIdx.x; i < kSM; i += kSpecBlk) put_state(state_out, m, i, Sst[i]);
         if (io_varm) {  // run_model: iogrid(31)'s k_io_prep + gridy of this m (block-uniform)
             if (holds) io_prep_m(Sst, tb, k, cc, [&](int f, double v) { S[f * kCW + cc] = v; });
@@ -1532,7 +1542,7 @@ __global__ __launch_bounds__(kSpecBlk) void k_st_spec(
         }
         return;  // block-uniform
     }
-    {
+    if (lead) {
         double2 *dst = reinterpret_cast<double2 *>(sm + (size_t)m * kSM);
         for (int i = threadIdx.x; i < kSM / 2; i += kSpecBlk) dst[i] = reinterpret_cast<const double2 *>(Sst)[i];
     }
@@ -1540,7 +1550,10 @@ __global__ __launch_bounds__(kSpecBlk) void k_st_spec(
     if (holds) inv_inputs(Sst, S, Fm, tb, m, next_j2, n1, nin);
     __syncthreads();
     stamp(dbg, sk, 5);
-    gridy_m(S, gridy_operands(pinv, m), varm_next, m, nin);
+    {
+        const int nt = (nin + 7) / 8, per = (nt + kSpecSplit - 1) / kSpecSplit;
+        gridy_m(S, gridy_operands(pinv, m), varm_next, m, nin, half * per, min(nt, (half + 1) * per));
+    }
     if (dbg) {  // (diagnostics only: the kernel ends here)
         __syncthreads();
         stamp(dbg, sk, 6);
@@ -2046,7 +2059,7 @@ int launch_step_fused(sml_dynamics *d, int j1, int j2, double dt, double alph, d
         SML_HIP(hipGetLastError());
     }
     const int j4 = (alph == 0.0) ? j2 : 1;
-    hipLaunchKernelGGL(k_st_spec, dim3(kMX), dim3(kSpecBlk), 0, st, d->d_vfm, sd.pfwd, sd.wt, d->d_sm, d->d_tend,
+    hipLaunchKernelGGL(k_st_spec, dim3(kMX * kSpecSplit), dim3(kSpecBlk), 0, st, d->d_vfm, sd.pfwd, sd.wt, d->d_sm, d->d_tend,
                        d->d_phi, d->d_phis, d->d_tcorh, d->d_qcorh, T, j1, j4, dt, alph, rob, wil, sd.pinv, d->d_varm,
                        next_j2, n1, nin, d->d_tabm + (size_t)(d->d_tab - d->d_tabs) * kMX * kTabMDoubles, d->d_state,
                        next_j2 > 0 ? nullptr : d->io_exit, d->d_dbg);
