@@ -369,7 +369,13 @@ def speedy_roofline(st, forcing, bc):
     g = pmc.get("k_st_gridspec", {})
     spec_last, inv = pmc.get("k_st_spec", {}), pmc.get("k_st_inv", {})
     valu_g = g.get("valu_f64_flops_per_dispatch")
-    specy_fl = spec_last.get("mfma_f64_flops_per_dispatch")  # specy (the launched-mode k_st_spec has no gridy)
+    # specy (the launched-mode k_st_spec has no gridy); each of its kSpecSplit blocks per
+    # m repeats the m's specy (csrc/sml_dynamics.hip), so the algorithmic flops are the
+    # counted ones / kSpecSplit and the kernel occupies kSpecSplit CUs per m
+    spec_split = 2
+    specy_fl = spec_last.get("mfma_f64_flops_per_dispatch")
+    if specy_fl:
+        specy_fl = specy_fl / spec_split
     gridy_fl = inv.get("mfma_f64_flops_per_dispatch")        # gridy (k_st_inv)
     out = {"source": "phase stamps (live, chained window) + profiles/speedy_pmc.json (work per dispatch)",
            "peak_f64_valu_tflops": F64_VALU_PEAK_TF, "peak_f64_mfma_tflops": F64_MFMA_PEAK_TF}
@@ -386,8 +392,9 @@ def speedy_roofline(st, forcing, bc):
         leg = specy_fl + gridy_fl
         sy = specy_fl / (ph_s["specy"] * 1e-6) / 1e12
         gy = gridy_fl / (ph_s["gridy"] * 1e-6) / 1e12
-        occ = F64_MFMA_PEAK_TF * nb_s / 256
+        occ = F64_MFMA_PEAK_TF * nb_s * spec_split / 256
         e.update({
+            "blocks": nb_s * spec_split,
             "legendre_mfma_flops": leg,
             "achieved_tflops_kernel": round(leg / (span_s * 1e-6) / 1e12, 3),
             "legendre_mfma_utilisation": {

@@ -85,7 +85,8 @@ struct sml_dynamics {
     double *d_phis = nullptr, *d_tcorh = nullptr, *d_qcorh = nullptr, *d_phi = nullptr;
     double *d_specin = nullptr, *d_varm = nullptr, *d_grid = nullptr, *d_gfwd = nullptr, *d_sfwd = nullptr;
     double *d_vfm = nullptr;  // fused step: m-major forward Fourier coefficients [m][73][lat][2]
-    double *d_sm = nullptr;   // fused step: m-major state [m][var 5][lev 2][kx][n p]
+    double *d_sm = nullptr;   // fused step: m-major state [2][m][var 5][lev 2][kx][n p], ping-pong:
+    int sm_cur = 0;           // k_st_spec reads buffer sm_cur and writes the other (see sm_buf)
     long long *d_dbg = nullptr;  // diagnostic phase stamps (SML_DYN_STAMPS=1)
     double *d_tend = nullptr;
     double *d_phys = nullptr;  // physics tendencies: staging for a host's, or the GPU phypar's output
@@ -1376,7 +1377,8 @@ __global__ __launch_bounds__(kGsThreads) void k_st_gridspec(
 // in LDS; with next_j2 > 0 the new state feeds the next step's inverse transforms
 __global__ __launch_bounds__(kSpecBlk) void k_st_spec(
     const double *__restrict__ vfm, const double *__restrict__ pfwd, const double *__restrict__ wt,
-    double *__restrict__ sm, double *__restrict__ Td, double *__restrict__ phi_out, const double *__restrict__ phis,
+    const double *__restrict__ sm, double *__restrict__ sm_out, double *__restrict__ Td, double *__restrict__ phi_out,
+    const double *__restrict__ phis,
     const double *__restrict__ tcorh, const double *__restrict__ qcorh, const DynTables *__restrict__ T, int j1,
     int j4, double dt, double alph, double rob, double wil, const double *__restrict__ pinv,
     double *__restrict__ varm_next, int next_j2, int n1, int nin, const double *__restrict__ tabm,
@@ -1542,8 +1544,8 @@ __global__ __launch_bounds__(kSpecBlk) void k_st_spec(
         }
         return;  // block-uniform
     }
-    if (lead) {
-        double2 *dst = reinterpret_cast<double2 *>(sm + (size_t)m * kSM);
+    if (lead) {  // into the other buffer: this m's second block may still be reading sm
+        double2 *dst = reinterpret_cast<double2 *>(sm_out + (size_t)m * kSM);
         for (int i = threadIdx.x; i < kSM / 2; i += kSpecBlk) dst[i] = reinterpret_cast<const double2 *>(Sst)[i];
     }
     // d) the next step's inverse-transform inputs (k_dyn_prep) and gridy
@@ -1867,7 +1869,7 @@ extern "C" int sml_dyn_create(double radius, sml_dynamics **out) {
         (rc = dalloc(&d->d_varm, (size_t)(kNInvMax > kNFwd ? kNInvMax : kNFwd) * kVF)) ||
         (rc = dalloc(&d->d_grid, (size_t)kNInvMax * kGF)) || (rc = dalloc(&d->d_gfwd, (size_t)kNFwd * kGF)) ||
         (rc = dalloc(&d->d_sfwd, (size_t)kNFwd * kSF)) || (rc = dalloc(&d->d_tend, kTendSize)) ||
-        (rc = dalloc(&d->d_vfm, (size_t)kMX * kVFm)) || (rc = dalloc(&d->d_sm, (size_t)kMX * kSM)) ||
+        (rc = dalloc(&d->d_vfm, (size_t)kMX * kVFm)) || (rc = dalloc(&d->d_sm, (size_t)2 * kMX * kSM)) ||
         (rc = dalloc(&d->d_phys, (size_t)4 * kKX * kGF)) || (rc = dalloc(&d->d_minmax, 8)) ||
         (rc = dalloc(&d->d_io, (size_t)4 * kKX * kGF + kGF)) || (rc = dalloc(&d->d_ptab, 1)) ||
         (rc = dalloc(&d->d_chk, (size_t)kNIo * (kSF + kVF + kGF))) ||
@@ -2026,6 +2028,10 @@ int launch_step_unfused(sml_dynamics *d, int j1, int j2, double dt, double alph,
 // prepares step (.., next_j2) and the state stays m-major, else it writes the
 // reference-layout state.
 
+// buffer b of the m-major state (two, so k_st_spec's second block of an m never
+// reads a slice its lead block already advanced)
+double *sm_buf(sml_dynamics *d, int b) { return d->d_sm + (size_t)b * kMX * kSM; }
+
 int launch_step_fused(sml_dynamics *d, int j1, int j2, double dt, double alph, double rob, double wil,
                       const double *d_phys, bool lradsw, hipStream_t st, bool chained, int next_j2) {
     const DynTables *T = d->d_tab;
@@ -2034,11 +2040,12 @@ int launch_step_fused(sml_dynamics *d, int j1, int j2, double dt, double alph, d
     const SpectralDev sd = spectral_dev(d->sp);
     if (dt <= 0.0) next_j2 = 0;  // tendencies only: the state does not advance
     const int conv_blocks = (kMX * kSM + 255) / 256;
-    if (!chained) {
-        hipLaunchKernelGGL(k_state_to_m, dim3(conv_blocks), dim3(256), 0, st, d->d_state, d->d_sm);
+    if (!chained) {  // a chain starts in buffer 0 (so a captured window replays the same pointers)
+        d->sm_cur = 0;
+        hipLaunchKernelGGL(k_state_to_m, dim3(conv_blocks), dim3(256), 0, st, d->d_state, sm_buf(d, 0));
         SML_HIP(hipGetLastError());
-        hipLaunchKernelGGL(k_st_inv, dim3(kMX), dim3(kSpecThreads), 0, st, d->d_sm, d->d_phis, T, sd.pinv, d->d_varm,
-                           j2, n1, nin);
+        hipLaunchKernelGGL(k_st_inv, dim3(kMX), dim3(kSpecThreads), 0, st, sm_buf(d, 0), d->d_phis, T, sd.pinv,
+                           d->d_varm, j2, n1, nin);
         SML_HIP(hipGetLastError());
     }
     if (phys) {
@@ -2059,7 +2066,10 @@ int launch_step_fused(sml_dynamics *d, int j1, int j2, double dt, double alph, d
         SML_HIP(hipGetLastError());
     }
     const int j4 = (alph == 0.0) ? j2 : 1;
-    hipLaunchKernelGGL(k_st_spec, dim3(kMX * kSpecSplit), dim3(kSpecBlk), 0, st, d->d_vfm, sd.pfwd, sd.wt, d->d_sm, d->d_tend,
+    const int cur = d->sm_cur;
+    if (next_j2 > 0) d->sm_cur = 1 - cur;  // the next step reads what this one writes
+    hipLaunchKernelGGL(k_st_spec, dim3(kMX * kSpecSplit), dim3(kSpecBlk), 0, st, d->d_vfm, sd.pfwd, sd.wt,
+                       sm_buf(d, cur), sm_buf(d, 1 - cur), d->d_tend,
                        d->d_phi, d->d_phis, d->d_tcorh, d->d_qcorh, T, j1, j4, dt, alph, rob, wil, sd.pinv, d->d_varm,
                        next_j2, n1, nin, d->d_tabm + (size_t)(d->d_tab - d->d_tabs) * kMX * kTabMDoubles, d->d_state,
                        next_j2 > 0 ? nullptr : d->io_exit, d->d_dbg);
@@ -2413,8 +2423,9 @@ extern "C" int sml_dyn_run_model(sml_dynamics *d, const double *d_grid4d, const 
         if (int rc = spectral_specx_io(d->sp, d_grid4d, d_logp, d->d_vfm, kNIoWind, st)) return rc;
         const SpectralDev sd = spectral_dev(d->sp);
         const bool phys = d->phys_on;
+        d->sm_cur = 0;  // the window's chain starts in buffer 0
         hipLaunchKernelGGL(k_io_entry, dim3(kMX), dim3(kSpecThreads), 0, st, d->d_vfm, sd.pfwd, sd.wt, d->d_state,
-                           d->d_sm, d->d_chk, d->d_phis,
+                           sm_buf(d, 0), d->d_chk, d->d_phis,
                            d->d_tabm + (size_t)(d->d_tab - d->d_tabs) * kMX * kTabMDoubles, sd.pinv, d->d_varm,
                            phys ? kNInv1P : kNInv1, phys ? kNInvP : kNInv);
         SML_HIP(hipGetLastError());
