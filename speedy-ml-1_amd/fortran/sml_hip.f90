@@ -321,6 +321,13 @@ module sml_hip
       integer(c_int) :: rc
     end function
 
+    function sml_dyn_set_check_cus(ctx, first_cu, num_cus) bind(C, name='sml_dyn_set_check_cus') result(rc)
+      import :: c_ptr, c_int
+      type(c_ptr), value :: ctx
+      integer(c_int), value :: first_cu, num_cus
+      integer(c_int) :: rc
+    end function
+
     ! ------------------------------------------------------------ communicator (RCCL)
     !> startmpi's world (mpires.f90:21-37) for the one collective of the hot path;
     !> the unique id travels through a file rank 0 writes
