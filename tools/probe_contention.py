@@ -1,5 +1,6 @@
 """Diagnostic: the SPEEDY window's time beside other work on the reservoir's CUs.
-Full-size reservoirs (1152 regions), SPEEDY on CUs [0, 64), the rest on [64, 256):
+Full-size reservoirs (1152 regions), SPEEDY on CUs [0, 64), the partner on [64, 224) as
+in the hybrid loop:
 alone, beside predict_begin (update + v_ml readout), beside a plain HBM copy and
 beside a plain HBM read of about the readout's byte count.
     python tools/probe_contention.py"""
@@ -36,7 +37,7 @@ dyn.set_physics(phys_boundary(dyn, forcing["phis"]))
 L = lib()
 s_side, s_main = ctypes.c_void_p(), ctypes.c_void_p()
 check(L.sml_stream_create_cu_range(0, 64, ctypes.byref(s_side)))
-check(L.sml_stream_create_cu_range(64, 192, ctypes.byref(s_main)))
+check(L.sml_stream_create_cu_range(64, 160, ctypes.byref(s_main)))
 side = torch.cuda.ExternalStream(s_side.value, device=dev)
 main = torch.cuda.ExternalStream(s_main.value, device=dev)
 nbytes = 3_700_000_000
