@@ -519,8 +519,15 @@ extern "C" int sml_hybrid_step(sml_hybrid *h) {
         return sml_hybrid_advance(h, h->ov);
     }
     const size_t slab = (size_t)h->maxc * h->nout;
-    SML_HIP(hipMemcpyAsync(h->d_send, h->ov, (size_t)h->nlocal * h->nout * 8, hipMemcpyDeviceToDevice, h->main));
-    if (int rc = sml_comm_allgather(h->comm, h->d_send, h->d_recv, (int64_t)slab, h->main)) return rc;
+    // even shares (1152 / N for N = 1, 2, 4, 8): the outvecs go out of ov as they are;
+    // uneven ones are padded to the largest share through d_send (one copy more on the
+    // critical path)
+    const double *send = h->ov;
+    if (h->nlocal != h->maxc) {
+        SML_HIP(hipMemcpyAsync(h->d_send, h->ov, (size_t)h->nlocal * h->nout * 8, hipMemcpyDeviceToDevice, h->main));
+        send = h->d_send;
+    }
+    if (int rc = sml_comm_allgather(h->comm, send, h->d_recv, (int64_t)slab, h->main)) return rc;
     const double *glob = h->d_recv;
     if (!h->contiguous) {
         const int total = h->numregions * h->nout;

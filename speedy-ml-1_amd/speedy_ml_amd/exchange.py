@@ -46,8 +46,13 @@ class OutvecExchange:
 
         if self.world == 1:
             return ov_local
-        self.send[:self.nlocal].copy_(ov_local)
-        dist.all_gather_into_tensor(self.recv, self.send, group=self.group)
+        if (self.nlocal == self.maxc and ov_local.is_contiguous() and ov_local.shape == self.send.shape
+                and ov_local.dtype == self.send.dtype):
+            src = ov_local  # even shares: sent as they are, no copy on the step's critical path
+        else:
+            self.send[:self.nlocal].copy_(ov_local)
+            src = self.send
+        dist.all_gather_into_tensor(self.recv, src, group=self.group)
         if self.contiguous:
             return self.recv
         torch.index_select(self.recv, 0, self.perm, out=self.glob)
