@@ -70,6 +70,10 @@ def parse():
     p.add_argument("--train-steps", type=int, default=4096, help="training time steps per region in that leg")
     p.add_argument("--reservoir-steps", type=int, default=50,
                    help="steps timed in the supplementary reservoir-only (configs[1]) leg (0 = skip)")
+    p.add_argument("--exchange", choices=("native", "torch"), default="native",
+                   help="N > 1: the outvec all-gather as the library's own ncclAllGather on the loop's main "
+                        "stream (speedy_ml_amd.comm, sml_hybrid_step; default) or torch.distributed's "
+                        "all_gather between predict and advance (its NCCL stream, two event hops)")
     p.add_argument("--sim-ranks", type=int, default=1,
                    help="diagnostic: run rank 0's share of an N-rank decomposition on this one GPU, the "
                         "all-gather replaced by a local copy (other ranks' outvecs stale); never the headline")
@@ -146,7 +150,13 @@ def main():
     # the hybrid loop (speedy_ml_amd/hybrid.py); --overlap puts SPEEDY's window on a
     # second stream beside the reservoir update + v_ml readout
     ncu = torch.cuda.get_device_properties(dev).multi_processor_count
-    loop = HybridLoop(res, dyn, exchange, dev, tisr=tisr, overlap=args.overlap, speedy_cus=args.speedy_cus)
+    comm = None
+    if world > 1 and sim == 1 and args.exchange == "native":
+        from speedy_ml_amd.comm import NativeComm
+
+        comm = NativeComm(world, rank)
+    loop = HybridLoop(res, dyn, exchange, dev, tisr=tisr, overlap=args.overlap, speedy_cus=args.speedy_cus,
+                      comm=comm)
     # initial inputs from the synthetic analysis state (start_prediction analogue)
     loop.start(t(g4h), t(g2h), t(prh), t(f4h), t(f2h))
     fb, lm, ov, g4, g2, pr, f4, f2 = loop.fb, loop.lm, loop.ov, loop.g4, loop.g2, loop.pr, loop.f4, loop.f2
@@ -263,7 +273,9 @@ def main():
                 "workload": f"configs[{2 if world == 1 else 3}]: full hybrid timestep -- reservoir predict for all "
                             "1152 subdomains, "
                             + ("outvec exchange (identity on one GPU)" if world == 1 else
-                               f"outvec all-gather over RCCL ({world} ranks)")
+                               f"outvec all-gather over RCCL ({world} ranks, "
+                               + ("the library's ncclAllGather on the loop's main stream)" if comm is not None
+                                  else "torch.distributed)"))
                             + ", assemble, SPEEDY 6-h window (iogrid(30), stepone + 24 leapfrog dyn_steps with "
                               "phypar physics, iogrid(31)) on the GPU, re-tile",
                 "regions": nreg,
@@ -309,6 +321,9 @@ def main():
             "training": training,
         }
         print(json.dumps(line), flush=True)
+    loop.close()  # before the communicators go: the loop's streams are drained first
+    if comm is not None:
+        comm.close()
     if world > 1:
         dist.destroy_process_group()
 

@@ -16,7 +16,8 @@ owns the device buffers (torch tensors: plumbing only) and supplies the exchange
 between the two halves of a step: `predict` leaves the local outvecs on the loop's
 main stream, `exchange` (speedy_ml_amd.exchange: torch.distributed all-gather, RCCL
 over xGMI when world > 1) runs on that stream, `advance` takes every region's
-outvecs.
+outvecs.  With a NativeComm (speedy_ml_amd.comm) the exchange is the library's own
+ncclAllGather on the main stream instead (sml_hybrid_step).
 
 Schedule (overlap=True): the reservoir's update and ~98 % of
 its readout bytes run on the main stream while SPEEDY integrates the previous
@@ -42,8 +43,8 @@ class HybridLoop:
     tisr inputs (device) or None (feedback tisr entries left as they are)."""
 
     def __init__(self, res, dyn, exchange, device, tisr=None, overlap: bool = True, nleap: int = 24,
-                 speedy_cus: int | None = None, delt: float = DELT):
-        self.res, self.dyn, self.exchange, self.tisr = res, dyn, exchange, tisr
+                 speedy_cus: int | None = None, delt: float = DELT, comm=None):
+        self.res, self.dyn, self.exchange, self.tisr, self.comm = res, dyn, exchange, tisr, comm
         self.overlap, self.nleap = overlap, nleap
         self.dev = torch.device(device)
         self.fb, self.lm, self.ov = res.alloc_io(self.dev)
@@ -55,7 +56,8 @@ class HybridLoop:
             speedy_cus = int(os.environ.get("SML_SPEEDY_CUS", "64"))
         h = ctypes.c_void_p()
         with torch.cuda.device(self.dev):
-            check(lib().sml_hybrid_create(res.handle, dyn._h, None, nleap, delt, ALPH, ROB, WIL, int(overlap),
+            check(lib().sml_hybrid_create(res.handle, dyn._h, comm.handle if comm is not None else None, nleap, delt,
+                                          ALPH, ROB, WIL, int(overlap),
                                           int(speedy_cus if overlap else 0), ctypes.byref(h)))
         self._h = h
         check(lib().sml_hybrid_set_buffers(h, ptr(self.fb), ptr(self.lm if res.ncs else None), ptr(self.ov),
@@ -99,7 +101,13 @@ class HybridLoop:
         check(lib().sml_hybrid_start(self._h, ptr(g4), ptr(g2), ptr(pr), ptr(f4), ptr(f2)))
 
     def step(self):
-        """One hybrid time step (asynchronous; `sync()` waits for it)."""
+        """One hybrid time step (asynchronous; `sync()` waits for it).  With a
+        NativeComm (speedy_ml_amd.comm) the whole step is native, its all-gather on
+        the main stream (sml_hybrid_step); else `exchange` runs between predict and
+        advance."""
+        if self.comm is not None:
+            check(lib().sml_hybrid_step(self._h))
+            return
         check(lib().sml_hybrid_predict(self._h))
         with torch.cuda.stream(self.main):
             glob = self.exchange(self.ov)  # RCCL all-gather over xGMI when world > 1

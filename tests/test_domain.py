@@ -63,3 +63,18 @@ def test_processor_decomposition_partitions():
 def test_radius_by_region_matches_oracle():
     for r in range(0, 1152, 7):
         assert domain.radius_by_region(r) == oracle.radius_by_region(r)
+
+
+def test_native_decomposition_matches_python():
+    """sml_processor_decomposition (the native loop's check of its communicator's
+    rank, sml_hybrid_create) gives every rank the regions the Python host loads."""
+    import ctypes
+
+    from speedy_ml_amd._lib import check, lib
+
+    buf = (ctypes.c_int * 1152)()
+    cnt = ctypes.c_int()
+    for nproc in (1, 2, 3, 4, 7, 8, 16):
+        for rank in range(nproc):
+            check(lib().sml_processor_decomposition(1152, nproc, rank, buf, ctypes.byref(cnt)))
+            assert list(buf[:cnt.value]) == domain.processor_decomposition(1152, nproc, rank), (nproc, rank)

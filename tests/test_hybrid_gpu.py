@@ -54,7 +54,7 @@ def test_begin_finish_matches_oracle_and_checks_order(cuda):
         assert xerr.max() < 1e-14, f"region {w.region}: state {xerr.max():.3e}"  # device vs glibc tanh
 
 
-def _loop(cuda, overlap, speedy_cus=None):
+def _loop(cuda, overlap, speedy_cus=None, comm=None):
     import torch
 
     from speedy_ml_amd.dynamics import Dynamics
@@ -77,7 +77,7 @@ def _loop(cuda, overlap, speedy_cus=None):
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(cuda)  # noqa: E731
     tisr = t(np.random.default_rng(13).standard_normal((1152, 16)))
     loop = HybridLoop(res, dyn, OutvecExchange(1152, 1, 0, device=cuda), cuda, tisr=tisr, overlap=overlap,
-                      speedy_cus=speedy_cus)
+                      speedy_cus=speedy_cus, comm=comm)
     g4, g2, pr = synthetic_grids(11)
     f4, f2, _ = synthetic_grids(12)
     loop.start(t(g4), t(g2), t(pr), t(f4), t(f2))
@@ -119,6 +119,33 @@ def test_overlapped_loop_is_bitwise_the_serial_loop(cuda, speedy_cus):
     last = sa[-1]
     assert np.isfinite(last["f4"]).all() and np.isfinite(last["ov"]).all()
     assert np.abs(last["f4"]).max() > 0
+
+
+def test_native_comm_step_is_bitwise_the_python_exchange_step(cuda):
+    """HybridLoop with the library's own RCCL communicator (speedy_ml_amd.comm,
+    sml_hybrid_step: the exchange inside the native step) vs the Python exchange
+    between predict and advance: the same results, bit for bit (one rank here; the
+    all-gather proper runs at N > 1)."""
+    import torch
+
+    from speedy_ml_amd.comm import NativeComm
+
+    runs = []
+    for native in (False, True):
+        comm = NativeComm(1, 0) if native else None
+        loop, _ = _loop(cuda, True, comm=comm)
+        for _ in range(2):
+            loop.step()
+        loop.sync()
+        runs.append(_snapshot(loop))
+        loop.close()
+        loop.dyn.close()
+        loop.res.close()
+        if comm is not None:
+            comm.close()
+        torch.cuda.synchronize()
+    for k in runs[0]:
+        np.testing.assert_array_equal(runs[0][k], runs[1][k], err_msg=k)
 
 
 def test_loop_matches_the_sequential_chain(cuda):
