@@ -101,36 +101,44 @@ __device__ inline const double *fband_row(const double *fb, double t) {
 }  // namespace phys
 
 #ifdef __HIPCC__
-// One column j of phypar's physics.  Inputs (registers): ua, va, ta, qa, phi [kx]
-// (k = 0 top) and psl = the column's ug1, vg1, tg1, qg1, phig1, pslg1
-// (phy_phypar.f90:53-66); bc = kNBc fields [ngp]; rad = radiation state (in/out,
-// column j); fbt = P->fband or a copy of it in LDS.  Outputs: the u, v, t, q
-// tendencies of the physics (phypar's additions to the dynamical tendencies).
-__device__ inline void phys_column(int j, const double *ua, const double *va, const double *ta, const double *qa_in,
-                                   const double *phi, double psl, const double *__restrict__ bc,
-                                   double *__restrict__ rad, const PhysTables *P, const double *fbt, bool lradsw,
-                                   double *ut_o, double *vt_o, double *tt_o, double *qt_o) {
+// phypar's pieces (phy_phypar.f90:79-196), composed by phys_column in the
+// reference's order; k_st_gridspec also runs the moist / diffusion part and the
+// longwave / surface part of a column on different waves (sml_dynamics.hip).
+// 1.2 thermodynamic variables (phy_phypar.f90:79-94)
+struct PhysThermo {
+    double psg, rps;
+    double qa[kKX], se[kKX], rh[kKX], qsat[kKX];
+};
+
+__device__ inline void phys_thermo(const double *ta, const double *qa_in, const double *phi, double psl,
+                                   const PhysTables *P, PhysThermo &h) {
+    using namespace phys;
+    constexpr int NL = kKX;
+    h.psg = exp(psl);
+    h.rps = 1. / h.psg;
+#pragma unroll
+    for (int k = 0; k < NL; ++k) {
+        h.qa[k] = fmax(qa_in[k], 0.);
+        h.se[k] = cp * ta[k] + phi[k];
+    }
+#pragma unroll
+    for (int k = 0; k < NL; ++k) {
+        h.qsat[k] = qsat_at(ta[k], h.psg, P->sig[k]);
+        h.rh[k] = h.qa[k] / h.qsat[k];
+    }
+}
+
+// 2.1 convmf + 2.2 lscond: tt, qt = 0 + the convection + the condensation tendencies
+// (phy_phypar.f90:96-119); precnv, precls and the cloud top (itop) for the
+// shortwave, icnv for vdifsc
+__device__ inline void phys_moist(const PhysThermo &h, const PhysTables *P, double *tt, double *qt, double &precnv_o,
+                                  double &precls_o, int &itop_o, int &icnv_o) {
     using namespace phys;
     constexpr int NL = kKX, nl1 = kKX - 1;  // nl1: 1-based index of the level above the bottom
-    auto BC = [&](int f) { return bc[(size_t)f * kNGP + j]; };
-    double *tau2 = rad + kRadTau2, *stratc = rad + kRadStratc, *tt_rsw = rad + kRadTtRsw, *ssrd = rad + kRadSsrd;
-    auto TAU = [&](int jb, int k) -> double & { return tau2[((size_t)jb * NL + k) * kNGP + j]; };
-
-    double qa[NL], se[NL], rh[NL], qsat[NL];
-    // 1.2 thermodynamic variables (phy_phypar.f90:79-94)
-    const double psg = exp(psl);
-    const double rps = 1. / psg;
-#pragma unroll
-    for (int k = 0; k < NL; ++k) {
-        qa[k] = fmax(qa_in[k], 0.);
-        se[k] = cp * ta[k] + phi[k];
-    }
-#pragma unroll
-    for (int k = 0; k < NL; ++k) {
-        qsat[k] = qsat_at(ta[k], psg, P->sig[k]);
-        rh[k] = qa[k] / qsat[k];
-    }
-
+    (void)nl1;
+    const double psg = h.psg, rps = h.rps;
+    const double *qa = h.qa, *se = h.se, *rh = h.rh, *qsat = h.qsat;
+    (void)psg; (void)rps; (void)qa; (void)se; (void)rh; (void)qsat;
     // 2.1 convmf (phy_convmf.f90:22-238); 1-based level indices as the reference
     double tt_cnv[NL], qt_cnv[NL];
 #pragma unroll
@@ -272,16 +280,32 @@ __device__ inline void phys_column(int j, const double *ua, const double *va, co
         for (int k = 2; k <= NL; ++k) precls = precls - (P->dsig[k - 1] * prg) * qt_lsc[k - 1];
         precls = precls * psg;
     }
-    double tt[NL], qt[NL];  // :118-119 (input tendencies are zero here)
+    // :118-119 (input tendencies are zero here)
 #pragma unroll
     for (int k = 0; k < NL; ++k) {
         tt[k] = 0. + tt_cnv[k] + tt_lsc[k];
         qt[k] = 0. + qt_cnv[k] + qt_lsc[k];
     }
-    const int jlat = j / kIX;
+    precnv_o = precnv;
+    precls_o = precls;
+    itop_o = itop;
+    icnv_o = icnv;
+}
 
-    // 3.1 shortwave radiation and longwave transmissivities (phy_phypar.f90:126-145)
-    if (lradsw) {
+// 3.1 shortwave radiation and longwave transmissivities (phy_phypar.f90:126-145),
+// the lradsw steps only: the radiation state of column j in rad
+__device__ inline void phys_sw(int j, const PhysThermo &h, const double *phi, double precnv, double precls, int itop,
+                               const double *__restrict__ bc, double *__restrict__ rad, const PhysTables *P) {
+    using namespace phys;
+    constexpr int NL = kKX, nl1 = kKX - 1;  // nl1: 1-based index of the level above the bottom
+    (void)nl1;
+    auto BC = [&](int f) { return bc[(size_t)f * kNGP + j]; };
+    double *tau2 = rad + kRadTau2, *stratc = rad + kRadStratc, *tt_rsw = rad + kRadTtRsw, *ssrd = rad + kRadSsrd;
+    auto TAU = [&](int jb, int k) -> double & { return tau2[((size_t)jb * NL + k) * kNGP + j]; };
+    (void)tau2; (void)stratc; (void)tt_rsw; (void)ssrd;
+    const double psg = h.psg, rps = h.rps;
+    const double *qa = h.qa, *se = h.se, *rh = h.rh, *qsat = h.qsat;
+    (void)psg; (void)rps; (void)qa; (void)se; (void)rh; (void)qsat;
         const double gse = (se[NL - 2] - se[NL - 1]) / (phi[NL - 2] - phi[NL - 1]);
         // cloud (phy_radiat.f90:123-152)
         constexpr int nlp = NL + 1;
@@ -406,6 +430,21 @@ __device__ inline void phys_column(int j, const double *ua, const double *va, co
         for (int k = 0; k < NL; ++k) tt_rsw[(size_t)k * kNGP + j] = dfabs[k] * rps * P->grdscp[k];
     }
 
+// 3.2 radlw(-1), 3.3 suflux, 3.4 radlw(1) (phy_phypar.f90:147-179): the longwave
+// temperature tendency tt_rlw and the surface fluxes of column j
+__device__ inline void phys_lw_sfc(int j, const double *ua, const double *va, const double *ta, const double *qa,
+                                   const double *phi, double psg, double rps, const double *__restrict__ bc,
+                                   const double *__restrict__ rad_in, const PhysTables *P, const double *fbt,
+                                   double *tt_rlw, double &ustr3_o, double &vstr3_o, double &shf3_o, double &evap3_o) {
+    using namespace phys;
+    constexpr int NL = kKX, nl1 = kKX - 1;  // nl1: 1-based index of the level above the bottom
+    (void)nl1;
+    double *rad = const_cast<double *>(rad_in);
+    auto BC = [&](int f) { return bc[(size_t)f * kNGP + j]; };
+    double *tau2 = rad + kRadTau2, *stratc = rad + kRadStratc, *tt_rsw = rad + kRadTtRsw, *ssrd = rad + kRadSsrd;
+    auto TAU = [&](int jb, int k) -> double & { return tau2[((size_t)jb * NL + k) * kNGP + j]; };
+    (void)tau2; (void)stratc; (void)tt_rsw; (void)ssrd;
+    const int jlat = j / kIX;
     // 3.2 radlw(-1): downward longwave (phy_radiat.f90:330-413)
     double st4a1[NL], st4a2[NL], flux[4], dfabs[NL], fsfcd;
     double fbk[NL][4];  // fband(nint(ta(k)), 1:4): one table row per level, for both radlw passes
@@ -577,15 +616,25 @@ __device__ inline void phys_column(int j, const double *ua, const double *va, co
         dfabs[1] = dfabs[1] - corlw2;
     }
 #pragma unroll
-    for (int k = 0; k < NL; ++k) {  // phy_phypar.f90:174-179
-        const double tt_rlw = dfabs[k] * rps * P->grdscp[k];
-        tt[k] = tt[k] + tt_rsw[(size_t)k * kNGP + j] + tt_rlw;
-    }
+    for (int k = 0; k < NL; ++k) tt_rlw[k] = dfabs[k] * rps * P->grdscp[k];
+    ustr3_o = ustr3;
+    vstr3_o = vstr3;
+    shf3_o = shf3;
+    evap3_o = evap3;
+}
 
+// 4.1 vdifsc (phy_vdifsc.f90:17-124): ttv, qtv (utv = vtv = 0 here)
+__device__ inline void phys_vdif(const PhysThermo &h, const double *phi, int icnv, const PhysTables *P, double *ttv,
+                                 double *qtv) {
+    using namespace phys;
+    constexpr int NL = kKX, nl1 = kKX - 1;  // nl1: 1-based index of the level above the bottom
+    (void)nl1;
+    const double psg = h.psg, rps = h.rps;
+    const double *qa = h.qa, *se = h.se, *rh = h.rh, *qsat = h.qsat;
+    (void)psg; (void)rps; (void)qa; (void)se; (void)rh; (void)qsat;
     // 4.1 vdifsc (phy_vdifsc.f90:17-124)
-    double utv[NL], vtv[NL], ttv[NL], qtv[NL];
 #pragma unroll
-    for (int k = 0; k < NL; ++k) utv[k] = vtv[k] = ttv[k] = qtv[k] = 0.;
+    for (int k = 0; k < NL; ++k) ttv[k] = qtv[k] = 0.;
     {
         constexpr int nlev = NL;
         const double cshc = P->dsig[nlev - 1] / 3600., cvdi = (P->sigh[nl1] - P->sigh[1]) / ((nl1 - 1) * 3600.);
@@ -644,6 +693,35 @@ __device__ inline void phys_column(int j, const double *ua, const double *va, co
             }
         }
     }
+}
+
+// One column j of phypar's physics.  Inputs (registers): ua, va, ta, qa, phi [kx]
+// (k = 0 top) and psl = the column's ug1, vg1, tg1, qg1, phig1, pslg1
+// (phy_phypar.f90:53-66); bc = kNBc fields [ngp]; rad = radiation state (in/out,
+// column j); fbt = P->fband or a copy of it in LDS.  Outputs: the u, v, t, q
+// tendencies of the physics (phypar's additions to the dynamical tendencies).
+__device__ inline void phys_column(int j, const double *ua, const double *va, const double *ta, const double *qa_in,
+                                   const double *phi, double psl, const double *__restrict__ bc,
+                                   double *__restrict__ rad, const PhysTables *P, const double *fbt, bool lradsw,
+                                   double *ut_o, double *vt_o, double *tt_o, double *qt_o) {
+    using namespace phys;
+    constexpr int NL = kKX;
+    PhysThermo h;
+    phys_thermo(ta, qa_in, phi, psl, P, h);
+    double tt[NL], qt[NL], precnv, precls;
+    int itop, icnv;
+    phys_moist(h, P, tt, qt, precnv, precls, itop, icnv);
+    if (lradsw) phys_sw(j, h, phi, precnv, precls, itop, bc, rad, P);
+    double tt_rlw[NL], ustr3, vstr3, shf3, evap3;
+    phys_lw_sfc(j, ua, va, ta, h.qa, phi, h.psg, h.rps, bc, rad, P, fbt, tt_rlw, ustr3, vstr3, shf3, evap3);
+    const double rps = h.rps;
+    const double *tt_rsw = rad + kRadTtRsw;
+#pragma unroll
+    for (int k = 0; k < NL; ++k) tt[k] = tt[k] + tt_rsw[(size_t)k * kNGP + j] + tt_rlw[k];  // :174-179
+    double utv[NL], vtv[NL], ttv[NL], qtv[NL];
+#pragma unroll
+    for (int k = 0; k < NL; ++k) utv[k] = vtv[k] = 0.;
+    phys_vdif(h, phi, icnv, P, ttv, qtv);
     // 4.2 surface fluxes into the bottom layer (phy_phypar.f90:186-191), then sums (:193-196)
     utv[NL - 1] = utv[NL - 1] + ustr3 * rps * P->grdsig[NL - 1];
     vtv[NL - 1] = vtv[NL - 1] + vstr3 * rps * P->grdsig[NL - 1];
