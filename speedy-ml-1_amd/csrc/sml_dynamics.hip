@@ -1311,15 +1311,14 @@ __global__ __launch_bounds__(kGsThreads) void k_st_gridspec(
     __syncthreads();
     stamp(dbg, 0, 1);
     const double cj = cosgr[j];
-    // phypar of column i.  On a shortwave step (lradsw) waves 2-3 run the whole column
-    // (phys_column).  Otherwise the column is split between the waves, the reference's
-    // expressions unchanged: waves 0-1, after the grid-point dynamics, do the moist
-    // part and the vertical diffusion (phys_thermo, phys_moist, phys_vdif: they need
-    // no radiation) while waves 2-3 do the longwave / surface chain (phys_lw_sfc),
-    // which used to follow them on the same lane; the moist side hands its 24 values
-    // over in B's spare columns [kNFwd, kRowLd) and waves 2-3 sum the tendencies in
+    // phypar of column i, split between the waves, the reference's expressions
+    // unchanged: waves 0-1, after the grid-point dynamics, do the moist part and the
+    // vertical diffusion (phys_thermo, phys_moist, phys_vdif: no radiation needed)
+    // while waves 2-3 do the longwave / surface chain (phys_lw_sfc) -- on a shortwave
+    // step (lradsw) after their own moist part and the shortwave (phys_sw needs the
+    // convective precipitation and cloud top).  The moist side hands its 24 values
+    // over in B's spare columns [kNFwd, kRowLd); waves 2-3 sum the tendencies in
     // phys_column's order.
-    const bool split = lradsw == 0;
     double rl_tt[kKX], rl_us = 0.0, rl_vs = 0.0, rl_sh = 0.0, rl_ev = 0.0, rl_rps = 0.0;
     static_assert(kRowLd - kNFwd >= 24, "moist-side hand-over: 24 spare slots per column in B");
     if (tid < 128) {
@@ -1328,36 +1327,35 @@ __global__ __launch_bounds__(kGsThreads) void k_st_gridspec(
             double dummy[kKX];
             gridpoint_column(j, n1, [&](int f) { return A[i * kRowLd + f]; }, false, dummy, dummy, dummy, dummy,
                              [&](int f, double v) { B[i * kRowLd + f] = v; }, T);
-            if (split) {  // the moist / diffusion part of column i's phypar
-                const double *Ai = A + i * kRowLd;
-                double ta[kKX], qa[kKX], ph[kKX];
+            // the moist / diffusion part of column i's phypar
+            const double *Ai = A + i * kRowLd;
+            double ta[kKX], qa[kKX], ph[kKX];
 #pragma unroll
-                for (int k = 0; k < kKX; ++k) {
-                    ta[k] = Ai[kPT1 + k];
-                    qa[k] = Ai[kPQ1 + k];
-                    ph[k] = Ai[kPPhi1 + k];
-                }
-                PhysThermo h;
-                phys_thermo(ta, qa, ph, Ai[kPPs1], PT, h);
-                double tt[kKX], qt[kKX], precnv, precls, ttv[kKX], qtv[kKX];
-                int itop, icnv;
-                phys_moist(h, PT, tt, qt, precnv, precls, itop, icnv);
-                phys_vdif(h, ph, icnv, PT, ttv, qtv);
-                double *Bh = B + i * kRowLd + kNFwd;
-                // tt[0] is +0 always (convection and condensation leave the top level alone)
-#pragma unroll
-                for (int k = 1; k < kKX; ++k) Bh[k - 1] = tt[k];
-#pragma unroll
-                for (int k = 0; k < kKX; ++k) Bh[7 + k] = ttv[k];
-#pragma unroll
-                for (int k = 0; k < kKX - 1; ++k) Bh[15 + k] = qt[k] + qtv[k];  // final above the surface layer
-                Bh[22] = qt[kKX - 1];
-                Bh[23] = qtv[kKX - 1];
+            for (int k = 0; k < kKX; ++k) {
+                ta[k] = Ai[kPT1 + k];
+                qa[k] = Ai[kPQ1 + k];
+                ph[k] = Ai[kPPhi1 + k];
             }
+            PhysThermo h;
+            phys_thermo(ta, qa, ph, Ai[kPPs1], PT, h);
+            double tt[kKX], qt[kKX], precnv, precls, ttv[kKX], qtv[kKX];
+            int itop, icnv;
+            phys_moist(h, PT, tt, qt, precnv, precls, itop, icnv);
+            phys_vdif(h, ph, icnv, PT, ttv, qtv);
+            double *Bh = B + i * kRowLd + kNFwd;
+            // tt[0] is +0 always (convection and condensation leave the top level alone)
+#pragma unroll
+            for (int k = 1; k < kKX; ++k) Bh[k - 1] = tt[k];
+#pragma unroll
+            for (int k = 0; k < kKX; ++k) Bh[7 + k] = ttv[k];
+#pragma unroll
+            for (int k = 0; k < kKX - 1; ++k) Bh[15 + k] = qt[k] + qtv[k];  // final above the surface layer
+            Bh[22] = qt[kKX - 1];
+            Bh[23] = qtv[kKX - 1];
         }
     } else if (tid - 128 < kIX) {
         const int i = tid - 128, pt = j * kIX + i;
-        double *Ai = A + i * kRowLd;
+        const double *Ai = A + i * kRowLd;
         double ua[kKX], va[kKX], ta[kKX], qa[kKX], ph[kKX];
 #pragma unroll
         for (int k = 0; k < kKX; ++k) {
@@ -1368,28 +1366,29 @@ __global__ __launch_bounds__(kGsThreads) void k_st_gridspec(
             ph[k] = Ai[kPPhi1 + k];
         }
         const double ps1 = Ai[kPPs1];
-        if (!split) {
-            double ut[kKX], vt[kKX], tt[kKX], qt[kKX];
-            phys_column(pt, ua, va, ta, qa, ph, ps1, bc, rad, PT, &PT->fband[0][0], true, ut, vt, tt, qt);
+        double psg, qc[kKX];
+        if (lradsw) {  // the shortwave first: its inputs are the moist part's (phys_column's order)
+            PhysThermo h;
+            phys_thermo(ta, qa, ph, ps1, PT, h);
+            double tt[kKX], qt[kKX], precnv, precls;
+            int itop, icnv;
+            phys_moist(h, PT, tt, qt, precnv, precls, itop, icnv);
+            phys_sw(pt, h, ph, precnv, precls, itop, bc, rad, PT);
+            psg = h.psg;
+            rl_rps = h.rps;
 #pragma unroll
-            for (int k = 0; k < kKX; ++k) {
-                Ai[phys_slot_col(k)] = ut[k];
-                Ai[phys_slot_col(kKX + k)] = vt[k];
-                Ai[phys_slot_col(2 * kKX + k)] = tt[k];
-                Ai[phys_slot_col(3 * kKX + k)] = qt[k];
-            }
-        } else {  // the longwave / surface chain (phys_thermo's psg, rps and clipped q)
-            const double psg = exp(ps1);
+            for (int k = 0; k < kKX; ++k) qc[k] = h.qa[k];
+        } else {  // phys_thermo's psg, rps and clipped q
+            psg = exp(ps1);
             rl_rps = 1. / psg;
-            double qc[kKX];
 #pragma unroll
             for (int k = 0; k < kKX; ++k) qc[k] = fmax(qa[k], 0.);
-            phys_lw_sfc(pt, ua, va, ta, qc, ph, psg, rl_rps, bc, rad, PT, &PT->fband[0][0], rl_tt, rl_us, rl_vs,
-                        rl_sh, rl_ev);
         }
+        phys_lw_sfc(pt, ua, va, ta, qc, ph, psg, rl_rps, bc, rad, PT, &PT->fband[0][0], rl_tt, rl_us, rl_vs, rl_sh,
+                    rl_ev);
     }
     __syncthreads();
-    if (split && tid >= 128 && tid - 128 < kIX) {  // phys_column's sums (phy_phypar.f90:174-196)
+    if (tid >= 128 && tid - 128 < kIX) {  // phys_column's sums (phy_phypar.f90:174-196)
         const int i = tid - 128, pt = j * kIX + i;
         double *Ai = A + i * kRowLd;
         const double *Bh = B + i * kRowLd + kNFwd;
@@ -1415,7 +1414,7 @@ __global__ __launch_bounds__(kGsThreads) void k_st_gridspec(
             Ai[phys_slot_col(3 * kKX + k)] = qtk;
         }
     }
-    if (split) __syncthreads();  // block-uniform
+    __syncthreads();
     stamp(dbg, 0, 2);
     // specx: transform f on lanes 2 f, 2 f + 1, lane h on the samples 2 i + h
     {
