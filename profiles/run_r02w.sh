@@ -4,7 +4,7 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
-R=r02w
+R=${R:-r02y}
 bash profiles/run_speedy_pmc.sh $R && cp gpurun_out/speedy_pmc_$R/speedy_pmc.json profiles/speedy_pmc.json \
   && cp profiles/speedy_pmc.json gpurun_out/speedy_pmc_$R.json && echo "speedy pmc ok" || exit 1
 R=$R bash profiles/run_r02.sh tests smoke bench prof || exit 1
