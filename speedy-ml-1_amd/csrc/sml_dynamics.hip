@@ -248,8 +248,14 @@ __global__ void k_dyn_prep(const double *__restrict__ st, double *__restrict__ s
 //   [utend 8 | -u*tgg 8 | -u*trg 8 | vtend 8 | -v*tgg 8 | -v*trg 8]  (x 1/cos in specx)
 //   [0.5(u^2+v^2) 8 | ttend 8 | trtend 8 | -umean*px - vmean*py]
 template <class GetF, class PutF>
+__device__ inline void gridpoint_products(int o2, GetF g, PutF put, const DynTables *T);
+
+// products = false: the products of :239-271 are left to gridpoint_products (the row
+// kernel runs them on the lane that has slack)
+template <class GetF, class PutF>
 __device__ inline void gridpoint_column(int j, int o2, GetF g, bool hasP, const double *pu, const double *pv,
-                                        const double *pt, const double *pq, PutF put, const DynTables *T) {
+                                        const double *pt, const double *pq, PutF put, const DynTables *T,
+                                        bool products = true) {
     double ug[kKX], vg[kKX], vorg[kKX], divg[kKX], tg[kKX], trg[kKX];
 #pragma unroll
     for (int k = 0; k < kKX; ++k) {
@@ -327,13 +333,20 @@ __device__ inline void gridpoint_column(int j, int o2, GetF g, bool hasP, const 
         put(8 * kKX + k, q);
     }
     // products for the spectral conversion (:239-271)
+    if (products) gridpoint_products(o2, g, put, T);
+}
+
+template <class GetF, class PutF>
+__device__ inline void gridpoint_products(int o2, GetF g, PutF put, const DynTables *T) {
 #pragma unroll
     for (int k = 0; k < kKX; ++k) {
-        put(kKX + k, -ug[k] * tgg[k]);
-        put(4 * kKX + k, -vg[k] * tgg[k]);
-        put(2 * kKX + k, -ug[k] * trg[k]);
-        put(5 * kKX + k, -vg[k] * trg[k]);
-        put(6 * kKX + k, 0.5 * (ug[k] * ug[k] + vg[k] * vg[k]));
+        const double ug = g(o2 + k), vg = g(o2 + kKX + k), trg = g(3 * kKX + k);
+        const double tgg = g(2 * kKX + k) - T->tref[k];
+        put(kKX + k, -ug * tgg);
+        put(4 * kKX + k, -vg * tgg);
+        put(2 * kKX + k, -ug * trg);
+        put(5 * kKX + k, -vg * trg);
+        put(6 * kKX + k, 0.5 * (ug * ug + vg * vg));
     }
 }
 
@@ -1326,7 +1339,7 @@ __global__ __launch_bounds__(kGsThreads) void k_st_gridspec(
             const int i = tid;
             double dummy[kKX];
             gridpoint_column(j, n1, [&](int f) { return A[i * kRowLd + f]; }, false, dummy, dummy, dummy, dummy,
-                             [&](int f, double v) { B[i * kRowLd + f] = v; }, T);
+                             [&](int f, double v) { B[i * kRowLd + f] = v; }, T, false);
             // the moist / diffusion part of column i's phypar
             const double *Ai = A + i * kRowLd;
             double ta[kKX], qa[kKX], ph[kKX];
@@ -1386,6 +1399,9 @@ __global__ __launch_bounds__(kGsThreads) void k_st_gridspec(
         }
         phys_lw_sfc(pt, ua, va, ta, qc, ph, psg, rl_rps, bc, rad, PT, &PT->fband[0][0], rl_tt, rl_us, rl_vs, rl_sh,
                     rl_ev);
+        // the grid-point dynamics' products (this side has the slack)
+        gridpoint_products(n1, [&](int f) { return A[i * kRowLd + f]; },
+                           [&](int f, double v) { B[i * kRowLd + f] = v; }, T);
     }
     __syncthreads();
     if (tid >= 128 && tid - 128 < kIX) {  // phys_column's sums (phy_phypar.f90:174-196)
