@@ -412,7 +412,7 @@ struct TabM {
     double el2[kNX], elz[kNX], dmp[kNX], dmp1[kNX], dmpd[kNX], dmp1d[kNX], dmps[kNX], dmp1s[kNX], trfilt[kNX];
     double vddym[kNX], vddyp[kNX], gradym[kNX], gradyp[kNX], uvdx[kNX], uvdym[kNX], uvdyp[kNX];
     double gradx, pad_;
-    double xj[kNX][kKX][kKX];
+    double xj[kKX][kKX][kNX];  // [k1][k][n]: n fastest, so a wave's lanes (one n each) hit distinct LDS banks
 };
 constexpr int kTabMDoubles = (int)(sizeof(TabM) / sizeof(double));
 constexpr int kTabMPad = 2048;  // d_tabm tail: k_st_spec stages whole 16-B rows of 512 threads
@@ -454,7 +454,7 @@ struct LTab {
     __device__ double gradx_m() const { return t->gradx; }
     __device__ double xc(int k1, int k) const { return t->xc[k1][k]; }
     __device__ double xd(int k1, int k) const { return t->xd[k1][k]; }
-    __device__ double xj(int n, int k1, int k) const { return t->xj[n][k1][k]; }
+    __device__ double xj(int n, int k1, int k) const { return t->xj[k1][k][n]; }
 };
 
 // the value at flat index i of m's TabM, read from the DynTables (host: the per-slot
@@ -482,8 +482,9 @@ __host__ __device__ inline double tabm_value(const DynTables *__restrict__ T, in
         return (&T->xd[0][0])[(off - offsetof(TabM, xd)) / sizeof(double)];
     if (off == offsetof(TabM, gradx)) return T->gradx[m];
     if (off >= offsetof(TabM, xj)) {
-        const int q = (int)((off - offsetof(TabM, xj)) / sizeof(double)), n = q / (kKX * kKX);
-        return m + n >= 1 ? (&T->xj[m + n - 1][0][0])[q % (kKX * kKX)] : 0.0;
+        const int q = (int)((off - offsetof(TabM, xj)) / sizeof(double));
+        const int k1 = q / (kKX * kNX), k = (q / kNX) % kKX, n = q % kNX;
+        return m + n >= 1 ? T->xj[m + n - 1][k1][k] : 0.0;
     }
     return 0.0;
 }
