@@ -495,18 +495,21 @@ template <class U, class V, class TB>
 __device__ inline void vds_gen(U u, V v, const TB &tb, int n, int p, double *vor, double *div) {
     const double gx = tb.gradx_m();
     // zp(2)=gradx*u(1), zp(1)=-gradx*u(2); zc likewise from v
-    const double zp = p == 1 ? gx * u(0, n) : -gx * u(1, n);
-    const double zc = p == 1 ? gx * v(0, n) : -gx * v(1, n);
-    if (n == 0) {
-        *vor = zc - tb.vddyp_n(0) * u(p, 1);
-        *div = zp + tb.vddyp_n(0) * v(p, 1);
-    } else if (n == kNX - 1) {
-        *vor = tb.vddym_n(n) * u(p, kNTRUN1 - 1);
-        *div = -tb.vddym_n(n) * v(p, kNTRUN1 - 1);
-    } else {
-        *vor = tb.vddym_n(n) * u(p, n - 1) - tb.vddyp_n(n) * u(p, n + 1) + zc;
-        *div = -tb.vddym_n(n) * v(p, n - 1) + tb.vddyp_n(n) * v(p, n + 1) + zp;
-    }
+    const double ux = u(1 - p, n), vx = v(1 - p, n);
+    const double zp = p == 1 ? gx * ux : -gx * ux;
+    const double zc = p == 1 ? gx * vx : -gx * vx;
+    // the n == 1 / n == ntrun+2 / interior cases all formed (neighbours clamped into
+    // the row), then selected: the reference's values without divergent branches,
+    // whose dependent reads cost a round trip per case where u, v live in LDS
+    static_assert(kNTRUN1 - 1 == kNX - 2, "vds's last row reads n - 1");
+    const int nm = n > 0 ? n - 1 : 0, np = n < kNX - 1 ? n + 1 : kNX - 1;
+    const double um = u(p, nm), up = u(p, np), vm = v(p, nm), vp = v(p, np);
+    const double dym = tb.vddym_n(n), dyp = tb.vddyp_n(n);
+    const double vor0 = zc - dyp * up, div0 = zp + dyp * vp;
+    const double vorl = dym * um, divl = -dym * vm;
+    const double vori = dym * um - dyp * up + zc, divi = -dym * vm + dyp * vp + zp;
+    *vor = n == 0 ? vor0 : n == kNX - 1 ? vorl : vori;
+    *div = n == 0 ? div0 : n == kNX - 1 ? divl : divi;
 }
 
 __device__ inline void vds_at(const double *u, const double *v, const DynTables *T, int m, int n, int p, double *vor,
@@ -576,10 +579,15 @@ __device__ inline void tail_coef(SA S, double *__restrict__ Td, double *__restri
     const double dumk_k1 = (k == kKX - 1) ? 0.0 : sig_k1 * (tb.tref(k + 1) - tb.tref(k));
     tdt = tdt - (dumk_k1 + dumk_k) * tb.dhsr(k) + tb.tref3(k) * (sig_k1 + sig_k) - tb.tref2(k) * dmeanc;
     // geop(j4)  (dyn_geop.f90:16-32)
+    // (every level's term formed, the ones below k selected away: the sum and its
+    // order are the reference's, and the LDS reads issue together instead of one
+    // dependent round trip per level of a runtime-bounded loop)
     double phi = phis[fc] + tb.xgeop1(kKX - 1) * sh[1][kKX - 1][cc];
 #pragma unroll
-    for (int kk = kKX - 2; kk >= k; --kk)
-        phi = phi + tb.xgeop2(kk + 1) * sh[1][kk + 1][cc] + tb.xgeop1(kk) * sh[1][kk][cc];
+    for (int kk = kKX - 2; kk >= 0; --kk) {
+        const double nx = phi + tb.xgeop2(kk + 1) * sh[1][kk + 1][cc] + tb.xgeop1(kk) * sh[1][kk][cc];
+        phi = kk >= k ? nx : phi;
+    }
     if (m == 0 && k >= 1 && k <= kKX - 2) phi = phi + tb.corf(k) * (sh[1][k + 1][cc] - sh[1][k - 1][cc]);
     if (phi_out) phi_out[(size_t)k * kSF + c] = phi;
     {
@@ -787,39 +795,44 @@ __device__ inline void inv_inputs(const double *Sst, double *In, const double *p
     auto put = [&](int f, double v) { In[f * kCW + cc] = v; };
 #pragma unroll
     for (int var = 0; var < 4; ++var) put(var * kKX + k, sv(var, j2, k, cc));
-    // uvspec (spe_spectral.f90:351-387) of level lev at k -> ucos (field fu), vcos (fv)
+    // uvspec (spe_spectral.f90:351-387) of level lev at k -> ucos (field fu), vcos (fv).
+    // Branch-free: every case's operands read (neighbour indices clamped) and its
+    // expression formed, then the case selected -- the same values as the reference's
+    // n == 1 / n == ntrun+2 / interior branches, without a divergent branch and its
+    // dependent LDS round trip per case (p and n vary across a wave's lanes)
+    static_assert(kNTRUN1 - 1 == kNX - 2, "uvspec's last row reads n - 1");
+    const int nm = n > 0 ? n - 1 : 0, np = n < kNX - 1 ? n + 1 : kNX - 1;
+    const bool first = n == 0, last = n == kNX - 1;
     auto uvspec = [&](int lev, int fu, int fv) {
-        auto vor = [&](int pp, int nn) { return sv(0, lev, k, 2 * nn + pp); };
-        auto div = [&](int pp, int nn) { return sv(1, lev, k, 2 * nn + pp); };
-        const double ux = tb.uvdx_n(n);
-        double u, v;
-        const double zc = p == 1 ? ux * div(0, n) : -ux * div(1, n);
-        if (n == 0) u = zc - tb.uvdyp_n(0) * vor(p, 1);
-        else if (n == kNX - 1) u = tb.uvdym_n(n) * vor(p, kNTRUN1 - 1);
-        else u = tb.uvdym_n(n) * vor(p, n - 1) - tb.uvdyp_n(n) * vor(p, n + 1) + zc;
-        const double zp = p == 1 ? ux * vor(0, n) : -ux * vor(1, n);
-        if (n == 0) v = zp + tb.uvdyp_n(0) * div(p, 1);
-        else if (n == kNX - 1) v = -tb.uvdym_n(n) * div(p, kNTRUN1 - 1);
-        else v = -tb.uvdym_n(n) * div(p, n - 1) + tb.uvdyp_n(n) * div(p, n + 1) + zp;
-        put(fu, u);
-        put(fv, v);
+        const double vor_m = sv(0, lev, k, 2 * nm + p), vor_p = sv(0, lev, k, 2 * np + p);
+        const double div_m = sv(1, lev, k, 2 * nm + p), div_p = sv(1, lev, k, 2 * np + p);
+        const double vor_x = sv(0, lev, k, 2 * n + 1 - p), div_x = sv(1, lev, k, 2 * n + 1 - p);
+        const double ux = tb.uvdx_n(n), uvdym = tb.uvdym_n(n), uvdyp = tb.uvdyp_n(n);
+        const double zc = p == 1 ? ux * div_x : -ux * div_x;
+        const double u0 = zc - uvdyp * vor_p, ul = uvdym * vor_m, um = uvdym * vor_m - uvdyp * vor_p + zc;
+        const double zp = p == 1 ? ux * vor_x : -ux * vor_x;
+        const double v0 = zp + uvdyp * div_p, vl = -uvdym * div_m, vm = -uvdym * div_m + uvdyp * div_p + zp;
+        put(fu, first ? u0 : last ? ul : um);
+        put(fv, first ? v0 : last ? vl : vm);
     };
     uvspec(j2, n1 + k, n1 + kKX + k);
-    if (k == 0) {  // grad(ps(j2))
-        put(n1 + 2 * kKX, p == 1 ? tb.gradx_m() * sv(4, j2, 0, 2 * n) : -tb.gradx_m() * sv(4, j2, 0, 2 * n + 1));
-        double v;
-        if (n == 0) v = tb.gradyp_n(0) * sv(4, j2, 0, 2 + p);
-        else if (n == kNX - 1) v = -tb.gradym_n(n) * sv(4, j2, 0, 2 * (kNTRUN1 - 1) + p);
-        else v = -tb.gradym_n(n) * sv(4, j2, 0, 2 * (n - 1) + p) + tb.gradyp_n(n) * sv(4, j2, 0, 2 * (n + 1) + p);
-        put(n1 + 2 * kKX + 1, v);
+    if (k == 0) {  // grad(ps(j2)) (wave-uniform branch; the n cases selected as in uvspec)
+        const double ps_x = sv(4, j2, 0, 2 * n + 1 - p), ps_m = sv(4, j2, 0, 2 * nm + p), ps_p = sv(4, j2, 0, 2 * np + p);
+        const double gx = tb.gradx_m(), gym = tb.gradym_n(n), gyp = tb.gradyp_n(n);
+        put(n1 + 2 * kKX, p == 1 ? gx * ps_x : -gx * ps_x);
+        const double v0 = gyp * ps_p, vl = -gym * ps_m, vm = -gym * ps_m + gyp * ps_p;
+        put(n1 + 2 * kKX + 1, first ? v0 : last ? vl : vm);
     }
     if (!phys) return;
     // phypar's level-1 inputs: t1, q1, geop(1) (geop_at), ps1, ucos1, vcos1
     put(kPT1 + k, sv(2, 1, k, cc));
     put(kPQ1 + k, sv(3, 1, k, cc));
     double phi = phis_m[cc] + tb.xgeop1(kKX - 1) * sv(2, 1, kKX - 1, cc);
-    for (int kk = kKX - 2; kk >= k; --kk)
-        phi = phi + tb.xgeop2(kk + 1) * sv(2, 1, kk + 1, cc) + tb.xgeop1(kk) * sv(2, 1, kk, cc);
+#pragma unroll
+    for (int kk = kKX - 2; kk >= 0; --kk) {  // levels below k selected away (as in tail_coef)
+        const double nx = phi + tb.xgeop2(kk + 1) * sv(2, 1, kk + 1, cc) + tb.xgeop1(kk) * sv(2, 1, kk, cc);
+        phi = kk >= k ? nx : phi;
+    }
     if (m == 0 && k >= 1 && k <= kKX - 2) phi = phi + tb.corf(k) * (sv(2, 1, k + 1, cc) - sv(2, 1, k - 1, cc));
     put(kPPhi1 + k, phi);
     if (k == 0) put(kPPs1, sv(4, 1, 0, cc));
@@ -1636,8 +1649,14 @@ __global__ __launch_bounds__(kSpecBlk) void k_st_spec(
         return;  // block-uniform
     }
     if (lead) {  // into the other buffer: this m's second block may still be reading sm
-        double2 *dst = reinterpret_cast<double2 *>(sm_out + (size_t)m * kSM);
-        for (int i = threadIdx.x; i < kSM / 2; i += kSpecBlk) dst[i] = reinterpret_cast<const double2 *>(Sst)[i];
+        // (five whole rows of the block, static_assert above: the LDS reads issue together)
+        double2 *dst = reinterpret_cast<double2 *>(sm_out + (size_t)m * kSM) + threadIdx.x;
+        const double2 *src = reinterpret_cast<const double2 *>(Sst) + threadIdx.x;
+        double2 v[RS];
+#pragma unroll
+        for (int q = 0; q < RS; ++q) v[q] = src[q * kSpecBlk];
+#pragma unroll
+        for (int q = 0; q < RS; ++q) dst[q * kSpecBlk] = v[q];
     }
     // d) the next step's inverse-transform inputs (k_dyn_prep) and gridy
     if (holds) inv_inputs(Sst, S, Fm, tb, m, next_j2, n1, nin);
