@@ -575,8 +575,11 @@ __device__ inline void tail_coef(SA S, double *__restrict__ Td, double *__restri
             sg = nx_;
         }
     }
-    const double dumk_k = (k == 0) ? 0.0 : sig_k * (tb.tref(k) - tb.tref(k - 1));
-    const double dumk_k1 = (k == kKX - 1) ? 0.0 : sig_k1 * (tb.tref(k + 1) - tb.tref(k));
+    // (neighbour levels clamped and the edge cases selected: no branch around a read)
+    const int km = k > 0 ? k - 1 : 0, kp = k < kKX - 1 ? k + 1 : kKX - 1;
+    const double trk = tb.tref(k), trm = tb.tref(km), trp = tb.tref(kp);
+    const double dumk_k = (k == 0) ? 0.0 : sig_k * (trk - trm);
+    const double dumk_k1 = (k == kKX - 1) ? 0.0 : sig_k1 * (trp - trk);
     tdt = tdt - (dumk_k1 + dumk_k) * tb.dhsr(k) + tb.tref3(k) * (sig_k1 + sig_k) - tb.tref2(k) * dmeanc;
     // geop(j4)  (dyn_geop.f90:16-32)
     // (every level's term formed, the ones below k selected away: the sum and its
@@ -588,7 +591,10 @@ __device__ inline void tail_coef(SA S, double *__restrict__ Td, double *__restri
         const double nx = phi + tb.xgeop2(kk + 1) * sh[1][kk + 1][cc] + tb.xgeop1(kk) * sh[1][kk][cc];
         phi = kk >= k ? nx : phi;
     }
-    if (m == 0 && k >= 1 && k <= kKX - 2) phi = phi + tb.corf(k) * (sh[1][k + 1][cc] - sh[1][k - 1][cc]);
+    {
+        const double pc = phi + tb.corf(k) * (sh[1][kp][cc] - sh[1][km][cc]);
+        if (m == 0 && k >= 1 && k <= kKX - 2) phi = pc;
+    }
     if (phi_out) phi_out[(size_t)k * kSF + c] = phi;
     {
         const double d1 = phi + kRgas * tb.tref(k) * S(4, j4, 0);
@@ -781,6 +787,30 @@ __device__ inline void put_state(double *__restrict__ st, int m, int i, double v
 }
 
 
+// uvspec (spe_spectral.f90:351-387) of coefficient (n, p) at level k, time level lev,
+// from an m's state slice Sst (smi layout) -> ucos (u), vcos (v).  Branch-free: every
+// case's operands read (neighbour indices clamped) and its expression formed, then the
+// case selected -- the reference's n == 1 / n == ntrun+2 / interior values without a
+// divergent branch and its dependent LDS round trip per case (n and p vary across a
+// wave's lanes)
+template <class TB>
+__device__ inline void uvspec_sel(const double *Sst, const TB &tb, int lev, int k, int n, int p, double *u,
+                                  double *v) {
+    static_assert(kNTRUN1 - 1 == kNX - 2, "uvspec's last row reads n - 1");
+    const int nm = n > 0 ? n - 1 : 0, np = n < kNX - 1 ? n + 1 : kNX - 1;
+    const bool first = n == 0, last = n == kNX - 1;
+    const double vor_m = Sst[smi(0, lev, k, 2 * nm + p)], vor_p = Sst[smi(0, lev, k, 2 * np + p)];
+    const double div_m = Sst[smi(1, lev, k, 2 * nm + p)], div_p = Sst[smi(1, lev, k, 2 * np + p)];
+    const double vor_x = Sst[smi(0, lev, k, 2 * n + 1 - p)], div_x = Sst[smi(1, lev, k, 2 * n + 1 - p)];
+    const double ux = tb.uvdx_n(n), uvdym = tb.uvdym_n(n), uvdyp = tb.uvdyp_n(n);
+    const double zc = p == 1 ? ux * div_x : -ux * div_x;
+    const double u0 = zc - uvdyp * vor_p, ul = uvdym * vor_m, um = uvdym * vor_m - uvdyp * vor_p + zc;
+    const double zp = p == 1 ? ux * vor_x : -ux * vor_x;
+    const double v0 = zp + uvdyp * div_p, vl = -uvdym * div_m, vm = -uvdym * div_m + uvdyp * div_p + zp;
+    *u = first ? u0 : last ? ul : um;
+    *v = first ? v0 : last ? vl : vm;
+}
+
 // The inverse-transform inputs of one m (k_dyn_prep's fields, same expressions)
 // from the m's state slice Sst (smi layout); writes In[f][kCW] for f < nin.  The
 // whole block calls it.
@@ -795,25 +825,14 @@ __device__ inline void inv_inputs(const double *Sst, double *In, const double *p
     auto put = [&](int f, double v) { In[f * kCW + cc] = v; };
 #pragma unroll
     for (int var = 0; var < 4; ++var) put(var * kKX + k, sv(var, j2, k, cc));
-    // uvspec (spe_spectral.f90:351-387) of level lev at k -> ucos (field fu), vcos (fv).
-    // Branch-free: every case's operands read (neighbour indices clamped) and its
-    // expression formed, then the case selected -- the same values as the reference's
-    // n == 1 / n == ntrun+2 / interior branches, without a divergent branch and its
-    // dependent LDS round trip per case (p and n vary across a wave's lanes)
-    static_assert(kNTRUN1 - 1 == kNX - 2, "uvspec's last row reads n - 1");
+    // uvspec of level lev at k -> ucos (field fu), vcos (fv)
     const int nm = n > 0 ? n - 1 : 0, np = n < kNX - 1 ? n + 1 : kNX - 1;
     const bool first = n == 0, last = n == kNX - 1;
     auto uvspec = [&](int lev, int fu, int fv) {
-        const double vor_m = sv(0, lev, k, 2 * nm + p), vor_p = sv(0, lev, k, 2 * np + p);
-        const double div_m = sv(1, lev, k, 2 * nm + p), div_p = sv(1, lev, k, 2 * np + p);
-        const double vor_x = sv(0, lev, k, 2 * n + 1 - p), div_x = sv(1, lev, k, 2 * n + 1 - p);
-        const double ux = tb.uvdx_n(n), uvdym = tb.uvdym_n(n), uvdyp = tb.uvdyp_n(n);
-        const double zc = p == 1 ? ux * div_x : -ux * div_x;
-        const double u0 = zc - uvdyp * vor_p, ul = uvdym * vor_m, um = uvdym * vor_m - uvdyp * vor_p + zc;
-        const double zp = p == 1 ? ux * vor_x : -ux * vor_x;
-        const double v0 = zp + uvdyp * div_p, vl = -uvdym * div_m, vm = -uvdym * div_m + uvdyp * div_p + zp;
-        put(fu, first ? u0 : last ? ul : um);
-        put(fv, first ? v0 : last ? vl : vm);
+        double u, v;
+        uvspec_sel(Sst, tb, lev, k, n, p, &u, &v);
+        put(fu, u);
+        put(fv, v);
     };
     uvspec(j2, n1 + k, n1 + kKX + k);
     if (k == 0) {  // grad(ps(j2)) (wave-uniform branch; the n cases selected as in uvspec)
@@ -833,7 +852,11 @@ __device__ inline void inv_inputs(const double *Sst, double *In, const double *p
         const double nx = phi + tb.xgeop2(kk + 1) * sv(2, 1, kk + 1, cc) + tb.xgeop1(kk) * sv(2, 1, kk, cc);
         phi = kk >= k ? nx : phi;
     }
-    if (m == 0 && k >= 1 && k <= kKX - 2) phi = phi + tb.corf(k) * (sv(2, 1, k + 1, cc) - sv(2, 1, k - 1, cc));
+    {
+        const int km = k > 0 ? k - 1 : 0, kp = k < kKX - 1 ? k + 1 : kKX - 1;
+        const double pc = phi + tb.corf(k) * (sv(2, 1, kp, cc) - sv(2, 1, km, cc));
+        if (m == 0 && k >= 1 && k <= kKX - 2) phi = pc;
+    }
     put(kPPhi1 + k, phi);
     if (k == 0) put(kPPs1, sv(4, 1, 0, cc));
     uvspec(1, n1 + 2 * kKX + 2 + k, n1 + 3 * kKX + 2 + k);
@@ -957,22 +980,8 @@ __device__ inline void gridy_io(const double *In, const GridyB &gb, double *__re
 template <class TB, class Put>
 __device__ inline void io_prep_m(const double *Sst, const TB &tb, int k, int cc, Put put) {
     const int n = cc >> 1, p = cc & 1;
-    auto vor = [&](int pp, int nn) { return Sst[smi(0, 1, k, 2 * nn + pp)]; };
-    auto div = [&](int pp, int nn) { return Sst[smi(1, 1, k, 2 * nn + pp)]; };
-    const double ux = tb.uvdx_n(n);
-    const double zp = p == 1 ? ux * vor(0, n) : -ux * vor(1, n);
-    const double zc = p == 1 ? ux * div(0, n) : -ux * div(1, n);
     double a, b;
-    if (n == 0) {
-        a = zc - tb.uvdyp_n(0) * vor(p, 1);
-        b = zp + tb.uvdyp_n(0) * div(p, 1);
-    } else if (n == kNX - 1) {
-        a = tb.uvdym_n(n) * vor(p, kNTRUN1 - 1);
-        b = -tb.uvdym_n(n) * div(p, kNTRUN1 - 1);
-    } else {
-        b = -tb.uvdym_n(n) * div(p, n - 1) + tb.uvdyp_n(n) * div(p, n + 1) + zp;
-        a = tb.uvdym_n(n) * vor(p, n - 1) - tb.uvdyp_n(n) * vor(p, n + 1) + zc;
-    }
+    uvspec_sel(Sst, tb, 1, k, n, p, &a, &b);
     put(k, a);
     put(kKX + k, b);
     put(2 * kKX + k, Sst[smi(2, 1, k, cc)]);
@@ -1845,32 +1854,26 @@ __global__ __launch_bounds__(kSpecThreads) void k_io_entry(const double *__restr
     __syncthreads();
     // c) k_io_prep: uvspec of level 1 and copies -> the safety check's inputs
     {
-        auto vor = [&](int pp, int nn) { return Sst[smi(0, 1, k, 2 * nn + pp)]; };
-        auto div = [&](int pp, int nn) { return Sst[smi(1, 1, k, 2 * nn + pp)]; };
-        const double ux = tb.uvdx_n(n);
-        const double zp = p == 1 ? ux * vor(0, n) : -ux * vor(1, n);
-        const double zc = p == 1 ? ux * div(0, n) : -ux * div(1, n);
         double a, b;
-        if (n == 0) {
-            a = zc - tb.uvdyp_n(0) * vor(p, 1);
-            b = zp + tb.uvdyp_n(0) * div(p, 1);
-        } else if (n == kNX - 1) {
-            a = tb.uvdym_n(n) * vor(p, kNTRUN1 - 1);
-            b = -tb.uvdym_n(n) * div(p, kNTRUN1 - 1);
-        } else {
-            b = -tb.uvdym_n(n) * div(p, n - 1) + tb.uvdyp_n(n) * div(p, n + 1) + zp;
-            a = tb.uvdym_n(n) * vor(p, n - 1) - tb.uvdyp_n(n) * vor(p, n + 1) + zc;
-        }
+        uvspec_sel(Sst, tb, 1, k, n, p, &a, &b);
         chk[(size_t)k * kSF + c] = a;
         chk[(size_t)(kKX + k) * kSF + c] = b;
         chk[(size_t)(2 * kKX + k) * kSF + c] = Sst[smi(2, 1, k, cc)];
         chk[(size_t)(3 * kKX + k) * kSF + c] = Sst[smi(3, 1, k, cc)];
         if (k == 0) chk[(size_t)(4 * kKX) * kSF + c] = Sst[smi(4, 1, 0, cc)];
     }
-    // d) the m-major slice for the window's first k_st_spec (k_state_to_m)
+    // d) the m-major slice for the window's first k_st_spec (k_state_to_m; whole rows
+    // of the block, the LDS reads issued together)
     {
-        double2 *dst = reinterpret_cast<double2 *>(sm + (size_t)m * kSM);
-        for (int i = tid; i < kSM / 2; i += blockDim.x) dst[i] = reinterpret_cast<const double2 *>(Sst)[i];
+        static_assert(kSM / 2 % kSpecThreads == 0, "slice rows");
+        constexpr int R = kSM / 2 / kSpecThreads;
+        double2 *dst = reinterpret_cast<double2 *>(sm + (size_t)m * kSM) + tid;
+        const double2 *src = reinterpret_cast<const double2 *>(Sst) + tid;
+        double2 v[R];
+#pragma unroll
+        for (int q = 0; q < R; ++q) v[q] = src[q * kSpecThreads];
+#pragma unroll
+        for (int q = 0; q < R; ++q) dst[q * kSpecThreads] = v[q];
     }
     // e) k_st_inv: step(1, 1)'s inverse inputs (j2 = 1) and gridy
     inv_inputs(Sst, In, Fm, tb, m, 1, n1, nin);
