@@ -868,6 +868,21 @@ __device__ inline void inv_inputs(const double *Sst, double *In, const double *p
 struct GridyB {
     double b00[4], b01[4], b10[4], b11[4];
 };
+// the same operands from a copy of pinv's m-slice [n][32] (LDS)
+__device__ inline GridyB gridy_operands_slice(const double *pm) {
+    const int l = threadIdx.x & 63, r = l & 15, kk = l >> 4;
+    GridyB g;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        const int n_odd = 2 * (4 * s + kk), n_even = n_odd + 1;
+        g.b00[s] = pm[n_odd * 32 + r];
+        g.b01[s] = pm[n_odd * 32 + 16 + r];
+        g.b10[s] = pm[n_even * 32 + r];
+        g.b11[s] = pm[n_even * 32 + 16 + r];
+    }
+    return g;
+}
+
 __device__ inline GridyB gridy_operands(const double *__restrict__ pinv, int m) {
     const int l = threadIdx.x & 63, r = l & 15, kk = l >> 4;
     const double *pm = pinv + (size_t)m * kNX * 32;
@@ -1544,6 +1559,12 @@ __global__ __launch_bounds__(kSpecBlk) void k_st_spec(
         const double *src = which == 0 ? phis : which == 1 ? tcorh : qcorh;
         rf = src[ci(cf & 1, m, cf >> 1)];
     }
+    // gridy's Legendre slice of this m (8 KB, one 16-B load per thread), staged in V
+    // behind the tables: each wave then reads its MFMA operands from LDS instead of
+    // every wave fetching the same 8 KB from memory in the gridy phase
+    constexpr int kPinvM = kNX * 32, kVPinv = 2 * RT * kSpecBlk;
+    static_assert(kPinvM == 2 * kSpecBlk && kVPinv + kPinvM <= kVFm && kVPinv % 2 == 0, "pinv slice staging in V");
+    const double2 rp = reinterpret_cast<const double2 *>(pinv + (size_t)m * kPinvM)[threadIdx.x];
     // specy operands: wave w's tiles all use this m's Legendre columns of its lanes
     const double *pm = pfwd + (size_t)m * kNX * kIY;
     double wv[kIY / 4], bS[kIY / 4], bD[kIY / 4];
@@ -1617,6 +1638,7 @@ __global__ __launch_bounds__(kSpecBlk) void k_st_spec(
         s2[3 * kSpecBlk] = rs3;
         s2[4 * kSpecBlk] = rs4;
         if (threadIdx.x < 3 * kCW) Fm[threadIdx.x] = rf;
+        reinterpret_cast<double2 *>(V + kVPinv)[threadIdx.x] = rp;
     }
     __syncthreads();  // S, Sst, Fm, the tables complete
     const LTab tb{tm};
@@ -1653,7 +1675,7 @@ __global__ __launch_bounds__(kSpecBlk) void k_st_spec(
         if (io_varm) {  // run_model: iogrid(31)'s k_io_prep + gridy of this m (block-uniform)
             if (holds) io_prep_m(Sst, tb, k, cc, [&](int f, double v) { S[f * kCW + cc] = v; });
             __syncthreads();
-            gridy_io(S, gridy_operands(pinv, m), io_varm, m, kNIo);
+            gridy_io(S, gridy_operands_slice(V + kVPinv), io_varm, m, kNIo);
         }
         return;  // block-uniform
     }
@@ -1673,7 +1695,7 @@ __global__ __launch_bounds__(kSpecBlk) void k_st_spec(
     stamp(dbg, sk, 5);
     {
         const int nt = (nin + 7) / 8, per = (nt + kSpecSplit - 1) / kSpecSplit;
-        gridy_m(S, gridy_operands(pinv, m), varm_next, m, nin, half * per, min(nt, (half + 1) * per));
+        gridy_m(S, gridy_operands_slice(V + kVPinv), varm_next, m, nin, half * per, min(nt, (half + 1) * per));
     }
     if (dbg) {  // (diagnostics only: the kernel ends here)
         __syncthreads();
