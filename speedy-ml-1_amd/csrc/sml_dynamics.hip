@@ -902,44 +902,37 @@ __device__ inline void gridy_m(const double *In, const GridyB &gb, double *__res
                                int tile0 = 0, int tile1 = -1) {
     const int wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
     const int l = threadIdx.x & 63, r = l & 15, kk = l >> 4;
-    const double *b00 = gb.b00, *b01 = gb.b01, *b10 = gb.b10, *b11 = gb.b11;
     const int tend = tile1 < 0 ? (nf + 7) / 8 : tile1;
-    for (int tile = tile0 + wave; tile < tend; tile += nw) {
+    // work unit u = (tile, latitude half): half 0 the rows j < 16 (b00 / b10), half 1
+    // j >= 16 (b01 / b11).  Whole tiles left the SIMDs uneven (k_st_spec's 6 tiles on
+    // 8 waves: 2 tiles on two SIMDs, 1 on the others); half tiles give every SIMD 1.5
+    for (int u = wave; u < 2 * (tend - tile0); u += nw) {
+        const int tile = tile0 + (u >> 1), half = u & 1;
         const int f0 = tile * 8;
         const int fa = f0 + (r >> 1), p = r & 1;
         const bool ok = fa < nf;
         const double *a = In + (ok ? fa : 0) * kCW + p;
-        d4 acc00 = {0, 0, 0, 0}, acc01 = acc00, acc10 = acc00, acc11 = acc00;
+        d4 accS = {0, 0, 0, 0}, accA = accS;
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
             const int n_odd = 2 * (4 * s + kk);  // n = 1,3,.. (1-based): symmetric part
             const int n_even = n_odd + 1;        // n = 2,4,..: antisymmetric part
             const double a0 = ok ? a[2 * n_odd] : 0.0;
             const double a1 = ok ? a[2 * n_even] : 0.0;
-            acc00 = MFMA64(a0, b00[s], acc00);
-            acc01 = MFMA64(a0, b01[s], acc01);
-            acc10 = MFMA64(a1, b10[s], acc10);
-            acc11 = MFMA64(a1, b11[s], acc11);
+            accS = MFMA64(a0, half ? gb.b01[s] : gb.b00[s], accS);
+            accA = MFMA64(a1, half ? gb.b11[s] : gb.b10[s], accA);
         }
+        const int j = 16 * half + r;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int row = kk + 4 * q;
             const int f = f0 + (row >> 1);
-            if (f >= nf) continue;
+            if (f >= nf || j >= kIY) continue;
             // m-major inverse Fourier coefficients vim[m][lat][f][p]
             double *vr = varm + (size_t)m * kVIm + f * 2 + (row & 1);
-            {
-                const int j = r;
-                const double sym = acc00[q], asym = acc10[q];
-                vr[(kIL - 1 - j) * kVIl] = sym + asym;
-                vr[j * kVIl] = sym - asym;
-            }
-            const int j = 16 + r;
-            if (j < kIY) {
-                const double sym = acc01[q], asym = acc11[q];
-                vr[(kIL - 1 - j) * kVIl] = sym + asym;
-                vr[j * kVIl] = sym - asym;
-            }
+            const double sym = accS[q], asym = accA[q];
+            vr[(kIL - 1 - j) * kVIl] = sym + asym;
+            vr[j * kVIl] = sym - asym;
         }
     }
 }
