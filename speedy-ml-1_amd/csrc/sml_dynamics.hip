@@ -241,20 +241,26 @@ __global__ void k_dyn_prep(const double *__restrict__ st, double *__restrict__ s
     }
 }
 
+// the grid-point dynamics' per-level constants and the Coriolis row (the DynTables
+// fields gridpoint_column reads), for an LDS copy in the row kernel
+struct GpTab {
+    double dhs[kKX], dhsr[kKX], fsgr[kKX], tref[kKX], tref3[kKX], coriol[kIL];
+};
+
 // grid-point dynamics of one column (grtend :60-217 and the products of :233-275).
 // g(f) = inverse-transformed field f at the column (layout of k_dyn_prep, kcos = 2
 // group at o2); hasP: add phypar's tendencies pu/pv/pt/pq [kx] where phypar adds
 // them (:225); put(f, v) receives the 73 forward-transform inputs
 //   [utend 8 | -u*tgg 8 | -u*trg 8 | vtend 8 | -v*tgg 8 | -v*trg 8]  (x 1/cos in specx)
 //   [0.5(u^2+v^2) 8 | ttend 8 | trtend 8 | -umean*px - vmean*py]
-template <class GetF, class PutF>
-__device__ inline void gridpoint_products(int o2, GetF g, PutF put, const DynTables *T);
+template <class GetF, class PutF, class TT>
+__device__ inline void gridpoint_products(int o2, GetF g, PutF put, const TT *T);
 
 // products = false: the products of :239-271 are left to gridpoint_products (the row
 // kernel runs them on the lane that has slack)
-template <class GetF, class PutF>
+template <class GetF, class PutF, class TT>
 __device__ inline void gridpoint_column(int j, int o2, GetF g, bool hasP, const double *pu, const double *pv,
-                                        const double *pt, const double *pq, PutF put, const DynTables *T,
+                                        const double *pt, const double *pq, PutF put, const TT *T,
                                         bool products = true) {
     double ug[kKX], vg[kKX], vorg[kKX], divg[kKX], tg[kKX], trg[kKX];
 #pragma unroll
@@ -336,8 +342,8 @@ __device__ inline void gridpoint_column(int j, int o2, GetF g, bool hasP, const 
     if (products) gridpoint_products(o2, g, put, T);
 }
 
-template <class GetF, class PutF>
-__device__ inline void gridpoint_products(int o2, GetF g, PutF put, const DynTables *T) {
+template <class GetF, class PutF, class TT>
+__device__ inline void gridpoint_products(int o2, GetF g, PutF put, const TT *T) {
 #pragma unroll
     for (int k = 0; k < kKX; ++k) {
         const double ug = g(o2 + k), vg = g(o2 + kKX + k), trg = g(3 * kKX + k);
@@ -1333,10 +1339,27 @@ __global__ __launch_bounds__(kGsThreads) void k_st_gridspec(
     const double *__restrict__ cosgr, const DynTables *__restrict__ T, const double *__restrict__ bc,
     double *__restrict__ rad, const PhysTables *__restrict__ PT, int lradsw, long long *dbg) {
     __shared__ double A[kFftN * kRowLd], B[kFftN * kRowLd], was[kFftWa];
+    // phypar's per-level constants (PhysTables before fband) and the grid-point
+    // dynamics' (GpTab) staged in LDS with gridx's loads: read from memory where they
+    // are used, each new line of them was a scalar-cache miss the column's dependent
+    // chain waited on (one per phase of the moist side)
+    constexpr int kPtS = (int)(offsetof(PhysTables, fband) / sizeof(double)), kGpS = (int)(sizeof(GpTab) / 8);
+    static_assert(kPtS + kGpS <= kGsThreads && kGpS == 5 * kKX + kIL, "table staging: one value per thread");
+    __shared__ double ptl[kPtS];
+    __shared__ GpTab gpt;
     constexpr int n1 = kNInv1P;
     constexpr int nphys = (n1 - kPT1) + (kNInvP - (n1 + 2 * kKX + 2));  // 25 + 16 = 41
     const int j = blockIdx.x, tid = threadIdx.x;
     stamp(dbg, 0, 0);
+    double rtab = 0.0;
+    if (tid < kPtS) {
+        rtab = reinterpret_cast<const double *>(PT)[tid];
+    } else if (tid < kPtS + kGpS) {
+        const int e = tid - kPtS, k = e % kKX;
+        const int w = e / kKX;
+        rtab = w == 0 ? T->dhs[k] : w == 1 ? T->dhsr[k] : w == 2 ? T->fsgr[k] : w == 3 ? T->tref[k]
+             : w == 4 ? T->tref3[k] : T->coriol[e - 5 * kKX];
+    }
     // gridx: transform t (the dynamics fields, then phypar's) on lanes 2 t, 2 t + 1;
     // its coefficients are loaded before the twiddles are staged, so the two loads
     // share one memory round trip
@@ -1349,11 +1372,14 @@ __global__ __launch_bounds__(kGsThreads) void k_st_gridspec(
         double xi[kMX2 - 1];
         if (act) row_gridx_load(varm, f, j, xi);
         if (tid < kFftWa) was[tid] = wa[tid];
+        if (tid < kPtS) ptl[tid] = rtab;
+        else if (tid < kPtS + kGpS) reinterpret_cast<double *>(&gpt)[tid - kPtS] = rtab;
         __syncthreads();
         if (act) row_gridx_half(A, xi, was, f, f >= n1, cosgr[j], h);
     }
     __syncthreads();
     stamp(dbg, 0, 1);
+    const PhysTables *PTl = reinterpret_cast<const PhysTables *>(ptl);  // (fband stays in PT)
     const double cj = cosgr[j];
     // phypar of column i, split between the waves, the reference's expressions
     // unchanged: waves 0-1, after the grid-point dynamics, do the moist part and the
@@ -1370,7 +1396,7 @@ __global__ __launch_bounds__(kGsThreads) void k_st_gridspec(
             const int i = tid;
             double dummy[kKX];
             gridpoint_column(j, n1, [&](int f) { return A[i * kRowLd + f]; }, false, dummy, dummy, dummy, dummy,
-                             [&](int f, double v) { B[i * kRowLd + f] = v; }, T, false);
+                             [&](int f, double v) { B[i * kRowLd + f] = v; }, &gpt, false);
             // the moist / diffusion part of column i's phypar
             const double *Ai = A + i * kRowLd;
             double ta[kKX], qa[kKX], ph[kKX];
@@ -1381,11 +1407,11 @@ __global__ __launch_bounds__(kGsThreads) void k_st_gridspec(
                 ph[k] = Ai[kPPhi1 + k];
             }
             PhysThermo h;
-            phys_thermo(ta, qa, ph, Ai[kPPs1], PT, h);
+            phys_thermo(ta, qa, ph, Ai[kPPs1], PTl, h);
             double tt[kKX], qt[kKX], precnv, precls, ttv[kKX], qtv[kKX];
             int itop, icnv;
-            phys_moist(h, PT, tt, qt, precnv, precls, itop, icnv);
-            phys_vdif(h, ph, icnv, PT, ttv, qtv);
+            phys_moist(h, PTl, tt, qt, precnv, precls, itop, icnv);
+            phys_vdif(h, ph, icnv, PTl, ttv, qtv);
             double *Bh = B + i * kRowLd + kNFwd;
             // tt[0] is +0 always (convection and condensation leave the top level alone)
 #pragma unroll
@@ -1413,11 +1439,11 @@ __global__ __launch_bounds__(kGsThreads) void k_st_gridspec(
         double psg, qc[kKX];
         if (lradsw) {  // the shortwave first: its inputs are the moist part's (phys_column's order)
             PhysThermo h;
-            phys_thermo(ta, qa, ph, ps1, PT, h);
+            phys_thermo(ta, qa, ph, ps1, PTl, h);
             double tt[kKX], qt[kKX], precnv, precls;
             int itop, icnv;
-            phys_moist(h, PT, tt, qt, precnv, precls, itop, icnv);
-            phys_sw(pt, h, ph, precnv, precls, itop, bc, rad, PT);
+            phys_moist(h, PTl, tt, qt, precnv, precls, itop, icnv);
+            phys_sw(pt, h, ph, precnv, precls, itop, bc, rad, PTl);
             psg = h.psg;
             rl_rps = h.rps;
 #pragma unroll
@@ -1428,11 +1454,11 @@ __global__ __launch_bounds__(kGsThreads) void k_st_gridspec(
 #pragma unroll
             for (int k = 0; k < kKX; ++k) qc[k] = fmax(qa[k], 0.);
         }
-        phys_lw_sfc(pt, ua, va, ta, qc, ph, psg, rl_rps, bc, rad, PT, &PT->fband[0][0], rl_tt, rl_us, rl_vs, rl_sh,
+        phys_lw_sfc(pt, ua, va, ta, qc, ph, psg, rl_rps, bc, rad, PTl, &PT->fband[0][0], rl_tt, rl_us, rl_vs, rl_sh,
                     rl_ev);
         // the grid-point dynamics' products (this side has the slack)
         gridpoint_products(n1, [&](int f) { return A[i * kRowLd + f]; },
-                           [&](int f, double v) { B[i * kRowLd + f] = v; }, T);
+                           [&](int f, double v) { B[i * kRowLd + f] = v; }, &gpt);
     }
     __syncthreads();
     if (tid >= 128 && tid - 128 < kIX) {  // phys_column's sums (phy_phypar.f90:174-196)
@@ -1447,10 +1473,10 @@ __global__ __launch_bounds__(kGsThreads) void k_st_gridspec(
             double ttv = Bh[7 + k], utv = 0., vtv = 0.;
             double qtk;
             if (k == kKX - 1) {
-                utv = utv + rl_us * rps * PT->grdsig[kKX - 1];
-                vtv = vtv + rl_vs * rps * PT->grdsig[kKX - 1];
-                ttv = ttv + rl_sh * rps * PT->grdscp[kKX - 1];
-                const double qtv = Bh[23] + rl_ev * rps * PT->grdsig[kKX - 1];
+                utv = utv + rl_us * rps * PTl->grdsig[kKX - 1];
+                vtv = vtv + rl_vs * rps * PTl->grdsig[kKX - 1];
+                ttv = ttv + rl_sh * rps * PTl->grdscp[kKX - 1];
+                const double qtv = Bh[23] + rl_ev * rps * PTl->grdsig[kKX - 1];
                 qtk = Bh[22] + qtv;
             } else {
                 qtk = Bh[15 + k];
