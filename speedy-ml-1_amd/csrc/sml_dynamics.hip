@@ -1389,7 +1389,7 @@ __global__ __launch_bounds__(kGsThreads) void k_st_gridspec(
     // convective precipitation and cloud top).  The moist side hands its 24 values
     // over in B's spare columns [kNFwd, kRowLd); waves 2-3 sum the tendencies in
     // phys_column's order.
-    double rl_tt[kKX], rl_us = 0.0, rl_vs = 0.0, rl_sh = 0.0, rl_ev = 0.0, rl_rps = 0.0;
+    double rl_tt[kKX], rl_rsw[kKX], rl_us = 0.0, rl_vs = 0.0, rl_sh = 0.0, rl_ev = 0.0, rl_rps = 0.0;
     static_assert(kRowLd - kNFwd >= 24, "moist-side hand-over: 24 spare slots per column in B");
     if (tid < 128) {
         if (tid < kIX) {  // grid-point dynamics of column i -> F in B[i][f]
@@ -1456,20 +1456,24 @@ __global__ __launch_bounds__(kGsThreads) void k_st_gridspec(
         }
         phys_lw_sfc(pt, ua, va, ta, qc, ph, psg, rl_rps, bc, rad, PTl, &PT->fband[0][0], rl_tt, rl_us, rl_vs, rl_sh,
                     rl_ev);
+        // the shortwave heating of the column (rad; written by phys_sw on a shortwave
+        // step, by this lane) for the sums after the barrier: loaded here, its memory
+        // round trip hides in this side's slack instead of following the barrier
+#pragma unroll
+        for (int k = 0; k < kKX; ++k) rl_rsw[k] = rad[kRadTtRsw + (size_t)k * kNGP + pt];
         // the grid-point dynamics' products (this side has the slack)
         gridpoint_products(n1, [&](int f) { return A[i * kRowLd + f]; },
                            [&](int f, double v) { B[i * kRowLd + f] = v; }, &gpt);
     }
     __syncthreads();
     if (tid >= 128 && tid - 128 < kIX) {  // phys_column's sums (phy_phypar.f90:174-196)
-        const int i = tid - 128, pt = j * kIX + i;
+        const int i = tid - 128;
         double *Ai = A + i * kRowLd;
         const double *Bh = B + i * kRowLd + kNFwd;
-        const double *tt_rsw = rad + kRadTtRsw;
         const double rps = rl_rps;
 #pragma unroll
         for (int k = 0; k < kKX; ++k) {
-            const double ttk = (k == 0 ? 0.0 : Bh[k - 1]) + tt_rsw[(size_t)k * kNGP + pt] + rl_tt[k];
+            const double ttk = (k == 0 ? 0.0 : Bh[k - 1]) + rl_rsw[k] + rl_tt[k];
             double ttv = Bh[7 + k], utv = 0., vtv = 0.;
             double qtk;
             if (k == kKX - 1) {
