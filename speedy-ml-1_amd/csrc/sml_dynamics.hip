@@ -1686,7 +1686,7 @@ __global__ __launch_bounds__(kSpecBlk) void k_st_spec(
     // c) sptend / implic / diffusion / time integration on the LDS state
     auto SA = [&](int var, int lev, int kk2) -> double & { return Sst[smi(var, lev, kk2, cc)]; };
     if (holds)
-        tail_coef<kCW>(SA, lead ? Td : nullptr, lead ? phi_out : nullptr, Fm, Fm + kCW, Fm + 2 * kCW, cc, tb, sh, cc, k, c, m, n, vo, dv - lapv, tdt0,
+        tail_coef<kCW>(SA, lead ? Td : nullptr, lead && next_j2 <= 0 ? phi_out : nullptr, Fm, Fm + kCW, Fm + 2 * kCW, cc, tb, sh, cc, k, c, m, n, vo, dv - lapv, tdt0,
                        trdt0, psdt, j1, j4, dt, alph, rob, wil);
     else
         tail_coef_barriers(alph);
