@@ -11,6 +11,7 @@
 #include <random>
 
 #include "sml_fft.hpp"
+#include "sml_fft_wa96.hpp"
 
 using namespace sml;
 
@@ -54,6 +55,9 @@ int main(int argc, char **argv) {
     int bad = 0;
     for (int i = 0; i < 94; ++i)
         if (std::memcmp(&wa[i], &wsave[n + i], 8)) { ++bad; std::printf("twiddle %d differs: %.17g %.17g\n", i, wa[i], wsave[n + i]); }
+    // the literal table the row kernel folds into its passes (sml_fft_wa96.hpp)
+    for (int i = 0; i < kFftWa; ++i)
+        if (std::memcmp(&wa[i], &kFftWa96[i], 8)) { ++bad; std::printf("kFftWa96[%d] differs: %.17g %.17g\n", i, wa[i], kFftWa96[i]); }
     std::mt19937_64 rng(42);
     std::normal_distribution<double> nd;
     int nbwd = 0, nfwd = 0, npair = 0;

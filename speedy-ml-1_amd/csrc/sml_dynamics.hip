@@ -36,6 +36,7 @@
 
 #include "sml_dynamics_tables.hpp"
 #include "sml_fft.hpp"
+#include "sml_fft_wa96.hpp"
 #include "sml_physics.hpp"
 #include "sml_spectral_internal.hpp"
 
@@ -1338,7 +1339,11 @@ __global__ __launch_bounds__(kGsThreads) void k_st_gridspec(
     const double *__restrict__ varm, double *__restrict__ vfm, const double *__restrict__ wa,
     const double *__restrict__ cosgr, const DynTables *__restrict__ T, const double *__restrict__ bc,
     double *__restrict__ rad, const PhysTables *__restrict__ PT, int lradsw, long long *dbg) {
-    __shared__ double A[kFftN * kRowLd], B[kFftN * kRowLd], was[kFftWa];
+    __shared__ double A[kFftN * kRowLd], B[kFftN * kRowLd];
+    // the FFT twiddles as literals (kFftWa96: the same values as wa, bit for bit), folded
+    // into the unrolled passes instead of LDS reads of a staged table
+    const double *was = kFftWa96;
+    (void)wa;
     // phypar's per-level constants (PhysTables before fband) and the grid-point
     // dynamics' (GpTab) staged in LDS with gridx's loads: read from memory where they
     // are used, each new line of them was a scalar-cache miss the column's dependent
@@ -1371,7 +1376,6 @@ __global__ __launch_bounds__(kGsThreads) void k_st_gridspec(
                                                          : n1 + 2 * kKX + 2 + (t - kNInv - (n1 - kPT1)));
         double xi[kMX2 - 1];
         if (act) row_gridx_load(varm, f, j, xi);
-        if (tid < kFftWa) was[tid] = wa[tid];
         if (tid < kPtS) ptl[tid] = rtab;
         else if (tid < kPtS + kGpS) reinterpret_cast<double *>(&gpt)[tid - kPtS] = rtab;
         __syncthreads();
