@@ -86,6 +86,7 @@ struct sml_dynamics {
     double *d_phis = nullptr, *d_tcorh = nullptr, *d_qcorh = nullptr, *d_phi = nullptr;
     double *d_specin = nullptr, *d_varm = nullptr, *d_grid = nullptr, *d_gfwd = nullptr, *d_sfwd = nullptr;
     double *d_vfm = nullptr;  // fused step: m-major forward Fourier coefficients [m][73][lat][2]
+    double *d_pfl = nullptr;  // specy's MFMA B operands in lane order [m][k-step][lane][S, D] (k_pack_pfwd)
     double *d_sm = nullptr;   // fused step: m-major state [2][m][var 5][lev 2][kx][n p], ping-pong:
     int sm_cur = 0;           // k_st_spec reads buffer sm_cur and writes the other (see sm_buf)
     long long *d_dbg = nullptr;  // diagnostic phase stamps (SML_DYN_STAMPS=1)
@@ -1527,11 +1528,24 @@ __global__ __launch_bounds__(kGsThreads) void k_st_gridspec(
     stamp(dbg, 0, 3);
 }
 
+// specy's MFMA B operands in lane order: lane l = 16 kk + r of k-step s takes
+// pfwd[m][n][j] at n = 2 r (S) and 2 r + 1 (D), j = 4 s + kk ([m][n 32][lat 24], the
+// spectral context's forward Legendre table) -> pfl[m][s][l][2]
+__global__ void k_pack_pfwd(const double *__restrict__ pfwd, double *__restrict__ pfl) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= kMX * (kIY / 4) * 64) return;
+    const int l = e % 64, s = (e / 64) % (kIY / 4), m = e / (64 * (kIY / 4));
+    const int r = l & 15, kk = l >> 4, j = 4 * s + kk;
+    const double *pm = pfwd + (size_t)m * kNX * kIY;
+    pfl[2 * (size_t)e] = pm[(2 * r) * kIY + j];
+    pfl[2 * (size_t)e + 1] = pm[(2 * r + 1) * kIY + j];
+}
+
 // one zonal wavenumber m: specy of the 73 forward transforms, combine and tail of
 // the m's 64 real coefficients x 8 levels (one thread each) on the m's state slice
 // in LDS; with next_j2 > 0 the new state feeds the next step's inverse transforms
 __global__ __launch_bounds__(kSpecBlk) void k_st_spec(
-    const double *__restrict__ vfm, const double *__restrict__ pfwd, const double *__restrict__ wt,
+    const double *__restrict__ vfm, const double *__restrict__ pfl, const double *__restrict__ wt,
     const double *__restrict__ sm, double *__restrict__ sm_out, double *__restrict__ Td, double *__restrict__ phi_out,
     const double *__restrict__ phis,
     const double *__restrict__ tcorh, const double *__restrict__ qcorh, const DynTables *__restrict__ T, int j1,
@@ -1592,15 +1606,17 @@ __global__ __launch_bounds__(kSpecBlk) void k_st_spec(
     constexpr int kPinvM = kNX * 32, kVPinv = 2 * RT * kSpecBlk;
     static_assert(kPinvM == 2 * kSpecBlk && kVPinv + kPinvM <= kVFm && kVPinv % 2 == 0, "pinv slice staging in V");
     const double2 rp = reinterpret_cast<const double2 *>(pinv + (size_t)m * kPinvM)[threadIdx.x];
-    // specy operands: wave w's tiles all use this m's Legendre columns of its lanes
-    const double *pm = pfwd + (size_t)m * kNX * kIY;
+    // specy operands: wave w's tiles all use this m's Legendre columns of its lanes,
+    // packed in lane order (k_pack_pfwd): one contiguous 1-KB load per k-step instead
+    // of two loads touching 16 lines each (the prologue is bound by its loads' lines)
+    const double2 *pl = reinterpret_cast<const double2 *>(pfl) + (size_t)m * (kIY / 4) * 64 + l;
     double wv[kIY / 4], bS[kIY / 4], bD[kIY / 4];
 #pragma unroll
     for (int s = 0; s < kIY / 4; ++s) {
-        const int j = 4 * s + kk;
-        wv[s] = wt[j];
-        bS[s] = pm[(2 * r) * kIY + j];
-        bD[s] = pm[(2 * r + 1) * kIY + j];
+        const double2 b = pl[s * 64];
+        wv[s] = wt[4 * s + kk];
+        bS[s] = b.x;
+        bD[s] = b.y;
     }
     if (dbg) __syncthreads();
     stamp(dbg, sk, 1);
@@ -1782,7 +1798,7 @@ __global__ void k_io_prep(const double *__restrict__ st, double *__restrict__ si
 // spectral module's layout; state: reference layout, level 1 written, level 2 read
 // into the m-major slice sm; chk: k_io_prep's output; varm: gridy for step(1, 1).
 __global__ __launch_bounds__(kSpecThreads) void k_io_entry(const double *__restrict__ vio,
-                                                           const double *__restrict__ pfwd,
+                                                           const double *__restrict__ pfl,
                                                            const double *__restrict__ wt, double *__restrict__ state,
                                                            double *__restrict__ sm, double *__restrict__ chk,
                                                            const double *__restrict__ phis,
@@ -1832,15 +1848,16 @@ __global__ __launch_bounds__(kSpecThreads) void k_io_entry(const double *__restr
     double vn[kIY / 4], vs[kIY / 4], wv[kIY / 4], bS[kIY / 4], bD[kIY / 4];
     if (spw) {
         const double *vr = vio + (size_t)(ok ? fa : 0) * kVarmField + 2 * m + (r & 1);
-        const double *pm = pfwd + (size_t)m * kNX * kIY;
+        const double2 *pl = reinterpret_cast<const double2 *>(pfl) + (size_t)m * (kIY / 4) * 64 + l;
 #pragma unroll
         for (int s = 0; s < kIY / 4; ++s) {
             const int j = 4 * s + kk;
             vn[s] = vr[(kIL - 1 - j) * kMX2];
             vs[s] = vr[j * kMX2];
             wv[s] = wt[j];
-            bS[s] = pm[(2 * r) * kIY + j];
-            bD[s] = pm[(2 * r + 1) * kIY + j];
+            const double2 b = pl[s * 64];  // the packed B operands (k_pack_pfwd)
+            bS[s] = b.x;
+            bD[s] = b.y;
         }
     }
     const GridyB gb = gridy_operands(pinv, m);
@@ -1981,7 +1998,7 @@ int dalloc(T **p, size_t count) {
 extern "C" int sml_dyn_destroy(sml_dynamics *d) {
     if (!d) return SML_OK;
     void *ptrs[] = {d->d_tabs, d->d_tabm, d->d_state, d->d_phis, d->d_tcorh, d->d_qcorh, d->d_phi, d->d_specin,
-                    d->d_varm, d->d_grid, d->d_gfwd, d->d_sfwd, d->d_tend, d->d_phys, d->d_minmax, d->d_io, d->d_vfm, d->d_sm, d->d_dbg,
+                    d->d_varm, d->d_grid, d->d_gfwd, d->d_sfwd, d->d_tend, d->d_phys, d->d_minmax, d->d_io, d->d_vfm, d->d_pfl, d->d_sm, d->d_dbg,
                     d->d_ptab, d->d_pbc, d->d_rad, d->d_pio};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
@@ -2032,6 +2049,7 @@ extern "C" int sml_dyn_create(double radius, sml_dynamics **out) {
         (rc = dalloc(&d->d_grid, (size_t)kNInvMax * kGF)) || (rc = dalloc(&d->d_gfwd, (size_t)kNFwd * kGF)) ||
         (rc = dalloc(&d->d_sfwd, (size_t)kNFwd * kSF)) || (rc = dalloc(&d->d_tend, kTendSize)) ||
         (rc = dalloc(&d->d_vfm, (size_t)kMX * kVFm)) || (rc = dalloc(&d->d_sm, (size_t)2 * kMX * kSM)) ||
+        (rc = dalloc(&d->d_pfl, (size_t)kMX * (kIY / 4) * 64 * 2)) ||
         (rc = dalloc(&d->d_phys, (size_t)4 * kKX * kGF)) || (rc = dalloc(&d->d_minmax, 8)) ||
         (rc = dalloc(&d->d_io, (size_t)4 * kKX * kGF + kGF)) || (rc = dalloc(&d->d_ptab, 1)) ||
         (rc = dalloc(&d->d_chk, (size_t)kNIo * (kSF + kVF + kGF))) ||
@@ -2043,6 +2061,12 @@ extern "C" int sml_dyn_create(double radius, sml_dynamics **out) {
     d->d_tab = d->d_tabs;
     hipError_t e = hipMemcpy(d->d_tab, &d->tab, sizeof(DynTables), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(d->d_ptab, &d->ptab, sizeof(PhysTables), hipMemcpyHostToDevice);
+    if (e == hipSuccess) {  // specy's packed B operands from the spectral context's forward Legendre table
+        const int n = kMX * (kIY / 4) * 64;
+        hipLaunchKernelGGL(k_pack_pfwd, dim3((n + 255) / 256), dim3(256), 0, 0, spectral_dev(d->sp).pfwd, d->d_pfl);
+        e = hipGetLastError();
+        if (e == hipSuccess) e = hipDeviceSynchronize();
+    }
     if (e != hipSuccess) {
         sml_dyn_destroy(d);
         return fail(SML_ERR_HIP, "sml_dyn_create: %s", hipGetErrorString(e));
@@ -2230,7 +2254,7 @@ int launch_step_fused(sml_dynamics *d, int j1, int j2, double dt, double alph, d
     const int j4 = (alph == 0.0) ? j2 : 1;
     const int cur = d->sm_cur;
     if (next_j2 > 0) d->sm_cur = 1 - cur;  // the next step reads what this one writes
-    hipLaunchKernelGGL(k_st_spec, dim3(kMX * kSpecSplit), dim3(kSpecBlk), 0, st, d->d_vfm, sd.pfwd, sd.wt,
+    hipLaunchKernelGGL(k_st_spec, dim3(kMX * kSpecSplit), dim3(kSpecBlk), 0, st, d->d_vfm, d->d_pfl, sd.wt,
                        sm_buf(d, cur), sm_buf(d, 1 - cur), d->d_tend,
                        d->d_phi, d->d_phis, d->d_tcorh, d->d_qcorh, T, j1, j4, dt, alph, rob, wil, sd.pinv, d->d_varm,
                        next_j2, n1, nin, d->d_tabm + (size_t)(d->d_tab - d->d_tabs) * kMX * kTabMDoubles, d->d_state,
@@ -2586,7 +2610,7 @@ extern "C" int sml_dyn_run_model(sml_dynamics *d, const double *d_grid4d, const 
         const SpectralDev sd = spectral_dev(d->sp);
         const bool phys = d->phys_on;
         d->sm_cur = 0;  // the window's chain starts in buffer 0
-        hipLaunchKernelGGL(k_io_entry, dim3(kMX), dim3(kSpecThreads), 0, st, d->d_vfm, sd.pfwd, sd.wt, d->d_state,
+        hipLaunchKernelGGL(k_io_entry, dim3(kMX), dim3(kSpecThreads), 0, st, d->d_vfm, d->d_pfl, sd.wt, d->d_state,
                            sm_buf(d, 0), d->d_chk, d->d_phis,
                            d->d_tabm + (size_t)(d->d_tab - d->d_tabs) * kMX * kTabMDoubles, sd.pinv, d->d_varm,
                            phys ? kNInv1P : kNInv1, phys ? kNInvP : kNInv);
