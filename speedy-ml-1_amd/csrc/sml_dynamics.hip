@@ -927,17 +927,20 @@ __device__ inline void gridy_m(const double *In, const GridyB &gb, double *__res
             const int n_even = n_odd + 1;        // n = 2,4,..: antisymmetric part
             const double a0 = ok ? a[2 * n_odd] : 0.0;
             const double a1 = ok ? a[2 * n_even] : 0.0;
-            accS = MFMA64(a0, half ? gb.b01[s] : gb.b00[s], accS);
-            accA = MFMA64(a1, half ? gb.b11[s] : gb.b10[s], accA);
+            // the transposed product (Legendre operand first: the same products summed
+            // in the same order), so a lane's outputs are latitude rows kk + 4 q of
+            // field-part column r: a store instruction writes 16 consecutive doubles of
+            // 4 latitudes (4 lines) instead of 4 of 16 latitudes (16 lines)
+            accS = MFMA64(half ? gb.b01[s] : gb.b00[s], a0, accS);
+            accA = MFMA64(half ? gb.b11[s] : gb.b10[s], a1, accA);
         }
-        const int j = 16 * half + r;
+        if (!ok) continue;
+        // m-major inverse Fourier coefficients vim[m][lat][f][p]: column r = 2 (fa - f0) + p
+        double *vr = varm + (size_t)m * kVIm + fa * 2 + p;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            const int row = kk + 4 * q;
-            const int f = f0 + (row >> 1);
-            if (f >= nf || j >= kIY) continue;
-            // m-major inverse Fourier coefficients vim[m][lat][f][p]
-            double *vr = varm + (size_t)m * kVIm + f * 2 + (row & 1);
+            const int j = 16 * half + kk + 4 * q;
+            if (j >= kIY) continue;
             const double sym = accS[q], asym = accA[q];
             vr[(kIL - 1 - j) * kVIl] = sym + asym;
             vr[j * kVIl] = sym - asym;
@@ -1122,15 +1125,15 @@ __device__ __attribute__((always_inline)) inline void row_specx_pair(const doubl
     auto O = [&](int i) { return S[(48 + i) * kRowLd + f]; };
     const double scale = 1. / (double)kIX;
     double *o = vfm + (size_t)j * kVLs + f * 2;
+    // (Re, Im) as one 16-B store: o is 16-B aligned (even offsets throughout vfm)
     auto out = [&](int m) {
         double re, im;
         fft::rfftf96_combine(E, O, m, wa, &re, &im);
-        o[(size_t)m * kVFm] = re * scale;
-        o[(size_t)m * kVFm + 1] = im * scale;
+        *reinterpret_cast<double2 *>(o + (size_t)m * kVFm) = double2{re * scale, im * scale};
     };
     if (h == 0) {
-        o[0] = (E(0) + O(0)) * scale;  // varm(1) = fvar(1) / ix, varm(2) = 0
-        o[1] = 0.0;
+        // varm(1) = fvar(1) / ix, varm(2) = 0
+        *reinterpret_cast<double2 *>(o) = double2{(E(0) + O(0)) * scale, 0.0};
 #pragma unroll
         for (int m = 1; m <= 15; ++m) out(m);
     } else {
