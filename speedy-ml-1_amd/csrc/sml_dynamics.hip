@@ -1476,7 +1476,6 @@ __global__ __launch_bounds__(kGsThreads) void k_st_gridspec(
     __syncthreads();
     if (tid >= 128 && tid - 128 < kIX) {  // phys_column's sums (phy_phypar.f90:174-196)
         const int i = tid - 128;
-        double *Ai = A + i * kRowLd;
         const double *Bh = B + i * kRowLd + kNFwd;
         const double rps = rl_rps;
 #pragma unroll
@@ -1493,10 +1492,13 @@ __global__ __launch_bounds__(kGsThreads) void k_st_gridspec(
             } else {
                 qtk = Bh[15 + k];
             }
-            Ai[phys_slot_col(k)] = 0. + utv;
-            Ai[phys_slot_col(kKX + k)] = 0. + vtv;
-            Ai[phys_slot_col(2 * kKX + k)] = ttk + ttv;
-            Ai[phys_slot_col(3 * kKX + k)] = qtk;
+            // F + P where grtend adds phypar's tendencies (u 0..7, v 24..31, t 56..63,
+            // q 64..71), the same additions specx made per sample: its lanes then read F only
+            double *Bi = B + i * kRowLd;
+            Bi[k] = Bi[k] + (0. + utv);
+            Bi[3 * kKX + k] = Bi[3 * kKX + k] + (0. + vtv);
+            Bi[7 * kKX + k] = Bi[7 * kKX + k] + (ttk + ttv);
+            Bi[8 * kKX + k] = Bi[8 * kKX + k] + qtk;
         }
     }
     __syncthreads();
@@ -1507,18 +1509,10 @@ __global__ __launch_bounds__(kGsThreads) void k_st_gridspec(
         const bool act = f < kNFwd;
         double x[48];
         if (act) {
-            // F field -> tendency slot of P: u 0..7, v 24..31, t 56..63, q 64..71
-            const int pf = f < kKX ? f : (f >= 3 * kKX && f < 4 * kKX) ? kKX + f - 3 * kKX
-                         : (f >= 7 * kKX && f < 9 * kKX) ? 2 * kKX + f - 7 * kKX : -1;
-            const double *fr = B + f + h * kRowLd, *pr = A + phys_slot_col(pf < 0 ? 0 : pf) + h * kRowLd;
-            // F, then + P (u, v, t, q), then x cosgr(j) (vdspec inputs): one branch per
-            // case around straight-line loops
+            // F (+ P already added in the sums), then x cosgr(j) (vdspec inputs)
+            const double *fr = B + f + h * kRowLd;
 #pragma unroll
             for (int i = 0; i < 48; ++i) x[i] = fr[2 * i * kRowLd];
-            if (pf >= 0) {
-#pragma unroll
-                for (int i = 0; i < 48; ++i) x[i] = x[i] + pr[2 * i * kRowLd];
-            }
             if (f < kNFwdScaled) {
 #pragma unroll
                 for (int i = 0; i < 48; ++i) x[i] = x[i] * cj;
