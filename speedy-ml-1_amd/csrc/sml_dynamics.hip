@@ -1470,8 +1470,9 @@ __global__ __launch_bounds__(kGsThreads) void k_st_gridspec(
 #pragma unroll
         for (int k = 0; k < kKX; ++k) rl_rsw[k] = rad[kRadTtRsw + (size_t)k * kNGP + pt];
         // the grid-point dynamics' products (this side has the slack)
+        // (the products below kNFwdScaled are vdspec inputs: x cosgr(j) here, not in specx)
         gridpoint_products(n1, [&](int f) { return A[i * kRowLd + f]; },
-                           [&](int f, double v) { B[i * kRowLd + f] = v; }, &gpt);
+                           [&](int f, double v) { B[i * kRowLd + f] = f < kNFwdScaled ? v * cj : v; }, &gpt);
     }
     __syncthreads();
     if (tid >= 128 && tid - 128 < kIX) {  // phys_column's sums (phy_phypar.f90:174-196)
@@ -1495,8 +1496,8 @@ __global__ __launch_bounds__(kGsThreads) void k_st_gridspec(
             // F + P where grtend adds phypar's tendencies (u 0..7, v 24..31, t 56..63,
             // q 64..71), the same additions specx made per sample: its lanes then read F only
             double *Bi = B + i * kRowLd;
-            Bi[k] = Bi[k] + (0. + utv);
-            Bi[3 * kKX + k] = Bi[3 * kKX + k] + (0. + vtv);
+            Bi[k] = (Bi[k] + (0. + utv)) * cj;  // (x cosgr(j): a vdspec input, scaled here for specx)
+            Bi[3 * kKX + k] = (Bi[3 * kKX + k] + (0. + vtv)) * cj;
             Bi[7 * kKX + k] = Bi[7 * kKX + k] + (ttk + ttv);
             Bi[8 * kKX + k] = Bi[8 * kKX + k] + qtk;
         }
@@ -1509,14 +1510,10 @@ __global__ __launch_bounds__(kGsThreads) void k_st_gridspec(
         const bool act = f < kNFwd;
         double x[48];
         if (act) {
-            // F (+ P already added in the sums), then x cosgr(j) (vdspec inputs)
+            // F (+ P, x cosgr(j) for the vdspec inputs: both applied where F was written)
             const double *fr = B + f + h * kRowLd;
 #pragma unroll
             for (int i = 0; i < 48; ++i) x[i] = fr[2 * i * kRowLd];
-            if (f < kNFwdScaled) {
-#pragma unroll
-                for (int i = 0; i < 48; ++i) x[i] = x[i] * cj;
-            }
             fft::rfftf48_reg(x, was);
         }
         __syncthreads();  // A's P columns are read: A becomes the pairs' meeting place
