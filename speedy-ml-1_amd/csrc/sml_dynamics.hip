@@ -1383,7 +1383,9 @@ __global__ __launch_bounds__(kGsThreads) void k_st_gridspec(
         if (tid < kPtS) ptl[tid] = rtab;
         else if (tid < kPtS + kGpS) reinterpret_cast<double *>(&gpt)[tid - kPtS] = rtab;
         __syncthreads();
-        if (act) row_gridx_half(A, xi, was, f, f >= n1, cosgr[j], h);
+        // (unscaled: the x cosgr(j) of the kcos = 2 fields [f >= n1] is applied where
+        // they are read, below -- the same multiply, off every gridx lane's chain)
+        if (act) row_gridx_half(A, xi, was, f, false, 1.0, h);
     }
     __syncthreads();
     stamp(dbg, 0, 1);
@@ -1403,8 +1405,8 @@ __global__ __launch_bounds__(kGsThreads) void k_st_gridspec(
         if (tid < kIX) {  // grid-point dynamics of column i -> F in B[i][f]
             const int i = tid;
             double dummy[kKX];
-            gridpoint_column(j, n1, [&](int f) { return A[i * kRowLd + f]; }, false, dummy, dummy, dummy, dummy,
-                             [&](int f, double v) { B[i * kRowLd + f] = v; }, &gpt, false);
+            gridpoint_column(j, n1, [&](int f) { return f >= n1 ? A[i * kRowLd + f] * cj : A[i * kRowLd + f]; }, false,
+                             dummy, dummy, dummy, dummy, [&](int f, double v) { B[i * kRowLd + f] = v; }, &gpt, false);
             // the moist / diffusion part of column i's phypar
             const double *Ai = A + i * kRowLd;
             double ta[kKX], qa[kKX], ph[kKX];
@@ -1437,8 +1439,8 @@ __global__ __launch_bounds__(kGsThreads) void k_st_gridspec(
         double ua[kKX], va[kKX], ta[kKX], qa[kKX], ph[kKX];
 #pragma unroll
         for (int k = 0; k < kKX; ++k) {
-            ua[k] = Ai[n1 + 2 * kKX + 2 + k];
-            va[k] = Ai[n1 + 3 * kKX + 2 + k];
+            ua[k] = Ai[n1 + 2 * kKX + 2 + k] * cj;
+            va[k] = Ai[n1 + 3 * kKX + 2 + k] * cj;
             ta[k] = Ai[kPT1 + k];
             qa[k] = Ai[kPQ1 + k];
             ph[k] = Ai[kPPhi1 + k];
@@ -1471,7 +1473,7 @@ __global__ __launch_bounds__(kGsThreads) void k_st_gridspec(
         for (int k = 0; k < kKX; ++k) rl_rsw[k] = rad[kRadTtRsw + (size_t)k * kNGP + pt];
         // the grid-point dynamics' products (this side has the slack)
         // (the products below kNFwdScaled are vdspec inputs: x cosgr(j) here, not in specx)
-        gridpoint_products(n1, [&](int f) { return A[i * kRowLd + f]; },
+        gridpoint_products(n1, [&](int f) { return f >= n1 ? A[i * kRowLd + f] * cj : A[i * kRowLd + f]; },
                            [&](int f, double v) { B[i * kRowLd + f] = f < kNFwdScaled ? v * cj : v; }, &gpt);
     }
     __syncthreads();
