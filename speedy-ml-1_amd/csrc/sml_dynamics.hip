@@ -1125,20 +1125,33 @@ __device__ __attribute__((always_inline)) inline void row_specx_pair(const doubl
     auto O = [&](int i) { return S[(48 + i) * kRowLd + f]; };
     const double scale = 1. / (double)kIX;
     double *o = vfm + (size_t)j * kVLs + f * 2;
-    // (Re, Im) as one 16-B store: o is 16-B aligned (even offsets throughout vfm)
-    auto out = [&](int m) {
-        double re, im;
-        fft::rfftf96_combine(E, O, m, wa, &re, &im);
+    // lane h does m = 16 h + i, i = 0..15, with the operands of its m selected per lane
+    // (the halves' different m ranges were divergent branches: each wave ran both);
+    // every m's expressions are rfftf96_combine's: E(2s-1) +- tr2, ti2 +- E(2s) with
+    // the sign taken as an exact negation, m = 0 and 24 special
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const int m0 = i, m1 = 16 + i;  // lane h = 0 / 1
+        const int s0 = m0, s1 = m1 < 24 ? m1 : 48 - m1;
+        const int m = h ? m1 : m0, sv = h ? s1 : s0;
+        if (m >= kMX) continue;  // (h = 1, i = 15)
+        const int sa = sv > 0 ? sv : 1;  // (m = 0: operands unused)
+        const double c = h ? wa[2 * (s1 > 0 ? s1 : 1) - 2] : wa[2 * (s0 > 0 ? s0 : 1) - 2];
+        const double sn = h ? wa[2 * (s1 > 0 ? s1 : 1) - 1] : wa[2 * (s0 > 0 ? s0 : 1) - 1];
+        const double e1 = E(2 * sa - 1), e2 = E(2 * sa), o1 = O(2 * sa - 1), o2 = O(2 * sa);
+        const double tr2 = c * o1 + sn * o2;
+        const double ti2 = c * o2 - sn * o1;
+        const bool lo = m < 24;
+        double re = lo ? e1 + tr2 : e1 - tr2;
+        double im = lo ? e2 + ti2 : ti2 - e2;
+        if (m == 0) {  // ch(1, 1) = cc(1, 1) + cc(1, 2); varm(2) = 0
+            re = E(0) + O(0);
+            im = 0.0;
+        } else if (m == 24) {  // ido even: ch(ido, 1) = cc(ido, 1), ch(1, 2) = -cc(ido, 2)
+            re = E(47);
+            im = -O(47);
+        }
         *reinterpret_cast<double2 *>(o + (size_t)m * kVFm) = double2{re * scale, im * scale};
-    };
-    if (h == 0) {
-        // varm(1) = fvar(1) / ix, varm(2) = 0
-        *reinterpret_cast<double2 *>(o) = double2{(E(0) + O(0)) * scale, 0.0};
-#pragma unroll
-        for (int m = 1; m <= 15; ++m) out(m);
-    } else {
-#pragma unroll
-        for (int m = 16; m <= kMX - 1; ++m) out(m);
     }
 }
 
