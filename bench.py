@@ -288,7 +288,7 @@ def main():
                 "speedy": "T30L8, 26 dyn_steps per window (nsteps 96/day, delt 900 s), physics on, "
                           "shortwave every 3rd step",
                 "streams": (f"overlapped: SPEEDY on CUs [0, {args.speedy_cus}), reservoir on CUs [{args.speedy_cus}, "
-                            f"{args.speedy_cus + min(ncu - args.speedy_cus, ncu * 5 // 8)})"
+                            f"{args.speedy_cus + (ncu - args.speedy_cus)})"
                             if args.overlap and args.speedy_cus > 0 else
                             "overlapped, no CU split" if args.overlap else "one stream"),
             },
@@ -296,8 +296,7 @@ def main():
             "finite": finite,
             "roofline": {
                 "kernel": (("k_res_readout<ml> (v_ml = W_out(:, ncs+1:) x~, GEMV, 17 rows per wave, 128-B-aligned rows; beside "
-                            + (f"SPEEDY's window on {min(ncu - args.speedy_cus, ncu * 5 // 8)} CUs of their own (less HBM pressure "
-                               "on the window than all of the rest), unpaced"
+                            + (f"SPEEDY's window on the {(ncu - args.speedy_cus)} CUs SPEEDY does not use, unpaced"
                                if args.speedy_cus > 0 else "SPEEDY's window on shared CUs, paced at 2048 waves")
                             + "; the one-pass form on all CUs: reservoir_only.roofline_unpaced)")
                            if args.overlap else

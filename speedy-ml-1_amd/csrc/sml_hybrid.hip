@@ -314,12 +314,13 @@ extern "C" int sml_hybrid_create(sml_reservoirs *res, sml_dynamics *dyn, sml_com
         void *s = nullptr, *m = nullptr;
         if (int rc = sml_stream_create_cu_range(0, speedy_cus, &s)) return bail(rc);
         h->side = (hipStream_t)s;
-        // the reservoir on CUs [speedy_cus, speedy_cus + res_cus): 5/8 of the chip by
-        // default (160 of 256).  Its begin (update + v_ml readout) still ends well
-        // inside the window, and the lower HBM pressure slows the window less
-        // (783 -> 789 steps/s vs all remaining 192 CUs).
+        // the reservoir on CUs [speedy_cus, speedy_cus + res_cus): all the CUs SPEEDY
+        // does not use by default.  With the window at 1.09 ms, 160 of the 192 were
+        // better (less HBM pressure on the window, +1 %); with the window at 0.78 ms
+        // the begin (update + v_ml readout, 0.88 ms on 160 CUs) no longer fits beside
+        // it, and 192 CUs are 2.4 % faster (same-box A/B).
         // SML_RES_CUS overrides the count.
-        int res_cus = std::min(ncu - speedy_cus, ncu * 5 / 8);
+        int res_cus = ncu - speedy_cus;
         if (const char *er = getenv("SML_RES_CUS")) res_cus = std::min(std::max(atoi(er), 1), ncu - speedy_cus);
         if (int rc = sml_stream_create_cu_range(speedy_cus, res_cus, &m)) return bail(rc);
         h->main = (hipStream_t)m;
