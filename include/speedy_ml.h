@@ -427,8 +427,19 @@ typedef struct sml_comm sml_comm;
 int sml_comm_unique_id(unsigned char *id128);
 int sml_comm_create(int world, int rank, const unsigned char *id128, sml_comm **out);
 int sml_comm_create_file(int world, int rank, const char *path, int timeout_s, sml_comm **out);
+/* a rank descriptor without a transport (no RCCL communicator): rank `rank` of
+ * `world` for sml_hybrid_create when the host moves the outvec slabs itself and
+ * advances with sml_hybrid_advance_slabs; sml_comm_allgather and sml_hybrid_step
+ * refuse it (SML_ERR_STATE) */
+int sml_comm_create_local(int world, int rank, sml_comm **out);
 int sml_comm_destroy(sml_comm *c);
 int sml_comm_rank(const sml_comm *c, int *world, int *rank);
+/* the all-gather's layout for `world` ranks of processor_decomposition
+ * (src/res_domain.f90:31-62): each rank's outvecs zero-padded to the largest share
+ * *maxc, received as [world][maxc][nout]; *contiguous = 1 when that is already global
+ * region order (even shares); perm[numregions] (may be NULL) = the slab row of each
+ * region.  Host only. */
+int sml_exchange_plan(int numregions, int world, int *maxc, int *contiguous, int32_t *perm);
 /* all-gather of equal slabs of `count` doubles: d_recv[world][count] (ncclAllGather) --
  * the outvec exchange that replaces sendrecievegrid's point-to-point gather/scatter
  * (src/mpires.f90:338-716) */
@@ -482,9 +493,26 @@ int sml_hybrid_start(sml_hybrid *h, const double *d_grid4d, const double *d_grid
  * global region order ([numregions][nout]) */
 int sml_hybrid_predict(sml_hybrid *h);
 int sml_hybrid_advance(sml_hybrid *h, const double *d_outvec_all);
+/* advance from the all-gather's output d_recv[world][maxc][nout] (sml_exchange_plan;
+ * rank q's rows zero-padded to maxc): permuted into global region order when the
+ * shares are uneven, then sml_hybrid_advance.  Replaces the root's receive loop
+ * and assembly of sendrecievegrid (src/mpires.f90:389-442). */
+int sml_hybrid_advance_slabs(sml_hybrid *h, const double *d_recv);
 /* predict + the loop's own exchange (identity on one rank, sml_comm_allgather
- * otherwise) + advance; asynchronous */
+ * otherwise) + advance_slabs; asynchronous */
 int sml_hybrid_step(sml_hybrid *h);
+/* the two cross-stream dependencies of the overlapped loop: SML_HOP_WAIT_VALUE (a
+ * sequence number written by the producer's stream, waited for by the consumer's:
+ * 3.9 us), SML_HOP_EVENTS (event record + wait: 10 us), or SML_HOP_AUTO (the
+ * default: wait-value, but events when dispatch is serialised -- AMD_SERIALIZE_KERNEL
+ * or rocprofv3's counter collection -- where a wait-value packet could stall its
+ * queue ahead of its producer; SML_HYBRID_EVENTS=1 also selects events).  Drains both
+ * streams before switching. */
+#define SML_HOP_AUTO 0
+#define SML_HOP_WAIT_VALUE 1
+#define SML_HOP_EVENTS 2
+int sml_hybrid_set_hop_mode(sml_hybrid *h, int mode);
+int sml_hybrid_hop_mode(const sml_hybrid *h, int *requested, int *effective);
 /* run_speedy of the last step (0: the reference ends the prediction,
  * parallelmain.f90:268-270); waits only for that step's safety check */
 int sml_hybrid_run_speedy(sml_hybrid *h, int *run);

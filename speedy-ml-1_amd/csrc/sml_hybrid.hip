@@ -56,12 +56,15 @@ struct sml_hybrid {
     // side, lm_t: side -> main): a sequence number in device memory that the
     // producer's stream writes and the consumer's waits for (CP stream memory
     // operations: 3.9 us from the producer's end to the consumer's start on gfx950,
-    // 10 us for an event record + wait; tools/probe_hop.hip).  SML_HYBRID_EVENTS=1
-    // keeps events.
+    // 10 us for an event record + wait; tools/probe_hop.hip).  A wait-value packet
+    // blocks its queue until the producer's write lands, so under serialised dispatch
+    // (rocprofv3 counter passes, AMD_SERIALIZE_KERNEL) it can stall ahead of that
+    // producer: SML_HOP_AUTO then takes event hops (sml_hybrid_set_hop_mode).
     enum { kHopGrid = 0, kHopLm = 1 };
     hipEvent_t ev[2] = {nullptr, nullptr};
     uint64_t *d_seq = nullptr, seq[2] = {0, 0};
     bool use_events = false;
+    int hop_mode = SML_HOP_AUTO;
     // caller-owned device buffers
     double *fb = nullptr, *lm = nullptr, *ov = nullptr, *g4 = nullptr, *g2 = nullptr, *pr = nullptr, *f4 = nullptr,
            *f2 = nullptr;
@@ -91,7 +94,8 @@ const char *nccl_msg(ncclResult_t r) { return ncclGetErrorString(r); }
         if (r_ != ncclSuccess) return ::sml::fail(SML_ERR_HIP, "%s:%d %s: %s", __FILE__, __LINE__, #expr, nccl_msg(r_)); \
     } while (0)
 
-// global region order from the all-gather's [rank][maxc] slabs
+// global region order from the all-gather's [rank][maxc] slabs: glob row r = slab row
+// perm[r] (sml_exchange_plan)
 __global__ void k_gather_rows(const double *__restrict__ recv, const int32_t *__restrict__ perm,
                               double *__restrict__ glob, int nout, int total) {
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
@@ -101,6 +105,38 @@ __global__ void k_gather_rows(const double *__restrict__ recv, const int32_t *__
 }
 
 }  // namespace
+
+// ------------------------------------------------------------- exchange plan
+// The all-gather's layout for `world` ranks of processor_decomposition
+// (res_domain.f90:31-62): every rank sends its outvecs zero-padded to the largest
+// share maxc, so the receive buffer is [world][maxc][nout]; region r (0-based) sits
+// at slab row perm[r] = rank * maxc + (position of r in the rank's list).  With even
+// shares (numregions % world == 0) the slabs are already global region order
+// (*contiguous = 1); else rank q in 1..left also owns region numregions - left + q - 1
+// at the end of its list and k_gather_rows applies perm.  perm may be NULL.
+extern "C" int sml_exchange_plan(int numregions, int world, int *maxc, int *contiguous, int32_t *perm) {
+    SML_REQUIRE(numregions > 0 && world >= 1 && world <= numregions && maxc && contiguous, "bad argument");
+    std::vector<int> all(numregions);
+    int mc = 0, c0 = -1;
+    bool contig = true;
+    for (int r = 0; r < world; ++r) mc = std::max(mc, processor_regions(numregions, world, r, all.data()));
+    std::vector<int32_t> p(numregions, -1);
+    for (int r = 0; r < world; ++r) {
+        const int c = processor_regions(numregions, world, r, all.data());
+        if (c0 < 0) c0 = c;
+        if (c != c0) contig = false;
+        for (int i = 0; i < c; ++i) {
+            SML_REQUIRE(p[all[i]] < 0, "region %d owned twice", all[i]);
+            p[all[i]] = r * mc + i;
+            if (all[i] != r * c0 + i) contig = false;
+        }
+    }
+    for (int r = 0; r < numregions; ++r) SML_REQUIRE(p[r] >= 0, "region %d owned by no rank", r);
+    *maxc = mc;
+    *contiguous = contig ? 1 : 0;
+    if (perm) std::memcpy(perm, p.data(), sizeof(int32_t) * numregions);
+    return SML_OK;
+}
 
 // ---------------------------------------------------------------- communicator
 extern "C" int sml_comm_unique_id(unsigned char *id) {
@@ -159,6 +195,19 @@ extern "C" int sml_comm_create_file(int world, int rank, const char *path, int t
     return sml_comm_create(world, rank, id, out);
 }
 
+// a rank descriptor without a transport: world and rank for sml_hybrid_create when
+// the host moves the outvec slabs itself (sml_hybrid_advance_slabs)
+extern "C" int sml_comm_create_local(int world, int rank, sml_comm **out) {
+    SML_REQUIRE(out && world >= 1 && rank >= 0 && rank < world, "bad argument");
+    *out = nullptr;
+    sml_comm *c = new (std::nothrow) sml_comm();
+    if (!c) return fail(SML_ERR_NOMEM, "host allocation failed");
+    c->world = world;
+    c->rank = rank;
+    *out = c;
+    return SML_OK;
+}
+
 extern "C" int sml_comm_destroy(sml_comm *c) {
     if (!c) return SML_OK;
     if (c->comm) (void)ncclCommDestroy(c->comm);
@@ -175,6 +224,7 @@ extern "C" int sml_comm_rank(const sml_comm *c, int *world, int *rank) {
 
 extern "C" int sml_comm_allgather(sml_comm *c, const double *d_send, double *d_recv, int64_t count, void *stream) {
     SML_REQUIRE(c && d_send && d_recv && count >= 0, "bad argument");
+    if (!c->comm) return fail(SML_ERR_STATE, "rank %d of %d is a local descriptor without a transport", c->rank, c->world);
     SML_NCCL(ncclAllGather(d_send, d_recv, (size_t)count, ncclDouble, c->comm, (hipStream_t)stream));
     return SML_OK;
 }
@@ -253,7 +303,41 @@ int hop_wait(sml_hybrid *h, int k, hipStream_t s) {
     return SML_OK;
 }
 
+// dispatch serialised by the runtime or a profiler: the HIP runtime's
+// AMD_SERIALIZE_KERNEL, rocprofv3's counter collection (ROCPROF_COUNTER_COLLECTION,
+// set by `rocprofv3 --pmc` / `-i`)
+bool env_on(const char *name) {
+    const char *e = getenv(name);
+    return e && *e && std::strcmp(e, "0") != 0 && std::strcmp(e, "false") != 0 && std::strcmp(e, "False") != 0;
+}
+
+bool dispatch_serialised() { return env_on("AMD_SERIALIZE_KERNEL") || env_on("ROCPROF_COUNTER_COLLECTION"); }
+
 }  // namespace
+
+// hop mode: SML_HOP_AUTO (wait-value hops unless dispatch is serialised or
+// SML_HYBRID_EVENTS=1), SML_HOP_WAIT_VALUE, SML_HOP_EVENTS.  Both streams are drained
+// first, so no wait of one kind is left pending on a signal of the other.
+extern "C" int sml_hybrid_set_hop_mode(sml_hybrid *h, int mode) {
+    SML_REQUIRE(h && (mode == SML_HOP_AUTO || mode == SML_HOP_WAIT_VALUE || mode == SML_HOP_EVENTS),
+                "bad hop mode %d", mode);
+    if (h->main) SML_HIP(hipStreamSynchronize(h->main));
+    if (h->side && h->side != h->main) SML_HIP(hipStreamSynchronize(h->side));
+    h->hop_mode = mode;
+    if (mode == SML_HOP_AUTO)
+        h->use_events = env_on("SML_HYBRID_EVENTS") || dispatch_serialised();
+    else
+        h->use_events = mode == SML_HOP_EVENTS;
+    return SML_OK;
+}
+
+// the requested mode and the one in effect (SML_HOP_WAIT_VALUE or SML_HOP_EVENTS)
+extern "C" int sml_hybrid_hop_mode(const sml_hybrid *h, int *requested, int *effective) {
+    SML_REQUIRE(h, "null context");
+    if (requested) *requested = h->hop_mode;
+    if (effective) *effective = h->use_events ? SML_HOP_EVENTS : SML_HOP_WAIT_VALUE;
+    return SML_OK;
+}
 
 extern "C" int sml_hybrid_destroy(sml_hybrid *h) {
     if (!h) return SML_OK;
@@ -347,32 +431,22 @@ extern "C" int sml_hybrid_create(sml_reservoirs *res, sml_dynamics *dyn, sml_com
     if (hipEventCreateWithFlags(&h->ev[0], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&h->ev[1], hipEventDisableTiming) != hipSuccess)
         return bail(fail(SML_ERR_HIP, "event"));
-    if (const char *e = getenv("SML_HYBRID_EVENTS")) h->use_events = atoi(e) != 0;
+    if (int rc = sml_hybrid_set_hop_mode(h, SML_HOP_AUTO)) return bail(rc);
     if (hipMalloc(&h->d_seq, 2 * sizeof(uint64_t)) != hipSuccess ||
         hipMemset(h->d_seq, 0, 2 * sizeof(uint64_t)) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
         return bail(fail(SML_ERR_HIP, "sequence counters"));
     if (world > 1) {
-        std::vector<int> all(h->numregions);
-        std::vector<int32_t> perm(h->numregions, -1);
-        h->maxc = 0;
-        std::vector<int> counts(world);
-        for (int r = 0; r < world; ++r) {
-            counts[r] = processor_regions(h->numregions, world, r, all.data());
-            h->maxc = std::max(h->maxc, counts[r]);
-        }
-        h->contiguous = true;
-        for (int r = 0; r < world; ++r) {
-            const int c = processor_regions(h->numregions, world, r, all.data());
-            if (c != counts[0]) h->contiguous = false;
-            for (int i = 0; i < c; ++i) {
-                perm[all[i]] = r * h->maxc + i;
-                if (all[i] != r * counts[0] + i) h->contiguous = false;
-            }
-        }
+        std::vector<int32_t> perm(h->numregions);
+        int contig = 1;
+        if (int rc = sml_exchange_plan(h->numregions, world, &h->maxc, &contig, perm.data())) return bail(rc);
+        h->contiguous = contig != 0;
         const size_t nout = h->nout;
-        if (hipMalloc(&h->d_send, (size_t)h->maxc * nout * 8) != hipSuccess ||
-            hipMalloc(&h->d_recv, (size_t)world * h->maxc * nout * 8) != hipSuccess ||
-            hipMemset(h->d_send, 0, (size_t)h->maxc * nout * 8) != hipSuccess)
+        // the staging buffers of the loop's own all-gather (a transport-less rank
+        // descriptor gets its slabs from the host: sml_hybrid_advance_slabs)
+        if (comm->comm &&
+            (hipMalloc(&h->d_send, (size_t)h->maxc * nout * 8) != hipSuccess ||
+             hipMalloc(&h->d_recv, (size_t)world * h->maxc * nout * 8) != hipSuccess ||
+             hipMemset(h->d_send, 0, (size_t)h->maxc * nout * 8) != hipSuccess))
             return bail(fail(SML_ERR_NOMEM, "exchange buffers"));
         if (!h->contiguous) {
             if (hipMalloc(&h->d_glob, (size_t)h->numregions * nout * 8) != hipSuccess ||
@@ -507,37 +581,44 @@ extern "C" int sml_hybrid_advance(sml_hybrid *h, const double *d_outvec_all) {
     return SML_OK;
 }
 
+// advance from the all-gather's output d_recv[world][maxc][nout] (sml_exchange_plan):
+// the slabs are global region order with even shares, else k_gather_rows permutes
+// them into it first (on the main stream)
+extern "C" int sml_hybrid_advance_slabs(sml_hybrid *h, const double *d_recv) {
+    SML_REQUIRE(h && d_recv, "null argument");
+    const int world = h->comm ? h->comm->world : 1;
+    if (world == 1 || h->contiguous) return sml_hybrid_advance(h, d_recv);
+    if (!h->predicted) return fail(SML_ERR_STATE, "sml_hybrid_advance_slabs without sml_hybrid_predict");
+    const int total = h->numregions * h->nout;
+    hipLaunchKernelGGL(k_gather_rows, dim3((total + 255) / 256), dim3(256), 0, h->main, d_recv, h->d_perm, h->d_glob,
+                       h->nout, total);
+    SML_HIP(hipGetLastError());
+    return sml_hybrid_advance(h, h->d_glob);
+}
+
 // one hybrid step with the loop's own exchange: identity on one rank, else the
 // all-gather of every rank's outvec slab (RCCL over xGMI) on the main stream
 extern "C" int sml_hybrid_step(sml_hybrid *h) {
     SML_REQUIRE(h, "null context");
-    if (int rc = sml_hybrid_predict(h)) return rc;
     const int world = h->comm ? h->comm->world : 1;
-    if (world == 1) {
-        if (h->nlocal != h->numregions)
-            return fail(SML_ERR_STATE, "one rank holds %d of %d regions: exchange through sml_hybrid_advance",
-                        h->nlocal, h->numregions);
-        return sml_hybrid_advance(h, h->ov);
-    }
-    const size_t slab = (size_t)h->maxc * h->nout;
+    if (world == 1 && h->nlocal != h->numregions)
+        return fail(SML_ERR_STATE, "one rank holds %d of %d regions: exchange through sml_hybrid_advance",
+                    h->nlocal, h->numregions);
+    if (world > 1 && !h->comm->comm)
+        return fail(SML_ERR_STATE, "rank %d of %d has no transport: exchange through sml_hybrid_advance_slabs",
+                    h->comm->rank, world);
+    if (int rc = sml_hybrid_predict(h)) return rc;
+    if (world == 1) return sml_hybrid_advance(h, h->ov);
     // even shares (1152 / N for N = 1, 2, 4, 8): the outvecs go out of ov as they are;
     // uneven ones are padded to the largest share through d_send (one copy more on the
-    // critical path)
+    // critical path; d_send's padding rows stay zero)
     const double *send = h->ov;
     if (h->nlocal != h->maxc) {
         SML_HIP(hipMemcpyAsync(h->d_send, h->ov, (size_t)h->nlocal * h->nout * 8, hipMemcpyDeviceToDevice, h->main));
         send = h->d_send;
     }
-    if (int rc = sml_comm_allgather(h->comm, send, h->d_recv, (int64_t)slab, h->main)) return rc;
-    const double *glob = h->d_recv;
-    if (!h->contiguous) {
-        const int total = h->numregions * h->nout;
-        hipLaunchKernelGGL(k_gather_rows, dim3((total + 255) / 256), dim3(256), 0, h->main, h->d_recv, h->d_perm,
-                           h->d_glob, h->nout, total);
-        SML_HIP(hipGetLastError());
-        glob = h->d_glob;
-    }
-    return sml_hybrid_advance(h, glob);
+    if (int rc = sml_comm_allgather(h->comm, send, h->d_recv, (int64_t)h->maxc * h->nout, h->main)) return rc;
+    return sml_hybrid_advance_slabs(h, h->d_recv);
 }
 
 // run_speedy after the last advance (mpires.f90:721, :1623): 0 ends the prediction

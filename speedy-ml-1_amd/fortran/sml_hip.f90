@@ -390,6 +390,41 @@ module sml_hip
       type(c_ptr), value :: h
       integer(c_int) :: rc
     end function
+    !> advance from the host's all-gather output d_recv(nout, maxc, world)
+    function sml_hybrid_advance_slabs(h, d_recv) bind(C, name='sml_hybrid_advance_slabs') result(rc)
+      import :: c_ptr, c_int
+      type(c_ptr), value :: h, d_recv
+      integer(c_int) :: rc
+    end function
+    !> cross-stream hops: 0 auto, 1 wait-value, 2 events
+    function sml_hybrid_set_hop_mode(h, mode) bind(C, name='sml_hybrid_set_hop_mode') result(rc)
+      import :: c_ptr, c_int
+      type(c_ptr), value :: h
+      integer(c_int), value :: mode
+      integer(c_int) :: rc
+    end function
+    function sml_hybrid_hop_mode(h, requested, effective) bind(C, name='sml_hybrid_hop_mode') result(rc)
+      import :: c_ptr, c_int
+      type(c_ptr), value :: h
+      integer(c_int), intent(out) :: requested, effective
+      integer(c_int) :: rc
+    end function
+    !> rank descriptor without a transport (the host moves the slabs)
+    function sml_comm_create_local(world, rank, comm) bind(C, name='sml_comm_create_local') result(rc)
+      import :: c_ptr, c_int
+      integer(c_int), value :: world, rank
+      type(c_ptr), intent(out) :: comm
+      integer(c_int) :: rc
+    end function
+    !> the all-gather's layout: maxc, contiguous, perm(numregions) (0-based slab rows)
+    function sml_exchange_plan(numregions, world, maxc, contiguous, perm) bind(C, name='sml_exchange_plan') &
+        result(rc)
+      import :: c_int
+      integer(c_int), value :: numregions, world
+      integer(c_int), intent(out) :: maxc, contiguous
+      integer(c_int), intent(out) :: perm(*)
+      integer(c_int) :: rc
+    end function
 
     ! ------------------------------------------------------------ host plumbing
     function sml_device_alloc(bytes, d_ptr) bind(C, name='sml_device_alloc') result(rc)

@@ -51,7 +51,11 @@ EXPORTED = (
     "sml_device_alloc", "sml_device_free", "sml_copy_to_device", "sml_copy_to_host", "sml_region_geometry",
     "sml_processor_decomposition", "sml_hybrid_set_tisr_table", "sml_tisr_date_index", "sml_res_tile_tisr_field",
     "sml_res_create_generic", "sml_res_step_slab", "sml_res_start_prediction",
+    "sml_comm_create_local", "sml_exchange_plan", "sml_hybrid_advance_slabs", "sml_hybrid_set_hop_mode",
+    "sml_hybrid_hop_mode",
 )
+
+SML_HOP_AUTO, SML_HOP_WAIT_VALUE, SML_HOP_EVENTS = 0, 1, 2
 
 
 class SmlError(RuntimeError):
@@ -200,6 +204,11 @@ def _declare(L: ctypes.CDLL) -> None:
         "sml_res_create_generic": [i, i, vp, vp, vp, vp, i, i, vp, i, d, pp],
         "sml_res_step_slab": [vp, vp, vp, vp, vp, vp],
         "sml_res_start_prediction": [vp, vp, i, ctypes.c_int64, vp, vp],
+        "sml_comm_create_local": [i, i, pp],
+        "sml_exchange_plan": [i, i, ip, ip, vp],
+        "sml_hybrid_advance_slabs": [vp, vp],
+        "sml_hybrid_set_hop_mode": [vp, i],
+        "sml_hybrid_hop_mode": [vp, ip, ip],
     }
     for name, args in sig.items():
         fn = getattr(L, name)

@@ -44,3 +44,44 @@ class NativeComm:
             self.close()
         except Exception:
             pass
+
+
+class LocalRank:
+    """Rank `rank` of `world` without a transport (sml_comm_create_local): a
+    HybridLoop created with it predicts its share of processor_decomposition and
+    advances from slabs the host gathered itself (HybridLoop.advance_slabs) -- the
+    sharded path without RCCL, e.g. every rank of an N-rank decomposition on one GPU."""
+
+    def __init__(self, world: int, rank: int):
+        h = ctypes.c_void_p()
+        check(lib().sml_comm_create_local(world, rank, ctypes.byref(h)))
+        self._h = h
+        self.world, self.rank = world, rank
+
+    @property
+    def handle(self):
+        return self._h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            check(lib().sml_comm_destroy(self._h))
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def exchange_plan(numregions: int, world: int):
+    """sml_exchange_plan: (maxc, contiguous, perm) of the all-gather's [world][maxc]
+    slabs; perm[r] = the slab row of region r."""
+    import numpy as np
+
+    from ._lib import ptr
+
+    maxc, contig = ctypes.c_int(), ctypes.c_int()
+    perm = np.zeros(numregions, dtype=np.int32)
+    check(lib().sml_exchange_plan(numregions, world, ctypes.byref(maxc), ctypes.byref(contig), ptr(perm)))
+    return maxc.value, bool(contig.value), perm

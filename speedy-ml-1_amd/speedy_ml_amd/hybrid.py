@@ -105,13 +105,33 @@ class HybridLoop:
         NativeComm (speedy_ml_amd.comm) the whole step is native, its all-gather on
         the main stream (sml_hybrid_step); else `exchange` runs between predict and
         advance."""
-        if self.comm is not None:
+        if self.comm is not None:  # a LocalRank at world > 1 is refused: no transport
             check(lib().sml_hybrid_step(self._h))
             return
         check(lib().sml_hybrid_predict(self._h))
         with torch.cuda.stream(self.main):
             glob = self.exchange(self.ov)  # RCCL all-gather over xGMI when world > 1
         check(lib().sml_hybrid_advance(self._h, ptr(glob)))
+
+    def predict(self):
+        """First half of a step: this rank's outvecs into `ov` (main stream)."""
+        check(lib().sml_hybrid_predict(self._h))
+
+    def advance_slabs(self, recv):
+        """Second half from an all-gather's output recv [world * maxc, nout] (device;
+        every rank's `ov` zero-padded to maxc, comm.exchange_plan), permuted into
+        region order when the shares are uneven (sml_hybrid_advance_slabs)."""
+        check(lib().sml_hybrid_advance_slabs(self._h, ptr(recv)))
+
+    def set_hop_mode(self, mode: int):
+        """SML_HOP_AUTO / SML_HOP_WAIT_VALUE / SML_HOP_EVENTS (include/speedy_ml.h)."""
+        check(lib().sml_hybrid_set_hop_mode(self._h, int(mode)))
+
+    def hop_mode(self):
+        """(requested, effective) hop mode."""
+        a, b = ctypes.c_int(), ctypes.c_int()
+        check(lib().sml_hybrid_hop_mode(self._h, ctypes.byref(a), ctypes.byref(b)))
+        return a.value, b.value
 
     def run_speedy(self) -> bool:
         """run_speedy of the last step: False when its window entry failed iogrid(30)'s

@@ -258,3 +258,50 @@ def test_tisr_by_date_from_a_table(cuda):
             got = fb[o[r + 1] - len(pts):o[r + 1]]
             np.testing.assert_array_equal(got, want, err_msg=f"region {r} step {t}")
     loop.close()
+
+
+def test_serialised_dispatch_takes_event_hops(cuda, tmp_path):
+    """Under serialised dispatch (AMD_SERIALIZE_KERNEL=3 here; rocprofv3's counter
+    passes alike) a wait-value hop could block its queue ahead of its producer:
+    SML_HOP_AUTO then takes event hops.  A fresh child process with serialisation
+    forced runs 3 steps within its time limit and is bitwise the default loop; an
+    explicit SML_HOP_EVENTS loop in this process is bitwise the default too."""
+    import os
+    import subprocess
+    import sys
+
+    import torch
+
+    from speedy_ml_amd._lib import SML_HOP_AUTO, SML_HOP_EVENTS, SML_HOP_WAIT_VALUE
+
+    out = str(tmp_path / "hop.npz")
+    env = dict(os.environ, AMD_SERIALIZE_KERNEL="3")
+    env.pop("SML_HYBRID_EVENTS", None)
+    child = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_hop_child.py")
+    p = subprocess.run([sys.executable, "-u", child, out], env=env, timeout=100, capture_output=True, text=True)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-2000:]
+    got = dict(np.load(out))
+    assert int(got["requested"]) == SML_HOP_AUTO and int(got["effective"]) == SML_HOP_EVENTS
+
+    runs = []
+    for mode in (None, SML_HOP_EVENTS):
+        loop, _ = _loop(cuda, True)
+        if mode is None:
+            assert loop.hop_mode() == (SML_HOP_AUTO, SML_HOP_WAIT_VALUE)
+        else:
+            loop.set_hop_mode(mode)
+            assert loop.hop_mode() == (mode, SML_HOP_EVENTS)
+        snaps = {}
+        for s in range(3):
+            loop.step()
+            loop.sync()
+            for k, v in _snapshot(loop).items():
+                snaps[f"{k}{s}"] = v
+        runs.append(snaps)
+        loop.close()
+        loop.dyn.close()
+        loop.res.close()
+        torch.cuda.synchronize()
+    for k in runs[0]:
+        np.testing.assert_array_equal(runs[1][k], runs[0][k], err_msg="events vs wait-value " + k)
+        np.testing.assert_array_equal(got[k], runs[0][k], err_msg="serialised child vs default " + k)
