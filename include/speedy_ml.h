@@ -479,6 +479,15 @@ int sml_hybrid_set_tisr_table(sml_hybrid *h, const double *d_table, int nhours, 
  * src/mod_calendar.f90:24-175, wrapped past 8760 as get_tisr_by_date does); *feb29
  * carries the SAVEd February of the reference's month table (0 at the start) */
 int sml_tisr_date_index(int startyear, int64_t hours_elapsed, int *feb29, int *index);
+/* get_current_time_delta_hour (src/mod_calendar.f90:24-92): date[4] = current year,
+ * month, day, hour after hours_elapsed hours from Jan 1 00 of startyear, with the same
+ * SAVEd-February latch *feb29.  Host only. */
+int sml_calendar_delta_hour(int startyear, int64_t hours_elapsed, int *feb29, int *date);
+/* the loop's copy of that latch (set_tisr_table resets it to 0): a host whose own
+ * calendar calls already met a leap year sets 1, as the reference's process-wide
+ * SAVEd table would hold (mod_reservoir.f90:355/632/638, mpires.f90:108/489) */
+int sml_hybrid_set_feb29(sml_hybrid *h, int feb29);
+int sml_hybrid_get_feb29(const sml_hybrid *h, int *feb29);
 /* the tisr entries of every local region's feedback from one hour's global tisr
  * field d_tisr_grid(96, 48): overlap tile, (x - mean(34)) / std(34) */
 int sml_res_tile_tisr_field(sml_reservoirs *c, const double *d_tisr_grid, double *d_feedback, void *stream);

@@ -243,8 +243,10 @@ namespace {
 bool leap_year(int y) { return (y % 4 == 0 && y % 100 != 0) || y % 400 == 0; }  // leap_year_check :94-106
 }  // namespace
 
-extern "C" int sml_tisr_date_index(int startyear, int64_t hours_elapsed, int *feb29, int *index) {
-    SML_REQUIRE(feb29 && index && hours_elapsed >= 0, "bad argument");
+// get_current_time_delta_hour (mod_calendar.f90:24-92): date[4] = currentyear,
+// currentmonth, currentday, currenthour after hours_elapsed hours from startyear
+extern "C" int sml_calendar_delta_hour(int startyear, int64_t hours_elapsed, int *feb29, int *date) {
+    SML_REQUIRE(feb29 && date && hours_elapsed >= 0, "bad argument");
     const int64_t hours_in_year = 8760, hours_in_a_day = 24;
     const int64_t years = hours_elapsed / hours_in_year;
     int year = (int)(years + startyear);
@@ -265,8 +267,18 @@ extern "C" int sml_tisr_date_index(int startyear, int64_t hours_elapsed, int *fe
         month = 12;
         year -= 1;
     }
-    const int day = (int)(ncal[month - 1] + counter);
-    const int hour = (int)(hours_elapsed % hours_in_a_day);
+    date[0] = year;
+    date[1] = month;
+    date[2] = (int)(ncal[month - 1] + counter);
+    date[3] = (int)(hours_elapsed % hours_in_a_day);
+    return SML_OK;
+}
+
+extern "C" int sml_tisr_date_index(int startyear, int64_t hours_elapsed, int *feb29, int *index) {
+    SML_REQUIRE(feb29 && index && hours_elapsed >= 0, "bad argument");
+    int d[4];
+    if (int rc = sml_calendar_delta_hour(startyear, hours_elapsed, feb29, d)) return rc;
+    const int year = d[0], month = d[1], day = d[2], hour = d[3];
     // numof_hours_into_year(year, month, day, hour) with the year's own leap table
     const bool ly = leap_year(year);
     const int nmon[12] = {31, ly ? 29 : 28, 31, 30, 31, 30, 31, 31, 30, 31, 30, 31};
@@ -493,6 +505,24 @@ extern "C" int sml_hybrid_set_tisr_table(sml_hybrid *h, const double *d_table, i
     h->tisr_step_hours = step_hours;
     h->tisr_feb29 = 0;
     h->t = 0;
+    return SML_OK;
+}
+
+// the SAVEd February of the reference's month table (mod_calendar.f90:40,61-63) as
+// the host's own calendar calls left it: every get_current_time_delta_hour of the
+// process shares it (training windows mod_reservoir.f90:355/632/638, the prediction
+// start mpires.f90:108/489, run_model :1545), so a host that met a leap year before
+// the loop's first tisr lookup passes 1 here.  sml_hybrid_set_tisr_table resets it
+// to 0 (a process whose calendar has not met a leap year).
+extern "C" int sml_hybrid_set_feb29(sml_hybrid *h, int feb29) {
+    SML_REQUIRE(h, "null context");
+    h->tisr_feb29 = feb29 != 0;
+    return SML_OK;
+}
+
+extern "C" int sml_hybrid_get_feb29(const sml_hybrid *h, int *feb29) {
+    SML_REQUIRE(h && feb29, "null argument");
+    *feb29 = h->tisr_feb29;
     return SML_OK;
 }
 

@@ -339,6 +339,12 @@ module sml_hip
       type(c_ptr), intent(out) :: comm
       integer(c_int) :: rc
     end function
+    function sml_comm_rank(comm, world, rank) bind(C, name='sml_comm_rank') result(rc)
+      import :: c_ptr, c_int
+      type(c_ptr), value :: comm
+      integer(c_int), intent(out) :: world, rank
+      integer(c_int) :: rc
+    end function
     function sml_comm_destroy(comm) bind(C, name='sml_comm_destroy') result(rc)
       import :: c_ptr, c_int
       type(c_ptr), value :: comm

@@ -11,6 +11,7 @@ program sml_interface_check
   use iso_c_binding
   use sml_hip
   use speedy_res_interface
+  use mpires, only: set_world
   implicit none
   character(len=1024) :: dir
   integer :: u, i, j
@@ -26,7 +27,13 @@ program sml_interface_check
 
   call get_command_argument(1, dir)
   mp%number_of_regions = 1152
-  call startspeedy(mp, grid, .true.)   ! region 0 (irank 0), GPU SPEEDY context
+  mp%overlap = 1
+  grid%num_vert_levels = 1
+  grid%vert_overlap = 0
+  ! the reference's startspeedy decomposes by the MPI world: with 1152 ranks, rank r
+  ! gets region r's extents (speedy_res_interface.f90:36)
+  call set_world(1152, 0)
+  call startspeedy(mp, grid, .true.)   ! region 0 (rank 0), GPU SPEEDY context
   allocate (vor(31 * 32 * 16), div(31 * 32 * 16), tt(31 * 32 * 16), tr(31 * 32 * 16), ps(31 * 32 * 2))
   allocate (phis(31 * 32), tcorh(31 * 32), qcorh(31 * 32), bc(4608 * 15))
   open (newunit=u, file=trim(dir) // '/speedy.bin', access='stream', form='unformatted', status='old')
@@ -48,7 +55,7 @@ program sml_interface_check
   tfield = truncate_letkf_code_version(field, int(trunc_twn))
   allocate (ext(12, nreg))
   do i = 1, nreg
-    mp%irank = regions(i)
+    call set_world(1152, int(regions(i)))
     call startspeedy(mp, grid, .false.)
     ext(:, i) = real([grid%res_xstart, grid%res_xend, grid%res_ystart, grid%res_yend, grid%resxchunk, &
                       grid%resychunk, grid%input_xstart, grid%input_xend, grid%input_ystart, grid%input_yend, &
@@ -60,4 +67,7 @@ program sml_interface_check
   close (u)
   j = calendar%currentyear
   print '(a,i0)', 'sml_interface_check ok, calendar year ', j
+  print '(a,4(1x,i0),a,4(1x,i0))', 'calendar', calendar%currentyear, calendar%currentmonth, calendar%currentday, &
+    calendar%currenthour, ' state', internal_state_vector%iyear0, internal_state_vector%imont0, &
+    internal_state_vector%iday, internal_state_vector%ihour
 end program

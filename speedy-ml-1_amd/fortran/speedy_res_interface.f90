@@ -15,150 +15,70 @@
 !>   truncate_letkf_code_version(field_orig, trunc_twn)    :817-837
 !>   internal_state_vector (module variable)               :17
 !>
-!> The derived types are the subsets of mod_utilities' types these routines touch
-!> (mod_utilities.f90:32-604).  What differs, and why:
-!>   * startspeedy does initializedomain + initialize_calendar as the reference, and
-!>     when runspeedy is set also creates the GPU SPEEDY context (speedy_gpu): the
-!>     device tables that agcm_init rebuilt every window are built once here.
+!> The derived types are mod_utilities' own (fortran/mod_utilities.f90: the
+!> reference's type, component and kind names), and the calendar is mod_calendar's,
+!> so the reference's callers compile against this module unchanged.  Like the
+!> reference module this one is all public: it re-exports the types it uses.
+!> What differs, and why:
+!>   * startspeedy does initializedomain(mpi_res%numprocs, mpi_res%proc_num, ...) +
+!>     initialize_calendar as the reference (:36-38; mpi_res from module mpires,
+!>     which the host fills from its communicator), with vert_level = 1 where the
+!>     reference passes an unset local, and when runspeedy is set also creates the
+!>     GPU SPEEDY context (speedy_gpu): the device tables that agcm_init rebuilt every
+!>     window are built once here.
 !>   * test_hybrid_speedy_component starts from internal_state_vector (the
-!>     reference reads one ERA-5 file from /scratch, absent here) and runs the
-!>     window loop through run_model on the GPU (sml_dyn_run_model) with the
-!>     reference's clips; hybrid_test_windows (default 500, as the reference's loop)
-!>     sets its length.  Its netCDF write of each window is not reproduced.
+!>     reference reads one ERA-5 file from /scratch, absent here), advances the
+!>     calendar and the state's date fields per window as the reference (:778,
+!>     :791-800) and runs the window loop through run_model on the GPU
+!>     (sml_dyn_run_model) with the reference's clips; hybrid_test_windows (default
+!>     500, as the reference's loop) sets its length.  Its netCDF write of each
+!>     window is not reproduced, and the date's boundary fields (fordate: the
+!>     coupler, out of scope) are the host's, set through sml_dyn_set_physics.
 !>   * The ERA / SPEEDY-state readers need the ERA-5 and SPEEDY_STATES netCDF-4
 !>     files (parallel HDF5 via MPI-IO) of the reference's /scratch tree; no such
 !>     files or library exist on this path, so they stop with a message naming the
 !>     file they would open, as nc_check stops on a missing file (mod_io.f90:1732-1744).
 !>   * write_restart_new and getspeedyvariable keep the reference's bodies (its
-!>     write is commented out; getspeedyvariable prints the step every `stride`).
+!>     write is commented out; getspeedyvariable prints the step every `stride`;
+!>     the step is this module's currentstep, stloop's clock of the GPU context,
+!>     where the reference reads mod_tsteps' counter of its CPU SPEEDY).
 module speedy_res_interface
-  use iso_c_binding
-  use sml_hip
+  use iso_c_binding, only: c_ptr, c_null_ptr, c_associated, c_int, c_int64_t, c_double, c_loc
+  use sml_hip, only: sml_check, sml_dyn_create, sml_dyn_get_clock, sml_device_alloc, sml_device_free, &
+                     sml_copy_to_device, sml_copy_to_host, sml_dyn_run_model, sml_dyn_last_safe
+  use mod_utilities, only: dp, speedy_data_type, era_data_type, state_vector_type, reservoir_type, grid_type, &
+                           model_parameters_type, opened_netcdf_type
+  use mod_calendar, only: calendar, initialize_calendar
   implicit none
-  private
 
-  integer, parameter, public :: dp = kind(1.d0)
-  integer, parameter, public :: numoftimestep = 17, stride = 1, vartime = numoftimestep / stride, &
-                                numofspeedyvars = 4, numoflevels = 8
+  ! the binding's names stay inside; everything else is public, as in the reference
+  private :: c_ptr, c_null_ptr, c_associated, c_int, c_int64_t, c_double, c_loc
+  private :: sml_check, sml_dyn_create, sml_dyn_get_clock, sml_device_alloc, sml_device_free, &
+             sml_copy_to_device, sml_copy_to_host, sml_dyn_run_model, sml_dyn_last_safe
 
-  !> subsets of mod_utilities.f90's types (field names as there)
-  type, public :: model_parameters_type
-    integer :: number_of_regions = 1152, num_of_regions_on_proc = 0, irank = 0, numprocs = 1
-    integer :: overlap = 1, num_vert_levels = 1, vert_loc_overlap = 0, timestep = 6
-    integer :: chunk_size_prediction = 136, chunk_size_speedy = 132
-    integer, allocatable :: region_indices(:)
-    logical :: run_speedy = .true., ml_only = .false., slab_ocean_model_bool = .false.
-    character(len=:), allocatable :: trial_name
-  end type
+  integer, parameter :: numoftimestep = 17, stride = 1, vartime = numoftimestep / stride, &
+                        numofspeedyvars = 4, numoflevels = 8
 
-  type, public :: grid_type
-    integer :: res_xstart, res_xend, res_ystart, res_yend, resxchunk, resychunk
-    integer :: input_xstart, input_xend, input_ystart, input_yend, inputxchunk, inputychunk
-    integer :: reszchunk = 8, inputzchunk = 8, res_zstart = 1, res_zend = 8, input_zstart = 1, input_zend = 8
-    integer :: num_vert_levels = 1, level_index = 1, vert_overlap = 0, number_of_regions = 1152, region = 0
-    logical :: pole = .false., periodicboundary = .false.
-    real(dp), allocatable :: mean(:), std(:)
-  end type
-
-  type, public :: reservoir_type
-    integer :: assigned_region = -1, n = 0, k = 0, reservoir_numinputs = 0
-    logical :: sst_bool = .false., sst_climo_bool = .false., tisr_input_bool = .true., precip_bool = .true.
-  end type
-
-  type, public :: state_vector_type
-    real(dp), allocatable :: variables3d(:, :, :, :), logp(:, :), sst_hybrid(:, :)
-    integer :: istart = 2, era_start = 3, era_hour = 1, era_hour_plus_one = 2
-    integer :: iyear0 = 1981, imont0 = 1, iday = 1, ihour = 0
-    logical :: is_safe_to_run_speedy = .true., hybrid_slab = .false.
-    real(dp) :: sst_bias = 0.0_dp
-  end type
-
-  type, public :: speedy_data_type
-    real(dp), allocatable :: speedyvariables(:, :, :, :, :), speedy_logp(:, :, :)
-  end type
-
-  type, public :: era_data_type
-    real(dp), allocatable :: eravariables(:, :, :, :, :), era_logp(:, :, :), era_tisr(:, :, :), &
-                             era_sst(:, :, :), era_sst_climo(:, :, :), era_precip(:, :, :)
-  end type
-
-  type, public :: opened_netcdf_type
-    character(len=:), allocatable :: filename
-    logical :: is_opened = .false.
-    integer :: ncid = -1
-  end type
-
-  !> mod_calendar's calendar (initialize_calendar(calendar, 1981, 1, 1, 0))
-  type, public :: calendar_type
-    integer :: startyear, startmonth, startday, starthour
-    integer :: currentyear, currentmonth, currentday, currenthour
-  end type
-
-  type(state_vector_type), public :: internal_state_vector
-  type(calendar_type), public :: calendar
+  type(state_vector_type) :: internal_state_vector
   !> the GPU SPEEDY context startspeedy creates (null until then)
-  type(c_ptr), public :: speedy_gpu = c_null_ptr
-  integer, public :: hybrid_test_windows = 500
-  integer, public :: currentstep = 0
-
-  public :: startspeedy, write_restart_new, getspeedyvariable, read_era_netcdf_opened, read_era, &
-            read_model_states, test_hybrid_speedy_component, truncate_letkf_code_version, initializedomain, &
-            initialize_calendar
+  type(c_ptr) :: speedy_gpu = c_null_ptr
+  integer :: hybrid_test_windows = 500
+  integer :: currentstep = 0
 
 contains
-
-  !> initializedomain (res_domain.f90:96-121): the region's extent and its overlap
-  !> input extent (getxyresextent / getoverlapindices, :123-204)
-  subroutine initializedomain(numregions, region, overlap, num_vert_levels, vert_level, vert_overlap, grid)
-    integer, intent(in) :: numregions, region, overlap, num_vert_levels, vert_level, vert_overlap
-    type(grid_type), intent(inout) :: grid
-    integer(c_int) :: g(12)
-    if (overlap /= 1) stop 'initializedomain: the GPU path is built for overlap = 1 (mod_reservoir.f90:58)'
-    call sml_check(sml_region_geometry(int(numregions, c_int), int(region, c_int), g), 'sml_region_geometry')
-    grid%number_of_regions = numregions
-    grid%region = region
-    grid%res_xstart = g(1)
-    grid%res_xend = g(2)
-    grid%res_ystart = g(3)
-    grid%res_yend = g(4)
-    grid%resxchunk = g(5)
-    grid%resychunk = g(6)
-    grid%input_xstart = g(7)
-    grid%input_xend = g(8)
-    grid%input_ystart = g(9)
-    grid%input_yend = g(10)
-    grid%inputxchunk = g(11)
-    grid%inputychunk = g(12)
-    grid%pole = grid%res_ystart == 1 .or. grid%res_yend == 48
-    grid%periodicboundary = grid%input_xstart > grid%res_xstart .or. grid%input_xend < grid%res_xend
-    grid%num_vert_levels = num_vert_levels
-    grid%level_index = vert_level
-    grid%vert_overlap = vert_overlap
-  end subroutine
-
-  subroutine initialize_calendar(cal, year, month, day, hour)
-    type(calendar_type), intent(inout) :: cal
-    integer, intent(in) :: year, month, day, hour
-    cal%startyear = year
-    cal%startmonth = month
-    cal%startday = day
-    cal%starthour = hour
-    cal%currentyear = year
-    cal%currentmonth = month
-    cal%currentday = day
-    cal%currenthour = hour
-  end subroutine
 
   !> :20-37 -- initializedomain(numprocs, proc_num, overlap, ...) and the calendar;
   !> with runspeedy, the GPU SPEEDY context (tables of indyns / parmtr / inifft)
   subroutine startspeedy(model_parameters, grid, runspeedy)
+    use mpires, only: mpi_res
+    use resdomain, only: initializedomain
     type(model_parameters_type), intent(in) :: model_parameters
     type(grid_type), intent(inout) :: grid
     logical, intent(in) :: runspeedy
     integer :: vert_level
     vert_level = 1
-    call initializedomain(model_parameters%number_of_regions, model_parameters%irank, model_parameters%overlap, &
-                          grid%num_vert_levels, vert_level, grid%vert_overlap, grid)
+    call initializedomain(mpi_res%numprocs, mpi_res%proc_num, model_parameters%overlap, grid%num_vert_levels, &
+                          vert_level, grid%vert_overlap, grid)
     call initialize_calendar(calendar, 1981, 1, 1, 0)
     if (runspeedy .and. .not. c_associated(speedy_gpu)) &
       call sml_check(sml_dyn_create(6.371e+6_c_double, speedy_gpu), 'sml_dyn_create')
@@ -203,7 +123,7 @@ contains
     integer, intent(in), optional :: timestep_arg
     character(len=4) :: year
     write (year, '(i4)') start_year
-    if (.false.) print *, reservoir%n, grid%region, model_parameters%irank, end_year, allocated(era_data%era_logp), &
+    if (.false.) print *, reservoir%n, grid%number_of_regions, model_parameters%irank, end_year, allocated(era_data%era_logp), &
                           size(netcdf_files), present(timestep_arg)
     call missing_input('read_era_netcdf_opened', '/scratch/user/troyarcomano/ERA_5/' // year // '/era_5_y' // year // &
                        '_regridded_mpi_fixed_var_gcc.nc')
@@ -219,7 +139,7 @@ contains
     integer, intent(in), optional :: timestep_arg
     character(len=4) :: year
     write (year, '(i4)') start_year
-    if (.false.) print *, reservoir%n, grid%region, model_parameters%irank, end_year, allocated(era_data%era_logp), &
+    if (.false.) print *, reservoir%n, grid%number_of_regions, model_parameters%irank, end_year, allocated(era_data%era_logp), &
                           present(timestep_arg)
     call missing_input('read_era', '/scratch/user/troyarcomano/ERA_5/' // year // '/era_5_y' // year // &
                        '_regridded_mpi_fixed_var_gcc.nc')
@@ -235,17 +155,20 @@ contains
     integer, intent(in), optional :: timestep_arg
     character(len=4) :: year
     write (year, '(i4)') start_year
-    if (.false.) print *, reservoir%n, grid%region, model_parameters%irank, end_year, &
+    if (.false.) print *, reservoir%n, grid%number_of_regions, model_parameters%irank, end_year, &
                           allocated(speedy_data%speedy_logp), present(timestep_arg)
     call missing_input('read_model_states', '/scratch/user/troyarcomano/SPEEDY_STATES/restart_6hour_y' // year // '.nc')
   end subroutine
 
-  !> :722-815 -- repeated SPEEDY windows from internal_state_vector: q clipped to
-  !> [0, 25] before each window, run_model (here sml_dyn_run_model: iogrid(30),
-  !> stepone + 24 leapfrog steps, iogrid(31), q floor 1e-6), q < 0 -> 0 after.
+  !> :722-815 -- repeated SPEEDY windows from internal_state_vector: the calendar
+  !> advanced to hour 86184 + i and the state's start / date fields set from it
+  !> (:778, :789-800), q clipped to [0, 25] before each window, run_model (here
+  !> sml_dyn_run_model: iogrid(30), stepone + 24 leapfrog steps, iogrid(31), q floor
+  !> 1e-6), q < 0 -> 0 after.
   !> The GPU context must have its state, forcing and physics set (startspeedy
   !> creates it).  Stops early when a window is unsafe (is_safe_to_run_speedy).
   subroutine test_hybrid_speedy_component()
+    use mod_calendar, only: get_current_time_delta_hour
     integer, parameter :: ng4 = 4 * 96 * 48 * 8, ng2 = 96 * 48
     type(c_ptr) :: d_in4, d_in2, d_out4, d_out2
     integer :: i
@@ -261,10 +184,19 @@ contains
     call sml_check(sml_device_alloc(8_c_int64_t * ng4, d_out4), 'sml_device_alloc')
     call sml_check(sml_device_alloc(8_c_int64_t * ng2, d_out2), 'sml_device_alloc')
     do i = 1, hybrid_test_windows
+      call get_current_time_delta_hour(calendar, 86184 + i)
       where (internal_state_vector%variables3d(4, :, :, :) < 0.0_dp) internal_state_vector%variables3d(4, :, :, :) = 0.0_dp
       where (internal_state_vector%variables3d(4, :, :, :) > 25.0_dp) &
         internal_state_vector%variables3d(4, :, :, :) = 25.0_dp
       internal_state_vector%is_safe_to_run_speedy = .true.
+      internal_state_vector%era_hour = 1
+      internal_state_vector%era_hour_plus_one = 2
+      internal_state_vector%istart = 2
+      internal_state_vector%era_start = 3
+      internal_state_vector%iyear0 = calendar%currentyear
+      internal_state_vector%imont0 = calendar%currentmonth
+      internal_state_vector%iday = calendar%currentday
+      internal_state_vector%ihour = calendar%currenthour
       v4 = internal_state_vector%variables3d
       lp = internal_state_vector%logp
       call sml_check(sml_copy_to_device(d_in4, c_loc(v4), 8_c_int64_t * ng4), 'sml_copy_to_device')

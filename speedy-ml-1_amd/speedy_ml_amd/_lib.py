@@ -52,7 +52,7 @@ EXPORTED = (
     "sml_processor_decomposition", "sml_hybrid_set_tisr_table", "sml_tisr_date_index", "sml_res_tile_tisr_field",
     "sml_res_create_generic", "sml_res_step_slab", "sml_res_start_prediction",
     "sml_comm_create_local", "sml_exchange_plan", "sml_hybrid_advance_slabs", "sml_hybrid_set_hop_mode",
-    "sml_hybrid_hop_mode",
+    "sml_hybrid_hop_mode", "sml_calendar_delta_hour", "sml_hybrid_set_feb29", "sml_hybrid_get_feb29",
 )
 
 SML_HOP_AUTO, SML_HOP_WAIT_VALUE, SML_HOP_EVENTS = 0, 1, 2
@@ -209,6 +209,9 @@ def _declare(L: ctypes.CDLL) -> None:
         "sml_hybrid_advance_slabs": [vp, vp],
         "sml_hybrid_set_hop_mode": [vp, i],
         "sml_hybrid_hop_mode": [vp, ip, ip],
+        "sml_calendar_delta_hour": [i, ctypes.c_int64, ip, ip],
+        "sml_hybrid_set_feb29": [vp, i],
+        "sml_hybrid_get_feb29": [vp, ip],
     }
     for name, args in sig.items():
         fn = getattr(L, name)

@@ -160,7 +160,17 @@ def test_speedy_res_interface_module(tmp_path, cuda):
         f.write(regions.tobytes())
     out = subprocess.run([_bin("sml_interface_check"), str(tmp_path)], capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stdout + out.stderr
-    assert "calendar year 1981" in out.stdout
+    # the calendar and the state's date fields advanced per window as the reference
+    # (speedy_res_interface.f90:778, 797-800): hour 86184 + nwin from 1981
+    import ctypes
+
+    from speedy_ml_amd._lib import lib
+
+    date, feb = (ctypes.c_int * 4)(), ctypes.c_int(0)
+    for i in range(1, nwin + 1):
+        assert lib().sml_calendar_delta_hour(1981, 86184 + i, ctypes.byref(feb), date) == 0
+    line = [ln for ln in out.stdout.splitlines() if ln.startswith("calendar")][0].split()
+    assert [int(v) for v in line[1:5]] == list(date) == [int(v) for v in line[6:10]], (line, list(date))
     raw = np.fromfile(tmp_path / "iface_out.bin", dtype=np.float64)
     v4 = raw[:g4.size].reshape(g4.shape)
     lp = raw[g4.size:g4.size + g2.size].reshape(g2.shape)

@@ -240,8 +240,13 @@ def test_tisr_by_date_from_a_table(cuda):
     dt = torch.from_numpy(table).to(cuda)
     start, base = 1981, 227520 + 24 * 40
     loop.set_tisr_table(dt, start, base)
+    # the host's calendar already met a leap year: the SAVEd February latch is 1
+    # (sml_hybrid_set_feb29; set_tisr_table reset it to 0)
+    got = ctypes.c_int(-1)
+    assert lib().sml_hybrid_get_feb29(loop._h, ctypes.byref(got)) == 0 and got.value == 0
+    assert lib().sml_hybrid_set_feb29(loop._h, 1) == 0
     o = loop.res.fb_offsets
-    feb = ctypes.c_int(0)
+    feb = ctypes.c_int(1)
     for t in (1, 2):
         loop.step()
         loop.sync()
