@@ -350,6 +350,15 @@ int sml_dyn_step_host(sml_dynamics *d, int j1, int j2, double dt, double alph, d
  * and d_phys arguments must be NULL; bc = NULL switches it off.  Call again when the
  * fields change (the coupler / sol_oz run once a day, ini_fordate.f90). */
 int sml_dyn_set_physics(sml_dynamics *d, const double *bc);
+/* the slab ocean's SST in the window (run_model's sst_hybrid, src/mpires.f90:1576-1584,
+ * applied by agcm_init's ini_sea, src/cpl_sea.f90:38-46): sst_am = the hybrid SST where
+ * the coupler's sst_am (bc's, ice-blended as sea2atm leaves it) is < 6 K above it, +
+ * sst_bias, then blended with the sea ice (sice, tice).  d_sst_grid(96, 48) device,
+ * read on `stream`; NULL restores the coupler's field.  Kept in force across
+ * sml_dyn_set_physics calls until replaced. */
+int sml_dyn_set_hybrid_sst(sml_dynamics *d, const double *d_sst_grid, double sst_bias, void *stream);
+/* sea-ice fraction / temperature sice_am, tice_am (host [ngp]; NULL = no ice) */
+int sml_dyn_set_sea_ice(sml_dynamics *d, const double *sice, const double *tice);
 /* stloop's clock (dyn_stloop.f90:37-56): istep and mod_lflags' lradsw.  sml_dyn_step
  * uses lradsw as it stands; sml_dyn_leapfrog sets lradsw = (mod(istep, 3) == 1)
  * before each step and advances istep, as stloop does.  Initial: istep 1, lradsw 1. */
@@ -510,6 +519,35 @@ int sml_hybrid_advance_slabs(sml_hybrid *h, const double *d_recv);
 /* predict + the loop's own exchange (identity on one rank, sml_comm_allgather
  * otherwise) + advance_slabs; asynchronous */
 int sml_hybrid_step(sml_hybrid *h);
+/* ---- slab ocean (src/parallelmain.f90:216-249; sendrecievegrid's sst half,
+ * src/mpires.f90:288-478, 575-767; run_model's sst_hybrid, :1576-1584, applied by
+ * ini_sea, src/cpl_sea.f90:38-46).  slab: a generic ML-only context
+ * (sml_res_create_generic, chunk_speedy 0, nout = resx*resy, out_index 35, leakage 1)
+ * over exactly this rank's regions with an sst input, in order, each with the 7*in2d
+ * inputs of atmo_training_data_idx (src/mod_slab_ocean_reservoir.f90:1532-1563).
+ * Every step the atmo feedback's lowest level, logp, sst and tisr enter a ring of
+ * timestep_slab/timestep - 1 columns; when mod(t*timestep, timestep_slab) == 0 the slab
+ * reservoirs predict from the ring's mean (predict_slab_ml, :1251-1296); their sst
+ * travels in the exchange rows (nout + resx*resy doubles per region, so d_outvec and a
+ * host exchange use sml_hybrid_exchange_width), is assembled into wholegrid_sst with
+ * base_sst_grid on land (sea_mask > 0) and the 272 K floor, enters the window's sst_am
+ * (sml_dyn_set_hybrid_sst) and, standardized with the slab's sst mean / std, the atmo
+ * feedback's sst entries.  d_base_sst / d_sea_mask (96, 48) device, read every slab
+ * step.  Call before sml_hybrid_set_buffers; train_on_sst_anomalies and
+ * non_stationary_ocn_climo (both off by default, mod_reservoir.f90:42-44) are not
+ * supported. */
+int sml_hybrid_set_slab(sml_hybrid *h, sml_reservoirs *slab, const double *d_base_sst, const double *d_sea_mask,
+                        int timestep, int timestep_slab, double sst_bias);
+/* start_prediction_slab's hand-over, after sml_hybrid_start: the slab reservoirs' sst
+ * d_slab_outvec[nslab][resx*resy] (unstandardized; their states synchronized by the
+ * host with sml_res_start_prediction) */
+int sml_hybrid_start_slab(sml_hybrid *h, const double *d_slab_outvec);
+/* doubles per region in the exchange rows: nout, or nout + resx*resy with the slab */
+int sml_hybrid_exchange_width(const sml_hybrid *h, int *width);
+/* device views of the slab state: wholegrid_sst(96, 48), the ring
+ * [timestep_slab/timestep - 1][*ring_len], the last slab feedback and slab outvecs */
+int sml_hybrid_slab_buffers(const sml_hybrid *h, const double **d_sst_grid, const double **d_ring, int *ring_len,
+                            const double **d_slab_feedback, const double **d_slab_outvec);
 /* the two cross-stream dependencies of the overlapped loop: SML_HOP_WAIT_VALUE (a
  * sequence number written by the producer's stream, waited for by the consumer's:
  * 3.9 us), SML_HOP_EVENTS (event record + wait: 10 us), or SML_HOP_AUTO (the
@@ -540,6 +578,11 @@ int sml_copy_to_host(void *dst, const void *d_src, int64_t bytes);
 int sml_region_geometry(int numregions, int region, int *g);
 /* processor_decomposition (src/res_domain.f90:31-62): 0-based regions of rank irank */
 int sml_processor_decomposition(int numregions, int numprocs, int irank, int *regions, int *count);
+/* the mean / std (36 each) local region i was loaded with (host copies) */
+int sml_res_mean_std(const sml_reservoirs *c, int i, double *mean, double *std);
+/* row stride (>= nout) of the outvec arrays the context writes and
+ * sml_exchange_assemble reads (the hybrid loop widens it for the slab ocean's sst) */
+int sml_res_set_outvec_ld(sml_reservoirs *c, int ld);
 /* numregions, nlocal, chunk_speedy, nout and the local region ids (any may be NULL) */
 int sml_res_info(const sml_reservoirs *c, int *numregions, int *nlocal, int *chunk_speedy, int *nout,
                  int *region_ids);

@@ -68,6 +68,8 @@ def _declare(L):
     L.orc_predict.argtypes = [i, i, i, vp, vp, vp, vp, vp, i, i, d, vp, vp, vp, vp, vp, vp, i]
     L.orc_predict_f32.argtypes = [i, i, i, vp, vp, vp, vp, vp, vp, i, i, d, vp, vp, vp, vp, vp, vp]
     L.orc_predict_regions.argtypes = [i, i, vp, vp, vp, vp, vp, vp, vp, vp, i, i, d, vp, vp, vp, vp, vp, vp]
+    L.orc_predict_f32_regions.argtypes = [i, i, vp, vp, vp] + [vp] * 6 + [i, i, d] + [vp] * 6
+    L.orc_predict_slab_ml_f32.argtypes = [i, i, vp, vp, vp, vp, vp, vp, i, d, vp, vp, vp, d, d]
     L.orc_unstandardize_res.argtypes = [vp, i, i, i, vp, vp, i, i, i, i]
     L.orc_assemble.argtypes = [i, vp, i, vp, vp, vp]
     L.orc_tile_feedback.argtypes = [i, i, vp, vp, vp, vp, vp, vp, vp, vp]
@@ -311,6 +313,92 @@ def predict_f32(rows, cols, vals_f32, win_col, win_val_f32, wout_f32, feedback, 
                           _p(xx), _p(out), _p(np.ascontiguousarray(mean, dtype=np.float64)),
                           _p(np.ascontiguousarray(std, dtype=np.float64)))
     return out, xx
+
+
+def predict_f32_regions(regs, feedbacks, local_models, xs, nthreads=8, chunk_speedy=132, leakage=1.0):
+    """predict_f32 over many regions with OpenMP.  regs: dicts with rows, cols, vals
+    (f32), win_col (i32), win_val (f32), wout (f32, (ncs+n, nout)), mean, std; xs
+    (float64 arrays) updated in place.  Returns outvecs [nreg, nout]."""
+    nreg = len(regs)
+    nout = regs[0]["wout"].shape[1]
+
+    def table(arrs):
+        return (ctypes.c_void_p * nreg)(*[a.ctypes.data for a in arrs])
+
+    n = np.array([len(r["win_col"]) for r in regs], dtype=np.int32)
+    ninp = np.array([len(f) for f in feedbacks], dtype=np.int32)
+    k = np.array([len(r["rows"]) for r in regs], dtype=np.int32)
+    fbs = [np.ascontiguousarray(f, dtype=np.float64) for f in feedbacks]
+    lms = [np.ascontiguousarray(m if m is not None else np.zeros(1), dtype=np.float64) for m in local_models]
+    out = np.zeros((nreg, nout))
+    tabs = [table([r[key] for r in regs]) for key in ("rows", "cols", "vals", "win_col", "win_val", "wout")]
+    lib().orc_predict_f32_regions(nreg, int(nthreads), _p(n), _p(ninp), _p(k), *tabs, nout, chunk_speedy, leakage,
+                                  table(fbs), table(lms), table(xs), _p(out), table([r["mean"] for r in regs]),
+                                  table([r["std"] for r in regs]))
+    return out
+
+
+# ---------------------------------------------------------------- slab ocean
+def predict_slab_ml_f32(rows, cols, vals_f32, win_col, win_val_f32, wout_f32, feedback, x, mean_sst, std_sst,
+                        leakage=1.0):
+    """predict_slab_ml (mod_slab_ocean_reservoir.f90:1251-1296).  Returns (outvec, x_new)."""
+    n = len(win_col)
+    nout = wout_f32.shape[1]
+    xx = np.array(x, dtype=np.float64, copy=True)
+    out = np.zeros(nout)
+    lib().orc_predict_slab_ml_f32(n, len(rows), _p(np.ascontiguousarray(rows, dtype=np.int32)),
+                                  _p(np.ascontiguousarray(cols, dtype=np.int32)),
+                                  _p(np.ascontiguousarray(vals_f32, dtype=np.float32)),
+                                  _p(np.ascontiguousarray(win_col, dtype=np.int32)),
+                                  _p(np.ascontiguousarray(win_val_f32, dtype=np.float32)),
+                                  _p(np.ascontiguousarray(wout_f32, dtype=np.float32)), nout, leakage,
+                                  _p(np.ascontiguousarray(feedback, dtype=np.float64)), _p(xx), _p(out),
+                                  float(mean_sst), float(std_sst))
+    return out, xx
+
+
+def slab_input_index(region, numregions=1152):
+    """atmo_training_data_idx (mod_slab_ocean_reservoir.f90:1550-1563), 0-based, into
+    the bottom-level atmo feedback of a region with an sst input: the lowest level's
+    4 variables (the last 4*in2d of atmo3d), logp, then sst, then tisr."""
+    geo = region_geometry(region, numregions)
+    in2d = geo["inputxchunk"] * geo["inputychunk"]
+    natmo = 4 * in2d * 8
+    return np.concatenate([np.arange(natmo - 4 * in2d, natmo + in2d), np.arange(natmo + 2 * in2d, natmo + 4 * in2d)])
+
+
+def tile_2d(region, grid2d, numregions=1152):
+    """tileoverlapgrid of one 2-D field (res_domain.f90:348-420): the region's
+    overlap input tile, x fastest (tile_4d_and_logp_to_local_state_input_slab)."""
+    geo = region_geometry(region, numregions)
+    ix, iy = geo["inputxchunk"], geo["inputychunk"]
+    xs = [(geo["input_xstart"] - 1 + lx) % 96 for lx in range(ix)]  # periodic wrap in x
+    ys = [geo["input_ystart"] - 1 + ly for ly in range(iy)]
+    return np.array([grid2d[y, x] for y in ys for x in xs])
+
+
+def sst_grid(sst_rows, base_sst, sea_mask, numregions=1152):
+    """sendrecievegrid's wholegrid_sst (mpires.f90:288-319, 458-472): base_sst_grid,
+    every region's sst (its slab outvec, or 272 K without one) tiled on its resolved
+    points (tile_full_2d_grid_with_local_res), base_sst_grid where sea_mask > 0, then
+    a 272 K floor (train_on_sst_anomalies off).  sst_rows [numregions][resx*resy];
+    grids (48, 96) == Fortran (96, 48)."""
+    g = np.array(base_sst, dtype=np.float64, copy=True)
+    for r in range(numregions):
+        geo = region_geometry(r, numregions)
+        rx, ry = geo["resxchunk"], geo["resychunk"]
+        g[geo["res_ystart"] - 1:geo["res_ystart"] - 1 + ry, geo["res_xstart"] - 1:geo["res_xstart"] - 1 + rx] = \
+            np.asarray(sst_rows[r]).reshape(ry, rx)
+    g = np.where(sea_mask > 0.0, base_sst, g)
+    return np.where(g < 272.0, 272.0, g)
+
+
+def hybrid_sst_am(sst_cpl, sst_hybrid, sice, tice, bias=0.0):
+    """ini_sea's hybrid block (cpl_sea.f90:38-46) on the coupler's (ice-blended) sst_am."""
+    s = np.where(sst_cpl - sst_hybrid < 6.0, sst_hybrid, sst_cpl)
+    s = s + bias
+    d = tice - s
+    return s + sice * d
 
 
 # ---------------------------------------------------------------- exchange / tiling

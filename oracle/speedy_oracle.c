@@ -708,6 +708,53 @@ void orc_predict_f32(int n, int ninp, int k, const int *rows, const int *cols, c
     free(xa);
 }
 
+/* orc_predict_f32 over many regions, OpenMP over regions (tests: the oracle chain of
+ * the full-size hybrid step).  Per-region arrays as pointer tables; outvecs [nreg][nout]. */
+void orc_predict_f32_regions(int nreg, int nthreads, const int *n, const int *ninp, const int *k,
+                             const int *const *rows, const int *const *cols, const float *const *vals,
+                             const int *const *win_col, const float *const *win_val, const float *const *wout,
+                             int nout, int chunk_speedy, double leakage, const double *const *feedback,
+                             const double *const *local_model, double *const *x, double *outvecs,
+                             const double *const *mean, const double *const *std)
+{
+#pragma omp parallel for num_threads(nthreads) schedule(dynamic, 1)
+    for (int r = 0; r < nreg; ++r)
+        orc_predict_f32(n[r], ninp[r], k[r], rows[r], cols[r], vals[r], win_col[r], win_val[r], wout[r], nout,
+                        chunk_speedy, leakage, feedback[r], local_model[r], x[r], outvecs + (size_t)r * nout,
+                        mean[r], std[r]);
+}
+
+/* predict_slab_ml (mod_slab_ocean_reservoir.f90:1251-1296): the slab-ocean reservoir's
+ * ML-only step --
+ *   y = A x (COO in file order), temp = matmul(win, feedback)  (:1274-1275)
+ *   x = (1-leak) x + leak tanh(y + temp)                        (:1277-1278)
+ *   x_augment = x with x(2:n:2)**2                              (:1280-1283)
+ *   outvec = matmul(wout, x_augment) * std(sst) + mean(sst)     (:1285-1287)
+ * W_in compressed (one entry per row), fp32 weights as in the file. */
+void orc_predict_slab_ml_f32(int n, int k, const int *rows, const int *cols, const float *vals, const int *win_col,
+                             const float *win_val, const float *wout, int nout, double leakage,
+                             const double *feedback, double *x, double *outvec, double mean_sst, double std_sst)
+{
+    double *y = (double *)calloc((size_t)n, sizeof(double));
+    for (int e = 0; e < k; ++e) y[rows[e] - 1] = y[rows[e] - 1] + (double)vals[e] * x[cols[e] - 1];
+    for (int i = 0; i < n; ++i) {
+        double t = (double)win_val[i] * feedback[win_col[i]];
+        double xn = tanh(y[i] + t);
+        x[i] = (1.0 - leakage) * x[i] + leakage * xn;
+    }
+    for (int o = 0; o < nout; ++o) outvec[o] = 0.0;
+    for (int jj = 0; jj < n; ++jj) {
+        double a = (jj & 1) ? x[jj] * x[jj] : x[jj];
+        const float *wc = wout + (size_t)jj * nout;
+        for (int o = 0; o < nout; ++o) outvec[o] = outvec[o] + (double)wc[o] * a;
+    }
+    for (int o = 0; o < nout; ++o) {
+        double t = outvec[o] * std_sst;
+        outvec[o] = t + mean_sst;
+    }
+    free(y);
+}
+
 /* ------------------------------------------------------------------------- */
 /* Exchange + tiling (mpires.f90:sendrecievegrid 218-780)                     */
 /* Global grids use the reference layout: grid4d(4,96,48,8) column-major,     */

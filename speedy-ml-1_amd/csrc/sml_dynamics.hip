@@ -112,6 +112,12 @@ struct sml_dynamics {
     PhysTables *d_ptab = nullptr;
     double *d_pbc = nullptr, *d_rad = nullptr, *d_pio = nullptr;
     bool phys_on = false;
+    // ini_sea's hybrid block (cpl_sea.f90:38-46): the coupler's sst_am as set_physics
+    // gave it, sea-ice fraction / temperature, and the hybrid SST grid last applied
+    // (sml_dyn_set_hybrid_sst; re-applied when set_physics brings a new sst_am)
+    double *d_sst_cpl = nullptr, *d_sice = nullptr, *d_tice = nullptr;
+    const double *hyb_sst = nullptr;
+    double hyb_bias = 0.0;
     // step kernels: the fused form (default: 2-3 launches per chained step) or the
     // 8/9-launch form (SML_DYN_FUSED=0 at creation; same results bit for bit)
     bool fused = true;
@@ -2008,7 +2014,7 @@ extern "C" int sml_dyn_destroy(sml_dynamics *d) {
     if (!d) return SML_OK;
     void *ptrs[] = {d->d_tabs, d->d_tabm, d->d_state, d->d_phis, d->d_tcorh, d->d_qcorh, d->d_phi, d->d_specin,
                     d->d_varm, d->d_grid, d->d_gfwd, d->d_sfwd, d->d_tend, d->d_phys, d->d_minmax, d->d_io, d->d_vfm, d->d_pfl, d->d_sm, d->d_dbg,
-                    d->d_ptab, d->d_pbc, d->d_rad, d->d_pio};
+                    d->d_ptab, d->d_pbc, d->d_rad, d->d_pio, d->d_sst_cpl, d->d_sice, d->d_tice};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     for (auto &r : d->replay)
@@ -2063,7 +2069,8 @@ extern "C" int sml_dyn_create(double radius, sml_dynamics **out) {
         (rc = dalloc(&d->d_io, (size_t)4 * kKX * kGF + kGF)) || (rc = dalloc(&d->d_ptab, 1)) ||
         (rc = dalloc(&d->d_chk, (size_t)kNIo * (kSF + kVF + kGF))) ||
         (rc = dalloc(&d->d_pbc, (size_t)kNBc * kNGP)) || (rc = dalloc(&d->d_rad, kRadSize)) ||
-        (rc = dalloc(&d->d_pio, (size_t)(5 * kKX + 1 + 4 * kKX) * kNGP))) {
+        (rc = dalloc(&d->d_pio, (size_t)(5 * kKX + 1 + 4 * kKX) * kNGP)) || (rc = dalloc(&d->d_sst_cpl, kNGP)) ||
+        (rc = dalloc(&d->d_sice, kNGP)) || (rc = dalloc(&d->d_tice, kNGP))) {
         sml_dyn_destroy(d);
         return rc;
     }
@@ -2437,6 +2444,43 @@ extern "C" int sml_dyn_get_clock(const sml_dynamics *d, int *istep, int *lradsw)
     return SML_OK;
 }
 
+namespace {
+// ini_sea's hybrid block (cpl_sea.f90:38-46) per grid point: where the coupler's
+// (ice-blended) sst_am is less than 6 K above the hybrid SST take the hybrid SST, add
+// the bias, blend with the sea ice as sea2atm does (cpl_sea.f90:197)
+__global__ void k_hybrid_sst(const double *__restrict__ cpl, const double *__restrict__ hyb,
+                             const double *__restrict__ sice, const double *__restrict__ tice, double bias,
+                             double *__restrict__ sst_am) {
+#pragma clang fp contract(off)  // the reference's separate multiply and add (this file contracts by default)
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= kNGP) return;
+    double s = cpl[p];
+    if (hyb) {
+        const double diff = s - hyb[p];
+        if (diff < 6.0) s = hyb[p];
+        s = s + bias;
+        const double d = tice[p] - s;
+        s = s + sice[p] * d;
+    }
+    sst_am[p] = s;
+}
+}  // namespace
+
+// run_model's SST hand-over (mpires.f90:1576-1584: internal_state_vector%sst_hybrid)
+// as agcm_init's ini_sea applies it to the window's sst_am (cpl_sea.f90:38-46):
+// d_sst_grid(96, 48) device; NULL restores the coupler's sst_am.  On `stream`, so a
+// loop orders it before its next window.
+extern "C" int sml_dyn_set_hybrid_sst(sml_dynamics *d, const double *d_sst_grid, double sst_bias, void *stream) {
+    SML_REQUIRE(d, "null context");
+    SML_REQUIRE(d->phys_on, "sml_dyn_set_physics must provide the boundary fields first");
+    d->hyb_sst = d_sst_grid;
+    d->hyb_bias = sst_bias;
+    hipLaunchKernelGGL(k_hybrid_sst, dim3((kNGP + 255) / 256), dim3(256), 0, (hipStream_t)stream, d->d_sst_cpl,
+                       d_sst_grid, d->d_sice, d->d_tice, sst_bias, d->d_pbc + (size_t)kBcSst * kNGP);
+    SML_HIP(hipGetLastError());
+    return SML_OK;
+}
+
 extern "C" int sml_dyn_set_physics(sml_dynamics *d, const double *bc) {
     SML_REQUIRE(d, "null context");
     if (!bc) {
@@ -2445,7 +2489,28 @@ extern "C" int sml_dyn_set_physics(sml_dynamics *d, const double *bc) {
     }
     SML_HIP(hipDeviceSynchronize());  // steps in flight may still read the old fields
     SML_HIP(hipMemcpy(d->d_pbc, bc, (size_t)kNBc * kNGP * 8, hipMemcpyHostToDevice));
+    SML_HIP(hipMemcpy(d->d_sst_cpl, bc + (size_t)kBcSst * kNGP, kNGP * 8, hipMemcpyHostToDevice));
     d->phys_on = true;
+    if (d->hyb_sst) {  // a hybrid SST is in force: ini_sea applies it to every new sst_am
+        if (int rc = sml_dyn_set_hybrid_sst(d, d->hyb_sst, d->hyb_bias, nullptr)) return rc;
+        SML_HIP(hipDeviceSynchronize());
+    }
+    return SML_OK;
+}
+
+// sea-ice fraction and temperature of the coupler (sice_am, tice_am; cpl_sea.f90:
+// 190-194), host [ngp] each; NULL = no ice (zero fraction)
+extern "C" int sml_dyn_set_sea_ice(sml_dynamics *d, const double *sice, const double *tice) {
+    SML_REQUIRE(d && (sice == nullptr) == (tice == nullptr), "sice and tice go together");
+    SML_HIP(hipDeviceSynchronize());
+    if (sice) {
+        SML_HIP(hipMemcpy(d->d_sice, sice, kNGP * 8, hipMemcpyHostToDevice));
+        SML_HIP(hipMemcpy(d->d_tice, tice, kNGP * 8, hipMemcpyHostToDevice));
+    } else {
+        SML_HIP(hipMemset(d->d_sice, 0, kNGP * 8));
+        SML_HIP(hipMemset(d->d_tice, 0, kNGP * 8));
+    }
+    if (d->hyb_sst) return sml_dyn_set_hybrid_sst(d, d->hyb_sst, d->hyb_bias, nullptr);
     return SML_OK;
 }
 

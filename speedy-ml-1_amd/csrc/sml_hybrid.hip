@@ -82,6 +82,21 @@ struct sml_hybrid {
     const double *tisr_table = nullptr;
     int tisr_nhours = 0, tisr_startyear = 0, tisr_feb29 = 0;
     int64_t tisr_base = 0, tisr_step_hours = 6, t = 0;
+    // the exchange row: the outvec (nout), + the slab ocean's sst of the region's
+    // resolved points when the slab is on (as sendrecievegrid sends them, mpires.f90:358-383)
+    int xw = 0;
+    // slab ocean (parallelmain.f90:216-249; mpires.f90:288-478, 575-767; cpl_sea.f90:38-46)
+    struct Slab {
+        sml_reservoirs *res = nullptr;  // the slab reservoirs of this rank's sst regions (generic, ML-only)
+        int nslab = 0, nsst = 4, ratio = 28, tot_fb = 0, n_sst_el = 0;
+        int timestep = 6, timestep_slab = 168;
+        double sst_bias = 0.0;
+        const double *base = nullptr, *mask = nullptr;  // base_sst_grid, sea_mask (96, 48)
+        double *d_fb = nullptr, *d_ov = nullptr, *d_ring = nullptr, *d_sst = nullptr, *d_ms = nullptr;
+        int32_t *d_ring_src = nullptr, *d_row = nullptr, *d_sst_src = nullptr, *d_sfb = nullptr, *d_sgrid = nullptr;
+        uint16_t *d_sreg = nullptr;
+        bool dirty = false, started = false;
+    } slab;
 };
 
 namespace {
@@ -102,6 +117,64 @@ __global__ void k_gather_rows(const double *__restrict__ recv, const int32_t *__
     if (e >= total) return;
     const int r = e / nout, o = e % nout;
     glob[e] = recv[(size_t)perm[r] * nout + o];
+}
+
+// ---- slab ocean kernels (mpires.f90:288-478, 575-767)
+// the slab feedback: the mean of the ring of the last timestep_slab/timestep - 1 atmo
+// feedback subsets, summed column by column as Fortran's sum(.., dim=2) (mpires.f90:757)
+__global__ void k_slab_avg(const double *__restrict__ ring, int ncol, int tot, double *__restrict__ fb) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= tot) return;
+    double s = 0.0;
+    for (int c = 0; c < ncol; ++c) s = s + ring[(size_t)c * tot + e];
+    fb[e] = s / (double)ncol;
+}
+
+// averaged_atmo_input_vec(:, col) = the atmo feedback at atmo_training_data_idx
+// (mpires.f90:755; the index list of trained_ocean_reservoir_prediction,
+// mod_slab_ocean_reservoir.f90:1550-1563)
+__global__ void k_slab_ring(const double *__restrict__ fb, const int32_t *__restrict__ src, int tot,
+                            double *__restrict__ col) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e < tot) col[e] = fb[src[e]];
+}
+
+// the sst columns of the exchange rows: 272 for a region without a slab prediction
+// (mpires.f90:366-372), the slab outvec otherwise
+__global__ void k_slab_rows(const double *__restrict__ slab_ov, const int32_t *__restrict__ row, int nslab, int nsst,
+                            int nlocal, int nout, int xw, bool fill, double *__restrict__ ov) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (fill) {
+        if (e < nlocal * nsst) ov[(size_t)(e / nsst) * xw + nout + e % nsst] = 272.0;
+        return;
+    }
+    if (e < nslab * nsst) ov[(size_t)row[e / nsst] * xw + nout + e % nsst] = slab_ov[e];
+}
+
+// wholegrid_sst from every region's sst columns (tile_full_2d_grid_with_local_res,
+// res_domain.f90), land / permanent ice to base_sst_grid, floor 272 K
+// (mpires.f90:458-472; train_on_sst_anomalies off)
+__global__ void k_sst_grid(const double *__restrict__ ov_all, const int32_t *__restrict__ src,
+                           const double *__restrict__ base, const double *__restrict__ mask, double *__restrict__ sst) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= kGrid2d) return;
+    double v = ov_all[src[p]];
+    if (mask[p] > 0.0) v = base[p];
+    if (v < 272.0) v = 272.0;
+    sst[p] = v;
+}
+
+// the atmo feedback's sst entries: the overlap tile of wholegrid_sst standardized with
+// the slab reservoir's sst mean / std (tile_4d_and_logp_to_local_state_input_slab +
+// standardize_data_given_pars1d, mpires.f90:575-581, copied over at :733-736)
+__global__ void k_sst_feedback(const double *__restrict__ sst, const int32_t *__restrict__ fbi,
+                               const int32_t *__restrict__ gi, const uint16_t *__restrict__ reg,
+                               const double *__restrict__ ms, int n, double *__restrict__ fb) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= n) return;
+    const int j = reg[e];
+    const double t = sst[gi[e]] - ms[2 * j];
+    fb[fbi[e]] = t / ms[2 * j + 1];
 }
 
 }  // namespace
@@ -315,6 +388,27 @@ int hop_wait(sml_hybrid *h, int k, hipStream_t s) {
     return SML_OK;
 }
 
+// the exchange staging for rows of h->xw doubles (world > 1): the loop's own
+// all-gather's send / receive slabs (when the communicator has a transport) and the
+// region-order copy of uneven shares
+int alloc_exchange(sml_hybrid *h) {
+    for (double **p : {&h->d_send, &h->d_recv, &h->d_glob})
+        if (*p) {
+            (void)hipFree(*p);
+            *p = nullptr;
+        }
+    const size_t row = (size_t)h->xw * 8;
+    const int world = h->comm->world;
+    if (h->comm->comm &&
+        (hipMalloc(&h->d_send, (size_t)h->maxc * row) != hipSuccess ||
+         hipMalloc(&h->d_recv, (size_t)world * h->maxc * row) != hipSuccess ||
+         hipMemset(h->d_send, 0, (size_t)h->maxc * row) != hipSuccess))
+        return fail(SML_ERR_NOMEM, "exchange buffers");
+    if (!h->contiguous && hipMalloc(&h->d_glob, (size_t)h->numregions * row) != hipSuccess)
+        return fail(SML_ERR_NOMEM, "exchange buffers");
+    return SML_OK;
+}
+
 // dispatch serialised by the runtime or a profiler: the HIP runtime's
 // AMD_SERIALIZE_KERNEL, rocprofv3's counter collection (ROCPROF_COUNTER_COLLECTION,
 // set by `rocprofv3 --pmc` / `-i`)
@@ -361,7 +455,9 @@ extern "C" int sml_hybrid_destroy(sml_hybrid *h) {
     }
     for (hipEvent_t e : h->ev)
         if (e) (void)hipEventDestroy(e);
-    void *ptrs[] = {h->d_send, h->d_recv, h->d_glob, h->d_perm, h->d_seq};
+    sml_hybrid::Slab &sl = h->slab;
+    void *ptrs[] = {h->d_send, h->d_recv, h->d_glob, h->d_perm, h->d_seq, sl.d_fb, sl.d_ov, sl.d_ring, sl.d_sst, sl.d_ms,
+                    sl.d_ring_src, sl.d_row, sl.d_sst_src, sl.d_sfb, sl.d_sgrid, sl.d_sreg};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     delete h;
@@ -447,25 +543,17 @@ extern "C" int sml_hybrid_create(sml_reservoirs *res, sml_dynamics *dyn, sml_com
     if (hipMalloc(&h->d_seq, 2 * sizeof(uint64_t)) != hipSuccess ||
         hipMemset(h->d_seq, 0, 2 * sizeof(uint64_t)) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
         return bail(fail(SML_ERR_HIP, "sequence counters"));
+    h->xw = h->nout;
     if (world > 1) {
         std::vector<int32_t> perm(h->numregions);
         int contig = 1;
         if (int rc = sml_exchange_plan(h->numregions, world, &h->maxc, &contig, perm.data())) return bail(rc);
         h->contiguous = contig != 0;
-        const size_t nout = h->nout;
-        // the staging buffers of the loop's own all-gather (a transport-less rank
-        // descriptor gets its slabs from the host: sml_hybrid_advance_slabs)
-        if (comm->comm &&
-            (hipMalloc(&h->d_send, (size_t)h->maxc * nout * 8) != hipSuccess ||
-             hipMalloc(&h->d_recv, (size_t)world * h->maxc * nout * 8) != hipSuccess ||
-             hipMemset(h->d_send, 0, (size_t)h->maxc * nout * 8) != hipSuccess))
+        if (!h->contiguous &&
+            (hipMalloc(&h->d_perm, (size_t)h->numregions * 4) != hipSuccess ||
+             hipMemcpy(h->d_perm, perm.data(), perm.size() * 4, hipMemcpyHostToDevice) != hipSuccess))
             return bail(fail(SML_ERR_NOMEM, "exchange buffers"));
-        if (!h->contiguous) {
-            if (hipMalloc(&h->d_glob, (size_t)h->numregions * nout * 8) != hipSuccess ||
-                hipMalloc(&h->d_perm, (size_t)h->numregions * 4) != hipSuccess ||
-                hipMemcpy(h->d_perm, perm.data(), perm.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
-                return bail(fail(SML_ERR_NOMEM, "exchange buffers"));
-        }
+        if (int rc = alloc_exchange(h)) return bail(rc);
     }
     *out = h;
     return SML_OK;
@@ -556,6 +644,217 @@ extern "C" int sml_hybrid_start(sml_hybrid *h, const double *d_g4, const double 
     return SML_OK;
 }
 
+// ------------------------------------------------------------------ slab ocean
+namespace {
+
+// predict_slab_ml for every slab reservoir of the rank on a slab step
+// (parallelmain.f90:236-249: mod(t*timestep, timestep_slab) == 0, the default
+// ml_only_ocean set by initialize_slab_ocean_model): the feedback is the mean of the
+// ring as the previous step's sendrecievegrid left it (mpires.f90:757), and the new
+// sst goes into the exchange rows
+int slab_predict(sml_hybrid *h) {
+    sml_hybrid::Slab &sl = h->slab;
+    if (!sl.res) return SML_OK;
+    if (!sl.started) return fail(SML_ERR_STATE, "sml_hybrid_start_slab first");
+    const int64_t tt = h->t + 1;
+    if ((tt * sl.timestep) % sl.timestep_slab != 0 || sl.nslab == 0) return SML_OK;
+    hipStream_t m = h->main;
+    hipLaunchKernelGGL(k_slab_avg, dim3((sl.tot_fb + 255) / 256), dim3(256), 0, m, sl.d_ring, sl.ratio - 1, sl.tot_fb,
+                       sl.d_fb);
+    SML_HIP(hipGetLastError());
+    if (int rc = sml_res_step(sl.res, sl.d_fb, nullptr, sl.d_ov, m)) return rc;
+    const int n = sl.nslab * sl.nsst;
+    hipLaunchKernelGGL(k_slab_rows, dim3((n + 255) / 256), dim3(256), 0, m, sl.d_ov, sl.d_row, sl.nslab, sl.nsst,
+                       h->nlocal, h->nout, h->xw, false, h->ov);
+    SML_HIP(hipGetLastError());
+    sl.dirty = true;
+    return SML_OK;
+}
+
+// sendrecievegrid's sst half (mpires.f90:288-319, 458-472, 575-581, 733-736) after a
+// change of any region's slab sst: wholegrid_sst from the exchange rows, the atmo
+// feedback's sst entries, and run_model's sst_hybrid into the window (cpl_sea.f90:38-46)
+int slab_sst(sml_hybrid *h, const double *d_all) {
+    sml_hybrid::Slab &sl = h->slab;
+    if (!sl.res || !sl.dirty) return SML_OK;
+    hipStream_t m = h->main;
+    hipLaunchKernelGGL(k_sst_grid, dim3((kGrid2d + 255) / 256), dim3(256), 0, m, d_all, sl.d_sst_src, sl.base, sl.mask,
+                       sl.d_sst);
+    SML_HIP(hipGetLastError());
+    if (sl.n_sst_el) {
+        hipLaunchKernelGGL(k_sst_feedback, dim3((sl.n_sst_el + 255) / 256), dim3(256), 0, m, sl.d_sst, sl.d_sfb,
+                           sl.d_sgrid, sl.d_sreg, sl.d_ms, sl.n_sst_el, h->fb);
+        SML_HIP(hipGetLastError());
+    }
+    if (int rc = sml_dyn_set_hybrid_sst(h->dyn, sl.d_sst, sl.sst_bias, m)) return rc;
+    sl.dirty = false;
+    return SML_OK;
+}
+
+template <typename T>
+int upload(T **d, const std::vector<T> &v) {
+    if (hipMalloc(d, std::max<size_t>(v.size(), 1) * sizeof(T)) != hipSuccess) return fail(SML_ERR_NOMEM, "slab tables");
+    if (!v.empty()) SML_HIP(hipMemcpy(*d, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+    return SML_OK;
+}
+
+}  // namespace
+
+// the slab ocean in the loop (parallelmain.f90:216-249, sendrecievegrid's sst half).
+// Before sml_hybrid_set_buffers: the exchange rows widen to nout + resx*resy.
+extern "C" int sml_hybrid_set_slab(sml_hybrid *h, sml_reservoirs *slab, const double *d_base_sst,
+                                   const double *d_sea_mask, int timestep, int timestep_slab, double sst_bias) {
+    SML_REQUIRE(h && slab && d_base_sst && d_sea_mask, "null argument");
+    SML_REQUIRE(!h->slab.res, "the slab ocean is set already");
+    SML_REQUIRE(!h->ov, "sml_hybrid_set_slab must precede sml_hybrid_set_buffers (the exchange rows widen)");
+    SML_REQUIRE(timestep > 0 && timestep_slab % timestep == 0 && timestep_slab / timestep >= 2,
+                "timestep_slab (%d) must be a multiple >= 2 of timestep (%d)", timestep_slab, timestep);
+    int snum = 0, nslab = 0, sncs = 0, snout = 0;
+    if (int rc = sml_res_info(slab, &snum, &nslab, &sncs, &snout, nullptr)) return rc;
+    SML_REQUIRE(snum == h->numregions && sncs == 0, "the slab context must be ML-only (chunk_speedy 0) over the "
+                "same %d regions", h->numregions);
+    RegionGeom g0;
+    SML_REQUIRE(region_geom(h->numregions, 0, &g0) && snout == g0.resx * g0.resy,
+                "the slab reservoirs predict the sst of the region's %d points, not %d", g0.resx * g0.resy, snout);
+    std::vector<int> ids(h->nlocal), sids(nslab);
+    std::vector<int64_t> off(h->nlocal + 1), soff(nslab + 1);
+    if (int rc = sml_res_info(h->res, nullptr, nullptr, nullptr, nullptr, ids.data())) return rc;
+    if (int rc = sml_res_info(slab, nullptr, nullptr, nullptr, nullptr, sids.data())) return rc;
+    if (int rc = sml_res_feedback_offsets(h->res, off.data())) return rc;
+    if (int rc = sml_res_feedback_offsets(slab, soff.data())) return rc;
+    // the slab reservoirs are those of the rank's regions with an sst input, in order
+    // (trained_ocean_reservoir_prediction: sst_bool_prediction <=> sst input)
+    std::vector<int32_t> ring_src, row, sfb, sgrid;
+    std::vector<uint16_t> sreg;
+    int j = 0;
+    for (int i = 0; i < h->nlocal; ++i) {
+        RegionGeom g;
+        region_geom(h->numregions, ids[i], &g);
+        const int in2d = g.inx * g.iny, natmo = kVars * in2d * kZGrid;
+        int ninp = 0;
+        if (int rc = sml_res_ninp(h->res, i, &ninp)) return rc;
+        const bool sst = ninp == region_ninp(g, true);
+        if (!sst) continue;
+        SML_REQUIRE(j < nslab && sids[j] == ids[i], "slab reservoir %d is not the rank's sst region %d (local %d)", j,
+                    ids[i], i);
+        int sninp = 0;
+        if (int rc = sml_res_ninp(slab, j, &sninp)) return rc;
+        SML_REQUIRE(sninp == 7 * in2d && soff[j + 1] - soff[j] == sninp,
+                    "slab reservoir of region %d: %d inputs, the atmo subset has %d", ids[i], sninp, 7 * in2d);
+        // atmo_training_data_idx (mod_slab_ocean_reservoir.f90:1550-1563): the lowest
+        // level's 4 variables and logp, the sst, the tisr of the atmo feedback
+        for (int e = natmo - kVars * in2d; e < natmo + in2d; ++e) ring_src.push_back((int32_t)(off[i] + e));
+        for (int e = natmo + 2 * in2d; e < natmo + 4 * in2d; ++e) ring_src.push_back((int32_t)(off[i] + e));
+        row.push_back(i);
+        for (int p = 0; p < in2d; ++p) {  // the sst entries of the atmo feedback
+            const int lx = p % g.inx, ly = p / g.inx;
+            sfb.push_back((int32_t)(off[i] + natmo + 2 * in2d + p));
+            sgrid.push_back(g2(input_x(g, lx + 1) - 1, g.in_ystart - 1 + ly));
+            sreg.push_back((uint16_t)j);
+        }
+        ++j;
+    }
+    SML_REQUIRE(j == nslab, "%d slab reservoirs for %d sst regions", nslab, j);
+    // wholegrid_sst point -> its region's exchange row and sst column
+    const int xw = h->nout + snout;
+    std::vector<int32_t> src(kGrid2d, -1);
+    for (int r = 0; r < h->numregions; ++r) {
+        RegionGeom g;
+        region_geom(h->numregions, r, &g);
+        for (int ly = 0; ly < g.resy; ++ly)
+            for (int lx = 0; lx < g.resx; ++lx)
+                src[g2(g.res_xstart - 1 + lx, g.res_ystart - 1 + ly)] = r * xw + h->nout + lx + g.resx * ly;
+    }
+    sml_hybrid::Slab &sl = h->slab;
+    sl.nslab = nslab;
+    sl.nsst = snout;
+    sl.ratio = timestep_slab / timestep;
+    sl.timestep = timestep;
+    sl.timestep_slab = timestep_slab;
+    sl.sst_bias = sst_bias;
+    sl.base = d_base_sst;
+    sl.mask = d_sea_mask;
+    sl.tot_fb = (int)ring_src.size();
+    sl.n_sst_el = (int)sfb.size();
+    if (int rc = upload(&sl.d_ring_src, ring_src)) return rc;
+    if (int rc = upload(&sl.d_row, row)) return rc;
+    if (int rc = upload(&sl.d_sst_src, src)) return rc;
+    if (int rc = upload(&sl.d_sfb, sfb)) return rc;
+    if (int rc = upload(&sl.d_sgrid, sgrid)) return rc;
+    if (int rc = upload(&sl.d_sreg, sreg)) return rc;
+    if (hipMalloc(&sl.d_fb, std::max<size_t>(sl.tot_fb, 1) * 8) != hipSuccess ||
+        hipMalloc(&sl.d_ov, std::max<size_t>((size_t)nslab * snout, 1) * 8) != hipSuccess ||
+        hipMalloc(&sl.d_ring, std::max<size_t>((size_t)(sl.ratio - 1) * sl.tot_fb, 1) * 8) != hipSuccess ||
+        hipMalloc(&sl.d_sst, (size_t)kGrid2d * 8) != hipSuccess ||
+        hipMalloc(&sl.d_ms, std::max<size_t>((size_t)2 * nslab, 1) * 8) != hipSuccess)
+        return fail(SML_ERR_NOMEM, "slab buffers");
+    SML_HIP(hipMemset(sl.d_sst, 0, (size_t)kGrid2d * 8));
+    h->xw = xw;
+    if (int rc = sml_res_set_outvec_ld(h->res, xw)) return rc;
+    if (h->comm && h->comm->world > 1)
+        if (int rc = alloc_exchange(h)) return rc;
+    sl.res = slab;
+    return SML_OK;
+}
+
+// start_prediction_slab's hand-over (mod_slab_ocean_reservoir.f90:769-800,
+// parallelmain.f90:216-222): the slab reservoirs' sst [nslab][resx*resy] until their
+// first prediction (the host synchronizes their states, sml_res_start_prediction);
+// 272 K in the exchange rows of regions without a slab (mpires.f90:366-372); the
+// ring of averaged inputs cleared (initialize_prediction_slab, :747-748).  After
+// sml_hybrid_start, before the first step; the first step's exchange builds the SST.
+extern "C" int sml_hybrid_start_slab(sml_hybrid *h, const double *d_slab_outvec) {
+    SML_REQUIRE(h && h->slab.res, "sml_hybrid_set_slab first");
+    SML_REQUIRE(h->ov && h->started, "sml_hybrid_start first");
+    sml_hybrid::Slab &sl = h->slab;
+    SML_REQUIRE(sl.nslab == 0 || d_slab_outvec, "null slab outvec");
+    std::vector<double> ms(2 * std::max(sl.nslab, 1));
+    for (int j = 0; j < sl.nslab; ++j) {
+        double mean[36], stdv[36];
+        if (int rc = sml_res_mean_std(sl.res, j, mean, stdv)) return rc;
+        ms[2 * j] = mean[35];  // sst_mean_std_idx = the atmo grid's, 36 (mod_slab_ocean_reservoir.f90:1548)
+        ms[2 * j + 1] = stdv[35];
+    }
+    hipStream_t m = h->main;
+    SML_HIP(hipMemcpyAsync(sl.d_ms, ms.data(), ms.size() * 8, hipMemcpyHostToDevice, m));
+    SML_HIP(hipMemsetAsync(sl.d_ring, 0, (size_t)(sl.ratio - 1) * sl.tot_fb * 8, m));
+    const int nfill = h->nlocal * sl.nsst, n = sl.nslab * sl.nsst;
+    hipLaunchKernelGGL(k_slab_rows, dim3((nfill + 255) / 256), dim3(256), 0, m, nullptr, nullptr, 0, sl.nsst, h->nlocal,
+                       h->nout, h->xw, true, h->ov);
+    if (n) {
+        SML_HIP(hipMemcpyAsync(sl.d_ov, d_slab_outvec, (size_t)n * 8, hipMemcpyDeviceToDevice, m));
+        hipLaunchKernelGGL(k_slab_rows, dim3((n + 255) / 256), dim3(256), 0, m, sl.d_ov, sl.d_row, sl.nslab, sl.nsst,
+                           h->nlocal, h->nout, h->xw, false, h->ov);
+    }
+    SML_HIP(hipGetLastError());
+    SML_HIP(hipStreamSynchronize(m));
+    sl.dirty = true;
+    sl.started = true;
+    return SML_OK;
+}
+
+// the exchange row length: nout, or nout + the slab sst of the region's points
+extern "C" int sml_hybrid_exchange_width(const sml_hybrid *h, int *width) {
+    SML_REQUIRE(h && width, "null argument");
+    *width = h->xw;
+    return SML_OK;
+}
+
+// the slab state for hosts and tests: wholegrid_sst(96, 48) of the last exchange, the
+// ring [timestep_slab/timestep - 1][tot] of averaged inputs (tot = *ring_len), the
+// last slab feedback and slab outvecs [nslab][resx*resy]
+extern "C" int sml_hybrid_slab_buffers(const sml_hybrid *h, const double **d_sst_grid, const double **d_ring,
+                                       int *ring_len, const double **d_slab_feedback, const double **d_slab_outvec) {
+    SML_REQUIRE(h && h->slab.res, "no slab ocean in this loop");
+    const sml_hybrid::Slab &sl = h->slab;
+    if (d_sst_grid) *d_sst_grid = sl.d_sst;
+    if (d_ring) *d_ring = sl.d_ring;
+    if (ring_len) *ring_len = sl.tot_fb;
+    if (d_slab_feedback) *d_slab_feedback = sl.d_fb;
+    if (d_slab_outvec) *d_slab_outvec = sl.d_ov;
+    return SML_OK;
+}
+
 // predict for every local region (parallelmain.f90:225-234): the local outvecs in
 // d_outvec on the main stream
 extern "C" int sml_hybrid_predict(sml_hybrid *h) {
@@ -564,12 +863,14 @@ extern "C" int sml_hybrid_predict(sml_hybrid *h) {
     if (h->predicted) return fail(SML_ERR_STATE, "sml_hybrid_predict twice without sml_hybrid_advance");
     if (h->overlap) {
         if (int rc = sml_res_step_begin(h->res, h->fb, h->main)) return rc;
+        if (int rc = slab_predict(h)) return rc;
         // SPEEDY's forecast of the previous window
         if (int rc = hop_wait(h, sml_hybrid::kHopLm, h->main)) return rc;
         // the local-model tiling fused into the v_p finish: one launch fewer on the critical path
         if (int rc = sml_res_step_finish_grid(h->res, h->f4, h->f2, h->lm, h->ov, h->main)) return rc;
     } else {  // one pass over W_out: the same sums as begin + finish
         if (int rc = sml_res_step(h->res, h->fb, h->lm, h->ov, h->main)) return rc;
+        if (int rc = slab_predict(h)) return rc;
     }
     h->predicted = true;
     return SML_OK;
@@ -582,6 +883,7 @@ extern "C" int sml_hybrid_advance(sml_hybrid *h, const double *d_outvec_all) {
     if (!h->predicted) return fail(SML_ERR_STATE, "sml_hybrid_advance without sml_hybrid_predict");
     hipStream_t m = h->main, s = h->side;
     if (int rc = sml_exchange_assemble(h->res, d_outvec_all, h->g4, h->g2, h->pr, m)) return rc;
+    if (int rc = slab_sst(h, d_outvec_all)) return rc;
     if (h->overlap)
         if (int rc = hop_signal(h, sml_hybrid::kHopGrid, m)) return rc;
     ++h->t;
@@ -596,6 +898,13 @@ extern "C" int sml_hybrid_advance(sml_hybrid *h, const double *d_outvec_all) {
             return fail(SML_ERR_ARG, "tisr hour %d outside the table's %d hours", idx, h->tisr_nhours);
         if (int rc = sml_res_tile_tisr_field(h->res, h->tisr_table + (size_t)(idx - 1) * kGrid2d, h->fb, m))
             return rc;
+    }
+    if (h->slab.res && h->slab.tot_fb) {  // averaged_atmo_input_vec(:, mod(t-1, R-1)+1), mpires.f90:755
+        sml_hybrid::Slab &sl = h->slab;
+        double *col = sl.d_ring + (size_t)((h->t - 1) % (sl.ratio - 1)) * sl.tot_fb;
+        hipLaunchKernelGGL(k_slab_ring, dim3((sl.tot_fb + 255) / 256), dim3(256), 0, m, h->fb, sl.d_ring_src, sl.tot_fb,
+                           col);
+        SML_HIP(hipGetLastError());
     }
     if (h->overlap)
         if (int rc = hop_wait(h, sml_hybrid::kHopGrid, s)) return rc;
@@ -619,9 +928,9 @@ extern "C" int sml_hybrid_advance_slabs(sml_hybrid *h, const double *d_recv) {
     const int world = h->comm ? h->comm->world : 1;
     if (world == 1 || h->contiguous) return sml_hybrid_advance(h, d_recv);
     if (!h->predicted) return fail(SML_ERR_STATE, "sml_hybrid_advance_slabs without sml_hybrid_predict");
-    const int total = h->numregions * h->nout;
+    const int total = h->numregions * h->xw;
     hipLaunchKernelGGL(k_gather_rows, dim3((total + 255) / 256), dim3(256), 0, h->main, d_recv, h->d_perm, h->d_glob,
-                       h->nout, total);
+                       h->xw, total);
     SML_HIP(hipGetLastError());
     return sml_hybrid_advance(h, h->d_glob);
 }
@@ -644,10 +953,10 @@ extern "C" int sml_hybrid_step(sml_hybrid *h) {
     // critical path; d_send's padding rows stay zero)
     const double *send = h->ov;
     if (h->nlocal != h->maxc) {
-        SML_HIP(hipMemcpyAsync(h->d_send, h->ov, (size_t)h->nlocal * h->nout * 8, hipMemcpyDeviceToDevice, h->main));
+        SML_HIP(hipMemcpyAsync(h->d_send, h->ov, (size_t)h->nlocal * h->xw * 8, hipMemcpyDeviceToDevice, h->main));
         send = h->d_send;
     }
-    if (int rc = sml_comm_allgather(h->comm, send, h->d_recv, (int64_t)h->maxc * h->nout, h->main)) return rc;
+    if (int rc = sml_comm_allgather(h->comm, send, h->d_recv, (int64_t)h->maxc * h->xw, h->main)) return rc;
     return sml_hybrid_advance_slabs(h, h->d_recv);
 }
 

@@ -70,6 +70,9 @@ struct RegionDev {
 
 struct sml_reservoirs {
     int numregions = 0, nlocal = 0, ncs = 0, nout = 0, nout_pad = 0, wdtype = SML_F32;
+    // row stride of the outvec arrays (sml_res_set_outvec_ld): nout, or wider when the
+    // hybrid loop carries the slab ocean's sst beside each outvec in its exchange rows
+    int ov_ld = 0;
     double leakage = 1.0;
     std::vector<int> region_ids, n, k, ninp, ld;
     std::vector<unsigned char> sst, loaded;
@@ -119,6 +122,7 @@ struct sml_reservoirs {
     int32_t *d_lm_src = nullptr;    // [nlocal*ncs]
     uint8_t *d_lm_l = nullptr;
     double *d_io = nullptr;         // staging for sml_res_step_host
+    size_t d_io_n = 0;
     std::vector<hipEvent_t> ev;     // 3 events per timed step (start, update done, readout done)
     int ev_cap = 0, ev_used = 0;
     bool timing = false;
@@ -400,8 +404,8 @@ __global__ __launch_bounds__(512) void k_res_readout(const RegionDev *__restrict
                                                      const double *__restrict__ local_model,
                                                      const double *__restrict__ meanstd,
                                                      const int8_t *__restrict__ outl, double *__restrict__ part,
-                                                     double *__restrict__ outvec, int nout, int nout_pad, int ncs,
-                                                     int groups, int nitems, int ipw) {
+                                                     double *__restrict__ outvec, int nout, int ov_ld, int nout_pad,
+                                                     int ncs, int groups, int nitems, int ipw) {
     // wave gw takes the items gw, gw + W, gw + 2W, .. (W waves; one item each unless
     // the launch is paced): the waves in flight together work on consecutive items.
     // NR = kRowsWide (17 rows a wave, 8 waves a region of 136 outputs): x_aug is read
@@ -446,7 +450,7 @@ __global__ __launch_bounds__(512) void k_res_readout(const RegionDev *__restrict
                 for (int q = 1; q < NR; ++q)
                     if (lane == q) vml = ml.v[q];
                 const double vp = vp_sum(wlm + rg.wlm, nout_pad, local_model + (size_t)r * ncs, ncs, o);
-                outvec[(size_t)r * nout + o] = unstd(vp + vml, meanstd + (size_t)r * 2 * kMeanStd, outl[o]);
+                outvec[(size_t)r * ov_ld + o] = unstd(vp + vml, meanstd + (size_t)r * 2 * kMeanStd, outl[o]);
             }
         }
     }
@@ -462,15 +466,15 @@ __global__ __launch_bounds__(256) void k_res_finish(const RegionDev *__restrict_
                                                     const double *__restrict__ local_model,
                                                     const double *__restrict__ meanstd,
                                                     const int8_t *__restrict__ outl, const double *__restrict__ part,
-                                                    double *__restrict__ outvec, int nout, int nout_pad, int ncs,
-                                                    int nlocal, double *__restrict__ raw = nullptr) {
+                                                    double *__restrict__ outvec, int nout, int ov_ld, int nout_pad,
+                                                    int ncs, int nlocal, double *__restrict__ raw = nullptr) {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     const int r = t / nout_pad, o = t % nout_pad;
     if (r >= nlocal || o >= nout) return;
     const double vp = vp_sum(wlm + R[r].wlm, nout_pad, local_model + (size_t)r * ncs, ncs, o);
     const double v = vp + part[(size_t)r * nout_pad + o];
     if (raw) raw[(size_t)r * nout + o] = v;
-    outvec[(size_t)r * nout + o] = unstd(v, meanstd + (size_t)r * 2 * kMeanStd, outl[o]);
+    outvec[(size_t)r * ov_ld + o] = unstd(v, meanstd + (size_t)r * 2 * kMeanStd, outl[o]);
 }
 
 // sml_res_step_finish_grid: k_tile_local_model + k_res_finish in one launch, one
@@ -484,7 +488,7 @@ __global__ __launch_bounds__(256) void k_res_finish_grid(
     const RegionDev *__restrict__ R, const WT *__restrict__ wlm, const int32_t *__restrict__ src,
     const uint8_t *__restrict__ lidx, const double *__restrict__ fc4, const double *__restrict__ fc2,
     double *__restrict__ lm_out, const double *__restrict__ meanstd, const int8_t *__restrict__ outl,
-    const double *__restrict__ part, double *__restrict__ outvec, int nout, int nout_pad, int ncs) {
+    const double *__restrict__ part, double *__restrict__ outvec, int nout, int ov_ld, int nout_pad, int ncs) {
     __shared__ double slm[kMaxNcs];
     const int r = blockIdx.x, t = threadIdx.x;
     const double *ms = meanstd + (size_t)r * 2 * kMeanStd;
@@ -501,18 +505,18 @@ __global__ __launch_bounds__(256) void k_res_finish_grid(
     __syncthreads();
     for (int o = t; o < nout; o += blockDim.x) {
         const double vp = vp_sum(wlm + R[r].wlm, nout_pad, slm, ncs, o);
-        outvec[(size_t)r * nout + o] = unstd(vp + part[(size_t)r * nout_pad + o], ms, outl[o]);
+        outvec[(size_t)r * ov_ld + o] = unstd(vp + part[(size_t)r * nout_pad + o], ms, outl[o]);
     }
 }
 
 // assemble: all regions' outvecs -> global grids, with the root's clips
 __global__ void k_assemble(const int32_t *__restrict__ dst, const double *__restrict__ ov, double *__restrict__ g4,
-                           double *__restrict__ g2, double *__restrict__ pr, int total) {
+                           double *__restrict__ g2, double *__restrict__ pr, int total, int nout, int ov_ld) {
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= total) return;
     const int d = dst[e];
     if (d < 0) return;
-    double v = ov[e];
+    double v = ov_ld == nout ? ov[e] : ov[(size_t)(e / nout) * ov_ld + e % nout];
     if (d < kGrid4d) {
         if ((d & 3) == 3 && v < 0.000001) v = 0.000001;  // mpires.f90:448-450
         g4[d] = v;
@@ -949,6 +953,7 @@ int res_create_impl(int numregions, int nlocal, const int *region_ids, const uns
     c->ncs = chunk_speedy;
     c->nout = nout;
     c->nout_pad = (nout + kRows - 1) / kRows * kRows;
+    c->ov_ld = nout;
     c->wdtype = weight_dtype;
     c->leakage = leakage;
     c->generic = ninp_generic != nullptr;
@@ -1079,6 +1084,15 @@ int res_create_impl(int numregions, int nlocal, const int *region_ids, const uns
 }
 }  // namespace
 
+// the row stride of every outvec array the context writes (sml_res_step*, the
+// finish kernels) and of sml_exchange_assemble's input (>= nout)
+extern "C" int sml_res_set_outvec_ld(sml_reservoirs *c, int ld) {
+    SML_REQUIRE(c && ld >= c->nout, "bad outvec row stride %d", ld);
+    SML_REQUIRE(!c->begun, "sml_res_set_outvec_ld inside a begun step");
+    c->ov_ld = ld;
+    return SML_OK;
+}
+
 extern "C" int sml_res_info(const sml_reservoirs *c, int *numregions, int *nlocal, int *chunk_speedy, int *nout,
                             int *region_ids) {
     SML_REQUIRE(c, "null context");
@@ -1094,6 +1108,15 @@ extern "C" int sml_res_ninp(const sml_reservoirs *c, int i, int *ninp) {
     if (int rc = check_region(c, i)) return rc;
     SML_REQUIRE(ninp, "ninp is null");
     *ninp = c->ninp[i];
+    return SML_OK;
+}
+
+// the mean / std (36 each) local region i standardizes with (host copy of the loaded ones)
+extern "C" int sml_res_mean_std(const sml_reservoirs *c, int i, double *mean, double *std) {
+    if (int rc = check_region(c, i)) return rc;
+    SML_REQUIRE(mean && std, "null argument");
+    std::memcpy(mean, &c->meanstd_h[(size_t)i * 2 * kMeanStd], kMeanStd * 8);
+    std::memcpy(std, &c->meanstd_h[(size_t)i * 2 * kMeanStd + kMeanStd], kMeanStd * 8);
     return SML_OK;
 }
 
@@ -1229,11 +1252,11 @@ void launch_readout(sml_reservoirs *c, const double *d_local_model, double *d_ou
         if (c->wdtype == SML_F32)
             hipLaunchKernelGGL(k_res_finish<float>, dim3((total + 255) / 256), dim3(256), 0, st, c->d_rd,
                                (const float *)c->d_wlm, d_local_model, c->d_meanstd, c->d_outl, c->d_part, d_outvec,
-                               c->nout, c->nout_pad, c->ncs, c->nlocal, d_raw);
+                               c->nout, c->ov_ld, c->nout_pad, c->ncs, c->nlocal, d_raw);
         else
             hipLaunchKernelGGL(k_res_finish<double>, dim3((total + 255) / 256), dim3(256), 0, st, c->d_rd,
                                (const double *)c->d_wlm, d_local_model, c->d_meanstd, c->d_outl, c->d_part,
-                               d_outvec, c->nout, c->nout_pad, c->ncs, c->nlocal, d_raw);
+                               d_outvec, c->nout, c->ov_ld, c->nout_pad, c->ncs, c->nlocal, d_raw);
     } else {
         const bool wide = c->nout_pad % kRowsWide == 0 && c->nout_pad / kRowsWide <= 8;
         const int rows = wide ? kRowsWide : kRows;
@@ -1252,7 +1275,7 @@ void launch_readout(sml_reservoirs *c, const double *d_local_model, double *d_ou
             constexpr int R = decltype(r_tag)::value;
             hipLaunchKernelGGL((k_res_readout<WT, kMode, R>), dim3(nblocks), dim3(64 * wpb), 0, st, c->d_rd,
                                (const WT *)c->d_wout, (const WT *)c->d_wlm, c->d_xaug, d_local_model, c->d_meanstd,
-                               c->d_outl, c->d_part, d_outvec, c->nout, c->nout_pad, c->ncs, groups, nitems, ipw);
+                               c->d_outl, c->d_part, d_outvec, c->nout, c->ov_ld, c->nout_pad, c->ncs, groups, nitems, ipw);
         };
         using RW = std::integral_constant<int, kRowsWide>;
         using RN = std::integral_constant<int, kRows>;
@@ -1337,11 +1360,11 @@ extern "C" int sml_res_step_finish_grid(sml_reservoirs *c, const double *d_fc4d,
     if (c->wdtype == SML_F32)
         hipLaunchKernelGGL(k_res_finish_grid<float>, dim3(c->nlocal), dim3(256), 0, st, c->d_rd,
                            (const float *)c->d_wlm, c->d_lm_src, c->d_lm_l, d_fc4d, d_fc2d, d_local_model,
-                           c->d_meanstd, c->d_outl, c->d_part, d_outvec, c->nout, c->nout_pad, c->ncs);
+                           c->d_meanstd, c->d_outl, c->d_part, d_outvec, c->nout, c->ov_ld, c->nout_pad, c->ncs);
     else
         hipLaunchKernelGGL(k_res_finish_grid<double>, dim3(c->nlocal), dim3(256), 0, st, c->d_rd,
                            (const double *)c->d_wlm, c->d_lm_src, c->d_lm_l, d_fc4d, d_fc2d, d_local_model,
-                           c->d_meanstd, c->d_outl, c->d_part, d_outvec, c->nout, c->nout_pad, c->ncs);
+                           c->d_meanstd, c->d_outl, c->d_part, d_outvec, c->nout, c->ov_ld, c->nout_pad, c->ncs);
     SML_HIP(hipGetLastError());
     c->begun = false;
     return SML_OK;
@@ -1409,14 +1432,19 @@ extern "C" int sml_res_step_host(sml_reservoirs *c, const double *feedback, cons
                                  double *outvec) {
     SML_REQUIRE(c && feedback && outvec, "null argument");
     SML_REQUIRE(c->ncs == 0 || local_model, "hybrid context needs local_model");
-    const size_t nfb = c->tot_fb, nlm = (size_t)c->nlocal * c->ncs, nov = (size_t)c->nlocal * c->nout;
-    if (!c->d_io)
+    const size_t nfb = c->tot_fb, nlm = (size_t)c->nlocal * c->ncs, nov = (size_t)c->nlocal * c->ov_ld;
+    if (c->d_io_n != nfb + nlm + nov) {  // sized for the current outvec stride
+        if (c->d_io) SML_HIP(hipFree(c->d_io));
+        c->d_io = nullptr;
         if (int rc = dalloc(&c->d_io, nfb + nlm + nov)) return rc;
+        c->d_io_n = nfb + nlm + nov;
+    }
     double *dfb = c->d_io, *dlm = dfb + nfb, *dov = dlm + nlm;
     SML_HIP(hipMemcpy(dfb, feedback, nfb * 8, hipMemcpyHostToDevice));
     if (nlm) SML_HIP(hipMemcpy(dlm, local_model, nlm * 8, hipMemcpyHostToDevice));
     if (int rc = sml_res_step(c, dfb, dlm, dov, nullptr)) return rc;
-    SML_HIP(hipMemcpy(outvec, dov, nov * 8, hipMemcpyDeviceToHost));
+    SML_HIP(hipMemcpy2D(outvec, (size_t)c->nout * 8, dov, (size_t)c->ov_ld * 8, (size_t)c->nout * 8, c->nlocal,
+                        hipMemcpyDeviceToHost));
     return SML_OK;
 }
 
@@ -1444,7 +1472,7 @@ extern "C" int sml_exchange_assemble(sml_reservoirs *c, const double *d_outvec_a
     SML_REQUIRE(!c->generic, "a generic (slab) context has no exchange tables");
     const int total = c->numregions * c->nout;
     hipLaunchKernelGGL(k_assemble, dim3((total + 255) / 256), dim3(256), 0, (hipStream_t)stream, c->d_asm_dst,
-                       d_outvec_all, d_grid4d, d_grid2d, d_precip, total);
+                       d_outvec_all, d_grid4d, d_grid2d, d_precip, total, c->nout, c->ov_ld);
     SML_HIP(hipGetLastError());
     return SML_OK;
 }

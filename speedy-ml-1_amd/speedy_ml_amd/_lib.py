@@ -53,6 +53,8 @@ EXPORTED = (
     "sml_res_create_generic", "sml_res_step_slab", "sml_res_start_prediction",
     "sml_comm_create_local", "sml_exchange_plan", "sml_hybrid_advance_slabs", "sml_hybrid_set_hop_mode",
     "sml_hybrid_hop_mode", "sml_calendar_delta_hour", "sml_hybrid_set_feb29", "sml_hybrid_get_feb29",
+    "sml_res_mean_std", "sml_res_set_outvec_ld", "sml_hybrid_set_slab", "sml_hybrid_start_slab",
+    "sml_hybrid_exchange_width", "sml_hybrid_slab_buffers", "sml_dyn_set_hybrid_sst", "sml_dyn_set_sea_ice",
 )
 
 SML_HOP_AUTO, SML_HOP_WAIT_VALUE, SML_HOP_EVENTS = 0, 1, 2
@@ -212,6 +214,14 @@ def _declare(L: ctypes.CDLL) -> None:
         "sml_calendar_delta_hour": [i, ctypes.c_int64, ip, ip],
         "sml_hybrid_set_feb29": [vp, i],
         "sml_hybrid_get_feb29": [vp, ip],
+        "sml_res_mean_std": [vp, i, vp, vp],
+        "sml_res_set_outvec_ld": [vp, i],
+        "sml_hybrid_set_slab": [vp, vp, vp, vp, i, i, d],
+        "sml_hybrid_start_slab": [vp, vp],
+        "sml_hybrid_exchange_width": [vp, ip],
+        "sml_hybrid_slab_buffers": [vp, pp, pp, ip, pp, pp],
+        "sml_dyn_set_hybrid_sst": [vp, vp, d, vp],
+        "sml_dyn_set_sea_ice": [vp, vp, vp],
     }
     for name, args in sig.items():
         fn = getattr(L, name)

@@ -43,9 +43,12 @@ class HybridLoop:
     tisr inputs (device) or None (feedback tisr entries left as they are)."""
 
     def __init__(self, res, dyn, exchange, device, tisr=None, overlap: bool = True, nleap: int = 24,
-                 speedy_cus: int | None = None, delt: float = DELT, comm=None):
+                 speedy_cus: int | None = None, delt: float = DELT, comm=None, slab=None):
+        """slab: None, or a SlabOcean (the slab-ocean reservoirs of this rank's sst
+        regions and the sst grids; sml_hybrid_set_slab) -- the exchange rows then carry
+        each region's slab sst beside its outvec (`ov` is [nlocal, exchange_width])."""
         self.res, self.dyn, self.exchange, self.tisr, self.comm = res, dyn, exchange, tisr, comm
-        self.overlap, self.nleap = overlap, nleap
+        self.overlap, self.nleap, self.slab = overlap, nleap, slab
         self.dev = torch.device(device)
         self.fb, self.lm, self.ov = res.alloc_io(self.dev)
         z = lambda *s: torch.zeros(s, dtype=torch.float64, device=self.dev)  # noqa: E731
@@ -60,6 +63,13 @@ class HybridLoop:
                                           ALPH, ROB, WIL, int(overlap),
                                           int(speedy_cus if overlap else 0), ctypes.byref(h)))
         self._h = h
+        if slab is not None:
+            check(lib().sml_hybrid_set_slab(h, slab.res.handle, ptr(slab.base_sst), ptr(slab.sea_mask),
+                                            int(slab.timestep), int(slab.timestep_slab), float(slab.sst_bias)))
+            w = ctypes.c_int()
+            check(lib().sml_hybrid_exchange_width(h, ctypes.byref(w)))
+            self.ov = torch.zeros((res.nlocal, w.value), dtype=torch.float64, device=self.dev)
+        self.exchange_width = int(self.ov.shape[1])
         check(lib().sml_hybrid_set_buffers(h, ptr(self.fb), ptr(self.lm if res.ncs else None), ptr(self.ov),
                                            ptr(self.g4), ptr(self.g2), ptr(self.pr), ptr(self.f4), ptr(self.f2),
                                            ptr(tisr)))
@@ -113,6 +123,31 @@ class HybridLoop:
             glob = self.exchange(self.ov)  # RCCL all-gather over xGMI when world > 1
         check(lib().sml_hybrid_advance(self._h, ptr(glob)))
 
+    def start_slab(self, slab_outvec):
+        """start_prediction_slab's hand-over: the slab reservoirs' sst [nslab, 4]
+        (device) until their first prediction (sml_hybrid_start_slab)."""
+        check(lib().sml_hybrid_start_slab(self._h, ptr(slab_outvec)))
+
+    def slab_state(self):
+        """Host copies of the loop's slab state (after its work completes):
+        wholegrid_sst [48, 96], the ring [ratio - 1, tot], the last slab feedback [tot]
+        and slab outvecs [nslab, 4]."""
+        import numpy as np
+
+        sst, ring, fb, ov = (ctypes.c_void_p() for _ in range(4))
+        n = ctypes.c_int()
+        check(lib().sml_hybrid_slab_buffers(self._h, ctypes.byref(sst), ctypes.byref(ring), ctypes.byref(n),
+                                            ctypes.byref(fb), ctypes.byref(ov)))
+        sl = self.slab
+        ratio = sl.timestep_slab // sl.timestep
+        out = {"sst": np.zeros((48, 96)), "ring": np.zeros((ratio - 1, n.value)), "feedback": np.zeros(n.value),
+               "outvec": np.zeros((sl.res.nlocal, 4))}
+        for key, src in (("sst", sst), ("ring", ring), ("feedback", fb), ("outvec", ov)):
+            a = out[key]
+            if a.size:
+                check(lib().sml_copy_to_host(ptr(a), src, a.nbytes))
+        return out
+
     def predict(self):
         """First half of a step: this rank's outvecs into `ov` (main stream)."""
         check(lib().sml_hybrid_predict(self._h))
@@ -142,3 +177,16 @@ class HybridLoop:
 
     def sync(self):
         check(lib().sml_hybrid_sync(self._h))
+
+
+class SlabOcean:
+    """The slab-ocean side of the loop (parallelmain.f90:216-249): `res`, a generic
+    ML-only Reservoirs over this rank's sst regions (7 * in2d inputs each, 4 sst
+    outputs, out_index 35); base_sst / sea_mask [48, 96] device tensors
+    (model_parameters%base_sst_grid / sea_mask, mod_reservoir.f90:845-883); the
+    timesteps in hours (mod_reservoir.f90:36-37: 6 and 168) and current_sst_bias."""
+
+    def __init__(self, res, base_sst, sea_mask, timestep: int = 6, timestep_slab: int = 168, sst_bias: float = 0.0):
+        self.res, self.base_sst, self.sea_mask = res, base_sst, sea_mask
+        self.timestep, self.timestep_slab, self.sst_bias = timestep, timestep_slab, sst_bias
+

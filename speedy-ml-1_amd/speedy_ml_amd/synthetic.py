@@ -107,6 +107,70 @@ def region_weights(region: int, sst: bool, seed: int = 1234, chunk_speedy: int =
     return RegionWeights(region, sst, n, ninp, k, rows, cols, vals, win, wout, mean, std)
 
 
+def slab_weights(region: int, seed: int = 4321, n_override: int | None = None) -> RegionWeights:
+    """A slab-ocean reservoir (initialize_slab_ocean_model, mod_slab_ocean_reservoir.f90:
+    9-134): m = 4000 nodes, degree 6 (density 6/4000), 7 * in2d inputs (the atmo
+    feedback's lowest level's 4 variables, logp, sst, tisr: :1532-1563), the sst of the
+    region's resolved points out (ML only: chunk_speedy 0).  n = NINT(4000/ninp) *
+    ninp, k = int(density n^2); W_in block diagonal, W_out U(-0.01, 0.01), the sst
+    mean / std (slot 36) of the climatology, the rest U(0,1) / 0.5 + U(0,1)."""
+    from .domain import region_geometry
+
+    geo = region_geometry(region)
+    in2d = geo.inx * geo.iny
+    ninp = 7 * in2d
+    q = int(np.floor(4000.0 / ninp + 0.5))
+    if n_override is not None:
+        q = max(1, n_override // ninp)
+    n = q * ninp
+    k = int((6.0 / 4000.0) * n * n)
+    rng = np.random.default_rng([seed, region, 5])
+    rows = np.empty(k, dtype=np.int32)
+    cols = np.empty(k, dtype=np.int32)
+    full, left = divmod(k, n)
+    for b in range(full):
+        rows[b * n:(b + 1) * n] = rng.permutation(n) + 1
+        cols[b * n:(b + 1) * n] = rng.permutation(n) + 1
+    if left:
+        rows[full * n:] = rng.permutation(n)[:left] + 1
+        cols[full * n:] = rng.permutation(n)[:left] + 1
+    vals = (rng.random(k) * (0.9 / 3.0)).astype(np.float32)  # radius 0.9 (:31)
+    win = np.zeros((ninp, n), dtype=np.float32)
+    blk = (0.6 * (2.0 * rng.random((ninp, q)) - 1.0)).astype(np.float32)  # sigma 0.6 (:34)
+    idx = np.arange(ninp)
+    for j in range(q):
+        win[idx, idx * q + j] = blk[:, j]
+    nout = geo.resx * geo.resy
+    wout = ((rng.random((n, nout), dtype=np.float32) * 2.0 - 1.0) * 0.01).astype(np.float32)
+    mean = rng.random(36).astype(np.float32).astype(np.float64)
+    std = (0.5 + rng.random(36)).astype(np.float32).astype(np.float64)
+    cm, cs = climatology_mean_std()
+    mean[35], std[35] = cm[35], cs[35]
+    return RegionWeights(region, True, n, ninp, k, rows, cols, vals, win, wout, mean, std)
+
+
+def slab_fields(seed: int = 77):
+    """Synthetic sea-surface fields on the T30 grid ((48, 96) == Fortran (96, 48)):
+    base_sst_grid (the year's first SST hour, floored at 272 K; mod_reservoir.f90:
+    855-867), sea_mask (1 = land / permanent ice: every hour < 273.1 K, :874-883), and
+    the coupler's sea-ice fraction and temperature (sice_am, tice_am) [ngp]."""
+    rng = np.random.default_rng(seed)
+    lat = np.linspace(-87.16, 87.16, 48)[:, None] * np.pi / 180.0
+    lon = np.arange(96)[None, :] * 2 * np.pi / 96
+    base = 271.0 + 31.0 * np.cos(lat) ** 2 + 0.8 * rng.standard_normal((48, 96))
+    base = np.where(base < 272.0, 272.0, base)
+    mask = ((np.sin(2 * lon) * np.cos(3 * lat) > 0.35) | (np.abs(lat) > 1.35)).astype(np.float64)
+    sice = np.clip((np.abs(lat) - 1.2) * 2.0, 0.0, 1.0) * np.ones((48, 96))
+    tice = 255.0 + 10.0 * rng.random((48, 96))
+    return base, mask, sice.ravel(), tice.ravel()
+
+
+def slab_start_outvec(region: int, seed: int = 88) -> np.ndarray:
+    """start_prediction_slab's outvec of one region: the sst of its 4 points (K)."""
+    rng = np.random.default_rng([seed, region])
+    return 285.0 + 8.0 * rng.standard_normal(4)
+
+
 def initial_state(region: int, n: int, seed: int = 99) -> np.ndarray:
     rng = np.random.default_rng([seed, region, 1])
     return 0.1 * (2.0 * rng.random(n) - 1.0)
