@@ -78,6 +78,10 @@ def parse():
     p.add_argument("--sim-ranks", type=int, default=1,
                    help="diagnostic: run rank 0's share of an N-rank decomposition on this one GPU, the "
                         "all-gather replaced by a local copy (other ranks' outvecs stale); never the headline")
+    p.add_argument("--slab", action=argparse.BooleanOptionalAction, default=True,
+                   help="the slab ocean in the loop, as the reference runs by default (mod_reservoir.f90:41): a "
+                        "slab reservoir per sst region, predict_slab_ml every 168 h (28 steps), its sst in the "
+                        "window (sml_hybrid_set_slab)")
     p.add_argument("--speedy-steps", type=int, default=48,
                    help="leapfrog steps timed in the supplementary SPEEDY-step leg (0 = skip)")
     return p.parse_args()
@@ -96,10 +100,10 @@ def main():
     from speedy_ml_amd import domain
     from speedy_ml_amd.dynamics import Dynamics
     from speedy_ml_amd.exchange import OutvecExchange
-    from speedy_ml_amd.hybrid import HybridLoop
+    from speedy_ml_amd.hybrid import HybridLoop, SlabOcean
     from speedy_ml_amd.reservoir import Reservoirs
-    from speedy_ml_amd.synthetic import (dyn_state, initial_state, phys_boundary, region_weights,
-                                         synthetic_grids)
+    from speedy_ml_amd.synthetic import (dyn_state, initial_state, phys_boundary, region_weights, slab_fields,
+                                         slab_start_outvec, slab_weights, synthetic_grids)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -130,9 +134,22 @@ def main():
         res.set_state(i, initial_state(r, w.n))
         if i % 144 == 0:
             log(rank, f"loaded {i}/{len(regions)} regions ({time.time() - t_setup:.1f}s)")
-    exchange = OutvecExchange(nreg, world, rank, device=dev)
+    slab_ocean, slab_ids = None, []
+    if args.slab:  # the slab-ocean reservoirs of this rank's sst regions (synthetic, n = 4032)
+        slab_ids = [r for r in regions if mask[r]]
+        sws = [slab_weights(r) for r in slab_ids]
+        slab_res = Reservoirs(slab_ids, [0] * len(slab_ids), [w.n for w in sws], [w.k for w in sws], chunk_speedy=0,
+                              nout=4, ninp=[w.ninp for w in sws], out_index=[35] * 4)
+        for j, w in enumerate(sws):
+            slab_res.load_region_weights(j, w)
+            slab_res.set_state(j, initial_state(slab_ids[j], w.n, seed=17))
+        del sws
+        base_h, smask_h, sice_h, tice_h = slab_fields()
+        slab_ocean = SlabOcean(slab_res, torch.from_numpy(base_h).to(dev), torch.from_numpy(smask_h).to(dev))
+        log(rank, f"slab ocean: {len(slab_ids)} slab reservoirs ({time.time() - t_setup:.1f}s)")
+    exchange = OutvecExchange(nreg, world, rank, device=dev, nout=136 + (4 if args.slab else 0))
     if sim > 1:  # rank 0 of `sim` ranks: its outvecs into a global array, the others stale
-        glob_sim = torch.zeros((nreg, 136), dtype=torch.float64, device=dev)
+        glob_sim = torch.zeros((nreg, 136 + (4 if args.slab else 0)), dtype=torch.float64, device=dev)
 
         def exchange(ov_local):
             glob_sim[:len(regions)].copy_(ov_local)
@@ -148,6 +165,11 @@ def main():
     dyn.set_state(st0)
     phys_bc = phys_boundary(dyn, forcing["phis"])
     dyn.set_physics(phys_bc)
+    if slab_ocean is not None:
+        from speedy_ml_amd._lib import check as _check, lib as _lib, ptr as _ptr
+
+        _check(_lib().sml_dyn_set_sea_ice(dyn._h, _ptr(np.ascontiguousarray(sice_h)),
+                                          _ptr(np.ascontiguousarray(tice_h))))
     # the hybrid loop (speedy_ml_amd/hybrid.py); --overlap puts SPEEDY's window on a
     # second stream beside the reservoir update + v_ml readout
     ncu = torch.cuda.get_device_properties(dev).multi_processor_count
@@ -157,9 +179,11 @@ def main():
 
         comm = NativeComm(world, rank)
     loop = HybridLoop(res, dyn, exchange, dev, tisr=tisr, overlap=args.overlap, speedy_cus=args.speedy_cus,
-                      comm=comm)
+                      comm=comm, slab=slab_ocean)
     # initial inputs from the synthetic analysis state (start_prediction analogue)
     loop.start(t(g4h), t(g2h), t(prh), t(f4h), t(f2h))
+    if slab_ocean is not None:
+        loop.start_slab(t(np.stack([slab_start_outvec(r) for r in slab_ids]) if slab_ids else np.zeros((0, 4))))
     fb, lm, ov, g4, g2, pr, f4, f2 = loop.fb, loop.lm, loop.ov, loop.g4, loop.g2, loop.pr, loop.f4, loop.f2
     torch.cuda.synchronize()
     log(rank, f"setup {time.time() - t_setup:.1f}s, {len(regions)} regions on rank 0")
@@ -278,7 +302,11 @@ def main():
                                + ("the library's ncclAllGather on the loop's main stream)" if comm is not None
                                   else "torch.distributed)"))
                             + ", assemble, SPEEDY 6-h window (iogrid(30), stepone + 24 leapfrog dyn_steps with "
-                              "phypar physics, iogrid(31)) on the GPU, re-tile",
+                              "phypar physics, iogrid(31)) on the GPU, re-tile"
+                            + (f"; slab ocean ON ({len(slab_ids)} slab reservoirs of n = 4032 on this rank, "
+                               "predict_slab_ml every 28th step, its sst in the window and the feedback)"
+                               if args.slab else "; slab ocean OFF"),
+                "slab_ocean": bool(args.slab),
                 "regions": nreg,
                 "regions_per_gpu": len(regions),
                 "reservoir_nodes": "5760/6160/6048/5880 (NINT(6000/ninp)*ninp)",
