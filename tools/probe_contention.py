@@ -37,7 +37,7 @@ dyn.set_physics(phys_boundary(dyn, forcing["phis"]))
 L = lib()
 s_side, s_main = ctypes.c_void_p(), ctypes.c_void_p()
 check(L.sml_stream_create_cu_range(0, 64, ctypes.byref(s_side)))
-check(L.sml_stream_create_cu_range(64, 160, ctypes.byref(s_main)))
+check(L.sml_stream_create_cu_range(64, int(os.environ.get("PARTNER_CUS", "192")), ctypes.byref(s_main)))
 side = torch.cuda.ExternalStream(s_side.value, device=dev)
 main = torch.cuda.ExternalStream(s_main.value, device=dev)
 nbytes = 3_700_000_000
