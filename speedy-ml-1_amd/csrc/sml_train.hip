@@ -161,6 +161,103 @@ __global__ __launch_bounds__(256) void k_train_gram(const double *__restrict__ S
             }
 }
 
+// k_train_gram with the LDS stages double-buffered: one barrier per stage instead of
+// two (the next stage's registers go to the other buffer while this one is read),
+// and the LDS rows padded to 144 doubles, so the two 16-lane halves of a ds_read_b64
+// group (consecutive k) fall on disjoint banks (a 132-double row shifts by 8 banks:
+// 2-way conflicts).  The same products summed in the same order as k_train_gram.
+constexpr int kLdsLd2 = kTile + 16;
+__global__ __launch_bounds__(256, 2) void k_train_gram2(const double *__restrict__ S, const double *__restrict__ T,
+                                                     const TrainRegion *__restrict__ regs, int m, int nout, int npad,
+                                                     double *__restrict__ G, double *__restrict__ B) {
+    __shared__ double sA[2][kKC][kLdsLd2];
+    __shared__ double sB[2][kKC][kLdsLd2];
+    const int r = blockIdx.y;
+    const TrainRegion R = regs[r];
+    const int C = npad / kTile;
+    int bi, bj;
+    bool strip;
+    if (!tile_of(blockIdx.x, C, &bi, &bj, &strip)) return;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int wr = w >> 1, wc = w & 1, l16 = lane & 15, kk = lane >> 4;
+    const double *Sr = S + R.s_off, *Tr = T + R.t_off;
+    const int naug = R.naug;
+    const int lrow = tid & (kTile - 1), lt0 = tid >> 7;
+    const int arow = bi * kTile + lrow;
+    const int brow = bj * kTile + lrow;
+    const bool a_ok = strip ? (arow < nout) : (arow < naug);
+    const bool b_ok = brow < naug;
+    const double *pa = strip ? Tr + arow : Sr + arow;
+    const long long lda = strip ? nout : naug;
+    const double *pb = Sr + brow;
+    double ra[kKC / 2], rb[kKC / 2];
+    auto fetch = [&](int t0) {
+#pragma unroll
+        for (int q = 0; q < kKC / 2; ++q) {
+            const int t = t0 + lt0 + 2 * q;
+            ra[q] = (a_ok && t < m) ? pa[(long long)t * lda] : 0.0;
+            rb[q] = (b_ok && t < m) ? pb[(long long)t * naug] : 0.0;
+        }
+    };
+    auto store = [&](int buf) {
+#pragma unroll
+        for (int q = 0; q < kKC / 2; ++q) {
+            sA[buf][lt0 + 2 * q][lrow] = ra[q];
+            sB[buf][lt0 + 2 * q][lrow] = rb[q];
+        }
+    };
+    d4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = d4{0, 0, 0, 0};
+    fetch(0);
+    store(0);
+    __syncthreads();
+    if (kKC < m) fetch(kKC);
+    int cur = 0;
+    for (int t0 = 0; t0 < m; t0 += kKC) {
+#pragma unroll
+        for (int s = 0; s < kKC / 4; ++s) {
+            double a[4], b[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) a[i] = sA[cur][4 * s + kk][wr * 64 + i * 16 + l16];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) b[j] = sB[cur][4 * s + kk][wc * 64 + j * 16 + l16];
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[i][j] = MFMA64(a[i], b[j], acc[i][j]);
+        }
+        if (t0 + kKC < m) {
+            store(cur ^ 1);
+            if (t0 + 2 * kKC < m) fetch(t0 + 2 * kKC);
+        }
+        __syncthreads();
+        cur ^= 1;
+    }
+    double *Gr = G + (size_t)r * npad * npad;
+    double *Br = B + (size_t)r * npad * nout;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int row = bi * kTile + wr * 64 + i * 16 + kk + 4 * q;
+                const int col = bj * kTile + wc * 64 + j * 16 + l16;
+                if (strip) {
+                    if (row < nout) {
+                        double *p = Br + (size_t)row * npad + col;
+                        *p = *p + acc[i][j][q];
+                    }
+                } else {
+                    double *p = Gr + (size_t)col * npad + row;
+                    *p = *p + acc[i][j][q];
+                }
+            }
+}
+
 // fit_chunk_hybrid regularisation on the padded, column-major Gram:
 // diag(i) += beta_model (i < ncs) / beta_res (i < naug); padding diag = 1, prior on B
 __global__ void k_train_regularise(double *__restrict__ G, double *__restrict__ B,
@@ -371,7 +468,7 @@ __global__ __launch_bounds__(256) void k_chol_panel(double *__restrict__ G, cons
 // A_ij -= sum_{k0 <= k < k0 + kw} L_ik L_jk^T for the lower-triangle tiles j <= i
 // of block columns jlo <= j < jhi: one GEMM of depth 128 kw per tile (the block
 // columns of L are contiguous in the column-major G).
-__global__ __launch_bounds__(256) void k_chol_update(double *__restrict__ G, int npad, int k0, int kw, int jlo,
+__global__ __launch_bounds__(256, 2) void k_chol_update(double *__restrict__ G, int npad, int k0, int kw, int jlo,
                                                      int jhi) {
     const int r = blockIdx.y, C = npad / kTile;
     int idx = blockIdx.x, j = jlo;
@@ -465,7 +562,7 @@ __device__ __forceinline__ void gemm_rhs(const double *__restrict__ pa, long lon
 // Block k of the triangular solves on B (npad x nout per region, column-major), in
 // place (one block reads the whole block row it overwrites):
 //   forward  (upper = 0): B_k = L_kk^-1 B_k        backward (upper = 1): B_k = L_kk^-T B_k
-__global__ __launch_bounds__(256) void k_solve_diag(const double *__restrict__ linv, double *__restrict__ B, int npad,
+__global__ __launch_bounds__(256, 2) void k_solve_diag(const double *__restrict__ linv, double *__restrict__ B, int npad,
                                                     int nout, int k, int upper) {
     const int r = blockIdx.y, C = npad / kTile;
     const double *Li = linv + ((size_t)r * C + k) * kTile * kTile;
@@ -479,7 +576,7 @@ __global__ __launch_bounds__(256) void k_solve_diag(const double *__restrict__ l
 // Update of block rows ilo <= i < ihi by the solved block rows [k0, k0 + kw), one
 // GEMM of depth 128 kw per block row:
 //   forward:  B_i -= sum_k L_ik Y_k        backward: B_i -= sum_k L_ki^T X_k
-__global__ __launch_bounds__(256) void k_solve_update(const double *__restrict__ G, double *__restrict__ B, int npad,
+__global__ __launch_bounds__(256, 2) void k_solve_update(const double *__restrict__ G, double *__restrict__ B, int npad,
                                                       int nout, int k0, int kw, int ilo, int upper) {
     const int r = blockIdx.y, i = ilo + (int)blockIdx.x;
     const double *Gr = G + (size_t)r * npad * npad;
@@ -497,6 +594,7 @@ __global__ __launch_bounds__(256) void k_solve_update(const double *__restrict__
 struct sml_train {
     int nlocal = 0, nout = 0, npad = 0, C = 0;
     int panel = kPanel;
+    int gram = 2;  // k_train_gram2 (double-buffered LDS); SML_GRAM_V=1: k_train_gram
     std::vector<int> naug;
     TrainRegion *d_regs = nullptr;
     double *d_G = nullptr, *d_B = nullptr;
@@ -536,6 +634,7 @@ extern "C" int sml_train_create(int nlocal, const int *naug, int nout, sml_train
     t->nlocal = nlocal;
     t->nout = nout;
     if (const char *e = getenv("SML_CHOL_PANEL")) t->panel = std::max(1, atoi(e));  // tuning knob
+    if (const char *e = getenv("SML_GRAM_V")) t->gram = atoi(e) == 1 ? 1 : 2;       // A/B knob
     t->naug.assign(naug, naug + nlocal);
     int mx = 0;
     for (int i = 0; i < nlocal; ++i) {
@@ -593,8 +692,12 @@ extern "C" int sml_train_accumulate(sml_train *t, const double *d_states, const 
         t->last_m = m;
     }
     const int tiles = t->C * (t->C + 1) / 2 + kStrip * t->C;
-    hipLaunchKernelGGL(k_train_gram, dim3(tiles, t->nlocal), dim3(256), 0, (hipStream_t)stream, d_states, d_targets,
-                       t->d_regs, m, t->nout, t->npad, t->d_G, t->d_B);
+    if (t->gram == 1)
+        hipLaunchKernelGGL(k_train_gram, dim3(tiles, t->nlocal), dim3(256), 0, (hipStream_t)stream, d_states,
+                           d_targets, t->d_regs, m, t->nout, t->npad, t->d_G, t->d_B);
+    else
+        hipLaunchKernelGGL(k_train_gram2, dim3(tiles, t->nlocal), dim3(256), 0, (hipStream_t)stream, d_states,
+                           d_targets, t->d_regs, m, t->nout, t->npad, t->d_G, t->d_B);
     SML_HIP(hipGetLastError());
     return SML_OK;
 }

@@ -71,6 +71,18 @@ module sml_hip
     end function
 
     ! ------------------------------------------------------------ reservoirs
+    !> a generic context (the slab-ocean reservoirs): ninp per region, outputs
+    !> unstandardized with mean / std slot out_index(o) (0-based, -1 = none)
+    function sml_res_create_generic(numregions, nlocal, region_ids, ninp, n, k, chunk_speedy, nout, out_index, &
+                                    weight_dtype, leakage, ctx) bind(C, name='sml_res_create_generic') result(rc)
+      import :: c_int, c_signed_char, c_double, c_ptr
+      integer(c_int), value :: numregions, nlocal, chunk_speedy, nout, weight_dtype
+      integer(c_int), intent(in) :: region_ids(*), ninp(*), n(*), k(*)
+      integer(c_signed_char), intent(in) :: out_index(*)
+      real(c_double), value :: leakage
+      type(c_ptr) :: ctx
+      integer(c_int) :: rc
+    end function
     function sml_res_create(numregions, nlocal, region_ids, sst_flags, n, k, chunk_speedy, nout, &
                             weight_dtype, leakage, ctx) bind(C, name='sml_res_create') result(rc)
       import :: c_int, c_signed_char, c_double, c_ptr
@@ -285,6 +297,12 @@ module sml_hip
       real(c_double), intent(in) :: bc(*)
       integer(c_int) :: rc
     end function
+    !> ini_sea's sea ice (sice_am, tice_am: ngp each; c_null_ptr twice = no ice)
+    function sml_dyn_set_sea_ice(ctx, sice, tice) bind(C, name='sml_dyn_set_sea_ice') result(rc)
+      import :: c_ptr, c_int
+      type(c_ptr), value :: ctx, sice, tice
+      integer(c_int) :: rc
+    end function
     function sml_dyn_set_rad_state(ctx, rad) bind(C, name='sml_dyn_set_rad_state') result(rc)
       import :: c_ptr, c_int
       type(c_ptr), value :: ctx, rad
@@ -394,6 +412,34 @@ module sml_hip
     function sml_hybrid_sync(h) bind(C, name='sml_hybrid_sync') result(rc)
       import :: c_ptr, c_int
       type(c_ptr), value :: h
+      integer(c_int) :: rc
+    end function
+    !> the slab ocean in the loop (before sml_hybrid_set_buffers; exchange rows widen)
+    function sml_hybrid_set_slab(h, slab, d_base_sst, d_sea_mask, timestep, timestep_slab, sst_bias) &
+        bind(C, name='sml_hybrid_set_slab') result(rc)
+      import :: c_ptr, c_int, c_double
+      type(c_ptr), value :: h, slab, d_base_sst, d_sea_mask
+      integer(c_int), value :: timestep, timestep_slab
+      real(c_double), value :: sst_bias
+      integer(c_int) :: rc
+    end function
+    function sml_hybrid_start_slab(h, d_slab_outvec) bind(C, name='sml_hybrid_start_slab') result(rc)
+      import :: c_ptr, c_int
+      type(c_ptr), value :: h, d_slab_outvec
+      integer(c_int) :: rc
+    end function
+    function sml_hybrid_exchange_width(h, width) bind(C, name='sml_hybrid_exchange_width') result(rc)
+      import :: c_ptr, c_int
+      type(c_ptr), value :: h
+      integer(c_int), intent(out) :: width
+      integer(c_int) :: rc
+    end function
+    function sml_hybrid_slab_buffers(h, d_sst_grid, d_ring, ring_len, d_slab_feedback, d_slab_outvec) &
+        bind(C, name='sml_hybrid_slab_buffers') result(rc)
+      import :: c_ptr, c_int
+      type(c_ptr), value :: h
+      type(c_ptr), intent(out) :: d_sst_grid, d_ring, d_slab_feedback, d_slab_outvec
+      integer(c_int), intent(out) :: ring_len
       integer(c_int) :: rc
     end function
     !> advance from the host's all-gather output d_recv(nout, maxc, world)

@@ -25,9 +25,19 @@
 !>   start.bin   analysis grid4d(4,96,48,8) grid2d(96,48) precip(96,48), forecast
 !>               grid4d grid2d, tisr(16, numregions), n(numregions) (int32), then
 !>               the saved state x of every region in order
-!> Output: out_rank<r>.bin = run_speedy(nsteps) as real, then outvec(136, nlocal),
+!>   slab.bin    (optional: the slab ocean, parallelmain.f90:216-249) timestep,
+!>               timestep_slab (int32), base_sst_grid(96,48), sea_mask(96,48),
+!>               sice_am(ix*il), tice_am(ix*il), the start sst(4, numregions)
+!>               (start_prediction_slab's outvec; unused where a region has no slab),
+!>               n(numregions) (int32, 0 = no slab) and each slab state x in order;
+!>               with weights/worker_XXXX_ocean_<trial_name>.nc per sst region
+!>               (read_trained_ocean_res, mod_io.f90:2958-3007: a region has a slab
+!>               reservoir iff its file exists)
+!> Output: out_rank<r>.bin = run_speedy(nsteps) as real, then the exchange rows
+!> (width, nlocal) (width = 136, or 140 with the slab: outvec + the region's sst),
 !> feedback, local_model(132, nlocal), grid4d, grid2d, precip, forecast grid4d,
-!> grid2d, and x of every local region.
+!> grid2d, x of every local region, and with the slab wholegrid_sst(96,48) and every
+!> slab state.
 program sml_hybrid_main
   use iso_c_binding
   use sml_hip
@@ -51,6 +61,16 @@ program sml_hybrid_main
   real(c_double), allocatable, target :: bc(:), g4(:), g2(:), pr(:), f4(:), f2(:), tisr_all(:, :), tisr(:, :)
   real(c_double), allocatable, target :: x(:), ov(:), fb(:), lm(:), runs(:)
   character(len=:), allocatable :: fname
+  ! slab ocean
+  logical :: slab_on
+  integer :: nslab, j, width
+  logical :: run_exists
+  integer(c_int) :: cw, ts, tss
+  integer(c_int), allocatable :: slab_ids(:), slab_ninp(:), slab_n(:), slab_k(:), nslab_all(:)
+  integer(c_signed_char) :: out_index(4)
+  type(c_ptr) :: slab, d_base, d_mask, d_sov, d_sst, d_ring, d_sfb, d_sov2
+  real(c_double), allocatable, target :: base(:), smask(:), sice(:), tice(:), sov_all(:, :), sov(:, :), sstg(:)
+  integer(c_int) :: ring_len
 
   call get_command_argument(1, dir)
   world = 1
@@ -89,6 +109,31 @@ program sml_hybrid_main
   do i = 1, nlocal
     call sml_read_trained_res(res, i - 1, weight_file(regions(i)))
   end do
+
+  ! --- trained_ocean_reservoir_prediction (mod_slab_ocean_reservoir.f90:1494-1569):
+  ! the slab reservoirs of the rank's regions whose ocean file exists
+  inquire (file=trim(dir) // '/slab.bin', exist=slab_on)
+  nslab = 0
+  if (slab_on) then
+    allocate (slab_ids(nlocal), slab_ninp(nlocal), slab_n(nlocal), slab_k(nlocal))
+    do i = 1, nlocal
+      inquire (file=ocean_file(regions(i)), exist=run_exists)
+      if (.not. run_exists) cycle
+      nslab = nslab + 1
+      call sml_weight_file_header(ocean_file(regions(i)), dims, std)
+      slab_ids(nslab) = regions(i)
+      slab_n(nslab) = int(dims(1), c_int)
+      slab_ninp(nslab) = int(dims(2), c_int)
+      slab_k(nslab) = int(dims(5), c_int)
+    end do
+    out_index = 35_c_signed_char  ! grid%sst_mean_std_idx = 36 (1-based)
+    call sml_check(sml_res_create_generic(int(numregions, c_int), int(nslab, c_int), slab_ids, slab_ninp, slab_n, &
+                                          slab_k, 0_c_int, 4_c_int, out_index, SML_F32, 1.0_c_double, slab), &
+                   'sml_res_create_generic')
+    do j = 1, nslab
+      call sml_read_trained_res(slab, j - 1, ocean_file(slab_ids(j)))
+    end do
+  end if
 
   ! --- SPEEDY: the state and forcing agcm_init leaves, physics boundary fields
   allocate (vor(31 * 32 * 8 * 2), div(31 * 32 * 8 * 2), tt(31 * 32 * 8 * 2), tr(31 * 32 * 8 * 2), ps(31 * 32 * 2))
@@ -136,9 +181,48 @@ program sml_hybrid_main
   ! --- the loop (parallelmain.f90:204-270)
   call sml_check(sml_hybrid_create(res, dyn, comm, int(nleap, c_int), delt, alph, rob, wil, int(overlap, c_int), &
                                    int(speedy_cus, c_int), hyb), 'sml_hybrid_create')
+  if (slab_on) then  ! before the buffers: the exchange rows carry the regions' sst
+    allocate (base(ng2), smask(ng2), sice(ng2), tice(ng2), sov_all(4, numregions), nslab_all(numregions))
+    open (newunit=u, file=trim(dir) // '/slab.bin', access='stream', form='unformatted', status='old')
+    read (u) ts, tss, base, smask, sice, tice, sov_all, nslab_all
+    j = 1
+    do i = 0, numregions - 1
+      if (nslab_all(i + 1) == 0) cycle
+      allocate (x(nslab_all(i + 1)))
+      read (u) x
+      if (j <= nslab) then
+        if (slab_ids(j) == i) then
+          if (nslab_all(i + 1) /= slab_n(j)) stop 'slab.bin: slab state size differs from the ocean file'
+          call sml_check(sml_res_set_state(slab, int(j - 1, c_int), x), 'sml_res_set_state(slab)')
+          j = j + 1
+        end if
+      end if
+      deallocate (x)
+    end do
+    close (u)
+    d_base = dalloc(8_c_int64_t * ng2)
+    d_mask = dalloc(8_c_int64_t * ng2)
+    call h2d(d_base, c_loc(base), ng2)
+    call h2d(d_mask, c_loc(smask), ng2)
+    call sml_check(sml_dyn_set_sea_ice(dyn, c_loc(sice), c_loc(tice)), 'sml_dyn_set_sea_ice')
+    call sml_check(sml_hybrid_set_slab(hyb, slab, d_base, d_mask, ts, tss, 0.0_c_double), 'sml_hybrid_set_slab')
+  end if
+  call sml_check(sml_hybrid_exchange_width(hyb, cw), 'sml_hybrid_exchange_width')
+  width = cw
+  call sml_check(sml_device_free(d_ov), 'sml_device_free')
+  d_ov = dalloc(8_c_int64_t * width * nlocal)
   call sml_check(sml_hybrid_set_buffers(hyb, d_fb, d_lm, d_ov, d_g4, d_g2, d_pr, d_f4, d_f2, d_tisr), &
                  'sml_hybrid_set_buffers')
   call sml_check(sml_hybrid_start(hyb, d_a4, d_a2, d_apr, d_b4, d_b2), 'sml_hybrid_start')
+  if (slab_on) then  ! start_prediction_slab's sst of the slab regions
+    allocate (sov(4, max(nslab, 1)))
+    do j = 1, nslab
+      sov(:, j) = sov_all(:, slab_ids(j) + 1)
+    end do
+    d_sov = dalloc(8_c_int64_t * 4 * max(nslab, 1))
+    call h2d(d_sov, c_loc(sov), 4 * max(nslab, 1))
+    call sml_check(sml_hybrid_start_slab(hyb, d_sov), 'sml_hybrid_start_slab')
+  end if
   allocate (runs(nsteps))
   runs = -1.0_c_double
   nsteps_done = 0
@@ -153,8 +237,8 @@ program sml_hybrid_main
   print '(a,i0,a,i0,a)', 'sml_hybrid_main: rank ', rank, ' ran ', nsteps_done, ' hybrid steps'
 
   ! --- outputs
-  allocate (ov(nout * nlocal), fb(fboff(nlocal + 1)), lm(ncs * nlocal))
-  call d2h(c_loc(ov), d_ov, nout * nlocal)
+  allocate (ov(width * nlocal), fb(fboff(nlocal + 1)), lm(ncs * nlocal))
+  call d2h(c_loc(ov), d_ov, width * nlocal)
   call d2h(c_loc(fb), d_fb, int(fboff(nlocal + 1)))
   call d2h(c_loc(lm), d_lm, ncs * nlocal)
   call d2h(c_loc(g4), d_g4, ng4)
@@ -171,10 +255,23 @@ program sml_hybrid_main
     write (u) x
     deallocate (x)
   end do
+  if (slab_on) then
+    allocate (sstg(ng2))
+    call sml_check(sml_hybrid_slab_buffers(hyb, d_sst, d_ring, ring_len, d_sfb, d_sov2), 'sml_hybrid_slab_buffers')
+    call d2h(c_loc(sstg), d_sst, ng2)
+    write (u) sstg
+    do j = 1, nslab
+      allocate (x(slab_n(j)))
+      call sml_check(sml_res_get_state(slab, j - 1, x), 'sml_res_get_state(slab)')
+      write (u) x
+      deallocate (x)
+    end do
+  end if
   close (u)
   call sml_check(sml_hybrid_destroy(hyb), 'sml_hybrid_destroy')
   call sml_check(sml_dyn_destroy(dyn), 'sml_dyn_destroy')
   call sml_check(sml_res_destroy(res), 'sml_res_destroy')
+  if (slab_on) call sml_check(sml_res_destroy(slab), 'sml_res_destroy(slab)')
   if (c_associated(comm)) call sml_check(sml_comm_destroy(comm), 'sml_comm_destroy')
   print '(a)', 'sml_hybrid_main ok'
 
@@ -187,6 +284,15 @@ contains
     character(len=4) :: w
     write (w, '(i0.4)') region
     f = trim(dir) // '/weights/worker_' // w // '_level_1_' // trim(trial) // '.nc'
+  end function
+
+  !> worker_XXXX_ocean_<trial_name>.nc (read_trained_ocean_res, mod_io.f90:2974-2977)
+  function ocean_file(region) result(f)
+    integer(c_int), intent(in) :: region
+    character(len=:), allocatable :: f
+    character(len=4) :: w
+    write (w, '(i0.4)') region
+    f = trim(dir) // '/weights/worker_' // w // '_ocean_' // trim(trial) // '.nc'
   end function
 
   function dalloc(bytes) result(p)

@@ -108,6 +108,115 @@ def test_fortran_hybrid_driver_matches_hybrid_loop(tmp_path, cuda):
     assert o == raw.size
 
 
+def test_fortran_hybrid_driver_with_slab_matches_hybrid_loop(tmp_path, cuda):
+    """sml_hybrid_main with the slab ocean (slab.bin + worker_XXXX_ocean_<trial>.nc,
+    read_trained_ocean_res's layout): a slab step every 2nd hybrid step over 4 steps,
+    bitwise the Python HybridLoop with the same SlabOcean."""
+    import torch
+
+    from speedy_ml_amd import domain
+    from speedy_ml_amd._lib import check, lib, ptr
+    from speedy_ml_amd.dynamics import Dynamics
+    from speedy_ml_amd.exchange import OutvecExchange
+    from speedy_ml_amd.hybrid import HybridLoop, SlabOcean
+    from speedy_ml_amd.reservoir import Reservoirs, write_region_netcdf
+    from speedy_ml_amd.synthetic import (dyn_state, initial_state, phys_boundary, region_weights, slab_fields,
+                                         slab_start_outvec, slab_weights, synthetic_grids)
+
+    nsteps, ts, tss = 4, 6, 12
+    mask = domain.load_sst_mask()
+    ws = [region_weights(r, bool(mask[r]), n_override=96, seed=5, climatology=True) for r in range(1152)]
+    sreg = [r for r in range(1152) if mask[r]]
+    sws = [slab_weights(r, n_override=200) for r in sreg]
+    base, smask, sice, tice = slab_fields()
+    sov_all = np.full((1152, 4), 272.0)
+    for r in sreg:
+        sov_all[r] = slab_start_outvec(r)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(cuda)  # noqa: E731
+    # the Python loop
+    res = Reservoirs(list(range(1152)), mask, [w.n for w in ws], [w.k for w in ws])
+    for i, w in enumerate(ws):
+        res.load_region_weights(i, w)
+        res.set_state(i, initial_state(w.region, w.n))
+    slab = Reservoirs(sreg, [0] * len(sreg), [w.n for w in sws], [w.k for w in sws], chunk_speedy=0, nout=4,
+                      ninp=[w.ninp for w in sws], out_index=[35] * 4)
+    for j, w in enumerate(sws):
+        slab.load_region_weights(j, w)
+        slab.set_state(j, initial_state(sreg[j], w.n, seed=17))
+    st0, forcing = dyn_state()
+    dyn = Dynamics()
+    dyn.set_forcing(**forcing)
+    dyn.set_state(st0)
+    dyn.set_physics(phys_boundary(dyn, forcing["phis"]))
+    check(lib().sml_dyn_set_sea_ice(dyn._h, ptr(np.ascontiguousarray(sice)), ptr(np.ascontiguousarray(tice))))
+    tisr = np.random.default_rng(13).standard_normal((1152, 16))
+    loop = HybridLoop(res, dyn, OutvecExchange(1152, 1, 0, device=cuda), cuda, tisr=t(tisr), speedy_cus=64,
+                      slab=SlabOcean(slab, t(base), t(smask), timestep=ts, timestep_slab=tss))
+    g4, g2, pr = synthetic_grids(11)
+    f4, f2, _ = synthetic_grids(12)
+    loop.start(t(g4), t(g2), t(pr), t(f4), t(f2))
+    loop.start_slab(t(sov_all[sreg]))
+    for _ in range(nsteps):
+        loop.step()
+    loop.sync()
+    want = {k: getattr(loop, k).cpu().numpy().copy() for k in ("ov", "fb", "lm", "g4", "g2", "pr", "f4", "f2")}
+    want["sst"] = loop.slab_state()["sst"]
+    want_x = [res.get_state(i) for i in range(1152)]
+    want_sx = [slab.get_state(j) for j in range(len(sreg))]
+    loop.close()
+    dyn.close()
+    res.close()
+    slab.close()
+    torch.cuda.synchronize()
+    # the same inputs as files
+    wdir = tmp_path / "weights"
+    wdir.mkdir()
+    for w in ws:
+        write_region_netcdf(str(wdir / f"worker_{w.region:04d}_level_1_{TRIAL}.nc"), w.win, w.wout, w.rows, w.cols,
+                            w.vals, w.mean, w.std)
+    for w in sws:
+        write_region_netcdf(str(wdir / f"worker_{w.region:04d}_ocean_{TRIAL}.nc"), w.win, w.wout, w.rows, w.cols,
+                            w.vals, w.mean, w.std)
+    (tmp_path / "setup.txt").write_text(f"1152 {nsteps} 24 1 64\n{TRIAL}\n")
+    _speedy_bin(tmp_path / "speedy.bin", Dynamics)
+    with open(tmp_path / "start.bin", "wb") as f:
+        for a in (g4, g2, pr, f4, f2, tisr):
+            f.write(np.ascontiguousarray(a, dtype=np.float64).tobytes())
+        f.write(np.array([w.n for w in ws], dtype=np.int32).tobytes())
+        for w in ws:
+            f.write(initial_state(w.region, w.n).tobytes())
+    nall = np.zeros(1152, dtype=np.int32)
+    for w in sws:
+        nall[w.region] = w.n
+    with open(tmp_path / "slab.bin", "wb") as f:
+        f.write(np.array([ts, tss], dtype=np.int32).tobytes())
+        for a in (base, smask, sice, tice, sov_all):
+            f.write(np.ascontiguousarray(a, dtype=np.float64).tobytes())
+        f.write(nall.tobytes())
+        for w in sws:
+            f.write(initial_state(w.region, w.n, seed=17).tobytes())
+    out = subprocess.run([_bin("sml_hybrid_main"), str(tmp_path)], capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-2000:]
+    raw = np.fromfile(tmp_path / "out_rank0.bin", dtype=np.float64)
+    o = 0
+
+    def take(n):
+        nonlocal o
+        a = raw[o:o + n]
+        o += n
+        return a
+
+    assert (take(nsteps) == 1.0).all()
+    for k in ("ov", "fb", "lm", "g4", "g2", "pr", "f4", "f2"):
+        np.testing.assert_array_equal(take(want[k].size), want[k].ravel(), err_msg=k)
+    for i, w in enumerate(ws):
+        np.testing.assert_array_equal(take(w.n), want_x[i], err_msg=f"state of region {i}")
+    np.testing.assert_array_equal(take(want["sst"].size), want["sst"].ravel(), err_msg="wholegrid_sst")
+    for j, w in enumerate(sws):
+        np.testing.assert_array_equal(take(w.n), want_sx[j], err_msg=f"slab state {j}")
+    assert o == raw.size
+
+
 def test_fortran_dropin_matches_reference_golden(tmp_path, cuda):
     from conftest import REPO
 

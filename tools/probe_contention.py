@@ -46,7 +46,7 @@ dst = torch.empty_like(src)
 src.uniform_()
 
 
-def window_ms(partner, reps=8):
+def window_ms(partner, reps=8, window=True):
     ts = []
     for _ in range(reps + 2):
         torch.cuda.synchronize()
@@ -59,7 +59,8 @@ def window_ms(partner, reps=8):
             p1.record()
         with torch.cuda.stream(side):
             e0.record()
-            dyn.window(24, stream=side)
+            if window:
+                dyn.window(24, stream=side)
             e1.record()
         torch.cuda.synchronize()
         ts.append((e0.elapsed_time(e1), p0.elapsed_time(p1)))
@@ -80,6 +81,8 @@ def read_only():
     torch.sum(src)
 
 
+w, p = window_ms(begin, window=False)
+print(f"predict_begin alone on the partner CUs: {p:.3f} ms")
 for name, fn in (("alone", None), ("beside predict_begin", begin), ("beside a 3.7 GB copy (7.4 GB traffic)", copy),
                  ("beside a 3.7 GB read (sum)", read_only), ("alone again", None)):
     w, p = window_ms(fn)
