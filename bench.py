@@ -595,28 +595,30 @@ def training_leg(dev, mask, args, world, rank):
         "solve_ms_per_region": round(solve_ms / len(naug), 3),
         "solve_info_ok": bool(ok.item() == 1.0),
         "solve_roofline": {
-            "kernels": "k_chol_diag / k_chol_panel / k_chol_update (right-looking, 128-blocked, fp64 MFMA) + "
-                       "k_solve_diag / k_solve_update (block forward / backward substitution)",
+            "kernels": "k_chol_diag / k_chol_panel / k_chol_update (right-looking, 128-blocked, fp64 MFMA, 2 waves "
+                       "per SIMD) + k_solve_diag / k_solve_update (block forward / backward substitution)",
             "bound": "mfma", "unit": "TFLOP/s",
             "achieved": round(solve_tf, 2),
-            "peak": round(peak.value, 2),
-            "frac": round(solve_tf / peak.value, 4),
-            "frac_of_nominal_peak": round(solve_tf / F64_MFMA_PEAK_TF, 4),
+            "peak": F64_MFMA_PEAK_TF,
+            "frac": round(solve_tf / F64_MFMA_PEAK_TF, 4),
+            "probe_tflops": round(peak.value, 2),
             "algorithmic_flops": solve_algo,
-            "previous": "rocSOLVER dpotrf + dpotrs strided-batched: 333.9 ms for 8 regions (41.7 ms per region), "
-                        "r02 bench",
+            "previous": "r02: 394 ms, 29.3 TF/s (1 wave per SIMD); rocSOLVER dpotrf + dpotrs strided-batched in r01: "
+                        "41.7 ms per region",
         },
         "roofline": {
-            "kernel": "k_train_gram (fp64 MFMA 16x16x4, 128x128 tiles, lower triangle + T S^T strip)",
+            "kernel": "k_train_gram2 (fp64 MFMA 16x16x4, 128x128 tiles, lower triangle + T S^T strip, LDS stages "
+                      "double-buffered, 2 waves per SIMD)",
             "bound": "mfma", "unit": "TFLOP/s",
             "achieved": round(achieved, 2),
             "issued_tflops": round(issued / (gram_ms * 1e-3) / 1e12, 2),
-            "peak": round(peak.value, 2),
-            "peak_source": "measured: back-to-back v_mfma_f64_16x16x4_f64 on every SIMD (sml_probe_mfma_f64), the "
-                           "sustained rate under a full-chip MFMA load; nominal 78.6 TF/s (64 clk per MFMA at 2.4 GHz)",
-            "frac": round(achieved / peak.value, 4),
-            "frac_of_nominal_peak": round(achieved / F64_MFMA_PEAK_TF, 4),
+            "peak": F64_MFMA_PEAK_TF,
+            "peak_source": "nominal: 64 clk per v_mfma_f64_16x16x4_f64 (2048 flop) on each of 1024 SIMDs at 2.4 GHz; "
+                           "the chip runs MFMA-dense loops below 2.4 GHz (MI355X_MICROARCH.md, DVFS give-back)",
+            "frac": round(achieved / F64_MFMA_PEAK_TF, 4),
+            "probe_tflops": round(peak.value, 2),
             "algorithmic_flops": algo,
+            "previous": "r02: k_train_gram (single-buffered LDS, 1 wave per SIMD) 636 ms, 34.3 TF/s",
         },
     }
 

@@ -318,8 +318,10 @@ __device__ __forceinline__ void gemm_tile(const double *__restrict__ pa, long lo
     using LA = TileLoader<TR, AT>;
     using LB = TileLoader<TC, BT>;
     constexpr int NI = TR / 32, NJ = TC / 32;
-    __shared__ double sA[kKC][TR + kLdsPad];
-    __shared__ double sB[kKC][TC + kLdsPad];
+    // LDS stages double-buffered (one barrier per stage), rows padded to a 16-double
+    // multiple + 16 (consecutive k on disjoint banks in a ds_read_b64 lane group)
+    __shared__ double sA[2][kKC][TR + 16];
+    __shared__ double sB[2][kKC][TC + 16];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int wr = w >> 1, wc = w & 1, l16 = lane & 15, kk = lane >> 4;
     const int arow = LA::row(tid), brow = LB::row(tid);
@@ -337,32 +339,41 @@ __device__ __forceinline__ void gemm_tile(const double *__restrict__ pa, long lo
             rb[q] = b_ok ? (BT ? pb[(long long)brow * ldb + l] : pb[(long long)l * ldb + brow]) : 0.0;
         }
     };
+    auto store = [&](int buf) {
+#pragma unroll
+        for (int q = 0; q < LA::PER; ++q) sA[buf][LA::l(tid, q)][arow] = ra[q];
+#pragma unroll
+        for (int q = 0; q < LB::PER; ++q) sB[buf][LB::l(tid, q)][brow] = rb[q];
+    };
     d4 acc[NI][NJ];
 #pragma unroll
     for (int i = 0; i < NI; ++i)
 #pragma unroll
         for (int j = 0; j < NJ; ++j) acc[i][j] = d4{0, 0, 0, 0};
     fetch(0);
+    store(0);
+    __syncthreads();
+    if (kKC < K) fetch(kKC);
+    int cur = 0;
     for (int t0 = 0; t0 < K; t0 += kKC) {
-        __syncthreads();
-#pragma unroll
-        for (int q = 0; q < LA::PER; ++q) sA[LA::l(tid, q)][arow] = ra[q];
-#pragma unroll
-        for (int q = 0; q < LB::PER; ++q) sB[LB::l(tid, q)][brow] = rb[q];
-        __syncthreads();
-        if (t0 + kKC < K) fetch(t0 + kKC);
 #pragma unroll
         for (int s = 0; s < kKC / 4; ++s) {
             double a[NI], b[NJ];
 #pragma unroll
-            for (int i = 0; i < NI; ++i) a[i] = sA[4 * s + kk][wr * (TR / 2) + i * 16 + l16];
+            for (int i = 0; i < NI; ++i) a[i] = sA[cur][4 * s + kk][wr * (TR / 2) + i * 16 + l16];
 #pragma unroll
-            for (int j = 0; j < NJ; ++j) b[j] = sB[4 * s + kk][wc * (TC / 2) + j * 16 + l16];
+            for (int j = 0; j < NJ; ++j) b[j] = sB[cur][4 * s + kk][wc * (TC / 2) + j * 16 + l16];
 #pragma unroll
             for (int i = 0; i < NI; ++i)
 #pragma unroll
                 for (int j = 0; j < NJ; ++j) acc[i][j] = MFMA64(a[i], b[j], acc[i][j]);
         }
+        if (t0 + kKC < K) {
+            store(cur ^ 1);
+            if (t0 + 2 * kKC < K) fetch(t0 + 2 * kKC);
+        }
+        __syncthreads();
+        cur ^= 1;
     }
 #pragma unroll
     for (int i = 0; i < NI; ++i)
@@ -501,8 +512,8 @@ __device__ __forceinline__ void gemm_rhs(const double *__restrict__ pa, long lon
                                          bool accumulate, int K = kTile) {
     using LA = TileLoader<kTile, AT>;
     constexpr int NJ = kRhs / 16, PB = kRhs * kKC / 256;
-    __shared__ double sA[kKC][kTile + kLdsPad];
-    __shared__ double sB[kKC][kRhs + kLdsPad];
+    __shared__ double sA[2][kKC][kTile + 16];  // double-buffered stages (as gemm_tile)
+    __shared__ double sB[2][kKC][kRhs + 16];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, l16 = lane & 15, kk = lane >> 4;
     const int arow = LA::row(tid);
     double ra[LA::PER], rb[PB];
@@ -518,32 +529,41 @@ __device__ __forceinline__ void gemm_rhs(const double *__restrict__ pa, long lon
             rb[q] = c < nb ? pb[(long long)c * ldb + t0 + (idx & 15)] : 0.0;
         }
     };
+    auto store = [&](int buf) {
+#pragma unroll
+        for (int q = 0; q < LA::PER; ++q) sA[buf][LA::l(tid, q)][arow] = ra[q];
+#pragma unroll
+        for (int q = 0; q < PB; ++q) sB[buf][(tid + 256 * q) & 15][(tid + 256 * q) >> 4] = rb[q];
+    };
     d4 acc[2][NJ];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < NJ; ++j) acc[i][j] = d4{0, 0, 0, 0};
     fetch(0);
+    store(0);
+    __syncthreads();
+    if (kKC < K) fetch(kKC);
+    int cur = 0;
     for (int t0 = 0; t0 < K; t0 += kKC) {
-        __syncthreads();
-#pragma unroll
-        for (int q = 0; q < LA::PER; ++q) sA[LA::l(tid, q)][arow] = ra[q];
-#pragma unroll
-        for (int q = 0; q < PB; ++q) sB[(tid + 256 * q) & 15][(tid + 256 * q) >> 4] = rb[q];
-        __syncthreads();
-        if (t0 + kKC < K) fetch(t0 + kKC);
 #pragma unroll
         for (int s = 0; s < kKC / 4; ++s) {
             double a[2], b[NJ];
 #pragma unroll
-            for (int i = 0; i < 2; ++i) a[i] = sA[4 * s + kk][w * 32 + i * 16 + l16];
+            for (int i = 0; i < 2; ++i) a[i] = sA[cur][4 * s + kk][w * 32 + i * 16 + l16];
 #pragma unroll
-            for (int j = 0; j < NJ; ++j) b[j] = sB[4 * s + kk][j * 16 + l16];
+            for (int j = 0; j < NJ; ++j) b[j] = sB[cur][4 * s + kk][j * 16 + l16];
 #pragma unroll
             for (int i = 0; i < 2; ++i)
 #pragma unroll
                 for (int j = 0; j < NJ; ++j) acc[i][j] = MFMA64(a[i], b[j], acc[i][j]);
         }
+        if (t0 + kKC < K) {
+            store(cur ^ 1);
+            if (t0 + 2 * kKC < K) fetch(t0 + 2 * kKC);
+        }
+        __syncthreads();
+        cur ^= 1;
     }
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -562,26 +582,25 @@ __device__ __forceinline__ void gemm_rhs(const double *__restrict__ pa, long lon
 // Block k of the triangular solves on B (npad x nout per region, column-major), in
 // place (one block reads the whole block row it overwrites):
 //   forward  (upper = 0): B_k = L_kk^-1 B_k        backward (upper = 1): B_k = L_kk^-T B_k
+template <bool upper>  // one gemm_rhs instance per kernel: its LDS stages are static
 __global__ __launch_bounds__(256, 2) void k_solve_diag(const double *__restrict__ linv, double *__restrict__ B, int npad,
-                                                    int nout, int k, int upper) {
+                                                    int nout, int k) {
     const int r = blockIdx.y, C = npad / kTile;
     const double *Li = linv + ((size_t)r * C + k) * kTile * kTile;
     double *Bk = B + (size_t)r * npad * nout + (size_t)k * kTile;
-    if (upper)
-        gemm_rhs<true>(Li, kTile, Bk, npad, nout, Bk, npad, 1.0, false);
-    else
-        gemm_rhs<false>(Li, kTile, Bk, npad, nout, Bk, npad, 1.0, false);
+    gemm_rhs<upper>(Li, kTile, Bk, npad, nout, Bk, npad, 1.0, false);
 }
 
 // Update of block rows ilo <= i < ihi by the solved block rows [k0, k0 + kw), one
 // GEMM of depth 128 kw per block row:
 //   forward:  B_i -= sum_k L_ik Y_k        backward: B_i -= sum_k L_ki^T X_k
+template <bool upper>
 __global__ __launch_bounds__(256, 2) void k_solve_update(const double *__restrict__ G, double *__restrict__ B, int npad,
-                                                      int nout, int k0, int kw, int ilo, int upper) {
+                                                      int nout, int k0, int kw, int ilo) {
     const int r = blockIdx.y, i = ilo + (int)blockIdx.x;
     const double *Gr = G + (size_t)r * npad * npad;
     double *Br = B + (size_t)r * npad * nout;
-    if (upper)  // A(rr, l) = L(k0 kTile + l, i kTile + rr): the transposed blocks (k, i)
+    if constexpr (upper)  // A(rr, l) = L(k0 kTile + l, i kTile + rr): the transposed blocks (k, i)
         gemm_rhs<true>(Gr + (size_t)i * kTile * npad + (size_t)k0 * kTile, npad, Br + (size_t)k0 * kTile, npad, nout,
                        Br + (size_t)i * kTile, npad, -1.0, true, kw * kTile);
     else
@@ -751,26 +770,26 @@ extern "C" int sml_train_solve(sml_train *t, int ncs, double beta_res, double be
     for (int p0 = 0; p0 < C; p0 += P) {  // L Y = B
         const int p1 = std::min(C, p0 + P);
         for (int k = p0; k < p1; ++k) {
-            hipLaunchKernelGGL(k_solve_diag, dim3(1, nl), dim3(256), 0, st, t->d_linv, t->d_B, npad, nout, k, 0);
+            hipLaunchKernelGGL(k_solve_diag<false>, dim3(1, nl), dim3(256), 0, st, t->d_linv, t->d_B, npad, nout, k);
             if (k + 1 < p1)
-                hipLaunchKernelGGL(k_solve_update, dim3(p1 - 1 - k, nl), dim3(256), 0, st, t->d_G, t->d_B, npad,
-                                   nout, k, 1, k + 1, 0);
+                hipLaunchKernelGGL(k_solve_update<false>, dim3(p1 - 1 - k, nl), dim3(256), 0, st, t->d_G, t->d_B,
+                                   npad, nout, k, 1, k + 1);
         }
         if (p1 < C)
-            hipLaunchKernelGGL(k_solve_update, dim3(C - p1, nl), dim3(256), 0, st, t->d_G, t->d_B, npad, nout, p0,
-                               p1 - p0, p1, 0);
+            hipLaunchKernelGGL(k_solve_update<false>, dim3(C - p1, nl), dim3(256), 0, st, t->d_G, t->d_B, npad, nout,
+                               p0, p1 - p0, p1);
     }
     for (int p1 = C; p1 > 0; p1 -= P) {  // L^T X = Y, panels from the bottom
         const int p0 = std::max(0, p1 - P);
         for (int k = p1 - 1; k >= p0; --k) {
-            hipLaunchKernelGGL(k_solve_diag, dim3(1, nl), dim3(256), 0, st, t->d_linv, t->d_B, npad, nout, k, 1);
+            hipLaunchKernelGGL(k_solve_diag<true>, dim3(1, nl), dim3(256), 0, st, t->d_linv, t->d_B, npad, nout, k);
             if (k > p0)
-                hipLaunchKernelGGL(k_solve_update, dim3(k - p0, nl), dim3(256), 0, st, t->d_G, t->d_B, npad, nout, k,
-                                   1, p0, 1);
+                hipLaunchKernelGGL(k_solve_update<true>, dim3(k - p0, nl), dim3(256), 0, st, t->d_G, t->d_B, npad,
+                                   nout, k, 1, p0);
         }
         if (p0 > 0)
-            hipLaunchKernelGGL(k_solve_update, dim3(p0, nl), dim3(256), 0, st, t->d_G, t->d_B, npad, nout, p0,
-                               p1 - p0, 0, 1);
+            hipLaunchKernelGGL(k_solve_update<true>, dim3(p0, nl), dim3(256), 0, st, t->d_G, t->d_B, npad, nout, p0,
+                               p1 - p0, 0);
     }
     SML_HIP(hipGetLastError());
     hipLaunchKernelGGL(k_train_wout, dim3((t->npad + 255) / 256, t->nlocal), dim3(256), 0, st, t->d_B, t->d_regs,
