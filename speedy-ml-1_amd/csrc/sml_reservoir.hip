@@ -591,6 +591,20 @@ int dalloc(T **p, size_t count) {
     return SML_OK;
 }
 
+// W_out's pool: SML_WOUT_MEM=uncached / coherent selects hipExtMallocWithFlags'
+// memory types (A/B experiments on how the readout's stream shares the memory-side
+// cache with SPEEDY's window); default hipMalloc
+int dalloc_wout(void **p, size_t bytes) {
+    const char *e = std::getenv("SML_WOUT_MEM");
+    if (e && (!std::strcmp(e, "uncached") || !std::strcmp(e, "coherent"))) {
+        const unsigned flags = !std::strcmp(e, "uncached") ? hipDeviceMallocUncached : hipDeviceMallocFinegrained;
+        SML_HIP(hipExtMallocWithFlags(p, bytes ? bytes : 16, flags));
+        return SML_OK;
+    }
+    SML_HIP(hipMalloc(p, bytes ? bytes : 16));
+    return SML_OK;
+}
+
 int dalloc_bytes(void **p, size_t bytes) {
     *p = nullptr;
     SML_HIP(hipMalloc(p, bytes ? bytes : 16));
@@ -1043,7 +1057,7 @@ int res_create_impl(int numregions, int nlocal, const int *region_ids, const uns
     if ((rc = dalloc(&c->d_rd, nlocal)) || (rc = dalloc(&c->d_a_rp, c->tot_a_rp)) ||
         (rc = dalloc(&c->d_a_col, c->tot_a_nz)) || (rc = dalloc_bytes(&c->d_a_val, c->tot_a_nz * wb)) ||
         (rc = dalloc(&c->d_w_rp, c->tot_w_rp)) || (rc = dalloc(&c->d_w_col, c->tot_w_nz)) ||
-        (rc = dalloc_bytes(&c->d_w_val, c->tot_w_nz * wb)) || (rc = dalloc_bytes(&c->d_wout, c->tot_wout * wb)) ||
+        (rc = dalloc_bytes(&c->d_w_val, c->tot_w_nz * wb)) || (rc = dalloc_wout(&c->d_wout, c->tot_wout * wb)) ||
         (rc = dalloc_bytes(&c->d_wlm, std::max<int64_t>(c->tot_wlm, 1) * wb)) ||
         (rc = dalloc(&c->d_x[0], c->tot_x)) || (rc = dalloc(&c->d_x[1], c->tot_x)) ||
         (rc = dalloc(&c->d_xaug, c->tot_xaug)) || (rc = dalloc(&c->d_meanstd, (size_t)nlocal * 2 * kMeanStd)) ||

@@ -318,10 +318,8 @@ __device__ __forceinline__ void gemm_tile(const double *__restrict__ pa, long lo
     using LA = TileLoader<TR, AT>;
     using LB = TileLoader<TC, BT>;
     constexpr int NI = TR / 32, NJ = TC / 32;
-    // LDS stages double-buffered (one barrier per stage), rows padded to a 16-double
-    // multiple + 16 (consecutive k on disjoint banks in a ds_read_b64 lane group)
-    __shared__ double sA[2][kKC][TR + 16];
-    __shared__ double sB[2][kKC][TC + 16];
+    __shared__ double sA[kKC][TR + kLdsPad];
+    __shared__ double sB[kKC][TC + kLdsPad];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int wr = w >> 1, wc = w & 1, l16 = lane & 15, kk = lane >> 4;
     const int arow = LA::row(tid), brow = LB::row(tid);
@@ -339,41 +337,32 @@ __device__ __forceinline__ void gemm_tile(const double *__restrict__ pa, long lo
             rb[q] = b_ok ? (BT ? pb[(long long)brow * ldb + l] : pb[(long long)l * ldb + brow]) : 0.0;
         }
     };
-    auto store = [&](int buf) {
-#pragma unroll
-        for (int q = 0; q < LA::PER; ++q) sA[buf][LA::l(tid, q)][arow] = ra[q];
-#pragma unroll
-        for (int q = 0; q < LB::PER; ++q) sB[buf][LB::l(tid, q)][brow] = rb[q];
-    };
     d4 acc[NI][NJ];
 #pragma unroll
     for (int i = 0; i < NI; ++i)
 #pragma unroll
         for (int j = 0; j < NJ; ++j) acc[i][j] = d4{0, 0, 0, 0};
     fetch(0);
-    store(0);
-    __syncthreads();
-    if (kKC < K) fetch(kKC);
-    int cur = 0;
     for (int t0 = 0; t0 < K; t0 += kKC) {
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < LA::PER; ++q) sA[LA::l(tid, q)][arow] = ra[q];
+#pragma unroll
+        for (int q = 0; q < LB::PER; ++q) sB[LB::l(tid, q)][brow] = rb[q];
+        __syncthreads();
+        if (t0 + kKC < K) fetch(t0 + kKC);
 #pragma unroll
         for (int s = 0; s < kKC / 4; ++s) {
             double a[NI], b[NJ];
 #pragma unroll
-            for (int i = 0; i < NI; ++i) a[i] = sA[cur][4 * s + kk][wr * (TR / 2) + i * 16 + l16];
+            for (int i = 0; i < NI; ++i) a[i] = sA[4 * s + kk][wr * (TR / 2) + i * 16 + l16];
 #pragma unroll
-            for (int j = 0; j < NJ; ++j) b[j] = sB[cur][4 * s + kk][wc * (TC / 2) + j * 16 + l16];
+            for (int j = 0; j < NJ; ++j) b[j] = sB[4 * s + kk][wc * (TC / 2) + j * 16 + l16];
 #pragma unroll
             for (int i = 0; i < NI; ++i)
 #pragma unroll
                 for (int j = 0; j < NJ; ++j) acc[i][j] = MFMA64(a[i], b[j], acc[i][j]);
         }
-        if (t0 + kKC < K) {
-            store(cur ^ 1);
-            if (t0 + 2 * kKC < K) fetch(t0 + 2 * kKC);
-        }
-        __syncthreads();
-        cur ^= 1;
     }
 #pragma unroll
     for (int i = 0; i < NI; ++i)
@@ -512,8 +501,8 @@ __device__ __forceinline__ void gemm_rhs(const double *__restrict__ pa, long lon
                                          bool accumulate, int K = kTile) {
     using LA = TileLoader<kTile, AT>;
     constexpr int NJ = kRhs / 16, PB = kRhs * kKC / 256;
-    __shared__ double sA[2][kKC][kTile + 16];  // double-buffered stages (as gemm_tile)
-    __shared__ double sB[2][kKC][kRhs + 16];
+    __shared__ double sA[kKC][kTile + kLdsPad];
+    __shared__ double sB[kKC][kRhs + kLdsPad];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, l16 = lane & 15, kk = lane >> 4;
     const int arow = LA::row(tid);
     double ra[LA::PER], rb[PB];
@@ -529,41 +518,32 @@ __device__ __forceinline__ void gemm_rhs(const double *__restrict__ pa, long lon
             rb[q] = c < nb ? pb[(long long)c * ldb + t0 + (idx & 15)] : 0.0;
         }
     };
-    auto store = [&](int buf) {
-#pragma unroll
-        for (int q = 0; q < LA::PER; ++q) sA[buf][LA::l(tid, q)][arow] = ra[q];
-#pragma unroll
-        for (int q = 0; q < PB; ++q) sB[buf][(tid + 256 * q) & 15][(tid + 256 * q) >> 4] = rb[q];
-    };
     d4 acc[2][NJ];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < NJ; ++j) acc[i][j] = d4{0, 0, 0, 0};
     fetch(0);
-    store(0);
-    __syncthreads();
-    if (kKC < K) fetch(kKC);
-    int cur = 0;
     for (int t0 = 0; t0 < K; t0 += kKC) {
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < LA::PER; ++q) sA[LA::l(tid, q)][arow] = ra[q];
+#pragma unroll
+        for (int q = 0; q < PB; ++q) sB[(tid + 256 * q) & 15][(tid + 256 * q) >> 4] = rb[q];
+        __syncthreads();
+        if (t0 + kKC < K) fetch(t0 + kKC);
 #pragma unroll
         for (int s = 0; s < kKC / 4; ++s) {
             double a[2], b[NJ];
 #pragma unroll
-            for (int i = 0; i < 2; ++i) a[i] = sA[cur][4 * s + kk][w * 32 + i * 16 + l16];
+            for (int i = 0; i < 2; ++i) a[i] = sA[4 * s + kk][w * 32 + i * 16 + l16];
 #pragma unroll
-            for (int j = 0; j < NJ; ++j) b[j] = sB[cur][4 * s + kk][j * 16 + l16];
+            for (int j = 0; j < NJ; ++j) b[j] = sB[4 * s + kk][j * 16 + l16];
 #pragma unroll
             for (int i = 0; i < 2; ++i)
 #pragma unroll
                 for (int j = 0; j < NJ; ++j) acc[i][j] = MFMA64(a[i], b[j], acc[i][j]);
         }
-        if (t0 + kKC < K) {
-            store(cur ^ 1);
-            if (t0 + 2 * kKC < K) fetch(t0 + 2 * kKC);
-        }
-        __syncthreads();
-        cur ^= 1;
     }
 #pragma unroll
     for (int i = 0; i < 2; ++i)
