@@ -18,6 +18,7 @@ import csv
 import glob
 import json
 import os
+import re
 import shutil
 import subprocess
 import sys
@@ -37,11 +38,11 @@ def _find(root, pattern):
 
 
 def _short(name: str) -> str:
-    if "k_res_readout" in name:  # <WT, mode>: mode 0 = v_ml half (step_begin), 1 = finish
-        wt = "float" if ("<float" in name or "IfL" in name) else "double"
-        mode = ("finish" if (", 1>" in name or "Li1E" in name) else
-                "full" if (", 2>" in name or "Li2E" in name) else "ml")
-        return f"k_res_readout_{mode}<{wt}>"
+    if "k_res_readout" in name:  # <WT, mode[, rows]>: 0 = v_ml half (step_begin), 1 = finish, 2 = one pass
+        m = re.search(r"k_res_readout<(\w+), (\d)", name)
+        wt = m.group(1) if m else ("float" if ("<float" in name or "IfL" in name) else "double")
+        mode = m.group(2) if m else ("1" if "Li1E" in name else "2" if "Li2E" in name else "0")
+        return f"k_res_readout_{ {'0': 'ml', '1': 'finish', '2': 'full'}[mode]}<{wt}>"
     for key in ("k_res_readout", "k_res_update", "k_tile_feedback", "k_tile_local_model", "k_assemble",
                 "k_gridy", "k_gridx", "k_specx", "k_specy", "k_vds", "k_uvspec"):
         if key in name:
