@@ -54,7 +54,8 @@ void hip_ok(hipError_t e, const char *what) {
 DropIn &ctx() {
     if (!g_drop.sp) {
         ok(sml_spectral_create(g_drop.radius, &g_drop.sp), "sml_spectral_create");
-        hip_ok(hipMalloc(&g_drop.d, sizeof(double) * (2 * kGF + 2 * kSF + 2 * kVF)), "hipMalloc");
+        // the scratch does not depend on the radius: allocated once, kept over re-inits
+        if (!g_drop.d) hip_ok(hipMalloc(&g_drop.d, sizeof(double) * (2 * kGF + 2 * kSF + 2 * kVF)), "hipMalloc");
     }
     return g_drop;
 }
