@@ -123,6 +123,9 @@ struct sml_dynamics {
     bool fused = true;
     // with GPU physics: k_st_grid + k_st_specx instead of k_st_gridspec (SML_DYN_SPLIT_GRID=1)
     bool split_grid = false;
+    // the fused step's hand-offs (vfm, varm, the m-major state) stored write-through
+    // (store2; SML_DYN_WT=1)
+    bool wt = false;
     // mod_lflags lradsw (module default .true.) and stloop's istep (at_gcm.f90:81)
     bool lradsw = true;
     int istep = 1;
@@ -750,6 +753,23 @@ __global__ __launch_bounds__(256) void k_dyn_tail(double *__restrict__ st, doubl
 typedef double d4 __attribute__((ext_vector_type(4)));
 #define MFMA64(a, b, c) __builtin_amdgcn_mfma_f64_16x16x4f64((a), (b), (c), 0, 0, 0)
 
+// Write-through 16-B store (cache policy sc1): the line leaves the XCD's L2 as it is
+// written, so the release at the kernel's end has none of it to write back -- the
+// inter-kernel hand-offs of the fused step (vfm, the next step's varm and state) when
+// Dyn::wt is on (SML_DYN_WT).  A raw buffer store (0x00020000: the gfx9 descriptor
+// word 3) so the compiler tracks it like any other vector-memory store.
+__device__ __attribute__((always_inline)) inline void store2(double *base, size_t idx, double a, double b, bool wt) {
+    if (wt) {
+        typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+        typedef double dv2 __attribute__((ext_vector_type(2)));
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7fffffff, 0x00020000);
+        const dv2 v = {a, b};
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, v), rs, (int)(idx * sizeof(double)), 0, 16);
+    } else {
+        *reinterpret_cast<double2 *>(base + idx) = double2{a, b};
+    }
+}
+
 constexpr int kCW = 2 * kNX;                  // real coefficients (n, p) of one m
 // iogrid's field-major work layout, both directions: [u 8 | v 8 | t 8 | q 8 | ps]
 constexpr int kNIo = 4 * kKX + 1;
@@ -913,7 +933,7 @@ __device__ inline GridyB gridy_operands(const double *__restrict__ pinv, int m) 
 }
 
 __device__ inline void gridy_m(const double *In, const GridyB &gb, double *__restrict__ varm, int m, int nf,
-                               int tile0 = 0, int tile1 = -1) {
+                               int tile0 = 0, int tile1 = -1, bool wt = false) {
     const int wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
     const int l = threadIdx.x & 63, r = l & 15, kk = l >> 4;
     const int tend = tile1 < 0 ? (nf + 7) / 8 : tile1;
@@ -939,6 +959,24 @@ __device__ inline void gridy_m(const double *In, const GridyB &gb, double *__res
             // 4 latitudes (4 lines) instead of 4 of 16 latitudes (16 lines)
             accS = MFMA64(half ? gb.b01[s] : gb.b00[s], a0, accS);
             accA = MFMA64(half ? gb.b11[s] : gb.b10[s], a1, accA);
+        }
+        if (wt) {
+            // the (Re, Im) pair of field fa is held by lanes r and r ^ 1: lane p stores
+            // both for the rows q = p, p + 2, as one 16-B write-through store each
+            // (the same values; ok is the same on both lanes of a pair)
+            double *vr = varm + (size_t)m * kVIm + fa * 2;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int j = 16 * half + kk + 4 * q;
+                const double n_own = accS[q] + accA[q], s_own = accS[q] - accA[q];
+                const double n_oth = __shfl_xor(n_own, 1), s_oth = __shfl_xor(s_own, 1);
+                if (!ok || j >= kIY || (q & 1) != p) continue;
+                const double nre = p ? n_oth : n_own, nim = p ? n_own : n_oth;
+                const double sre = p ? s_oth : s_own, sim = p ? s_own : s_oth;
+                store2(vr, (size_t)(kIL - 1 - j) * kVIl, nre, nim, true);
+                store2(vr, (size_t)j * kVIl, sre, sim, true);
+            }
+            continue;
         }
         if (!ok) continue;
         // m-major inverse Fourier coefficients vim[m][lat][f][p]: column r = 2 (fa - f0) + p
@@ -1120,7 +1158,7 @@ __device__ __attribute__((always_inline)) inline void row_gridx_half(double *A, 
 __device__ __attribute__((always_inline)) inline void row_specx_pair(const double *x48, double *S, bool act,
                                                                      double *__restrict__ vfm,
                                                                      const double *__restrict__ wa, int f, int j,
-                                                                     int h) {
+                                                                     int h, bool wt = false) {
     if (act) {
 #pragma unroll
         for (int i = 0; i < 48; ++i) S[(48 * h + i) * kRowLd + f] = x48[i];
@@ -1130,7 +1168,6 @@ __device__ __attribute__((always_inline)) inline void row_specx_pair(const doubl
     auto E = [&](int i) { return S[i * kRowLd + f]; };
     auto O = [&](int i) { return S[(48 + i) * kRowLd + f]; };
     const double scale = 1. / (double)kIX;
-    double *o = vfm + (size_t)j * kVLs + f * 2;
     // lane h does m = 16 h + i, i = 0..15, with the operands of its m selected per lane
     // (the halves' different m ranges were divergent branches: each wave ran both);
     // every m's expressions are rfftf96_combine's: E(2s-1) +- tr2, ti2 +- E(2s) with
@@ -1157,7 +1194,7 @@ __device__ __attribute__((always_inline)) inline void row_specx_pair(const doubl
             re = E(47);
             im = -O(47);
         }
-        *reinterpret_cast<double2 *>(o + (size_t)m * kVFm) = double2{re * scale, im * scale};
+        store2(vfm, (size_t)j * kVLs + f * 2 + (size_t)m * kVFm, re * scale, im * scale, wt);
     }
 }
 
@@ -1361,7 +1398,7 @@ __device__ inline int phys_slot_col(int s) { return s < 3 * kKX + 1 ? kPT1 + s :
 __global__ __launch_bounds__(kGsThreads) void k_st_gridspec(
     const double *__restrict__ varm, double *__restrict__ vfm, const double *__restrict__ wa,
     const double *__restrict__ cosgr, const DynTables *__restrict__ T, const double *__restrict__ bc,
-    double *__restrict__ rad, const PhysTables *__restrict__ PT, int lradsw, long long *dbg) {
+    double *__restrict__ rad, const PhysTables *__restrict__ PT, int lradsw, int wt, long long *dbg) {
     __shared__ double A[kFftN * kRowLd], B[kFftN * kRowLd];
     // the FFT twiddles as literals (kFftWa96: the same values as wa, bit for bit), folded
     // into the unrolled passes instead of LDS reads of a staged table
@@ -1538,7 +1575,7 @@ __global__ __launch_bounds__(kGsThreads) void k_st_gridspec(
             fft::rfftf48_reg(x, was);
         }
         __syncthreads();  // A's P columns are read: A becomes the pairs' meeting place
-        row_specx_pair(x, A, act, vfm, was, f, j, h);
+        row_specx_pair(x, A, act, vfm, was, f, j, h, wt != 0);
     }
     stamp(dbg, 0, 3);
 }
@@ -1566,7 +1603,7 @@ __global__ __launch_bounds__(kSpecBlk) void k_st_spec(
     const double *__restrict__ tcorh, const double *__restrict__ qcorh, const DynTables *__restrict__ T, int j1,
     int j4, double dt, double alph, double rob, double wil, const double *__restrict__ pinv,
     double *__restrict__ varm_next, int next_j2, int n1, int nin, const double *__restrict__ tabm,
-    double *__restrict__ state_out, double *__restrict__ io_varm, long long *dbg) {
+    double *__restrict__ state_out, double *__restrict__ io_varm, int wthru, long long *dbg) {
     __shared__ double V[kVFm];            // this m's tables (TabM)
     __shared__ double S[kNInvMax * kCW];  // specy output [f][2 n + p]; then the next step's inputs
     __shared__ double sh[2][kKX][kCW];
@@ -1739,13 +1776,13 @@ __global__ __launch_bounds__(kSpecBlk) void k_st_spec(
     }
     if (lead) {  // into the other buffer: this m's second block may still be reading sm
         // (five whole rows of the block, static_assert above: the LDS reads issue together)
-        double2 *dst = reinterpret_cast<double2 *>(sm_out + (size_t)m * kSM) + threadIdx.x;
         const double2 *src = reinterpret_cast<const double2 *>(Sst) + threadIdx.x;
         double2 v[RS];
 #pragma unroll
         for (int q = 0; q < RS; ++q) v[q] = src[q * kSpecBlk];
 #pragma unroll
-        for (int q = 0; q < RS; ++q) dst[q * kSpecBlk] = v[q];
+        for (int q = 0; q < RS; ++q)
+            store2(sm_out, (size_t)m * kSM + 2 * ((size_t)q * kSpecBlk + threadIdx.x), v[q].x, v[q].y, wthru != 0);
     }
     // d) the next step's inverse-transform inputs (k_dyn_prep) and gridy
     if (holds) inv_inputs(Sst, S, Fm, tb, m, next_j2, n1, nin);
@@ -1753,7 +1790,8 @@ __global__ __launch_bounds__(kSpecBlk) void k_st_spec(
     stamp(dbg, sk, 5);
     {
         const int nt = (nin + 7) / 8, per = (nt + kSpecSplit - 1) / kSpecSplit;
-        gridy_m(S, gridy_operands_slice(V + kVPinv), varm_next, m, nin, half * per, min(nt, (half + 1) * per));
+        gridy_m(S, gridy_operands_slice(V + kVPinv), varm_next, m, nin, half * per, min(nt, (half + 1) * per),
+                wthru != 0);
     }
     if (dbg) {  // (diagnostics only: the kernel ends here)
         __syncthreads();
@@ -2052,6 +2090,7 @@ extern "C" int sml_dyn_create(double radius, sml_dynamics **out) {
     build_phys_tables(d->tab, &d->ptab);
     if (const char *e = std::getenv("SML_DYN_FUSED")) d->fused = *e && *e != '0';
     if (const char *e = std::getenv("SML_DYN_SPLIT_GRID")) d->split_grid = *e && *e != '0';
+    if (const char *e = std::getenv("SML_DYN_WT")) d->wt = *e && *e != '0';
     if (const char *e = std::getenv("SML_DYN_STAMPS"))
         if (*e && *e != '0' && (rc = dalloc(reinterpret_cast<double **>(&d->d_dbg), kStampKernels * kStampBlocks * kStamps))) {
             sml_dyn_destroy(d);
@@ -2259,7 +2298,7 @@ int launch_step_fused(sml_dynamics *d, int j1, int j2, double dt, double alph, d
                                sd.wa, sd.cosgr, d->d_dbg);
         } else {
             hipLaunchKernelGGL(k_st_gridspec, dim3(kIL), dim3(kGsThreads), 0, st, d->d_varm, d->d_vfm, sd.wa, sd.cosgr,
-                               T, d->d_pbc, d->d_rad, d->d_ptab, lradsw ? 1 : 0, d->d_dbg);
+                               T, d->d_pbc, d->d_rad, d->d_ptab, lradsw ? 1 : 0, d->wt ? 1 : 0, d->d_dbg);
         }
         SML_HIP(hipGetLastError());
     } else {
@@ -2274,7 +2313,7 @@ int launch_step_fused(sml_dynamics *d, int j1, int j2, double dt, double alph, d
                        sm_buf(d, cur), sm_buf(d, 1 - cur), d->d_tend,
                        d->d_phi, d->d_phis, d->d_tcorh, d->d_qcorh, T, j1, j4, dt, alph, rob, wil, sd.pinv, d->d_varm,
                        next_j2, n1, nin, d->d_tabm + (size_t)(d->d_tab - d->d_tabs) * kMX * kTabMDoubles, d->d_state,
-                       next_j2 > 0 ? nullptr : d->io_exit, d->d_dbg);
+                       next_j2 > 0 ? nullptr : d->io_exit, d->wt ? 1 : 0, d->d_dbg);
     SML_HIP(hipGetLastError());
     return SML_OK;
 }

@@ -333,3 +333,41 @@ def test_window_graph_is_bitwise_the_launched_window(pg, cuda):
         np.testing.assert_array_equal(a[f], b[f])
     for k in ra:
         np.testing.assert_array_equal(ra[k], rb[k])
+
+
+def test_write_through_handoffs_are_bitwise_the_default(pg, cuda):
+    """SML_DYN_WT=1 stores the fused step's hand-offs (vfm, the next step's varm and
+    the m-major state) write-through (sml_dynamics.hip store2: cache policy sc1, 16-B
+    stores, gridy's Re/Im pairs exchanged between neighbouring lanes): the same values
+    in the same places, so two chained windows with physics are bitwise the default's."""
+    import os
+
+    import torch
+
+    from speedy_ml_amd.dynamics import Dynamics
+    from speedy_ml_amd.synthetic import dyn_state
+
+    st, forcing = dyn_state(5)
+    out = []
+    for wt in ("0", "1"):
+        os.environ["SML_DYN_WT"] = wt
+        try:
+            d = Dynamics()
+        finally:
+            os.environ.pop("SML_DYN_WT", None)
+        d.set_forcing(**forcing)
+        d.set_state(st)
+        d.set_physics(_window_bc(pg, d))
+        d.set_rad_state(None)
+        d.set_clock(1, True)
+        d.window(24)
+        d.window(24)
+        torch.cuda.synchronize()
+        out.append((d.get_state(), d.get_rad_state(), d.get_phi()))
+        d.close()
+    (a, ra, pa), (b, rb, pb) = out
+    for f in oracle.DYN_FIELDS:
+        np.testing.assert_array_equal(a[f], b[f])
+    for k in ra:
+        np.testing.assert_array_equal(ra[k], rb[k])
+    np.testing.assert_array_equal(pa, pb)
