@@ -32,8 +32,21 @@ check(L.sml_stream_create_cu_range(0, 64, ctypes.byref(s_side)))
 check(L.sml_stream_create_cu_range(64, 192, ctypes.byref(s_main)))
 side = torch.cuda.ExternalStream(s_side.value, device=dev)
 main = torch.cuda.ExternalStream(s_main.value, device=dev)
-src = torch.empty(3_700_000_000 // 8, dtype=torch.float64, device=dev)
+NB = 3_700_000_000
+MEM = os.environ.get("PARTNER_MEM", "default")  # default | uncached | finegrained: the partner's buffer
+if MEM == "default":
+    src = torch.empty(NB // 8, dtype=torch.float64, device=dev)
+else:
+    hip = ctypes.CDLL("libamdhip64.so")
+    ptr = ctypes.c_void_p()
+    assert hip.hipExtMallocWithFlags(ctypes.byref(ptr), ctypes.c_size_t(NB), {"uncached": 3, "finegrained": 1}[MEM]) == 0
+
+    class _Buf:  # a torch view of the hipExtMallocWithFlags buffer
+        __cuda_array_interface__ = {"shape": (NB // 8,), "typestr": "<f8", "data": (ptr.value, False), "version": 2}
+
+    src = torch.as_tensor(_Buf(), device=dev)
 src.uniform_()
+print("partner buffer:", MEM)
 K = {0: ("grid", ["gridx", "physics+sums", "specx"]),
      1: ("spec", ["load", "specy", "combine", "tail", "inv_inputs", "gridy"]),
      3: ("spec_last", ["load", "specy", "combine", "tail"])}
