@@ -198,13 +198,20 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
+        host = []
         for _ in range(nsteps):
+            h0 = time.perf_counter()
             fn()
+            host.append(time.perf_counter() - h0)
+        th = time.perf_counter() - t0
         loop.sync()
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         dt = time.perf_counter() - t0
+        if os.environ.get("SML_BENCH_HOST"):  # diagnostic: does the host keep ahead of the GPU?
+            log(rank, f"host: enqueue {th * 1e3 / nsteps:.3f} ms/step of {dt * 1e3 / nsteps:.3f}; per call median "
+                      f"{np.median(host) * 1e3:.3f} max {max(host) * 1e3:.3f} ms")
         if world > 1:
             t = torch.tensor([dt], dtype=torch.float64, device=dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)

@@ -123,6 +123,7 @@ struct sml_dynamics {
     bool fused = true;
     // with GPU physics: k_st_grid + k_st_specx instead of k_st_gridspec (SML_DYN_SPLIT_GRID=1)
     bool split_grid = false;
+    bool nograph = false;  // SML_DYN_NOGRAPH=1: the window's launches issued directly, not replayed
     // the fused step's hand-offs (vfm, varm, the m-major state) stored write-through
     // (store2; SML_DYN_WT=1)
     bool wt = false;
@@ -2090,6 +2091,7 @@ extern "C" int sml_dyn_create(double radius, sml_dynamics **out) {
     build_phys_tables(d->tab, &d->ptab);
     if (const char *e = std::getenv("SML_DYN_FUSED")) d->fused = *e && *e != '0';
     if (const char *e = std::getenv("SML_DYN_SPLIT_GRID")) d->split_grid = *e && *e != '0';
+    if (const char *e = std::getenv("SML_DYN_NOGRAPH")) d->nograph = *e && *e != '0';
     if (const char *e = std::getenv("SML_DYN_WT")) d->wt = *e && *e != '0';
     if (const char *e = std::getenv("SML_DYN_STAMPS"))
         if (*e && *e != '0' && (rc = dalloc(reinterpret_cast<double **>(&d->d_dbg), kStampKernels * kStampBlocks * kStamps))) {
@@ -2423,6 +2425,23 @@ int window_impl(sml_dynamics *d, int nleap, double delt, double alph, double rob
         tab[i] = d->d_tab;
     }
     const bool entry = d->lradsw;
+    if (d->nograph) {  // the same launches, issued one by one on the stream (A/B: SML_DYN_NOGRAPH=1)
+        hipStream_t st = (hipStream_t)stream;
+        d->d_tab = tab[0];
+        d->io_exit = prepared ? d->d_varm : nullptr;
+        int rc = launch_step(d, 1, 1, dts[0], alph, rob, wil, nullptr, entry, st, prepared, 2);
+        d->d_tab = tab[1];
+        if (!rc) rc = launch_step(d, 1, 2, dts[1], alph, rob, wil, nullptr, entry, st, true, nleap > 0 ? 2 : 0);
+        d->d_tab = tab[2];
+        for (int i = 0; i < nleap && !rc; ++i)
+            rc = launch_step(d, 2, 2, dts[2], alph, rob, wil, nullptr, (1 + i) % kNstrad == 1, st, true,
+                             i + 1 < nleap ? 2 : 0);
+        d->io_exit = nullptr;
+        if (rc) return rc;
+        d->istep = 1 + nleap;
+        if (nleap > 0) d->lradsw = (nleap % kNstrad == 1);
+        return SML_OK;
+    }
     sml_dynamics::WindowReplay &r = d->wreplay[(entry ? 1 : 0) + (prepared ? 2 : 0)];
     const double key[8] = {(double)nleap, delt,  alph, rob, wil, d->phys_on ? 1.0 : 0.0, d->fused ? 1.0 : 0.0,
                            prepared ? 2.0 : 1.0};
