@@ -192,6 +192,15 @@ int sml_res_step_finish_grid(sml_reservoirs *c, const double *d_fc4d, const doub
  * both share CUs; on CUs of their own (sml_stream_create_cu_range) it is not needed.
  * The environment variable SML_READ_WAVES, when set, takes precedence. */
 int sml_res_set_read_waves(sml_reservoirs *c, int waves);
+/* the form of sml_res_step_begin (predict's update + the v_ml half of the readout,
+ * src/mod_reservoir.f90:1440-1455): 0 = the update grid, then the readout grid;
+ * 1 = one launch, a block per region that updates its state and then streams its
+ * W_out rows (k_res_begin, up to 3 blocks per CU); 2 = the same with the W_out loads
+ * unrolled twice (1 block per CU).  Every form gives bit-identical states and sums.
+ * The fused forms need the 17-row readout and <= 64 KB of LDS per region; otherwise
+ * form 0 runs (sml_res_begin_fused says which).  SML_BEGIN, when set, overrides. */
+int sml_res_set_begin_mode(sml_reservoirs *c, int mode);
+int sml_res_begin_fused(const sml_reservoirs *c, int *fused);
 /* synchronize (src/mod_reservoir.f90:1352-1378), the spin-up of start_prediction
  * (:938-959): `length` updates x = (1-leak) x + leak tanh(A x + W_in u_t) for every
  * local region, no readout.  d_inputs holds `length` blocks in the packed feedback

@@ -108,6 +108,10 @@ struct sml_reservoirs {
     // SML_READ_WAVES overrides both.
     int read_waves = 2048;
     int upd_blocks = 0;  // cap on the update's grid in sml_res_step_begin (0: none; SML_UPD_BLOCKS)
+    // sml_res_step_begin's form (sml_res_set_begin_mode; SML_BEGIN overrides): 0 the
+    // update grid then the v_ml readout grid, 1 one fused launch (k_res_begin, 2 blocks
+    // per CU), 2 fused with the readout's loads unrolled twice (1 block per CU)
+    int begin_mode = 0;
     bool begun = false;             // sml_res_step_begin issued, finish pending
     int8_t *d_outl = nullptr;
     int32_t *d_asm_dst = nullptr;   // [numregions*nout] -> concatenated grid index
@@ -219,7 +223,7 @@ __device__ inline int ell_col(const uint4 &c, int s) {
 // padding slots hold 0 * x[0] after the row's real entries, so the file-order sum
 // is unchanged), otherwise from the CSR copy.  The next pass's ELL loads are issued
 // before the current pass computes.
-template <typename WT, bool kLds>
+template <typename WT, bool kLds, int kThr = kUpdThreads>
 __device__ __attribute__((always_inline)) inline void update_block(
     int lb, double *smem, const RegionDev *__restrict__ R, const int32_t *__restrict__ a_rp,
     const uint16_t *__restrict__ a_col, const WT *__restrict__ a_val, const int32_t *__restrict__ w_rp,
@@ -239,8 +243,8 @@ __device__ __attribute__((always_inline)) inline void update_block(
     const double *xs = xo, *fs = fb;
     if (kLds) {
         double *sx = smem, *sf = smem + lds_x;
-        for (int j = tid; j < n; j += kUpdThreads) sx[j] = xo[j];
-        for (int j = tid; j < rg.ninp; j += kUpdThreads) sf[j] = fb[j];
+        for (int j = tid; j < n; j += kThr) sx[j] = xo[j];
+        for (int j = tid; j < rg.ninp; j += kThr) sf[j] = fb[j];
         __syncthreads();
         xs = sx;
         fs = sf;
@@ -251,11 +255,11 @@ __device__ __attribute__((always_inline)) inline void update_block(
     const int32_t *wp = w_rp + rg.w_rp;
     const uint16_t *wc = w_col + rg.w_nz;
     const WT *wv = w_val + rg.w_nz;
-    for (int base = beg; base < end; base += kUpdThreads) {
+    for (int base = beg; base < end; base += kThr) {
         const int i = base + tid;
         const bool live = i < end;
-        const int inext = i + kUpdThreads;
-        if (base + kUpdThreads < end) load_row(nxt, rg, ell, inext, inext < end);
+        const int inext = i + kThr;
+        if (base + kThr < end) load_row(nxt, rg, ell, inext, inext < end);
         if (live) {
             // y = A x, entries of row i in the file's order (COO semantics, duplicates add)
             double y = 0.0;
@@ -337,14 +341,14 @@ struct Rows {
     double v[R];
 };
 
-template <typename WT, int R, typename XF>
+template <typename WT, int R, int kUnroll = 2, typename XF>
 __device__ __attribute__((always_inline)) inline Rows<R> rows_dot(const WT *W, int ld, int lane, int c0, int c1,
                                                                XF xload) {
     typedef typename Vec4<WT>::N V;
     double acc[R];
 #pragma unroll
     for (int q = 0; q < R; ++q) acc[q] = 0.0;
-#pragma unroll 2
+#pragma unroll kUnroll
     for (int j = c0 + lane * 4; j < c1; j += 256) {
         const double4 xv = xload(j);
         V w[R];
@@ -453,6 +457,51 @@ __global__ __launch_bounds__(512) void k_res_readout(const RegionDev *__restrict
                 outvec[(size_t)r * ov_ld + o] = unstd(vp + vml, meanstd + (size_t)r * 2 * kMeanStd, outl[o]);
             }
         }
+    }
+}
+
+// sml_res_step_begin's two launches (k_res_update, then k_res_readout<kReadML>) as
+// one, a block per region: the block updates its region's state (update_block, the
+// same rows in the same order, kBeginThreads rows per pass) and then each of its
+// waves forms one 17-row item of v_ml exactly as k_res_readout does (rows_dot: the
+// same lanes, columns and butterfly), reading x~ back from x_aug, which this block
+// has just written (same workgroup: visible after the barrier).  The update's
+// latency-bound SpMV + tanh of one block then overlaps the W_out stream of the other
+// blocks on its CU, instead of running as a grid of its own before the stream.
+// Requires the wide readout (nout_pad = 17 g, g <= 8) and the LDS-staged update.
+constexpr int kBeginThreads = 512;
+template <typename WT, int kUnroll, int kMinWaves>
+__global__ __launch_bounds__(kBeginThreads, kMinWaves) void k_res_begin(
+    const RegionDev *__restrict__ R, const int32_t *__restrict__ a_rp, const uint16_t *__restrict__ a_col,
+    const WT *__restrict__ a_val, const int32_t *__restrict__ w_rp, const uint16_t *__restrict__ w_col,
+    const WT *__restrict__ w_val, Ell ell, const double *__restrict__ x_old, double *__restrict__ x_new,
+    double *__restrict__ xaug, const double *__restrict__ feedback, int ncs, double leak, int lds_x,
+    const WT *__restrict__ wout, double *__restrict__ part, int nout_pad, int groups) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    const int r = blockIdx.x;
+    update_block<WT, true, kBeginThreads>(r, smem, R, a_rp, a_col, a_val, w_rp, w_col, w_val, ell, x_old, x_new,
+                                          xaug, feedback, ncs, leak, 1, lds_x);
+    __syncthreads();  // the region's x_aug complete (workgroup scope)
+    const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
+    if (g >= groups) return;  // wave-uniform
+    const RegionDev rg = R[r];
+    const int ld = rg.ld;
+    const WT *W = wout + rg.wout + (size_t)(g * kRowsWide) * ld;
+    const double *xa = xaug + rg.xaug;
+    // k_res_readout<kReadML>'s item (r, g): the same x~ loads (zero below ncs)
+    const Rows<kRowsWide> ml = rows_dot<WT, kRowsWide, kUnroll>(W, ld, lane, ncs & ~(kLdAlign - 1), ld, [=](int j) {
+        double4 xv = *reinterpret_cast<const double4 *>(xa + j);
+        if (j < ncs) {
+            if (j + 0 < ncs) xv.x = 0.0;
+            if (j + 1 < ncs) xv.y = 0.0;
+            if (j + 2 < ncs) xv.z = 0.0;
+            if (j + 3 < ncs) xv.w = 0.0;
+        }
+        return xv;
+    });
+    if (lane == 0) {
+#pragma unroll
+        for (int q = 0; q < kRowsWide; ++q) part[(size_t)r * nout_pad + g * kRowsWide + q] = ml.v[q];
     }
 }
 
@@ -1179,6 +1228,22 @@ extern "C" int sml_res_set_read_waves(sml_reservoirs *c, int waves) {
     return SML_OK;
 }
 
+namespace {
+bool begin_fusable(const sml_reservoirs *c);
+}
+
+extern "C" int sml_res_set_begin_mode(sml_reservoirs *c, int mode) {
+    SML_REQUIRE(c && mode >= 0 && mode <= 2, "bad argument");
+    c->begin_mode = mode;
+    return SML_OK;
+}
+
+extern "C" int sml_res_begin_fused(const sml_reservoirs *c, int *fused) {
+    SML_REQUIRE(c && fused, "null argument");
+    *fused = begin_fusable(c) ? 1 : 0;
+    return SML_OK;
+}
+
 extern "C" int sml_res_enable_timing(sml_reservoirs *c, int capacity) {
     SML_REQUIRE(c, "null context");
     SML_REQUIRE(capacity >= 0, "capacity must be >= 0");
@@ -1252,6 +1317,43 @@ int launch_update(sml_reservoirs *c, const double *xo, double *xn, const double 
     return SML_OK;
 }
 
+int begin_mode(const sml_reservoirs *c) {
+    if (const char *e = std::getenv("SML_BEGIN")) return std::atoi(e);
+    return c->begin_mode;
+}
+
+// the fused begin needs the wide readout (8 waves of 17 rows per region at most)
+// and the update's LDS staging (2 blocks per CU: <= 64 KB each)
+bool begin_fusable(const sml_reservoirs *c) {
+    const int lds_x = (c->maxn + 1) / 2 * 2;
+    return begin_mode(c) > 0 && c->nout_pad % kRowsWide == 0 && c->nout_pad / kRowsWide <= kBeginThreads / 64 &&
+           (size_t)(lds_x + c->maxninp) * sizeof(double) <= 64 * 1024;
+}
+
+int launch_begin(sml_reservoirs *c, const double *xo, double *xn, const double *d_feedback, hipStream_t st) {
+    const int lds_x = (c->maxn + 1) / 2 * 2;
+    const size_t lds = (size_t)(lds_x + c->maxninp) * sizeof(double);
+    const int groups = c->nout_pad / kRowsWide;
+    Ell ell{c->d_a_ell_col, c->d_a_ell_val, c->d_w_ell_col, c->d_w_ell_val};
+    auto go = [&](auto wt_tag, auto kern) {
+        using WT = decltype(wt_tag);
+        hipLaunchKernelGGL(kern, dim3(c->nlocal), dim3(kBeginThreads), lds, st, c->d_rd, c->d_a_rp, c->d_a_col,
+                           (const WT *)c->d_a_val, c->d_w_rp, c->d_w_col, (const WT *)c->d_w_val, ell, xo, xn,
+                           c->d_xaug, d_feedback, c->ncs, c->leakage, lds_x, (const WT *)c->d_wout, c->d_part,
+                           c->nout_pad, groups);
+    };
+    const bool two = begin_mode(c) == 2;
+    if (c->wdtype == SML_F32) {
+        if (two) go(float{}, k_res_begin<float, 2, 2>);
+        else go(float{}, k_res_begin<float, 1, 4>);
+    } else {
+        if (two) go(double{}, k_res_begin<double, 2, 2>);
+        else go(double{}, k_res_begin<double, 1, 4>);
+    }
+    SML_HIP(hipGetLastError());
+    return SML_OK;
+}
+
 int check_loaded(const sml_reservoirs *c) {
     for (int i = 0; i < c->nlocal; ++i)
         if (!c->loaded[i]) return fail(SML_ERR_STATE, "local region %d has no weights loaded", i);
@@ -1316,9 +1418,14 @@ extern "C" int sml_res_step_begin(sml_reservoirs *c, const double *d_feedback, v
     const bool rec = c->timing && c->ev_used < c->ev_cap;
     hipEvent_t *ev = rec ? &c->ev[3 * c->ev_used] : nullptr;
     if (rec) SML_HIP(hipEventRecord(ev[0], st));
-    if (int rc = launch_update(c, xo, xn, d_feedback, st, true)) return rc;  // beside SPEEDY's window
-    if (rec) SML_HIP(hipEventRecord(ev[1], st));
-    launch_readout<kReadML>(c, nullptr, nullptr, st);
+    if (begin_fusable(c)) {  // one launch: the update's time is inside the readout's (update_ms 0)
+        if (rec) SML_HIP(hipEventRecord(ev[1], st));
+        if (int rc = launch_begin(c, xo, xn, d_feedback, st)) return rc;
+    } else {
+        if (int rc = launch_update(c, xo, xn, d_feedback, st, true)) return rc;  // beside SPEEDY's window
+        if (rec) SML_HIP(hipEventRecord(ev[1], st));
+        launch_readout<kReadML>(c, nullptr, nullptr, st);
+    }
     SML_HIP(hipGetLastError());
     if (rec) {
         SML_HIP(hipEventRecord(ev[2], st));

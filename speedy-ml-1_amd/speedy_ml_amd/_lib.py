@@ -30,6 +30,7 @@ EXPORTED = (
     "sml_res_load_region_f32", "sml_res_load_region_f64", "sml_res_set_state", "sml_res_get_state",
     "sml_res_step", "sml_res_step_begin", "sml_res_step_finish", "sml_res_step_finish_grid", "sml_res_step_host", "sml_res_synchronize",
     "sml_res_footprint", "sml_res_enable_timing", "sml_res_kernel_times", "sml_res_set_read_waves",
+    "sml_res_set_begin_mode", "sml_res_begin_fused",
     "sml_exchange_assemble",
     "sml_res_tile_inputs", "sml_res_tile_feedback", "sml_res_tile_local_model",
     "sml_nc_read_region", "sml_nc_write_region",
@@ -129,6 +130,8 @@ def _declare(L: ctypes.CDLL) -> None:
         "sml_res_footprint": [vp, i64p, i64p],
         "sml_res_enable_timing": [vp, i],
         "sml_res_set_read_waves": [vp, i],
+        "sml_res_set_begin_mode": [vp, i],
+        "sml_res_begin_fused": [vp, vp],
         "sml_res_kernel_times": [vp, vp, vp, i, ctypes.POINTER(ctypes.c_int)],
         "sml_exchange_assemble": [vp, vp, vp, vp, vp, vp],
         "sml_res_tile_inputs": [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp],

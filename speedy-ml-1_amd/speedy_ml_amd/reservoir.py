@@ -130,6 +130,18 @@ class Reservoirs:
         """Cap on the v_ml readout's waves in predict_begin (0 = uncapped)."""
         check(lib().sml_res_set_read_waves(self._h, int(waves)))
 
+    def set_begin_mode(self, mode: int):
+        """predict_begin's form: 0 update grid + readout grid, 1 / 2 one fused launch
+        (sml_res_set_begin_mode); bit-identical results."""
+        check(lib().sml_res_set_begin_mode(self._h, int(mode)))
+
+    @property
+    def begin_fused(self) -> bool:
+        """Whether predict_begin runs as the fused launch (the mode and this context's shapes)."""
+        f = ctypes.c_int()
+        check(lib().sml_res_begin_fused(self._h, ctypes.byref(f)))
+        return bool(f.value)
+
     def predict_finish(self, d_local_model, d_outvec, stream=None):
         """Second half: outvec = W_out(:, 1:ncs) local_model + v_ml, unstandardized."""
         check(lib().sml_res_step_finish(self._h, ptr(d_local_model if self.ncs else None), ptr(d_outvec),

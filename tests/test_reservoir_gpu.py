@@ -407,3 +407,45 @@ def test_predict_slab_matches_oracle(cuda):
         d_lm, d_next = d_next, d_lm  # the raw outvec is the next local model
     with pytest.raises(SmlError):
         res.predict_slab(torch.from_numpy(fb).to(cuda), d_lm, d_lm, d_ov)  # aliasing refused
+
+
+@pytest.mark.parametrize("weight_dtype", ["f32", "f64"])
+@pytest.mark.parametrize("mode", [1, 2])
+def test_fused_begin_is_bitwise_the_two_launch_begin(cuda, weight_dtype, mode):
+    """sml_res_set_begin_mode 1 / 2 (k_res_begin: update + v_ml readout, one block per
+    region) vs mode 0 (k_res_update grid, then k_res_readout<ml> grid): outvecs and
+    states bitwise over 3 chained begin + finish steps at full reservoir size."""
+    import torch
+
+    from speedy_ml_amd.reservoir import Reservoirs
+
+    cases = CASES[:4]
+    ws = [region_weights(r, s, seed=5) for r, s in cases]
+    fbs = [np.concatenate([feedback_vector(w.region, w.ninp) for w in ws]) * (1.0 + 0.1 * k) for k in range(3)]
+    lm = torch.from_numpy(np.stack([local_model_vector(w.region) for w in ws])).to(cuda)
+    outs = {}
+    for m in (0, mode):
+        res = Reservoirs([w.region for w in ws], [w.sst for w in ws], [w.n for w in ws], [w.k for w in ws],
+                         weight_dtype=weight_dtype)
+        for i, w in enumerate(ws):
+            if weight_dtype == "f64":
+                res.load_region(i, w.rows, w.cols, w.vals.astype(np.float64), w.win.astype(np.float64),
+                                w.wout.astype(np.float64), w.mean, w.std)
+            else:
+                res.load_region_weights(i, w)
+            res.set_state(i, initial_state(w.region, w.n))
+        res.set_begin_mode(m)
+        assert res.begin_fused == (m > 0)
+        ov = torch.zeros((len(ws), 136), dtype=torch.float64, device=cuda)
+        seq = []
+        for fbh in fbs:
+            res.predict_begin(torch.from_numpy(fbh).to(cuda))
+            res.predict_finish(lm, ov)
+            torch.cuda.synchronize()
+            seq.append((ov.cpu().numpy().copy(), [res.get_state(i) for i in range(len(ws))]))
+        outs[m] = seq
+        res.close()
+    for (oa, xa), (ob, xb) in zip(outs[0], outs[mode]):
+        np.testing.assert_array_equal(oa, ob)
+        for a, b in zip(xa, xb):
+            np.testing.assert_array_equal(a, b)
