@@ -561,7 +561,7 @@ __global__ void k_dyn_combine(const double *__restrict__ S, double *__restrict__
 
 // tail: sptend + geop + implic + hordif + drag + timint of one real coefficient c
 // (= Re/Im of (m, n)) at level k, given grtend's spectral tendencies of (c, k).
-// The CW coefficients x 8 levels of a block share sh[2][kx][CW] (LDS) for the
+// The CW coefficients x 8 levels of a block share sh[3][kx][CW] (LDS) for the
 // vertical couplings (dmeanc, sigdtc, geop, implic's level matrices); every sum
 // runs over k in the reference's order.  The whole block must call it (barriers).
 template <int CW, class SA, class TB>
@@ -621,12 +621,13 @@ __device__ inline void tail_coef(SA S, double *__restrict__ Td, double *__restri
     }
     // ---- implic(divdt, tdt, psdt)  (dyn_implic.f90:22-67)
     if (alph != 0.0) {
-        __syncthreads();  // sh reuse
-        sh[0][k][cc] = tdt;
+        // tdt into the third plane: sptend's reads of sh[0] need no barrier of their
+        // own before it (sh[1]'s geop reads end at the next one, before yf is written)
+        sh[2][k][cc] = tdt;
         __syncthreads();
         double ye = 0.0;
 #pragma unroll
-        for (int k1 = 0; k1 < kKX; ++k1) ye = ye + tb.xd(k1, k) * sh[0][k1][cc];
+        for (int k1 = 0; k1 < kKX; ++k1) ye = ye + tb.xd(k1, k) * sh[2][k1][cc];
         ye = ye + tb.tref1(k) * psdt;
         sh[1][k][cc] = divdt + tb.elz_n(n) * ye;  // yf
         __syncthreads();
@@ -695,11 +696,10 @@ __device__ inline void tail_coef(SA S, double *__restrict__ Td, double *__restri
 }
 
 // the barriers tail_coef executes, for threads of a block that hold no coefficient
-// (keep in step with tail_coef: 1 in sptend, 4 in implic when alph != 0)
+// (keep in step with tail_coef: 1 in sptend, 3 in implic when alph != 0)
 __device__ inline void tail_coef_barriers(double alph) {
     __syncthreads();
     if (alph != 0.0) {
-        __syncthreads();
         __syncthreads();
         __syncthreads();
         __syncthreads();
@@ -713,7 +713,7 @@ __global__ __launch_bounds__(256) void k_dyn_tail(double *__restrict__ st, doubl
                                                   const double *__restrict__ tcorh, const double *__restrict__ qcorh,
                                                   const DynTables *__restrict__ T, int j1, int j4, double dt,
                                                   double alph, double rob, double wil) {
-    __shared__ double sh[2][kKX][kTailC];
+    __shared__ double sh[3][kKX][kTailC];
     const int cc = threadIdx.x & (kTailC - 1), k = threadIdx.x / kTailC;
     const int c = blockIdx.x * kTailC + cc;  // 0 .. 1983 = 2 * (m + mx n) + p
     const int mn = c >> 1, m = mn % kMX, n = mn / kMX;
@@ -1066,6 +1066,16 @@ __device__ inline void load_forcing_m(double *Fm, const double *__restrict__ phi
 constexpr int kSpecThreads = kCW * kKX;  // 512: one thread per (coefficient, level) of one m
 constexpr int kSpecBlk = 512;             // k_st_spec's block (768: specy -0.6 us, staging +1.2 us, gridy unchanged)
 constexpr int kSpecSplit = 2;             // k_st_spec blocks per m (the next step's gridy tiles split between them)
+// k_st_spec's grid: block b takes m = b % kSpecStride, half = b / kSpecStride.  A
+// launch places block b on the same XCD every time (tools/probe_xcd_l2.hip), so
+// with a stride of 32 (two idle blocks) both blocks of an m share the XCD of the
+// lead block that wrote the m's state in the previous step: its slice and the m's
+// tables are L2 hits for both (stride 31: the second block's state read crosses XCDs)
+#ifndef SML_SPEC_STRIDE
+#define SML_SPEC_STRIDE 31
+#endif
+constexpr int kSpecStride = SML_SPEC_STRIDE;
+static_assert(kSpecStride >= kMX, "k_st_spec grid stride");
 
 // window start: the inverse transforms of step (.., j2) from the m-major state
 __global__ __launch_bounds__(kSpecThreads) void k_st_inv(const double *__restrict__ sm, const double *__restrict__ phis,
@@ -1607,13 +1617,14 @@ __global__ __launch_bounds__(kSpecBlk) void k_st_spec(
     double *__restrict__ state_out, double *__restrict__ io_varm, int wthru, long long *dbg) {
     __shared__ double V[kVFm];            // this m's tables (TabM)
     __shared__ double S[kNInvMax * kCW];  // specy output [f][2 n + p]; then the next step's inputs
-    __shared__ double sh[2][kKX][kCW];
+    __shared__ double sh[3][kKX][kCW];
     __shared__ double Sst[kSM];           // this m's state, updated in place
     __shared__ double Fm[3 * kCW];        // phis, tcorh, qcorh of this m
     // kSpecSplit blocks per m: each repeats the m's specy, combine and tail (on CUs that
     // would idle), and takes its share of the next step's gridy tiles; the lead block
     // (half 0) alone writes the state, phi and the stamps
-    const int m = blockIdx.x % kMX, half = blockIdx.x / kMX;
+    const int m = blockIdx.x % kSpecStride, half = blockIdx.x / kSpecStride;
+    if (m >= kMX) return;  // (block-uniform: the grid's idle blocks)
     const bool lead = half == 0;
     if (!lead) dbg = nullptr;
     const int wave = threadIdx.x >> 6, l = threadIdx.x & 63, r = l & 15, kk = l >> 4;
@@ -2311,7 +2322,7 @@ int launch_step_fused(sml_dynamics *d, int j1, int j2, double dt, double alph, d
     const int j4 = (alph == 0.0) ? j2 : 1;
     const int cur = d->sm_cur;
     if (next_j2 > 0) d->sm_cur = 1 - cur;  // the next step reads what this one writes
-    hipLaunchKernelGGL(k_st_spec, dim3(kMX * kSpecSplit), dim3(kSpecBlk), 0, st, d->d_vfm, d->d_pfl, sd.wt,
+    hipLaunchKernelGGL(k_st_spec, dim3(kSpecStride * kSpecSplit), dim3(kSpecBlk), 0, st, d->d_vfm, d->d_pfl, sd.wt,
                        sm_buf(d, cur), sm_buf(d, 1 - cur), d->d_tend,
                        d->d_phi, d->d_phis, d->d_tcorh, d->d_qcorh, T, j1, j4, dt, alph, rob, wil, sd.pinv, d->d_varm,
                        next_j2, n1, nin, d->d_tabm + (size_t)(d->d_tab - d->d_tabs) * kMX * kTabMDoubles, d->d_state,
