@@ -1067,12 +1067,17 @@ constexpr int kSpecThreads = kCW * kKX;  // 512: one thread per (coefficient, le
 constexpr int kSpecBlk = 512;             // k_st_spec's block (768: specy -0.6 us, staging +1.2 us, gridy unchanged)
 constexpr int kSpecSplit = 2;             // k_st_spec blocks per m (the next step's gridy tiles split between them)
 // k_st_spec's grid: block b takes m = b % kSpecStride, half = b / kSpecStride.  A
-// launch places block b on the same XCD every time (tools/probe_xcd_l2.hip), so
-// with a stride of 32 (two idle blocks) both blocks of an m share the XCD of the
-// lead block that wrote the m's state in the previous step: its slice and the m's
-// tables are L2 hits for both (stride 31: the second block's state read crosses XCDs)
+// launch on a stream places block b on the same XCD every time, the same for every
+// kernel of the stream (tools/probe_xcd_l2.hip: XCD = (b + c) mod 8), so with a
+// stride of 32 (two idle blocks) both blocks of an m share the XCD of the lead block
+// that wrote the m's state in the previous step (and of k_io_entry's block m): the
+// slice and the m's tables are L2 hits for both, and the second block's copy of the
+// m's Fourier coefficients merges with the first's in that L2.  Stride 31 (62 blocks):
+// the second block's reads cross XCDs; same-box A/B: window 0.822 -> 0.800 ms,
+// 1006.6 / 1013.5 -> 1018.9 / 1032.2 steps/s (profiles/r03d).  Speed only: any
+// placement gives the same results.
 #ifndef SML_SPEC_STRIDE
-#define SML_SPEC_STRIDE 31
+#define SML_SPEC_STRIDE 32
 #endif
 constexpr int kSpecStride = SML_SPEC_STRIDE;
 static_assert(kSpecStride >= kMX, "k_st_spec grid stride");
