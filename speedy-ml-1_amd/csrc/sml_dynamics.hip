@@ -1411,6 +1411,10 @@ static_assert(kNInv <= 64 && kNInvP - kNInv <= 64 && kIX <= 128 && kNFwd <= kGsT
 // (t1 q1 phi1 ps1 at kPT1.., then ucos1 ..)
 __device__ inline int phys_slot_col(int s) { return s < 3 * kKX + 1 ? kPT1 + s : kNInv1P + 2 * kKX + 2 + (s - (3 * kKX + 1)); }
 
+// kWT (SML_DYN_WT): the write-through hand-off stores, a compile-time choice -- with
+// a run-time flag every store of specx's last pass carried both paths (specx 3.1 ->
+// 4.8 us in the default build, r03c)
+template <bool kWT>
 __global__ __launch_bounds__(kGsThreads) void k_st_gridspec(
     const double *__restrict__ varm, double *__restrict__ vfm, const double *__restrict__ wa,
     const double *__restrict__ cosgr, const DynTables *__restrict__ T, const double *__restrict__ bc,
@@ -1591,7 +1595,8 @@ __global__ __launch_bounds__(kGsThreads) void k_st_gridspec(
             fft::rfftf48_reg(x, was);
         }
         __syncthreads();  // A's P columns are read: A becomes the pairs' meeting place
-        row_specx_pair(x, A, act, vfm, was, f, j, h, wt != 0);
+        row_specx_pair(x, A, act, vfm, was, f, j, h, kWT);
+        (void)wt;
     }
     stamp(dbg, 0, 3);
 }
@@ -1612,6 +1617,7 @@ __global__ void k_pack_pfwd(const double *__restrict__ pfwd, double *__restrict_
 // one zonal wavenumber m: specy of the 73 forward transforms, combine and tail of
 // the m's 64 real coefficients x 8 levels (one thread each) on the m's state slice
 // in LDS; with next_j2 > 0 the new state feeds the next step's inverse transforms
+template <bool kWT>
 __global__ __launch_bounds__(kSpecBlk) void k_st_spec(
     const double *__restrict__ vfm, const double *__restrict__ pfl, const double *__restrict__ wt,
     const double *__restrict__ sm, double *__restrict__ sm_out, double *__restrict__ Td, double *__restrict__ phi_out,
@@ -1799,7 +1805,7 @@ __global__ __launch_bounds__(kSpecBlk) void k_st_spec(
         for (int q = 0; q < RS; ++q) v[q] = src[q * kSpecBlk];
 #pragma unroll
         for (int q = 0; q < RS; ++q)
-            store2(sm_out, (size_t)m * kSM + 2 * ((size_t)q * kSpecBlk + threadIdx.x), v[q].x, v[q].y, wthru != 0);
+            store2(sm_out, (size_t)m * kSM + 2 * ((size_t)q * kSpecBlk + threadIdx.x), v[q].x, v[q].y, kWT);
     }
     // d) the next step's inverse-transform inputs (k_dyn_prep) and gridy
     if (holds) inv_inputs(Sst, S, Fm, tb, m, next_j2, n1, nin);
@@ -1808,7 +1814,7 @@ __global__ __launch_bounds__(kSpecBlk) void k_st_spec(
     {
         const int nt = (nin + 7) / 8, per = (nt + kSpecSplit - 1) / kSpecSplit;
         gridy_m(S, gridy_operands_slice(V + kVPinv), varm_next, m, nin, half * per, min(nt, (half + 1) * per),
-                wthru != 0);
+                kWT);
     }
     if (dbg) {  // (diagnostics only: the kernel ends here)
         __syncthreads();
@@ -2315,7 +2321,7 @@ int launch_step_fused(sml_dynamics *d, int j1, int j2, double dt, double alph, d
             hipLaunchKernelGGL(k_st_specx, dim3(kIL), dim3(kSpecxThreads), 0, st, d->d_gfwd, d->d_phys, d->d_vfm,
                                sd.wa, sd.cosgr, d->d_dbg);
         } else {
-            hipLaunchKernelGGL(k_st_gridspec, dim3(kIL), dim3(kGsThreads), 0, st, d->d_varm, d->d_vfm, sd.wa, sd.cosgr,
+            hipLaunchKernelGGL(d->wt ? k_st_gridspec<true> : k_st_gridspec<false>, dim3(kIL), dim3(kGsThreads), 0, st, d->d_varm, d->d_vfm, sd.wa, sd.cosgr,
                                T, d->d_pbc, d->d_rad, d->d_ptab, lradsw ? 1 : 0, d->wt ? 1 : 0, d->d_dbg);
         }
         SML_HIP(hipGetLastError());
@@ -2327,7 +2333,7 @@ int launch_step_fused(sml_dynamics *d, int j1, int j2, double dt, double alph, d
     const int j4 = (alph == 0.0) ? j2 : 1;
     const int cur = d->sm_cur;
     if (next_j2 > 0) d->sm_cur = 1 - cur;  // the next step reads what this one writes
-    hipLaunchKernelGGL(k_st_spec, dim3(kSpecStride * kSpecSplit), dim3(kSpecBlk), 0, st, d->d_vfm, d->d_pfl, sd.wt,
+    hipLaunchKernelGGL(d->wt ? k_st_spec<true> : k_st_spec<false>, dim3(kSpecStride * kSpecSplit), dim3(kSpecBlk), 0, st, d->d_vfm, d->d_pfl, sd.wt,
                        sm_buf(d, cur), sm_buf(d, 1 - cur), d->d_tend,
                        d->d_phi, d->d_phis, d->d_tcorh, d->d_qcorh, T, j1, j4, dt, alph, rob, wil, sd.pinv, d->d_varm,
                        next_j2, n1, nin, d->d_tabm + (size_t)(d->d_tab - d->d_tabs) * kMX * kTabMDoubles, d->d_state,

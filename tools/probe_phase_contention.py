@@ -46,7 +46,13 @@ else:
 
     src = torch.as_tensor(_Buf(), device=dev)
 src.uniform_()
-print("partner buffer:", MEM)
+# PARTNER_KIND: sum (torch.sum, the default) | nt | plain (tools/libstream_partner.so)
+KIND = os.environ.get("PARTNER_KIND", "sum")
+if KIND != "sum":
+    SP = ctypes.CDLL(os.path.join(REPO, "tools", "libstream_partner.so"))
+    SP.sp_read.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+    sink = torch.zeros(8, dtype=torch.float64, device=dev)
+print("partner buffer:", MEM, "partner:", KIND)
 K = {0: ("grid", ["gridx", "physics+sums", "specx"]),
      1: ("spec", ["load", "specy", "combine", "tail", "inv_inputs", "gridy"]),
      3: ("spec_last", ["load", "specy", "combine", "tail"])}
@@ -59,8 +65,13 @@ def run(partner, reps=6):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         if partner:
             with torch.cuda.stream(main):
-                torch.sum(src)
-                torch.sum(src)
+                if KIND == "sum":
+                    torch.sum(src)
+                    torch.sum(src)
+                else:  # tools/libstream_partner.so: nt or plain 16-B loads, 8 blocks per partner CU
+                    for _ in range(2):
+                        assert SP.sp_read(ctypes.c_void_p(src.data_ptr()), ctypes.c_size_t(NB), ctypes.c_void_p(sink.data_ptr()),
+                                          1 if KIND == "nt" else 0, 192 * 8, s_main) == 0
         with torch.cuda.stream(side):
             e0.record()
             d.window(24, stream=side)
