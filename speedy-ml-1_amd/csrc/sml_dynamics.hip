@@ -1079,6 +1079,9 @@ constexpr int kSpecSplit = 2;             // k_st_spec blocks per m (the next st
 #ifndef SML_SPEC_STRIDE
 #define SML_SPEC_STRIDE 32
 #endif
+#ifndef SML_SPEC_VFM_FIRST
+#define SML_SPEC_VFM_FIRST 0
+#endif
 constexpr int kSpecStride = SML_SPEC_STRIDE;
 static_assert(kSpecStride >= kMX, "k_st_spec grid stride");
 
@@ -1641,6 +1644,32 @@ __global__ __launch_bounds__(kSpecBlk) void k_st_spec(
     const int wave = threadIdx.x >> 6, l = threadIdx.x & 63, r = l & 15, kk = l >> 4;
     const int sk = next_j2 > 0 ? 1 : 3;
     stamp(dbg, sk, 0);
+    // a) specy (k_specy's tiling: 8 fields x Re/Im per wave), the wave's A operands
+    // read from vfm [lat][f][p] (per instruction 4 latitudes x 128 contiguous bytes)
+    const double *vm = vfm + (size_t)m * kVFm;
+    // at most two tiles per wave (10 tiles, 8 waves): both tiles' loads are issued
+    // before the first MFMA, so the second tile costs no memory round trip of its own
+    constexpr int kTiles = (kNFwd + 7) / 8, kWaves = kSpecBlk / 64;
+    static_assert(kTiles <= 2 * kWaves, "specy: two tiles per wave at most");
+    auto tile_load = [&](int tile, double (&vn)[kIY / 4], double (&vs)[kIY / 4]) {
+        const int fa = tile * 8 + (r >> 1);
+        const double *vr = vm + (fa < kNFwd ? fa : 0) * 2 + (r & 1);
+#pragma unroll
+        for (int s = 0; s < kIY / 4; ++s) {
+            const int j = 4 * s + kk;
+            vn[s] = vr[(kIL - 1 - j) * kVLs];
+            vs[s] = vr[j * kVLs];
+        }
+    };
+    // SML_SPEC_VFM_FIRST: specy's Fourier operands -- the hand-off from the row kernel,
+    // the loads specy waits on -- issued before the state / table loads (needed only
+    // after specy), so their memory round trip starts first
+    double vn0[kIY / 4], vs0[kIY / 4], vn1[kIY / 4], vs1[kIY / 4];
+    const bool two = wave + kWaves < kTiles;  // wave-uniform
+#if SML_SPEC_VFM_FIRST
+    tile_load(wave, vn0, vs0);
+    if (two) tile_load(wave + kWaves, vn1, vs1);
+#endif
     constexpr int RT = (kTabMDoubles / 2 + kSpecBlk - 1) / kSpecBlk;
     // three named registers, not an array: held across specy, an array was kept in scratch
     static_assert((RT == 2 || RT == 3) && 2 * RT * kSpecBlk <= kVFm && 2 * RT * kSpecBlk - kTabMDoubles <= kTabMPad,
@@ -1695,23 +1724,6 @@ __global__ __launch_bounds__(kSpecBlk) void k_st_spec(
     }
     if (dbg) __syncthreads();
     stamp(dbg, sk, 1);
-    // a) specy (k_specy's tiling: 8 fields x Re/Im per wave), the wave's A operands
-    // read from vfm [lat][f][p] (per instruction 4 latitudes x 128 contiguous bytes)
-    const double *vm = vfm + (size_t)m * kVFm;
-    // at most two tiles per wave (10 tiles, 8 waves): both tiles' loads are issued
-    // before the first MFMA, so the second tile costs no memory round trip of its own
-    constexpr int kTiles = (kNFwd + 7) / 8, kWaves = kSpecBlk / 64;
-    static_assert(kTiles <= 2 * kWaves, "specy: two tiles per wave at most");
-    auto tile_load = [&](int tile, double (&vn)[kIY / 4], double (&vs)[kIY / 4]) {
-        const int fa = tile * 8 + (r >> 1);
-        const double *vr = vm + (fa < kNFwd ? fa : 0) * 2 + (r & 1);
-#pragma unroll
-        for (int s = 0; s < kIY / 4; ++s) {
-            const int j = 4 * s + kk;
-            vn[s] = vr[(kIL - 1 - j) * kVLs];
-            vs[s] = vr[j * kVLs];
-        }
-    };
     auto tile_mma = [&](int tile, const double (&vn)[kIY / 4], const double (&vs)[kIY / 4]) {
         const int f0 = tile * 8;
         const bool ok = f0 + (r >> 1) < kNFwd;
@@ -1736,10 +1748,10 @@ __global__ __launch_bounds__(kSpecBlk) void k_st_spec(
         }
     };
     {
-        double vn0[kIY / 4], vs0[kIY / 4], vn1[kIY / 4], vs1[kIY / 4];
-        const bool two = wave + kWaves < kTiles;  // wave-uniform
+#if !SML_SPEC_VFM_FIRST
         tile_load(wave, vn0, vs0);
         if (two) tile_load(wave + kWaves, vn1, vs1);
+#endif
         tile_mma(wave, vn0, vs0);
         if (two) tile_mma(wave + kWaves, vn1, vs1);
     }

@@ -183,6 +183,21 @@ module sml_hip
       integer(c_int) :: rc
     end function
 
+    ! sml_res_step_begin's form: 0 update + readout grids, 1 / 2 one fused launch (bitwise the same)
+    function sml_res_set_begin_mode(ctx, mode) bind(C, name='sml_res_set_begin_mode') result(rc)
+      import :: c_ptr, c_int
+      type(c_ptr), value :: ctx
+      integer(c_int), value :: mode
+      integer(c_int) :: rc
+    end function
+
+    function sml_res_begin_fused(ctx, fused) bind(C, name='sml_res_begin_fused') result(rc)
+      import :: c_ptr, c_int
+      type(c_ptr), value :: ctx
+      integer(c_int) :: fused
+      integer(c_int) :: rc
+    end function
+
     ! a stream on the logical CUs [first_cu, first_cu + num_cus) (hipExtStreamCreateWithCUMask)
     function sml_stream_create_cu_range(first_cu, num_cus, stream) bind(C, name='sml_stream_create_cu_range') result(rc)
       import :: c_ptr, c_int
