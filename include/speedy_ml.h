@@ -187,6 +187,13 @@ int sml_res_step_finish(sml_reservoirs *c, const double *d_local_model, double *
  * d_local_model (may be NULL) also receives the tiled vectors. */
 int sml_res_step_finish_grid(sml_reservoirs *c, const double *d_fc4d, const double *d_fc2d, double *d_local_model,
                              double *d_outvec, void *stream);
+/* sml_res_step_finish_grid + sml_exchange_assemble of the same outvecs in one launch
+ * (sendrecievegrid's assembly with the root's clips, src/mpires.f90:430-478): for a
+ * context that holds every region in global order (one rank), where the exchange is
+ * the identity.  d_outvec receives the outvecs as well; identical results. */
+int sml_res_step_finish_assemble(sml_reservoirs *c, const double *d_fc4d, const double *d_fc2d,
+                                 double *d_local_model, double *d_outvec, double *d_grid4d, double *d_grid2d,
+                                 double *d_precip, void *stream);
 /* cap on the waves of the v_ml readout issued by sml_res_step_begin (0 = one wave per
  * 8-row item, the default cap is 2048).  The cap leaves HBM headroom for SPEEDY when
  * both share CUs; on CUs of their own (sml_stream_create_cu_range) it is not needed.

@@ -76,6 +76,9 @@ struct sml_hybrid {
     double *d_send = nullptr, *d_recv = nullptr, *d_glob = nullptr;
     int32_t *d_perm = nullptr;
     bool started = false, predicted = false, advanced = false;
+    // sml_hybrid_step on one rank: the finish also assembled the grids (the exchange is
+    // the identity), so the advance that follows skips sml_exchange_assemble
+    bool assembled = false;
     // get_tisr_by_date (mpires.f90:1644-1676): a table of hourly global tisr fields
     // [nhours][48][96] on the device, the calendar's start year, the hours before the
     // first prediction step and the hours per step; t = steps advanced so far
@@ -856,18 +859,29 @@ extern "C" int sml_hybrid_slab_buffers(const sml_hybrid *h, const double **d_sst
 }
 
 // predict for every local region (parallelmain.f90:225-234): the local outvecs in
-// d_outvec on the main stream
-extern "C" int sml_hybrid_predict(sml_hybrid *h) {
+// d_outvec on the main stream; with `assemble` (sml_hybrid_step on one rank) the
+// finish also scatters them into the global grids
+namespace {
+int predict_impl(sml_hybrid *h, bool assemble) {
     SML_REQUIRE(h, "null context");
     if (!h->started) return fail(SML_ERR_STATE, "sml_hybrid_start first");
     if (h->predicted) return fail(SML_ERR_STATE, "sml_hybrid_predict twice without sml_hybrid_advance");
+    h->assembled = false;
     if (h->overlap) {
         if (int rc = sml_res_step_begin(h->res, h->fb, h->main)) return rc;
         if (int rc = slab_predict(h)) return rc;
         // SPEEDY's forecast of the previous window
         if (int rc = hop_wait(h, sml_hybrid::kHopLm, h->main)) return rc;
-        // the local-model tiling fused into the v_p finish: one launch fewer on the critical path
-        if (int rc = sml_res_step_finish_grid(h->res, h->f4, h->f2, h->lm, h->ov, h->main)) return rc;
+        // the local-model tiling fused into the v_p finish: one launch fewer on the
+        // critical path; on one rank the assembly too (one more)
+        if (assemble) {
+            if (int rc = sml_res_step_finish_assemble(h->res, h->f4, h->f2, h->lm, h->ov, h->g4, h->g2, h->pr,
+                                                      h->main))
+                return rc;
+            h->assembled = true;
+        } else if (int rc = sml_res_step_finish_grid(h->res, h->f4, h->f2, h->lm, h->ov, h->main)) {
+            return rc;
+        }
     } else {  // one pass over W_out: the same sums as begin + finish
         if (int rc = sml_res_step(h->res, h->fb, h->lm, h->ov, h->main)) return rc;
         if (int rc = slab_predict(h)) return rc;
@@ -875,6 +889,9 @@ extern "C" int sml_hybrid_predict(sml_hybrid *h) {
     h->predicted = true;
     return SML_OK;
 }
+}  // namespace
+
+extern "C" int sml_hybrid_predict(sml_hybrid *h) { return predict_impl(h, false); }
 
 // sendrecievegrid's assembly + run_model + re-tiling (mpires.f90:300-751) from the
 // outvecs of every region in global region order ([numregions][nout], device)
@@ -882,7 +899,11 @@ extern "C" int sml_hybrid_advance(sml_hybrid *h, const double *d_outvec_all) {
     SML_REQUIRE(h && d_outvec_all, "null argument");
     if (!h->predicted) return fail(SML_ERR_STATE, "sml_hybrid_advance without sml_hybrid_predict");
     hipStream_t m = h->main, s = h->side;
-    if (int rc = sml_exchange_assemble(h->res, d_outvec_all, h->g4, h->g2, h->pr, m)) return rc;
+    // (sml_hybrid_step on one rank: its predict assembled these very outvecs already)
+    const bool done = h->assembled && d_outvec_all == h->ov;
+    h->assembled = false;
+    if (!done)
+        if (int rc = sml_exchange_assemble(h->res, d_outvec_all, h->g4, h->g2, h->pr, m)) return rc;
     if (int rc = slab_sst(h, d_outvec_all)) return rc;
     if (h->overlap)
         if (int rc = hop_signal(h, sml_hybrid::kHopGrid, m)) return rc;
@@ -946,7 +967,11 @@ extern "C" int sml_hybrid_step(sml_hybrid *h) {
     if (world > 1 && !h->comm->comm)
         return fail(SML_ERR_STATE, "rank %d of %d has no transport: exchange through sml_hybrid_advance_slabs",
                     h->comm->rank, world);
-    if (int rc = sml_hybrid_predict(h)) return rc;
+    // one rank: the exchange is the identity, so the finish assembles the grids itself
+    // (SML_HYBRID_ASM=0: the separate assembly, for A/B)
+    const char *e = std::getenv("SML_HYBRID_ASM");
+    const bool fuse = world == 1 && h->overlap && sml::res_in_global_order(h->res) && !(e && *e == '0');
+    if (int rc = predict_impl(h, fuse)) return rc;
     if (world == 1) return sml_hybrid_advance(h, h->ov);
     // even shares (1152 / N for N = 1, 2, 4, 8): the outvecs go out of ov as they are;
     // uneven ones are padded to the largest share through d_send (one copy more on the

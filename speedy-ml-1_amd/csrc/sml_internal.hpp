@@ -13,6 +13,11 @@ namespace sml {
 
 int fail(int code, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
 void clear_error();
+}  // namespace sml
+struct sml_reservoirs;
+namespace sml {
+// the context holds every region, in global order (its local index is the region id)
+bool res_in_global_order(const sml_reservoirs *c);
 
 // --------------------------------------------------------------- geometry
 // Restatement of the res_domain.f90 decomposition used by every reservoir of the

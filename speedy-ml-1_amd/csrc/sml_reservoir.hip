@@ -532,12 +532,32 @@ __global__ __launch_bounds__(256) void k_res_finish(const RegionDev *__restrict_
 // thread finishes one output with vp_sum over the LDS copy: the same values, sums
 // and order as the two-launch form, one kernel boundary fewer on the hybrid step's
 // critical path
-template <typename WT>
+// kAsm (sml_res_step_finish_assemble, one rank holding every region in order): each
+// output is also scattered into the global grids with the root's clips, exactly as
+// k_assemble does from the outvec (every grid point has one writer), so the
+// assembly's own launch leaves the critical path
+__device__ inline void assemble_one(int d, double v, double *__restrict__ g4, double *__restrict__ g2,
+                                    double *__restrict__ pr) {
+    if (d < 0) return;
+    if (d < kGrid4d) {
+        if ((d & 3) == 3 && v < 0.000001) v = 0.000001;  // mpires.f90:448-450
+        g4[d] = v;
+    } else if (d < kGrid4d + kGrid2d) {
+        g2[d - kGrid4d] = v;
+    } else {
+        if (v < 0.00001) v = 0.0;  // mpires.f90:474-478
+        pr[d - kGrid4d - kGrid2d] = v;
+    }
+}
+
+template <typename WT, bool kAsm = false>
 __global__ __launch_bounds__(256) void k_res_finish_grid(
     const RegionDev *__restrict__ R, const WT *__restrict__ wlm, const int32_t *__restrict__ src,
     const uint8_t *__restrict__ lidx, const double *__restrict__ fc4, const double *__restrict__ fc2,
     double *__restrict__ lm_out, const double *__restrict__ meanstd, const int8_t *__restrict__ outl,
-    const double *__restrict__ part, double *__restrict__ outvec, int nout, int ov_ld, int nout_pad, int ncs) {
+    const double *__restrict__ part, double *__restrict__ outvec, int nout, int ov_ld, int nout_pad, int ncs,
+    const int32_t *__restrict__ asm_dst = nullptr, double *__restrict__ g4 = nullptr, double *__restrict__ g2 = nullptr,
+    double *__restrict__ pr = nullptr) {
     __shared__ double slm[kMaxNcs];
     const int r = blockIdx.x, t = threadIdx.x;
     const double *ms = meanstd + (size_t)r * 2 * kMeanStd;
@@ -554,7 +574,9 @@ __global__ __launch_bounds__(256) void k_res_finish_grid(
     __syncthreads();
     for (int o = t; o < nout; o += blockDim.x) {
         const double vp = vp_sum(wlm + R[r].wlm, nout_pad, slm, ncs, o);
-        outvec[(size_t)r * ov_ld + o] = unstd(vp + part[(size_t)r * nout_pad + o], ms, outl[o]);
+        const double v = unstd(vp + part[(size_t)r * nout_pad + o], ms, outl[o]);
+        outvec[(size_t)r * ov_ld + o] = v;
+        if constexpr (kAsm) assemble_one(asm_dst[(size_t)r * nout + o], v, g4, g2, pr);
     }
 }
 
@@ -565,16 +587,7 @@ __global__ void k_assemble(const int32_t *__restrict__ dst, const double *__rest
     if (e >= total) return;
     const int d = dst[e];
     if (d < 0) return;
-    double v = ov_ld == nout ? ov[e] : ov[(size_t)(e / nout) * ov_ld + e % nout];
-    if (d < kGrid4d) {
-        if ((d & 3) == 3 && v < 0.000001) v = 0.000001;  // mpires.f90:448-450
-        g4[d] = v;
-    } else if (d < kGrid4d + kGrid2d) {
-        g2[d - kGrid4d] = v;
-    } else {
-        if (v < 0.00001) v = 0.0;  // mpires.f90:474-478
-        pr[d - kGrid4d - kGrid2d] = v;
-    }
+    assemble_one(d, ov_ld == nout ? ov[e] : ov[(size_t)(e / nout) * ov_ld + e % nout], g4, g2, pr);
 }
 
 __device__ inline double grid_at(int src, const double *g4, const double *g2, const double *pr) {
@@ -1486,6 +1499,39 @@ extern "C" int sml_res_step_finish_grid(sml_reservoirs *c, const double *d_fc4d,
         hipLaunchKernelGGL(k_res_finish_grid<double>, dim3(c->nlocal), dim3(256), 0, st, c->d_rd,
                            (const double *)c->d_wlm, c->d_lm_src, c->d_lm_l, d_fc4d, d_fc2d, d_local_model,
                            c->d_meanstd, c->d_outl, c->d_part, d_outvec, c->nout, c->ov_ld, c->nout_pad, c->ncs);
+    SML_HIP(hipGetLastError());
+    c->begun = false;
+    return SML_OK;
+}
+
+bool sml::res_in_global_order(const sml_reservoirs *c) {
+    if (!c || c->generic || c->nlocal != c->numregions) return false;
+    for (int i = 0; i < c->nlocal; ++i)
+        if (c->region_ids[i] != i) return false;
+    return true;
+}
+
+extern "C" int sml_res_step_finish_assemble(sml_reservoirs *c, const double *d_fc4d, const double *d_fc2d,
+                                            double *d_local_model, double *d_outvec, double *d_grid4d,
+                                            double *d_grid2d, double *d_precip, void *stream) {
+    SML_REQUIRE(c, "null context");
+    SML_REQUIRE(sml::res_in_global_order(c), "the fused assembly needs every region on this rank, in global order");
+    if (c->nlocal == 0) return SML_OK;
+    SML_REQUIRE(d_outvec && d_grid4d && d_grid2d && d_precip && (c->ncs == 0 || (d_fc4d && d_fc2d)),
+                "null device buffer");
+    SML_REQUIRE(c->ncs <= kMaxNcs, "ncs %d exceeds %d", c->ncs, kMaxNcs);
+    if (!c->begun) return fail(SML_ERR_STATE, "sml_res_step_finish_assemble without sml_res_step_begin");
+    hipStream_t st = (hipStream_t)stream;
+    if (c->wdtype == SML_F32)
+        hipLaunchKernelGGL((k_res_finish_grid<float, true>), dim3(c->nlocal), dim3(256), 0, st, c->d_rd,
+                           (const float *)c->d_wlm, c->d_lm_src, c->d_lm_l, d_fc4d, d_fc2d, d_local_model,
+                           c->d_meanstd, c->d_outl, c->d_part, d_outvec, c->nout, c->ov_ld, c->nout_pad, c->ncs,
+                           c->d_asm_dst, d_grid4d, d_grid2d, d_precip);
+    else
+        hipLaunchKernelGGL((k_res_finish_grid<double, true>), dim3(c->nlocal), dim3(256), 0, st, c->d_rd,
+                           (const double *)c->d_wlm, c->d_lm_src, c->d_lm_l, d_fc4d, d_fc2d, d_local_model,
+                           c->d_meanstd, c->d_outl, c->d_part, d_outvec, c->nout, c->ov_ld, c->nout_pad, c->ncs,
+                           c->d_asm_dst, d_grid4d, d_grid2d, d_precip);
     SML_HIP(hipGetLastError());
     c->begun = false;
     return SML_OK;

@@ -28,7 +28,7 @@ EXPORTED = (
     "sml_grid_host", "sml_spec_host",
     "sml_res_create", "sml_res_destroy", "sml_res_ninp", "sml_res_feedback_offsets",
     "sml_res_load_region_f32", "sml_res_load_region_f64", "sml_res_set_state", "sml_res_get_state",
-    "sml_res_step", "sml_res_step_begin", "sml_res_step_finish", "sml_res_step_finish_grid", "sml_res_step_host", "sml_res_synchronize",
+    "sml_res_step", "sml_res_step_begin", "sml_res_step_finish", "sml_res_step_finish_grid", "sml_res_step_finish_assemble", "sml_res_step_host", "sml_res_synchronize",
     "sml_res_footprint", "sml_res_enable_timing", "sml_res_kernel_times", "sml_res_set_read_waves",
     "sml_res_set_begin_mode", "sml_res_begin_fused",
     "sml_exchange_assemble",
@@ -125,6 +125,7 @@ def _declare(L: ctypes.CDLL) -> None:
         "sml_res_step_begin": [vp, vp, vp],
         "sml_res_step_finish": [vp, vp, vp, vp],
         "sml_res_step_finish_grid": [vp, vp, vp, vp, vp, vp],
+        "sml_res_step_finish_assemble": [vp, vp, vp, vp, vp, vp, vp, vp, vp],
         "sml_res_step_host": [vp, vp, vp, vp],
         "sml_res_synchronize": [vp, vp, i, ctypes.c_int64, vp],
         "sml_res_footprint": [vp, i64p, i64p],

@@ -115,7 +115,10 @@ class HybridLoop:
         NativeComm (speedy_ml_amd.comm) the whole step is native, its all-gather on
         the main stream (sml_hybrid_step); else `exchange` runs between predict and
         advance."""
-        if self.comm is not None:  # a LocalRank at world > 1 is refused: no transport
+        # one rank whose exchange is the identity (OutvecExchange of world 1): the native
+        # step too, whose finish then assembles the grids in the same launch
+        identity = self.comm is None and getattr(self.exchange, "world", None) == 1
+        if self.comm is not None or identity:  # a LocalRank at world > 1 is refused: no transport
             check(lib().sml_hybrid_step(self._h))
             return
         check(lib().sml_hybrid_predict(self._h))

@@ -126,6 +126,12 @@ class Reservoirs:
         check(lib().sml_res_step_finish_grid(self._h, ptr(d_fc4d), ptr(d_fc2d), ptr(d_local_model), ptr(d_outvec),
                                              stream_ptr(stream)))
 
+    def predict_finish_assemble(self, d_fc4d, d_fc2d, d_local_model, d_outvec, g4, g2, pr, stream=None):
+        """predict_finish_grid + assemble(d_outvec, g4, g2, pr) in one launch (one rank
+        holding every region in order; same results)."""
+        check(lib().sml_res_step_finish_assemble(self._h, ptr(d_fc4d), ptr(d_fc2d), ptr(d_local_model),
+                                                 ptr(d_outvec), ptr(g4), ptr(g2), ptr(pr), stream_ptr(stream)))
+
     def set_read_waves(self, waves: int):
         """Cap on the v_ml readout's waves in predict_begin (0 = uncapped)."""
         check(lib().sml_res_set_read_waves(self._h, int(waves)))

@@ -449,3 +449,49 @@ def test_fused_begin_is_bitwise_the_two_launch_begin(cuda, weight_dtype, mode):
         np.testing.assert_array_equal(oa, ob)
         for a, b in zip(xa, xb):
             np.testing.assert_array_equal(a, b)
+
+
+def test_finish_assemble_is_bitwise_finish_then_assemble(cuda):
+    """sml_res_step_finish_assemble (one rank, every region in order: the finish also
+    scatters the outvecs into the global grids with the root's clips) vs
+    finish_grid -> assemble: outvecs, local models and all three grids bitwise; a
+    context that does not hold every region is refused."""
+    import torch
+
+    from speedy_ml_amd import SmlError
+    from speedy_ml_amd.reservoir import Reservoirs
+    from speedy_ml_amd.synthetic import synthetic_grids
+
+    mask = domain.load_sst_mask()
+    ws = [region_weights(r, bool(mask[r]), n_override=96, seed=3) for r in range(domain.NUM_REGIONS)]
+    g4h, g2h, prh = synthetic_grids(5)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(cuda)  # noqa: E731
+    outs = {}
+    for fused in (False, True):
+        res = Reservoirs([w.region for w in ws], [w.sst for w in ws], [w.n for w in ws], [w.k for w in ws])
+        for i, w in enumerate(ws):
+            res.load_region_weights(i, w)
+            res.set_state(i, initial_state(w.region, w.n))
+        fb = t(np.concatenate([feedback_vector(w.region, w.ninp) for w in ws]))
+        lm = torch.zeros((len(ws), 132), dtype=torch.float64, device=cuda)
+        ov = torch.zeros((len(ws), 136), dtype=torch.float64, device=cuda)
+        g4 = torch.full((4 * 96 * 48 * 8,), -1.0, dtype=torch.float64, device=cuda)
+        g2 = torch.full((96 * 48,), -1.0, dtype=torch.float64, device=cuda)
+        pr = torch.full((96 * 48,), -1.0, dtype=torch.float64, device=cuda)
+        res.predict_begin(fb)
+        if fused:
+            res.predict_finish_assemble(t(g4h), t(g2h), lm, ov, g4, g2, pr)
+        else:
+            res.predict_finish_grid(t(g4h), t(g2h), lm, ov)
+            res.assemble(ov, g4, g2, pr)
+        torch.cuda.synchronize()
+        outs[fused] = [a.cpu().numpy() for a in (ov, lm, g4, g2, pr)]
+        res.close()
+    for name, a, b in zip(("ov", "lm", "g4", "g2", "pr"), outs[False], outs[True]):
+        np.testing.assert_array_equal(a, b, err_msg=name)
+    assert (outs[True][2] != -1.0).all() and (outs[True][4] >= 0).all()  # every grid point assembled
+    part = Reservoirs([w.region for w in ws[:4]], [w.sst for w in ws[:4]], [w.n for w in ws[:4]],
+                      [w.k for w in ws[:4]])
+    with pytest.raises(SmlError, match="every region"):
+        part.predict_finish_assemble(None, None, None, None, None, None, None)
+    part.close()
