@@ -1526,30 +1526,31 @@ __global__ __launch_bounds__(kGsThreads) void k_st_gridspec(
         }
         const double ps1 = Ai[kPPs1];
         double psg, qc[kKX];
+        RadCol rc;     // the column's radiation state: from phys_sw on a shortwave step, else from rad
         if (lradsw) {  // the shortwave first: its inputs are the moist part's (phys_column's order)
             PhysThermo h;
             phys_thermo(ta, qa, ph, ps1, PTl, h);
             double tt[kKX], qt[kKX], precnv, precls;
             int itop, icnv;
             phys_moist(h, PTl, tt, qt, precnv, precls, itop, icnv);
-            phys_sw(pt, h, ph, precnv, precls, itop, bc, rad, PTl);
+            phys_sw(pt, h, ph, precnv, precls, itop, bc, rad, PTl, rc);
             psg = h.psg;
             rl_rps = h.rps;
 #pragma unroll
             for (int k = 0; k < kKX; ++k) qc[k] = h.qa[k];
         } else {  // phys_thermo's psg, rps and clipped q
+            rad_load(pt, rad, rc);  // (the loads issued together, ahead of the chain that uses them)
             psg = exp(ps1);
             rl_rps = 1. / psg;
 #pragma unroll
             for (int k = 0; k < kKX; ++k) qc[k] = fmax(qa[k], 0.);
         }
-        phys_lw_sfc(pt, ua, va, ta, qc, ph, psg, rl_rps, bc, rad, PTl, &PT->fband[0][0], rl_tt, rl_us, rl_vs, rl_sh,
+        phys_lw_sfc(pt, ua, va, ta, qc, ph, psg, rl_rps, bc, rc, PTl, &PT->fband[0][0], rl_tt, rl_us, rl_vs, rl_sh,
                     rl_ev);
-        // the shortwave heating of the column (rad; written by phys_sw on a shortwave
-        // step, by this lane) for the sums after the barrier: loaded here, its memory
-        // round trip hides in this side's slack instead of following the barrier
+        // the shortwave heating of the column for the sums after the barrier (from rc:
+        // phys_sw's on a shortwave step, rad's otherwise)
 #pragma unroll
-        for (int k = 0; k < kKX; ++k) rl_rsw[k] = rad[kRadTtRsw + (size_t)k * kNGP + pt];
+        for (int k = 0; k < kKX; ++k) rl_rsw[k] = rc.ttrsw[k];
         // the grid-point dynamics' products (this side has the slack)
         // (the products below kNFwdScaled are vdspec inputs: x cosgr(j) here, not in specx)
         gridpoint_products(n1, [&](int f) { return f >= n1 ? A[i * kRowLd + f] * cj : A[i * kRowLd + f]; },

@@ -292,17 +292,37 @@ __device__ inline void phys_moist(const PhysThermo &h, const PhysTables *P, doub
     icnv_o = icnv;
 }
 
+// column j's radiation state -- rad's tau2 (4 bands x kx), stratc (2), ssrd, tt_rsw
+// (kx) -- in registers: on a shortwave step the longwave / surface chain takes what
+// phys_sw computed straight from it instead of re-reading rad (a dependent memory
+// round trip per field on the column's chain); otherwise rad_load reads it at once
+struct RadCol {
+    double tau[4][kKX];
+    double strat[2], ssrd, ttrsw[kKX];
+};
+
+__device__ inline void rad_load(int j, const double *__restrict__ rad, RadCol &rc) {
+#pragma unroll
+    for (int jb = 0; jb < 4; ++jb)
+#pragma unroll
+        for (int k = 0; k < kKX; ++k) rc.tau[jb][k] = rad[kRadTau2 + ((size_t)jb * kKX + k) * kNGP + j];
+    rc.strat[0] = rad[kRadStratc + j];
+    rc.strat[1] = rad[kRadStratc + kNGP + j];
+    rc.ssrd = rad[kRadSsrd + j];
+#pragma unroll
+    for (int k = 0; k < kKX; ++k) rc.ttrsw[k] = rad[kRadTtRsw + (size_t)k * kNGP + j];
+}
+
 // 3.1 shortwave radiation and longwave transmissivities (phy_phypar.f90:126-145),
-// the lradsw steps only: the radiation state of column j in rad
+// the lradsw steps only: the radiation state of column j into rc and rad
 __device__ inline void phys_sw(int j, const PhysThermo &h, const double *phi, double precnv, double precls, int itop,
-                               const double *__restrict__ bc, double *__restrict__ rad, const PhysTables *P) {
+                               const double *__restrict__ bc, double *__restrict__ rad, const PhysTables *P,
+                               RadCol &rc) {
     using namespace phys;
     constexpr int NL = kKX, nl1 = kKX - 1;  // nl1: 1-based index of the level above the bottom
     (void)nl1;
     auto BC = [&](int f) { return bc[(size_t)f * kNGP + j]; };
-    double *tau2 = rad + kRadTau2, *stratc = rad + kRadStratc, *tt_rsw = rad + kRadTtRsw, *ssrd = rad + kRadSsrd;
-    auto TAU = [&](int jb, int k) -> double & { return tau2[((size_t)jb * NL + k) * kNGP + j]; };
-    (void)tau2; (void)stratc; (void)tt_rsw; (void)ssrd;
+    auto TAU = [&](int jb, int k) -> double & { return rc.tau[jb][k]; };
     const double psg = h.psg, rps = h.rps;
     const double *qa = h.qa, *se = h.se, *rh = h.rh, *qsat = h.qsat;
     (void)psg; (void)rps; (void)qa; (void)se; (void)rh; (void)qsat;
@@ -398,7 +418,7 @@ __device__ inline void phys_sw(int j, const PhysThermo &h, const double *phi, do
             dfabs[k - 1] = dfabs[k - 1] - f1;
             f1 = f1 + t3[k - 1];
         }
-        ssrd[j] = fsfcd;
+        rc.ssrd = fsfcd;
         // longwave transmissivities (phy_radiat.f90:262-300)
         double deltap = psg * P->dsig[0];
         TAU(0, 0) = exp(-deltap * ablwin);
@@ -424,26 +444,33 @@ __device__ inline void phys_sw(int j, const PhysThermo &h, const double *phi, do
             TAU(3, k - 1) = exp(-deltap * fmax(ablwv2 * qa[k - 1], acl));
         }
         const double eps1 = epslw / (P->dsig[0] + P->dsig[1]);
-        stratc[j] = BC(kBcStratz) * psg;
-        stratc[kNGP + j] = eps1 * psg;
+        rc.strat[0] = BC(kBcStratz) * psg;
+        rc.strat[1] = eps1 * psg;
 #pragma unroll
-        for (int k = 0; k < NL; ++k) tt_rsw[(size_t)k * kNGP + j] = dfabs[k] * rps * P->grdscp[k];
+        for (int k = 0; k < NL; ++k) rc.ttrsw[k] = dfabs[k] * rps * P->grdscp[k];
+        // the column's state for the steps until the next shortwave step
+#pragma unroll
+        for (int jb = 0; jb < 4; ++jb)
+#pragma unroll
+            for (int k = 0; k < NL; ++k) rad[kRadTau2 + ((size_t)jb * NL + k) * kNGP + j] = rc.tau[jb][k];
+        rad[kRadStratc + j] = rc.strat[0];
+        rad[kRadStratc + kNGP + j] = rc.strat[1];
+        rad[kRadSsrd + j] = rc.ssrd;
+#pragma unroll
+        for (int k = 0; k < NL; ++k) rad[kRadTtRsw + (size_t)k * kNGP + j] = rc.ttrsw[k];
     }
 
 // 3.2 radlw(-1), 3.3 suflux, 3.4 radlw(1) (phy_phypar.f90:147-179): the longwave
 // temperature tendency tt_rlw and the surface fluxes of column j
 __device__ inline void phys_lw_sfc(int j, const double *ua, const double *va, const double *ta, const double *qa,
                                    const double *phi, double psg, double rps, const double *__restrict__ bc,
-                                   const double *__restrict__ rad_in, const PhysTables *P, const double *fbt,
+                                   const RadCol &rc, const PhysTables *P, const double *fbt,
                                    double *tt_rlw, double &ustr3_o, double &vstr3_o, double &shf3_o, double &evap3_o) {
     using namespace phys;
     constexpr int NL = kKX, nl1 = kKX - 1;  // nl1: 1-based index of the level above the bottom
     (void)nl1;
-    double *rad = const_cast<double *>(rad_in);
     auto BC = [&](int f) { return bc[(size_t)f * kNGP + j]; };
-    double *tau2 = rad + kRadTau2, *stratc = rad + kRadStratc, *tt_rsw = rad + kRadTtRsw, *ssrd = rad + kRadSsrd;
-    auto TAU = [&](int jb, int k) -> double & { return tau2[((size_t)jb * NL + k) * kNGP + j]; };
-    (void)tau2; (void)stratc; (void)tt_rsw; (void)ssrd;
+    auto TAU = [&](int jb, int k) { return rc.tau[jb][k]; };
     const int jlat = j / kIX;
     // 3.2 radlw(-1): downward longwave (phy_radiat.f90:330-413)
     double st4a1[NL], st4a2[NL], flux[4], dfabs[NL], fsfcd;
@@ -513,7 +540,7 @@ __device__ inline void phys_lw_sfc(int j, const double *ua, const double *va, co
         const double esbc = emisfc * sbc, esbc4 = 4. * esbc, dlambda = clambsn - clambda;
         const double u0 = fwind0 * ua[nlev - 1], v0 = fwind0 * va[nlev - 1];
         const double gtemp0 = 1. - ftemp0, rcp = 1. / cp, rdphi0 = -1. / (rd * 288. * P->sigl[nlev - 1]);
-        const double phi0 = BC(kBcPhis0), fmask = BC(kBcFmask1), ssrdj = ssrd[j];
+        const double phi0 = BC(kBcPhis0), fmask = BC(kBcFmask1), ssrdj = rc.ssrd;
         double t1[2], t2[2], denvvs[3], qsat0[2];
         const double dt1 = P->wvi[nlev - 1][1] * (ta[nlev - 1] - ta[nl1 - 1]);
         t1[0] = ta[nlev - 1] + dt1;
@@ -610,8 +637,8 @@ __device__ inline void phys_lw_sfc(int j, const double *ua, const double *va, co
             flux[jb] = tau * flux[jb] + emis * brad;
             dfabs[0] = dfabs[0] - flux[jb];
         }
-        const double corlw1 = P->dsig[0] * stratc[kNGP + j] * st4a1[0] + stratc[j];
-        const double corlw2 = P->dsig[1] * stratc[kNGP + j] * st4a1[1];
+        const double corlw1 = P->dsig[0] * rc.strat[1] * st4a1[0] + rc.strat[0];
+        const double corlw2 = P->dsig[1] * rc.strat[1] * st4a1[1];
         dfabs[0] = dfabs[0] - corlw1;
         dfabs[1] = dfabs[1] - corlw2;
     }
@@ -711,13 +738,16 @@ __device__ inline void phys_column(int j, const double *ua, const double *va, co
     double tt[NL], qt[NL], precnv, precls;
     int itop, icnv;
     phys_moist(h, P, tt, qt, precnv, precls, itop, icnv);
-    if (lradsw) phys_sw(j, h, phi, precnv, precls, itop, bc, rad, P);
+    RadCol rc;
+    if (lradsw)
+        phys_sw(j, h, phi, precnv, precls, itop, bc, rad, P, rc);
+    else
+        rad_load(j, rad, rc);
     double tt_rlw[NL], ustr3, vstr3, shf3, evap3;
-    phys_lw_sfc(j, ua, va, ta, h.qa, phi, h.psg, h.rps, bc, rad, P, fbt, tt_rlw, ustr3, vstr3, shf3, evap3);
+    phys_lw_sfc(j, ua, va, ta, h.qa, phi, h.psg, h.rps, bc, rc, P, fbt, tt_rlw, ustr3, vstr3, shf3, evap3);
     const double rps = h.rps;
-    const double *tt_rsw = rad + kRadTtRsw;
 #pragma unroll
-    for (int k = 0; k < NL; ++k) tt[k] = tt[k] + tt_rsw[(size_t)k * kNGP + j] + tt_rlw[k];  // :174-179
+    for (int k = 0; k < NL; ++k) tt[k] = tt[k] + rc.ttrsw[k] + tt_rlw[k];  // :174-179
     double utv[NL], vtv[NL], ttv[NL], qtv[NL];
 #pragma unroll
     for (int k = 0; k < NL; ++k) utv[k] = vtv[k] = 0.;
