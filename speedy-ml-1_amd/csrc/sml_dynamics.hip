@@ -1525,6 +1525,10 @@ __global__ __launch_bounds__(kGsThreads) void k_st_gridspec(
             ph[k] = Ai[kPPhi1 + k];
         }
         const double ps1 = Ai[kPPs1];
+        // the column's boundary fields and fband rows, loaded before the chain that uses them
+        double bcv[kNBc], fbk[kKX][4];
+        bc_load(pt, bc, bcv);
+        fband_rows(&PT->fband[0][0], ta, fbk);
         double psg, qc[kKX];
         RadCol rc;     // the column's radiation state: from phys_sw on a shortwave step, else from rad
         if (lradsw) {  // the shortwave first: its inputs are the moist part's (phys_column's order)
@@ -1533,7 +1537,7 @@ __global__ __launch_bounds__(kGsThreads) void k_st_gridspec(
             double tt[kKX], qt[kKX], precnv, precls;
             int itop, icnv;
             phys_moist(h, PTl, tt, qt, precnv, precls, itop, icnv);
-            phys_sw(pt, h, ph, precnv, precls, itop, bc, rad, PTl, rc);
+            phys_sw(pt, h, ph, precnv, precls, itop, bcv, rad, PTl, rc);
             psg = h.psg;
             rl_rps = h.rps;
 #pragma unroll
@@ -1545,8 +1549,8 @@ __global__ __launch_bounds__(kGsThreads) void k_st_gridspec(
 #pragma unroll
             for (int k = 0; k < kKX; ++k) qc[k] = fmax(qa[k], 0.);
         }
-        phys_lw_sfc(pt, ua, va, ta, qc, ph, psg, rl_rps, bc, rc, PTl, &PT->fband[0][0], rl_tt, rl_us, rl_vs, rl_sh,
-                    rl_ev);
+        phys_lw_sfc(pt, ua, va, ta, qc, ph, psg, rl_rps, bcv, rc, PTl, &PT->fband[0][0], fbk, rl_tt, rl_us, rl_vs,
+                    rl_sh, rl_ev);
         // the shortwave heating of the column for the sums after the barrier (from rc:
         // phys_sw's on a shortwave step, rad's otherwise)
 #pragma unroll

@@ -313,15 +313,34 @@ __device__ inline void rad_load(int j, const double *__restrict__ rad, RadCol &r
     for (int k = 0; k < kKX; ++k) rc.ttrsw[k] = rad[kRadTtRsw + (size_t)k * kNGP + j];
 }
 
+// column j's boundary fields (bc[f][ngp], f < kNBc) in registers, loaded at once at
+// the start of the column's chain: phys_sw and phys_lw_sfc read them in the middle of
+// theirs, a dependent memory round trip each where the compiler left the load
+__device__ inline void bc_load(int j, const double *__restrict__ bc, double (&bcv)[kNBc]) {
+#pragma unroll
+    for (int f = 0; f < kNBc; ++f) bcv[f] = bc[(size_t)f * kNGP + j];
+}
+
+// the fband rows of the column's levels (radlw's fband(nint(ta(k)), 1:4)), read once
+// for both radlw passes as soon as ta is known
+__device__ inline void fband_rows(const double *fbt, const double *ta, double (&fbk)[kKX][4]) {
+#pragma unroll
+    for (int k = 0; k < kKX; ++k) {
+        const double *row = phys::fband_row(fbt, ta[k]);
+#pragma unroll
+        for (int jb = 0; jb < 4; ++jb) fbk[k][jb] = row[jb];
+    }
+}
+
 // 3.1 shortwave radiation and longwave transmissivities (phy_phypar.f90:126-145),
 // the lradsw steps only: the radiation state of column j into rc and rad
 __device__ inline void phys_sw(int j, const PhysThermo &h, const double *phi, double precnv, double precls, int itop,
-                               const double *__restrict__ bc, double *__restrict__ rad, const PhysTables *P,
+                               const double (&bcv)[kNBc], double *__restrict__ rad, const PhysTables *P,
                                RadCol &rc) {
     using namespace phys;
     constexpr int NL = kKX, nl1 = kKX - 1;  // nl1: 1-based index of the level above the bottom
     (void)nl1;
-    auto BC = [&](int f) { return bc[(size_t)f * kNGP + j]; };
+    auto BC = [&](int f) { return bcv[f]; };
     auto TAU = [&](int jb, int k) -> double & { return rc.tau[jb][k]; };
     const double psg = h.psg, rps = h.rps;
     const double *qa = h.qa, *se = h.se, *rh = h.rh, *qsat = h.qsat;
@@ -463,24 +482,19 @@ __device__ inline void phys_sw(int j, const PhysThermo &h, const double *phi, do
 // 3.2 radlw(-1), 3.3 suflux, 3.4 radlw(1) (phy_phypar.f90:147-179): the longwave
 // temperature tendency tt_rlw and the surface fluxes of column j
 __device__ inline void phys_lw_sfc(int j, const double *ua, const double *va, const double *ta, const double *qa,
-                                   const double *phi, double psg, double rps, const double *__restrict__ bc,
+                                   const double *phi, double psg, double rps, const double (&bcv)[kNBc],
                                    const RadCol &rc, const PhysTables *P, const double *fbt,
-                                   double *tt_rlw, double &ustr3_o, double &vstr3_o, double &shf3_o, double &evap3_o) {
+                                   const double (&fbk)[kKX][4], double *tt_rlw, double &ustr3_o, double &vstr3_o,
+                                   double &shf3_o, double &evap3_o) {
     using namespace phys;
     constexpr int NL = kKX, nl1 = kKX - 1;  // nl1: 1-based index of the level above the bottom
     (void)nl1;
-    auto BC = [&](int f) { return bc[(size_t)f * kNGP + j]; };
+    auto BC = [&](int f) { return bcv[f]; };
     auto TAU = [&](int jb, int k) { return rc.tau[jb][k]; };
     const int jlat = j / kIX;
     // 3.2 radlw(-1): downward longwave (phy_radiat.f90:330-413)
     double st4a1[NL], st4a2[NL], flux[4], dfabs[NL], fsfcd;
-    double fbk[NL][4];  // fband(nint(ta(k)), 1:4): one table row per level, for both radlw passes
-#pragma unroll
-    for (int k = 0; k < NL; ++k) {
-        const double *row = fband_row(fbt, ta[k]);
-#pragma unroll
-        for (int jb = 0; jb < 4; ++jb) fbk[k][jb] = row[jb];
-    }
+    // (fbk: fband(nint(ta(k)), 1:4), one table row per level for both radlw passes, fband_rows)
     {
 #pragma unroll
         for (int k = 1; k <= nl1; ++k) st4a1[k - 1] = ta[k - 1] + P->wvi[k - 1][1] * (ta[k] - ta[k - 1]);
@@ -738,13 +752,16 @@ __device__ inline void phys_column(int j, const double *ua, const double *va, co
     double tt[NL], qt[NL], precnv, precls;
     int itop, icnv;
     phys_moist(h, P, tt, qt, precnv, precls, itop, icnv);
+    double bcv[kNBc], fbk[NL][4];
+    bc_load(j, bc, bcv);
+    fband_rows(fbt, ta, fbk);
     RadCol rc;
     if (lradsw)
-        phys_sw(j, h, phi, precnv, precls, itop, bc, rad, P, rc);
+        phys_sw(j, h, phi, precnv, precls, itop, bcv, rad, P, rc);
     else
         rad_load(j, rad, rc);
     double tt_rlw[NL], ustr3, vstr3, shf3, evap3;
-    phys_lw_sfc(j, ua, va, ta, h.qa, phi, h.psg, h.rps, bc, rc, P, fbt, tt_rlw, ustr3, vstr3, shf3, evap3);
+    phys_lw_sfc(j, ua, va, ta, h.qa, phi, h.psg, h.rps, bcv, rc, P, fbt, fbk, tt_rlw, ustr3, vstr3, shf3, evap3);
     const double rps = h.rps;
 #pragma unroll
     for (int k = 0; k < NL; ++k) tt[k] = tt[k] + rc.ttrsw[k] + tt_rlw[k];  // :174-179
