@@ -48,6 +48,8 @@ else:
 src.uniform_()
 # PARTNER_KIND: sum (torch.sum, the default) | nt | plain (tools/libstream_partner.so)
 KIND = os.environ.get("PARTNER_KIND", "sum")
+# NLEAP: leapfrog steps of the window (24, the hybrid's; 22 ends on a shortwave step)
+NLEAP = int(os.environ.get("NLEAP", "24"))
 if KIND != "sum":
     SP = ctypes.CDLL(os.path.join(REPO, "tools", "libstream_partner.so"))
     SP.sp_read.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
@@ -74,7 +76,7 @@ def run(partner, reps=6):
                                           1 if KIND == "nt" else 0, 192 * 8, s_main) == 0
         with torch.cuda.stream(side):
             e0.record()
-            d.window(24, stream=side)
+            d.window(NLEAP, stream=side)
             e1.record()
         torch.cuda.synchronize()
         wins.append(e0.elapsed_time(e1))
