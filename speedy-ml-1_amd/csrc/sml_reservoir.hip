@@ -288,8 +288,10 @@ __device__ __attribute__((always_inline)) inline void update_block(
 
 // logical blocks (region, part) = nlog; with a grid smaller than nlog (the paced
 // update that runs beside SPEEDY's window) each block takes logical blocks in rounds
-template <typename WT, bool kLds>
-__global__ __launch_bounds__(kUpdThreads) void k_res_update(
+// kMinW: waves per SIMD the registers must allow (4: one 1024-thread block per CU; 8:
+// two, so one block's x staging and SpMV overlap the other's -- 64 VGPRs)
+template <typename WT, bool kLds, int kMinW = 4>
+__global__ __launch_bounds__(kUpdThreads, kMinW) void k_res_update(
     const RegionDev *__restrict__ R, const int32_t *__restrict__ a_rp, const uint16_t *__restrict__ a_col,
     const WT *__restrict__ a_val, const int32_t *__restrict__ w_rp, const uint16_t *__restrict__ w_col,
     const WT *__restrict__ w_val, Ell ell, const double *__restrict__ x_old, double *__restrict__ x_new,
@@ -1309,10 +1311,13 @@ int launch_update(sml_reservoirs *c, const double *xo, double *xn, const double 
     // beside SPEEDY's window (sml_res_step_begin) the grid may be capped (upd_blocks):
     // fewer blocks in flight, each taking logical blocks in rounds
     dim3 ug(paced && c->upd_blocks > 0 ? std::min(nlog, c->upd_blocks) : nlog);
+    const char *eo = std::getenv("SML_UPD_OCC");
+    const bool occ2 = eo && *eo == '2';
 #define SML_UPD(WT, L)                                                                                            \
-    hipLaunchKernelGGL((k_res_update<WT, L>), ug, dim3(kUpdThreads), L ? lds : 0, st, c->d_rd, c->d_a_rp,          \
-                       c->d_a_col, (const WT *)c->d_a_val, c->d_w_rp, c->d_w_col, (const WT *)c->d_w_val, ell,    \
-                       xo, xn, c->d_xaug, d_feedback, c->ncs, c->leakage, bpr, lds_x, nlog)
+    hipLaunchKernelGGL(occ2 ? (k_res_update<WT, L, 8>) : (k_res_update<WT, L, 4>), ug, dim3(kUpdThreads),        \
+                       L ? lds : 0, st, c->d_rd, c->d_a_rp, c->d_a_col, (const WT *)c->d_a_val, c->d_w_rp,        \
+                       c->d_w_col, (const WT *)c->d_w_val, ell, xo, xn, c->d_xaug, d_feedback, c->ncs, c->leakage, \
+                       bpr, lds_x, nlog)
     Ell ell{c->d_a_ell_col, c->d_a_ell_val, c->d_w_ell_col, c->d_w_ell_val};
     if (c->wdtype == SML_F32) {
         if (use_lds)
