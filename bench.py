@@ -78,6 +78,9 @@ def parse():
     p.add_argument("--sim-ranks", type=int, default=1,
                    help="diagnostic: run rank 0's share of an N-rank decomposition on this one GPU, the "
                         "all-gather replaced by a local copy (other ranks' outvecs stale); never the headline")
+    p.add_argument("--pipelined", action=argparse.BooleanOptionalAction, default=True,
+                   help="each step also issues the next step's reservoir begin (sml_hybrid_set_pipelined): "
+                        "the loop a long run is in, also for the first timed step after the warmup's sync")
     p.add_argument("--slab", action=argparse.BooleanOptionalAction, default=True,
                    help="the slab ocean in the loop, as the reference runs by default (mod_reservoir.f90:41): a "
                         "slab reservoir per sst region, predict_slab_ml every 168 h (28 steps), its sst in the "
@@ -180,6 +183,8 @@ def main():
         comm = NativeComm(world, rank)
     loop = HybridLoop(res, dyn, exchange, dev, tisr=tisr, overlap=args.overlap, speedy_cus=args.speedy_cus,
                       comm=comm, slab=slab_ocean)
+    if args.pipelined:
+        loop.set_pipelined(True)
     # initial inputs from the synthetic analysis state (start_prediction analogue)
     loop.start(t(g4h), t(g2h), t(prh), t(f4h), t(f2h))
     if slab_ocean is not None:
@@ -223,6 +228,9 @@ def main():
     loop.sync()
     dt = timed(step, args.steps, timing=True)
     upd_ms, rd_ms = res.kernel_times()
+    if args.pipelined and args.overlap:  # the next step's begin is in flight: close it (untimed)
+        res.predict_finish(lm, ov, stream=loop.main)
+        torch.cuda.synchronize()
     _, safe = dyn.from_grid(g4.cpu().numpy(), g2.cpu().numpy())
     finite = bool(torch.isfinite(f4).all().item()) and bool(torch.isfinite(ov).all().item())
 
@@ -323,6 +331,9 @@ def main():
                                + (f" [DIAGNOSTIC: rank 0 of {sim} simulated ranks, exchange local]" if sim > 1 else ""),
                 "speedy": "T30L8, 26 dyn_steps per window (nsteps 96/day, delt 900 s), physics on, "
                           "shortwave every 3rd step",
+                "loop": ("pipelined: each step issues the next step's reservoir begin beside its window, so the "
+                         "timed steps run begins 2..K+1 and windows 1..K -- K of each, none skipped"
+                         if args.pipelined and args.overlap else "each step issues its own begin"),
                 "streams": (f"overlapped: SPEEDY on CUs [0, {args.speedy_cus}), reservoir on CUs [{args.speedy_cus}, "
                             f"{args.speedy_cus + (ncu - args.speedy_cus)})"
                             if args.overlap and args.speedy_cus > 0 else

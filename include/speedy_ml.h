@@ -576,6 +576,13 @@ int sml_hybrid_slab_buffers(const sml_hybrid *h, const double **d_sst_grid, cons
 #define SML_HOP_EVENTS 2
 int sml_hybrid_set_hop_mode(sml_hybrid *h, int mode);
 int sml_hybrid_hop_mode(const sml_hybrid *h, int *requested, int *effective);
+/* pipelined loop (default off): each advance also issues the NEXT step's reservoir
+ * begin (update + v_ml readout of the feedback it has just tiled) on the main stream,
+ * so a loop restarted after a sync does not pay one begin outside the overlap; every
+ * step's outvecs, grids and forecast are bitwise those of the default loop, but after
+ * a step (and a sync) the reservoir states are one update ahead (the next step's).
+ * The next predict only finishes that begin. */
+int sml_hybrid_set_pipelined(sml_hybrid *h, int on);
 /* run_speedy of the last step (0: the reference ends the prediction,
  * parallelmain.f90:268-270); waits only for that step's safety check */
 int sml_hybrid_run_speedy(sml_hybrid *h, int *run);

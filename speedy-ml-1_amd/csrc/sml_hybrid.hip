@@ -79,6 +79,10 @@ struct sml_hybrid {
     // sml_hybrid_step on one rank: the finish also assembled the grids (the exchange is
     // the identity), so the advance that follows skips sml_exchange_assemble
     bool assembled = false;
+    // pipelined (sml_hybrid_set_pipelined): each advance issues the next step's begin
+    // (update + v_ml readout) on the main stream as soon as its feedback is tiled;
+    // begun_next: that begin is in flight, so the next predict only finishes
+    bool pipelined = false, begun_next = false;
     // get_tisr_by_date (mpires.f90:1644-1676): a table of hourly global tisr fields
     // [nhours][48][96] on the device, the calendar's start year, the hours before the
     // first prediction step and the hours per step; t = steps advanced so far
@@ -437,6 +441,14 @@ extern "C" int sml_hybrid_set_hop_mode(sml_hybrid *h, int mode) {
         h->use_events = env_on("SML_HYBRID_EVENTS") || dispatch_serialised();
     else
         h->use_events = mode == SML_HOP_EVENTS;
+    return SML_OK;
+}
+
+// pipelined loop (see sml_hybrid::pipelined); switching it off keeps a begin already
+// in flight for the next predict
+extern "C" int sml_hybrid_set_pipelined(sml_hybrid *h, int on) {
+    SML_REQUIRE(h, "null context");
+    h->pipelined = on != 0;
     return SML_OK;
 }
 
@@ -868,7 +880,9 @@ int predict_impl(sml_hybrid *h, bool assemble) {
     if (h->predicted) return fail(SML_ERR_STATE, "sml_hybrid_predict twice without sml_hybrid_advance");
     h->assembled = false;
     if (h->overlap) {
-        if (int rc = sml_res_step_begin(h->res, h->fb, h->main)) return rc;
+        if (!h->begun_next)  // (pipelined: the previous advance issued it already)
+            if (int rc = sml_res_step_begin(h->res, h->fb, h->main)) return rc;
+        h->begun_next = false;
         if (int rc = slab_predict(h)) return rc;
         // SPEEDY's forecast of the previous window
         if (int rc = hop_wait(h, sml_hybrid::kHopLm, h->main)) return rc;
@@ -935,6 +949,12 @@ extern "C" int sml_hybrid_advance(sml_hybrid *h, const double *d_outvec_all) {
         if (int rc = hop_signal(h, sml_hybrid::kHopLm, s)) return rc;
     } else if (h->ncs) {
         if (int rc = sml_res_tile_local_model(h->res, h->f4, h->f2, h->lm, s)) return rc;
+    }
+    // pipelined: the next step's begin from the feedback just tiled, on the main stream,
+    // beside this window (it would be the next predict's first launch anyway)
+    if (h->pipelined && h->overlap) {
+        if (int rc = sml_res_step_begin(h->res, h->fb, h->main)) return rc;
+        h->begun_next = true;
     }
     h->predicted = false;
     h->advanced = true;

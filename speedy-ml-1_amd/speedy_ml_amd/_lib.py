@@ -56,6 +56,7 @@ EXPORTED = (
     "sml_hybrid_hop_mode", "sml_calendar_delta_hour", "sml_hybrid_set_feb29", "sml_hybrid_get_feb29",
     "sml_res_mean_std", "sml_res_set_outvec_ld", "sml_hybrid_set_slab", "sml_hybrid_start_slab",
     "sml_hybrid_exchange_width", "sml_hybrid_slab_buffers", "sml_dyn_set_hybrid_sst", "sml_dyn_set_sea_ice",
+    "sml_hybrid_set_pipelined",
 )
 
 SML_HOP_AUTO, SML_HOP_WAIT_VALUE, SML_HOP_EVENTS = 0, 1, 2
@@ -132,6 +133,7 @@ def _declare(L: ctypes.CDLL) -> None:
         "sml_res_enable_timing": [vp, i],
         "sml_res_set_read_waves": [vp, i],
         "sml_res_set_begin_mode": [vp, i],
+        "sml_hybrid_set_pipelined": [vp, i],
         "sml_res_begin_fused": [vp, vp],
         "sml_res_kernel_times": [vp, vp, vp, i, ctypes.POINTER(ctypes.c_int)],
         "sml_exchange_assemble": [vp, vp, vp, vp, vp, vp],

@@ -161,6 +161,11 @@ class HybridLoop:
         region order when the shares are uneven (sml_hybrid_advance_slabs)."""
         check(lib().sml_hybrid_advance_slabs(self._h, ptr(recv)))
 
+    def set_pipelined(self, on: bool = True):
+        """Each step also issues the next step's reservoir begin (sml_hybrid_set_pipelined):
+        the same outvecs, grids and forecasts; the reservoir states run one update ahead."""
+        check(lib().sml_hybrid_set_pipelined(self._h, 1 if on else 0))
+
     def set_hop_mode(self, mode: int):
         """SML_HOP_AUTO / SML_HOP_WAIT_VALUE / SML_HOP_EVENTS (include/speedy_ml.h)."""
         check(lib().sml_hybrid_set_hop_mode(self._h, int(mode)))

@@ -310,3 +310,37 @@ def test_serialised_dispatch_takes_event_hops(cuda, tmp_path):
     for k in runs[0]:
         np.testing.assert_array_equal(runs[1][k], runs[0][k], err_msg="events vs wait-value " + k)
         np.testing.assert_array_equal(got[k], runs[0][k], err_msg="serialised child vs default " + k)
+
+
+def test_pipelined_loop_steps_are_bitwise_the_default_loop(cuda):
+    """sml_hybrid_set_pipelined: every step's outvecs, feedback, local model, assembled
+    and forecast grids bitwise those of the default loop (3 steps, synced after each);
+    the reservoir state after step t is the default loop's after t + 1 updates."""
+    import torch
+
+    runs = {}
+    for pipe in (False, True):
+        loop, _ = _loop(cuda, True)
+        if pipe:
+            loop.set_pipelined(True)
+        snaps = []
+        for _ in range(3):
+            loop.step()
+            loop.sync()
+            snaps.append(_snapshot(loop))
+        runs[pipe] = (snaps, [loop.res.get_state(i) for i in (0, 700)])
+        if not pipe:  # one more begin: the default loop's states then match the pipelined loop's
+            loop.res.predict_begin(loop.fb, stream=loop.main)
+            loop.res.predict_finish(loop.lm, loop.ov, stream=loop.main)
+            torch.cuda.synchronize()
+            runs[pipe] = (snaps, [loop.res.get_state(i) for i in (0, 700)])
+        loop.close()
+        loop.dyn.close()
+        loop.res.close()
+        torch.cuda.synchronize()
+    (sa, xa), (sb, xb) = runs[False], runs[True]
+    for a, b in zip(sa, sb):
+        for k in a:
+            np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+    for a, b in zip(xa, xb):
+        np.testing.assert_array_equal(a, b)
