@@ -470,6 +470,13 @@ module sml_hip
       integer(c_int), value :: mode
       integer(c_int) :: rc
     end function
+    ! each advance also issues the next step's reservoir begin (states one update ahead)
+    function sml_hybrid_set_pipelined(h, on) bind(C, name='sml_hybrid_set_pipelined') result(rc)
+      import :: c_ptr, c_int
+      type(c_ptr), value :: h
+      integer(c_int), value :: on
+      integer(c_int) :: rc
+    end function
     function sml_hybrid_hop_mode(h, requested, effective) bind(C, name='sml_hybrid_hop_mode') result(rc)
       import :: c_ptr, c_int
       type(c_ptr), value :: h
