@@ -114,6 +114,22 @@ constexpr int kFftThreads = 64;
 // straight into iogrid(31)'s variables3d(4, ix, il, kx) (var = T, u, v, q) and logp
 // instead of grid (ppo_iogrid.f90:590-595); ex.mm set: run_model's exit on top
 // (sml_spectral_internal.hpp IoExit: q floor, the unsafe window's pass-through)
+// transform t -> (field f, latitude j) of the FFT kernels.  For iogrid's 33 fields
+// of the (var, x, y, z)-ordered grid the four variables of one (level, latitude) are
+// neighbouring transforms, so a wave's 8-B loads / stores of grid point e cover 64-B
+// runs (4 variables x the pair's 2 points) instead of 64 scattered words; else
+// consecutive transforms are consecutive latitudes of one field
+__device__ inline void fft_fj(int t, bool io, int &f, int &j) {
+    if (io && t < 4 * kKX * kIL) {
+        const int q = t >> 2;
+        f = (t & 3) * kKX + q % kKX;
+        j = q / kKX;
+    } else {
+        f = t / kIL;
+        j = t % kIL;
+    }
+}
+
 __global__ __launch_bounds__(kFftThreads) void k_gridx(const double *__restrict__ varm, double *__restrict__ grid,
                                                        const double *__restrict__ wa, const double *__restrict__ cosgr,
                                                        int nf, int c0, int c1, double *__restrict__ g4,
@@ -126,7 +142,8 @@ __global__ __launch_bounds__(kFftThreads) void k_gridx(const double *__restrict_
     const int id = blockIdx.x * kFftThreads + threadIdx.x;
     const bool act = id < 2 * nf * kIL;
     const int t = id >> 1, h = id & 1;
-    const int f = act ? t / kIL : 0, j = act ? t % kIL : 0;
+    int f = 0, j = 0;
+    if (act) fft_fj(t, g4 && nf == 4 * kKX + 1, f, j);
     double xi[kMX2 - 1];
     if (act) {
         const double *v = varm + (size_t)f * kVarmField + j * kMX2;
@@ -204,7 +221,8 @@ __global__ __launch_bounds__(kFftThreads) void k_specx(const double *__restrict_
     const int id = blockIdx.x * kFftThreads + threadIdx.x;
     const bool act = id < 2 * nf * kIL;
     const int t = id >> 1, h = id & 1, pr = threadIdx.x >> 1;
-    const int f = act ? t / kIL : 0, j = act ? t % kIL : 0;
+    int f = 0, j = 0;
+    if (act) fft_fj(t, g4 && nf == 4 * kKX + 1, f, j);
     double x[kFftN / 2];
     const bool sc = act && scale_tab && f < nscaled;
     double s0 = 1.0;
