@@ -25,6 +25,14 @@ is reported beside the headline as `reservoir_only`.
 
 Usage: python bench.py [--gpus N --steps K --warmup W]
        python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
+
+`python bench.py --gpus N` (N > 1, WORLD_SIZE unset) launches its N ranks itself:
+the parent starts N fresh child processes of this script, one per GPU, with RANK /
+LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT set -- the role
+startmpi plays under mpirun in the reference (src/mpires.f90:21-37) -- before it
+touches the GPU itself (it never does), relays rank 0's JSON line and exits non-zero
+when any rank fails or the launch times out.  Under torch.distributed.run (WORLD_SIZE
+set) every process is already one rank and runs directly.
 """
 from __future__ import annotations
 
@@ -32,6 +40,9 @@ import argparse
 import json
 import os
 import platform
+import signal
+import socket
+import subprocess
 import sys
 import time
 
@@ -87,7 +98,112 @@ def parse():
                         "window (sml_hybrid_set_slab)")
     p.add_argument("--speedy-steps", type=int, default=48,
                    help="leapfrog steps timed in the supplementary SPEEDY-step leg (0 = skip)")
+    p.add_argument("--poll-run-speedy", action=argparse.BooleanOptionalAction, default=True,
+                   help="after every timed step the host reads run_speedy and ends the loop when it is false, "
+                        "as parallelmain.f90:268-270 does (sml_hybrid_run_speedy waits for that step's safety "
+                        "check); --no-poll-run-speedy times the enqueued chain alone")
+    p.add_argument("--launch-timeout", type=float, default=1500.0,
+                   help="--gpus N > 1 without WORLD_SIZE: seconds before the launcher ends its ranks")
+    p.add_argument("--dry-run", choices=("env", "gloo", "fail"), default=None,
+                   help=argparse.SUPPRESS)  # launcher self-test (tests/test_bench_launch.py): no GPU, no torch.cuda
     return p.parse_args()
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(args) -> int:
+    """One fresh process per GPU (startmpi's role, mpires.f90:21-37): rank r gets
+    RANK = LOCAL_RANK = r, WORLD_SIZE = N and a 127.0.0.1 rendezvous.  Runs before
+    anything touches the GPU and never execs; rank 0's stdout (the JSON line) is
+    this process's stdout, the other ranks' goes to stderr.  Returns the exit code:
+    0 when every rank succeeded, else the first failure's (or 124 on a timeout), after
+    ending the ranks still running."""
+    n = args.gpus
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # the box's driver supports dmabuf IPC only
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=None if r == 0 else sys.stderr, start_new_session=False))
+    print(f"[bench] launched {n} ranks (pids {[p.pid for p in procs]}), rendezvous 127.0.0.1:{port}",
+          file=sys.stderr, flush=True)
+
+    def stop_all(sig=signal.SIGTERM):
+        for p in procs:
+            if p.poll() is None:
+                try:
+                    p.send_signal(sig)
+                except OSError:
+                    pass
+
+    def on_signal(signum, _frame):
+        stop_all(signum)
+
+    old = {s: signal.signal(s, on_signal) for s in (signal.SIGTERM, signal.SIGINT)}
+    t0, rc = time.time(), 0
+    try:
+        while True:
+            codes = [p.poll() for p in procs]
+            bad = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
+            if bad:
+                r, c = bad[0]
+                print(f"[bench] rank {r} exited with {c}: ending the other ranks", file=sys.stderr, flush=True)
+                rc = c if c > 0 else 128 - c
+                break
+            if all(c == 0 for c in codes):
+                break
+            if time.time() - t0 > args.launch_timeout:
+                print(f"[bench] launch timed out after {args.launch_timeout:.0f} s", file=sys.stderr, flush=True)
+                rc = 124
+                break
+            time.sleep(0.2)
+    finally:
+        if rc:
+            stop_all()
+            t1 = time.time()
+            while any(p.poll() is None for p in procs) and time.time() - t1 < 15:
+                time.sleep(0.2)
+            stop_all(signal.SIGKILL)
+        for p in procs:
+            p.wait()
+        for s_, h in old.items():
+            signal.signal(s_, h)
+    return rc
+
+
+def dry_run(args) -> None:
+    """Launcher self-test: report this rank's environment (env), or join a gloo group
+    over the launcher's rendezvous and gather every rank's (gloo); `fail`: rank 1
+    exits with 3 while rank 0 waits, so the launcher must end rank 0 and fail."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    me = {k: os.environ.get(k) for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}
+    me["pid"] = os.getpid()
+    if args.dry_run == "fail":
+        if rank == 1:
+            sys.exit(3)
+        time.sleep(120)
+        return
+    if args.dry_run == "gloo":
+        import torch.distributed as dist
+
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        allv = [None] * world
+        dist.all_gather_object(allv, me)
+        dist.barrier()
+        dist.destroy_process_group()
+        if rank == 0:
+            print(json.dumps({"dry_run": "gloo", "n_gpus": world, "ranks": allv}), flush=True)
+        return
+    print(json.dumps({"dry_run": "env", "n_gpus": world, "rank": me}), flush=True)
 
 
 def log(rank, *a):
@@ -97,6 +213,11 @@ def log(rank, *a):
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
+    if args.dry_run:
+        dry_run(args)
+        return
     import torch
     import torch.distributed as dist
 
@@ -193,8 +314,21 @@ def main():
     torch.cuda.synchronize()
     log(rank, f"setup {time.time() - t_setup:.1f}s, {len(regions)} regions on rank 0")
 
+    ended = []  # the step after which run_speedy was false (the reference's loop exit)
+    ran = [0]   # steps the last timed region ran
+
     def step():
         loop.step()
+
+    def step_polled():
+        """parallelmain.f90:268-270: after every step the host reads run_speedy (rank 0
+        decides in the reference and broadcasts it, mpires.f90:721; here every rank's
+        redundant window gives the same flag) and ends the prediction when it is false."""
+        loop.step()
+        if not loop.run_speedy():
+            ended.append(True)
+            return False
+        return True
 
     def timed(fn, nsteps, timing=False):
         if timing:
@@ -204,10 +338,14 @@ def main():
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         host = []
+        ran[0] = 0
         for _ in range(nsteps):
             h0 = time.perf_counter()
-            fn()
+            go = fn()
             host.append(time.perf_counter() - h0)
+            ran[0] += 1
+            if go is False:  # run_speedy false: the reference's loop ends here
+                break
         th = time.perf_counter() - t0
         loop.sync()
         torch.cuda.synchronize()
@@ -226,8 +364,12 @@ def main():
     for _ in range(args.warmup):
         step()
     loop.sync()
-    dt = timed(step, args.steps, timing=True)
+    poll = args.poll_run_speedy and sim == 1  # (--sim-ranks: the other ranks' rows are stale, the check fails)
+    dt = timed(step_polled if poll else step, args.steps, timing=True)
     upd_ms, rd_ms = res.kernel_times()
+    steps_done = ran[0]
+    # the poll's cost: the same K steps again without the host waiting on run_speedy
+    dt_nopoll = timed(step, args.steps) if poll and not ended else None
     if args.pipelined and args.overlap:  # the next step's begin is in flight: close it (untimed)
         res.predict_finish(lm, ov, stream=loop.main)
         torch.cuda.synchronize()
@@ -295,7 +437,7 @@ def main():
     training = training_leg(dev, mask, args, world, rank) if args.train_regions > 0 else None
 
     if rank == 0:
-        steps_per_s = args.steps / dt
+        steps_per_s = steps_done / dt
         line = {
             "metric": "hybrid timesteps/sec, T30L8 + 1152x6k-node reservoirs; 1/2/4/8-GPU scaling",
             "value": round(steps_per_s, 3),
@@ -303,7 +445,7 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(dt / args.steps * 1e3, 4),
+            "ms_per_step": round(dt / steps_done * 1e3, 4),
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
@@ -339,6 +481,12 @@ def main():
                             if args.overlap and args.speedy_cus > 0 else
                             "overlapped, no CU split" if args.overlap else "one stream"),
             },
+            "run_speedy_poll": ({"per_step": True, "ended_after_step": steps_done if ended else None,
+                                 "note": "the host reads run_speedy after every timed step and would end the loop "
+                                         "on false (parallelmain.f90:268-270); the same K steps without the poll",
+                                 "value_without_poll": round(args.steps / dt_nopoll, 3) if dt_nopoll else None,
+                                 "cost_pct": round((dt - dt_nopoll) / dt_nopoll * 100, 2) if dt_nopoll else None}
+                                if poll else {"per_step": False}),
             "last_window_safe": bool(safe),
             "finite": finite,
             "roofline": {
@@ -449,22 +597,35 @@ def speedy_roofline(st, forcing, bc):
                   "frac_of_occupied_cus": round(tf / occ, 4), "frac_of_chip": round(tf / F64_VALU_PEAK_TF, 5)})
     out["k_st_gridspec"] = e
     e = {"blocks": nb_s, "span_us": span_s, "phases_us": ph_s, "bound": "latency (phase chain with barriers)"}
-    if specy_fl and gridy_fl:
+    # algorithmic Legendre work: the reference sums only
+    # m <= nsh2(n) (spe_spectral.f90:476-493 gridy, :513-535 specy): 50.6 kflop per
+    # inverse field (24 latitude pairs x 1054 FMA) and 50.5 kflop per forward field;
+    # a fused step runs 73 forward (specx -> specy) and 91 inverse (gridy -> gridx) fields
+    specy_algo, gridy_algo = 73 * 50.5e3, 91 * 50.6e3
+    occ = F64_MFMA_PEAK_TF * nb_s * spec_split / 256
+    sy = specy_algo / (ph_s["specy"] * 1e-6) / 1e12
+    gy = gridy_algo / (ph_s["gridy"] * 1e-6) / 1e12
+    leg_algo = specy_algo + gridy_algo
+    e.update({
+        "blocks": nb_s * spec_split,
+        "legendre_algorithmic_flops": leg_algo,
+        "achieved_tflops_kernel": round(leg_algo / (span_s * 1e-6) / 1e12, 3),
+        "legendre_mfma_utilisation": {
+            "basis": "algorithmic flops (the triangle m <= nsh2(n) the reference sums) / phase time",
+            "specy_tflops": round(sy, 3), "gridy_tflops": round(gy, 3),
+            "specy_frac_of_occupied_cus": round(sy / occ, 4), "gridy_frac_of_occupied_cus": round(gy / occ, 4),
+            "specy_frac_of_chip": round(sy / F64_MFMA_PEAK_TF, 5),
+            "gridy_frac_of_chip": round(gy / F64_MFMA_PEAK_TF, 5),
+            "step_frac_of_chip": round(leg_algo / (span_s * 1e-6) / 1e12 / F64_MFMA_PEAK_TF, 5),
+        }})
+    if specy_fl and gridy_fl:  # what the MFMAs issued (PMC), padding and the zero triangle included
         leg = specy_fl + gridy_fl
-        sy = specy_fl / (ph_s["specy"] * 1e-6) / 1e12
-        gy = gridy_fl / (ph_s["gridy"] * 1e-6) / 1e12
-        occ = F64_MFMA_PEAK_TF * nb_s * spec_split / 256
-        e.update({
-            "blocks": nb_s * spec_split,
-            "legendre_mfma_flops": leg,
-            "achieved_tflops_kernel": round(leg / (span_s * 1e-6) / 1e12, 3),
-            "legendre_mfma_utilisation": {
-                "specy_tflops": round(sy, 3), "gridy_tflops": round(gy, 3),
-                "specy_frac_of_occupied_cus": round(sy / occ, 4), "gridy_frac_of_occupied_cus": round(gy / occ, 4),
-                "specy_frac_of_chip": round(sy / F64_MFMA_PEAK_TF, 5),
-                "gridy_frac_of_chip": round(gy / F64_MFMA_PEAK_TF, 5),
-                "step_frac_of_chip": round(leg / (span_s * 1e-6) / 1e12 / F64_MFMA_PEAK_TF, 5),
-            }})
+        e["legendre_issued"] = {
+            "source": "SQ_INSTS_VALU_MFMA_MOPS_F64 x 512 per dispatch (profiles/speedy_pmc.json)",
+            "flops": leg, "specy_flops": specy_fl, "gridy_flops": gridy_fl,
+            "issued_over_algorithmic": round(leg / leg_algo, 3),
+            "specy_tflops": round(specy_fl / (ph_s["specy"] * 1e-6) / 1e12, 3),
+            "gridy_tflops": round(gridy_fl / (ph_s["gridy"] * 1e-6) / 1e12, 3)}
     out["k_st_spec"] = e
     return out
 

@@ -181,6 +181,13 @@ int sml_res_step(sml_reservoirs *c, const double *d_feedback, const double *d_lo
  * before the next begin (SML_ERR_STATE otherwise). */
 int sml_res_step_begin(sml_reservoirs *c, const double *d_feedback, void *stream);
 int sml_res_step_finish(sml_reservoirs *c, const double *d_local_model, double *d_outvec, void *stream);
+/* discard a begun step (a begin without its finish, e.g. the pipelined loop's
+ * next begin when the host restarts the prediction): waits for the device, then rolls
+ * the state back to the one the begin read.  No-op when nothing is begun.
+ * sml_res_set_state discards a begun step itself.  sml_res_step_begun: 1 while a
+ * begin waits for its finish. */
+int sml_res_step_cancel(sml_reservoirs *c);
+int sml_res_step_begun(const sml_reservoirs *c, int *begun);
 /* finish straight from SPEEDY's forecast grids: the local-model tiling of
  * sml_res_tile_local_model (res_domain.f90:1000-1031, standardize_state_vec_res
  * :1189-1293) fused into sml_res_step_finish, one launch; identical results.
@@ -583,6 +590,15 @@ int sml_hybrid_hop_mode(const sml_hybrid *h, int *requested, int *effective);
  * a step (and a sync) the reservoir states are one update ahead (the next step's).
  * The next predict only finishes that begin. */
 int sml_hybrid_set_pipelined(sml_hybrid *h, int on);
+/* the exchange through the communicator's transport even at world 1 (default off): a
+ * one-rank loop with an RCCL communicator (sml_comm_create at world 1) then runs
+ * sml_hybrid_step's world > 1 path -- outvecs to the send slab, ncclAllGather on the
+ * main stream, sml_hybrid_advance_slabs from the receive slab, separate assembly --
+ * instead of the identity exchange fused into the finish.  Same results, bitwise;
+ * for exercising the transport on one GPU.  Refused without a transport. */
+int sml_hybrid_set_force_exchange(sml_hybrid *h, int on);
+/* the number of ncclAllGather calls sml_hybrid_step has issued on this loop */
+int sml_hybrid_exchanges(const sml_hybrid *h, int64_t *allgathers);
 /* run_speedy of the last step (0: the reference ends the prediction,
  * parallelmain.f90:268-270); waits only for that step's safety check */
 int sml_hybrid_run_speedy(sml_hybrid *h, int *run);

@@ -83,6 +83,12 @@ struct sml_hybrid {
     // (update + v_ml readout) on the main stream as soon as its feedback is tiled;
     // begun_next: that begin is in flight, so the next predict only finishes
     bool pipelined = false, begun_next = false;
+    // sml_hybrid_set_force_exchange: a world-1 loop with a transport takes the world > 1
+    // exchange path (send slab -> ncclAllGather -> advance from the receive slab)
+    bool force_exchange = false;
+    int64_t allgathers = 0;  // ncclAllGather calls issued by sml_hybrid_step (sml_hybrid_exchanges)
+    // SML_HYBRID_ASM=0 (read at create): the one-rank step assembles separately (A/B)
+    bool fuse_asm = true;
     // get_tisr_by_date (mpires.f90:1644-1676): a table of hourly global tisr fields
     // [nhours][48][96] on the device, the calendar's start year, the hours before the
     // first prediction step and the hours per step; t = steps advanced so far
@@ -406,7 +412,7 @@ int alloc_exchange(sml_hybrid *h) {
         }
     const size_t row = (size_t)h->xw * 8;
     const int world = h->comm->world;
-    if (h->comm->comm &&
+    if (h->comm->comm && h->maxc > 0 &&
         (hipMalloc(&h->d_send, (size_t)h->maxc * row) != hipSuccess ||
          hipMalloc(&h->d_recv, (size_t)world * h->maxc * row) != hipSuccess ||
          hipMemset(h->d_send, 0, (size_t)h->maxc * row) != hipSuccess))
@@ -449,6 +455,21 @@ extern "C" int sml_hybrid_set_hop_mode(sml_hybrid *h, int mode) {
 extern "C" int sml_hybrid_set_pipelined(sml_hybrid *h, int on) {
     SML_REQUIRE(h, "null context");
     h->pipelined = on != 0;
+    return SML_OK;
+}
+
+extern "C" int sml_hybrid_set_force_exchange(sml_hybrid *h, int on) {
+    SML_REQUIRE(h, "null context");
+    if (on && !h->force_exchange) {
+        SML_REQUIRE(h->comm && h->comm->comm, "forcing the exchange needs a communicator with a transport");
+        SML_REQUIRE(!h->predicted, "sml_hybrid_set_force_exchange between predict and advance");
+        if (h->comm->world == 1) {  // the one-rank plan: maxc = every region, contiguous
+            h->maxc = h->nlocal;
+            h->contiguous = true;
+            if (int rc = alloc_exchange(h)) return rc;
+        }
+    }
+    h->force_exchange = on != 0;
     return SML_OK;
 }
 
@@ -551,6 +572,7 @@ extern "C" int sml_hybrid_create(sml_reservoirs *res, sml_dynamics *dyn, sml_com
             h->side = h->main;
         }
     }
+    if (const char *e = std::getenv("SML_HYBRID_ASM")) h->fuse_asm = *e != '0';
     if (hipEventCreateWithFlags(&h->ev[0], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&h->ev[1], hipEventDisableTiming) != hipSuccess)
         return bail(fail(SML_ERR_HIP, "event"));
@@ -645,6 +667,13 @@ extern "C" int sml_hybrid_start(sml_hybrid *h, const double *d_g4, const double 
     SML_REQUIRE(h && h->fb, "sml_hybrid_set_buffers first");
     SML_REQUIRE(d_g4 && d_g2 && d_pr && d_f4 && d_f2, "null argument");
     SML_HIP(hipDeviceSynchronize());
+    // a restart after a pipelined run: the begin the last advance issued was built from
+    // the old feedback -- discard it (the state rolls back to the one it read), so the
+    // first predict begins from the feedback tiled here
+    if (h->begun_next) {
+        if (int rc = sml_res_step_cancel(h->res)) return rc;
+        h->begun_next = false;
+    }
     const size_t n4 = (size_t)kGrid4d * 8, n2 = (size_t)kGrid2d * 8;
     if (d_g4 != h->g4) SML_HIP(hipMemcpyAsync(h->g4, d_g4, n4, hipMemcpyDeviceToDevice, h->main));
     if (d_g2 != h->g2) SML_HIP(hipMemcpyAsync(h->g2, d_g2, n2, hipMemcpyDeviceToDevice, h->main));
@@ -672,7 +701,11 @@ int slab_predict(sml_hybrid *h) {
     if (!sl.res) return SML_OK;
     if (!sl.started) return fail(SML_ERR_STATE, "sml_hybrid_start_slab first");
     const int64_t tt = h->t + 1;
-    if ((tt * sl.timestep) % sl.timestep_slab != 0 || sl.nslab == 0) return SML_OK;
+    if ((tt * sl.timestep) % sl.timestep_slab != 0) return SML_OK;
+    // a slab step on every rank: the other ranks' rows carry new sst, so wholegrid_sst
+    // and the window's sst are rebuilt here too, even when this rank predicts none
+    sl.dirty = true;
+    if (sl.nslab == 0) return SML_OK;
     hipStream_t m = h->main;
     hipLaunchKernelGGL(k_slab_avg, dim3((sl.tot_fb + 255) / 256), dim3(256), 0, m, sl.d_ring, sl.ratio - 1, sl.tot_fb,
                        sl.d_fb);
@@ -682,7 +715,6 @@ int slab_predict(sml_hybrid *h) {
     hipLaunchKernelGGL(k_slab_rows, dim3((n + 255) / 256), dim3(256), 0, m, sl.d_ov, sl.d_row, sl.nslab, sl.nsst,
                        h->nlocal, h->nout, h->xw, false, h->ov);
     SML_HIP(hipGetLastError());
-    sl.dirty = true;
     return SML_OK;
 }
 
@@ -806,7 +838,7 @@ extern "C" int sml_hybrid_set_slab(sml_hybrid *h, sml_reservoirs *slab, const do
     SML_HIP(hipMemset(sl.d_sst, 0, (size_t)kGrid2d * 8));
     h->xw = xw;
     if (int rc = sml_res_set_outvec_ld(h->res, xw)) return rc;
-    if (h->comm && h->comm->world > 1)
+    if (h->comm && (h->comm->world > 1 || h->force_exchange))
         if (int rc = alloc_exchange(h)) return rc;
     sl.res = slab;
     return SML_OK;
@@ -880,7 +912,12 @@ int predict_impl(sml_hybrid *h, bool assemble) {
     if (h->predicted) return fail(SML_ERR_STATE, "sml_hybrid_predict twice without sml_hybrid_advance");
     h->assembled = false;
     if (h->overlap) {
-        if (!h->begun_next)  // (pipelined: the previous advance issued it already)
+        // (pipelined: the previous advance issued it already, unless the host discarded
+        // it since -- sml_res_set_state / sml_res_step_cancel)
+        int begun = 0;
+        if (h->begun_next)
+            if (int rc = sml_res_step_begun(h->res, &begun)) return rc;
+        if (!begun)
             if (int rc = sml_res_step_begin(h->res, h->fb, h->main)) return rc;
         h->begun_next = false;
         if (int rc = slab_predict(h)) return rc;
@@ -967,7 +1004,7 @@ extern "C" int sml_hybrid_advance(sml_hybrid *h, const double *d_outvec_all) {
 extern "C" int sml_hybrid_advance_slabs(sml_hybrid *h, const double *d_recv) {
     SML_REQUIRE(h && d_recv, "null argument");
     const int world = h->comm ? h->comm->world : 1;
-    if (world == 1 || h->contiguous) return sml_hybrid_advance(h, d_recv);
+    if (world == 1 || h->contiguous) return sml_hybrid_advance(h, d_recv);  // slabs in region order
     if (!h->predicted) return fail(SML_ERR_STATE, "sml_hybrid_advance_slabs without sml_hybrid_predict");
     const int total = h->numregions * h->xw;
     hipLaunchKernelGGL(k_gather_rows, dim3((total + 255) / 256), dim3(256), 0, h->main, d_recv, h->d_perm, h->d_glob,
@@ -988,11 +1025,13 @@ extern "C" int sml_hybrid_step(sml_hybrid *h) {
         return fail(SML_ERR_STATE, "rank %d of %d has no transport: exchange through sml_hybrid_advance_slabs",
                     h->comm->rank, world);
     // one rank: the exchange is the identity, so the finish assembles the grids itself
-    // (SML_HYBRID_ASM=0: the separate assembly, for A/B)
-    const char *e = std::getenv("SML_HYBRID_ASM");
-    const bool fuse = world == 1 && h->overlap && sml::res_in_global_order(h->res) && !(e && *e == '0');
+    // (SML_HYBRID_ASM=0: the separate assembly, for A/B); forced, it goes through the
+    // transport as at world > 1
+    const bool identity = world == 1 && !h->force_exchange;
+    const bool fuse = identity && h->overlap && sml::res_in_global_order(h->res) && h->fuse_asm;
     if (int rc = predict_impl(h, fuse)) return rc;
-    if (world == 1) return sml_hybrid_advance(h, h->ov);
+    if (identity) return sml_hybrid_advance(h, h->ov);
+    // (world > 1, or world 1 forced through the transport)
     // even shares (1152 / N for N = 1, 2, 4, 8): the outvecs go out of ov as they are;
     // uneven ones are padded to the largest share through d_send (one copy more on the
     // critical path; d_send's padding rows stay zero)
@@ -1002,7 +1041,14 @@ extern "C" int sml_hybrid_step(sml_hybrid *h) {
         send = h->d_send;
     }
     if (int rc = sml_comm_allgather(h->comm, send, h->d_recv, (int64_t)h->maxc * h->xw, h->main)) return rc;
+    ++h->allgathers;
     return sml_hybrid_advance_slabs(h, h->d_recv);
+}
+
+extern "C" int sml_hybrid_exchanges(const sml_hybrid *h, int64_t *allgathers) {
+    SML_REQUIRE(h && allgathers, "null argument");
+    *allgathers = h->allgathers;
+    return SML_OK;
 }
 
 // run_speedy after the last advance (mpires.f90:721, :1623): 0 ends the prediction

@@ -112,6 +112,11 @@ struct sml_reservoirs {
     // update grid then the v_ml readout grid, 1 one fused launch (k_res_begin, 2 blocks
     // per CU), 2 fused with the readout's loads unrolled twice (1 block per CU)
     int begin_mode = 0;
+    // A/B knobs read once at create (SML_UPD_PARTS: parts per region of the update,
+    // 0 = automatic; SML_UPD_OCC=2: the update's 8-waves-per-EU launch bound; SML_BEGIN:
+    // overrides begin_mode when >= 0), never on the enqueue path of a step
+    int upd_parts = 0, begin_env = -1;
+    bool upd_occ2 = false;
     bool begun = false;             // sml_res_step_begin issued, finish pending
     int8_t *d_outl = nullptr;
     int32_t *d_asm_dst = nullptr;   // [numregions*nout] -> concatenated grid index
@@ -1038,6 +1043,9 @@ int res_create_impl(int numregions, int nlocal, const int *region_ids, const uns
     if (c->generic) c->out_l.assign(out_index, out_index + nout);
     if (const char *e = std::getenv("SML_READ_WAVES")) c->read_waves = std::max(0, std::atoi(e));
     if (const char *e = std::getenv("SML_UPD_BLOCKS")) c->upd_blocks = std::max(0, std::atoi(e));
+    if (const char *e = std::getenv("SML_UPD_PARTS")) c->upd_parts = std::max(0, std::atoi(e));
+    if (const char *e = std::getenv("SML_UPD_OCC")) c->upd_occ2 = *e == '2';
+    if (const char *e = std::getenv("SML_BEGIN")) c->begin_env = std::max(0, std::min(2, std::atoi(e)));
     SML_REQUIRE(c->read_waves >= 0, "bad read_waves");
     (void)hipGetDevice(&c->device);
     c->region_ids.assign(region_ids, region_ids + nlocal);
@@ -1225,6 +1233,8 @@ extern "C" int sml_res_load_region_f64(sml_reservoirs *c, int i, const int *rows
 extern "C" int sml_res_set_state(sml_reservoirs *c, int i, const double *x) {
     if (int rc = check_region(c, i)) return rc;
     SML_REQUIRE(x, "x is null");
+    // a begun step read the state being replaced: it is discarded (sml_res_step_cancel)
+    if (int rc = sml_res_step_cancel(c)) return rc;
     SML_HIP(hipMemcpy(c->d_x[c->cur] + c->rd[i].x, x, (size_t)c->n[i] * 8, hipMemcpyHostToDevice));
     return SML_OK;
 }
@@ -1302,7 +1312,7 @@ int launch_update(sml_reservoirs *c, const double *xo, double *xn, const double 
     // 1152 regions, 1 part 119 us, 2 parts 128 us, 4 parts 165 us (profiles/r01m)
     const int max_parts = std::max(1, (c->maxn + kUpdThreads - 1) / kUpdThreads);
     int parts = std::max(1, std::min(max_parts, (512 + c->nlocal - 1) / c->nlocal));
-    if (const char *e = std::getenv("SML_UPD_PARTS")) parts = std::max(1, std::min(max_parts, std::atoi(e)));
+    if (c->upd_parts > 0) parts = std::min(max_parts, c->upd_parts);
     const int lds_x = (c->maxn + 1) / 2 * 2;
     const size_t lds = (size_t)(lds_x + c->maxninp) * sizeof(double);
     const bool use_lds = lds <= 64 * 1024;
@@ -1311,8 +1321,7 @@ int launch_update(sml_reservoirs *c, const double *xo, double *xn, const double 
     // beside SPEEDY's window (sml_res_step_begin) the grid may be capped (upd_blocks):
     // fewer blocks in flight, each taking logical blocks in rounds
     dim3 ug(paced && c->upd_blocks > 0 ? std::min(nlog, c->upd_blocks) : nlog);
-    const char *eo = std::getenv("SML_UPD_OCC");
-    const bool occ2 = eo && *eo == '2';
+    const bool occ2 = c->upd_occ2;
 #define SML_UPD(WT, L)                                                                                            \
     hipLaunchKernelGGL(occ2 ? (k_res_update<WT, L, 8>) : (k_res_update<WT, L, 4>), ug, dim3(kUpdThreads),        \
                        L ? lds : 0, st, c->d_rd, c->d_a_rp, c->d_a_col, (const WT *)c->d_a_val, c->d_w_rp,        \
@@ -1336,8 +1345,7 @@ int launch_update(sml_reservoirs *c, const double *xo, double *xn, const double 
 }
 
 int begin_mode(const sml_reservoirs *c) {
-    if (const char *e = std::getenv("SML_BEGIN")) return std::atoi(e);
-    return c->begin_mode;
+    return c->begin_env >= 0 ? c->begin_env : c->begin_mode;
 }
 
 // the fused begin needs the wide readout (8 waves of 17 rows per region at most)
@@ -1451,6 +1459,25 @@ extern "C" int sml_res_step_begin(sml_reservoirs *c, const double *d_feedback, v
     }
     c->cur = 1 - c->cur;
     c->begun = true;
+    return SML_OK;
+}
+
+// discard a begun step (sml_res_step_begin without its finish): wait for it, then
+// roll the state back -- the begin read x from one buffer and wrote the update into
+// the other, so the old state is intact; x_aug and the v_ml partial sums are scratch
+// that the next begin rewrites.  A no-op when no step is begun.
+extern "C" int sml_res_step_cancel(sml_reservoirs *c) {
+    SML_REQUIRE(c, "null context");
+    if (!c->begun) return SML_OK;
+    SML_HIP(hipDeviceSynchronize());
+    c->cur = 1 - c->cur;
+    c->begun = false;
+    return SML_OK;
+}
+
+extern "C" int sml_res_step_begun(const sml_reservoirs *c, int *begun) {
+    SML_REQUIRE(c && begun, "null argument");
+    *begun = c->begun ? 1 : 0;
     return SML_OK;
 }
 

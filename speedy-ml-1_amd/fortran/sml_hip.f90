@@ -176,6 +176,19 @@ module sml_hip
       integer(c_int) :: rc
     end function
 
+    ! discard a begun step (state rolled back); 1 in begun while a begin waits for its finish
+    function sml_res_step_cancel(ctx) bind(C, name='sml_res_step_cancel') result(rc)
+      import :: c_ptr, c_int
+      type(c_ptr), value :: ctx
+      integer(c_int) :: rc
+    end function
+    function sml_res_step_begun(ctx, begun) bind(C, name='sml_res_step_begun') result(rc)
+      import :: c_ptr, c_int
+      type(c_ptr), value :: ctx
+      integer(c_int), intent(out) :: begun
+      integer(c_int) :: rc
+    end function
+
     function sml_res_set_read_waves(ctx, waves) bind(C, name='sml_res_set_read_waves') result(rc)
       import :: c_ptr, c_int
       type(c_ptr), value :: ctx
@@ -475,6 +488,19 @@ module sml_hip
       import :: c_ptr, c_int
       type(c_ptr), value :: h
       integer(c_int), value :: on
+      integer(c_int) :: rc
+    end function
+    ! a world-1 loop with a transport exchanges through it (ncclAllGather) as at world > 1
+    function sml_hybrid_set_force_exchange(h, on) bind(C, name='sml_hybrid_set_force_exchange') result(rc)
+      import :: c_ptr, c_int
+      type(c_ptr), value :: h
+      integer(c_int), value :: on
+      integer(c_int) :: rc
+    end function
+    function sml_hybrid_exchanges(h, allgathers) bind(C, name='sml_hybrid_exchanges') result(rc)
+      import :: c_ptr, c_int, c_int64_t
+      type(c_ptr), value :: h
+      integer(c_int64_t), intent(out) :: allgathers
       integer(c_int) :: rc
     end function
     function sml_hybrid_hop_mode(h, requested, effective) bind(C, name='sml_hybrid_hop_mode') result(rc)

@@ -56,7 +56,8 @@ EXPORTED = (
     "sml_hybrid_hop_mode", "sml_calendar_delta_hour", "sml_hybrid_set_feb29", "sml_hybrid_get_feb29",
     "sml_res_mean_std", "sml_res_set_outvec_ld", "sml_hybrid_set_slab", "sml_hybrid_start_slab",
     "sml_hybrid_exchange_width", "sml_hybrid_slab_buffers", "sml_dyn_set_hybrid_sst", "sml_dyn_set_sea_ice",
-    "sml_hybrid_set_pipelined",
+    "sml_hybrid_set_pipelined", "sml_res_step_cancel", "sml_res_step_begun", "sml_hybrid_set_force_exchange",
+    "sml_hybrid_exchanges",
 )
 
 SML_HOP_AUTO, SML_HOP_WAIT_VALUE, SML_HOP_EVENTS = 0, 1, 2
@@ -228,6 +229,10 @@ def _declare(L: ctypes.CDLL) -> None:
         "sml_hybrid_slab_buffers": [vp, pp, pp, ip, pp, pp],
         "sml_dyn_set_hybrid_sst": [vp, vp, d, vp],
         "sml_dyn_set_sea_ice": [vp, vp, vp],
+        "sml_res_step_cancel": [vp],
+        "sml_res_step_begun": [vp, ip],
+        "sml_hybrid_set_force_exchange": [vp, i],
+        "sml_hybrid_exchanges": [vp, i64p],
     }
     for name, args in sig.items():
         fn = getattr(L, name)

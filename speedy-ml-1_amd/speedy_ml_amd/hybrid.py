@@ -166,6 +166,17 @@ class HybridLoop:
         the same outvecs, grids and forecasts; the reservoir states run one update ahead."""
         check(lib().sml_hybrid_set_pipelined(self._h, 1 if on else 0))
 
+    def set_force_exchange(self, on: bool = True):
+        """With a NativeComm at world 1: run the world > 1 exchange path anyway (send
+        slab -> ncclAllGather -> advance from the receive slab; sml_hybrid_set_force_exchange)."""
+        check(lib().sml_hybrid_set_force_exchange(self._h, 1 if on else 0))
+
+    def exchanges(self) -> int:
+        """ncclAllGather calls the native step has issued (sml_hybrid_exchanges)."""
+        n = ctypes.c_int64()
+        check(lib().sml_hybrid_exchanges(self._h, ctypes.byref(n)))
+        return n.value
+
     def set_hop_mode(self, mode: int):
         """SML_HOP_AUTO / SML_HOP_WAIT_VALUE / SML_HOP_EVENTS (include/speedy_ml.h)."""
         check(lib().sml_hybrid_set_hop_mode(self._h, int(mode)))

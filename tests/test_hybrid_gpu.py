@@ -344,3 +344,40 @@ def test_pipelined_loop_steps_are_bitwise_the_default_loop(cuda):
             np.testing.assert_array_equal(a[k], b[k], err_msg=k)
     for a, b in zip(xa, xb):
         np.testing.assert_array_equal(a, b)
+
+
+def test_pipelined_loop_restart_is_bitwise_the_default_loop(cuda):
+    """A host that restarts the prediction after a pipelined run (sml_hybrid_start
+    again -- a new prediction_num, parallelmain.f90:206-212): the begin the last
+    advance issued was built from the old feedback, so sml_hybrid_start discards it
+    (sml_res_step_cancel: the state rolls back to the one it read) and the first
+    predict begins from the new feedback.  The steps after the restart are bitwise the
+    default loop's."""
+    import torch
+
+    from speedy_ml_amd.synthetic import synthetic_grids
+
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(cuda)  # noqa: E731
+    runs = {}
+    for pipe in (False, True):
+        loop, _ = _loop(cuda, True)
+        loop.set_pipelined(pipe)
+        for _ in range(2):
+            loop.step()
+        loop.sync()
+        g4, g2, pr = synthetic_grids(21)
+        f4, f2, _ = synthetic_grids(22)
+        loop.start(t(g4), t(g2), t(pr), t(f4), t(f2))
+        snaps = []
+        for _ in range(2):
+            loop.step()
+            loop.sync()
+            snaps.append(_snapshot(loop))
+        runs[pipe] = snaps
+        loop.close()
+        loop.dyn.close()
+        loop.res.close()
+        torch.cuda.synchronize()
+    for a, b in zip(runs[False], runs[True]):
+        for k in a:
+            np.testing.assert_array_equal(a[k], b[k], err_msg=k)

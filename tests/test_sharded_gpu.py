@@ -156,3 +156,146 @@ def test_transportless_rank_refuses_the_native_step(cuda):
         loop.step()
     _close(loop)
     comm.close()
+
+
+# ---------------------------------------------------------------------------
+# configs[3] as bench.py runs it: the slab ocean on (exchange rows of 140: each
+# region's 136-value outvec and its slab sst, sendrecievegrid's SST half,
+# mpires.f90:358-383 workers -> root, :458-472 wholegrid_sst, :575-581 / :733-736 the
+# SST back into every rank's feedback) and the pipelined loop.  One rank owns no sst
+# region at all (rank 1 of 8: its regions' sst flags are cleared in the mask the
+# one-rank loop uses too), so on a slab step it predicts no slab yet must rebuild
+# wholegrid_sst from the other ranks' rows.
+SLAB_STEPS = 4          # timestep_slab 24 h: the 4th hybrid step is a slab step
+SLAB_HOURS = 24
+
+
+def _slab_mask():
+    m = domain.load_sst_mask().copy()
+    m[domain.processor_decomposition(NREG, 8, 1)] = 0
+    return m
+
+
+def _slab_setup(cuda, regions, mask, comm):
+    import torch
+
+    from speedy_ml_amd._lib import check, lib, ptr
+    from speedy_ml_amd.dynamics import Dynamics
+    from speedy_ml_amd.exchange import OutvecExchange
+    from speedy_ml_amd.hybrid import HybridLoop, SlabOcean
+    from speedy_ml_amd.reservoir import Reservoirs
+    from speedy_ml_amd.synthetic import (dyn_state, phys_boundary, slab_fields, slab_start_outvec, slab_weights,
+                                         synthetic_grids)
+
+    sizes = [domain.reservoir_sizes(r, bool(mask[r])) for r in regions]
+    res = Reservoirs(list(regions), mask[regions], [s.n for s in sizes], [s.k for s in sizes])
+    for i, r in enumerate(regions):
+        res.load_region_weights(i, _weights(r, mask))
+        res.set_state(i, initial_state(r, sizes[i].n))
+    sids = [int(r) for r in regions if mask[r]]
+    sws = [slab_weights(r) for r in sids]
+    slab = Reservoirs(sids, [0] * len(sids), [w.n for w in sws], [w.k for w in sws], chunk_speedy=0, nout=4,
+                      ninp=[w.ninp for w in sws], out_index=[35] * 4)
+    for j, w in enumerate(sws):
+        slab.load_region_weights(j, w)
+        slab.set_state(j, initial_state(sids[j], w.n, seed=17))
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(cuda)  # noqa: E731
+    base, smask, sice, tice = slab_fields()
+    st0, forcing = dyn_state()
+    dyn = Dynamics()
+    dyn.set_forcing(**forcing)
+    dyn.set_state(st0)
+    dyn.set_physics(phys_boundary(dyn, forcing["phis"]))
+    check(lib().sml_dyn_set_sea_ice(dyn._h, ptr(np.ascontiguousarray(sice)), ptr(np.ascontiguousarray(tice))))
+    tisr = np.random.default_rng(13).standard_normal((NREG, 16))[regions]
+    ex = OutvecExchange(NREG, 1, 0, device=cuda) if comm is None else None
+    so = SlabOcean(slab, t(base), t(smask), timestep=6, timestep_slab=SLAB_HOURS)
+    loop = HybridLoop(res, dyn, ex, cuda, tisr=t(tisr), comm=comm, slab=so)
+    assert loop.exchange_width == 140
+    loop.set_pipelined(True)
+    g4, g2, pr = synthetic_grids(11)
+    f4, f2, _ = synthetic_grids(12)
+    loop.start(t(g4), t(g2), t(pr), t(f4), t(f2))
+    loop.start_slab(t(np.stack([slab_start_outvec(r) for r in sids]) if sids else np.zeros((0, 4))))
+    loop.sync()
+    loop._keep = (slab, so)
+    return loop, sids
+
+
+def _slab_snap(loop):
+    s = _snap(loop)
+    st = loop.slab_state()
+    s["sst"], s["sov"] = st["sst"], st["outvec"]
+    return s
+
+
+@pytest.fixture(scope="module")
+def one_rank_slab(cuda):
+    """The one-rank slab + pipelined loop over all 1152 full-size regions, SLAB_STEPS steps."""
+    mask = _slab_mask()
+    loop, sids = _slab_setup(cuda, np.arange(NREG), mask, None)
+    snaps, runs = [], []
+    for _ in range(SLAB_STEPS):
+        loop.step()
+        loop.sync()
+        snaps.append(_slab_snap(loop))
+        runs.append(loop.run_speedy())
+    offs = loop.res.fb_offsets.copy()
+    _close(loop)
+    loop._keep[0].close()
+    return snaps, runs, offs, sids
+
+
+@pytest.mark.parametrize("world", [8, 7])
+def test_sharded_slab_pipelined_step_is_bitwise_the_one_rank_loop(cuda, one_rank_slab, world):
+    import torch
+
+    from speedy_ml_amd.comm import LocalRank, exchange_plan
+
+    snaps1, runs1, offs1, sids1 = one_rank_slab
+    mask = _slab_mask()
+    maxc, contiguous, perm = exchange_plan(NREG, world)
+    shares = [np.array(domain.processor_decomposition(NREG, world, q)) for q in range(world)]
+    comms = [LocalRank(world, q) for q in range(world)]
+    built = [_slab_setup(cuda, shares[q], mask, comms[q]) for q in range(world)]
+    loops = [b[0] for b in built]
+    if world == 8:
+        assert built[1][1] == [], "rank 1 of 8 must own no sst region"
+    recv = torch.zeros((world * maxc, 140), dtype=torch.float64, device=cuda)
+    slab_step_seen = False
+    for step in range(SLAB_STEPS):
+        for lp in loops:
+            lp.predict()
+        for lp in loops:
+            lp.main.synchronize()
+        recv.zero_()
+        for q, lp in enumerate(loops):
+            recv[q * maxc:q * maxc + len(shares[q])] = lp.ov  # ncclAllGather's [rank][maxc] slabs
+        torch.cuda.synchronize()
+        for lp in loops:
+            lp.advance_slabs(recv)
+        for lp in loops:
+            lp.sync()
+        want = snaps1[step]
+        slab_step_seen |= ((step + 1) * 6) % SLAB_HOURS == 0
+        for q, lp in enumerate(loops):
+            got = _slab_snap(lp)
+            s = shares[q]
+            tag = f"world {world} rank {q} step {step + 1}"
+            np.testing.assert_array_equal(got["ov"], want["ov"][s], err_msg=tag + " ov (outvec + slab sst)")
+            np.testing.assert_array_equal(got["lm"], want["lm"][s], err_msg=tag + " lm")
+            fb1 = np.concatenate([want["fb"][offs1[r]:offs1[r + 1]] for r in s])
+            np.testing.assert_array_equal(got["fb"], fb1, err_msg=tag + " fb")
+            for k in ("g4", "g2", "pr", "f4", "f2", "sst"):
+                np.testing.assert_array_equal(got[k], want[k], err_msg=f"{tag} {k}")
+            mine = [sids1.index(r) for r in built[q][1]]
+            np.testing.assert_array_equal(got["sov"], want["sov"][mine], err_msg=tag + " slab outvec")
+            assert lp.run_speedy() == runs1[step], tag
+    assert slab_step_seen
+    # the slab step changed the sst the window sees (else the test would not cover it)
+    assert not np.array_equal(snaps1[SLAB_STEPS - 1]["sst"], snaps1[0]["sst"])
+    for lp in loops:
+        _close(lp)
+        lp._keep[0].close()
+    for c in comms:
+        c.close()
