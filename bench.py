@@ -92,6 +92,10 @@ def parse():
     p.add_argument("--pipelined", action=argparse.BooleanOptionalAction, default=True,
                    help="each step also issues the next step's reservoir begin (sml_hybrid_set_pipelined): "
                         "the loop a long run is in, also for the first timed step after the warmup's sync")
+    p.add_argument("--chain", choices=("auto", "two-streams", "speedy"), default="auto",
+                   help="where the step's serial chain (v_p finish, exchange, assembly, tiling) runs "
+                        "(sml_hybrid_set_chain): auto = SPEEDY's stream right behind the window at N > 1 (and in "
+                        "the --sim-ranks diagnostic), the reservoir's stream between two hops at N = 1")
     p.add_argument("--slab", action=argparse.BooleanOptionalAction, default=True,
                    help="the slab ocean in the loop, as the reference runs by default (mod_reservoir.f90:41): a "
                         "slab reservoir per sst region, predict_slab_ml every 168 h (28 steps), its sst in the "
@@ -306,6 +310,11 @@ def main():
                       comm=comm, slab=slab_ocean)
     if args.pipelined:
         loop.set_pipelined(True)
+    from speedy_ml_amd._lib import SML_CHAIN_SPEEDY, SML_CHAIN_TWO_STREAMS
+
+    if args.chain != "auto" or sim > 1:  # (--sim-ranks stands for world > 1, whose default is SPEEDY's stream)
+        loop.set_chain(SML_CHAIN_TWO_STREAMS if args.chain == "two-streams" else SML_CHAIN_SPEEDY)
+    chain_eff = loop.chain()[1]
     # initial inputs from the synthetic analysis state (start_prediction analogue)
     loop.start(t(g4h), t(g2h), t(prh), t(f4h), t(f2h))
     if slab_ocean is not None:
@@ -476,7 +485,10 @@ def main():
                 "loop": ("pipelined: each step issues the next step's reservoir begin beside its window, so the "
                          "timed steps run begins 2..K+1 and windows 1..K -- K of each, none skipped"
                          if args.pipelined and args.overlap else "each step issues its own begin"),
-                "streams": (f"overlapped: SPEEDY on CUs [0, {args.speedy_cus}), reservoir on CUs [{args.speedy_cus}, "
+                "chain": ("the step's serial chain (v_p finish, exchange, assembly, tiling) on SPEEDY's stream behind "
+                      "the window" if chain_eff == SML_CHAIN_SPEEDY else
+                      "the step's serial chain on the reservoir's stream, two cross-stream hops per step"),
+            "streams": (f"overlapped: SPEEDY on CUs [0, {args.speedy_cus}), reservoir on CUs [{args.speedy_cus}, "
                             f"{args.speedy_cus + (ncu - args.speedy_cus)})"
                             if args.overlap and args.speedy_cus > 0 else
                             "overlapped, no CU split" if args.overlap else "one stream"),

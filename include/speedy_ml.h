@@ -597,6 +597,21 @@ int sml_hybrid_set_pipelined(sml_hybrid *h, int on);
  * instead of the identity exchange fused into the finish.  Same results, bitwise;
  * for exercising the transport on one GPU.  Refused without a transport. */
 int sml_hybrid_set_force_exchange(sml_hybrid *h, int on);
+/* where a step's serial chain runs -- the v_p finish with the local-model tiling, the
+ * exchange, the assembly and the re-tiling: SML_CHAIN_TWO_STREAMS on the reservoir's
+ * (main) stream, between a hop from SPEEDY's stream (the forecast) and one back (the
+ * assembled grid); SML_CHAIN_SPEEDY on SPEEDY's stream right behind the window, so no
+ * hop sits on the critical path (the main stream keeps only the reservoir begin, which
+ * waits for the feedback and signals the finish); SML_CHAIN_AUTO (default) takes
+ * SPEEDY's stream at world > 1.  Bitwise the same results.  Drains both streams. */
+#define SML_CHAIN_AUTO 0
+#define SML_CHAIN_TWO_STREAMS 1
+#define SML_CHAIN_SPEEDY 2
+int sml_hybrid_set_chain(sml_hybrid *h, int mode);
+int sml_hybrid_chain(const sml_hybrid *h, int *requested, int *effective);
+/* the stream the local outvecs are ready on after sml_hybrid_predict: a host-driven
+ * exchange runs there before sml_hybrid_advance */
+int sml_hybrid_exchange_stream(const sml_hybrid *h, void **stream);
 /* the number of ncclAllGather calls sml_hybrid_step has issued on this loop */
 int sml_hybrid_exchanges(const sml_hybrid *h, int64_t *allgathers);
 /* run_speedy of the last step (0: the reference ends the prediction,

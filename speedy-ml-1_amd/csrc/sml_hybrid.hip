@@ -60,9 +60,17 @@ struct sml_hybrid {
     // blocks its queue until the producer's write lands, so under serialised dispatch
     // (rocprofv3 counter passes, AMD_SERIALIZE_KERNEL) it can stall ahead of that
     // producer: SML_HOP_AUTO then takes event hops (sml_hybrid_set_hop_mode).
-    enum { kHopGrid = 0, kHopLm = 1 };
-    hipEvent_t ev[2] = {nullptr, nullptr};
-    uint64_t *d_seq = nullptr, seq[2] = {0, 0};
+    // (the chain on SPEEDY's stream, SML_CHAIN_SPEEDY, uses two others instead: fb_t,
+    // side -> main, before the next begin; begun_t, main -> side, before the finish)
+    enum { kHopGrid = 0, kHopLm = 1, kHopFb = 2, kHopBegun = 3, kHops = 4 };
+    hipEvent_t ev[kHops] = {nullptr, nullptr, nullptr, nullptr};
+    uint64_t *d_seq = nullptr, seq[kHops] = {0, 0, 0, 0};
+    // where the step's serial chain runs (sml_hybrid_set_chain): false, the two-stream
+    // schedule above (the finish, exchange, assembly and tiling on the main stream,
+    // two hops around every window); true, all of it on SPEEDY's stream right after the
+    // window, the main stream keeping only the reservoir begin (and the slab predict)
+    int chain_mode = SML_CHAIN_AUTO;
+    bool chain = false;
     bool use_events = false;
     int hop_mode = SML_HOP_AUTO;
     // caller-owned device buffers
@@ -458,6 +466,40 @@ extern "C" int sml_hybrid_set_pipelined(sml_hybrid *h, int on) {
     return SML_OK;
 }
 
+// the step's serial chain (finish -> exchange -> assembly -> tiling): on the main
+// stream between two cross-stream hops (SML_CHAIN_TWO_STREAMS), or on SPEEDY's stream
+// right after the window (SML_CHAIN_SPEEDY); SML_CHAIN_AUTO takes SPEEDY's stream when
+// the rank holds a share of a world > 1 decomposition (its begin is short enough to
+// finish beside the window; at world 1 the begin is as long as the window and the
+// finish belongs on the reservoir's 192 CUs).  Drains both streams first.
+extern "C" int sml_hybrid_set_chain(sml_hybrid *h, int mode) {
+    SML_REQUIRE(h && (mode == SML_CHAIN_AUTO || mode == SML_CHAIN_TWO_STREAMS || mode == SML_CHAIN_SPEEDY),
+                "bad chain mode %d", mode);
+    SML_REQUIRE(!h->predicted, "sml_hybrid_set_chain between predict and advance");
+    if (h->main) SML_HIP(hipStreamSynchronize(h->main));
+    if (h->side && h->side != h->main) SML_HIP(hipStreamSynchronize(h->side));
+    h->chain_mode = mode;
+    const int world = h->comm ? h->comm->world : 1;
+    const bool want = mode == SML_CHAIN_SPEEDY || (mode == SML_CHAIN_AUTO && world > 1);
+    h->chain = want && h->overlap && h->side != h->main;
+    return SML_OK;
+}
+
+extern "C" int sml_hybrid_chain(const sml_hybrid *h, int *requested, int *effective) {
+    SML_REQUIRE(h, "null context");
+    if (requested) *requested = h->chain_mode;
+    if (effective) *effective = h->chain ? SML_CHAIN_SPEEDY : SML_CHAIN_TWO_STREAMS;
+    return SML_OK;
+}
+
+// the stream the local outvecs are ready on after sml_hybrid_predict, and on which a
+// host-driven exchange should run before sml_hybrid_advance
+extern "C" int sml_hybrid_exchange_stream(const sml_hybrid *h, void **stream) {
+    SML_REQUIRE(h && stream, "null argument");
+    *stream = h->chain ? h->side : h->main;
+    return SML_OK;
+}
+
 extern "C" int sml_hybrid_set_force_exchange(sml_hybrid *h, int on) {
     SML_REQUIRE(h, "null context");
     if (on && !h->force_exchange) {
@@ -573,12 +615,11 @@ extern "C" int sml_hybrid_create(sml_reservoirs *res, sml_dynamics *dyn, sml_com
         }
     }
     if (const char *e = std::getenv("SML_HYBRID_ASM")) h->fuse_asm = *e != '0';
-    if (hipEventCreateWithFlags(&h->ev[0], hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&h->ev[1], hipEventDisableTiming) != hipSuccess)
-        return bail(fail(SML_ERR_HIP, "event"));
+    for (hipEvent_t &e : h->ev)
+        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return bail(fail(SML_ERR_HIP, "event"));
     if (int rc = sml_hybrid_set_hop_mode(h, SML_HOP_AUTO)) return bail(rc);
-    if (hipMalloc(&h->d_seq, 2 * sizeof(uint64_t)) != hipSuccess ||
-        hipMemset(h->d_seq, 0, 2 * sizeof(uint64_t)) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
+    if (hipMalloc(&h->d_seq, sml_hybrid::kHops * sizeof(uint64_t)) != hipSuccess ||
+        hipMemset(h->d_seq, 0, sml_hybrid::kHops * sizeof(uint64_t)) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
         return bail(fail(SML_ERR_HIP, "sequence counters"));
     h->xw = h->nout;
     if (world > 1) {
@@ -592,6 +633,7 @@ extern "C" int sml_hybrid_create(sml_reservoirs *res, sml_dynamics *dyn, sml_com
             return bail(fail(SML_ERR_NOMEM, "exchange buffers"));
         if (int rc = alloc_exchange(h)) return bail(rc);
     }
+    if (int rc = sml_hybrid_set_chain(h, SML_CHAIN_AUTO)) return bail(rc);
     *out = h;
     return SML_OK;
 }
@@ -683,6 +725,8 @@ extern "C" int sml_hybrid_start(sml_hybrid *h, const double *d_g4, const double 
     if (int rc = sml_res_tile_inputs(h->res, h->g4, h->g2, h->pr, h->f4, h->f2, h->tisr, h->fb, h->lm, h->main))
         return rc;
     if (int rc = hop_signal(h, sml_hybrid::kHopLm, h->main)) return rc;
+    if (int rc = hop_signal(h, sml_hybrid::kHopFb, h->main)) return rc;
+    SML_HIP(hipStreamSynchronize(h->main));  // (the chain on SPEEDY's stream reads these on the other stream)
     h->started = true;
     h->predicted = h->advanced = false;
     return SML_OK;
@@ -721,10 +765,9 @@ int slab_predict(sml_hybrid *h) {
 // sendrecievegrid's sst half (mpires.f90:288-319, 458-472, 575-581, 733-736) after a
 // change of any region's slab sst: wholegrid_sst from the exchange rows, the atmo
 // feedback's sst entries, and run_model's sst_hybrid into the window (cpl_sea.f90:38-46)
-int slab_sst(sml_hybrid *h, const double *d_all) {
+int slab_sst(sml_hybrid *h, const double *d_all, hipStream_t m) {
     sml_hybrid::Slab &sl = h->slab;
     if (!sl.res || !sl.dirty) return SML_OK;
-    hipStream_t m = h->main;
     hipLaunchKernelGGL(k_sst_grid, dim3((kGrid2d + 255) / 256), dim3(256), 0, m, d_all, sl.d_sst_src, sl.base, sl.mask,
                        sl.d_sst);
     SML_HIP(hipGetLastError());
@@ -917,20 +960,29 @@ int predict_impl(sml_hybrid *h, bool assemble) {
         int begun = 0;
         if (h->begun_next)
             if (int rc = sml_res_step_begun(h->res, &begun)) return rc;
-        if (!begun)
+        if (!begun) {
+            // (chain on SPEEDY's stream: the feedback was tiled there)
+            if (h->chain)
+                if (int rc = hop_wait(h, sml_hybrid::kHopFb, h->main)) return rc;
             if (int rc = sml_res_step_begin(h->res, h->fb, h->main)) return rc;
+        }
         h->begun_next = false;
         if (int rc = slab_predict(h)) return rc;
-        // SPEEDY's forecast of the previous window
-        if (int rc = hop_wait(h, sml_hybrid::kHopLm, h->main)) return rc;
+        hipStream_t xs = h->main;
+        if (h->chain) {  // the finish follows the window on SPEEDY's stream, once the begin is done
+            xs = h->side;
+            if (int rc = hop_signal(h, sml_hybrid::kHopBegun, h->main)) return rc;
+            if (int rc = hop_wait(h, sml_hybrid::kHopBegun, xs)) return rc;
+        } else if (int rc = hop_wait(h, sml_hybrid::kHopLm, h->main)) {  // SPEEDY's forecast of the previous window
+            return rc;
+        }
         // the local-model tiling fused into the v_p finish: one launch fewer on the
         // critical path; on one rank the assembly too (one more)
         if (assemble) {
-            if (int rc = sml_res_step_finish_assemble(h->res, h->f4, h->f2, h->lm, h->ov, h->g4, h->g2, h->pr,
-                                                      h->main))
+            if (int rc = sml_res_step_finish_assemble(h->res, h->f4, h->f2, h->lm, h->ov, h->g4, h->g2, h->pr, xs))
                 return rc;
             h->assembled = true;
-        } else if (int rc = sml_res_step_finish_grid(h->res, h->f4, h->f2, h->lm, h->ov, h->main)) {
+        } else if (int rc = sml_res_step_finish_grid(h->res, h->f4, h->f2, h->lm, h->ov, xs)) {
             return rc;
         }
     } else {  // one pass over W_out: the same sums as begin + finish
@@ -950,16 +1002,20 @@ extern "C" int sml_hybrid_advance(sml_hybrid *h, const double *d_outvec_all) {
     SML_REQUIRE(h && d_outvec_all, "null argument");
     if (!h->predicted) return fail(SML_ERR_STATE, "sml_hybrid_advance without sml_hybrid_predict");
     hipStream_t m = h->main, s = h->side;
+    // the serial chain's stream: the main stream (two hops around the window), or
+    // SPEEDY's, right behind the window (sml_hybrid_set_chain)
+    hipStream_t c = h->chain ? s : m;
+    const bool hops = h->overlap && !h->chain;
     // (sml_hybrid_step on one rank: its predict assembled these very outvecs already)
     const bool done = h->assembled && d_outvec_all == h->ov;
     h->assembled = false;
     if (!done)
-        if (int rc = sml_exchange_assemble(h->res, d_outvec_all, h->g4, h->g2, h->pr, m)) return rc;
-    if (int rc = slab_sst(h, d_outvec_all)) return rc;
-    if (h->overlap)
+        if (int rc = sml_exchange_assemble(h->res, d_outvec_all, h->g4, h->g2, h->pr, c)) return rc;
+    if (int rc = slab_sst(h, d_outvec_all, c)) return rc;
+    if (hops)
         if (int rc = hop_signal(h, sml_hybrid::kHopGrid, m)) return rc;
     ++h->t;
-    if (int rc = sml_res_tile_feedback(h->res, h->g4, h->g2, h->pr, h->tisr_table ? nullptr : h->tisr, h->fb, m))
+    if (int rc = sml_res_tile_feedback(h->res, h->g4, h->g2, h->pr, h->tisr_table ? nullptr : h->tisr, h->fb, c))
         return rc;
     if (h->tisr_table) {  // get_tisr_by_date(..., timestep - 1, ...) for the next feedback (mpires.f90:726-728)
         int idx = 0;
@@ -968,29 +1024,33 @@ extern "C" int sml_hybrid_advance(sml_hybrid *h, const double *d_outvec_all) {
             return rc;
         if (idx < 1 || idx > h->tisr_nhours)
             return fail(SML_ERR_ARG, "tisr hour %d outside the table's %d hours", idx, h->tisr_nhours);
-        if (int rc = sml_res_tile_tisr_field(h->res, h->tisr_table + (size_t)(idx - 1) * kGrid2d, h->fb, m))
+        if (int rc = sml_res_tile_tisr_field(h->res, h->tisr_table + (size_t)(idx - 1) * kGrid2d, h->fb, c))
             return rc;
     }
     if (h->slab.res && h->slab.tot_fb) {  // averaged_atmo_input_vec(:, mod(t-1, R-1)+1), mpires.f90:755
         sml_hybrid::Slab &sl = h->slab;
         double *col = sl.d_ring + (size_t)((h->t - 1) % (sl.ratio - 1)) * sl.tot_fb;
-        hipLaunchKernelGGL(k_slab_ring, dim3((sl.tot_fb + 255) / 256), dim3(256), 0, m, h->fb, sl.d_ring_src, sl.tot_fb,
+        hipLaunchKernelGGL(k_slab_ring, dim3((sl.tot_fb + 255) / 256), dim3(256), 0, c, h->fb, sl.d_ring_src, sl.tot_fb,
                            col);
         SML_HIP(hipGetLastError());
     }
-    if (h->overlap)
+    if (h->chain)  // the next begin (main stream) reads this feedback
+        if (int rc = hop_signal(h, sml_hybrid::kHopFb, c)) return rc;
+    if (hops)
         if (int rc = hop_wait(h, sml_hybrid::kHopGrid, s)) return rc;
     if (int rc = sml_dyn_run_model(h->dyn, h->g4, h->g2, h->nleap, h->delt, h->alph, h->rob, h->wil, h->f4, h->f2, s))
         return rc;
-    if (h->overlap) {
+    if (hops) {
         if (int rc = hop_signal(h, sml_hybrid::kHopLm, s)) return rc;
-    } else if (h->ncs) {
+    } else if (!h->overlap && h->ncs) {
         if (int rc = sml_res_tile_local_model(h->res, h->f4, h->f2, h->lm, s)) return rc;
     }
     // pipelined: the next step's begin from the feedback just tiled, on the main stream,
     // beside this window (it would be the next predict's first launch anyway)
     if (h->pipelined && h->overlap) {
-        if (int rc = sml_res_step_begin(h->res, h->fb, h->main)) return rc;
+        if (h->chain)
+            if (int rc = hop_wait(h, sml_hybrid::kHopFb, m)) return rc;
+        if (int rc = sml_res_step_begin(h->res, h->fb, m)) return rc;
         h->begun_next = true;
     }
     h->predicted = false;
@@ -1007,8 +1067,8 @@ extern "C" int sml_hybrid_advance_slabs(sml_hybrid *h, const double *d_recv) {
     if (world == 1 || h->contiguous) return sml_hybrid_advance(h, d_recv);  // slabs in region order
     if (!h->predicted) return fail(SML_ERR_STATE, "sml_hybrid_advance_slabs without sml_hybrid_predict");
     const int total = h->numregions * h->xw;
-    hipLaunchKernelGGL(k_gather_rows, dim3((total + 255) / 256), dim3(256), 0, h->main, d_recv, h->d_perm, h->d_glob,
-                       h->xw, total);
+    hipLaunchKernelGGL(k_gather_rows, dim3((total + 255) / 256), dim3(256), 0, h->chain ? h->side : h->main, d_recv,
+                       h->d_perm, h->d_glob, h->xw, total);
     SML_HIP(hipGetLastError());
     return sml_hybrid_advance(h, h->d_glob);
 }
@@ -1035,12 +1095,13 @@ extern "C" int sml_hybrid_step(sml_hybrid *h) {
     // even shares (1152 / N for N = 1, 2, 4, 8): the outvecs go out of ov as they are;
     // uneven ones are padded to the largest share through d_send (one copy more on the
     // critical path; d_send's padding rows stay zero)
+    hipStream_t xs = h->chain ? h->side : h->main;
     const double *send = h->ov;
     if (h->nlocal != h->maxc) {
-        SML_HIP(hipMemcpyAsync(h->d_send, h->ov, (size_t)h->nlocal * h->xw * 8, hipMemcpyDeviceToDevice, h->main));
+        SML_HIP(hipMemcpyAsync(h->d_send, h->ov, (size_t)h->nlocal * h->xw * 8, hipMemcpyDeviceToDevice, xs));
         send = h->d_send;
     }
-    if (int rc = sml_comm_allgather(h->comm, send, h->d_recv, (int64_t)h->maxc * h->xw, h->main)) return rc;
+    if (int rc = sml_comm_allgather(h->comm, send, h->d_recv, (int64_t)h->maxc * h->xw, xs)) return rc;
     ++h->allgathers;
     return sml_hybrid_advance_slabs(h, h->d_recv);
 }
@@ -1067,8 +1128,12 @@ extern "C" int sml_hybrid_run_speedy(sml_hybrid *h, int *run) {
 extern "C" int sml_hybrid_sync(sml_hybrid *h) {
     SML_REQUIRE(h, "null context");
     if (h->overlap && h->advanced && h->ncs) {
-        if (int rc = hop_wait(h, sml_hybrid::kHopLm, h->main)) return rc;
-        if (int rc = sml_res_tile_local_model(h->res, h->f4, h->f2, h->lm, h->main)) return rc;
+        if (h->chain) {
+            if (int rc = sml_res_tile_local_model(h->res, h->f4, h->f2, h->lm, h->side)) return rc;
+        } else {
+            if (int rc = hop_wait(h, sml_hybrid::kHopLm, h->main)) return rc;
+            if (int rc = sml_res_tile_local_model(h->res, h->f4, h->f2, h->lm, h->main)) return rc;
+        }
     }
     SML_HIP(hipStreamSynchronize(h->main));
     SML_HIP(hipStreamSynchronize(h->side));

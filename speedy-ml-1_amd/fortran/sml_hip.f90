@@ -497,6 +497,25 @@ module sml_hip
       integer(c_int), value :: on
       integer(c_int) :: rc
     end function
+    !> the step's serial chain: 0 auto, 1 the two-stream schedule, 2 on SPEEDY's stream
+    function sml_hybrid_set_chain(h, mode) bind(C, name='sml_hybrid_set_chain') result(rc)
+      import :: c_ptr, c_int
+      type(c_ptr), value :: h
+      integer(c_int), value :: mode
+      integer(c_int) :: rc
+    end function
+    function sml_hybrid_chain(h, requested, effective) bind(C, name='sml_hybrid_chain') result(rc)
+      import :: c_ptr, c_int
+      type(c_ptr), value :: h
+      integer(c_int), intent(out) :: requested, effective
+      integer(c_int) :: rc
+    end function
+    function sml_hybrid_exchange_stream(h, stream) bind(C, name='sml_hybrid_exchange_stream') result(rc)
+      import :: c_ptr, c_int
+      type(c_ptr), value :: h
+      type(c_ptr), intent(out) :: stream
+      integer(c_int) :: rc
+    end function
     function sml_hybrid_exchanges(h, allgathers) bind(C, name='sml_hybrid_exchanges') result(rc)
       import :: c_ptr, c_int, c_int64_t
       type(c_ptr), value :: h

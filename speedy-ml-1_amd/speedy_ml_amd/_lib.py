@@ -57,10 +57,11 @@ EXPORTED = (
     "sml_res_mean_std", "sml_res_set_outvec_ld", "sml_hybrid_set_slab", "sml_hybrid_start_slab",
     "sml_hybrid_exchange_width", "sml_hybrid_slab_buffers", "sml_dyn_set_hybrid_sst", "sml_dyn_set_sea_ice",
     "sml_hybrid_set_pipelined", "sml_res_step_cancel", "sml_res_step_begun", "sml_hybrid_set_force_exchange",
-    "sml_hybrid_exchanges",
+    "sml_hybrid_exchanges", "sml_hybrid_set_chain", "sml_hybrid_chain", "sml_hybrid_exchange_stream",
 )
 
 SML_HOP_AUTO, SML_HOP_WAIT_VALUE, SML_HOP_EVENTS = 0, 1, 2
+SML_CHAIN_AUTO, SML_CHAIN_TWO_STREAMS, SML_CHAIN_SPEEDY = 0, 1, 2
 
 
 class SmlError(RuntimeError):
@@ -233,6 +234,9 @@ def _declare(L: ctypes.CDLL) -> None:
         "sml_res_step_begun": [vp, ip],
         "sml_hybrid_set_force_exchange": [vp, i],
         "sml_hybrid_exchanges": [vp, i64p],
+        "sml_hybrid_set_chain": [vp, i],
+        "sml_hybrid_chain": [vp, ip, ip],
+        "sml_hybrid_exchange_stream": [vp, pp],
     }
     for name, args in sig.items():
         fn = getattr(L, name)

@@ -77,6 +77,25 @@ class HybridLoop:
         check(lib().sml_hybrid_streams(h, ctypes.byref(m), ctypes.byref(s)))
         self.main = torch.cuda.ExternalStream(m.value, device=self.dev)
         self.side = torch.cuda.ExternalStream(s.value, device=self.dev) if s.value != m.value else self.main
+        self._set_xstream()
+
+    def _set_xstream(self):
+        """The stream the local outvecs are ready on after predict (sml_hybrid_exchange_stream)."""
+        x = ctypes.c_void_p()
+        check(lib().sml_hybrid_exchange_stream(self._h, ctypes.byref(x)))
+        self.xstream = self.side if x.value == self.side.cuda_stream else self.main
+
+    def set_chain(self, mode: int):
+        """SML_CHAIN_AUTO / SML_CHAIN_TWO_STREAMS / SML_CHAIN_SPEEDY (include/speedy_ml.h):
+        where the finish -> exchange -> assembly -> tiling chain runs."""
+        check(lib().sml_hybrid_set_chain(self._h, int(mode)))
+        self._set_xstream()
+
+    def chain(self):
+        """(requested, effective) chain mode."""
+        a, b = ctypes.c_int(), ctypes.c_int()
+        check(lib().sml_hybrid_chain(self._h, ctypes.byref(a), ctypes.byref(b)))
+        return a.value, b.value
 
     def close(self):
         """Wait for the loop's work and release its streams."""
@@ -122,7 +141,7 @@ class HybridLoop:
             check(lib().sml_hybrid_step(self._h))
             return
         check(lib().sml_hybrid_predict(self._h))
-        with torch.cuda.stream(self.main):
+        with torch.cuda.stream(self.xstream):
             glob = self.exchange(self.ov)  # RCCL all-gather over xGMI when world > 1
         check(lib().sml_hybrid_advance(self._h, ptr(glob)))
 
@@ -152,7 +171,7 @@ class HybridLoop:
         return out
 
     def predict(self):
-        """First half of a step: this rank's outvecs into `ov` (main stream)."""
+        """First half of a step: this rank's outvecs into `ov` (on `xstream`)."""
         check(lib().sml_hybrid_predict(self._h))
 
     def advance_slabs(self, recv):

@@ -111,7 +111,7 @@ def test_every_rank_of_the_sharded_step_is_bitwise_the_one_rank_loop(cuda, one_r
         for lp in loops:
             lp.predict()
         for lp in loops:
-            lp.main.synchronize()
+            lp.xstream.synchronize()
         recv.zero_()  # the padding rows of a short share
         for q, lp in enumerate(loops):
             recv[q * maxc:q * maxc + len(shares[q])] = lp.ov  # ncclAllGather's [rank][maxc] slabs
@@ -267,7 +267,7 @@ def test_sharded_slab_pipelined_step_is_bitwise_the_one_rank_loop(cuda, one_rank
         for lp in loops:
             lp.predict()
         for lp in loops:
-            lp.main.synchronize()
+            lp.xstream.synchronize()
         recv.zero_()
         for q, lp in enumerate(loops):
             recv[q * maxc:q * maxc + len(shares[q])] = lp.ov  # ncclAllGather's [rank][maxc] slabs
