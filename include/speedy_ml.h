@@ -206,6 +206,13 @@ int sml_res_step_finish_assemble(sml_reservoirs *c, const double *d_fc4d, const 
  * both share CUs; on CUs of their own (sml_stream_create_cu_range) it is not needed.
  * The environment variable SML_READ_WAVES, when set, takes precedence. */
 int sml_res_set_read_waves(sml_reservoirs *c, int waves);
+/* the number of CUs the context's launches get (its stream's CU mask; 0 = the whole
+ * device): the balanced state update runs one block per CU over equal shares of all
+ * local rows.  sml_res_update_balanced: 1 when the update takes that form (every
+ * region's A / W_in in ELL form, n <= 7168, ninp <= 1024), 0 for the per-region form;
+ * both give bit-identical states. */
+int sml_res_set_update_cus(sml_reservoirs *c, int cus);
+int sml_res_update_balanced(sml_reservoirs *c, int *balanced);
 /* the form of sml_res_step_begin (predict's update + the v_ml half of the readout,
  * src/mod_reservoir.f90:1440-1455): 0 = the update grid, then the readout grid;
  * 1 = one launch, a block per region that updates its state and then streams its

@@ -106,6 +106,7 @@ struct sml_hybrid {
     // the exchange row: the outvec (nout), + the slab ocean's sst of the region's
     // resolved points when the slab is on (as sendrecievegrid sends them, mpires.f90:358-383)
     int xw = 0;
+    int res_cus = 0;  // the CUs of the main stream's mask (0: no mask)
     // slab ocean (parallelmain.f90:216-249; mpires.f90:288-478, 575-767; cpl_sea.f90:38-46)
     struct Slab {
         sml_reservoirs *res = nullptr;  // the slab reservoirs of this rank's sst regions (generic, ML-only)
@@ -602,6 +603,8 @@ extern "C" int sml_hybrid_create(sml_reservoirs *res, sml_dynamics *dyn, sml_com
                                : sml_dyn_set_check_cus(dyn, speedy_cus, res_cus))
             return bail(rc);
         if (int rc = sml_res_set_read_waves(res, 0)) return bail(rc);  // pacing pays only on shared CUs
+        if (int rc = sml_res_set_update_cus(res, res_cus)) return bail(rc);  // one balanced-update block per CU
+        h->res_cus = res_cus;
     } else {
         if (hipStreamCreateWithFlags(&h->main, hipStreamNonBlocking) != hipSuccess)
             return bail(fail(SML_ERR_HIP, "stream"));
@@ -881,6 +884,8 @@ extern "C" int sml_hybrid_set_slab(sml_hybrid *h, sml_reservoirs *slab, const do
     SML_HIP(hipMemset(sl.d_sst, 0, (size_t)kGrid2d * 8));
     h->xw = xw;
     if (int rc = sml_res_set_outvec_ld(h->res, xw)) return rc;
+    if (h->res_cus > 0)  // the slab step runs on the main stream too
+        if (int rc = sml_res_set_update_cus(slab, h->res_cus)) return rc;
     if (h->comm && (h->comm->world > 1 || h->force_exchange))
         if (int rc = alloc_exchange(h)) return rc;
     sl.res = slab;

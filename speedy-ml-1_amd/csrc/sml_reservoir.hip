@@ -117,6 +117,15 @@ struct sml_reservoirs {
     // overrides begin_mode when >= 0), never on the enqueue path of a step
     int upd_parts = 0, begin_env = -1;
     bool upd_occ2 = false;
+    // the balanced update (k_res_update_bal; SML_UPD_BAL=0 at create: k_res_update):
+    // row0 [nlocal+1] = the regions' rows concatenated; blk_r0 [grid] = the region each
+    // block's share starts in, for the grid it was built for (upd_grid: the CUs the
+    // launches get, sml_res_set_update_cus; 0 = every CU of the device)
+    bool upd_bal = true;
+    int upd_cus = 0, bal_grid = 0, ncu = 0;
+    int ell_ok = -1;  // every local region's A and W_in in ELL form (-1: recount after a load)
+    int32_t *d_row0 = nullptr, *d_blk_r0 = nullptr;
+    std::vector<int32_t> row0_h;
     bool begun = false;             // sml_res_step_begin issued, finish pending
     int8_t *d_outl = nullptr;
     int32_t *d_asm_dst = nullptr;   // [numregions*nout] -> concatenated grid index
@@ -310,6 +319,126 @@ __global__ __launch_bounds__(kUpdThreads, kMinW) void k_res_update(
             update_block<WT, kLds>(lb, smem, R, a_rp, a_col, a_val, w_rp, w_col, w_val, ell, x_old, x_new, xaug,
                                    feedback, ncs, leak, parts, lds_x);
         if (base + (int)gridDim.x < nlog) __syncthreads();  // the block's LDS, reused next round
+    }
+}
+
+// ---------------------------------------------------------------- balanced update
+// k_res_update_bal: the same rows, the same arithmetic (bitwise k_res_update's ELL
+// path), laid out for HBM instead of per region.  k_res_update runs a block per
+// (region, part): at 1152 regions on 256 CUs (one 1024-thread block per CU: 71 VGPRs)
+// that is 4.5 rounds of blocks -- the fifth a half-empty tail -- each block staging
+// its region's x in LDS behind a barrier and then keeping one pass of A rows in
+// flight (55 KB per CU: ~0.5 of 8 TB/s at the loaded latency).
+// Here a persistent grid of one block per CU takes a contiguous, equal share of all
+// the rank's rows (the regions concatenated; r0 of each block from a host table), so
+// no block waits on a tail; a pass never straddles regions (a share is a run of
+// segments, one per region it touches); the A / W_in rows of the next TWO passes are
+// in flight while a pass computes (~110 KB per CU), whatever segment they belong to;
+// and the next segment's x / feedback are loaded while the current segment's last
+// pass computes and stored into the second of two LDS buffers, so a segment switch
+// costs one barrier, not a memory round trip.  Needs every region in ELL form, n <=
+// kStageX * 1024, ninp <= 1024 and two buffers in LDS; else k_res_update runs.
+constexpr int kStageX = 7;
+
+struct PassDesc {
+    int r, base, end, seg;
+    bool live;
+};
+
+struct StageRegs {
+    double x[kStageX];
+    double f;
+};
+
+template <typename WT>
+__global__ __launch_bounds__(kUpdThreads, 4) void k_res_update_bal(
+    const RegionDev *__restrict__ R, const int32_t *__restrict__ row0, const int32_t *__restrict__ blk_r0, int nlocal,
+    int64_t total, Ell ell, const double *__restrict__ x_old, double *__restrict__ x_new, double *__restrict__ xaug,
+    const double *__restrict__ feedback, int ncs, double leak, int lds_x, int lds_buf) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    const int G = gridDim.x;
+    const int b = xcd_remap(blockIdx.x, G);
+    const int g0 = (int)(total * b / G), g1 = (int)(total * (b + 1) / G);
+    if (g0 >= g1) return;  // block-uniform
+    const int tid = threadIdx.x;
+    auto seg_at = [&](int r, int seg) -> PassDesc {
+        const int a = row0[r], e = row0[r + 1];
+        return PassDesc{r, max(g0, a) - a, min(g1, e) - a, seg, true};
+    };
+    auto succ = [&](const PassDesc &p) -> PassDesc {
+        if (!p.live) return p;
+        if (p.base + kUpdThreads < p.end) return PassDesc{p.r, p.base + kUpdThreads, p.end, p.seg, true};
+        const int r = p.r + 1;
+        if (r >= nlocal || row0[r] >= g1) return PassDesc{r, 0, 0, p.seg + 1, false};
+        return seg_at(r, p.seg + 1);
+    };
+    auto load = [&](RowRegs<WT> &q, const PassDesc &p) {
+        if (!p.live) return;
+        const RegionDev rg = R[p.r];
+        load_row(q, rg, ell, p.base + tid, p.base + tid < p.end);
+    };
+    auto stage_load = [&](StageRegs &sr, int r) {
+        const RegionDev rg = R[r];
+        const double *xo = x_old + rg.x;
+#pragma unroll
+        for (int q = 0; q < kStageX; ++q) {
+            const int j = tid + q * kUpdThreads;
+            if (j < rg.n) sr.x[q] = xo[j];
+        }
+        if (tid < rg.ninp) sr.f = feedback[rg.fb + tid];
+    };
+    auto stage_store = [&](const StageRegs &sr, int r, double *buf) {
+        const RegionDev rg = R[r];
+#pragma unroll
+        for (int q = 0; q < kStageX; ++q) {
+            const int j = tid + q * kUpdThreads;
+            if (j < rg.n) buf[j] = sr.x[q];
+        }
+        if (tid < rg.ninp) buf[lds_x + tid] = sr.f;
+    };
+    PassDesc P0 = seg_at(blk_r0[b], 0);
+    RowRegs<WT> L0, L1, L2;
+    load(L0, P0);
+    PassDesc P1 = succ(P0);
+    load(L1, P1);
+    {
+        StageRegs sr;
+        stage_load(sr, P0.r);
+        stage_store(sr, P0.r, smem);
+    }
+    __syncthreads();
+    PassDesc P2 = succ(P1);
+    while (P0.live) {  // block-uniform
+        load(L2, P2);
+        const bool newseg = P1.live && P1.seg != P0.seg;
+        StageRegs sr;
+        if (newseg) stage_load(sr, P1.r);
+        {  // the pass: update_block's ELL row, expression for expression
+            const RegionDev rg = R[P0.r];
+            const double *xs = smem + (size_t)(P0.seg & 1) * lds_buf, *fs = xs + lds_x;
+            const int i = P0.base + tid;
+            if (i < P0.end) {
+                double y = 0.0;
+#pragma unroll
+                for (int s = 0; s < kEllA; ++s)
+                    if (s < rg.a_w) y = y + (double)L0.v[s] * xs[ell_col(L0.c, s)];
+                double t = 0.0;
+                t = t + (double)L0.wv * fs[L0.wc];
+                const double xn = tanh(y + t);
+                const double xv = (1.0 - leak) * xs[i] + leak * xn;
+                x_new[rg.x + i] = xv;
+                xaug[rg.xaug + ncs + i] = (i & 1) ? xv * xv : xv;  // x_temp(2:n:2)**2 (1-based even)
+            }
+        }
+        if (newseg) {  // the other buffer: its last reader (segment P0.seg - 1) finished before the last barrier
+            stage_store(sr, P1.r, smem + (size_t)(P1.seg & 1) * lds_buf);
+            __syncthreads();
+        }
+        P0 = P1;
+        L0 = L1;
+        P1 = P2;
+        L1 = L2;
+        P2 = succ(P2);
     }
 }
 
@@ -956,6 +1085,7 @@ int load_region_impl(sml_reservoirs *c, int i, const int *rows, const int *cols,
     if (int rc = ell(wrp, wcol, wval, c->w_ell_cap[i], c->d_w_ell_col, c->d_w_ell_val, rgm.w_ell, &rgm.w_w))
         return rc;
     SML_HIP(hipMemcpy(c->d_rd + i, &rgm, sizeof(RegionDev), hipMemcpyHostToDevice));
+    c->ell_ok = -1;
     double ms[2 * kMeanStd];
     std::memcpy(ms, mean, sizeof(double) * kMeanStd);
     std::memcpy(ms + kMeanStd, std, sizeof(double) * kMeanStd);
@@ -982,7 +1112,7 @@ extern "C" int sml_res_destroy(sml_reservoirs *c) {
     void *ptrs[] = {c->d_rd,    c->d_a_rp,    c->d_w_rp,   c->d_a_col,  c->d_w_col,  c->d_a_val,  c->d_w_val,
                     c->d_wout,  c->d_x[0],    c->d_x[1],   c->d_xaug,   c->d_meanstd, c->d_outl,  c->d_asm_dst,
                     c->d_fb_src, c->d_fb_l,   c->d_fb_reg, c->d_lm_src, c->d_lm_l,   c->d_io,     c->d_part,
-                    c->d_wlm,   c->d_tisr_fb, c->d_tisr_grid, c->d_tisr_reg};
+                    c->d_wlm,   c->d_tisr_fb, c->d_tisr_grid, c->d_tisr_reg, c->d_row0, c->d_blk_r0};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     for (hipEvent_t e : c->ev)
@@ -1046,8 +1176,10 @@ int res_create_impl(int numregions, int nlocal, const int *region_ids, const uns
     if (const char *e = std::getenv("SML_UPD_PARTS")) c->upd_parts = std::max(0, std::atoi(e));
     if (const char *e = std::getenv("SML_UPD_OCC")) c->upd_occ2 = *e == '2';
     if (const char *e = std::getenv("SML_BEGIN")) c->begin_env = std::max(0, std::min(2, std::atoi(e)));
+    if (const char *e = std::getenv("SML_UPD_BAL")) c->upd_bal = *e != '0';
     SML_REQUIRE(c->read_waves >= 0, "bad read_waves");
     (void)hipGetDevice(&c->device);
+    (void)hipDeviceGetAttribute(&c->ncu, hipDeviceAttributeMultiprocessorCount, c->device);
     c->region_ids.assign(region_ids, region_ids + nlocal);
     c->sst.assign(sst_flags, sst_flags + nlocal);
     c->n.assign(n, n + nlocal);
@@ -1165,6 +1297,13 @@ int res_create_impl(int numregions, int nlocal, const int *region_ids, const uns
         sml_res_destroy(c);
         return rc;
     }
+    c->row0_h.assign(nlocal + 1, 0);
+    for (int i = 0; i < nlocal; ++i) c->row0_h[i + 1] = c->row0_h[i] + n[i];
+    if ((rc = dalloc(&c->d_row0, nlocal + 1)) ||
+        hipMemcpy(c->d_row0, c->row0_h.data(), (nlocal + 1) * 4, hipMemcpyHostToDevice) != hipSuccess) {
+        sml_res_destroy(c);
+        return rc ? rc : fail(SML_ERR_HIP, "row table");
+    }
     *out = c;
     return SML_OK;
 }
@@ -1247,6 +1386,26 @@ extern "C" int sml_res_get_state(sml_reservoirs *c, int i, double *x) {
     return SML_OK;
 }
 
+namespace {
+bool bal_usable(sml_reservoirs *c);
+}
+
+// the CUs the context's launches get (a CU-masked stream: the hybrid loop's reservoir
+// stream); the balanced update runs one block per CU.  0 = every CU of the device.
+extern "C" int sml_res_set_update_cus(sml_reservoirs *c, int cus) {
+    SML_REQUIRE(c && cus >= 0, "bad argument");
+    c->upd_cus = cus;
+    return SML_OK;
+}
+
+// 1 when sml_res_step / _begin run the balanced update (k_res_update_bal), 0 for the
+// per-region k_res_update (a region in CSR form, n > 7168, ninp > 1024, SML_UPD_BAL=0)
+extern "C" int sml_res_update_balanced(sml_reservoirs *c, int *balanced) {
+    SML_REQUIRE(c && balanced, "null argument");
+    *balanced = bal_usable(c) ? 1 : 0;
+    return SML_OK;
+}
+
 extern "C" int sml_res_set_read_waves(sml_reservoirs *c, int waves) {
     SML_REQUIRE(c && waves >= 0, "bad argument");
     if (!std::getenv("SML_READ_WAVES")) c->read_waves = waves;
@@ -1304,8 +1463,53 @@ extern "C" int sml_res_kernel_times(sml_reservoirs *c, float *update_ms, float *
 
 namespace {
 // x_new = (1 - leak) x + leak tanh(A x + W_in u) for every local region (+ x~, x_aug)
+bool bal_usable(sml_reservoirs *c) {
+    if (!c->upd_bal || c->nlocal == 0) return false;
+    if (c->ell_ok < 0) {
+        c->ell_ok = 1;
+        for (int i = 0; i < c->nlocal; ++i)
+            if (c->rd[i].a_w <= 0 || c->rd[i].w_w <= 0) c->ell_ok = 0;
+    }
+    const size_t lds = 2 * (size_t)((c->maxn + 1) / 2 * 2 + c->maxninp) * sizeof(double);
+    return c->ell_ok == 1 && c->maxn <= kStageX * kUpdThreads && c->maxninp <= kUpdThreads && lds <= 160 * 1024;
+}
+
+int launch_update_bal(sml_reservoirs *c, const double *xo, double *xn, const double *d_feedback, hipStream_t st,
+                      bool paced) {
+    const int64_t total = c->row0_h[c->nlocal];
+    int G = c->upd_cus > 0 ? c->upd_cus : std::max(c->ncu, 1);  // one block per CU the launch gets
+    if (paced && c->upd_blocks > 0) G = std::min(G, c->upd_blocks);
+    G = (int)std::max<int64_t>(1, std::min<int64_t>(G, total));
+    if (G != c->bal_grid) {  // each block's first region, for this grid
+        std::vector<int32_t> r0(G);
+        for (int b = 0; b < G; ++b) {
+            const int64_t g0 = total * b / G;
+            r0[b] = (int32_t)(std::upper_bound(c->row0_h.begin(), c->row0_h.end(), (int32_t)g0) - c->row0_h.begin() - 1);
+        }
+        if (c->d_blk_r0) SML_HIP(hipFree(c->d_blk_r0));
+        c->d_blk_r0 = nullptr;
+        if (int rc = dalloc(&c->d_blk_r0, G)) return rc;
+        SML_HIP(hipMemcpy(c->d_blk_r0, r0.data(), G * 4, hipMemcpyHostToDevice));
+        c->bal_grid = G;
+    }
+    const int lds_x = (c->maxn + 1) / 2 * 2, lds_buf = lds_x + c->maxninp;
+    const size_t lds = 2 * (size_t)lds_buf * sizeof(double);
+    Ell ell{c->d_a_ell_col, c->d_a_ell_val, c->d_w_ell_col, c->d_w_ell_val};
+    if (c->wdtype == SML_F32)
+        hipLaunchKernelGGL(k_res_update_bal<float>, dim3(G), dim3(kUpdThreads), lds, st, c->d_rd, c->d_row0,
+                           c->d_blk_r0, c->nlocal, total, ell, xo, xn, c->d_xaug, d_feedback, c->ncs, c->leakage, lds_x,
+                           lds_buf);
+    else
+        hipLaunchKernelGGL(k_res_update_bal<double>, dim3(G), dim3(kUpdThreads), lds, st, c->d_rd, c->d_row0,
+                           c->d_blk_r0, c->nlocal, total, ell, xo, xn, c->d_xaug, d_feedback, c->ncs, c->leakage, lds_x,
+                           lds_buf);
+    SML_HIP(hipGetLastError());
+    return SML_OK;
+}
+
 int launch_update(sml_reservoirs *c, const double *xo, double *xn, const double *d_feedback, hipStream_t st,
                   bool paced = false) {
+    if (bal_usable(c)) return launch_update_bal(c, xo, xn, d_feedback, st, paced);
     // parts per region: enough blocks to fill the 512 resident 1024-thread block slots
     // (2 per CU with ~54 KB LDS each) once, each part at least one 1024-row pass.  Every
     // part stages the region's whole x, so more parts cost HBM traffic: measured on

@@ -189,6 +189,20 @@ module sml_hip
       integer(c_int) :: rc
     end function
 
+    ! the CUs the context's launches get (one balanced-update block per CU); 0 = all
+    function sml_res_set_update_cus(ctx, cus) bind(C, name='sml_res_set_update_cus') result(rc)
+      import :: c_ptr, c_int
+      type(c_ptr), value :: ctx
+      integer(c_int), value :: cus
+      integer(c_int) :: rc
+    end function
+    function sml_res_update_balanced(ctx, balanced) bind(C, name='sml_res_update_balanced') result(rc)
+      import :: c_ptr, c_int
+      type(c_ptr), value :: ctx
+      integer(c_int), intent(out) :: balanced
+      integer(c_int) :: rc
+    end function
+
     function sml_res_set_read_waves(ctx, waves) bind(C, name='sml_res_set_read_waves') result(rc)
       import :: c_ptr, c_int
       type(c_ptr), value :: ctx

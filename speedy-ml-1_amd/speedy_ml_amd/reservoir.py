@@ -136,6 +136,16 @@ class Reservoirs:
         """Cap on the v_ml readout's waves in predict_begin (0 = uncapped)."""
         check(lib().sml_res_set_read_waves(self._h, int(waves)))
 
+    def set_update_cus(self, cus: int):
+        """The CUs this context's launches get (sml_res_set_update_cus; 0 = the device)."""
+        check(lib().sml_res_set_update_cus(self._h, int(cus)))
+
+    def update_balanced(self) -> bool:
+        """Whether the state update runs as k_res_update_bal (sml_res_update_balanced)."""
+        b = ctypes.c_int()
+        check(lib().sml_res_update_balanced(self._h, ctypes.byref(b)))
+        return bool(b.value)
+
     def set_begin_mode(self, mode: int):
         """predict_begin's form: 0 update grid + readout grid, 1 / 2 one fused launch
         (sml_res_set_begin_mode); bit-identical results."""

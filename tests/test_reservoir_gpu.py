@@ -495,3 +495,55 @@ def test_finish_assemble_is_bitwise_finish_then_assemble(cuda):
     with pytest.raises(SmlError, match="every region"):
         part.predict_finish_assemble(None, None, None, None, None, None, None)
     part.close()
+
+
+@pytest.mark.parametrize("cus", [0, 192, 7, 1])
+def test_balanced_update_is_bitwise_the_per_region_update(cuda, cus):
+    """k_res_update_bal (a persistent grid, one block per CU, each block an equal share
+    of all the rank's rows, two passes of A rows in flight, the next region's x staged
+    into a second LDS buffer) against k_res_update (a block per region; SML_UPD_BAL=0
+    at create): the states, x_aug-fed outvecs and the begin / finish split bitwise over
+    3 steps, for grids of every CU (0), the hybrid loop's reservoir CUs (192), an odd
+    grid (7: shares straddle many regions) and one block (every region in turn)."""
+    import os
+
+    import torch
+
+    from speedy_ml_amd.reservoir import Reservoirs
+
+    mask = domain.load_sst_mask()
+    regions = list(range(0, 1152, 9))  # 128 regions of every shape class, full size
+    ws = [region_weights(r, bool(mask[r])) for r in regions]
+    fb = np.concatenate([feedback_vector(r, w.ninp) for r, w in zip(regions, ws)])
+    lm = np.stack([local_model_vector(r) for r in regions])
+    outs, states = {}, {}
+    for bal in (False, True):
+        if not bal:
+            os.environ["SML_UPD_BAL"] = "0"
+        try:
+            res = Reservoirs(regions, mask[regions], [w.n for w in ws], [w.k for w in ws])
+        finally:
+            os.environ.pop("SML_UPD_BAL", None)
+        for i, w in enumerate(ws):
+            res.load_region_weights(i, w)
+            res.set_state(i, initial_state(regions[i], w.n))
+        res.set_update_cus(cus)
+        assert res.update_balanced() == bal
+        dfb, dlm = torch.from_numpy(fb).to(cuda), torch.from_numpy(lm).to(cuda)
+        ov = torch.zeros((len(regions), 136), dtype=torch.float64, device=cuda)
+        got = []
+        for step in range(3):
+            if step == 1:  # the split form: begin (the update + v_ml) then finish
+                res.predict_begin(dfb)
+                res.predict_finish(dlm, ov)
+            else:
+                res.predict(dfb, dlm, ov)
+            torch.cuda.synchronize()
+            got.append(ov.cpu().numpy().copy())
+        outs[bal] = got
+        states[bal] = [res.get_state(i) for i in range(len(regions))]
+        res.close()
+    for a, b in zip(outs[False], outs[True]):
+        np.testing.assert_array_equal(a, b)
+    for i, (a, b) in enumerate(zip(states[False], states[True])):
+        np.testing.assert_array_equal(a, b, err_msg=f"region {regions[i]}")

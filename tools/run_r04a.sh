@@ -1,7 +1,16 @@
+# round 4: new GPU tests (forced RCCL exchange, sharded slab + pipelined, restart,
+# balanced update), then same-box bench A/Bs: the default, the per-region update,
+# and the --sim-ranks 8 chain on SPEEDY's stream vs the two-stream chain
 set -o pipefail
-timeout -k 10 700 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_force_exchange_gpu.py tests/test_hybrid_gpu.py tests/test_sharded_gpu.py > gpurun_out/t1.log 2>&1 || exit 1
-B="--no-cpu-baseline --train-regions 0 --reservoir-steps 0 --speedy-steps 0"
-timeout -k 10 180 python bench.py $B > gpurun_out/b1.json 2> gpurun_out/b1.err || exit 2
-timeout -k 10 180 python bench.py $B --sim-ranks 8 --chain speedy > gpurun_out/b_sim8_speedy.json 2>> gpurun_out/b1.err || exit 3
-timeout -k 10 180 python bench.py $B --sim-ranks 8 --chain two-streams > gpurun_out/b_sim8_two.json 2>> gpurun_out/b1.err || exit 4
-timeout -k 10 180 python bench.py $B --sim-ranks 8 --chain speedy > gpurun_out/b_sim8_speedy2.json 2>> gpurun_out/b1.err || exit 5
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_reservoir_gpu.py -k balanced tests/test_force_exchange_gpu.py tests/test_hybrid_gpu.py tests/test_sharded_gpu.py > gpurun_out/t1.log 2>&1 || exit 1
+B="--no-cpu-baseline --train-regions 0 --speedy-steps 0"
+run() { name=$1; shift; timeout -k 10 180 "$@" > gpurun_out/$name.json 2>> gpurun_out/bench.err || exit 2; }
+run b_default python bench.py $B
+run b_updold env SML_UPD_BAL=0 python bench.py $B
+run b_default2 python bench.py $B
+run b_updold2 env SML_UPD_BAL=0 python bench.py $B
+run b_sim8_speedy python bench.py $B --reservoir-steps 0 --sim-ranks 8 --chain speedy
+run b_sim8_two python bench.py $B --reservoir-steps 0 --sim-ranks 8 --chain two-streams
+run b_sim8_speedy2 python bench.py $B --reservoir-steps 0 --sim-ranks 8 --chain speedy
+run b_sim8_two2 python bench.py $B --reservoir-steps 0 --sim-ranks 8 --chain two-streams
