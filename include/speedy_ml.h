@@ -605,11 +605,11 @@ int sml_hybrid_set_pipelined(sml_hybrid *h, int on);
  * for exercising the transport on one GPU.  Refused without a transport. */
 int sml_hybrid_set_force_exchange(sml_hybrid *h, int on);
 /* where a step's serial chain runs -- the v_p finish with the local-model tiling, the
- * exchange, the assembly and the re-tiling: SML_CHAIN_TWO_STREAMS on the reservoir's
- * (main) stream, between a hop from SPEEDY's stream (the forecast) and one back (the
- * assembled grid); SML_CHAIN_SPEEDY on SPEEDY's stream right behind the window, so no
- * hop sits on the critical path (the main stream keeps only the reservoir begin, which
- * waits for the feedback and signals the finish); SML_CHAIN_AUTO (default) takes
+ * exchange and the assembly: SML_CHAIN_TWO_STREAMS on the reservoir's (main) stream,
+ * between a hop from SPEEDY's stream (the forecast) and one back (the assembled grid);
+ * SML_CHAIN_SPEEDY on SPEEDY's stream right behind the window, so no hop sits on the
+ * critical path (the main stream keeps the re-tiling and the reservoir begin, which
+ * wait for the assembled grid and signal the finish); SML_CHAIN_AUTO (default) takes
  * SPEEDY's stream at world > 1.  Bitwise the same results.  Drains both streams. */
 #define SML_CHAIN_AUTO 0
 #define SML_CHAIN_TWO_STREAMS 1

@@ -60,15 +60,18 @@ struct sml_hybrid {
     // blocks its queue until the producer's write lands, so under serialised dispatch
     // (rocprofv3 counter passes, AMD_SERIALIZE_KERNEL) it can stall ahead of that
     // producer: SML_HOP_AUTO then takes event hops (sml_hybrid_set_hop_mode).
-    // (the chain on SPEEDY's stream, SML_CHAIN_SPEEDY, uses two others instead: fb_t,
-    // side -> main, before the next begin; begun_t, main -> side, before the finish)
-    enum { kHopGrid = 0, kHopLm = 1, kHopFb = 2, kHopBegun = 3, kHops = 4 };
-    hipEvent_t ev[kHops] = {nullptr, nullptr, nullptr, nullptr};
-    uint64_t *d_seq = nullptr, seq[kHops] = {0, 0, 0, 0};
+    // (the chain on SPEEDY's stream, SML_CHAIN_SPEEDY, hops the other way: grid_t,
+    // side -> main, before the re-tiling; begun_t, main -> side, before the finish)
+    enum { kHopGrid = 0, kHopLm = 1, kHopBegun = 2, kHops = 3 };
+    hipEvent_t ev[kHops] = {nullptr, nullptr, nullptr};
+    uint64_t *d_seq = nullptr, seq[kHops] = {0, 0, 0};
     // where the step's serial chain runs (sml_hybrid_set_chain): false, the two-stream
-    // schedule above (the finish, exchange, assembly and tiling on the main stream,
-    // two hops around every window); true, all of it on SPEEDY's stream right after the
-    // window, the main stream keeping only the reservoir begin (and the slab predict)
+    // schedule above (the finish, exchange and assembly on the main stream, two hops
+    // around every window); true, on SPEEDY's stream right after the window:
+    //   side : window_t-1 .. wait(begun_t) finish -> [all-gather] -> assemble -> signal(grid_t) -> window_t
+    //   main :   wait(grid_t-1) tile fb_t -> begin_t -> signal(begun_t)        wait(grid_t) tile ..
+    // so no hop sits between two pieces of the critical path (the re-tiling and the
+    // begin, which need the assembled grid, are the main stream's)
     int chain_mode = SML_CHAIN_AUTO;
     bool chain = false;
     bool use_events = false;
@@ -728,7 +731,6 @@ extern "C" int sml_hybrid_start(sml_hybrid *h, const double *d_g4, const double 
     if (int rc = sml_res_tile_inputs(h->res, h->g4, h->g2, h->pr, h->f4, h->f2, h->tisr, h->fb, h->lm, h->main))
         return rc;
     if (int rc = hop_signal(h, sml_hybrid::kHopLm, h->main)) return rc;
-    if (int rc = hop_signal(h, sml_hybrid::kHopFb, h->main)) return rc;
     SML_HIP(hipStreamSynchronize(h->main));  // (the chain on SPEEDY's stream reads these on the other stream)
     h->started = true;
     h->predicted = h->advanced = false;
@@ -965,12 +967,8 @@ int predict_impl(sml_hybrid *h, bool assemble) {
         int begun = 0;
         if (h->begun_next)
             if (int rc = sml_res_step_begun(h->res, &begun)) return rc;
-        if (!begun) {
-            // (chain on SPEEDY's stream: the feedback was tiled there)
-            if (h->chain)
-                if (int rc = hop_wait(h, sml_hybrid::kHopFb, h->main)) return rc;
+        if (!begun)
             if (int rc = sml_res_step_begin(h->res, h->fb, h->main)) return rc;
-        }
         h->begun_next = false;
         if (int rc = slab_predict(h)) return rc;
         hipStream_t xs = h->main;
@@ -1007,8 +1005,8 @@ extern "C" int sml_hybrid_advance(sml_hybrid *h, const double *d_outvec_all) {
     SML_REQUIRE(h && d_outvec_all, "null argument");
     if (!h->predicted) return fail(SML_ERR_STATE, "sml_hybrid_advance without sml_hybrid_predict");
     hipStream_t m = h->main, s = h->side;
-    // the serial chain's stream: the main stream (two hops around the window), or
-    // SPEEDY's, right behind the window (sml_hybrid_set_chain)
+    // the assembly's stream: the main stream (two hops around the window), or SPEEDY's,
+    // right behind the window (sml_hybrid_set_chain); the re-tiling is the main stream's
     hipStream_t c = h->chain ? s : m;
     const bool hops = h->overlap && !h->chain;
     // (sml_hybrid_step on one rank: its predict assembled these very outvecs already)
@@ -1017,10 +1015,12 @@ extern "C" int sml_hybrid_advance(sml_hybrid *h, const double *d_outvec_all) {
     if (!done)
         if (int rc = sml_exchange_assemble(h->res, d_outvec_all, h->g4, h->g2, h->pr, c)) return rc;
     if (int rc = slab_sst(h, d_outvec_all, c)) return rc;
-    if (hops)
-        if (int rc = hop_signal(h, sml_hybrid::kHopGrid, m)) return rc;
+    if (h->overlap)  // the assembled grid: to SPEEDY's stream (two-stream) / to the main stream (chain)
+        if (int rc = hop_signal(h, sml_hybrid::kHopGrid, c)) return rc;
+    if (h->chain)
+        if (int rc = hop_wait(h, sml_hybrid::kHopGrid, m)) return rc;
     ++h->t;
-    if (int rc = sml_res_tile_feedback(h->res, h->g4, h->g2, h->pr, h->tisr_table ? nullptr : h->tisr, h->fb, c))
+    if (int rc = sml_res_tile_feedback(h->res, h->g4, h->g2, h->pr, h->tisr_table ? nullptr : h->tisr, h->fb, m))
         return rc;
     if (h->tisr_table) {  // get_tisr_by_date(..., timestep - 1, ...) for the next feedback (mpires.f90:726-728)
         int idx = 0;
@@ -1029,18 +1029,16 @@ extern "C" int sml_hybrid_advance(sml_hybrid *h, const double *d_outvec_all) {
             return rc;
         if (idx < 1 || idx > h->tisr_nhours)
             return fail(SML_ERR_ARG, "tisr hour %d outside the table's %d hours", idx, h->tisr_nhours);
-        if (int rc = sml_res_tile_tisr_field(h->res, h->tisr_table + (size_t)(idx - 1) * kGrid2d, h->fb, c))
+        if (int rc = sml_res_tile_tisr_field(h->res, h->tisr_table + (size_t)(idx - 1) * kGrid2d, h->fb, m))
             return rc;
     }
     if (h->slab.res && h->slab.tot_fb) {  // averaged_atmo_input_vec(:, mod(t-1, R-1)+1), mpires.f90:755
         sml_hybrid::Slab &sl = h->slab;
         double *col = sl.d_ring + (size_t)((h->t - 1) % (sl.ratio - 1)) * sl.tot_fb;
-        hipLaunchKernelGGL(k_slab_ring, dim3((sl.tot_fb + 255) / 256), dim3(256), 0, c, h->fb, sl.d_ring_src, sl.tot_fb,
+        hipLaunchKernelGGL(k_slab_ring, dim3((sl.tot_fb + 255) / 256), dim3(256), 0, m, h->fb, sl.d_ring_src, sl.tot_fb,
                            col);
         SML_HIP(hipGetLastError());
     }
-    if (h->chain)  // the next begin (main stream) reads this feedback
-        if (int rc = hop_signal(h, sml_hybrid::kHopFb, c)) return rc;
     if (hops)
         if (int rc = hop_wait(h, sml_hybrid::kHopGrid, s)) return rc;
     if (int rc = sml_dyn_run_model(h->dyn, h->g4, h->g2, h->nleap, h->delt, h->alph, h->rob, h->wil, h->f4, h->f2, s))
@@ -1053,8 +1051,6 @@ extern "C" int sml_hybrid_advance(sml_hybrid *h, const double *d_outvec_all) {
     // pipelined: the next step's begin from the feedback just tiled, on the main stream,
     // beside this window (it would be the next predict's first launch anyway)
     if (h->pipelined && h->overlap) {
-        if (h->chain)
-            if (int rc = hop_wait(h, sml_hybrid::kHopFb, m)) return rc;
         if (int rc = sml_res_step_begin(h->res, h->fb, m)) return rc;
         h->begun_next = true;
     }
