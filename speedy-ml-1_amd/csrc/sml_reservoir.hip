@@ -122,6 +122,7 @@ struct sml_reservoirs {
     // block's share starts in, for the grid it was built for (upd_grid: the CUs the
     // launches get, sml_res_set_update_cus; 0 = every CU of the device)
     bool upd_bal = true;
+    bool finish_ungrouped = false;  // SML_FIN_UNGROUPED=1 at create: the finish one thread per output (A/B)
     int upd_cus = 0, bal_grid = 0, ncu = 0;
     int ell_ok = -1;  // every local region's A and W_in in ELL form (-1: recount after a load)
     int32_t *d_row0 = nullptr, *d_blk_r0 = nullptr;
@@ -515,17 +516,28 @@ __device__ __attribute__((always_inline)) inline Rows<R> rows_dot(const WT *W, i
     return out;
 }
 
-// v_p = W_out(o, 1:ncs) local_model over the columns in order, from the transposed
-// block wl = [ncs][nout_pad] (a wave's lanes read neighbouring outputs of a column)
+// v_p = W_out(o, 1:ncs) local_model from the transposed block wl = [ncs][nout_pad] (a
+// wave's lanes read neighbouring outputs of a column), summed in kFinGroups groups of
+// consecutive columns -- each group a sequential fma chain from 0, the groups added in
+// order -- so the finish can run the groups on different threads (k_res_finish_grid)
+// and every other form (k_res_finish, the one-pass readout) gets the same bits
+constexpr int kFinGroups = 7;
+constexpr int kFinGsz = 19;  // the grouped finish's column-group bound (ncs 132: 6 x 19 + 18)
+__device__ inline int fin_gsz(int ncs) { return (ncs + kFinGroups - 1) / kFinGroups; }
+
 template <typename WT>
 __device__ inline double vp_sum(const WT *__restrict__ wl, int nout_pad, const double *__restrict__ lm, int ncs,
                                 int o) {
-    // 12 column loads in flight per thread (one thread per output, ~2 waves per
-    // region): the sum stays sequential in j
-    double s = 0.0;
-#pragma unroll 12
-    for (int j = 0; j < ncs; ++j) s = fma((double)wl[(size_t)j * nout_pad + o], lm[j], s);
-    return s;
+    const int gsz = fin_gsz(ncs);
+    double v = 0.0;
+    for (int g = 0; g < kFinGroups; ++g) {
+        const int j0 = g * gsz, j1 = min(ncs, j0 + gsz);
+        double s = 0.0;
+#pragma unroll 4
+        for (int j = j0; j < j1; ++j) s = fma((double)wl[(size_t)j * nout_pad + o], lm[j], s);
+        v = g == 0 ? s : v + s;
+    }
+    return v;
 }
 
 // unstandardize_state_vec_res: x*std + mean (two roundings) where the output has a slot
@@ -686,7 +698,29 @@ __device__ inline void assemble_one(int d, double v, double *__restrict__ g4, do
     }
 }
 
-template <typename WT, bool kAsm = false>
+template <typename WT>
+struct Quad {
+    WT v[4];
+};
+template <typename WT>
+__device__ inline Quad<WT> load_quad(const WT *p) {
+    Quad<WT> q;
+    if constexpr (sizeof(WT) == 4) {
+        const float4 a = *reinterpret_cast<const float4 *>(p);
+        q.v[0] = a.x; q.v[1] = a.y; q.v[2] = a.z; q.v[3] = a.w;
+    } else {
+        const double2 a = *reinterpret_cast<const double2 *>(p), b = *reinterpret_cast<const double2 *>(p + 2);
+        q.v[0] = a.x; q.v[1] = a.y; q.v[2] = b.x; q.v[3] = b.y;
+    }
+    return q;
+}
+
+// kGrouped (nout_pad <= 4 * 36, ncs <= kFinGroups * kFinGsz): thread t takes outputs
+// 4 (t % nq) .. + 3 over column group t / nq, its W_out loads (one 16-B load per
+// column) issued before the local-model gather, so they fly while the forecast is
+// read; the kFinGroups partial sums meet in LDS and are added in group order
+// (vp_sum's order).  Else one thread per output with vp_sum.
+template <typename WT, bool kAsm = false, bool kGrouped = true>
 __global__ __launch_bounds__(256) void k_res_finish_grid(
     const RegionDev *__restrict__ R, const WT *__restrict__ wlm, const int32_t *__restrict__ src,
     const uint8_t *__restrict__ lidx, const double *__restrict__ fc4, const double *__restrict__ fc2,
@@ -695,8 +729,23 @@ __global__ __launch_bounds__(256) void k_res_finish_grid(
     const int32_t *__restrict__ asm_dst = nullptr, double *__restrict__ g4 = nullptr, double *__restrict__ g2 = nullptr,
     double *__restrict__ pr = nullptr) {
     __shared__ double slm[kMaxNcs];
+    __shared__ double red[kGrouped ? kFinGroups * 144 : 1];
     const int r = blockIdx.x, t = threadIdx.x;
     const double *ms = meanstd + (size_t)r * 2 * kMeanStd;
+    const WT *wl = wlm + R[r].wlm;
+    const int nq = nout_pad / 4, gsz = fin_gsz(ncs);
+    const int q = t % nq, g = t / nq;
+    const int j0 = g * gsz, j1 = min(ncs, j0 + gsz);
+    Quad<WT> w[kFinGsz];
+    if constexpr (kGrouped) {
+        // every load issued, unpredicated (columns past the group's end clamped into the
+        // block and not summed): one memory round trip for all of them
+        const int gq = g < kFinGroups ? g : 0;
+        const int jlast = max(ncs - 1, 0);
+#pragma unroll
+        for (int jj = 0; jj < kFinGsz; ++jj)
+            w[jj] = load_quad(wl + (size_t)min(gq * gsz + jj, jlast) * nout_pad + 4 * q);
+    }
     for (int j = t; j < ncs; j += blockDim.x) {
         const int e = r * ncs + j;
         const int s = src[e];
@@ -708,8 +757,33 @@ __global__ __launch_bounds__(256) void k_res_finish_grid(
         if (lm_out) lm_out[e] = x;
     }
     __syncthreads();
+    if constexpr (kGrouped) {
+        // (keep the W_out quads in their storage precision until here: converted early
+        // they would hold twice the registers across the gather)
+        __builtin_amdgcn_sched_barrier(0);
+        if (g < kFinGroups) {
+            double acc[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int jj = 0; jj < kFinGsz; ++jj)
+                if (j0 + jj < j1) {
+                    const double x = slm[j0 + jj];
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) acc[k] = fma((double)w[jj].v[k], x, acc[k]);
+                }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) red[g * nout_pad + 4 * q + k] = acc[k];
+        }
+        __syncthreads();
+    }
     for (int o = t; o < nout; o += blockDim.x) {
-        const double vp = vp_sum(wlm + R[r].wlm, nout_pad, slm, ncs, o);
+        double vp;
+        if constexpr (kGrouped) {
+            vp = red[o];
+#pragma unroll
+            for (int gg = 1; gg < kFinGroups; ++gg) vp = vp + red[gg * nout_pad + o];
+        } else {
+            vp = vp_sum(wl, nout_pad, slm, ncs, o);
+        }
         const double v = unstd(vp + part[(size_t)r * nout_pad + o], ms, outl[o]);
         outvec[(size_t)r * ov_ld + o] = v;
         if constexpr (kAsm) assemble_one(asm_dst[(size_t)r * nout + o], v, g4, g2, pr);
@@ -1177,6 +1251,7 @@ int res_create_impl(int numregions, int nlocal, const int *region_ids, const uns
     if (const char *e = std::getenv("SML_UPD_OCC")) c->upd_occ2 = *e == '2';
     if (const char *e = std::getenv("SML_BEGIN")) c->begin_env = std::max(0, std::min(2, std::atoi(e)));
     if (const char *e = std::getenv("SML_UPD_BAL")) c->upd_bal = *e != '0';
+    if (const char *e = std::getenv("SML_FIN_UNGROUPED")) c->finish_ungrouped = *e == '1';
     SML_REQUIRE(c->read_waves >= 0, "bad read_waves");
     (void)hipGetDevice(&c->device);
     (void)hipDeviceGetAttribute(&c->ncu, hipDeviceAttributeMultiprocessorCount, c->device);
@@ -1718,6 +1793,34 @@ extern "C" int sml_res_step_slab(sml_reservoirs *c, const double *d_feedback, co
     return SML_OK;
 }
 
+namespace {
+// the finish from SPEEDY's forecast grids (k_res_finish_grid), grouped when the shape
+// allows (nout_pad <= 144 in quads, ncs <= kFinGroups * kFinGsz), with or without the
+// assembly
+template <bool kAsm>
+void launch_finish_grid(sml_reservoirs *c, const double *d_fc4d, const double *d_fc2d, double *d_local_model,
+                        double *d_outvec, double *d_grid4d, double *d_grid2d, double *d_precip, hipStream_t st) {
+    const bool grouped = c->nout_pad % 4 == 0 && c->nout_pad <= 144 && c->nout_pad / 4 * kFinGroups <= 256 &&
+                         (c->ncs + kFinGroups - 1) / kFinGroups <= kFinGsz && !c->finish_ungrouped;
+    auto go = [&](auto wt_tag, auto grouped_tag) {
+        using WT = decltype(wt_tag);
+        hipLaunchKernelGGL((k_res_finish_grid<WT, kAsm, decltype(grouped_tag)::value>), dim3(c->nlocal), dim3(256), 0,
+                           st, c->d_rd, (const WT *)c->d_wlm, c->d_lm_src, c->d_lm_l, d_fc4d, d_fc2d, d_local_model,
+                           c->d_meanstd, c->d_outl, c->d_part, d_outvec, c->nout, c->ov_ld, c->nout_pad, c->ncs,
+                           c->d_asm_dst, d_grid4d, d_grid2d, d_precip);
+    };
+    using G1 = std::integral_constant<bool, true>;
+    using G0 = std::integral_constant<bool, false>;
+    if (c->wdtype == SML_F32) {
+        if (grouped) go(float{}, G1{});
+        else go(float{}, G0{});
+    } else {
+        if (grouped) go(double{}, G1{});
+        else go(double{}, G0{});
+    }
+}
+}  // namespace
+
 extern "C" int sml_res_step_finish_grid(sml_reservoirs *c, const double *d_fc4d, const double *d_fc2d,
                                         double *d_local_model, double *d_outvec, void *stream) {
     SML_REQUIRE(c, "null context");
@@ -1726,15 +1829,8 @@ extern "C" int sml_res_step_finish_grid(sml_reservoirs *c, const double *d_fc4d,
     SML_REQUIRE(!c->generic || c->ncs == 0, "a generic (slab) context has no local-model tiling");
     SML_REQUIRE(c->ncs <= kMaxNcs, "ncs %d exceeds %d", c->ncs, kMaxNcs);
     if (!c->begun) return fail(SML_ERR_STATE, "sml_res_step_finish_grid without sml_res_step_begin");
-    hipStream_t st = (hipStream_t)stream;
-    if (c->wdtype == SML_F32)
-        hipLaunchKernelGGL(k_res_finish_grid<float>, dim3(c->nlocal), dim3(256), 0, st, c->d_rd,
-                           (const float *)c->d_wlm, c->d_lm_src, c->d_lm_l, d_fc4d, d_fc2d, d_local_model,
-                           c->d_meanstd, c->d_outl, c->d_part, d_outvec, c->nout, c->ov_ld, c->nout_pad, c->ncs);
-    else
-        hipLaunchKernelGGL(k_res_finish_grid<double>, dim3(c->nlocal), dim3(256), 0, st, c->d_rd,
-                           (const double *)c->d_wlm, c->d_lm_src, c->d_lm_l, d_fc4d, d_fc2d, d_local_model,
-                           c->d_meanstd, c->d_outl, c->d_part, d_outvec, c->nout, c->ov_ld, c->nout_pad, c->ncs);
+    launch_finish_grid<false>(c, d_fc4d, d_fc2d, d_local_model, d_outvec, nullptr, nullptr, nullptr,
+                              (hipStream_t)stream);
     SML_HIP(hipGetLastError());
     c->begun = false;
     return SML_OK;
@@ -1757,17 +1853,8 @@ extern "C" int sml_res_step_finish_assemble(sml_reservoirs *c, const double *d_f
                 "null device buffer");
     SML_REQUIRE(c->ncs <= kMaxNcs, "ncs %d exceeds %d", c->ncs, kMaxNcs);
     if (!c->begun) return fail(SML_ERR_STATE, "sml_res_step_finish_assemble without sml_res_step_begin");
-    hipStream_t st = (hipStream_t)stream;
-    if (c->wdtype == SML_F32)
-        hipLaunchKernelGGL((k_res_finish_grid<float, true>), dim3(c->nlocal), dim3(256), 0, st, c->d_rd,
-                           (const float *)c->d_wlm, c->d_lm_src, c->d_lm_l, d_fc4d, d_fc2d, d_local_model,
-                           c->d_meanstd, c->d_outl, c->d_part, d_outvec, c->nout, c->ov_ld, c->nout_pad, c->ncs,
-                           c->d_asm_dst, d_grid4d, d_grid2d, d_precip);
-    else
-        hipLaunchKernelGGL((k_res_finish_grid<double, true>), dim3(c->nlocal), dim3(256), 0, st, c->d_rd,
-                           (const double *)c->d_wlm, c->d_lm_src, c->d_lm_l, d_fc4d, d_fc2d, d_local_model,
-                           c->d_meanstd, c->d_outl, c->d_part, d_outvec, c->nout, c->ov_ld, c->nout_pad, c->ncs,
-                           c->d_asm_dst, d_grid4d, d_grid2d, d_precip);
+    launch_finish_grid<true>(c, d_fc4d, d_fc2d, d_local_model, d_outvec, d_grid4d, d_grid2d, d_precip,
+                             (hipStream_t)stream);
     SML_HIP(hipGetLastError());
     c->begun = false;
     return SML_OK;

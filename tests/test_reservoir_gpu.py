@@ -7,6 +7,8 @@ ulp) and the W_out readout's summation order (wave reductions vs sequential):
   state x : |err| <= 1e-14 * (1 + |x|)
   outvec  : |err| <= 1e-11 * (1 + |outvec|)
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -260,9 +262,11 @@ def test_dense_win_grows_the_pool(cuda):
 
 @pytest.mark.parametrize("weight_dtype", ["f32", "f64"])
 def test_finish_grid_equals_tile_then_finish(cuda, weight_dtype):
-    """sml_res_step_finish_grid (local-model tiling fused into the v_p finish) vs
-    begin -> tile_local_model -> finish: outvecs and the tiled local model bitwise,
-    with and without the local-model output."""
+    """sml_res_step_finish_grid (local-model tiling fused into the v_p finish; v_p in 7
+    column groups on different threads, added in group order) vs begin ->
+    tile_local_model -> finish (one thread per output, the same groups in turn): outvecs
+    and the tiled local model bitwise, with and without the local-model output, and
+    with the finish one thread per output (SML_FIN_UNGROUPED)."""
     import torch
 
     from speedy_ml_amd.reservoir import Reservoirs
@@ -272,9 +276,14 @@ def test_finish_grid_equals_tile_then_finish(cuda, weight_dtype):
     g4, g2, pr = synthetic_grids(7)
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(cuda)  # noqa: E731
     outs = {}
-    for mode in ("fused", "fused_nolm", "two"):
-        res = Reservoirs([w.region for w in ws], [w.sst for w in ws], [w.n for w in ws], [w.k for w in ws],
-                         weight_dtype=weight_dtype)
+    for mode in ("fused", "fused_nolm", "two", "fused_ungrouped"):
+        if mode == "fused_ungrouped":  # the finish one thread per output (vp_sum), not in column groups
+            os.environ["SML_FIN_UNGROUPED"] = "1"
+        try:
+            res = Reservoirs([w.region for w in ws], [w.sst for w in ws], [w.n for w in ws], [w.k for w in ws],
+                             weight_dtype=weight_dtype)
+        finally:
+            os.environ.pop("SML_FIN_UNGROUPED", None)
         for i, w in enumerate(ws):
             if weight_dtype == "f64":
                 res.load_region(i, w.rows, w.cols, w.vals.astype(np.float64), w.win.astype(np.float64),
@@ -296,6 +305,7 @@ def test_finish_grid_equals_tile_then_finish(cuda, weight_dtype):
         res.close()
     np.testing.assert_array_equal(outs["fused"][0], outs["two"][0])
     np.testing.assert_array_equal(outs["fused_nolm"][0], outs["two"][0])
+    np.testing.assert_array_equal(outs["fused_ungrouped"][0], outs["two"][0])
     np.testing.assert_array_equal(outs["fused"][1], outs["two"][1])
     assert (outs["fused_nolm"][1] == -7.0).all()  # no local-model output requested
 
