@@ -1800,7 +1800,7 @@ namespace {
 template <bool kAsm>
 void launch_finish_grid(sml_reservoirs *c, const double *d_fc4d, const double *d_fc2d, double *d_local_model,
                         double *d_outvec, double *d_grid4d, double *d_grid2d, double *d_precip, hipStream_t st) {
-    const bool grouped = c->nout_pad % 4 == 0 && c->nout_pad <= 144 && c->nout_pad / 4 * kFinGroups <= 256 &&
+    const bool grouped = c->ncs > 0 && c->nout_pad % 4 == 0 && c->nout_pad <= 144 && c->nout_pad / 4 * kFinGroups <= 256 &&
                          (c->ncs + kFinGroups - 1) / kFinGroups <= kFinGsz && !c->finish_ungrouped;
     auto go = [&](auto wt_tag, auto grouped_tag) {
         using WT = decltype(wt_tag);
