@@ -766,8 +766,10 @@ def training_leg(dev, mask, args, world, rank):
     # executed by the tiles (128 x 128, padded): the MFMA work actually issued
     C = npad // 128
     issued = len(naug) * (C * (C + 1) // 2 + 2 * C) * 2.0 * 128 * 128 * m * nb
-    peak = ctypes.c_double()
-    check(lib().sml_probe_mfma_f64(20000, ctypes.byref(peak)))
+    peak, ghz = ctypes.c_double(), ctypes.c_double()
+    check(lib().sml_probe_mfma_f64_clock(20000, ctypes.byref(peak), ctypes.byref(ghz)))
+    # the nominal peak at the clock the chip holds under back-to-back fp64 MFMA
+    peak_clk = F64_MFMA_PEAK_TF * ghz.value / 2.4 if ghz.value > 0 else None
     tr.close()
     del S, T
     torch.cuda.empty_cache()
@@ -793,6 +795,8 @@ def training_leg(dev, mask, args, world, rank):
             "peak": F64_MFMA_PEAK_TF,
             "frac": round(solve_tf / F64_MFMA_PEAK_TF, 4),
             "probe_tflops": round(peak.value, 2),
+            "probe_clock_ghz": round(ghz.value, 3),
+            "frac_at_probe_clock": round(solve_tf / peak_clk, 4) if peak_clk else None,
             "algorithmic_flops": solve_algo,
             "previous": "r02: 394 ms, 29.3 TF/s (1 wave per SIMD); rocSOLVER dpotrf + dpotrs strided-batched in r01: "
                         "41.7 ms per region",
@@ -808,6 +812,9 @@ def training_leg(dev, mask, args, world, rank):
                            "the chip runs MFMA-dense loops below 2.4 GHz (MI355X_MICROARCH.md, DVFS give-back)",
             "frac": round(achieved / F64_MFMA_PEAK_TF, 4),
             "probe_tflops": round(peak.value, 2),
+            "probe_clock_ghz": round(ghz.value, 3),
+            "peak_at_probe_clock": round(peak_clk, 2) if peak_clk else None,
+            "frac_at_probe_clock": round(achieved / peak_clk, 4) if peak_clk else None,
             "algorithmic_flops": algo,
             "previous": "r02: k_train_gram (single-buffered LDS, 1 wave per SIMD) 636 ms, 34.3 TF/s",
         },

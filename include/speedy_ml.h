@@ -445,6 +445,9 @@ int sml_train_get_gram(sml_train *t, int i, double *G, double *B);
 /* measurement: sustained fp64 MFMA rate of the current device (TFLOP/s), from
  * back-to-back v_mfma_f64_16x16x4_f64 chains on every SIMD */
 int sml_probe_mfma_f64(int iters, double *tflops);
+/* the same probe with the median in-kernel core clock of the timed run (GHz): the
+ * clock the chip holds under back-to-back fp64 MFMA (DVFS), against the nominal 2.4 */
+int sml_probe_mfma_f64_clock(int iters, double *tflops, double *ghz);
 
 /* ------------------------------------------------------------------ streams */
 /* A HIP stream whose kernels run only on the logical CUs [first_cu, first_cu +

@@ -799,11 +799,20 @@ extern "C" int sml_train_get_gram(sml_train *t, int i, double *G, double *B) {
 // every SIMD: the chip's sustained fp64 MFMA rate, the `peak` of the training
 // roofline (MI355X_MICROARCH.md lists no fp64 MFMA figure).
 namespace {
-__global__ __launch_bounds__(256) void k_probe_mfma_f64(int iters, double *sink) {
+// stamps (optional): thread 0 of each block records the core-clock counter
+// (s_memtime) and the 100-MHz real-time counter (s_memrealtime) around its loop, so
+// the host gets the clock the chip held under the load (MI355X_MICROARCH.md, DVFS
+// give-back item 6: the in-kernel clock = d memtime / d memrealtime x 100 MHz)
+__global__ __launch_bounds__(256) void k_probe_mfma_f64(int iters, double *sink, long long *stamps) {
     d4 acc[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) acc[i] = d4{0, 0, 0, 0};
     double a = 1.0 + threadIdx.x * 1e-9, b = 1.0 - threadIdx.x * 1e-9;
+    long long c0 = 0, r0 = 0;
+    if (stamps && threadIdx.x == 0) {
+        c0 = clock64();
+        r0 = wall_clock64();
+    }
     for (int it = 0; it < iters; ++it) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) acc[i] = MFMA64(a, b, acc[i]);
@@ -812,23 +821,31 @@ __global__ __launch_bounds__(256) void k_probe_mfma_f64(int iters, double *sink)
 #pragma unroll
     for (int i = 0; i < 8; ++i) s += acc[i][0] + acc[i][1] + acc[i][2] + acc[i][3];
     if (s == 12345.678) sink[0] = s;  // keep the chain live
+    if (stamps && threadIdx.x == 0) {
+        stamps[2 * blockIdx.x] = clock64() - c0;
+        stamps[2 * blockIdx.x + 1] = wall_clock64() - r0;
+    }
 }
 }  // namespace
 
-extern "C" int sml_probe_mfma_f64(int iters, double *tflops) {
+// the sustained fp64 MFMA rate and, when ghz is given, the median in-kernel core
+// clock of the timed run (GHz)
+extern "C" int sml_probe_mfma_f64_clock(int iters, double *tflops, double *ghz) {
     SML_REQUIRE(tflops && iters > 0, "bad argument");
     int dev = 0, ncu = 0;
     SML_HIP(hipGetDevice(&dev));
     SML_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+    const int blocks = ncu * 2;  // 8 waves per CU = 2 per SIMD
     double *sink = nullptr;
+    long long *stamps = nullptr;
     SML_HIP(hipMalloc(&sink, 8));
+    if (ghz) SML_HIP(hipMalloc(&stamps, (size_t)2 * blocks * sizeof(long long)));
     hipEvent_t e0, e1;
     SML_HIP(hipEventCreate(&e0));
     SML_HIP(hipEventCreate(&e1));
-    const int blocks = ncu * 2;  // 8 waves per CU = 2 per SIMD
-    hipLaunchKernelGGL(k_probe_mfma_f64, dim3(blocks), dim3(256), 0, nullptr, iters / 10, sink);  // warm-up
+    hipLaunchKernelGGL(k_probe_mfma_f64, dim3(blocks), dim3(256), 0, nullptr, iters / 10, sink, nullptr);  // warm-up
     SML_HIP(hipEventRecord(e0, nullptr));
-    hipLaunchKernelGGL(k_probe_mfma_f64, dim3(blocks), dim3(256), 0, nullptr, iters, sink);
+    hipLaunchKernelGGL(k_probe_mfma_f64, dim3(blocks), dim3(256), 0, nullptr, iters, sink, stamps);
     SML_HIP(hipEventRecord(e1, nullptr));
     SML_HIP(hipEventSynchronize(e1));
     float ms = 0;
@@ -838,5 +855,17 @@ extern "C" int sml_probe_mfma_f64(int iters, double *tflops) {
     (void)hipFree(sink);
     const double flops = (double)blocks * 4 * iters * 8 * 2.0 * 16 * 16 * 4;
     *tflops = flops / (ms * 1e-3) / 1e12;
+    if (ghz) {
+        std::vector<long long> h((size_t)2 * blocks);
+        SML_HIP(hipMemcpy(h.data(), stamps, h.size() * sizeof(long long), hipMemcpyDeviceToHost));
+        (void)hipFree(stamps);
+        std::vector<double> f;
+        for (int b = 0; b < blocks; ++b)
+            if (h[2 * b + 1] > 0) f.push_back((double)h[2 * b] / (double)h[2 * b + 1] * 0.1);  // 100 MHz -> GHz
+        std::sort(f.begin(), f.end());
+        *ghz = f.empty() ? 0.0 : f[f.size() / 2];
+    }
     return SML_OK;
 }
+
+extern "C" int sml_probe_mfma_f64(int iters, double *tflops) { return sml_probe_mfma_f64_clock(iters, tflops, nullptr); }
