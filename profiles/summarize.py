@@ -43,7 +43,7 @@ def _short(name: str) -> str:
         wt = m.group(1) if m else ("float" if ("<float" in name or "IfL" in name) else "double")
         mode = m.group(2) if m else ("1" if "Li1E" in name else "2" if "Li2E" in name else "0")
         return f"k_res_readout_{ {'0': 'ml', '1': 'finish', '2': 'full'}[mode]}<{wt}>"
-    for key in ("k_res_readout", "k_res_update", "k_tile_feedback", "k_tile_local_model", "k_assemble",
+    for key in ("k_res_readout", "k_res_update_bal", "k_res_update", "k_res_finish_grid", "k_tile_feedback", "k_tile_local_model", "k_assemble",
                 "k_gridy", "k_gridx", "k_specx", "k_specy", "k_vds", "k_uvspec"):
         if key in name:
             if "IfE" in name or "<float>" in name:

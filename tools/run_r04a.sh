@@ -13,3 +13,5 @@ run b_sim8_speedy python bench.py $B --reservoir-steps 0 --sim-ranks 8 --chain s
 run b_sim8_two python bench.py $B --reservoir-steps 0 --sim-ranks 8 --chain two-streams
 run b_sim8_speedy2 python bench.py $B --reservoir-steps 0 --sim-ranks 8 --chain speedy
 run b_sim8_two2 python bench.py $B --reservoir-steps 0 --sim-ranks 8 --chain two-streams
+run b_n1_chain_speedy python bench.py $B --reservoir-steps 0 --chain speedy
+run b_n1_chain_two python bench.py $B --reservoir-steps 0
