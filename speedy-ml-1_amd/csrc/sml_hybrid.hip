@@ -913,7 +913,8 @@ extern "C" int sml_hybrid_start_slab(sml_hybrid *h, const double *d_slab_outvec)
         ms[2 * j + 1] = stdv[35];
     }
     hipStream_t m = h->main;
-    SML_HIP(hipMemcpyAsync(sl.d_ms, ms.data(), ms.size() * 8, hipMemcpyHostToDevice, m));
+    if (sl.nslab)  // (a rank without sst regions has no slab mean / std)
+        SML_HIP(hipMemcpyAsync(sl.d_ms, ms.data(), (size_t)2 * sl.nslab * 8, hipMemcpyHostToDevice, m));
     SML_HIP(hipMemsetAsync(sl.d_ring, 0, (size_t)(sl.ratio - 1) * sl.tot_fb * 8, m));
     const int nfill = h->nlocal * sl.nsst, n = sl.nslab * sl.nsst;
     hipLaunchKernelGGL(k_slab_rows, dim3((nfill + 255) / 256), dim3(256), 0, m, nullptr, nullptr, 0, sl.nsst, h->nlocal,

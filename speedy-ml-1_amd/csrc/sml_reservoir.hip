@@ -528,15 +528,23 @@ __device__ inline int fin_gsz(int ncs) { return (ncs + kFinGroups - 1) / kFinGro
 template <typename WT>
 __device__ inline double vp_sum(const WT *__restrict__ wl, int nout_pad, const double *__restrict__ lm, int ncs,
                                 int o) {
+    // the kFinGroups chains advance together (independent FMAs, their loads in flight
+    // together); each is still the sequential sum of its own columns
     const int gsz = fin_gsz(ncs);
-    double v = 0.0;
-    for (int g = 0; g < kFinGroups; ++g) {
-        const int j0 = g * gsz, j1 = min(ncs, j0 + gsz);
-        double s = 0.0;
-#pragma unroll 4
-        for (int j = j0; j < j1; ++j) s = fma((double)wl[(size_t)j * nout_pad + o], lm[j], s);
-        v = g == 0 ? s : v + s;
+    double s[kFinGroups];
+#pragma unroll
+    for (int g = 0; g < kFinGroups; ++g) s[g] = 0.0;
+#pragma unroll 2
+    for (int jj = 0; jj < gsz; ++jj) {
+#pragma unroll
+        for (int g = 0; g < kFinGroups; ++g) {
+            const int j = g * gsz + jj;
+            if (j < ncs) s[g] = fma((double)wl[(size_t)j * nout_pad + o], lm[j], s[g]);
+        }
     }
+    double v = s[0];
+#pragma unroll
+    for (int g = 1; g < kFinGroups; ++g) v = v + s[g];
     return v;
 }
 

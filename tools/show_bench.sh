@@ -1,4 +1,4 @@
-tail -5 gpurun_out/t1.log; grep -E "passed|failed|FAILED|Error" gpurun_out/t1.log | tail -5
+grep -E "PASSED|FAILED|ERROR" gpurun_out/t1.log | grep -v PASSED | head -20; tail -3 gpurun_out/t1.log; tail -2 gpurun_out/smoke.log
 for f in gpurun_out/b_*.json; do echo -n "$f "; python -c "
 import json,sys
 try:
