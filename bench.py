@@ -93,9 +93,9 @@ def parse():
                    help="each step also issues the next step's reservoir begin (sml_hybrid_set_pipelined): "
                         "the loop a long run is in, also for the first timed step after the warmup's sync")
     p.add_argument("--chain", choices=("auto", "two-streams", "speedy"), default="auto",
-                   help="where the step's serial chain (v_p finish, exchange, assembly, tiling) runs "
-                        "(sml_hybrid_set_chain): auto = SPEEDY's stream right behind the window at N > 1 (and in "
-                        "the --sim-ranks diagnostic), the reservoir's stream between two hops at N = 1")
+                   help="where the step's serial chain (v_p finish, exchange, assembly) runs (sml_hybrid_set_chain): "
+                        "auto = the reservoir's stream between two hops (measured faster at N = 1 and 8-rank shares), "
+                        "speedy = SPEEDY's stream right behind the window")
     p.add_argument("--slab", action=argparse.BooleanOptionalAction, default=True,
                    help="the slab ocean in the loop, as the reference runs by default (mod_reservoir.f90:41): a "
                         "slab reservoir per sst region, predict_slab_ml every 168 h (28 steps), its sst in the "
@@ -312,7 +312,7 @@ def main():
         loop.set_pipelined(True)
     from speedy_ml_amd._lib import SML_CHAIN_SPEEDY, SML_CHAIN_TWO_STREAMS
 
-    if args.chain != "auto" or sim > 1:  # (--sim-ranks stands for world > 1, whose default is SPEEDY's stream)
+    if args.chain != "auto":
         loop.set_chain(SML_CHAIN_TWO_STREAMS if args.chain == "two-streams" else SML_CHAIN_SPEEDY)
     chain_eff = loop.chain()[1]
     # initial inputs from the synthetic analysis state (start_prediction analogue)

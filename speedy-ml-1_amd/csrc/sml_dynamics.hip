@@ -100,6 +100,13 @@ struct sml_dynamics {
     hipStream_t chk_stream = nullptr;
     hipEvent_t ev_fork = nullptr, ev_chk = nullptr;
     bool chk_pending = false;  // work on chk_stream that the next user of d_chk must wait for
+    // run_model's exit learns the check's result from a device counter instead of an
+    // event wait on its stream (chk_flag; SML_CHK_FLAG=0 at create: the event): the
+    // check's k_io_minmax adds 4 per check, the exit polls for 4 * chk_count
+    bool chk_flag = true;
+    unsigned *d_chk_cnt = nullptr, *d_chk_late = nullptr;
+    unsigned chk_count = 0;
+    bool chk_counted = false;  // the last launch_io_check added to the counter
     // host copy of the last check's min/max (pinned; written behind the check on its
     // stream, ev_mm marks it): run_speedy for a host loop without a device sync
     double *h_mm = nullptr;
@@ -2047,7 +2054,11 @@ __global__ __launch_bounds__(kSpecThreads) void k_io_entry(const double *__restr
 __device__ inline double nmin(double a, double b) { return (a != a || b != b) ? __builtin_nan("") : (b < a ? b : a); }
 __device__ inline double nmax(double a, double b) { return (a != a || b != b) ? __builtin_nan("") : (b > a ? b : a); }
 
-__global__ __launch_bounds__(1024) void k_io_minmax(const double *__restrict__ G, double *__restrict__ mm) {
+// cnt (may be null): the hand-off counter the run_model exit polls -- each block stores
+// its min / max sc1, drains its stores and adds 1 (MI355X_MICROARCH.md, inter-workgroup
+// visibility: an agent-scope atomic add per storing workgroup, sc1 stores and loads)
+__global__ __launch_bounds__(1024) void k_io_minmax(const double *__restrict__ G, double *__restrict__ mm,
+                                                     unsigned *__restrict__ cnt) {
     __shared__ double smin[16], smax[16];
     const int v = blockIdx.x;
     const double *f = G + (size_t)v * kKX * kGF;
@@ -2072,8 +2083,15 @@ __global__ __launch_bounds__(1024) void k_io_minmax(const double *__restrict__ G
             lo = nmin(lo, smin[i]);
             hi = nmax(hi, smax[i]);
         }
-        mm[2 * v] = lo;
-        mm[2 * v + 1] = hi;
+        if (cnt) {
+            __hip_atomic_store(mm + 2 * v, lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(mm + 2 * v + 1, hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            mm[2 * v] = lo;
+            mm[2 * v + 1] = hi;
+        }
     }
 }
 
@@ -2109,6 +2127,7 @@ extern "C" int sml_dyn_destroy(sml_dynamics *d) {
     if (d->ev_mm) (void)hipEventDestroy(d->ev_mm);
     if (d->h_mm) (void)hipHostFree(d->h_mm);
     if (d->d_chk) (void)hipFree(d->d_chk);
+    if (d->d_chk_cnt) (void)hipFree(d->d_chk_cnt);
     if (d->sp) sml_spectral_destroy(d->sp);
     delete d;
     return SML_OK;
@@ -2132,6 +2151,7 @@ extern "C" int sml_dyn_create(double radius, sml_dynamics **out) {
     if (const char *e = std::getenv("SML_DYN_SPLIT_GRID")) d->split_grid = *e && *e != '0';
     if (const char *e = std::getenv("SML_DYN_NOGRAPH")) d->nograph = *e && *e != '0';
     if (const char *e = std::getenv("SML_DYN_WT")) d->wt = *e && *e != '0';
+    if (const char *e = std::getenv("SML_CHK_FLAG")) d->chk_flag = *e != '0';
     if (const char *e = std::getenv("SML_DYN_STAMPS"))
         if (*e && *e != '0' && (rc = dalloc(reinterpret_cast<double **>(&d->d_dbg), kStampKernels * kStampBlocks * kStamps))) {
             sml_dyn_destroy(d);
@@ -2146,6 +2166,7 @@ extern "C" int sml_dyn_create(double radius, sml_dynamics **out) {
         (rc = dalloc(&d->d_vfm, (size_t)kMX * kVFm)) || (rc = dalloc(&d->d_sm, (size_t)2 * kMX * kSM)) ||
         (rc = dalloc(&d->d_pfl, (size_t)kMX * (kIY / 4) * 64 * 2)) ||
         (rc = dalloc(&d->d_phys, (size_t)4 * kKX * kGF)) || (rc = dalloc(&d->d_minmax, 8)) ||
+        (rc = dalloc(&d->d_chk_cnt, 2)) ||
         (rc = dalloc(&d->d_io, (size_t)4 * kKX * kGF + kGF)) || (rc = dalloc(&d->d_ptab, 1)) ||
         (rc = dalloc(&d->d_chk, (size_t)kNIo * (kSF + kVF + kGF))) ||
         (rc = dalloc(&d->d_pbc, (size_t)kNBc * kNGP)) || (rc = dalloc(&d->d_rad, kRadSize)) ||
@@ -2154,6 +2175,7 @@ extern "C" int sml_dyn_create(double radius, sml_dynamics **out) {
         sml_dyn_destroy(d);
         return rc;
     }
+    d->d_chk_late = d->d_chk_cnt + 1;
     d->d_tab = d->d_tabs;
     hipError_t e = hipMemcpy(d->d_tab, &d->tab, sizeof(DynTables), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(d->d_ptab, &d->ptab, sizeof(PhysTables), hipMemcpyHostToDevice);
@@ -2695,8 +2717,12 @@ int launch_io_check(sml_dynamics *d, hipStream_t st, double *d_minmax) {
     if (int rc = spectral_gridy(d->sp, cs, cv, kNIo, cst)) return rc;
     if (int rc = spectral_gridx_range(d->sp, cv, cg, kNIo, 0, kNIoWind, cst)) return rc;
     double *mm = d_minmax ? d_minmax : d->d_minmax;
-    hipLaunchKernelGGL(k_io_minmax, dim3(4), dim3(1024), 0, cst, cg, mm);
+    // on the check stream, for run_model's exit: the counter hand-off (4 adds per check)
+    const bool counted = cst != st && d->chk_flag && !d_minmax;
+    hipLaunchKernelGGL(k_io_minmax, dim3(4), dim3(1024), 0, cst, cg, mm, counted ? d->d_chk_cnt : nullptr);
     SML_HIP(hipGetLastError());
+    if (counted) ++d->chk_count;
+    d->chk_counted = counted;
     d->mm_last = mm;
     d->mm_issued = false;
     if (cst != st) {  // a host copy for sml_dyn_last_safe, behind the check on its stream
@@ -2792,7 +2818,17 @@ extern "C" int sml_dyn_run_model(sml_dynamics *d, const double *d_grid4d, const 
         if (int rc = sml_dyn_from_grid(d, d_grid4d, d_logp, nullptr, stream)) return rc;
         if (int rc = sml_dyn_window(d, nleap, delt, alph, rob, wil, stream)) return rc;
     }
-    if (d->chk_pending) {  // the exit reads the check's min/max
+    IoExit ex{0.000001, d->mm_last, d_grid4d, d_logp};
+    if (d->chk_pending && d->chk_counted) {
+        // the exit kernel itself waits for the check's counter: no event wait (a
+        // barrier packet with a cross-queue dependency) on the window's stream.  The
+        // check is complete once the exit has run, so the next user of d_chk needs no
+        // wait either
+        ex.cnt = d->d_chk_cnt;
+        ex.target = 4u * d->chk_count;
+        ex.late = d->d_chk_late;
+        d->chk_pending = false;
+    } else if (d->chk_pending) {  // the exit reads the check's min/max
         SML_HIP(hipStreamWaitEvent(st, d->ev_chk, 0));
         d->chk_pending = false;
     }
@@ -2802,8 +2838,7 @@ extern "C" int sml_dyn_run_model(sml_dynamics *d, const double *d_grid4d, const 
         SML_HIP(hipGetLastError());
         if (int rc = spectral_gridy(d->sp, d->d_specin, d->d_varm, kNIo, st)) return rc;
     }
-    return spectral_gridx_run_model_exit(d->sp, d->d_varm, d_fc4d, d_fc2d, kNIoWind,
-                                         IoExit{0.000001, d->mm_last, d_grid4d, d_logp}, st);
+    return spectral_gridx_run_model_exit(d->sp, d->d_varm, d_fc4d, d_fc2d, kNIoWind, ex, st);
 }
 
 extern "C" int sml_dyn_set_check_cus(sml_dynamics *d, int first_cu, int num_cus) {
@@ -2842,6 +2877,16 @@ extern "C" int sml_dyn_last_safe(sml_dynamics *d, int *safe, double *minmax) {
     }
     *safe = sml_dyn_is_safe(mm);
     if (minmax) std::memcpy(minmax, mm, sizeof mm);
+    return SML_OK;
+}
+
+// a run_model exit that gave up waiting for its safety check (1 s; never expected):
+// checked by the hybrid loop's sync, after the streams drained
+int sml::dyn_check_late(sml_dynamics *d) {
+    if (!d || !d->d_chk_late) return SML_OK;
+    unsigned late = 0;
+    SML_HIP(hipMemcpy(&late, d->d_chk_late, sizeof late, hipMemcpyDeviceToHost));
+    if (late) return fail(SML_ERR_STATE, "run_model's exit did not receive the safety check within 1 s");
     return SML_OK;
 }
 

@@ -472,10 +472,12 @@ extern "C" int sml_hybrid_set_pipelined(sml_hybrid *h, int on) {
 
 // the step's serial chain (finish -> exchange -> assembly -> tiling): on the main
 // stream between two cross-stream hops (SML_CHAIN_TWO_STREAMS), or on SPEEDY's stream
-// right after the window (SML_CHAIN_SPEEDY); SML_CHAIN_AUTO takes SPEEDY's stream when
-// the rank holds a share of a world > 1 decomposition (its begin is short enough to
-// finish beside the window; at world 1 the begin is as long as the window and the
-// finish belongs on the reservoir's 192 CUs).  Drains both streams first.
+// right after the window (SML_CHAIN_SPEEDY).  SML_CHAIN_AUTO is the two-stream form:
+// measured same-box (r04a), the chain on SPEEDY's stream was 19-20 us per step SLOWER
+// at world 1 and in the 8-rank share -- its two remaining stream operations
+// (hipStreamWaitValue64 / WriteValue64 run as blit kernels, ~6 us each, satisfied or
+// not) stay on the critical path, and the finish and assembly get 64 CUs instead of
+// 192.  Drains both streams first.
 extern "C" int sml_hybrid_set_chain(sml_hybrid *h, int mode) {
     SML_REQUIRE(h && (mode == SML_CHAIN_AUTO || mode == SML_CHAIN_TWO_STREAMS || mode == SML_CHAIN_SPEEDY),
                 "bad chain mode %d", mode);
@@ -483,9 +485,7 @@ extern "C" int sml_hybrid_set_chain(sml_hybrid *h, int mode) {
     if (h->main) SML_HIP(hipStreamSynchronize(h->main));
     if (h->side && h->side != h->main) SML_HIP(hipStreamSynchronize(h->side));
     h->chain_mode = mode;
-    const int world = h->comm ? h->comm->world : 1;
-    const bool want = mode == SML_CHAIN_SPEEDY || (mode == SML_CHAIN_AUTO && world > 1);
-    h->chain = want && h->overlap && h->side != h->main;
+    h->chain = mode == SML_CHAIN_SPEEDY && h->overlap && h->side != h->main;
     return SML_OK;
 }
 
@@ -1139,7 +1139,7 @@ extern "C" int sml_hybrid_sync(sml_hybrid *h) {
     }
     SML_HIP(hipStreamSynchronize(h->main));
     SML_HIP(hipStreamSynchronize(h->side));
-    return SML_OK;
+    return sml::dyn_check_late(h->dyn);
 }
 
 // ------------------------------------------------------------- device memory

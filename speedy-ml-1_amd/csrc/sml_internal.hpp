@@ -18,6 +18,8 @@ struct sml_reservoirs;
 namespace sml {
 // the context holds every region, in global order (its local index is the region id)
 bool res_in_global_order(const sml_reservoirs *c);
+// sml_dynamics: the run_model exit's safety-check hand-off timed out (SML_ERR_STATE)
+int dyn_check_late(sml_dynamics *d);
 
 // --------------------------------------------------------------- geometry
 // Restatement of the res_domain.f90 decomposition used by every reservoir of the

@@ -529,18 +529,30 @@ template <typename WT>
 __device__ inline double vp_sum(const WT *__restrict__ wl, int nout_pad, const double *__restrict__ lm, int ncs,
                                 int o) {
     // the kFinGroups chains advance together (independent FMAs, their loads in flight
-    // together); each is still the sequential sum of its own columns
+    // together); each is still the sequential sum of its own columns.  Only the last
+    // group can be short when (kFinGroups - 1) * gsz <= ncs (every ncs >= 36): the
+    // others run unguarded, so no load waits behind a branch
     const int gsz = fin_gsz(ncs);
     double s[kFinGroups];
 #pragma unroll
     for (int g = 0; g < kFinGroups; ++g) s[g] = 0.0;
+    if ((kFinGroups - 1) * gsz <= ncs) {
+        const int last = ncs - (kFinGroups - 1) * gsz;  // columns of the last group (<= gsz)
 #pragma unroll 2
-    for (int jj = 0; jj < gsz; ++jj) {
+        for (int jj = 0; jj < gsz; ++jj) {
 #pragma unroll
-        for (int g = 0; g < kFinGroups; ++g) {
-            const int j = g * gsz + jj;
-            if (j < ncs) s[g] = fma((double)wl[(size_t)j * nout_pad + o], lm[j], s[g]);
+            for (int g = 0; g < kFinGroups - 1; ++g) {
+                const int j = g * gsz + jj;
+                s[g] = fma((double)wl[(size_t)j * nout_pad + o], lm[j], s[g]);
+            }
         }
+        for (int jj = 0; jj < last; ++jj) {
+            const int j = (kFinGroups - 1) * gsz + jj;
+            s[kFinGroups - 1] = fma((double)wl[(size_t)j * nout_pad + o], lm[j], s[kFinGroups - 1]);
+        }
+    } else {
+        for (int g = 0; g < kFinGroups; ++g)
+            for (int j = g * gsz; j < min(ncs, (g + 1) * gsz); ++j) s[g] = fma((double)wl[(size_t)j * nout_pad + o], lm[j], s[g]);
     }
     double v = s[0];
 #pragma unroll

@@ -152,7 +152,25 @@ __global__ __launch_bounds__(kFftThreads) void k_gridx(const double *__restrict_
         for (int e = 1; e <= kMX2 - 2; ++e) xi[e] = v[e + 1];
     }
     double mmv[8];
-    if (ex.mm) {
+    if (ex.mm && ex.cnt) {
+        // the safety check ran on another stream: wait for its hand-off counter (one
+        // relaxed sc1 poll per step of lane 0, MI355X_MICROARCH.md inter-workgroup
+        // visibility: the producer stored mm sc1 and drained before its atomic add),
+        // then read mm with sc1 loads
+        if (threadIdx.x == 0) {
+            const long long t0 = wall_clock64();
+            while (__hip_atomic_load(ex.cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < ex.target) {
+                __builtin_amdgcn_s_sleep(2);
+                if (wall_clock64() - t0 > 100000000ll) {  // ~1 s at 100 MHz: never hang the queue
+                    __hip_atomic_store(ex.late, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    break;
+                }
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < 8; ++q) mmv[q] = __hip_atomic_load(ex.mm + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else if (ex.mm) {
 #pragma unroll
         for (int q = 0; q < 8; ++q) mmv[q] = ex.mm[q];
     }

@@ -48,6 +48,12 @@ int spectral_gridx_io(sml_spectral *s, const double *varm, double *g4, double *l
 struct IoExit {
     double qfloor;
     const double *mm, *in4, *inlp;
+    // the check's hand-off without a stream hop (sml_dynamics chk_flag): mm is final
+    // once *cnt >= target (the check's min/max blocks each add 1 after their sc1
+    // stores); a hand-off that does not arrive within ~1 s sets *late and goes on
+    const unsigned *cnt = nullptr;
+    unsigned target = 0;
+    unsigned *late = nullptr;
 };
 int spectral_gridx_run_model_exit(sml_spectral *s, const double *varm, double *g4, double *logp, int nwind,
                                   IoExit ex, hipStream_t st);

@@ -259,6 +259,11 @@ def test_sharded_slab_pipelined_step_is_bitwise_the_one_rank_loop(cuda, one_rank
     comms = [LocalRank(world, q) for q in range(world)]
     built = [_slab_setup(cuda, shares[q], mask, comms[q]) for q in range(world)]
     loops = [b[0] for b in built]
+    # odd ranks run the chain on SPEEDY's stream (sml_hybrid_set_chain): the same bits
+    from speedy_ml_amd._lib import SML_CHAIN_SPEEDY
+
+    for q in range(1, world, 2):
+        loops[q].set_chain(SML_CHAIN_SPEEDY)
     if world == 8:
         assert built[1][1] == [], "rank 1 of 8 must own no sst region"
     recv = torch.zeros((world * maxc, 140), dtype=torch.float64, device=cuda)
