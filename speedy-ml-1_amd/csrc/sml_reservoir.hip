@@ -528,31 +528,33 @@ __device__ inline int fin_gsz(int ncs) { return (ncs + kFinGroups - 1) / kFinGro
 template <typename WT>
 __device__ inline double vp_sum(const WT *__restrict__ wl, int nout_pad, const double *__restrict__ lm, int ncs,
                                 int o) {
-    // the kFinGroups chains advance together (independent FMAs, their loads in flight
-    // together); each is still the sequential sum of its own columns.  Only the last
-    // group can be short when (kFinGroups - 1) * gsz <= ncs (every ncs >= 36): the
-    // others run unguarded, so no load waits behind a branch
+    // the kFinGroups chains advance together; each is still the sequential sum of its
+    // own columns.  Every load of a round of kVpU columns per chain is issued before
+    // the round's FMAs (indices past a chain's end clamped into the block, those FMAs
+    // selected away): one memory round trip per round, not one per column
+    constexpr int kVpU = 2;
     const int gsz = fin_gsz(ncs);
     double s[kFinGroups];
 #pragma unroll
     for (int g = 0; g < kFinGroups; ++g) s[g] = 0.0;
-    if ((kFinGroups - 1) * gsz <= ncs) {
-        const int last = ncs - (kFinGroups - 1) * gsz;  // columns of the last group (<= gsz)
-#pragma unroll 2
-        for (int jj = 0; jj < gsz; ++jj) {
+    for (int jj0 = 0; jj0 < gsz; jj0 += kVpU) {
+        double w[kVpU][kFinGroups], x[kVpU][kFinGroups];
 #pragma unroll
-            for (int g = 0; g < kFinGroups - 1; ++g) {
-                const int j = g * gsz + jj;
-                s[g] = fma((double)wl[(size_t)j * nout_pad + o], lm[j], s[g]);
+        for (int u = 0; u < kVpU; ++u)
+#pragma unroll
+            for (int g = 0; g < kFinGroups; ++g) {
+                const int jc = min(g * gsz + jj0 + u, ncs - 1);
+                w[u][g] = (double)wl[(size_t)jc * nout_pad + o];
+                x[u][g] = lm[jc];
             }
-        }
-        for (int jj = 0; jj < last; ++jj) {
-            const int j = (kFinGroups - 1) * gsz + jj;
-            s[kFinGroups - 1] = fma((double)wl[(size_t)j * nout_pad + o], lm[j], s[kFinGroups - 1]);
-        }
-    } else {
-        for (int g = 0; g < kFinGroups; ++g)
-            for (int j = g * gsz; j < min(ncs, (g + 1) * gsz); ++j) s[g] = fma((double)wl[(size_t)j * nout_pad + o], lm[j], s[g]);
+#pragma unroll
+        for (int u = 0; u < kVpU; ++u)
+#pragma unroll
+            for (int g = 0; g < kFinGroups; ++g) {
+                const int jj = jj0 + u, j = g * gsz + jj;
+                const double t = fma(w[u][g], x[u][g], s[g]);
+                s[g] = (jj < gsz && j < ncs) ? t : s[g];
+            }
     }
     double v = s[0];
 #pragma unroll
