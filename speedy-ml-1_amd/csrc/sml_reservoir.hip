@@ -224,6 +224,21 @@ __device__ inline void load_row(RowRegs<WT> &q, const RegionDev &rg, const Ell &
     }
 }
 
+// the reservoir's activation, tanh (mod_reservoir.f90:1447).  OCML's tanh(double) is
+// ~150 f64 instructions (a double-double exp and a compensated division): in the
+// state update that is more VALU time per row than the row's bytes take to stream
+// at 8 TB/s.  tanh(x) = em / (em + 2), em = expm1(2|x|), sign restored: expm1 keeps
+// small |x| exact to an ulp (no 1 - 2 / (e + 1) cancellation), the division rounds
+// once; |x| > 20 gives 1 (tanh(20) = 1 - 8.5e-18 rounds to 1).  Within 3 ulp of
+// glibc's tanh (the oracle's; tests bound states at 1e-14), NaN and -0 preserved.
+// Every state update form uses it, so they stay bitwise equal to each other.
+__device__ __attribute__((always_inline)) inline double res_tanh(double x) {
+    double a = fabs(x);
+    a = a > 20.0 ? 20.0 : a;  // (NaN stays NaN)
+    const double em = expm1(2.0 * a);
+    return copysign(em / (em + 2.0), x);
+}
+
 __device__ inline int ell_col(const uint4 &c, int s) {
     const uint32_t w = s < 2 ? c.x : s < 4 ? c.y : s < 6 ? c.z : c.w;
     return (s & 1) ? (int)(w >> 16) : (int)(w & 0xffffu);
@@ -292,7 +307,7 @@ __device__ __attribute__((always_inline)) inline void update_block(
             } else {
                 for (int e = wp[i], e1 = wp[i + 1]; e < e1; ++e) t = t + (double)wv[e] * fs[wc[e]];
             }
-            const double xn = tanh(y + t);
+            const double xn = res_tanh(y + t);
             const double xv = (1.0 - leak) * xs[i] + leak * xn;
             x_new[rg.x + i] = xv;
             xaug[rg.xaug + ncs + i] = (i & 1) ? xv * xv : xv;  // x_temp(2:n:2)**2 (1-based even)
@@ -425,7 +440,7 @@ __global__ __launch_bounds__(kUpdThreads, 4) void k_res_update_bal(
                     if (s < rg.a_w) y = y + (double)L0.v[s] * xs[ell_col(L0.c, s)];
                 double t = 0.0;
                 t = t + (double)L0.wv * fs[L0.wc];
-                const double xn = tanh(y + t);
+                const double xn = res_tanh(y + t);
                 const double xv = (1.0 - leak) * xs[i] + leak * xn;
                 x_new[rg.x + i] = xv;
                 xaug[rg.xaug + ncs + i] = (i & 1) ? xv * xv : xv;  // x_temp(2:n:2)**2 (1-based even)
