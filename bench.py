@@ -399,6 +399,7 @@ def main():
     rd_avg_s = float(np.mean(rd_ms)) * 1e-3
     upd_avg_s = float(np.mean(upd_ms)) * 1e-3
     achieved = rd_bytes / rd_avg_s / 1e9
+    upd_bytes = sum(8 * (2 + wb) * s.n + (2 + wb) * s.n + 3 * 8 * s.n + 8 * s.ninp for s in sizes)
     _, algo_step = res.footprint()
     traffic = None
     pmc_path = os.path.join(REPO, "profiles", "readout_pmc.json")
@@ -414,6 +415,8 @@ def main():
     # supplementary: the reservoir side alone (configs[1]), SPEEDY's step alone
     reservoir_only = None
     if args.reservoir_steps > 0:
+        res.set_update_cus(0)  # this leg runs on the whole device: one balanced-update block per CU of all 256
+
         def rstep():
             res.predict(fb, lm, ov)
             glob = exchange(ov)
@@ -431,7 +434,9 @@ def main():
                    "achieved": round(full_bytes / u_rd_s / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                    "frac": round(full_bytes / u_rd_s / 1e9 / HBM_PEAK_GBS, 4),
                    "algorithmic_bytes_per_launch": full_bytes, "readout_avg_ms": round(u_rd_s * 1e3, 4),
-                   "update_avg_ms": round(float(np.mean(u_upd)), 4)}
+                   "update_avg_ms": round(float(np.mean(u_upd)), 4),
+                   "update_achieved_GBps": round(upd_bytes / (float(np.mean(u_upd)) * 1e-3) / 1e9, 1),
+                   "update_frac": round(upd_bytes / (float(np.mean(u_upd)) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
         reservoir_only = {
             "workload": "configs[1]: predict for all 1152 subdomains + outvec exchange + assemble + re-tile "
                         "(SPEEDY forecast grids held fixed)",
@@ -519,6 +524,12 @@ def main():
                 "fp64_weight_equivalent_GBps": round(rd_bytes_f64 / rd_avg_s / 1e9, 1),
                 "readout_avg_ms": round(rd_avg_s * 1e3, 4),
                 "update_avg_ms": round(upd_avg_s * 1e3, 4),
+                # the state update beside the window (k_res_update_bal, 192 CUs): A as ELL rows of 8
+                # slots (u16 column + weight), W_in's one entry per row, x read once (LDS staging),
+                # x and x~ written, the feedback read
+                "update_algorithmic_bytes": upd_bytes,
+                "update_achieved_GBps": round(upd_bytes / upd_avg_s / 1e9, 1),
+                "update_frac": round(upd_bytes / upd_avg_s / 1e9 / HBM_PEAK_GBS, 4),
                 "step_algorithmic_bytes": algo_step,
             },
             "cpu_baseline": cpu,

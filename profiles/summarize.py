@@ -115,6 +115,15 @@ def main():
             out["algorithmic_bytes_per_launch"] = bench.get("roofline", {}).get("algorithmic_bytes_per_launch")
         json.dump(out, open(os.path.join(HERE, "readout_pmc.json"), "w"), indent=1)
         lines += ["", f"{name} HBM traffic per launch (2 x FETCH + WRITE): {hbm / 1e9:.3f} GB"]
+    # the state update (k_res_update_bal beside the window; k_res_update when not balanced)
+    up = sorted([r for r in rows if r[0].startswith(("k_res_update_bal", "k_res_update"))], key=lambda r: -r[1] * r[2])
+    if up and up[0][4] is not None and up[0][5] is not None:
+        name, calls, avg, _, fk, wk = up[0]
+        hbm_raw = (fk + wk) * 1024.0
+        hbm_x2 = (2.0 * fk + wk) * 1024.0
+        ab = (bench.get("roofline", {}) or {}).get("update_algorithmic_bytes")
+        lines += ["", f"{name} HBM traffic per launch: {hbm_raw / 1e6:.1f} MB (FETCH raw + WRITE), "
+                      f"{hbm_x2 / 1e6:.1f} MB (FETCH x2 + WRITE)" + (f"; algorithmic {ab / 1e6:.1f} MB" if ab else "")]
     open(os.path.join(HERE, f"{rnd}_summary.md"), "w").write("\n".join(lines) + "\n")
     print("\n".join(lines))
 
