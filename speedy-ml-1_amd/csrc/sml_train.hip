@@ -33,7 +33,6 @@
 #include <vector>
 
 #include "sml_internal.hpp"
-#include "sml_mfma44.hpp"
 
 using namespace sml;
 
@@ -207,12 +206,11 @@ __global__ __launch_bounds__(256, 2) void k_train_gram2(const double *__restrict
             sB[buf][lt0 + 2 * q][lrow] = rb[q];
         }
     };
-    // the 16x16x4 steps as v_mfma_f64_4x4x4_f64 (sml_mfma44.hpp: 1.57x the issue rate)
-    Acc44 acc44[4][4];
+    d4 acc[4][4];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc44[i][j] = acc44_zero();
+        for (int j = 0; j < 4; ++j) acc[i][j] = d4{0, 0, 0, 0};
     fetch(0);
     store(0);
     __syncthreads();
@@ -227,11 +225,9 @@ __global__ __launch_bounds__(256, 2) void k_train_gram2(const double *__restrict
 #pragma unroll
             for (int j = 0; j < 4; ++j) b[j] = sB[cur][4 * s + kk][wc * 64 + j * 16 + l16];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const B44 bj = b44(b[j]);
+            for (int i = 0; i < 4; ++i)
 #pragma unroll
-                for (int i = 0; i < 4; ++i) mfma44(a[i], bj, acc44[i][j]);
-            }
+                for (int j = 0; j < 4; ++j) acc[i][j] = MFMA64(a[i], b[j], acc[i][j]);
         }
         if (t0 + kKC < m) {
             store(cur ^ 1);
@@ -240,16 +236,12 @@ __global__ __launch_bounds__(256, 2) void k_train_gram2(const double *__restrict
         __syncthreads();
         cur ^= 1;
     }
-    // (every wave is past its last read of the stages: the loop ends on a barrier)
-    double *scr = &sA[0][0][0] + w * 256;
-
     double *Gr = G + (size_t)r * npad * npad;
     double *Br = B + (size_t)r * npad * nout;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const d4 acc = acc44_to_d4(acc44[i][j], scr);  // one tile at a time: no second set of registers
+        for (int j = 0; j < 4; ++j)
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const int row = bi * kTile + wr * 64 + i * 16 + kk + 4 * q;
@@ -257,14 +249,13 @@ __global__ __launch_bounds__(256, 2) void k_train_gram2(const double *__restrict
                 if (strip) {
                     if (row < nout) {
                         double *p = Br + (size_t)row * npad + col;
-                        *p = *p + acc[q];
+                        *p = *p + acc[i][j][q];
                     }
                 } else {
                     double *p = Gr + (size_t)col * npad + row;
-                    *p = *p + acc[q];
+                    *p = *p + acc[i][j][q];
                 }
             }
-        }
 }
 
 // fit_chunk_hybrid regularisation on the padded, column-major Gram:
@@ -346,11 +337,11 @@ __device__ __forceinline__ void gemm_tile(const double *__restrict__ pa, long lo
             rb[q] = b_ok ? (BT ? pb[(long long)brow * ldb + l] : pb[(long long)l * ldb + brow]) : 0.0;
         }
     };
-    Acc44 acc44[NI][NJ];  // (sml_mfma44.hpp)
+    d4 acc[NI][NJ];
 #pragma unroll
     for (int i = 0; i < NI; ++i)
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) acc44[i][j] = acc44_zero();
+        for (int j = 0; j < NJ; ++j) acc[i][j] = d4{0, 0, 0, 0};
     fetch(0);
     for (int t0 = 0; t0 < K; t0 += kKC) {
         __syncthreads();
@@ -368,32 +359,24 @@ __device__ __forceinline__ void gemm_tile(const double *__restrict__ pa, long lo
 #pragma unroll
             for (int j = 0; j < NJ; ++j) b[j] = sB[4 * s + kk][wc * (TC / 2) + j * 16 + l16];
 #pragma unroll
-            for (int j = 0; j < NJ; ++j) {
-                const B44 bj = b44(b[j]);
+            for (int i = 0; i < NI; ++i)
 #pragma unroll
-                for (int i = 0; i < NI; ++i) mfma44(a[i], bj, acc44[i][j]);
-            }
+                for (int j = 0; j < NJ; ++j) acc[i][j] = MFMA64(a[i], b[j], acc[i][j]);
         }
     }
-    static_assert(kKC * (TR + kLdsPad) >= 4 * 256, "the relayout scratch (a wave's 256 doubles) lives in sA");
-    __syncthreads();  // every wave past its last read of sA
-    double *scr = &sA[0][0] + w * 256;
-
 #pragma unroll
     for (int i = 0; i < NI; ++i)
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-            const d4 acc = acc44_to_d4(acc44[i][j], scr);
+        for (int j = 0; j < NJ; ++j)
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const int row = wr * (TR / 2) + i * 16 + kk + 4 * q;
                 const int col = wc * (TC / 2) + j * 16 + l16;
                 if (row < arows && col < brows) {
                     double *p = po + (long long)col * ldo + row;
-                    *p = (accumulate ? *p : 0.0) + alpha * acc[q];
+                    *p = (accumulate ? *p : 0.0) + alpha * acc[i][j][q];
                 }
             }
-        }
 }
 
 constexpr int kDiagThreads = 1024;            // 8 threads per row of the diagonal block
@@ -535,11 +518,11 @@ __device__ __forceinline__ void gemm_rhs(const double *__restrict__ pa, long lon
             rb[q] = c < nb ? pb[(long long)c * ldb + t0 + (idx & 15)] : 0.0;
         }
     };
-    Acc44 acc44[2][NJ];  // (sml_mfma44.hpp)
+    d4 acc[2][NJ];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) acc44[i][j] = acc44_zero();
+        for (int j = 0; j < NJ; ++j) acc[i][j] = d4{0, 0, 0, 0};
     fetch(0);
     for (int t0 = 0; t0 < K; t0 += kKC) {
         __syncthreads();
@@ -551,34 +534,29 @@ __device__ __forceinline__ void gemm_rhs(const double *__restrict__ pa, long lon
         if (t0 + kKC < K) fetch(t0 + kKC);
 #pragma unroll
         for (int s = 0; s < kKC / 4; ++s) {
-            double a[2];
+            double a[2], b[NJ];
 #pragma unroll
             for (int i = 0; i < 2; ++i) a[i] = sA[4 * s + kk][w * 32 + i * 16 + l16];
 #pragma unroll
-            for (int j = 0; j < NJ; ++j) {  // (b read per column tile: 9 of them would not fit beside 18 tiles)
-                const B44 bj = b44(sB[4 * s + kk][j * 16 + l16]);
+            for (int j = 0; j < NJ; ++j) b[j] = sB[4 * s + kk][j * 16 + l16];
 #pragma unroll
-                for (int i = 0; i < 2; ++i) mfma44(a[i], bj, acc44[i][j]);
-            }
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < NJ; ++j) acc[i][j] = MFMA64(a[i], b[j], acc[i][j]);
         }
     }
-    __syncthreads();  // every wave past its last read of sA (the relayout scratch)
-    double *scr = &sA[0][0] + w * 256;
-
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-            const d4 acc = acc44_to_d4(acc44[i][j], scr);
+        for (int j = 0; j < NJ; ++j)
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const int row = w * 32 + i * 16 + kk + 4 * q, col = j * 16 + l16;
                 if (col < nb) {
                     double *p = po + (long long)col * ldo + row;
-                    *p = (accumulate ? *p : 0.0) + alpha * acc[q];
+                    *p = (accumulate ? *p : 0.0) + alpha * acc[i][j][q];
                 }
             }
-        }
 }
 
 // Block k of the triangular solves on B (npad x nout per region, column-major), in

@@ -53,15 +53,52 @@ __global__ __launch_bounds__(256) void k4(int iters, double *sink, long long *st
     }
 }
 
-template <int NACC, bool kSmall = false>
+// a GEMM-like issue pattern: 4 A x 4 B operand registers, 16 accumulators, every
+// MFMA a different (a, b) pair (the training kernels' inner loop)
+template <int NACC>
+__global__ __launch_bounds__(256) void k4g(int iters, double *sink, long long *st) {
+    double acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = 0.0;
+    double a[4], b[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        a[i] = 1.0 + (threadIdx.x + i) * 1e-9;
+        b[i] = 1.0 - (threadIdx.x + i) * 1e-9;
+    }
+    long long c0 = clock64(), r0 = wall_clock64();
+    for (int it = 0; it < iters; ++it) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f64_4x4x4f64(a[i], b[j], acc[i][j], 0, 0, 0);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a[i] = __builtin_amdgcn_mov_dpp(0, 0, 0xf, 0xf, false) * 0.0 + a[i];
+    }
+    double s = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) s += acc[i][j];
+    if (s == 12345.678) sink[0] = s;
+    if (threadIdx.x == 0) {
+        st[2 * blockIdx.x] = clock64() - c0;
+        st[2 * blockIdx.x + 1] = wall_clock64() - r0;
+    }
+}
+
+template <int NACC, int kKind = 0>
 void run(int ncu, int wps) {
+    constexpr bool kSmall = kKind != 0;
     const int blocks = ncu * wps;  // 256 threads = 1 wave per SIMD per block
     double *sink;
     long long *st;
     hipMalloc(&sink, 8);
     hipMalloc(&st, 2 * blocks * sizeof(long long));
     const int iters = 20000;
-    auto kern = kSmall ? k4<NACC> : k<NACC>;
+    auto kern = kKind == 2 ? k4g<NACC> : kKind == 1 ? k4<NACC> : k<NACC>;
     hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, 0, iters / 10, sink, st);
     hipEvent_t e0, e1;
     hipEventCreate(&e0);
@@ -80,7 +117,7 @@ void run(int ncu, int wps) {
     std::sort(f.begin(), f.end());
     const double flops = (double)blocks * 4 * iters * NACC * 2.0 * 16 * 16 * 4;  // 4x4x4 x 16 blocks: the same 2048
     printf("%s NACC %2d  waves/SIMD %d: %7.2f TFLOP/s, clock %.3f GHz, %.1f clk per MFMA per SIMD\n",
-           kSmall ? "4x4x4  " : "16x16x4", NACC, wps, flops / (ms * 1e-3) / 1e12, f[f.size() / 2],
+           kKind == 2 ? "4x4x4 g" : kSmall ? "4x4x4  " : "16x16x4", NACC, wps, flops / (ms * 1e-3) / 1e12, f[f.size() / 2],
            (double)ms * 1e-3 * f[f.size() / 2] * 1e9 / ((double)iters * NACC * wps));
     hipFree(sink);
     hipFree(st);
@@ -93,8 +130,9 @@ int main() {
         run<4>(ncu, wps);
         run<8>(ncu, wps);
         run<16>(ncu, wps);
-        run<8, true>(ncu, wps);
-        run<16, true>(ncu, wps);
+        run<8, 1>(ncu, wps);
+        run<16, 1>(ncu, wps);
+        run<16, 2>(ncu, wps);
     }
     return 0;
 }
