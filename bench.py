@@ -278,8 +278,18 @@ def main():
     exchange = OutvecExchange(nreg, world, rank, device=dev, nout=136 + (4 if args.slab else 0))
     if sim > 1:  # rank 0 of `sim` ranks: its outvecs into a global array, the others stale
         glob_sim = torch.zeros((nreg, 136 + (4 if args.slab else 0)), dtype=torch.float64, device=dev)
+        sim_filled = []
 
         def exchange(ov_local):
+            if not sim_filled:
+                # the other ranks' rows once, from this rank's first outvecs repeated (every
+                # region's row has the same variable layout): the assembled state stays in
+                # iogrid's safe range, so the window's entry check passes and run_model's
+                # exit takes the integrated path, as on a real rank
+                nl = len(regions)
+                idx = torch.arange(nreg, device=dev) % nl
+                glob_sim.copy_(ov_local[idx])
+                sim_filled.append(True)
             glob_sim[:len(regions)].copy_(ov_local)
             return glob_sim
     g4h, g2h, prh = synthetic_grids(11)
@@ -373,7 +383,7 @@ def main():
     for _ in range(args.warmup):
         step()
     loop.sync()
-    poll = args.poll_run_speedy and sim == 1  # (--sim-ranks: the other ranks' rows are stale, the check fails)
+    poll = args.poll_run_speedy
     dt = timed(step_polled if poll else step, args.steps, timing=True)
     upd_ms, rd_ms = res.kernel_times()
     steps_done = ran[0]
@@ -399,7 +409,7 @@ def main():
     rd_avg_s = float(np.mean(rd_ms)) * 1e-3
     upd_avg_s = float(np.mean(upd_ms)) * 1e-3
     achieved = rd_bytes / rd_avg_s / 1e9
-    upd_bytes = sum(8 * (2 + wb) * s.n + (2 + wb) * s.n + 3 * 8 * s.n + 8 * s.ninp for s in sizes)
+    upd_bytes = sum(8 * (2 + wb) * s.n + (2 + wb) * s.n + 2 * 8 * s.n + 8 * s.ninp for s in sizes)
     _, algo_step = res.footprint()
     traffic = None
     pmc_path = os.path.join(REPO, "profiles", "readout_pmc.json")

@@ -582,15 +582,20 @@ int sml_hybrid_exchange_width(const sml_hybrid *h, int *width);
 int sml_hybrid_slab_buffers(const sml_hybrid *h, const double **d_sst_grid, const double **d_ring, int *ring_len,
                             const double **d_slab_feedback, const double **d_slab_outvec);
 /* the two cross-stream dependencies of the overlapped loop: SML_HOP_WAIT_VALUE (a
- * sequence number written by the producer's stream, waited for by the consumer's:
- * 3.9 us), SML_HOP_EVENTS (event record + wait: 10 us), or SML_HOP_AUTO (the
- * default: wait-value, but events when dispatch is serialised -- AMD_SERIALIZE_KERNEL
- * or rocprofv3's counter collection -- where a wait-value packet could stall its
- * queue ahead of its producer; SML_HYBRID_EVENTS=1 also selects events).  Drains both
- * streams before switching. */
+ * sequence number written by the producer's stream, waited for by the consumer's, as
+ * CP stream memory operations), SML_HOP_EVENTS (event record + wait), SML_HOP_KERNEL
+ * (the same sequence number, stored by a one-lane kernel behind the producer and
+ * polled by a one-lane kernel ahead of the consumer; a wait that has not seen its
+ * value after ~4 s gives up and sml_hybrid_sync returns SML_ERR_STATE), or
+ * SML_HOP_AUTO (the default: wait-value, but events when dispatch is serialised --
+ * AMD_SERIALIZE_KERNEL or rocprofv3's counter collection -- where a waiting packet or
+ * kernel could stall its queue ahead of its producer; SML_HYBRID_EVENTS=1 also
+ * selects events, SML_HYBRID_HOPK=1 kernel hops).  Drains both streams before
+ * switching. */
 #define SML_HOP_AUTO 0
 #define SML_HOP_WAIT_VALUE 1
 #define SML_HOP_EVENTS 2
+#define SML_HOP_KERNEL 3
 int sml_hybrid_set_hop_mode(sml_hybrid *h, int mode);
 int sml_hybrid_hop_mode(const sml_hybrid *h, int *requested, int *effective);
 /* pipelined loop (default off): each advance also issues the NEXT step's reservoir

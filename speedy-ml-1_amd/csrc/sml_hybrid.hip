@@ -62,7 +62,12 @@ struct sml_hybrid {
     // producer: SML_HOP_AUTO then takes event hops (sml_hybrid_set_hop_mode).
     // (the chain on SPEEDY's stream, SML_CHAIN_SPEEDY, hops the other way: grid_t,
     // side -> main, before the re-tiling; begun_t, main -> side, before the finish)
+    // SML_HOP_KERNEL: the same sequence numbers, written by a one-lane kernel behind the
+    // producer and polled by a one-lane kernel ahead of the consumer (k_hop_signal /
+    // k_hop_wait): ordinary dispatches, where the CP's stream operations run as blit
+    // kernels with ~6 us of their own and a ~6 us boundary in front
     enum { kHopGrid = 0, kHopLm = 1, kHopBegun = 2, kHops = 3 };
+    static constexpr int kSeqStride = 16;  // one 128-B line per hop's word; the late word after them
     hipEvent_t ev[kHops] = {nullptr, nullptr, nullptr};
     uint64_t *d_seq = nullptr, seq[kHops] = {0, 0, 0};
     // where the step's serial chain runs (sml_hybrid_set_chain): false, the two-stream
@@ -74,7 +79,7 @@ struct sml_hybrid {
     // begin, which need the assembled grid, are the main stream's)
     int chain_mode = SML_CHAIN_AUTO;
     bool chain = false;
-    bool use_events = false;
+    bool use_events = false, use_kernels = false;
     int hop_mode = SML_HOP_AUTO;
     // caller-owned device buffers
     double *fb = nullptr, *lm = nullptr, *ov = nullptr, *g4 = nullptr, *g2 = nullptr, *pr = nullptr, *f4 = nullptr,
@@ -393,22 +398,57 @@ extern "C" int sml_tisr_date_index(int startyear, int64_t hours_elapsed, int *fe
 // ------------------------------------------------------------------ hybrid loop
 namespace {
 
+// SML_HOP_KERNEL's two kernels.  The producer's data is released by its own kernel's
+// end (the dispatch after it on the same stream starts behind that release), so the
+// signal is one relaxed agent-scope store of the sequence number (a vector store,
+// write-through: MI355X_MICROARCH.md inter-workgroup visibility), and the consumer's
+// next dispatch acquires at its start like any kernel's.  The wait polls with relaxed
+// agent loads and s_sleep from one lane; it never spins forever: after ~4 s it marks
+// the late word (sml_hybrid_sync reports it) and lets the stream go on.
+__global__ void k_hop_signal(uint64_t *flag, uint64_t v) {
+    if (threadIdx.x == 0) __hip_atomic_store(flag, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ void k_hop_wait(const uint64_t *flag, uint64_t v, unsigned *late) {
+    if (threadIdx.x != 0) return;
+    const long long t0 = wall_clock64();
+    while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < v) {
+        __builtin_amdgcn_s_sleep(1);
+        if (wall_clock64() - t0 > 400000000ll) {  // ~4 s at wall_clock64's 100 MHz
+            __hip_atomic_store(late, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+        }
+    }
+}
+
+unsigned *hop_late_word(sml_hybrid *h) {
+    return reinterpret_cast<unsigned *>(h->d_seq + sml_hybrid::kHops * sml_hybrid::kSeqStride);
+}
+
 // producer side of hop `k`: ordered after everything issued on `s` so far
 int hop_signal(sml_hybrid *h, int k, hipStream_t s) {
+    uint64_t *w = h->d_seq + k * sml_hybrid::kSeqStride;
     if (h->use_events) {
         SML_HIP(hipEventRecord(h->ev[k], s));
+    } else if (h->use_kernels) {
+        hipLaunchKernelGGL(k_hop_signal, dim3(1), dim3(64), 0, s, w, ++h->seq[k]);
+        SML_HIP(hipGetLastError());
     } else {
-        SML_HIP(hipStreamWriteValue64(s, h->d_seq + k, ++h->seq[k], 0));
+        SML_HIP(hipStreamWriteValue64(s, w, ++h->seq[k], 0));
     }
     return SML_OK;
 }
 
 // consumer side: `s` waits for the latest signal of hop `k`
 int hop_wait(sml_hybrid *h, int k, hipStream_t s) {
+    uint64_t *w = h->d_seq + k * sml_hybrid::kSeqStride;
     if (h->use_events) {
         SML_HIP(hipStreamWaitEvent(s, h->ev[k], 0));
+    } else if (h->use_kernels) {
+        hipLaunchKernelGGL(k_hop_wait, dim3(1), dim3(64), 0, s, w, h->seq[k], hop_late_word(h));
+        SML_HIP(hipGetLastError());
     } else {
-        SML_HIP(hipStreamWaitValue64(s, h->d_seq + k, h->seq[k], hipStreamWaitValueGte, ~0ull));
+        SML_HIP(hipStreamWaitValue64(s, w, h->seq[k], hipStreamWaitValueGte, ~0ull));
     }
     return SML_OK;
 }
@@ -450,15 +490,19 @@ bool dispatch_serialised() { return env_on("AMD_SERIALIZE_KERNEL") || env_on("RO
 // SML_HYBRID_EVENTS=1), SML_HOP_WAIT_VALUE, SML_HOP_EVENTS.  Both streams are drained
 // first, so no wait of one kind is left pending on a signal of the other.
 extern "C" int sml_hybrid_set_hop_mode(sml_hybrid *h, int mode) {
-    SML_REQUIRE(h && (mode == SML_HOP_AUTO || mode == SML_HOP_WAIT_VALUE || mode == SML_HOP_EVENTS),
+    SML_REQUIRE(h && (mode == SML_HOP_AUTO || mode == SML_HOP_WAIT_VALUE || mode == SML_HOP_EVENTS ||
+                      mode == SML_HOP_KERNEL),
                 "bad hop mode %d", mode);
     if (h->main) SML_HIP(hipStreamSynchronize(h->main));
     if (h->side && h->side != h->main) SML_HIP(hipStreamSynchronize(h->side));
     h->hop_mode = mode;
-    if (mode == SML_HOP_AUTO)
+    if (mode == SML_HOP_AUTO) {
         h->use_events = env_on("SML_HYBRID_EVENTS") || dispatch_serialised();
-    else
+        h->use_kernels = !h->use_events && env_on("SML_HYBRID_HOPK");
+    } else {
         h->use_events = mode == SML_HOP_EVENTS;
+        h->use_kernels = mode == SML_HOP_KERNEL;
+    }
     return SML_OK;
 }
 
@@ -523,7 +567,7 @@ extern "C" int sml_hybrid_set_force_exchange(sml_hybrid *h, int on) {
 extern "C" int sml_hybrid_hop_mode(const sml_hybrid *h, int *requested, int *effective) {
     SML_REQUIRE(h, "null context");
     if (requested) *requested = h->hop_mode;
-    if (effective) *effective = h->use_events ? SML_HOP_EVENTS : SML_HOP_WAIT_VALUE;
+    if (effective) *effective = h->use_events ? SML_HOP_EVENTS : h->use_kernels ? SML_HOP_KERNEL : SML_HOP_WAIT_VALUE;
     return SML_OK;
 }
 
@@ -624,8 +668,9 @@ extern "C" int sml_hybrid_create(sml_reservoirs *res, sml_dynamics *dyn, sml_com
     for (hipEvent_t &e : h->ev)
         if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return bail(fail(SML_ERR_HIP, "event"));
     if (int rc = sml_hybrid_set_hop_mode(h, SML_HOP_AUTO)) return bail(rc);
-    if (hipMalloc(&h->d_seq, sml_hybrid::kHops * sizeof(uint64_t)) != hipSuccess ||
-        hipMemset(h->d_seq, 0, sml_hybrid::kHops * sizeof(uint64_t)) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
+    constexpr size_t seq_bytes = (sml_hybrid::kHops + 1) * sml_hybrid::kSeqStride * sizeof(uint64_t);
+    if (hipMalloc(&h->d_seq, seq_bytes) != hipSuccess || hipMemset(h->d_seq, 0, seq_bytes) != hipSuccess ||
+        hipDeviceSynchronize() != hipSuccess)
         return bail(fail(SML_ERR_HIP, "sequence counters"));
     h->xw = h->nout;
     if (world > 1) {
@@ -977,6 +1022,13 @@ int predict_impl(sml_hybrid *h, bool assemble) {
             xs = h->side;
             if (int rc = hop_signal(h, sml_hybrid::kHopBegun, h->main)) return rc;
             if (int rc = hop_wait(h, sml_hybrid::kHopBegun, xs)) return rc;
+        } else if (h->use_kernels && h->nlocal > 0) {
+            // SPEEDY's forecast of the previous window, waited for inside the finish: its
+            // weights load while the window runs (k_res_finish_grid's wflag; the main
+            // stream's later work still follows the finish, so it follows the window too)
+            if (int rc = sml::res_finish_wait(h->res, h->d_seq + sml_hybrid::kHopLm * sml_hybrid::kSeqStride,
+                                              h->seq[sml_hybrid::kHopLm], hop_late_word(h)))
+                return rc;
         } else if (int rc = hop_wait(h, sml_hybrid::kHopLm, h->main)) {  // SPEEDY's forecast of the previous window
             return rc;
         }
@@ -1139,6 +1191,15 @@ extern "C" int sml_hybrid_sync(sml_hybrid *h) {
     }
     SML_HIP(hipStreamSynchronize(h->main));
     SML_HIP(hipStreamSynchronize(h->side));
+    if (h->use_kernels) {  // a kernel hop that gave up waiting: the consumer ran on stale data
+        unsigned late = 0;
+        SML_HIP(hipMemcpy(&late, hop_late_word(h), sizeof(late), hipMemcpyDeviceToHost));
+        if (late) {
+            SML_HIP(hipMemset(hop_late_word(h), 0, sizeof(late)));
+            return fail(SML_ERR_STATE, "a cross-stream hop (SML_HOP_KERNEL) timed out: the steps since the last "
+                                       "sync ran on stale data");
+        }
+    }
     return sml::dyn_check_late(h->dyn);
 }
 

@@ -20,6 +20,9 @@ namespace sml {
 bool res_in_global_order(const sml_reservoirs *c);
 // sml_dynamics: the run_model exit's safety-check hand-off timed out (SML_ERR_STATE)
 int dyn_check_late(sml_dynamics *d);
+// the next sml_res_step_finish_grid / _finish_assemble launch waits in-kernel until
+// *flag >= value (device words; *late set if it gave up), its weights loaded first
+int res_finish_wait(sml_reservoirs *c, const uint64_t *flag, uint64_t value, unsigned *late);
 
 // --------------------------------------------------------------- geometry
 // Restatement of the res_domain.f90 decomposition used by every reservoir of the

@@ -80,7 +80,7 @@ struct sml_reservoirs {
     std::vector<RegionDev> rd;
     int64_t tot_wlm = 0;  // elements of the transposed local-model blocks (pool d_wlm)
     void *d_wlm = nullptr;
-    int64_t tot_a_rp = 0, tot_a_nz = 0, tot_w_rp = 0, tot_w_nz = 0, tot_wout = 0, tot_x = 0, tot_xaug = 0,
+    int64_t tot_a_rp = 0, tot_a_nz = 0, tot_w_rp = 0, tot_w_nz = 0, tot_wout = 0, tot_xaug = 0,
             tot_fb = 0;
     std::vector<int64_t> w_nz_cap;  // reserved W_in CSR nnz per region (n at create: one entry per row as
                                     // trained; grow_win_pool re-lays the pool for a denser W_in)
@@ -98,7 +98,7 @@ struct sml_reservoirs {
     void *d_a_ell_val = nullptr, *d_w_ell_val = nullptr;
     double *d_x[2] = {nullptr, nullptr};
     int cur = 0;
-    double *d_xaug = nullptr, *d_meanstd = nullptr;
+    double *d_meanstd = nullptr;
     double *d_part = nullptr;       // [nlocal][nout_pad] W_out(:, ncs+1:) x~ of the step in flight
     // cap on the waves of the v_ml readout (the half that runs beside SPEEDY's window;
     // 0: one wave per item).  Sharing CUs with SPEEDY, uncapped it takes ~6 TB/s and
@@ -123,6 +123,10 @@ struct sml_reservoirs {
     // launches get, sml_res_set_update_cus; 0 = every CU of the device)
     bool upd_bal = true;
     bool finish_ungrouped = false;  // SML_FIN_UNGROUPED=1 at create: the finish one thread per output (A/B)
+    // the next grid finish waits in-kernel for *fin_wflag >= fin_wval (sml::res_finish_wait)
+    const uint64_t *fin_wflag = nullptr;
+    uint64_t fin_wval = 0;
+    unsigned *fin_wlate = nullptr;
     int upd_cus = 0, bal_grid = 0, ncu = 0;
     int ell_ok = -1;  // every local region's A and W_in in ELL form (-1: recount after a load)
     int32_t *d_row0 = nullptr, *d_blk_r0 = nullptr;
@@ -258,8 +262,8 @@ __device__ __attribute__((always_inline)) inline void update_block(
     int lb, double *smem, const RegionDev *__restrict__ R, const int32_t *__restrict__ a_rp,
     const uint16_t *__restrict__ a_col, const WT *__restrict__ a_val, const int32_t *__restrict__ w_rp,
     const uint16_t *__restrict__ w_col, const WT *__restrict__ w_val, const Ell &ell,
-    const double *__restrict__ x_old, double *__restrict__ x_new, double *__restrict__ xaug,
-    const double *__restrict__ feedback, int ncs, double leak, int parts, int lds_x) {
+    const double *__restrict__ x_old, double *__restrict__ x_new,
+    const double *__restrict__ feedback, double leak, int parts, int lds_x) {
     const int r = lb / parts, part = lb % parts;
     const RegionDev rg = R[r];
     const int n = rg.n, tid = threadIdx.x;
@@ -309,8 +313,7 @@ __device__ __attribute__((always_inline)) inline void update_block(
             }
             const double xn = res_tanh(y + t);
             const double xv = (1.0 - leak) * xs[i] + leak * xn;
-            x_new[rg.x + i] = xv;
-            xaug[rg.xaug + ncs + i] = (i & 1) ? xv * xv : xv;  // x_temp(2:n:2)**2 (1-based even)
+            x_new[rg.x + i] = xv;  // (x~ = x with x(2:n:2)**2: squared by the readout's loads, rd_x)
         }
         cur = nxt;
     }
@@ -325,15 +328,14 @@ __global__ __launch_bounds__(kUpdThreads, kMinW) void k_res_update(
     const RegionDev *__restrict__ R, const int32_t *__restrict__ a_rp, const uint16_t *__restrict__ a_col,
     const WT *__restrict__ a_val, const int32_t *__restrict__ w_rp, const uint16_t *__restrict__ w_col,
     const WT *__restrict__ w_val, Ell ell, const double *__restrict__ x_old, double *__restrict__ x_new,
-    double *__restrict__ xaug, const double *__restrict__ feedback, int ncs,
-    double leak, int parts, int lds_x, int nlog) {
+    const double *__restrict__ feedback, double leak, int parts, int lds_x, int nlog) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const int off = xcd_remap(blockIdx.x, gridDim.x);
     for (int base = 0; base < nlog; base += gridDim.x) {
         const int lb = base + off;
         if (lb < nlog)  // block-uniform
-            update_block<WT, kLds>(lb, smem, R, a_rp, a_col, a_val, w_rp, w_col, w_val, ell, x_old, x_new, xaug,
-                                   feedback, ncs, leak, parts, lds_x);
+            update_block<WT, kLds>(lb, smem, R, a_rp, a_col, a_val, w_rp, w_col, w_val, ell, x_old, x_new,
+                                   feedback, leak, parts, lds_x);
         if (base + (int)gridDim.x < nlog) __syncthreads();  // the block's LDS, reused next round
     }
 }
@@ -369,8 +371,8 @@ struct StageRegs {
 template <typename WT>
 __global__ __launch_bounds__(kUpdThreads, 4) void k_res_update_bal(
     const RegionDev *__restrict__ R, const int32_t *__restrict__ row0, const int32_t *__restrict__ blk_r0, int nlocal,
-    int64_t total, Ell ell, const double *__restrict__ x_old, double *__restrict__ x_new, double *__restrict__ xaug,
-    const double *__restrict__ feedback, int ncs, double leak, int lds_x, int lds_buf) {
+    int64_t total, Ell ell, const double *__restrict__ x_old, double *__restrict__ x_new,
+    const double *__restrict__ feedback, double leak, int lds_x, int lds_buf) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const int G = gridDim.x;
     const int b = xcd_remap(blockIdx.x, G);
@@ -443,7 +445,6 @@ __global__ __launch_bounds__(kUpdThreads, 4) void k_res_update_bal(
                 const double xn = res_tanh(y + t);
                 const double xv = (1.0 - leak) * xs[i] + leak * xn;
                 x_new[rg.x + i] = xv;
-                xaug[rg.xaug + ncs + i] = (i & 1) ? xv * xv : xv;  // x_temp(2:n:2)**2 (1-based even)
             }
         }
         if (newseg) {  // the other buffer: its last reader (segment P0.seg - 1) finished before the last barrier
@@ -586,10 +587,24 @@ __device__ inline double unstd(double v, const double *ms, int l) {
     return v;
 }
 
+// x~ over the columns j .. j + 3 of a region's ld-wide row (xr: the row's start; the
+// state x sits from column ncs on): x_aug = [local_model; x~], x~ = x with its 1-based
+// even entries squared (x_temp(2:n:2)**2, mod_reservoir.f90:1452-1455), the columns
+// below ncs zero.  The squares are formed here, where x~ is consumed, instead of in a
+// copy written by the update (the same multiply, so the same bits)
+__device__ __attribute__((always_inline)) inline double4 rd_x(const double *xr, int j, int ncs) {
+    double4 v = *reinterpret_cast<const double4 *>(xr + j);
+    auto f = [&](double x, int c) {
+        const int i = j + c - ncs;  // 0-based state index
+        return i < 0 ? 0.0 : (i & 1) ? x * x : x;
+    };
+    return double4{f(v.x, 0), f(v.y, 1), f(v.z, 2), f(v.w, 3)};
+}
+
 template <typename WT, int kMode, int NR>
 __global__ __launch_bounds__(512) void k_res_readout(const RegionDev *__restrict__ R, const WT *__restrict__ wout,
                                                      const WT *__restrict__ wlm,
-                                                     const double *__restrict__ xaug,
+                                                     const double *__restrict__ xst,
                                                      const double *__restrict__ local_model,
                                                      const double *__restrict__ meanstd,
                                                      const int8_t *__restrict__ outl, double *__restrict__ part,
@@ -612,18 +627,9 @@ __global__ __launch_bounds__(512) void k_res_readout(const RegionDev *__restrict
         const int ld = rg.ld;
         const WT *W = wout + rg.wout + (size_t)(g * NR) * ld;
         Rows<NR> ml{};
-        {   // v_ml: x~ from x_aug, columns ncs .. ld
-            const double *xa = xaug + rg.xaug;
-            ml = rows_dot<WT, NR>(W, ld, lane, ncs & ~(kLdAlign - 1), ld, [=](int j) {
-                double4 xv = *reinterpret_cast<const double4 *>(xa + j);
-                if (j < ncs) {  // the groups below column ncs (from the aligned start)
-                    if (j + 0 < ncs) xv.x = 0.0;
-                    if (j + 1 < ncs) xv.y = 0.0;
-                    if (j + 2 < ncs) xv.z = 0.0;
-                    if (j + 3 < ncs) xv.w = 0.0;
-                }
-                return xv;
-            });
+        {   // v_ml: x~ from the state, columns ncs .. ld (zero below ncs from the aligned start)
+            const double *xa = xst + rg.xaug;
+            ml = rows_dot<WT, NR>(W, ld, lane, ncs & ~(kLdAlign - 1), ld, [=](int j) { return rd_x(xa, j, ncs); });
         }
         const int o0 = g * NR;
         if (kMode == kReadML) {  // every lane holds all 8 sums after the butterfly; lane 0 writes them
@@ -660,30 +666,21 @@ __global__ __launch_bounds__(kBeginThreads, kMinWaves) void k_res_begin(
     const RegionDev *__restrict__ R, const int32_t *__restrict__ a_rp, const uint16_t *__restrict__ a_col,
     const WT *__restrict__ a_val, const int32_t *__restrict__ w_rp, const uint16_t *__restrict__ w_col,
     const WT *__restrict__ w_val, Ell ell, const double *__restrict__ x_old, double *__restrict__ x_new,
-    double *__restrict__ xaug, const double *__restrict__ feedback, int ncs, double leak, int lds_x,
-    const WT *__restrict__ wout, double *__restrict__ part, int nout_pad, int groups) {
+    const double *__restrict__ feedback, int ncs, double leak, int lds_x, const WT *__restrict__ wout, double *__restrict__ part, int nout_pad, int groups) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const int r = blockIdx.x;
     update_block<WT, true, kBeginThreads>(r, smem, R, a_rp, a_col, a_val, w_rp, w_col, w_val, ell, x_old, x_new,
-                                          xaug, feedback, ncs, leak, 1, lds_x);
-    __syncthreads();  // the region's x_aug complete (workgroup scope)
+                                          feedback, leak, 1, lds_x);
+    __syncthreads();  // the region's new state complete (workgroup scope)
     const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
     if (g >= groups) return;  // wave-uniform
     const RegionDev rg = R[r];
     const int ld = rg.ld;
     const WT *W = wout + rg.wout + (size_t)(g * kRowsWide) * ld;
-    const double *xa = xaug + rg.xaug;
+    const double *xa = x_new + rg.xaug;
     // k_res_readout<kReadML>'s item (r, g): the same x~ loads (zero below ncs)
-    const Rows<kRowsWide> ml = rows_dot<WT, kRowsWide, kUnroll>(W, ld, lane, ncs & ~(kLdAlign - 1), ld, [=](int j) {
-        double4 xv = *reinterpret_cast<const double4 *>(xa + j);
-        if (j < ncs) {
-            if (j + 0 < ncs) xv.x = 0.0;
-            if (j + 1 < ncs) xv.y = 0.0;
-            if (j + 2 < ncs) xv.z = 0.0;
-            if (j + 3 < ncs) xv.w = 0.0;
-        }
-        return xv;
-    });
+    const Rows<kRowsWide> ml = rows_dot<WT, kRowsWide, kUnroll>(W, ld, lane, ncs & ~(kLdAlign - 1), ld,
+                                                                [=](int j) { return rd_x(xa, j, ncs); });
     if (lane == 0) {
 #pragma unroll
         for (int q = 0; q < kRowsWide; ++q) part[(size_t)r * nout_pad + g * kRowsWide + q] = ml.v[q];
@@ -757,6 +754,15 @@ __device__ inline Quad<WT> load_quad(const WT *p) {
 // column) issued before the local-model gather, so they fly while the forecast is
 // read; the kFinGroups partial sums meet in LDS and are added in group order
 // (vp_sum's order).  Else one thread per output with vp_sum.
+//
+// wflag (may be null): the forecast grids come from another stream, whose one-lane
+// signal kernel stores a sequence number >= wval behind SPEEDY's exit (SML_HOP_KERNEL;
+// sml_hybrid.hip k_hop_signal).  The kernel then goes in ahead of the forecast: its
+// W_out(:, 1:ncs) block, the gather's tables and mean / std are loaded while the window
+// still runs, and only the forecast values wait -- one relaxed poll by one lane,
+// one agent-scope acquire by that wave, a barrier (MI355X_MICROARCH.md
+// inter-workgroup visibility, the consumer form), then plain loads.  The poll gives
+// up after ~4 s, marks *wlate and goes on (sml_hybrid_sync reports it).
 template <typename WT, bool kAsm = false, bool kGrouped = true>
 __global__ __launch_bounds__(256) void k_res_finish_grid(
     const RegionDev *__restrict__ R, const WT *__restrict__ wlm, const int32_t *__restrict__ src,
@@ -764,7 +770,8 @@ __global__ __launch_bounds__(256) void k_res_finish_grid(
     double *__restrict__ lm_out, const double *__restrict__ meanstd, const int8_t *__restrict__ outl,
     const double *__restrict__ part, double *__restrict__ outvec, int nout, int ov_ld, int nout_pad, int ncs,
     const int32_t *__restrict__ asm_dst = nullptr, double *__restrict__ g4 = nullptr, double *__restrict__ g2 = nullptr,
-    double *__restrict__ pr = nullptr) {
+    double *__restrict__ pr = nullptr, const uint64_t *__restrict__ wflag = nullptr, uint64_t wval = 0,
+    unsigned *__restrict__ wlate = nullptr) {
     __shared__ double slm[kMaxNcs];
     __shared__ double red[kGrouped ? kFinGroups * 144 : 1];
     const int r = blockIdx.x, t = threadIdx.x;
@@ -783,15 +790,38 @@ __global__ __launch_bounds__(256) void k_res_finish_grid(
         for (int jj = 0; jj < kFinGsz; ++jj)
             w[jj] = load_quad(wl + (size_t)min(gq * gsz + jj, jlast) * nout_pad + 4 * q);
     }
-    for (int j = t; j < ncs; j += blockDim.x) {
-        const int e = r * ncs + j;
-        const int s = src[e];
-        const double v = s < kGrid4d ? fc4[s] : fc2[s - kGrid4d];
+    // the gather's tables and standardization (ncs <= kMaxNcs = blockDim: one entry per thread)
+    const bool gj = t < ncs;
+    int gs = 0;
+    double gmean = 0.0, gstd = 1.0;
+    if (gj) {
+        const int e = r * ncs + t;
+        gs = src[e];
         const int l = lidx[e];
-        const double d = v - ms[l];
-        const double x = d / ms[kMeanStd + l];
-        slm[j] = x;
-        if (lm_out) lm_out[e] = x;
+        gmean = ms[l];
+        gstd = ms[kMeanStd + l];
+    }
+    if (wflag) {
+        if (t == 0) {
+            const long long c0 = wall_clock64();
+            while (__hip_atomic_load(wflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < wval) {
+                __builtin_amdgcn_s_sleep(1);
+                if (wall_clock64() - c0 > 400000000ll) {  // ~4 s at wall_clock64's 100 MHz
+                    __hip_atomic_store(wlate, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    break;
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __syncthreads();
+    }
+    if (gj) {
+        const double v = gs < kGrid4d ? fc4[gs] : fc2[gs - kGrid4d];
+        const double d = v - gmean;
+        const double x = d / gstd;
+        slm[t] = x;
+        if (lm_out) lm_out[r * ncs + t] = x;
     }
     __syncthreads();
     if constexpr (kGrouped) {
@@ -1221,7 +1251,7 @@ extern "C" int sml_res_destroy(sml_reservoirs *c) {
     for (void *p : ells)
         if (p) (void)hipFree(p);
     void *ptrs[] = {c->d_rd,    c->d_a_rp,    c->d_w_rp,   c->d_a_col,  c->d_w_col,  c->d_a_val,  c->d_w_val,
-                    c->d_wout,  c->d_x[0],    c->d_x[1],   c->d_xaug,   c->d_meanstd, c->d_outl,  c->d_asm_dst,
+                    c->d_wout,  c->d_x[0],    c->d_x[1],   c->d_meanstd, c->d_outl,  c->d_asm_dst,
                     c->d_fb_src, c->d_fb_l,   c->d_fb_reg, c->d_lm_src, c->d_lm_l,   c->d_io,     c->d_part,
                     c->d_wlm,   c->d_tisr_fb, c->d_tisr_grid, c->d_tisr_reg, c->d_row0, c->d_blk_r0};
     for (void *p : ptrs)
@@ -1346,10 +1376,13 @@ int res_create_impl(int numregions, int nlocal, const int *region_ids, const uns
         c->tot_wout += (int64_t)c->nout_pad * c->ld[i];
         r.wlm = c->tot_wlm;
         c->tot_wlm += (int64_t)c->ncs * c->nout_pad;
-        r.x = c->tot_x;
-        c->tot_x += n[i];
+        // the state's slot is the x~ column block of the region's ld-wide row (column
+        // ncs on, 32-column aligned start, zero padding after n): the readout streams
+        // x~ straight from the state the update wrote, squaring the even-numbered
+        // entries as it loads them, so the update writes 8 B per row less
         r.xaug = c->tot_xaug;
         c->tot_xaug += c->ld[i];
+        r.x = r.xaug + chunk_speedy;
         r.fb = c->tot_fb;
         c->tot_fb += c->ninp[i];
         c->maxn = std::max(c->maxn, n[i]);
@@ -1375,8 +1408,8 @@ int res_create_impl(int numregions, int nlocal, const int *region_ids, const uns
         (rc = dalloc(&c->d_w_rp, c->tot_w_rp)) || (rc = dalloc(&c->d_w_col, c->tot_w_nz)) ||
         (rc = dalloc_bytes(&c->d_w_val, c->tot_w_nz * wb)) || (rc = dalloc_wout(&c->d_wout, c->tot_wout * wb)) ||
         (rc = dalloc_bytes(&c->d_wlm, std::max<int64_t>(c->tot_wlm, 1) * wb)) ||
-        (rc = dalloc(&c->d_x[0], c->tot_x)) || (rc = dalloc(&c->d_x[1], c->tot_x)) ||
-        (rc = dalloc(&c->d_xaug, c->tot_xaug)) || (rc = dalloc(&c->d_meanstd, (size_t)nlocal * 2 * kMeanStd)) ||
+        (rc = dalloc(&c->d_x[0], c->tot_xaug)) || (rc = dalloc(&c->d_x[1], c->tot_xaug)) ||
+        (rc = dalloc(&c->d_meanstd, (size_t)nlocal * 2 * kMeanStd)) ||
         (rc = dalloc(&c->d_part, (size_t)std::max(nlocal, 1) * c->nout_pad))) {
         sml_res_destroy(c);
         return rc;
@@ -1386,9 +1419,8 @@ int res_create_impl(int numregions, int nlocal, const int *region_ids, const uns
     if (e == hipSuccess) e = hipMemset(c->d_w_rp, 0, std::max<int64_t>(c->tot_w_rp, 1) * 4);
     if (e == hipSuccess) e = hipMemset(c->d_wout, 0, std::max<int64_t>(c->tot_wout * wb, 16));
     if (e == hipSuccess) e = hipMemset(c->d_wlm, 0, std::max<int64_t>(c->tot_wlm, 1) * wb);
-    if (e == hipSuccess) e = hipMemset(c->d_x[0], 0, std::max<int64_t>(c->tot_x, 1) * 8);
-    if (e == hipSuccess) e = hipMemset(c->d_x[1], 0, std::max<int64_t>(c->tot_x, 1) * 8);
-    if (e == hipSuccess) e = hipMemset(c->d_xaug, 0, std::max<int64_t>(c->tot_xaug, 1) * 8);
+    if (e == hipSuccess) e = hipMemset(c->d_x[0], 0, std::max<int64_t>(c->tot_xaug, 1) * 8);
+    if (e == hipSuccess) e = hipMemset(c->d_x[1], 0, std::max<int64_t>(c->tot_xaug, 1) * 8);
     if (e == hipSuccess && nlocal)
         e = hipMemcpy(c->d_rd, c->rd.data(), sizeof(RegionDev) * nlocal, hipMemcpyHostToDevice);
     if (e != hipSuccess) {
@@ -1609,12 +1641,10 @@ int launch_update_bal(sml_reservoirs *c, const double *xo, double *xn, const dou
     Ell ell{c->d_a_ell_col, c->d_a_ell_val, c->d_w_ell_col, c->d_w_ell_val};
     if (c->wdtype == SML_F32)
         hipLaunchKernelGGL(k_res_update_bal<float>, dim3(G), dim3(kUpdThreads), lds, st, c->d_rd, c->d_row0,
-                           c->d_blk_r0, c->nlocal, total, ell, xo, xn, c->d_xaug, d_feedback, c->ncs, c->leakage, lds_x,
-                           lds_buf);
+                           c->d_blk_r0, c->nlocal, total, ell, xo, xn, d_feedback, c->leakage, lds_x, lds_buf);
     else
         hipLaunchKernelGGL(k_res_update_bal<double>, dim3(G), dim3(kUpdThreads), lds, st, c->d_rd, c->d_row0,
-                           c->d_blk_r0, c->nlocal, total, ell, xo, xn, c->d_xaug, d_feedback, c->ncs, c->leakage, lds_x,
-                           lds_buf);
+                           c->d_blk_r0, c->nlocal, total, ell, xo, xn, d_feedback, c->leakage, lds_x, lds_buf);
     SML_HIP(hipGetLastError());
     return SML_OK;
 }
@@ -1641,8 +1671,7 @@ int launch_update(sml_reservoirs *c, const double *xo, double *xn, const double 
 #define SML_UPD(WT, L)                                                                                            \
     hipLaunchKernelGGL(occ2 ? (k_res_update<WT, L, 8>) : (k_res_update<WT, L, 4>), ug, dim3(kUpdThreads),        \
                        L ? lds : 0, st, c->d_rd, c->d_a_rp, c->d_a_col, (const WT *)c->d_a_val, c->d_w_rp,        \
-                       c->d_w_col, (const WT *)c->d_w_val, ell, xo, xn, c->d_xaug, d_feedback, c->ncs, c->leakage, \
-                       bpr, lds_x, nlog)
+                       c->d_w_col, (const WT *)c->d_w_val, ell, xo, xn, d_feedback, c->leakage, bpr, lds_x, nlog)
     Ell ell{c->d_a_ell_col, c->d_a_ell_val, c->d_w_ell_col, c->d_w_ell_val};
     if (c->wdtype == SML_F32) {
         if (use_lds)
@@ -1681,7 +1710,7 @@ int launch_begin(sml_reservoirs *c, const double *xo, double *xn, const double *
         using WT = decltype(wt_tag);
         hipLaunchKernelGGL(kern, dim3(c->nlocal), dim3(kBeginThreads), lds, st, c->d_rd, c->d_a_rp, c->d_a_col,
                            (const WT *)c->d_a_val, c->d_w_rp, c->d_w_col, (const WT *)c->d_w_val, ell, xo, xn,
-                           c->d_xaug, d_feedback, c->ncs, c->leakage, lds_x, (const WT *)c->d_wout, c->d_part,
+                           d_feedback, c->ncs, c->leakage, lds_x, (const WT *)c->d_wout, c->d_part,
                            c->nout_pad, groups);
     };
     const bool two = begin_mode(c) == 2;
@@ -1702,9 +1731,11 @@ int check_loaded(const sml_reservoirs *c) {
     return SML_OK;
 }
 
+// xs: the state the readout's x~ comes from (the one the update just wrote; unused
+// by the finish)
 template <int kMode>
-void launch_readout(sml_reservoirs *c, const double *d_local_model, double *d_outvec, hipStream_t st,
-                    double *d_raw = nullptr) {
+void launch_readout(sml_reservoirs *c, const double *xs, const double *d_local_model, double *d_outvec,
+                    hipStream_t st, double *d_raw = nullptr) {
     if constexpr (kMode == kReadFinish) {
         const int total = c->nlocal * c->nout_pad;
         if (c->wdtype == SML_F32)
@@ -1732,7 +1763,7 @@ void launch_readout(sml_reservoirs *c, const double *d_local_model, double *d_ou
             using WT = decltype(wt_tag);
             constexpr int R = decltype(r_tag)::value;
             hipLaunchKernelGGL((k_res_readout<WT, kMode, R>), dim3(nblocks), dim3(64 * wpb), 0, st, c->d_rd,
-                               (const WT *)c->d_wout, (const WT *)c->d_wlm, c->d_xaug, d_local_model, c->d_meanstd,
+                               (const WT *)c->d_wout, (const WT *)c->d_wlm, xs, d_local_model, c->d_meanstd,
                                c->d_outl, c->d_part, d_outvec, c->nout, c->ov_ld, c->nout_pad, c->ncs, groups, nitems, ipw);
         };
         using RW = std::integral_constant<int, kRowsWide>;
@@ -1766,7 +1797,7 @@ extern "C" int sml_res_step_begin(sml_reservoirs *c, const double *d_feedback, v
     } else {
         if (int rc = launch_update(c, xo, xn, d_feedback, st, true)) return rc;  // beside SPEEDY's window
         if (rec) SML_HIP(hipEventRecord(ev[1], st));
-        launch_readout<kReadML>(c, nullptr, nullptr, st);
+        launch_readout<kReadML>(c, xn, nullptr, nullptr, st);
     }
     SML_HIP(hipGetLastError());
     if (rec) {
@@ -1804,7 +1835,7 @@ extern "C" int sml_res_step_finish(sml_reservoirs *c, const double *d_local_mode
     SML_REQUIRE(c->ncs == 0 || d_local_model, "hybrid context needs d_local_model");
     if (!c->begun) return fail(SML_ERR_STATE, "sml_res_step_finish without sml_res_step_begin");
     hipStream_t st = (hipStream_t)stream;
-    launch_readout<kReadFinish>(c, d_local_model, d_outvec, st);
+    launch_readout<kReadFinish>(c, nullptr, d_local_model, d_outvec, st);
     SML_HIP(hipGetLastError());
     c->begun = false;
     return SML_OK;
@@ -1824,7 +1855,7 @@ extern "C" int sml_res_step_slab(sml_reservoirs *c, const double *d_feedback, co
     SML_REQUIRE(c->ncs == c->nout, "predict_slab feeds its outvec back: chunk_speedy (%d) must equal nout (%d)",
                 c->ncs, c->nout);
     if (int rc = sml_res_step_begin(c, d_feedback, stream)) return rc;
-    launch_readout<kReadFinish>(c, d_local_model, d_outvec, (hipStream_t)stream, d_local_model_next);
+    launch_readout<kReadFinish>(c, nullptr, d_local_model, d_outvec, (hipStream_t)stream, d_local_model_next);
     SML_HIP(hipGetLastError());
     c->begun = false;
     return SML_OK;
@@ -1844,7 +1875,7 @@ void launch_finish_grid(sml_reservoirs *c, const double *d_fc4d, const double *d
         hipLaunchKernelGGL((k_res_finish_grid<WT, kAsm, decltype(grouped_tag)::value>), dim3(c->nlocal), dim3(256), 0,
                            st, c->d_rd, (const WT *)c->d_wlm, c->d_lm_src, c->d_lm_l, d_fc4d, d_fc2d, d_local_model,
                            c->d_meanstd, c->d_outl, c->d_part, d_outvec, c->nout, c->ov_ld, c->nout_pad, c->ncs,
-                           c->d_asm_dst, d_grid4d, d_grid2d, d_precip);
+                           c->d_asm_dst, d_grid4d, d_grid2d, d_precip, c->fin_wflag, c->fin_wval, c->fin_wlate);
     };
     using G1 = std::integral_constant<bool, true>;
     using G0 = std::integral_constant<bool, false>;
@@ -1855,8 +1886,19 @@ void launch_finish_grid(sml_reservoirs *c, const double *d_fc4d, const double *d
         if (grouped) go(double{}, G1{});
         else go(double{}, G0{});
     }
+    c->fin_wflag = nullptr;  // one launch
+    c->fin_wlate = nullptr;
 }
 }  // namespace
+
+int sml::res_finish_wait(sml_reservoirs *c, const uint64_t *flag, uint64_t value, unsigned *late) {
+    SML_REQUIRE(c && flag && late, "null argument");
+    SML_REQUIRE(c->ncs <= 256, "the in-kernel wait needs ncs <= the finish block");
+    c->fin_wflag = flag;
+    c->fin_wval = value;
+    c->fin_wlate = late;
+    return SML_OK;
+}
 
 extern "C" int sml_res_step_finish_grid(sml_reservoirs *c, const double *d_fc4d, const double *d_fc2d,
                                         double *d_local_model, double *d_outvec, void *stream) {
@@ -1911,7 +1953,7 @@ extern "C" int sml_res_step(sml_reservoirs *c, const double *d_feedback, const d
     if (rec) SML_HIP(hipEventRecord(ev[0], st));
     if (int rc = launch_update(c, c->d_x[c->cur], c->d_x[1 - c->cur], d_feedback, st)) return rc;
     if (rec) SML_HIP(hipEventRecord(ev[1], st));
-    launch_readout<kReadFull>(c, d_local_model, d_outvec, st);
+    launch_readout<kReadFull>(c, c->d_x[1 - c->cur], d_local_model, d_outvec, st);
     SML_HIP(hipGetLastError());
     if (rec) {
         SML_HIP(hipEventRecord(ev[2], st));

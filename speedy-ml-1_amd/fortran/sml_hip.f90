@@ -490,7 +490,7 @@ module sml_hip
       type(c_ptr), value :: h, d_recv
       integer(c_int) :: rc
     end function
-    !> cross-stream hops: 0 auto, 1 wait-value, 2 events
+    !> cross-stream hops: 0 auto, 1 wait-value, 2 events, 3 one-lane signal / wait kernels
     function sml_hybrid_set_hop_mode(h, mode) bind(C, name='sml_hybrid_set_hop_mode') result(rc)
       import :: c_ptr, c_int
       type(c_ptr), value :: h

@@ -61,7 +61,7 @@ EXPORTED = (
     "sml_res_set_update_cus", "sml_res_update_balanced", "sml_probe_mfma_f64_clock",
 )
 
-SML_HOP_AUTO, SML_HOP_WAIT_VALUE, SML_HOP_EVENTS = 0, 1, 2
+SML_HOP_AUTO, SML_HOP_WAIT_VALUE, SML_HOP_EVENTS, SML_HOP_KERNEL = 0, 1, 2, 3
 SML_CHAIN_AUTO, SML_CHAIN_TWO_STREAMS, SML_CHAIN_SPEEDY = 0, 1, 2
 
 

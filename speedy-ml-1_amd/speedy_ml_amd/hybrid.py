@@ -197,7 +197,7 @@ class HybridLoop:
         return n.value
 
     def set_hop_mode(self, mode: int):
-        """SML_HOP_AUTO / SML_HOP_WAIT_VALUE / SML_HOP_EVENTS (include/speedy_ml.h)."""
+        """SML_HOP_AUTO / SML_HOP_WAIT_VALUE / SML_HOP_EVENTS / SML_HOP_KERNEL (include/speedy_ml.h)."""
         check(lib().sml_hybrid_set_hop_mode(self._h, int(mode)))
 
     def hop_mode(self):

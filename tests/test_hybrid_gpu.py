@@ -269,15 +269,16 @@ def test_serialised_dispatch_takes_event_hops(cuda, tmp_path):
     """Under serialised dispatch (AMD_SERIALIZE_KERNEL=3 here; rocprofv3's counter
     passes alike) a wait-value hop could block its queue ahead of its producer:
     SML_HOP_AUTO then takes event hops.  A fresh child process with serialisation
-    forced runs 3 steps within its time limit and is bitwise the default loop; an
-    explicit SML_HOP_EVENTS loop in this process is bitwise the default too."""
+    forced runs 3 steps within its time limit and is bitwise the default loop; explicit
+    SML_HOP_EVENTS, SML_HOP_WAIT_VALUE and SML_HOP_KERNEL loops in this process are
+    bitwise the default too."""
     import os
     import subprocess
     import sys
 
     import torch
 
-    from speedy_ml_amd._lib import SML_HOP_AUTO, SML_HOP_EVENTS, SML_HOP_WAIT_VALUE
+    from speedy_ml_amd._lib import SML_HOP_AUTO, SML_HOP_EVENTS, SML_HOP_KERNEL, SML_HOP_WAIT_VALUE
 
     out = str(tmp_path / "hop.npz")
     env = dict(os.environ, AMD_SERIALIZE_KERNEL="3")
@@ -288,14 +289,15 @@ def test_serialised_dispatch_takes_event_hops(cuda, tmp_path):
     got = dict(np.load(out))
     assert int(got["requested"]) == SML_HOP_AUTO and int(got["effective"]) == SML_HOP_EVENTS
 
+    auto = SML_HOP_KERNEL if os.environ.get("SML_HYBRID_HOPK", "0") not in ("", "0") else SML_HOP_WAIT_VALUE
     runs = []
-    for mode in (None, SML_HOP_EVENTS):
+    for mode in (None, SML_HOP_EVENTS, SML_HOP_WAIT_VALUE, SML_HOP_KERNEL):
         loop, _ = _loop(cuda, True)
         if mode is None:
-            assert loop.hop_mode() == (SML_HOP_AUTO, SML_HOP_WAIT_VALUE)
+            assert loop.hop_mode() == (SML_HOP_AUTO, auto)
         else:
             loop.set_hop_mode(mode)
-            assert loop.hop_mode() == (mode, SML_HOP_EVENTS)
+            assert loop.hop_mode() == (mode, mode)
         snaps = {}
         for s in range(3):
             loop.step()
@@ -308,7 +310,8 @@ def test_serialised_dispatch_takes_event_hops(cuda, tmp_path):
         loop.res.close()
         torch.cuda.synchronize()
     for k in runs[0]:
-        np.testing.assert_array_equal(runs[1][k], runs[0][k], err_msg="events vs wait-value " + k)
+        for name, r in zip(("events", "wait-value", "kernel hops"), runs[1:]):
+            np.testing.assert_array_equal(r[k], runs[0][k], err_msg=f"{name} vs the default {k}")
         np.testing.assert_array_equal(got[k], runs[0][k], err_msg="serialised child vs default " + k)
 
 
