@@ -587,11 +587,12 @@ int sml_hybrid_slab_buffers(const sml_hybrid *h, const double **d_sst_grid, cons
  * (the same sequence number, stored by a one-lane kernel behind the producer and
  * polled by a one-lane kernel ahead of the consumer; a wait that has not seen its
  * value after ~4 s gives up and sml_hybrid_sync returns SML_ERR_STATE), or
- * SML_HOP_AUTO (the default: wait-value, but events when dispatch is serialised --
+ * SML_HOP_AUTO (the default: kernel hops, but events when dispatch is serialised --
  * AMD_SERIALIZE_KERNEL or rocprofv3's counter collection -- where a waiting packet or
  * kernel could stall its queue ahead of its producer; SML_HYBRID_EVENTS=1 also
- * selects events, SML_HYBRID_HOPK=1 kernel hops).  Drains both streams before
- * switching. */
+ * selects events, SML_HYBRID_HOPK=0 wait-value).  In the kernel mode the v_p finish
+ * and run_model's entry wait for their inputs inside their own kernels.  Drains both
+ * streams before switching. */
 #define SML_HOP_AUTO 0
 #define SML_HOP_WAIT_VALUE 1
 #define SML_HOP_EVENTS 2

@@ -105,6 +105,8 @@ struct sml_dynamics {
     // check's k_io_minmax adds 4 per check, the exit polls for 4 * chk_count
     bool chk_flag = true;
     unsigned *d_chk_cnt = nullptr, *d_chk_late = nullptr;
+    // the next run_model's entry waits in-kernel for its input grids (sml::dyn_run_model_wait)
+    HopWait entry_wait;
     unsigned chk_count = 0;
     bool chk_counted = false;  // the last launch_io_check added to the counter
     // host copy of the last check's min/max (pinned; written behind the check on its
@@ -2755,7 +2757,9 @@ extern "C" int sml_dyn_from_grid(sml_dynamics *d, const double *d_grid4d, const 
     }
     // entry (:503-518): real(4) copies, q clip, then vdspec kcos = 2 (x cosgr) on the
     // winds and none on the rest: one specx launch reading variables3d / logp
-    if (int rc = spectral_specx_io(d->sp, d_grid4d, d_logp, d->d_varm, kNIoWind, st)) return rc;
+    const HopWait w = d->entry_wait;
+    d->entry_wait = HopWait{};  // one launch
+    if (int rc = spectral_specx_io(d->sp, d_grid4d, d_logp, d->d_varm, kNIoWind, st, w)) return rc;
     if (int rc = spectral_specy(d->sp, d->d_varm, d->d_sfwd, kNIo, st)) return rc;
     hipLaunchKernelGGL(k_io_combine, dim3((kMN + 127) / 128, kKX), dim3(128), 0, st, d->d_sfwd, d->d_state, T);
     SML_HIP(hipGetLastError());
@@ -2803,7 +2807,9 @@ extern "C" int sml_dyn_run_model(sml_dynamics *d, const double *d_grid4d, const 
             SML_HIP(hipStreamWaitEvent(st, d->ev_chk, 0));
             d->chk_pending = false;
         }
-        if (int rc = spectral_specx_io(d->sp, d_grid4d, d_logp, d->d_vfm, kNIoWind, st)) return rc;
+        const HopWait w = d->entry_wait;
+        d->entry_wait = HopWait{};  // one launch
+        if (int rc = spectral_specx_io(d->sp, d_grid4d, d_logp, d->d_vfm, kNIoWind, st, w)) return rc;
         const SpectralDev sd = spectral_dev(d->sp);
         const bool phys = d->phys_on;
         d->sm_cur = 0;  // the window's chain starts in buffer 0
@@ -2882,6 +2888,12 @@ extern "C" int sml_dyn_last_safe(sml_dynamics *d, int *safe, double *minmax) {
 
 // a run_model exit that gave up waiting for its safety check (1 s; never expected):
 // checked by the hybrid loop's sync, after the streams drained
+int sml::dyn_run_model_wait(sml_dynamics *d, const uint64_t *flag, uint64_t value, unsigned *late) {
+    SML_REQUIRE(d && flag && late, "null argument");
+    d->entry_wait = HopWait{flag, value, late};
+    return SML_OK;
+}
+
 int sml::dyn_check_late(sml_dynamics *d) {
     if (!d || !d->d_chk_late) return SML_OK;
     unsigned late = 0;

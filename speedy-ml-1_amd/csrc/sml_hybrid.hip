@@ -62,10 +62,12 @@ struct sml_hybrid {
     // producer: SML_HOP_AUTO then takes event hops (sml_hybrid_set_hop_mode).
     // (the chain on SPEEDY's stream, SML_CHAIN_SPEEDY, hops the other way: grid_t,
     // side -> main, before the re-tiling; begun_t, main -> side, before the finish)
-    // SML_HOP_KERNEL: the same sequence numbers, written by a one-lane kernel behind the
-    // producer and polled by a one-lane kernel ahead of the consumer (k_hop_signal /
-    // k_hop_wait): ordinary dispatches, where the CP's stream operations run as blit
-    // kernels with ~6 us of their own and a ~6 us boundary in front
+    // SML_HOP_KERNEL (the default unless dispatch is serialised): the same sequence
+    // numbers, stored by a one-lane kernel behind the producer (k_hop_signal) and
+    // polled by the consumer -- inside the v_p finish and run_model's entry specx, which
+    // load everything else first, or by a one-lane k_hop_wait elsewhere.  The CP's
+    // stream operations run as blit kernels of ~6 us each with a ~6 us boundary in
+    // front; measured in an 8-rank share, the chain around the window 45.7 -> 34.8 us
     enum { kHopGrid = 0, kHopLm = 1, kHopBegun = 2, kHops = 3 };
     static constexpr int kSeqStride = 16;  // one 128-B line per hop's word; the late word after them
     hipEvent_t ev[kHops] = {nullptr, nullptr, nullptr};
@@ -497,8 +499,11 @@ extern "C" int sml_hybrid_set_hop_mode(sml_hybrid *h, int mode) {
     if (h->side && h->side != h->main) SML_HIP(hipStreamSynchronize(h->side));
     h->hop_mode = mode;
     if (mode == SML_HOP_AUTO) {
+        // kernel hops unless dispatch is serialised (a waiting kernel would hold its queue
+        // ahead of its producer) or SML_HYBRID_EVENTS / SML_HYBRID_HOPK=0 asks otherwise
         h->use_events = env_on("SML_HYBRID_EVENTS") || dispatch_serialised();
-        h->use_kernels = !h->use_events && env_on("SML_HYBRID_HOPK");
+        const char *hk = getenv("SML_HYBRID_HOPK");
+        h->use_kernels = !h->use_events && !(hk && *hk == '0');
     } else {
         h->use_events = mode == SML_HOP_EVENTS;
         h->use_kernels = mode == SML_HOP_KERNEL;
@@ -1092,8 +1097,15 @@ extern "C" int sml_hybrid_advance(sml_hybrid *h, const double *d_outvec_all) {
                            col);
         SML_HIP(hipGetLastError());
     }
-    if (hops)
-        if (int rc = hop_wait(h, sml_hybrid::kHopGrid, s)) return rc;
+    if (hops) {
+        if (h->use_kernels) {  // the entry's specx waits for the assembled grid in-kernel
+            if (int rc = sml::dyn_run_model_wait(h->dyn, h->d_seq + sml_hybrid::kHopGrid * sml_hybrid::kSeqStride,
+                                                 h->seq[sml_hybrid::kHopGrid], hop_late_word(h)))
+                return rc;
+        } else if (int rc = hop_wait(h, sml_hybrid::kHopGrid, s)) {
+            return rc;
+        }
+    }
     if (int rc = sml_dyn_run_model(h->dyn, h->g4, h->g2, h->nleap, h->delt, h->alph, h->rob, h->wil, h->f4, h->f2, s))
         return rc;
     if (hops) {

@@ -23,6 +23,9 @@ int dyn_check_late(sml_dynamics *d);
 // the next sml_res_step_finish_grid / _finish_assemble launch waits in-kernel until
 // *flag >= value (device words; *late set if it gave up), its weights loaded first
 int res_finish_wait(sml_reservoirs *c, const uint64_t *flag, uint64_t value, unsigned *late);
+// the next sml_dyn_run_model / sml_dyn_from_grid waits in-kernel (its entry specx)
+// until *flag >= value before it reads its input grids
+int dyn_run_model_wait(sml_dynamics *d, const uint64_t *flag, uint64_t value, unsigned *late);
 
 // --------------------------------------------------------------- geometry
 // Restatement of the res_domain.f90 decomposition used by every reservoir of the

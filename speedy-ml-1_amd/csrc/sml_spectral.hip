@@ -230,9 +230,30 @@ __global__ __launch_bounds__(kFftThreads) void k_specx(const double *__restrict_
                                                        const double *__restrict__ wa,
                                                        const double *__restrict__ scale_tab, int nf, int nscaled,
                                                        const double *__restrict__ g4 = nullptr,
-                                                       const double *__restrict__ logp = nullptr) {
+                                                       const double *__restrict__ logp = nullptr,
+                                                       HopWait wait = {}) {
     __shared__ double was[kFftWa];
     __shared__ double S[kFftN * (kFftThreads / 2)];  // a pair's two n = 48 halves (E, O)
+    // wait.flag: the grid comes from another stream (SML_HOP_KERNEL): the twiddles are
+    // staged first, then one lane polls, acquires at agent scope and releases the
+    // block (MI355X_MICROARCH.md inter-workgroup visibility, the consumer form)
+    if (wait.flag) {
+        if (threadIdx.x < kFftWa) was[threadIdx.x] = wa[threadIdx.x];
+        if (threadIdx.x + kFftThreads < kFftWa) was[threadIdx.x + kFftThreads] = wa[threadIdx.x + kFftThreads];
+        if (threadIdx.x == 0) {
+            const long long c0 = wall_clock64();
+            while (__hip_atomic_load(wait.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < wait.value) {
+                __builtin_amdgcn_s_sleep(1);
+                if (wall_clock64() - c0 > 400000000ll) {  // ~4 s at wall_clock64's 100 MHz
+                    __hip_atomic_store(wait.late, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    break;
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __syncthreads();
+    }
     // transform (f, j) on the thread pair 2 t, 2 t + 1: thread h transforms the samples
     // 2 i + h (rfftf48), the pair meets in LDS for rfftf's last pass (rfftf96_combine).
     // The samples are loaded before the twiddles are staged (one memory round trip).
@@ -263,9 +284,11 @@ __global__ __launch_bounds__(kFftThreads) void k_specx(const double *__restrict_
             for (int i = 0; i < kFftN / 2; ++i) x[i] = g[2 * i];
         }
     }
-    if (threadIdx.x < kFftWa) was[threadIdx.x] = wa[threadIdx.x];
-    if (threadIdx.x + kFftThreads < kFftWa) was[threadIdx.x + kFftThreads] = wa[threadIdx.x + kFftThreads];
-    __syncthreads();
+    if (!wait.flag) {
+        if (threadIdx.x < kFftWa) was[threadIdx.x] = wa[threadIdx.x];
+        if (threadIdx.x + kFftThreads < kFftWa) was[threadIdx.x + kFftThreads] = wa[threadIdx.x + kFftThreads];
+        __syncthreads();
+    }
     if (act) {
         if (g4) {  // iogrid(30)'s real(4) copies, q < 0 -> 0 on the copy
             const bool qf = f / kKX == 3;
@@ -733,10 +756,10 @@ int spectral_specx_split(sml_spectral *s, const double *grid, double *varm, int 
 }
 
 int spectral_specx_io(sml_spectral *s, const double *g4, const double *logp, double *varm, int nwind,
-                      hipStream_t st) {
+                      hipStream_t st, HopWait wait) {
     constexpr int nf = 4 * kKX + 1;
     hipLaunchKernelGGL(k_specx, dim3((2 * nf * kIL + kFftThreads - 1) / kFftThreads), dim3(kFftThreads), 0, st, nullptr, varm,
-                       s->d_wa, s->d_cosgr, nf, nwind, g4, logp);
+                       s->d_wa, s->d_cosgr, nf, nwind, g4, logp, wait);
     SML_HIP(hipGetLastError());
     return SML_OK;
 }

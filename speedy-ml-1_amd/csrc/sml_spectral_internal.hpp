@@ -36,8 +36,15 @@ int spectral_gridx_range(sml_spectral *s, const double *varm, double *grid, int 
 // iogrid(30)'s entry / iogrid(31)'s exit: specx from / gridx into variables3d and
 // logp directly (real(4) copies and the q clip on entry).  gridx_io: the 33 Fourier fields [u v t q | ps] (kcos = 2 for the first
 // nwind) straight into variables3d(4, ix, il, kx) and logp(ix, il)
+// wait (optional): a cross-stream hand-off the kernel waits for in-kernel before it
+// reads g4 / logp (*flag >= value; ~4 s, then *late is set and it goes on)
+struct HopWait {
+    const uint64_t *flag = nullptr;
+    uint64_t value = 0;
+    unsigned *late = nullptr;
+};
 int spectral_specx_io(sml_spectral *s, const double *g4, const double *logp, double *varm, int nwind,
-                      hipStream_t st);
+                      hipStream_t st, HopWait wait = {});
 int spectral_gridx_io(sml_spectral *s, const double *varm, double *g4, double *logp, int nwind, hipStream_t st);
 
 // run_model's exit (src/mpires.f90:1605-1628) around iogrid(31): the forecast's q is

@@ -289,7 +289,9 @@ def test_serialised_dispatch_takes_event_hops(cuda, tmp_path):
     got = dict(np.load(out))
     assert int(got["requested"]) == SML_HOP_AUTO and int(got["effective"]) == SML_HOP_EVENTS
 
-    auto = SML_HOP_KERNEL if os.environ.get("SML_HYBRID_HOPK", "0") not in ("", "0") else SML_HOP_WAIT_VALUE
+    auto = SML_HOP_WAIT_VALUE if os.environ.get("SML_HYBRID_HOPK") == "0" else SML_HOP_KERNEL
+    if os.environ.get("SML_HYBRID_EVENTS", "0") not in ("", "0"):
+        auto = SML_HOP_EVENTS
     runs = []
     for mode in (None, SML_HOP_EVENTS, SML_HOP_WAIT_VALUE, SML_HOP_KERNEL):
         loop, _ = _loop(cuda, True)
