@@ -409,7 +409,11 @@ def main():
     rd_avg_s = float(np.mean(rd_ms)) * 1e-3
     upd_avg_s = float(np.mean(upd_ms)) * 1e-3
     achieved = rd_bytes / rd_avg_s / 1e9
-    upd_bytes = sum(8 * (2 + wb) * s.n + (2 + wb) * s.n + 2 * 8 * s.n + 8 * s.ninp for s in sizes)
+    # the update's algorithmic bytes: A's k entries (column + value), W_in's n values (its
+    # block-diagonal column i / q is computed, not read: mod_reservoir.f90:260-278), the
+    # state in and out, the feedback (r04b; before, A was counted as 8 ELL slots per row
+    # and W_in's column as read: 48 n + 6 n instead of (2 + wb) k + wb n)
+    upd_bytes = sum((2 + wb) * s.k + wb * s.n + 2 * 8 * s.n + 8 * s.ninp for s in sizes)
     _, algo_step = res.footprint()
     traffic = None
     pmc_path = os.path.join(REPO, "profiles", "readout_pmc.json")

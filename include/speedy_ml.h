@@ -213,6 +213,13 @@ int sml_res_set_read_waves(sml_reservoirs *c, int waves);
  * both give bit-identical states. */
 int sml_res_set_update_cus(sml_reservoirs *c, int cus);
 int sml_res_update_balanced(sml_reservoirs *c, int *balanced);
+/* the compressed form of local region i's A and W_in the state update reads
+ * (DESIGN.md §3.1): a_width = A's ELL main slots per row (0: the CSR copy),
+ * a_overflow = 1 when rows of a_width + 1 entries keep their last entry in an
+ * overflow list, win_q > 0 when W_in is block-diagonal with win_q rows per input (its
+ * column i / win_q is computed, not read), win_ell = 1 when W_in is read in ELL form.
+ * Layout only: every form gives bit-identical states. */
+int sml_res_ell_layout(sml_reservoirs *c, int i, int *a_width, int *a_overflow, int *win_q, int *win_ell);
 /* the form of sml_res_step_begin (predict's update + the v_ml half of the readout,
  * src/mod_reservoir.f90:1440-1455): 0 = the update grid, then the readout grid;
  * 1 = one launch, a block per region that updates its state and then streams its

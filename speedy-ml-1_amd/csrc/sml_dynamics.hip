@@ -107,6 +107,8 @@ struct sml_dynamics {
     unsigned *d_chk_cnt = nullptr, *d_chk_late = nullptr;
     // the next run_model's entry waits in-kernel for its input grids (sml::dyn_run_model_wait)
     HopWait entry_wait;
+    // the next run_model's exit signals its forecast in-kernel (sml::dyn_run_model_signal)
+    uint64_t *exit_sig = nullptr;
     unsigned chk_count = 0;
     bool chk_counted = false;  // the last launch_io_check added to the counter
     // host copy of the last check's min/max (pinned; written behind the check on its
@@ -2825,6 +2827,8 @@ extern "C" int sml_dyn_run_model(sml_dynamics *d, const double *d_grid4d, const 
         if (int rc = sml_dyn_window(d, nleap, delt, alph, rob, wil, stream)) return rc;
     }
     IoExit ex{0.000001, d->mm_last, d_grid4d, d_logp};
+    ex.sig = d->exit_sig;
+    d->exit_sig = nullptr;  // one launch
     if (d->chk_pending && d->chk_counted) {
         // the exit kernel itself waits for the check's counter: no event wait (a
         // barrier packet with a cross-queue dependency) on the window's stream.  The
@@ -2891,6 +2895,16 @@ extern "C" int sml_dyn_last_safe(sml_dynamics *d, int *safe, double *minmax) {
 int sml::dyn_run_model_wait(sml_dynamics *d, const uint64_t *flag, uint64_t value, unsigned *late) {
     SML_REQUIRE(d && flag && late, "null argument");
     d->entry_wait = HopWait{flag, value, late};
+    return SML_OK;
+}
+
+// the next run_model's exit kernel adds *adds to *counter once its forecast is
+// released (each of its blocks adds 1): the hybrid loop's forecast hop without a
+// signal kernel behind the exit
+int sml::dyn_run_model_signal(sml_dynamics *d, uint64_t *counter, int *adds) {
+    SML_REQUIRE(d && counter && adds, "null argument");
+    d->exit_sig = counter;
+    *adds = spectral_exit_blocks();
     return SML_OK;
 }
 

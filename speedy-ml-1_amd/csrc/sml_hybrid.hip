@@ -82,6 +82,12 @@ struct sml_hybrid {
     int chain_mode = SML_CHAIN_AUTO;
     bool chain = false;
     bool use_events = false, use_kernels = false;
+    // kernel hops: the forecast hop signalled by run_model's exit kernel itself (each of
+    // its blocks releases its stores and adds 1 to the hop's word) instead of a signal
+    // kernel behind it -- SML_HOP_FUSED=1 at create; measured same-box within noise of
+    // the signal kernel (N = 1: 1118-1123 vs 1125-1131, 8-rank share 1190-1197 vs 1191),
+    // so not the default
+    bool fused_lm_signal = false;
     int hop_mode = SML_HOP_AUTO;
     // caller-owned device buffers
     double *fb = nullptr, *lm = nullptr, *ov = nullptr, *g4 = nullptr, *g2 = nullptr, *pr = nullptr, *f4 = nullptr,
@@ -670,6 +676,7 @@ extern "C" int sml_hybrid_create(sml_reservoirs *res, sml_dynamics *dyn, sml_com
         }
     }
     if (const char *e = std::getenv("SML_HYBRID_ASM")) h->fuse_asm = *e != '0';
+    if (const char *e = std::getenv("SML_HOP_FUSED")) h->fused_lm_signal = *e == '1';
     for (hipEvent_t &e : h->ev)
         if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return bail(fail(SML_ERR_HIP, "event"));
     if (int rc = sml_hybrid_set_hop_mode(h, SML_HOP_AUTO)) return bail(rc);
@@ -1106,9 +1113,16 @@ extern "C" int sml_hybrid_advance(sml_hybrid *h, const double *d_outvec_all) {
             return rc;
         }
     }
+    int exit_adds = 0;
+    if (hops && h->use_kernels && h->fused_lm_signal)
+        if (int rc = sml::dyn_run_model_signal(h->dyn, h->d_seq + sml_hybrid::kHopLm * sml_hybrid::kSeqStride,
+                                               &exit_adds))
+            return rc;
     if (int rc = sml_dyn_run_model(h->dyn, h->g4, h->g2, h->nleap, h->delt, h->alph, h->rob, h->wil, h->f4, h->f2, s))
         return rc;
-    if (hops) {
+    if (exit_adds > 0) {  // the exit's blocks each add 1 to the hop's word once released
+        h->seq[sml_hybrid::kHopLm] += (uint64_t)exit_adds;
+    } else if (hops) {
         if (int rc = hop_signal(h, sml_hybrid::kHopLm, s)) return rc;
     } else if (!h->overlap && h->ncs) {
         if (int rc = sml_res_tile_local_model(h->res, h->f4, h->f2, h->lm, s)) return rc;

@@ -26,6 +26,7 @@ int res_finish_wait(sml_reservoirs *c, const uint64_t *flag, uint64_t value, uns
 // the next sml_dyn_run_model / sml_dyn_from_grid waits in-kernel (its entry specx)
 // until *flag >= value before it reads its input grids
 int dyn_run_model_wait(sml_dynamics *d, const uint64_t *flag, uint64_t value, unsigned *late);
+int dyn_run_model_signal(sml_dynamics *d, uint64_t *counter, int *adds);
 
 // --------------------------------------------------------------- geometry
 // Restatement of the res_domain.f90 decomposition used by every reservoir of the

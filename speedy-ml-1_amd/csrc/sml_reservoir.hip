@@ -54,16 +54,28 @@ constexpr int kMeanStd = 36;    // mean/std vector length (mod_reservoir.f90:181
 constexpr int kTisrStride = 16; // packed tisr input: [nlocal][16]
 constexpr int kSrcKeep = -1;    // feedback entry left untouched (sst)
 
-constexpr int kEllA = 8;  // ELL slots per row for A, row-major (makesparse rows hold floor(k/n) or +1 <= 8)
+constexpr int kEllA = 8;  // ELL slots reserved per row for A (makesparse rows hold floor(k/n) or +1 <= 8)
 constexpr int kEllW = 1;  // ELL slots per row for W_in (the trained W_in has one entry per row)
 
+// A's ELL copy (r04b): a_w "main" slots per row, stored as slot pairs, pair-major
+// ([pair][n] of (col, col) u16 pairs and of (val, val) pairs: lane i's row is one
+// 4-B + one 8-B load per pair, coalesced across the wave), a_w chosen per region to
+// move the fewest bytes.  makesparse rows hold floor(k/n) or floor(k/n) + 1 entries
+// (mod_linalg.f90:180-218): with a_ov the rows holding a_w + 1 keep their last entry
+// in an overflow list instead of padding every row to the longest -- a bit per row
+// (u64 words) + a count per word locate it.  The dominant 4x4+sst region (n 6048,
+// 4.8 % of rows one longer) moves 36.5 B of A per row instead of 48.
 struct RegionDev {
     int n, ninp, ld;
-    int a_w, w_w;  // ELL widths of A and W_in (0 = use the CSR copy)
-    int pad_;
+    int a_w, w_w;  // A's ELL main width in slots (0 = use the CSR copy); W_in ELL (1) or CSR (0)
+    int a_ov;      // 1: rows of a_w + 1 entries, the last in the overflow list
+    int w_q;       // > 0: W_in's column of row i is i / w_q = umulhi(i, w_magic), not stored
+    uint32_t w_magic;
     int64_t a_rp, a_nz, w_rp, w_nz, wout, x, xaug, fb;
     int64_t wlm;  // W_out(:, 1:ncs) transposed, [ncs][nout_pad], in the W_out pool after the row-major blocks
-    int64_t a_ell, w_ell;  // offsets into the ELL pools (row-major [n][slots])
+    int64_t a_ell, w_ell;  // offsets into the ELL pools (A: pair-major as above; W_in: [n])
+    int64_t a_om;          // overflow bit words / per-word counts: [ceil(n / 64)] each
+    int64_t a_oe;          // overflow entries (col, val) in row order: [n] reserved
 };
 
 }  // namespace
@@ -93,9 +105,16 @@ struct sml_reservoirs {
     void *d_a_val = nullptr, *d_w_val = nullptr, *d_wout = nullptr;
     // ELL copies (row-major per region), used when rows are short enough
     std::vector<int> a_ell_cap, w_ell_cap;  // slots per row reserved per region
-    int64_t tot_a_ell = 0, tot_w_ell = 0;
+    int64_t tot_a_ell = 0, tot_w_ell = 0, tot_a_om = 0, tot_a_oe = 0;
     uint16_t *d_a_ell_col = nullptr, *d_w_ell_col = nullptr;
     void *d_a_ell_val = nullptr, *d_w_ell_val = nullptr;
+    uint64_t *d_a_om = nullptr;   // A's overflow bits, one word per 64 rows
+    uint32_t *d_a_ob = nullptr;   // overflow entries before each word (region-local)
+    uint16_t *d_a_oc = nullptr;   // overflow entries: column
+    void *d_a_ov = nullptr;       //                   value
+    void *d_zero = nullptr;       // 256 zero bytes: the target of the balanced update's unused loads
+    bool no_ell = false;          // SML_NO_ELL=1 at create: CSR copies only (A/B, tests)
+    int upd_depth = 2;            // passes in flight in the balanced update (SML_UPD_DEPTH=3 at create)
     double *d_x[2] = {nullptr, nullptr};
     int cur = 0;
     double *d_meanstd = nullptr;
@@ -175,17 +194,28 @@ struct Ell {
     const void *a_val;
     const uint16_t *w_col;
     const void *w_val;
+    const uint64_t *a_om;  // A's overflow bits / counts / entries (RegionDev::a_ov)
+    const uint32_t *a_ob;
+    const uint16_t *a_oc;
+    const void *a_ov;
+    const void *zero;  // 256 zero bytes
 };
 
-// Row loads of one pass, issued ahead of their use (software pipelining).  A's ELL
-// is row-major [n][8]: one 16-B load brings a row's 8 column indices, two 16-B
-// (fp32) or four 16-B (fp64) loads its values, coalesced across the wave.
+// Row loads of one pass, issued ahead of their use (software pipelining): A's main
+// slots as up to 4 (col, col) / (val, val) pairs, W_in's entry, and -- for a region
+// with an overflow list -- the row's overflow word and count, then (resolve_ovf, one
+// stage later) its overflow entry.
 template <typename WT>
 struct RowRegs {
-    uint4 c;
+    uint32_t c[kEllA / 2];
     WT v[kEllA];
     uint32_t wc;
     WT wv;
+    uint64_t om;
+    uint32_t ob;
+    uint32_t oc;
+    WT ov;
+    bool oh;
 };
 
 // A and W_in are streamed once per step: non-temporal loads (SML_UPD_NT), like the
@@ -203,28 +233,93 @@ __device__ inline T stream_load(const T *p) {
 }
 
 template <typename WT>
+struct Pair;
+template <>
+struct Pair<float> {
+    typedef float N __attribute__((ext_vector_type(2)));
+};
+template <>
+struct Pair<double> {
+    typedef double N __attribute__((ext_vector_type(2)));
+};
+
+// pair p of row i (slots 2p, 2p + 1) from the pair-major ELL copy
+template <typename WT>
+__device__ inline void load_pair(RowRegs<WT> &q, int p, const uint32_t *cp, const WT *vp) {
+    typedef typename Pair<WT>::N V2;
+    q.c[p] = stream_load(cp);
+    const V2 v = stream_load(reinterpret_cast<const V2 *>(vp));
+    q.v[2 * p] = v.x;
+    q.v[2 * p + 1] = v.y;
+}
+
+__device__ inline uint32_t win_col_implicit(const RegionDev &rg, int i) {
+    return __umulhi((uint32_t)i, rg.w_magic);  // = i / w_q for every i < n (checked at load)
+}
+
+// every load of row i, branching on the region's widths (k_res_update, k_res_begin)
+template <typename WT>
 __device__ inline void load_row(RowRegs<WT> &q, const RegionDev &rg, const Ell &ell, int i, bool live) {
     if (live && rg.a_w > 0) {
-        const nt_u4 c = stream_load(reinterpret_cast<const nt_u4 *>(ell.a_col + rg.a_ell + (size_t)i * kEllA));
-        q.c = make_uint4(c.x, c.y, c.z, c.w);
-        const WT *ev = (const WT *)ell.a_val + rg.a_ell + (size_t)i * kEllA;
-        if constexpr (sizeof(WT) == 4) {
-            const nt_f4 a = stream_load(reinterpret_cast<const nt_f4 *>(ev)),
-                        b = stream_load(reinterpret_cast<const nt_f4 *>(ev) + 1);
-            q.v[0] = a.x; q.v[1] = a.y; q.v[2] = a.z; q.v[3] = a.w;
-            q.v[4] = b.x; q.v[5] = b.y; q.v[6] = b.z; q.v[7] = b.w;
-        } else {
+        const uint32_t *cb = reinterpret_cast<const uint32_t *>(ell.a_col + rg.a_ell);
+        const WT *vb = (const WT *)ell.a_val + rg.a_ell;
+        const int np = (rg.a_w + 1) >> 1, n = rg.n;
 #pragma unroll
-            for (int s = 0; s < kEllA / 2; ++s) {
-                const nt_d2 a = stream_load(reinterpret_cast<const nt_d2 *>(ev) + s);
-                q.v[2 * s] = a.x;
-                q.v[2 * s + 1] = a.y;
-            }
+        for (int p = 0; p < kEllA / 2; ++p)
+            if (p < np) load_pair(q, p, cb + (size_t)p * n + i, vb + 2 * ((size_t)p * n + i));
+        if (rg.a_ov) {
+            q.om = stream_load(ell.a_om + rg.a_om + (i >> 6));
+            q.ob = stream_load(ell.a_ob + rg.a_om + (i >> 6));
         }
     }
     if (live && rg.w_w > 0) {
-        q.wc = stream_load(ell.w_col + rg.w_ell + i);
+        q.wc = rg.w_q > 0 ? win_col_implicit(rg, i) : (uint32_t)stream_load(ell.w_col + rg.w_ell + i);
         q.wv = stream_load((const WT *)ell.w_val + rg.w_ell + i);
+    }
+}
+
+// the same loads for the balanced update: NP pairs from every region (pairs past a
+// narrower region's own load the zero bytes, so the pair loads carry no branch); the
+// overflow word / count and the stored W_in column only where the region has them --
+// a branch uniform across the pass (a pass never straddles regions)
+template <typename WT, int NP, bool OVF>
+__device__ inline void load_row_fixed(RowRegs<WT> &q, const RegionDev &rg, const Ell &ell, int i) {
+    const uint32_t *cb = reinterpret_cast<const uint32_t *>(ell.a_col + rg.a_ell);
+    const WT *vb = (const WT *)ell.a_val + rg.a_ell;
+    const uint32_t *zc = reinterpret_cast<const uint32_t *>(ell.zero);
+    const WT *zv = reinterpret_cast<const WT *>(ell.zero);
+    const int np = (rg.a_w + 1) >> 1, n = rg.n;
+    if (OVF) {
+        q.om = 0;
+        q.ob = 0;
+        if (rg.a_ov) {
+            q.om = stream_load(ell.a_om + rg.a_om + (i >> 6));
+            q.ob = stream_load(ell.a_ob + rg.a_om + (i >> 6));
+        }
+    }
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+        const bool in = p < np;
+        load_pair(q, p, in ? cb + (size_t)p * n + i : zc, in ? vb + 2 * ((size_t)p * n + i) : zv);
+    }
+    if (rg.w_q > 0)
+        q.wc = win_col_implicit(rg, i);
+    else
+        q.wc = stream_load(ell.w_col + rg.w_ell + i);
+    q.wv = stream_load((const WT *)ell.w_val + rg.w_ell + i);
+}
+
+// row i's overflow entry, if any: its bit in the word, its index = the word's count +
+// the bits below it (kFixed: the balanced update's streaming loads)
+template <typename WT, bool kFixed>
+__device__ inline void resolve_ovf(RowRegs<WT> &q, const RegionDev &rg, const Ell &ell, int i) {
+    const int b = i & 63;
+    const uint64_t below = b ? q.om << (64 - b) : 0ull;  // the bits of rows i - b .. i - 1
+    q.oh = rg.a_ov && ((q.om >> b) & 1ull);
+    const int64_t e = rg.a_oe + q.ob + __popcll(below);
+    if (q.oh) {  // (the lanes of the rows one longer: 5-16 % of them where a region has any)
+        q.oc = kFixed ? stream_load(ell.a_oc + e) : ell.a_oc[e];
+        q.ov = kFixed ? stream_load((const WT *)ell.a_ov + e) : ((const WT *)ell.a_ov)[e];
     }
 }
 
@@ -243,20 +338,38 @@ __device__ __attribute__((always_inline)) inline double res_tanh(double x) {
     return copysign(em / (em + 2.0), x);
 }
 
-__device__ inline int ell_col(const uint4 &c, int s) {
-    const uint32_t w = s < 2 ? c.x : s < 4 ? c.y : s < 6 ? c.z : c.w;
-    return (s & 1) ? (int)(w >> 16) : (int)(w & 0xffffu);
+template <typename WT>
+__device__ inline int ell_col(const RowRegs<WT> &q, int s) {
+    return (int)((q.c[s >> 1] >> (16 * (s & 1))) & 0xffffu);
+}
+
+// x_new(i) from the row's loads: y = A x over the main slots in order, then the
+// overflow entry (the row's file order: makesparse's blocks, CSR-stable), temp =
+// W_in u, tanh, leak -- one expression for every ELL form of the update
+template <typename WT>
+__device__ __attribute__((always_inline)) inline double ell_row_value(const RowRegs<WT> &q, const RegionDev &rg,
+                                                                      const double *xs, const double *fs, int i,
+                                                                      double leak) {
+    double y = 0.0;
+#pragma unroll
+    for (int s = 0; s < kEllA; ++s)
+        if (s < rg.a_w) y = y + (double)q.v[s] * xs[ell_col(q, s)];
+    if (q.oh) y = y + (double)q.ov * xs[q.oc];
+    double t = 0.0;
+    t = t + (double)q.wv * fs[q.wc];
+    const double xn = res_tanh(y + t);
+    return (1.0 - leak) * xs[i] + leak * xn;
 }
 
 // update: logical block = (region, part); a part is a contiguous range of rows
 // walked in passes of 1024 rows.  With kLds the region's state x and feedback u
 // are staged once per block in LDS and the SpMV's random column gathers hit LDS
 // instead of the L2 (one L2 transaction per gathered double otherwise).  A and
-// W_in are read in ELL form when the region's rows are short (row-major [n][8]:
-// a row's slots arrive in 16-B loads, coalesced across the wave;
+// W_in are read in ELL form when the region's rows are short (pair-major, RegionDev;
 // padding slots hold 0 * x[0] after the row's real entries, so the file-order sum
 // is unchanged), otherwise from the CSR copy.  The next pass's ELL loads are issued
-// before the current pass computes.
+// before the current pass computes (the overflow entry, when the region has a list,
+// is fetched when the row is computed: this form is not the one the loop runs).
 template <typename WT, bool kLds, int kThr = kUpdThreads>
 __device__ __attribute__((always_inline)) inline void update_block(
     int lb, double *smem, const RegionDev *__restrict__ R, const int32_t *__restrict__ a_rp,
@@ -298,9 +411,12 @@ __device__ __attribute__((always_inline)) inline void update_block(
             // y = A x, entries of row i in the file's order (COO semantics, duplicates add)
             double y = 0.0;
             if (rg.a_w > 0) {
+                cur.oh = false;
+                if (rg.a_ov) resolve_ovf<WT, false>(cur, rg, ell, i);
 #pragma unroll
                 for (int s = 0; s < kEllA; ++s)
-                    if (s < rg.a_w) y = y + (double)cur.v[s] * xs[ell_col(cur.c, s)];
+                    if (s < rg.a_w) y = y + (double)cur.v[s] * xs[ell_col(cur, s)];
+                if (cur.oh) y = y + (double)cur.ov * xs[cur.oc];  // the row's last entry (ell_row_value)
             } else {
                 for (int e = rp[i], e1 = rp[i + 1]; e < e1; ++e) y = y + (double)av[e] * xs[ac[e]];
             }
@@ -368,7 +484,7 @@ struct StageRegs {
     double f;
 };
 
-template <typename WT>
+template <typename WT, int NP, bool OVF, int kDepth = 2>
 __global__ __launch_bounds__(kUpdThreads, 4) void k_res_update_bal(
     const RegionDev *__restrict__ R, const int32_t *__restrict__ row0, const int32_t *__restrict__ blk_r0, int nlocal,
     int64_t total, Ell ell, const double *__restrict__ x_old, double *__restrict__ x_new,
@@ -390,10 +506,21 @@ __global__ __launch_bounds__(kUpdThreads, 4) void k_res_update_bal(
         if (r >= nlocal || row0[r] >= g1) return PassDesc{r, 0, 0, p.seg + 1, false};
         return seg_at(r, p.seg + 1);
     };
+    // a lane past its segment's end loads row 0's data (in range, never used): the
+    // same loads in every lane and every pass
     auto load = [&](RowRegs<WT> &q, const PassDesc &p) {
         if (!p.live) return;
         const RegionDev rg = R[p.r];
-        load_row(q, rg, ell, p.base + tid, p.base + tid < p.end);
+        const int i = p.base + tid;
+        load_row_fixed<WT, NP, OVF>(q, rg, ell, i < p.end ? i : 0);
+    };
+    auto resolve = [&](RowRegs<WT> &q, const PassDesc &p) {
+        q.oh = false;
+        if (!OVF || !p.live) return;
+        const RegionDev rg = R[p.r];
+        if (!rg.a_ov) return;  // pass-uniform
+        const int i = p.base + tid;
+        resolve_ovf<WT, true>(q, rg, ell, i < p.end ? i : 0);
     };
     auto stage_load = [&](StageRegs &sr, int r) {
         const RegionDev rg = R[r];
@@ -414,20 +541,33 @@ __global__ __launch_bounds__(kUpdThreads, 4) void k_res_update_bal(
         }
         if (tid < rg.ninp) buf[lds_x + tid] = sr.f;
     };
+    // kDepth passes in flight while one computes: L1 .. L{kDepth} (P1 .. P{kDepth})
+    static_assert(kDepth == 2 || kDepth == 3, "update pipeline depth");
     PassDesc P0 = seg_at(blk_r0[b], 0);
-    RowRegs<WT> L0, L1, L2;
+    RowRegs<WT> L0, L1, L2, L3;
     load(L0, P0);
+    resolve(L0, P0);
     PassDesc P1 = succ(P0);
     load(L1, P1);
+    PassDesc P2 = succ(P1), P3 = P2;
+    if constexpr (kDepth == 3) {
+        load(L2, P2);
+        P3 = succ(P2);
+    }
     {
         StageRegs sr;
         stage_load(sr, P0.r);
         stage_store(sr, P0.r, smem);
     }
     __syncthreads();
-    PassDesc P2 = succ(P1);
     while (P0.live) {  // block-uniform
-        load(L2, P2);
+        // P1's overflow entries before the next pass's loads: compute(P1) then waits for
+        // nothing issued after them (the in-order vmcnt), so kDepth passes stay in flight
+        resolve(L1, P1);
+        if constexpr (kDepth == 3)
+            load(L3, P3);
+        else
+            load(L2, P2);
         const bool newseg = P1.live && P1.seg != P0.seg;
         StageRegs sr;
         if (newseg) stage_load(sr, P1.r);
@@ -435,17 +575,7 @@ __global__ __launch_bounds__(kUpdThreads, 4) void k_res_update_bal(
             const RegionDev rg = R[P0.r];
             const double *xs = smem + (size_t)(P0.seg & 1) * lds_buf, *fs = xs + lds_x;
             const int i = P0.base + tid;
-            if (i < P0.end) {
-                double y = 0.0;
-#pragma unroll
-                for (int s = 0; s < kEllA; ++s)
-                    if (s < rg.a_w) y = y + (double)L0.v[s] * xs[ell_col(L0.c, s)];
-                double t = 0.0;
-                t = t + (double)L0.wv * fs[L0.wc];
-                const double xn = res_tanh(y + t);
-                const double xv = (1.0 - leak) * xs[i] + leak * xn;
-                x_new[rg.x + i] = xv;
-            }
+            if (i < P0.end) x_new[rg.x + i] = ell_row_value(L0, rg, xs, fs, i, leak);
         }
         if (newseg) {  // the other buffer: its last reader (segment P0.seg - 1) finished before the last barrier
             stage_store(sr, P1.r, smem + (size_t)(P1.seg & 1) * lds_buf);
@@ -455,7 +585,13 @@ __global__ __launch_bounds__(kUpdThreads, 4) void k_res_update_bal(
         L0 = L1;
         P1 = P2;
         L1 = L2;
-        P2 = succ(P2);
+        if constexpr (kDepth == 3) {
+            P2 = P3;
+            L2 = L3;
+            P3 = succ(P3);
+        } else {
+            P2 = succ(P2);
+        }
     }
 }
 
@@ -1201,30 +1337,95 @@ int load_region_impl(sml_reservoirs *c, int i, const int *rows, const int *cols,
             for (int o = 0; o < nout; ++o) wl[(size_t)j * c->nout_pad + o] = (StoT)wout[(size_t)j * nout + o];
         SML_HIP(hipMemcpy((char *)c->d_wlm + rg.wlm * wb, wl.data(), wl.size() * wb, hipMemcpyHostToDevice));
     }
-    // --- ELL copies when every row fits the reserved slots (row-major [n][cap], file
-    // order within a row, zero-padded after the row's entries)
-    auto ell = [&](const std::vector<int32_t> &p, const std::vector<uint16_t> &col, const std::vector<StoT> &val,
-                   int cap, uint16_t *dcol, void *dval, int64_t off, int *width) -> int {
-        int w = 0;
-        for (int r = 0; r < n; ++r) w = std::max(w, p[r + 1] - p[r]);
-        *width = 0;
-        if (w == 0 || w > cap) return SML_OK;
-        std::vector<uint16_t> ec((size_t)cap * n, 0);
-        std::vector<StoT> ev((size_t)cap * n, (StoT)0);
-        for (int r = 0; r < n; ++r)
-            for (int e = p[r]; e < p[r + 1]; ++e) {
-                ec[(size_t)r * cap + (e - p[r])] = col[e];
-                ev[(size_t)r * cap + (e - p[r])] = val[e];
-            }
-        SML_HIP(hipMemcpy(dcol + off, ec.data(), ec.size() * 2, hipMemcpyHostToDevice));
-        SML_HIP(hipMemcpy((char *)dval + off * wb, ev.data(), ev.size() * wb, hipMemcpyHostToDevice));
-        *width = w;
-        return SML_OK;
-    };
+    // --- ELL copies (RegionDev): A pair-major with the main width that moves the fewest
+    // bytes, W_in one slot per row -- file order within a row, zero-padded after the
+    // row's entries; a region whose rows do not fit keeps the CSR copies only
     RegionDev &rgm = c->rd[i];
-    if (int rc = ell(rp, acol, aval, c->a_ell_cap[i], c->d_a_ell_col, c->d_a_ell_val, rgm.a_ell, &rgm.a_w)) return rc;
-    if (int rc = ell(wrp, wcol, wval, c->w_ell_cap[i], c->d_w_ell_col, c->d_w_ell_val, rgm.w_ell, &rgm.w_w))
-        return rc;
+    rgm.a_w = rgm.w_w = rgm.a_ov = rgm.w_q = 0;
+    rgm.w_magic = 0;
+    if (c->a_ell_cap[i] > 0) {
+        int maxlen = 0, nmax = 0;
+        for (int r = 0; r < n; ++r) maxlen = std::max(maxlen, rp[r + 1] - rp[r]);
+        for (int r = 0; r < n; ++r) nmax += (rp[r + 1] - rp[r]) == maxlen;
+        if (maxlen >= 1 && maxlen <= c->a_ell_cap[i]) {
+            // bytes per row: the pairs (odd widths padded), + for an overflow list its bit
+            // words / counts (12 B per 64 rows) and an entry per row of maxlen entries
+            const double eb = 2.0 + (double)wb;
+            auto cost = [&](int w, bool ov) {
+                return 2 * ((w + 1) / 2) * eb * n + (ov ? 12.0 * ((n + 63) / 64) + eb * nmax : 0.0);
+            };
+            int w = maxlen;
+            bool ov = false;
+            if (maxlen >= 2 && cost(maxlen - 1, true) < cost(maxlen, false)) {
+                w = maxlen - 1;
+                ov = true;
+            }
+            const int np = (w + 1) / 2;
+            std::vector<uint16_t> ec((size_t)2 * np * n, 0);
+            std::vector<StoT> ev((size_t)2 * np * n, (StoT)0);
+            const int nw = (n + 63) / 64;
+            std::vector<uint64_t> om(ov ? nw : 0, 0ull);
+            std::vector<uint32_t> ob(ov ? nw : 0, 0u);
+            std::vector<uint16_t> oc;
+            std::vector<StoT> ovv;
+            for (int r = 0; r < n; ++r) {
+                if (ov && (r & 63) == 0) ob[r >> 6] = (uint32_t)oc.size();
+                for (int e = rp[r]; e < rp[r + 1]; ++e) {
+                    const int s = e - rp[r];
+                    if (s < w) {  // pair s / 2, half s % 2 of row r
+                        const size_t at = (size_t)(s >> 1) * 2 * n + 2 * (size_t)r + (s & 1);
+                        ec[at] = acol[e];
+                        ev[at] = aval[e];
+                    } else {  // s == w: the overflow entry
+                        om[r >> 6] |= 1ull << (r & 63);
+                        oc.push_back(acol[e]);
+                        ovv.push_back(aval[e]);
+                    }
+                }
+            }
+            SML_HIP(hipMemcpy(c->d_a_ell_col + rgm.a_ell, ec.data(), ec.size() * 2, hipMemcpyHostToDevice));
+            SML_HIP(hipMemcpy((char *)c->d_a_ell_val + rgm.a_ell * wb, ev.data(), ev.size() * wb,
+                              hipMemcpyHostToDevice));
+            if (ov) {
+                SML_HIP(hipMemcpy(c->d_a_om + rgm.a_om, om.data(), om.size() * 8, hipMemcpyHostToDevice));
+                SML_HIP(hipMemcpy(c->d_a_ob + rgm.a_om, ob.data(), ob.size() * 4, hipMemcpyHostToDevice));
+                if (!oc.empty()) {
+                    SML_HIP(hipMemcpy(c->d_a_oc + rgm.a_oe, oc.data(), oc.size() * 2, hipMemcpyHostToDevice));
+                    SML_HIP(hipMemcpy((char *)c->d_a_ov + rgm.a_oe * wb, ovv.data(), ovv.size() * wb,
+                                      hipMemcpyHostToDevice));
+                }
+            }
+            rgm.a_w = w;
+            rgm.a_ov = ov ? 1 : 0;
+        }
+    }
+    if (c->w_ell_cap[i] > 0) {
+        bool one = true;  // exactly one entry per row (train_reservoir's W_in, mod_reservoir.f90:260-278)
+        for (int r = 0; r < n && one; ++r) one = wrp[r + 1] - wrp[r] == 1;
+        if (one) {
+            std::vector<uint16_t> ec(n);
+            std::vector<StoT> ev(n);
+            for (int r = 0; r < n; ++r) {
+                ec[r] = wcol[wrp[r]];
+                ev[r] = wval[wrp[r]];
+            }
+            // block-diagonal (rows (j-1) q + 1 .. j q read input j, q = n / ninp): the
+            // column is i / q, computed as umulhi(i, magic), so only the value is read
+            const int q = ninp > 0 && n % ninp == 0 ? n / ninp : 0;
+            bool implicit = q > 0;
+            const uint32_t magic = q > 0 ? (uint32_t)((0x100000000ull + q - 1) / q) : 0u;
+            for (int r = 0; r < n && implicit; ++r)
+                implicit = ec[r] == r / q && (uint32_t)(((uint64_t)r * magic) >> 32) == (uint32_t)(r / q);
+            SML_HIP(hipMemcpy(c->d_w_ell_col + rgm.w_ell, ec.data(), ec.size() * 2, hipMemcpyHostToDevice));
+            SML_HIP(hipMemcpy((char *)c->d_w_ell_val + rgm.w_ell * wb, ev.data(), ev.size() * wb,
+                              hipMemcpyHostToDevice));
+            rgm.w_w = 1;
+            if (implicit) {
+                rgm.w_q = q;
+                rgm.w_magic = magic;
+            }
+        }
+    }
     SML_HIP(hipMemcpy(c->d_rd + i, &rgm, sizeof(RegionDev), hipMemcpyHostToDevice));
     c->ell_ok = -1;
     double ms[2 * kMeanStd];
@@ -1247,7 +1448,8 @@ int check_region(const sml_reservoirs *c, int i) {
 // ------------------------------------------------------------------ API
 extern "C" int sml_res_destroy(sml_reservoirs *c) {
     if (!c) return SML_OK;
-    void *ells[] = {c->d_a_ell_col, c->d_w_ell_col, c->d_a_ell_val, c->d_w_ell_val};
+    void *ells[] = {c->d_a_ell_col, c->d_w_ell_col, c->d_a_ell_val, c->d_w_ell_val, c->d_a_om,
+                    c->d_a_ob,      c->d_a_oc,      c->d_a_ov,      c->d_zero};
     for (void *p : ells)
         if (p) (void)hipFree(p);
     void *ptrs[] = {c->d_rd,    c->d_a_rp,    c->d_w_rp,   c->d_a_col,  c->d_w_col,  c->d_a_val,  c->d_w_val,
@@ -1319,6 +1521,8 @@ int res_create_impl(int numregions, int nlocal, const int *region_ids, const uns
     if (const char *e = std::getenv("SML_BEGIN")) c->begin_env = std::max(0, std::min(2, std::atoi(e)));
     if (const char *e = std::getenv("SML_UPD_BAL")) c->upd_bal = *e != '0';
     if (const char *e = std::getenv("SML_FIN_UNGROUPED")) c->finish_ungrouped = *e == '1';
+    if (const char *e = std::getenv("SML_NO_ELL")) c->no_ell = *e == '1';
+    if (const char *e = std::getenv("SML_UPD_DEPTH")) c->upd_depth = std::atoi(e) == 3 ? 3 : 2;
     SML_REQUIRE(c->read_waves >= 0, "bad read_waves");
     (void)hipGetDevice(&c->device);
     (void)hipDeviceGetAttribute(&c->ncu, hipDeviceAttributeMultiprocessorCount, c->device);
@@ -1363,7 +1567,6 @@ int res_create_impl(int numregions, int nlocal, const int *region_ids, const uns
         r.n = n[i];
         r.ninp = c->ninp[i];
         r.ld = c->ld[i];
-        r.pad_ = 0;
         r.a_rp = c->tot_a_rp;
         c->tot_a_rp += n[i] + 1;
         r.a_nz = c->tot_a_nz;
@@ -1388,18 +1591,30 @@ int res_create_impl(int numregions, int nlocal, const int *region_ids, const uns
         c->maxn = std::max(c->maxn, n[i]);
         c->maxninp = std::max(c->maxninp, c->ninp[i]);
         // makesparse rows hold floor(k/n) or floor(k/n)+1 entries (per-block permutations)
-        c->a_ell_cap.push_back(k[i] / n[i] + 1 <= kEllA ? kEllA : 0);
-        c->w_ell_cap.push_back(kEllW);
-        r.a_w = r.w_w = 0;
+        c->a_ell_cap.push_back(!c->no_ell && k[i] / n[i] + 1 <= kEllA ? kEllA : 0);
+        c->w_ell_cap.push_back(c->no_ell ? 0 : kEllW);
+        r.a_w = r.w_w = r.a_ov = r.w_q = 0;
+        r.w_magic = 0;
         r.a_ell = c->tot_a_ell;
         c->tot_a_ell += (int64_t)c->a_ell_cap.back() * n[i];
         r.w_ell = c->tot_w_ell;
         c->tot_w_ell += (int64_t)c->w_ell_cap.back() * n[i];
+        r.a_om = c->tot_a_om;
+        c->tot_a_om += c->a_ell_cap.back() ? (n[i] + 63) / 64 : 0;
+        r.a_oe = c->tot_a_oe;
+        c->tot_a_oe += c->a_ell_cap.back() ? n[i] : 0;
     }
     const size_t wb = wbytes(c);
     int rc;
-    if ((rc = dalloc(&c->d_a_ell_col, c->tot_a_ell)) || (rc = dalloc_bytes(&c->d_a_ell_val, c->tot_a_ell * wb)) ||
-        (rc = dalloc(&c->d_w_ell_col, c->tot_w_ell)) || (rc = dalloc_bytes(&c->d_w_ell_val, c->tot_w_ell * wb))) {
+    if ((rc = dalloc(&c->d_a_ell_col, std::max<int64_t>(c->tot_a_ell, 1))) ||
+        (rc = dalloc_bytes(&c->d_a_ell_val, std::max<int64_t>(c->tot_a_ell, 1) * wb)) ||
+        (rc = dalloc(&c->d_w_ell_col, std::max<int64_t>(c->tot_w_ell, 1))) ||
+        (rc = dalloc_bytes(&c->d_w_ell_val, std::max<int64_t>(c->tot_w_ell, 1) * wb)) ||
+        (rc = dalloc(&c->d_a_om, std::max<int64_t>(c->tot_a_om, 1))) ||
+        (rc = dalloc(&c->d_a_ob, std::max<int64_t>(c->tot_a_om, 1))) ||
+        (rc = dalloc(&c->d_a_oc, std::max<int64_t>(c->tot_a_oe, 1))) ||
+        (rc = dalloc_bytes(&c->d_a_ov, std::max<int64_t>(c->tot_a_oe, 1) * wb)) ||
+        (rc = dalloc_bytes(&c->d_zero, 256))) {
         sml_res_destroy(c);
         return rc;
     }
@@ -1415,6 +1630,7 @@ int res_create_impl(int numregions, int nlocal, const int *region_ids, const uns
         return rc;
     }
     hipError_t e = hipSuccess;
+    if (e == hipSuccess) e = hipMemset(c->d_zero, 0, 256);
     if (e == hipSuccess) e = hipMemset(c->d_a_rp, 0, std::max<int64_t>(c->tot_a_rp, 1) * 4);
     if (e == hipSuccess) e = hipMemset(c->d_w_rp, 0, std::max<int64_t>(c->tot_w_rp, 1) * 4);
     if (e == hipSuccess) e = hipMemset(c->d_wout, 0, std::max<int64_t>(c->tot_wout * wb, 16));
@@ -1550,6 +1766,18 @@ extern "C" int sml_res_update_balanced(sml_reservoirs *c, int *balanced) {
     return SML_OK;
 }
 
+extern "C" int sml_res_ell_layout(sml_reservoirs *c, int i, int *a_width, int *a_overflow, int *win_q,
+                                  int *win_ell) {
+    if (int rc = check_region(c, i)) return rc;
+    SML_REQUIRE(a_width && a_overflow && win_q && win_ell, "null argument");
+    const RegionDev &r = c->rd[i];
+    *a_width = r.a_w;
+    *a_overflow = r.a_ov;
+    *win_q = r.w_q;
+    *win_ell = r.w_w;
+    return SML_OK;
+}
+
 extern "C" int sml_res_set_read_waves(sml_reservoirs *c, int waves) {
     SML_REQUIRE(c && waves >= 0, "bad argument");
     if (!std::getenv("SML_READ_WAVES")) c->read_waves = waves;
@@ -1606,6 +1834,11 @@ extern "C" int sml_res_kernel_times(sml_reservoirs *c, float *update_ms, float *
 }
 
 namespace {
+Ell make_ell(const sml_reservoirs *c) {
+    return Ell{c->d_a_ell_col, c->d_a_ell_val, c->d_w_ell_col, c->d_w_ell_val, c->d_a_om,
+               c->d_a_ob,      c->d_a_oc,      c->d_a_ov,      c->d_zero};
+}
+
 // x_new = (1 - leak) x + leak tanh(A x + W_in u) for every local region (+ x~, x_aug)
 bool bal_usable(sml_reservoirs *c) {
     if (!c->upd_bal || c->nlocal == 0) return false;
@@ -1638,13 +1871,39 @@ int launch_update_bal(sml_reservoirs *c, const double *xo, double *xn, const dou
     }
     const int lds_x = (c->maxn + 1) / 2 * 2, lds_buf = lds_x + c->maxninp;
     const size_t lds = 2 * (size_t)lds_buf * sizeof(double);
-    Ell ell{c->d_a_ell_col, c->d_a_ell_val, c->d_w_ell_col, c->d_w_ell_val};
+    const Ell ell = make_ell(c);
+    // the pairs every pass loads (the widest region's; 2 at least) and whether any
+    // region keeps an overflow list
+    int np = 2;
+    bool ovf = false;
+    for (int i = 0; i < c->nlocal; ++i) {
+        np = std::max(np, (c->rd[i].a_w + 1) / 2);
+        ovf = ovf || c->rd[i].a_ov;
+    }
+    auto go = [&](auto kern) {
+        hipLaunchKernelGGL(kern, dim3(G), dim3(kUpdThreads), lds, st, c->d_rd, c->d_row0, c->d_blk_r0, c->nlocal,
+                           total, ell, xo, xn, d_feedback, c->leakage, lds_x, lds_buf);
+    };
+#define SML_BAL_D(WT, D)                                                                                    \
+    do {                                                                                                    \
+        if (np == 2) ovf ? go(k_res_update_bal<WT, 2, true, D>) : go(k_res_update_bal<WT, 2, false, D>);    \
+        else if (np == 3) ovf ? go(k_res_update_bal<WT, 3, true, D>) : go(k_res_update_bal<WT, 3, false, D>); \
+        else ovf ? go(k_res_update_bal<WT, 4, true, D>) : go(k_res_update_bal<WT, 4, false, D>);             \
+    } while (0)
+#define SML_BAL(WT)                       \
+    do {                                  \
+        if (c->upd_depth == 3 && wb4)     \
+            SML_BAL_D(WT, 3);             \
+        else                              \
+            SML_BAL_D(WT, 2);             \
+    } while (0)
+    const bool wb4 = c->wdtype == SML_F32;  // (fp64 weights: depth 2 only, for the registers)
     if (c->wdtype == SML_F32)
-        hipLaunchKernelGGL(k_res_update_bal<float>, dim3(G), dim3(kUpdThreads), lds, st, c->d_rd, c->d_row0,
-                           c->d_blk_r0, c->nlocal, total, ell, xo, xn, d_feedback, c->leakage, lds_x, lds_buf);
+        SML_BAL(float);
     else
-        hipLaunchKernelGGL(k_res_update_bal<double>, dim3(G), dim3(kUpdThreads), lds, st, c->d_rd, c->d_row0,
-                           c->d_blk_r0, c->nlocal, total, ell, xo, xn, d_feedback, c->leakage, lds_x, lds_buf);
+        SML_BAL(double);
+#undef SML_BAL
+#undef SML_BAL_D
     SML_HIP(hipGetLastError());
     return SML_OK;
 }
@@ -1672,7 +1931,7 @@ int launch_update(sml_reservoirs *c, const double *xo, double *xn, const double 
     hipLaunchKernelGGL(occ2 ? (k_res_update<WT, L, 8>) : (k_res_update<WT, L, 4>), ug, dim3(kUpdThreads),        \
                        L ? lds : 0, st, c->d_rd, c->d_a_rp, c->d_a_col, (const WT *)c->d_a_val, c->d_w_rp,        \
                        c->d_w_col, (const WT *)c->d_w_val, ell, xo, xn, d_feedback, c->leakage, bpr, lds_x, nlog)
-    Ell ell{c->d_a_ell_col, c->d_a_ell_val, c->d_w_ell_col, c->d_w_ell_val};
+    const Ell ell = make_ell(c);
     if (c->wdtype == SML_F32) {
         if (use_lds)
             SML_UPD(float, true);
@@ -1705,7 +1964,7 @@ int launch_begin(sml_reservoirs *c, const double *xo, double *xn, const double *
     const int lds_x = (c->maxn + 1) / 2 * 2;
     const size_t lds = (size_t)(lds_x + c->maxninp) * sizeof(double);
     const int groups = c->nout_pad / kRowsWide;
-    Ell ell{c->d_a_ell_col, c->d_a_ell_val, c->d_w_ell_col, c->d_w_ell_val};
+    const Ell ell = make_ell(c);
     auto go = [&](auto wt_tag, auto kern) {
         using WT = decltype(wt_tag);
         hipLaunchKernelGGL(kern, dim3(c->nlocal), dim3(kBeginThreads), lds, st, c->d_rd, c->d_a_rp, c->d_a_col,

@@ -130,6 +130,54 @@ __device__ inline void fft_fj(int t, bool io, int &f, int &j) {
     }
 }
 
+// k_gridx's transform and stores of one thread (rfftb half h of transform (f, j))
+__device__ __attribute__((always_inline)) inline void gridx_store(const double (&xi)[kMX2 - 1], int h, int f, int j,
+                                                                  const double *was, const double *__restrict__ cosgr,
+                                                                  int c0, int c1, double *__restrict__ grid,
+                                                                  double *__restrict__ g4, double *__restrict__ logp,
+                                                                  const IoExit &ex, const double (&mmv)[8]) {
+    double y[kFftN / 2];
+    fft::rfftb96_half([&](int e) { return e <= kMX2 - 2 ? xi[e] : 0.0; }, h, y, was);
+    const bool k2 = f >= c0 && f < c1;
+    const double cj = k2 ? cosgr[j] : 1.0;
+    double *g = grid + (size_t)f * kGridField + j * kIX;
+    int gs = 1;
+    if (g4) {
+        const int grp = f / kKX, k = f % kKX;
+        size_t o;
+        if (grp < 4) {
+            const int var = grp == 0 ? 1 : grp == 1 ? 2 : grp == 2 ? 0 : 3;
+            o = var + 4 * ((size_t)kGridField * k + j * kIX);
+            g = g4 + o;
+            gs = 4;
+        } else {
+            o = (size_t)j * kIX;
+            g = logp + o;
+        }
+        if (ex.mm) {  // run_model's exit (uniform across the launch: every thread reads the same flag)
+            const bool q = grp == 3;
+            if (!io_state_safe(mmv)) {  // integration skipped: the input grid comes back
+                const double *src = grp < 4 ? ex.in4 + o : ex.inlp + o;
+#pragma unroll
+                for (int qq = 0; qq < kFftN / 2; ++qq) {
+                    const int e = 2 * qq + h;
+                    const double vv = src[e * gs];
+                    g[e * gs] = (q && vv < ex.qfloor) ? ex.qfloor : vv;
+                }
+                return;
+            }
+#pragma unroll
+            for (int qq = 0; qq < kFftN / 2; ++qq) {
+                const double vv = k2 ? y[qq] * cj : y[qq];
+                g[(2 * qq + h) * gs] = (q && vv < ex.qfloor) ? ex.qfloor : vv;
+            }
+            return;
+        }
+    }
+#pragma unroll
+    for (int qq = 0; qq < kFftN / 2; ++qq) g[(2 * qq + h) * gs] = k2 ? y[qq] * cj : y[qq];
+}
+
 __global__ __launch_bounds__(kFftThreads) void k_gridx(const double *__restrict__ varm, double *__restrict__ grid,
                                                        const double *__restrict__ wa, const double *__restrict__ cosgr,
                                                        int nf, int c0, int c1, double *__restrict__ g4,
@@ -177,47 +225,15 @@ __global__ __launch_bounds__(kFftThreads) void k_gridx(const double *__restrict_
     if (threadIdx.x < kFftWa) was[threadIdx.x] = wa[threadIdx.x];
     if (threadIdx.x + kFftThreads < kFftWa) was[threadIdx.x + kFftThreads] = wa[threadIdx.x + kFftThreads];
     __syncthreads();
-    if (!act) return;
-    double y[kFftN / 2];
-    fft::rfftb96_half([&](int e) { return e <= kMX2 - 2 ? xi[e] : 0.0; }, h, y, was);
-    const bool k2 = f >= c0 && f < c1;
-    const double cj = k2 ? cosgr[j] : 1.0;
-    double *g = grid + (size_t)f * kGridField + j * kIX;
-    int gs = 1;
-    if (g4) {
-        const int grp = f / kKX, k = f % kKX;
-        size_t o;
-        if (grp < 4) {
-            const int var = grp == 0 ? 1 : grp == 1 ? 2 : grp == 2 ? 0 : 3;
-            o = var + 4 * ((size_t)kGridField * k + j * kIX);
-            g = g4 + o;
-            gs = 4;
-        } else {
-            o = (size_t)j * kIX;
-            g = logp + o;
-        }
-        if (ex.mm) {  // run_model's exit (uniform across the launch: every thread reads the same flag)
-            const bool q = grp == 3;
-            if (!io_state_safe(mmv)) {  // integration skipped: the input grid comes back
-                const double *src = grp < 4 ? ex.in4 + o : ex.inlp + o;
-#pragma unroll
-                for (int qq = 0; qq < kFftN / 2; ++qq) {
-                    const int e = 2 * qq + h;
-                    const double vv = src[e * gs];
-                    g[e * gs] = (q && vv < ex.qfloor) ? ex.qfloor : vv;
-                }
-                return;
-            }
-#pragma unroll
-            for (int qq = 0; qq < kFftN / 2; ++qq) {
-                const double vv = k2 ? y[qq] * cj : y[qq];
-                g[(2 * qq + h) * gs] = (q && vv < ex.qfloor) ? ex.qfloor : vv;
-            }
-            return;
+    if (act) gridx_store(xi, h, f, j, was, cosgr, c0, c1, grid, g4, logp, ex, mmv);
+    if (ex.sig) {  // MI355X_MICROARCH.md inter-workgroup visibility, the producer form
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            __hip_atomic_fetch_add(ex.sig, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
-#pragma unroll
-    for (int qq = 0; qq < kFftN / 2; ++qq) g[(2 * qq + h) * gs] = k2 ? y[qq] * cj : y[qq];
 }
 
 // specx (spe_subfft_fftpack.f90:55-87): fvar = vorg(:, j) (the first nscaled fields
@@ -728,6 +744,8 @@ int spectral_gridx_range(sml_spectral *s, const double *varm, double *grid, int 
 int spectral_gridx_io(sml_spectral *s, const double *varm, double *g4, double *logp, int nwind, hipStream_t st) {
     return spectral_gridx_run_model_exit(s, varm, g4, logp, nwind, IoExit{}, st);
 }
+
+int spectral_exit_blocks() { return (2 * (4 * kKX + 1) * kIL + kFftThreads - 1) / kFftThreads; }
 
 int spectral_gridx_run_model_exit(sml_spectral *s, const double *varm, double *g4, double *logp, int nwind,
                                   IoExit ex, hipStream_t st) {

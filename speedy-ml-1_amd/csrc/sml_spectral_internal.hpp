@@ -61,7 +61,12 @@ struct IoExit {
     const unsigned *cnt = nullptr;
     unsigned target = 0;
     unsigned *late = nullptr;
+    // the forecast's hand-off to another stream without a signal kernel: each block,
+    // its stores drained and released at agent scope, adds 1 (spectral_exit_blocks()
+    // adds per launch) -- the consumer polls *sig >= its count
+    uint64_t *sig = nullptr;
 };
+int spectral_exit_blocks();
 int spectral_gridx_run_model_exit(sml_spectral *s, const double *varm, double *g4, double *logp, int nwind,
                                   IoExit ex, hipStream_t st);
 

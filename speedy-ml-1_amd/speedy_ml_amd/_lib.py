@@ -58,7 +58,7 @@ EXPORTED = (
     "sml_hybrid_exchange_width", "sml_hybrid_slab_buffers", "sml_dyn_set_hybrid_sst", "sml_dyn_set_sea_ice",
     "sml_hybrid_set_pipelined", "sml_res_step_cancel", "sml_res_step_begun", "sml_hybrid_set_force_exchange",
     "sml_hybrid_exchanges", "sml_hybrid_set_chain", "sml_hybrid_chain", "sml_hybrid_exchange_stream",
-    "sml_res_set_update_cus", "sml_res_update_balanced", "sml_probe_mfma_f64_clock",
+    "sml_res_set_update_cus", "sml_res_update_balanced", "sml_probe_mfma_f64_clock", "sml_res_ell_layout",
 )
 
 SML_HOP_AUTO, SML_HOP_WAIT_VALUE, SML_HOP_EVENTS, SML_HOP_KERNEL = 0, 1, 2, 3
@@ -240,9 +240,12 @@ def _declare(L: ctypes.CDLL) -> None:
         "sml_hybrid_exchange_stream": [vp, pp],
         "sml_res_set_update_cus": [vp, i],
         "sml_res_update_balanced": [vp, ip],
+        "sml_res_ell_layout": [vp, i, ip, ip, ip, ip],
         "sml_probe_mfma_f64_clock": [i, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)],
     }
     for name, args in sig.items():
+        if os.environ.get("SML_LIB") and not hasattr(L, name):
+            continue  # an older build for an A/B: entry points added since are absent
         fn = getattr(L, name)
         fn.argtypes = args
         fn.restype = i

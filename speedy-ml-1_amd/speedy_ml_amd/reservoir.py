@@ -146,6 +146,12 @@ class Reservoirs:
         check(lib().sml_res_update_balanced(self._h, ctypes.byref(b)))
         return bool(b.value)
 
+    def ell_layout(self, i: int) -> dict:
+        """Local region i's compressed A / W_in form (sml_res_ell_layout)."""
+        v = [ctypes.c_int() for _ in range(4)]
+        check(lib().sml_res_ell_layout(self._h, int(i), *[ctypes.byref(x) for x in v]))
+        return dict(a_width=v[0].value, a_overflow=bool(v[1].value), win_q=v[2].value, win_ell=bool(v[3].value))
+
     def set_begin_mode(self, mode: int):
         """predict_begin's form: 0 update grid + readout grid, 1 / 2 one fused launch
         (sml_res_set_begin_mode); bit-identical results."""

@@ -557,3 +557,72 @@ def test_balanced_update_is_bitwise_the_per_region_update(cuda, cus):
         np.testing.assert_array_equal(a, b)
     for i, (a, b) in enumerate(zip(states[False], states[True])):
         np.testing.assert_array_equal(a, b, err_msg=f"region {regions[i]}")
+
+
+def test_ell_layouts_are_bitwise_the_csr_update(cuda):
+    """A's ELL main width chosen per region (pair-major slots, an overflow list for the
+    rows one longer) and W_in's implicit block-diagonal column: every
+    layout the builder picks gives the states and outvecs of the CSR copies
+    (SML_NO_ELL=1) bit for bit, in the balanced and the per-region update, over 3
+    steps -- and the oracle's within its tolerance.  Regions: every full-size shape
+    class (n 6048 with 4.8 % of rows one longer -> overflow; 5880 / 5760 -> 6 slots;
+    6160 -> overflow), a region of 2- and 3-entry rows (2 slots + overflow), and a W_in
+    whose columns are permuted (not block-diagonal: its column is read)."""
+    import os
+
+    import torch
+
+    from speedy_ml_amd.reservoir import Reservoirs
+
+    mask = domain.load_sst_mask()
+    regions = [0, 5, 23, 24, 600, 1127, 1151, 300, 301]
+    ws = [region_weights(r, bool(mask[r])) for r in regions[:7]]
+    w3 = region_weights(300, bool(mask[300]), n_override=3000)  # k = 0.001 n^2 ~ 2.6 n: rows of 2 or 3
+    wp = region_weights(301, bool(mask[301]), n_override=2000)
+    perm = np.random.default_rng(5).permutation(wp.ninp)
+    wp.win = wp.win[perm].copy()  # each row still one entry, columns no longer i / q
+    ws += [w3, wp]
+    fb = np.concatenate([feedback_vector(r, w.ninp) for r, w in zip(regions, ws)])
+    lm = np.stack([local_model_vector(r) for r in regions])
+    outs, states, layouts = {}, {}, {}
+    for form in ("csr", "per_region", "balanced"):
+        env = {"csr": {"SML_NO_ELL": "1", "SML_UPD_BAL": "0"}, "per_region": {"SML_UPD_BAL": "0"}, "balanced": {}}[form]
+        os.environ.update(env)
+        try:
+            res = Reservoirs(regions, mask[regions], [w.n for w in ws], [w.k for w in ws])
+        finally:
+            for k in env:
+                os.environ.pop(k, None)
+        for i, w in enumerate(ws):
+            res.load_region_weights(i, w)
+            res.set_state(i, initial_state(regions[i], w.n))
+        assert res.update_balanced() == (form == "balanced")
+        layouts[form] = [res.ell_layout(i) for i in range(len(regions))]
+        dfb, dlm = torch.from_numpy(fb).to(cuda), torch.from_numpy(lm).to(cuda)
+        ov = torch.zeros((len(regions), 136), dtype=torch.float64, device=cuda)
+        got = []
+        for step in range(3):
+            res.predict(dfb, dlm, ov)
+            torch.cuda.synchronize()
+            got.append(ov.cpu().numpy().copy())
+        outs[form] = got
+        states[form] = [res.get_state(i) for i in range(len(regions))]
+        res.close()
+    assert all(lay["a_width"] == 0 and not lay["win_ell"] for lay in layouts["csr"])
+    lay = layouts["balanced"]
+    by_n = {w.n: lay[i] for i, w in enumerate(ws[:7])}
+    assert by_n[6048]["a_width"] == 6 and by_n[6048]["a_overflow"]
+    assert by_n[5880]["a_width"] == 6 and not by_n[5880]["a_overflow"]
+    assert lay[7]["a_width"] == 2 and lay[7]["a_overflow"]
+    assert all(lay[i]["win_q"] == ws[i].n // ws[i].ninp for i in range(8))
+    assert lay[8]["win_q"] == 0 and lay[8]["win_ell"]
+    for form in ("per_region", "balanced"):
+        for a, b in zip(outs["csr"], outs[form]):
+            np.testing.assert_array_equal(a, b, err_msg=form)
+        for i, (a, b) in enumerate(zip(states["csr"], states[form])):
+            np.testing.assert_array_equal(a, b, err_msg=f"{form} region {regions[i]}")
+    # and the oracle, one step from the start state
+    o = np.concatenate([[0], np.cumsum([w.ninp for w in ws])])
+    for i, w in enumerate(ws):
+        ref, x1 = _oracle_step(w, initial_state(w.region, w.n), fb[o[i]:o[i + 1]], lm[i])
+        _check(outs["balanced"][0][i], ref, OUT_TOL)
