@@ -109,6 +109,8 @@ struct sml_dynamics {
     HopWait entry_wait;
     // the next run_model's exit signals its forecast in-kernel (sml::dyn_run_model_signal)
     uint64_t *exit_sig = nullptr;
+    // the next run_model's entry signals its input grid in-kernel (sml::dyn_run_model_entry_signal)
+    uint64_t *entry_sig = nullptr;
     unsigned chk_count = 0;
     bool chk_counted = false;  // the last launch_io_check added to the counter
     // host copy of the last check's min/max (pinned; written behind the check on its
@@ -2759,8 +2761,10 @@ extern "C" int sml_dyn_from_grid(sml_dynamics *d, const double *d_grid4d, const 
     }
     // entry (:503-518): real(4) copies, q clip, then vdspec kcos = 2 (x cosgr) on the
     // winds and none on the rest: one specx launch reading variables3d / logp
-    const HopWait w = d->entry_wait;
+    HopWait w = d->entry_wait;
+    w.sig = d->entry_sig;
     d->entry_wait = HopWait{};  // one launch
+    d->entry_sig = nullptr;
     if (int rc = spectral_specx_io(d->sp, d_grid4d, d_logp, d->d_varm, kNIoWind, st, w)) return rc;
     if (int rc = spectral_specy(d->sp, d->d_varm, d->d_sfwd, kNIo, st)) return rc;
     hipLaunchKernelGGL(k_io_combine, dim3((kMN + 127) / 128, kKX), dim3(128), 0, st, d->d_sfwd, d->d_state, T);
@@ -2809,8 +2813,10 @@ extern "C" int sml_dyn_run_model(sml_dynamics *d, const double *d_grid4d, const 
             SML_HIP(hipStreamWaitEvent(st, d->ev_chk, 0));
             d->chk_pending = false;
         }
-        const HopWait w = d->entry_wait;
+        HopWait w = d->entry_wait;
+        w.sig = d->entry_sig;
         d->entry_wait = HopWait{};  // one launch
+        d->entry_sig = nullptr;
         if (int rc = spectral_specx_io(d->sp, d_grid4d, d_logp, d->d_vfm, kNIoWind, st, w)) return rc;
         const SpectralDev sd = spectral_dev(d->sp);
         const bool phys = d->phys_on;
@@ -2901,6 +2907,22 @@ int sml::dyn_run_model_wait(sml_dynamics *d, const uint64_t *flag, uint64_t valu
 // the next run_model's exit kernel adds *adds to *counter once its forecast is
 // released (each of its blocks adds 1): the hybrid loop's forecast hop without a
 // signal kernel behind the exit
+// the event behind the last safety check issued on the check stream (null if none)
+int sml::dyn_check_event(sml_dynamics *d, void **ev) {
+    SML_REQUIRE(d && ev, "null argument");
+    *ev = d->chk_stream ? (void *)d->ev_chk : nullptr;
+    return SML_OK;
+}
+
+// the next run_model's entry kernel (iogrid(30)'s specx) adds *adds to *counter as it
+// starts: its input grid is complete and released by then
+int sml::dyn_run_model_entry_signal(sml_dynamics *d, uint64_t *counter, int *adds) {
+    SML_REQUIRE(d && counter && adds, "null argument");
+    d->entry_sig = counter;
+    *adds = spectral_specx_io_blocks();
+    return SML_OK;
+}
+
 int sml::dyn_run_model_signal(sml_dynamics *d, uint64_t *counter, int *adds) {
     SML_REQUIRE(d && counter && adds, "null argument");
     d->exit_sig = counter;

@@ -1033,11 +1033,25 @@ int predict_impl(sml_hybrid *h, bool assemble) {
         if (h->chain) {  // the finish follows the window on SPEEDY's stream, once the begin is done
             xs = h->side;
             if (int rc = hop_signal(h, sml_hybrid::kHopBegun, h->main)) return rc;
-            if (int rc = hop_wait(h, sml_hybrid::kHopBegun, xs)) return rc;
+            if (h->use_kernels && h->nlocal > 0) {  // waited for inside the finish (no wait kernel)
+                if (int rc = sml::res_finish_wait(h->res, h->d_seq + sml_hybrid::kHopBegun * sml_hybrid::kSeqStride,
+                                                  h->seq[sml_hybrid::kHopBegun], hop_late_word(h)))
+                    return rc;
+            } else if (int rc = hop_wait(h, sml_hybrid::kHopBegun, xs)) {
+                return rc;
+            }
         } else if (h->use_kernels && h->nlocal > 0) {
             // SPEEDY's forecast of the previous window, waited for inside the finish: its
             // weights load while the window runs (k_res_finish_grid's wflag; the main
-            // stream's later work still follows the finish, so it follows the window too)
+            // stream's later work still follows the finish, so it follows the window too).
+            // The finish's blocks spin on the reservoir's CUs, and the window's exit (the
+            // forecast's producer) waits for its safety check, which runs on those CUs:
+            // the finish launches only once that check is done (a CP wait on the main
+            // stream, satisfied while the window still runs), or a host that enqueues
+            // steps without polling run_speedy could starve the check behind the finish
+            void *ev = nullptr;
+            if (int rc = sml::dyn_check_event(h->dyn, &ev)) return rc;
+            if (ev) SML_HIP(hipStreamWaitEvent(h->main, (hipEvent_t)ev, 0));
             if (int rc = sml::res_finish_wait(h->res, h->d_seq + sml_hybrid::kHopLm * sml_hybrid::kSeqStride,
                                               h->seq[sml_hybrid::kHopLm], hop_late_word(h)))
                 return rc;
@@ -1080,8 +1094,24 @@ extern "C" int sml_hybrid_advance(sml_hybrid *h, const double *d_outvec_all) {
     if (!done)
         if (int rc = sml_exchange_assemble(h->res, d_outvec_all, h->g4, h->g2, h->pr, c)) return rc;
     if (int rc = slab_sst(h, d_outvec_all, c)) return rc;
-    if (h->overlap)  // the assembled grid: to SPEEDY's stream (two-stream) / to the main stream (chain)
+    // chain on SPEEDY's stream with kernel hops: the next run_model's entry specx signals
+    // the assembled grid as it starts (no signal kernel in front of the window); run_model
+    // is then enqueued before the main stream's wait for that signal -- every in-kernel
+    // wait is enqueued after its producer, so no wait can hold a hardware queue that its
+    // producer sits behind
+    const bool entry_sig = h->overlap && h->chain && h->use_kernels;
+    if (entry_sig) {
+        int adds = 0;
+        if (int rc = sml::dyn_run_model_entry_signal(h->dyn, h->d_seq + sml_hybrid::kHopGrid * sml_hybrid::kSeqStride,
+                                                     &adds))
+            return rc;
+        h->seq[sml_hybrid::kHopGrid] += (uint64_t)adds;
+        if (int rc = sml_dyn_run_model(h->dyn, h->g4, h->g2, h->nleap, h->delt, h->alph, h->rob, h->wil, h->f4, h->f2,
+                                       s))
+            return rc;
+    } else if (h->overlap) {  // the assembled grid: to SPEEDY's stream (two-stream) / to the main stream (chain)
         if (int rc = hop_signal(h, sml_hybrid::kHopGrid, c)) return rc;
+    }
     if (h->chain)
         if (int rc = hop_wait(h, sml_hybrid::kHopGrid, m)) return rc;
     ++h->t;
@@ -1118,8 +1148,10 @@ extern "C" int sml_hybrid_advance(sml_hybrid *h, const double *d_outvec_all) {
         if (int rc = sml::dyn_run_model_signal(h->dyn, h->d_seq + sml_hybrid::kHopLm * sml_hybrid::kSeqStride,
                                                &exit_adds))
             return rc;
-    if (int rc = sml_dyn_run_model(h->dyn, h->g4, h->g2, h->nleap, h->delt, h->alph, h->rob, h->wil, h->f4, h->f2, s))
-        return rc;
+    if (!entry_sig)
+        if (int rc = sml_dyn_run_model(h->dyn, h->g4, h->g2, h->nleap, h->delt, h->alph, h->rob, h->wil, h->f4, h->f2,
+                                       s))
+            return rc;
     if (exit_adds > 0) {  // the exit's blocks each add 1 to the hop's word once released
         h->seq[sml_hybrid::kHopLm] += (uint64_t)exit_adds;
     } else if (hops) {

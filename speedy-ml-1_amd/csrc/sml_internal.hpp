@@ -27,6 +27,8 @@ int res_finish_wait(sml_reservoirs *c, const uint64_t *flag, uint64_t value, uns
 // until *flag >= value before it reads its input grids
 int dyn_run_model_wait(sml_dynamics *d, const uint64_t *flag, uint64_t value, unsigned *late);
 int dyn_run_model_signal(sml_dynamics *d, uint64_t *counter, int *adds);
+int dyn_run_model_entry_signal(sml_dynamics *d, uint64_t *counter, int *adds);
+int dyn_check_event(sml_dynamics *d, void **ev);  // a hipEvent_t
 
 // --------------------------------------------------------------- geometry
 // Restatement of the res_domain.f90 decomposition used by every reservoir of the

@@ -250,6 +250,7 @@ __global__ __launch_bounds__(kFftThreads) void k_specx(const double *__restrict_
                                                        HopWait wait = {}) {
     __shared__ double was[kFftWa];
     __shared__ double S[kFftN * (kFftThreads / 2)];  // a pair's two n = 48 halves (E, O)
+    if (wait.sig && threadIdx.x == 0) __hip_atomic_fetch_add(wait.sig, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // wait.flag: the grid comes from another stream (SML_HOP_KERNEL): the twiddles are
     // staged first, then one lane polls, acquires at agent scope and releases the
     // block (MI355X_MICROARCH.md inter-workgroup visibility, the consumer form)
@@ -772,6 +773,8 @@ int spectral_specx_split(sml_spectral *s, const double *grid, double *varm, int 
     SML_HIP(hipGetLastError());
     return SML_OK;
 }
+
+int spectral_specx_io_blocks() { return (2 * (4 * kKX + 1) * kIL + kFftThreads - 1) / kFftThreads; }
 
 int spectral_specx_io(sml_spectral *s, const double *g4, const double *logp, double *varm, int nwind,
                       hipStream_t st, HopWait wait) {

@@ -42,7 +42,12 @@ struct HopWait {
     const uint64_t *flag = nullptr;
     uint64_t value = 0;
     unsigned *late = nullptr;
+    // signal at the kernel's start: lane 0 of each block adds 1 (the kernel's input
+    // grid was released by the kernel before it on the stream; the chain on SPEEDY's
+    // stream hands the assembled grid to the main stream's re-tiling this way)
+    uint64_t *sig = nullptr;
 };
+int spectral_specx_io_blocks();
 int spectral_specx_io(sml_spectral *s, const double *g4, const double *logp, double *varm, int nwind,
                       hipStream_t st, HopWait wait = {});
 int spectral_gridx_io(sml_spectral *s, const double *varm, double *g4, double *logp, int nwind, hipStream_t st);

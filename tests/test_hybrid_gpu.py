@@ -386,3 +386,35 @@ def test_pipelined_loop_restart_is_bitwise_the_default_loop(cuda):
     for a, b in zip(runs[False], runs[True]):
         for k in a:
             np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+
+
+def test_chain_on_speedys_stream_is_bitwise_the_two_stream_loop(cuda):
+    """sml_hybrid_set_chain(SML_CHAIN_SPEEDY) on one rank, pipelined, kernel hops: the
+    finish waits for its begin inside the kernel and run_model's entry specx signals the
+    assembled grid to the re-tiling as it starts (no hop kernel on SPEEDY's stream).
+    4 steps issued back to back, then one sync: every buffer bitwise the two-stream
+    loop's.  Both loops enqueue the steps without polling run_speedy: the two-stream
+    loop's finish (spinning on the reservoir's CUs) must not starve the safety check the
+    window's exit waits for."""
+    import torch
+
+    from speedy_ml_amd._lib import SML_CHAIN_SPEEDY, SML_CHAIN_TWO_STREAMS
+
+    runs = {}
+    for mode in (SML_CHAIN_TWO_STREAMS, SML_CHAIN_SPEEDY):
+        loop, _ = _loop(cuda, True)
+        loop.set_pipelined(True)
+        loop.set_chain(mode)
+        for _ in range(4):
+            loop.step()
+        loop.sync()
+        runs[mode] = (_snapshot(loop), [loop.res.get_state(i) for i in (0, 700)])
+        loop.close()
+        loop.dyn.close()
+        loop.res.close()
+        torch.cuda.synchronize()
+    (sa, xa), (sb, xb) = runs[SML_CHAIN_TWO_STREAMS], runs[SML_CHAIN_SPEEDY]
+    for k in sa:
+        np.testing.assert_array_equal(sa[k], sb[k], err_msg=k)
+    for a, b in zip(xa, xb):
+        np.testing.assert_array_equal(a, b)
