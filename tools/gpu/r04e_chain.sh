@@ -14,9 +14,8 @@ for i in 1 2; do
     C=two-streams; [ $v = B ] && C=speedy
     $T 240 $B --chain $C > gpurun_out/r04e/n1_$v$i.json 2> gpurun_out/r04e/n1_$v$i.err || { tail -5 gpurun_out/r04e/n1_$v$i.err; exit 1; }
     $T 240 $B --chain $C --sim-ranks 8 > gpurun_out/r04e/s8_$v$i.json 2> gpurun_out/r04e/s8_$v$i.err || { tail -5 gpurun_out/r04e/s8_$v$i.err; exit 1; }
-    $T 240 $B --chain $C --sim-ranks 2 > gpurun_out/r04e/s2_$v$i.json 2> gpurun_out/r04e/s2_$v$i.err || { tail -5 gpurun_out/r04e/s2_$v$i.err; exit 1; }
     python3 -c "
-import json; a=json.load(open('gpurun_out/r04e/n1_$v$i.json')); b=json.load(open('gpurun_out/r04e/s8_$v$i.json')); c=json.load(open('gpurun_out/r04e/s2_$v$i.json'))
-print('$v', 'N1', a['value'], 'sim2', c['value'], 'sim8', b['value'], b['ms_per_step'])"
+import json; a=json.load(open('gpurun_out/r04e/n1_$v$i.json')); b=json.load(open('gpurun_out/r04e/s8_$v$i.json'))
+print('$v', 'N1', a['value'], 'sim8', b['value'], b['ms_per_step'])"
   done
 done
