@@ -532,7 +532,11 @@ extern "C" int sml_hybrid_set_pipelined(sml_hybrid *h, int on) {
 // at world 1 and in the 8-rank share -- its two remaining stream operations
 // (hipStreamWaitValue64 / WriteValue64 run as blit kernels, ~6 us each, satisfied or
 // not) stay on the critical path, and the finish and assembly get 64 CUs instead of
-// 192.  Drains both streams first.
+// 192.  With kernel hops it has no hop kernel on SPEEDY's stream at all (the finish
+// waits for its begin in-kernel, the entry specx signals the grid) and still loses
+// (r04, profiles/r04/chain_nohop: N = 1 1104 / 1109 vs 1123 / 1123 steps/s, 8-rank
+// share 1185 / 1186 vs 1194 / 1195): the finish and assembly on 64 CUs cost more than
+// the two signal kernels.  Drains both streams first.
 extern "C" int sml_hybrid_set_chain(sml_hybrid *h, int mode) {
     SML_REQUIRE(h && (mode == SML_CHAIN_AUTO || mode == SML_CHAIN_TWO_STREAMS || mode == SML_CHAIN_SPEEDY),
                 "bad chain mode %d", mode);
