@@ -788,9 +788,20 @@ def training_leg(dev, mask, args, world, rank):
     npad = tr.npad
     # algorithmic flops: lower-triangle Gram (naug(naug+1)/2 dot products) + T S^T, 2 flops per FMA
     algo = sum(2.0 * (n * (n + 1) / 2 + 136 * n) * m * nb for n in naug)
-    # executed by the tiles (128 x 128, padded): the MFMA work actually issued
-    C = npad // 128
-    issued = len(naug) * (C * (C + 1) // 2 + 2 * C) * 2.0 * 128 * 128 * m * nb
+    # the MFMA work actually issued: each tile's 64 x 64 wave sub-tiles that hold output
+    # (k_train_gram2 skips the blocks past a region's naug, the sub-tiles above a
+    # diagonal tile's diagonal and those past naug / nout)
+    def live_quads(n):
+        cr, q = (n + 127) // 128, 0
+        for bi in range(cr):
+            for bj in range(bi + 1):
+                q += sum(1 for wr in (0, 1) for wc in (0, 1)
+                         if bi * 128 + wr * 64 < n and bj * 128 + wc * 64 < n and not (bi == bj and wr < wc))
+        for bi in range(2):
+            for bj in range(cr):
+                q += sum(1 for wr in (0, 1) for wc in (0, 1) if bi * 128 + wr * 64 < 136 and bj * 128 + wc * 64 < n)
+        return q
+    issued = sum(live_quads(n) for n in naug) * 2.0 * 64 * 64 * m * nb
     peak, ghz = ctypes.c_double(), ctypes.c_double()
     check(lib().sml_probe_mfma_f64_clock(20000, ctypes.byref(peak), ctypes.byref(ghz)))
     # the nominal peak at the clock the chip holds under back-to-back fp64 MFMA
@@ -824,20 +835,21 @@ def training_leg(dev, mask, args, world, rank):
             "probe_clock_ghz": round(ghz.value, 3),
             "frac_at_probe_clock": round(solve_tf / peak_clk, 4) if peak_clk else None,
             "algorithmic_flops": solve_algo,
-            "previous": "r02: 394 ms, 29.3 TF/s (1 wave per SIMD); rocSOLVER dpotrf + dpotrs strided-batched in r01: "
-                        "41.7 ms per region",
+            "previous": "r04a: 290.7 ms, 39.8 TF/s (every region factored at the batch's padded size); r02: 394 ms, "
+                        "29.3 TF/s (1 wave per SIMD); rocSOLVER dpotrf + dpotrs strided-batched in r01: 41.7 ms per "
+                        "region",
         },
         "roofline": {
             "kernel": "k_train_gram2 (fp64 MFMA 16x16x4, 128x128 tiles, lower triangle + T S^T strip, LDS stages "
-                      "double-buffered, 2 waves per SIMD)",
+                      "double-buffered, 2 waves per SIMD; blocks past a region's naug and wave sub-tiles without "
+                      "output skipped)",
             "bound": "mfma", "unit": "TFLOP/s",
             "achieved": round(achieved, 2),
             "issued_tflops": round(issued / (gram_ms * 1e-3) / 1e12, 2),
             "peak": F64_MFMA_PEAK_TF,
             "peak_source": "nominal: 64 clk per v_mfma_f64_16x16x4_f64 (2048 flop) on each of 1024 SIMDs at 2.4 GHz.  "
-                           "Measured (tools/probe_mfma_f64.hip, probe_clock_ghz): the chip holds ~2.39 GHz, but the "
-                           "instruction issues once per ~105 clk per SIMD back to back, so probe_tflops (~47.5) is "
-                           "the sustained ceiling of the 16x16x4 form; frac_of_probe is against it",
+                           "probe_tflops: back-to-back 16x16x4 MFMAs of tools/probe_mfma_f64.hip (~47.5 at ~2.39 GHz) "
+                           "-- not a ceiling: this Gram kernel issued 57.5 TF/s of MFMA work in r04a (issued_tflops)",
             "frac": round(achieved / F64_MFMA_PEAK_TF, 4),
             "probe_tflops": round(peak.value, 2),
             "frac_of_probe": round(achieved / peak.value, 4),
@@ -845,7 +857,8 @@ def training_leg(dev, mask, args, world, rank):
             "peak_at_probe_clock": round(peak_clk, 2) if peak_clk else None,
             "frac_at_probe_clock": round(achieved / peak_clk, 4) if peak_clk else None,
             "algorithmic_flops": algo,
-            "previous": "r02: k_train_gram (single-buffered LDS, 1 wave per SIMD) 636 ms, 34.3 TF/s",
+            "previous": "r04a: 462.0 ms, 47.5 TF/s (every tile of the batch's padded size issued: 57.5 TF/s); r02: "
+                        "k_train_gram (single-buffered LDS, 1 wave per SIMD) 636 ms, 34.3 TF/s",
         },
     }
 

@@ -53,6 +53,12 @@ struct TrainRegion {
     int pad_;
 };
 
+// block columns of region r holding data: the batch's tiles are sized for its largest
+// naug (npad); a region's blocks at or past ceil(naug / 128) are padding -- zero in S,
+// identity in the regularised G -- so every kernel below skips them (adding exact zeros,
+// or factoring / inverting an identity block, is all they would do: bitwise the same)
+__device__ inline int live_blocks(const TrainRegion *regs, int r) { return (regs[r].naug + kTile - 1) / kTile; }
+
 // tile index -> (bi, bj): lower triangle of the C x C Gram tiles first, then the
 // kStrip x C strip tiles (rows = outputs).
 __device__ inline bool tile_of(int idx, int C, int *bi, int *bj, bool *strip) {
@@ -178,10 +184,17 @@ __global__ __launch_bounds__(256, 2) void k_train_gram2(const double *__restrict
     int bi, bj;
     bool strip;
     if (!tile_of(blockIdx.x, C, &bi, &bj, &strip)) return;
+    const int Cr = (R.naug + kTile - 1) / kTile;
+    if ((strip ? bj : bi) >= Cr) return;  // padding (bi >= bj)
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int wr = w >> 1, wc = w & 1, l16 = lane & 15, kk = lane >> 4;
     const double *Sr = S + R.s_off, *Tr = T + R.t_off;
     const int naug = R.naug;
+    // a wave whose 64 x 64 sub-tile holds no output (rows past naug / nout, columns
+    // past naug, or above the diagonal of a diagonal tile) loads its share of the LDS
+    // stages and skips its MFMAs, leaving the SIMD to the other block's waves
+    const bool wlive = (bi * kTile + wr * 64 < (strip ? nout : naug)) && (bj * kTile + wc * 64 < naug) &&
+                       !(!strip && bi == bj && wr < wc);
     const int lrow = tid & (kTile - 1), lt0 = tid >> 7;
     const int arow = bi * kTile + lrow;
     const int brow = bj * kTile + lrow;
@@ -217,17 +230,19 @@ __global__ __launch_bounds__(256, 2) void k_train_gram2(const double *__restrict
     if (kKC < m) fetch(kKC);
     int cur = 0;
     for (int t0 = 0; t0 < m; t0 += kKC) {
+        if (wlive) {  // wave-uniform
 #pragma unroll
-        for (int s = 0; s < kKC / 4; ++s) {
-            double a[4], b[4];
+            for (int s = 0; s < kKC / 4; ++s) {
+                double a[4], b[4];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) a[i] = sA[cur][4 * s + kk][wr * 64 + i * 16 + l16];
+                for (int i = 0; i < 4; ++i) a[i] = sA[cur][4 * s + kk][wr * 64 + i * 16 + l16];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) b[j] = sB[cur][4 * s + kk][wc * 64 + j * 16 + l16];
+                for (int j = 0; j < 4; ++j) b[j] = sB[cur][4 * s + kk][wc * 64 + j * 16 + l16];
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
+                for (int i = 0; i < 4; ++i)
 #pragma unroll
-                for (int j = 0; j < 4; ++j) acc[i][j] = MFMA64(a[i], b[j], acc[i][j]);
+                    for (int j = 0; j < 4; ++j) acc[i][j] = MFMA64(a[i], b[j], acc[i][j]);
+            }
         }
         if (t0 + kKC < m) {
             store(cur ^ 1);
@@ -236,6 +251,7 @@ __global__ __launch_bounds__(256, 2) void k_train_gram2(const double *__restrict
         __syncthreads();
         cur ^= 1;
     }
+    if (!wlive) return;
     double *Gr = G + (size_t)r * npad * npad;
     double *Br = B + (size_t)r * npad * nout;
 #pragma unroll
@@ -311,10 +327,14 @@ struct TileLoader {
 // po[c * ldo + r].  128 x 128 tiles for the wide trailing update, 64-wide ones for
 // the narrow launches (panel, triangular solves), where one tile's MFMA chain is the
 // launch's latency.
+// lower: the tile is on the diagonal of a symmetric update and only its lower triangle
+// is read later -- the wave above the diagonal (wr < wc) loads its share of the LDS
+// stages and skips its MFMAs and stores
 template <int TR, int TC, bool AT, bool BT>
 __device__ __forceinline__ void gemm_tile(const double *__restrict__ pa, long long lda, int arows,
                                           const double *__restrict__ pb, long long ldb, int brows, double *po,
-                                          long long ldo, double alpha, bool accumulate, int K = kTile) {
+                                          long long ldo, double alpha, bool accumulate, int K = kTile,
+                                          bool lower = false) {
     using LA = TileLoader<TR, AT>;
     using LB = TileLoader<TC, BT>;
     constexpr int NI = TR / 32, NJ = TC / 32;
@@ -351,6 +371,7 @@ __device__ __forceinline__ void gemm_tile(const double *__restrict__ pa, long lo
         for (int q = 0; q < LB::PER; ++q) sB[LB::l(tid, q)][brow] = rb[q];
         __syncthreads();
         if (t0 + kKC < K) fetch(t0 + kKC);
+        if (lower && wr < wc) continue;  // wave-uniform
 #pragma unroll
         for (int s = 0; s < kKC / 4; ++s) {
             double a[NI], b[NJ];
@@ -364,6 +385,7 @@ __device__ __forceinline__ void gemm_tile(const double *__restrict__ pa, long lo
                 for (int j = 0; j < NJ; ++j) acc[i][j] = MFMA64(a[i], b[j], acc[i][j]);
         }
     }
+    if (lower && wr < wc) return;
 #pragma unroll
     for (int i = 0; i < NI; ++i)
 #pragma unroll
@@ -394,10 +416,12 @@ constexpr size_t kDiagLds = (size_t)(kTile * kDiagLd + 2 * kTile) * sizeof(doubl
 // diagonal) to linv for the panel GEMM and the triangular solves.  info: potrf's
 // (first non-positive pivot, 1-based global index).
 __global__ __launch_bounds__(kDiagThreads) void k_chol_diag(double *__restrict__ G, double *__restrict__ linv,
-                                                            int npad, int k, int *__restrict__ info) {
+                                                            int npad, int k, int *__restrict__ info,
+                                                            const TrainRegion *__restrict__ regs) {
     extern __shared__ double S[];  // S[i * kDiagLd + c]
     double *ldg = S + kTile * kDiagLd, *xd = ldg + kTile;
     const int r = blockIdx.x, C = npad / kTile;
+    if (k >= live_blocks(regs, r)) return;  // an identity block: L = L^-1 = I, already in G
     const int tid = threadIdx.x, i = tid & (kTile - 1), h = tid >> 7;
     double *A = G + (size_t)r * npad * npad + (size_t)k * kTile * npad + (size_t)k * kTile;
     for (int c = h; c < kTile; c += kDiagH) S[i * kDiagLd + c] = c <= i ? A[(size_t)c * npad + i] : 0.0;
@@ -457,8 +481,9 @@ __global__ __launch_bounds__(kDiagThreads) void k_chol_diag(double *__restrict__
 // L_ik = A_ik L_kk^-T for the blocks i > k below the diagonal, in place: a block
 // owns 64 rows x all 128 columns (it reads the whole rows it overwrites)
 __global__ __launch_bounds__(256) void k_chol_panel(double *__restrict__ G, const double *__restrict__ linv, int npad,
-                                                    int k) {
+                                                    int k, const TrainRegion *__restrict__ regs) {
     const int r = blockIdx.y, C = npad / kTile, i = k + 1 + (blockIdx.x >> 1), r0 = (blockIdx.x & 1) * 64;
+    if (i >= live_blocks(regs, r)) return;  // A_ik = 0: L_ik = 0
     double *Gr = G + (size_t)r * npad * npad;
     double *A = Gr + (size_t)k * kTile * npad + (size_t)i * kTile + r0;
     const double *Li = linv + ((size_t)r * C + k) * kTile * kTile;
@@ -469,17 +494,18 @@ __global__ __launch_bounds__(256) void k_chol_panel(double *__restrict__ G, cons
 // of block columns jlo <= j < jhi: one GEMM of depth 128 kw per tile (the block
 // columns of L are contiguous in the column-major G).
 __global__ __launch_bounds__(256, 2) void k_chol_update(double *__restrict__ G, int npad, int k0, int kw, int jlo,
-                                                     int jhi) {
+                                                     int jhi, const TrainRegion *__restrict__ regs) {
     const int r = blockIdx.y, C = npad / kTile;
     int idx = blockIdx.x, j = jlo;
     while (j < jhi && idx >= C - j) idx -= C - j++;
     if (j >= jhi) return;
     const int i = j + idx;
+    if (i >= live_blocks(regs, r)) return;  // L_ik = 0 for the padding rows (i >= j > k)
     double *Gr = G + (size_t)r * npad * npad;
     const double *Lik = Gr + (size_t)k0 * kTile * npad + (size_t)i * kTile;
     const double *Ljk = Gr + (size_t)k0 * kTile * npad + (size_t)j * kTile;
     double *Aij = Gr + (size_t)j * kTile * npad + (size_t)i * kTile;
-    gemm_tile<128, 128, false, false>(Lik, npad, kTile, Ljk, npad, kTile, Aij, npad, -1.0, true, kw * kTile);
+    gemm_tile<128, 128, false, false>(Lik, npad, kTile, Ljk, npad, kTile, Aij, npad, -1.0, true, kw * kTile, i == j);
 }
 
 static int update_tiles(int C, int jlo, int jhi) {
@@ -564,8 +590,9 @@ __device__ __forceinline__ void gemm_rhs(const double *__restrict__ pa, long lon
 //   forward  (upper = 0): B_k = L_kk^-1 B_k        backward (upper = 1): B_k = L_kk^-T B_k
 template <bool upper>  // one gemm_rhs instance per kernel: its LDS stages are static
 __global__ __launch_bounds__(256, 2) void k_solve_diag(const double *__restrict__ linv, double *__restrict__ B, int npad,
-                                                    int nout, int k) {
+                                                    int nout, int k, const TrainRegion *__restrict__ regs) {
     const int r = blockIdx.y, C = npad / kTile;
+    if (k >= live_blocks(regs, r)) return;  // B_k = 0 (padding rows), L_kk = I
     const double *Li = linv + ((size_t)r * C + k) * kTile * kTile;
     double *Bk = B + (size_t)r * npad * nout + (size_t)k * kTile;
     gemm_rhs<upper>(Li, kTile, Bk, npad, nout, Bk, npad, 1.0, false);
@@ -576,8 +603,12 @@ __global__ __launch_bounds__(256, 2) void k_solve_diag(const double *__restrict_
 //   forward:  B_i -= sum_k L_ik Y_k        backward: B_i -= sum_k L_ki^T X_k
 template <bool upper>
 __global__ __launch_bounds__(256, 2) void k_solve_update(const double *__restrict__ G, double *__restrict__ B, int npad,
-                                                      int nout, int k0, int kw, int ilo) {
+                                                      int nout, int k0, int kw, int ilo,
+                                                      const TrainRegion *__restrict__ regs) {
     const int r = blockIdx.y, i = ilo + (int)blockIdx.x;
+    const int Cr = live_blocks(regs, r);
+    // padding block rows stay 0; backward, solved rows k0.. past the data are 0
+    if (i >= Cr || (upper && k0 >= Cr)) return;
     const double *Gr = G + (size_t)r * npad * npad;
     double *Br = B + (size_t)r * npad * nout;
     if constexpr (upper)  // A(rr, l) = L(k0 kTile + l, i kTile + rr): the transposed blocks (k, i)
@@ -731,16 +762,16 @@ extern "C" int sml_train_solve(sml_train *t, int ncs, double beta_res, double be
         for (int k = p0; k < p1; ++k) {
             if (k > p0)
                 hipLaunchKernelGGL(k_chol_update, dim3(C - k, nl), dim3(256), 0, st, t->d_G, npad, p0, k - p0, k,
-                                   k + 1);
+                                   k + 1, t->d_regs);
             hipLaunchKernelGGL(k_chol_diag, dim3(nl), dim3(kDiagThreads), kDiagLds, st, t->d_G, t->d_linv, npad, k,
-                               t->d_info);
+                               t->d_info, t->d_regs);
             if (k < C - 1)
                 hipLaunchKernelGGL(k_chol_panel, dim3(2 * (C - 1 - k), nl), dim3(256), 0, st, t->d_G, t->d_linv,
-                                   npad, k);
+                                   npad, k, t->d_regs);
         }
         if (p1 < C)
             hipLaunchKernelGGL(k_chol_update, dim3(update_tiles(C, p1, C), nl), dim3(256), 0, st, t->d_G, npad, p0,
-                               p1 - p0, p1, C);
+                               p1 - p0, p1, C, t->d_regs);
     }
     // potrs, blocked by panels of P block rows: inside a panel, right-looking (block
     // row k's diagonal inverse, then its update of the panel's remaining rows at
@@ -750,26 +781,28 @@ extern "C" int sml_train_solve(sml_train *t, int ncs, double beta_res, double be
     for (int p0 = 0; p0 < C; p0 += P) {  // L Y = B
         const int p1 = std::min(C, p0 + P);
         for (int k = p0; k < p1; ++k) {
-            hipLaunchKernelGGL(k_solve_diag<false>, dim3(1, nl), dim3(256), 0, st, t->d_linv, t->d_B, npad, nout, k);
+            hipLaunchKernelGGL(k_solve_diag<false>, dim3(1, nl), dim3(256), 0, st, t->d_linv, t->d_B, npad, nout, k,
+                               t->d_regs);
             if (k + 1 < p1)
                 hipLaunchKernelGGL(k_solve_update<false>, dim3(p1 - 1 - k, nl), dim3(256), 0, st, t->d_G, t->d_B,
-                                   npad, nout, k, 1, k + 1);
+                                   npad, nout, k, 1, k + 1, t->d_regs);
         }
         if (p1 < C)
             hipLaunchKernelGGL(k_solve_update<false>, dim3(C - p1, nl), dim3(256), 0, st, t->d_G, t->d_B, npad, nout,
-                               p0, p1 - p0, p1);
+                               p0, p1 - p0, p1, t->d_regs);
     }
     for (int p1 = C; p1 > 0; p1 -= P) {  // L^T X = Y, panels from the bottom
         const int p0 = std::max(0, p1 - P);
         for (int k = p1 - 1; k >= p0; --k) {
-            hipLaunchKernelGGL(k_solve_diag<true>, dim3(1, nl), dim3(256), 0, st, t->d_linv, t->d_B, npad, nout, k);
+            hipLaunchKernelGGL(k_solve_diag<true>, dim3(1, nl), dim3(256), 0, st, t->d_linv, t->d_B, npad, nout, k,
+                               t->d_regs);
             if (k > p0)
                 hipLaunchKernelGGL(k_solve_update<true>, dim3(k - p0, nl), dim3(256), 0, st, t->d_G, t->d_B, npad,
-                                   nout, k, 1, p0);
+                                   nout, k, 1, p0, t->d_regs);
         }
         if (p0 > 0)
             hipLaunchKernelGGL(k_solve_update<true>, dim3(p0, nl), dim3(256), 0, st, t->d_G, t->d_B, npad, nout, p0,
-                               p1 - p0, 0);
+                               p1 - p0, 0, t->d_regs);
     }
     SML_HIP(hipGetLastError());
     hipLaunchKernelGGL(k_train_wout, dim3((t->npad + 255) / 256, t->nlocal), dim3(256), 0, st, t->d_B, t->d_regs,
