@@ -138,8 +138,9 @@ struct sml_dynamics {
     bool split_grid = false;
     bool nograph = false;  // SML_DYN_NOGRAPH=1: the window's launches issued directly, not replayed
     // the fused step's hand-offs (vfm, varm, the m-major state) stored write-through
-    // (store2; SML_DYN_WT=1)
-    bool wt = false;
+    // (store2): SML_DYN_WT=1 both step kernels, 2 the row kernel's (vfm) only, 3 the
+    // per-m kernel's (varm, state) only
+    int wt = 0;
     // mod_lflags lradsw (module default .true.) and stloop's istep (at_gcm.f90:81)
     bool lradsw = true;
     int istep = 1;
@@ -2156,7 +2157,7 @@ extern "C" int sml_dyn_create(double radius, sml_dynamics **out) {
     if (const char *e = std::getenv("SML_DYN_FUSED")) d->fused = *e && *e != '0';
     if (const char *e = std::getenv("SML_DYN_SPLIT_GRID")) d->split_grid = *e && *e != '0';
     if (const char *e = std::getenv("SML_DYN_NOGRAPH")) d->nograph = *e && *e != '0';
-    if (const char *e = std::getenv("SML_DYN_WT")) d->wt = *e && *e != '0';
+    if (const char *e = std::getenv("SML_DYN_WT")) d->wt = std::max(0, std::min(3, std::atoi(e)));
     if (const char *e = std::getenv("SML_CHK_FLAG")) d->chk_flag = *e != '0';
     if (const char *e = std::getenv("SML_DYN_STAMPS"))
         if (*e && *e != '0' && (rc = dalloc(reinterpret_cast<double **>(&d->d_dbg), kStampKernels * kStampBlocks * kStamps))) {
@@ -2366,8 +2367,9 @@ int launch_step_fused(sml_dynamics *d, int j1, int j2, double dt, double alph, d
             hipLaunchKernelGGL(k_st_specx, dim3(kIL), dim3(kSpecxThreads), 0, st, d->d_gfwd, d->d_phys, d->d_vfm,
                                sd.wa, sd.cosgr, d->d_dbg);
         } else {
-            hipLaunchKernelGGL(d->wt ? k_st_gridspec<true> : k_st_gridspec<false>, dim3(kIL), dim3(kGsThreads), 0, st, d->d_varm, d->d_vfm, sd.wa, sd.cosgr,
-                               T, d->d_pbc, d->d_rad, d->d_ptab, lradsw ? 1 : 0, d->wt ? 1 : 0, d->d_dbg);
+            const bool wrow = d->wt == 1 || d->wt == 2;
+            hipLaunchKernelGGL(wrow ? k_st_gridspec<true> : k_st_gridspec<false>, dim3(kIL), dim3(kGsThreads), 0, st, d->d_varm, d->d_vfm, sd.wa, sd.cosgr,
+                               T, d->d_pbc, d->d_rad, d->d_ptab, lradsw ? 1 : 0, wrow ? 1 : 0, d->d_dbg);
         }
         SML_HIP(hipGetLastError());
     } else {
@@ -2378,11 +2380,12 @@ int launch_step_fused(sml_dynamics *d, int j1, int j2, double dt, double alph, d
     const int j4 = (alph == 0.0) ? j2 : 1;
     const int cur = d->sm_cur;
     if (next_j2 > 0) d->sm_cur = 1 - cur;  // the next step reads what this one writes
-    hipLaunchKernelGGL(d->wt ? k_st_spec<true> : k_st_spec<false>, dim3(kSpecStride * kSpecSplit), dim3(kSpecBlk), 0, st, d->d_vfm, d->d_pfl, sd.wt,
+    const bool wspec = d->wt == 1 || d->wt == 3;
+    hipLaunchKernelGGL(wspec ? k_st_spec<true> : k_st_spec<false>, dim3(kSpecStride * kSpecSplit), dim3(kSpecBlk), 0, st, d->d_vfm, d->d_pfl, sd.wt,
                        sm_buf(d, cur), sm_buf(d, 1 - cur), d->d_tend,
                        d->d_phi, d->d_phis, d->d_tcorh, d->d_qcorh, T, j1, j4, dt, alph, rob, wil, sd.pinv, d->d_varm,
                        next_j2, n1, nin, d->d_tabm + (size_t)(d->d_tab - d->d_tabs) * kMX * kTabMDoubles, d->d_state,
-                       next_j2 > 0 ? nullptr : d->io_exit, d->wt ? 1 : 0, d->d_dbg);
+                       next_j2 > 0 ? nullptr : d->io_exit, wspec ? 1 : 0, d->d_dbg);
     SML_HIP(hipGetLastError());
     return SML_OK;
 }
