@@ -220,9 +220,6 @@ struct RowRegs {
 
 // A and W_in are streamed once per step: non-temporal loads (SML_UPD_NT), like the
 // readout's W_out, so they do not evict the data of the SPEEDY window running beside
-typedef uint32_t nt_u4 __attribute__((ext_vector_type(4)));
-typedef float nt_f4 __attribute__((ext_vector_type(4)));
-typedef double nt_d2 __attribute__((ext_vector_type(2)));
 template <typename T>
 __device__ inline T stream_load(const T *p) {
 #if SML_UPD_NT
