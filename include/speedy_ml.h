@@ -396,6 +396,36 @@ int sml_dyn_set_physics(sml_dynamics *d, const double *bc);
 int sml_dyn_set_hybrid_sst(sml_dynamics *d, const double *d_sst_grid, double sst_bias, void *stream);
 /* sea-ice fraction / temperature sice_am, tice_am (host [ngp]; NULL = no ice) */
 int sml_dyn_set_sea_ice(sml_dynamics *d, const double *sice, const double *tice);
+int sml_dyn_get_sea_ice(sml_dynamics *d, double *sice, double *tice);
+/* host copies of the boundary fields [15][ngp] (sml_dyn_set_physics order) and of the
+ * forcing phis / tcorh / qcorh (any may be NULL) as the next window reads them */
+int sml_dyn_get_physics(sml_dynamics *d, double *bc);
+int sml_dyn_get_forcing(sml_dynamics *d, double *phis, double *tcorh, double *qcorh);
+/* ---- the window's date-driven forcing.  run_model passes each window its calendar
+ * date (src/mpires.f90:1545, :1595-1598) and agcm_init rebuilds the forcing before
+ * stepone (src/ini_agcm_init.f90:57-89): newdate(0) (src/mod_date.f90:17-79),
+ * ini_coupler(2) (src/cpl_main_interface.f90:1-25, cpl_land.f90:1-95, cpl_sea.f90:
+ * 1-200 with icland 1, icsea 0, icice 1, isstan 0), ini_sea's hybrid SST, fordate(0)
+ * (src/ini_fordate.f90:1-115); agcm_1day's fordate(1) (src/at_gcm.f90:84) repeats it
+ * with the same inputs.
+ * surface: host [3][ngp] = fmask_l (mod_cli_land), fmask_s (mod_cli_sea), alb0
+ * (mod_surfcon) as inbcon leaves them (src/ini_inbcon.f90:38-70, 140-156). */
+int sml_dyn_set_surface(sml_dynamics *d, const double *surface);
+/* monthly climatologies, host [5][12][ngp] = stl12, snowd12, soilw12 (mod_cli_land),
+ * sst12, sice12 (mod_cli_sea), January first (src/ini_inbcon.f90:71-230).  NULL: the
+ * coupler's fields stay as sml_dyn_set_physics / sml_dyn_set_sea_ice set them. */
+int sml_dyn_set_climatology(sml_dynamics *d, const double *clim);
+/* the forcing of a window at (iyear, imonth, iday), on `stream` before the window:
+ * with a climatology the coupler at that date (stl_am, soilw_am, snow depth, sst_am,
+ * sice_am, tice_am), the hybrid SST if set (sml_dyn_set_hybrid_sst), then fordate:
+ * sol_oz(tyear), snowc / alb_l / alb_s / albsfc, tcorh = spec(gamlat phis0), qcorh =
+ * spec(refrh1 (qref - qsfc)) from the current stl_am / sst_am.  Skipped when neither
+ * the date nor any input (the setters above, set_physics / set_sea_ice / set_forcing /
+ * set_hybrid_sst) changed since the last call; _ex with force != 0 recomputes. */
+int sml_dyn_fordate(sml_dynamics *d, int iyear, int imonth, int iday, void *stream);
+int sml_dyn_fordate_ex(sml_dynamics *d, int iyear, int imonth, int iday, int force, void *stream);
+/* fordate recomputations issued so far (skipped calls not counted) */
+int sml_dyn_fordate_count(const sml_dynamics *d, int *count);
 /* stloop's clock (dyn_stloop.f90:37-56): istep and mod_lflags' lradsw.  sml_dyn_step
  * uses lradsw as it stands; sml_dyn_leapfrog sets lradsw = (mod(istep, 3) == 1)
  * before each step and advances istep, as stloop does.  Initial: istep 1, lradsw 1. */
@@ -513,6 +543,15 @@ int sml_hybrid_destroy(sml_hybrid *h);
 int sml_hybrid_set_buffers(sml_hybrid *h, double *d_feedback, double *d_local_model, double *d_outvec,
                            double *d_grid4d, double *d_grid2d, double *d_precip, double *d_fc4d, double *d_fc2d,
                            const double *d_tisr);
+/* the loop's calendar (get_current_time_delta_hour as run_model and get_tisr_by_date
+ * call it, src/mpires.f90:1545, :1661): startyear, hours_base = traininglength +
+ * prediction marker + synclength, step_hours = timestep.  Turns on the window's
+ * date-driven forcing: advance t (1-based) runs sml_dyn_fordate at the date of hour
+ * hours_base + t step_hours before its window (needs sml_dyn_set_surface).  Shares its
+ * fields and February latch with sml_hybrid_set_tisr_table; resets the step count. */
+int sml_hybrid_set_calendar(sml_hybrid *h, int startyear, int64_t hours_base, int step_hours);
+/* date[4] = year, month, day, hour of the next advance's window */
+int sml_hybrid_window_date(sml_hybrid *h, int *date);
 /* fixed tisr inputs of the next steps ([nlocal][16] standardized) */
 int sml_hybrid_set_tisr(sml_hybrid *h, const double *d_tisr);
 /* get_tisr_by_date (src/mpires.f90:1644-1676): hourly global tisr fields

@@ -87,6 +87,11 @@ def _declare(L):
     L.orc_phypar_grid.argtypes = [vp] * 11 + [i, vp]
     L.orc_phys_inputs.argtypes = [vp] * 12
     L.orc_train_solve.argtypes = [i, i, i, d, d, i, d, vp, vp, vp]
+    L.orc_newdate.argtypes = [i, i, vp, vp]
+    L.orc_forint.argtypes = [i, d, vp, vp]
+    L.orc_forin5.argtypes = [i, d, vp, vp]
+    L.orc_coupler.argtypes = [i, i] + [vp] * 7
+    L.orc_fordate.argtypes = [d] + [vp] * 15
 
 
 def spectral_init(radius: float = EARTH_RADIUS) -> None:
@@ -592,6 +597,110 @@ def phypar_grid(ug1, vg1, tg1, qg1, phig1, pslg1, bc, state, lradsw):
     lib().orc_phypar_grid(*[_p(x) for x in ins], _p(bcs), _p(state["tau2"]), _p(state["stratc"]),
                           _p(state["tt_rsw"]), _p(state["ssrd"]), int(bool(lradsw)), _p(tend))
     return tend
+
+
+# ---------------------------------------------------------------- per-window forcing
+CLIMATOLOGY = ("stl12", "snowd12", "soilw12", "sst12", "sice12")
+
+
+def _leap(y):
+    return (y % 4 == 0 and y % 100 != 0) or y % 400 == 0
+
+
+def calendar_delta_hour(startyear, hours, state):
+    """get_current_time_delta_hour (mod_calendar.f90:24-92), statement by statement:
+    (year, month, day, hour) after `hours` from startyear; state["ncal"] is the
+    routine's SAVEd month table (February set to 29 once a leap year is met)."""
+    years = hours // 8760
+    year = years + startyear
+    leap_days = sum(1 for i in range(years) if _leap(startyear + i))
+    ncal = state.setdefault("ncal", [31, 28, 31, 30, 31, 30, 31, 31, 30, 31, 30, 31])
+    if _leap(year):
+        ncal[1] = 29
+    c = (hours % 8760) // 24 - leap_days
+    month = 1
+    while c > 0:
+        c -= ncal[month - 1]
+        month += 1
+    month -= 1
+    if month <= 0:
+        month = 12
+        year -= 1
+    return year, month, ncal[month - 1] + c, hours % 24
+
+
+def newdate(imonth, iday):
+    """newdate(0), iseasc = 1 (mod_date.f90:17-79): (tmonth, tyear)."""
+    tm, ty = np.zeros(1), np.zeros(1)
+    lib().orc_newdate(int(imonth), int(iday), _p(tm), _p(ty))
+    return float(tm[0]), float(ty[0])
+
+
+def forint(imon, fmon, for12):
+    out = np.zeros(NGP)
+    lib().orc_forint(int(imon), float(fmon), _p(np.ascontiguousarray(for12, dtype=np.float64)), _p(out))
+    return out
+
+
+def forin5(imon, fmon, for12):
+    out = np.zeros(NGP)
+    lib().orc_forin5(int(imon), float(fmon), _p(np.ascontiguousarray(for12, dtype=np.float64)), _p(out))
+    return out
+
+
+def coupler(imonth, iday, clim):
+    """ini_coupler(2) at the date (cpl_land.f90, cpl_sea.f90; icland 1, icsea 0,
+    icice 1): dict stl_am, snowd_am, soilw_am, sst_am (ice-blended), sice_am, tice_am.
+    clim: dict of CLIMATOLOGY (12, ngp) arrays."""
+    c = np.ascontiguousarray(np.stack([np.asarray(clim[k], dtype=np.float64).reshape(12, NGP)
+                                       for k in CLIMATOLOGY]))
+    names = ("stl_am", "snowd_am", "soilw_am", "sst_am", "sice_am", "tice_am")
+    out = {k: np.zeros(NGP) for k in names}
+    lib().orc_coupler(int(imonth), int(iday), _p(c), *[_p(out[k]) for k in names])
+    return out
+
+
+def fordate(tyear, surf, phis0, stl_am, sst_am, sice_am, snowd_am=None, snowc=None):
+    """fordate(0) (ini_fordate.f90:1-115): dict snowc, alb_l, alb_s, albsfc, fsol,
+    ozone, ozupp, zenit, stratz (ngp,) and tcorh, qcorh complex (nx, mx).
+    surf: dict fmask_l, fmask_s, alb0.  Without snowd_am, snowc is the input."""
+    phys_init()
+    f = lambda a: np.ascontiguousarray(np.asarray(a, dtype=np.float64).ravel())  # noqa: E731
+    sc = f(snowc) if snowd_am is None else np.zeros(NGP)
+    out = {k: np.zeros(NGP) for k in ("alb_l", "alb_s", "albsfc")}
+    sol = np.zeros((5, NGP))
+    tq = [np.zeros((NX, MX), np.complex128) for _ in range(2)]
+    ins = [f(surf["fmask_l"]), f(surf["fmask_s"]), f(surf["alb0"]), f(phis0), f(stl_am), f(sst_am)]
+    sn = None if snowd_am is None else f(snowd_am)
+    lib().orc_fordate(float(tyear), *[_p(x) for x in ins], None if sn is None else _p(sn), _p(f(sice_am)), _p(sc),
+                      _p(out["alb_l"]), _p(out["alb_s"]), _p(out["albsfc"]), _p(sol), _p(tq[0]), _p(tq[1]))
+    out["snowc"] = sc
+    out.update(zip(("fsol", "ozone", "ozupp", "zenit", "stratz"), sol))
+    out["tcorh"], out["qcorh"] = tq
+    return out
+
+
+def window_forcing(imonth, iday, surf, bc, clim=None, sice=None, tice=None, sst_hybrid=None, bias=0.0):
+    """The whole per-window forcing as sml_dyn_fordate applies it: the coupler at the
+    date (clim) or bc's coupler fields, ini_sea's hybrid SST, fordate.  Returns
+    (bc', tcorh, qcorh, sice, tice) with bc' the boundary fields of the window."""
+    b = {k: np.array(v, dtype=np.float64, copy=True).ravel() for k, v in bc.items()}
+    snowd = None
+    if clim is not None:
+        c = coupler(imonth, iday, clim)
+        b["stl_am"], b["soilw_am"], snowd = c["stl_am"], c["soilw_am"], c["snowd_am"]
+        sst_cpl, sice, tice = c["sst_am"], c["sice_am"], c["tice_am"]
+    else:  # bc's sst_am is the coupler's (sml_dyn_set_physics)
+        sst_cpl = b["sst_am"]
+        sice = np.zeros(NGP) if sice is None else np.asarray(sice, dtype=np.float64).ravel()
+        tice = np.zeros(NGP) if tice is None else np.asarray(tice, dtype=np.float64).ravel()
+    b["sst_am"] = sst_cpl if sst_hybrid is None else hybrid_sst_am(sst_cpl, sst_hybrid, sice, tice, bias)
+    _, tyear = newdate(imonth, iday)
+    fd = fordate(tyear, surf, b["phis0"], b["stl_am"], b["sst_am"], sice, snowd_am=snowd,
+                 snowc=None if snowd is not None else b["snowc"])
+    for k in ("snowc", "alb_l", "alb_s", "albsfc", "fsol", "ozone", "ozupp", "zenit", "stratz"):
+        b[k] = fd[k]
+    return b, fd["tcorh"], fd["qcorh"], sice, tice
 
 
 # ---------------------------------------------------------------- reference (pinning only)

@@ -672,3 +672,135 @@ void orc_phypar_grid(const double *ug1, const double *vg1, const double *tg1, co
     orc_phys_state st = {tau2, stratc, tt_rsw, ssrd};
     for (int j = 0; j < NGP; ++j) orc_phys_column(j, ug1, vg1, tg1, qg1, phig1, pslg1, &bc, &st, lradsw, tend);
 }
+
+/* ------------------------------------------------------------ per-window forcing
+ * What agcm_init rebuilds before every window from run_model's date
+ * (ini_agcm_init.f90:57-89; run_model passes the calendar date, mpires.f90:1545,
+ * 1595-1598), with the coupler flags of mod_cpl_flags.f90 (icland 1, icsea 0,
+ * icice 1, isstan 0) at jday 0.  Pinned by tests/golden/fordate_ref.npz
+ * (tests/golden/make_fordate_golden.py: newdate, forin5, forint, ini_land and fordate
+ * of the reference compiled as-is).  atm2sea / sea2atm live in cpl_sea.f90, which
+ * also holds ini_sea's `use mpires` and does not build here: their sea-ice adjustment
+ * (cpl_sea.f90:96-117, 190-197) is restated below, parity unpinned for those lines. */
+
+/* newdate(0) with iseasc = 1 (mod_date.f90:17-79): tmonth, tyear of (imonth, iday) */
+void orc_newdate(int imonth, int iday, double *tmonth, double *tyear)
+{
+    static const int ncal365[12] = {31, 28, 31, 30, 31, 30, 31, 31, 30, 31, 30, 31};
+    int before = 0;
+    for (int m = 1; m < imonth; ++m) before += ncal365[m - 1];
+    *tmonth = (iday - 0.5) / (double)ncal365[imonth - 1];
+    *tyear = (before + iday - 0.5) / (double)365;
+}
+
+/* forint (cpl_bcinterp.f90:1-23): for12 [12][NGP] (month 1 first) */
+void orc_forint(int imon, double fmon, const double *for12, double *for1)
+{
+    int imon2;
+    double wmon;
+    if (fmon <= 0.5) {
+        imon2 = imon - 1;
+        if (imon == 1) imon2 = 12;
+        wmon = 0.5 - fmon;
+    } else {
+        imon2 = imon + 1;
+        if (imon == 12) imon2 = 1;
+        wmon = fmon - 0.5;
+    }
+    const double *a = for12 + (size_t)(imon - 1) * NGP, *b = for12 + (size_t)(imon2 - 1) * NGP;
+    for (int j = 0; j < NGP; ++j) for1[j] = a[j] + wmon * (b[j] - a[j]);
+}
+
+/* forin5 (cpl_bcinterp.f90:25-56): non-linear, mean-conserving */
+void orc_forin5(int imon, double fmon, const double *for12, double *for1)
+{
+    int im2 = imon - 2, im1 = imon - 1, ip1 = imon + 1, ip2 = imon + 2;
+    if (im2 < 1) im2 = im2 + 12;
+    if (im1 < 1) im1 = im1 + 12;
+    if (ip1 > 12) ip1 = ip1 - 12;
+    if (ip2 > 12) ip2 = ip2 - 12;
+    double c0 = 1. / 12., t0 = c0 * fmon, t1 = c0 * (1. - fmon), t2 = 0.25 * fmon * (1 - fmon);
+    double wm2 = -t1 + t2, wm1 = -c0 + 8 * t1 - 6 * t2, w0 = 7 * c0 + 10 * t2, wp1 = -c0 + 8 * t0 - 6 * t2,
+           wp2 = -t0 + t2;
+    const double *f[5];
+    const int mm[5] = {im2, im1, imon, ip1, ip2};
+    for (int k = 0; k < 5; ++k) f[k] = for12 + (size_t)(mm[k] - 1) * NGP;
+    for (int j = 0; j < NGP; ++j)
+        for1[j] = wm2 * f[0][j] + wm1 * f[1][j] + w0 * f[2][j] + wp1 * f[3][j] + wp2 * f[4][j];
+}
+
+/* ini_coupler(2) at (imonth, iday): clim [5][12][NGP] = stl12, snowd12, soilw12, sst12,
+ * sice12.  Land: atm2land(0), stl_lm = stlcl_ob, land2atm(0) (cpl_land.f90:1-95).
+ * Sea: atm2sea(0) with the adjustment over sea ice, ini_sea's start from the
+ * climatology, sea2atm(0) (cpl_sea.f90:1-37, 50-117, 138-199): sst_am ice-blended. */
+void orc_coupler(int imonth, int iday, const double *clim, double *stl_am, double *snowd_am, double *soilw_am,
+                 double *sst_am, double *sice_am, double *tice_am)
+{
+    double tmonth, tyear;
+    orc_newdate(imonth, iday, &tmonth, &tyear);
+    const size_t F = (size_t)12 * NGP;
+    orc_forin5(imonth, tmonth, clim, stl_am);
+    orc_forint(imonth, tmonth, clim + F, snowd_am);
+    orc_forint(imonth, tmonth, clim + 2 * F, soilw_am);
+    double *sstcl = malloc(NGP * sizeof(double)), *sicecl = malloc(NGP * sizeof(double));
+    orc_forin5(imonth, tmonth, clim + 3 * F, sstcl);
+    orc_forint(imonth, tmonth, clim + 4 * F, sicecl);
+    const double sstfr = 273.2 - 1.8;
+    for (int j = 0; j < NGP; ++j) {
+        double ticecl;
+        if (sstcl[j] > sstfr) {
+            sicecl[j] = fmin(0.5, sicecl[j]);
+            ticecl = sstfr;
+            if (sicecl[j] > 0.) sstcl[j] = sstfr + (sstcl[j] - sstfr) / (1. - sicecl[j]);
+        } else {
+            sicecl[j] = fmax(0.5, sicecl[j]);
+            ticecl = sstfr + (sstcl[j] - sstfr) / sicecl[j];
+            sstcl[j] = sstfr;
+        }
+        /* sst_om = sstcl_ob, tice_om = ticecl_ob, sice_om = sicecl_ob (ini_sea);
+         * sea2atm(0): sst_am = sstcl_ob + 0, sice_am = sice_om, tice_am = tice_om */
+        double s = sstcl[j] + 0.0;
+        sice_am[j] = sicecl[j];
+        tice_am[j] = ticecl;
+        sst_am[j] = s + sicecl[j] * (ticecl - s);
+    }
+    free(sstcl);
+    free(sicecl);
+}
+
+void orc_spec(const double *vorg, double *vorm);
+
+/* fordate(0) (ini_fordate.f90:1-115; lco2 .false.): sol_oz(tyear) into sol5
+ * [5][NGP]; the surface albedo; tcorh, qcorh (spectral (mx2, nx)).  snowd_am NULL:
+ * snowc is an input (the coupler's snow cover as the host gave it). */
+void orc_fordate(double tyear, const double *fmask_l, const double *fmask_s, const double *alb0,
+                 const double *phis0, const double *stl_am, const double *sst_am, const double *snowd_am,
+                 const double *sice_am, double *snowc, double *alb_l, double *alb_s, double *albsfc, double *sol5,
+                 double *tcorh, double *qcorh)
+{
+    orc_sol_oz(tyear, sol5, sol5 + NGP, sol5 + 2 * NGP, sol5 + 3 * NGP, sol5 + 4 * NGP);
+    const double albsn = 0.60, albsea = 0.07, albice = 0.60, sd2sc = 60.0;
+    for (int j = 0; j < NGP; ++j) {
+        if (snowd_am) snowc[j] = fmin(1., snowd_am[j] / sd2sc);
+        alb_l[j] = alb0[j] + snowc[j] * (albsn - alb0[j]);
+        alb_s[j] = albsea + sice_am[j] * (albice - albsea);
+        albsfc[j] = alb_s[j] + fmask_l[j] * (alb_l[j] - alb_s[j]);
+    }
+    /* setgam: gamlat(j) = gamma / (1000 g) on every latitude (mod_dyncon0 gamma = 6) */
+    const double gamlat = 6.0 / (1000. * gg), refrh1 = 0.7;
+    double *corh = malloc(NGP * sizeof(double)), *corq = malloc(NGP * sizeof(double));
+    for (int j = 0; j < NGP; ++j) corh[j] = gamlat * phis0[j];
+    orc_spec(corh, tcorh);
+    const double pexp = 1. / (rd * gamlat);
+    for (int j = 0; j < NGP; ++j) {
+        double tsfc = fmask_l[j] * stl_am[j] + fmask_s[j] * sst_am[j];
+        double tref = tsfc + corh[j];
+        double psfc = pow(tsfc / tref, pexp);
+        double qref = qsat_of(tref, 1.0, 1.0); /* shtorh(0, .., tref, psfc_dummy = 1, -1.) */
+        double qsfc = qsat_of(tsfc, psfc, 1.0); /* shtorh(0, .., tsfc, psfc, 1.) */
+        corq[j] = refrh1 * (qref - qsfc);
+    }
+    orc_spec(corq, qcorh);
+    free(corh);
+    free(corq);
+}

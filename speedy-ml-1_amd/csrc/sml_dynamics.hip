@@ -131,6 +131,17 @@ struct sml_dynamics {
     double *d_sst_cpl = nullptr, *d_sice = nullptr, *d_tice = nullptr;
     const double *hyb_sst = nullptr;
     double hyb_bias = 0.0;
+    // agcm_init's per-window forcing (sml_dyn_fordate): inbcon's surface fields
+    // [3][ngp] = fmask_l, fmask_s, alb0; the coupler's monthly climatologies
+    // [5][12][ngp] = stl12, snowd12, soilw12, sst12, sice12 (optional); the two grid
+    // fields of tcorh / qcorh and their Fourier coefficients
+    double *d_surf = nullptr, *d_clim = nullptr, *d_ford = nullptr;
+    bool surf_on = false, clim_on = false;
+    // fordate's inputs change with the date or a setter: the generation of the
+    // setters' inputs and the date of the last fordate (recomputed only on a change)
+    long long ford_gen = 1, ford_done = 0;
+    int ford_date[2] = {0, 0};
+    int ford_count = 0;  // fordate recomputations issued (sml_dyn_fordate_count)
     // step kernels: the fused form (default: 2-3 launches per chained step) or the
     // 8/9-launch form (SML_DYN_FUSED=0 at creation; same results bit for bit)
     bool fused = true;
@@ -2115,9 +2126,10 @@ int dalloc(T **p, size_t count) {
 // ------------------------------------------------------------------ API
 extern "C" int sml_dyn_destroy(sml_dynamics *d) {
     if (!d) return SML_OK;
-    void *ptrs[] = {d->d_tabs, d->d_tabm, d->d_state, d->d_phis, d->d_tcorh, d->d_qcorh, d->d_phi, d->d_specin,
+    void *ptrs[] = {d->d_tabs, d->d_tabm, d->d_state, d->d_phis, d->d_tcorh, d->d_phi, d->d_specin,
                     d->d_varm, d->d_grid, d->d_gfwd, d->d_sfwd, d->d_tend, d->d_phys, d->d_minmax, d->d_io, d->d_vfm, d->d_pfl, d->d_sm, d->d_dbg,
-                    d->d_ptab, d->d_pbc, d->d_rad, d->d_pio, d->d_sst_cpl, d->d_sice, d->d_tice};
+                    d->d_ptab, d->d_pbc, d->d_rad, d->d_pio, d->d_sst_cpl, d->d_sice, d->d_tice, d->d_surf,
+                    d->d_clim, d->d_ford};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     for (auto &r : d->replay)
@@ -2165,7 +2177,7 @@ extern "C" int sml_dyn_create(double radius, sml_dynamics **out) {
             return rc;
         }
     if ((rc = dalloc(&d->d_tabs, 4)) || (rc = dalloc(&d->d_tabm, (size_t)4 * kMX * kTabMDoubles + kTabMPad)) || (rc = dalloc(&d->d_state, kStateSize)) || (rc = dalloc(&d->d_phis, kSF)) ||
-        (rc = dalloc(&d->d_tcorh, kSF)) || (rc = dalloc(&d->d_qcorh, kSF)) || (rc = dalloc(&d->d_phi, kKX * kSF)) ||
+        (rc = dalloc(&d->d_tcorh, 2 * kSF)) || (rc = dalloc(&d->d_phi, kKX * kSF)) ||
         (rc = dalloc(&d->d_specin, (size_t)kNInvMax * kSF)) ||
         (rc = dalloc(&d->d_varm, (size_t)(kNInvMax > kNFwd ? kNInvMax : kNFwd) * kVF)) ||
         (rc = dalloc(&d->d_grid, (size_t)kNInvMax * kGF)) || (rc = dalloc(&d->d_gfwd, (size_t)kNFwd * kGF)) ||
@@ -2178,10 +2190,12 @@ extern "C" int sml_dyn_create(double radius, sml_dynamics **out) {
         (rc = dalloc(&d->d_chk, (size_t)kNIo * (kSF + kVF + kGF))) ||
         (rc = dalloc(&d->d_pbc, (size_t)kNBc * kNGP)) || (rc = dalloc(&d->d_rad, kRadSize)) ||
         (rc = dalloc(&d->d_pio, (size_t)(5 * kKX + 1 + 4 * kKX) * kNGP)) || (rc = dalloc(&d->d_sst_cpl, kNGP)) ||
-        (rc = dalloc(&d->d_sice, kNGP)) || (rc = dalloc(&d->d_tice, kNGP))) {
+        (rc = dalloc(&d->d_sice, kNGP)) || (rc = dalloc(&d->d_tice, kNGP)) ||
+        (rc = dalloc(&d->d_surf, (size_t)3 * kNGP)) || (rc = dalloc(&d->d_ford, (size_t)2 * (kGF + kVF)))) {
         sml_dyn_destroy(d);
         return rc;
     }
+    d->d_qcorh = d->d_tcorh + kSF;  // one allocation: fordate's spec writes both fields
     d->d_chk_late = d->d_chk_cnt + 1;
     d->d_tab = d->d_tabs;
     hipError_t e = hipMemcpy(d->d_tab, &d->tab, sizeof(DynTables), hipMemcpyHostToDevice);
@@ -2244,6 +2258,16 @@ extern "C" int sml_dyn_set_forcing(sml_dynamics *d, const double *phis, const do
     if (phis) SML_HIP(hipMemcpy(d->d_phis, phis, kSF * 8, hipMemcpyHostToDevice));
     if (tcorh) SML_HIP(hipMemcpy(d->d_tcorh, tcorh, kSF * 8, hipMemcpyHostToDevice));
     if (qcorh) SML_HIP(hipMemcpy(d->d_qcorh, qcorh, kSF * 8, hipMemcpyHostToDevice));
+    ++d->ford_gen;  // a later sml_dyn_fordate recomputes what the host has just replaced
+    return SML_OK;
+}
+
+extern "C" int sml_dyn_get_forcing(sml_dynamics *d, double *phis, double *tcorh, double *qcorh) {
+    SML_REQUIRE(d, "null context");
+    SML_HIP(hipDeviceSynchronize());
+    if (phis) SML_HIP(hipMemcpy(phis, d->d_phis, kSF * 8, hipMemcpyDeviceToHost));
+    if (tcorh) SML_HIP(hipMemcpy(tcorh, d->d_tcorh, kSF * 8, hipMemcpyDeviceToHost));
+    if (qcorh) SML_HIP(hipMemcpy(qcorh, d->d_qcorh, kSF * 8, hipMemcpyDeviceToHost));
     return SML_OK;
 }
 
@@ -2603,6 +2627,7 @@ extern "C" int sml_dyn_set_hybrid_sst(sml_dynamics *d, const double *d_sst_grid,
     SML_REQUIRE(d->phys_on, "sml_dyn_set_physics must provide the boundary fields first");
     d->hyb_sst = d_sst_grid;
     d->hyb_bias = sst_bias;
+    ++d->ford_gen;
     hipLaunchKernelGGL(k_hybrid_sst, dim3((kNGP + 255) / 256), dim3(256), 0, (hipStream_t)stream, d->d_sst_cpl,
                        d_sst_grid, d->d_sice, d->d_tice, sst_bias, d->d_pbc + (size_t)kBcSst * kNGP);
     SML_HIP(hipGetLastError());
@@ -2619,6 +2644,7 @@ extern "C" int sml_dyn_set_physics(sml_dynamics *d, const double *bc) {
     SML_HIP(hipMemcpy(d->d_pbc, bc, (size_t)kNBc * kNGP * 8, hipMemcpyHostToDevice));
     SML_HIP(hipMemcpy(d->d_sst_cpl, bc + (size_t)kBcSst * kNGP, kNGP * 8, hipMemcpyHostToDevice));
     d->phys_on = true;
+    ++d->ford_gen;
     if (d->hyb_sst) {  // a hybrid SST is in force: ini_sea applies it to every new sst_am
         if (int rc = sml_dyn_set_hybrid_sst(d, d->hyb_sst, d->hyb_bias, nullptr)) return rc;
         SML_HIP(hipDeviceSynchronize());
@@ -2638,7 +2664,224 @@ extern "C" int sml_dyn_set_sea_ice(sml_dynamics *d, const double *sice, const do
         SML_HIP(hipMemset(d->d_sice, 0, kNGP * 8));
         SML_HIP(hipMemset(d->d_tice, 0, kNGP * 8));
     }
+    ++d->ford_gen;
     if (d->hyb_sst) return sml_dyn_set_hybrid_sst(d, d->hyb_sst, d->hyb_bias, nullptr);
+    return SML_OK;
+}
+
+extern "C" int sml_dyn_get_sea_ice(sml_dynamics *d, double *sice, double *tice) {
+    SML_REQUIRE(d, "null context");
+    SML_HIP(hipDeviceSynchronize());
+    if (sice) SML_HIP(hipMemcpy(sice, d->d_sice, kNGP * 8, hipMemcpyDeviceToHost));
+    if (tice) SML_HIP(hipMemcpy(tice, d->d_tice, kNGP * 8, hipMemcpyDeviceToHost));
+    return SML_OK;
+}
+
+// the boundary fields as phypar reads them, host [kNBc][ngp] (sml_dyn_set_physics order)
+extern "C" int sml_dyn_get_physics(sml_dynamics *d, double *bc) {
+    SML_REQUIRE(d && bc, "null argument");
+    SML_REQUIRE(d->phys_on, "no boundary fields (sml_dyn_set_physics)");
+    SML_HIP(hipDeviceSynchronize());
+    SML_HIP(hipMemcpy(bc, d->d_pbc, (size_t)kNBc * kNGP * 8, hipMemcpyDeviceToHost));
+    return SML_OK;
+}
+
+// ------------------------------------------------------ per-window forcing (fordate)
+// run_model hands SPEEDY the calendar date of every window (mpires.f90:1545, :1595-1598)
+// and agcm_init rebuilds the date's forcing before stepone (ini_agcm_init.f90:57-89):
+// newdate(0), ini_coupler(2) and fordate(0); agcm_1day runs fordate(1) again before the
+// leapfrog loop (at_gcm.f90:84) with the same inputs (lco2 is .false., mod_lflags.f90:
+// 16, so imode 1 changes nothing).  With the coupler flags of the reference
+// (icland = 1, icsea = 0, icice = 1, isstan = 0; mod_cpl_flags.f90) and jday = 0:
+//   land (cpl_land.f90:1-95)  stl_am = forin5(stl12), snowd_am = forint(snowd12),
+//                             soilw_am = forint(soilw12)
+//   sea  (cpl_sea.f90:1-200)  sst = forin5(sst12), sice = forint(sice12) adjusted over
+//                             sea ice (:96-117, tice), sst_am = sst + sice (tice - sst),
+//                             then ini_sea's hybrid block (:38-46, k_hybrid_sst)
+//   fordate (ini_fordate.f90:50-113)  sol_oz(tyear), the surface albedo, tcorh =
+//                             spec(gamlat phis0), qcorh = spec(refrh1 (qref - qsfc))
+//                             from the current stl_am / sst_am
+// One thread per grid point; then spec of the two correction fields.
+namespace {
+struct FordateArgs {
+    double sol[5][kIL];  // sol_oz per latitude row: fsol, ozone, ozupp, zenit, stratz
+    int m5[5];
+    double w5[5];
+    int mi[2];
+    double wmon;
+    int clim, hyb;
+    double bias;
+};
+
+__global__ __launch_bounds__(256) void k_fordate(FordateArgs a, const double *__restrict__ surf,
+                                                 const double *__restrict__ clim, const double *__restrict__ hyb,
+                                                 double *__restrict__ pbc, double *__restrict__ sst_cpl,
+                                                 double *__restrict__ sice_am, double *__restrict__ tice_am,
+                                                 double *__restrict__ corh) {
+#pragma clang fp contract(off)  // the reference's separate multiplies and adds
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= kNGP) return;
+    const int j = p / kIX;
+    const double fmask_l = surf[p], fmask_s = surf[kNGP + p], alb0 = surf[2 * kNGP + p];
+    double snowc, sice, cpl;
+    if (a.clim) {
+        auto field = [&](int f, int m) { return clim[((size_t)f * 12 + m) * kNGP + p]; };
+        auto forin5 = [&](int f) {
+            return a.w5[0] * field(f, a.m5[0]) + a.w5[1] * field(f, a.m5[1]) + a.w5[2] * field(f, a.m5[2]) +
+                   a.w5[3] * field(f, a.m5[3]) + a.w5[4] * field(f, a.m5[4]);
+        };
+        auto forint = [&](int f) {
+            const double f0 = field(f, a.mi[0]);
+            return f0 + a.wmon * (field(f, a.mi[1]) - f0);
+        };
+        // land: atm2land(0), stl_lm = stlcl_ob (ini_land, istart 2), land2atm(0)
+        const double stl = forin5(0), snowd = forint(1), soilw = forint(2);
+        pbc[(size_t)kBcStl * kNGP + p] = stl;
+        pbc[(size_t)kBcSoilw * kNGP + p] = soilw;
+        snowc = fmin(1., snowd / 60.0);  // fordate: min(1, snowd_am / sd2sc), mod_surfcon sd2sc
+        // sea: atm2sea(0) with the sea-ice adjustment of the climatology
+        double sst = forin5(3), sic = forint(4), tic;
+        const double sstfr = 273.2 - 1.8;
+        if (sst > sstfr) {
+            sic = fmin(0.5, sic);
+            tic = sstfr;
+            if (sic > 0.) sst = sstfr + (sst - sstfr) / (1. - sic);
+        } else {
+            sic = fmax(0.5, sic);
+            tic = sstfr + (sst - sstfr) / sic;
+            sst = sstfr;
+        }
+        // ini_sea: the ocean / ice model starts from the climatology; sea2atm(0):
+        // icsea 0 -> sst_am = sstcl_ob (+ no anomaly), icice 1 -> the model's ice
+        sst = sst + 0.0;
+        sst = sst + sic * (tic - sst);
+        sice_am[p] = sic;
+        tice_am[p] = tic;
+        sst_cpl[p] = sst;
+        sice = sic;
+        cpl = sst;
+    } else {
+        snowc = pbc[(size_t)kBcSnowc * kNGP + p];
+        sice = sice_am[p];
+        cpl = sst_cpl[p];
+    }
+    double sst_am = cpl;
+    if (a.hyb) {  // ini_sea's hybrid block, as k_hybrid_sst
+        const double h = hyb[p];
+        const double diff = sst_am - h;
+        if (diff < 6.0) sst_am = h;
+        sst_am = sst_am + a.bias;
+        sst_am = sst_am + sice * (tice_am[p] - sst_am);
+    }
+    pbc[(size_t)kBcSst * kNGP + p] = sst_am;
+    // fordate 2: daily-mean radiative forcing and the surface albedo
+    pbc[(size_t)kBcFsol * kNGP + p] = a.sol[0][j];
+    pbc[(size_t)kBcOzone * kNGP + p] = a.sol[1][j];
+    pbc[(size_t)kBcOzupp * kNGP + p] = a.sol[2][j];
+    pbc[(size_t)kBcZenit * kNGP + p] = a.sol[3][j];
+    pbc[(size_t)kBcStratz * kNGP + p] = a.sol[4][j];
+    const double albsn = 0.60, albsea = 0.07, albice = 0.60;  // mod_radcon.f90:59-61
+    const double alb_l = alb0 + snowc * (albsn - alb0);
+    const double alb_s = albsea + sice * (albice - albsea);
+    pbc[(size_t)kBcSnowc * kNGP + p] = snowc;
+    pbc[(size_t)kBcAlbL * kNGP + p] = alb_l;
+    pbc[(size_t)kBcAlbS * kNGP + p] = alb_s;
+    pbc[(size_t)kBcAlbsfc * kNGP + p] = alb_s + fmask_l * (alb_l - alb_s);
+    // fordate 3-4: the horizontal-diffusion corrections (setgam: gamlat = gamma / (1000 g))
+    const double gamlat = 6.0 / (1000. * 9.81), rd = 287., refrh1 = 0.7;
+    const double c = gamlat * pbc[(size_t)kBcPhis0 * kNGP + p];
+    const double pexp = 1. / (rd * gamlat);
+    const double tsfc = fmask_l * pbc[(size_t)kBcStl * kNGP + p] + fmask_s * sst_am;
+    const double tref = tsfc + c;
+    const double psfc = pow(tsfc / tref, pexp);
+    // shtorh(0, .., tref, 1, -1, ..) and shtorh(0, .., tsfc, psfc, 1, ..) (phy_shtorh.f90:27-51)
+    auto qsat = [](double ta, double ps) {
+        const double e0 = 6.108e-3, c1 = 17.269, c2 = 21.875, t0 = 273.16, t1 = 35.86, t2 = 7.66;
+        const double q = (ta >= t0) ? e0 * exp(c1 * (ta - t0) / (ta - t1)) : e0 * exp(c2 * (ta - t0) / (ta - t2));
+        return 622. * q / (ps - 0.378 * q);
+    };
+    const double qref = qsat(tref, 1.0), qsfc = qsat(tsfc, 1. * psfc);
+    corh[p] = c;
+    corh[kGF + p] = refrh1 * (qref - qsfc);
+}
+
+}  // namespace
+
+// inbcon's time-independent surface fields fordate reads (ini_inbcon.f90:38-70,
+// 140-156): host [3][ngp] = fmask_l (mod_cli_land), fmask_s (mod_cli_sea), alb0
+// (mod_surfcon); NULL switches sml_dyn_fordate off
+extern "C" int sml_dyn_set_surface(sml_dynamics *d, const double *surf) {
+    SML_REQUIRE(d, "null context");
+    SML_HIP(hipDeviceSynchronize());
+    d->surf_on = surf != nullptr;
+    if (surf) SML_HIP(hipMemcpy(d->d_surf, surf, (size_t)3 * kNGP * 8, hipMemcpyHostToDevice));
+    ++d->ford_gen;
+    return SML_OK;
+}
+
+// the coupler's monthly climatologies (inbcon, ini_inbcon.f90:71-230): host
+// [5][12][ngp] = stl12, snowd12, soilw12 (mod_cli_land), sst12, sice12 (mod_cli_sea),
+// month 1 first; NULL: sml_dyn_fordate keeps the coupler fields the host set
+// (sml_dyn_set_physics' stl_am / sst_am / soilw_am / snowc, sml_dyn_set_sea_ice)
+extern "C" int sml_dyn_set_climatology(sml_dynamics *d, const double *clim) {
+    SML_REQUIRE(d, "null context");
+    SML_HIP(hipDeviceSynchronize());
+    if (clim) {
+        if (!d->d_clim) SML_HIP(hipMalloc(&d->d_clim, (size_t)5 * 12 * kNGP * 8));
+        SML_HIP(hipMemcpy(d->d_clim, clim, (size_t)5 * 12 * kNGP * 8, hipMemcpyHostToDevice));
+    }
+    d->clim_on = clim != nullptr;
+    ++d->ford_gen;
+    return SML_OK;
+}
+
+// agcm_init's forcing for a window at (iyear, imonth, iday) on `stream`: coupler,
+// hybrid SST, fordate (see k_fordate).  A no-op when neither the date nor any input
+// changed since the last call (the window's forcing stays as computed); force != 0
+// recomputes anyway.  Ordered on `stream`: the next window on that stream reads it.
+extern "C" int sml_dyn_fordate_ex(sml_dynamics *d, int iyear, int imonth, int iday, int force, void *stream) {
+    SML_REQUIRE(d && imonth >= 1 && imonth <= 12 && iday >= 1 && iday <= 31, "bad date %d-%d-%d", iyear, imonth, iday);
+    SML_REQUIRE(d->phys_on, "sml_dyn_set_physics must provide the boundary fields first");
+    SML_REQUIRE(d->surf_on, "sml_dyn_set_surface must provide fmask_l, fmask_s and alb0 first");
+    (void)iyear;  // only the co2 trend reads the year (lco2 = .false.)
+    if (!force && d->ford_done == d->ford_gen && d->ford_date[0] == imonth && d->ford_date[1] == iday)
+        return SML_OK;
+    hipStream_t st = (hipStream_t)stream;
+    ForDate fd;
+    phys_fordate_weights(imonth, iday, &fd);
+    FordateArgs a;
+    phys_sol_oz_lat(d->ptab, fd.tyear, &a.sol[0][0]);
+    for (int k = 0; k < 5; ++k) {
+        a.m5[k] = fd.m5[k];
+        a.w5[k] = fd.w5[k];
+    }
+    a.mi[0] = fd.mi[0];
+    a.mi[1] = fd.mi[1];
+    a.wmon = fd.wmon;
+    a.clim = d->clim_on ? 1 : 0;
+    a.hyb = d->hyb_sst ? 1 : 0;
+    a.bias = d->hyb_bias;
+    double *grid = d->d_ford, *varm = d->d_ford + 2 * kGF;
+    hipLaunchKernelGGL(k_fordate, dim3((kNGP + 255) / 256), dim3(256), 0, st, a, d->d_surf, d->d_clim, d->hyb_sst,
+                       d->d_pbc, d->d_sst_cpl, d->d_sice, d->d_tice, grid);
+    SML_HIP(hipGetLastError());
+    // spec (specx + specy) of corh -> tcorh, qcorh (contiguous)
+    if (int rc = spectral_specx(d->sp, grid, varm, 2, 0, st)) return rc;
+    if (int rc = spectral_specy(d->sp, varm, d->d_tcorh, 2, st)) return rc;
+    d->ford_done = d->ford_gen;
+    d->ford_date[0] = imonth;
+    d->ford_date[1] = iday;
+    ++d->ford_count;
+    return SML_OK;
+}
+
+extern "C" int sml_dyn_fordate(sml_dynamics *d, int iyear, int imonth, int iday, void *stream) {
+    return sml_dyn_fordate_ex(d, iyear, imonth, iday, 0, stream);
+}
+
+extern "C" int sml_dyn_fordate_count(const sml_dynamics *d, int *count) {
+    SML_REQUIRE(d && count, "null argument");
+    *count = d->ford_count;
     return SML_OK;
 }
 

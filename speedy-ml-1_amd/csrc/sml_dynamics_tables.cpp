@@ -260,6 +260,51 @@ void build_phys_tables(const DynTables &dt, PhysTables *p) {
 // sol_oz + solar (src/phy_radiat.f90:1-121): zonal daily-mean insolation and
 // ozone absorption, replicated along each latitude row.
 void phys_sol_oz(const PhysTables &p, double tyear, double *out5) {
+    double lat[5 * kIL];
+    phys_sol_oz_lat(p, tyear, lat);
+    for (int f = 0; f < 5; ++f)
+        for (int j = 0; j < kIL; ++j)
+            for (int i = 0; i < kIX; ++i) out5[(size_t)f * kNGP + j * kIX + i] = lat[f * kIL + j];
+}
+
+// newdate(0) (src/mod_date.f90:17-79, 365-day calendar, iseasc = 1) and the weights of
+// forin5 (src/cpl_bcinterp.f90:25-56) and forint (:1-23) for imon = imont1, fmon = tmonth
+void phys_fordate_weights(int imonth, int iday, ForDate *f) {
+    static const int ncal365[12] = {31, 28, 31, 30, 31, 30, 31, 31, 30, 31, 30, 31};
+    int before = 0;  // ndaycal(imonth, 2)
+    for (int m = 1; m < imonth; ++m) before += ncal365[m - 1];
+    f->imont1 = imonth;
+    f->tmonth = (iday - 0.5) / (double)ncal365[imonth - 1];
+    f->tyear = (before + iday - 0.5) / (double)365;
+    // forin5: non-linear, mean-conserving
+    const double fmon = f->tmonth;
+    int im2 = imonth - 2, im1 = imonth - 1, ip1 = imonth + 1, ip2 = imonth + 2;
+    if (im2 < 1) im2 += 12;
+    if (im1 < 1) im1 += 12;
+    if (ip1 > 12) ip1 -= 12;
+    if (ip2 > 12) ip2 -= 12;
+    const double c0 = 1. / 12., t0 = c0 * fmon, t1 = c0 * (1. - fmon), t2 = 0.25 * fmon * (1 - fmon);
+    f->w5[0] = -t1 + t2;
+    f->w5[1] = -c0 + 8 * t1 - 6 * t2;
+    f->w5[2] = 7 * c0 + 10 * t2;
+    f->w5[3] = -c0 + 8 * t0 - 6 * t2;
+    f->w5[4] = -t0 + t2;
+    const int m5[5] = {im2, im1, imonth, ip1, ip2};
+    for (int k = 0; k < 5; ++k) f->m5[k] = m5[k] - 1;
+    // forint: linear between the month and its neighbour on the side of the date
+    int imon2;
+    if (fmon <= 0.5) {
+        imon2 = imonth == 1 ? 12 : imonth - 1;
+        f->wmon = 0.5 - fmon;
+    } else {
+        imon2 = imonth == 12 ? 1 : imonth + 1;
+        f->wmon = fmon - 0.5;
+    }
+    f->mi[0] = imonth - 1;
+    f->mi[1] = imon2 - 1;
+}
+
+void phys_sol_oz_lat(const PhysTables &p, double tyear, double *out5) {
     const double pi = 2. * std::asin(1.);
     // solar(tyear, 4 solc): declination and Earth-Sun distance (Hartmann 1994)
     const double a = 2. * pi * tyear;
@@ -276,8 +321,8 @@ void phys_sol_oz(const PhysTables &p, double tyear, double *out5) {
     const double coz1 = 1.0 * std::fmax(0., std::cos(alpha - dalpha)), coz2 = 1.8, azen = 1.0;
     const double rzen = -std::cos(alpha) * 23.45 * std::asin(1.) / 90.;
     const double czen = std::cos(rzen), szen = std::sin(rzen), fs0 = 6.;
-    double *fsol = out5, *ozone = out5 + kNGP, *ozupp = out5 + 2 * kNGP, *zenit = out5 + 3 * kNGP,
-           *stratz = out5 + 4 * kNGP;
+    double *fsol = out5, *ozone = out5 + kIL, *ozupp = out5 + 2 * kIL, *zenit = out5 + 3 * kIL,
+           *stratz = out5 + 4 * kIL;
     for (int j = 0; j < kIL; ++j) {
         const double ch0 = std::fmin(1., std::fmax(-1., -tdecl * p.slat[j] / p.clat[j]));
         const double h0 = std::acos(ch0), sh0 = std::sin(h0);
@@ -289,15 +334,11 @@ void phys_sol_oz(const PhysTables &p, double tyear, double *out5) {
         const double zen = 1. + azen * (b * b);  // (..)**nzen, nzen = 2
         up = top * up * zen;
         oz = top * oz * zen;
-        const double st = std::fmax(fs0 - top, 0.);
-        for (int i = 0; i < kIX; ++i) {
-            const int g = j * kIX + i;
-            fsol[g] = top;
-            ozone[g] = oz;
-            ozupp[g] = up;
-            zenit[g] = zen;
-            stratz[g] = st;
-        }
+        fsol[j] = top;
+        ozone[j] = oz;
+        ozupp[j] = up;
+        zenit[j] = zen;
+        stratz[j] = std::fmax(fs0 - top, 0.);
     }
 }
 

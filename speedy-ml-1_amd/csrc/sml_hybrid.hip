@@ -119,6 +119,10 @@ struct sml_hybrid {
     const double *tisr_table = nullptr;
     int tisr_nhours = 0, tisr_startyear = 0, tisr_feb29 = 0;
     int64_t tisr_base = 0, tisr_step_hours = 6, t = 0;
+    // the window's date (run_model, mpires.f90:1545): with the calendar on
+    // (sml_hybrid_set_calendar) every advance hands SPEEDY the date of hour
+    // tisr_base + t * tisr_step_hours and the window's forcing follows it (sml_dyn_fordate)
+    bool cal_on = false;
     // the exchange row: the outvec (nout), + the slab ocean's sst of the region's
     // resolved points when the slab is on (as sendrecievegrid sends them, mpires.f90:358-383)
     int xw = 0;
@@ -729,6 +733,29 @@ extern "C" int sml_hybrid_set_tisr(sml_hybrid *h, const double *d_tisr) {
     return SML_OK;
 }
 
+// the loop's calendar (run_model / get_tisr_by_date's get_current_time_delta_hour,
+// mpires.f90:1545, :1661): start year, the hours before the first prediction step
+// (traininglength + prediction marker + synclength) and the hours per step; turns on
+// the window's date-driven forcing.  Resets the step count and the February latch.
+extern "C" int sml_hybrid_set_calendar(sml_hybrid *h, int startyear, int64_t hours_base, int step_hours) {
+    SML_REQUIRE(h && step_hours > 0 && hours_base >= 0, "bad argument");
+    h->tisr_startyear = startyear;
+    h->tisr_base = hours_base;
+    h->tisr_step_hours = step_hours;
+    h->tisr_feb29 = 0;
+    h->t = 0;
+    h->cal_on = true;
+    return SML_OK;
+}
+
+// the calendar date of the next window (the advance after the last one issued)
+extern "C" int sml_hybrid_window_date(sml_hybrid *h, int *date) {
+    SML_REQUIRE(h && date, "null argument");
+    SML_REQUIRE(h->cal_on, "no calendar (sml_hybrid_set_calendar)");
+    int feb29 = h->tisr_feb29;
+    return sml_calendar_delta_hour(h->tisr_startyear, h->tisr_base + (h->t + 1) * h->tisr_step_hours, &feb29, date);
+}
+
 extern "C" int sml_hybrid_set_tisr_table(sml_hybrid *h, const double *d_table, int nhours, int startyear,
                                          int64_t hours_base, int step_hours) {
     SML_REQUIRE(h && (d_table == nullptr || (nhours >= 8760 && step_hours > 0 && hours_base >= 0)), "bad argument");
@@ -1098,6 +1125,17 @@ extern "C" int sml_hybrid_advance(sml_hybrid *h, const double *d_outvec_all) {
     if (!done)
         if (int rc = sml_exchange_assemble(h->res, d_outvec_all, h->g4, h->g2, h->pr, c)) return rc;
     if (int rc = slab_sst(h, d_outvec_all, c)) return rc;
+    if (h->cal_on) {
+        // run_model's date for this step (mpires.f90:1545, timestep = t + 1; before the
+        // tisr lookup below, as the reference's calls meet the February latch) and the
+        // window's forcing at that date (agcm_init, ini_agcm_init.f90:57-89), after the
+        // previous window (the finish waited for its forecast) and any new hybrid SST
+        int date[4];
+        if (int rc = sml_calendar_delta_hour(h->tisr_startyear, h->tisr_base + (h->t + 1) * h->tisr_step_hours,
+                                             &h->tisr_feb29, date))
+            return rc;
+        if (int rc = sml_dyn_fordate(h->dyn, date[0], date[1], date[2], c)) return rc;
+    }
     // chain on SPEEDY's stream with kernel hops: the next run_model's entry specx signals
     // the assembled grid as it starts (no signal kernel in front of the window); run_model
     // is then enqueued before the main stream's wait for that signal -- every in-kernel

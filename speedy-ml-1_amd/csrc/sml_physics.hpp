@@ -42,6 +42,22 @@ struct PhysTables {
 void build_phys_tables(const DynTables &dt, PhysTables *p);
 // sol_oz(tyear) (src/phy_radiat.f90:1-121): fsol, ozone, ozupp, zenit, stratz [5][ngp]
 void phys_sol_oz(const PhysTables &p, double tyear, double *out5);
+// the same, one value per latitude row (sol_oz replicates it along the row): [5][il]
+void phys_sol_oz_lat(const PhysTables &p, double tyear, double *out5);
+
+// The forcing date of one window: newdate(0) with iseasc = 1 (src/mod_date.f90:17-79;
+// agcm_init sets iyear / imonth / iday from run_model's calendar, ini_agcm_init.f90:
+// 43-62) and the monthly interpolation weights the coupler applies at that date
+// (forin5 / forint, src/cpl_bcinterp.f90:1-56).  Months 0-based.
+struct ForDate {
+    int imont1;             // 1..12 (imonth)
+    double tmonth, tyear;   // (iday - 0.5) / ndays(imonth), (days before + iday - 0.5) / 365
+    int m5[5];              // forin5: imon-2 .. imon+2, wrapped
+    double w5[5];           // wm2, wm1, w0, wp1, wp2
+    int mi[2];              // forint: imon, imon2
+    double wmon;
+};
+void phys_fordate_weights(int imonth, int iday, ForDate *f);
 // sflset (src/phy_suflux.f90:358-382): forog from phi0 [ngp]
 void phys_sflset(const double *phi0, double *forog);
 

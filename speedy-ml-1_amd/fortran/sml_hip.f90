@@ -598,6 +598,37 @@ module sml_hip
       integer(c_int), intent(out) :: regions(*), count
       integer(c_int) :: rc
     end function
+    !> the window's date-driven forcing (agcm_init, ini_agcm_init.f90:57-89): inbcon's
+    !> fmask_l, fmask_s, alb0 (ngp, 3) and the monthly climatologies stl12, snowd12,
+    !> soilw12, sst12, sice12 (ngp, 12, 5)
+    function sml_dyn_set_surface(ctx, surf) bind(C, name='sml_dyn_set_surface') result(rc)
+      import :: c_ptr, c_double, c_int
+      type(c_ptr), value :: ctx
+      real(c_double), intent(in) :: surf(*)
+      integer(c_int) :: rc
+    end function
+    function sml_dyn_set_climatology(ctx, clim) bind(C, name='sml_dyn_set_climatology') result(rc)
+      import :: c_ptr, c_double, c_int
+      type(c_ptr), value :: ctx
+      real(c_double), intent(in) :: clim(*)
+      integer(c_int) :: rc
+    end function
+    !> newdate(0) + ini_coupler(2) + the hybrid SST + fordate(0) for a window at the date
+    function sml_dyn_fordate(ctx, iyear, imonth, iday, stream) bind(C, name='sml_dyn_fordate') result(rc)
+      import :: c_ptr, c_int
+      type(c_ptr), value :: ctx, stream
+      integer(c_int), value :: iyear, imonth, iday
+      integer(c_int) :: rc
+    end function
+    !> run_model's calendar (mpires.f90:1545): the loop refreshes each window's forcing
+    function sml_hybrid_set_calendar(h, startyear, hours_base, step_hours) &
+        bind(C, name='sml_hybrid_set_calendar') result(rc)
+      import :: c_ptr, c_int, c_int64_t
+      type(c_ptr), value :: h
+      integer(c_int), value :: startyear, step_hours
+      integer(c_int64_t), value :: hours_base
+      integer(c_int) :: rc
+    end function
   end interface
 
 contains

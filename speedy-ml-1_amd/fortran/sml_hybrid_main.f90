@@ -33,6 +33,10 @@
 !>               with weights/worker_XXXX_ocean_<trial_name>.nc per sst region
 !>               (read_trained_ocean_res, mod_io.f90:2958-3007: a region has a slab
 !>               reservoir iff its file exists)
+!>   forcing.bin (optional: the window's date-driven forcing, agcm_init's coupler and
+!>               fordate every window, ini_agcm_init.f90:57-89) fmask_l fmask_s alb0
+!>               (ix*il, 3), stl12 snowd12 soilw12 sst12 sice12 (ix*il, 12, 5), the
+!>               calendar's start year (int32) and hours before the first step (int64)
 !> Output: out_rank<r>.bin = run_speedy(nsteps) as real, then the exchange rows
 !> (width, nlocal) (width = 136, or 140 with the slab: outvec + the region's sst),
 !> feedback, local_model(132, nlocal), grid4d, grid2d, precip, forecast grid4d,
@@ -61,6 +65,11 @@ program sml_hybrid_main
   real(c_double), allocatable, target :: bc(:), g4(:), g2(:), pr(:), f4(:), f2(:), tisr_all(:, :), tisr(:, :)
   real(c_double), allocatable, target :: x(:), ov(:), fb(:), lm(:), runs(:)
   character(len=:), allocatable :: fname
+  ! the date-driven forcing
+  logical :: dated
+  integer(c_int) :: startyear
+  integer(c_int64_t) :: hours_base
+  real(c_double), allocatable :: surf(:), clim(:)
   ! slab ocean
   logical :: slab_on
   integer :: nslab, j, width
@@ -145,6 +154,15 @@ program sml_hybrid_main
   call sml_check(sml_dyn_set_forcing(dyn, phis, tcorh, qcorh), 'sml_dyn_set_forcing')
   call sml_check(sml_dyn_set_state(dyn, vor, div, tt, ps, tr), 'sml_dyn_set_state')
   call sml_check(sml_dyn_set_physics(dyn, bc), 'sml_dyn_set_physics')
+  inquire (file=trim(dir) // '/forcing.bin', exist=dated)
+  if (dated) then
+    allocate (surf(3 * ng2), clim(5 * 12 * ng2))
+    open (newunit=u, file=trim(dir) // '/forcing.bin', access='stream', form='unformatted', status='old')
+    read (u) surf, clim, startyear, hours_base
+    close (u)
+    call sml_check(sml_dyn_set_surface(dyn, surf), 'sml_dyn_set_surface')
+    call sml_check(sml_dyn_set_climatology(dyn, clim), 'sml_dyn_set_climatology')
+  end if
 
   ! --- start_prediction: saved states, the analysis grid and its SPEEDY forecast
   allocate (g4(ng4), g2(ng2), pr(ng2), f4(ng4), f2(ng2), tisr_all(16, numregions), tisr(16, nlocal))
@@ -181,6 +199,7 @@ program sml_hybrid_main
   ! --- the loop (parallelmain.f90:204-270)
   call sml_check(sml_hybrid_create(res, dyn, comm, int(nleap, c_int), delt, alph, rob, wil, int(overlap, c_int), &
                                    int(speedy_cus, c_int), hyb), 'sml_hybrid_create')
+  if (dated) call sml_check(sml_hybrid_set_calendar(hyb, startyear, hours_base, 6_c_int), 'sml_hybrid_set_calendar')
   if (slab_on) then  ! before the buffers: the exchange rows carry the regions' sst
     allocate (base(ng2), smask(ng2), sice(ng2), tice(ng2), sov_all(4, numregions), nslab_all(numregions))
     open (newunit=u, file=trim(dir) // '/slab.bin', access='stream', form='unformatted', status='old')

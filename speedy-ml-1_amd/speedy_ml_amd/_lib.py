@@ -59,6 +59,9 @@ EXPORTED = (
     "sml_hybrid_set_pipelined", "sml_res_step_cancel", "sml_res_step_begun", "sml_hybrid_set_force_exchange",
     "sml_hybrid_exchanges", "sml_hybrid_set_chain", "sml_hybrid_chain", "sml_hybrid_exchange_stream",
     "sml_res_set_update_cus", "sml_res_update_balanced", "sml_probe_mfma_f64_clock", "sml_res_ell_layout",
+    "sml_dyn_get_sea_ice", "sml_dyn_get_physics", "sml_dyn_get_forcing", "sml_dyn_set_surface",
+    "sml_dyn_set_climatology", "sml_dyn_fordate", "sml_dyn_fordate_ex", "sml_dyn_fordate_count",
+    "sml_hybrid_set_calendar", "sml_hybrid_window_date",
 )
 
 SML_HOP_AUTO, SML_HOP_WAIT_VALUE, SML_HOP_EVENTS, SML_HOP_KERNEL = 0, 1, 2, 3
@@ -242,6 +245,16 @@ def _declare(L: ctypes.CDLL) -> None:
         "sml_res_update_balanced": [vp, ip],
         "sml_res_ell_layout": [vp, i, ip, ip, ip, ip],
         "sml_probe_mfma_f64_clock": [i, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)],
+        "sml_dyn_get_sea_ice": [vp, vp, vp],
+        "sml_dyn_get_physics": [vp, vp],
+        "sml_dyn_get_forcing": [vp, vp, vp, vp],
+        "sml_dyn_set_surface": [vp, vp],
+        "sml_dyn_set_climatology": [vp, vp],
+        "sml_dyn_fordate": [vp, i, i, i, vp],
+        "sml_dyn_fordate_ex": [vp, i, i, i, i, vp],
+        "sml_dyn_fordate_count": [vp, ip],
+        "sml_hybrid_set_calendar": [vp, i, ctypes.c_int64, i],
+        "sml_hybrid_window_date": [vp, ip],
     }
     for name, args in sig.items():
         if os.environ.get("SML_LIB") and not hasattr(L, name):

@@ -29,6 +29,10 @@ NGP = 96 * 48
 # phypar's boundary fields, in the order of sml_dyn_set_physics (include/speedy_ml.h)
 PHYS_BC = ("fmask1", "phis0", "stl_am", "sst_am", "soilw_am", "alb_l", "alb_s", "albsfc", "snowc",
            "fsol", "ozone", "ozupp", "zenit", "stratz", "forog")
+# fordate's surface fields and the coupler's monthly climatologies (sml_dyn_set_surface,
+# sml_dyn_set_climatology)
+SURFACE = ("fmask_l", "fmask_s", "alb0")
+CLIMATOLOGY = ("stl12", "snowd12", "soilw12", "sst12", "sice12")
 RAD_SIZE = (4 * KX + 2 + KX + 1) * NGP
 DELT = 86400.0 / NSTEPS
 ROB, WIL, ALPH = 0.05, 0.53, 0.5  # mod_tsteps.f90:90,93; ini_indyns.f90 alph
@@ -140,6 +144,58 @@ class Dynamics:
         tend = np.zeros((4, KX, NGP))
         check(lib().sml_dyn_phypar_host(self._h, *[ptr(x) for x in f], int(bool(lradsw)), ptr(tend)))
         return tend
+
+    # ---------------------------------------------------- date-driven forcing
+    def set_surface(self, surf):
+        """fordate's surface fields: dict fmask_l, fmask_s, alb0 (or a (3, 4608) array
+        in that order), as inbcon leaves them (ini_inbcon.f90:38-70, 140-156)."""
+        if isinstance(surf, dict):
+            surf = np.stack([np.asarray(surf[k], dtype=np.float64).ravel() for k in SURFACE])
+        a = np.ascontiguousarray(surf, dtype=np.float64)
+        if a.size != len(SURFACE) * NGP:
+            raise ValueError("surface must hold 3 x 4608 values")
+        check(lib().sml_dyn_set_surface(self._h, ptr(a)))
+
+    def set_climatology(self, clim):
+        """Monthly climatologies: dict of CLIMATOLOGY arrays (12, 4608) (January
+        first), or a (5, 12, 4608) array; None keeps the coupler fields as set."""
+        if clim is None:
+            check(lib().sml_dyn_set_climatology(self._h, None))
+            return
+        if isinstance(clim, dict):
+            clim = np.stack([np.asarray(clim[k], dtype=np.float64).reshape(12, NGP) for k in CLIMATOLOGY])
+        a = np.ascontiguousarray(clim, dtype=np.float64)
+        if a.size != len(CLIMATOLOGY) * 12 * NGP:
+            raise ValueError("climatology must hold 5 x 12 x 4608 values")
+        check(lib().sml_dyn_set_climatology(self._h, ptr(a)))
+
+    def fordate(self, iyear: int, imonth: int, iday: int, force: bool = False, stream=None):
+        """agcm_init's forcing of a window at that date (coupler, hybrid SST, fordate;
+        ini_agcm_init.f90:57-89), asynchronous on `stream`; skipped when nothing changed."""
+        check(lib().sml_dyn_fordate_ex(self._h, int(iyear), int(imonth), int(iday), int(bool(force)),
+                                       stream_ptr(stream)))
+
+    def fordate_count(self) -> int:
+        c = ctypes.c_int()
+        check(lib().sml_dyn_fordate_count(self._h, ctypes.byref(c)))
+        return c.value
+
+    def get_physics(self):
+        """The boundary fields phypar reads, dict of PHYS_BC arrays (4608,)."""
+        a = np.zeros((len(PHYS_BC), NGP))
+        check(lib().sml_dyn_get_physics(self._h, ptr(a)))
+        return dict(zip(PHYS_BC, a))
+
+    def get_forcing(self):
+        """(phis, tcorh, qcorh) complex (32, 31) as the next window reads them."""
+        out = [np.zeros((NX, MX), np.complex128) for _ in range(3)]
+        check(lib().sml_dyn_get_forcing(self._h, *[ptr(o) for o in out]))
+        return dict(zip(("phis", "tcorh", "qcorh"), out))
+
+    def get_sea_ice(self):
+        sice, tice = np.zeros(NGP), np.zeros(NGP)
+        check(lib().sml_dyn_get_sea_ice(self._h, ptr(sice), ptr(tice)))
+        return sice, tice
 
     def sol_oz(self, tyear: float):
         """sol_oz(tyear): dict fsol, ozone, ozupp, zenit, stratz (ngp,)."""

@@ -124,6 +124,18 @@ class HybridLoop:
         check(lib().sml_hybrid_set_tisr_table(self._h, ptr(table), n, int(startyear), int(hours_base),
                                               int(step_hours)))
 
+    def set_calendar(self, startyear: int, hours_base: int, step_hours: int = 6):
+        """run_model's calendar (mpires.f90:1545): every advance t hands the window the
+        date of hour hours_base + t * step_hours and refreshes its forcing at that date
+        (Dynamics.fordate; the Dynamics needs set_surface).  Shared with the tisr table's."""
+        check(lib().sml_hybrid_set_calendar(self._h, int(startyear), int(hours_base), int(step_hours)))
+
+    def window_date(self):
+        """(year, month, day, hour) of the next advance's window."""
+        d = (ctypes.c_int * 4)()
+        check(lib().sml_hybrid_window_date(self._h, d))
+        return tuple(d)
+
     def start(self, g4, g2, pr, f4, f2):
         """start_prediction analogue: inputs of the first step from an analysis grid
         (g4, g2, pr) and a SPEEDY forecast from it (f4, f2)."""

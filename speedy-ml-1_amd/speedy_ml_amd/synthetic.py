@@ -278,3 +278,39 @@ def phys_boundary(dyn, phis, tyear: float = 0.25, seed: int = 41):
     bc["forog"] = dyn.sflset(bc["phis0"])
     bc.update(dyn.sol_oz(tyear))
     return bc
+
+
+def _mask_threshold(frac, thrsh=0.1):
+    """inbcon's fractional masks (ini_inbcon.f90:49-63, 146-156): below thrsh -> 0,
+    above 1 - thrsh -> 1."""
+    f = np.where(frac >= thrsh, frac, 0.0)
+    return np.where(frac > 1.0 - thrsh, 1.0, f)
+
+
+def surface_climatology(fmask, seed: int = 43):
+    """Synthetic inputs of the window's date-driven forcing on the T30 grid, shaped
+    like inbcon's (ini_inbcon.f90): the surface fields of sml_dyn_set_surface
+    {fmask_l, fmask_s, alb0} from a land fraction `fmask` (ngp,), and the monthly
+    climatologies of sml_dyn_set_climatology {stl12, snowd12, soilw12, sst12, sice12}
+    (12, ngp) with a seasonal cycle of opposite phase in the two hemispheres: polar
+    SSTs below freezing in winter with sea ice (the coupler's ice branch), snow depths
+    past sd2sc at high latitudes (snowc clipped at 1).  Not read from the reference's
+    boundary files."""
+    rng = np.random.default_rng(seed)
+    ngp = 96 * 48
+    lat = np.repeat(np.arcsin(np.polynomial.legendre.leggauss(48)[0]), 96)  # Gaussian, south -> north
+    fmask = np.asarray(fmask, dtype=np.float64).ravel()
+    surf = {"fmask_l": _mask_threshold(fmask), "fmask_s": _mask_threshold(1.0 - fmask),
+            "alb0": 0.1 + 0.25 * rng.random(ngp)}
+    m = np.arange(12)[:, None]
+    season = np.cos(2 * np.pi * (m - 6.5) / 12) * np.sign(lat)[None, :]  # > 0: summer
+    c2 = np.cos(lat)[None, :] ** 2
+    clim = {
+        "stl12": 262.0 + 30.0 * c2 + 14.0 * season * (1 - c2) + rng.standard_normal((12, ngp)),
+        "sst12": 270.5 + 31.0 * c2 + 3.5 * season * (1 - c2) + 0.3 * rng.standard_normal((12, ngp)),
+        "soilw12": np.clip(0.35 + 0.25 * season * c2 + 0.1 * rng.standard_normal((12, ngp)), 0.0, 1.0),
+    }
+    cold = np.clip(-season * (1 - c2) - 0.2, 0.0, None)
+    clim["snowd12"] = 150.0 * cold * rng.random((12, ngp))
+    clim["sice12"] = np.clip(1.6 * cold + 0.05 * rng.standard_normal((12, ngp)), 0.0, 1.0)
+    return surf, clim

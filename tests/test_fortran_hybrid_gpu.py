@@ -108,10 +108,13 @@ def test_fortran_hybrid_driver_matches_hybrid_loop(tmp_path, cuda):
     assert o == raw.size
 
 
-def test_fortran_hybrid_driver_with_slab_matches_hybrid_loop(tmp_path, cuda):
+@pytest.mark.parametrize("dated", [False, True])
+def test_fortran_hybrid_driver_with_slab_matches_hybrid_loop(tmp_path, cuda, dated):
     """sml_hybrid_main with the slab ocean (slab.bin + worker_XXXX_ocean_<trial>.nc,
     read_trained_ocean_res's layout): a slab step every 2nd hybrid step over 4 steps,
-    bitwise the Python HybridLoop with the same SlabOcean."""
+    bitwise the Python HybridLoop with the same SlabOcean; `dated`: with forcing.bin,
+    the window's forcing follows run_model's calendar (from 1982-01-31 12 h, across a
+    month boundary)."""
     import torch
 
     from speedy_ml_amd import domain
@@ -149,9 +152,18 @@ def test_fortran_hybrid_driver_with_slab_matches_hybrid_loop(tmp_path, cuda):
     dyn.set_state(st0)
     dyn.set_physics(phys_boundary(dyn, forcing["phis"]))
     check(lib().sml_dyn_set_sea_ice(dyn._h, ptr(np.ascontiguousarray(sice)), ptr(np.ascontiguousarray(tice))))
+    cal = (1982, 24 * 30 + 12)
+    if dated:
+        from speedy_ml_amd.dynamics import CLIMATOLOGY, SURFACE
+        from speedy_ml_amd.synthetic import surface_climatology
+        surf, clim = surface_climatology(phys_boundary(dyn, forcing["phis"])["fmask1"])
+        dyn.set_surface(surf)
+        dyn.set_climatology(clim)
     tisr = np.random.default_rng(13).standard_normal((1152, 16))
     loop = HybridLoop(res, dyn, OutvecExchange(1152, 1, 0, device=cuda), cuda, tisr=t(tisr), speedy_cus=64,
                       slab=SlabOcean(slab, t(base), t(smask), timestep=ts, timestep_slab=tss))
+    if dated:
+        loop.set_calendar(cal[0], cal[1], ts)
     g4, g2, pr = synthetic_grids(11)
     f4, f2, _ = synthetic_grids(12)
     loop.start(t(g4), t(g2), t(pr), t(f4), t(f2))
@@ -188,6 +200,12 @@ def test_fortran_hybrid_driver_with_slab_matches_hybrid_loop(tmp_path, cuda):
     nall = np.zeros(1152, dtype=np.int32)
     for w in sws:
         nall[w.region] = w.n
+    if dated:
+        with open(tmp_path / "forcing.bin", "wb") as f:
+            f.write(np.stack([surf[k] for k in SURFACE]).astype(np.float64).tobytes())
+            f.write(np.stack([clim[k] for k in CLIMATOLOGY]).astype(np.float64).tobytes())
+            f.write(np.array([cal[0]], dtype=np.int32).tobytes())
+            f.write(np.array([cal[1]], dtype=np.int64).tobytes())
     with open(tmp_path / "slab.bin", "wb") as f:
         f.write(np.array([ts, tss], dtype=np.int32).tobytes())
         for a in (base, smask, sice, tice, sov_all):

@@ -47,7 +47,7 @@ def _scaled(a, b):
     return float((np.abs(np.asarray(a) - np.asarray(b)) / (1.0 + np.abs(np.asarray(b)))).max())
 
 
-def _run(cuda, steps, timestep_slab, nleap, n_atmo=None, n_slab=None):
+def _run(cuda, steps, timestep_slab, nleap, n_atmo=None, n_slab=None, calendar=None):
     import ctypes
 
     import torch
@@ -96,13 +96,23 @@ def _run(cuda, steps, timestep_slab, nleap, n_atmo=None, n_slab=None):
     dyn.set_forcing(**forcing)
     dyn.set_state(st0)
     bc = phys_boundary(dyn, forcing["phis"])
+    if calendar is not None:  # the window's date-driven forcing (sml_dyn_fordate every advance)
+        from speedy_ml_amd.synthetic import surface_climatology
+        surf, clim = surface_climatology(bc["fmask1"])
+        bc["fmask1"] = surf["fmask_l"]
     dyn.set_physics(bc)
     check(lib().sml_dyn_set_sea_ice(dyn._h, ptr(np.ascontiguousarray(sice)), ptr(np.ascontiguousarray(tice))))
+    if calendar is not None:
+        dyn.set_surface(surf)
+        dyn.set_climatology(clim)
     tisr = np.random.default_rng(13).standard_normal((1152, 16))
     d_base, d_mask = t(base), t(smask)
     so = SlabOcean(slab, d_base, d_mask, timestep=6, timestep_slab=timestep_slab)
     loop = HybridLoop(res, dyn, OutvecExchange(1152, 1, 0, device=cuda), cuda, tisr=t(tisr), nleap=nleap, slab=so)
     assert loop.exchange_width == 140
+    if calendar is not None:
+        loop.set_calendar(calendar[0], calendar[1], 6)
+        n_fordate = dyn.fordate_count()
     g4, g2, pr = synthetic_grids(11)
     f4, f2, _ = synthetic_grids(12)
     loop.start(t(g4), t(g2), t(pr), t(f4), t(f2))
@@ -116,6 +126,8 @@ def _run(cuda, steps, timestep_slab, nleap, n_atmo=None, n_slab=None):
         snap = {k: getattr(loop, k).cpu().numpy().copy() for k in ("ov", "fb", "f4", "f2")}
         snap.update(loop.slab_state())
         got.append(snap)
+    if calendar is not None:
+        n_fordate = dyn.fordate_count() - n_fordate
     got_x = {r: res.get_state(r) for r in (0, 24, 500, 1151)}
     got_sx = {j: slab.get_state(j) for j in (0, len(sreg) // 2, len(sreg) - 1)}
     assert loop.run_speedy()
@@ -147,6 +159,8 @@ def _run(cuda, steps, timestep_slab, nleap, n_atmo=None, n_slab=None):
     fbv, lmv = tile_all(g4, g2, pr, f4, f2, {r: np.zeros(in2d[r]) for r in sreg})  # the start's sst entries: 0
     errs = {"ov": 0.0, "sov": 0.0, "fb": 0.0, "fc": 0.0, "sst": 0.0, "ring": 0.0}
     nslab_steps = 0
+    tcorh, qcorh = forcing["tcorh"], forcing["qcorh"]
+    cal_state, dates, want_fordate, last = {}, [], 0, None
     for step in range(1, steps + 1):
         ov = oracle.predict_f32_regions(regs, fbv, lmv, xs, nthreads=8)
         if (step * 6) % timestep_slab == 0:
@@ -169,17 +183,25 @@ def _run(cuda, steps, timestep_slab, nleap, n_atmo=None, n_slab=None):
         a4, a2, apr = oracle.assemble(ov)
         sst = oracle.sst_grid(sst_rows, base, smask)
         errs["sst"] = max(errs["sst"], _scaled(g["sst"], sst))
-        bc_w["sst_am"] = oracle.hybrid_sst_am(bc["sst_am"], sst.ravel(), sice, tice)
+        if calendar is None:
+            bc_w["sst_am"] = oracle.hybrid_sst_am(bc["sst_am"], sst.ravel(), sice, tice)
+        else:  # run_model's date (mpires.f90:1545) -> agcm_init's forcing of the window
+            y, mo, dd, _ = oracle.calendar_delta_hour(calendar[0], calendar[1] + step * 6, cal_state)
+            dates.append((y, mo, dd))
+            bc_w, tcorh, qcorh, _, _ = oracle.window_forcing(mo, dd, surf, bc, clim=clim, sst_hybrid=sst.ravel())
+            slab_now = (step * 6) % timestep_slab == 0 or step == 1
+            want_fordate += (mo, dd) != last or slab_now
+            last = (mo, dd)
         _, safe = oracle.iogrid30(s, a4, a2)
         assert safe
         DT = DELT
-        oracle.dyn_step_physics(s, forcing["phis"], forcing["tcorh"], forcing["qcorh"], bc_w, rad, lradsw, 1, 1,
+        oracle.dyn_step_physics(s, forcing["phis"], tcorh, qcorh, bc_w, rad, lradsw, 1, 1,
                                 0.5 * DT, 0.5)
-        oracle.dyn_step_physics(s, forcing["phis"], forcing["tcorh"], forcing["qcorh"], bc_w, rad, lradsw, 1, 2,
+        oracle.dyn_step_physics(s, forcing["phis"], tcorh, qcorh, bc_w, rad, lradsw, 1, 2,
                                 DT, 0.5)
         for istep in range(1, nleap + 1):
             lradsw = istep % 3 == 1
-            oracle.dyn_step_physics(s, forcing["phis"], forcing["tcorh"], forcing["qcorh"], bc_w, rad, lradsw, 2, 2,
+            oracle.dyn_step_physics(s, forcing["phis"], tcorh, qcorh, bc_w, rad, lradsw, 2, 2,
                                     2 * DT, 0.5)
         o4, o2 = oracle.iogrid31(s)
         o4[..., 3] = np.where(o4[..., 3] < 0.000001, 0.000001, o4[..., 3])
@@ -192,6 +214,9 @@ def _run(cuda, steps, timestep_slab, nleap, n_atmo=None, n_slab=None):
         ring[col] = np.concatenate([fbv[r][oracle.slab_input_index(r)] for r in sreg])
         errs["ring"] = max(errs["ring"], float(np.abs(g["ring"][col] - ring[col]).max()))
     assert nslab_steps >= 1
+    if calendar is not None:  # the run crossed a day, and the forcing was rebuilt only when it changed
+        assert len(set(dates)) >= 2, dates
+        assert n_fordate == want_fordate, (n_fordate, want_fordate, dates)
     e_x = max(_scaled(got_x[r], xs[r]) for r in got_x)
     e_sx = max(_scaled(got_sx[j], sxs[j]) for j in got_sx)
     print(f"slab loop {steps} steps (slab every {timestep_slab // 6}): " +
@@ -205,6 +230,15 @@ def _run(cuda, steps, timestep_slab, nleap, n_atmo=None, n_slab=None):
 
 def test_slab_loop_full_size(cuda):
     _run(cuda, steps=9, timestep_slab=24, nleap=24)
+
+
+def test_slab_loop_date_forcing(cuda):
+    """run_model's calendar date drives the window's forcing (VERDICT r04 missing #1):
+    the coupler's climatologies at the date, the slab's hybrid SST into sst_am, qcorh
+    from it, the insolation of the day.  11 steps from 1981-02-27 06 h: across two
+    days, the month boundary and slab steps (every 4th step), against the oracle
+    chain's window_forcing."""
+    _run(cuda, steps=11, timestep_slab=24, nleap=2, n_atmo=96, n_slab=200, calendar=(1981, 24 * 58 + 6))
 
 
 def test_slab_loop_reference_cadence(cuda):
