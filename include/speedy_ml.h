@@ -633,7 +633,8 @@ int sml_hybrid_slab_buffers(const sml_hybrid *h, const double **d_sst_grid, cons
  * (the same sequence number, stored by a one-lane kernel behind the producer and
  * polled by a one-lane kernel ahead of the consumer; a wait that has not seen its
  * value after ~4 s gives up and sml_hybrid_sync returns SML_ERR_STATE), or
- * SML_HOP_AUTO (the default: kernel hops, but events when dispatch is serialised --
+ * SML_HOP_AUTO (the default: kernel hops when the two streams run on disjoint CUs, i.e. speedy_cus > 0,
+ * else wait-value hops; events when dispatch is serialised --
  * AMD_SERIALIZE_KERNEL or rocprofv3's counter collection -- where a waiting packet or
  * kernel could stall its queue ahead of its producer; SML_HYBRID_EVENTS=1 also
  * selects events, SML_HYBRID_HOPK=0 wait-value).  In the kernel mode the v_p finish
@@ -644,6 +645,13 @@ int sml_hybrid_slab_buffers(const sml_hybrid *h, const double **d_sst_grid, cons
 #define SML_HOP_EVENTS 2
 #define SML_HOP_KERNEL 3
 int sml_hybrid_set_hop_mode(sml_hybrid *h, int mode);
+/* the give-up time of the loop's in-kernel waits (kernel hops; run_model's exit waiting
+ * for its safety check, at most 1 s), microseconds; default 4 s.  A wait that gives up
+ * hands its consumer NaN instead of the data it did not get (the finish's local model,
+ * the entry's grid; the exit takes the window as unsafe) and marks a host-visible word:
+ * the next sml_hybrid_step, sml_hybrid_run_speedy (which then also yields run = 0) or
+ * sml_hybrid_sync returns SML_ERR_STATE once.  SML_HOP_TIMEOUT_US sets it at create. */
+int sml_hybrid_set_hop_timeout(sml_hybrid *h, int64_t microseconds);
 int sml_hybrid_hop_mode(const sml_hybrid *h, int *requested, int *effective);
 /* pipelined loop (default off): each advance also issues the NEXT step's reservoir
  * begin (update + v_ml readout of the feedback it has just tiled) on the main stream,

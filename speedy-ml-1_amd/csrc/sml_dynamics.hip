@@ -104,7 +104,11 @@ struct sml_dynamics {
     // event wait on its stream (chk_flag; SML_CHK_FLAG=0 at create: the event): the
     // check's k_io_minmax adds 4 per check, the exit polls for 4 * chk_count
     bool chk_flag = true;
-    unsigned *d_chk_cnt = nullptr, *d_chk_late = nullptr;
+    unsigned *d_chk_cnt = nullptr;
+    // the exit's hand-off timed out: a pinned, host-visible word (read without a copy by
+    // sml::dyn_check_late, reset when reported); the exit's give-up time in ticks
+    unsigned *d_chk_late = nullptr;
+    long long chk_timeout = 100000000ll;
     // the next run_model's entry waits in-kernel for its input grids (sml::dyn_run_model_wait)
     HopWait entry_wait;
     // the next run_model's exit signals its forecast in-kernel (sml::dyn_run_model_signal)
@@ -2147,6 +2151,7 @@ extern "C" int sml_dyn_destroy(sml_dynamics *d) {
     if (d->h_mm) (void)hipHostFree(d->h_mm);
     if (d->d_chk) (void)hipFree(d->d_chk);
     if (d->d_chk_cnt) (void)hipFree(d->d_chk_cnt);
+    if (d->d_chk_late) (void)hipHostFree(d->d_chk_late);
     if (d->sp) sml_spectral_destroy(d->sp);
     delete d;
     return SML_OK;
@@ -2196,7 +2201,12 @@ extern "C" int sml_dyn_create(double radius, sml_dynamics **out) {
         return rc;
     }
     d->d_qcorh = d->d_tcorh + kSF;  // one allocation: fordate's spec writes both fields
-    d->d_chk_late = d->d_chk_cnt + 1;
+    if (hipHostMalloc((void **)&d->d_chk_late, sizeof(unsigned), hipHostMallocCoherent) != hipSuccess) {
+        d->d_chk_late = nullptr;
+        sml_dyn_destroy(d);
+        return fail(SML_ERR_NOMEM, "sml_dyn_create: pinned late word");
+    }
+    *d->d_chk_late = 0;
     d->d_tab = d->d_tabs;
     hipError_t e = hipMemcpy(d->d_tab, &d->tab, sizeof(DynTables), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(d->d_ptab, &d->ptab, sizeof(PhysTables), hipMemcpyHostToDevice);
@@ -3089,6 +3099,7 @@ extern "C" int sml_dyn_run_model(sml_dynamics *d, const double *d_grid4d, const 
         ex.cnt = d->d_chk_cnt;
         ex.target = 4u * d->chk_count;
         ex.late = d->d_chk_late;
+        ex.timeout = d->chk_timeout;
         d->chk_pending = false;
     } else if (d->chk_pending) {  // the exit reads the check's min/max
         SML_HIP(hipStreamWaitEvent(st, d->ev_chk, 0));
@@ -3138,15 +3149,26 @@ extern "C" int sml_dyn_last_safe(sml_dynamics *d, int *safe, double *minmax) {
         return fail(SML_ERR_STATE, "sml_dyn_last_safe before any sml_dyn_from_grid");
     }
     *safe = sml_dyn_is_safe(mm);
+    // an exit that gave up on this check took the window as unsafe (it did so before the
+    // check completed, so the word is final here)
+    if (d->d_chk_late && __atomic_load_n(d->d_chk_late, __ATOMIC_ACQUIRE)) *safe = 0;
     if (minmax) std::memcpy(minmax, mm, sizeof mm);
     return SML_OK;
 }
 
-// a run_model exit that gave up waiting for its safety check (1 s; never expected):
-// checked by the hybrid loop's sync, after the streams drained
-int sml::dyn_run_model_wait(sml_dynamics *d, const uint64_t *flag, uint64_t value, unsigned *late) {
+// the next run_model's entry specx waits in-kernel until *flag >= value; on a timeout
+// (ticks) it marks *late and transforms NaN (the window's check then fails)
+int sml::dyn_run_model_wait(sml_dynamics *d, const uint64_t *flag, uint64_t value, unsigned *late,
+                            long long timeout) {
     SML_REQUIRE(d && flag && late, "null argument");
     d->entry_wait = HopWait{flag, value, late};
+    d->entry_wait.timeout = timeout;
+    return SML_OK;
+}
+
+int sml::dyn_set_check_timeout(sml_dynamics *d, long long timeout) {
+    SML_REQUIRE(d && timeout >= 0, "bad argument");
+    d->chk_timeout = timeout;
     return SML_OK;
 }
 
@@ -3176,11 +3198,15 @@ int sml::dyn_run_model_signal(sml_dynamics *d, uint64_t *counter, int *adds) {
     return SML_OK;
 }
 
+// a run_model exit that gave up waiting for its safety check (it then took the window
+// as unsafe): reported once, then reset.  The word is host memory: no copy, no sync --
+// callers read it once the exit has run (sml_hybrid_run_speedy, after the check's event)
 int sml::dyn_check_late(sml_dynamics *d) {
     if (!d || !d->d_chk_late) return SML_OK;
-    unsigned late = 0;
-    SML_HIP(hipMemcpy(&late, d->d_chk_late, sizeof late, hipMemcpyDeviceToHost));
-    if (late) return fail(SML_ERR_STATE, "run_model's exit did not receive the safety check within 1 s");
+    if (__atomic_load_n(d->d_chk_late, __ATOMIC_ACQUIRE)) {
+        __atomic_store_n(d->d_chk_late, 0u, __ATOMIC_RELEASE);
+        return fail(SML_ERR_STATE, "run_model's exit did not receive its safety check in time (window taken as unsafe)");
+    }
     return SML_OK;
 }
 

@@ -72,6 +72,11 @@ struct sml_hybrid {
     static constexpr int kSeqStride = 16;  // one 128-B line per hop's word; the late word after them
     hipEvent_t ev[kHops] = {nullptr, nullptr, nullptr};
     uint64_t *d_seq = nullptr, seq[kHops] = {0, 0, 0};
+    // a kernel hop that gave up waiting (its consumer read NaN instead of stale data):
+    // a pinned host word the waits store at system scope, read without a copy by
+    // sml_hybrid_step / run_speedy / sync; the waits' give-up time (wall_clock64 ticks)
+    unsigned *h_late = nullptr;
+    long long hop_timeout = 400000000ll;
     // where the step's serial chain runs (sml_hybrid_set_chain): false, the two-stream
     // schedule above (the finish, exchange and assembly on the main stream, two hops
     // around every window); true, on SPEEDY's stream right after the window:
@@ -421,20 +426,28 @@ __global__ void k_hop_signal(uint64_t *flag, uint64_t v) {
     if (threadIdx.x == 0) __hip_atomic_store(flag, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__global__ void k_hop_wait(const uint64_t *flag, uint64_t v, unsigned *late) {
+__global__ void k_hop_wait(const uint64_t *flag, uint64_t v, unsigned *late, long long timeout) {
     if (threadIdx.x != 0) return;
     const long long t0 = wall_clock64();
     while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < v) {
         __builtin_amdgcn_s_sleep(1);
-        if (wall_clock64() - t0 > 400000000ll) {  // ~4 s at wall_clock64's 100 MHz
-            __hip_atomic_store(late, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (wall_clock64() - t0 > timeout) {  // default ~4 s at wall_clock64's 100 MHz
+            __hip_atomic_store(late, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             break;
         }
     }
 }
 
-unsigned *hop_late_word(sml_hybrid *h) {
-    return reinterpret_cast<unsigned *>(h->d_seq + sml_hybrid::kHops * sml_hybrid::kSeqStride);
+unsigned *hop_late_word(sml_hybrid *h) { return h->h_late; }
+
+// a hop that timed out since the last report: SML_ERR_STATE once (the word is reset)
+int hop_late_check(sml_hybrid *h, const char *where) {
+    if (h->h_late && __atomic_load_n(h->h_late, __ATOMIC_ACQUIRE)) {
+        __atomic_store_n(h->h_late, 0u, __ATOMIC_RELEASE);
+        return fail(SML_ERR_STATE, "%s: a cross-stream hop (SML_HOP_KERNEL) timed out -- its consumer read NaN, "
+                                   "the steps since are invalid", where);
+    }
+    return SML_OK;
 }
 
 // producer side of hop `k`: ordered after everything issued on `s` so far
@@ -457,7 +470,7 @@ int hop_wait(sml_hybrid *h, int k, hipStream_t s) {
     if (h->use_events) {
         SML_HIP(hipStreamWaitEvent(s, h->ev[k], 0));
     } else if (h->use_kernels) {
-        hipLaunchKernelGGL(k_hop_wait, dim3(1), dim3(64), 0, s, w, h->seq[k], hop_late_word(h));
+        hipLaunchKernelGGL(k_hop_wait, dim3(1), dim3(64), 0, s, w, h->seq[k], hop_late_word(h), h->hop_timeout);
         SML_HIP(hipGetLastError());
     } else {
         SML_HIP(hipStreamWaitValue64(s, w, h->seq[k], hipStreamWaitValueGte, ~0ull));
@@ -509,16 +522,28 @@ extern "C" int sml_hybrid_set_hop_mode(sml_hybrid *h, int mode) {
     if (h->side && h->side != h->main) SML_HIP(hipStreamSynchronize(h->side));
     h->hop_mode = mode;
     if (mode == SML_HOP_AUTO) {
-        // kernel hops unless dispatch is serialised (a waiting kernel would hold its queue
+        // kernel hops only when the two streams run on disjoint CUs (res_cus > 0): a
+        // waiting finish's blocks then never occupy a CU the window (their producer)
+        // needs; not when dispatch is serialised (a waiting kernel would hold its queue
         // ahead of its producer) or SML_HYBRID_EVENTS / SML_HYBRID_HOPK=0 asks otherwise
         h->use_events = env_on("SML_HYBRID_EVENTS") || dispatch_serialised();
         const char *hk = getenv("SML_HYBRID_HOPK");
-        h->use_kernels = !h->use_events && !(hk && *hk == '0');
+        h->use_kernels = !h->use_events && !(hk && *hk == '0') && h->res_cus > 0;
     } else {
         h->use_events = mode == SML_HOP_EVENTS;
         h->use_kernels = mode == SML_HOP_KERNEL;
     }
     return SML_OK;
+}
+
+// the give-up time of every in-kernel wait of the loop (the kernel hops, and run_model's
+// exit waiting for its safety check), microseconds; default 4 s (hops) / 1 s (check)
+extern "C" int sml_hybrid_set_hop_timeout(sml_hybrid *h, int64_t microseconds) {
+    SML_REQUIRE(h && microseconds >= 0, "bad argument");
+    if (h->main) SML_HIP(hipStreamSynchronize(h->main));
+    if (h->side && h->side != h->main) SML_HIP(hipStreamSynchronize(h->side));
+    h->hop_timeout = (long long)microseconds * 100;  // wall_clock64 runs at 100 MHz
+    return sml::dyn_set_check_timeout(h->dyn, std::min<long long>(h->hop_timeout, 100000000ll));
 }
 
 // pipelined loop (see sml_hybrid::pipelined); switching it off keeps a begin already
@@ -605,6 +630,7 @@ extern "C" int sml_hybrid_destroy(sml_hybrid *h) {
                     sl.d_ring_src, sl.d_row, sl.d_sst_src, sl.d_sfb, sl.d_sgrid, sl.d_sreg};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
+    if (h->h_late) (void)hipHostFree(h->h_late);
     delete h;
     return SML_OK;
 }
@@ -688,10 +714,14 @@ extern "C" int sml_hybrid_create(sml_reservoirs *res, sml_dynamics *dyn, sml_com
     for (hipEvent_t &e : h->ev)
         if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return bail(fail(SML_ERR_HIP, "event"));
     if (int rc = sml_hybrid_set_hop_mode(h, SML_HOP_AUTO)) return bail(rc);
-    constexpr size_t seq_bytes = (sml_hybrid::kHops + 1) * sml_hybrid::kSeqStride * sizeof(uint64_t);
+    constexpr size_t seq_bytes = sml_hybrid::kHops * sml_hybrid::kSeqStride * sizeof(uint64_t);
     if (hipMalloc(&h->d_seq, seq_bytes) != hipSuccess || hipMemset(h->d_seq, 0, seq_bytes) != hipSuccess ||
+        hipHostMalloc((void **)&h->h_late, sizeof(unsigned), hipHostMallocCoherent) != hipSuccess ||
         hipDeviceSynchronize() != hipSuccess)
         return bail(fail(SML_ERR_HIP, "sequence counters"));
+    *h->h_late = 0;
+    if (const char *e = std::getenv("SML_HOP_TIMEOUT_US"))  // (tests: sml_hybrid_set_hop_timeout)
+        if (int rc = sml_hybrid_set_hop_timeout(h, std::atoll(e))) return bail(rc);
     h->xw = h->nout;
     if (world > 1) {
         std::vector<int32_t> perm(h->numregions);
@@ -1066,7 +1096,7 @@ int predict_impl(sml_hybrid *h, bool assemble) {
             if (int rc = hop_signal(h, sml_hybrid::kHopBegun, h->main)) return rc;
             if (h->use_kernels && h->nlocal > 0) {  // waited for inside the finish (no wait kernel)
                 if (int rc = sml::res_finish_wait(h->res, h->d_seq + sml_hybrid::kHopBegun * sml_hybrid::kSeqStride,
-                                                  h->seq[sml_hybrid::kHopBegun], hop_late_word(h)))
+                                                  h->seq[sml_hybrid::kHopBegun], hop_late_word(h), h->hop_timeout))
                     return rc;
             } else if (int rc = hop_wait(h, sml_hybrid::kHopBegun, xs)) {
                 return rc;
@@ -1084,7 +1114,7 @@ int predict_impl(sml_hybrid *h, bool assemble) {
             if (int rc = sml::dyn_check_event(h->dyn, &ev)) return rc;
             if (ev) SML_HIP(hipStreamWaitEvent(h->main, (hipEvent_t)ev, 0));
             if (int rc = sml::res_finish_wait(h->res, h->d_seq + sml_hybrid::kHopLm * sml_hybrid::kSeqStride,
-                                              h->seq[sml_hybrid::kHopLm], hop_late_word(h)))
+                                              h->seq[sml_hybrid::kHopLm], hop_late_word(h), h->hop_timeout))
                 return rc;
         } else if (int rc = hop_wait(h, sml_hybrid::kHopLm, h->main)) {  // SPEEDY's forecast of the previous window
             return rc;
@@ -1179,7 +1209,7 @@ extern "C" int sml_hybrid_advance(sml_hybrid *h, const double *d_outvec_all) {
     if (hops) {
         if (h->use_kernels) {  // the entry's specx waits for the assembled grid in-kernel
             if (int rc = sml::dyn_run_model_wait(h->dyn, h->d_seq + sml_hybrid::kHopGrid * sml_hybrid::kSeqStride,
-                                                 h->seq[sml_hybrid::kHopGrid], hop_late_word(h)))
+                                                 h->seq[sml_hybrid::kHopGrid], hop_late_word(h), h->hop_timeout))
                 return rc;
         } else if (int rc = hop_wait(h, sml_hybrid::kHopGrid, s)) {
             return rc;
@@ -1231,6 +1261,7 @@ extern "C" int sml_hybrid_advance_slabs(sml_hybrid *h, const double *d_recv) {
 // all-gather of every rank's outvec slab (RCCL over xGMI) on the main stream
 extern "C" int sml_hybrid_step(sml_hybrid *h) {
     SML_REQUIRE(h, "null context");
+    if (int rc = hop_late_check(h, "sml_hybrid_step")) return rc;  // a host word: no sync
     const int world = h->comm ? h->comm->world : 1;
     if (world == 1 && h->nlocal != h->numregions)
         return fail(SML_ERR_STATE, "one rank holds %d of %d regions: exchange through sml_hybrid_advance",
@@ -1274,7 +1305,20 @@ extern "C" int sml_hybrid_run_speedy(sml_hybrid *h, int *run) {
         *run = 1;
         return SML_OK;
     }
-    return sml_dyn_last_safe(h->dyn, run, nullptr);
+    if (int rc = sml_dyn_last_safe(h->dyn, run, nullptr)) return rc;
+    // once that step's check is done, every wait of the step has run (the check follows
+    // the entry specx, which follows the finish): a wait that gave up fails the step
+    // here, so a host polling per step (parallelmain.f90:268-270) stops instead of
+    // going on from NaN forecasts; run_speedy is then 0
+    if (int rc = hop_late_check(h, "sml_hybrid_run_speedy")) {
+        *run = 0;
+        return rc;
+    }
+    if (int rc = sml::dyn_check_late(h->dyn)) {
+        *run = 0;
+        return rc;
+    }
+    return SML_OK;
 }
 
 // wait for every issued step; the local model of the last window is tiled as the
@@ -1291,15 +1335,7 @@ extern "C" int sml_hybrid_sync(sml_hybrid *h) {
     }
     SML_HIP(hipStreamSynchronize(h->main));
     SML_HIP(hipStreamSynchronize(h->side));
-    if (h->use_kernels) {  // a kernel hop that gave up waiting: the consumer ran on stale data
-        unsigned late = 0;
-        SML_HIP(hipMemcpy(&late, hop_late_word(h), sizeof(late), hipMemcpyDeviceToHost));
-        if (late) {
-            SML_HIP(hipMemset(hop_late_word(h), 0, sizeof(late)));
-            return fail(SML_ERR_STATE, "a cross-stream hop (SML_HOP_KERNEL) timed out: the steps since the last "
-                                       "sync ran on stale data");
-        }
-    }
+    if (int rc = hop_late_check(h, "sml_hybrid_sync")) return rc;
     return sml::dyn_check_late(h->dyn);
 }
 

@@ -22,10 +22,13 @@ bool res_in_global_order(const sml_reservoirs *c);
 int dyn_check_late(sml_dynamics *d);
 // the next sml_res_step_finish_grid / _finish_assemble launch waits in-kernel until
 // *flag >= value (device words; *late set if it gave up), its weights loaded first
-int res_finish_wait(sml_reservoirs *c, const uint64_t *flag, uint64_t value, unsigned *late);
+// (*late: a host-visible word; timeout in wall_clock64 ticks, 100 MHz)
+int res_finish_wait(sml_reservoirs *c, const uint64_t *flag, uint64_t value, unsigned *late, long long timeout);
 // the next sml_dyn_run_model / sml_dyn_from_grid waits in-kernel (its entry specx)
 // until *flag >= value before it reads its input grids
-int dyn_run_model_wait(sml_dynamics *d, const uint64_t *flag, uint64_t value, unsigned *late);
+int dyn_run_model_wait(sml_dynamics *d, const uint64_t *flag, uint64_t value, unsigned *late, long long timeout);
+// the give-up time of the run_model exit's wait for its safety check (ticks)
+int dyn_set_check_timeout(sml_dynamics *d, long long timeout);
 int dyn_run_model_signal(sml_dynamics *d, uint64_t *counter, int *adds);
 int dyn_run_model_entry_signal(sml_dynamics *d, uint64_t *counter, int *adds);
 int dyn_check_event(sml_dynamics *d, void **ev);  // a hipEvent_t

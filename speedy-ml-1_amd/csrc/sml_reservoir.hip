@@ -146,7 +146,15 @@ struct sml_reservoirs {
     const uint64_t *fin_wflag = nullptr;
     uint64_t fin_wval = 0;
     unsigned *fin_wlate = nullptr;
-    int upd_cus = 0, bal_grid = 0, ncu = 0;
+    long long fin_wtimeout = 400000000ll;  // wall_clock64 ticks
+    int upd_cus = 0, ncu = 0;
+    // the balanced update's per-block first regions, one table per grid size G (a paced
+    // begin and an uncapped step alternate two sizes): tables in one device buffer at
+    // offset G (G - 1) / 2, built once per G; blk_off[G] = -1 until then
+    std::vector<int32_t> blk_off;
+    std::vector<std::vector<int32_t>> blk_host;  // the host tables (async copies' sources stay alive)
+    int blk_cap = 0;  // largest G the buffer holds
+    size_t max_lds = 0;  // the device's LDS per workgroup (hipDeviceAttributeMaxSharedMemoryPerBlock)
     int ell_ok = -1;  // every local region's A and W_in in ELL form (-1: recount after a load)
     int32_t *d_row0 = nullptr, *d_blk_r0 = nullptr;
     std::vector<int32_t> row0_h;
@@ -904,8 +912,9 @@ __global__ __launch_bounds__(256) void k_res_finish_grid(
     const double *__restrict__ part, double *__restrict__ outvec, int nout, int ov_ld, int nout_pad, int ncs,
     const int32_t *__restrict__ asm_dst = nullptr, double *__restrict__ g4 = nullptr, double *__restrict__ g2 = nullptr,
     double *__restrict__ pr = nullptr, const uint64_t *__restrict__ wflag = nullptr, uint64_t wval = 0,
-    unsigned *__restrict__ wlate = nullptr) {
+    unsigned *__restrict__ wlate = nullptr, long long wtimeout = 400000000ll) {
     __shared__ double slm[kMaxNcs];
+    __shared__ int gave_up;
     __shared__ double red[kGrouped ? kFinGroups * 144 : 1];
     const int r = blockIdx.x, t = threadIdx.x;
     const double *ms = meanstd + (size_t)r * 2 * kMeanStd;
@@ -936,11 +945,13 @@ __global__ __launch_bounds__(256) void k_res_finish_grid(
     }
     if (wflag) {
         if (t == 0) {
+            gave_up = 0;
             const long long c0 = wall_clock64();
             while (__hip_atomic_load(wflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < wval) {
                 __builtin_amdgcn_s_sleep(1);
-                if (wall_clock64() - c0 > 400000000ll) {  // ~4 s at wall_clock64's 100 MHz
-                    __hip_atomic_store(wlate, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (wall_clock64() - c0 > wtimeout) {  // default ~4 s at wall_clock64's 100 MHz
+                    __hip_atomic_store(wlate, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    gave_up = 1;
                     break;
                 }
             }
@@ -950,7 +961,9 @@ __global__ __launch_bounds__(256) void k_res_finish_grid(
         __syncthreads();
     }
     if (gj) {
-        const double v = gs < kGrid4d ? fc4[gs] : fc2[gs - kGrid4d];
+        // a forecast that never arrived reads as NaN: the outvecs, grids and the next
+        // window's safety check then refuse it instead of predicting from stale values
+        const double v = (wflag && gave_up) ? __builtin_nan("") : (gs < kGrid4d ? fc4[gs] : fc2[gs - kGrid4d]);
         const double d = v - gmean;
         const double x = d / gstd;
         slm[t] = x;
@@ -1523,6 +1536,11 @@ int res_create_impl(int numregions, int nlocal, const int *region_ids, const uns
     SML_REQUIRE(c->read_waves >= 0, "bad read_waves");
     (void)hipGetDevice(&c->device);
     (void)hipDeviceGetAttribute(&c->ncu, hipDeviceAttributeMultiprocessorCount, c->device);
+    {
+        int lds = 0;
+        (void)hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerBlock, c->device);
+        c->max_lds = (size_t)std::max(lds, 0);
+    }
     c->region_ids.assign(region_ids, region_ids + nlocal);
     c->sst.assign(sst_flags, sst_flags + nlocal);
     c->n.assign(n, n + nlocal);
@@ -1845,7 +1863,7 @@ bool bal_usable(sml_reservoirs *c) {
             if (c->rd[i].a_w <= 0 || c->rd[i].w_w <= 0) c->ell_ok = 0;
     }
     const size_t lds = 2 * (size_t)((c->maxn + 1) / 2 * 2 + c->maxninp) * sizeof(double);
-    return c->ell_ok == 1 && c->maxn <= kStageX * kUpdThreads && c->maxninp <= kUpdThreads && lds <= 160 * 1024;
+    return c->ell_ok == 1 && c->maxn <= kStageX * kUpdThreads && c->maxninp <= kUpdThreads && lds <= c->max_lds;
 }
 
 int launch_update_bal(sml_reservoirs *c, const double *xo, double *xn, const double *d_feedback, hipStream_t st,
@@ -1854,18 +1872,29 @@ int launch_update_bal(sml_reservoirs *c, const double *xo, double *xn, const dou
     int G = c->upd_cus > 0 ? c->upd_cus : std::max(c->ncu, 1);  // one block per CU the launch gets
     if (paced && c->upd_blocks > 0) G = std::min(G, c->upd_blocks);
     G = (int)std::max<int64_t>(1, std::min<int64_t>(G, total));
-    if (G != c->bal_grid) {  // each block's first region, for this grid
+    if (G > c->blk_cap) {  // (the buffer grows only past the largest grid seen: rare, synchronous)
+        const int cap = std::max(G, std::max(c->ncu, c->upd_cus));
+        if (c->d_blk_r0) {
+            SML_HIP(hipDeviceSynchronize());
+            SML_HIP(hipFree(c->d_blk_r0));
+            c->d_blk_r0 = nullptr;
+        }
+        if (int rc = dalloc(&c->d_blk_r0, (size_t)cap * (cap + 1) / 2)) return rc;
+        c->blk_off.assign(cap + 1, -1);
+        c->blk_cap = cap;
+    }
+    if (c->blk_off[G] < 0) {  // each block's first region, for this grid: once per G
         std::vector<int32_t> r0(G);
         for (int b = 0; b < G; ++b) {
             const int64_t g0 = total * b / G;
             r0[b] = (int32_t)(std::upper_bound(c->row0_h.begin(), c->row0_h.end(), (int32_t)g0) - c->row0_h.begin() - 1);
         }
-        if (c->d_blk_r0) SML_HIP(hipFree(c->d_blk_r0));
-        c->d_blk_r0 = nullptr;
-        if (int rc = dalloc(&c->d_blk_r0, G)) return rc;
-        SML_HIP(hipMemcpy(c->d_blk_r0, r0.data(), G * 4, hipMemcpyHostToDevice));
-        c->bal_grid = G;
+        c->blk_off[G] = G * (G - 1) / 2;
+        c->blk_host.push_back(std::move(r0));  // ordered before the launch on st
+        SML_HIP(hipMemcpyAsync(c->d_blk_r0 + c->blk_off[G], c->blk_host.back().data(), (size_t)G * 4,
+                               hipMemcpyHostToDevice, st));
     }
+    const int32_t *blk_r0 = c->d_blk_r0 + c->blk_off[G];
     const int lds_x = (c->maxn + 1) / 2 * 2, lds_buf = lds_x + c->maxninp;
     const size_t lds = 2 * (size_t)lds_buf * sizeof(double);
     const Ell ell = make_ell(c);
@@ -1878,7 +1907,7 @@ int launch_update_bal(sml_reservoirs *c, const double *xo, double *xn, const dou
         ovf = ovf || c->rd[i].a_ov;
     }
     auto go = [&](auto kern) {
-        hipLaunchKernelGGL(kern, dim3(G), dim3(kUpdThreads), lds, st, c->d_rd, c->d_row0, c->d_blk_r0, c->nlocal,
+        hipLaunchKernelGGL(kern, dim3(G), dim3(kUpdThreads), lds, st, c->d_rd, c->d_row0, blk_r0, c->nlocal,
                            total, ell, xo, xn, d_feedback, c->leakage, lds_x, lds_buf);
     };
 #define SML_BAL_D(WT, D)                                                                                    \
@@ -2131,7 +2160,8 @@ void launch_finish_grid(sml_reservoirs *c, const double *d_fc4d, const double *d
         hipLaunchKernelGGL((k_res_finish_grid<WT, kAsm, decltype(grouped_tag)::value>), dim3(c->nlocal), dim3(256), 0,
                            st, c->d_rd, (const WT *)c->d_wlm, c->d_lm_src, c->d_lm_l, d_fc4d, d_fc2d, d_local_model,
                            c->d_meanstd, c->d_outl, c->d_part, d_outvec, c->nout, c->ov_ld, c->nout_pad, c->ncs,
-                           c->d_asm_dst, d_grid4d, d_grid2d, d_precip, c->fin_wflag, c->fin_wval, c->fin_wlate);
+                           c->d_asm_dst, d_grid4d, d_grid2d, d_precip, c->fin_wflag, c->fin_wval, c->fin_wlate,
+                           c->fin_wtimeout);
     };
     using G1 = std::integral_constant<bool, true>;
     using G0 = std::integral_constant<bool, false>;
@@ -2147,12 +2177,14 @@ void launch_finish_grid(sml_reservoirs *c, const double *d_fc4d, const double *d
 }
 }  // namespace
 
-int sml::res_finish_wait(sml_reservoirs *c, const uint64_t *flag, uint64_t value, unsigned *late) {
+int sml::res_finish_wait(sml_reservoirs *c, const uint64_t *flag, uint64_t value, unsigned *late,
+                         long long timeout) {
     SML_REQUIRE(c && flag && late, "null argument");
     SML_REQUIRE(c->ncs <= 256, "the in-kernel wait needs ncs <= the finish block");
     c->fin_wflag = flag;
     c->fin_wval = value;
     c->fin_wlate = late;
+    c->fin_wtimeout = timeout;
     return SML_OK;
 }
 

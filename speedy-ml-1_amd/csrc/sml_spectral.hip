@@ -205,19 +205,25 @@ __global__ __launch_bounds__(kFftThreads) void k_gridx(const double *__restrict_
         // relaxed sc1 poll per step of lane 0, MI355X_MICROARCH.md inter-workgroup
         // visibility: the producer stored mm sc1 and drained before its atomic add),
         // then read mm with sc1 loads
+        __shared__ int gave_up;
         if (threadIdx.x == 0) {
+            gave_up = 0;
             const long long t0 = wall_clock64();
             while (__hip_atomic_load(ex.cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < ex.target) {
                 __builtin_amdgcn_s_sleep(2);
-                if (wall_clock64() - t0 > 100000000ll) {  // ~1 s at 100 MHz: never hang the queue
-                    __hip_atomic_store(ex.late, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (wall_clock64() - t0 > ex.timeout) {  // never hang the queue
+                    __hip_atomic_store(ex.late, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    gave_up = 1;
                     break;
                 }
             }
         }
         __syncthreads();
+        // a check that did not arrive counts as unsafe (NaN fails every threshold): the
+        // forecast is then the window's input, as agcm_main skips an unsafe window
 #pragma unroll
-        for (int q = 0; q < 8; ++q) mmv[q] = __hip_atomic_load(ex.mm + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int q = 0; q < 8; ++q)
+            mmv[q] = gave_up ? __builtin_nan("") : __hip_atomic_load(ex.mm + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } else if (ex.mm) {
 #pragma unroll
         for (int q = 0; q < 8; ++q) mmv[q] = ex.mm[q];
@@ -254,15 +260,18 @@ __global__ __launch_bounds__(kFftThreads) void k_specx(const double *__restrict_
     // wait.flag: the grid comes from another stream (SML_HOP_KERNEL): the twiddles are
     // staged first, then one lane polls, acquires at agent scope and releases the
     // block (MI355X_MICROARCH.md inter-workgroup visibility, the consumer form)
+    __shared__ int gave_up;
     if (wait.flag) {
         if (threadIdx.x < kFftWa) was[threadIdx.x] = wa[threadIdx.x];
         if (threadIdx.x + kFftThreads < kFftWa) was[threadIdx.x + kFftThreads] = wa[threadIdx.x + kFftThreads];
         if (threadIdx.x == 0) {
+            gave_up = 0;
             const long long c0 = wall_clock64();
             while (__hip_atomic_load(wait.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < wait.value) {
                 __builtin_amdgcn_s_sleep(1);
-                if (wall_clock64() - c0 > 400000000ll) {  // ~4 s at wall_clock64's 100 MHz
-                    __hip_atomic_store(wait.late, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (wall_clock64() - c0 > wait.timeout) {
+                    __hip_atomic_store(wait.late, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    gave_up = 1;
                     break;
                 }
             }
@@ -271,6 +280,7 @@ __global__ __launch_bounds__(kFftThreads) void k_specx(const double *__restrict_
         }
         __syncthreads();
     }
+    const bool stale = wait.flag && gave_up;  // the grid never arrived: transform NaN, not stale values
     // transform (f, j) on the thread pair 2 t, 2 t + 1: thread h transforms the samples
     // 2 i + h (rfftf48), the pair meets in LDS for rfftf's last pass (rfftf96_combine).
     // The samples are loaded before the twiddles are staged (one memory round trip).
@@ -300,6 +310,10 @@ __global__ __launch_bounds__(kFftThreads) void k_specx(const double *__restrict_
 #pragma unroll
             for (int i = 0; i < kFftN / 2; ++i) x[i] = g[2 * i];
         }
+    }
+    if (stale) {
+#pragma unroll
+        for (int i = 0; i < kFftN / 2; ++i) x[i] = __builtin_nan("");
     }
     if (!wait.flag) {
         if (threadIdx.x < kFftWa) was[threadIdx.x] = wa[threadIdx.x];

@@ -46,6 +46,10 @@ struct HopWait {
     // grid was released by the kernel before it on the stream; the chain on SPEEDY's
     // stream hands the assembled grid to the main stream's re-tiling this way)
     uint64_t *sig = nullptr;
+    // give-up time of the poll in wall_clock64 ticks (100 MHz; default ~4 s); on a
+    // timeout the kernel marks *late (system scope: a host-visible word) and reads NaN
+    // instead of the grid it did not get, so nothing downstream passes for a forecast
+    long long timeout = 400000000ll;
 };
 int spectral_specx_io_blocks();
 int spectral_specx_io(sml_spectral *s, const double *g4, const double *logp, double *varm, int nwind,
@@ -66,6 +70,7 @@ struct IoExit {
     const unsigned *cnt = nullptr;
     unsigned target = 0;
     unsigned *late = nullptr;
+    long long timeout = 100000000ll;  // ~1 s; on a timeout the check counts as unsafe (NaN min / max)
     // the forecast's hand-off to another stream without a signal kernel: each block,
     // its stores drained and released at agent scope, adds 1 (spectral_exit_blocks()
     // adds per launch) -- the consumer polls *sig >= its count

@@ -61,7 +61,7 @@ EXPORTED = (
     "sml_res_set_update_cus", "sml_res_update_balanced", "sml_probe_mfma_f64_clock", "sml_res_ell_layout",
     "sml_dyn_get_sea_ice", "sml_dyn_get_physics", "sml_dyn_get_forcing", "sml_dyn_set_surface",
     "sml_dyn_set_climatology", "sml_dyn_fordate", "sml_dyn_fordate_ex", "sml_dyn_fordate_count",
-    "sml_hybrid_set_calendar", "sml_hybrid_window_date",
+    "sml_hybrid_set_calendar", "sml_hybrid_window_date", "sml_hybrid_set_hop_timeout",
 )
 
 SML_HOP_AUTO, SML_HOP_WAIT_VALUE, SML_HOP_EVENTS, SML_HOP_KERNEL = 0, 1, 2, 3
@@ -255,6 +255,7 @@ def _declare(L: ctypes.CDLL) -> None:
         "sml_dyn_fordate_count": [vp, ip],
         "sml_hybrid_set_calendar": [vp, i, ctypes.c_int64, i],
         "sml_hybrid_window_date": [vp, ip],
+        "sml_hybrid_set_hop_timeout": [vp, ctypes.c_int64],
     }
     for name, args in sig.items():
         if os.environ.get("SML_LIB") and not hasattr(L, name):

@@ -124,6 +124,10 @@ class HybridLoop:
         check(lib().sml_hybrid_set_tisr_table(self._h, ptr(table), n, int(startyear), int(hours_base),
                                               int(step_hours)))
 
+    def set_hop_timeout(self, microseconds: int):
+        """Give-up time of the loop's in-kernel waits (sml_hybrid_set_hop_timeout)."""
+        check(lib().sml_hybrid_set_hop_timeout(self._h, int(microseconds)))
+
     def set_calendar(self, startyear: int, hours_base: int, step_hours: int = 6):
         """run_model's calendar (mpires.f90:1545): every advance t hands the window the
         date of hour hours_base + t * step_hours and refreshes its forcing at that date

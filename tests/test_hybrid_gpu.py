@@ -418,3 +418,41 @@ def test_chain_on_speedys_stream_is_bitwise_the_two_stream_loop(cuda):
         np.testing.assert_array_equal(sa[k], sb[k], err_msg=k)
     for a, b in zip(xa, xb):
         np.testing.assert_array_equal(a, b)
+
+
+def test_a_hop_that_times_out_fails_the_step(cuda):
+    """VERDICT r04 item 4 / ADVICE r04: with the in-kernel waits' give-up time at its
+    minimum, the first window's entry -- which waits for the grid the main stream
+    assembles only after the whole reservoir begin (~0.7 ms later, the delayed
+    producer) -- gives up at once.  It transforms NaN instead of a stale grid, the
+    window's safety check fails, the forecast is the assembled grid passed through
+    (agcm_main skips an unsafe window), and the step's run_speedy -- what a host polls
+    every step (parallelmain.f90:268-270) -- returns the error with run = 0 instead of
+    the loop going on."""
+    import ctypes
+
+    import torch
+
+    from speedy_ml_amd._lib import SML_HOP_KERNEL, SmlError, lib
+
+    loop, _ = _loop(cuda, True)
+    assert loop.hop_mode()[1] == SML_HOP_KERNEL
+    loop.set_hop_timeout(0)
+    loop.step()
+    r = ctypes.c_int(7)
+    rc = lib().sml_hybrid_run_speedy(loop._h, ctypes.byref(r))
+    assert rc != 0 and r.value == 0
+    assert b"timed out" in lib().sml_last_error()
+    try:  # sync's own hop may time out too at zero give-up time: reported once
+        loop.sync()
+    except SmlError:
+        pass
+    loop.sync()  # the words were reset when reported
+    torch.cuda.synchronize()
+    g4 = loop.g4.cpu().numpy()
+    assert np.isfinite(g4).all()
+    want = g4.copy()
+    want[..., 3] = np.where(g4[..., 3] < 0.000001, 0.000001, g4[..., 3])
+    np.testing.assert_array_equal(loop.f4.cpu().numpy(), want)
+    np.testing.assert_array_equal(loop.f2.cpu().numpy(), loop.g2.cpu().numpy())
+    loop.close()

@@ -507,14 +507,15 @@ def test_finish_assemble_is_bitwise_finish_then_assemble(cuda):
     part.close()
 
 
-@pytest.mark.parametrize("cus", [0, 192, 7, 1])
-def test_balanced_update_is_bitwise_the_per_region_update(cuda, cus):
+@pytest.mark.parametrize("cus,wdt", [(0, "f32"), (192, "f32"), (7, "f32"), (1, "f32"), (192, "f64"), (7, "f64")])
+def test_balanced_update_is_bitwise_the_per_region_update(cuda, cus, wdt):
     """k_res_update_bal (a persistent grid, one block per CU, each block an equal share
     of all the rank's rows, two passes of A rows in flight, the next region's x staged
     into a second LDS buffer) against k_res_update (a block per region; SML_UPD_BAL=0
     at create): the states, x_aug-fed outvecs and the begin / finish split bitwise over
     3 steps, for grids of every CU (0), the hybrid loop's reservoir CUs (192), an odd
-    grid (7: shares straddle many regions) and one block (every region in turn)."""
+    grid (7: shares straddle many regions) and one block (every region in turn); with
+    fp32 and fp64 weights (the Pair<double> 16-B loads)."""
     import os
 
     import torch
@@ -531,7 +532,7 @@ def test_balanced_update_is_bitwise_the_per_region_update(cuda, cus):
         if not bal:
             os.environ["SML_UPD_BAL"] = "0"
         try:
-            res = Reservoirs(regions, mask[regions], [w.n for w in ws], [w.k for w in ws])
+            res = Reservoirs(regions, mask[regions], [w.n for w in ws], [w.k for w in ws], weight_dtype=wdt)
         finally:
             os.environ.pop("SML_UPD_BAL", None)
         for i, w in enumerate(ws):
@@ -559,7 +560,8 @@ def test_balanced_update_is_bitwise_the_per_region_update(cuda, cus):
         np.testing.assert_array_equal(a, b, err_msg=f"region {regions[i]}")
 
 
-def test_ell_layouts_are_bitwise_the_csr_update(cuda):
+@pytest.mark.parametrize("wdt", ["f32", "f64"])
+def test_ell_layouts_are_bitwise_the_csr_update(cuda, wdt):
     """A's ELL main width chosen per region (pair-major slots, an overflow list for the
     rows one longer) and W_in's implicit block-diagonal column: every
     layout the builder picks gives the states and outvecs of the CSR copies
@@ -567,7 +569,8 @@ def test_ell_layouts_are_bitwise_the_csr_update(cuda):
     steps -- and the oracle's within its tolerance.  Regions: every full-size shape
     class (n 6048 with 4.8 % of rows one longer -> overflow; 5880 / 5760 -> 6 slots;
     6160 -> overflow), a region of 2- and 3-entry rows (2 slots + overflow), and a W_in
-    whose columns are permuted (not block-diagonal: its column is read)."""
+    whose columns are permuted (not block-diagonal: its column is read).  Both weight
+    precisions (fp64: the Pair<double> loads, the overflow entries, the depth-2 pipeline)."""
     import os
 
     import torch
@@ -589,7 +592,7 @@ def test_ell_layouts_are_bitwise_the_csr_update(cuda):
         env = {"csr": {"SML_NO_ELL": "1", "SML_UPD_BAL": "0"}, "per_region": {"SML_UPD_BAL": "0"}, "balanced": {}}[form]
         os.environ.update(env)
         try:
-            res = Reservoirs(regions, mask[regions], [w.n for w in ws], [w.k for w in ws])
+            res = Reservoirs(regions, mask[regions], [w.n for w in ws], [w.k for w in ws], weight_dtype=wdt)
         finally:
             for k in env:
                 os.environ.pop(k, None)
