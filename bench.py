@@ -100,6 +100,10 @@ def parse():
                    help="the slab ocean in the loop, as the reference runs by default (mod_reservoir.f90:41): a "
                         "slab reservoir per sst region, predict_slab_ml every 168 h (28 steps), its sst in the "
                         "window (sml_hybrid_set_slab)")
+    p.add_argument("--date-forcing", action=argparse.BooleanOptionalAction, default=True,
+                   help="run_model's calendar drives each window's forcing (agcm_init: the coupler's monthly "
+                        "climatologies at the date, the hybrid SST, fordate; sml_hybrid_set_calendar), from "
+                        "1982-01-01 00 h as the loop's first hour; --no-date-forcing holds the start's forcing")
     p.add_argument("--speedy-steps", type=int, default=48,
                    help="leapfrog steps timed in the supplementary SPEEDY-step leg (0 = skip)")
     p.add_argument("--poll-run-speedy", action=argparse.BooleanOptionalAction, default=True,
@@ -302,7 +306,15 @@ def main():
     dyn.set_forcing(**forcing)
     dyn.set_state(st0)
     phys_bc = phys_boundary(dyn, forcing["phis"])
+    if args.date_forcing:  # inbcon's surface fields and monthly climatologies (synthetic)
+        from speedy_ml_amd.synthetic import surface_climatology
+
+        surf_h, clim_h = surface_climatology(phys_bc["fmask1"])
+        phys_bc["fmask1"] = surf_h["fmask_l"]
     dyn.set_physics(phys_bc)
+    if args.date_forcing:
+        dyn.set_surface(surf_h)
+        dyn.set_climatology(clim_h)
     if slab_ocean is not None:
         from speedy_ml_amd._lib import check as _check, lib as _lib, ptr as _ptr
 
@@ -318,6 +330,8 @@ def main():
         comm = NativeComm(world, rank)
     loop = HybridLoop(res, dyn, exchange, dev, tisr=tisr, overlap=args.overlap, speedy_cus=args.speedy_cus,
                       comm=comm, slab=slab_ocean)
+    if args.date_forcing:  # the hours before the first step: traininglength + marker + synclength in the reference
+        loop.set_calendar(1981, 24 * 365, 6)
     if args.pipelined:
         loop.set_pipelined(True)
     from speedy_ml_amd._lib import SML_CHAIN_SPEEDY, SML_CHAIN_TWO_STREAMS
@@ -384,9 +398,11 @@ def main():
         step()
     loop.sync()
     poll = args.poll_run_speedy
+    n_ford0 = dyn.fordate_count()
     dt = timed(step_polled if poll else step, args.steps, timing=True)
     upd_ms, rd_ms = res.kernel_times()
     steps_done = ran[0]
+    n_ford = dyn.fordate_count() - n_ford0
     # the poll's cost: the same K steps again without the host waiting on run_speedy
     dt_nopoll = timed(step, args.steps) if poll and not ended else None
     if args.pipelined and args.overlap:  # the next step's begin is in flight: close it (untimed)
@@ -457,6 +473,29 @@ def main():
             "value": round(args.reservoir_steps / rdt, 3), "unit": "hybrid timesteps/s",
             "ms_per_step": round(rdt / args.reservoir_steps * 1e3, 4), "steps": args.reservoir_steps,
             "roofline_unpaced": unpaced}
+    date_forcing = {"on": False}
+    if args.date_forcing:
+        # the forcing's own cost: forced recomputations (the coupler at a date + hybrid SST
+        # + fordate: one grid-point kernel and spec of tcorh / qcorh), on one stream
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        for i in range(3):
+            dyn.fordate(1982, 1 + i % 12, 1 + i % 28, force=True)
+        ev0.record()
+        nrep = 50
+        for i in range(nrep):
+            dyn.fordate(1982, 1 + i % 12, 1 + i % 28, force=True)
+        ev1.record()
+        torch.cuda.synchronize()
+        f_ms = ev0.elapsed_time(ev1) / nrep
+        date_forcing = {
+            "on": True,
+            "calendar": "startyear 1981, hours_base 8760 (1982-01-01), 6 h per step: each window's date as "
+                        "run_model's get_current_time_delta_hour gives it (mpires.f90:1545)",
+            "recomputed_windows": n_ford, "timed_windows": steps_done,
+            "note": "recomputed when the date (once a day: every 4th step) or the slab's hybrid SST changed; "
+                    "on the reservoir stream before the grid hop, i.e. on the critical path of those steps",
+            "recompute_ms": round(f_ms, 4),
+            "per_step_ms": round(f_ms * n_ford / max(steps_done, 1), 4)}
     dyn.close()
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.cpu_threads > 0:
@@ -518,6 +557,7 @@ def main():
                                  "value_without_poll": round(args.steps / dt_nopoll, 3) if dt_nopoll else None,
                                  "cost_pct": round((dt - dt_nopoll) / dt_nopoll * 100, 2) if dt_nopoll else None}
                                 if poll else {"per_step": False}),
+            "date_forcing": date_forcing,
             "last_window_safe": bool(safe),
             "finite": finite,
             "roofline": {
