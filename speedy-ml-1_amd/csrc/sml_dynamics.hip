@@ -1512,9 +1512,11 @@ __global__ __launch_bounds__(kGsThreads) void k_st_gridspec(
     if (tid < 128) {
         if (tid < kIX) {  // grid-point dynamics of column i -> F in B[i][f]
             const int i = tid;
+            SML_PST(8);
             double dummy[kKX];
             gridpoint_column(j, n1, [&](int f) { return f >= n1 ? A[i * kRowLd + f] * cj : A[i * kRowLd + f]; }, false,
                              dummy, dummy, dummy, dummy, [&](int f, double v) { B[i * kRowLd + f] = v; }, &gpt, false);
+            SML_PST(9);
             // the moist / diffusion part of column i's phypar
             const double *Ai = A + i * kRowLd;
             double ta[kKX], qa[kKX], ph[kKX];
@@ -1526,10 +1528,13 @@ __global__ __launch_bounds__(kGsThreads) void k_st_gridspec(
             }
             PhysThermo h;
             phys_thermo(ta, qa, ph, Ai[kPPs1], PTl, h);
+            SML_PST(10);
             double tt[kKX], qt[kKX], precnv, precls, ttv[kKX], qtv[kKX];
             int itop, icnv;
             phys_moist(h, PTl, tt, qt, precnv, precls, itop, icnv);
+            SML_PST(11);
             phys_vdif(h, ph, icnv, PTl, ttv, qtv);
+            SML_PST(12);
             double *Bh = B + i * kRowLd + kNFwd;
             // tt[0] is +0 always (convection and condensation leave the top level alone)
 #pragma unroll
@@ -1540,9 +1545,11 @@ __global__ __launch_bounds__(kGsThreads) void k_st_gridspec(
             for (int k = 0; k < kKX - 1; ++k) Bh[15 + k] = qt[k] + qtv[k];  // final above the surface layer
             Bh[22] = qt[kKX - 1];
             Bh[23] = qtv[kKX - 1];
+            SML_PST(13);
         }
     } else if (tid - 128 < kIX) {
         const int i = tid - 128, pt = j * kIX + i;
+        SML_PST(0);
         const double *Ai = A + i * kRowLd;
         double ua[kKX], va[kKX], ta[kKX], qa[kKX], ph[kKX];
 #pragma unroll
@@ -1563,10 +1570,13 @@ __global__ __launch_bounds__(kGsThreads) void k_st_gridspec(
         if (lradsw) {  // the shortwave first: its inputs are the moist part's (phys_column's order)
             PhysThermo h;
             phys_thermo(ta, qa, ph, ps1, PTl, h);
+            SML_PST(16);
             double tt[kKX], qt[kKX], precnv, precls;
             int itop, icnv;
             phys_moist(h, PTl, tt, qt, precnv, precls, itop, icnv);
+            SML_PST(17);
             phys_sw(pt, h, ph, precnv, precls, itop, bcv, rad, PTl, rc);
+            SML_PST(18);
             psg = h.psg;
             rl_rps = h.rps;
 #pragma unroll
@@ -1578,8 +1588,10 @@ __global__ __launch_bounds__(kGsThreads) void k_st_gridspec(
 #pragma unroll
             for (int k = 0; k < kKX; ++k) qc[k] = fmax(qa[k], 0.);
         }
+        SML_PST(1);
         phys_lw_sfc(pt, ua, va, ta, qc, ph, psg, rl_rps, bcv, rc, PTl, &PT->fband[0][0], fbk, rl_tt, rl_us, rl_vs,
                     rl_sh, rl_ev);
+        SML_PST(4);
         // the shortwave heating of the column for the sums after the barrier (from rc:
         // phys_sw's on a shortwave step, rad's otherwise)
 #pragma unroll
@@ -1588,8 +1600,10 @@ __global__ __launch_bounds__(kGsThreads) void k_st_gridspec(
         // (the products below kNFwdScaled are vdspec inputs: x cosgr(j) here, not in specx)
         gridpoint_products(n1, [&](int f) { return f >= n1 ? A[i * kRowLd + f] * cj : A[i * kRowLd + f]; },
                            [&](int f, double v) { B[i * kRowLd + f] = f < kNFwdScaled ? v * cj : v; }, &gpt);
+        SML_PST(5);
     }
     __syncthreads();
+    SML_PST(20);
     if (tid >= 128 && tid - 128 < kIX) {  // phys_column's sums (phy_phypar.f90:174-196)
         const int i = tid - 128;
         const double *Bh = B + i * kRowLd + kNFwd;
@@ -3249,6 +3263,15 @@ extern "C" int sml_dyn_step_host(sml_dynamics *d, int j1, int j2, double dt, dou
 
 // diagnostic: the phase stamps of the last fused launches ([4][96][8] wall_clock64
 // ticks, 100 MHz); not part of the ABI header
+#ifdef SML_PSTAMPS
+// the physics sub-phase stamps of the last row kernel (profiling build only)
+extern "C" int sml_dbg_pst(long long *out) {
+    SML_HIP(hipDeviceSynchronize());
+    SML_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pst), sizeof(long long) * kIL * 32, 0, hipMemcpyDeviceToHost));
+    return SML_OK;
+}
+#endif
+
 extern "C" int sml_dbg_dyn_stamps(sml_dynamics *d, long long *out) {
     SML_REQUIRE(d && out && d->d_dbg, "stamps not enabled (SML_DYN_STAMPS=1 at creation)");
     SML_HIP(hipDeviceSynchronize());

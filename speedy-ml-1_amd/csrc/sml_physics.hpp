@@ -117,6 +117,21 @@ __device__ inline const double *fband_row(const double *fb, double t) {
 }  // namespace phys
 
 #ifdef __HIPCC__
+// sub-phase stamps of the row kernel's physics, a profiling build only
+// (-DSML_PSTAMPS, tools/probe_pst.py): lane 0 of each wave records wall_clock64 at
+// slot s of its block (48 blocks x 32 slots); compiled out otherwise
+#ifdef SML_PSTAMPS
+static __device__ long long g_pst[kIL * 32];
+#define SML_PST(s)                                                                          \
+    do {                                                                                   \
+        if ((threadIdx.x & 63) == 0) g_pst[blockIdx.x * 32 + (s)] = wall_clock64();         \
+    } while (0)
+#else
+#define SML_PST(s) \
+    do {           \
+    } while (0)
+#endif
+
 // phypar's pieces (phy_phypar.f90:79-196), composed by phys_column in the
 // reference's order; k_st_gridspec also runs the moist / diffusion part and the
 // longwave / surface part of a column on different waves (sml_dynamics.hip).
@@ -562,6 +577,7 @@ __device__ inline void phys_lw_sfc(int j, const double *ua, const double *va, co
         fsfcd = fsfcd + corlw;
     }
     const double slrd = fsfcd;
+    SML_PST(2);
 
     // 3.3 suflux with lfluxland = .true. (phy_suflux.f90:1-355)
     double ustr3, vstr3, shf3, evap3, slru3, tsfc;
@@ -640,6 +656,7 @@ __device__ inline void phys_lw_sfc(int j, const double *ua, const double *va, co
         tsfc = tsea + fmask * (stl - tsea);
     }
 
+    SML_PST(3);
     // 3.4 radlw(1): upward longwave (phy_radiat.f90:414-458)
     {
         const double refsfc = 1. - emisfc, fsfcu = slru3;
