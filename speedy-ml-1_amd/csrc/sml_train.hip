@@ -45,6 +45,7 @@ constexpr int kTile = 128;  // C tile edge
 constexpr int kKC = 16;     // time steps per LDS stage
 constexpr int kLdsPad = 4;  // row padding (doubles) against bank conflicts
 constexpr int kStrip = 2;   // tile rows of the T S^T strip (nout <= 256)
+constexpr int kRhs = 144;   // right-hand sides of the solves: nout = 136 rounded up to the 16-wide MFMA tile
 constexpr int kPanel = 8;   // block columns per Cholesky panel (default): trailing-update depth 1024
 
 struct TrainRegion {
@@ -294,16 +295,25 @@ __global__ void k_train_regularise(double *__restrict__ G, double *__restrict__ 
     }
 }
 
-// solution X(j, o) (npad x nout per region) -> wout(nout, naug) column-major
-__global__ void k_train_wout(const double *__restrict__ X, const TrainRegion *__restrict__ regs, int npad, int nout,
-                             const long long *__restrict__ wout_off, double *__restrict__ wout) {
-    const int j = blockIdx.x * blockDim.x + threadIdx.x;
-    const int r = blockIdx.y;
+// solution X(j, o) (npad x nout per region) -> wout(nout, naug) column-major: a
+// transpose through LDS, 32 j per block -- read along j, write along o, both coalesced
+constexpr int kWoutJ = 32;
+__global__ __launch_bounds__(256) void k_train_wout(const double *__restrict__ X, const TrainRegion *__restrict__ regs,
+                                                    int npad, int nout, const long long *__restrict__ wout_off,
+                                                    double *__restrict__ wout) {
+    __shared__ double tile[kWoutJ][kRhs + 1];
+    const int j0 = blockIdx.x * kWoutJ, r = blockIdx.y, tid = threadIdx.x;
     const int naug = regs[r].naug;
-    if (j >= naug) return;
-    const double *x = X + (size_t)r * npad * nout + j;
-    double *w = wout + wout_off[r] + (size_t)j * nout;
-    for (int o = 0; o < nout; ++o) w[o] = x[(size_t)o * npad];
+    if (j0 >= naug) return;
+    const double *x = X + (size_t)r * npad * nout;
+    for (int idx = tid; idx < kWoutJ * nout; idx += 256) {
+        const int o = idx / kWoutJ, jj = idx % kWoutJ;
+        tile[jj][o] = j0 + jj < naug ? x[(size_t)o * npad + j0 + jj] : 0.0;
+    }
+    __syncthreads();
+    double *w = wout + wout_off[r] + (size_t)j0 * nout;
+    const int nj = min(kWoutJ, naug - j0);
+    for (int idx = tid; idx < nj * nout; idx += 256) w[idx] = tile[idx / nout][idx % nout];
 }
 
 // ------------------------------------------------------------ batched Cholesky
@@ -514,21 +524,22 @@ static int update_tiles(int C, int jlo, int jhi) {
     return n;
 }
 
-// One 128 x kRhs tile of the triangular solves (all right-hand sides at once, so a
-// block of L is read once per pass): 4 waves stacked by rows, each 32 rows x kRhs
-// columns = 2 x 9 MFMA tiles;
+// One 128 x NC tile of the triangular solves (NC = kRhs: all right-hand sides at
+// once, so a block of L is read once per pass; NC = kRhs / 3 for the latency-bound
+// in-panel launches, three blocks per tile row): 4 waves stacked by rows, each 32
+// rows x NC columns = 2 x NC / 16 MFMA tiles;
 //   O(r, c) = (accumulate ? O(r, c) : 0) + alpha * sum_{l < K} A(r, l) B(c, l)
 // A as TileLoader<128, AT>; B(c, l) at pb[c * ldb + l] (a row range of the
 // right-hand sides), columns c >= nb read as zero and are not stored.
-constexpr int kRhs = 144;  // nout = 136 rounded up to the 16-wide MFMA tile
-template <bool AT>
+template <bool AT, int NC>
 __device__ __forceinline__ void gemm_rhs(const double *__restrict__ pa, long long lda, const double *__restrict__ pb,
                                          long long ldb, int nb, double *po, long long ldo, double alpha,
                                          bool accumulate, int K = kTile) {
     using LA = TileLoader<kTile, AT>;
-    constexpr int NJ = kRhs / 16, PB = kRhs * kKC / 256;
+    constexpr int NJ = NC / 16, PB = NC * kKC / 256;
+    static_assert(NC % 16 == 0 && (NC * kKC) % 256 == 0, "column group");
     __shared__ double sA[kKC][kTile + kLdsPad];
-    __shared__ double sB[kKC][kRhs + kLdsPad];
+    __shared__ double sB[kKC][NC + kLdsPad];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, l16 = lane & 15, kk = lane >> 4;
     const int arow = LA::row(tid);
     double ra[LA::PER], rb[PB];
@@ -586,37 +597,39 @@ __device__ __forceinline__ void gemm_rhs(const double *__restrict__ pa, long lon
 }
 
 // Block k of the triangular solves on B (npad x nout per region, column-major), in
-// place (one block reads the whole block row it overwrites):
+// place (one block reads the whole block row it overwrites), right-hand sides
+// [NC z, NC (z + 1)) per block (every output column's sums are the same whichever
+// group computes it):
 //   forward  (upper = 0): B_k = L_kk^-1 B_k        backward (upper = 1): B_k = L_kk^-T B_k
-template <bool upper>  // one gemm_rhs instance per kernel: its LDS stages are static
+template <bool upper, int NC>  // one gemm_rhs instance per kernel: its LDS stages are static
 __global__ __launch_bounds__(256, 2) void k_solve_diag(const double *__restrict__ linv, double *__restrict__ B, int npad,
                                                     int nout, int k, const TrainRegion *__restrict__ regs) {
-    const int r = blockIdx.y, C = npad / kTile;
-    if (k >= live_blocks(regs, r)) return;  // B_k = 0 (padding rows), L_kk = I
+    const int r = blockIdx.y, C = npad / kTile, c0 = NC * blockIdx.z;
+    if (k >= live_blocks(regs, r) || c0 >= nout) return;  // B_k = 0 (padding rows), L_kk = I
     const double *Li = linv + ((size_t)r * C + k) * kTile * kTile;
-    double *Bk = B + (size_t)r * npad * nout + (size_t)k * kTile;
-    gemm_rhs<upper>(Li, kTile, Bk, npad, nout, Bk, npad, 1.0, false);
+    double *Bk = B + (size_t)r * npad * nout + (size_t)c0 * npad + (size_t)k * kTile;
+    gemm_rhs<upper, NC>(Li, kTile, Bk, npad, nout - c0, Bk, npad, 1.0, false);
 }
 
 // Update of block rows ilo <= i < ihi by the solved block rows [k0, k0 + kw), one
 // GEMM of depth 128 kw per block row:
 //   forward:  B_i -= sum_k L_ik Y_k        backward: B_i -= sum_k L_ki^T X_k
-template <bool upper>
+template <bool upper, int NC>
 __global__ __launch_bounds__(256, 2) void k_solve_update(const double *__restrict__ G, double *__restrict__ B, int npad,
                                                       int nout, int k0, int kw, int ilo,
                                                       const TrainRegion *__restrict__ regs) {
-    const int r = blockIdx.y, i = ilo + (int)blockIdx.x;
+    const int r = blockIdx.y, i = ilo + (int)blockIdx.x, c0 = NC * blockIdx.z;
     const int Cr = live_blocks(regs, r);
     // padding block rows stay 0; backward, solved rows k0.. past the data are 0
-    if (i >= Cr || (upper && k0 >= Cr)) return;
+    if (i >= Cr || (upper && k0 >= Cr) || c0 >= nout) return;
     const double *Gr = G + (size_t)r * npad * npad;
-    double *Br = B + (size_t)r * npad * nout;
+    double *Br = B + (size_t)r * npad * nout + (size_t)c0 * npad;
     if constexpr (upper)  // A(rr, l) = L(k0 kTile + l, i kTile + rr): the transposed blocks (k, i)
-        gemm_rhs<true>(Gr + (size_t)i * kTile * npad + (size_t)k0 * kTile, npad, Br + (size_t)k0 * kTile, npad, nout,
-                       Br + (size_t)i * kTile, npad, -1.0, true, kw * kTile);
+        gemm_rhs<true, NC>(Gr + (size_t)i * kTile * npad + (size_t)k0 * kTile, npad, Br + (size_t)k0 * kTile, npad,
+                           nout - c0, Br + (size_t)i * kTile, npad, -1.0, true, kw * kTile);
     else
-        gemm_rhs<false>(Gr + (size_t)k0 * kTile * npad + (size_t)i * kTile, npad, Br + (size_t)k0 * kTile, npad, nout,
-                        Br + (size_t)i * kTile, npad, -1.0, true, kw * kTile);
+        gemm_rhs<false, NC>(Gr + (size_t)k0 * kTile * npad + (size_t)i * kTile, npad, Br + (size_t)k0 * kTile, npad,
+                            nout - c0, Br + (size_t)i * kTile, npad, -1.0, true, kw * kTile);
 }
 
 }  // namespace
@@ -625,6 +638,8 @@ struct sml_train {
     int nlocal = 0, nout = 0, npad = 0, C = 0;
     int panel = kPanel;
     int gram = 2;  // k_train_gram2 (double-buffered LDS); SML_GRAM_V=1: k_train_gram
+    // the triangular solves' in-panel launches in three right-hand-side groups
+    bool rhs_split = true;
     std::vector<int> naug;
     TrainRegion *d_regs = nullptr;
     double *d_G = nullptr, *d_B = nullptr;
@@ -665,6 +680,7 @@ extern "C" int sml_train_create(int nlocal, const int *naug, int nout, sml_train
     t->nout = nout;
     if (const char *e = getenv("SML_CHOL_PANEL")) t->panel = std::max(1, atoi(e));  // tuning knob
     if (const char *e = getenv("SML_GRAM_V")) t->gram = atoi(e) == 1 ? 1 : 2;       // A/B knob
+    if (const char *e = getenv("SML_SOLVE_SPLIT")) t->rhs_split = *e != '0';        // A/B knob
     t->naug.assign(naug, naug + nlocal);
     int mx = 0;
     for (int i = 0; i < nlocal; ++i) {
@@ -778,34 +794,40 @@ extern "C" int sml_train_solve(sml_train *t, int ncs, double beta_res, double be
     // depth 128 -- a handful of tiles per region, latency-bound, so the shortest
     // chain); then the rows beyond the panel take the whole panel's update at depth
     // 128 P (MFMA-bound).
+    // the in-panel launches (diagonal blocks, one-block-deep updates) in three column
+    // groups of the right-hand sides (SML_SOLVE_SPLIT=0: one), the wide ones whole
+    const bool sp = t->rhs_split;
+    const dim3 g1(1, nl, sp ? 3 : 1);
     for (int p0 = 0; p0 < C; p0 += P) {  // L Y = B
         const int p1 = std::min(C, p0 + P);
         for (int k = p0; k < p1; ++k) {
-            hipLaunchKernelGGL(k_solve_diag<false>, dim3(1, nl), dim3(256), 0, st, t->d_linv, t->d_B, npad, nout, k,
-                               t->d_regs);
+            hipLaunchKernelGGL((sp ? k_solve_diag<false, kRhs / 3> : k_solve_diag<false, kRhs>), g1, dim3(256), 0, st,
+                               t->d_linv, t->d_B, npad, nout, k, t->d_regs);
             if (k + 1 < p1)
-                hipLaunchKernelGGL(k_solve_update<false>, dim3(p1 - 1 - k, nl), dim3(256), 0, st, t->d_G, t->d_B,
-                                   npad, nout, k, 1, k + 1, t->d_regs);
+                hipLaunchKernelGGL((sp ? k_solve_update<false, kRhs / 3> : k_solve_update<false, kRhs>),
+                                   dim3(p1 - 1 - k, nl, g1.z), dim3(256), 0, st, t->d_G, t->d_B, npad, nout, k, 1,
+                                   k + 1, t->d_regs);
         }
         if (p1 < C)
-            hipLaunchKernelGGL(k_solve_update<false>, dim3(C - p1, nl), dim3(256), 0, st, t->d_G, t->d_B, npad, nout,
-                               p0, p1 - p0, p1, t->d_regs);
+            hipLaunchKernelGGL((k_solve_update<false, kRhs>), dim3(C - p1, nl), dim3(256), 0, st, t->d_G, t->d_B, npad,
+                               nout, p0, p1 - p0, p1, t->d_regs);
     }
     for (int p1 = C; p1 > 0; p1 -= P) {  // L^T X = Y, panels from the bottom
         const int p0 = std::max(0, p1 - P);
         for (int k = p1 - 1; k >= p0; --k) {
-            hipLaunchKernelGGL(k_solve_diag<true>, dim3(1, nl), dim3(256), 0, st, t->d_linv, t->d_B, npad, nout, k,
-                               t->d_regs);
+            hipLaunchKernelGGL((sp ? k_solve_diag<true, kRhs / 3> : k_solve_diag<true, kRhs>), g1, dim3(256), 0, st,
+                               t->d_linv, t->d_B, npad, nout, k, t->d_regs);
             if (k > p0)
-                hipLaunchKernelGGL(k_solve_update<true>, dim3(k - p0, nl), dim3(256), 0, st, t->d_G, t->d_B, npad,
-                                   nout, k, 1, p0, t->d_regs);
+                hipLaunchKernelGGL((sp ? k_solve_update<true, kRhs / 3> : k_solve_update<true, kRhs>),
+                                   dim3(k - p0, nl, g1.z), dim3(256), 0, st, t->d_G, t->d_B, npad, nout, k, 1, p0,
+                                   t->d_regs);
         }
         if (p0 > 0)
-            hipLaunchKernelGGL(k_solve_update<true>, dim3(p0, nl), dim3(256), 0, st, t->d_G, t->d_B, npad, nout, p0,
-                               p1 - p0, 0, t->d_regs);
+            hipLaunchKernelGGL((k_solve_update<true, kRhs>), dim3(p0, nl), dim3(256), 0, st, t->d_G, t->d_B, npad, nout,
+                               p0, p1 - p0, 0, t->d_regs);
     }
     SML_HIP(hipGetLastError());
-    hipLaunchKernelGGL(k_train_wout, dim3((t->npad + 255) / 256, t->nlocal), dim3(256), 0, st, t->d_B, t->d_regs,
+    hipLaunchKernelGGL(k_train_wout, dim3(t->npad / kWoutJ, t->nlocal), dim3(256), 0, st, t->d_B, t->d_regs,
                        t->npad, t->nout, t->d_wout_off, d_wout);
     SML_HIP(hipGetLastError());
     if (info) SML_HIP(hipMemcpyAsync(info, t->d_info, t->nlocal * sizeof(int), hipMemcpyDeviceToHost, st));
