@@ -173,7 +173,21 @@ struct sml_dynamics {
         hipGraphExec_t exec = nullptr;
         double key[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         DynTables *tab[3] = {nullptr, nullptr, nullptr};
+        // run_model's exit captured behind the window (exit_graph): its arguments (the
+        // per-launch values come from d_xa, written by each run_model's k_io_entry)
+        bool has_exit = false;
+        const void *exit_key[10] = {};
     } wreplay[4];  // [prepared entry (sml_dyn_run_model)][entry lradsw]
+    // run_model's exit inside the window graph (SML_EXIT_GRAPH=0 at create: launched
+    // after it): saves the graph's exit boundary and two launches on the critical path
+    bool exit_graph = true;
+    // the next run_model's exit is followed by a store of exit_store_value to
+    // *exit_store (sml::dyn_run_model_exit_store: the hybrid loop's forecast hop)
+    uint64_t *exit_store = nullptr;
+    uint64_t exit_store_value = 0;
+    // a graph-captured exit's per-launch values: [0] the check count it waits for, [1]
+    // the hop value its store writes -- stored by the launch's k_io_entry
+    uint64_t *d_xa = nullptr;
     // while a run_model window is captured: the Fourier buffer its last k_st_spec fills
     // with iogrid(31)'s gridy (spectral layout), else null
     double *io_exit = nullptr;
@@ -1940,7 +1954,14 @@ __global__ __launch_bounds__(kSpecThreads) void k_io_entry(const double *__restr
                                                            const double *__restrict__ phis,
                                                            const double *__restrict__ tabm,
                                                            const double *__restrict__ pinv, double *__restrict__ varm,
-                                                           int n1, int nin) {
+                                                           int n1, int nin, uint64_t *__restrict__ xa, uint64_t xa0,
+                                                           uint64_t xa1) {
+    // a graph-captured exit's per-launch values (sml_dyn_run_model): ordered before the
+    // window graph by this kernel's end
+    if (xa && blockIdx.x == 0 && threadIdx.x == 0) {
+        xa[0] = xa0;
+        xa[1] = xa1;
+    }
     __shared__ double S[kNIo * kCW];  // specy output [f][2 n + p]
     __shared__ double Sst[kSM];       // this m's state slice
     __shared__ double In[kNInvMax * kCW];
@@ -2093,6 +2114,16 @@ __device__ inline double nmax(double a, double b) { return (a != a || b != b) ? 
 // cnt (may be null): the hand-off counter the run_model exit polls -- each block stores
 // its min / max sc1, drains its stores and adds 1 (MI355X_MICROARCH.md, inter-workgroup
 // visibility: an agent-scope atomic add per storing workgroup, sc1 stores and loads)
+// the hybrid loop's forecast hop behind run_model's exit: one relaxed agent-scope
+// vector store of the hop's sequence number, xa[1] (the exit's stores were released by
+// its kernel's end; as sml_hybrid's k_hop_signal)
+__global__ void k_flag_store_value(uint64_t *flag, uint64_t v) {
+    if (threadIdx.x == 0) __hip_atomic_store(flag, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__global__ void k_flag_store(uint64_t *flag, const uint64_t *xa) {
+    if (threadIdx.x == 0) __hip_atomic_store(flag, xa[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __global__ __launch_bounds__(1024) void k_io_minmax(const double *__restrict__ G, double *__restrict__ mm,
                                                      unsigned *__restrict__ cnt) {
     __shared__ double smin[16], smax[16];
@@ -2154,6 +2185,7 @@ extern "C" int sml_dyn_destroy(sml_dynamics *d) {
         if (r.exec) (void)hipGraphExecDestroy(r.exec);
     for (auto &r : d->wreplay)
         if (r.exec) (void)hipGraphExecDestroy(r.exec);
+    if (d->d_xa) (void)hipFree(d->d_xa);
     if (d->cap_stream) (void)hipStreamDestroy(d->cap_stream);
     if (d->chk_stream) {
         (void)hipStreamSynchronize(d->chk_stream);
@@ -2190,6 +2222,7 @@ extern "C" int sml_dyn_create(double radius, sml_dynamics **out) {
     if (const char *e = std::getenv("SML_DYN_NOGRAPH")) d->nograph = *e && *e != '0';
     if (const char *e = std::getenv("SML_DYN_WT")) d->wt = std::max(0, std::min(3, std::atoi(e)));
     if (const char *e = std::getenv("SML_CHK_FLAG")) d->chk_flag = *e != '0';
+    if (const char *e = std::getenv("SML_EXIT_GRAPH")) d->exit_graph = *e != '0';
     if (const char *e = std::getenv("SML_DYN_STAMPS"))
         if (*e && *e != '0' && (rc = dalloc(reinterpret_cast<double **>(&d->d_dbg), kStampKernels * kStampBlocks * kStamps))) {
             sml_dyn_destroy(d);
@@ -2520,8 +2553,17 @@ extern "C" int sml_dyn_leapfrog(sml_dynamics *d, int nsteps, double dt, double a
 // (entry lradsw, delt, alph, rob, wil, physics on, impint slots) and replayed with
 // a single launch, so the host thread never waits on the window's ~200 kernels.
 namespace {
+// run_model's exit as window_impl captures it behind the window: iogrid(31)'s gridx
+// (IoExit) and an optional one-lane store (the hybrid loop's forecast hop)
+struct ExitSpec {
+    const double *varm;
+    double *fc4, *fc2;
+    IoExit ex;
+    uint64_t *store;
+    uint64_t store_value;
+};
 int window_impl(sml_dynamics *d, int nleap, double delt, double alph, double rob, double wil, void *stream,
-                bool prepared);
+                bool prepared, const ExitSpec *exit = nullptr);
 }  // namespace
 
 extern "C" int sml_dyn_window(sml_dynamics *d, int nleap, double delt, double alph, double rob, double wil,
@@ -2535,7 +2577,7 @@ namespace {
 // (k_io_entry, fused path of sml_dyn_run_model), so the graph starts at the row
 // kernel of the first step
 int window_impl(sml_dynamics *d, int nleap, double delt, double alph, double rob, double wil, void *stream,
-                bool prepared) {
+                bool prepared, const ExitSpec *exit) {
     const double dts[3] = {0.5 * delt, delt, 2.0 * delt};
     DynTables *tab[3];
     for (int i = 0; i < 3; ++i) {  // 4 cached slots hold all three tables at once
@@ -2563,11 +2605,22 @@ int window_impl(sml_dynamics *d, int nleap, double delt, double alph, double rob
     sml_dynamics::WindowReplay &r = d->wreplay[(entry ? 1 : 0) + (prepared ? 2 : 0)];
     const double key[8] = {(double)nleap, delt,  alph, rob, wil, d->phys_on ? 1.0 : 0.0, d->fused ? 1.0 : 0.0,
                            prepared ? 2.0 : 1.0};
-    if (!(r.exec && std::memcmp(key, r.key, sizeof key) == 0 && std::memcmp(tab, r.tab, sizeof tab) == 0)) {
+    // the exit's fixed arguments (its count and the store's value change per launch)
+    const void *exit_key[10] = {};
+    if (exit) {
+        const void *k[10] = {exit->varm,   exit->fc4,     exit->fc2,    exit->ex.mm,
+                             exit->ex.in4, exit->ex.inlp, exit->ex.cnt, (const void *)(intptr_t)exit->ex.timeout,
+                             exit->store,  exit->ex.sig};
+        std::memcpy(exit_key, k, sizeof k);
+    }
+    const bool exit_same =
+        r.has_exit == (exit != nullptr) && (!exit || std::memcmp(exit_key, r.exit_key, sizeof exit_key) == 0);
+    if (!(r.exec && exit_same && std::memcmp(key, r.key, sizeof key) == 0 && std::memcmp(tab, r.tab, sizeof tab) == 0)) {
         if (r.exec) {
             SML_HIP(hipGraphExecDestroy(r.exec));
             r.exec = nullptr;
         }
+        r.has_exit = false;
         if (!d->cap_stream) SML_HIP(hipStreamCreateWithFlags(&d->cap_stream, hipStreamNonBlocking));
         hipGraph_t g = nullptr;
         SML_HIP(hipStreamBeginCapture(d->cap_stream, hipStreamCaptureModeThreadLocal));
@@ -2582,6 +2635,14 @@ int window_impl(sml_dynamics *d, int nleap, double delt, double alph, double rob
         for (int i = 0; i < nleap && !rc; ++i)
             rc = launch_step(d, 2, 2, dts[2], alph, rob, wil, nullptr, (1 + i) % kNstrad == 1, d->cap_stream, true,
                              i + 1 < nleap ? 2 : 0);
+        if (!rc && exit) {  // iogrid(31)'s gridx and the hop's store behind the window
+            rc = spectral_gridx_run_model_exit(d->sp, exit->varm, exit->fc4, exit->fc2, kNIoWind, exit->ex,
+                                               d->cap_stream);
+            if (!rc && exit->store) {
+                hipLaunchKernelGGL(k_flag_store, dim3(1), dim3(64), 0, d->cap_stream, exit->store, exit->ex.xa);
+                if (hipGetLastError() != hipSuccess) rc = fail(SML_ERR_HIP, "k_flag_store capture");
+            }
+        }
         hipError_t e = hipStreamEndCapture(d->cap_stream, &g);
         d->io_exit = nullptr;
         if (rc) {
@@ -2590,11 +2651,14 @@ int window_impl(sml_dynamics *d, int nleap, double delt, double alph, double rob
         }
         if (e != hipSuccess) return fail(SML_ERR_HIP, "sml_dyn_window capture: %s", hipGetErrorString(e));
         e = hipGraphInstantiate(&r.exec, g, nullptr, nullptr, 0);
-        (void)hipGraphDestroy(g);
         if (e != hipSuccess) {
+            (void)hipGraphDestroy(g);
             r.exec = nullptr;
             return fail(SML_ERR_HIP, "sml_dyn_window instantiate: %s", hipGetErrorString(e));
         }
+        (void)hipGraphDestroy(g);
+        r.has_exit = exit != nullptr;
+        std::memcpy(r.exit_key, exit_key, sizeof exit_key);
         std::memcpy(r.key, key, sizeof key);
         std::memcpy(r.tab, tab, sizeof tab);
     }
@@ -3091,12 +3155,35 @@ extern "C" int sml_dyn_run_model(sml_dynamics *d, const double *d_grid4d, const 
         const SpectralDev sd = spectral_dev(d->sp);
         const bool phys = d->phys_on;
         d->sm_cur = 0;  // the window's chain starts in buffer 0
+        // the exit inside the window graph: needs the check's counter hand-off (no event
+        // wait between the window and the exit; the check below counts whenever chk_flag
+        // is on) and the graph path.  Its per-launch values go through d_xa
+        hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+        SML_HIP(hipStreamIsCapturing(st, &cap));
+        const bool xg = d->exit_graph && !d->nograph && d->chk_flag && cap == hipStreamCaptureStatusNone;
+        if (xg && !d->d_xa) SML_HIP(hipMalloc(&d->d_xa, 2 * sizeof(uint64_t)));
         hipLaunchKernelGGL(k_io_entry, dim3(kMX), dim3(kSpecThreads), 0, st, d->d_vfm, d->d_pfl, sd.wt, d->d_state,
                            sm_buf(d, 0), d->d_chk, d->d_phis,
                            d->d_tabm + (size_t)(d->d_tab - d->d_tabs) * kMX * kTabMDoubles, sd.pinv, d->d_varm,
-                           phys ? kNInv1P : kNInv1, phys ? kNInvP : kNInv);
+                           phys ? kNInv1P : kNInv1, phys ? kNInvP : kNInv, xg ? d->d_xa : nullptr,
+                           (uint64_t)(4u * (d->chk_count + 1)), d->exit_store_value);
         SML_HIP(hipGetLastError());
         if (int rc = launch_io_check(d, st, nullptr)) return rc;
+        if (xg) {
+            if (!(d->chk_pending && d->chk_counted))
+                return fail(SML_ERR_STATE, "sml_dyn_run_model: the safety check did not take the counter hand-off");
+            ExitSpec es{d->d_varm, d_fc4d, d_fc2d, IoExit{0.000001, d->mm_last, d_grid4d, d_logp}, d->exit_store,
+                        0};
+            es.ex.cnt = d->d_chk_cnt;
+            es.ex.xa = d->d_xa;
+            es.ex.sig = d->exit_sig;  // the forecast hop from the exit's blocks (sml::dyn_run_model_signal)
+            d->exit_sig = nullptr;    // one launch
+            es.ex.late = d->d_chk_late;
+            es.ex.timeout = d->chk_timeout;
+            d->chk_pending = false;
+            d->exit_store = nullptr;  // one launch
+            return window_impl(d, nleap, delt, alph, rob, wil, stream, true, &es);
+        }
         if (int rc = window_impl(d, nleap, delt, alph, rob, wil, stream, true)) return rc;
     } else {
         if (int rc = sml_dyn_from_grid(d, d_grid4d, d_logp, nullptr, stream)) return rc;
@@ -3125,7 +3212,13 @@ extern "C" int sml_dyn_run_model(sml_dynamics *d, const double *d_grid4d, const 
         SML_HIP(hipGetLastError());
         if (int rc = spectral_gridy(d->sp, d->d_specin, d->d_varm, kNIo, st)) return rc;
     }
-    return spectral_gridx_run_model_exit(d->sp, d->d_varm, d_fc4d, d_fc2d, kNIoWind, ex, st);
+    if (int rc = spectral_gridx_run_model_exit(d->sp, d->d_varm, d_fc4d, d_fc2d, kNIoWind, ex, st)) return rc;
+    if (d->exit_store) {
+        hipLaunchKernelGGL(k_flag_store_value, dim3(1), dim3(64), 0, st, d->exit_store, d->exit_store_value);
+        SML_HIP(hipGetLastError());
+        d->exit_store = nullptr;  // one launch
+    }
+    return SML_OK;
 }
 
 extern "C" int sml_dyn_set_check_cus(sml_dynamics *d, int first_cu, int num_cus) {
@@ -3202,6 +3295,15 @@ int sml::dyn_run_model_entry_signal(sml_dynamics *d, uint64_t *counter, int *add
     SML_REQUIRE(d && counter && adds, "null argument");
     d->entry_sig = counter;
     *adds = spectral_specx_io_blocks();
+    return SML_OK;
+}
+
+// the next run_model's exit is followed (on its stream, inside the window graph when the
+// exit is captured there) by a one-lane store of value to *flag
+int sml::dyn_run_model_exit_store(sml_dynamics *d, uint64_t *flag, uint64_t value) {
+    SML_REQUIRE(d && flag, "null argument");
+    d->exit_store = flag;
+    d->exit_store_value = value;
     return SML_OK;
 }
 

@@ -1154,6 +1154,7 @@ extern "C" int sml_hybrid_advance(sml_hybrid *h, const double *d_outvec_all) {
     h->assembled = false;
     if (!done)
         if (int rc = sml_exchange_assemble(h->res, d_outvec_all, h->g4, h->g2, h->pr, c)) return rc;
+    const bool sst_new = h->slab.res && h->slab.dirty;  // a new hybrid SST reaches sst_am this step
     if (int rc = slab_sst(h, d_outvec_all, c)) return rc;
     if (h->cal_on) {
         // run_model's date for this step (mpires.f90:1545, timestep = t + 1; before the
@@ -1164,7 +1165,9 @@ extern "C" int sml_hybrid_advance(sml_hybrid *h, const double *d_outvec_all) {
         if (int rc = sml_calendar_delta_hour(h->tisr_startyear, h->tisr_base + (h->t + 1) * h->tisr_step_hours,
                                              &h->tisr_feb29, date))
             return rc;
-        if (int rc = sml_dyn_fordate(h->dyn, date[0], date[1], date[2], c)) return rc;
+        // on SPEEDY's stream, behind the previous window and beside the finish / assembly,
+        // unless this step's new SST (written on c) must reach qcorh first
+        if (int rc = sml_dyn_fordate(h->dyn, date[0], date[1], date[2], sst_new ? c : s)) return rc;
     }
     // chain on SPEEDY's stream with kernel hops: the next run_model's entry specx signals
     // the assembled grid as it starts (no signal kernel in front of the window); run_model
@@ -1220,13 +1223,20 @@ extern "C" int sml_hybrid_advance(sml_hybrid *h, const double *d_outvec_all) {
         if (int rc = sml::dyn_run_model_signal(h->dyn, h->d_seq + sml_hybrid::kHopLm * sml_hybrid::kSeqStride,
                                                &exit_adds))
             return rc;
+    // kernel hops: the forecast's signal is a store that run_model issues right behind
+    // its exit (inside the window graph when the exit is captured there)
+    const bool exit_store = hops && h->use_kernels && exit_adds == 0;
+    if (exit_store)
+        if (int rc = sml::dyn_run_model_exit_store(h->dyn, h->d_seq + sml_hybrid::kHopLm * sml_hybrid::kSeqStride,
+                                                   ++h->seq[sml_hybrid::kHopLm]))
+            return rc;
     if (!entry_sig)
         if (int rc = sml_dyn_run_model(h->dyn, h->g4, h->g2, h->nleap, h->delt, h->alph, h->rob, h->wil, h->f4, h->f2,
                                        s))
             return rc;
     if (exit_adds > 0) {  // the exit's blocks each add 1 to the hop's word once released
         h->seq[sml_hybrid::kHopLm] += (uint64_t)exit_adds;
-    } else if (hops) {
+    } else if (hops && !exit_store) {
         if (int rc = hop_signal(h, sml_hybrid::kHopLm, s)) return rc;
     } else if (!h->overlap && h->ncs) {
         if (int rc = sml_res_tile_local_model(h->res, h->f4, h->f2, h->lm, s)) return rc;

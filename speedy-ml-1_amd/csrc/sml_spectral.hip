@@ -209,7 +209,8 @@ __global__ __launch_bounds__(kFftThreads) void k_gridx(const double *__restrict_
         if (threadIdx.x == 0) {
             gave_up = 0;
             const long long t0 = wall_clock64();
-            while (__hip_atomic_load(ex.cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < ex.target) {
+            const unsigned target = ex.xa ? (unsigned)ex.xa[0] : ex.target;
+            while (__hip_atomic_load(ex.cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
                 __builtin_amdgcn_s_sleep(2);
                 if (wall_clock64() - t0 > ex.timeout) {  // never hang the queue
                     __hip_atomic_store(ex.late, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);

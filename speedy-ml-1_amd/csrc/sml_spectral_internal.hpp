@@ -75,6 +75,9 @@ struct IoExit {
     // its stores drained and released at agent scope, adds 1 (spectral_exit_blocks()
     // adds per launch) -- the consumer polls *sig >= its count
     uint64_t *sig = nullptr;
+    // the count to wait for, from device memory instead of `target` (xa[0], written by
+    // this run_model's k_io_entry): an exit replayed inside a graph keeps its arguments
+    const uint64_t *xa = nullptr;
 };
 int spectral_exit_blocks();
 int spectral_gridx_run_model_exit(sml_spectral *s, const double *varm, double *g4, double *logp, int nwind,
