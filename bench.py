@@ -493,7 +493,8 @@ def main():
                         "run_model's get_current_time_delta_hour gives it (mpires.f90:1545)",
             "recomputed_windows": n_ford, "timed_windows": steps_done,
             "note": "recomputed when the date (once a day: every 4th step) or the slab's hybrid SST changed; "
-                    "on the reservoir stream before the grid hop, i.e. on the critical path of those steps",
+                    "on SPEEDY's stream behind the previous window (beside the finish and assembly), or, on a "
+                    "step with a new hybrid SST, behind that SST on the reservoir stream before the grid hop",
             "recompute_ms": round(f_ms, 4),
             "per_step_ms": round(f_ms * n_ford / max(steps_done, 1), 4)}
     dyn.close()
