@@ -196,6 +196,10 @@ __global__ __launch_bounds__(256, 2) void k_train_gram2(const double *__restrict
     // stages and skips its MFMAs, leaving the SIMD to the other block's waves
     const bool wlive = (bi * kTile + wr * 64 < (strip ? nout : naug)) && (bj * kTile + wc * 64 < naug) &&
                        !(!strip && bi == bj && wr < wc);
+    // and inside a live wave, its 16-row / 16-column MFMA tiles past naug / nout
+    const int ni = min(4, max(0, ((strip ? nout : naug) - bi * kTile - wr * 64 + 15) / 16));
+    const int nj = min(4, max(0, (naug - bj * kTile - wc * 64 + 15) / 16));
+    const bool full = ni == 4 && nj == 4;
     const int lrow = tid & (kTile - 1), lt0 = tid >> 7;
     const int arow = bi * kTile + lrow;
     const int brow = bj * kTile + lrow;
@@ -239,10 +243,18 @@ __global__ __launch_bounds__(256, 2) void k_train_gram2(const double *__restrict
                 for (int i = 0; i < 4; ++i) a[i] = sA[cur][4 * s + kk][wr * 64 + i * 16 + l16];
 #pragma unroll
                 for (int j = 0; j < 4; ++j) b[j] = sB[cur][4 * s + kk][wc * 64 + j * 16 + l16];
+                if (full) {
 #pragma unroll
-                for (int i = 0; i < 4; ++i)
+                    for (int i = 0; i < 4; ++i)
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) acc[i][j] = MFMA64(a[i], b[j], acc[i][j]);
+                        for (int j = 0; j < 4; ++j) acc[i][j] = MFMA64(a[i], b[j], acc[i][j]);
+                } else {  // a tile at a region's edge
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+#pragma unroll
+                        for (int j = 0; j < 4; ++j)
+                            if (i < ni && j < nj) acc[i][j] = MFMA64(a[i], b[j], acc[i][j]);
+                }
             }
         }
         if (t0 + kKC < m) {
@@ -490,7 +502,7 @@ __global__ __launch_bounds__(kDiagThreads) void k_chol_diag(double *__restrict__
 
 // L_ik = A_ik L_kk^-T for the blocks i > k below the diagonal, in place: a block
 // owns 64 rows x all 128 columns (it reads the whole rows it overwrites)
-__global__ __launch_bounds__(256) void k_chol_panel(double *__restrict__ G, const double *__restrict__ linv, int npad,
+__global__ __launch_bounds__(256, 3) void k_chol_panel(double *__restrict__ G, const double *__restrict__ linv, int npad,
                                                     int k, const TrainRegion *__restrict__ regs) {
     const int r = blockIdx.y, C = npad / kTile, i = k + 1 + (blockIdx.x >> 1), r0 = (blockIdx.x & 1) * 64;
     if (i >= live_blocks(regs, r)) return;  // A_ik = 0: L_ik = 0
