@@ -38,6 +38,7 @@
 #include "sml_fft.hpp"
 #include "sml_fft_wa96.hpp"
 #include "sml_physics.hpp"
+#include "sml_physics_quad.hpp"
 #include "sml_spectral_internal.hpp"
 
 using namespace sml;
@@ -151,6 +152,10 @@ struct sml_dynamics {
     bool fused = true;
     // with GPU physics: k_st_grid + k_st_specx instead of k_st_gridspec (SML_DYN_SPLIT_GRID=1)
     bool split_grid = false;
+    // the row kernel's phypar on four lanes per column (k_st_gridspec_q, SML_DYN_QUAD=1:
+    // bitwise the default, measured slower); default: one lane per column
+    // split over two wave pairs (k_st_gridspec)
+    bool quad = false;
     bool nograph = false;  // SML_DYN_NOGRAPH=1: the window's launches issued directly, not replayed
     // the fused step's hand-offs (vfm, varm, the m-major state) stored write-through
     // (store2): SML_DYN_WT=1 both step kernels, 2 the row kernel's (vfm) only, 3 the
@@ -1666,6 +1671,143 @@ __global__ __launch_bounds__(kGsThreads) void k_st_gridspec(
     stamp(dbg, 0, 3);
 }
 
+// The row kernel with phypar on four lanes per column (sml_physics_quad.hpp; opt-in,
+// SML_DYN_QUAD=1): 8 waves, two per SIMD.  gridx as in
+// k_st_gridspec (lane pairs, waves 0-2); then waves 0-1 run the row's grid-point
+// dynamics and products (one column per thread) beside waves 2-7, whose 384 lanes are
+// 96 quads running phypar level- and band-parallel; each quad then adds its column's
+// tendencies into F (phys_column's sums, one level pair per lane); specx as before.
+// phypar's non-transform inputs (boundary fields, a longwave-only step's radiation
+// state) are loaded by the quads at the start, under gridx.
+constexpr int kGqThreads = 512;
+static_assert(kGqThreads - 128 == 4 * kIX, "one quad per column on waves 2-7");
+template <bool kWT>
+__global__ __launch_bounds__(kGqThreads) void k_st_gridspec_q(
+    const double *__restrict__ varm, double *__restrict__ vfm, const double *__restrict__ wa,
+    const double *__restrict__ cosgr, const DynTables *__restrict__ T, const double *__restrict__ bc,
+    double *__restrict__ rad, const PhysTables *__restrict__ PT, int lradsw, int wt, long long *dbg) {
+    __shared__ double A[kFftN * kRowLd], B[kFftN * kRowLd];
+    const double *was = kFftWa96;
+    (void)wa;
+    constexpr int kPtS = (int)(offsetof(PhysTables, fband) / sizeof(double)), kGpS = (int)(sizeof(GpTab) / 8);
+    static_assert(kPtS + kGpS <= kGqThreads, "table staging: one value per thread");
+    static_assert(kRowLd - kNFwd >= 24 && kRowLd - 1 >= 86, "quad slots in B's and A's spare columns");
+    static_assert(kPT1 == 32 && kPPs1 == 56 && kNInv1P + 2 * kKX + 2 == 75 && kNInvP <= 91,
+                  "quad::lw_slot: A's columns 32..56 and 75..96 are phypar's inputs and spare");
+    __shared__ double ptl[kPtS];
+    __shared__ GpTab gpt;
+    __shared__ QuadK qk;
+    __shared__ double fsr[4 * kIX];  // radlw(1)'s surface row per (column, band), quad_fsr
+    constexpr int n1 = kNInv1P;
+    constexpr int nphys = (n1 - kPT1) + (kNInvP - (n1 + 2 * kKX + 2));  // 25 + 16 = 41
+    const int j = blockIdx.x, tid = threadIdx.x;
+    const bool isq = tid >= 128;
+    const int qi = isq ? (tid - 128) >> 2 : 0, qq = tid & 3, qpt = j * kIX + qi;
+    stamp(dbg, 0, 0);
+    double rtab = 0.0;
+    if (tid < kPtS) {
+        rtab = reinterpret_cast<const double *>(PT)[tid];
+    } else if (tid < kPtS + kGpS) {
+        const int e = tid - kPtS, k = e % kKX;
+        const int w = e / kKX;
+        rtab = w == 0 ? T->dhs[k] : w == 1 ? T->dhsr[k] : w == 2 ? T->fsgr[k] : w == 3 ? T->tref[k]
+             : w == 4 ? T->tref3[k] : T->coriol[e - 5 * kKX];
+    }
+    {
+        const int t = tid >> 1, h = tid & 1;
+        const bool act = t < kNInv + nphys;
+        const int f = t < kNInv ? (t < kNInv1 ? t : n1 + (t - kNInv1))
+                                : (t - kNInv < n1 - kPT1 ? kPT1 + (t - kNInv)
+                                                         : n1 + 2 * kKX + 2 + (t - kNInv - (n1 - kPT1)));
+        double xi[kMX2 - 1];
+        if (act) row_gridx_load(varm, f, j, xi);
+        if (tid < kPtS) ptl[tid] = rtab;
+        else if (tid < kPtS + kGpS) reinterpret_cast<double *>(&gpt)[tid - kPtS] = rtab;
+        __syncthreads();
+        if (act) row_gridx_half(A, xi, was, f, false, 1.0, h);
+        // the quads' surface rows (two dependent loads) and per-block constants, by the
+        // lanes gridx leaves idle
+        for (int e = tid - 192; e >= 0 && e < 4 * kIX; e += kGqThreads - 192)
+            fsr[e] = quad_fsr(bc, &PT->fband[0][0], j * kIX + (e >> 2), e & 3);
+        if (tid == kGqThreads - 1) {
+            const PhysTables *PTl = reinterpret_cast<const PhysTables *>(ptl);
+            phys_entr(PTl, qk.entr);
+            phys_vdif_consts(PTl, qk.vk);
+        }
+    }
+    __syncthreads();
+    stamp(dbg, 0, 1);
+    const PhysTables *PTl = reinterpret_cast<const PhysTables *>(ptl);  // (fband stays in PT)
+    const double cj = cosgr[j];
+    QuadOut qo;
+    SML_PST_T(21, 128);
+    SML_PST_T(8, 0);
+    if (tid < kIX) {  // grid-point dynamics of column i -> F in B[i][f], then its products
+        const int i = tid;
+        auto g = [&](int f) { return f >= n1 ? A[i * kRowLd + f] * cj : A[i * kRowLd + f]; };
+        double dummy[kKX];
+        gridpoint_column(j, n1, g, false, dummy, dummy, dummy, dummy, [&](int f, double v) { B[i * kRowLd + f] = v; },
+                         &gpt, false);
+        // (the products below kNFwdScaled are vdspec inputs: x cosgr(j) here, not in specx)
+        gridpoint_products(n1, g, [&](int f, double v) { B[i * kRowLd + f] = f < kNFwdScaled ? v * cj : v; }, &gpt);
+        SML_PST_T(9, 0);
+    } else if (isq) {
+        // a longwave-only step's radiation state (loaded here, not under gridx: held
+        // across it, it pushed the gridx lanes' registers into scratch)
+        QuadPre pre;
+        {
+            if (!lradsw) {
+#pragma unroll
+                for (int k = 0; k < kKX; ++k) pre.tau[k] = rad[kRadTau2 + ((size_t)qq * kKX + k) * kNGP + qpt];
+                pre.strat0 = rad[kRadStratc + qpt];
+                pre.strat1 = rad[kRadStratc + kNGP + qpt];
+                pre.ssrd = rad[kRadSsrd + qpt];
+#pragma unroll
+                for (int s = 0; s < 2; ++s) pre.ttrsw[s] = rad[kRadTtRsw + (size_t)(2 * qq + s) * kNGP + qpt];
+            }
+        }
+        double *Ai = A + qi * kRowLd;
+        const double u7 = Ai[n1 + 2 * kKX + 2 + kKX - 1] * cj, v7 = Ai[n1 + 3 * kKX + 2 + kKX - 1] * cj;
+        phys_quad<kPT1, kPQ1, kPPhi1, kPPs1>(qq, qpt, j, Ai, B + qi * kRowLd + kNFwd, u7, v7, pre, bc, rad, PTl, &qk, &PT->fband[0][0],
+                  fsr[tid - 128], lradsw != 0, qo);
+        SML_PST_T(29, 128);
+    }
+    __syncthreads();
+    SML_PST_T(20, 128);
+    if (isq) {  // phys_column's sums (phy_phypar.f90:174-196) into F, the quad lane's two levels
+        double *Bi = B + qi * kRowLd;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const int k = 2 * qq + s;
+            const double ttk = qo.ttm[s] + qo.rsw[s] + qo.rlw[s];
+            const double utv = k == kKX - 1 ? qo.utv7 : 0., vtv = k == kKX - 1 ? qo.vtv7 : 0.;
+            // F + P where grtend adds phypar's tendencies (u 0..7, v 24..31, t 56..63, q 64..71)
+            Bi[k] = (Bi[k] + (0. + utv)) * cj;  // (x cosgr(j): a vdspec input, scaled here for specx)
+            Bi[3 * kKX + k] = (Bi[3 * kKX + k] + (0. + vtv)) * cj;
+            Bi[7 * kKX + k] = Bi[7 * kKX + k] + (ttk + qo.ttv[s]);
+            Bi[8 * kKX + k] = Bi[8 * kKX + k] + qo.qtk[s];
+        }
+    }
+    __syncthreads();
+    stamp(dbg, 0, 2);
+    // specx: transform f on lanes 2 f, 2 f + 1, lane h on the samples 2 i + h
+    {
+        const int f = tid >> 1, h = tid & 1;
+        const bool act = f < kNFwd;
+        double x[48];
+        if (act) {
+            const double *fr = B + f + h * kRowLd;
+#pragma unroll
+            for (int i = 0; i < 48; ++i) x[i] = fr[2 * i * kRowLd];
+            fft::rfftf48_reg(x, was);
+        }
+        __syncthreads();  // A's P columns are read: A becomes the pairs' meeting place
+        row_specx_pair(x, A, act, vfm, was, f, j, h, kWT);
+        (void)wt;
+    }
+    stamp(dbg, 0, 3);
+}
+
 // specy's MFMA B operands in lane order: lane l = 16 kk + r of k-step s takes
 // pfwd[m][n][j] at n = 2 r (S) and 2 r + 1 (D), j = 4 s + kk ([m][n 32][lat 24], the
 // spectral context's forward Legendre table) -> pfl[m][s][l][2]
@@ -2219,6 +2361,7 @@ extern "C" int sml_dyn_create(double radius, sml_dynamics **out) {
     build_phys_tables(d->tab, &d->ptab);
     if (const char *e = std::getenv("SML_DYN_FUSED")) d->fused = *e && *e != '0';
     if (const char *e = std::getenv("SML_DYN_SPLIT_GRID")) d->split_grid = *e && *e != '0';
+    if (const char *e = std::getenv("SML_DYN_QUAD")) d->quad = *e && *e != '0';
     if (const char *e = std::getenv("SML_DYN_NOGRAPH")) d->nograph = *e && *e != '0';
     if (const char *e = std::getenv("SML_DYN_WT")) d->wt = std::max(0, std::min(3, std::atoi(e)));
     if (const char *e = std::getenv("SML_CHK_FLAG")) d->chk_flag = *e != '0';
@@ -2449,8 +2592,14 @@ int launch_step_fused(sml_dynamics *d, int j1, int j2, double dt, double alph, d
                                sd.wa, sd.cosgr, d->d_dbg);
         } else {
             const bool wrow = d->wt == 1 || d->wt == 2;
-            hipLaunchKernelGGL(wrow ? k_st_gridspec<true> : k_st_gridspec<false>, dim3(kIL), dim3(kGsThreads), 0, st, d->d_varm, d->d_vfm, sd.wa, sd.cosgr,
-                               T, d->d_pbc, d->d_rad, d->d_ptab, lradsw ? 1 : 0, wrow ? 1 : 0, d->d_dbg);
+            if (d->quad)
+                hipLaunchKernelGGL(wrow ? k_st_gridspec_q<true> : k_st_gridspec_q<false>, dim3(kIL), dim3(kGqThreads), 0,
+                                   st, d->d_varm, d->d_vfm, sd.wa, sd.cosgr, T, d->d_pbc, d->d_rad, d->d_ptab,
+                                   lradsw ? 1 : 0, wrow ? 1 : 0, d->d_dbg);
+            else
+                hipLaunchKernelGGL(wrow ? k_st_gridspec<true> : k_st_gridspec<false>, dim3(kIL), dim3(kGsThreads), 0, st,
+                                   d->d_varm, d->d_vfm, sd.wa, sd.cosgr, T, d->d_pbc, d->d_rad, d->d_ptab,
+                                   lradsw ? 1 : 0, wrow ? 1 : 0, d->d_dbg);
         }
         SML_HIP(hipGetLastError());
     } else {

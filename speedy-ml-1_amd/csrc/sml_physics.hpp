@@ -126,9 +126,17 @@ static __device__ long long g_pst[kIL * 32];
     do {                                                                                   \
         if ((threadIdx.x & 63) == 0) g_pst[blockIdx.x * 32 + (s)] = wall_clock64();         \
     } while (0)
+// the same from one given thread (the quad row kernel's waves share roles)
+#define SML_PST_T(s, t)                                                                     \
+    do {                                                                                   \
+        if (threadIdx.x == (t)) g_pst[blockIdx.x * 32 + (s)] = wall_clock64();              \
+    } while (0)
 #else
 #define SML_PST(s) \
     do {           \
+    } while (0)
+#define SML_PST_T(s, t) \
+    do {                \
     } while (0)
 #endif
 
@@ -159,19 +167,34 @@ __device__ inline void phys_thermo(const double *ta, const double *qa_in, const 
     }
 }
 
-// 2.1 convmf + 2.2 lscond: tt, qt = 0 + the convection + the condensation tendencies
-// (phy_phypar.f90:96-119); precnv, precls and the cloud top (itop) for the
-// shortwave, icnv for vdifsc
-__device__ inline void phys_moist(const PhysThermo &h, const PhysTables *P, double *tt, double *qt, double &precnv_o,
-                                  double &precls_o, int &itop_o, int &icnv_o) {
+// convmf's entrainment profile (phy_convmf.f90:52-60): entr(k), k = 2..nlev-1
+// (1-based), normalised to entmax; a function of the sigma levels only
+__device__ inline void phys_entr(const PhysTables *P, double (&entr)[kKX + 1]) {
     using namespace phys;
-    constexpr int NL = kKX, nl1 = kKX - 1;  // nl1: 1-based index of the level above the bottom
-    (void)nl1;
-    const double psg = h.psg, rps = h.rps;
-    const double *qa = h.qa, *se = h.se, *rh = h.rh, *qsat = h.qsat;
-    (void)psg; (void)rps; (void)qa; (void)se; (void)rh; (void)qsat;
-    // 2.1 convmf (phy_convmf.f90:22-238); 1-based level indices as the reference
-    double tt_cnv[NL], qt_cnv[NL];
+    constexpr int nl1 = kKX - 1;
+#pragma unroll
+    for (int k = 0; k <= kKX; ++k) entr[k] = 0.;
+    double sentr = 0.;
+#pragma unroll
+    for (int k = 2; k <= nl1; ++k) {
+        const double e = fmax(0., P->sig[k - 1] - 0.5);
+        entr[k] = e * e;
+        sentr = sentr + entr[k];
+    }
+    sentr = entmax / sentr;
+#pragma unroll
+    for (int k = 2; k <= nl1; ++k) entr[k] = entr[k] * sentr;
+}
+
+// 2.1 convmf (phy_convmf.f90:22-238), 1-based level indices as the reference: the
+// unscaled fluxes dfse / dfqa of every level into tt_cnv / qt_cnv (level k at k - 1),
+// the convective precipitation and the cloud top itop (nlev + 1: no convection)
+__device__ inline void phys_convmf(const PhysThermo &h, const PhysTables *P, const double *entr, double *tt_cnv,
+                                   double *qt_cnv, double &precnv_o, int &itop_o) {
+    using namespace phys;
+    constexpr int NL = kKX, nl1 = kKX - 1;
+    const double psg = h.psg;
+    const double *qa = h.qa, *se = h.se, *qsat = h.qsat;
 #pragma unroll
     for (int k = 0; k < NL; ++k) tt_cnv[k] = qt_cnv[k] = 0.;
     double cbmf = 0., precnv = 0.;
@@ -179,19 +202,9 @@ __device__ inline void phys_moist(const PhysThermo &h, const PhysTables *P, doub
     {
         constexpr int nlev = NL, nlp = NL + 1;
         const double fqmax = 5., fm0 = p0 * P->dsig[nlev - 1] / (gg * trcnv * 3600), rdps = 2. / (1. - psmin);
-        double mss[NL + 1], entr[NL + 1];
-        double sentr = 0.;
+        double mss[NL + 1];
 #pragma unroll
         for (int k = 2; k <= nlev; ++k) mss[k] = se[k - 1] + alhc * qsat[k - 1];
-#pragma unroll
-        for (int k = 2; k <= nl1; ++k) {
-            const double e = fmax(0., P->sig[k - 1] - 0.5);
-            entr[k] = e * e;
-            sentr = sentr + entr[k];
-        }
-        sentr = entmax / sentr;
-#pragma unroll
-        for (int k = 2; k <= nl1; ++k) entr[k] = entr[k] * sentr;
         const double rlhc = 1. / alhc;
         double qdif = 0., msthr = 0.;
         itop = nlp;
@@ -277,6 +290,24 @@ __device__ inline void phys_moist(const PhysThermo &h, const PhysTables *P, doub
             }
         }
     }
+    precnv_o = precnv;
+    itop_o = itop;
+}
+
+// 2.1 convmf + 2.2 lscond: tt, qt = 0 + the convection + the condensation tendencies
+// (phy_phypar.f90:96-119); precnv, precls and the cloud top (itop) for the
+// shortwave, icnv for vdifsc
+__device__ inline void phys_moist(const PhysThermo &h, const PhysTables *P, double *tt, double *qt, double &precnv_o,
+                                  double &precls_o, int &itop_o, int &icnv_o) {
+    using namespace phys;
+    constexpr int NL = kKX;
+    const double psg = h.psg, rps = h.rps;
+    const double *qa = h.qa, *qsat = h.qsat;
+    double entr[kKX + 1];
+    phys_entr(P, entr);
+    double tt_cnv[NL], qt_cnv[NL], precnv;
+    int itop;
+    phys_convmf(h, P, entr, tt_cnv, qt_cnv, precnv, itop);
 #pragma unroll
     for (int k = 1; k < NL; ++k) {  // phy_phypar.f90:100-105, k = 2..nlev
         tt_cnv[k] = tt_cnv[k] * rps * P->grdscp[k];
@@ -697,30 +728,44 @@ __device__ inline void phys_lw_sfc(int j, const double *ua, const double *va, co
     evap3_o = evap3;
 }
 
+// vdifsc's constants (phy_vdifsc.f90:36-57): functions of the sigma levels only
+struct VdifK {
+    double fshcq, fshcse, fvdiq, fvdise;
+    double rsig[kKX], rsig1[kKX];  // rsig1(k), k = 1..nlev-1 (rsig1[kKX - 1] unused)
+};
+__device__ inline void phys_vdif_consts(const PhysTables *P, VdifK &v) {
+    using namespace phys;
+    constexpr int NL = kKX, nl1 = kKX - 1, nlev = NL;
+    const double cshc = P->dsig[nlev - 1] / 3600., cvdi = (P->sigh[nl1] - P->sigh[1]) / ((nl1 - 1) * 3600.);
+    v.fshcq = cshc / trshc;
+    v.fshcse = cshc / (trshc * cp);
+    v.fvdiq = cvdi / trvdi;
+    v.fvdise = cvdi / (trvds * cp);
+#pragma unroll
+    for (int k = 1; k <= nl1; ++k) {
+        v.rsig[k - 1] = 1. / P->dsig[k - 1];
+        v.rsig1[k - 1] = 1. / (1. - P->sigh[k]);
+    }
+    v.rsig[nlev - 1] = 1. / P->dsig[nlev - 1];
+    v.rsig1[nlev - 1] = 0.;
+}
+
 // 4.1 vdifsc (phy_vdifsc.f90:17-124): ttv, qtv (utv = vtv = 0 here)
 __device__ inline void phys_vdif(const PhysThermo &h, const double *phi, int icnv, const PhysTables *P, double *ttv,
                                  double *qtv) {
     using namespace phys;
     constexpr int NL = kKX, nl1 = kKX - 1;  // nl1: 1-based index of the level above the bottom
     (void)nl1;
-    const double psg = h.psg, rps = h.rps;
     const double *qa = h.qa, *se = h.se, *rh = h.rh, *qsat = h.qsat;
-    (void)psg; (void)rps; (void)qa; (void)se; (void)rh; (void)qsat;
     // 4.1 vdifsc (phy_vdifsc.f90:17-124)
 #pragma unroll
     for (int k = 0; k < NL; ++k) ttv[k] = qtv[k] = 0.;
     {
         constexpr int nlev = NL;
-        const double cshc = P->dsig[nlev - 1] / 3600., cvdi = (P->sigh[nl1] - P->sigh[1]) / ((nl1 - 1) * 3600.);
-        const double fshcq = cshc / trshc, fshcse = cshc / (trshc * cp);
-        const double fvdiq = cvdi / trvdi, fvdise = cvdi / (trvds * cp);
-        double rsig[NL], rsig1[NL];
-#pragma unroll
-        for (int k = 1; k <= nl1; ++k) {
-            rsig[k - 1] = 1. / P->dsig[k - 1];
-            rsig1[k - 1] = 1. / (1. - P->sigh[k]);
-        }
-        rsig[nlev - 1] = 1. / P->dsig[nlev - 1];
+        VdifK vk;
+        phys_vdif_consts(P, vk);
+        const double fshcq = vk.fshcq, fshcse = vk.fshcse, fvdiq = vk.fvdiq, fvdise = vk.fvdise;
+        const double *rsig = vk.rsig, *rsig1 = vk.rsig1;
         double drh0 = rhgrad * (P->sig[nlev - 1] - P->sig[nl1 - 1]);
         double fvdiq2 = fvdiq * P->sigh[nl1];
         // shallow convection

@@ -371,3 +371,43 @@ def test_write_through_handoffs_are_bitwise_the_default(pg, cuda):
     for k in ra:
         np.testing.assert_array_equal(ra[k], rb[k])
     np.testing.assert_array_equal(pa, pb)
+
+
+def test_quad_physics_row_kernel_is_bitwise_the_column_kernel(pg, cuda):
+    """k_st_gridspec_q (phypar on four lanes per column: per-level work on the level's
+    lane, the longwave bands one per lane, sml_physics_quad.hpp) against k_st_gridspec
+    (one lane per column, SML_DYN_QUAD=0): every expression and every sum's order is the
+    same, so two chained windows with physics -- shortwave and longwave-only steps,
+    the radiation state carried between them -- are bitwise equal (state, radiation
+    state, geopotential)."""
+    import os
+
+    import torch
+
+    from speedy_ml_amd.dynamics import Dynamics
+    from speedy_ml_amd.synthetic import dyn_state
+
+    st, forcing = dyn_state(7)
+    out = []
+    for quad in ("0", "1"):
+        os.environ["SML_DYN_QUAD"] = quad
+        try:
+            d = Dynamics()
+        finally:
+            os.environ.pop("SML_DYN_QUAD", None)
+        d.set_forcing(**forcing)
+        d.set_state(st)
+        d.set_physics(_window_bc(pg, d))
+        d.set_rad_state(None)
+        d.set_clock(1, True)
+        d.window(24)
+        d.window(24)
+        torch.cuda.synchronize()
+        out.append((d.get_state(), d.get_rad_state(), d.get_phi()))
+        d.close()
+    (a, ra, pa), (b, rb, pb) = out
+    for f in oracle.DYN_FIELDS:
+        np.testing.assert_array_equal(a[f], b[f], err_msg=f)
+    for k in ra:
+        np.testing.assert_array_equal(ra[k], rb[k], err_msg=k)
+    np.testing.assert_array_equal(pa, pb)
