@@ -186,6 +186,50 @@ __device__ inline void phys_entr(const PhysTables *P, double (&entr)[kKX + 1]) {
     for (int k = 2; k <= nl1; ++k) entr[k] = entr[k] * sentr;
 }
 
+// convmf's trigger (phy_convmf.f90:62-118): the cloud top itop (nlev + 1: no
+// convection), the humidity excess qdif; 1-based level indices as the reference
+__device__ inline void phys_convmf_trigger(const PhysThermo &h, const PhysTables *P, int &itop_o, double &qdif_o) {
+    using namespace phys;
+    constexpr int NL = kKX, nl1 = kKX - 1, nlev = NL, nlp = NL + 1;
+    const double psg = h.psg;
+    const double *qa = h.qa, *se = h.se, *qsat = h.qsat;
+    double mss[NL + 1];
+#pragma unroll
+    for (int k = 2; k <= nlev; ++k) mss[k] = se[k - 1] + alhc * qsat[k - 1];
+    const double rlhc = 1. / alhc;
+    double qdif = 0., msthr = 0.;
+    int itop = nlp;
+    if (psg > psmin) {
+        const double mse0 = se[nlev - 1] + alhc * qa[nlev - 1];
+        double mse1 = se[nl1 - 1] + alhc * qa[nl1 - 1];
+        mse1 = fmin(mse0, mse1);
+        const double mss0 = fmax(mse0, mss[nlev]);
+        int ktop1 = nlev, ktop2 = nlev;
+#pragma unroll
+        for (int k = nlev - 3; k >= 3; --k) {
+            const double mss2 = mss[k] + P->wvi[k - 1][1] * (mss[k + 1] - mss[k]);
+            if (mss0 > mss2) ktop1 = k;
+            if (mse1 > mss2) {
+                ktop2 = k;
+                msthr = mss2;
+            }
+        }
+        if (ktop1 < nlev) {
+            const double qthr0 = rhbl * qsat[nlev - 1], qthr1 = rhbl * qsat[nl1 - 1];
+            const bool lqthr = (qa[nlev - 1] > qthr0 && qa[nl1 - 1] > qthr1);
+            if (ktop2 < nlev) {
+                itop = ktop1;
+                qdif = fmax(qa[nlev - 1] - qthr0, (mse0 - msthr) * rlhc);
+            } else if (lqthr) {
+                itop = ktop1;
+                qdif = qa[nlev - 1] - qthr0;
+            }
+        }
+    }
+    itop_o = itop;
+    qdif_o = qdif;
+}
+
 // 2.1 convmf (phy_convmf.f90:22-238), 1-based level indices as the reference: the
 // unscaled fluxes dfse / dfqa of every level into tt_cnv / qt_cnv (level k at k - 1),
 // the convective precipitation and the cloud top itop (nlev + 1: no convection)
@@ -202,39 +246,8 @@ __device__ inline void phys_convmf(const PhysThermo &h, const PhysTables *P, con
     {
         constexpr int nlev = NL, nlp = NL + 1;
         const double fqmax = 5., fm0 = p0 * P->dsig[nlev - 1] / (gg * trcnv * 3600), rdps = 2. / (1. - psmin);
-        double mss[NL + 1];
-#pragma unroll
-        for (int k = 2; k <= nlev; ++k) mss[k] = se[k - 1] + alhc * qsat[k - 1];
-        const double rlhc = 1. / alhc;
-        double qdif = 0., msthr = 0.;
-        itop = nlp;
-        if (psg > psmin) {
-            const double mse0 = se[nlev - 1] + alhc * qa[nlev - 1];
-            double mse1 = se[nl1 - 1] + alhc * qa[nl1 - 1];
-            mse1 = fmin(mse0, mse1);
-            const double mss0 = fmax(mse0, mss[nlev]);
-            int ktop1 = nlev, ktop2 = nlev;
-#pragma unroll
-            for (int k = nlev - 3; k >= 3; --k) {
-                const double mss2 = mss[k] + P->wvi[k - 1][1] * (mss[k + 1] - mss[k]);
-                if (mss0 > mss2) ktop1 = k;
-                if (mse1 > mss2) {
-                    ktop2 = k;
-                    msthr = mss2;
-                }
-            }
-            if (ktop1 < nlev) {
-                const double qthr0 = rhbl * qsat[nlev - 1], qthr1 = rhbl * qsat[nl1 - 1];
-                const bool lqthr = (qa[nlev - 1] > qthr0 && qa[nl1 - 1] > qthr1);
-                if (ktop2 < nlev) {
-                    itop = ktop1;
-                    qdif = fmax(qa[nlev - 1] - qthr0, (mse0 - msthr) * rlhc);
-                } else if (lqthr) {
-                    itop = ktop1;
-                    qdif = qa[nlev - 1] - qthr0;
-                }
-            }
-        }
+        double qdif;
+        phys_convmf_trigger(h, P, itop, qdif);
         if (itop != nlp) {  // itop is in 3 .. nlev-3 here
             double dfse[NL + 1], dfqa[NL + 1];
 #pragma unroll

@@ -500,6 +500,166 @@ __global__ __launch_bounds__(kDiagThreads) void k_chol_diag(double *__restrict__
     }
 }
 
+// The diagonal factor blocked (default; SML_CHOL_DIAG=1: k_chol_diag): the same
+// outputs -- L_kk into G, L_kk^-1 into linv, potrf's info -- from the 128 x 128 block
+// as four 32-column sub-blocks.  Sub-block P: one wave factors its 32 x 32 diagonal
+// block and inverts it (k_chol_diag's column steps restricted to the sub-block, no
+// workgroup barrier: the wave's LDS operations complete in order); every wave then
+// forms the rows below, L_IP = A_IP X_PP^T, and the trailing update inside the block,
+// A_IJ -= L_IP L_JP^T, as 16 x 16 f64 MFMA tiles from LDS.  After the last sub-block
+// the inverse's off-diagonal blocks, X_IJ = -X_II sum_{J <= K < I} L_IK X_KJ, row of
+// blocks by row.  About 20 workgroup barriers instead of k_chol_diag's 256; the same
+// factorisation up to rounding (the update sums are blocked).
+constexpr int kSub = 32;                     // sub-block edge
+constexpr int kTs = kSub + 1;                // LDS stride of the T_J scratch blocks
+constexpr size_t kDiagBLds = kDiagLds + (size_t)3 * kSub * kTs * sizeof(double);
+
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+// one 16 x 16 tile of O = A B^T over K (a multiple of 4): fa(r, t), fb(c, t) for
+// r, c < 16; acc[q] = O(kk + 4 q, l16) (lane = 16 kk + l16), gemm_tile's layout
+template <class FA, class FB>
+__device__ __forceinline__ d4 mfma_tile16(FA fa, FB fb, int K) {
+    const int lane = threadIdx.x & 63, l16 = lane & 15, kk = lane >> 4;
+    d4 acc = {0, 0, 0, 0};
+    for (int t0 = 0; t0 < K; t0 += 4) acc = MFMA64(fa(l16, t0 + kk), fb(l16, t0 + kk), acc);
+    return acc;
+}
+
+__global__ __launch_bounds__(kDiagThreads) void k_chol_diag_b(double *__restrict__ G, double *__restrict__ linv,
+                                                              int npad, int k, int *__restrict__ info,
+                                                              const TrainRegion *__restrict__ regs) {
+    extern __shared__ double S[];  // S[i * kDiagLd + c]: L(i, c) for c < i, X(i, c) at S[c][i]
+    double *ldg = S + kTile * kDiagLd, *xd = ldg + kTile, *Tb = xd + kTile;
+    const int r = blockIdx.x, C = npad / kTile;
+    if (k >= live_blocks(regs, r)) return;  // an identity block: L = L^-1 = I, already in G
+    constexpr int ld = kDiagLd;
+    const int tid = threadIdx.x, i = tid & (kTile - 1), h = tid >> 7;
+    const int w = tid >> 6, lane = tid & 63, l16 = lane & 15, kk = lane >> 4;
+    double *A = G + (size_t)r * npad * npad + (size_t)k * kTile * npad + (size_t)k * kTile;
+    for (int c = h; c < kTile; c += kDiagH) S[i * ld + c] = c <= i ? A[(size_t)c * npad + i] : 0.0;
+    // X(t, c) of the lower-triangular inverse (row t, column c; 0 above the diagonal)
+    auto Xv = [&](int t, int c) { return t > c ? S[c * ld + t] : (t == c ? xd[t] : 0.0); };
+    for (int P = 0; P < kTile / kSub; ++P) {
+        const int o = P * kSub;
+        __syncthreads();
+        if (w == 0) {  // the sub-block's column steps (k_chol_diag's, on rows / columns o..o+31)
+            const int si = lane & (kSub - 1), sh = lane >> 5;
+            for (int j = 0; j < kSub; ++j) {
+                const double d = S[(o + j) * ld + o + j];
+                const double inv = 1.0 / sqrt(d);
+                if (lane == 0) {
+                    ldg[o + j] = sqrt(d);
+                    xd[o + j] = inv;
+                    if (!(d > 0.0) && info[r] == 0) info[r] = k * kTile + o + j + 1;
+                }
+                if (sh == 0 && si > j) S[(o + si) * ld + o + j] *= inv;  // L(si, j)
+                if (sh == 1 && si < j) S[(o + si) * ld + o + j] *= inv;  // X(j, c = si), stored at S[c][j]
+                wave_sync();
+                if (si > j) {
+                    const double lij = S[(o + si) * ld + o + j];
+                    double *Si = S + (o + si) * ld + o;
+                    for (int l0 = j + 1 + sh; l0 <= si; l0 += 8) {  // L(si, l) -= L(si, j) L(l, j)
+                        double a[4], b[4];
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            const int l = l0 + 2 * u;
+                            if (l <= si) {
+                                a[u] = Si[l];
+                                b[u] = S[(o + l) * ld + o + j];
+                            }
+                        }
+#pragma unroll
+                        for (int u = 0; u < 4; ++u)
+                            if (l0 + 2 * u <= si) Si[l0 + 2 * u] = a[u] - lij * b[u];
+                    }
+                    for (int c0 = sh; c0 < j; c0 += 8) {  // X(si, c) -= L(si, j) X(j, c)
+                        double a[4], b[4];
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            const int c = c0 + 2 * u;
+                            if (c < j) {
+                                a[u] = S[(o + c) * ld + o + si];
+                                b[u] = S[(o + c) * ld + o + j];
+                            }
+                        }
+#pragma unroll
+                        for (int u = 0; u < 4; ++u)
+                            if (c0 + 2 * u < j) S[(o + c0 + 2 * u) * ld + o + si] = a[u] - lij * b[u];
+                    }
+                    if (sh == 1) S[(o + j) * ld + o + si] -= lij * xd[o + j];  // X(si, j)
+                }
+                wave_sync();
+            }
+        }
+        __syncthreads();
+        const int below = kTile - o - kSub;  // rows under the sub-block
+        if (below == 0) break;
+        // L_IP = A_IP X_PP^T (rows o+32.., columns o..o+31): every tile read before any is written
+        const int ntp = 2 * (below / 16);
+        d4 accp = {0, 0, 0, 0};
+        int pr0 = 0, pc0 = 0;
+        if (w < ntp) {
+            pr0 = o + kSub + 16 * (w >> 1);
+            pc0 = o + 16 * (w & 1);
+            accp = mfma_tile16([&](int rr, int t) { return S[(pr0 + rr) * ld + o + t]; },
+                               [&](int cc, int t) { return Xv(pc0 + cc, o + t); }, kSub);
+        }
+        __syncthreads();
+        if (w < ntp) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) S[(pr0 + kk + 4 * q) * ld + pc0 + l16] = accp[q];
+        }
+        __syncthreads();
+        // the trailing update inside the block: the lower-triangle 16-tiles (a >= b) of
+        // rows / columns o+32..127, A(i, c) -= sum_t L(i, t) L(c, t), t in the sub-block
+        const int nT = below / 16, ntu = nT * (nT + 1) / 2;
+        for (int u = w; u < ntu; u += kDiagThreads / 64) {
+            int a = 0, rem = u;
+            while (rem > a) rem -= ++a;  // u = a (a + 1) / 2 + b
+            const int b = rem;
+            const int r0 = o + kSub + 16 * a, c0 = o + kSub + 16 * b;
+            const d4 acc = mfma_tile16([&](int rr, int t) { return S[(r0 + rr) * ld + o + t]; },
+                                       [&](int cc, int t) { return S[(c0 + cc) * ld + o + t]; }, kSub);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int row = r0 + kk + 4 * q, col = c0 + l16;
+                if (a != b || col <= row) S[row * ld + col] -= acc[q];
+            }
+        }
+    }
+    // the inverse's off-diagonal blocks, block row I by block row:
+    //   T_J = sum_{t in [32 J, 32 I)} L(32 I + u, t) X(t, 32 J + c);   X_IJ = -X_II T_J
+    for (int I = 1; I < kTile / kSub; ++I) {
+        const int oi = I * kSub;
+        if (w < 4 * I) {
+            const int J = w >> 2, u0 = 16 * ((w >> 1) & 1), c0 = 16 * (w & 1), oj = J * kSub;
+            const d4 acc = mfma_tile16([&](int rr, int t) { return S[(oi + u0 + rr) * ld + oj + t]; },
+                                       [&](int cc, int t) { return Xv(oj + t, oj + c0 + cc); }, oi - oj);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) Tb[J * kSub * kTs + (u0 + kk + 4 * q) * kTs + c0 + l16] = acc[q];
+        }
+        __syncthreads();
+        if (w < 4 * I) {
+            const int J = w >> 2, u0 = 16 * ((w >> 1) & 1), c0 = 16 * (w & 1), oj = J * kSub;
+            const double *TJ = Tb + J * kSub * kTs;
+            const d4 acc = mfma_tile16([&](int rr, int v) { return Xv(oi + u0 + rr, oi + v); },
+                                       [&](int cc, int v) { return TJ[v * kTs + c0 + cc]; }, kSub);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) S[(oj + c0 + l16) * ld + oi + u0 + kk + 4 * q] = -acc[q];
+        }
+        __syncthreads();
+    }
+    double *Li = linv + ((size_t)r * C + k) * kTile * kTile;
+    for (int c = h; c < kTile; c += kDiagH) {
+        if (c <= i) A[(size_t)c * npad + i] = c < i ? S[i * ld + c] : ldg[i];
+        Li[(size_t)c * kTile + i] = c < i ? S[c * ld + i] : (c == i ? xd[i] : 0.0);
+    }
+}
+
 // L_ik = A_ik L_kk^-T for the blocks i > k below the diagonal, in place: a block
 // owns 64 rows x all 128 columns (it reads the whole rows it overwrites)
 __global__ __launch_bounds__(256, 3) void k_chol_panel(double *__restrict__ G, const double *__restrict__ linv, int npad,
@@ -652,6 +812,8 @@ struct sml_train {
     int gram = 2;  // k_train_gram2 (double-buffered LDS); SML_GRAM_V=1: k_train_gram
     // the triangular solves' in-panel launches in three right-hand-side groups
     bool rhs_split = true;
+    // the blocked diagonal factor (k_chol_diag_b); SML_CHOL_DIAG=1: k_chol_diag
+    bool diag_b = true;
     std::vector<int> naug;
     TrainRegion *d_regs = nullptr;
     double *d_G = nullptr, *d_B = nullptr;
@@ -693,6 +855,7 @@ extern "C" int sml_train_create(int nlocal, const int *naug, int nout, sml_train
     if (const char *e = getenv("SML_CHOL_PANEL")) t->panel = std::max(1, atoi(e));  // tuning knob
     if (const char *e = getenv("SML_GRAM_V")) t->gram = atoi(e) == 1 ? 1 : 2;       // A/B knob
     if (const char *e = getenv("SML_SOLVE_SPLIT")) t->rhs_split = *e != '0';        // A/B knob
+    if (const char *e = getenv("SML_CHOL_DIAG")) t->diag_b = atoi(e) != 1;          // A/B knob
     t->naug.assign(naug, naug + nlocal);
     int mx = 0;
     for (int i = 0; i < nlocal; ++i) {
@@ -726,6 +889,8 @@ extern "C" int sml_train_create(int nlocal, const int *naug, int nout, sml_train
     if (!lds_set) {
         SML_HIP(hipFuncSetAttribute((const void *)k_chol_diag, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     (int)kDiagLds));
+        SML_HIP(hipFuncSetAttribute((const void *)k_chol_diag_b, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)kDiagBLds));
         lds_set = true;
     }
     *out = t;
@@ -791,8 +956,12 @@ extern "C" int sml_train_solve(sml_train *t, int ncs, double beta_res, double be
             if (k > p0)
                 hipLaunchKernelGGL(k_chol_update, dim3(C - k, nl), dim3(256), 0, st, t->d_G, npad, p0, k - p0, k,
                                    k + 1, t->d_regs);
-            hipLaunchKernelGGL(k_chol_diag, dim3(nl), dim3(kDiagThreads), kDiagLds, st, t->d_G, t->d_linv, npad, k,
-                               t->d_info, t->d_regs);
+            if (t->diag_b)
+                hipLaunchKernelGGL(k_chol_diag_b, dim3(nl), dim3(kDiagThreads), kDiagBLds, st, t->d_G, t->d_linv, npad,
+                                   k, t->d_info, t->d_regs);
+            else
+                hipLaunchKernelGGL(k_chol_diag, dim3(nl), dim3(kDiagThreads), kDiagLds, st, t->d_G, t->d_linv, npad, k,
+                                   t->d_info, t->d_regs);
             if (k < C - 1)
                 hipLaunchKernelGGL(k_chol_panel, dim3(2 * (C - 1 - k), nl), dim3(256), 0, st, t->d_G, t->d_linv,
                                    npad, k, t->d_regs);

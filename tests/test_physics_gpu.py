@@ -373,13 +373,14 @@ def test_write_through_handoffs_are_bitwise_the_default(pg, cuda):
     np.testing.assert_array_equal(pa, pb)
 
 
-def test_quad_physics_row_kernel_is_bitwise_the_column_kernel(pg, cuda):
-    """k_st_gridspec_q (phypar on four lanes per column: per-level work on the level's
-    lane, the longwave bands one per lane, sml_physics_quad.hpp) against k_st_gridspec
-    (one lane per column, SML_DYN_QUAD=0): every expression and every sum's order is the
-    same, so two chained windows with physics -- shortwave and longwave-only steps,
-    the radiation state carried between them -- are bitwise equal (state, radiation
-    state, geopotential)."""
+@pytest.mark.parametrize("knob", [("SML_DYN_QUAD", "1")])
+def test_row_kernel_variants_are_bitwise_the_default(pg, cuda, knob):
+    """The row kernel's alternative schedules against the default, two chained windows
+    with physics (shortwave and longwave-only steps, the radiation state carried):
+    SML_DYN_QUAD=1 -- k_st_gridspec_q, phypar on four lanes per column (per-level work
+    on the level's lane, the longwave bands one per lane, sml_physics_quad.hpp).  Every
+    expression and every sum's order is the same, so state, radiation state and
+    geopotential are bitwise equal."""
     import os
 
     import torch
@@ -389,12 +390,13 @@ def test_quad_physics_row_kernel_is_bitwise_the_column_kernel(pg, cuda):
 
     st, forcing = dyn_state(7)
     out = []
-    for quad in ("0", "1"):
-        os.environ["SML_DYN_QUAD"] = quad
+    for val in (None, knob[1]):
+        if val is not None:
+            os.environ[knob[0]] = val
         try:
             d = Dynamics()
         finally:
-            os.environ.pop("SML_DYN_QUAD", None)
+            os.environ.pop(knob[0], None)
         d.set_forcing(**forcing)
         d.set_state(st)
         d.set_physics(_window_bc(pg, d))
