@@ -514,6 +514,21 @@ constexpr int kSub = 32;                     // sub-block edge
 constexpr int kTs = kSub + 1;                // LDS stride of the T_J scratch blocks
 constexpr size_t kDiagBLds = kDiagLds + (size_t)3 * kSub * kTs * sizeof(double);
 
+// phase stamps of k_chol_diag_b (profiling build, -DSML_DSTAMPS): thread 0 of block 0
+// of the launch for block column g_dst_k records wall_clock64 at slot s
+#ifdef SML_DSTAMPS
+__device__ long long g_dst[32];
+__device__ int g_dst_k = 0;
+#define SML_DST(s)                                                                   \
+    do {                                                                             \
+        if (threadIdx.x == 0 && blockIdx.x == 0 && k == g_dst_k) g_dst[s] = wall_clock64(); \
+    } while (0)
+#else
+#define SML_DST(s) \
+    do {           \
+    } while (0)
+#endif
+
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -540,12 +555,14 @@ __global__ __launch_bounds__(kDiagThreads) void k_chol_diag_b(double *__restrict
     const int tid = threadIdx.x, i = tid & (kTile - 1), h = tid >> 7;
     const int w = tid >> 6, lane = tid & 63, l16 = lane & 15, kk = lane >> 4;
     double *A = G + (size_t)r * npad * npad + (size_t)k * kTile * npad + (size_t)k * kTile;
+    SML_DST(0);
     for (int c = h; c < kTile; c += kDiagH) S[i * ld + c] = c <= i ? A[(size_t)c * npad + i] : 0.0;
     // X(t, c) of the lower-triangular inverse (row t, column c; 0 above the diagonal)
     auto Xv = [&](int t, int c) { return t > c ? S[c * ld + t] : (t == c ? xd[t] : 0.0); };
     for (int P = 0; P < kTile / kSub; ++P) {
         const int o = P * kSub;
         __syncthreads();
+        SML_DST(1 + 4 * P);
         if (w == 0) {  // the sub-block's column steps (k_chol_diag's, on rows / columns o..o+31)
             const int si = lane & (kSub - 1), sh = lane >> 5;
             for (int j = 0; j < kSub; ++j) {
@@ -596,6 +613,7 @@ __global__ __launch_bounds__(kDiagThreads) void k_chol_diag_b(double *__restrict
             }
         }
         __syncthreads();
+        SML_DST(2 + 4 * P);
         const int below = kTile - o - kSub;  // rows under the sub-block
         if (below == 0) break;
         // L_IP = A_IP X_PP^T (rows o+32.., columns o..o+31): every tile read before any is written
@@ -614,6 +632,7 @@ __global__ __launch_bounds__(kDiagThreads) void k_chol_diag_b(double *__restrict
             for (int q = 0; q < 4; ++q) S[(pr0 + kk + 4 * q) * ld + pc0 + l16] = accp[q];
         }
         __syncthreads();
+        SML_DST(3 + 4 * P);
         // the trailing update inside the block: the lower-triangle 16-tiles (a >= b) of
         // rows / columns o+32..127, A(i, c) -= sum_t L(i, t) L(c, t), t in the sub-block
         const int nT = below / 16, ntu = nT * (nT + 1) / 2;
@@ -631,6 +650,7 @@ __global__ __launch_bounds__(kDiagThreads) void k_chol_diag_b(double *__restrict
             }
         }
     }
+    SML_DST(17);
     // the inverse's off-diagonal blocks, block row I by block row:
     //   T_J = sum_{t in [32 J, 32 I)} L(32 I + u, t) X(t, 32 J + c);   X_IJ = -X_II T_J
     for (int I = 1; I < kTile / kSub; ++I) {
@@ -653,11 +673,14 @@ __global__ __launch_bounds__(kDiagThreads) void k_chol_diag_b(double *__restrict
         }
         __syncthreads();
     }
+    SML_DST(18);
     double *Li = linv + ((size_t)r * C + k) * kTile * kTile;
     for (int c = h; c < kTile; c += kDiagH) {
         if (c <= i) A[(size_t)c * npad + i] = c < i ? S[i * ld + c] : ldg[i];
         Li[(size_t)c * kTile + i] = c < i ? S[c * ld + i] : (c == i ? xd[i] : 0.0);
     }
+    __syncthreads();
+    SML_DST(19);
 }
 
 // L_ik = A_ik L_kk^-T for the blocks i > k below the diagonal, in place: a block
@@ -1105,3 +1128,14 @@ extern "C" int sml_probe_mfma_f64_clock(int iters, double *tflops, double *ghz) 
 }
 
 extern "C" int sml_probe_mfma_f64(int iters, double *tflops) { return sml_probe_mfma_f64_clock(iters, tflops, nullptr); }
+
+#ifdef SML_DSTAMPS
+// diagnostic (profiling build): the stamps of k_chol_diag_b's launch for block column k
+extern "C" int sml_dbg_diag_stamps(int k, long long *out) {
+    SML_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_dst_k), &k, sizeof(int), 0, hipMemcpyHostToDevice));
+    if (!out) return SML_OK;
+    SML_HIP(hipDeviceSynchronize());
+    SML_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_dst), sizeof(long long) * 32, 0, hipMemcpyDeviceToHost));
+    return SML_OK;
+}
+#endif
