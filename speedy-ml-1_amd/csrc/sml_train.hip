@@ -510,9 +510,15 @@ __global__ __launch_bounds__(kDiagThreads) void k_chol_diag(double *__restrict__
 // the inverse's off-diagonal blocks, X_IJ = -X_II sum_{J <= K < I} L_IK X_KJ, row of
 // blocks by row.  About 20 workgroup barriers instead of k_chol_diag's 256; the same
 // factorisation up to rounding (the update sums are blocked).
-constexpr int kSub = 32;                     // sub-block edge
+#ifndef SML_DIAG_SUB
+#define SML_DIAG_SUB 16
+#endif
+constexpr int kSub = SML_DIAG_SUB;           // sub-block edge (16 or 32)
+constexpr int kNS = kTile / kSub, kNT = kSub / 16;  // sub-blocks; 16-tiles per sub-block edge
+constexpr int kSH = 64 / kSub;               // lanes per row in the sub-block steps
 constexpr int kTs = kSub + 1;                // LDS stride of the T_J scratch blocks
-constexpr size_t kDiagBLds = kDiagLds + (size_t)3 * kSub * kTs * sizeof(double);
+constexpr size_t kDiagBLds = kDiagLds + (size_t)(kNS - 1) * kSub * kTs * sizeof(double);
+static_assert(kSub == 16 || kSub == 32, "sub-block edge");
 
 // phase stamps of k_chol_diag_b (profiling build, -DSML_DSTAMPS): thread 0 of block 0
 // of the launch for block column g_dst_k records wall_clock64 at slot s
@@ -559,12 +565,12 @@ __global__ __launch_bounds__(kDiagThreads) void k_chol_diag_b(double *__restrict
     for (int c = h; c < kTile; c += kDiagH) S[i * ld + c] = c <= i ? A[(size_t)c * npad + i] : 0.0;
     // X(t, c) of the lower-triangular inverse (row t, column c; 0 above the diagonal)
     auto Xv = [&](int t, int c) { return t > c ? S[c * ld + t] : (t == c ? xd[t] : 0.0); };
-    for (int P = 0; P < kTile / kSub; ++P) {
+    for (int P = 0; P < kNS; ++P) {
         const int o = P * kSub;
         __syncthreads();
         SML_DST(1 + 4 * P);
         if (w == 0) {  // the sub-block's column steps (k_chol_diag's, on rows / columns o..o+31)
-            const int si = lane & (kSub - 1), sh = lane >> 5;
+            const int si = lane & (kSub - 1), sh = lane / kSub;
             for (int j = 0; j < kSub; ++j) {
                 const double d = S[(o + j) * ld + o + j];
                 const double inv = 1.0 / sqrt(d);
@@ -574,16 +580,16 @@ __global__ __launch_bounds__(kDiagThreads) void k_chol_diag_b(double *__restrict
                     if (!(d > 0.0) && info[r] == 0) info[r] = k * kTile + o + j + 1;
                 }
                 if (sh == 0 && si > j) S[(o + si) * ld + o + j] *= inv;  // L(si, j)
-                if (sh == 1 && si < j) S[(o + si) * ld + o + j] *= inv;  // X(j, c = si), stored at S[c][j]
+                if (sh == kSH - 1 && si < j) S[(o + si) * ld + o + j] *= inv;  // X(j, c = si), stored at S[c][j]
                 wave_sync();
                 if (si > j) {
                     const double lij = S[(o + si) * ld + o + j];
                     double *Si = S + (o + si) * ld + o;
-                    for (int l0 = j + 1 + sh; l0 <= si; l0 += 8) {  // L(si, l) -= L(si, j) L(l, j)
+                    for (int l0 = j + 1 + sh; l0 <= si; l0 += 4 * kSH) {  // L(si, l) -= L(si, j) L(l, j)
                         double a[4], b[4];
 #pragma unroll
                         for (int u = 0; u < 4; ++u) {
-                            const int l = l0 + 2 * u;
+                            const int l = l0 + kSH * u;
                             if (l <= si) {
                                 a[u] = Si[l];
                                 b[u] = S[(o + l) * ld + o + j];
@@ -591,13 +597,13 @@ __global__ __launch_bounds__(kDiagThreads) void k_chol_diag_b(double *__restrict
                         }
 #pragma unroll
                         for (int u = 0; u < 4; ++u)
-                            if (l0 + 2 * u <= si) Si[l0 + 2 * u] = a[u] - lij * b[u];
+                            if (l0 + kSH * u <= si) Si[l0 + kSH * u] = a[u] - lij * b[u];
                     }
-                    for (int c0 = sh; c0 < j; c0 += 8) {  // X(si, c) -= L(si, j) X(j, c)
+                    for (int c0 = sh; c0 < j; c0 += 4 * kSH) {  // X(si, c) -= L(si, j) X(j, c)
                         double a[4], b[4];
 #pragma unroll
                         for (int u = 0; u < 4; ++u) {
-                            const int c = c0 + 2 * u;
+                            const int c = c0 + kSH * u;
                             if (c < j) {
                                 a[u] = S[(o + c) * ld + o + si];
                                 b[u] = S[(o + c) * ld + o + j];
@@ -605,9 +611,9 @@ __global__ __launch_bounds__(kDiagThreads) void k_chol_diag_b(double *__restrict
                         }
 #pragma unroll
                         for (int u = 0; u < 4; ++u)
-                            if (c0 + 2 * u < j) S[(o + c0 + 2 * u) * ld + o + si] = a[u] - lij * b[u];
+                            if (c0 + kSH * u < j) S[(o + c0 + kSH * u) * ld + o + si] = a[u] - lij * b[u];
                     }
-                    if (sh == 1) S[(o + j) * ld + o + si] -= lij * xd[o + j];  // X(si, j)
+                    if (sh == kSH - 1) S[(o + j) * ld + o + si] -= lij * xd[o + j];  // X(si, j)
                 }
                 wave_sync();
             }
@@ -617,12 +623,12 @@ __global__ __launch_bounds__(kDiagThreads) void k_chol_diag_b(double *__restrict
         const int below = kTile - o - kSub;  // rows under the sub-block
         if (below == 0) break;
         // L_IP = A_IP X_PP^T (rows o+32.., columns o..o+31): every tile read before any is written
-        const int ntp = 2 * (below / 16);
+        const int ntp = kNT * (below / 16);
         d4 accp = {0, 0, 0, 0};
         int pr0 = 0, pc0 = 0;
         if (w < ntp) {
-            pr0 = o + kSub + 16 * (w >> 1);
-            pc0 = o + 16 * (w & 1);
+            pr0 = o + kSub + 16 * (w / kNT);
+            pc0 = o + 16 * (w % kNT);
             accp = mfma_tile16([&](int rr, int t) { return S[(pr0 + rr) * ld + o + t]; },
                                [&](int cc, int t) { return Xv(pc0 + cc, o + t); }, kSub);
         }
@@ -653,18 +659,18 @@ __global__ __launch_bounds__(kDiagThreads) void k_chol_diag_b(double *__restrict
     SML_DST(17);
     // the inverse's off-diagonal blocks, block row I by block row:
     //   T_J = sum_{t in [32 J, 32 I)} L(32 I + u, t) X(t, 32 J + c);   X_IJ = -X_II T_J
-    for (int I = 1; I < kTile / kSub; ++I) {
+    for (int I = 1; I < kNS; ++I) {
         const int oi = I * kSub;
-        if (w < 4 * I) {
-            const int J = w >> 2, u0 = 16 * ((w >> 1) & 1), c0 = 16 * (w & 1), oj = J * kSub;
+        for (int u = w; u < kNT * kNT * I; u += kDiagThreads / 64) {
+            const int J = u / (kNT * kNT), u0 = 16 * ((u / kNT) % kNT), c0 = 16 * (u % kNT), oj = J * kSub;
             const d4 acc = mfma_tile16([&](int rr, int t) { return S[(oi + u0 + rr) * ld + oj + t]; },
                                        [&](int cc, int t) { return Xv(oj + t, oj + c0 + cc); }, oi - oj);
 #pragma unroll
             for (int q = 0; q < 4; ++q) Tb[J * kSub * kTs + (u0 + kk + 4 * q) * kTs + c0 + l16] = acc[q];
         }
         __syncthreads();
-        if (w < 4 * I) {
-            const int J = w >> 2, u0 = 16 * ((w >> 1) & 1), c0 = 16 * (w & 1), oj = J * kSub;
+        for (int u = w; u < kNT * kNT * I; u += kDiagThreads / 64) {
+            const int J = u / (kNT * kNT), u0 = 16 * ((u / kNT) % kNT), c0 = 16 * (u % kNT), oj = J * kSub;
             const double *TJ = Tb + J * kSub * kTs;
             const d4 acc = mfma_tile16([&](int rr, int v) { return Xv(oi + u0 + rr, oi + v); },
                                        [&](int cc, int v) { return TJ[v * kTs + c0 + cc]; }, kSub);
