@@ -39,6 +39,7 @@
 #include "sml_fft_wa96.hpp"
 #include "sml_physics.hpp"
 #include "sml_physics_quad.hpp"
+#include "sml_physics_pair.hpp"
 #include "sml_spectral_internal.hpp"
 
 using namespace sml;
@@ -152,10 +153,11 @@ struct sml_dynamics {
     bool fused = true;
     // with GPU physics: k_st_grid + k_st_specx instead of k_st_gridspec (SML_DYN_SPLIT_GRID=1)
     bool split_grid = false;
-    // the row kernel's phypar on four lanes per column (k_st_gridspec_q, SML_DYN_QUAD=1:
-    // bitwise the default, measured slower); default: one lane per column
-    // split over two wave pairs (k_st_gridspec)
-    bool quad = false;
+    // the row kernel's schedule (SML_DYN_QUAD): 2 (default) k_st_gridspec_p -- the grid-point
+    // dynamics, the moist side and the longwave side on waves of their own, the longwave on
+    // two lanes per column; 1: k_st_gridspec_q (phypar on four lanes per column, measured
+    // slower); 0: k_st_gridspec (one lane per column, two wave pairs).  All bitwise equal.
+    int quad = 2;
     bool nograph = false;  // SML_DYN_NOGRAPH=1: the window's launches issued directly, not replayed
     // the fused step's hand-offs (vfm, varm, the m-major state) stored write-through
     // (store2): SML_DYN_WT=1 both step kernels, 2 the row kernel's (vfm) only, 3 the
@@ -1808,6 +1810,165 @@ __global__ __launch_bounds__(kGqThreads) void k_st_gridspec_q(
     stamp(dbg, 0, 3);
 }
 
+// The row kernel with each of phypar's roles on waves of its own (SML_DYN_QUAD=2): 8
+// waves, two per SIMD.  gridx as in k_st_gridspec; then waves 0-1 run the grid-point
+// dynamics and products, waves 2-3 the moist part and vdifsc (one column per lane, the
+// hand-over of k_st_gridspec), waves 4-6 the longwave / surface chain -- on a shortwave
+// step after its own moist part and the shortwave -- on two lanes per column
+// (sml_physics_pair.hpp), which then sum the tendencies into F (phys_column's sums, four
+// levels per lane); specx as before.  The same arithmetic as k_st_gridspec.
+constexpr int kGpThreads = 512;
+template <bool kWT>
+__global__ __launch_bounds__(kGpThreads) void k_st_gridspec_p(
+    const double *__restrict__ varm, double *__restrict__ vfm, const double *__restrict__ wa,
+    const double *__restrict__ cosgr, const DynTables *__restrict__ T, const double *__restrict__ bc,
+    double *__restrict__ rad, const PhysTables *__restrict__ PT, int lradsw, int wt, long long *dbg) {
+    __shared__ double A[kFftN * kRowLd], B[kFftN * kRowLd];
+    const double *was = kFftWa96;
+    (void)wa;
+    constexpr int kPtS = (int)(offsetof(PhysTables, fband) / sizeof(double)), kGpS = (int)(sizeof(GpTab) / 8);
+    static_assert(kPtS + kGpS <= kGpThreads, "table staging: one value per thread");
+    static_assert(kRowLd - kNFwd >= 24, "moist-side hand-over: 24 spare slots per column in B");
+    __shared__ double ptl[kPtS];
+    __shared__ GpTab gpt;
+    __shared__ double fsr[4 * kIX];  // radlw(1)'s surface row per (column, band), quad_fsr
+    constexpr int n1 = kNInv1P;
+    constexpr int nphys = (n1 - kPT1) + (kNInvP - (n1 + 2 * kKX + 2));  // 25 + 16 = 41
+    const int j = blockIdx.x, tid = threadIdx.x;
+    const bool isp = tid >= 256 && tid < 256 + 2 * kIX;  // the longwave side's pairs
+    const int pi = isp ? (tid - 256) >> 1 : 0, ph_ = tid & 1, ppt = j * kIX + pi;
+    stamp(dbg, 0, 0);
+    double rtab = 0.0;
+    if (tid < kPtS) {
+        rtab = reinterpret_cast<const double *>(PT)[tid];
+    } else if (tid < kPtS + kGpS) {
+        const int e = tid - kPtS, k = e % kKX;
+        const int w = e / kKX;
+        rtab = w == 0 ? T->dhs[k] : w == 1 ? T->dhsr[k] : w == 2 ? T->fsgr[k] : w == 3 ? T->tref[k]
+             : w == 4 ? T->tref3[k] : T->coriol[e - 5 * kKX];
+    }
+    {
+        const int t = tid >> 1, h = tid & 1;
+        const bool act = t < kNInv + nphys;
+        const int f = t < kNInv ? (t < kNInv1 ? t : n1 + (t - kNInv1))
+                                : (t - kNInv < n1 - kPT1 ? kPT1 + (t - kNInv)
+                                                         : n1 + 2 * kKX + 2 + (t - kNInv - (n1 - kPT1)));
+        double xi[kMX2 - 1];
+        if (act) row_gridx_load(varm, f, j, xi);
+        if (tid < kPtS) ptl[tid] = rtab;
+        else if (tid < kPtS + kGpS) reinterpret_cast<double *>(&gpt)[tid - kPtS] = rtab;
+        __syncthreads();
+        if (act) row_gridx_half(A, xi, was, f, false, 1.0, h);
+        // the surface rows (two dependent loads), by the lanes gridx leaves idle
+        for (int e = tid - 192; e >= 0 && e < 4 * kIX; e += kGpThreads - 192)
+            fsr[e] = quad_fsr(bc, &PT->fband[0][0], j * kIX + (e >> 2), e & 3);
+    }
+    __syncthreads();
+    stamp(dbg, 0, 1);
+    const PhysTables *PTl = reinterpret_cast<const PhysTables *>(ptl);  // (fband stays in PT)
+    const double cj = cosgr[j];
+    PairOut po;
+    if (tid < kIX) {  // grid-point dynamics of column i -> F in B[i][f], then its products
+        const int i = tid;
+        auto g = [&](int f) { return f >= n1 ? A[i * kRowLd + f] * cj : A[i * kRowLd + f]; };
+        double dummy[kKX];
+        gridpoint_column(j, n1, g, false, dummy, dummy, dummy, dummy, [&](int f, double v) { B[i * kRowLd + f] = v; },
+                         &gpt, false);
+        // (the products below kNFwdScaled are vdspec inputs: x cosgr(j) here, not in specx)
+        gridpoint_products(n1, g, [&](int f, double v) { B[i * kRowLd + f] = f < kNFwdScaled ? v * cj : v; }, &gpt);
+    } else if (tid >= 128 && tid < 128 + kIX) {  // the moist / diffusion part of column i's phypar
+        const int i = tid - 128;
+        const double *Ai = A + i * kRowLd;
+        double ta[kKX], qa[kKX], ph[kKX];
+#pragma unroll
+        for (int k = 0; k < kKX; ++k) {
+            ta[k] = Ai[kPT1 + k];
+            qa[k] = Ai[kPQ1 + k];
+            ph[k] = Ai[kPPhi1 + k];
+        }
+        PhysThermo h;
+        phys_thermo(ta, qa, ph, Ai[kPPs1], PTl, h);
+        double tt[kKX], qt[kKX], precnv, precls, ttv[kKX], qtv[kKX];
+        int itop, icnv;
+        phys_moist(h, PTl, tt, qt, precnv, precls, itop, icnv);
+        phys_vdif(h, ph, icnv, PTl, ttv, qtv);
+        double *Bh = B + i * kRowLd + kNFwd;
+        // tt[0] is +0 always (convection and condensation leave the top level alone)
+#pragma unroll
+        for (int k = 1; k < kKX; ++k) Bh[k - 1] = tt[k];
+#pragma unroll
+        for (int k = 0; k < kKX; ++k) Bh[7 + k] = ttv[k];
+#pragma unroll
+        for (int k = 0; k < kKX - 1; ++k) Bh[15 + k] = qt[k] + qtv[k];  // final above the surface layer
+        Bh[22] = qt[kKX - 1];
+        Bh[23] = qtv[kKX - 1];
+    } else if (isp) {  // the longwave / surface chain (and the shortwave) of column pi, two lanes
+        PairPre pre;
+        if (!lradsw) {
+#pragma unroll
+            for (int b = 0; b < 2; ++b)
+#pragma unroll
+                for (int k = 0; k < kKX; ++k)
+                    pre.tau[b][k] = rad[kRadTau2 + ((size_t)(2 * ph_ + b) * kKX + k) * kNGP + ppt];
+            pre.strat0 = rad[kRadStratc + ppt];
+            pre.strat1 = rad[kRadStratc + kNGP + ppt];
+            pre.ssrd = rad[kRadSsrd + ppt];
+#pragma unroll
+            for (int s = 0; s < 4; ++s) pre.ttrsw[s] = rad[kRadTtRsw + (size_t)(4 * ph_ + s) * kNGP + ppt];
+        }
+        const double *Ai = A + pi * kRowLd;
+        const double u7 = Ai[n1 + 2 * kKX + 2 + kKX - 1] * cj, v7 = Ai[n1 + 3 * kKX + 2 + kKX - 1] * cj;
+        const double fs2[2] = {fsr[4 * pi + 2 * ph_], fsr[4 * pi + 2 * ph_ + 1]};
+        phys_pair<kPT1, kPQ1, kPPhi1, kPPs1>(ph_, ppt, j, Ai, u7, v7, pre, bc, rad, PTl, &PT->fband[0][0], fs2,
+                                             lradsw != 0, po);
+    }
+    __syncthreads();
+    if (isp) {  // phys_column's sums (phy_phypar.f90:174-196), the pair lane's four levels
+        const double *Bh = B + pi * kRowLd + kNFwd;
+        double *Bi = B + pi * kRowLd;
+        const double rps = po.rps;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const int k = 4 * ph_ + s;
+            const double ttk = (k == 0 ? 0.0 : Bh[k > 0 ? k - 1 : 0]) + po.rsw[s] + po.rlw[s];
+            double ttv = Bh[7 + k], utv = 0., vtv = 0.;
+            double qtk;
+            if (k == kKX - 1) {
+                utv = utv + po.ust * rps * PTl->grdsig[kKX - 1];
+                vtv = vtv + po.vst * rps * PTl->grdsig[kKX - 1];
+                ttv = ttv + po.shf * rps * PTl->grdscp[kKX - 1];
+                const double qtv = Bh[23] + po.evp * rps * PTl->grdsig[kKX - 1];
+                qtk = Bh[22] + qtv;
+            } else {
+                qtk = Bh[15 + k];
+            }
+            // F + P where grtend adds phypar's tendencies (u 0..7, v 24..31, t 56..63, q 64..71)
+            Bi[k] = (Bi[k] + (0. + utv)) * cj;  // (x cosgr(j): a vdspec input, scaled here for specx)
+            Bi[3 * kKX + k] = (Bi[3 * kKX + k] + (0. + vtv)) * cj;
+            Bi[7 * kKX + k] = Bi[7 * kKX + k] + (ttk + ttv);
+            Bi[8 * kKX + k] = Bi[8 * kKX + k] + qtk;
+        }
+    }
+    __syncthreads();
+    stamp(dbg, 0, 2);
+    // specx: transform f on lanes 2 f, 2 f + 1, lane h on the samples 2 i + h
+    {
+        const int f = tid >> 1, h = tid & 1;
+        const bool act = f < kNFwd;
+        double x[48];
+        if (act) {
+            const double *fr = B + f + h * kRowLd;
+#pragma unroll
+            for (int i = 0; i < 48; ++i) x[i] = fr[2 * i * kRowLd];
+            fft::rfftf48_reg(x, was);
+        }
+        __syncthreads();  // A's P columns are read: A becomes the pairs' meeting place
+        row_specx_pair(x, A, act, vfm, was, f, j, h, kWT);
+        (void)wt;
+    }
+    stamp(dbg, 0, 3);
+}
+
 // specy's MFMA B operands in lane order: lane l = 16 kk + r of k-step s takes
 // pfwd[m][n][j] at n = 2 r (S) and 2 r + 1 (D), j = 4 s + kk ([m][n 32][lat 24], the
 // spectral context's forward Legendre table) -> pfl[m][s][l][2]
@@ -2361,7 +2522,7 @@ extern "C" int sml_dyn_create(double radius, sml_dynamics **out) {
     build_phys_tables(d->tab, &d->ptab);
     if (const char *e = std::getenv("SML_DYN_FUSED")) d->fused = *e && *e != '0';
     if (const char *e = std::getenv("SML_DYN_SPLIT_GRID")) d->split_grid = *e && *e != '0';
-    if (const char *e = std::getenv("SML_DYN_QUAD")) d->quad = *e && *e != '0';
+    if (const char *e = std::getenv("SML_DYN_QUAD")) d->quad = std::max(0, std::min(2, std::atoi(e)));
     if (const char *e = std::getenv("SML_DYN_NOGRAPH")) d->nograph = *e && *e != '0';
     if (const char *e = std::getenv("SML_DYN_WT")) d->wt = std::max(0, std::min(3, std::atoi(e)));
     if (const char *e = std::getenv("SML_CHK_FLAG")) d->chk_flag = *e != '0';
@@ -2592,7 +2753,11 @@ int launch_step_fused(sml_dynamics *d, int j1, int j2, double dt, double alph, d
                                sd.wa, sd.cosgr, d->d_dbg);
         } else {
             const bool wrow = d->wt == 1 || d->wt == 2;
-            if (d->quad)
+            if (d->quad == 2)
+                hipLaunchKernelGGL(wrow ? k_st_gridspec_p<true> : k_st_gridspec_p<false>, dim3(kIL), dim3(kGpThreads), 0,
+                                   st, d->d_varm, d->d_vfm, sd.wa, sd.cosgr, T, d->d_pbc, d->d_rad, d->d_ptab,
+                                   lradsw ? 1 : 0, wrow ? 1 : 0, d->d_dbg);
+            else if (d->quad == 1)
                 hipLaunchKernelGGL(wrow ? k_st_gridspec_q<true> : k_st_gridspec_q<false>, dim3(kIL), dim3(kGqThreads), 0,
                                    st, d->d_varm, d->d_vfm, sd.wa, sd.cosgr, T, d->d_pbc, d->d_rad, d->d_ptab,
                                    lradsw ? 1 : 0, wrow ? 1 : 0, d->d_dbg);
