@@ -1868,6 +1868,9 @@ __global__ __launch_bounds__(kGpThreads) void k_st_gridspec_p(
     const PhysTables *PTl = reinterpret_cast<const PhysTables *>(ptl);  // (fband stays in PT)
     const double cj = cosgr[j];
     PairOut po;
+    SML_PST_T(8, 0);
+    SML_PST_T(10, 128);
+    SML_PST_T(14, 256);
     if (tid < kIX) {  // grid-point dynamics of column i -> F in B[i][f], then its products
         const int i = tid;
         auto g = [&](int f) { return f >= n1 ? A[i * kRowLd + f] * cj : A[i * kRowLd + f]; };
@@ -1876,6 +1879,7 @@ __global__ __launch_bounds__(kGpThreads) void k_st_gridspec_p(
                          &gpt, false);
         // (the products below kNFwdScaled are vdspec inputs: x cosgr(j) here, not in specx)
         gridpoint_products(n1, g, [&](int f, double v) { B[i * kRowLd + f] = f < kNFwdScaled ? v * cj : v; }, &gpt);
+        SML_PST_T(9, 0);
     } else if (tid >= 128 && tid < 128 + kIX) {  // the moist / diffusion part of column i's phypar
         const int i = tid - 128;
         const double *Ai = A + i * kRowLd;
@@ -1888,9 +1892,11 @@ __global__ __launch_bounds__(kGpThreads) void k_st_gridspec_p(
         }
         PhysThermo h;
         phys_thermo(ta, qa, ph, Ai[kPPs1], PTl, h);
+        SML_PST_T(11, 128);
         double tt[kKX], qt[kKX], precnv, precls, ttv[kKX], qtv[kKX];
         int itop, icnv;
         phys_moist(h, PTl, tt, qt, precnv, precls, itop, icnv);
+        SML_PST_T(12, 128);
         phys_vdif(h, ph, icnv, PTl, ttv, qtv);
         double *Bh = B + i * kRowLd + kNFwd;
         // tt[0] is +0 always (convection and condensation leave the top level alone)
@@ -1902,6 +1908,7 @@ __global__ __launch_bounds__(kGpThreads) void k_st_gridspec_p(
         for (int k = 0; k < kKX - 1; ++k) Bh[15 + k] = qt[k] + qtv[k];  // final above the surface layer
         Bh[22] = qt[kKX - 1];
         Bh[23] = qtv[kKX - 1];
+        SML_PST_T(13, 128);
     } else if (isp) {  // the longwave / surface chain (and the shortwave) of column pi, two lanes
         PairPre pre;
         if (!lradsw) {
@@ -1921,8 +1928,11 @@ __global__ __launch_bounds__(kGpThreads) void k_st_gridspec_p(
         const double fs2[2] = {fsr[4 * pi + 2 * ph_], fsr[4 * pi + 2 * ph_ + 1]};
         phys_pair<kPT1, kPQ1, kPPhi1, kPPs1>(ph_, ppt, j, Ai, u7, v7, pre, bc, rad, PTl, &PT->fband[0][0], fs2,
                                              lradsw != 0, po);
+        SML_PST_T(18, 256);
+        SML_PST_T(19, 384);
     }
     __syncthreads();
+    SML_PST_T(20, 256);
     if (isp) {  // phys_column's sums (phy_phypar.f90:174-196), the pair lane's four levels
         const double *Bh = B + pi * kRowLd + kNFwd;
         double *Bi = B + pi * kRowLd;

@@ -250,6 +250,7 @@ __device__ __forceinline__ void phys_pair(int h, int pt, int jlat, const double 
         for (int j = 0; j < 4; ++j) rsw[j] = pre.ttrsw[j];
     }
 
+    SML_PST_T(15, 256);
     if (lradsw) load_fbq();
     // 3.2 radlw(-1) (phy_radiat.f90:330-413): the blackbody terms on both lanes, bands
     // 2h, 2h + 1's downward fluxes after each level
@@ -334,6 +335,7 @@ __device__ __forceinline__ void phys_pair(int h, int pt, int jlat, const double 
         dl[j] = L == NL - 1 ? dc : d;
     }
     const double slrd = fsfcd;
+    SML_PST_T(16, 256);
 
     // 3.3 suflux with lfluxland = .true. (phy_suflux.f90:1-355), both lanes
     double ustr3, vstr3, shf3, evap3, slru3;
@@ -408,6 +410,7 @@ __device__ __forceinline__ void phys_pair(int h, int pt, int jlat, const double 
         slru3 = slru2 + fmask * (slru1 - slru2);
     }
 
+    SML_PST_T(17, 256);
     // 3.4 radlw(1) (phy_radiat.f90:414-458): bands 2h, 2h + 1 upward
     const double refsfc = 1. - emisfc, fsfcu = slru3;
     double fu[2][NL], fs0[2];  // band 2h + b's flux after level k going up; its surface start
