@@ -1832,11 +1832,27 @@ __global__ __launch_bounds__(kGpThreads) void k_st_gridspec_p(
     __shared__ double ptl[kPtS];
     __shared__ GpTab gpt;
     __shared__ double fsr[4 * kIX];  // radlw(1)'s surface row per (column, band), quad_fsr
+    constexpr int kMh = 3 + kKX;
+    __shared__ double mhs[kIX * kMh];  // a shortwave step's moist-part hand-over (precnv, precls, itop, rh)
     constexpr int n1 = kNInv1P;
     constexpr int nphys = (n1 - kPT1) + (kNInvP - (n1 + 2 * kKX + 2));  // 25 + 16 = 41
     const int j = blockIdx.x, tid = threadIdx.x;
     const bool isp = tid >= 256 && tid < 256 + 2 * kIX;  // the longwave side's pairs
     const int pi = isp ? (tid - 256) >> 1 : 0, ph_ = tid & 1, ppt = j * kIX + pi;
+    // a longwave-only step's radiation state of the pair lane (bands 2h, 2h + 1, its levels)
+    auto pair_pre_load = [&](PairPre &pre) {
+        if (lradsw) return;
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int k = 0; k < kKX; ++k)
+                pre.tau[b][k] = rad[kRadTau2 + ((size_t)(2 * ph_ + b) * kKX + k) * kNGP + ppt];
+        pre.strat0 = rad[kRadStratc + ppt];
+        pre.strat1 = rad[kRadStratc + kNGP + ppt];
+        pre.ssrd = rad[kRadSsrd + ppt];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) pre.ttrsw[s] = rad[kRadTtRsw + (size_t)(4 * ph_ + s) * kNGP + ppt];
+    };
     stamp(dbg, 0, 0);
     double rtab = 0.0;
     if (tid < kPtS) {
@@ -1880,54 +1896,61 @@ __global__ __launch_bounds__(kGpThreads) void k_st_gridspec_p(
         // (the products below kNFwdScaled are vdspec inputs: x cosgr(j) here, not in specx)
         gridpoint_products(n1, g, [&](int f, double v) { B[i * kRowLd + f] = f < kNFwdScaled ? v * cj : v; }, &gpt);
         SML_PST_T(9, 0);
-    } else if (tid >= 128 && tid < 128 + kIX) {  // the moist / diffusion part of column i's phypar
-        const int i = tid - 128;
-        const double *Ai = A + i * kRowLd;
-        double ta[kKX], qa[kKX], ph[kKX];
+    }
+    // the moist / diffusion part of column i's phypar (waves 2-3); on a shortwave step its
+    // moist part's results go to the longwave side through mhs at a block barrier
+    const bool ism = tid >= 128 && tid < 128 + kIX;
+    const int mi = ism ? tid - 128 : 0;
+    PhysThermo mth;
+    double mtt[kKX], mqt[kKX], mph[kKX];
+    int micnv = 0;
+    if (ism) {
+        const double *Ai = A + mi * kRowLd;
+        double ta[kKX], qa[kKX];
 #pragma unroll
         for (int k = 0; k < kKX; ++k) {
             ta[k] = Ai[kPT1 + k];
             qa[k] = Ai[kPQ1 + k];
-            ph[k] = Ai[kPPhi1 + k];
+            mph[k] = Ai[kPPhi1 + k];
         }
-        PhysThermo h;
-        phys_thermo(ta, qa, ph, Ai[kPPs1], PTl, h);
+        phys_thermo(ta, qa, mph, Ai[kPPs1], PTl, mth);
         SML_PST_T(11, 128);
-        double tt[kKX], qt[kKX], precnv, precls, ttv[kKX], qtv[kKX];
-        int itop, icnv;
-        phys_moist(h, PTl, tt, qt, precnv, precls, itop, icnv);
+        double precnv, precls;
+        int itop;
+        phys_moist(mth, PTl, mtt, mqt, precnv, precls, itop, micnv);
         SML_PST_T(12, 128);
-        phys_vdif(h, ph, icnv, PTl, ttv, qtv);
-        double *Bh = B + i * kRowLd + kNFwd;
+        if (lradsw) {
+            double *m = mhs + mi * kMh;
+            m[0] = precnv;
+            m[1] = precls;
+            m[2] = (double)itop;
+#pragma unroll
+            for (int k = 0; k < kKX; ++k) m[3 + k] = mth.rh[k];
+        }
+    }
+    if (lradsw) __syncthreads();
+    if (ism) {
+        double ttv[kKX], qtv[kKX];
+        phys_vdif(mth, mph, micnv, PTl, ttv, qtv);
+        double *Bh = B + mi * kRowLd + kNFwd;
         // tt[0] is +0 always (convection and condensation leave the top level alone)
 #pragma unroll
-        for (int k = 1; k < kKX; ++k) Bh[k - 1] = tt[k];
+        for (int k = 1; k < kKX; ++k) Bh[k - 1] = mtt[k];
 #pragma unroll
         for (int k = 0; k < kKX; ++k) Bh[7 + k] = ttv[k];
 #pragma unroll
-        for (int k = 0; k < kKX - 1; ++k) Bh[15 + k] = qt[k] + qtv[k];  // final above the surface layer
-        Bh[22] = qt[kKX - 1];
+        for (int k = 0; k < kKX - 1; ++k) Bh[15 + k] = mqt[k] + qtv[k];  // final above the surface layer
+        Bh[22] = mqt[kKX - 1];
         Bh[23] = qtv[kKX - 1];
         SML_PST_T(13, 128);
     } else if (isp) {  // the longwave / surface chain (and the shortwave) of column pi, two lanes
         PairPre pre;
-        if (!lradsw) {
-#pragma unroll
-            for (int b = 0; b < 2; ++b)
-#pragma unroll
-                for (int k = 0; k < kKX; ++k)
-                    pre.tau[b][k] = rad[kRadTau2 + ((size_t)(2 * ph_ + b) * kKX + k) * kNGP + ppt];
-            pre.strat0 = rad[kRadStratc + ppt];
-            pre.strat1 = rad[kRadStratc + kNGP + ppt];
-            pre.ssrd = rad[kRadSsrd + ppt];
-#pragma unroll
-            for (int s = 0; s < 4; ++s) pre.ttrsw[s] = rad[kRadTtRsw + (size_t)(4 * ph_ + s) * kNGP + ppt];
-        }
+        pair_pre_load(pre);  // (before gridx instead: the gridx lanes' registers spilled, gridx 3.3 -> 3.9 us)
         const double *Ai = A + pi * kRowLd;
         const double u7 = Ai[n1 + 2 * kKX + 2 + kKX - 1] * cj, v7 = Ai[n1 + 3 * kKX + 2 + kKX - 1] * cj;
         const double fs2[2] = {fsr[4 * pi + 2 * ph_], fsr[4 * pi + 2 * ph_ + 1]};
         phys_pair<kPT1, kPQ1, kPPhi1, kPPs1>(ph_, ppt, j, Ai, u7, v7, pre, bc, rad, PTl, &PT->fband[0][0], fs2,
-                                             lradsw != 0, po);
+                                             mhs + pi * kMh, lradsw != 0, po);
         SML_PST_T(18, 256);
         SML_PST_T(19, 384);
     }

@@ -50,12 +50,13 @@ __device__ __forceinline__ double oth(const double (&a)[kKX], int h, int j) { re
 // The longwave / surface chain of column pt on pair lane h (and the shortwave before it
 // on a lradsw step).  Ai: the column's row in A (t, q, phi at kOT / kOQ / kOPhi + k,
 // log ps at kOPs); u7 / v7: the bottom level's wind (x cosgr); fsr: fband(nint(tsfc),
-// 2h + b) for b = 0, 1; P: PhysTables (LDS copy); fbt: fband (global).
+// 2h + b) for b = 0, 1; P: PhysTables (LDS copy); fbt: fband (global); mh: on a
+// shortwave step the moist side's precnv, precls, itop and rh of the column (LDS).
 template <int kOT, int kOQ, int kOPhi, int kOPs>
 __device__ __forceinline__ void phys_pair(int h, int pt, int jlat, const double *Ai, double u7, double v7,
                                           const PairPre &pre, const double *__restrict__ bc, double *__restrict__ rad,
                                           const PhysTables *P, const double *__restrict__ fbt, const double (&fsr)[2],
-                                          bool lradsw, PairOut &o) {
+                                          const double *mh, bool lradsw, PairOut &o) {
     using namespace phys;
     using pairx::oth;
     using pairx::own;
@@ -85,18 +86,22 @@ __device__ __forceinline__ void phys_pair(int h, int pt, int jlat, const double 
     double psg, rps, qc[NL];
     double tq[2][NL], strat0, strat1, ssrd, rsw[4];
     if (lradsw) {
-        // the moist part on the whole column (phys_column's order: the shortwave needs its
-        // precipitation and cloud top), then cloud and radsw (phys_sw) level- and band-split
-        PhysThermo th;
-        phys_thermo(ta, qa, ph, ps1, P, th);
-        double tt[NL], qt[NL], precnv, precls;
-        int itop, icnv;
-        phys_moist(th, P, tt, qt, precnv, precls, itop, icnv);
-        psg = th.psg;
-        rps = th.rps;
+        // the moist part's results from the moist side (mh: precnv, precls, itop, rh(1..8),
+        // phys_moist / phys_thermo's values, handed over at the block barrier of a
+        // shortwave step), then cloud and radsw (phys_sw) level- and band-split
+        psg = exp(ps1);
+        rps = 1. / psg;
 #pragma unroll
-        for (int k = 0; k < NL; ++k) qc[k] = th.qa[k];
-        const double *qa_ = th.qa, *se = th.se, *rh = th.rh;
+        for (int k = 0; k < NL; ++k) qc[k] = fmax(qa[k], 0.);
+        const double precnv = mh[0], precls = mh[1];
+        const int itop = (int)mh[2];
+        double rh[NL], se[NL];
+#pragma unroll
+        for (int k = 0; k < NL; ++k) {
+            rh[k] = mh[3 + k];
+            se[k] = cp * ta[k] + ph[k];
+        }
+        const double *qa_ = qc;
         const double gse = (se[NL - 2] - se[NL - 1]) / (ph[NL - 2] - ph[NL - 1]);
         constexpr int nlp = NL + 1;
         const double rrcl = 1. / (rhcl2 - rhcl1);
