@@ -334,11 +334,11 @@ __global__ __launch_bounds__(256) void k_train_wout(const double *__restrict__ X
 // l = tid / TM + (256 / TM) q -- rows contiguous across lanes; transposed ones
 // (T = true, X(row, l) at p[row * ld + l]): row = tid / (kKC / PER), l = PER
 // (tid % (kKC / PER)) + q -- PER contiguous values per lane.
-template <int TM, bool T>
+template <int TM, bool T, int KC = kKC>
 struct TileLoader {
-    static constexpr int PER = kKC * TM / 256;
-    __device__ static int row(int tid) { return T ? tid / (kKC / PER) : tid % TM; }
-    __device__ static int l(int tid, int q) { return T ? (tid % (kKC / PER)) * PER + q : tid / TM + (256 / TM) * q; }
+    static constexpr int PER = KC * TM / 256;
+    __device__ static int row(int tid) { return T ? tid / (KC / PER) : tid % TM; }
+    __device__ static int l(int tid, int q) { return T ? (tid % (KC / PER)) * PER + q : tid / TM + (256 / TM) * q; }
 };
 
 // One TR x TC output tile (4 waves, wave (wr, wc) owns (TR/2) x (TC/2) = (TR/32) x
@@ -351,17 +351,18 @@ struct TileLoader {
 // launch's latency.
 // lower: the tile is on the diagonal of a symmetric update and only its lower triangle
 // is read later -- the wave above the diagonal (wr < wc) loads its share of the LDS
-// stages and skips its MFMAs and stores
-template <int TR, int TC, bool AT, bool BT>
+// stages and skips its MFMAs and stores.  KC: values of l per LDS stage (the MFMA chain
+// of an element runs over l in the same order whatever KC)
+template <int TR, int TC, bool AT, bool BT, int KC = kKC>
 __device__ __forceinline__ void gemm_tile(const double *__restrict__ pa, long long lda, int arows,
                                           const double *__restrict__ pb, long long ldb, int brows, double *po,
                                           long long ldo, double alpha, bool accumulate, int K = kTile,
                                           bool lower = false) {
-    using LA = TileLoader<TR, AT>;
-    using LB = TileLoader<TC, BT>;
+    using LA = TileLoader<TR, AT, KC>;
+    using LB = TileLoader<TC, BT, KC>;
     constexpr int NI = TR / 32, NJ = TC / 32;
-    __shared__ double sA[kKC][TR + kLdsPad];
-    __shared__ double sB[kKC][TC + kLdsPad];
+    __shared__ double sA[KC][TR + kLdsPad];
+    __shared__ double sB[KC][TC + kLdsPad];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int wr = w >> 1, wc = w & 1, l16 = lane & 15, kk = lane >> 4;
     const int arow = LA::row(tid), brow = LB::row(tid);
@@ -385,17 +386,17 @@ __device__ __forceinline__ void gemm_tile(const double *__restrict__ pa, long lo
 #pragma unroll
         for (int j = 0; j < NJ; ++j) acc[i][j] = d4{0, 0, 0, 0};
     fetch(0);
-    for (int t0 = 0; t0 < K; t0 += kKC) {
+    for (int t0 = 0; t0 < K; t0 += KC) {
         __syncthreads();
 #pragma unroll
         for (int q = 0; q < LA::PER; ++q) sA[LA::l(tid, q)][arow] = ra[q];
 #pragma unroll
         for (int q = 0; q < LB::PER; ++q) sB[LB::l(tid, q)][brow] = rb[q];
         __syncthreads();
-        if (t0 + kKC < K) fetch(t0 + kKC);
+        if (t0 + KC < K) fetch(t0 + KC);
         if (lower && wr < wc) continue;  // wave-uniform
 #pragma unroll
-        for (int s = 0; s < kKC / 4; ++s) {
+        for (int s = 0; s < KC / 4; ++s) {
             double a[NI], b[NJ];
 #pragma unroll
             for (int i = 0; i < NI; ++i) a[i] = sA[4 * s + kk][wr * (TR / 2) + i * 16 + l16];
@@ -703,7 +704,9 @@ __global__ __launch_bounds__(256, 3) void k_chol_panel(double *__restrict__ G, c
 
 // A_ij -= sum_{k0 <= k < k0 + kw} L_ik L_jk^T for the lower-triangle tiles j <= i
 // of block columns jlo <= j < jhi: one GEMM of depth 128 kw per tile (the block
-// columns of L are contiguous in the column-major G).
+// columns of L are contiguous in the column-major G).  KC: the GEMM's LDS stage depth
+// (SML_CHOL_KC)
+template <int KC>
 __global__ __launch_bounds__(256, 2) void k_chol_update(double *__restrict__ G, int npad, int k0, int kw, int jlo,
                                                      int jhi, const TrainRegion *__restrict__ regs) {
     const int r = blockIdx.y, C = npad / kTile;
@@ -716,7 +719,29 @@ __global__ __launch_bounds__(256, 2) void k_chol_update(double *__restrict__ G, 
     const double *Lik = Gr + (size_t)k0 * kTile * npad + (size_t)i * kTile;
     const double *Ljk = Gr + (size_t)k0 * kTile * npad + (size_t)j * kTile;
     double *Aij = Gr + (size_t)j * kTile * npad + (size_t)i * kTile;
-    gemm_tile<128, 128, false, false>(Lik, npad, kTile, Ljk, npad, kTile, Aij, npad, -1.0, true, kw * kTile, i == j);
+    gemm_tile<128, 128, false, false, KC>(Lik, npad, kTile, Ljk, npad, kTile, Aij, npad, -1.0, true, kw * kTile,
+                                          i == j);
+}
+
+// Block column k > k0 of a panel below its diagonal, fused (default; SML_CHOL_FUSE=0:
+// k_chol_update then k_chol_panel): rows r0 .. r0 + 63 of block i take the left-looking
+// update by the panel's earlier block columns k0 .. k - 1 (k_chol_update's GEMM, in place),
+// then L_ik = A_ik L_kk^-T (k_chol_panel's GEMM) on the same rows, read back from L2 by the
+// workgroup that wrote them -- one HBM read of the slab instead of two, one launch fewer
+// per block column.  The same sums per element as the two launches (the tile shape does
+// not change an element's MFMA chain), so the factor is bitwise the same.
+__global__ __launch_bounds__(256, 3) void k_chol_upanel(double *__restrict__ G, const double *__restrict__ linv,
+                                                     int npad, int k0, int k, const TrainRegion *__restrict__ regs) {
+    const int r = blockIdx.y, C = npad / kTile, i = k + 1 + (blockIdx.x >> 1), r0 = (blockIdx.x & 1) * 64;
+    if (i >= live_blocks(regs, r)) return;  // A_ik = 0: L_ik = 0
+    double *Gr = G + (size_t)r * npad * npad;
+    const double *Lip = Gr + (size_t)k0 * kTile * npad + (size_t)i * kTile + r0;
+    const double *Lkp = Gr + (size_t)k0 * kTile * npad + (size_t)k * kTile;
+    double *A = Gr + (size_t)k * kTile * npad + (size_t)i * kTile + r0;
+    gemm_tile<64, 128, false, false>(Lip, npad, 64, Lkp, npad, kTile, A, npad, -1.0, true, (k - k0) * kTile);
+    __syncthreads();  // the slab's updated rows, stored by every wave, before any is read
+    const double *Li = linv + ((size_t)r * C + k) * kTile * kTile;
+    gemm_tile<64, 128, false, false>(A, npad, 64, Li, kTile, kTile, A, npad, 1.0, false);
 }
 
 static int update_tiles(int C, int jlo, int jhi) {
@@ -843,6 +868,10 @@ struct sml_train {
     bool rhs_split = true;
     // the blocked diagonal factor (k_chol_diag_b); SML_CHOL_DIAG=1: k_chol_diag
     bool diag_b = true;
+    // the in-panel update fused with the panel (k_chol_upanel); SML_CHOL_FUSE=0: two launches
+    bool fuse = true;
+    // the trailing update's LDS stage depth (SML_CHOL_KC: 16 or 32)
+    int update_kc = kKC;
     std::vector<int> naug;
     TrainRegion *d_regs = nullptr;
     double *d_G = nullptr, *d_B = nullptr;
@@ -885,6 +914,8 @@ extern "C" int sml_train_create(int nlocal, const int *naug, int nout, sml_train
     if (const char *e = getenv("SML_GRAM_V")) t->gram = atoi(e) == 1 ? 1 : 2;       // A/B knob
     if (const char *e = getenv("SML_SOLVE_SPLIT")) t->rhs_split = *e != '0';        // A/B knob
     if (const char *e = getenv("SML_CHOL_DIAG")) t->diag_b = atoi(e) != 1;          // A/B knob
+    if (const char *e = getenv("SML_CHOL_FUSE")) t->fuse = *e != '0';               // A/B knob
+    if (const char *e = getenv("SML_CHOL_KC")) t->update_kc = atoi(e) == 32 ? 32 : kKC;  // A/B knob
     t->naug.assign(naug, naug + nlocal);
     int mx = 0;
     for (int i = 0; i < nlocal; ++i) {
@@ -982,22 +1013,27 @@ extern "C" int sml_train_solve(sml_train *t, int ncs, double beta_res, double be
     for (int p0 = 0; p0 < C; p0 += P) {
         const int p1 = std::min(C, p0 + P);
         for (int k = p0; k < p1; ++k) {
+            const bool fused = t->fuse && k > p0;  // (then the update launch covers the diagonal tile only)
             if (k > p0)
-                hipLaunchKernelGGL(k_chol_update, dim3(C - k, nl), dim3(256), 0, st, t->d_G, npad, p0, k - p0, k,
-                                   k + 1, t->d_regs);
+                hipLaunchKernelGGL(k_chol_update<kKC>, dim3(fused ? 1 : C - k, nl), dim3(256), 0, st, t->d_G, npad, p0,
+                                   k - p0, k, k + 1, t->d_regs);
             if (t->diag_b)
                 hipLaunchKernelGGL(k_chol_diag_b, dim3(nl), dim3(kDiagThreads), kDiagBLds, st, t->d_G, t->d_linv, npad,
                                    k, t->d_info, t->d_regs);
             else
                 hipLaunchKernelGGL(k_chol_diag, dim3(nl), dim3(kDiagThreads), kDiagLds, st, t->d_G, t->d_linv, npad, k,
                                    t->d_info, t->d_regs);
-            if (k < C - 1)
+            if (k < C - 1 && fused)
+                hipLaunchKernelGGL(k_chol_upanel, dim3(2 * (C - 1 - k), nl), dim3(256), 0, st, t->d_G, t->d_linv,
+                                   npad, p0, k, t->d_regs);
+            else if (k < C - 1)
                 hipLaunchKernelGGL(k_chol_panel, dim3(2 * (C - 1 - k), nl), dim3(256), 0, st, t->d_G, t->d_linv,
                                    npad, k, t->d_regs);
         }
-        if (p1 < C)
-            hipLaunchKernelGGL(k_chol_update, dim3(update_tiles(C, p1, C), nl), dim3(256), 0, st, t->d_G, npad, p0,
-                               p1 - p0, p1, C, t->d_regs);
+        if (p1 < C)  // the trailing update (72 % of the solve's time)
+            hipLaunchKernelGGL((t->update_kc == 32 ? k_chol_update<32> : k_chol_update<kKC>),
+                               dim3(update_tiles(C, p1, C), nl), dim3(256), 0, st, t->d_G, npad, p0, p1 - p0, p1, C,
+                               t->d_regs);
     }
     // potrs, blocked by panels of P block rows: inside a panel, right-looking (block
     // row k's diagonal inverse, then its update of the panel's remaining rows at
