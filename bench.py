@@ -211,7 +211,9 @@ def dry_run(args) -> None:
         if rank == 0:
             print(json.dumps({"dry_run": "gloo", "n_gpus": world, "ranks": allv}), flush=True)
         return
-    print(json.dumps({"dry_run": "env", "n_gpus": world, "rank": me}), flush=True)
+    # one write per line (print's text and newline are two): the ranks share the stderr pipe
+    sys.stdout.write(json.dumps({"dry_run": "env", "n_gpus": world, "rank": me}) + "\n")
+    sys.stdout.flush()
 
 
 def log(rank, *a):
