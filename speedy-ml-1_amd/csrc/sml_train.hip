@@ -744,6 +744,22 @@ __global__ __launch_bounds__(256, 3) void k_chol_upanel(double *__restrict__ G, 
     gemm_tile<64, 128, false, false>(A, npad, 64, Li, kTile, kTile, A, npad, 1.0, false);
 }
 
+// The left-looking update of a panel's diagonal tile (k, k) by block columns k0 .. k - 1
+// on the fused path, as three workgroups per region: the 64 x 64 quadrants (0, 0), (1, 0),
+// (1, 1) -- exactly the waves k_chol_update's lower tile runs (its quadrant above the
+// diagonal skipped), each quadrant's chain on four waves instead of one, three times
+// the workgroups for a launch of one tile per region.  Bitwise the 128 x 128 form.
+__global__ __launch_bounds__(256, 2) void k_chol_update_diag(double *__restrict__ G, int npad, int k0, int k,
+                                                          const TrainRegion *__restrict__ regs) {
+    const int r = blockIdx.y, q = blockIdx.x, r0 = q == 0 ? 0 : 64, c0 = q == 2 ? 64 : 0;
+    if (k >= live_blocks(regs, r)) return;  // (padding block columns are never factored)
+    double *Gr = G + (size_t)r * npad * npad;
+    const double *Lkp = Gr + (size_t)k0 * kTile * npad + (size_t)k * kTile;
+    double *Akk = Gr + (size_t)k * kTile * npad + (size_t)k * kTile;
+    gemm_tile<64, 64, false, false>(Lkp + r0, npad, 64, Lkp + c0, npad, 64, Akk + (size_t)c0 * npad + r0, npad, -1.0,
+                                    true, (k - k0) * kTile);
+}
+
 static int update_tiles(int C, int jlo, int jhi) {
     int n = 0;
     for (int j = jlo; j < jhi; ++j) n += C - j;
@@ -870,6 +886,9 @@ struct sml_train {
     bool diag_b = true;
     // the in-panel update fused with the panel (k_chol_upanel); SML_CHOL_FUSE=0: two launches
     bool fuse = true;
+    // the fused path's diagonal-tile update as three 64 x 64 quadrants (k_chol_update_diag);
+    // SML_CHOL_DSPLIT=0: one 128 x 128 lower tile
+    bool diag_split = true;
     // the trailing update's LDS stage depth (SML_CHOL_KC: 16 or 32)
     int update_kc = kKC;
     std::vector<int> naug;
@@ -915,6 +934,7 @@ extern "C" int sml_train_create(int nlocal, const int *naug, int nout, sml_train
     if (const char *e = getenv("SML_SOLVE_SPLIT")) t->rhs_split = *e != '0';        // A/B knob
     if (const char *e = getenv("SML_CHOL_DIAG")) t->diag_b = atoi(e) != 1;          // A/B knob
     if (const char *e = getenv("SML_CHOL_FUSE")) t->fuse = *e != '0';               // A/B knob
+    if (const char *e = getenv("SML_CHOL_DSPLIT")) t->diag_split = *e != '0';      // A/B knob
     if (const char *e = getenv("SML_CHOL_KC")) t->update_kc = atoi(e) == 32 ? 32 : kKC;  // A/B knob
     t->naug.assign(naug, naug + nlocal);
     int mx = 0;
@@ -1014,7 +1034,9 @@ extern "C" int sml_train_solve(sml_train *t, int ncs, double beta_res, double be
         const int p1 = std::min(C, p0 + P);
         for (int k = p0; k < p1; ++k) {
             const bool fused = t->fuse && k > p0;  // (then the update launch covers the diagonal tile only)
-            if (k > p0)
+            if (fused && t->diag_split)
+                hipLaunchKernelGGL(k_chol_update_diag, dim3(3, nl), dim3(256), 0, st, t->d_G, npad, p0, k, t->d_regs);
+            else if (k > p0)
                 hipLaunchKernelGGL(k_chol_update<kKC>, dim3(fused ? 1 : C - k, nl), dim3(256), 0, st, t->d_G, npad, p0,
                                    k - p0, k, k + 1, t->d_regs);
             if (t->diag_b)
