@@ -776,7 +776,7 @@ static int update_tiles(int C, int jlo, int jhi) {
 template <bool AT, int NC>
 __device__ __forceinline__ void gemm_rhs(const double *__restrict__ pa, long long lda, const double *__restrict__ pb,
                                          long long ldb, int nb, double *po, long long ldo, double alpha,
-                                         bool accumulate, int K = kTile) {
+                                         bool accumulate, int K = kTile, bool te = false) {
     using LA = TileLoader<kTile, AT>;
     constexpr int NJ = NC / 16, PB = NC * kKC / 256;
     static_assert(NC % 16 == 0 && (NC * kKC) % 256 == 0, "column group");
@@ -824,6 +824,33 @@ __device__ __forceinline__ void gemm_rhs(const double *__restrict__ pa, long lon
                 for (int j = 0; j < NJ; ++j) acc[i][j] = MFMA64(a[i], b[j], acc[i][j]);
         }
     }
+    if (te) {
+        // each 16 x 16 tile transposed through the wave's LDS scratch (sA, free after the
+        // last stage), so a read-modify-write instruction covers 16 consecutive rows of 4
+        // columns (whole 128-B lines) instead of 4 rows of 16; the same expression per element
+        __syncthreads();
+        double *scr = &sA[0][0] + w * (16 * 17);
+        const int a = lane >> 4, b = lane & 15;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) scr[l16 * 17 + kk + 4 * q] = acc[i][j][q];
+                wave_sync();
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int c = 4 * q + a, row = w * 32 + i * 16 + b, col = j * 16 + c;
+                    const double v = scr[c * 17 + b];
+                    if (col < nb) {
+                        double *p = po + (long long)col * ldo + row;
+                        *p = (accumulate ? *p : 0.0) + alpha * v;
+                    }
+                }
+                wave_sync();
+            }
+        return;
+    }
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -845,12 +872,12 @@ __device__ __forceinline__ void gemm_rhs(const double *__restrict__ pa, long lon
 //   forward  (upper = 0): B_k = L_kk^-1 B_k        backward (upper = 1): B_k = L_kk^-T B_k
 template <bool upper, int NC>  // one gemm_rhs instance per kernel: its LDS stages are static
 __global__ __launch_bounds__(256, 2) void k_solve_diag(const double *__restrict__ linv, double *__restrict__ B, int npad,
-                                                    int nout, int k, const TrainRegion *__restrict__ regs) {
+                                                    int nout, int k, const TrainRegion *__restrict__ regs, int te) {
     const int r = blockIdx.y, C = npad / kTile, c0 = NC * blockIdx.z;
     if (k >= live_blocks(regs, r) || c0 >= nout) return;  // B_k = 0 (padding rows), L_kk = I
     const double *Li = linv + ((size_t)r * C + k) * kTile * kTile;
     double *Bk = B + (size_t)r * npad * nout + (size_t)c0 * npad + (size_t)k * kTile;
-    gemm_rhs<upper, NC>(Li, kTile, Bk, npad, nout - c0, Bk, npad, 1.0, false);
+    gemm_rhs<upper, NC>(Li, kTile, Bk, npad, nout - c0, Bk, npad, 1.0, false, kTile, te != 0);
 }
 
 // Update of block rows ilo <= i < ihi by the solved block rows [k0, k0 + kw), one
@@ -859,7 +886,7 @@ __global__ __launch_bounds__(256, 2) void k_solve_diag(const double *__restrict_
 template <bool upper, int NC>
 __global__ __launch_bounds__(256, 2) void k_solve_update(const double *__restrict__ G, double *__restrict__ B, int npad,
                                                       int nout, int k0, int kw, int ilo,
-                                                      const TrainRegion *__restrict__ regs) {
+                                                      const TrainRegion *__restrict__ regs, int te) {
     const int r = blockIdx.y, i = ilo + (int)blockIdx.x, c0 = NC * blockIdx.z;
     const int Cr = live_blocks(regs, r);
     // padding block rows stay 0; backward, solved rows k0.. past the data are 0
@@ -868,10 +895,10 @@ __global__ __launch_bounds__(256, 2) void k_solve_update(const double *__restric
     double *Br = B + (size_t)r * npad * nout + (size_t)c0 * npad;
     if constexpr (upper)  // A(rr, l) = L(k0 kTile + l, i kTile + rr): the transposed blocks (k, i)
         gemm_rhs<true, NC>(Gr + (size_t)i * kTile * npad + (size_t)k0 * kTile, npad, Br + (size_t)k0 * kTile, npad,
-                           nout - c0, Br + (size_t)i * kTile, npad, -1.0, true, kw * kTile);
+                           nout - c0, Br + (size_t)i * kTile, npad, -1.0, true, kw * kTile, te != 0);
     else
         gemm_rhs<false, NC>(Gr + (size_t)k0 * kTile * npad + (size_t)i * kTile, npad, Br + (size_t)k0 * kTile, npad,
-                            nout - c0, Br + (size_t)i * kTile, npad, -1.0, true, kw * kTile);
+                            nout - c0, Br + (size_t)i * kTile, npad, -1.0, true, kw * kTile, te != 0);
 }
 
 }  // namespace
@@ -889,6 +916,9 @@ struct sml_train {
     // the fused path's diagonal-tile update as three 64 x 64 quadrants (k_chol_update_diag);
     // SML_CHOL_DSPLIT=0: one 128 x 128 lower tile
     bool diag_split = true;
+    // the solves' in-panel epilogues through an LDS transpose (gemm_rhs te; the wide
+    // launches store directly, where it measured slower); SML_SOLVE_TE=0: direct
+    bool solve_te = true;
     // the trailing update's LDS stage depth (SML_CHOL_KC: 16 or 32)
     int update_kc = kKC;
     std::vector<int> naug;
@@ -935,6 +965,7 @@ extern "C" int sml_train_create(int nlocal, const int *naug, int nout, sml_train
     if (const char *e = getenv("SML_CHOL_DIAG")) t->diag_b = atoi(e) != 1;          // A/B knob
     if (const char *e = getenv("SML_CHOL_FUSE")) t->fuse = *e != '0';               // A/B knob
     if (const char *e = getenv("SML_CHOL_DSPLIT")) t->diag_split = *e != '0';      // A/B knob
+    if (const char *e = getenv("SML_SOLVE_TE")) t->solve_te = *e != '0';           // A/B knob
     if (const char *e = getenv("SML_CHOL_KC")) t->update_kc = atoi(e) == 32 ? 32 : kKC;  // A/B knob
     t->naug.assign(naug, naug + nlocal);
     int mx = 0;
@@ -1066,33 +1097,34 @@ extern "C" int sml_train_solve(sml_train *t, int ncs, double beta_res, double be
     // groups of the right-hand sides (SML_SOLVE_SPLIT=0: one), the wide ones whole
     const bool sp = t->rhs_split;
     const dim3 g1(1, nl, sp ? 3 : 1);
+    const int te = t->solve_te ? 1 : 0;
     for (int p0 = 0; p0 < C; p0 += P) {  // L Y = B
         const int p1 = std::min(C, p0 + P);
         for (int k = p0; k < p1; ++k) {
             hipLaunchKernelGGL((sp ? k_solve_diag<false, kRhs / 3> : k_solve_diag<false, kRhs>), g1, dim3(256), 0, st,
-                               t->d_linv, t->d_B, npad, nout, k, t->d_regs);
+                               t->d_linv, t->d_B, npad, nout, k, t->d_regs, te);
             if (k + 1 < p1)
                 hipLaunchKernelGGL((sp ? k_solve_update<false, kRhs / 3> : k_solve_update<false, kRhs>),
                                    dim3(p1 - 1 - k, nl, g1.z), dim3(256), 0, st, t->d_G, t->d_B, npad, nout, k, 1,
-                                   k + 1, t->d_regs);
+                                   k + 1, t->d_regs, te);
         }
         if (p1 < C)
             hipLaunchKernelGGL((k_solve_update<false, kRhs>), dim3(C - p1, nl), dim3(256), 0, st, t->d_G, t->d_B, npad,
-                               nout, p0, p1 - p0, p1, t->d_regs);
+                               nout, p0, p1 - p0, p1, t->d_regs, 0);
     }
     for (int p1 = C; p1 > 0; p1 -= P) {  // L^T X = Y, panels from the bottom
         const int p0 = std::max(0, p1 - P);
         for (int k = p1 - 1; k >= p0; --k) {
             hipLaunchKernelGGL((sp ? k_solve_diag<true, kRhs / 3> : k_solve_diag<true, kRhs>), g1, dim3(256), 0, st,
-                               t->d_linv, t->d_B, npad, nout, k, t->d_regs);
+                               t->d_linv, t->d_B, npad, nout, k, t->d_regs, te);
             if (k > p0)
                 hipLaunchKernelGGL((sp ? k_solve_update<true, kRhs / 3> : k_solve_update<true, kRhs>),
                                    dim3(k - p0, nl, g1.z), dim3(256), 0, st, t->d_G, t->d_B, npad, nout, k, 1, p0,
-                                   t->d_regs);
+                                   t->d_regs, te);
         }
         if (p0 > 0)
             hipLaunchKernelGGL((k_solve_update<true, kRhs>), dim3(p0, nl), dim3(256), 0, st, t->d_G, t->d_B, npad, nout,
-                               p0, p1 - p0, 0, t->d_regs);
+                               p0, p1 - p0, 0, t->d_regs, 0);
     }
     SML_HIP(hipGetLastError());
     hipLaunchKernelGGL(k_train_wout, dim3(t->npad / kWoutJ, t->nlocal), dim3(256), 0, st, t->d_B, t->d_regs,
