@@ -329,6 +329,13 @@ __global__ __launch_bounds__(256) void k_train_wout(const double *__restrict__ X
 }
 
 // ------------------------------------------------------------ batched Cholesky
+// a wave's LDS operations complete in issue order: a fence for the compiler and a wave
+// barrier order one lane's LDS writes before another lane's reads
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
 // Operand loader of the tile GEMM: a TM-row operand, kKC values of l per stage.
 // Column-major operands (T = false, X(row, l) at p[l * ld + row]): row = tid % TM,
 // l = tid / TM + (256 / TM) q -- rows contiguous across lanes; transposed ones
@@ -357,7 +364,7 @@ template <int TR, int TC, bool AT, bool BT, int KC = kKC>
 __device__ __forceinline__ void gemm_tile(const double *__restrict__ pa, long long lda, int arows,
                                           const double *__restrict__ pb, long long ldb, int brows, double *po,
                                           long long ldo, double alpha, bool accumulate, int K = kTile,
-                                          bool lower = false) {
+                                          bool lower = false, bool te = false) {
     using LA = TileLoader<TR, AT, KC>;
     using LB = TileLoader<TC, BT, KC>;
     constexpr int NI = TR / 32, NJ = TC / 32;
@@ -407,6 +414,35 @@ __device__ __forceinline__ void gemm_tile(const double *__restrict__ pa, long lo
 #pragma unroll
                 for (int j = 0; j < NJ; ++j) acc[i][j] = MFMA64(a[i], b[j], acc[i][j]);
         }
+    }
+    if (te) {
+        // each 16 x 16 tile transposed through the wave's LDS scratch (sA, free after the
+        // last stage; gemm_rhs's te): a read-modify-write instruction covers 16 consecutive
+        // rows of 4 columns, whole 128-B lines; the same expression per element
+        static_assert(KC * (TR + kLdsPad) >= 4 * 16 * 17, "the waves' transpose scratch fits in sA");
+        __syncthreads();
+        if (lower && wr < wc) return;
+        double *scr = &sA[0][0] + w * (16 * 17);
+        const int a = lane >> 4, b = lane & 15;
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) scr[l16 * 17 + kk + 4 * q] = acc[i][j][q];
+                wave_sync();
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int row = wr * (TR / 2) + i * 16 + b, col = wc * (TC / 2) + j * 16 + 4 * q + a;
+                    const double v = scr[(4 * q + a) * 17 + b];
+                    if (row < arows && col < brows) {
+                        double *p = po + (long long)col * ldo + row;
+                        *p = (accumulate ? *p : 0.0) + alpha * v;
+                    }
+                }
+                wave_sync();
+            }
+        return;
     }
     if (lower && wr < wc) return;
 #pragma unroll
@@ -535,11 +571,6 @@ __device__ int g_dst_k = 0;
     do {           \
     } while (0)
 #endif
-
-__device__ __forceinline__ void wave_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-}
 
 // one 16 x 16 tile of O = A B^T over K (a multiple of 4): fa(r, t), fb(c, t) for
 // r, c < 16; acc[q] = O(kk + 4 q, l16) (lane = 16 kk + l16), gemm_tile's layout
@@ -693,13 +724,13 @@ __global__ __launch_bounds__(kDiagThreads) void k_chol_diag_b(double *__restrict
 // L_ik = A_ik L_kk^-T for the blocks i > k below the diagonal, in place: a block
 // owns 64 rows x all 128 columns (it reads the whole rows it overwrites)
 __global__ __launch_bounds__(256, 3) void k_chol_panel(double *__restrict__ G, const double *__restrict__ linv, int npad,
-                                                    int k, const TrainRegion *__restrict__ regs) {
+                                                    int k, const TrainRegion *__restrict__ regs, int te) {
     const int r = blockIdx.y, C = npad / kTile, i = k + 1 + (blockIdx.x >> 1), r0 = (blockIdx.x & 1) * 64;
     if (i >= live_blocks(regs, r)) return;  // A_ik = 0: L_ik = 0
     double *Gr = G + (size_t)r * npad * npad;
     double *A = Gr + (size_t)k * kTile * npad + (size_t)i * kTile + r0;
     const double *Li = linv + ((size_t)r * C + k) * kTile * kTile;
-    gemm_tile<64, 128, false, false>(A, npad, 64, Li, kTile, kTile, A, npad, 1.0, false);
+    gemm_tile<64, 128, false, false>(A, npad, 64, Li, kTile, kTile, A, npad, 1.0, false, kTile, false, te != 0);
 }
 
 // A_ij -= sum_{k0 <= k < k0 + kw} L_ik L_jk^T for the lower-triangle tiles j <= i
@@ -731,17 +762,19 @@ __global__ __launch_bounds__(256, 2) void k_chol_update(double *__restrict__ G, 
 // per block column.  The same sums per element as the two launches (the tile shape does
 // not change an element's MFMA chain), so the factor is bitwise the same.
 __global__ __launch_bounds__(256, 3) void k_chol_upanel(double *__restrict__ G, const double *__restrict__ linv,
-                                                     int npad, int k0, int k, const TrainRegion *__restrict__ regs) {
+                                                     int npad, int k0, int k, const TrainRegion *__restrict__ regs,
+                                                     int te) {
     const int r = blockIdx.y, C = npad / kTile, i = k + 1 + (blockIdx.x >> 1), r0 = (blockIdx.x & 1) * 64;
     if (i >= live_blocks(regs, r)) return;  // A_ik = 0: L_ik = 0
     double *Gr = G + (size_t)r * npad * npad;
     const double *Lip = Gr + (size_t)k0 * kTile * npad + (size_t)i * kTile + r0;
     const double *Lkp = Gr + (size_t)k0 * kTile * npad + (size_t)k * kTile;
     double *A = Gr + (size_t)k * kTile * npad + (size_t)i * kTile + r0;
-    gemm_tile<64, 128, false, false>(Lip, npad, 64, Lkp, npad, kTile, A, npad, -1.0, true, (k - k0) * kTile);
+    gemm_tile<64, 128, false, false>(Lip, npad, 64, Lkp, npad, kTile, A, npad, -1.0, true, (k - k0) * kTile, false,
+                                     te != 0);
     __syncthreads();  // the slab's updated rows, stored by every wave, before any is read
     const double *Li = linv + ((size_t)r * C + k) * kTile * kTile;
-    gemm_tile<64, 128, false, false>(A, npad, 64, Li, kTile, kTile, A, npad, 1.0, false);
+    gemm_tile<64, 128, false, false>(A, npad, 64, Li, kTile, kTile, A, npad, 1.0, false, kTile, false, te != 0);
 }
 
 // The left-looking update of a panel's diagonal tile (k, k) by block columns k0 .. k - 1
@@ -750,14 +783,14 @@ __global__ __launch_bounds__(256, 3) void k_chol_upanel(double *__restrict__ G, 
 // diagonal skipped), each quadrant's chain on four waves instead of one, three times
 // the workgroups for a launch of one tile per region.  Bitwise the 128 x 128 form.
 __global__ __launch_bounds__(256, 2) void k_chol_update_diag(double *__restrict__ G, int npad, int k0, int k,
-                                                          const TrainRegion *__restrict__ regs) {
+                                                          const TrainRegion *__restrict__ regs, int te) {
     const int r = blockIdx.y, q = blockIdx.x, r0 = q == 0 ? 0 : 64, c0 = q == 2 ? 64 : 0;
     if (k >= live_blocks(regs, r)) return;  // (padding block columns are never factored)
     double *Gr = G + (size_t)r * npad * npad;
     const double *Lkp = Gr + (size_t)k0 * kTile * npad + (size_t)k * kTile;
     double *Akk = Gr + (size_t)k * kTile * npad + (size_t)k * kTile;
     gemm_tile<64, 64, false, false>(Lkp + r0, npad, 64, Lkp + c0, npad, 64, Akk + (size_t)c0 * npad + r0, npad, -1.0,
-                                    true, (k - k0) * kTile);
+                                    true, (k - k0) * kTile, false, te != 0);
 }
 
 static int update_tiles(int C, int jlo, int jhi) {
@@ -919,6 +952,10 @@ struct sml_train {
     // the solves' in-panel epilogues through an LDS transpose (gemm_rhs te; the wide
     // launches store directly, where it measured slower); SML_SOLVE_TE=0: direct
     bool solve_te = true;
+    // the factor's shallow launches (the fused in-panel update + panel, the diagonal tile's
+    // update, the first panels) with the same transposed epilogue (gemm_tile te);
+    // SML_CHOL_TE=0: direct
+    bool chol_te = true;
     // the trailing update's LDS stage depth (SML_CHOL_KC: 16 or 32)
     int update_kc = kKC;
     std::vector<int> naug;
@@ -966,6 +1003,7 @@ extern "C" int sml_train_create(int nlocal, const int *naug, int nout, sml_train
     if (const char *e = getenv("SML_CHOL_FUSE")) t->fuse = *e != '0';               // A/B knob
     if (const char *e = getenv("SML_CHOL_DSPLIT")) t->diag_split = *e != '0';      // A/B knob
     if (const char *e = getenv("SML_SOLVE_TE")) t->solve_te = *e != '0';           // A/B knob
+    if (const char *e = getenv("SML_CHOL_TE")) t->chol_te = *e != '0';             // A/B knob
     if (const char *e = getenv("SML_CHOL_KC")) t->update_kc = atoi(e) == 32 ? 32 : kKC;  // A/B knob
     t->naug.assign(naug, naug + nlocal);
     int mx = 0;
@@ -1060,13 +1098,14 @@ extern "C" int sml_train_solve(sml_train *t, int ncs, double beta_res, double be
     // columns (depth 128 (k - p0)), then its diagonal factor and L_ik below it;
     // after the panel, one right-looking update of the whole trailing matrix at
     // depth 128 x panel.
-    const int P = t->panel;
+    const int P = t->panel, cte = t->chol_te ? 1 : 0;
     for (int p0 = 0; p0 < C; p0 += P) {
         const int p1 = std::min(C, p0 + P);
         for (int k = p0; k < p1; ++k) {
             const bool fused = t->fuse && k > p0;  // (then the update launch covers the diagonal tile only)
             if (fused && t->diag_split)
-                hipLaunchKernelGGL(k_chol_update_diag, dim3(3, nl), dim3(256), 0, st, t->d_G, npad, p0, k, t->d_regs);
+                hipLaunchKernelGGL(k_chol_update_diag, dim3(3, nl), dim3(256), 0, st, t->d_G, npad, p0, k, t->d_regs,
+                                   cte);
             else if (k > p0)
                 hipLaunchKernelGGL(k_chol_update<kKC>, dim3(fused ? 1 : C - k, nl), dim3(256), 0, st, t->d_G, npad, p0,
                                    k - p0, k, k + 1, t->d_regs);
@@ -1078,10 +1117,10 @@ extern "C" int sml_train_solve(sml_train *t, int ncs, double beta_res, double be
                                    t->d_info, t->d_regs);
             if (k < C - 1 && fused)
                 hipLaunchKernelGGL(k_chol_upanel, dim3(2 * (C - 1 - k), nl), dim3(256), 0, st, t->d_G, t->d_linv,
-                                   npad, p0, k, t->d_regs);
+                                   npad, p0, k, t->d_regs, cte);
             else if (k < C - 1)
                 hipLaunchKernelGGL(k_chol_panel, dim3(2 * (C - 1 - k), nl), dim3(256), 0, st, t->d_G, t->d_linv,
-                                   npad, k, t->d_regs);
+                                   npad, k, t->d_regs, cte);
         }
         if (p1 < C)  // the trailing update (72 % of the solve's time)
             hipLaunchKernelGGL((t->update_kc == 32 ? k_chol_update<32> : k_chol_update<kKC>),

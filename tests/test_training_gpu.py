@@ -173,7 +173,7 @@ def test_solve_reports_the_first_non_positive_pivot(cuda):
 
 
 @pytest.mark.parametrize("knobs, bitwise", [({"SML_CHOL_FUSE": "0"}, True), ({"SML_CHOL_DSPLIT": "0"}, True),
-                                            ({"SML_SOLVE_SPLIT": "0"}, True), ({"SML_SOLVE_TE": "0"}, True),
+                                            ({"SML_SOLVE_SPLIT": "0"}, True), ({"SML_SOLVE_TE": "0"}, True), ({"SML_CHOL_TE": "0"}, True),
                                             ({"SML_CHOL_DIAG": "1"}, False)])
 def test_cholesky_schedules_against_the_default(cuda, knobs, bitwise):
     """The factor's and solves' launch schedules reorder no arithmetic, so W_out is
@@ -181,7 +181,8 @@ def test_cholesky_schedules_against_the_default(cuda, knobs, bitwise):
     launches (default: k_chol_upanel); SML_CHOL_DSPLIT=0 -- the diagonal tile's update
     as one lower 128 x 128 tile (default: three quadrant workgroups, k_chol_update_diag);
     SML_SOLVE_SPLIT=0 -- the solves' in-panel launches on all right-hand sides at once;
-    SML_SOLVE_TE=0 -- their epilogues stored directly (default: through an LDS transpose).
+    SML_SOLVE_TE=0 -- their epilogues stored directly (default: through an LDS transpose);
+    SML_CHOL_TE=0 -- the same for the factor's shallow launches.
     SML_CHOL_DIAG=1 -- k_chol_diag, column by column -- sums the diagonal block's updates
     in another order than the blocked default (k_chol_diag_b's 16 x 16 MFMA tiles): the
     two agree to rounding, within W_TOL.  Panels of three block columns over npad = 896,
