@@ -357,7 +357,10 @@ int sml_dyn_is_safe(const double *minmax);
  * agcm_main skips the integration (at_gcm.f90:37): the forecast is then the input
  * grid with q floored (run_model's copy, :1550-1553).  The check runs beside the
  * window; sml_dyn_last_safe reads its outcome.  The forecast buffers must not alias
- * the inputs. */
+ * the inputs.  The window runs as a replayed hipGraph with the exit captured in it,
+ * keyed on d_grid4d / d_logp / d_fc4d / d_fc2d: keep those buffers stable across calls
+ * (the hybrid loop does) -- a caller alternating them gets the same results but
+ * re-instantiates the ~200-node graph on every call. */
 int sml_dyn_run_model(sml_dynamics *d, const double *d_grid4d, const double *d_logp, int nleap, double delt,
                       double alph, double rob, double wil, double *d_fc4d, double *d_fc2d, void *stream);
 /* is_safe_to_run_speedy of the last sml_dyn_from_grid / sml_dyn_run_model, i.e. the
@@ -370,6 +373,14 @@ int sml_dyn_last_safe(sml_dynamics *d, int *safe, double *minmax);
  * lets it use any CU.  The hybrid loop puts it on CUs neither SPEEDY's nor the
  * reservoir's stream uses, so its kernels never share a CU with the window's. */
 int sml_dyn_set_check_cus(sml_dynamics *d, int first_cu, int num_cus);
+/* the give-up time (microseconds, default 1 s) of run_model's exit waiting in-kernel
+ * for the check beside the window: an exit that gives up takes its window as unsafe
+ * (the forecast is the input grid) and sml_dyn_last_safe reports that window -- and
+ * only that window -- unsafe.  The hybrid loop sets it with its hop timeout. */
+int sml_dyn_set_check_timeout(sml_dynamics *d, int64_t microseconds);
+/* the check's stream (NULL before sml_dyn_set_check_cus or the first check): work a
+ * host enqueues there runs before the next window's check */
+int sml_dyn_check_stream(const sml_dynamics *d, void **stream);
 /* synchronous host-buffer variants */
 int sml_dyn_from_grid_host(sml_dynamics *d, const double *grid4d, const double *logp, double *minmax, int *safe);
 int sml_dyn_to_grid_host(sml_dynamics *d, double *grid4d, double *logp);

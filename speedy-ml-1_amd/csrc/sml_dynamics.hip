@@ -107,7 +107,8 @@ struct sml_dynamics {
     // check's k_io_minmax adds 4 per check, the exit polls for 4 * chk_count
     bool chk_flag = true;
     unsigned *d_chk_cnt = nullptr;
-    // the exit's hand-off timed out: a pinned, host-visible word (read without a copy by
+    // the exit's hand-off timed out: a pinned, host-visible word holding the counter
+    // target of the check it gave up on (read without a copy by sml_dyn_last_safe and
     // sml::dyn_check_late, reset when reported); the exit's give-up time in ticks
     unsigned *d_chk_late = nullptr;
     long long chk_timeout = 100000000ll;
@@ -3275,7 +3276,12 @@ extern "C" int sml_dyn_set_climatology(sml_dynamics *d, const double *clim) {
 // changed since the last call (the window's forcing stays as computed); force != 0
 // recomputes anyway.  Ordered on `stream`: the next window on that stream reads it.
 extern "C" int sml_dyn_fordate_ex(sml_dynamics *d, int iyear, int imonth, int iday, int force, void *stream) {
-    SML_REQUIRE(d && imonth >= 1 && imonth <= 12 && iday >= 1 && iday <= 31, "bad date %d-%d-%d", iyear, imonth, iday);
+    // the days of newdate's 365-day table (ini_fordate / mod_date), plus February 29,
+    // which the reference calendar emits once its SAVEd February latch is set
+    // (mod_calendar.f90:40, 61-63); a later day would extrapolate tmonth past the month
+    static const int kMonthDays[12] = {31, 29, 31, 30, 31, 30, 31, 31, 30, 31, 30, 31};
+    SML_REQUIRE(d && imonth >= 1 && imonth <= 12 && iday >= 1 && iday <= kMonthDays[imonth - 1],
+                "bad date %d-%d-%d", iyear, imonth, iday);
     SML_REQUIRE(d->phys_on, "sml_dyn_set_physics must provide the boundary fields first");
     SML_REQUIRE(d->surf_on, "sml_dyn_set_surface must provide fmask_l, fmask_s and alb0 first");
     (void)iyear;  // only the co2 trend reads the year (lco2 = .false.)
@@ -3604,8 +3610,12 @@ extern "C" int sml_dyn_last_safe(sml_dynamics *d, int *safe, double *minmax) {
     }
     *safe = sml_dyn_is_safe(mm);
     // an exit that gave up on this check took the window as unsafe (it did so before the
-    // check completed, so the word is final here)
-    if (d->d_chk_late && __atomic_load_n(d->d_chk_late, __ATOMIC_ACQUIRE)) *safe = 0;
+    // check completed, so the word is final here).  The word holds the counter target of
+    // the check the exit gave up on (4 * its number): a late exit of an earlier window,
+    // not yet reported through sml::dyn_check_late, does not make this one unsafe
+    if (d->d_chk_late && d->chk_counted &&
+        __atomic_load_n(d->d_chk_late, __ATOMIC_ACQUIRE) == 4u * d->chk_count)
+        *safe = 0;
     if (minmax) std::memcpy(minmax, mm, sizeof mm);
     return SML_OK;
 }
@@ -3623,6 +3633,18 @@ int sml::dyn_run_model_wait(sml_dynamics *d, const uint64_t *flag, uint64_t valu
 int sml::dyn_set_check_timeout(sml_dynamics *d, long long timeout) {
     SML_REQUIRE(d && timeout >= 0, "bad argument");
     d->chk_timeout = timeout;
+    return SML_OK;
+}
+
+extern "C" int sml_dyn_set_check_timeout(sml_dynamics *d, int64_t microseconds) {
+    SML_REQUIRE(d && microseconds >= 0, "bad argument");
+    if (d->chk_stream) SML_HIP(hipStreamSynchronize(d->chk_stream));
+    return sml::dyn_set_check_timeout(d, (long long)std::min<int64_t>(microseconds, INT64_MAX / 100) * 100);
+}
+
+extern "C" int sml_dyn_check_stream(const sml_dynamics *d, void **stream) {
+    SML_REQUIRE(d && stream, "null argument");
+    *stream = d->chk_stream;
     return SML_OK;
 }
 
@@ -3646,9 +3668,9 @@ int sml::dyn_run_model_entry_signal(sml_dynamics *d, uint64_t *counter, int *add
 }
 
 // the next run_model's exit is followed (on its stream, inside the window graph when the
-// exit is captured there) by a one-lane store of value to *flag
+// exit is captured there) by a one-lane store of value to *flag; flag = NULL withdraws it
 int sml::dyn_run_model_exit_store(sml_dynamics *d, uint64_t *flag, uint64_t value) {
-    SML_REQUIRE(d && flag, "null argument");
+    SML_REQUIRE(d, "null argument");
     d->exit_store = flag;
     d->exit_store_value = value;
     return SML_OK;

@@ -1225,15 +1225,21 @@ extern "C" int sml_hybrid_advance(sml_hybrid *h, const double *d_outvec_all) {
             return rc;
     // kernel hops: the forecast's signal is a store that run_model issues right behind
     // its exit (inside the window graph when the exit is captured there)
+    // (the loop's sequence number moves only once run_model is enqueued: a run_model
+    // that fails leaves no store pending and no finish waiting for one)
     const bool exit_store = hops && h->use_kernels && exit_adds == 0;
+    const uint64_t lm_next = h->seq[sml_hybrid::kHopLm] + 1;
     if (exit_store)
         if (int rc = sml::dyn_run_model_exit_store(h->dyn, h->d_seq + sml_hybrid::kHopLm * sml_hybrid::kSeqStride,
-                                                   ++h->seq[sml_hybrid::kHopLm]))
+                                                   lm_next))
             return rc;
     if (!entry_sig)
         if (int rc = sml_dyn_run_model(h->dyn, h->g4, h->g2, h->nleap, h->delt, h->alph, h->rob, h->wil, h->f4, h->f2,
-                                       s))
+                                       s)) {
+            if (exit_store) (void)sml::dyn_run_model_exit_store(h->dyn, nullptr, 0);
             return rc;
+        }
+    if (exit_store) h->seq[sml_hybrid::kHopLm] = lm_next;
     if (exit_adds > 0) {  // the exit's blocks each add 1 to the hop's word once released
         h->seq[sml_hybrid::kHopLm] += (uint64_t)exit_adds;
     } else if (hops && !exit_store) {

@@ -213,7 +213,9 @@ __global__ __launch_bounds__(kFftThreads) void k_gridx(const double *__restrict_
             while (__hip_atomic_load(ex.cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
                 __builtin_amdgcn_s_sleep(2);
                 if (wall_clock64() - t0 > ex.timeout) {  // never hang the queue
-                    __hip_atomic_store(ex.late, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    // the mark names the check given up on (its counter target, >= 4), so
+                    // sml_dyn_last_safe fails that window only, not every later one
+                    __hip_atomic_store(ex.late, target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                     gave_up = 1;
                     break;
                 }

@@ -387,6 +387,13 @@ module sml_hip
       integer(c_int), value :: first_cu, num_cus
       integer(c_int) :: rc
     end function
+    !> give-up time (microseconds) of run_model's exit waiting for the check beside the window
+    function sml_dyn_set_check_timeout(ctx, microseconds) bind(C, name='sml_dyn_set_check_timeout') result(rc)
+      import :: c_ptr, c_int, c_int64_t
+      type(c_ptr), value :: ctx
+      integer(c_int64_t), value :: microseconds
+      integer(c_int) :: rc
+    end function
 
     ! ------------------------------------------------------------ communicator (RCCL)
     !> startmpi's world (mpires.f90:21-37) for the one collective of the hot path;

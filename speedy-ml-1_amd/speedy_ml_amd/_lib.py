@@ -62,6 +62,7 @@ EXPORTED = (
     "sml_dyn_get_sea_ice", "sml_dyn_get_physics", "sml_dyn_get_forcing", "sml_dyn_set_surface",
     "sml_dyn_set_climatology", "sml_dyn_fordate", "sml_dyn_fordate_ex", "sml_dyn_fordate_count",
     "sml_hybrid_set_calendar", "sml_hybrid_window_date", "sml_hybrid_set_hop_timeout",
+    "sml_dyn_set_check_timeout", "sml_dyn_check_stream",
 )
 
 SML_HOP_AUTO, SML_HOP_WAIT_VALUE, SML_HOP_EVENTS, SML_HOP_KERNEL = 0, 1, 2, 3
@@ -188,6 +189,8 @@ def _declare(L: ctypes.CDLL) -> None:
         "sml_dyn_run_model": [vp, vp, vp, i, d, d, d, d, vp, vp, vp],
         "sml_dyn_last_safe": [vp, ip, vp],
         "sml_dyn_set_check_cus": [vp, i, i],
+        "sml_dyn_set_check_timeout": [vp, ctypes.c_int64],
+        "sml_dyn_check_stream": [vp, pp],
         "sml_res_info": [vp, ip, ip, ip, ip, vp],
         "sml_comm_unique_id": [vp],
         "sml_comm_create": [i, i, vp, pp],

@@ -139,3 +139,22 @@ def test_fordate_is_recomputed_only_when_an_input_changes(cuda):
     dyn.fordate(1982, 3, 2, force=True)
     assert dyn.fordate_count() == n + 3
     dyn.close()
+
+
+def test_fordate_rejects_days_past_the_month(cuda):
+    """a day past its month (2-30, 4-31) is refused instead of extrapolating
+    newdate's tmonth; February 29 -- which the reference calendar emits once its
+    February latch is set (mod_calendar.f90:40, 61-63) -- is accepted."""
+    from speedy_ml_amd._lib import SmlError
+
+    fmask, phis_c, surf, clim, _, _ = inputs()
+    dyn, bc = _dyn(phis_c, fmask, surf)
+    dyn.set_physics(bc)
+    dyn.set_surface(surf)
+    dyn.set_climatology(clim)
+    for mo, dd in ((2, 30), (4, 31), (6, 31), (9, 31), (11, 31), (1, 0), (13, 1)):
+        with pytest.raises(SmlError):
+            dyn.fordate(1982, mo, dd)
+    for mo, dd in ((2, 29), (1, 31), (12, 31)):
+        dyn.fordate(1984, mo, dd)
+    dyn.close()

@@ -166,3 +166,46 @@ def test_fused_and_unfused_run_model_agree(cuda):
             ref = np.abs(b4[k, :, :, v]).max()
             assert np.abs(a4[k, :, :, v] - b4[k, :, :, v]).max() <= UNFUSED_TOL * ref, (v, k)
     assert np.abs(a2 - b2).max() <= UNFUSED_TOL * np.abs(b2).max()
+
+
+def test_a_late_exit_fails_its_own_window_only(cuda, dyn):
+    """run_model's exit that gives up waiting for its safety check
+    takes its window as unsafe (the forecast is the input grid) and marks a late word.
+    That word must fail that window only: a standalone Dynamics (no hybrid loop to
+    report and reset it) whose next window's check arrives in time reads safe again.
+    The check is held back by a sleep kernel on the check stream (CU-masked, a queue of
+    its own) while the exit's give-up time is zero; the windows run on a stream of their
+    own (the legacy stream would wait for the sleep too)."""
+    import ctypes
+
+    import torch
+
+    from speedy_ml_amd._lib import check, lib
+
+    check(lib().sml_dyn_set_check_cus(dyn._h, 192, 64))
+    g4, g2 = _grids(seed=5)
+    dg4, dg2 = _t(g4, cuda), _t(g2, cuda)
+    f4 = torch.zeros_like(dg4)
+    f2 = torch.zeros_like(dg2)
+    ws = torch.cuda.Stream()
+    dyn.run_model(dg4, dg2, f4, f2, nleap=3, stream=ws)  # a first window: the check stream exists, the exit on time
+    assert dyn.last_safe()[0]
+    s = ctypes.c_void_p()
+    check(lib().sml_dyn_check_stream(dyn._h, ctypes.byref(s)))
+    assert s.value
+    chk = torch.cuda.ExternalStream(s.value, device=cuda)
+    check(lib().sml_dyn_set_check_timeout(dyn._h, 0))
+    with torch.cuda.stream(chk):
+        torch.cuda._sleep(200_000_000)  # ~85 ms ahead of the next check
+    dyn.run_model(dg4, dg2, f4, f2, nleap=3, stream=ws)
+    safe_late, _ = dyn.last_safe()
+    torch.cuda.synchronize()
+    late_f4 = f4.cpu().numpy()
+    check(lib().sml_dyn_set_check_timeout(dyn._h, 1_000_000))
+    dyn.run_model(dg4, dg2, f4, f2, nleap=3, stream=ws)
+    safe_next, _ = dyn.last_safe()
+    assert not safe_late, "the exit gave up on its check: that window is unsafe"
+    want = g4.copy()
+    want[..., 3] = np.where(g4[..., 3] < 0.000001, 0.000001, g4[..., 3])
+    np.testing.assert_array_equal(late_f4, want)  # agcm_main's pass-through
+    assert safe_next, "a late exit of an earlier window must not make this one unsafe"
