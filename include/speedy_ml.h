@@ -203,9 +203,19 @@ int sml_res_step_finish_assemble(sml_reservoirs *c, const double *d_fc4d, const 
                                  double *d_precip, void *stream);
 /* cap on the waves of the v_ml readout issued by sml_res_step_begin (0 = one wave per
  * 8-row item, the default cap is 2048).  The cap leaves HBM headroom for SPEEDY when
- * both share CUs; on CUs of their own (sml_stream_create_cu_range) it is not needed.
- * The environment variable SML_READ_WAVES, when set, takes precedence. */
+ * both share CUs; on CUs of their own (sml_stream_create_cu_range) it is not needed. */
 int sml_res_set_read_waves(sml_reservoirs *c, int waves);
+/* The fallback paths, forced for every region -- the defaults take them only where a
+ * region's structure does not fit the fast layout, and give the same bits: A and W_in
+ * read from their CSR copies (SML_RES_PATH_CSR; before any region is loaded), the
+ * state update one block per (region, part) instead of the balanced persistent grid
+ * (SML_RES_PATH_PER_REGION), the v_p finish one thread per output instead of in
+ * column groups (SML_RES_PATH_UNGROUPED_FINISH).  For tests and for a host bisecting a
+ * difference; 0 restores the defaults. */
+#define SML_RES_PATH_CSR 1
+#define SML_RES_PATH_PER_REGION 2
+#define SML_RES_PATH_UNGROUPED_FINISH 4
+int sml_res_set_reference_paths(sml_reservoirs *c, int flags);
 /* the number of CUs the context's launches get (its stream's CU mask; 0 = the whole
  * device): the balanced state update runs one block per CU over equal shares of all
  * local rows.  sml_res_update_balanced: 1 when the update takes that form (every
@@ -226,7 +236,7 @@ int sml_res_ell_layout(sml_reservoirs *c, int i, int *a_width, int *a_overflow, 
  * W_out rows (k_res_begin, up to 3 blocks per CU); 2 = the same with the W_out loads
  * unrolled twice (1 block per CU).  Every form gives bit-identical states and sums.
  * The fused forms need the 17-row readout and <= 64 KB of LDS per region; otherwise
- * form 0 runs (sml_res_begin_fused says which).  SML_BEGIN, when set, overrides. */
+ * form 0 runs (sml_res_begin_fused says which). */
 int sml_res_set_begin_mode(sml_reservoirs *c, int mode);
 int sml_res_begin_fused(const sml_reservoirs *c, int *fused);
 /* synchronize (src/mod_reservoir.f90:1352-1378), the spin-up of start_prediction
@@ -378,6 +388,12 @@ int sml_dyn_set_check_cus(sml_dynamics *d, int first_cu, int num_cus);
  * (the forecast is the input grid) and sml_dyn_last_safe reports that window -- and
  * only that window -- unsafe.  The hybrid loop sets it with its hop timeout. */
 int sml_dyn_set_check_timeout(sml_dynamics *d, int64_t microseconds);
+/* the step kernels' form: 1 (default) the fused step -- two launches per leapfrog step,
+ * a*b + c contracted into FMAs, within 1e-13 of the reference's window; 0 the 8/9-launch
+ * step whose Fourier transforms are FFTPACK's separate multiplies and adds, bit-exact
+ * with the reference's rfftb / rfftf (the two agree to rounding, 1e-11 after 6 steps).
+ * Takes effect at the next step / window. */
+int sml_dyn_set_fused(sml_dynamics *d, int fused);
 /* the check's stream (NULL before sml_dyn_set_check_cus or the first check): work a
  * host enqueues there runs before the next window's check */
 int sml_dyn_check_stream(const sml_dynamics *d, void **stream);
@@ -486,6 +502,9 @@ int sml_train_accumulate(sml_train *t, const double *d_states, const double *d_t
 int sml_train_solve(sml_train *t, int ncs, double beta_res, double beta_model, int using_prior, double prior_val,
                     double *d_wout, int *info, void *stream);
 int sml_train_npad(const sml_train *t, int *npad);
+/* block columns per Cholesky panel (default 8): the in-panel steps are left-looking,
+ * the trailing update after each panel right-looking at depth 128 x panel */
+int sml_train_set_panel(sml_train *t, int panel);
 /* host copies for tests: G (npad x npad, column-major, lower triangle valid) and
  * B(j, o) (npad x nout) of local region i */
 int sml_train_get_gram(sml_train *t, int i, double *G, double *B);
@@ -648,7 +667,7 @@ int sml_hybrid_slab_buffers(const sml_hybrid *h, const double **d_sst_grid, cons
  * else wait-value hops; events when dispatch is serialised --
  * AMD_SERIALIZE_KERNEL or rocprofv3's counter collection -- where a waiting packet or
  * kernel could stall its queue ahead of its producer; SML_HYBRID_EVENTS=1 also
- * selects events, SML_HYBRID_HOPK=0 wait-value).  In the kernel mode the v_p finish
+ * selects events).  In the kernel mode the v_p finish
  * and run_model's entry wait for their inputs inside their own kernels.  Drains both
  * streams before switching. */
 #define SML_HOP_AUTO 0
@@ -661,7 +680,7 @@ int sml_hybrid_set_hop_mode(sml_hybrid *h, int mode);
  * hands its consumer NaN instead of the data it did not get (the finish's local model,
  * the entry's grid; the exit takes the window as unsafe) and marks a host-visible word:
  * the next sml_hybrid_step, sml_hybrid_run_speedy (which then also yields run = 0) or
- * sml_hybrid_sync returns SML_ERR_STATE once.  SML_HOP_TIMEOUT_US sets it at create. */
+ * sml_hybrid_sync returns SML_ERR_STATE once. */
 int sml_hybrid_set_hop_timeout(sml_hybrid *h, int64_t microseconds);
 int sml_hybrid_hop_mode(const sml_hybrid *h, int *requested, int *effective);
 /* pipelined loop (default off): each advance also issues the NEXT step's reservoir

@@ -38,7 +38,6 @@
 #include "sml_fft.hpp"
 #include "sml_fft_wa96.hpp"
 #include "sml_physics.hpp"
-#include "sml_physics_quad.hpp"
 #include "sml_physics_pair.hpp"
 #include "sml_spectral_internal.hpp"
 
@@ -103,9 +102,8 @@ struct sml_dynamics {
     hipEvent_t ev_fork = nullptr, ev_chk = nullptr;
     bool chk_pending = false;  // work on chk_stream that the next user of d_chk must wait for
     // run_model's exit learns the check's result from a device counter instead of an
-    // event wait on its stream (chk_flag; SML_CHK_FLAG=0 at create: the event): the
-    // check's k_io_minmax adds 4 per check, the exit polls for 4 * chk_count
-    bool chk_flag = true;
+    // event wait on its stream: the check's k_io_minmax adds 4 per check, the exit polls
+    // for 4 * chk_count (an event wait only where the check is not counted: capture)
     unsigned *d_chk_cnt = nullptr;
     // the exit's hand-off timed out: a pinned, host-visible word holding the counter
     // target of the check it gave up on (read without a copy by sml_dyn_last_safe and
@@ -114,8 +112,6 @@ struct sml_dynamics {
     long long chk_timeout = 100000000ll;
     // the next run_model's entry waits in-kernel for its input grids (sml::dyn_run_model_wait)
     HopWait entry_wait;
-    // the next run_model's exit signals its forecast in-kernel (sml::dyn_run_model_signal)
-    uint64_t *exit_sig = nullptr;
     // the next run_model's entry signals its input grid in-kernel (sml::dyn_run_model_entry_signal)
     uint64_t *entry_sig = nullptr;
     unsigned chk_count = 0;
@@ -149,21 +145,11 @@ struct sml_dynamics {
     long long ford_gen = 1, ford_done = 0;
     int ford_date[2] = {0, 0};
     int ford_count = 0;  // fordate recomputations issued (sml_dyn_fordate_count)
-    // step kernels: the fused form (default: 2-3 launches per chained step) or the
-    // 8/9-launch form (SML_DYN_FUSED=0 at creation; same results bit for bit)
+    // step kernels: the fused form (default: 2-3 launches per chained step, FMA
+    // contraction) or the 8/9-launch form whose transforms are FFTPACK's separate
+    // multiplies and adds (sml_dyn_set_fused; the two agree to rounding)
     bool fused = true;
-    // with GPU physics: k_st_grid + k_st_specx instead of k_st_gridspec (SML_DYN_SPLIT_GRID=1)
-    bool split_grid = false;
-    // the row kernel's schedule (SML_DYN_QUAD): 2 (default) k_st_gridspec_p -- the grid-point
-    // dynamics, the moist side and the longwave side on waves of their own, the longwave on
-    // two lanes per column; 1: k_st_gridspec_q (phypar on four lanes per column, measured
-    // slower); 0: k_st_gridspec (one lane per column, two wave pairs).  All bitwise equal.
-    int quad = 2;
     bool nograph = false;  // SML_DYN_NOGRAPH=1: the window's launches issued directly, not replayed
-    // the fused step's hand-offs (vfm, varm, the m-major state) stored write-through
-    // (store2): SML_DYN_WT=1 both step kernels, 2 the row kernel's (vfm) only, 3 the
-    // per-m kernel's (varm, state) only
-    int wt = 0;
     // mod_lflags lradsw (module default .true.) and stloop's istep (at_gcm.f90:81)
     bool lradsw = true;
     int istep = 1;
@@ -184,11 +170,8 @@ struct sml_dynamics {
         // run_model's exit captured behind the window (exit_graph): its arguments (the
         // per-launch values come from d_xa, written by each run_model's k_io_entry)
         bool has_exit = false;
-        const void *exit_key[10] = {};
+        const void *exit_key[9] = {};
     } wreplay[4];  // [prepared entry (sml_dyn_run_model)][entry lradsw]
-    // run_model's exit inside the window graph (SML_EXIT_GRAPH=0 at create: launched
-    // after it): saves the graph's exit boundary and two launches on the critical path
-    bool exit_graph = true;
     // the next run_model's exit is followed by a store of exit_store_value to
     // *exit_store (sml::dyn_run_model_exit_store: the hybrid loop's forecast hop)
     uint64_t *exit_store = nullptr;
@@ -783,17 +766,15 @@ __global__ __launch_bounds__(256) void k_dyn_tail(double *__restrict__ st, doubl
 // (spectral <-> Fourier per zonal wavenumber m, Fourier <-> grid per latitude row):
 //   k_st_rows   (latitude row j, no GPU physics): gridx (FFT) -> LDS -> grid-point
 //               dynamics -> LDS -> specx (FFT)
-//   k_st_grid   (with GPU physics): blocks 0..47 a row's dynamics (gridx + grid-
-//               point dynamics), blocks 48..95 the same row's physics (gridx of the
-//               level-1 fields + phypar) side by side in one launch
-//   k_st_specx  (with GPU physics): dynamics + physics tendencies, specx (FFT)
+//   k_st_gridspec_p (with GPU physics): gridx, the grid-point dynamics beside phypar
+//               (its roles on waves of their own), specx, in one launch per row
 //   k_st_spec   (zonal wavenumber m, 512 threads = 64 coefficients x 8 levels):
 //               specy -> combine (vds, lap) -> sptend / geop / implic / hordif /
 //               timint -> the NEXT step's inverse-transform inputs from the new
 //               state (uvspec, grad, geop) -> gridy
 //   k_st_inv    (m): the inverse-transform inputs + gridy from the state in memory,
 //               for a step that follows no fused step (window start)
-// A leapfrog step is 2 launches (with GPU physics: k_st_gridspec + k_st_spec)
+// A leapfrog step is 2 launches (with GPU physics: k_st_gridspec_p + k_st_spec)
 // instead of 8 / 9.  Each block first stages everything it reads -- the m's slice of
 // the state, the row's Fourier coefficients -- in LDS with coalesced loads: the
 // fused step keeps its own m-major copies of the state ([m][var][lev][k][n p],
@@ -805,21 +786,11 @@ __global__ __launch_bounds__(256) void k_dyn_tail(double *__restrict__ st, doubl
 typedef double d4 __attribute__((ext_vector_type(4)));
 #define MFMA64(a, b, c) __builtin_amdgcn_mfma_f64_16x16x4f64((a), (b), (c), 0, 0, 0)
 
-// Write-through 16-B store (cache policy sc1): the line leaves the XCD's L2 as it is
-// written, so the release at the kernel's end has none of it to write back -- the
-// inter-kernel hand-offs of the fused step (vfm, the next step's varm and state) when
-// Dyn::wt is on (SML_DYN_WT).  A raw buffer store (0x00020000: the gfx9 descriptor
-// word 3) so the compiler tracks it like any other vector-memory store.
-__device__ __attribute__((always_inline)) inline void store2(double *base, size_t idx, double a, double b, bool wt) {
-    if (wt) {
-        typedef unsigned int u4 __attribute__((ext_vector_type(4)));
-        typedef double dv2 __attribute__((ext_vector_type(2)));
-        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7fffffff, 0x00020000);
-        const dv2 v = {a, b};
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, v), rs, (int)(idx * sizeof(double)), 0, 16);
-    } else {
-        *reinterpret_cast<double2 *>(base + idx) = double2{a, b};
-    }
+// one 16-B store of a (Re, Im) pair: the inter-kernel hand-offs of the fused step (vfm,
+// the next step's varm and state).  (Stored write-through, sc1, the kernel boundary
+// got cheaper but the stores far slower: measured and removed)
+__device__ __attribute__((always_inline)) inline void store2(double *base, size_t idx, double a, double b) {
+    *reinterpret_cast<double2 *>(base + idx) = double2{a, b};
 }
 
 constexpr int kCW = 2 * kNX;                  // real coefficients (n, p) of one m
@@ -985,7 +956,7 @@ __device__ inline GridyB gridy_operands(const double *__restrict__ pinv, int m) 
 }
 
 __device__ inline void gridy_m(const double *In, const GridyB &gb, double *__restrict__ varm, int m, int nf,
-                               int tile0 = 0, int tile1 = -1, bool wt = false) {
+                               int tile0 = 0, int tile1 = -1) {
     const int wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
     const int l = threadIdx.x & 63, r = l & 15, kk = l >> 4;
     const int tend = tile1 < 0 ? (nf + 7) / 8 : tile1;
@@ -1011,24 +982,6 @@ __device__ inline void gridy_m(const double *In, const GridyB &gb, double *__res
             // 4 latitudes (4 lines) instead of 4 of 16 latitudes (16 lines)
             accS = MFMA64(half ? gb.b01[s] : gb.b00[s], a0, accS);
             accA = MFMA64(half ? gb.b11[s] : gb.b10[s], a1, accA);
-        }
-        if (wt) {
-            // the (Re, Im) pair of field fa is held by lanes r and r ^ 1: lane p stores
-            // both for the rows q = p, p + 2, as one 16-B write-through store each
-            // (the same values; ok is the same on both lanes of a pair)
-            double *vr = varm + (size_t)m * kVIm + fa * 2;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int j = 16 * half + kk + 4 * q;
-                const double n_own = accS[q] + accA[q], s_own = accS[q] - accA[q];
-                const double n_oth = __shfl_xor(n_own, 1), s_oth = __shfl_xor(s_own, 1);
-                if (!ok || j >= kIY || (q & 1) != p) continue;
-                const double nre = p ? n_oth : n_own, nim = p ? n_own : n_oth;
-                const double sre = p ? s_oth : s_own, sim = p ? s_own : s_oth;
-                store2(vr, (size_t)(kIL - 1 - j) * kVIl, nre, nim, true);
-                store2(vr, (size_t)j * kVIl, sre, sim, true);
-            }
-            continue;
         }
         if (!ok) continue;
         // m-major inverse Fourier coefficients vim[m][lat][f][p]: column r = 2 (fa - f0) + p
@@ -1228,7 +1181,7 @@ __device__ __attribute__((always_inline)) inline void row_gridx_half(double *A, 
 __device__ __attribute__((always_inline)) inline void row_specx_pair(const double *x48, double *S, bool act,
                                                                      double *__restrict__ vfm,
                                                                      const double *__restrict__ wa, int f, int j,
-                                                                     int h, bool wt = false) {
+                                                                     int h) {
     if (act) {
 #pragma unroll
         for (int i = 0; i < 48; ++i) S[(48 * h + i) * kRowLd + f] = x48[i];
@@ -1264,7 +1217,7 @@ __device__ __attribute__((always_inline)) inline void row_specx_pair(const doubl
             re = E(47);
             im = -O(47);
         }
-        store2(vfm, (size_t)j * kVLs + f * 2 + (size_t)m * kVFm, re * scale, im * scale, wt);
+        store2(vfm, (size_t)j * kVLs + f * 2 + (size_t)m * kVFm, re * scale, im * scale);
     }
 }
 
@@ -1318,512 +1271,22 @@ __global__ __launch_bounds__(kRowThreads) void k_st_rows(const double *__restric
     stamp(dbg, 0, 4);
 }
 
-// With GPU physics the grid stage splits by role in ONE launch: blocks 0..47 take a
-// latitude row's dynamics (gridx of the 50 level-j2 fields, grid-point dynamics ->
-// F), blocks 48..95 the same row's physics (gridx of phypar's 41 level-1 fields,
-// phypar per column -> P); the two halves of the step's grid work run side by side
-// and meet in k_st_specx, which adds P to F where grtend adds it (dyn_grtend.f90:225).
-__global__ __launch_bounds__(kRowThreads) void k_st_grid(
-    const double *__restrict__ varm, double *__restrict__ F, double *__restrict__ P, const double *__restrict__ wa,
-    const double *__restrict__ cosgr, const DynTables *__restrict__ T, const double *__restrict__ bc,
-    double *__restrict__ rad, const PhysTables *__restrict__ PT, int lradsw, long long *dbg) {
-    __shared__ double A[kFftN * kRowLd], was[kFftWa];
-    constexpr int n1 = kNInv1P, nin = kNInvP;
-    if (threadIdx.x < kFftWa) was[threadIdx.x] = wa[threadIdx.x];
-    __syncthreads();
-    constexpr int nphys = (n1 - kPT1) + (nin - (n1 + 2 * kKX + 2));  // 25 + 16 = 41
-    const bool is_phys = blockIdx.x >= kIL;
-    const int j = is_phys ? blockIdx.x - kIL : blockIdx.x, tid = threadIdx.x;
-    const double cj = cosgr[j];
-    stamp(dbg, 0, 0);
-    // gridx of the role's fields (field index f of the step's nin inverse transforms)
-    if (!is_phys) {
-        if (tid < kNInv) {
-            const int f = tid < kNInv1 ? tid : n1 + (tid - kNInv1);  // [vor div t tr] | [ucos vcos psdx psdy]
-            row_gridx(A, varm, was, f, j, f >= n1, cj);
-        }
-    } else if (tid < nphys) {
-        const int f = tid < n1 - kPT1 ? kPT1 + tid : n1 + 2 * kKX + 2 + (tid - (n1 - kPT1));
-        row_gridx(A, varm, was, f, j, f >= n1, cj);
-    }
-    __syncthreads();
-    stamp(dbg, 0, 1);
-    if (tid >= kIX) return;
-    const int i = tid, pt = j * kIX + i;
-    auto g = [&](int f) { return A[i * kRowLd + f]; };
-    if (!is_phys) {
-        double dummy[kKX];
-        gridpoint_column(j, n1, g, false, dummy, dummy, dummy, dummy,
-                         [&](int f, double v) { F[(size_t)f * kGF + pt] = v; }, T);
-        stamp(dbg, 0, 2);
-        return;
-    }
-    double ua[kKX], va[kKX], ta[kKX], qa[kKX], ph[kKX], ut[kKX], vt[kKX], tt[kKX], qt[kKX];
-#pragma unroll
-    for (int k = 0; k < kKX; ++k) {
-        ua[k] = g(n1 + 2 * kKX + 2 + k);
-        va[k] = g(n1 + 3 * kKX + 2 + k);
-        ta[k] = g(kPT1 + k);
-        qa[k] = g(kPQ1 + k);
-        ph[k] = g(kPPhi1 + k);
-    }
-    phys_column(pt, ua, va, ta, qa, ph, g(kPPs1), bc, rad, PT, &PT->fband[0][0], lradsw != 0, ut, vt, tt, qt);
-#pragma unroll
-    for (int k = 0; k < kKX; ++k) {
-        P[(size_t)k * kGF + pt] = ut[k];
-        P[(size_t)(kKX + k) * kGF + pt] = vt[k];
-        P[(size_t)(2 * kKX + k) * kGF + pt] = tt[k];
-        P[(size_t)(3 * kKX + k) * kGF + pt] = qt[k];
-    }
-    stamp(dbg, 0, 2);
-}
-
-// specx (with GPU physics), one latitude row per block: the row's F[f][ngp] and the
-// physics tendencies P[4 kx][ngp] staged in LDS with coalesced loads (all issued
-// before the first LDS store; 8 waves for the memory-level parallelism); then one
-// field per thread: F (+ P for the u, v, t, q fields: the dynamical tendency first,
-// as grtend adds them), x cosgr(j) for vdspec's inputs, rfftf -> m-major coefficients
-constexpr int kSpecxThreads = 512;
-__global__ __launch_bounds__(kSpecxThreads) void k_st_specx(const double *__restrict__ F, const double *__restrict__ P,
-                                                            double *__restrict__ vfm, const double *__restrict__ wa,
-                                                            const double *__restrict__ cosgr, long long *dbg) {
-    constexpr int LB = kNFwd + 2, LP = 4 * kKX + 1;        // element-major: lanes (fields) hit distinct banks
-    __shared__ double B[kIX * LB], PB[kIX * LP];            // [lon][f], [lon][slot]
-    __shared__ double was[kFftWa];                          // twiddles: LDS broadcast reads inside the FFT
-    const int j = blockIdx.x, tid = threadIdx.x;
-    stamp(dbg, 2, 0);
-    if (tid < kFftWa) was[tid] = wa[tid];
-    {
-        constexpr int NF = kNFwd * (kIX / 2), NP = 4 * kKX * (kIX / 2);
-        constexpr int RF = (NF + kSpecxThreads - 1) / kSpecxThreads, RP = (NP + kSpecxThreads - 1) / kSpecxThreads;
-        double2 rf[RF], rp[RP];
-#pragma unroll
-        for (int q = 0; q < RF; ++q) {
-            const int i = tid + q * kSpecxThreads, ii = i < NF ? i : NF - 1;
-            rf[q] = reinterpret_cast<const double2 *>(F + (size_t)(ii / (kIX / 2)) * kGF + j * kIX)[ii % (kIX / 2)];
-        }
-#pragma unroll
-        for (int q = 0; q < RP; ++q) {
-            const int i = tid + q * kSpecxThreads, ii = i < NP ? i : NP - 1;
-            rp[q] = reinterpret_cast<const double2 *>(P + (size_t)(ii / (kIX / 2)) * kGF + j * kIX)[ii % (kIX / 2)];
-        }
-#pragma unroll
-        for (int q = 0; q < RF; ++q) {
-            const int i = tid + q * kSpecxThreads, f = i / (kIX / 2), e = 2 * (i % (kIX / 2));
-            if (i < NF) {
-                B[e * LB + f] = rf[q].x;
-                B[(e + 1) * LB + f] = rf[q].y;
-            }
-        }
-#pragma unroll
-        for (int q = 0; q < RP; ++q) {
-            const int i = tid + q * kSpecxThreads, f = i / (kIX / 2), e = 2 * (i % (kIX / 2));
-            if (i < NP) {
-                PB[e * LP + f] = rp[q].x;
-                PB[(e + 1) * LP + f] = rp[q].y;
-            }
-        }
-    }
-    __syncthreads();
-    stamp(dbg, 2, 1);
-    if (tid < kNFwd) {
-        const int f = tid;
-        // F field -> tendency slot of P: u 0..7, v 24..31, t 56..63, q 64..71
-        const int pf = f < kKX ? f : (f >= 3 * kKX && f < 4 * kKX) ? kKX + f - 3 * kKX
-                     : (f >= 7 * kKX && f < 9 * kKX) ? 2 * kKX + f - 7 * kKX : -1;
-        const double cj = cosgr[j];
-        const double *fr = B + f, *pr = PB + (pf < 0 ? 0 : pf);
-        double x[kFftN];
-        // F, then + P (u, v, t, q), then x cosgr(j) (vdspec inputs): one branch per
-        // case around straight-line loops, not a branch per element
-#pragma unroll
-        for (int e = 0; e < kFftN; ++e) x[e] = fr[e * LB];
-        if (pf >= 0) {
-#pragma unroll
-            for (int e = 0; e < kFftN; ++e) x[e] = x[e] + pr[e * LP];
-        }
-        if (f < kNFwdScaled) {
-#pragma unroll
-            for (int e = 0; e < kFftN; ++e) x[e] = x[e] * cj;
-        }
-        row_specx(x, vfm, was, f, j);
-    }
-    stamp(dbg, 2, 2);
-}
-
-// With GPU physics, one latitude row per block (4 waves): gridx of the row's 91
-// inverse transforms (wave 0 the 50 dynamics fields, wave 1 phypar's 41 level-1
-// fields, side by side), then the row's grid-point dynamics (waves 0-1, one column
-// per thread, F -> B) beside phypar (waves 2-3, one column per thread: P into A's
-// columns that only phypar reads, after it has read them), then specx of the 73
-// forward transforms (F, + P where grtend adds it, x cosgr(j) for vdspec's inputs;
-// one transform per thread, spread over the 4 waves) straight into the m-major
-// coefficients.  The same arithmetic as k_st_grid -> k_st_specx, one launch.
-constexpr int kGsThreads = 256;
-static_assert(kNInv <= 64 && kNInvP - kNInv <= 64 && kIX <= 128 && kNFwd <= kGsThreads, "k_st_gridspec roles");
-// P slot s (u 0..7, v 8..15, t 16..23, q 24..31) -> a column of A that only phypar reads
-// (t1 q1 phi1 ps1 at kPT1.., then ucos1 ..)
-__device__ inline int phys_slot_col(int s) { return s < 3 * kKX + 1 ? kPT1 + s : kNInv1P + 2 * kKX + 2 + (s - (3 * kKX + 1)); }
-
-// kWT (SML_DYN_WT): the write-through hand-off stores, a compile-time choice -- with
-// a run-time flag every store of specx's last pass carried both paths (specx 3.1 ->
-// 4.8 us in the default build, r03c)
-template <bool kWT>
-__global__ __launch_bounds__(kGsThreads) void k_st_gridspec(
-    const double *__restrict__ varm, double *__restrict__ vfm, const double *__restrict__ wa,
-    const double *__restrict__ cosgr, const DynTables *__restrict__ T, const double *__restrict__ bc,
-    double *__restrict__ rad, const PhysTables *__restrict__ PT, int lradsw, int wt, long long *dbg) {
-    __shared__ double A[kFftN * kRowLd], B[kFftN * kRowLd];
-    // the FFT twiddles as literals (kFftWa96: the same values as wa, bit for bit), folded
-    // into the unrolled passes instead of LDS reads of a staged table
-    const double *was = kFftWa96;
-    (void)wa;
-    // phypar's per-level constants (PhysTables before fband) and the grid-point
-    // dynamics' (GpTab) staged in LDS with gridx's loads: read from memory where they
-    // are used, each new line of them was a scalar-cache miss the column's dependent
-    // chain waited on (one per phase of the moist side)
-    constexpr int kPtS = (int)(offsetof(PhysTables, fband) / sizeof(double)), kGpS = (int)(sizeof(GpTab) / 8);
-    static_assert(kPtS + kGpS <= kGsThreads && kGpS == 5 * kKX + kIL, "table staging: one value per thread");
-    __shared__ double ptl[kPtS];
-    __shared__ GpTab gpt;
-    constexpr int n1 = kNInv1P;
-    constexpr int nphys = (n1 - kPT1) + (kNInvP - (n1 + 2 * kKX + 2));  // 25 + 16 = 41
-    const int j = blockIdx.x, tid = threadIdx.x;
-    stamp(dbg, 0, 0);
-    double rtab = 0.0;
-    if (tid < kPtS) {
-        rtab = reinterpret_cast<const double *>(PT)[tid];
-    } else if (tid < kPtS + kGpS) {
-        const int e = tid - kPtS, k = e % kKX;
-        const int w = e / kKX;
-        rtab = w == 0 ? T->dhs[k] : w == 1 ? T->dhsr[k] : w == 2 ? T->fsgr[k] : w == 3 ? T->tref[k]
-             : w == 4 ? T->tref3[k] : T->coriol[e - 5 * kKX];
-    }
-    // gridx: transform t (the dynamics fields, then phypar's) on lanes 2 t, 2 t + 1;
-    // its coefficients are loaded before the twiddles are staged, so the two loads
-    // share one memory round trip
-    {
-        const int t = tid >> 1, h = tid & 1;
-        const bool act = t < kNInv + nphys;
-        const int f = t < kNInv ? (t < kNInv1 ? t : n1 + (t - kNInv1))  // [vor div t tr] | [ucos vcos psdx psdy]
-                                : (t - kNInv < n1 - kPT1 ? kPT1 + (t - kNInv)
-                                                         : n1 + 2 * kKX + 2 + (t - kNInv - (n1 - kPT1)));
-        double xi[kMX2 - 1];
-        if (act) row_gridx_load(varm, f, j, xi);
-        if (tid < kPtS) ptl[tid] = rtab;
-        else if (tid < kPtS + kGpS) reinterpret_cast<double *>(&gpt)[tid - kPtS] = rtab;
-        __syncthreads();
-        // (unscaled: the x cosgr(j) of the kcos = 2 fields [f >= n1] is applied where
-        // they are read, below -- the same multiply, off every gridx lane's chain)
-        if (act) row_gridx_half(A, xi, was, f, false, 1.0, h);
-    }
-    __syncthreads();
-    stamp(dbg, 0, 1);
-    const PhysTables *PTl = reinterpret_cast<const PhysTables *>(ptl);  // (fband stays in PT)
-    const double cj = cosgr[j];
-    // phypar of column i, split between the waves, the reference's expressions
-    // unchanged: waves 0-1, after the grid-point dynamics, do the moist part and the
-    // vertical diffusion (phys_thermo, phys_moist, phys_vdif: no radiation needed)
-    // while waves 2-3 do the longwave / surface chain (phys_lw_sfc) -- on a shortwave
-    // step (lradsw) after their own moist part and the shortwave (phys_sw needs the
-    // convective precipitation and cloud top).  The moist side hands its 24 values
-    // over in B's spare columns [kNFwd, kRowLd); waves 2-3 sum the tendencies in
-    // phys_column's order.
-    double rl_tt[kKX], rl_rsw[kKX], rl_us = 0.0, rl_vs = 0.0, rl_sh = 0.0, rl_ev = 0.0, rl_rps = 0.0;
-    static_assert(kRowLd - kNFwd >= 24, "moist-side hand-over: 24 spare slots per column in B");
-    if (tid < 128) {
-        if (tid < kIX) {  // grid-point dynamics of column i -> F in B[i][f]
-            const int i = tid;
-            SML_PST(8);
-            double dummy[kKX];
-            gridpoint_column(j, n1, [&](int f) { return f >= n1 ? A[i * kRowLd + f] * cj : A[i * kRowLd + f]; }, false,
-                             dummy, dummy, dummy, dummy, [&](int f, double v) { B[i * kRowLd + f] = v; }, &gpt, false);
-            SML_PST(9);
-            // the moist / diffusion part of column i's phypar
-            const double *Ai = A + i * kRowLd;
-            double ta[kKX], qa[kKX], ph[kKX];
-#pragma unroll
-            for (int k = 0; k < kKX; ++k) {
-                ta[k] = Ai[kPT1 + k];
-                qa[k] = Ai[kPQ1 + k];
-                ph[k] = Ai[kPPhi1 + k];
-            }
-            PhysThermo h;
-            phys_thermo(ta, qa, ph, Ai[kPPs1], PTl, h);
-            SML_PST(10);
-            double tt[kKX], qt[kKX], precnv, precls, ttv[kKX], qtv[kKX];
-            int itop, icnv;
-            phys_moist(h, PTl, tt, qt, precnv, precls, itop, icnv);
-            SML_PST(11);
-            phys_vdif(h, ph, icnv, PTl, ttv, qtv);
-            SML_PST(12);
-            double *Bh = B + i * kRowLd + kNFwd;
-            // tt[0] is +0 always (convection and condensation leave the top level alone)
-#pragma unroll
-            for (int k = 1; k < kKX; ++k) Bh[k - 1] = tt[k];
-#pragma unroll
-            for (int k = 0; k < kKX; ++k) Bh[7 + k] = ttv[k];
-#pragma unroll
-            for (int k = 0; k < kKX - 1; ++k) Bh[15 + k] = qt[k] + qtv[k];  // final above the surface layer
-            Bh[22] = qt[kKX - 1];
-            Bh[23] = qtv[kKX - 1];
-            SML_PST(13);
-        }
-    } else if (tid - 128 < kIX) {
-        const int i = tid - 128, pt = j * kIX + i;
-        SML_PST(0);
-        const double *Ai = A + i * kRowLd;
-        double ua[kKX], va[kKX], ta[kKX], qa[kKX], ph[kKX];
-#pragma unroll
-        for (int k = 0; k < kKX; ++k) {
-            ua[k] = Ai[n1 + 2 * kKX + 2 + k] * cj;
-            va[k] = Ai[n1 + 3 * kKX + 2 + k] * cj;
-            ta[k] = Ai[kPT1 + k];
-            qa[k] = Ai[kPQ1 + k];
-            ph[k] = Ai[kPPhi1 + k];
-        }
-        const double ps1 = Ai[kPPs1];
-        // the column's boundary fields and fband rows, loaded before the chain that uses them
-        double bcv[kNBc], fbk[kKX][4];
-        bc_load(pt, bc, bcv);
-        fband_rows(&PT->fband[0][0], ta, fbk);
-        double psg, qc[kKX];
-        RadCol rc;     // the column's radiation state: from phys_sw on a shortwave step, else from rad
-        if (lradsw) {  // the shortwave first: its inputs are the moist part's (phys_column's order)
-            PhysThermo h;
-            phys_thermo(ta, qa, ph, ps1, PTl, h);
-            SML_PST(16);
-            double tt[kKX], qt[kKX], precnv, precls;
-            int itop, icnv;
-            phys_moist(h, PTl, tt, qt, precnv, precls, itop, icnv);
-            SML_PST(17);
-            phys_sw(pt, h, ph, precnv, precls, itop, bcv, rad, PTl, rc);
-            SML_PST(18);
-            psg = h.psg;
-            rl_rps = h.rps;
-#pragma unroll
-            for (int k = 0; k < kKX; ++k) qc[k] = h.qa[k];
-        } else {  // phys_thermo's psg, rps and clipped q
-            rad_load(pt, rad, rc);  // (the loads issued together, ahead of the chain that uses them)
-            psg = exp(ps1);
-            rl_rps = 1. / psg;
-#pragma unroll
-            for (int k = 0; k < kKX; ++k) qc[k] = fmax(qa[k], 0.);
-        }
-        SML_PST(1);
-        phys_lw_sfc(pt, ua, va, ta, qc, ph, psg, rl_rps, bcv, rc, PTl, &PT->fband[0][0], fbk, rl_tt, rl_us, rl_vs,
-                    rl_sh, rl_ev);
-        SML_PST(4);
-        // the shortwave heating of the column for the sums after the barrier (from rc:
-        // phys_sw's on a shortwave step, rad's otherwise)
-#pragma unroll
-        for (int k = 0; k < kKX; ++k) rl_rsw[k] = rc.ttrsw[k];
-        // the grid-point dynamics' products (this side has the slack)
-        // (the products below kNFwdScaled are vdspec inputs: x cosgr(j) here, not in specx)
-        gridpoint_products(n1, [&](int f) { return f >= n1 ? A[i * kRowLd + f] * cj : A[i * kRowLd + f]; },
-                           [&](int f, double v) { B[i * kRowLd + f] = f < kNFwdScaled ? v * cj : v; }, &gpt);
-        SML_PST(5);
-    }
-    __syncthreads();
-    SML_PST(20);
-    if (tid >= 128 && tid - 128 < kIX) {  // phys_column's sums (phy_phypar.f90:174-196)
-        const int i = tid - 128;
-        const double *Bh = B + i * kRowLd + kNFwd;
-        const double rps = rl_rps;
-#pragma unroll
-        for (int k = 0; k < kKX; ++k) {
-            const double ttk = (k == 0 ? 0.0 : Bh[k - 1]) + rl_rsw[k] + rl_tt[k];
-            double ttv = Bh[7 + k], utv = 0., vtv = 0.;
-            double qtk;
-            if (k == kKX - 1) {
-                utv = utv + rl_us * rps * PTl->grdsig[kKX - 1];
-                vtv = vtv + rl_vs * rps * PTl->grdsig[kKX - 1];
-                ttv = ttv + rl_sh * rps * PTl->grdscp[kKX - 1];
-                const double qtv = Bh[23] + rl_ev * rps * PTl->grdsig[kKX - 1];
-                qtk = Bh[22] + qtv;
-            } else {
-                qtk = Bh[15 + k];
-            }
-            // F + P where grtend adds phypar's tendencies (u 0..7, v 24..31, t 56..63,
-            // q 64..71), the same additions specx made per sample: its lanes then read F only
-            double *Bi = B + i * kRowLd;
-            Bi[k] = (Bi[k] + (0. + utv)) * cj;  // (x cosgr(j): a vdspec input, scaled here for specx)
-            Bi[3 * kKX + k] = (Bi[3 * kKX + k] + (0. + vtv)) * cj;
-            Bi[7 * kKX + k] = Bi[7 * kKX + k] + (ttk + ttv);
-            Bi[8 * kKX + k] = Bi[8 * kKX + k] + qtk;
-        }
-    }
-    __syncthreads();
-    stamp(dbg, 0, 2);
-    // specx: transform f on lanes 2 f, 2 f + 1, lane h on the samples 2 i + h
-    {
-        const int f = tid >> 1, h = tid & 1;
-        const bool act = f < kNFwd;
-        double x[48];
-        if (act) {
-            // F (+ P, x cosgr(j) for the vdspec inputs: both applied where F was written)
-            const double *fr = B + f + h * kRowLd;
-#pragma unroll
-            for (int i = 0; i < 48; ++i) x[i] = fr[2 * i * kRowLd];
-            fft::rfftf48_reg(x, was);
-        }
-        __syncthreads();  // A's P columns are read: A becomes the pairs' meeting place
-        row_specx_pair(x, A, act, vfm, was, f, j, h, kWT);
-        (void)wt;
-    }
-    stamp(dbg, 0, 3);
-}
-
-// The row kernel with phypar on four lanes per column (sml_physics_quad.hpp; opt-in,
-// SML_DYN_QUAD=1): 8 waves, two per SIMD.  gridx as in
-// k_st_gridspec (lane pairs, waves 0-2); then waves 0-1 run the row's grid-point
-// dynamics and products (one column per thread) beside waves 2-7, whose 384 lanes are
-// 96 quads running phypar level- and band-parallel; each quad then adds its column's
-// tendencies into F (phys_column's sums, one level pair per lane); specx as before.
-// phypar's non-transform inputs (boundary fields, a longwave-only step's radiation
-// state) are loaded by the quads at the start, under gridx.
-constexpr int kGqThreads = 512;
-static_assert(kGqThreads - 128 == 4 * kIX, "one quad per column on waves 2-7");
-template <bool kWT>
-__global__ __launch_bounds__(kGqThreads) void k_st_gridspec_q(
-    const double *__restrict__ varm, double *__restrict__ vfm, const double *__restrict__ wa,
-    const double *__restrict__ cosgr, const DynTables *__restrict__ T, const double *__restrict__ bc,
-    double *__restrict__ rad, const PhysTables *__restrict__ PT, int lradsw, int wt, long long *dbg) {
-    __shared__ double A[kFftN * kRowLd], B[kFftN * kRowLd];
-    const double *was = kFftWa96;
-    (void)wa;
-    constexpr int kPtS = (int)(offsetof(PhysTables, fband) / sizeof(double)), kGpS = (int)(sizeof(GpTab) / 8);
-    static_assert(kPtS + kGpS <= kGqThreads, "table staging: one value per thread");
-    static_assert(kRowLd - kNFwd >= 24 && kRowLd - 1 >= 86, "quad slots in B's and A's spare columns");
-    static_assert(kPT1 == 32 && kPPs1 == 56 && kNInv1P + 2 * kKX + 2 == 75 && kNInvP <= 91,
-                  "quad::lw_slot: A's columns 32..56 and 75..96 are phypar's inputs and spare");
-    __shared__ double ptl[kPtS];
-    __shared__ GpTab gpt;
-    __shared__ QuadK qk;
-    __shared__ double fsr[4 * kIX];  // radlw(1)'s surface row per (column, band), quad_fsr
-    constexpr int n1 = kNInv1P;
-    constexpr int nphys = (n1 - kPT1) + (kNInvP - (n1 + 2 * kKX + 2));  // 25 + 16 = 41
-    const int j = blockIdx.x, tid = threadIdx.x;
-    const bool isq = tid >= 128;
-    const int qi = isq ? (tid - 128) >> 2 : 0, qq = tid & 3, qpt = j * kIX + qi;
-    stamp(dbg, 0, 0);
-    double rtab = 0.0;
-    if (tid < kPtS) {
-        rtab = reinterpret_cast<const double *>(PT)[tid];
-    } else if (tid < kPtS + kGpS) {
-        const int e = tid - kPtS, k = e % kKX;
-        const int w = e / kKX;
-        rtab = w == 0 ? T->dhs[k] : w == 1 ? T->dhsr[k] : w == 2 ? T->fsgr[k] : w == 3 ? T->tref[k]
-             : w == 4 ? T->tref3[k] : T->coriol[e - 5 * kKX];
-    }
-    {
-        const int t = tid >> 1, h = tid & 1;
-        const bool act = t < kNInv + nphys;
-        const int f = t < kNInv ? (t < kNInv1 ? t : n1 + (t - kNInv1))
-                                : (t - kNInv < n1 - kPT1 ? kPT1 + (t - kNInv)
-                                                         : n1 + 2 * kKX + 2 + (t - kNInv - (n1 - kPT1)));
-        double xi[kMX2 - 1];
-        if (act) row_gridx_load(varm, f, j, xi);
-        if (tid < kPtS) ptl[tid] = rtab;
-        else if (tid < kPtS + kGpS) reinterpret_cast<double *>(&gpt)[tid - kPtS] = rtab;
-        __syncthreads();
-        if (act) row_gridx_half(A, xi, was, f, false, 1.0, h);
-        // the quads' surface rows (two dependent loads) and per-block constants, by the
-        // lanes gridx leaves idle
-        for (int e = tid - 192; e >= 0 && e < 4 * kIX; e += kGqThreads - 192)
-            fsr[e] = quad_fsr(bc, &PT->fband[0][0], j * kIX + (e >> 2), e & 3);
-        if (tid == kGqThreads - 1) {
-            const PhysTables *PTl = reinterpret_cast<const PhysTables *>(ptl);
-            phys_entr(PTl, qk.entr);
-            phys_vdif_consts(PTl, qk.vk);
-        }
-    }
-    __syncthreads();
-    stamp(dbg, 0, 1);
-    const PhysTables *PTl = reinterpret_cast<const PhysTables *>(ptl);  // (fband stays in PT)
-    const double cj = cosgr[j];
-    QuadOut qo;
-    SML_PST_T(21, 128);
-    SML_PST_T(8, 0);
-    if (tid < kIX) {  // grid-point dynamics of column i -> F in B[i][f], then its products
-        const int i = tid;
-        auto g = [&](int f) { return f >= n1 ? A[i * kRowLd + f] * cj : A[i * kRowLd + f]; };
-        double dummy[kKX];
-        gridpoint_column(j, n1, g, false, dummy, dummy, dummy, dummy, [&](int f, double v) { B[i * kRowLd + f] = v; },
-                         &gpt, false);
-        // (the products below kNFwdScaled are vdspec inputs: x cosgr(j) here, not in specx)
-        gridpoint_products(n1, g, [&](int f, double v) { B[i * kRowLd + f] = f < kNFwdScaled ? v * cj : v; }, &gpt);
-        SML_PST_T(9, 0);
-    } else if (isq) {
-        // a longwave-only step's radiation state (loaded here, not under gridx: held
-        // across it, it pushed the gridx lanes' registers into scratch)
-        QuadPre pre;
-        {
-            if (!lradsw) {
-#pragma unroll
-                for (int k = 0; k < kKX; ++k) pre.tau[k] = rad[kRadTau2 + ((size_t)qq * kKX + k) * kNGP + qpt];
-                pre.strat0 = rad[kRadStratc + qpt];
-                pre.strat1 = rad[kRadStratc + kNGP + qpt];
-                pre.ssrd = rad[kRadSsrd + qpt];
-#pragma unroll
-                for (int s = 0; s < 2; ++s) pre.ttrsw[s] = rad[kRadTtRsw + (size_t)(2 * qq + s) * kNGP + qpt];
-            }
-        }
-        double *Ai = A + qi * kRowLd;
-        const double u7 = Ai[n1 + 2 * kKX + 2 + kKX - 1] * cj, v7 = Ai[n1 + 3 * kKX + 2 + kKX - 1] * cj;
-        phys_quad<kPT1, kPQ1, kPPhi1, kPPs1>(qq, qpt, j, Ai, B + qi * kRowLd + kNFwd, u7, v7, pre, bc, rad, PTl, &qk, &PT->fband[0][0],
-                  fsr[tid - 128], lradsw != 0, qo);
-        SML_PST_T(29, 128);
-    }
-    __syncthreads();
-    SML_PST_T(20, 128);
-    if (isq) {  // phys_column's sums (phy_phypar.f90:174-196) into F, the quad lane's two levels
-        double *Bi = B + qi * kRowLd;
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-            const int k = 2 * qq + s;
-            const double ttk = qo.ttm[s] + qo.rsw[s] + qo.rlw[s];
-            const double utv = k == kKX - 1 ? qo.utv7 : 0., vtv = k == kKX - 1 ? qo.vtv7 : 0.;
-            // F + P where grtend adds phypar's tendencies (u 0..7, v 24..31, t 56..63, q 64..71)
-            Bi[k] = (Bi[k] + (0. + utv)) * cj;  // (x cosgr(j): a vdspec input, scaled here for specx)
-            Bi[3 * kKX + k] = (Bi[3 * kKX + k] + (0. + vtv)) * cj;
-            Bi[7 * kKX + k] = Bi[7 * kKX + k] + (ttk + qo.ttv[s]);
-            Bi[8 * kKX + k] = Bi[8 * kKX + k] + qo.qtk[s];
-        }
-    }
-    __syncthreads();
-    stamp(dbg, 0, 2);
-    // specx: transform f on lanes 2 f, 2 f + 1, lane h on the samples 2 i + h
-    {
-        const int f = tid >> 1, h = tid & 1;
-        const bool act = f < kNFwd;
-        double x[48];
-        if (act) {
-            const double *fr = B + f + h * kRowLd;
-#pragma unroll
-            for (int i = 0; i < 48; ++i) x[i] = fr[2 * i * kRowLd];
-            fft::rfftf48_reg(x, was);
-        }
-        __syncthreads();  // A's P columns are read: A becomes the pairs' meeting place
-        row_specx_pair(x, A, act, vfm, was, f, j, h, kWT);
-        (void)wt;
-    }
-    stamp(dbg, 0, 3);
-}
-
-// The row kernel with each of phypar's roles on waves of its own (SML_DYN_QUAD=2): 8
-// waves, two per SIMD.  gridx as in k_st_gridspec; then waves 0-1 run the grid-point
-// dynamics and products, waves 2-3 the moist part and vdifsc (one column per lane, the
-// hand-over of k_st_gridspec), waves 4-6 the longwave / surface chain -- on a shortwave
-// step after its own moist part and the shortwave -- on two lanes per column
-// (sml_physics_pair.hpp), which then sum the tendencies into F (phys_column's sums, four
-// levels per lane); specx as before.  The same arithmetic as k_st_gridspec.
+// With GPU physics, one latitude row per block: the row kernel.  8 waves, two per SIMD.
+// gridx of the row's 91 inverse transforms (the 50 level-j2 dynamics fields and
+// phypar's 41 level-1 fields) on lane pairs; then waves 0-1 run the grid-point dynamics
+// and products (one column per thread, F -> B), waves 2-3 phypar's moist part and
+// vdifsc (one column per lane, its results handed over in B's spare columns), waves 4-6
+// the longwave / surface chain -- on a shortwave step after its own moist part and the
+// shortwave -- on two lanes per column (sml_physics_pair.hpp), which then sum the
+// tendencies into F (phys_column's sums, four levels per lane); then specx of the 73
+// forward transforms (F + P where grtend adds it, x cosgr(j) for vdspec's inputs) on
+// lane pairs straight into the m-major coefficients.  Every expression and sum order is
+// phys_column's (the one-lane-per-column form it replaced bit for bit, r05).
 constexpr int kGpThreads = 512;
-template <bool kWT>
 __global__ __launch_bounds__(kGpThreads) void k_st_gridspec_p(
     const double *__restrict__ varm, double *__restrict__ vfm, const double *__restrict__ wa,
     const double *__restrict__ cosgr, const DynTables *__restrict__ T, const double *__restrict__ bc,
-    double *__restrict__ rad, const PhysTables *__restrict__ PT, int lradsw, int wt, long long *dbg) {
+    double *__restrict__ rad, const PhysTables *__restrict__ PT, int lradsw, long long *dbg) {
     __shared__ double A[kFftN * kRowLd], B[kFftN * kRowLd];
     const double *was = kFftWa96;
     (void)wa;
@@ -1832,7 +1295,7 @@ __global__ __launch_bounds__(kGpThreads) void k_st_gridspec_p(
     static_assert(kRowLd - kNFwd >= 24, "moist-side hand-over: 24 spare slots per column in B");
     __shared__ double ptl[kPtS];
     __shared__ GpTab gpt;
-    __shared__ double fsr[4 * kIX];  // radlw(1)'s surface row per (column, band), quad_fsr
+    __shared__ double fsr[4 * kIX];  // radlw(1)'s surface row per (column, band), sfc_fband
     constexpr int kMh = 3 + kKX;
     __shared__ double mhs[kIX * kMh];  // a shortwave step's moist-part hand-over (precnv, precls, itop, rh)
     constexpr int n1 = kNInv1P;
@@ -1878,7 +1341,7 @@ __global__ __launch_bounds__(kGpThreads) void k_st_gridspec_p(
         if (act) row_gridx_half(A, xi, was, f, false, 1.0, h);
         // the surface rows (two dependent loads), by the lanes gridx leaves idle
         for (int e = tid - 192; e >= 0 && e < 4 * kIX; e += kGpThreads - 192)
-            fsr[e] = quad_fsr(bc, &PT->fband[0][0], j * kIX + (e >> 2), e & 3);
+            fsr[e] = sfc_fband(bc, &PT->fband[0][0], j * kIX + (e >> 2), e & 3);
     }
     __syncthreads();
     stamp(dbg, 0, 1);
@@ -1997,8 +1460,7 @@ __global__ __launch_bounds__(kGpThreads) void k_st_gridspec_p(
             fft::rfftf48_reg(x, was);
         }
         __syncthreads();  // A's P columns are read: A becomes the pairs' meeting place
-        row_specx_pair(x, A, act, vfm, was, f, j, h, kWT);
-        (void)wt;
+        row_specx_pair(x, A, act, vfm, was, f, j, h);
     }
     stamp(dbg, 0, 3);
 }
@@ -2019,7 +1481,6 @@ __global__ void k_pack_pfwd(const double *__restrict__ pfwd, double *__restrict_
 // one zonal wavenumber m: specy of the 73 forward transforms, combine and tail of
 // the m's 64 real coefficients x 8 levels (one thread each) on the m's state slice
 // in LDS; with next_j2 > 0 the new state feeds the next step's inverse transforms
-template <bool kWT>
 __global__ __launch_bounds__(kSpecBlk) void k_st_spec(
     const double *__restrict__ vfm, const double *__restrict__ pfl, const double *__restrict__ wt,
     const double *__restrict__ sm, double *__restrict__ sm_out, double *__restrict__ Td, double *__restrict__ phi_out,
@@ -2027,7 +1488,7 @@ __global__ __launch_bounds__(kSpecBlk) void k_st_spec(
     const double *__restrict__ tcorh, const double *__restrict__ qcorh, const DynTables *__restrict__ T, int j1,
     int j4, double dt, double alph, double rob, double wil, const double *__restrict__ pinv,
     double *__restrict__ varm_next, int next_j2, int n1, int nin, const double *__restrict__ tabm,
-    double *__restrict__ state_out, double *__restrict__ io_varm, int wthru, long long *dbg) {
+    double *__restrict__ state_out, double *__restrict__ io_varm, long long *dbg) {
     __shared__ double V[kVFm];            // this m's tables (TabM)
     __shared__ double S[kNInvMax * kCW];  // specy output [f][2 n + p]; then the next step's inputs
     __shared__ double sh[3][kKX][kCW];
@@ -2216,7 +1677,7 @@ __global__ __launch_bounds__(kSpecBlk) void k_st_spec(
         for (int q = 0; q < RS; ++q) v[q] = src[q * kSpecBlk];
 #pragma unroll
         for (int q = 0; q < RS; ++q)
-            store2(sm_out, (size_t)m * kSM + 2 * ((size_t)q * kSpecBlk + threadIdx.x), v[q].x, v[q].y, kWT);
+            store2(sm_out, (size_t)m * kSM + 2 * ((size_t)q * kSpecBlk + threadIdx.x), v[q].x, v[q].y);
     }
     // d) the next step's inverse-transform inputs (k_dyn_prep) and gridy
     if (holds) inv_inputs(Sst, S, Fm, tb, m, next_j2, n1, nin);
@@ -2224,8 +1685,7 @@ __global__ __launch_bounds__(kSpecBlk) void k_st_spec(
     stamp(dbg, sk, 5);
     {
         const int nt = (nin + 7) / 8, per = (nt + kSpecSplit - 1) / kSpecSplit;
-        gridy_m(S, gridy_operands_slice(V + kVPinv), varm_next, m, nin, half * per, min(nt, (half + 1) * per),
-                kWT);
+        gridy_m(S, gridy_operands_slice(V + kVPinv), varm_next, m, nin, half * per, min(nt, (half + 1) * per));
     }
     if (dbg) {  // (diagnostics only: the kernel ends here)
         __syncthreads();
@@ -2554,13 +2014,7 @@ extern "C" int sml_dyn_create(double radius, sml_dynamics **out) {
     }
     build_dyn_indyns(spectral_host_tables(d->sp), &d->tab);
     build_phys_tables(d->tab, &d->ptab);
-    if (const char *e = std::getenv("SML_DYN_FUSED")) d->fused = *e && *e != '0';
-    if (const char *e = std::getenv("SML_DYN_SPLIT_GRID")) d->split_grid = *e && *e != '0';
-    if (const char *e = std::getenv("SML_DYN_QUAD")) d->quad = std::max(0, std::min(2, std::atoi(e)));
     if (const char *e = std::getenv("SML_DYN_NOGRAPH")) d->nograph = *e && *e != '0';
-    if (const char *e = std::getenv("SML_DYN_WT")) d->wt = std::max(0, std::min(3, std::atoi(e)));
-    if (const char *e = std::getenv("SML_CHK_FLAG")) d->chk_flag = *e != '0';
-    if (const char *e = std::getenv("SML_EXIT_GRAPH")) d->exit_graph = *e != '0';
     if (const char *e = std::getenv("SML_DYN_STAMPS"))
         if (*e && *e != '0' && (rc = dalloc(reinterpret_cast<double **>(&d->d_dbg), kStampKernels * kStampBlocks * kStamps))) {
             sml_dyn_destroy(d);
@@ -2779,27 +2233,8 @@ int launch_step_fused(sml_dynamics *d, int j1, int j2, double dt, double alph, d
         SML_HIP(hipGetLastError());
     }
     if (phys) {
-        if (d->split_grid) {  // the two-launch form (A/B reference)
-            hipLaunchKernelGGL(k_st_grid, dim3(2 * kIL), dim3(kRowThreads), 0, st, d->d_varm, d->d_gfwd, d->d_phys,
-                               sd.wa, sd.cosgr, T, d->d_pbc, d->d_rad, d->d_ptab, lradsw ? 1 : 0, d->d_dbg);
-            SML_HIP(hipGetLastError());
-            hipLaunchKernelGGL(k_st_specx, dim3(kIL), dim3(kSpecxThreads), 0, st, d->d_gfwd, d->d_phys, d->d_vfm,
-                               sd.wa, sd.cosgr, d->d_dbg);
-        } else {
-            const bool wrow = d->wt == 1 || d->wt == 2;
-            if (d->quad == 2)
-                hipLaunchKernelGGL(wrow ? k_st_gridspec_p<true> : k_st_gridspec_p<false>, dim3(kIL), dim3(kGpThreads), 0,
-                                   st, d->d_varm, d->d_vfm, sd.wa, sd.cosgr, T, d->d_pbc, d->d_rad, d->d_ptab,
-                                   lradsw ? 1 : 0, wrow ? 1 : 0, d->d_dbg);
-            else if (d->quad == 1)
-                hipLaunchKernelGGL(wrow ? k_st_gridspec_q<true> : k_st_gridspec_q<false>, dim3(kIL), dim3(kGqThreads), 0,
-                                   st, d->d_varm, d->d_vfm, sd.wa, sd.cosgr, T, d->d_pbc, d->d_rad, d->d_ptab,
-                                   lradsw ? 1 : 0, wrow ? 1 : 0, d->d_dbg);
-            else
-                hipLaunchKernelGGL(wrow ? k_st_gridspec<true> : k_st_gridspec<false>, dim3(kIL), dim3(kGsThreads), 0, st,
-                                   d->d_varm, d->d_vfm, sd.wa, sd.cosgr, T, d->d_pbc, d->d_rad, d->d_ptab,
-                                   lradsw ? 1 : 0, wrow ? 1 : 0, d->d_dbg);
-        }
+        hipLaunchKernelGGL(k_st_gridspec_p, dim3(kIL), dim3(kGpThreads), 0, st, d->d_varm, d->d_vfm, sd.wa, sd.cosgr, T,
+                           d->d_pbc, d->d_rad, d->d_ptab, lradsw ? 1 : 0, d->d_dbg);
         SML_HIP(hipGetLastError());
     } else {
         hipLaunchKernelGGL(k_st_rows, dim3(kIL), dim3(kRowThreads), 0, st, d->d_varm, d->d_vfm, sd.wa, sd.cosgr, T,
@@ -2809,12 +2244,11 @@ int launch_step_fused(sml_dynamics *d, int j1, int j2, double dt, double alph, d
     const int j4 = (alph == 0.0) ? j2 : 1;
     const int cur = d->sm_cur;
     if (next_j2 > 0) d->sm_cur = 1 - cur;  // the next step reads what this one writes
-    const bool wspec = d->wt == 1 || d->wt == 3;
-    hipLaunchKernelGGL(wspec ? k_st_spec<true> : k_st_spec<false>, dim3(kSpecStride * kSpecSplit), dim3(kSpecBlk), 0, st, d->d_vfm, d->d_pfl, sd.wt,
+    hipLaunchKernelGGL(k_st_spec, dim3(kSpecStride * kSpecSplit), dim3(kSpecBlk), 0, st, d->d_vfm, d->d_pfl, sd.wt,
                        sm_buf(d, cur), sm_buf(d, 1 - cur), d->d_tend,
                        d->d_phi, d->d_phis, d->d_tcorh, d->d_qcorh, T, j1, j4, dt, alph, rob, wil, sd.pinv, d->d_varm,
                        next_j2, n1, nin, d->d_tabm + (size_t)(d->d_tab - d->d_tabs) * kMX * kTabMDoubles, d->d_state,
-                       next_j2 > 0 ? nullptr : d->io_exit, wspec ? 1 : 0, d->d_dbg);
+                       next_j2 > 0 ? nullptr : d->io_exit, d->d_dbg);
     SML_HIP(hipGetLastError());
     return SML_OK;
 }
@@ -2954,11 +2388,11 @@ int window_impl(sml_dynamics *d, int nleap, double delt, double alph, double rob
     const double key[8] = {(double)nleap, delt,  alph, rob, wil, d->phys_on ? 1.0 : 0.0, d->fused ? 1.0 : 0.0,
                            prepared ? 2.0 : 1.0};
     // the exit's fixed arguments (its count and the store's value change per launch)
-    const void *exit_key[10] = {};
+    const void *exit_key[9] = {};
     if (exit) {
-        const void *k[10] = {exit->varm,   exit->fc4,     exit->fc2,    exit->ex.mm,
-                             exit->ex.in4, exit->ex.inlp, exit->ex.cnt, (const void *)(intptr_t)exit->ex.timeout,
-                             exit->store,  exit->ex.sig};
+        const void *k[9] = {exit->varm,   exit->fc4,     exit->fc2,    exit->ex.mm,
+                            exit->ex.in4, exit->ex.inlp, exit->ex.cnt, (const void *)(intptr_t)exit->ex.timeout,
+                            exit->store};
         std::memcpy(exit_key, k, sizeof k);
     }
     const bool exit_same =
@@ -3411,7 +2845,7 @@ int launch_io_check(sml_dynamics *d, hipStream_t st, double *d_minmax) {
     if (int rc = spectral_gridx_range(d->sp, cv, cg, kNIo, 0, kNIoWind, cst)) return rc;
     double *mm = d_minmax ? d_minmax : d->d_minmax;
     // on the check stream, for run_model's exit: the counter hand-off (4 adds per check)
-    const bool counted = cst != st && d->chk_flag && !d_minmax;
+    const bool counted = cst != st && !d_minmax;
     hipLaunchKernelGGL(k_io_minmax, dim3(4), dim3(1024), 0, cst, cg, mm, counted ? d->d_chk_cnt : nullptr);
     SML_HIP(hipGetLastError());
     if (counted) ++d->chk_count;
@@ -3509,11 +2943,11 @@ extern "C" int sml_dyn_run_model(sml_dynamics *d, const double *d_grid4d, const 
         const bool phys = d->phys_on;
         d->sm_cur = 0;  // the window's chain starts in buffer 0
         // the exit inside the window graph: needs the check's counter hand-off (no event
-        // wait between the window and the exit; the check below counts whenever chk_flag
-        // is on) and the graph path.  Its per-launch values go through d_xa
+        // wait between the window and the exit; the check below counts unless captured)
+        // and the graph path.  Its per-launch values go through d_xa
         hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
         SML_HIP(hipStreamIsCapturing(st, &cap));
-        const bool xg = d->exit_graph && !d->nograph && d->chk_flag && cap == hipStreamCaptureStatusNone;
+        const bool xg = !d->nograph && cap == hipStreamCaptureStatusNone;
         if (xg && !d->d_xa) SML_HIP(hipMalloc(&d->d_xa, 2 * sizeof(uint64_t)));
         hipLaunchKernelGGL(k_io_entry, dim3(kMX), dim3(kSpecThreads), 0, st, d->d_vfm, d->d_pfl, sd.wt, d->d_state,
                            sm_buf(d, 0), d->d_chk, d->d_phis,
@@ -3529,8 +2963,6 @@ extern "C" int sml_dyn_run_model(sml_dynamics *d, const double *d_grid4d, const 
                         0};
             es.ex.cnt = d->d_chk_cnt;
             es.ex.xa = d->d_xa;
-            es.ex.sig = d->exit_sig;  // the forecast hop from the exit's blocks (sml::dyn_run_model_signal)
-            d->exit_sig = nullptr;    // one launch
             es.ex.late = d->d_chk_late;
             es.ex.timeout = d->chk_timeout;
             d->chk_pending = false;
@@ -3543,8 +2975,6 @@ extern "C" int sml_dyn_run_model(sml_dynamics *d, const double *d_grid4d, const 
         if (int rc = sml_dyn_window(d, nleap, delt, alph, rob, wil, stream)) return rc;
     }
     IoExit ex{0.000001, d->mm_last, d_grid4d, d_logp};
-    ex.sig = d->exit_sig;
-    d->exit_sig = nullptr;  // one launch
     if (d->chk_pending && d->chk_counted) {
         // the exit kernel itself waits for the check's counter: no event wait (a
         // barrier packet with a cross-queue dependency) on the window's stream.  The
@@ -3642,15 +3072,18 @@ extern "C" int sml_dyn_set_check_timeout(sml_dynamics *d, int64_t microseconds) 
     return sml::dyn_set_check_timeout(d, (long long)std::min<int64_t>(microseconds, INT64_MAX / 100) * 100);
 }
 
+extern "C" int sml_dyn_set_fused(sml_dynamics *d, int fused) {
+    SML_REQUIRE(d, "null context");
+    d->fused = fused != 0;
+    return SML_OK;
+}
+
 extern "C" int sml_dyn_check_stream(const sml_dynamics *d, void **stream) {
     SML_REQUIRE(d && stream, "null argument");
     *stream = d->chk_stream;
     return SML_OK;
 }
 
-// the next run_model's exit kernel adds *adds to *counter once its forecast is
-// released (each of its blocks adds 1): the hybrid loop's forecast hop without a
-// signal kernel behind the exit
 // the event behind the last safety check issued on the check stream (null if none)
 int sml::dyn_check_event(sml_dynamics *d, void **ev) {
     SML_REQUIRE(d && ev, "null argument");
@@ -3673,13 +3106,6 @@ int sml::dyn_run_model_exit_store(sml_dynamics *d, uint64_t *flag, uint64_t valu
     SML_REQUIRE(d, "null argument");
     d->exit_store = flag;
     d->exit_store_value = value;
-    return SML_OK;
-}
-
-int sml::dyn_run_model_signal(sml_dynamics *d, uint64_t *counter, int *adds) {
-    SML_REQUIRE(d && counter && adds, "null argument");
-    d->exit_sig = counter;
-    *adds = spectral_exit_blocks();
     return SML_OK;
 }
 

@@ -87,12 +87,6 @@ struct sml_hybrid {
     int chain_mode = SML_CHAIN_AUTO;
     bool chain = false;
     bool use_events = false, use_kernels = false;
-    // kernel hops: the forecast hop signalled by run_model's exit kernel itself (each of
-    // its blocks releases its stores and adds 1 to the hop's word) instead of a signal
-    // kernel behind it -- SML_HOP_FUSED=1 at create; measured same-box within noise of
-    // the signal kernel (N = 1: 1118-1123 vs 1125-1131, 8-rank share 1190-1197 vs 1191),
-    // so not the default
-    bool fused_lm_signal = false;
     int hop_mode = SML_HOP_AUTO;
     // caller-owned device buffers
     double *fb = nullptr, *lm = nullptr, *ov = nullptr, *g4 = nullptr, *g2 = nullptr, *pr = nullptr, *f4 = nullptr,
@@ -116,8 +110,6 @@ struct sml_hybrid {
     // exchange path (send slab -> ncclAllGather -> advance from the receive slab)
     bool force_exchange = false;
     int64_t allgathers = 0;  // ncclAllGather calls issued by sml_hybrid_step (sml_hybrid_exchanges)
-    // SML_HYBRID_ASM=0 (read at create): the one-rank step assembles separately (A/B)
-    bool fuse_asm = true;
     // get_tisr_by_date (mpires.f90:1644-1676): a table of hourly global tisr fields
     // [nhours][48][96] on the device, the calendar's start year, the hours before the
     // first prediction step and the hours per step; t = steps advanced so far
@@ -511,9 +503,10 @@ bool dispatch_serialised() { return env_on("AMD_SERIALIZE_KERNEL") || env_on("RO
 
 }  // namespace
 
-// hop mode: SML_HOP_AUTO (wait-value hops unless dispatch is serialised or
-// SML_HYBRID_EVENTS=1), SML_HOP_WAIT_VALUE, SML_HOP_EVENTS.  Both streams are drained
-// first, so no wait of one kind is left pending on a signal of the other.
+// hop mode: SML_HOP_AUTO (kernel hops on CU-disjoint streams, event hops when dispatch
+// is serialised or SML_HYBRID_EVENTS=1, wait-value hops otherwise), SML_HOP_WAIT_VALUE,
+// SML_HOP_EVENTS, SML_HOP_KERNEL.  Both streams are drained first, so no wait of one
+// kind is left pending on a signal of the other.
 extern "C" int sml_hybrid_set_hop_mode(sml_hybrid *h, int mode) {
     SML_REQUIRE(h && (mode == SML_HOP_AUTO || mode == SML_HOP_WAIT_VALUE || mode == SML_HOP_EVENTS ||
                       mode == SML_HOP_KERNEL),
@@ -525,10 +518,10 @@ extern "C" int sml_hybrid_set_hop_mode(sml_hybrid *h, int mode) {
         // kernel hops only when the two streams run on disjoint CUs (res_cus > 0): a
         // waiting finish's blocks then never occupy a CU the window (their producer)
         // needs; not when dispatch is serialised (a waiting kernel would hold its queue
-        // ahead of its producer) or SML_HYBRID_EVENTS / SML_HYBRID_HOPK=0 asks otherwise
+        // ahead of its producer) or SML_HYBRID_EVENTS=1 asks for event hops (the PMC
+        // passes of profiles/collect.sh)
         h->use_events = env_on("SML_HYBRID_EVENTS") || dispatch_serialised();
-        const char *hk = getenv("SML_HYBRID_HOPK");
-        h->use_kernels = !h->use_events && !(hk && *hk == '0') && h->res_cus > 0;
+        h->use_kernels = !h->use_events && h->res_cus > 0;
     } else {
         h->use_events = mode == SML_HOP_EVENTS;
         h->use_kernels = mode == SML_HOP_KERNEL;
@@ -709,8 +702,6 @@ extern "C" int sml_hybrid_create(sml_reservoirs *res, sml_dynamics *dyn, sml_com
             h->side = h->main;
         }
     }
-    if (const char *e = std::getenv("SML_HYBRID_ASM")) h->fuse_asm = *e != '0';
-    if (const char *e = std::getenv("SML_HOP_FUSED")) h->fused_lm_signal = *e == '1';
     for (hipEvent_t &e : h->ev)
         if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return bail(fail(SML_ERR_HIP, "event"));
     if (int rc = sml_hybrid_set_hop_mode(h, SML_HOP_AUTO)) return bail(rc);
@@ -720,8 +711,6 @@ extern "C" int sml_hybrid_create(sml_reservoirs *res, sml_dynamics *dyn, sml_com
         hipDeviceSynchronize() != hipSuccess)
         return bail(fail(SML_ERR_HIP, "sequence counters"));
     *h->h_late = 0;
-    if (const char *e = std::getenv("SML_HOP_TIMEOUT_US"))  // (tests: sml_hybrid_set_hop_timeout)
-        if (int rc = sml_hybrid_set_hop_timeout(h, std::atoll(e))) return bail(rc);
     h->xw = h->nout;
     if (world > 1) {
         std::vector<int32_t> perm(h->numregions);
@@ -1218,16 +1207,12 @@ extern "C" int sml_hybrid_advance(sml_hybrid *h, const double *d_outvec_all) {
             return rc;
         }
     }
-    int exit_adds = 0;
-    if (hops && h->use_kernels && h->fused_lm_signal)
-        if (int rc = sml::dyn_run_model_signal(h->dyn, h->d_seq + sml_hybrid::kHopLm * sml_hybrid::kSeqStride,
-                                               &exit_adds))
-            return rc;
     // kernel hops: the forecast's signal is a store that run_model issues right behind
-    // its exit (inside the window graph when the exit is captured there)
-    // (the loop's sequence number moves only once run_model is enqueued: a run_model
-    // that fails leaves no store pending and no finish waiting for one)
-    const bool exit_store = hops && h->use_kernels && exit_adds == 0;
+    // its exit (inside the window graph when the exit is captured there); the loop's
+    // sequence number moves only once run_model is enqueued, so a run_model that fails
+    // leaves no store pending and no finish waiting for one.  (The exit's own blocks
+    // signalling instead, an agent-scope release each, measured no faster: DESIGN.md §4c)
+    const bool exit_store = hops && h->use_kernels;
     const uint64_t lm_next = h->seq[sml_hybrid::kHopLm] + 1;
     if (exit_store)
         if (int rc = sml::dyn_run_model_exit_store(h->dyn, h->d_seq + sml_hybrid::kHopLm * sml_hybrid::kSeqStride,
@@ -1240,9 +1225,7 @@ extern "C" int sml_hybrid_advance(sml_hybrid *h, const double *d_outvec_all) {
             return rc;
         }
     if (exit_store) h->seq[sml_hybrid::kHopLm] = lm_next;
-    if (exit_adds > 0) {  // the exit's blocks each add 1 to the hop's word once released
-        h->seq[sml_hybrid::kHopLm] += (uint64_t)exit_adds;
-    } else if (hops && !exit_store) {
+    if (hops && !exit_store) {
         if (int rc = hop_signal(h, sml_hybrid::kHopLm, s)) return rc;
     } else if (!h->overlap && h->ncs) {
         if (int rc = sml_res_tile_local_model(h->res, h->f4, h->f2, h->lm, s)) return rc;
@@ -1285,11 +1268,10 @@ extern "C" int sml_hybrid_step(sml_hybrid *h) {
     if (world > 1 && !h->comm->comm)
         return fail(SML_ERR_STATE, "rank %d of %d has no transport: exchange through sml_hybrid_advance_slabs",
                     h->comm->rank, world);
-    // one rank: the exchange is the identity, so the finish assembles the grids itself
-    // (SML_HYBRID_ASM=0: the separate assembly, for A/B); forced, it goes through the
-    // transport as at world > 1
+    // one rank: the exchange is the identity, so the finish assembles the grids itself;
+    // forced, it goes through the transport as at world > 1
     const bool identity = world == 1 && !h->force_exchange;
-    const bool fuse = identity && h->overlap && sml::res_in_global_order(h->res) && h->fuse_asm;
+    const bool fuse = identity && h->overlap && sml::res_in_global_order(h->res);
     if (int rc = predict_impl(h, fuse)) return rc;
     if (identity) return sml_hybrid_advance(h, h->ov);
     // (world > 1, or world 1 forced through the transport)

@@ -29,7 +29,6 @@ int res_finish_wait(sml_reservoirs *c, const uint64_t *flag, uint64_t value, uns
 int dyn_run_model_wait(sml_dynamics *d, const uint64_t *flag, uint64_t value, unsigned *late, long long timeout);
 // the give-up time of the run_model exit's wait for its safety check (ticks)
 int dyn_set_check_timeout(sml_dynamics *d, long long timeout);
-int dyn_run_model_signal(sml_dynamics *d, uint64_t *counter, int *adds);
 // the next run_model's exit is followed by a one-lane store of value to *flag (inside the
 // window graph when the exit is captured there)
 int dyn_run_model_exit_store(sml_dynamics *d, uint64_t *flag, uint64_t value);

@@ -30,6 +30,17 @@ struct PairOut {
     double ust, vst, shf, evp, rps;
 };
 
+// radlw(1)'s surface emission row fband(nint(tsfc), jb) of column pt (suflux's tsfc =
+// sst + fmask (stl - sst), phy_suflux.f90, from the boundary fields alone): the row
+// kernel stages it during gridx, off the physics' chain of dependent loads
+__device__ __forceinline__ double sfc_fband(const double *__restrict__ bc, const double *__restrict__ fbt, int pt,
+                                            int jb) {
+    const double tsea = bc[(size_t)kBcSst * kNGP + pt], fmask = bc[(size_t)kBcFmask1 * kNGP + pt];
+    const double stl = bc[(size_t)kBcStl * kNGP + pt];
+    const double tsfc = tsea + fmask * (stl - tsea);
+    return phys::fband_row(fbt, tsfc)[jb];
+}
+
 namespace pairx {
 
 // the partner's value (lanes ^ 1: DPP quad permutation 1 0 3 2)

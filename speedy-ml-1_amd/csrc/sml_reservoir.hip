@@ -113,8 +113,7 @@ struct sml_reservoirs {
     uint16_t *d_a_oc = nullptr;   // overflow entries: column
     void *d_a_ov = nullptr;       //                   value
     void *d_zero = nullptr;       // 256 zero bytes: the target of the balanced update's unused loads
-    bool no_ell = false;          // SML_NO_ELL=1 at create: CSR copies only (A/B, tests)
-    int upd_depth = 2;            // passes in flight in the balanced update (SML_UPD_DEPTH=3 at create)
+    bool no_ell = false;          // CSR copies only (sml_res_set_reference_paths)
     double *d_x[2] = {nullptr, nullptr};
     int cur = 0;
     double *d_meanstd = nullptr;
@@ -124,24 +123,20 @@ struct sml_reservoirs {
     // SPEEDY's latency-bound kernels stall behind it; paced at 2048 waves (~4.7 TB/s)
     // the overlapped step is 1.75 ms instead of 1.98 (profiles/r01p).  On CUs of its
     // own the pacing does not matter: sml_res_set_read_waves(0).
-    // SML_READ_WAVES overrides both.
     int read_waves = 2048;
-    int upd_blocks = 0;  // cap on the update's grid in sml_res_step_begin (0: none; SML_UPD_BLOCKS)
-    // sml_res_step_begin's form (sml_res_set_begin_mode; SML_BEGIN overrides): 0 the
-    // update grid then the v_ml readout grid, 1 one fused launch (k_res_begin, 2 blocks
-    // per CU), 2 fused with the readout's loads unrolled twice (1 block per CU)
+    // sml_res_step_begin's form (sml_res_set_begin_mode): 0 the update grid then the
+    // v_ml readout grid, 1 one fused launch (k_res_begin, 2 blocks per CU), 2 fused with
+    // the readout's loads unrolled twice (1 block per CU)
     int begin_mode = 0;
-    // A/B knobs read once at create (SML_UPD_PARTS: parts per region of the update,
-    // 0 = automatic; SML_UPD_OCC=2: the update's 8-waves-per-EU launch bound; SML_BEGIN:
-    // overrides begin_mode when >= 0), never on the enqueue path of a step
-    int upd_parts = 0, begin_env = -1;
-    bool upd_occ2 = false;
-    // the balanced update (k_res_update_bal; SML_UPD_BAL=0 at create: k_res_update):
+    // the balanced update (k_res_update_bal; k_res_update per region where the layout
+    // does not fit it, or forced by sml_res_set_reference_paths):
     // row0 [nlocal+1] = the regions' rows concatenated; blk_r0 [grid] = the region each
     // block's share starts in, for the grid it was built for (upd_grid: the CUs the
     // launches get, sml_res_set_update_cus; 0 = every CU of the device)
     bool upd_bal = true;
-    bool finish_ungrouped = false;  // SML_FIN_UNGROUPED=1 at create: the finish one thread per output (A/B)
+    // the v_p finish one thread per output (vp_sum) instead of in column groups: the
+    // fallback when ncs does not fit the groups, or forced (sml_res_set_reference_paths)
+    bool finish_ungrouped = false;
     // the next grid finish waits in-kernel for *fin_wflag >= fin_wval (sml::res_finish_wait)
     const uint64_t *fin_wflag = nullptr;
     uint64_t fin_wval = 0;
@@ -1076,20 +1071,6 @@ int dalloc(T **p, size_t count) {
     return SML_OK;
 }
 
-// W_out's pool: SML_WOUT_MEM=uncached / coherent selects hipExtMallocWithFlags'
-// memory types (A/B experiments on how the readout's stream shares the memory-side
-// cache with SPEEDY's window); default hipMalloc
-int dalloc_wout(void **p, size_t bytes) {
-    const char *e = std::getenv("SML_WOUT_MEM");
-    if (e && (!std::strcmp(e, "uncached") || !std::strcmp(e, "coherent"))) {
-        const unsigned flags = !std::strcmp(e, "uncached") ? hipDeviceMallocUncached : hipDeviceMallocFinegrained;
-        SML_HIP(hipExtMallocWithFlags(p, bytes ? bytes : 16, flags));
-        return SML_OK;
-    }
-    SML_HIP(hipMalloc(p, bytes ? bytes : 16));
-    return SML_OK;
-}
-
 int dalloc_bytes(void **p, size_t bytes) {
     *p = nullptr;
     SML_HIP(hipMalloc(p, bytes ? bytes : 16));
@@ -1524,16 +1505,6 @@ int res_create_impl(int numregions, int nlocal, const int *region_ids, const uns
     c->leakage = leakage;
     c->generic = ninp_generic != nullptr;
     if (c->generic) c->out_l.assign(out_index, out_index + nout);
-    if (const char *e = std::getenv("SML_READ_WAVES")) c->read_waves = std::max(0, std::atoi(e));
-    if (const char *e = std::getenv("SML_UPD_BLOCKS")) c->upd_blocks = std::max(0, std::atoi(e));
-    if (const char *e = std::getenv("SML_UPD_PARTS")) c->upd_parts = std::max(0, std::atoi(e));
-    if (const char *e = std::getenv("SML_UPD_OCC")) c->upd_occ2 = *e == '2';
-    if (const char *e = std::getenv("SML_BEGIN")) c->begin_env = std::max(0, std::min(2, std::atoi(e)));
-    if (const char *e = std::getenv("SML_UPD_BAL")) c->upd_bal = *e != '0';
-    if (const char *e = std::getenv("SML_FIN_UNGROUPED")) c->finish_ungrouped = *e == '1';
-    if (const char *e = std::getenv("SML_NO_ELL")) c->no_ell = *e == '1';
-    if (const char *e = std::getenv("SML_UPD_DEPTH")) c->upd_depth = std::atoi(e) == 3 ? 3 : 2;
-    SML_REQUIRE(c->read_waves >= 0, "bad read_waves");
     (void)hipGetDevice(&c->device);
     (void)hipDeviceGetAttribute(&c->ncu, hipDeviceAttributeMultiprocessorCount, c->device);
     {
@@ -1636,7 +1607,7 @@ int res_create_impl(int numregions, int nlocal, const int *region_ids, const uns
     if ((rc = dalloc(&c->d_rd, nlocal)) || (rc = dalloc(&c->d_a_rp, c->tot_a_rp)) ||
         (rc = dalloc(&c->d_a_col, c->tot_a_nz)) || (rc = dalloc_bytes(&c->d_a_val, c->tot_a_nz * wb)) ||
         (rc = dalloc(&c->d_w_rp, c->tot_w_rp)) || (rc = dalloc(&c->d_w_col, c->tot_w_nz)) ||
-        (rc = dalloc_bytes(&c->d_w_val, c->tot_w_nz * wb)) || (rc = dalloc_wout(&c->d_wout, c->tot_wout * wb)) ||
+        (rc = dalloc_bytes(&c->d_w_val, c->tot_w_nz * wb)) || (rc = dalloc_bytes(&c->d_wout, c->tot_wout * wb)) ||
         (rc = dalloc_bytes(&c->d_wlm, std::max<int64_t>(c->tot_wlm, 1) * wb)) ||
         (rc = dalloc(&c->d_x[0], c->tot_xaug)) || (rc = dalloc(&c->d_x[1], c->tot_xaug)) ||
         (rc = dalloc(&c->d_meanstd, (size_t)nlocal * 2 * kMeanStd)) ||
@@ -1774,7 +1745,7 @@ extern "C" int sml_res_set_update_cus(sml_reservoirs *c, int cus) {
 }
 
 // 1 when sml_res_step / _begin run the balanced update (k_res_update_bal), 0 for the
-// per-region k_res_update (a region in CSR form, n > 7168, ninp > 1024, SML_UPD_BAL=0)
+// per-region k_res_update (a region in CSR form, n > 7168, ninp > 1024, SML_RES_PATH_PER_REGION)
 extern "C" int sml_res_update_balanced(sml_reservoirs *c, int *balanced) {
     SML_REQUIRE(c && balanced, "null argument");
     *balanced = bal_usable(c) ? 1 : 0;
@@ -1793,9 +1764,34 @@ extern "C" int sml_res_ell_layout(sml_reservoirs *c, int i, int *a_width, int *a
     return SML_OK;
 }
 
+// the fallback paths forced for every region (bitwise the defaults, which take them
+// only where a region's structure does not fit): SML_RES_PATH_CSR -- A and W_in from
+// their CSR copies, no ELL layout (before any region is loaded); SML_RES_PATH_PER_REGION
+// -- k_res_update, a block per (region, part), instead of the balanced update;
+// SML_RES_PATH_UNGROUPED_FINISH -- the v_p finish one thread per output
+extern "C" int sml_res_set_reference_paths(sml_reservoirs *c, int flags) {
+    SML_REQUIRE(c && (flags & ~7) == 0, "bad argument");
+    const bool csr = flags & SML_RES_PATH_CSR;
+    if (csr != c->no_ell) {
+        for (unsigned char l : c->loaded)
+            SML_REQUIRE(!l, "sml_res_set_reference_paths(SML_RES_PATH_CSR) after a region was loaded");
+        c->no_ell = csr;
+        // (the ELL buffers stay sized for the default: a region is laid out in ELL only
+        // while its cap is non-zero, at load)
+        for (int i = 0; i < c->nlocal; ++i) {
+            c->a_ell_cap[i] = !csr && c->k[i] / c->n[i] + 1 <= kEllA ? kEllA : 0;
+            c->w_ell_cap[i] = csr ? 0 : kEllW;
+        }
+        c->ell_ok = -1;
+    }
+    c->upd_bal = !(flags & SML_RES_PATH_PER_REGION);
+    c->finish_ungrouped = flags & SML_RES_PATH_UNGROUPED_FINISH;
+    return SML_OK;
+}
+
 extern "C" int sml_res_set_read_waves(sml_reservoirs *c, int waves) {
     SML_REQUIRE(c && waves >= 0, "bad argument");
-    if (!std::getenv("SML_READ_WAVES")) c->read_waves = waves;
+    c->read_waves = waves;
     return SML_OK;
 }
 
@@ -1866,11 +1862,9 @@ bool bal_usable(sml_reservoirs *c) {
     return c->ell_ok == 1 && c->maxn <= kStageX * kUpdThreads && c->maxninp <= kUpdThreads && lds <= c->max_lds;
 }
 
-int launch_update_bal(sml_reservoirs *c, const double *xo, double *xn, const double *d_feedback, hipStream_t st,
-                      bool paced) {
+int launch_update_bal(sml_reservoirs *c, const double *xo, double *xn, const double *d_feedback, hipStream_t st) {
     const int64_t total = c->row0_h[c->nlocal];
     int G = c->upd_cus > 0 ? c->upd_cus : std::max(c->ncu, 1);  // one block per CU the launch gets
-    if (paced && c->upd_blocks > 0) G = std::min(G, c->upd_blocks);
     G = (int)std::max<int64_t>(1, std::min<int64_t>(G, total));
     if (G > c->blk_cap) {  // (the buffer grows only past the largest grid seen: rare, synchronous)
         const int cap = std::max(G, std::max(c->ncu, c->upd_cus));
@@ -1910,51 +1904,38 @@ int launch_update_bal(sml_reservoirs *c, const double *xo, double *xn, const dou
         hipLaunchKernelGGL(kern, dim3(G), dim3(kUpdThreads), lds, st, c->d_rd, c->d_row0, blk_r0, c->nlocal,
                            total, ell, xo, xn, d_feedback, c->leakage, lds_x, lds_buf);
     };
-#define SML_BAL_D(WT, D)                                                                                    \
+    // two passes of A / W_in rows in flight (a third measured slower: 114-124 VGPRs)
+#define SML_BAL(WT)                                                                                         \
     do {                                                                                                    \
-        if (np == 2) ovf ? go(k_res_update_bal<WT, 2, true, D>) : go(k_res_update_bal<WT, 2, false, D>);    \
-        else if (np == 3) ovf ? go(k_res_update_bal<WT, 3, true, D>) : go(k_res_update_bal<WT, 3, false, D>); \
-        else ovf ? go(k_res_update_bal<WT, 4, true, D>) : go(k_res_update_bal<WT, 4, false, D>);             \
+        if (np == 2) ovf ? go(k_res_update_bal<WT, 2, true, 2>) : go(k_res_update_bal<WT, 2, false, 2>);    \
+        else if (np == 3) ovf ? go(k_res_update_bal<WT, 3, true, 2>) : go(k_res_update_bal<WT, 3, false, 2>); \
+        else ovf ? go(k_res_update_bal<WT, 4, true, 2>) : go(k_res_update_bal<WT, 4, false, 2>);             \
     } while (0)
-#define SML_BAL(WT)                       \
-    do {                                  \
-        if (c->upd_depth == 3 && wb4)     \
-            SML_BAL_D(WT, 3);             \
-        else                              \
-            SML_BAL_D(WT, 2);             \
-    } while (0)
-    const bool wb4 = c->wdtype == SML_F32;  // (fp64 weights: depth 2 only, for the registers)
     if (c->wdtype == SML_F32)
         SML_BAL(float);
     else
         SML_BAL(double);
 #undef SML_BAL
-#undef SML_BAL_D
     SML_HIP(hipGetLastError());
     return SML_OK;
 }
 
-int launch_update(sml_reservoirs *c, const double *xo, double *xn, const double *d_feedback, hipStream_t st,
-                  bool paced = false) {
-    if (bal_usable(c)) return launch_update_bal(c, xo, xn, d_feedback, st, paced);
+int launch_update(sml_reservoirs *c, const double *xo, double *xn, const double *d_feedback, hipStream_t st) {
+    if (bal_usable(c)) return launch_update_bal(c, xo, xn, d_feedback, st);
     // parts per region: enough blocks to fill the 512 resident 1024-thread block slots
     // (2 per CU with ~54 KB LDS each) once, each part at least one 1024-row pass.  Every
     // part stages the region's whole x, so more parts cost HBM traffic: measured on
     // 1152 regions, 1 part 119 us, 2 parts 128 us, 4 parts 165 us (profiles/r01m)
     const int max_parts = std::max(1, (c->maxn + kUpdThreads - 1) / kUpdThreads);
-    int parts = std::max(1, std::min(max_parts, (512 + c->nlocal - 1) / c->nlocal));
-    if (c->upd_parts > 0) parts = std::min(max_parts, c->upd_parts);
+    const int parts = std::max(1, std::min(max_parts, (512 + c->nlocal - 1) / c->nlocal));
     const int lds_x = (c->maxn + 1) / 2 * 2;
     const size_t lds = (size_t)(lds_x + c->maxninp) * sizeof(double);
     const bool use_lds = lds <= 64 * 1024;
     const int bpr = parts;
     const int nlog = bpr * c->nlocal;
-    // beside SPEEDY's window (sml_res_step_begin) the grid may be capped (upd_blocks):
-    // fewer blocks in flight, each taking logical blocks in rounds
-    dim3 ug(paced && c->upd_blocks > 0 ? std::min(nlog, c->upd_blocks) : nlog);
-    const bool occ2 = c->upd_occ2;
+    const dim3 ug(nlog);
 #define SML_UPD(WT, L)                                                                                            \
-    hipLaunchKernelGGL(occ2 ? (k_res_update<WT, L, 8>) : (k_res_update<WT, L, 4>), ug, dim3(kUpdThreads),        \
+    hipLaunchKernelGGL((k_res_update<WT, L, 4>), ug, dim3(kUpdThreads),                                          \
                        L ? lds : 0, st, c->d_rd, c->d_a_rp, c->d_a_col, (const WT *)c->d_a_val, c->d_w_rp,        \
                        c->d_w_col, (const WT *)c->d_w_val, ell, xo, xn, d_feedback, c->leakage, bpr, lds_x, nlog)
     const Ell ell = make_ell(c);
@@ -1974,9 +1955,7 @@ int launch_update(sml_reservoirs *c, const double *xo, double *xn, const double 
     return SML_OK;
 }
 
-int begin_mode(const sml_reservoirs *c) {
-    return c->begin_env >= 0 ? c->begin_env : c->begin_mode;
-}
+int begin_mode(const sml_reservoirs *c) { return c->begin_mode; }
 
 // the fused begin needs the wide readout (8 waves of 17 rows per region at most)
 // and the update's LDS staging (2 blocks per CU: <= 64 KB each)
@@ -2080,7 +2059,7 @@ extern "C" int sml_res_step_begin(sml_reservoirs *c, const double *d_feedback, v
         if (rec) SML_HIP(hipEventRecord(ev[1], st));
         if (int rc = launch_begin(c, xo, xn, d_feedback, st)) return rc;
     } else {
-        if (int rc = launch_update(c, xo, xn, d_feedback, st, true)) return rc;  // beside SPEEDY's window
+        if (int rc = launch_update(c, xo, xn, d_feedback, st)) return rc;  // beside SPEEDY's window
         if (rec) SML_HIP(hipEventRecord(ev[1], st));
         launch_readout<kReadML>(c, xn, nullptr, nullptr, st);
     }

@@ -235,14 +235,6 @@ __global__ __launch_bounds__(kFftThreads) void k_gridx(const double *__restrict_
     if (threadIdx.x + kFftThreads < kFftWa) was[threadIdx.x + kFftThreads] = wa[threadIdx.x + kFftThreads];
     __syncthreads();
     if (act) gridx_store(xi, h, f, j, was, cosgr, c0, c1, grid, g4, logp, ex, mmv);
-    if (ex.sig) {  // MI355X_MICROARCH.md inter-workgroup visibility, the producer form
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            __hip_atomic_fetch_add(ex.sig, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
 }
 
 // specx (spe_subfft_fftpack.f90:55-87): fvar = vorg(:, j) (the first nscaled fields
@@ -763,7 +755,6 @@ int spectral_gridx_io(sml_spectral *s, const double *varm, double *g4, double *l
     return spectral_gridx_run_model_exit(s, varm, g4, logp, nwind, IoExit{}, st);
 }
 
-int spectral_exit_blocks() { return (2 * (4 * kKX + 1) * kIL + kFftThreads - 1) / kFftThreads; }
 
 int spectral_gridx_run_model_exit(sml_spectral *s, const double *varm, double *g4, double *logp, int nwind,
                                   IoExit ex, hipStream_t st) {

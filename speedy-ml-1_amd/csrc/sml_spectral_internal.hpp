@@ -71,15 +71,10 @@ struct IoExit {
     unsigned target = 0;
     unsigned *late = nullptr;
     long long timeout = 100000000ll;  // ~1 s; on a timeout the check counts as unsafe (NaN min / max)
-    // the forecast's hand-off to another stream without a signal kernel: each block,
-    // its stores drained and released at agent scope, adds 1 (spectral_exit_blocks()
-    // adds per launch) -- the consumer polls *sig >= its count
-    uint64_t *sig = nullptr;
     // the count to wait for, from device memory instead of `target` (xa[0], written by
     // this run_model's k_io_entry): an exit replayed inside a graph keeps its arguments
     const uint64_t *xa = nullptr;
 };
-int spectral_exit_blocks();
 int spectral_gridx_run_model_exit(sml_spectral *s, const double *varm, double *g4, double *logp, int nwind,
                                   IoExit ex, hipStream_t st);
 

@@ -18,7 +18,7 @@
 // SPD (regularised Gram), so it is a Cholesky factorisation instead of dgesv's LU --
 // the same solution up to rounding x cond(G) -- written here for the batch
 // (right-looking, 128 x 128 blocks, in place on the padded column-major G):
-//   per block column k: k_chol_diag factors the diagonal block in LDS and inverts
+//   per block column k: k_chol_diag_b factors the diagonal block in LDS and inverts
 //   its triangle (one workgroup per region); k_chol_panel forms L_ik = A_ik L_kk^-T
 //   as a GEMM against that inverse; k_chol_update subtracts L_ik L_jk^T from every
 //   trailing tile (the n^3/3 flops, fp64 MFMA) -- then the two triangular solves
@@ -81,98 +81,14 @@ __device__ inline bool tile_of(int idx, int C, int *bi, int *bj, bool *strip) {
     return true;
 }
 
-// One workgroup (4 waves, 2 x 2) per (region, 128 x 128 tile); wave (wr, wc) owns a
-// 64 x 64 sub-tile = 4 x 4 MFMA 16x16 tiles.  K loop over the batch's time steps in
-// stages of 16, register-prefetched one stage ahead.
-__global__ __launch_bounds__(256) void k_train_gram(const double *__restrict__ S, const double *__restrict__ T,
-                                                    const TrainRegion *__restrict__ regs, int m, int nout, int npad,
-                                                    double *__restrict__ G, double *__restrict__ B) {
-    __shared__ double sA[kKC][kTile + kLdsPad];
-    __shared__ double sB[kKC][kTile + kLdsPad];
-    const int r = blockIdx.y;
-    const TrainRegion R = regs[r];
-    const int C = npad / kTile;
-    int bi, bj;
-    bool strip;
-    if (!tile_of(blockIdx.x, C, &bi, &bj, &strip)) return;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int wr = w >> 1, wc = w & 1, l16 = lane & 15, kk = lane >> 4;
-    const double *Sr = S + R.s_off, *Tr = T + R.t_off;
-    const int naug = R.naug;
-    // loader: thread -> (row = tid & 127, t = (tid >> 7) + 2q), q = 0..7
-    const int lrow = tid & (kTile - 1), lt0 = tid >> 7;
-    const int arow = bi * kTile + lrow;  // A rows: Gram rows (i) or outputs (o)
-    const int brow = bj * kTile + lrow;  // B rows: Gram columns (j)
-    const bool a_ok = strip ? (arow < nout) : (arow < naug);
-    const bool b_ok = brow < naug;
-    const double *pa = strip ? Tr + arow : Sr + arow;
-    const long long lda = strip ? nout : naug;
-    const double *pb = Sr + brow;
-    double ra[kKC / 2], rb[kKC / 2];
-    auto fetch = [&](int t0) {
-#pragma unroll
-        for (int q = 0; q < kKC / 2; ++q) {
-            const int t = t0 + lt0 + 2 * q;
-            ra[q] = (a_ok && t < m) ? pa[(long long)t * lda] : 0.0;
-            rb[q] = (b_ok && t < m) ? pb[(long long)t * naug] : 0.0;
-        }
-    };
-    d4 acc[4][4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = d4{0, 0, 0, 0};
-    fetch(0);
-    for (int t0 = 0; t0 < m; t0 += kKC) {
-        __syncthreads();
-#pragma unroll
-        for (int q = 0; q < kKC / 2; ++q) {
-            sA[lt0 + 2 * q][lrow] = ra[q];
-            sB[lt0 + 2 * q][lrow] = rb[q];
-        }
-        __syncthreads();
-        if (t0 + kKC < m) fetch(t0 + kKC);
-#pragma unroll
-        for (int s = 0; s < kKC / 4; ++s) {
-            double a[4], b[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) a[i] = sA[4 * s + kk][wr * 64 + i * 16 + l16];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) b[j] = sB[4 * s + kk][wc * 64 + j * 16 + l16];
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-#pragma unroll
-                for (int j = 0; j < 4; ++j) acc[i][j] = MFMA64(a[i], b[j], acc[i][j]);
-        }
-    }
-    // accumulate into G (column-major npad x npad) or B (B(j, o) at j + npad*o)
-    double *Gr = G + (size_t)r * npad * npad;
-    double *Br = B + (size_t)r * npad * nout;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int row = bi * kTile + wr * 64 + i * 16 + kk + 4 * q;
-                const int col = bj * kTile + wc * 64 + j * 16 + l16;
-                if (strip) {
-                    if (row < nout) {
-                        double *p = Br + (size_t)row * npad + col;
-                        *p = *p + acc[i][j][q];
-                    }
-                } else {
-                    double *p = Gr + (size_t)col * npad + row;
-                    *p = *p + acc[i][j][q];
-                }
-            }
-}
-
-// k_train_gram with the LDS stages double-buffered: one barrier per stage instead of
-// two (the next stage's registers go to the other buffer while this one is read),
-// and the LDS rows padded to 144 doubles, so the two 16-lane halves of a ds_read_b64
-// group (consecutive k) fall on disjoint banks (a 132-double row shifts by 8 banks:
-// 2-way conflicts).  The same products summed in the same order as k_train_gram.
+// The Gram and cross product: one workgroup (4 waves, 2 x 2) per (region, 128 x 128
+// tile); wave (wr, wc) owns a 64 x 64 sub-tile = 4 x 4 MFMA 16x16 tiles.  K loop over
+// the batch's time steps in stages of 16, register-prefetched one stage ahead into
+// double-buffered LDS stages: one barrier per stage (the next stage's registers go to
+// the other buffer while this one is read), the LDS rows padded to 144 doubles so the
+// two 16-lane halves of a ds_read_b64 group (consecutive k) fall on disjoint banks (a
+// 132-double row shifts by 8 banks: 2-way conflicts).  (The single-buffered form, two
+// barriers per stage, measured slower: DESIGN.md §3.4.)
 constexpr int kLdsLd2 = kTile + 16;
 __global__ __launch_bounds__(256, 2) void k_train_gram2(const double *__restrict__ S, const double *__restrict__ T,
                                                      const TrainRegion *__restrict__ regs, int m, int nout, int npad,
@@ -465,88 +381,18 @@ constexpr int kDiagLd = kTile + 1;            // LDS row stride (doubles)
 constexpr int kDiagH = kDiagThreads / kTile;  // entries of a row per thread stride
 constexpr size_t kDiagLds = (size_t)(kTile * kDiagLd + 2 * kTile) * sizeof(double);
 
-// Diagonal block k of every region: A_kk = L_kk L_kk^T (potrf's unblocked step,
-// column by column) and X = L_kk^-1, both in one LDS array -- L in the lower
-// triangle, X^T in the strict upper triangle, diag(L) and diag(X) apart.  Step j
-// scales L's column j and finishes X's row j, then updates L's trailing triangle
-// and X's rows below j.  Thread (i = row, h) walks row i's entries with stride 8,
-// four independent LDS reads in flight per chunk (the loop is LDS-latency bound).
-// L_kk goes back to G (lower triangle), L_kk^-1 (column-major, zeros above the
-// diagonal) to linv for the panel GEMM and the triangular solves.  info: potrf's
-// (first non-positive pivot, 1-based global index).
-__global__ __launch_bounds__(kDiagThreads) void k_chol_diag(double *__restrict__ G, double *__restrict__ linv,
-                                                            int npad, int k, int *__restrict__ info,
-                                                            const TrainRegion *__restrict__ regs) {
-    extern __shared__ double S[];  // S[i * kDiagLd + c]
-    double *ldg = S + kTile * kDiagLd, *xd = ldg + kTile;
-    const int r = blockIdx.x, C = npad / kTile;
-    if (k >= live_blocks(regs, r)) return;  // an identity block: L = L^-1 = I, already in G
-    const int tid = threadIdx.x, i = tid & (kTile - 1), h = tid >> 7;
-    double *A = G + (size_t)r * npad * npad + (size_t)k * kTile * npad + (size_t)k * kTile;
-    for (int c = h; c < kTile; c += kDiagH) S[i * kDiagLd + c] = c <= i ? A[(size_t)c * npad + i] : 0.0;
-    double *Si = S + i * kDiagLd;
-    for (int j = 0; j < kTile; ++j) {
-        __syncthreads();
-        const double d = S[j * kDiagLd + j];
-        const double inv = 1.0 / sqrt(d);
-        if (tid == 0) {
-            ldg[j] = sqrt(d);
-            xd[j] = inv;
-            if (!(d > 0.0) && info[r] == 0) info[r] = k * kTile + j + 1;
-        }
-        if (h == 0 && i > j) Si[j] *= inv;  // L(i, j)
-        if (h == 1 && i < j) Si[j] *= inv;  // X(j, c = i), stored at S[c][j]
-        __syncthreads();
-        if (i <= j) continue;
-        const double lij = Si[j];
-        for (int l0 = j + 1 + h; l0 <= i; l0 += 4 * kDiagH) {  // L(i, l) -= L(i, j) L(l, j), j < l <= i
-            double a[4], b[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int l = l0 + u * kDiagH;
-                if (l <= i) {
-                    a[u] = Si[l];
-                    b[u] = S[l * kDiagLd + j];
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-                if (l0 + u * kDiagH <= i) Si[l0 + u * kDiagH] = a[u] - lij * b[u];
-        }
-        for (int c0 = h; c0 < j; c0 += 4 * kDiagH) {  // X(i, c) -= L(i, j) X(j, c), c < j
-            double a[4], b[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int c = c0 + u * kDiagH;
-                if (c < j) {
-                    a[u] = S[c * kDiagLd + i];
-                    b[u] = S[c * kDiagLd + j];
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-                if (c0 + u * kDiagH < j) S[(c0 + u * kDiagH) * kDiagLd + i] = a[u] - lij * b[u];
-        }
-        if (h == kDiagH - 1) S[j * kDiagLd + i] -= lij * xd[j];  // X(i, j)
-    }
-    __syncthreads();
-    double *Li = linv + ((size_t)r * C + k) * kTile * kTile;
-    for (int c = h; c < kTile; c += kDiagH) {
-        if (c <= i) A[(size_t)c * npad + i] = c < i ? S[i * kDiagLd + c] : ldg[i];
-        Li[(size_t)c * kTile + i] = c < i ? S[c * kDiagLd + i] : (c == i ? xd[i] : 0.0);
-    }
-}
-
-// The diagonal factor blocked (default; SML_CHOL_DIAG=1: k_chol_diag): the same
-// outputs -- L_kk into G, L_kk^-1 into linv, potrf's info -- from the 128 x 128 block
-// as four 32-column sub-blocks.  Sub-block P: one wave factors its 32 x 32 diagonal
-// block and inverts it (k_chol_diag's column steps restricted to the sub-block, no
-// workgroup barrier: the wave's LDS operations complete in order); every wave then
+// Diagonal block k of every region, A_kk = L_kk L_kk^T and X = L_kk^-1: L_kk goes back
+// to G (lower triangle), L_kk^-1 (column-major, zeros above the diagonal) to linv for
+// the panel GEMM and the triangular solves, and potrf's info (first non-positive
+// pivot, 1-based global index) -- from the 128 x 128 block as sub-blocks of kSub
+// columns.  Sub-block P: one wave factors its kSub x kSub diagonal block and inverts
+// it (potrf's unblocked column steps restricted to the sub-block, no workgroup barrier: the wave's LDS operations complete in order); every wave then
 // forms the rows below, L_IP = A_IP X_PP^T, and the trailing update inside the block,
 // A_IJ -= L_IP L_JP^T, as 16 x 16 f64 MFMA tiles from LDS.  After the last sub-block
 // the inverse's off-diagonal blocks, X_IJ = -X_II sum_{J <= K < I} L_IK X_KJ, row of
-// blocks by row.  About 20 workgroup barriers instead of k_chol_diag's 256; the same
-// factorisation up to rounding (the update sums are blocked).
+// blocks by row.  About 20 workgroup barriers instead of the column-by-column form's
+// 256 (r05: 269 -> 122 us per launch); the same factorisation up to rounding (the
+// update sums are blocked).
 #ifndef SML_DIAG_SUB
 #define SML_DIAG_SUB 16
 #endif
@@ -601,7 +447,7 @@ __global__ __launch_bounds__(kDiagThreads) void k_chol_diag_b(double *__restrict
         const int o = P * kSub;
         __syncthreads();
         SML_DST(1 + 4 * P);
-        if (w == 0) {  // the sub-block's column steps (k_chol_diag's, on rows / columns o..o+31)
+        if (w == 0) {  // the sub-block's column steps (potrf's unblocked ones, on rows / columns o..o+kSub-1)
             const int si = lane & (kSub - 1), sh = lane / kSub;
             for (int j = 0; j < kSub; ++j) {
                 const double d = S[(o + j) * ld + o + j];
@@ -736,7 +582,7 @@ __global__ __launch_bounds__(256, 3) void k_chol_panel(double *__restrict__ G, c
 // A_ij -= sum_{k0 <= k < k0 + kw} L_ik L_jk^T for the lower-triangle tiles j <= i
 // of block columns jlo <= j < jhi: one GEMM of depth 128 kw per tile (the block
 // columns of L are contiguous in the column-major G).  KC: the GEMM's LDS stage depth
-// (SML_CHOL_KC)
+// (16; 32-deep stages spilled at two waves per SIMD)
 template <int KC>
 __global__ __launch_bounds__(256, 2) void k_chol_update(double *__restrict__ G, int npad, int k0, int kw, int jlo,
                                                      int jhi, const TrainRegion *__restrict__ regs) {
@@ -754,8 +600,8 @@ __global__ __launch_bounds__(256, 2) void k_chol_update(double *__restrict__ G, 
                                           i == j);
 }
 
-// Block column k > k0 of a panel below its diagonal, fused (default; SML_CHOL_FUSE=0:
-// k_chol_update then k_chol_panel): rows r0 .. r0 + 63 of block i take the left-looking
+// Block column k > k0 of a panel below its diagonal, fused (k_chol_update then
+// k_chol_panel as one launch): rows r0 .. r0 + 63 of block i take the left-looking
 // update by the panel's earlier block columns k0 .. k - 1 (k_chol_update's GEMM, in place),
 // then L_ik = A_ik L_kk^-T (k_chol_panel's GEMM) on the same rows, read back from L2 by the
 // workgroup that wrote them -- one HBM read of the slab instead of two, one launch fewer
@@ -938,26 +784,7 @@ __global__ __launch_bounds__(256, 2) void k_solve_update(const double *__restric
 
 struct sml_train {
     int nlocal = 0, nout = 0, npad = 0, C = 0;
-    int panel = kPanel;
-    int gram = 2;  // k_train_gram2 (double-buffered LDS); SML_GRAM_V=1: k_train_gram
-    // the triangular solves' in-panel launches in three right-hand-side groups
-    bool rhs_split = true;
-    // the blocked diagonal factor (k_chol_diag_b); SML_CHOL_DIAG=1: k_chol_diag
-    bool diag_b = true;
-    // the in-panel update fused with the panel (k_chol_upanel); SML_CHOL_FUSE=0: two launches
-    bool fuse = true;
-    // the fused path's diagonal-tile update as three 64 x 64 quadrants (k_chol_update_diag);
-    // SML_CHOL_DSPLIT=0: one 128 x 128 lower tile
-    bool diag_split = true;
-    // the solves' in-panel epilogues through an LDS transpose (gemm_rhs te; the wide
-    // launches store directly, where it measured slower); SML_SOLVE_TE=0: direct
-    bool solve_te = true;
-    // the factor's shallow launches (the fused in-panel update + panel, the diagonal tile's
-    // update, the first panels) with the same transposed epilogue (gemm_tile te);
-    // SML_CHOL_TE=0: direct
-    bool chol_te = true;
-    // the trailing update's LDS stage depth (SML_CHOL_KC: 16 or 32)
-    int update_kc = kKC;
+    int panel = kPanel;  // block columns per Cholesky panel (sml_train_set_panel)
     std::vector<int> naug;
     TrainRegion *d_regs = nullptr;
     double *d_G = nullptr, *d_B = nullptr;
@@ -996,15 +823,6 @@ extern "C" int sml_train_create(int nlocal, const int *naug, int nout, sml_train
     if (!t) return fail(SML_ERR_NOMEM, "host allocation failed");
     t->nlocal = nlocal;
     t->nout = nout;
-    if (const char *e = getenv("SML_CHOL_PANEL")) t->panel = std::max(1, atoi(e));  // tuning knob
-    if (const char *e = getenv("SML_GRAM_V")) t->gram = atoi(e) == 1 ? 1 : 2;       // A/B knob
-    if (const char *e = getenv("SML_SOLVE_SPLIT")) t->rhs_split = *e != '0';        // A/B knob
-    if (const char *e = getenv("SML_CHOL_DIAG")) t->diag_b = atoi(e) != 1;          // A/B knob
-    if (const char *e = getenv("SML_CHOL_FUSE")) t->fuse = *e != '0';               // A/B knob
-    if (const char *e = getenv("SML_CHOL_DSPLIT")) t->diag_split = *e != '0';      // A/B knob
-    if (const char *e = getenv("SML_SOLVE_TE")) t->solve_te = *e != '0';           // A/B knob
-    if (const char *e = getenv("SML_CHOL_TE")) t->chol_te = *e != '0';             // A/B knob
-    if (const char *e = getenv("SML_CHOL_KC")) t->update_kc = atoi(e) == 32 ? 32 : kKC;  // A/B knob
     t->naug.assign(naug, naug + nlocal);
     int mx = 0;
     for (int i = 0; i < nlocal; ++i) {
@@ -1036,8 +854,6 @@ extern "C" int sml_train_create(int nlocal, const int *naug, int nout, sml_train
     SML_HIP(hipMemcpy(t->d_wout_off, wo.data(), nlocal * sizeof(long long), hipMemcpyHostToDevice));
     static bool lds_set = false;
     if (!lds_set) {
-        SML_HIP(hipFuncSetAttribute((const void *)k_chol_diag, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (int)kDiagLds));
         SML_HIP(hipFuncSetAttribute((const void *)k_chol_diag_b, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     (int)kDiagBLds));
         lds_set = true;
@@ -1064,12 +880,8 @@ extern "C" int sml_train_accumulate(sml_train *t, const double *d_states, const 
         t->last_m = m;
     }
     const int tiles = t->C * (t->C + 1) / 2 + kStrip * t->C;
-    if (t->gram == 1)
-        hipLaunchKernelGGL(k_train_gram, dim3(tiles, t->nlocal), dim3(256), 0, (hipStream_t)stream, d_states,
-                           d_targets, t->d_regs, m, t->nout, t->npad, t->d_G, t->d_B);
-    else
-        hipLaunchKernelGGL(k_train_gram2, dim3(tiles, t->nlocal), dim3(256), 0, (hipStream_t)stream, d_states,
-                           d_targets, t->d_regs, m, t->nout, t->npad, t->d_G, t->d_B);
+    hipLaunchKernelGGL(k_train_gram2, dim3(tiles, t->nlocal), dim3(256), 0, (hipStream_t)stream, d_states, d_targets,
+                       t->d_regs, m, t->nout, t->npad, t->d_G, t->d_B);
     SML_HIP(hipGetLastError());
     return SML_OK;
 }
@@ -1097,24 +909,20 @@ extern "C" int sml_train_solve(sml_train *t, int ncs, double beta_res, double be
     // left-looking: block column k first takes the update from the panel's earlier
     // columns (depth 128 (k - p0)), then its diagonal factor and L_ik below it;
     // after the panel, one right-looking update of the whole trailing matrix at
-    // depth 128 x panel.
-    const int P = t->panel, cte = t->chol_te ? 1 : 0;
+    // depth 128 x panel.  Block column k > p0 of a panel: its diagonal tile's update
+    // (three quadrant workgroups), the diagonal factor, then the update and L_ik of the
+    // blocks below fused (k_chol_upanel); the panel's first column: the factor and
+    // k_chol_panel.  The shallow launches store through an LDS transpose (cte).
+    const int P = t->panel, cte = 1;
     for (int p0 = 0; p0 < C; p0 += P) {
         const int p1 = std::min(C, p0 + P);
         for (int k = p0; k < p1; ++k) {
-            const bool fused = t->fuse && k > p0;  // (then the update launch covers the diagonal tile only)
-            if (fused && t->diag_split)
+            const bool fused = k > p0;
+            if (fused)
                 hipLaunchKernelGGL(k_chol_update_diag, dim3(3, nl), dim3(256), 0, st, t->d_G, npad, p0, k, t->d_regs,
                                    cte);
-            else if (k > p0)
-                hipLaunchKernelGGL(k_chol_update<kKC>, dim3(fused ? 1 : C - k, nl), dim3(256), 0, st, t->d_G, npad, p0,
-                                   k - p0, k, k + 1, t->d_regs);
-            if (t->diag_b)
-                hipLaunchKernelGGL(k_chol_diag_b, dim3(nl), dim3(kDiagThreads), kDiagBLds, st, t->d_G, t->d_linv, npad,
-                                   k, t->d_info, t->d_regs);
-            else
-                hipLaunchKernelGGL(k_chol_diag, dim3(nl), dim3(kDiagThreads), kDiagLds, st, t->d_G, t->d_linv, npad, k,
-                                   t->d_info, t->d_regs);
+            hipLaunchKernelGGL(k_chol_diag_b, dim3(nl), dim3(kDiagThreads), kDiagBLds, st, t->d_G, t->d_linv, npad, k,
+                               t->d_info, t->d_regs);
             if (k < C - 1 && fused)
                 hipLaunchKernelGGL(k_chol_upanel, dim3(2 * (C - 1 - k), nl), dim3(256), 0, st, t->d_G, t->d_linv,
                                    npad, p0, k, t->d_regs, cte);
@@ -1123,9 +931,8 @@ extern "C" int sml_train_solve(sml_train *t, int ncs, double beta_res, double be
                                    npad, k, t->d_regs, cte);
         }
         if (p1 < C)  // the trailing update (72 % of the solve's time)
-            hipLaunchKernelGGL((t->update_kc == 32 ? k_chol_update<32> : k_chol_update<kKC>),
-                               dim3(update_tiles(C, p1, C), nl), dim3(256), 0, st, t->d_G, npad, p0, p1 - p0, p1, C,
-                               t->d_regs);
+            hipLaunchKernelGGL(k_chol_update<kKC>, dim3(update_tiles(C, p1, C), nl), dim3(256), 0, st, t->d_G, npad, p0,
+                               p1 - p0, p1, C, t->d_regs);
     }
     // potrs, blocked by panels of P block rows: inside a panel, right-looking (block
     // row k's diagonal inverse, then its update of the panel's remaining rows at
@@ -1133,19 +940,19 @@ extern "C" int sml_train_solve(sml_train *t, int ncs, double beta_res, double be
     // chain); then the rows beyond the panel take the whole panel's update at depth
     // 128 P (MFMA-bound).
     // the in-panel launches (diagonal blocks, one-block-deep updates) in three column
-    // groups of the right-hand sides (SML_SOLVE_SPLIT=0: one), the wide ones whole
-    const bool sp = t->rhs_split;
-    const dim3 g1(1, nl, sp ? 3 : 1);
-    const int te = t->solve_te ? 1 : 0;
+    // groups of the right-hand sides, their epilogues through an LDS transpose (te); the
+    // wide ones whole, stored directly
+    constexpr int kG = kRhs / 3;
+    const dim3 g1(1, nl, 3);
+    const int te = 1;
     for (int p0 = 0; p0 < C; p0 += P) {  // L Y = B
         const int p1 = std::min(C, p0 + P);
         for (int k = p0; k < p1; ++k) {
-            hipLaunchKernelGGL((sp ? k_solve_diag<false, kRhs / 3> : k_solve_diag<false, kRhs>), g1, dim3(256), 0, st,
-                               t->d_linv, t->d_B, npad, nout, k, t->d_regs, te);
+            hipLaunchKernelGGL((k_solve_diag<false, kG>), g1, dim3(256), 0, st, t->d_linv, t->d_B, npad, nout, k,
+                               t->d_regs, te);
             if (k + 1 < p1)
-                hipLaunchKernelGGL((sp ? k_solve_update<false, kRhs / 3> : k_solve_update<false, kRhs>),
-                                   dim3(p1 - 1 - k, nl, g1.z), dim3(256), 0, st, t->d_G, t->d_B, npad, nout, k, 1,
-                                   k + 1, t->d_regs, te);
+                hipLaunchKernelGGL((k_solve_update<false, kG>), dim3(p1 - 1 - k, nl, g1.z), dim3(256), 0, st, t->d_G,
+                                   t->d_B, npad, nout, k, 1, k + 1, t->d_regs, te);
         }
         if (p1 < C)
             hipLaunchKernelGGL((k_solve_update<false, kRhs>), dim3(C - p1, nl), dim3(256), 0, st, t->d_G, t->d_B, npad,
@@ -1154,12 +961,11 @@ extern "C" int sml_train_solve(sml_train *t, int ncs, double beta_res, double be
     for (int p1 = C; p1 > 0; p1 -= P) {  // L^T X = Y, panels from the bottom
         const int p0 = std::max(0, p1 - P);
         for (int k = p1 - 1; k >= p0; --k) {
-            hipLaunchKernelGGL((sp ? k_solve_diag<true, kRhs / 3> : k_solve_diag<true, kRhs>), g1, dim3(256), 0, st,
-                               t->d_linv, t->d_B, npad, nout, k, t->d_regs, te);
+            hipLaunchKernelGGL((k_solve_diag<true, kG>), g1, dim3(256), 0, st, t->d_linv, t->d_B, npad, nout, k,
+                               t->d_regs, te);
             if (k > p0)
-                hipLaunchKernelGGL((sp ? k_solve_update<true, kRhs / 3> : k_solve_update<true, kRhs>),
-                                   dim3(k - p0, nl, g1.z), dim3(256), 0, st, t->d_G, t->d_B, npad, nout, k, 1, p0,
-                                   t->d_regs, te);
+                hipLaunchKernelGGL((k_solve_update<true, kG>), dim3(k - p0, nl, g1.z), dim3(256), 0, st, t->d_G,
+                                   t->d_B, npad, nout, k, 1, p0, t->d_regs, te);
         }
         if (p0 > 0)
             hipLaunchKernelGGL((k_solve_update<true, kRhs>), dim3(p0, nl), dim3(256), 0, st, t->d_G, t->d_B, npad, nout,
@@ -1170,6 +976,13 @@ extern "C" int sml_train_solve(sml_train *t, int ncs, double beta_res, double be
                        t->npad, t->nout, t->d_wout_off, d_wout);
     SML_HIP(hipGetLastError());
     if (info) SML_HIP(hipMemcpyAsync(info, t->d_info, t->nlocal * sizeof(int), hipMemcpyDeviceToHost, st));
+    return SML_OK;
+}
+
+// block columns per Cholesky panel (default 8): the trailing update's depth is 128 x P
+extern "C" int sml_train_set_panel(sml_train *t, int panel) {
+    SML_REQUIRE(t && panel >= 1, "bad argument");
+    t->panel = panel;
     return SML_OK;
 }
 

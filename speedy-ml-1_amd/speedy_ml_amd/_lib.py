@@ -62,11 +62,13 @@ EXPORTED = (
     "sml_dyn_get_sea_ice", "sml_dyn_get_physics", "sml_dyn_get_forcing", "sml_dyn_set_surface",
     "sml_dyn_set_climatology", "sml_dyn_fordate", "sml_dyn_fordate_ex", "sml_dyn_fordate_count",
     "sml_hybrid_set_calendar", "sml_hybrid_window_date", "sml_hybrid_set_hop_timeout",
-    "sml_dyn_set_check_timeout", "sml_dyn_check_stream",
+    "sml_dyn_set_check_timeout", "sml_dyn_check_stream", "sml_dyn_set_fused", "sml_res_set_reference_paths",
+    "sml_train_set_panel",
 )
 
 SML_HOP_AUTO, SML_HOP_WAIT_VALUE, SML_HOP_EVENTS, SML_HOP_KERNEL = 0, 1, 2, 3
 SML_CHAIN_AUTO, SML_CHAIN_TWO_STREAMS, SML_CHAIN_SPEEDY = 0, 1, 2
+SML_RES_PATH_CSR, SML_RES_PATH_PER_REGION, SML_RES_PATH_UNGROUPED_FINISH = 1, 2, 4
 
 
 class SmlError(RuntimeError):
@@ -191,6 +193,9 @@ def _declare(L: ctypes.CDLL) -> None:
         "sml_dyn_set_check_cus": [vp, i, i],
         "sml_dyn_set_check_timeout": [vp, ctypes.c_int64],
         "sml_dyn_check_stream": [vp, pp],
+        "sml_dyn_set_fused": [vp, i],
+        "sml_res_set_reference_paths": [vp, i],
+        "sml_train_set_panel": [vp, i],
         "sml_res_info": [vp, ip, ip, ip, ip, vp],
         "sml_comm_unique_id": [vp],
         "sml_comm_create": [i, i, vp, pp],

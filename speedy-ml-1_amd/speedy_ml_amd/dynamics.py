@@ -59,6 +59,11 @@ class Dynamics:
 
     __del__ = close
 
+    def set_fused(self, fused: bool):
+        """The fused step (default; FMA-contracted transforms, 2 launches per step) or
+        the unfused 8/9-launch step with FFTPACK-exact transforms (sml_dyn_set_fused)."""
+        check(lib().sml_dyn_set_fused(self._h, int(bool(fused))))
+
     def impint(self, dt: float, alph: float = ALPH):
         check(lib().sml_dyn_impint(self._h, dt, alph))
         self._dtal = (dt, alph)

@@ -152,6 +152,13 @@ class Reservoirs:
         check(lib().sml_res_ell_layout(self._h, int(i), *[ctypes.byref(x) for x in v]))
         return dict(a_width=v[0].value, a_overflow=bool(v[1].value), win_q=v[2].value, win_ell=bool(v[3].value))
 
+    def set_reference_paths(self, csr: bool = False, per_region: bool = False, ungrouped_finish: bool = False):
+        """Force the fallback paths for every region (sml_res_set_reference_paths): A /
+        W_in from their CSR copies (before any region is loaded), the per-region state
+        update, the v_p finish one thread per output -- bitwise the defaults."""
+        flags = (1 if csr else 0) | (2 if per_region else 0) | (4 if ungrouped_finish else 0)
+        check(lib().sml_res_set_reference_paths(self._h, flags))
+
     def set_begin_mode(self, mode: int):
         """predict_begin's form: 0 update grid + readout grid, 1 / 2 one fused launch
         (sml_res_set_begin_mode); bit-identical results."""

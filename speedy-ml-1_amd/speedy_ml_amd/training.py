@@ -41,6 +41,10 @@ class Trainer:
 
     __del__ = close
 
+    def set_panel(self, panel: int):
+        """Block columns per Cholesky panel (sml_train_set_panel; default 8)."""
+        check(lib().sml_train_set_panel(self._h, int(panel)))
+
     def reset(self, stream=None):
         check(lib().sml_train_reset(self._h, stream_ptr(stream)))
 

@@ -289,7 +289,7 @@ def test_serialised_dispatch_takes_event_hops(cuda, tmp_path):
     got = dict(np.load(out))
     assert int(got["requested"]) == SML_HOP_AUTO and int(got["effective"]) == SML_HOP_EVENTS
 
-    auto = SML_HOP_WAIT_VALUE if os.environ.get("SML_HYBRID_HOPK") == "0" else SML_HOP_KERNEL
+    auto = SML_HOP_KERNEL
     if os.environ.get("SML_HYBRID_EVENTS", "0") not in ("", "0"):
         auto = SML_HOP_EVENTS
     runs = []

@@ -199,8 +199,6 @@ def test_fused_step_agrees_with_unfused_step_to_rounding(pg, cuda, physics):
     a*b + c within an expression into one FMA (sml_dynamics.hip, -ffp-contract=on),
     so the two agree to rounding (FUSED_TOL per field and level after a run of steps
     and two windows: state, radiation state, tendencies, geopotential)."""
-    import os
-
     import torch
 
     from speedy_ml_amd.dynamics import Dynamics
@@ -209,11 +207,8 @@ def test_fused_step_agrees_with_unfused_step_to_rounding(pg, cuda, physics):
     st, forcing = dyn_state(9)
     out = []
     for fused in ("0", "1"):
-        os.environ["SML_DYN_FUSED"] = fused
-        try:
-            d = Dynamics()
-        finally:
-            os.environ.pop("SML_DYN_FUSED", None)
+        d = Dynamics()
+        d.set_fused(fused == "1")
         d.set_forcing(**forcing)
         d.set_state(st)
         if physics:
@@ -260,8 +255,6 @@ def test_fused_window_chain_drift_against_fftpack_exact_chain(pg, cuda):
     error growth; the per-window maximum relative difference (per field, over levels)
     is printed and stays below CHAIN_DRIFT_TOL.  The measured growth is recorded in
     DESIGN.md (SPEEDY window numerics)."""
-    import os
-
     import torch
 
     from speedy_ml_amd.dynamics import Dynamics
@@ -270,11 +263,8 @@ def test_fused_window_chain_drift_against_fftpack_exact_chain(pg, cuda):
     st, forcing = dyn_state(9)
     chains = []
     for fused in ("0", "1"):
-        os.environ["SML_DYN_FUSED"] = fused
-        try:
-            d = Dynamics()
-        finally:
-            os.environ.pop("SML_DYN_FUSED", None)
+        d = Dynamics()
+        d.set_fused(fused == "1")
         d.set_forcing(**forcing)
         d.set_state(st)
         d.set_physics(_window_bc(pg, d))
@@ -335,84 +325,3 @@ def test_window_graph_is_bitwise_the_launched_window(pg, cuda):
         np.testing.assert_array_equal(ra[k], rb[k])
 
 
-def test_write_through_handoffs_are_bitwise_the_default(pg, cuda):
-    """SML_DYN_WT=1 stores the fused step's hand-offs (vfm, the next step's varm and
-    the m-major state) write-through (sml_dynamics.hip store2: cache policy sc1, 16-B
-    stores, gridy's Re/Im pairs exchanged between neighbouring lanes): the same values
-    in the same places, so two chained windows with physics are bitwise the default's."""
-    import os
-
-    import torch
-
-    from speedy_ml_amd.dynamics import Dynamics
-    from speedy_ml_amd.synthetic import dyn_state
-
-    st, forcing = dyn_state(5)
-    out = []
-    for wt in ("0", "1"):
-        os.environ["SML_DYN_WT"] = wt
-        try:
-            d = Dynamics()
-        finally:
-            os.environ.pop("SML_DYN_WT", None)
-        d.set_forcing(**forcing)
-        d.set_state(st)
-        d.set_physics(_window_bc(pg, d))
-        d.set_rad_state(None)
-        d.set_clock(1, True)
-        d.window(24)
-        d.window(24)
-        torch.cuda.synchronize()
-        out.append((d.get_state(), d.get_rad_state(), d.get_phi()))
-        d.close()
-    (a, ra, pa), (b, rb, pb) = out
-    for f in oracle.DYN_FIELDS:
-        np.testing.assert_array_equal(a[f], b[f])
-    for k in ra:
-        np.testing.assert_array_equal(ra[k], rb[k])
-    np.testing.assert_array_equal(pa, pb)
-
-
-@pytest.mark.parametrize("knob", [("SML_DYN_QUAD", "0"), ("SML_DYN_QUAD", "1")])
-def test_row_kernel_variants_are_bitwise_the_default(pg, cuda, knob):
-    """The row kernel's schedules against the default (SML_DYN_QUAD=2, k_st_gridspec_p:
-    the grid-point dynamics, the moist side and the longwave side on waves of their own,
-    the longwave / shortwave on two lanes per column, sml_physics_pair.hpp), two chained windows
-    with physics (shortwave and longwave-only steps, the radiation state carried):
-    SML_DYN_QUAD=0 -- k_st_gridspec, phypar one lane per column;
-    SML_DYN_QUAD=1 -- k_st_gridspec_q, phypar on four lanes per column (per-level work
-    on the level's lane, the longwave bands one per lane, sml_physics_quad.hpp).
-    Every expression and every sum's order is the same, so state, radiation state and
-    geopotential are bitwise equal."""
-    import os
-
-    import torch
-
-    from speedy_ml_amd.dynamics import Dynamics
-    from speedy_ml_amd.synthetic import dyn_state
-
-    st, forcing = dyn_state(7)
-    out = []
-    for val in (None, knob[1]):
-        if val is not None:
-            os.environ[knob[0]] = val
-        try:
-            d = Dynamics()
-        finally:
-            os.environ.pop(knob[0], None)
-        d.set_forcing(**forcing)
-        d.set_state(st)
-        d.set_physics(_window_bc(pg, d))
-        d.set_rad_state(None)
-        d.set_clock(1, True)
-        d.window(24)
-        d.window(24)
-        torch.cuda.synchronize()
-        out.append((d.get_state(), d.get_rad_state(), d.get_phi()))
-        d.close()
-    (a, ra, pa), (b, rb, pb) = out
-    for f in oracle.DYN_FIELDS:
-        np.testing.assert_array_equal(a[f], b[f], err_msg=f)
-    for k in ra:
-        np.testing.assert_array_equal(ra[k], rb[k], err_msg=k)
-    np.testing.assert_array_equal(pa, pb)

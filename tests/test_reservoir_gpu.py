@@ -266,7 +266,7 @@ def test_finish_grid_equals_tile_then_finish(cuda, weight_dtype):
     column groups on different threads, added in group order) vs begin ->
     tile_local_model -> finish (one thread per output, the same groups in turn): outvecs
     and the tiled local model bitwise, with and without the local-model output, and
-    with the finish one thread per output (SML_FIN_UNGROUPED)."""
+    with the finish one thread per output (SML_RES_PATH_UNGROUPED_FINISH)."""
     import torch
 
     from speedy_ml_amd.reservoir import Reservoirs
@@ -277,13 +277,10 @@ def test_finish_grid_equals_tile_then_finish(cuda, weight_dtype):
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(cuda)  # noqa: E731
     outs = {}
     for mode in ("fused", "fused_nolm", "two", "fused_ungrouped"):
+        res = Reservoirs([w.region for w in ws], [w.sst for w in ws], [w.n for w in ws], [w.k for w in ws],
+                         weight_dtype=weight_dtype)
         if mode == "fused_ungrouped":  # the finish one thread per output (vp_sum), not in column groups
-            os.environ["SML_FIN_UNGROUPED"] = "1"
-        try:
-            res = Reservoirs([w.region for w in ws], [w.sst for w in ws], [w.n for w in ws], [w.k for w in ws],
-                             weight_dtype=weight_dtype)
-        finally:
-            os.environ.pop("SML_FIN_UNGROUPED", None)
+            res.set_reference_paths(ungrouped_finish=True)
         for i, w in enumerate(ws):
             if weight_dtype == "f64":
                 res.load_region(i, w.rows, w.cols, w.vals.astype(np.float64), w.win.astype(np.float64),
@@ -511,13 +508,11 @@ def test_finish_assemble_is_bitwise_finish_then_assemble(cuda):
 def test_balanced_update_is_bitwise_the_per_region_update(cuda, cus, wdt):
     """k_res_update_bal (a persistent grid, one block per CU, each block an equal share
     of all the rank's rows, two passes of A rows in flight, the next region's x staged
-    into a second LDS buffer) against k_res_update (a block per region; SML_UPD_BAL=0
-    at create): the states, x_aug-fed outvecs and the begin / finish split bitwise over
+    into a second LDS buffer) against k_res_update (a block per region;
+    SML_RES_PATH_PER_REGION): the states, x_aug-fed outvecs and the begin / finish split bitwise over
     3 steps, for grids of every CU (0), the hybrid loop's reservoir CUs (192), an odd
     grid (7: shares straddle many regions) and one block (every region in turn); with
     fp32 and fp64 weights (the Pair<double> 16-B loads)."""
-    import os
-
     import torch
 
     from speedy_ml_amd.reservoir import Reservoirs
@@ -529,12 +524,8 @@ def test_balanced_update_is_bitwise_the_per_region_update(cuda, cus, wdt):
     lm = np.stack([local_model_vector(r) for r in regions])
     outs, states = {}, {}
     for bal in (False, True):
-        if not bal:
-            os.environ["SML_UPD_BAL"] = "0"
-        try:
-            res = Reservoirs(regions, mask[regions], [w.n for w in ws], [w.k for w in ws], weight_dtype=wdt)
-        finally:
-            os.environ.pop("SML_UPD_BAL", None)
+        res = Reservoirs(regions, mask[regions], [w.n for w in ws], [w.k for w in ws], weight_dtype=wdt)
+        res.set_reference_paths(per_region=not bal)
         for i, w in enumerate(ws):
             res.load_region_weights(i, w)
             res.set_state(i, initial_state(regions[i], w.n))
@@ -565,14 +556,12 @@ def test_ell_layouts_are_bitwise_the_csr_update(cuda, wdt):
     """A's ELL main width chosen per region (pair-major slots, an overflow list for the
     rows one longer) and W_in's implicit block-diagonal column: every
     layout the builder picks gives the states and outvecs of the CSR copies
-    (SML_NO_ELL=1) bit for bit, in the balanced and the per-region update, over 3
+    (SML_RES_PATH_CSR) bit for bit, in the balanced and the per-region update, over 3
     steps -- and the oracle's within its tolerance.  Regions: every full-size shape
     class (n 6048 with 4.8 % of rows one longer -> overflow; 5880 / 5760 -> 6 slots;
     6160 -> overflow), a region of 2- and 3-entry rows (2 slots + overflow), and a W_in
     whose columns are permuted (not block-diagonal: its column is read).  Both weight
     precisions (fp64: the Pair<double> loads, the overflow entries, the depth-2 pipeline)."""
-    import os
-
     import torch
 
     from speedy_ml_amd.reservoir import Reservoirs
@@ -589,13 +578,8 @@ def test_ell_layouts_are_bitwise_the_csr_update(cuda, wdt):
     lm = np.stack([local_model_vector(r) for r in regions])
     outs, states, layouts = {}, {}, {}
     for form in ("csr", "per_region", "balanced"):
-        env = {"csr": {"SML_NO_ELL": "1", "SML_UPD_BAL": "0"}, "per_region": {"SML_UPD_BAL": "0"}, "balanced": {}}[form]
-        os.environ.update(env)
-        try:
-            res = Reservoirs(regions, mask[regions], [w.n for w in ws], [w.k for w in ws], weight_dtype=wdt)
-        finally:
-            for k in env:
-                os.environ.pop(k, None)
+        res = Reservoirs(regions, mask[regions], [w.n for w in ws], [w.k for w in ws], weight_dtype=wdt)
+        res.set_reference_paths(csr=form == "csr", per_region=form != "balanced")
         for i, w in enumerate(ws):
             res.load_region_weights(i, w)
             res.set_state(i, initial_state(regions[i], w.n))

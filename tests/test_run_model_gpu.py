@@ -125,12 +125,10 @@ def test_safety_thresholds_match_iogrid(cuda, dyn):
 def test_fused_and_unfused_run_model_agree(cuda):
     """sml_dyn_run_model's fused form (k_io_entry + the prepared window graph with
     iogrid(31)'s prep / gridy in its last kernel) against the unfused chain
-    (SML_DYN_FUSED=0: from_grid, the 8/9-launch steps, k_io_prep + gridy + gridx):
-    the unfused steps' Fourier transforms are FFTPACK's separate multiplies and
+    (sml_dyn_set_fused(0): from_grid, the 8/9-launch steps, k_io_prep + gridy +
+    gridx): the unfused steps' Fourier transforms are FFTPACK's separate multiplies and
     adds, the fused ones contract a*b + c, so the forecasts agree to rounding
     (UNFUSED_TOL x max |field| per variable and level after 6 leapfrog steps)."""
-    import os
-
     import torch
 
     from speedy_ml_amd.dynamics import Dynamics
@@ -140,12 +138,9 @@ def test_fused_and_unfused_run_model_agree(cuda):
     g4, g2 = _grids(seed=17)
     dg4, dg2 = _t(g4, cuda), _t(g2, cuda)
     outs = []
-    for fused in ("1", "0"):
-        os.environ["SML_DYN_FUSED"] = fused
-        try:
-            d = Dynamics()
-        finally:
-            os.environ.pop("SML_DYN_FUSED", None)
+    for fused in (True, False):
+        d = Dynamics()
+        d.set_fused(fused)
         st0, forcing = dyn_state()
         d.set_forcing(**forcing)
         d.set_state(st0)

@@ -172,46 +172,24 @@ def test_solve_reports_the_first_non_positive_pivot(cuda):
     tr.close()
 
 
-@pytest.mark.parametrize("knobs, bitwise", [({"SML_CHOL_FUSE": "0"}, True), ({"SML_CHOL_DSPLIT": "0"}, True),
-                                            ({"SML_SOLVE_SPLIT": "0"}, True), ({"SML_SOLVE_TE": "0"}, True), ({"SML_CHOL_TE": "0"}, True),
-                                            ({"SML_CHOL_DIAG": "1"}, False)])
-def test_cholesky_schedules_against_the_default(cuda, knobs, bitwise):
-    """The factor's and solves' launch schedules reorder no arithmetic, so W_out is
-    bitwise the default's: SML_CHOL_FUSE=0 -- the in-panel update and the panel as two
-    launches (default: k_chol_upanel); SML_CHOL_DSPLIT=0 -- the diagonal tile's update
-    as one lower 128 x 128 tile (default: three quadrant workgroups, k_chol_update_diag);
-    SML_SOLVE_SPLIT=0 -- the solves' in-panel launches on all right-hand sides at once;
-    SML_SOLVE_TE=0 -- their epilogues stored directly (default: through an LDS transpose);
-    SML_CHOL_TE=0 -- the same for the factor's shallow launches.
-    SML_CHOL_DIAG=1 -- k_chol_diag, column by column -- sums the diagonal block's updates
-    in another order than the blocked default (k_chol_diag_b's 16 x 16 MFMA tiles): the
-    two agree to rounding, within W_TOL.  Panels of three block columns over npad = 896,
-    so in-panel, fused and trailing updates all run."""
-    import os
-
+def test_cholesky_panel_widths_agree(cuda):
+    """The factor with panels of three block columns (sml_train_set_panel) against the
+    default eight, over npad = 896: the narrow panels run every kind of launch --
+    left-looking in-panel steps (the diagonal tile's quadrant update, the fused update +
+    L_ik), the panel's first column, and right-looking trailing updates between panels
+    -- whose sums group differently, so W_out agrees within W_TOL."""
     from speedy_ml_amd.training import Trainer
 
     naugs, nout, m = [777, 401, 640], 136, 1000
     S, T = _data(naugs, nout, m, seed=13)
     ws = []
-    for extra in ({}, knobs):
-        env = dict(extra, SML_CHOL_PANEL="3")
-        old = {k: os.environ.get(k) for k in env}
-        os.environ.update(env)
-        try:
-            tr = Trainer(naugs, nout)
-        finally:
-            for k, v in old.items():
-                if v is None:
-                    os.environ.pop(k, None)
-                else:
-                    os.environ[k] = v
+    for panel in (None, 3):
+        tr = Trainer(naugs, nout)
+        if panel is not None:
+            tr.set_panel(panel)
         _accumulate(tr, S, T, 2, cuda)
         w, info = tr.solve(132, 0.3, 1.0, True, 0.5)
         assert (info == 0).all()
         ws.append(w.cpu().numpy().copy())
         tr.close()
-    if bitwise:
-        np.testing.assert_array_equal(ws[0], ws[1])
-    else:
-        assert np.abs(ws[1] - ws[0]).max() <= W_TOL * np.abs(ws[0]).max()
+    assert np.abs(ws[1] - ws[0]).max() <= W_TOL * np.abs(ws[0]).max()

@@ -12,7 +12,6 @@ import torch
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "speedy-ml-1_amd"))
-os.environ["SML_DYN_FUSED"] = "1"
 os.environ["SML_DYN_STAMPS"] = "1"
 from speedy_ml_amd._lib import check, lib  # noqa: E402
 from speedy_ml_amd.dynamics import Dynamics  # noqa: E402
