@@ -40,6 +40,9 @@
 #include "sml_physics.hpp"
 #include "sml_physics_pair.hpp"
 #include "sml_spectral_internal.hpp"
+#include "sml_timeline.hpp"
+
+SML_TL_DEFINE(dynamics)
 
 using namespace sml;
 
@@ -1287,6 +1290,7 @@ __global__ __launch_bounds__(kGpThreads) void k_st_gridspec_p(
     const double *__restrict__ varm, double *__restrict__ vfm, const double *__restrict__ wa,
     const double *__restrict__ cosgr, const DynTables *__restrict__ T, const double *__restrict__ bc,
     double *__restrict__ rad, const PhysTables *__restrict__ PT, int lradsw, long long *dbg) {
+    SML_TL_SCOPE(sml::tl::kRow);
     __shared__ double A[kFftN * kRowLd], B[kFftN * kRowLd];
     const double *was = kFftWa96;
     (void)wa;
@@ -1489,6 +1493,7 @@ __global__ __launch_bounds__(kSpecBlk) void k_st_spec(
     int j4, double dt, double alph, double rob, double wil, const double *__restrict__ pinv,
     double *__restrict__ varm_next, int next_j2, int n1, int nin, const double *__restrict__ tabm,
     double *__restrict__ state_out, double *__restrict__ io_varm, long long *dbg) {
+    SML_TL_SCOPE(sml::tl::kSpec);
     __shared__ double V[kVFm];            // this m's tables (TabM)
     __shared__ double S[kNInvMax * kCW];  // specy output [f][2 n + p]; then the next step's inputs
     __shared__ double sh[3][kKX][kCW];
@@ -1753,6 +1758,7 @@ __global__ __launch_bounds__(kSpecThreads) void k_io_entry(const double *__restr
                                                            const double *__restrict__ pinv, double *__restrict__ varm,
                                                            int n1, int nin, uint64_t *__restrict__ xa, uint64_t xa0,
                                                            uint64_t xa1) {
+    SML_TL_SCOPE(sml::tl::kIoEntry);
     // a graph-captured exit's per-launch values (sml_dyn_run_model): ordered before the
     // window graph by this kernel's end
     if (xa && blockIdx.x == 0 && threadIdx.x == 0) {
@@ -1915,14 +1921,17 @@ __device__ inline double nmax(double a, double b) { return (a != a || b != b) ? 
 // vector store of the hop's sequence number, xa[1] (the exit's stores were released by
 // its kernel's end; as sml_hybrid's k_hop_signal)
 __global__ void k_flag_store_value(uint64_t *flag, uint64_t v) {
+    SML_TL_SCOPE(sml::tl::kExitStore);
     if (threadIdx.x == 0) __hip_atomic_store(flag, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __global__ void k_flag_store(uint64_t *flag, const uint64_t *xa) {
+    SML_TL_SCOPE(sml::tl::kExitStore);
     if (threadIdx.x == 0) __hip_atomic_store(flag, xa[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __global__ __launch_bounds__(1024) void k_io_minmax(const double *__restrict__ G, double *__restrict__ mm,
                                                      unsigned *__restrict__ cnt) {
+    SML_TL_SCOPE(sml::tl::kCheckMinmax);
     __shared__ double smin[16], smax[16];
     const int v = blockIdx.x;
     const double *f = G + (size_t)v * kKX * kGF;
@@ -2589,6 +2598,7 @@ __global__ __launch_bounds__(256) void k_fordate(FordateArgs a, const double *__
                                                  double *__restrict__ sice_am, double *__restrict__ tice_am,
                                                  double *__restrict__ corh) {
 #pragma clang fp contract(off)  // the reference's separate multiplies and adds
+    SML_TL_SCOPE(sml::tl::kFordate);
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= kNGP) return;
     const int j = p / kIX;

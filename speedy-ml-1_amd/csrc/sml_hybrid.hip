@@ -34,6 +34,9 @@
 #include <vector>
 
 #include "sml_internal.hpp"
+#include "sml_timeline.hpp"
+
+SML_TL_DEFINE(hybrid)
 
 using namespace sml;
 
@@ -415,6 +418,7 @@ namespace {
 // agent loads and s_sleep from one lane; it never spins forever: after ~4 s it marks
 // the late word (sml_hybrid_sync reports it) and lets the stream go on.
 __global__ void k_hop_signal(uint64_t *flag, uint64_t v) {
+    SML_TL_SCOPE(sml::tl::kHopSignal);
     if (threadIdx.x == 0) __hip_atomic_store(flag, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
@@ -1335,6 +1339,34 @@ extern "C" int sml_hybrid_sync(sml_hybrid *h) {
     SML_HIP(hipStreamSynchronize(h->side));
     if (int rc = hop_late_check(h, "sml_hybrid_sync")) return rc;
     return sml::dyn_check_late(h->dyn);
+}
+
+// ------------------------------------------------------------- diagnostics
+// The step-accounting timeline (sml_timeline.hpp; profiling build only, -DSML_TL): a
+// device buffer of per-launch start / end times of the step's kernels, attached to
+// every translation unit.  *d_buf = the buffer (sml::tl::Buf), *kinds / *ring its
+// shape; SML_ERR_STATE in a build without the timeline.  Not declared in the public
+// header (tools/step_accounting.py, bench.py --timeline).
+extern "C" int sml_dbg_timeline(void **d_buf, int *kinds, int *ring) {
+    SML_REQUIRE(d_buf && kinds && ring, "null argument");
+    static sml::tl::Buf *buf = nullptr;
+    if (!buf) {
+        sml::tl::Buf *b = nullptr;
+        SML_HIP(hipMalloc(&b, sizeof(sml::tl::Buf)));
+        SML_HIP(hipMemset(b, 0, sizeof(sml::tl::Buf)));
+        SML_HIP(hipMemset(b->t0, 0xff, sizeof b->t0));
+        if (sml::tl_attach_dynamics(b) || sml::tl_attach_spectral(b) || sml::tl_attach_reservoir(b) ||
+            sml::tl_attach_hybrid(b)) {
+            (void)hipFree(b);
+            return fail(SML_ERR_STATE, "this build has no step timeline (compile with -DSML_TL)");
+        }
+        SML_HIP(hipDeviceSynchronize());
+        buf = b;
+    }
+    *d_buf = buf;
+    *kinds = sml::tl::kKinds;
+    *ring = sml::tl::kRing;
+    return SML_OK;
 }
 
 // ------------------------------------------------------------- device memory

@@ -32,6 +32,9 @@
 #include <vector>
 
 #include "sml_internal.hpp"
+#include "sml_timeline.hpp"
+
+SML_TL_DEFINE(reservoir)
 
 #ifndef SML_READ_NT
 #define SML_READ_NT 1
@@ -445,6 +448,7 @@ __global__ __launch_bounds__(kUpdThreads, kMinW) void k_res_update(
     const WT *__restrict__ a_val, const int32_t *__restrict__ w_rp, const uint16_t *__restrict__ w_col,
     const WT *__restrict__ w_val, Ell ell, const double *__restrict__ x_old, double *__restrict__ x_new,
     const double *__restrict__ feedback, double leak, int parts, int lds_x, int nlog) {
+    SML_TL_SCOPE(sml::tl::kUpdate);
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const int off = xcd_remap(blockIdx.x, gridDim.x);
     for (int base = 0; base < nlog; base += gridDim.x) {
@@ -489,6 +493,7 @@ __global__ __launch_bounds__(kUpdThreads, 4) void k_res_update_bal(
     const RegionDev *__restrict__ R, const int32_t *__restrict__ row0, const int32_t *__restrict__ blk_r0, int nlocal,
     int64_t total, Ell ell, const double *__restrict__ x_old, double *__restrict__ x_new,
     const double *__restrict__ feedback, double leak, int lds_x, int lds_buf) {
+    SML_TL_SCOPE(sml::tl::kUpdate);
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const int G = gridDim.x;
     const int b = xcd_remap(blockIdx.x, G);
@@ -746,6 +751,7 @@ __global__ __launch_bounds__(512) void k_res_readout(const RegionDev *__restrict
                                                      const int8_t *__restrict__ outl, double *__restrict__ part,
                                                      double *__restrict__ outvec, int nout, int ov_ld, int nout_pad,
                                                      int ncs, int groups, int nitems, int ipw) {
+    SML_TL_SCOPE(sml::tl::kReadout);
     // wave gw takes the items gw, gw + W, gw + 2W, .. (W waves; one item each unless
     // the launch is paced): the waves in flight together work on consecutive items.
     // NR = kRowsWide (17 rows a wave, 8 waves a region of 136 outputs): x_aug is read
@@ -955,6 +961,7 @@ __global__ __launch_bounds__(256) void k_res_finish_grid(
         }
         __syncthreads();
     }
+    SML_TL_SCOPE(sml::tl::kFinish);  // (after the wait: when the forecast arrived)
     if (gj) {
         // a forecast that never arrived reads as NaN: the outvecs, grids and the next
         // window's safety check then refuse it instead of predicting from stale values
@@ -1020,6 +1027,7 @@ __global__ void k_tile_feedback(const int32_t *__restrict__ src, const uint8_t *
                                 const double *__restrict__ g4, const double *__restrict__ g2,
                                 const double *__restrict__ pr, const double *__restrict__ tisr,
                                 double *__restrict__ feedback, int total) {
+    SML_TL_SCOPE(sml::tl::kTileFeedback);
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= total) return;
     const int s = src[e];

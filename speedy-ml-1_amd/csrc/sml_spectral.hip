@@ -28,6 +28,9 @@
 #include "sml_fft.hpp"
 #include "sml_dynamics_tables.hpp"  // (+ sml_spectral_tables.hpp): kx for the iogrid exit layout
 #include "sml_spectral_internal.hpp"  // IoExit, io_state_safe
+#include "sml_timeline.hpp"
+
+SML_TL_DEFINE(spectral)
 
 using namespace sml;
 
@@ -182,6 +185,7 @@ __global__ __launch_bounds__(kFftThreads) void k_gridx(const double *__restrict_
                                                        const double *__restrict__ wa, const double *__restrict__ cosgr,
                                                        int nf, int c0, int c1, double *__restrict__ g4,
                                                        double *__restrict__ logp, IoExit ex) {
+    SML_TL_SCOPE(ex.mm ? sml::tl::kExitGridx : -1);
     __shared__ double was[kFftWa];  // twiddles: LDS broadcast reads inside the FFT
     // transform (f, j) on the thread pair 2 t, 2 t + 1: thread h does half h of
     // FFTPACK's rfftb (sml_fft.hpp rfftb96_half), the grid points 2 q + h.  The
@@ -275,6 +279,7 @@ __global__ __launch_bounds__(kFftThreads) void k_specx(const double *__restrict_
         }
         __syncthreads();
     }
+    SML_TL_SCOPE(g4 ? sml::tl::kEntrySpecx : -1);  // (after the wait: when the grid arrived)
     const bool stale = wait.flag && gave_up;  // the grid never arrived: transform NaN, not stale values
     // transform (f, j) on the thread pair 2 t, 2 t + 1: thread h transforms the samples
     // 2 i + h (rfftf48), the pair meets in LDS for rfftf's last pass (rfftf96_combine).
