@@ -1343,29 +1343,31 @@ extern "C" int sml_hybrid_sync(sml_hybrid *h) {
 
 // ------------------------------------------------------------- diagnostics
 // The step-accounting timeline (sml_timeline.hpp; profiling build only, -DSML_TL): a
-// device buffer of per-launch start / end times of the step's kernels, attached to
-// every translation unit.  *d_buf = the buffer (sml::tl::Buf), *kinds / *ring its
-// shape; SML_ERR_STATE in a build without the timeline.  Not declared in the public
-// header (tools/step_accounting.py, bench.py --timeline).
-extern "C" int sml_dbg_timeline(void **d_buf, int *kinds, int *ring) {
-    SML_REQUIRE(d_buf && kinds && ring, "null argument");
+// device buffer of per-(launch, block) start / end times of the step's kernels,
+// attached to every translation unit; reset != 0 zeroes it (after the device is idle).
+// *d_buf = the buffer (sml::tl::Buf), *bytes its size; SML_ERR_STATE in a build
+// without the timeline.  Not in the public header (tools/probe_step_accounting.py).
+extern "C" int sml_dbg_timeline(void **d_buf, int64_t *bytes, int reset) {
+    SML_REQUIRE(d_buf && bytes, "null argument");
     static sml::tl::Buf *buf = nullptr;
     if (!buf) {
         sml::tl::Buf *b = nullptr;
         SML_HIP(hipMalloc(&b, sizeof(sml::tl::Buf)));
-        SML_HIP(hipMemset(b, 0, sizeof(sml::tl::Buf)));
-        SML_HIP(hipMemset(b->t0, 0xff, sizeof b->t0));
         if (sml::tl_attach_dynamics(b) || sml::tl_attach_spectral(b) || sml::tl_attach_reservoir(b) ||
             sml::tl_attach_hybrid(b)) {
             (void)hipFree(b);
             return fail(SML_ERR_STATE, "this build has no step timeline (compile with -DSML_TL)");
         }
-        SML_HIP(hipDeviceSynchronize());
         buf = b;
+        reset = 1;
+    }
+    if (reset) {
+        SML_HIP(hipDeviceSynchronize());
+        SML_HIP(hipMemset(buf, 0, sizeof(sml::tl::Buf)));
+        SML_HIP(hipDeviceSynchronize());
     }
     *d_buf = buf;
-    *kinds = sml::tl::kKinds;
-    *ring = sml::tl::kRing;
+    *bytes = (int64_t)sizeof(sml::tl::Buf);
     return SML_OK;
 }
 

@@ -1008,6 +1008,7 @@ __global__ __launch_bounds__(256) void k_res_finish_grid(
 // assemble: all regions' outvecs -> global grids, with the root's clips
 __global__ void k_assemble(const int32_t *__restrict__ dst, const double *__restrict__ ov, double *__restrict__ g4,
                            double *__restrict__ g2, double *__restrict__ pr, int total, int nout, int ov_ld) {
+    SML_TL_SCOPE(sml::tl::kAssemble);
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= total) return;
     const int d = dst[e];
