@@ -170,18 +170,32 @@ struct sml_dynamics {
         hipGraphExec_t exec = nullptr;
         double key[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         DynTables *tab[3] = {nullptr, nullptr, nullptr};
-        // run_model's exit captured behind the window (exit_graph): its arguments (the
-        // per-launch values come from d_xa, written by each run_model's k_io_entry)
+        // run_model's exit captured behind the window, and with it the entry (iogrid(30)'s
+        // specx + k_io_entry) in front of it: their arguments (the per-launch values come
+        // from d_xa, written before each launch)
         bool has_exit = false;
-        const void *exit_key[9] = {};
+        const void *exit_key[16] = {};
     } wreplay[4];  // [prepared entry (sml_dyn_run_model)][entry lradsw]
     // the next run_model's exit is followed by a store of exit_store_value to
     // *exit_store (sml::dyn_run_model_exit_store: the hybrid loop's forecast hop)
     uint64_t *exit_store = nullptr;
     uint64_t exit_store_value = 0;
-    // a graph-captured exit's per-launch values: [0] the check count it waits for, [1]
-    // the hop value its store writes -- stored by the launch's k_io_entry
+    // a graph-captured run_model's per-launch values: [0] the check count the exit waits
+    // for, [1] the hop value its store writes, [2] the hop value the entry specx waits for,
+    // [3] the window's number, which its first row kernel hands the safety check
+    // (k_set_xa right before the graph; k_io_entry when only the exit is captured)
     uint64_t *d_xa = nullptr;
+    // the entry inside the window graph (run_model, no capture of the caller's, not under
+    // serialised dispatch): the safety check then waits on its own stream for *d_go >=
+    // the window's number, which the window's first row kernel stores as it starts
+    // (k_io_entry's outputs are released by then) -- no event fork after k_io_entry
+    bool entry_graph = true;
+    bool serialized = false;  // AMD_SERIALIZE_KERNEL / rocprofv3's counter collection at create
+    uint64_t *d_go = nullptr;
+    uint64_t go_count = 0;
+    // the next fused step's row kernel hands *go_src to *go_dst at its start (one launch)
+    const uint64_t *go_src_next = nullptr;
+    uint64_t *go_dst_next = nullptr;
     // while a run_model window is captured: the Fourier buffer its last k_st_spec fills
     // with iogrid(31)'s gridy (spectral layout), else null
     double *io_exit = nullptr;
@@ -1289,8 +1303,14 @@ constexpr int kGpThreads = 512;
 __global__ __launch_bounds__(kGpThreads) void k_st_gridspec_p(
     const double *__restrict__ varm, double *__restrict__ vfm, const double *__restrict__ wa,
     const double *__restrict__ cosgr, const DynTables *__restrict__ T, const double *__restrict__ bc,
-    double *__restrict__ rad, const PhysTables *__restrict__ PT, int lradsw, long long *dbg) {
+    double *__restrict__ rad, const PhysTables *__restrict__ PT, int lradsw, const uint64_t *__restrict__ go_src,
+    uint64_t *__restrict__ go_dst, long long *dbg) {
     SML_TL_SCOPE(sml::tl::kRow);
+    // the window's first row kernel in a graph that holds the entry: the entry's outputs
+    // (the safety check's inputs) were released by k_io_entry's end, so the check may go
+    // (a relaxed agent-scope vector store, as k_hop_signal)
+    if (go_dst && blockIdx.x == 0 && threadIdx.x == 0)
+        __hip_atomic_store(go_dst, *go_src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __shared__ double A[kFftN * kRowLd], B[kFftN * kRowLd];
     const double *was = kFftWa96;
     (void)wa;
@@ -1924,13 +1944,47 @@ __global__ void k_flag_store_value(uint64_t *flag, uint64_t v) {
     SML_TL_SCOPE(sml::tl::kExitStore);
     if (threadIdx.x == 0) __hip_atomic_store(flag, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// a graph-captured run_model's per-launch values (WindowReplay, sml_dynamics::d_xa),
+// launched right before the graph on its stream: behind the previous window, off the
+// chain (the graph's entry waits for its grid anyway)
+__global__ void k_set_xa(uint64_t *xa, uint64_t v0, uint64_t v1, uint64_t v2, uint64_t v3) {
+    if (threadIdx.x == 0) {
+        xa[0] = v0;
+        xa[1] = v1;
+        xa[2] = v2;
+        xa[3] = v3;
+    }
+}
+
+// the safety check's go on its own stream when the entry is inside the window graph:
+// one lane polls *go (stored by the window's first row kernel) and acquires at agent
+// scope; the check's kernels follow on the stream.  Never spins forever: on a timeout it
+// marks *late with late_value (the exit's target for this check, so sml_dyn_last_safe
+// fails this window) and the check reads whatever d_chk holds
+__global__ void k_check_go(const uint64_t *go, uint64_t want, unsigned *late, unsigned late_value, long long timeout) {
+    if (threadIdx.x != 0) return;
+    const long long t0 = wall_clock64();
+    while (__hip_atomic_load(go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
+        __builtin_amdgcn_s_sleep(2);
+        if (wall_clock64() - t0 > timeout) {
+            __hip_atomic_store(late, late_value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            break;
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+}
+
 __global__ void k_flag_store(uint64_t *flag, const uint64_t *xa) {
     SML_TL_SCOPE(sml::tl::kExitStore);
     if (threadIdx.x == 0) __hip_atomic_store(flag, xa[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// late / self: a check whose go hand-off gave up (k_check_go stored self into *late)
+// reports NaN, so the exit takes the window as unsafe instead of trusting inputs the
+// entry may not have written yet
 __global__ __launch_bounds__(1024) void k_io_minmax(const double *__restrict__ G, double *__restrict__ mm,
-                                                     unsigned *__restrict__ cnt) {
+                                                     unsigned *__restrict__ cnt, const unsigned *__restrict__ late,
+                                                     unsigned self) {
     SML_TL_SCOPE(sml::tl::kCheckMinmax);
     __shared__ double smin[16], smax[16];
     const int v = blockIdx.x;
@@ -1956,6 +2010,8 @@ __global__ __launch_bounds__(1024) void k_io_minmax(const double *__restrict__ G
             lo = nmin(lo, smin[i]);
             hi = nmax(hi, smax[i]);
         }
+        if (late && __hip_atomic_load(late, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == self)
+            lo = hi = __builtin_nan("");
         if (cnt) {
             __hip_atomic_store(mm + 2 * v, lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(mm + 2 * v + 1, hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1992,6 +2048,7 @@ extern "C" int sml_dyn_destroy(sml_dynamics *d) {
     for (auto &r : d->wreplay)
         if (r.exec) (void)hipGraphExecDestroy(r.exec);
     if (d->d_xa) (void)hipFree(d->d_xa);
+    if (d->d_go) (void)hipFree(d->d_go);
     if (d->cap_stream) (void)hipStreamDestroy(d->cap_stream);
     if (d->chk_stream) {
         (void)hipStreamSynchronize(d->chk_stream);
@@ -2024,6 +2081,10 @@ extern "C" int sml_dyn_create(double radius, sml_dynamics **out) {
     build_dyn_indyns(spectral_host_tables(d->sp), &d->tab);
     build_phys_tables(d->tab, &d->ptab);
     if (const char *e = std::getenv("SML_DYN_NOGRAPH")) d->nograph = *e && *e != '0';
+    // dispatch serialised by the runtime or a profiler's counter passes: the check must
+    // not wait for a kernel enqueued after it (launch_io_check's go hand-off)
+    for (const char *v : {"AMD_SERIALIZE_KERNEL", "ROCPROF_COUNTER_COLLECTION"})
+        if (const char *e = std::getenv(v)) d->serialized = d->serialized || (*e && std::strcmp(e, "0") != 0);
     if (const char *e = std::getenv("SML_DYN_STAMPS"))
         if (*e && *e != '0' && (rc = dalloc(reinterpret_cast<double **>(&d->d_dbg), kStampKernels * kStampBlocks * kStamps))) {
             sml_dyn_destroy(d);
@@ -2243,7 +2304,9 @@ int launch_step_fused(sml_dynamics *d, int j1, int j2, double dt, double alph, d
     }
     if (phys) {
         hipLaunchKernelGGL(k_st_gridspec_p, dim3(kIL), dim3(kGpThreads), 0, st, d->d_varm, d->d_vfm, sd.wa, sd.cosgr, T,
-                           d->d_pbc, d->d_rad, d->d_ptab, lradsw ? 1 : 0, d->d_dbg);
+                           d->d_pbc, d->d_rad, d->d_ptab, lradsw ? 1 : 0, d->go_src_next, d->go_dst_next, d->d_dbg);
+        d->go_src_next = nullptr;  // one launch
+        d->go_dst_next = nullptr;
         SML_HIP(hipGetLastError());
     } else {
         hipLaunchKernelGGL(k_st_rows, dim3(kIL), dim3(kRowThreads), 0, st, d->d_varm, d->d_vfm, sd.wa, sd.cosgr, T,
@@ -2346,13 +2409,25 @@ extern "C" int sml_dyn_leapfrog(sml_dynamics *d, int nsteps, double dt, double a
 namespace {
 // run_model's exit as window_impl captures it behind the window: iogrid(31)'s gridx
 // (IoExit) and an optional one-lane store (the hybrid loop's forecast hop)
+// and, with `entry`, run_model's entry in front of the window: iogrid(30)'s specx (its
+// hop wait's value from d_xa) and k_io_entry, the first row kernel handing *go_src to the
+// safety check's *go
+struct EntrySpec {
+    const double *g4, *logp;
+    HopWait w;
+    uint64_t *go;
+    const uint64_t *go_src;
+};
 struct ExitSpec {
     const double *varm;
     double *fc4, *fc2;
     IoExit ex;
     uint64_t *store;
     uint64_t store_value;
+    const EntrySpec *entry = nullptr;
 };
+int launch_entry(sml_dynamics *d, const double *d_grid4d, const double *d_logp, HopWait w, hipStream_t st,
+                 uint64_t *xa, uint64_t xa0, uint64_t xa1);
 int window_impl(sml_dynamics *d, int nleap, double delt, double alph, double rob, double wil, void *stream,
                 bool prepared, const ExitSpec *exit = nullptr);
 }  // namespace
@@ -2396,12 +2471,17 @@ int window_impl(sml_dynamics *d, int nleap, double delt, double alph, double rob
     sml_dynamics::WindowReplay &r = d->wreplay[(entry ? 1 : 0) + (prepared ? 2 : 0)];
     const double key[8] = {(double)nleap, delt,  alph, rob, wil, d->phys_on ? 1.0 : 0.0, d->fused ? 1.0 : 0.0,
                            prepared ? 2.0 : 1.0};
-    // the exit's fixed arguments (its count and the store's value change per launch)
-    const void *exit_key[9] = {};
+    // the exit's (and entry's) fixed arguments (the counts and hop values change per
+    // launch: d_xa)
+    const void *exit_key[16] = {};
     if (exit) {
-        const void *k[9] = {exit->varm,   exit->fc4,     exit->fc2,    exit->ex.mm,
-                            exit->ex.in4, exit->ex.inlp, exit->ex.cnt, (const void *)(intptr_t)exit->ex.timeout,
-                            exit->store};
+        const EntrySpec *en = exit->entry;
+        const void *k[16] = {exit->varm,   exit->fc4,     exit->fc2,    exit->ex.mm,
+                             exit->ex.in4, exit->ex.inlp, exit->ex.cnt, (const void *)(intptr_t)exit->ex.timeout,
+                             exit->store,  en ? (const void *)1 : nullptr,
+                             en ? en->w.flag : nullptr, en ? en->w.late : nullptr, en ? en->w.sig : nullptr,
+                             en ? (const void *)(intptr_t)en->w.timeout : nullptr, en ? en->w.vptr : nullptr,
+                             en ? en->go : nullptr};
         std::memcpy(exit_key, k, sizeof k);
     }
     const bool exit_same =
@@ -2417,9 +2497,20 @@ int window_impl(sml_dynamics *d, int nleap, double delt, double alph, double rob
         SML_HIP(hipStreamBeginCapture(d->cap_stream, hipStreamCaptureModeThreadLocal));
         // consecutive steps chained: each step's last kernel prepares the next one's
         // inverse transforms (j2 = 1 for step(1, 1), then 2)
+        int rc = SML_OK;
+        if (exit && exit->entry) {  // run_model's entry (specx + k_io_entry) in front of the window
+            // (with the tables the entry read when it was launched before the graph: the
+            // last impint's, 2 delt, as the previous window left them)
+            const EntrySpec *en = exit->entry;
+            rc = launch_entry(d, en->g4, en->logp, en->w, d->cap_stream, nullptr, 0, 0);
+            d->go_src_next = en->go_src;  // the first row kernel lets the safety check go
+            d->go_dst_next = en->go;
+        }
         d->d_tab = tab[0];
         d->io_exit = prepared ? d->d_varm : nullptr;  // run_model: the exit's gridy in the last kernel
-        int rc = launch_step(d, 1, 1, dts[0], alph, rob, wil, nullptr, entry, d->cap_stream, prepared, 2);
+        if (!rc) rc = launch_step(d, 1, 1, dts[0], alph, rob, wil, nullptr, entry, d->cap_stream, prepared, 2);
+        d->go_src_next = nullptr;
+        d->go_dst_next = nullptr;
         d->d_tab = tab[1];
         if (!rc) rc = launch_step(d, 1, 2, dts[1], alph, rob, wil, nullptr, entry, d->cap_stream, true, nleap > 0 ? 2 : 0);
         d->d_tab = tab[2];
@@ -2836,7 +2927,9 @@ namespace {
 // d_chk (k_io_prep / k_io_entry, already on st): the re-grid and its min / max run on
 // chk_stream beside the window.  A caller's d_minmax is ready in st's order; the
 // internal one (nullptr) only for the next user of d_chk (which waits for it).
-int launch_io_check(sml_dynamics *d, hipStream_t st, double *d_minmax) {
+// go > 0 (the entry inside the window graph): instead of an event fork from st, the
+// check's stream waits in-kernel for the window's first row kernel to store go
+int launch_io_check(sml_dynamics *d, hipStream_t st, double *d_minmax, uint64_t go = 0) {
     double *cs = d->d_chk, *cv = cs + (size_t)kNIo * kSF, *cg = cv + (size_t)kNIo * kVF;
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
     SML_HIP(hipStreamIsCapturing(st, &cap));
@@ -2847,16 +2940,25 @@ int launch_io_check(sml_dynamics *d, hipStream_t st, double *d_minmax) {
             SML_HIP(hipEventCreateWithFlags(&d->ev_fork, hipEventDisableTiming));
             SML_HIP(hipEventCreateWithFlags(&d->ev_chk, hipEventDisableTiming));
         }
-        SML_HIP(hipEventRecord(d->ev_fork, st));
-        SML_HIP(hipStreamWaitEvent(d->chk_stream, d->ev_fork, 0));
         cst = d->chk_stream;
+        if (go) {
+            hipLaunchKernelGGL(k_check_go, dim3(1), dim3(64), 0, cst, d->d_go, go, d->d_chk_late,
+                               4u * (d->chk_count + 1), d->chk_timeout);
+            SML_HIP(hipGetLastError());
+        } else {
+            SML_HIP(hipEventRecord(d->ev_fork, st));
+            SML_HIP(hipStreamWaitEvent(d->chk_stream, d->ev_fork, 0));
+        }
+    } else if (go) {
+        return fail(SML_ERR_STATE, "launch_io_check: a go hand-off while the stream is captured");
     }
     if (int rc = spectral_gridy(d->sp, cs, cv, kNIo, cst)) return rc;
     if (int rc = spectral_gridx_range(d->sp, cv, cg, kNIo, 0, kNIoWind, cst)) return rc;
     double *mm = d_minmax ? d_minmax : d->d_minmax;
     // on the check stream, for run_model's exit: the counter hand-off (4 adds per check)
     const bool counted = cst != st && !d_minmax;
-    hipLaunchKernelGGL(k_io_minmax, dim3(4), dim3(1024), 0, cst, cg, mm, counted ? d->d_chk_cnt : nullptr);
+    hipLaunchKernelGGL(k_io_minmax, dim3(4), dim3(1024), 0, cst, cg, mm, counted ? d->d_chk_cnt : nullptr,
+                       go ? d->d_chk_late : nullptr, 4u * (d->chk_count + 1));
     SML_HIP(hipGetLastError());
     if (counted) ++d->chk_count;
     d->chk_counted = counted;
@@ -2877,6 +2979,23 @@ int launch_io_check(sml_dynamics *d, hipStream_t st, double *d_minmax) {
             d->chk_pending = false;
         }
     }
+    return SML_OK;
+}
+
+// run_model's entry: iogrid(30)'s specx (waiting for its grid when w.flag) and the per-m
+// k_io_entry (specy, the combine into level 1, the check's inputs, the m-major state,
+// step(1, 1)'s gridy); xa: an exit captured in the window graph takes its per-launch
+// values from there (k_io_entry stores xa0 / xa1), else null
+int launch_entry(sml_dynamics *d, const double *d_grid4d, const double *d_logp, HopWait w, hipStream_t st,
+                 uint64_t *xa, uint64_t xa0, uint64_t xa1) {
+    if (int rc = spectral_specx_io(d->sp, d_grid4d, d_logp, d->d_vfm, kNIoWind, st, w)) return rc;
+    const SpectralDev sd = spectral_dev(d->sp);
+    const bool phys = d->phys_on;
+    hipLaunchKernelGGL(k_io_entry, dim3(kMX), dim3(kSpecThreads), 0, st, d->d_vfm, d->d_pfl, sd.wt, d->d_state,
+                       sm_buf(d, 0), d->d_chk, d->d_phis,
+                       d->d_tabm + (size_t)(d->d_tab - d->d_tabs) * kMX * kTabMDoubles, sd.pinv, d->d_varm,
+                       phys ? kNInv1P : kNInv1, phys ? kNInvP : kNInv, xa, xa0, xa1);
+    SML_HIP(hipGetLastError());
     return SML_OK;
 }
 }  // namespace
@@ -2948,8 +3067,6 @@ extern "C" int sml_dyn_run_model(sml_dynamics *d, const double *d_grid4d, const 
         w.sig = d->entry_sig;
         d->entry_wait = HopWait{};  // one launch
         d->entry_sig = nullptr;
-        if (int rc = spectral_specx_io(d->sp, d_grid4d, d_logp, d->d_vfm, kNIoWind, st, w)) return rc;
-        const SpectralDev sd = spectral_dev(d->sp);
         const bool phys = d->phys_on;
         d->sm_cur = 0;  // the window's chain starts in buffer 0
         // the exit inside the window graph: needs the check's counter hand-off (no event
@@ -2958,13 +3075,44 @@ extern "C" int sml_dyn_run_model(sml_dynamics *d, const double *d_grid4d, const 
         hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
         SML_HIP(hipStreamIsCapturing(st, &cap));
         const bool xg = !d->nograph && cap == hipStreamCaptureStatusNone;
-        if (xg && !d->d_xa) SML_HIP(hipMalloc(&d->d_xa, 2 * sizeof(uint64_t)));
-        hipLaunchKernelGGL(k_io_entry, dim3(kMX), dim3(kSpecThreads), 0, st, d->d_vfm, d->d_pfl, sd.wt, d->d_state,
-                           sm_buf(d, 0), d->d_chk, d->d_phis,
-                           d->d_tabm + (size_t)(d->d_tab - d->d_tabs) * kMX * kTabMDoubles, sd.pinv, d->d_varm,
-                           phys ? kNInv1P : kNInv1, phys ? kNInvP : kNInv, xg ? d->d_xa : nullptr,
-                           (uint64_t)(4u * (d->chk_count + 1)), d->exit_store_value);
-        SML_HIP(hipGetLastError());
+        if (xg && !d->d_xa) SML_HIP(hipMalloc(&d->d_xa, 4 * sizeof(uint64_t)));
+        // and the entry inside it too (r06): specx + k_io_entry as the graph's first
+        // nodes, the safety check forked by the first row kernel's go store instead of an
+        // event after k_io_entry -- one launch boundary fewer on the chain, and the graph's
+        // launch hidden behind the entry's wait.  Not under serialised dispatch (the check,
+        // enqueued after the graph, would run after the exit that waits for it)
+        if (xg && phys && d->entry_graph && !d->serialized) {
+            if (!d->d_go) {
+                SML_HIP(hipMalloc(&d->d_go, sizeof(uint64_t)));
+                SML_HIP(hipMemset(d->d_go, 0, sizeof(uint64_t)));
+                SML_HIP(hipDeviceSynchronize());
+                d->go_count = 0;
+            }
+            const uint64_t go = ++d->go_count;
+            hipLaunchKernelGGL(k_set_xa, dim3(1), dim3(64), 0, st, d->d_xa, (uint64_t)(4u * (d->chk_count + 1)),
+                               d->exit_store_value, w.value, go);
+            SML_HIP(hipGetLastError());
+            EntrySpec en{d_grid4d, d_logp, w, d->d_go, d->d_xa + 3};
+            if (w.flag) en.w.vptr = d->d_xa + 2;
+            ExitSpec es{d->d_varm, d_fc4d, d_fc2d, IoExit{0.000001, d->d_minmax, d_grid4d, d_logp}, d->exit_store,
+                        0};
+            es.ex.cnt = d->d_chk_cnt;
+            es.ex.xa = d->d_xa;
+            es.ex.late = d->d_chk_late;
+            es.ex.timeout = d->chk_timeout;
+            es.entry = &en;
+            d->exit_store = nullptr;  // one launch
+            if (int rc = window_impl(d, nleap, delt, alph, rob, wil, stream, true, &es)) return rc;
+            // enqueued after the graph, so whatever queue it shares, its producer is ahead
+            if (int rc = launch_io_check(d, st, nullptr, go)) return rc;
+            if (!(d->chk_pending && d->chk_counted && d->mm_last == d->d_minmax))
+                return fail(SML_ERR_STATE, "sml_dyn_run_model: the safety check did not take the counter hand-off");
+            d->chk_pending = false;  // the exit waits for the check's counter itself
+            return SML_OK;
+        }
+        if (int rc = launch_entry(d, d_grid4d, d_logp, w, st, xg ? d->d_xa : nullptr,
+                                  (uint64_t)(4u * (d->chk_count + 1)), d->exit_store_value))
+            return rc;
         if (int rc = launch_io_check(d, st, nullptr)) return rc;
         if (xg) {
             if (!(d->chk_pending && d->chk_counted))

@@ -1309,7 +1309,9 @@ extern "C" int sml_hybrid_run_speedy(sml_hybrid *h, int *run) {
     }
     if (int rc = sml_dyn_last_safe(h->dyn, run, nullptr)) return rc;
     // once that step's check is done, every wait of the step has run (the check follows
-    // the entry specx, which follows the finish): a wait that gave up fails the step
+    // the entry specx -- behind k_io_entry, or behind the window's first row kernel's go
+    // when the entry is inside the window graph -- which follows the finish), or the
+    // check's own hand-off gave up (reported below): a wait that gave up fails the step
     // here, so a host polling per step (parallelmain.f90:268-270) stops instead of
     // going on from NaN forecasts; run_speedy is then 0
     if (int rc = hop_late_check(h, "sml_hybrid_run_speedy")) {

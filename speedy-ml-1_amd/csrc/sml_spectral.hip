@@ -266,7 +266,8 @@ __global__ __launch_bounds__(kFftThreads) void k_specx(const double *__restrict_
         if (threadIdx.x == 0) {
             gave_up = 0;
             const long long c0 = wall_clock64();
-            while (__hip_atomic_load(wait.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < wait.value) {
+            const uint64_t want = wait.vptr ? *wait.vptr : wait.value;
+            while (__hip_atomic_load(wait.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
                 __builtin_amdgcn_s_sleep(1);
                 if (wall_clock64() - c0 > wait.timeout) {
                     __hip_atomic_store(wait.late, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);

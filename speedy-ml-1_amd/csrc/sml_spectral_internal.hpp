@@ -50,6 +50,9 @@ struct HopWait {
     // timeout the kernel marks *late (system scope: a host-visible word) and reads NaN
     // instead of the grid it did not get, so nothing downstream passes for a forecast
     long long timeout = 400000000ll;
+    // the value to wait for, from device memory instead of `value` (a wait captured in a
+    // graph keeps its arguments: the kernel before it on the stream writes this word)
+    const uint64_t *vptr = nullptr;
 };
 int spectral_specx_io_blocks();
 int spectral_specx_io(sml_spectral *s, const double *g4, const double *logp, double *varm, int nwind,

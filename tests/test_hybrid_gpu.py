@@ -442,7 +442,10 @@ def test_a_hop_that_times_out_fails_the_step(cuda):
     r = ctypes.c_int(7)
     rc = lib().sml_hybrid_run_speedy(loop._h, ctypes.byref(r))
     assert rc != 0 and r.value == 0
-    assert b"timed out" in lib().sml_last_error()
+    # the entry's hop gave up, or -- the safety check waiting for the window's go at the
+    # same zero give-up time -- the check's hand-off: either is reported, once
+    msg = lib().sml_last_error()
+    assert b"timed out" in msg or b"did not receive its safety check" in msg, msg
     try:  # sync's own hop may time out too at zero give-up time: reported once
         loop.sync()
     except SmlError:
