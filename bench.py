@@ -80,6 +80,8 @@ def parse():
                    help="regions per rank in the supplementary W_out-training leg, one batch resident in HBM "
                         "(144 x 8 ranks = all 1152; 0 = skip)")
     p.add_argument("--train-steps", type=int, default=4096, help="training time steps per region in that leg")
+    p.add_argument("--train-batches", type=int, default=4,
+                   help="chunking_matmul batches the training steps are accumulated in (one Gram launch each)")
     p.add_argument("--reservoir-steps", type=int, default=50,
                    help="steps timed in the supplementary reservoir-only (configs[1]) leg (0 = skip)")
     p.add_argument("--exchange", choices=("native", "torch"), default="native",
@@ -802,7 +804,7 @@ def training_leg(dev, mask, args, world, rank):
     per = args.train_regions
     regions = [(rank * per + i) % 1152 for i in range(per)]
     naug = [132 + domain.reservoir_sizes(r, bool(mask[r])).n for r in regions]
-    nb = 4
+    nb = args.train_batches
     m = args.train_steps // nb
     gen = torch.Generator(device=dev)
     gen.manual_seed(3 + rank)

@@ -37,6 +37,7 @@
 using namespace sml;
 
 typedef double d4 __attribute__((ext_vector_type(4)));
+typedef double d2 __attribute__((ext_vector_type(2)));
 #define MFMA64(a, b, c) __builtin_amdgcn_mfma_f64_16x16x4f64((a), (b), (c), 0, 0, 0)
 
 namespace {
@@ -90,6 +91,9 @@ __device__ inline bool tile_of(int idx, int C, int *bi, int *bj, bool *strip) {
 // 132-double row shifts by 8 banks: 2-way conflicts).  (The single-buffered form, two
 // barriers per stage, measured slower: DESIGN.md §3.4.)
 constexpr int kLdsLd2 = kTile + 16;
+#ifndef SML_GDIAG
+#define SML_GDIAG 0
+#endif
 __global__ __launch_bounds__(256, 2) void k_train_gram2(const double *__restrict__ S, const double *__restrict__ T,
                                                      const TrainRegion *__restrict__ regs, int m, int nout, int npad,
                                                      double *__restrict__ G, double *__restrict__ B) {
@@ -116,28 +120,54 @@ __global__ __launch_bounds__(256, 2) void k_train_gram2(const double *__restrict
     const int ni = min(4, max(0, ((strip ? nout : naug) - bi * kTile - wr * 64 + 15) / 16));
     const int nj = min(4, max(0, (naug - bj * kTile - wc * 64 + 15) / 16));
     const bool full = ni == 4 && nj == 4;
-    const int lrow = tid & (kTile - 1), lt0 = tid >> 7;
-    const int arow = bi * kTile + lrow;
-    const int brow = bj * kTile + lrow;
-    const bool a_ok = strip ? (arow < nout) : (arow < naug);
-    const bool b_ok = brow < naug;
-    const double *pa = strip ? Tr + arow : Sr + arow;
-    const long long lda = strip ? nout : naug;
-    const double *pb = Sr + brow;
-    double ra[kKC / 2], rb[kKC / 2];
+    // LDS staging: a thread moves row pairs (2 r2, 2 r2 + 1) of time rows tq + 4 q, one
+    // 16-B load and one 16-B LDS store each (4 + 4 per stage: the stage's instruction
+    // count is what bounds the kernel).  Rows and steps clamped into the
+    // operand, so the loads are unconditional; the values past naug / nout / m are
+    // selected to 0 at the store, after the load's wait (a select right after the load
+    // would wait there, and the stage ahead would not be a prefetch) -- on the tiles at a
+    // region's edge only
+    const int r2 = tid & 63, tq = __builtin_amdgcn_readfirstlane(tid >> 6);  // the time row: per wave
+    const int rowsA = strip ? nout : naug;
+    const int ar = bi * kTile + 2 * r2, br = bj * kTile + 2 * r2;
+    const int ac = min(ar, rowsA - 2), bc = min(br, naug - 2);  // nout, naug >= 2
+    // a scalar base per time row plus the lane's row offset
+    const double *pa = (strip ? Tr : Sr) + bi * kTile, *pb = Sr + bj * kTile;
+    const int oa = ac - bi * kTile, ob = bc - bj * kTile;
+    const long long lda = rowsA;
+    const bool inner = __builtin_amdgcn_readfirstlane(bi * kTile + kTile <= rowsA && bj * kTile + kTile <= naug &&
+                                                      m % kKC == 0);
+#if SML_GDIAG == 1  // diagnostic: every block reads region 0's first 128 rows (L2-resident)
+    pa = pb = S;
+#endif
+    d2 ra[kKC / 4], rb[kKC / 4];
     auto fetch = [&](int t0) {
 #pragma unroll
-        for (int q = 0; q < kKC / 2; ++q) {
-            const int t = t0 + lt0 + 2 * q;
-            ra[q] = (a_ok && t < m) ? pa[(long long)t * lda] : 0.0;
-            rb[q] = (b_ok && t < m) ? pb[(long long)t * naug] : 0.0;
+        for (int q = 0; q < kKC / 4; ++q) {
+            const long long tc = min(t0 + tq + 4 * q, m - 1);
+#if SML_GDIAG == 2  // diagnostic: no global load
+            ra[q] = rb[q] = d2{(double)(tc & 7), 1.0};
+#else
+            ra[q] = *(const d2 *)(pa + tc * lda + oa);
+            rb[q] = *(const d2 *)(pb + tc * naug + ob);
+#endif
         }
     };
-    auto store = [&](int buf) {
+    // the pair as loaded from the clamped start c, for rows (x, x + 1) of n
+    auto pick = [](d2 v, int x, int c, int n, bool t_ok) {
+        return d2{t_ok && x < n ? (x == c ? v.x : v.y) : 0.0, t_ok && x + 1 < n && x == c ? v.y : 0.0};
+    };
+    auto store = [&](int buf, int t0) {
 #pragma unroll
-        for (int q = 0; q < kKC / 2; ++q) {
-            sA[buf][lt0 + 2 * q][lrow] = ra[q];
-            sB[buf][lt0 + 2 * q][lrow] = rb[q];
+        for (int q = 0; q < kKC / 4; ++q) {
+            d2 va = ra[q], vb = rb[q];
+            if (!inner) {
+                const bool t_ok = t0 + tq + 4 * q < m;
+                va = pick(va, ar, ac, rowsA, t_ok);
+                vb = pick(vb, br, bc, naug, t_ok);
+            }
+            *(d2 *)&sA[buf][tq + 4 * q][2 * r2] = va;
+            *(d2 *)&sB[buf][tq + 4 * q][2 * r2] = vb;
         }
     };
     d4 acc[4][4];
@@ -146,12 +176,13 @@ __global__ __launch_bounds__(256, 2) void k_train_gram2(const double *__restrict
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = d4{0, 0, 0, 0};
     fetch(0);
-    store(0);
+    store(0, 0);
     __syncthreads();
     if (kKC < m) fetch(kKC);
     int cur = 0;
     for (int t0 = 0; t0 < m; t0 += kKC) {
-        if (wlive) {  // wave-uniform
+        if (wlive && full) {  // wave-uniform; the stage's four k-steps one branch-free block,
+                              // so step s + 1's LDS reads issue under step s's MFMAs
 #pragma unroll
             for (int s = 0; s < kKC / 4; ++s) {
                 double a[4], b[4];
@@ -159,24 +190,32 @@ __global__ __launch_bounds__(256, 2) void k_train_gram2(const double *__restrict
                 for (int i = 0; i < 4; ++i) a[i] = sA[cur][4 * s + kk][wr * 64 + i * 16 + l16];
 #pragma unroll
                 for (int j = 0; j < 4; ++j) b[j] = sB[cur][4 * s + kk][wc * 64 + j * 16 + l16];
-                if (full) {
 #pragma unroll
-                    for (int i = 0; i < 4; ++i)
+                for (int i = 0; i < 4; ++i)
 #pragma unroll
-                        for (int j = 0; j < 4; ++j) acc[i][j] = MFMA64(a[i], b[j], acc[i][j]);
-                } else {  // a tile at a region's edge
+                    for (int j = 0; j < 4; ++j) acc[i][j] = MFMA64(a[i], b[j], acc[i][j]);
+            }
+        } else if (wlive) {  // a tile at a region's edge
 #pragma unroll
-                    for (int i = 0; i < 4; ++i)
+            for (int s = 0; s < kKC / 4; ++s) {
+                double a[4], b[4];
 #pragma unroll
-                        for (int j = 0; j < 4; ++j)
-                            if (i < ni && j < nj) acc[i][j] = MFMA64(a[i], b[j], acc[i][j]);
-                }
+                for (int i = 0; i < 4; ++i) a[i] = sA[cur][4 * s + kk][wr * 64 + i * 16 + l16];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) b[j] = sB[cur][4 * s + kk][wc * 64 + j * 16 + l16];
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        if (i < ni && j < nj) acc[i][j] = MFMA64(a[i], b[j], acc[i][j]);
             }
         }
+#if SML_GDIAG != 3  // diagnostic 3: the stages are never refilled
         if (t0 + kKC < m) {
-            store(cur ^ 1);
+            store(cur ^ 1, t0 + kKC);
             if (t0 + 2 * kKC < m) fetch(t0 + 2 * kKC);
         }
+#endif
         __syncthreads();
         cur ^= 1;
     }
@@ -267,8 +306,8 @@ struct TileLoader {
 // One TR x TC output tile (4 waves, wave (wr, wc) owns (TR/2) x (TC/2) = (TR/32) x
 // (TC/32) MFMA 16x16 tiles):
 //   O(r, c) = (accumulate ? O(r, c) : 0) + alpha * sum_{l < K} A(r, l) B(c, l)
-// A is TR x K, B is TC x K (K a multiple of 16) (layout flags AT / BT as TileLoader); rows >= arows /
-// brows read as zero and are not stored.  O is column-major: O(r, c) at
+// A is TR x K, B is TC x K (K a multiple of 16), both column-major (A(r, l) at
+// pa[l * lda + r]); rows >= arows / brows are not stored.  O is column-major: O(r, c) at
 // po[c * ldo + r].  128 x 128 tiles for the wide trailing update, 64-wide ones for
 // the narrow launches (panel, triangular solves), where one tile's MFMA chain is the
 // launch's latency.
@@ -276,32 +315,31 @@ struct TileLoader {
 // is read later -- the wave above the diagonal (wr < wc) loads its share of the LDS
 // stages and skips its MFMAs and stores.  KC: values of l per LDS stage (the MFMA chain
 // of an element runs over l in the same order whatever KC)
-template <int TR, int TC, bool AT, bool BT, int KC = kKC>
+template <int TR, int TC, int KC = kKC>
 __device__ __forceinline__ void gemm_tile(const double *__restrict__ pa, long long lda, int arows,
                                           const double *__restrict__ pb, long long ldb, int brows, double *po,
                                           long long ldo, double alpha, bool accumulate, int K = kTile,
                                           bool lower = false, bool te = false) {
-    using LA = TileLoader<TR, AT, KC>;
-    using LB = TileLoader<TC, BT, KC>;
     constexpr int NI = TR / 32, NJ = TC / 32;
     __shared__ double sA[KC][TR + kLdsPad];
     __shared__ double sB[KC][TC + kLdsPad];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int wr = w >> 1, wc = w & 1, l16 = lane & 15, kk = lane >> 4;
-    const int arow = LA::row(tid), brow = LB::row(tid);
-    const bool a_ok = arow < arows, b_ok = brow < brows;
-    double ra[LA::PER], rb[LB::PER];
+    // LDS staging as k_train_gram2's: row pairs (2 p, 2 p + 1) of time rows u + TQ q, one
+    // 16-B load and one 16-B LDS store each; every caller passes whole tiles (arows = TR,
+    // brows = TC, the rows of G's / linv's blocks), so the loads are unmasked
+    constexpr int RPA = TR / 2, RPB = TC / 2, TQA = 256 / RPA, TQB = 256 / RPB;
+    constexpr int NQA = KC / TQA, NQB = KC / TQB;
+    static_assert(NQA * TQA == KC && NQB * TQB == KC, "stage rows");
+    const int pa2 = tid % RPA, pb2 = tid % RPB;
+    const int ua = RPA == 64 ? __builtin_amdgcn_readfirstlane(tid / RPA) : tid / RPA;
+    const int ub = RPB == 64 ? __builtin_amdgcn_readfirstlane(tid / RPB) : tid / RPB;
+    d2 ra[NQA], rb[NQB];
     auto fetch = [&](int t0) {
 #pragma unroll
-        for (int q = 0; q < LA::PER; ++q) {
-            const int l = t0 + LA::l(tid, q);
-            ra[q] = a_ok ? (AT ? pa[(long long)arow * lda + l] : pa[(long long)l * lda + arow]) : 0.0;
-        }
+        for (int q = 0; q < NQA; ++q) ra[q] = *(const d2 *)(pa + (long long)(t0 + ua + TQA * q) * lda + 2 * pa2);
 #pragma unroll
-        for (int q = 0; q < LB::PER; ++q) {
-            const int l = t0 + LB::l(tid, q);
-            rb[q] = b_ok ? (BT ? pb[(long long)brow * ldb + l] : pb[(long long)l * ldb + brow]) : 0.0;
-        }
+        for (int q = 0; q < NQB; ++q) rb[q] = *(const d2 *)(pb + (long long)(t0 + ub + TQB * q) * ldb + 2 * pb2);
     };
     d4 acc[NI][NJ];
 #pragma unroll
@@ -312,9 +350,9 @@ __device__ __forceinline__ void gemm_tile(const double *__restrict__ pa, long lo
     for (int t0 = 0; t0 < K; t0 += KC) {
         __syncthreads();
 #pragma unroll
-        for (int q = 0; q < LA::PER; ++q) sA[LA::l(tid, q)][arow] = ra[q];
+        for (int q = 0; q < NQA; ++q) *(d2 *)&sA[ua + TQA * q][2 * pa2] = ra[q];
 #pragma unroll
-        for (int q = 0; q < LB::PER; ++q) sB[LB::l(tid, q)][brow] = rb[q];
+        for (int q = 0; q < NQB; ++q) *(d2 *)&sB[ub + TQB * q][2 * pb2] = rb[q];
         __syncthreads();
         if (t0 + KC < K) fetch(t0 + KC);
         if (lower && wr < wc) continue;  // wave-uniform
@@ -576,7 +614,7 @@ __global__ __launch_bounds__(256, 3) void k_chol_panel(double *__restrict__ G, c
     double *Gr = G + (size_t)r * npad * npad;
     double *A = Gr + (size_t)k * kTile * npad + (size_t)i * kTile + r0;
     const double *Li = linv + ((size_t)r * C + k) * kTile * kTile;
-    gemm_tile<64, 128, false, false>(A, npad, 64, Li, kTile, kTile, A, npad, 1.0, false, kTile, false, te != 0);
+    gemm_tile<64, 128>(A, npad, 64, Li, kTile, kTile, A, npad, 1.0, false, kTile, false, te != 0);
 }
 
 // A_ij -= sum_{k0 <= k < k0 + kw} L_ik L_jk^T for the lower-triangle tiles j <= i
@@ -596,7 +634,7 @@ __global__ __launch_bounds__(256, 2) void k_chol_update(double *__restrict__ G, 
     const double *Lik = Gr + (size_t)k0 * kTile * npad + (size_t)i * kTile;
     const double *Ljk = Gr + (size_t)k0 * kTile * npad + (size_t)j * kTile;
     double *Aij = Gr + (size_t)j * kTile * npad + (size_t)i * kTile;
-    gemm_tile<128, 128, false, false, KC>(Lik, npad, kTile, Ljk, npad, kTile, Aij, npad, -1.0, true, kw * kTile,
+    gemm_tile<128, 128, KC>(Lik, npad, kTile, Ljk, npad, kTile, Aij, npad, -1.0, true, kw * kTile,
                                           i == j);
 }
 
@@ -616,11 +654,11 @@ __global__ __launch_bounds__(256, 3) void k_chol_upanel(double *__restrict__ G, 
     const double *Lip = Gr + (size_t)k0 * kTile * npad + (size_t)i * kTile + r0;
     const double *Lkp = Gr + (size_t)k0 * kTile * npad + (size_t)k * kTile;
     double *A = Gr + (size_t)k * kTile * npad + (size_t)i * kTile + r0;
-    gemm_tile<64, 128, false, false>(Lip, npad, 64, Lkp, npad, kTile, A, npad, -1.0, true, (k - k0) * kTile, false,
+    gemm_tile<64, 128>(Lip, npad, 64, Lkp, npad, kTile, A, npad, -1.0, true, (k - k0) * kTile, false,
                                      te != 0);
     __syncthreads();  // the slab's updated rows, stored by every wave, before any is read
     const double *Li = linv + ((size_t)r * C + k) * kTile * kTile;
-    gemm_tile<64, 128, false, false>(A, npad, 64, Li, kTile, kTile, A, npad, 1.0, false, kTile, false, te != 0);
+    gemm_tile<64, 128>(A, npad, 64, Li, kTile, kTile, A, npad, 1.0, false, kTile, false, te != 0);
 }
 
 // The left-looking update of a panel's diagonal tile (k, k) by block columns k0 .. k - 1
@@ -635,7 +673,7 @@ __global__ __launch_bounds__(256, 2) void k_chol_update_diag(double *__restrict_
     double *Gr = G + (size_t)r * npad * npad;
     const double *Lkp = Gr + (size_t)k0 * kTile * npad + (size_t)k * kTile;
     double *Akk = Gr + (size_t)k * kTile * npad + (size_t)k * kTile;
-    gemm_tile<64, 64, false, false>(Lkp + r0, npad, 64, Lkp + c0, npad, 64, Akk + (size_t)c0 * npad + r0, npad, -1.0,
+    gemm_tile<64, 64>(Lkp + r0, npad, 64, Lkp + c0, npad, 64, Akk + (size_t)c0 * npad + r0, npad, -1.0,
                                     true, (k - k0) * kTile, false, te != 0);
 }
 

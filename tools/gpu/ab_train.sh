@@ -5,7 +5,7 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT"; tag=$1; shift; o=gpurun_out/$tag; mkdir -p $o
 timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_training_gpu.py > $o/tests.log 2>&1 || { tail -20 $o/tests.log; exit 1; }
 tail -1 $o/tests.log
-B="bench.py --no-cpu-baseline --reservoir-steps 0 --speedy-steps 0 --steps 2 --warmup 1"
+B="bench.py --no-cpu-baseline --reservoir-steps 0 --speedy-steps 0 --steps 2 --warmup 1 ${TRAIN_ARGS:-}"
 for rep in 1 2; do
   i=0
   for cfg in "$@"; do
