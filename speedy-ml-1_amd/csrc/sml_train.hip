@@ -291,18 +291,6 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_wave_barrier();
 }
 
-// Operand loader of the tile GEMM: a TM-row operand, kKC values of l per stage.
-// Column-major operands (T = false, X(row, l) at p[l * ld + row]): row = tid % TM,
-// l = tid / TM + (256 / TM) q -- rows contiguous across lanes; transposed ones
-// (T = true, X(row, l) at p[row * ld + l]): row = tid / (kKC / PER), l = PER
-// (tid % (kKC / PER)) + q -- PER contiguous values per lane.
-template <int TM, bool T, int KC = kKC>
-struct TileLoader {
-    static constexpr int PER = KC * TM / 256;
-    __device__ static int row(int tid) { return T ? tid / (KC / PER) : tid % TM; }
-    __device__ static int l(int tid, int q) { return T ? (tid % (KC / PER)) * PER + q : tid / TM + (256 / TM) * q; }
-};
-
 // One TR x TC output tile (4 waves, wave (wr, wc) owns (TR/2) x (TC/2) = (TR/32) x
 // (TC/32) MFMA 16x16 tiles):
 //   O(r, c) = (accumulate ? O(r, c) : 0) + alpha * sum_{l < K} A(r, l) B(c, l)
@@ -688,30 +676,54 @@ static int update_tiles(int C, int jlo, int jhi) {
 // in-panel launches, three blocks per tile row): 4 waves stacked by rows, each 32
 // rows x NC columns = 2 x NC / 16 MFMA tiles;
 //   O(r, c) = (accumulate ? O(r, c) : 0) + alpha * sum_{l < K} A(r, l) B(c, l)
-// A as TileLoader<128, AT>; B(c, l) at pb[c * ldb + l] (a row range of the
-// right-hand sides), columns c >= nb read as zero and are not stored.
+// A(r, l) at pa[l * lda + r] (AT = false) or pa[r * lda + l] (AT = true); B(c, l) at
+// pb[c * ldb + l] (a row range of the right-hand sides), columns c >= nb read as zero
+// and are not stored.
 template <bool AT, int NC>
 __device__ __forceinline__ void gemm_rhs(const double *__restrict__ pa, long long lda, const double *__restrict__ pb,
                                          long long ldb, int nb, double *po, long long ldo, double alpha,
                                          bool accumulate, int K = kTile, bool te = false) {
-    using LA = TileLoader<kTile, AT>;
-    constexpr int NJ = NC / 16, PB = NC * kKC / 256;
-    static_assert(NC % 16 == 0 && (NC * kKC) % 256 == 0, "column group");
+    constexpr int NJ = NC / 16;
+    static_assert(NC % 16 == 0, "column group");
     __shared__ double sA[kKC][kTile + kLdsPad];
     __shared__ double sB[kKC][NC + kLdsPad];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, l16 = lane & 15, kk = lane >> 4;
-    const int arow = LA::row(tid);
-    double ra[LA::PER], rb[PB];
+    // 16-B loads as gemm_tile's.  A column-major (AT = false): row pairs of time rows;
+    // transposed (AT = true, A(r, l) at pa[r * lda + l]): l pairs (2 lp, 2 lp + 1) of
+    // rows ar + 32 q, two LDS stores each.  B: l pairs of columns c = idx / 8, the columns
+    // past nb loaded from column nb - 1 and selected to 0 at the LDS store
+    constexpr int NQA = 4, NPB = NC * kKC / 2, NQB = (NPB + 255) / 256;
+    const int pa2 = tid & 63, ua = __builtin_amdgcn_readfirstlane(tid >> 6);  // AT = false
+    const int lp = tid & 7, ar = tid >> 3;                                     // AT = true
+    d2 ra[NQA], rb[NQB];
     auto fetch = [&](int t0) {
 #pragma unroll
-        for (int q = 0; q < LA::PER; ++q) {
-            const int l = t0 + LA::l(tid, q);
-            ra[q] = AT ? pa[(long long)arow * lda + l] : pa[(long long)l * lda + arow];
+        for (int q = 0; q < NQA; ++q)
+            ra[q] = AT ? *(const d2 *)(pa + (long long)(ar + 32 * q) * lda + t0 + 2 * lp)
+                       : *(const d2 *)(pa + (long long)(t0 + ua + 4 * q) * lda + 2 * pa2);
+#pragma unroll
+        for (int q = 0; q < NQB; ++q) {
+            const int idx = min(tid + 256 * q, NPB - 1), c = min(idx >> 3, nb - 1);
+            rb[q] = *(const d2 *)(pb + (long long)c * ldb + t0 + 2 * (idx & 7));
+        }
+    };
+    auto store = [&]() {
+#pragma unroll
+        for (int q = 0; q < NQA; ++q) {
+            if (AT) {
+                sA[2 * lp][ar + 32 * q] = ra[q].x;
+                sA[2 * lp + 1][ar + 32 * q] = ra[q].y;
+            } else {
+                *(d2 *)&sA[ua + 4 * q][2 * pa2] = ra[q];
+            }
         }
 #pragma unroll
-        for (int q = 0; q < PB; ++q) {  // 16 lanes read one column's 16 contiguous values
-            const int idx = tid + 256 * q, c = idx >> 4;
-            rb[q] = c < nb ? pb[(long long)c * ldb + t0 + (idx & 15)] : 0.0;
+        for (int q = 0; q < NQB; ++q) {
+            const int idx = tid + 256 * q, c = idx >> 3;
+            if (idx < NPB) {
+                sB[2 * (idx & 7)][c] = c < nb ? rb[q].x : 0.0;
+                sB[2 * (idx & 7) + 1][c] = c < nb ? rb[q].y : 0.0;
+            }
         }
     };
     d4 acc[2][NJ];
@@ -722,10 +734,7 @@ __device__ __forceinline__ void gemm_rhs(const double *__restrict__ pa, long lon
     fetch(0);
     for (int t0 = 0; t0 < K; t0 += kKC) {
         __syncthreads();
-#pragma unroll
-        for (int q = 0; q < LA::PER; ++q) sA[LA::l(tid, q)][arow] = ra[q];
-#pragma unroll
-        for (int q = 0; q < PB; ++q) sB[(tid + 256 * q) & 15][(tid + 256 * q) >> 4] = rb[q];
+        store();
         __syncthreads();
         if (t0 + kKC < K) fetch(t0 + kKC);
 #pragma unroll
