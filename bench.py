@@ -869,8 +869,9 @@ def training_leg(dev, mask, args, world, rank):
         "solve_ms_per_region": round(solve_ms / len(naug), 3),
         "solve_info_ok": bool(ok.item() == 1.0),
         "solve_roofline": {
-            "kernels": "k_chol_diag / k_chol_panel / k_chol_update (right-looking, 128-blocked, fp64 MFMA, 2 waves "
-                       "per SIMD) + k_solve_diag / k_solve_update (block forward / backward substitution)",
+            "kernels": "k_chol_diag_b / k_chol_panel / k_chol_upanel / k_chol_update (right-looking over panels "
+                       "of 8 block columns, left-looking inside, 128-blocked, fp64 MFMA, 16-B LDS staging) + "
+                       "k_solve_diag / k_solve_update (block forward / backward substitution)",
             "bound": "mfma", "unit": "TFLOP/s",
             "achieved": round(solve_tf, 2),
             "peak": F64_MFMA_PEAK_TF,
@@ -886,8 +887,8 @@ def training_leg(dev, mask, args, world, rank):
         },
         "roofline": {
             "kernel": "k_train_gram2 (fp64 MFMA 16x16x4, 128x128 tiles, lower triangle + T S^T strip, LDS stages "
-                      "double-buffered, 2 waves per SIMD; blocks past a region's naug and wave sub-tiles without "
-                      "output skipped)",
+                      "double-buffered and filled by 16-B row-pair loads / stores, 2 waves per SIMD; blocks past a "
+                      "region's naug and wave sub-tiles without output skipped)",
             "bound": "mfma", "unit": "TFLOP/s",
             "achieved": round(achieved, 2),
             "issued_tflops": round(issued / (gram_ms * 1e-3) / 1e12, 2),

@@ -91,14 +91,30 @@ __device__ inline bool tile_of(int idx, int C, int *bi, int *bj, bool *strip) {
 // 132-double row shifts by 8 banks: 2-way conflicts).  (The single-buffered form, two
 // barriers per stage, measured slower: DESIGN.md §3.4.)
 constexpr int kLdsLd2 = kTile + 16;
+
+// One 16-B-per-lane global -> LDS copy (global_load_lds_dwordx4): lane l's 16 bytes from
+// g land at LDS byte address lds + 16 l.  In inline asm (as the CDNA guide's recipe:
+// M0 saved, set and restored in the one statement) because the builtin makes hipcc wait
+// vmcnt(0) around every such load; hipcc does not count these loads, so their
+// completion is waited for by hand (lds_dma_wait) before the barrier that publishes them.
+__device__ __forceinline__ void lds_dma16(const void *g, unsigned lds) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(g), "s"(lds)
+                 : "memory");
+}
+__device__ __forceinline__ void lds_dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ unsigned lds_addr(const double *p) {
+    return (unsigned)(size_t)(const __attribute__((address_space(3))) double *)p;
+}
 #ifndef SML_GDIAG
 #define SML_GDIAG 0
 #endif
 __global__ __launch_bounds__(256, 2) void k_train_gram2(const double *__restrict__ S, const double *__restrict__ T,
                                                      const TrainRegion *__restrict__ regs, int m, int nout, int npad,
                                                      double *__restrict__ G, double *__restrict__ B) {
-    __shared__ double sA[2][kKC][kLdsLd2];
-    __shared__ double sB[2][kKC][kLdsLd2];
+    __shared__ double sm[2][2][kKC][kLdsLd2];  // [stage buffer][A, B][time row][row]: one LDS object
     const int r = blockIdx.y;
     const TrainRegion R = regs[r];
     const int C = npad / kTile;
@@ -166,8 +182,8 @@ __global__ __launch_bounds__(256, 2) void k_train_gram2(const double *__restrict
                 va = pick(va, ar, ac, rowsA, t_ok);
                 vb = pick(vb, br, bc, naug, t_ok);
             }
-            *(d2 *)&sA[buf][tq + 4 * q][2 * r2] = va;
-            *(d2 *)&sB[buf][tq + 4 * q][2 * r2] = vb;
+            *(d2 *)&sm[buf][0][tq + 4 * q][2 * r2] = va;
+            *(d2 *)&sm[buf][1][tq + 4 * q][2 * r2] = vb;
         }
     };
     d4 acc[4][4];
@@ -175,21 +191,18 @@ __global__ __launch_bounds__(256, 2) void k_train_gram2(const double *__restrict
     for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = d4{0, 0, 0, 0};
-    fetch(0);
-    store(0, 0);
-    __syncthreads();
-    if (kKC < m) fetch(kKC);
-    int cur = 0;
-    for (int t0 = 0; t0 < m; t0 += kKC) {
+    auto compute = [&](int cur) {
+        const double(*sA)[kLdsLd2] = sm[cur][0];
+        const double(*sB)[kLdsLd2] = sm[cur][1];
         if (wlive && full) {  // wave-uniform; the stage's four k-steps one branch-free block,
                               // so step s + 1's LDS reads issue under step s's MFMAs
 #pragma unroll
             for (int s = 0; s < kKC / 4; ++s) {
                 double a[4], b[4];
 #pragma unroll
-                for (int i = 0; i < 4; ++i) a[i] = sA[cur][4 * s + kk][wr * 64 + i * 16 + l16];
+                for (int i = 0; i < 4; ++i) a[i] = sA[4 * s + kk][wr * 64 + i * 16 + l16];
 #pragma unroll
-                for (int j = 0; j < 4; ++j) b[j] = sB[cur][4 * s + kk][wc * 64 + j * 16 + l16];
+                for (int j = 0; j < 4; ++j) b[j] = sB[4 * s + kk][wc * 64 + j * 16 + l16];
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -200,9 +213,9 @@ __global__ __launch_bounds__(256, 2) void k_train_gram2(const double *__restrict
             for (int s = 0; s < kKC / 4; ++s) {
                 double a[4], b[4];
 #pragma unroll
-                for (int i = 0; i < 4; ++i) a[i] = sA[cur][4 * s + kk][wr * 64 + i * 16 + l16];
+                for (int i = 0; i < 4; ++i) a[i] = sA[4 * s + kk][wr * 64 + i * 16 + l16];
 #pragma unroll
-                for (int j = 0; j < 4; ++j) b[j] = sB[cur][4 * s + kk][wc * 64 + j * 16 + l16];
+                for (int j = 0; j < 4; ++j) b[j] = sB[4 * s + kk][wc * 64 + j * 16 + l16];
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -210,14 +223,50 @@ __global__ __launch_bounds__(256, 2) void k_train_gram2(const double *__restrict
                         if (i < ni && j < nj) acc[i][j] = MFMA64(a[i], b[j], acc[i][j]);
             }
         }
-#if SML_GDIAG != 3  // diagnostic 3: the stages are never refilled
-        if (t0 + kKC < m) {
-            store(cur ^ 1, t0 + kKC);
-            if (t0 + 2 * kKC < m) fetch(t0 + 2 * kKC);
-        }
-#endif
+    };
+    // inner tiles with 16-B-aligned operand rows: the stages filled by LDS-DMA (a wave
+    // copies time rows 4 w .. 4 w + 3 of A and of B, one 1-KiB instruction each), the
+    // next stage's copies issued before this stage's MFMAs
+    const bool glds = inner && __builtin_amdgcn_readfirstlane((((size_t)pa | (size_t)pb) & 15) == 0 &&
+                                                              (lda & 1) == 0 && (naug & 1) == 0);
+    if (glds && SML_GDIAG == 0) {
+        const int wu = __builtin_amdgcn_readfirstlane(w);
+        auto dma = [&](int buf, int t0) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const long long t = t0 + 4 * wu + u;
+                lds_dma16(pa + t * lda + 2 * lane, lds_addr(&sm[buf][0][4 * wu + u][0]));
+                lds_dma16(pb + t * naug + 2 * lane, lds_addr(&sm[buf][1][4 * wu + u][0]));
+            }
+        };
+        dma(0, 0);
+        lds_dma_wait();
         __syncthreads();
-        cur ^= 1;
+        int cur = 0;
+        for (int t0 = 0; t0 < m; t0 += kKC) {
+            if (t0 + kKC < m) dma(cur ^ 1, t0 + kKC);
+            compute(cur);
+            lds_dma_wait();
+            __syncthreads();
+            cur ^= 1;
+        }
+    } else {
+        fetch(0);
+        store(0, 0);
+        __syncthreads();
+        if (kKC < m) fetch(kKC);
+        int cur = 0;
+        for (int t0 = 0; t0 < m; t0 += kKC) {
+            compute(cur);
+#if SML_GDIAG != 3  // diagnostic 3: the stages are never refilled
+            if (t0 + kKC < m) {
+                store(cur ^ 1, t0 + kKC);
+                if (t0 + 2 * kKC < m) fetch(t0 + 2 * kKC);
+            }
+#endif
+            __syncthreads();
+            cur ^= 1;
+        }
     }
     if (!wlive) return;
     double *Gr = G + (size_t)r * npad * npad;
@@ -303,14 +352,20 @@ __device__ __forceinline__ void wave_sync() {
 // is read later -- the wave above the diagonal (wr < wc) loads its share of the LDS
 // stages and skips its MFMAs and stores.  KC: values of l per LDS stage (the MFMA chain
 // of an element runs over l in the same order whatever KC)
-template <int TR, int TC, int KC = kKC>
+// DMA (the 128 x 128 trailing update): the stages double-buffered and filled by LDS-DMA as
+// k_train_gram2's inner tiles (a wave copies 4 time rows of A and of B per stage, one
+// 1-KiB instruction each), the next stage's copies issued before this stage's MFMAs
+template <int TR, int TC, int KC = kKC, bool DMA = false>
 __device__ __forceinline__ void gemm_tile(const double *__restrict__ pa, long long lda, int arows,
                                           const double *__restrict__ pb, long long ldb, int brows, double *po,
                                           long long ldo, double alpha, bool accumulate, int K = kTile,
                                           bool lower = false, bool te = false) {
-    constexpr int NI = TR / 32, NJ = TC / 32;
-    __shared__ double sA[KC][TR + kLdsPad];
-    __shared__ double sB[KC][TC + kLdsPad];
+    constexpr int NI = TR / 32, NJ = TC / 32, NB = DMA ? 2 : 1;
+    static_assert(!DMA || (TR == 128 && TC == 128 && KC == 16), "LDS-DMA: one 128-row time row per instruction");
+    __shared__ double sA_[NB][KC][TR + kLdsPad];
+    __shared__ double sB_[NB][KC][TC + kLdsPad];
+    double(*sA)[TR + kLdsPad] = sA_[0];
+    double(*sB)[TC + kLdsPad] = sB_[0];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int wr = w >> 1, wc = w & 1, l16 = lane & 15, kk = lane >> 4;
     // LDS staging as k_train_gram2's: row pairs (2 p, 2 p + 1) of time rows u + TQ q, one
@@ -334,6 +389,44 @@ __device__ __forceinline__ void gemm_tile(const double *__restrict__ pa, long lo
     for (int i = 0; i < NI; ++i)
 #pragma unroll
         for (int j = 0; j < NJ; ++j) acc[i][j] = d4{0, 0, 0, 0};
+    auto compute = [&](const double(*cA)[TR + kLdsPad], const double(*cB)[TC + kLdsPad]) {
+        if (lower && wr < wc) return;  // wave-uniform
+#pragma unroll
+        for (int s = 0; s < KC / 4; ++s) {
+            double a[NI], b[NJ];
+#pragma unroll
+            for (int i = 0; i < NI; ++i) a[i] = cA[4 * s + kk][wr * (TR / 2) + i * 16 + l16];
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) b[j] = cB[4 * s + kk][wc * (TC / 2) + j * 16 + l16];
+#pragma unroll
+            for (int i = 0; i < NI; ++i)
+#pragma unroll
+                for (int j = 0; j < NJ; ++j) acc[i][j] = MFMA64(a[i], b[j], acc[i][j]);
+        }
+    };
+    if constexpr (DMA) {
+        const int wu = __builtin_amdgcn_readfirstlane(w);
+        auto dma = [&](int buf, int t0) {
+#pragma unroll
+            for (int u = 0; u < KC / 4; ++u) {
+                const long long t = t0 + 4 * wu + u;
+                lds_dma16(pa + t * lda + 2 * lane, lds_addr(&sA_[buf][4 * wu + u][0]));
+                lds_dma16(pb + t * ldb + 2 * lane, lds_addr(&sB_[buf][4 * wu + u][0]));
+            }
+        };
+        __syncthreads();  // a previous tile's readers of these stages (k_chol_upanel's two calls)
+        dma(0, 0);
+        lds_dma_wait();
+        __syncthreads();
+        int cur = 0;
+        for (int t0 = 0; t0 < K; t0 += KC) {
+            if (t0 + KC < K) dma(cur ^ 1, t0 + KC);
+            compute(sA_[cur], sB_[cur]);
+            lds_dma_wait();
+            __syncthreads();
+            cur ^= 1;
+        }
+    } else {
     fetch(0);
     for (int t0 = 0; t0 < K; t0 += KC) {
         __syncthreads();
@@ -343,19 +436,8 @@ __device__ __forceinline__ void gemm_tile(const double *__restrict__ pa, long lo
         for (int q = 0; q < NQB; ++q) *(d2 *)&sB[ub + TQB * q][2 * pb2] = rb[q];
         __syncthreads();
         if (t0 + KC < K) fetch(t0 + KC);
-        if (lower && wr < wc) continue;  // wave-uniform
-#pragma unroll
-        for (int s = 0; s < KC / 4; ++s) {
-            double a[NI], b[NJ];
-#pragma unroll
-            for (int i = 0; i < NI; ++i) a[i] = sA[4 * s + kk][wr * (TR / 2) + i * 16 + l16];
-#pragma unroll
-            for (int j = 0; j < NJ; ++j) b[j] = sB[4 * s + kk][wc * (TC / 2) + j * 16 + l16];
-#pragma unroll
-            for (int i = 0; i < NI; ++i)
-#pragma unroll
-                for (int j = 0; j < NJ; ++j) acc[i][j] = MFMA64(a[i], b[j], acc[i][j]);
-        }
+        compute(sA, sB);
+    }
     }
     if (te) {
         // each 16 x 16 tile transposed through the wave's LDS scratch (sA, free after the
@@ -605,6 +687,9 @@ __global__ __launch_bounds__(256, 3) void k_chol_panel(double *__restrict__ G, c
     gemm_tile<64, 128>(A, npad, 64, Li, kTile, kTile, A, npad, 1.0, false, kTile, false, te != 0);
 }
 
+#ifndef SML_UPD_DMA
+#define SML_UPD_DMA 1
+#endif
 // A_ij -= sum_{k0 <= k < k0 + kw} L_ik L_jk^T for the lower-triangle tiles j <= i
 // of block columns jlo <= j < jhi: one GEMM of depth 128 kw per tile (the block
 // columns of L are contiguous in the column-major G).  KC: the GEMM's LDS stage depth
@@ -622,7 +707,7 @@ __global__ __launch_bounds__(256, 2) void k_chol_update(double *__restrict__ G, 
     const double *Lik = Gr + (size_t)k0 * kTile * npad + (size_t)i * kTile;
     const double *Ljk = Gr + (size_t)k0 * kTile * npad + (size_t)j * kTile;
     double *Aij = Gr + (size_t)j * kTile * npad + (size_t)i * kTile;
-    gemm_tile<128, 128, KC>(Lik, npad, kTile, Ljk, npad, kTile, Aij, npad, -1.0, true, kw * kTile,
+    gemm_tile<128, 128, KC, SML_UPD_DMA>(Lik, npad, kTile, Ljk, npad, kTile, Aij, npad, -1.0, true, kw * kTile,
                                           i == j);
 }
 
