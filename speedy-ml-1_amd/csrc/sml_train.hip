@@ -389,8 +389,12 @@ __device__ __forceinline__ void gemm_tile(const double *__restrict__ pa, long lo
     for (int i = 0; i < NI; ++i)
 #pragma unroll
         for (int j = 0; j < NJ; ++j) acc[i][j] = d4{0, 0, 0, 0};
+    // rows at or past arows (a region's last, partial block: padding, whose rows of L are
+    // 0) take nothing from the GEMM: a wave whose rows all lie there skips its MFMAs, and
+    // the epilogue does not store them -- bitwise what the full tile leaves there
+    const bool wlive = !(lower && wr < wc) && wr * (TR / 2) < arows;
     auto compute = [&](const double(*cA)[TR + kLdsPad], const double(*cB)[TC + kLdsPad]) {
-        if (lower && wr < wc) return;  // wave-uniform
+        if (!wlive) return;  // wave-uniform
 #pragma unroll
         for (int s = 0; s < KC / 4; ++s) {
             double a[NI], b[NJ];
@@ -680,11 +684,12 @@ __global__ __launch_bounds__(kDiagThreads) void k_chol_diag_b(double *__restrict
 __global__ __launch_bounds__(256, 3) void k_chol_panel(double *__restrict__ G, const double *__restrict__ linv, int npad,
                                                     int k, const TrainRegion *__restrict__ regs, int te) {
     const int r = blockIdx.y, C = npad / kTile, i = k + 1 + (blockIdx.x >> 1), r0 = (blockIdx.x & 1) * 64;
-    if (i >= live_blocks(regs, r)) return;  // A_ik = 0: L_ik = 0
+    const int rows = min(64, regs[r].naug - i * kTile - r0);  // the slab's data rows
+    if (rows <= 0) return;  // A_ik = 0: L_ik = 0 (padding)
     double *Gr = G + (size_t)r * npad * npad;
     double *A = Gr + (size_t)k * kTile * npad + (size_t)i * kTile + r0;
     const double *Li = linv + ((size_t)r * C + k) * kTile * kTile;
-    gemm_tile<64, 128>(A, npad, 64, Li, kTile, kTile, A, npad, 1.0, false, kTile, false, te != 0);
+    gemm_tile<64, 128>(A, npad, rows, Li, kTile, kTile, A, npad, 1.0, false, kTile, false, te != 0);
 }
 
 #ifndef SML_UPD_DMA
@@ -707,7 +712,8 @@ __global__ __launch_bounds__(256, 2) void k_chol_update(double *__restrict__ G, 
     const double *Lik = Gr + (size_t)k0 * kTile * npad + (size_t)i * kTile;
     const double *Ljk = Gr + (size_t)k0 * kTile * npad + (size_t)j * kTile;
     double *Aij = Gr + (size_t)j * kTile * npad + (size_t)i * kTile;
-    gemm_tile<128, 128, KC, SML_UPD_DMA>(Lik, npad, kTile, Ljk, npad, kTile, Aij, npad, -1.0, true, kw * kTile,
+    const int rows = min(kTile, regs[r].naug - i * kTile);  // block row i's data rows
+    gemm_tile<128, 128, KC, SML_UPD_DMA>(Lik, npad, rows, Ljk, npad, kTile, Aij, npad, -1.0, true, kw * kTile,
                                           i == j);
 }
 
@@ -722,16 +728,16 @@ __global__ __launch_bounds__(256, 3) void k_chol_upanel(double *__restrict__ G, 
                                                      int npad, int k0, int k, const TrainRegion *__restrict__ regs,
                                                      int te) {
     const int r = blockIdx.y, C = npad / kTile, i = k + 1 + (blockIdx.x >> 1), r0 = (blockIdx.x & 1) * 64;
-    if (i >= live_blocks(regs, r)) return;  // A_ik = 0: L_ik = 0
+    const int rows = min(64, regs[r].naug - i * kTile - r0);  // the slab's data rows
+    if (rows <= 0) return;  // A_ik = 0: L_ik = 0 (padding)
     double *Gr = G + (size_t)r * npad * npad;
     const double *Lip = Gr + (size_t)k0 * kTile * npad + (size_t)i * kTile + r0;
     const double *Lkp = Gr + (size_t)k0 * kTile * npad + (size_t)k * kTile;
     double *A = Gr + (size_t)k * kTile * npad + (size_t)i * kTile + r0;
-    gemm_tile<64, 128>(Lip, npad, 64, Lkp, npad, kTile, A, npad, -1.0, true, (k - k0) * kTile, false,
-                                     te != 0);
+    gemm_tile<64, 128>(Lip, npad, rows, Lkp, npad, kTile, A, npad, -1.0, true, (k - k0) * kTile, false, te != 0);
     __syncthreads();  // the slab's updated rows, stored by every wave, before any is read
     const double *Li = linv + ((size_t)r * C + k) * kTile * kTile;
-    gemm_tile<64, 128>(A, npad, 64, Li, kTile, kTile, A, npad, 1.0, false, kTile, false, te != 0);
+    gemm_tile<64, 128>(A, npad, rows, Li, kTile, kTile, A, npad, 1.0, false, kTile, false, te != 0);
 }
 
 // The left-looking update of a panel's diagonal tile (k, k) by block columns k0 .. k - 1
