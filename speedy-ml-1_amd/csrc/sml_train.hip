@@ -355,7 +355,9 @@ __device__ __forceinline__ void wave_sync() {
 // DMA (the 128 x 128 trailing update): the stages double-buffered and filled by LDS-DMA as
 // k_train_gram2's inner tiles (a wave copies 4 time rows of A and of B per stage, one
 // 1-KiB instruction each), the next stage's copies issued before this stage's MFMAs
-template <int TR, int TC, int KC = kKC, bool DMA = false>
+// DW: lower's waves on the diagonal also skip their 16 x 16 tiles above it (a separate
+// instance: in the trailing update the branch costs more registers than it saves)
+template <int TR, int TC, int KC = kKC, bool DMA = false, bool DW = false>
 __device__ __forceinline__ void gemm_tile(const double *__restrict__ pa, long long lda, int arows,
                                           const double *__restrict__ pb, long long ldb, int brows, double *po,
                                           long long ldo, double alpha, bool accumulate, int K = kTile,
@@ -392,9 +394,28 @@ __device__ __forceinline__ void gemm_tile(const double *__restrict__ pa, long lo
     // rows at or past arows (a region's last, partial block: padding, whose rows of L are
     // 0) take nothing from the GEMM: a wave whose rows all lie there skips its MFMAs, and
     // the epilogue does not store them -- bitwise what the full tile leaves there
+    // lower, the waves on the diagonal (wr = wc): their 16 x 16 tiles above the diagonal
+    // are not read later either, so they are skipped (left 0, stored as + 0)
     const bool wlive = !(lower && wr < wc) && wr * (TR / 2) < arows;
+    const bool dw = DW && __builtin_amdgcn_readfirstlane(lower && wr == wc);
     auto compute = [&](const double(*cA)[TR + kLdsPad], const double(*cB)[TC + kLdsPad]) {
         if (!wlive) return;  // wave-uniform
+        if (dw) {
+            static_assert(TR != TC || NI == NJ, "square wave tiles");
+#pragma unroll
+            for (int s = 0; s < KC / 4; ++s) {
+                double a[NI], b[NJ];
+#pragma unroll
+                for (int i = 0; i < NI; ++i) a[i] = cA[4 * s + kk][wr * (TR / 2) + i * 16 + l16];
+#pragma unroll
+                for (int j = 0; j < NJ; ++j) b[j] = cB[4 * s + kk][wc * (TC / 2) + j * 16 + l16];
+#pragma unroll
+                for (int i = 0; i < NI; ++i)
+#pragma unroll
+                    for (int j = 0; j <= i && j < NJ; ++j) acc[i][j] = MFMA64(a[i], b[j], acc[i][j]);
+            }
+            return;
+        }
 #pragma unroll
         for (int s = 0; s < KC / 4; ++s) {
             double a[NI], b[NJ];
@@ -752,8 +773,8 @@ __global__ __launch_bounds__(256, 2) void k_chol_update_diag(double *__restrict_
     double *Gr = G + (size_t)r * npad * npad;
     const double *Lkp = Gr + (size_t)k0 * kTile * npad + (size_t)k * kTile;
     double *Akk = Gr + (size_t)k * kTile * npad + (size_t)k * kTile;
-    gemm_tile<64, 64>(Lkp + r0, npad, 64, Lkp + c0, npad, 64, Akk + (size_t)c0 * npad + r0, npad, -1.0,
-                                    true, (k - k0) * kTile, false, te != 0);
+    gemm_tile<64, 64, kKC, false, true>(Lkp + r0, npad, 64, Lkp + c0, npad, 64, Akk + (size_t)c0 * npad + r0, npad,
+                                        -1.0, true, (k - k0) * kTile, q != 1, te != 0);  // (0, 0), (1, 1): diagonal
 }
 
 static int update_tiles(int C, int jlo, int jhi) {
@@ -773,7 +794,7 @@ static int update_tiles(int C, int jlo, int jhi) {
 template <bool AT, int NC>
 __device__ __forceinline__ void gemm_rhs(const double *__restrict__ pa, long long lda, const double *__restrict__ pb,
                                          long long ldb, int nb, double *po, long long ldo, double alpha,
-                                         bool accumulate, int K = kTile, bool te = false) {
+                                         bool accumulate, int K = kTile, bool te = false, int arows = kTile) {
     constexpr int NJ = NC / 16;
     static_assert(NC % 16 == 0, "column group");
     __shared__ double sA[kKC][kTile + kLdsPad];
@@ -828,6 +849,7 @@ __device__ __forceinline__ void gemm_rhs(const double *__restrict__ pa, long lon
         store();
         __syncthreads();
         if (t0 + kKC < K) fetch(t0 + kKC);
+        if (w * 32 >= arows) continue;  // wave-uniform: rows of a partial last block's padding
 #pragma unroll
         for (int s = 0; s < kKC / 4; ++s) {
             double a[2], b[NJ];
@@ -859,7 +881,7 @@ __device__ __forceinline__ void gemm_rhs(const double *__restrict__ pa, long lon
                 for (int q = 0; q < 4; ++q) {
                     const int c = 4 * q + a, row = w * 32 + i * 16 + b, col = j * 16 + c;
                     const double v = scr[c * 17 + b];
-                    if (col < nb) {
+                    if (col < nb && row < arows) {
                         double *p = po + (long long)col * ldo + row;
                         *p = (accumulate ? *p : 0.0) + alpha * v;
                     }
@@ -875,7 +897,7 @@ __device__ __forceinline__ void gemm_rhs(const double *__restrict__ pa, long lon
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const int row = w * 32 + i * 16 + kk + 4 * q, col = j * 16 + l16;
-                if (col < nb) {
+                if (col < nb && row < arows) {
                     double *p = po + (long long)col * ldo + row;
                     *p = (accumulate ? *p : 0.0) + alpha * acc[i][j][q];
                 }
@@ -894,7 +916,8 @@ __global__ __launch_bounds__(256, 2) void k_solve_diag(const double *__restrict_
     if (k >= live_blocks(regs, r) || c0 >= nout) return;  // B_k = 0 (padding rows), L_kk = I
     const double *Li = linv + ((size_t)r * C + k) * kTile * kTile;
     double *Bk = B + (size_t)r * npad * nout + (size_t)c0 * npad + (size_t)k * kTile;
-    gemm_rhs<upper, NC>(Li, kTile, Bk, npad, nout - c0, Bk, npad, 1.0, false, kTile, te != 0);
+    gemm_rhs<upper, NC>(Li, kTile, Bk, npad, nout - c0, Bk, npad, 1.0, false, kTile, te != 0,
+                        min(kTile, regs[r].naug - k * kTile));
 }
 
 // Update of block rows ilo <= i < ihi by the solved block rows [k0, k0 + kw), one
@@ -910,12 +933,13 @@ __global__ __launch_bounds__(256, 2) void k_solve_update(const double *__restric
     if (i >= Cr || (upper && k0 >= Cr) || c0 >= nout) return;
     const double *Gr = G + (size_t)r * npad * npad;
     double *Br = B + (size_t)r * npad * nout + (size_t)c0 * npad;
+    const int rows = min(kTile, regs[r].naug - i * kTile);  // block row i's data rows
     if constexpr (upper)  // A(rr, l) = L(k0 kTile + l, i kTile + rr): the transposed blocks (k, i)
         gemm_rhs<true, NC>(Gr + (size_t)i * kTile * npad + (size_t)k0 * kTile, npad, Br + (size_t)k0 * kTile, npad,
-                           nout - c0, Br + (size_t)i * kTile, npad, -1.0, true, kw * kTile, te != 0);
+                           nout - c0, Br + (size_t)i * kTile, npad, -1.0, true, kw * kTile, te != 0, rows);
     else
         gemm_rhs<false, NC>(Gr + (size_t)k0 * kTile * npad + (size_t)i * kTile, npad, Br + (size_t)k0 * kTile, npad,
-                            nout - c0, Br + (size_t)i * kTile, npad, -1.0, true, kw * kTile, te != 0);
+                            nout - c0, Br + (size_t)i * kTile, npad, -1.0, true, kw * kTile, te != 0, rows);
 }
 
 }  // namespace
