@@ -893,9 +893,10 @@ def training_leg(dev, mask, args, world, rank):
             "achieved": round(achieved, 2),
             "issued_tflops": round(issued / (gram_ms * 1e-3) / 1e12, 2),
             "peak": F64_MFMA_PEAK_TF,
-            "peak_source": "nominal: 64 clk per v_mfma_f64_16x16x4_f64 (2048 flop) on each of 1024 SIMDs at 2.4 GHz.  "
-                           "probe_tflops: back-to-back 16x16x4 MFMAs of tools/probe_mfma_f64.hip (~47.5 at ~2.39 GHz) "
-                           "-- not a ceiling: this Gram kernel issued 57.5 TF/s of MFMA work in r04a (issued_tflops)",
+            "peak_source": "nominal: 64 clk per v_mfma_f64_16x16x4_f64 (2048 flop) on each of 1024 SIMDs at 2.4 GHz; "
+                           "the Gram's own inner loop from LDS operands reaches 77.35 TF/s = 0.984 of it "
+                           "(tools/probe_lds_mfma.hip).  probe_tflops: back-to-back register-operand 16x16x4 MFMAs "
+                           "of tools/probe_mfma_f64.hip (~47.5) -- not a ceiling",
             "frac": round(achieved / F64_MFMA_PEAK_TF, 4),
             "probe_tflops": round(peak.value, 2),
             "frac_of_probe": round(achieved / peak.value, 4),
