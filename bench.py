@@ -551,9 +551,10 @@ def main():
                 "chain": ("the step's serial chain (v_p finish, exchange, assembly, tiling) on SPEEDY's stream behind "
                       "the window" if chain_eff == SML_CHAIN_SPEEDY else
                       "the step's serial chain on the reservoir's stream, two cross-stream hops per step"),
-            "streams": (f"overlapped: SPEEDY on CUs [0, {args.speedy_cus}), reservoir on CUs [{args.speedy_cus}, "
-                            f"{args.speedy_cus + (ncu - args.speedy_cus)})"
-                            if args.overlap and args.speedy_cus > 0 else
+            "streams": (f"overlapped: SPEEDY on CUs [0, {loop.speedy_cus}), reservoir on CUs [{loop.speedy_cus}, "
+                            f"{loop.speedy_cus + loop.res_cus}) (one CU per 6 of the rank's {res.nlocal} regions, "
+                            f"at least 64), the safety check on the rest"
+                            if loop.res_cus > 0 else
                             "overlapped, no CU split" if args.overlap else "one stream"),
             },
             "run_speedy_poll": ({"per_step": True, "ended_after_step": steps_done if ended else None,
@@ -567,8 +568,9 @@ def main():
             "finite": finite,
             "roofline": {
                 "kernel": (("k_res_readout<ml> (v_ml = W_out(:, ncs+1:) x~, GEMV, 17 rows per wave, 128-B-aligned rows; beside "
-                            + (f"SPEEDY's window on the {(ncu - args.speedy_cus)} CUs SPEEDY does not use, unpaced"
-                               if args.speedy_cus > 0 else "SPEEDY's window on shared CUs, paced at 2048 waves")
+                            + (f"SPEEDY's window on {loop.res_cus} of the {ncu - loop.speedy_cus} CUs SPEEDY does "
+                               "not use, unpaced"
+                               if loop.res_cus > 0 else "SPEEDY's window on shared CUs, paced at 2048 waves")
                             + "; the one-pass form on all CUs: reservoir_only.roofline_unpaced)")
                            if args.overlap else
                            "k_res_readout<full> (W_out [local_model; x~] + unstandardize, GEMV, 17 waves x 8 rows "

@@ -611,6 +611,10 @@ int sml_hybrid_get_feb29(const sml_hybrid *h, int *feb29);
 int sml_res_tile_tisr_field(sml_reservoirs *c, const double *d_tisr_grid, double *d_feedback, void *stream);
 /* the loop's main (reservoir + exchange) and side (SPEEDY) streams */
 int sml_hybrid_streams(const sml_hybrid *h, void **main, void **side);
+/* the CU split of the two streams: SPEEDY's CUs [0, speedy_cus) and the reservoir's
+ * [speedy_cus, speedy_cus + res_cus) (one CU per 6 of the rank's regions, a multiple of
+ * 8, 64..256 - speedy_cus; SML_RES_CUS overrides); both 0 without a split */
+int sml_hybrid_cus(const sml_hybrid *h, int *speedy_cus, int *res_cus);
 /* start_prediction's hand-over: inputs of the first step from an analysis grid and
  * a SPEEDY forecast of it (src/mod_reservoir.f90:938-959) */
 int sml_hybrid_start(sml_hybrid *h, const double *d_grid4d, const double *d_grid2d, const double *d_precip,

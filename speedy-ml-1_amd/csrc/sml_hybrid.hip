@@ -126,7 +126,8 @@ struct sml_hybrid {
     // the exchange row: the outvec (nout), + the slab ocean's sst of the region's
     // resolved points when the slab is on (as sendrecievegrid sends them, mpires.f90:358-383)
     int xw = 0;
-    int res_cus = 0;  // the CUs of the main stream's mask (0: no mask)
+    int res_cus = 0;     // the CUs of the main stream's mask (0: no mask)
+    int speedy_cus = 0;  // the CUs of the side (SPEEDY) stream's mask (0: no mask)
     // slab ocean (parallelmain.f90:216-249; mpires.f90:288-478, 575-767; cpl_sea.f90:38-46)
     struct Slab {
         sml_reservoirs *res = nullptr;  // the slab reservoirs of this rank's sst regions (generic, ML-only)
@@ -674,13 +675,15 @@ extern "C" int sml_hybrid_create(sml_reservoirs *res, sml_dynamics *dyn, sml_com
         void *s = nullptr, *m = nullptr;
         if (int rc = sml_stream_create_cu_range(0, speedy_cus, &s)) return bail(rc);
         h->side = (hipStream_t)s;
-        // the reservoir on CUs [speedy_cus, speedy_cus + res_cus): all the CUs SPEEDY
-        // does not use by default.  With the window at 1.09 ms, 160 of the 192 were
-        // better (less HBM pressure on the window, +1 %); with the window at 0.78 ms
-        // the begin (update + v_ml readout, 0.88 ms on 160 CUs) no longer fits beside
-        // it, and 192 CUs are 2.4 % faster (same-box A/B).
-        // SML_RES_CUS overrides the count.
-        int res_cus = ncu - speedy_cus;
+        // the reservoir on CUs [speedy_cus, speedy_cus + res_cus): one CU per 6 of the
+        // rank's regions (a multiple of 8: the same count on every XCD), at least 64, at
+        // most all the CUs SPEEDY does not use.  At 6 regions per CU the begin (update +
+        // v_ml readout) takes about the window's time beside it; more CUs only add HBM
+        // pressure on the window, fewer make the begin the critical path.  Same box
+        // (DESIGN.md §4): N = 1 (1152 regions) 192 CUs 1137 vs 160 1095; the 2-rank share
+        // 96 CUs 1254 vs 192 1230; 4-rank 64 1282 vs 192 1264; 8-rank 64 1298 vs 192
+        // 1290 steps/s.  SML_RES_CUS overrides the count.
+        int res_cus = std::min(ncu - speedy_cus, std::max(64, ((h->nlocal + 5) / 6 + 7) / 8 * 8));
         if (const char *er = getenv("SML_RES_CUS")) res_cus = std::min(std::max(atoi(er), 1), ncu - speedy_cus);
         if (int rc = sml_stream_create_cu_range(speedy_cus, res_cus, &m)) return bail(rc);
         h->main = (hipStream_t)m;
@@ -694,6 +697,7 @@ extern "C" int sml_hybrid_create(sml_reservoirs *res, sml_dynamics *dyn, sml_com
         if (int rc = sml_res_set_read_waves(res, 0)) return bail(rc);  // pacing pays only on shared CUs
         if (int rc = sml_res_set_update_cus(res, res_cus)) return bail(rc);  // one balanced-update block per CU
         h->res_cus = res_cus;
+        h->speedy_cus = speedy_cus;
     } else {
         if (hipStreamCreateWithFlags(&h->main, hipStreamNonBlocking) != hipSuccess)
             return bail(fail(SML_ERR_HIP, "stream"));
@@ -814,6 +818,13 @@ extern "C" int sml_hybrid_streams(const sml_hybrid *h, void **main, void **side)
     SML_REQUIRE(h, "null context");
     if (main) *main = h->main;
     if (side) *side = h->side;
+    return SML_OK;
+}
+
+extern "C" int sml_hybrid_cus(const sml_hybrid *h, int *speedy_cus, int *res_cus) {
+    SML_REQUIRE(h, "null context");
+    if (speedy_cus) *speedy_cus = h->speedy_cus;
+    if (res_cus) *res_cus = h->res_cus;
     return SML_OK;
 }
 

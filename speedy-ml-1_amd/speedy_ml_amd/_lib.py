@@ -47,7 +47,7 @@ EXPORTED = (
     "sml_comm_unique_id", "sml_comm_create", "sml_comm_create_file", "sml_comm_destroy", "sml_comm_rank",
     "sml_comm_allgather",
     "sml_hybrid_create", "sml_hybrid_destroy", "sml_hybrid_set_buffers", "sml_hybrid_set_tisr",
-    "sml_hybrid_streams", "sml_hybrid_start", "sml_hybrid_predict", "sml_hybrid_advance", "sml_hybrid_step",
+    "sml_hybrid_streams", "sml_hybrid_cus", "sml_hybrid_start", "sml_hybrid_predict", "sml_hybrid_advance", "sml_hybrid_step",
     "sml_hybrid_run_speedy", "sml_hybrid_sync",
     "sml_device_alloc", "sml_device_free", "sml_copy_to_device", "sml_copy_to_host", "sml_region_geometry",
     "sml_processor_decomposition", "sml_hybrid_set_tisr_table", "sml_tisr_date_index", "sml_res_tile_tisr_field",
@@ -208,6 +208,7 @@ def _declare(L: ctypes.CDLL) -> None:
         "sml_hybrid_set_buffers": [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp],
         "sml_hybrid_set_tisr": [vp, vp],
         "sml_hybrid_streams": [vp, pp, pp],
+        "sml_hybrid_cus": [vp, ip, ip],
         "sml_hybrid_start": [vp, vp, vp, vp, vp, vp],
         "sml_hybrid_predict": [vp],
         "sml_hybrid_advance": [vp, vp],

@@ -77,6 +77,9 @@ class HybridLoop:
         check(lib().sml_hybrid_streams(h, ctypes.byref(m), ctypes.byref(s)))
         self.main = torch.cuda.ExternalStream(m.value, device=self.dev)
         self.side = torch.cuda.ExternalStream(s.value, device=self.dev) if s.value != m.value else self.main
+        sc, rc = ctypes.c_int(), ctypes.c_int()
+        check(lib().sml_hybrid_cus(h, ctypes.byref(sc), ctypes.byref(rc)))
+        self.speedy_cus, self.res_cus = sc.value, rc.value  # the CU split (0, 0: none)
         self._set_xstream()
 
     def _set_xstream(self):
