@@ -63,6 +63,13 @@ def _setup(cuda, regions, mask, comm):
     return loop
 
 
+def _want_res_cus(nlocal, ncu, speedy_cus=64):
+    """sml_hybrid_create's CU split: one reservoir CU per 6 of the rank's regions, a
+    multiple of 8, at least 64, at most every CU SPEEDY leaves."""
+    c = -(-nlocal // 6)
+    return min(ncu - speedy_cus, max(64, -(-c // 8) * 8))
+
+
 def _close(loop):
     loop.close()
     loop.dyn.close()
@@ -81,6 +88,10 @@ def one_rank(cuda):
     """The single-rank HybridLoop over all 1152 full-size regions: 3 steps."""
     mask = domain.load_sst_mask()
     loop = _setup(cuda, np.arange(NREG), mask, None)
+    import torch
+
+    ncu = torch.cuda.get_device_properties(cuda).multi_processor_count
+    assert (loop.speedy_cus, loop.res_cus) == (64, _want_res_cus(NREG, ncu))  # 192 of 256
     snaps, runs = [], []
     for _ in range(STEPS):
         loop.step()
@@ -106,6 +117,9 @@ def test_every_rank_of_the_sharded_step_is_bitwise_the_one_rank_loop(cuda, one_r
     shares = [np.array(domain.processor_decomposition(NREG, world, q)) for q in range(world)]
     comms = [LocalRank(world, q) for q in range(world)]
     loops = [_setup(cuda, shares[q], mask, comms[q]) for q in range(world)]
+    ncu = torch.cuda.get_device_properties(cuda).multi_processor_count
+    for q, lp in enumerate(loops):  # a share's reservoir stream: 64 CUs (144 / 165 regions)
+        assert (lp.speedy_cus, lp.res_cus) == (64, _want_res_cus(len(shares[q]), ncu)), q
     recv = torch.zeros((world * maxc, 136), dtype=torch.float64, device=cuda)
     for step in range(STEPS):
         for lp in loops:
