@@ -3188,7 +3188,13 @@ extern "C" int sml_dyn_last_safe(sml_dynamics *d, int *safe, double *minmax) {
     SML_REQUIRE(d && safe, "null argument");
     double mm[8];
     if (d->mm_issued) {
-        SML_HIP(hipEventSynchronize(d->ev_mm));
+        // a host loop polls this once per step (parallelmain.f90:268-270): spin on the
+        // event rather than hipEventSynchronize, whose wait policy may yield the thread
+        // on a loaded host and wake it late, stalling the next step's enqueue
+        hipError_t q;
+        while ((q = hipEventQuery(d->ev_mm)) == hipErrorNotReady) {
+        }
+        SML_HIP(q);
         std::memcpy(mm, d->h_mm, sizeof mm);
     } else if (d->mm_last) {  // issued on the caller's stream (capture): synchronous copy
         SML_HIP(hipDeviceSynchronize());
