@@ -368,9 +368,9 @@ int sml_dyn_is_safe(const double *minmax);
  * grid with q floored (run_model's copy, :1550-1553).  The check runs beside the
  * window; sml_dyn_last_safe reads its outcome.  The forecast buffers must not alias
  * the inputs.  The window runs as a replayed hipGraph with the exit captured in it,
- * keyed on d_grid4d / d_logp / d_fc4d / d_fc2d: keep those buffers stable across calls
- * (the hybrid loop does) -- a caller alternating them gets the same results but
- * re-instantiates the ~200-node graph on every call. */
+ * keyed on d_grid4d / d_logp / d_fc4d / d_fc2d; up to four such graphs are kept, so a
+ * caller alternating two or three buffer sets (ping-pong) replays one per set, and only
+ * a fifth set evicts (re-captures) one. */
 int sml_dyn_run_model(sml_dynamics *d, const double *d_grid4d, const double *d_logp, int nleap, double delt,
                       double alph, double rob, double wil, double *d_fc4d, double *d_fc2d, void *stream);
 /* is_safe_to_run_speedy of the last sml_dyn_from_grid / sml_dyn_run_model, i.e. the

@@ -175,7 +175,13 @@ struct sml_dynamics {
         // from d_xa, written before each launch)
         bool has_exit = false;
         const void *exit_key[16] = {};
-    } wreplay[4];  // [prepared entry (sml_dyn_run_model)][entry lradsw]
+    };
+    // [prepared entry (sml_dyn_run_model)][entry lradsw] x kReplayWays graphs each, so a
+    // caller alternating its forecast / input buffers (ping-pong) replays one graph per
+    // buffer set instead of re-capturing the window every call; round-robin eviction
+    static constexpr int kReplayWays = 4;
+    WindowReplay wreplay[4][kReplayWays];
+    int wreplay_next[4] = {0, 0, 0, 0};
     // the next run_model's exit is followed by a store of exit_store_value to
     // *exit_store (sml::dyn_run_model_exit_store: the hybrid loop's forecast hop)
     uint64_t *exit_store = nullptr;
@@ -2045,8 +2051,9 @@ extern "C" int sml_dyn_destroy(sml_dynamics *d) {
         if (p) (void)hipFree(p);
     for (auto &r : d->replay)
         if (r.exec) (void)hipGraphExecDestroy(r.exec);
-    for (auto &r : d->wreplay)
-        if (r.exec) (void)hipGraphExecDestroy(r.exec);
+    for (auto &cls : d->wreplay)
+        for (auto &r : cls)
+            if (r.exec) (void)hipGraphExecDestroy(r.exec);
     if (d->d_xa) (void)hipFree(d->d_xa);
     if (d->d_go) (void)hipFree(d->d_go);
     if (d->cap_stream) (void)hipStreamDestroy(d->cap_stream);
@@ -2468,7 +2475,7 @@ int window_impl(sml_dynamics *d, int nleap, double delt, double alph, double rob
         if (nleap > 0) d->lradsw = (nleap % kNstrad == 1);
         return SML_OK;
     }
-    sml_dynamics::WindowReplay &r = d->wreplay[(entry ? 1 : 0) + (prepared ? 2 : 0)];
+    const int cls = (entry ? 1 : 0) + (prepared ? 2 : 0);
     const double key[8] = {(double)nleap, delt,  alph, rob, wil, d->phys_on ? 1.0 : 0.0, d->fused ? 1.0 : 0.0,
                            prepared ? 2.0 : 1.0};
     // the exit's (and entry's) fixed arguments (the counts and hop values change per
@@ -2484,9 +2491,20 @@ int window_impl(sml_dynamics *d, int nleap, double delt, double alph, double rob
                              en ? en->go : nullptr};
         std::memcpy(exit_key, k, sizeof k);
     }
-    const bool exit_same =
-        r.has_exit == (exit != nullptr) && (!exit || std::memcmp(exit_key, r.exit_key, sizeof exit_key) == 0);
-    if (!(r.exec && exit_same && std::memcmp(key, r.key, sizeof key) == 0 && std::memcmp(tab, r.tab, sizeof tab) == 0)) {
+    auto same = [&](const sml_dynamics::WindowReplay &w) {
+        return w.exec && w.has_exit == (exit != nullptr) &&
+               (!exit || std::memcmp(exit_key, w.exit_key, sizeof exit_key) == 0) &&
+               std::memcmp(key, w.key, sizeof key) == 0 && std::memcmp(tab, w.tab, sizeof tab) == 0;
+    };
+    sml_dynamics::WindowReplay *hit = nullptr;
+    for (auto &w : d->wreplay[cls])
+        if (same(w)) hit = &w;
+    if (!hit) {  // capture into the class's next way
+        hit = &d->wreplay[cls][d->wreplay_next[cls]];
+        d->wreplay_next[cls] = (d->wreplay_next[cls] + 1) % sml_dynamics::kReplayWays;
+    }
+    sml_dynamics::WindowReplay &r = *hit;
+    if (!same(r)) {
         if (r.exec) {
             SML_HIP(hipGraphExecDestroy(r.exec));
             r.exec = nullptr;

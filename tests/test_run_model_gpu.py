@@ -204,3 +204,47 @@ def test_a_late_exit_fails_its_own_window_only(cuda, dyn):
     want[..., 3] = np.where(g4[..., 3] < 0.000001, 0.000001, g4[..., 3])
     np.testing.assert_array_equal(late_f4, want)  # agcm_main's pass-through
     assert safe_next, "a late exit of an earlier window must not make this one unsafe"
+
+
+def test_run_model_with_alternating_buffers_is_bitwise_the_fixed_buffer_chain(cuda):
+    """A caller that ping-pongs its input / forecast buffers (run_model's window graph is
+    keyed on them: one cached graph per buffer set) gets the chain a caller copying into
+    fixed buffers gets."""
+    import torch
+
+    from speedy_ml_amd.dynamics import Dynamics
+    from speedy_ml_amd.synthetic import dyn_state, phys_boundary
+
+    def ctx():
+        st0, forcing = dyn_state()
+        d = Dynamics()
+        d.set_forcing(**forcing)
+        d.set_state(st0)
+        d.set_physics(phys_boundary(d, forcing["phis"]))
+        d.set_rad_state(None)
+        d.set_clock(1, True)
+        return d
+
+    g4, g2 = _grids()
+    a, b = ctx(), ctx()
+    try:
+        # fixed: the forecast copied back into one input buffer pair
+        i4, i2 = _t(g4, cuda), _t(g2, cuda)
+        o4, o2 = torch.zeros_like(i4), torch.zeros_like(i2)
+        for _ in range(3):
+            a.run_model(i4, i2, o4, o2, nleap=4)
+            i4.copy_(o4)
+            i2.copy_(o2)
+        # ping-pong: P -> Q, Q -> P, P -> Q (the third call replays the first's graph)
+        p4, p2 = _t(g4, cuda), _t(g2, cuda)
+        q4, q2 = torch.zeros_like(p4), torch.zeros_like(p2)
+        b.run_model(p4, p2, q4, q2, nleap=4)
+        b.run_model(q4, q2, p4, p2, nleap=4)
+        b.run_model(p4, p2, q4, q2, nleap=4)
+        torch.cuda.synchronize()
+        assert a.last_safe()[0] and b.last_safe()[0]
+        np.testing.assert_array_equal(q4.cpu().numpy(), o4.cpu().numpy())
+        np.testing.assert_array_equal(q2.cpu().numpy(), o2.cpu().numpy())
+    finally:
+        a.close()
+        b.close()
