@@ -904,22 +904,6 @@ __device__ __forceinline__ void gemm_rhs(const double *__restrict__ pa, long lon
             }
 }
 
-// Block k of the triangular solves on B (npad x nout per region, column-major), in
-// place (one block reads the whole block row it overwrites), right-hand sides
-// [NC z, NC (z + 1)) per block (every output column's sums are the same whichever
-// group computes it):
-//   forward  (upper = 0): B_k = L_kk^-1 B_k        backward (upper = 1): B_k = L_kk^-T B_k
-template <bool upper, int NC>  // one gemm_rhs instance per kernel: its LDS stages are static
-__global__ __launch_bounds__(256, 2) void k_solve_diag(const double *__restrict__ linv, double *__restrict__ B, int npad,
-                                                    int nout, int k, const TrainRegion *__restrict__ regs, int te) {
-    const int r = blockIdx.y, C = npad / kTile, c0 = NC * blockIdx.z;
-    if (k >= live_blocks(regs, r) || c0 >= nout) return;  // B_k = 0 (padding rows), L_kk = I
-    const double *Li = linv + ((size_t)r * C + k) * kTile * kTile;
-    double *Bk = B + (size_t)r * npad * nout + (size_t)c0 * npad + (size_t)k * kTile;
-    gemm_rhs<upper, NC>(Li, kTile, Bk, npad, nout - c0, Bk, npad, 1.0, false, kTile, te != 0,
-                        min(kTile, regs[r].naug - k * kTile));
-}
-
 // Update of block rows ilo <= i < ihi by the solved block rows [k0, k0 + kw), one
 // GEMM of depth 128 kw per block row:
 //   forward:  B_i -= sum_k L_ik Y_k        backward: B_i -= sum_k L_ki^T X_k
@@ -940,6 +924,42 @@ __global__ __launch_bounds__(256, 2) void k_solve_update(const double *__restric
     else
         gemm_rhs<false, NC>(Gr + (size_t)k0 * kTile * npad + (size_t)i * kTile, npad, Br + (size_t)k0 * kTile, npad,
                             nout - c0, Br + (size_t)i * kTile, npad, -1.0, true, kw * kTile, te != 0, rows);
+}
+
+// A block row of a panel's triangular solve in one launch, left-looking (k_chol_upanel's
+// form for the solves): the row's update by the panel's rows already solved, then its
+// diagonal block -- forward (upper = 0) for block row i of panel [p0, p1):
+//   B_i -= sum_{p0 <= k < i} L_ik Y_k,  Y_i = L_ii^-1 B_i
+// backward (upper = 1): B_i -= sum_{i < k < p1} L_ki^T X_k,  X_i = L_ii^-T B_i.
+// Each output column's sum is the right-looking form's, the depth-128 terms gathered
+// into one GEMM (the same products, summed in one MFMA chain instead of several
+// read-modify-writes: agrees to rounding); one launch per block row instead of two
+// per block column, the update and the diagonal block on the same workgroup
+template <bool upper, int NC>
+__global__ __launch_bounds__(256, 2) void k_solve_lpanel(const double *__restrict__ linv, const double *__restrict__ G,
+                                                      double *__restrict__ B, int npad, int nout, int p0, int p1,
+                                                      int i, const TrainRegion *__restrict__ regs, int te) {
+    const int r = blockIdx.y, C = npad / kTile, c0 = NC * blockIdx.z;
+    const int Cr = live_blocks(regs, r);
+    if (i >= Cr || c0 >= nout) return;  // padding block rows stay 0
+    const double *Gr = G + (size_t)r * npad * npad;
+    double *Br = B + (size_t)r * npad * nout + (size_t)c0 * npad;
+    double *Bi = Br + (size_t)i * kTile;
+    const int rows = min(kTile, regs[r].naug - i * kTile);  // block row i's data rows
+    if constexpr (upper) {
+        const int k1 = min(p1, Cr);  // solved rows i + 1 .. k1 - 1 (X past the data is 0)
+        if (k1 > i + 1)
+            gemm_rhs<true, NC>(Gr + (size_t)i * kTile * npad + (size_t)(i + 1) * kTile, npad,
+                               Br + (size_t)(i + 1) * kTile, npad, nout - c0, Bi, npad, -1.0, true,
+                               (k1 - 1 - i) * kTile, te != 0, rows);
+    } else {
+        if (i > p0)
+            gemm_rhs<false, NC>(Gr + (size_t)p0 * kTile * npad + (size_t)i * kTile, npad, Br + (size_t)p0 * kTile,
+                                npad, nout - c0, Bi, npad, -1.0, true, (i - p0) * kTile, te != 0, rows);
+    }
+    __syncthreads();  // the row's updated values, stored by every wave, before any is read
+    const double *Li = linv + ((size_t)r * C + i) * kTile * kTile;
+    gemm_rhs<upper, NC>(Li, kTile, Bi, npad, nout - c0, Bi, npad, 1.0, false, kTile, te != 0, rows);
 }
 
 }  // namespace
@@ -1109,26 +1129,18 @@ extern "C" int sml_train_solve(sml_train *t, int ncs, double beta_res, double be
     const int te = 1;
     for (int p0 = 0; p0 < C; p0 += P) {  // L Y = B
         const int p1 = std::min(C, p0 + P);
-        for (int k = p0; k < p1; ++k) {
-            hipLaunchKernelGGL((k_solve_diag<false, kG>), g1, dim3(256), 0, st, t->d_linv, t->d_B, npad, nout, k,
-                               t->d_regs, te);
-            if (k + 1 < p1)
-                hipLaunchKernelGGL((k_solve_update<false, kG>), dim3(p1 - 1 - k, nl, g1.z), dim3(256), 0, st, t->d_G,
-                                   t->d_B, npad, nout, k, 1, k + 1, t->d_regs, te);
-        }
+        for (int i = p0; i < p1; ++i)
+            hipLaunchKernelGGL((k_solve_lpanel<false, kG>), g1, dim3(256), 0, st, t->d_linv, t->d_G, t->d_B, npad,
+                               nout, p0, p1, i, t->d_regs, te);
         if (p1 < C)
             hipLaunchKernelGGL((k_solve_update<false, kRhs>), dim3(C - p1, nl), dim3(256), 0, st, t->d_G, t->d_B, npad,
                                nout, p0, p1 - p0, p1, t->d_regs, 0);
     }
     for (int p1 = C; p1 > 0; p1 -= P) {  // L^T X = Y, panels from the bottom
         const int p0 = std::max(0, p1 - P);
-        for (int k = p1 - 1; k >= p0; --k) {
-            hipLaunchKernelGGL((k_solve_diag<true, kG>), g1, dim3(256), 0, st, t->d_linv, t->d_B, npad, nout, k,
-                               t->d_regs, te);
-            if (k > p0)
-                hipLaunchKernelGGL((k_solve_update<true, kG>), dim3(k - p0, nl, g1.z), dim3(256), 0, st, t->d_G,
-                                   t->d_B, npad, nout, k, 1, p0, t->d_regs, te);
-        }
+        for (int i = p1 - 1; i >= p0; --i)
+            hipLaunchKernelGGL((k_solve_lpanel<true, kG>), g1, dim3(256), 0, st, t->d_linv, t->d_G, t->d_B, npad,
+                               nout, p0, p1, i, t->d_regs, te);
         if (p0 > 0)
             hipLaunchKernelGGL((k_solve_update<true, kRhs>), dim3(p0, nl), dim3(256), 0, st, t->d_G, t->d_B, npad, nout,
                                p0, p1 - p0, 0, t->d_regs, 0);
