@@ -17,7 +17,7 @@ for f in sorted(glob.glob(o + '/p*/**/*counter_collection.csv', recursive=True))
     acc = collections.defaultdict(lambda: collections.defaultdict(float)); n = collections.Counter()
     for r in csv.DictReader(open(f)):
         k = r['Kernel_Name']
-        if not any(x in k for x in ('k_train', 'k_chol_update', 'k_chol_upanel')): continue
+        if not any(x in k for x in ('k_train', 'k_chol_update', 'k_chol_upanel', 'k_solve')): continue
         k = k.split('(')[0].split('::')[-1]
         acc[k][r['Counter_Name']] += float(r['Counter_Value'])
         n[(k, r['Counter_Name'])] += 1
