@@ -874,7 +874,8 @@ def training_leg(dev, mask, args, world, rank):
             "kernels": "k_chol_diag_b / k_chol_panel / k_chol_upanel / k_chol_update (right-looking over panels "
                        "of 8 block columns, left-looking inside, 128-blocked, fp64 MFMA, 16-B LDS staging) + "
                        "k_solve_lpanel / k_solve_update (block forward / backward substitution: a panel's "
-                       "block rows left-looking, one launch each; the rows below or above by the panel)",
+                       "block rows left-looking, one launch each; the rows below or above by the panel; each "
+                       "panel's forward substitution on a second stream beside the later panels' factorisation)",
             "bound": "mfma", "unit": "TFLOP/s",
             "achieved": round(solve_tf, 2),
             "peak": F64_MFMA_PEAK_TF,

@@ -498,7 +498,9 @@ int sml_train_accumulate(sml_train *t, const double *d_states, const double *d_t
  * prior(i,i) = prior_val*beta_model^2 on b_trans when using_prior), solve
  * G W^T = B^T, write W_out(nout, naug_i) column-major per region back to back into
  * d_wout.  info (host, nlocal ints, may be NULL): potrf status per region (0 = ok,
- * filled when the stream completes).  Destroys the accumulators. */
+ * filled when the stream completes).  Destroys the accumulators.  Stream-ordered on
+ * `stream`; the forward substitution runs on a stream of the context (forked from and
+ * joined back to `stream` by events inside the call, graph-capturable), without a CU mask. */
 int sml_train_solve(sml_train *t, int ncs, double beta_res, double beta_model, int using_prior, double prior_val,
                     double *d_wout, int *info, void *stream);
 int sml_train_npad(const sml_train *t, int *npad);

@@ -975,6 +975,10 @@ struct sml_train {
     int *d_info = nullptr;
     long long s_total = 0, t_total = 0;
     int last_m = -1;
+    // the forward substitution's stream (beside the factorisation, sml_train_solve) and
+    // its fork / join events, created on the first solve
+    hipStream_t fwd = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
 };
 
 static void set_offsets(sml_train *t, int m, std::vector<TrainRegion> &h) {
@@ -993,6 +997,9 @@ extern "C" int sml_train_destroy(sml_train *t) {
     void *ptrs[] = {t->d_regs, t->d_G, t->d_B, t->d_wout_off, t->d_info, t->d_linv};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
+    if (t->ev_fork) (void)hipEventDestroy(t->ev_fork);
+    if (t->ev_join) (void)hipEventDestroy(t->ev_join);
+    if (t->fwd) (void)hipStreamDestroy(t->fwd);
     delete t;
     return SML_OK;
 }
@@ -1087,6 +1094,37 @@ extern "C" int sml_train_solve(sml_train *t, int ncs, double beta_res, double be
     SML_HIP(hipGetLastError());
     SML_HIP(hipMemsetAsync(t->d_info, 0, t->nlocal * sizeof(int), st));
     const int C = t->C, nl = t->nlocal, npad = t->npad, nout = t->nout;
+    // potrs, blocked by panels of P block rows: inside a panel, left-looking (block row i
+    // of the panel takes the update by the panel's rows already solved, then its diagonal
+    // inverse: k_solve_lpanel, latency-bound, one launch per row); then the rows beyond
+    // the panel take the whole panel's update at depth 128 P (MFMA-bound).  The in-panel
+    // launches in three column groups of the right-hand sides, their epilogues through an
+    // LDS transpose (te); the wide ones whole, stored directly.
+    //
+    // The forward substitution L Y = B of panel p reads only the factor's block columns
+    // of panels <= p (final once panel p's columns are done: later panels write columns
+    // >= p1 only) and writes only B, which the factorisation never reads, so it runs on
+    // a second stream forked after each panel's columns, beside the factorisation of the
+    // later panels: its latency-bound in-panel launches fill the CUs the diagonal factors
+    // (one workgroup per region) leave idle.  Every kernel and every element's sums are
+    // the same as on one stream (bitwise); the backward substitution joins after both.
+    constexpr int kG = kRhs / 3;
+    const dim3 g1(1, nl, 3);
+    const int te = 1;
+    if (!t->fwd) {
+        SML_HIP(hipStreamCreateWithFlags(&t->fwd, hipStreamNonBlocking));
+        SML_HIP(hipEventCreateWithFlags(&t->ev_fork, hipEventDisableTiming));
+        SML_HIP(hipEventCreateWithFlags(&t->ev_join, hipEventDisableTiming));
+    }
+    hipStream_t fw = t->fwd;
+    auto forward_panel = [&](int p0, int p1) {  // L Y = B for block rows p0 .. p1 - 1
+        for (int i = p0; i < p1; ++i)
+            hipLaunchKernelGGL((k_solve_lpanel<false, kG>), g1, dim3(256), 0, fw, t->d_linv, t->d_G, t->d_B, npad,
+                               nout, p0, p1, i, t->d_regs, te);
+        if (p1 < C)
+            hipLaunchKernelGGL((k_solve_update<false, kRhs>), dim3(C - p1, nl), dim3(256), 0, fw, t->d_G, t->d_B, npad,
+                               nout, p0, p1 - p0, p1, t->d_regs, 0);
+    };
     // potrf: G = L L^T over panels of t->panel block columns.  Inside a panel,
     // left-looking: block column k first takes the update from the panel's earlier
     // columns (depth 128 (k - p0)), then its diagonal factor and L_ik below it;
@@ -1095,6 +1133,9 @@ extern "C" int sml_train_solve(sml_train *t, int ncs, double beta_res, double be
     // (three quadrant workgroups), the diagonal factor, then the update and L_ik of the
     // blocks below fused (k_chol_upanel); the panel's first column: the factor and
     // k_chol_panel.  The shallow launches store through an LDS transpose (cte).
+    // (A lookahead split of the trailing update -- the next panel's columns on the chain,
+    // the rest on a third stream beside the next panel's factorisation -- measured no
+    // better, and slower on a default-priority chain: DESIGN.md §3.4.)
     const int P = t->panel, cte = 1;
     for (int p0 = 0; p0 < C; p0 += P) {
         const int p1 = std::min(C, p0 + P);
@@ -1112,30 +1153,20 @@ extern "C" int sml_train_solve(sml_train *t, int ncs, double beta_res, double be
                 hipLaunchKernelGGL(k_chol_panel, dim3(2 * (C - 1 - k), nl), dim3(256), 0, st, t->d_G, t->d_linv,
                                    npad, k, t->d_regs, cte);
         }
-        if (p1 < C)  // the trailing update (72 % of the solve's time)
+        SML_HIP(hipGetLastError());
+        // fork: panel p's forward substitution behind its columns (and, on fw, behind
+        // the earlier panels' forward substitution)
+        SML_HIP(hipEventRecord(t->ev_fork, st));
+        SML_HIP(hipStreamWaitEvent(fw, t->ev_fork, 0));
+        forward_panel(p0, p1);
+        SML_HIP(hipGetLastError());
+        if (p1 < C)  // the trailing update (the factorisation's largest launch)
             hipLaunchKernelGGL(k_chol_update<kKC>, dim3(update_tiles(C, p1, C), nl), dim3(256), 0, st, t->d_G, npad, p0,
                                p1 - p0, p1, C, t->d_regs);
     }
-    // potrs, blocked by panels of P block rows: inside a panel, right-looking (block
-    // row k's diagonal inverse, then its update of the panel's remaining rows at
-    // depth 128 -- a handful of tiles per region, latency-bound, so the shortest
-    // chain); then the rows beyond the panel take the whole panel's update at depth
-    // 128 P (MFMA-bound).
-    // the in-panel launches (diagonal blocks, one-block-deep updates) in three column
-    // groups of the right-hand sides, their epilogues through an LDS transpose (te); the
-    // wide ones whole, stored directly
-    constexpr int kG = kRhs / 3;
-    const dim3 g1(1, nl, 3);
-    const int te = 1;
-    for (int p0 = 0; p0 < C; p0 += P) {  // L Y = B
-        const int p1 = std::min(C, p0 + P);
-        for (int i = p0; i < p1; ++i)
-            hipLaunchKernelGGL((k_solve_lpanel<false, kG>), g1, dim3(256), 0, st, t->d_linv, t->d_G, t->d_B, npad,
-                               nout, p0, p1, i, t->d_regs, te);
-        if (p1 < C)
-            hipLaunchKernelGGL((k_solve_update<false, kRhs>), dim3(C - p1, nl), dim3(256), 0, st, t->d_G, t->d_B, npad,
-                               nout, p0, p1 - p0, p1, t->d_regs, 0);
-    }
+    // join: the backward substitution reads Y
+    SML_HIP(hipEventRecord(t->ev_join, fw));
+    SML_HIP(hipStreamWaitEvent(st, t->ev_join, 0));
     for (int p1 = C; p1 > 0; p1 -= P) {  // L^T X = Y, panels from the bottom
         const int p0 = std::max(0, p1 - P);
         for (int i = p1 - 1; i >= p0; --i)

@@ -193,3 +193,34 @@ def test_cholesky_panel_widths_agree(cuda):
         ws.append(w.cpu().numpy().copy())
         tr.close()
     assert np.abs(ws[1] - ws[0]).max() <= W_TOL * np.abs(ws[0]).max()
+
+
+def test_forked_forward_substitution_is_deterministic(cuda):
+    """Panels of two block columns over npad = 896 (four panels): each panel's forward
+    substitution runs on the context's second stream beside the later panels'
+    factorisation (sml_train_solve's fork / join).  It reads only finished block columns
+    and writes only B, so three solves of the same sums are bitwise equal, and W_out
+    agrees with the oracle."""
+    from speedy_ml_amd.training import Trainer
+
+    naugs, nout, m = [777, 401, 640], 136, 1000
+    S, T = _data(naugs, nout, m, seed=17)
+    tr = Trainer(naugs, nout)
+    tr.set_panel(2)
+    ws = []
+    for _ in range(3):
+        tr.reset()
+        _accumulate(tr, S, T, 2, cuda)
+        w, info = tr.solve(132, 0.3, 1.0, True, 0.5)
+        assert (info == 0).all()
+        ws.append(w.cpu().numpy().copy())
+    assert all(np.array_equal(ws[0], w) for w in ws[1:])
+    views = tr.wout_views(w)
+    for i, n in enumerate(naugs):
+        Go = np.zeros((n, n))
+        Bo = np.zeros((n, nout))
+        oracle.train_accumulate(S[i], T[i], Go, Bo)
+        wo, _ = oracle.train_solve(Go, Bo, 132, 0.3, 1.0, True, 0.5)
+        got = views[i].cpu().numpy()
+        assert np.abs(got - wo).max() <= W_TOL * np.abs(wo).max(), (i, np.abs(got - wo).max())
+    tr.close()
