@@ -82,6 +82,8 @@ def parse():
     p.add_argument("--train-steps", type=int, default=4096, help="training time steps per region in that leg")
     p.add_argument("--train-batches", type=int, default=4,
                    help="chunking_matmul batches the training steps are accumulated in (one Gram launch each)")
+    p.add_argument("--train-panel", type=int, default=8,
+                   help="block columns per Cholesky panel in that leg (sml_train_set_panel)")
     p.add_argument("--reservoir-steps", type=int, default=50,
                    help="steps timed in the supplementary reservoir-only (configs[1]) leg (0 = skip)")
     p.add_argument("--exchange", choices=("native", "torch"), default="native",
@@ -813,6 +815,8 @@ def training_leg(dev, mask, args, world, rank):
     S = torch.tanh(torch.randn(sum(naug) * m, dtype=torch.float64, device=dev, generator=gen))
     T = torch.randn(len(naug) * m * 136, dtype=torch.float64, device=dev, generator=gen)
     tr = Trainer(naug)
+    if args.train_panel != 8:
+        tr.set_panel(args.train_panel)
     tr.accumulate(S, T, m)  # warm-up
     tr.reset()
     torch.cuda.synchronize()
